@@ -1,0 +1,48 @@
+# LambdaGap-MI355X native build: host C++17 (g++/OpenMP) + HIP kernels for
+# gfx950 (hipcc), linked into one shared library used by the Python package
+# (ctypes) and by the CLI. Device code is cross-compiled; no GPU is needed to build.
+ROCM ?= /opt/rocm
+HIPCC ?= $(ROCM)/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+BUILD ?= build
+OUT ?= lambdagap_amd/lib
+JOBS ?= 8
+
+CXXFLAGS ?= -O3 -g0 -std=c++17 -fPIC -fopenmp -Wall -Wno-unused-function -Wno-sign-compare -Iinclude -Isrc \
+            -D__HIP_PLATFORM_AMD__=1 -I$(ROCM)/include
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Isrc -munsafe-fp-atomics \
+            -Wno-unused-result -ffp-contract=fast
+LDFLAGS ?= -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
+
+CPP_SRCS := $(shell find src -name '*.cpp' ! -path 'src/cli/*' | sort)
+HIP_SRCS := $(shell find src -name '*.hip' | sort)
+CPP_OBJS := $(patsubst src/%.cpp,$(BUILD)/%.o,$(CPP_SRCS))
+HIP_OBJS := $(patsubst src/%.hip,$(BUILD)/%.hip.o,$(HIP_SRCS))
+HEADERS := $(shell find include src -name '*.h' -o -name '*.def' -o -name '*.hpp')
+
+LIB := $(OUT)/lib_lambdagap.so
+CLI := $(OUT)/lambdagap
+
+all: $(LIB) $(CLI)
+
+$(BUILD)/%.o: src/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/%.hip.o: src/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(CPP_OBJS) $(HIP_OBJS)
+	@mkdir -p $(OUT)
+	$(CXX) -o $@ $^ $(LDFLAGS)
+
+$(CLI): src/cli/main.cpp $(LIB) $(HEADERS)
+	@mkdir -p $(OUT)
+	$(CXX) $(CXXFLAGS) -o $@ src/cli/main.cpp -L$(OUT) -l_lambdagap -Wl,-rpath,'$$ORIGIN' -fopenmp
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(CLI)
+
+.PHONY: all clean

@@ -1,0 +1,57 @@
+// Tree learner interface (reference include/LightGBM/tree_learner.h:27-114,
+// factory src/treelearner/tree_learner.cpp:15-57). Host learners: serial
+// (correctness oracle), feature/data/voting parallel over Network. Device
+// learners (HIP, MI355X) implement the same interface and additionally own the
+// device-resident score / gradients (OwnsScore() == true).
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "lgap/config.h"
+#include "lgap/dataset.h"
+#include "lgap/objective.h"
+#include "lgap/tree.h"
+
+namespace lgap {
+
+class TreeLearner {
+ public:
+  virtual ~TreeLearner() = default;
+  virtual void Init(const Dataset* train_data, bool is_constant_hessian) = 0;
+  virtual void ResetConfig(const Config* config) = 0;
+  virtual void ResetIsConstantHessian(bool) {}
+  // Bagging: subset of row indices used to grow the next tree (nullptr = all rows).
+  virtual void SetBaggingData(const data_size_t* used_indices, data_size_t num_data) = 0;
+  virtual std::unique_ptr<Tree> Train(const score_t* gradients, const score_t* hessians, bool is_first_tree) = 0;
+  // Refit leaf values of an existing tree structure (uses the leaf partition of leaf_pred).
+  virtual std::unique_ptr<Tree> FitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
+                                                  const score_t* gradients, const score_t* hessians) = 0;
+  // Adds tree outputs to the training score using the learner's leaf partition.
+  virtual void AddPredictionToScore(const Tree* tree, double* out_score) const = 0;
+  // L1 / quantile / MAPE leaf renewal (serial_tree_learner.cpp:924-962).
+  virtual void RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj, const double* score,
+                               data_size_t total_num_data, const data_size_t* bag_indices, data_size_t bag_cnt) const = 0;
+  // Row indices of a leaf of the last trained tree (in original numbering).
+  virtual std::vector<data_size_t> LeafIndices(int leaf) const = 0;
+
+  // ---- device-resident boosting (HIP learners)
+  virtual bool OwnsScore() const { return false; }
+  virtual bool SupportsDeviceGradients(const ObjectiveFunction*) const { return false; }
+  virtual void DeviceInitScore(const std::vector<double>& host_score, int num_tree_per_iter) { (void)host_score; (void)num_tree_per_iter; }
+  virtual void DeviceComputeGradients(const ObjectiveFunction*) {}
+  virtual void DeviceSetGradients(const score_t*, const score_t*, int) {}
+  virtual std::unique_ptr<Tree> DeviceTrain(int class_id, bool is_first_tree) { (void)class_id; (void)is_first_tree; return nullptr; }
+  virtual void DeviceAddTreeToScore(const Tree*, int class_id) { (void)class_id; }
+  virtual void DeviceAddConstant(double, int class_id) { (void)class_id; }
+  virtual void DeviceGetScore(std::vector<double>*) const {}
+  virtual void DeviceGetGradients(std::vector<score_t>*, std::vector<score_t>*) const {}
+  virtual std::string DeviceName() const { return "cpu"; }
+
+  static std::unique_ptr<TreeLearner> Create(const std::string& learner_type, const std::string& device_type,
+                                             bool linear_tree, const Config* config);
+};
+
+}  // namespace lgap

@@ -1,0 +1,1678 @@
+// HIP leaf-wise tree learner for MI355X (gfx950).
+//
+// Data layout (device-resident for the whole training run):
+//   rowbins  N x stride dwords   packed group bins of a row (histogram input:
+//                                one lane per dword, so a wave reads a
+//                                contiguous 256 B run of consecutive rows)
+//   colbins  G x N               group-major copy (partition decisions and the
+//                                split column are 1 byte/row streams)
+//   gh       K x N float2        (gradient, hessian), class-major
+//   idx[0/1] N ints              ping-pong row-index buffers (stable partition)
+//   idx[2]   bag list            root rows when bagging
+//
+// Growth of one tree is a FIXED kernel sequence (no host round trips):
+//   init, root_sums, hist(root), scan(root),
+//   repeat num_leaves-1 times:
+//     select   best leaf (argmax over leaves of the per-leaf best split)
+//     p_count  per-4096-row-tile left counts of the parent range
+//     p_scan   exclusive scan of tile counts
+//     p_scatter  stable partition of row indices into the other buffer
+//     post     leaf bookkeeping: ranges, sums, depth, monotone bounds,
+//              smaller/larger child, histogram-slot handoff, min_data/max_depth
+//     hist     LDS-privatised histogram of the smaller child (fp32 LDS atomics,
+//              fp64 global accumulation), most-frequent bins never touched
+//     scan     one wave per feature: larger = parent - smaller (subtraction
+//              trick), mfb reconstruction, both-direction threshold scan with
+//              wave prefix sums, categorical scan, extra-trees draws
+// Every launch has a fixed grid; kernels exit early when the tree is done, so
+// the sequence is captured once into a hipGraph and replayed per tree.
+// Data-parallel training all-reduces the smaller child's histogram (and the
+// root sums) over RCCL between `hist` and `scan`; every rank then scans all
+// features redundantly, so no best-split exchange is needed.
+//
+// Reference parity: serial_tree_learner.cpp:170-680 (growth loop, smaller /
+// larger handling, BeforeFindBestSplit), feature_histogram.hpp:830-1057
+// (threshold scans), cuda_best_split_finder.cu / cuda_histogram_constructor.cu
+// (the reference's GPU learner, whose role this file fills).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "device/grad_kernels.h"
+#include "device/hip_common.h"
+#include "device/runtime_internal.h"
+#include "device/tree_kernels.h"
+#include "learner/serial_tree_learner.h"
+#include "lgap/common.h"
+#include "lgap/device_api.h"
+#include "lgap/network.h"
+#include "lgap/objective.h"
+#include "lgap/rank_math.h"
+#include "lgap/split_math.h"
+
+namespace lgap {
+namespace device {
+namespace {
+
+constexpr int kHistThreads = 512;
+constexpr int kHistMinRows = 2048;
+constexpr int kHistLdsBytes = 56 * 1024;
+constexpr int kPartThreads = 256;
+constexpr int kPartIters = 16;
+constexpr int kTileRows = kPartThreads * kPartIters;
+constexpr int kScanWaves = 4;
+constexpr int kNodeThreads = 256;
+
+struct Args {
+  const uint32_t* rowbins;
+  const uint8_t* colbins;
+  const float2* gh;
+  int* idx[3];
+  int N, stride_dw, width, num_groups, TB, F, L, max_tiles;
+  const int* gstart;
+  const DevFeature* feat;
+  const HistTile* tiles;
+  const uint8_t* used_bytree;
+  const uint8_t* bynode;
+  const TreeParams* tp;
+  Ctl* ctl;
+  LeafRange* range;
+  double2* lsum;
+  double* lout;
+  int* gcount;
+  int* depth;
+  int* slot;
+  LeafBounds* bounds;
+  SplitInfo* best;
+  SplitRec* rec;
+  double* slots;
+  double* staging;
+  uint8_t* splittable;
+  SplitInfo* scan_out;
+  int* tile_cnt;
+  int* tile_off;
+  unsigned* rng;
+  double* cat_scratch;
+  int max_cat_bin;
+  int max_depth;
+  int distributed;
+  int use_monotone;
+  double monotone_penalty;
+  SplitParams sp;
+};
+
+// ---------------------------------------------------------------------------
+// small device helpers
+
+__device__ __forceinline__ uint32_t DecodeBin(int offset, int num_bin, int mfb, uint32_t gb) {
+  const int local = static_cast<int>(gb) - offset;
+  if (local < 0 || local >= num_bin - 1) return static_cast<uint32_t>(mfb);
+  return static_cast<uint32_t>(local < mfb ? local : local + 1);
+}
+
+struct SplitDesc {
+  int group, offset, num_bin, mfb, default_bin, missing, thr, default_left, is_cat;
+  uint32_t bits[kMaxCatWords];
+};
+
+__device__ __forceinline__ bool GoLeft(const SplitDesc& d, uint32_t gb) {
+  const uint32_t b = DecodeBin(d.offset, d.num_bin, d.mfb, gb);
+  if (d.is_cat) {
+    const uint32_t w = b >> 5;
+    return w < static_cast<uint32_t>(kMaxCatWords) && ((d.bits[w] >> (b & 31u)) & 1u);
+  }
+  if ((d.missing == 1 && b == static_cast<uint32_t>(d.default_bin)) ||
+      (d.missing == 2 && b == static_cast<uint32_t>(d.num_bin - 1))) {
+    return d.default_left != 0;
+  }
+  return b <= static_cast<uint32_t>(d.thr);
+}
+
+__device__ __forceinline__ uint32_t ColBin(const Args& a, int g, int row) {
+  const size_t o = static_cast<size_t>(g) * a.N + row;
+  return a.width == 1 ? a.colbins[o] : reinterpret_cast<const uint16_t*>(a.colbins)[o];
+}
+
+__device__ __forceinline__ int RowAt(const Args& a, int buf, int pos) { return buf < 0 ? pos : a.idx[buf][pos]; }
+
+// block = 256 threads: sum of an int
+__device__ int BlockSumInt(int v, int* sh) {
+  v = WaveSum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  int s = 0;
+  for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) s += sh[i];
+  return s;
+}
+
+__device__ __forceinline__ double SafeGain(const SplitInfo& s) {
+  double g = s.gain;
+  if (g != g) g = kMinScore;
+  return s.feature < 0 ? kMinScore : g;
+}
+
+__device__ __forceinline__ unsigned LcgNext(unsigned* x) {
+  *x = 214013u * *x + 2531011u;
+  return *x;
+}
+__device__ __forceinline__ int RandNextInt(unsigned* x, int lo, int hi) {
+  const int v = static_cast<int>(LcgNext(x) & 0x7FFFFFFFu);
+  return v % (hi - lo) + lo;
+}
+
+__device__ double MonotonePenaltyAt(double pen, int depth) {
+  if (pen >= depth + 1.0) return kEpsilon;
+  if (pen <= 1.0) return 1.0 - pen / pow(2.0, static_cast<double>(depth)) + kEpsilon;
+  return 1.0 - pow(2.0, pen - 1.0 - depth) + kEpsilon;
+}
+
+// ---------------------------------------------------------------------------
+// tree setup
+
+__global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
+  const TreeParams tp = *a.tp;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    Ctl c;
+    c.num_leaves = 1;
+    c.done = 0;
+    c.smaller = 0;
+    c.larger = -1;
+    c.skip = 0;
+    c.num_splits = 0;
+    c.split_leaf = -1;
+    c.new_leaf = -1;
+    c.parent_buf = tp.root_buf;
+    c.parent_start = 0;
+    c.parent_count = tp.root_count;
+    c.target_buf = 0;
+    c.left_count = 0;
+    c.cls = tp.cls;
+    c.scan_round = 0;
+    c.pad = 0;
+    *a.ctl = c;
+    LeafRange r;
+    r.buf = tp.root_buf;
+    r.start = 0;
+    r.count = tp.root_count;
+    r.pad = 0;
+    a.range[0] = r;
+    a.lsum[0] = make_double2(0.0, 0.0);
+    a.gcount[0] = tp.root_gcount;
+    a.depth[0] = 0;
+    a.lout[0] = 0.0;
+  }
+  for (int i = t; i < a.L; i += blockDim.x) {
+    a.slot[i] = i;
+    a.bounds[i] = LeafBounds();
+    a.best[i].Reset();
+  }
+  for (int f = t; f < a.F; f += blockDim.x) a.splittable[f] = 1;
+}
+
+__global__ __launch_bounds__(256) void k_root_sums(Args a) {
+  __shared__ double sh[8];
+  const TreeParams tp = *a.tp;
+  const float2* gh = a.gh + static_cast<size_t>(tp.cls) * a.N;
+  double g = 0.0, h = 0.0;
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tp.root_count; i += stride) {
+    const float2 v = gh[RowAt(a, tp.root_buf, i)];
+    g += v.x;
+    h += v.y;
+  }
+  g = WaveSum(g);
+  h = WaveSum(h);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[w] = g;
+    sh[4 + w] = h;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sg = 0.0, shh = 0.0;
+    for (int i = 0; i < 4; ++i) {
+      sg += sh[i];
+      shh += sh[4 + i];
+    }
+    atomicAdd(&a.lsum[0].x, sg);
+    atomicAdd(&a.lsum[0].y, shh);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// histogram of the smaller leaf into `staging` (fp64), LDS-privatised per block
+
+template <int W>
+__global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
+  extern __shared__ float lds[];
+  const Ctl* cp = a.ctl;
+  if (cp->done || cp->skip) return;
+  const int leaf = cp->smaller;
+  const int cls = cp->cls;
+  const HistTile tile = a.tiles[blockIdx.y];
+  const LeafRange r = a.range[leaf];
+  const int n = r.count;
+  int nb = (n + kHistMinRows - 1) / kHistMinRows;
+  if (nb > static_cast<int>(gridDim.x)) nb = gridDim.x;
+  if (static_cast<int>(blockIdx.x) >= nb) return;
+  const int chunk = (n + nb - 1) / nb;
+  const int rb = blockIdx.x * chunk;
+  const int re = min(n, rb + chunk);
+  int* gst = reinterpret_cast<int*>(lds + 2 * tile.nbins);
+  for (int i = threadIdx.x; i < 2 * tile.nbins; i += blockDim.x) lds[i] = 0.f;
+  for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
+  __syncthreads();
+  const int tpr = tile.d1 - tile.d0;
+  const int rpi = blockDim.x / tpr;
+  const int myr = threadIdx.x / tpr;
+  const int myd = threadIdx.x - myr * tpr;
+  if (myr < rpi) {
+    constexpr int per = 4 / W;
+    const int dw = tile.d0 + myd;
+    const int gfirst = dw * per;
+    const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
+    const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf];
+    for (int p = rb + myr; p < re; p += rpi) {
+      const int row = idx ? idx[r.start + p] : r.start + p;
+      const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
+      const float2 v = gh[row];
+#pragma unroll
+      for (int k = 0; k < per; ++k) {
+        const uint32_t b = W == 1 ? ((word >> (8 * k)) & 0xFFu) : ((word >> (16 * k)) & 0xFFFFu);
+        const int g = gfirst + k;
+        if (b != 0u && g < tile.g1) {
+          const int o = gst[g - tile.g0] + static_cast<int>(b);
+          atomicAdd(&lds[2 * o], v.x);
+          atomicAdd(&lds[2 * o + 1], v.y);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  double* st = a.staging + 2 * static_cast<size_t>(tile.bin0);
+  for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
+    const float g = lds[2 * i], h = lds[2 * i + 1];
+    if (g != 0.f || h != 0.f) {
+      atomicAdd(&st[2 * i], static_cast<double>(g));
+      atomicAdd(&st[2 * i + 1], static_cast<double>(h));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// split scan: one wave per feature
+
+struct Cand {
+  double gain, lg, lh;
+  int lc, thr;
+};
+
+// wave argmax; prefer_high: ties go to the larger threshold
+__device__ __forceinline__ Cand WaveBest(Cand c, bool prefer_high) {
+  int src = threadIdx.x & 63;
+  double bg = c.gain;
+  int bt = c.thr;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(bg, o, kWave);
+    const int ot = __shfl_xor(bt, o, kWave);
+    const int os = __shfl_xor(src, o, kWave);
+    bool take = og > bg;
+    if (og == bg) take = prefer_high ? (ot > bt) : (ot < bt);
+    if (take) {
+      bg = og;
+      bt = ot;
+      src = os;
+    }
+  }
+  Cand r;
+  r.gain = bg;
+  r.thr = bt;
+  r.lg = __shfl(c.lg, src, kWave);
+  r.lh = __shfl(c.lh, src, kWave);
+  r.lc = __shfl(c.lc, src, kWave);
+  return r;
+}
+
+__device__ __forceinline__ void BinValue(const double* H, int mfb, int b, double mg, double mh, double* g, double* h) {
+  if (b == mfb) {
+    *g = mg;
+    *h = mh;
+  } else {
+    const int k = b < mfb ? b : b - 1;
+    *g = H[2 * k];
+    *h = H[2 * k + 1];
+  }
+}
+
+// Numerical threshold search over a full feature histogram (implicit mfb),
+// matching FindBestNumerical in split_math.h. Returns splittable; lane 0's
+// `out` holds the result.
+__device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const double* H, double sg, double sh_raw,
+                                  int n, double po, const LeafBounds& bounds, int rand_thr, double mg, double mh,
+                                  SplitInfo* out) {
+  const int lane = threadIdx.x & 63;
+  const SplitParams& p = a.sp;
+  const double sum_h = sh_raw + 2 * kEpsilon;
+  const double cnt_factor = n / sum_h;
+  const double shift = LeafGain(sg, sum_h, p, n, po) + p.min_gain_to_split;
+  const int nb = fi.num_bin;
+  const bool two_dir = nb > 2 && fi.missing != 0;
+  const bool skip_def = two_dir && fi.missing == 1;
+  const bool na = two_dir && fi.missing == 2;
+  const int top = nb - 1 - (na ? 1 : 0);
+  const bool use_rand = p.extra_trees != 0;
+  const int8_t mono = fi.monotone;
+  // ---- reverse pass (right side accumulates from the top bin down)
+  Cand rb;
+  rb.gain = kMinScore;
+  rb.thr = -1;
+  rb.lg = rb.lh = 0.0;
+  rb.lc = 0;
+  bool sp = false;
+  double cg = 0.0, ch = 0.0;
+  int cc = 0;
+  for (int base = nb - 1; base >= 0; base -= 64) {
+    const int b = base - lane;
+    double g = 0.0, h = 0.0;
+    int c = 0;
+    const bool incl = b >= 0 && !(skip_def && b == fi.default_bin) && !(na && b == nb - 1);
+    if (incl) {
+      BinValue(H, fi.mfb, b, mg, mh, &g, &h);
+      c = RoundCount(h * cnt_factor);
+    }
+    double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
+    int sci = WaveInclusiveScan(c);
+    const double rg = cg + sgi, rh_raw = ch + shi;
+    const int rc = cc + sci;
+    cg += __shfl(sgi, 63, kWave);
+    ch += __shfl(shi, 63, kWave);
+    cc += __shfl(sci, 63, kWave);
+    if (b >= 1 && b <= top && !(skip_def && b == fi.default_bin)) {
+      const int thr = b - 1;
+      const double rh = kEpsilon + rh_raw;
+      const int lc = n - rc;
+      const double lh = sum_h - rh;
+      if (rc >= p.min_data_in_leaf && rh >= p.min_sum_hessian_in_leaf && lc >= p.min_data_in_leaf &&
+          lh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
+        const double lg = sg - rg;
+        const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
+        if (gain > shift) {
+          sp = true;
+          if (gain > rb.gain) {
+            rb.gain = gain;
+            rb.thr = thr;
+            rb.lg = lg;
+            rb.lh = lh;
+            rb.lc = lc;
+          }
+        }
+      }
+    }
+  }
+  // ---- forward pass
+  Cand fb;
+  fb.gain = kMinScore;
+  fb.thr = 0x7fffffff;
+  fb.lg = fb.lh = 0.0;
+  fb.lc = 0;
+  if (two_dir) {
+    cg = ch = 0.0;
+    cc = 0;
+    for (int base = 0; base < nb; base += 64) {
+      const int b = base + lane;
+      double g = 0.0, h = 0.0;
+      int c = 0;
+      const bool incl = b < nb && !(skip_def && b == fi.default_bin);
+      if (incl) {
+        BinValue(H, fi.mfb, b, mg, mh, &g, &h);
+        c = RoundCount(h * cnt_factor);
+      }
+      double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
+      int sci = WaveInclusiveScan(c);
+      const double lg = cg + sgi, lh_raw = ch + shi;
+      const int lc = cc + sci;
+      cg += __shfl(sgi, 63, kWave);
+      ch += __shfl(shi, 63, kWave);
+      cc += __shfl(sci, 63, kWave);
+      if (b <= nb - 2 && !(skip_def && b == fi.default_bin)) {
+        const int thr = b;
+        const double lh = kEpsilon + lh_raw;
+        const int rc = n - lc;
+        const double rh = sum_h - lh;
+        if (lc >= p.min_data_in_leaf && lh >= p.min_sum_hessian_in_leaf && rc >= p.min_data_in_leaf &&
+            rh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
+          const double rg = sg - lg;
+          const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
+          if (gain > shift) {
+            sp = true;
+            if (gain > fb.gain) {
+              fb.gain = gain;
+              fb.thr = thr;
+              fb.lg = lg;
+              fb.lh = lh;
+              fb.lc = lc;
+            }
+          }
+        }
+      }
+    }
+  }
+  const bool any = __any(sp) != 0;
+  const Cand r = WaveBest(rb, true);
+  const Cand f = two_dir ? WaveBest(fb, false) : fb;
+  if (lane == 0) {
+    out->Reset();
+    out->monotone_type = fi.monotone;
+    out->default_left = 1;
+    if (any) {
+      Cand w = r;
+      int dl = 1;
+      if (two_dir && f.gain > r.gain) {
+        w = f;
+        dl = 0;
+      }
+      if (w.gain > kMinScore) {
+        out->threshold = static_cast<uint32_t>(w.thr);
+        out->left_output = LeafOutput(w.lg, w.lh, p, w.lc, po, bounds);
+        out->left_count = w.lc;
+        out->left_sum_gradient = w.lg;
+        out->left_sum_hessian = w.lh - kEpsilon;
+        out->right_output = LeafOutput(sg - w.lg, sum_h - w.lh, p, n - w.lc, po, bounds);
+        out->right_count = n - w.lc;
+        out->right_sum_gradient = sg - w.lg;
+        out->right_sum_hessian = sum_h - w.lh - kEpsilon;
+        out->gain = (w.gain - shift) * fi.penalty;
+        out->default_left = dl;
+      }
+    }
+    if (!two_dir && fi.missing == 2) out->default_left = 0;
+  }
+  return any;
+}
+
+__global__ __launch_bounds__(kScanWaves * 64) void k_scan(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
+  const Ctl c = *a.ctl;
+  if (c.done || c.skip || f >= a.F) return;
+  const DevFeature fi = a.feat[f];
+  const int nst = fi.num_bin - 1;
+  const size_t slot_stride = 2 * static_cast<size_t>(a.TB);
+  const int s_slot = a.slot[c.smaller];
+  const int l_slot = c.larger >= 0 ? a.slot[c.larger] : -1;
+  double* hs = a.slots + s_slot * slot_stride + 2 * static_cast<size_t>(fi.hist_offset);
+  double* hl = l_slot >= 0 ? a.slots + l_slot * slot_stride + 2 * static_cast<size_t>(fi.hist_offset) : nullptr;
+  double* st = a.staging + 2 * static_cast<size_t>(fi.hist_offset);
+  for (int k = lane; k < nst; k += 64) {
+    const double g = st[2 * k], h = st[2 * k + 1];
+    st[2 * k] = 0.0;
+    st[2 * k + 1] = 0.0;
+    hs[2 * k] = g;
+    hs[2 * k + 1] = h;
+    if (hl) {
+      hl[2 * k] -= g;
+      hl[2 * k + 1] -= h;
+    }
+  }
+  __threadfence_block();
+  if (c.num_leaves == 1 && f == 0 && lane == 0) {
+    SplitParams p0 = a.sp;
+    p0.path_smooth = 0.0;
+    a.lout[0] = LeafOutputRaw(a.lsum[0].x, a.lsum[0].y, p0, a.gcount[0], 0.0);
+  }
+  const bool skip_both = !a.used_bytree[f] || (c.larger >= 0 && !a.splittable[static_cast<size_t>(s_slot) * a.F + f]);
+  for (int sel = 0; sel < 2; ++sel) {
+    const int leaf = sel ? c.larger : c.smaller;
+    if (leaf < 0) break;
+    SplitInfo* out = a.scan_out + static_cast<size_t>(sel) * a.F + f;
+    if (skip_both) {
+      if (lane == 0) out->Reset();
+      continue;
+    }
+    const int lslot = sel ? l_slot : s_slot;
+    const double* H = sel ? hl : hs;
+    const double2 sums = a.lsum[leaf];
+    const int n = a.gcount[leaf];
+    double po;
+    if (c.num_leaves == 1) {
+      SplitParams p0 = a.sp;
+      p0.path_smooth = 0.0;
+      po = LeafOutputRaw(sums.x, sums.y, p0, n, 0.0);
+    } else {
+      po = a.lout[leaf];
+    }
+    const LeafBounds bounds = a.bounds[leaf];
+    // mfb reconstruction
+    double sgs = 0.0, shs = 0.0;
+    for (int k = lane; k < nst; k += 64) {
+      sgs += H[2 * k];
+      shs += H[2 * k + 1];
+    }
+    sgs = WaveSum(sgs);
+    shs = WaveSum(shs);
+    const double mg = sums.x - sgs, mh = sums.y - shs;
+    bool sp;
+    if (fi.bin_type == 0) {
+      int rand_thr = 0;
+      if (a.sp.extra_trees) {
+        if (lane == 0 && fi.num_bin - 2 > 0) rand_thr = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
+        rand_thr = __shfl(rand_thr, 0, kWave);
+      }
+      sp = ScanNumericalWave(a, fi, H, sums.x, sums.y, n, po, bounds, rand_thr, mg, mh, out);
+    } else {
+      // categorical: expand the full histogram into scratch, lane 0 runs the sequential scan
+      double* full = a.cat_scratch + static_cast<size_t>(f) * 3 * a.max_cat_bin;
+      int* order = reinterpret_cast<int*>(full + 2 * a.max_cat_bin);
+      for (int b = lane; b < fi.num_bin; b += 64) {
+        double g, h;
+        BinValue(H, fi.mfb, b, mg, mh, &g, &h);
+        full[2 * b] = g;
+        full[2 * b + 1] = h;
+      }
+      __threadfence_block();
+      int spi = 0;
+      if (lane == 0) {
+        FeatureScanMeta m;
+        m.num_bin = fi.num_bin;
+        m.default_bin = static_cast<uint32_t>(fi.default_bin);
+        m.missing_type = fi.missing;
+        m.bin_type = fi.bin_type;
+        m.monotone = fi.monotone;
+        m.penalty = fi.penalty;
+        m.rand_threshold = 0;
+        if (a.sp.extra_trees) {
+          if (fi.num_bin <= a.sp.max_cat_to_onehot) {
+            if (fi.num_bin - 1 > 0) m.rand_threshold = RandNextInt(&a.rng[f], 1, fi.num_bin);
+          } else {
+            const double cf = n / (sums.y + 2 * kEpsilon);
+            int used = 0;
+            for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(full[2 * b + 1] * cf) >= a.sp.cat_smooth;
+            int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
+            int max_thr = max(min(max_num_cat, used) - 1, 0);
+            if (max_thr > 0) m.rand_threshold = RandNextInt(&a.rng[f], 0, max_thr);
+          }
+        }
+        SplitInfo tmp;
+        tmp.Reset();
+        spi = FindBestCategorical(full, m, a.sp, sums.x, sums.y, n, po, bounds, order, &tmp) ? 1 : 0;
+        *out = tmp;
+      }
+      sp = __shfl(spi, 0, kWave) != 0;
+    }
+    if (lane == 0) {
+      a.splittable[static_cast<size_t>(lslot) * a.F + f] = sp ? 1 : 0;
+      if (!sp) {
+        out->Reset();
+      } else {
+        out->feature = f;
+        if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, a.depth[leaf]);
+        if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// best split of the new leaves, then the best leaf overall
+
+__device__ __forceinline__ bool CandBetter(double ga, int fa, int la, double gb, int fb, int lb) {
+  if (ga != gb) return ga > gb;
+  if (fa != fb) return fa < fb;
+  return la < lb;
+}
+
+__global__ __launch_bounds__(kNodeThreads) void k_select(Args a) {
+  __shared__ double s_g[kNodeThreads];
+  __shared__ int s_f[kNodeThreads];
+  __shared__ int s_l[kNodeThreads];
+  Ctl* cp = a.ctl;
+  if (cp->done) return;
+  const int t = threadIdx.x;
+  const Ctl c = *cp;
+  if (!c.skip) {
+    for (int sel = 0; sel < 2; ++sel) {
+      const int leaf = sel ? c.larger : c.smaller;
+      if (leaf < 0) continue;
+      double bg = kMinScore;
+      int bf = 0x7fffffff;
+      for (int f = t; f < a.F; f += blockDim.x) {
+        const SplitInfo& s = a.scan_out[static_cast<size_t>(sel) * a.F + f];
+        if (s.feature < 0) continue;
+        const double g = SafeGain(s);
+        if (CandBetter(g, f, 0, bg, bf, 0)) {
+          bg = g;
+          bf = f;
+        }
+      }
+      s_g[t] = bg;
+      s_f[t] = bf;
+      __syncthreads();
+      for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
+        if (t < o && CandBetter(s_g[t + o], s_f[t + o], 0, s_g[t], s_f[t], 0)) {
+          s_g[t] = s_g[t + o];
+          s_f[t] = s_f[t + o];
+        }
+        __syncthreads();
+      }
+      if (t == 0) {
+        if (s_f[0] != 0x7fffffff) a.best[leaf] = a.scan_out[static_cast<size_t>(sel) * a.F + s_f[0]];
+        else a.best[leaf].Reset();
+      }
+      __syncthreads();
+    }
+  }
+  double bg = kMinScore;
+  int bf = 0x7fffffff, bl = 0x7fffffff;
+  for (int l = t; l < c.num_leaves; l += blockDim.x) {
+    const SplitInfo& s = a.best[l];
+    const double g = SafeGain(s);
+    const int f = s.feature < 0 ? 0x7fffffff : s.feature;
+    if (CandBetter(g, f, l, bg, bf, bl)) {
+      bg = g;
+      bf = f;
+      bl = l;
+    }
+  }
+  s_g[t] = bg;
+  s_f[t] = bf;
+  s_l[t] = bl;
+  __syncthreads();
+  for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
+    if (t < o && CandBetter(s_g[t + o], s_f[t + o], s_l[t + o], s_g[t], s_f[t], s_l[t])) {
+      s_g[t] = s_g[t + o];
+      s_f[t] = s_f[t + o];
+      s_l[t] = s_l[t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (!c.skip) cp->scan_round = c.scan_round + 1;
+    const int l = s_l[0];
+    if (l == 0x7fffffff || a.best[l].feature < 0 || !(a.best[l].gain > 0.0)) {
+      cp->done = 1;
+      return;
+    }
+    const LeafRange pr = a.range[l];
+    cp->split_leaf = l;
+    cp->new_leaf = c.num_leaves;
+    cp->parent_buf = pr.buf;
+    cp->parent_start = pr.start;
+    cp->parent_count = pr.count;
+    cp->target_buf = pr.buf == 0 ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// stable partition of the split leaf's row indices
+
+__device__ void LoadSplitDesc(const Args& a, int leaf, SplitDesc* d) {
+  const SplitInfo& s = a.best[leaf];
+  const DevFeature fi = a.feat[s.feature];
+  d->group = fi.group;
+  d->offset = fi.offset;
+  d->num_bin = fi.num_bin;
+  d->mfb = fi.mfb;
+  d->default_bin = fi.default_bin;
+  d->missing = fi.missing;
+  d->thr = static_cast<int>(s.threshold);
+  d->default_left = s.default_left;
+  d->is_cat = fi.bin_type != 0;
+  for (int w = 0; w < kMaxCatWords; ++w) d->bits[w] = d->is_cat ? s.cat_bitset[w] : 0u;
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
+  __shared__ SplitDesc d;
+  __shared__ int sh[8];
+  const Ctl* cp = a.ctl;
+  if (cp->done) return;
+  const int leaf = cp->split_leaf;
+  const int pbuf = cp->parent_buf, pstart = cp->parent_start, pcount = cp->parent_count;
+  if (threadIdx.x == 0) LoadSplitDesc(a, leaf, &d);
+  __syncthreads();
+  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int cnt = 0;
+#pragma unroll 4
+    for (int k = 0; k < kPartIters; ++k) {
+      const int pos = tile * kTileRows + k * kPartThreads + threadIdx.x;
+      if (pos < pcount) {
+        const int row = RowAt(a, pbuf, pstart + pos);
+        cnt += GoLeft(d, ColBin(a, d.group, row)) ? 1 : 0;
+      }
+    }
+    cnt = BlockSumInt(cnt, sh);
+    if (threadIdx.x == 0) a.tile_cnt[tile] = cnt;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_part_scan(Args a) {
+  __shared__ int sh[1024];
+  Ctl* cp = a.ctl;
+  if (cp->done) return;
+  const int pcount = cp->parent_count;
+  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
+  const int t = threadIdx.x;
+  const int per = (ntiles + blockDim.x - 1) / blockDim.x;
+  const int b = t * per, e = min(ntiles, b + per);
+  int s = 0;
+  for (int i = b; i < e; ++i) s += a.tile_cnt[i];
+  sh[t] = s;
+  __syncthreads();
+  for (int o = 1; o < static_cast<int>(blockDim.x); o <<= 1) {
+    const int v = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += v;
+    __syncthreads();
+  }
+  int run = sh[t] - s;  // exclusive prefix
+  for (int i = b; i < e; ++i) {
+    const int c = a.tile_cnt[i];
+    a.tile_off[i] = run;
+    run += c;
+  }
+  if (t == static_cast<int>(blockDim.x) - 1) cp->left_count = sh[t];
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
+  __shared__ SplitDesc d;
+  __shared__ int s_wl[kPartThreads / 64];
+  __shared__ int s_wv[kPartThreads / 64];
+  const Ctl* cp = a.ctl;
+  if (cp->done) return;
+  const int leaf = cp->split_leaf;
+  const int pbuf = cp->parent_buf, pstart = cp->parent_start, pcount = cp->parent_count;
+  const int nl_total = cp->left_count;
+  int* out = a.idx[cp->target_buf] + pstart;
+  if (threadIdx.x == 0) LoadSplitDesc(a, leaf, &d);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int lbase = a.tile_off[tile];
+    int rbase = tile * kTileRows - lbase;
+    for (int k = 0; k < kPartIters; ++k) {
+      const int pos = tile * kTileRows + k * kPartThreads + threadIdx.x;
+      const bool valid = pos < pcount;
+      int row = 0;
+      bool left = false;
+      if (valid) {
+        row = RowAt(a, pbuf, pstart + pos);
+        left = GoLeft(d, ColBin(a, d.group, row));
+      }
+      const unsigned long long ml = __ballot(valid && left);
+      const unsigned long long mv = __ballot(valid);
+      if (lane == 0) {
+        s_wl[w] = __popcll(ml);
+        s_wv[w] = __popcll(mv);
+      }
+      __syncthreads();
+      int pl = 0, pv = 0, tl = 0, tv = 0;
+      for (int i = 0; i < kPartThreads / 64; ++i) {
+        if (i < w) {
+          pl += s_wl[i];
+          pv += s_wv[i];
+        }
+        tl += s_wl[i];
+        tv += s_wv[i];
+      }
+      if (valid) {
+        const int rl = pl + __popcll(ml & lt_mask);
+        const int rv = pv + __popcll(mv & lt_mask);
+        if (left) out[lbase + rl] = row;
+        else out[nl_total + rbase + (rv - rl)] = row;
+      }
+      lbase += tl;
+      rbase += tv - tl;
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bookkeeping after a split (BeforeFindBestSplit for the two children)
+
+__global__ __launch_bounds__(kNodeThreads) void k_post(Args a) {
+  __shared__ int s_skip, s_from, s_to;
+  Ctl* cp = a.ctl;
+  if (cp->done) return;
+  if (threadIdx.x == 0) {
+    Ctl c = *cp;
+    const int l = c.split_leaf, r = c.new_leaf;
+    const SplitInfo info = a.best[l];
+    const int lc = c.left_count, rc = c.parent_count - lc;
+    LeafRange rl, rr;
+    rl.buf = rr.buf = c.target_buf;
+    rl.start = c.parent_start;
+    rl.count = lc;
+    rr.start = c.parent_start + lc;
+    rr.count = rc;
+    rl.pad = rr.pad = 0;
+    a.range[l] = rl;
+    a.range[r] = rr;
+    const int glc = a.distributed ? info.left_count : lc;
+    const int grc = a.distributed ? info.right_count : rc;
+    SplitRec& rec = a.rec[c.num_splits];
+    rec.leaf = l;
+    rec.left_count = glc;
+    rec.right_count = grc;
+    rec.pad = 0;
+    rec.info = info;
+    c.num_splits += 1;
+    c.num_leaves += 1;
+    a.lsum[l] = make_double2(info.left_sum_gradient, info.left_sum_hessian);
+    a.lsum[r] = make_double2(info.right_sum_gradient, info.right_sum_hessian);
+    a.lout[l] = info.left_output;
+    a.lout[r] = info.right_output;
+    a.gcount[l] = glc;
+    a.gcount[r] = grc;
+    const int d = a.depth[l] + 1;
+    a.depth[l] = d;
+    a.depth[r] = d;
+    LeafBounds bl = a.bounds[l], br = bl;
+    if (a.use_monotone && info.num_cat_threshold == 0) {
+      const double mid = (info.left_output + info.right_output) / 2.0f;
+      if (info.monotone_type < 0) {
+        bl.min = fmax(bl.min, mid);
+        br.max = fmin(br.max, mid);
+      } else if (info.monotone_type > 0) {
+        bl.max = fmin(bl.max, mid);
+        br.min = fmax(br.min, mid);
+      }
+    }
+    a.bounds[l] = bl;
+    a.bounds[r] = br;
+    int smaller, larger;
+    if (glc < grc) {
+      smaller = l;
+      larger = r;
+    } else {
+      smaller = r;
+      larger = l;
+    }
+    const int md = a.sp.min_data_in_leaf;
+    const bool skip = (a.max_depth > 0 && d >= a.max_depth) || (grc < md * 2 && glc < md * 2);
+    c.smaller = smaller;
+    c.larger = larger;
+    c.skip = skip ? 1 : 0;
+    if (skip) {
+      a.best[l].Reset();
+      a.best[r].Reset();
+    } else {
+      const int ps = a.slot[l];
+      if (larger == r) {
+        a.slot[r] = ps;
+        a.slot[l] = r;
+      } else {
+        a.slot[r] = r;
+      }
+      s_from = ps;
+      s_to = a.slot[smaller];
+    }
+    s_skip = skip ? 1 : 0;
+    *cp = c;
+  }
+  __syncthreads();
+  if (!s_skip) {
+    const uint8_t* src = a.splittable + static_cast<size_t>(s_from) * a.F;
+    uint8_t* dst = a.splittable + static_cast<size_t>(s_to) * a.F;
+    for (int f = threadIdx.x; f < a.F; f += blockDim.x) dst[f] = src[f];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// score update: traverse one uploaded tree over the packed rows
+
+__global__ __launch_bounds__(256) void k_add_tree(const uint32_t* __restrict__ rowbins, int stride_dw, int width,
+                                                  int N, const DevNode* __restrict__ nodes, int num_nodes,
+                                                  const uint32_t* __restrict__ cat_bits,
+                                                  const double* __restrict__ leaf_value, double* __restrict__ score) {
+  extern __shared__ DevNode s_nodes[];
+  for (int i = threadIdx.x; i < num_nodes; i += blockDim.x) s_nodes[i] = nodes[i];
+  __syncthreads();
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+    const uint8_t* row = reinterpret_cast<const uint8_t*>(rowbins + static_cast<size_t>(i) * stride_dw);
+    int node = 0;
+    while (node >= 0) {
+      const DevNode& nd = s_nodes[node];
+      const uint32_t gb = width == 1 ? row[nd.group] : reinterpret_cast<const uint16_t*>(row)[nd.group];
+      const uint32_t b = DecodeBin(nd.offset, nd.num_bin, nd.mfb, gb);
+      bool left;
+      if (nd.decision & 1) {
+        const uint32_t wd = b >> 5;
+        left = static_cast<int>(wd) < nd.cat_nwords && ((cat_bits[nd.cat_begin + wd] >> (b & 31u)) & 1u);
+      } else if ((nd.missing == 1 && b == static_cast<uint32_t>(nd.default_bin)) ||
+                 (nd.missing == 2 && b == static_cast<uint32_t>(nd.num_bin - 1))) {
+        left = (nd.decision & 2) != 0;
+      } else {
+        left = b <= static_cast<uint32_t>(nd.threshold);
+      }
+      node = left ? nd.left : nd.right;
+    }
+    score[i] += leaf_value[~node];
+  }
+}
+
+// ---------------------------------------------------------------------------
+
+template <typename T>
+class PinnedBuf {
+ public:
+  ~PinnedBuf() {
+    if (p_) (void)hipHostFree(p_);
+  }
+  T* Get(size_t n) {
+    if (n > n_) {
+      if (p_) HIP_CHECK(hipHostFree(p_));
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_), std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault));
+      n_ = n;
+    }
+    return p_;
+  }
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+class DeviceTreeLearner : public TreeLearner {
+ public:
+  DeviceTreeLearner(const Config* config, bool data_parallel) : config_(config), data_parallel_(data_parallel) {}
+
+  ~DeviceTreeLearner() override {
+    if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  void Init(const Dataset* train, bool is_constant_hessian) override {
+    (void)is_constant_hessian;
+    data_ = train;
+    N_ = train->num_data();
+    F_ = train->num_features();
+    G_ = train->num_groups();
+    TB_ = train->num_total_bin();
+    width_ = train->bin_width();
+    stride_dw_ = train->row_stride() / 4;
+    if (data_parallel_ && !CommActive() && Network::num_machines() > 1) {
+      Log::Fatal("Data-parallel HIP training needs an RCCL communicator (LGBM_DeviceCommInit)");
+    }
+    distributed_ = data_parallel_ && CommActive();
+    device_id_ = CommActive() ? CommDevice() : std::max(0, config_->gpu_device_id);
+    HIP_CHECK(hipSetDevice(device_id_));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device_id_));
+    device_name_ = std::string(prop.name) + " (" + prop.gcnArchName + ")";
+    num_cu_ = prop.multiProcessorCount;
+    if (!stream_) HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (!config_->interaction_constraints_vector.empty()) {
+      Log::Fatal("interaction_constraints are not supported by the HIP learner yet; use device_type=cpu");
+    }
+    if (!config_->forcedsplits_filename.empty()) {
+      Log::Fatal("forcedsplits_filename is not supported by the HIP learner yet; use device_type=cpu");
+    }
+    UploadData();
+    ResetConfig(config_);
+    Log::Info("HIP tree learner on %s: %d rows, %d features, %d groups, %d bins%s", device_name_.c_str(), N_, F_, G_,
+              TB_, distributed_ ? " (data-parallel over RCCL)" : "");
+  }
+
+  void ResetConfig(const Config* config) override {
+    config_ = config;
+    col_sampler_.Init(data_, config_);
+    L_ = std::max(2, config_->num_leaves);
+    AllocState();
+    InvalidateGraph();
+  }
+
+  void SetBaggingData(const data_size_t* used, data_size_t n) override {
+    if (used == nullptr || n >= N_) {
+      bag_cnt_ = N_;
+      use_bag_ = false;
+    } else {
+      bag_cnt_ = n;
+      use_bag_ = true;
+      idx_[2].Upload(used, n, stream_);
+    }
+  }
+
+  std::unique_ptr<Tree> Train(const score_t* g, const score_t* h, bool is_first_tree) override {
+    DeviceSetGradients(g, h, 1);
+    return DeviceTrain(0, is_first_tree);
+  }
+
+  std::unique_ptr<Tree> FitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred, const score_t* g,
+                                          const score_t* h) override {
+    // refit is a one-off host pass over leaf assignments; the host learner computes it
+    SerialTreeLearner host(config_);
+    host.Init(data_, false);
+    return host.FitByExistingTree(old_tree, leaf_pred, g, h);
+  }
+
+  void AddPredictionToScore(const Tree* tree, double* out_score) const override {
+    tree->AddPredictionToScore(*data_, N_, out_score);
+  }
+
+  void RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj, const double* score, data_size_t,
+                       const data_size_t*, data_size_t) const override {
+    if (obj == nullptr || !obj->IsRenewTreeOutput()) return;
+    const int nl = tree->num_leaves();
+    std::vector<double> outs(nl, 0.0);
+    std::vector<int> nonzero(nl, 1);
+    for (int l = 0; l < nl; ++l) {
+      auto rows = LeafIndices(l);
+      if (!rows.empty()) outs[l] = obj->RenewTreeOutput(tree->LeafOutput(l), score, rows.data(), static_cast<data_size_t>(rows.size()));
+      else nonzero[l] = 0;
+    }
+    if (Network::num_machines() > 1) {
+      Network::GlobalSum(&outs);
+      Network::GlobalSum(&nonzero);
+      for (int l = 0; l < nl; ++l) outs[l] = nonzero[l] > 0 ? outs[l] / nonzero[l] : 0.0;
+    }
+    for (int l = 0; l < nl; ++l) tree->SetLeafOutput(l, outs[l]);
+  }
+
+  std::vector<data_size_t> LeafIndices(int leaf) const override {
+    if (leaf < 0 || leaf >= static_cast<int>(h_range_.size())) return {};
+    const LeafRange r = h_range_[leaf];
+    std::vector<data_size_t> out(r.count);
+    if (r.count == 0) return out;
+    if (r.buf < 0) {
+      for (int i = 0; i < r.count; ++i) out[i] = r.start + i;
+    } else {
+      HIP_CHECK(hipMemcpyAsync(out.data(), idx_[r.buf].get() + r.start, sizeof(int) * r.count, hipMemcpyDeviceToHost,
+                               stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    return out;
+  }
+
+  // ---- device-resident boosting
+  bool OwnsScore() const override { return true; }
+
+  bool SupportsDeviceGradients(const ObjectiveFunction* obj) const override {
+    if (obj == nullptr) return false;
+    switch (obj->device_kind()) {
+      case DeviceGradKind::kPointwise:
+        return obj->pointwise() != nullptr && obj->effective_label() != nullptr;
+      case DeviceGradKind::kSoftmax:
+        return obj->effective_label() != nullptr;
+      case DeviceGradKind::kLambdarank: {
+        const Metadata& md = data_->metadata();
+        if (md.positions() != nullptr || md.num_queries() == 0) return false;
+        const data_size_t* qb = md.query_boundaries();
+        for (data_size_t q = 0; q < md.num_queries(); ++q) {
+          if (qb[q + 1] - qb[q] > kMaxDeviceQuery) return false;
+        }
+        return true;
+      }
+      default:
+        return false;
+    }
+  }
+
+  void DeviceInitScore(const std::vector<double>& host_score, int num_tree_per_iter) override {
+    K_ = num_tree_per_iter;
+    score_.Resize(static_cast<size_t>(K_) * N_);
+    score_.Upload(host_score, stream_);
+    gh_.Resize(static_cast<size_t>(K_) * N_);
+    if (graph_exec_) InvalidateGraph();
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  void DeviceComputeGradients(const ObjectiveFunction* obj) override {
+    PrepareObjective(obj);
+    switch (obj->device_kind()) {
+      case DeviceGradKind::kPointwise:
+        LaunchPointwiseGrad(*obj->pointwise(), score_.get(), label_.get(), weight_.size() ? weight_.get() : nullptr,
+                            aux_.size() ? aux_.get() : nullptr, N_, gh_.get(), stream_);
+        break;
+      case DeviceGradKind::kSoftmax:
+        LaunchSoftmaxGrad(K_, static_cast<double>(K_) / (K_ - 1.0), score_.get(), label_.get(),
+                          weight_.size() ? weight_.get() : nullptr, N_, gh_.get(), stream_);
+        break;
+      case DeviceGradKind::kLambdarank: {
+        RankKernelArgs ra = rank_args_;
+        ra.score = score_.get();
+        ra.gh = gh_.get();
+        LaunchLambdarankGrad(ra, stream_);
+        break;
+      }
+      default:
+        Log::Fatal("Objective %s has no device gradient kernel", obj->GetName());
+    }
+  }
+
+  void DeviceSetGradients(const score_t* g, const score_t* h, int num_class) override {
+    const size_t n = static_cast<size_t>(num_class) * N_;
+    if (gh_.size() < n) gh_.Resize(n);
+    float2* p = pin_gh_.Get(n);
+    for (size_t i = 0; i < n; ++i) p[i] = make_float2(g[i], h[i]);
+    HIP_CHECK(hipMemcpyAsync(gh_.get(), p, n * sizeof(float2), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  void DeviceGetGradients(std::vector<score_t>* g, std::vector<score_t>* h) const override {
+    const size_t n = static_cast<size_t>(K_) * N_;
+    std::vector<float2> tmp(n);
+    HIP_CHECK(hipMemcpyAsync(tmp.data(), gh_.get(), n * sizeof(float2), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    g->resize(n);
+    h->resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      (*g)[i] = tmp[i].x;
+      (*h)[i] = tmp[i].y;
+    }
+  }
+
+  void DeviceGetScore(std::vector<double>* out) const override {
+    out->resize(static_cast<size_t>(K_) * N_);
+    score_.Download(out->data(), out->size(), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  void DeviceAddConstant(double v, int k) override {
+    LaunchAddConstant(score_.get() + static_cast<size_t>(k) * N_, N_, v, stream_);
+  }
+
+  void DeviceAddTreeToScore(const Tree* tree, int k) override {
+    double* s = score_.get() + static_cast<size_t>(k) * N_;
+    if (tree->num_leaves() <= 1) {
+      if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, N_, tree->LeafOutput(0), stream_);
+      return;
+    }
+    if (tree->is_linear()) Log::Fatal("Linear trees cannot be applied on the device");
+    const int nn = tree->num_leaves() - 1;
+    const auto& cb = tree->cat_boundaries_inner();
+    const auto& ct = tree->cat_threshold_inner();
+    // pack nodes + leaf values + categorical words into one pinned upload
+    const size_t node_bytes = sizeof(DevNode) * nn;
+    const size_t leaf_bytes = sizeof(double) * tree->num_leaves();
+    const size_t cat_bytes = sizeof(uint32_t) * std::max<size_t>(1, ct.size());
+    const size_t total = node_bytes + leaf_bytes + cat_bytes;
+    char* hp = pin_tree_.Get(total);
+    DevNode* nodes = reinterpret_cast<DevNode*>(hp);
+    for (int i = 0; i < nn; ++i) {
+      const FeatureInfo& fi = data_->feature(tree->split_feature_inner(i));
+      DevNode& d = nodes[i];
+      d.group = fi.group;
+      d.offset = fi.offset;
+      d.num_bin = fi.num_bin;
+      d.mfb = static_cast<int>(fi.mfb);
+      d.default_bin = static_cast<int>(fi.default_bin);
+      const int8_t dt = tree->decision_type(i);
+      d.missing = Tree::GetMissingType(dt);
+      d.decision = (Tree::GetDecisionType(dt, kCategoricalMask) ? 1 : 0) | (Tree::GetDecisionType(dt, kDefaultLeftMask) ? 2 : 0);
+      d.left = tree->left_child(i);
+      d.right = tree->right_child(i);
+      if (d.decision & 1) {
+        const int ci = static_cast<int>(tree->threshold_in_bin(i));
+        d.cat_begin = cb[ci];
+        d.cat_nwords = cb[ci + 1] - cb[ci];
+        d.threshold = 0;
+      } else {
+        d.threshold = static_cast<int>(tree->threshold_in_bin(i));
+        d.cat_begin = 0;
+        d.cat_nwords = 0;
+      }
+    }
+    double* lv = reinterpret_cast<double*>(hp + node_bytes);
+    for (int l = 0; l < tree->num_leaves(); ++l) lv[l] = tree->LeafOutput(l);
+    uint32_t* cw = reinterpret_cast<uint32_t*>(hp + node_bytes + leaf_bytes);
+    for (size_t i = 0; i < ct.size(); ++i) cw[i] = ct[i];
+    tree_buf_.Resize(std::max(tree_buf_.size(), total));
+    HIP_CHECK(hipMemcpyAsync(tree_buf_.get(), hp, total, hipMemcpyHostToDevice, stream_));
+    const DevNode* dn = reinterpret_cast<const DevNode*>(tree_buf_.get());
+    const double* dl = reinterpret_cast<const double*>(tree_buf_.get() + node_bytes);
+    const uint32_t* dc = reinterpret_cast<const uint32_t*>(tree_buf_.get() + node_bytes + leaf_bytes);
+    const int grid = std::min(DivUp(N_, 256), num_cu_ * 8);
+    k_add_tree<<<std::max(grid, 1), 256, node_bytes, stream_>>>(rowbins_.get(), stride_dw_, width_, N_, dn, nn, dc, dl, s);
+    HIP_CHECK(hipGetLastError());
+    // the pinned staging buffer is reused by the next call: wait for the copy
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  std::unique_ptr<Tree> DeviceTrain(int class_id, bool is_first_tree) override {
+    (void)is_first_tree;
+    ScopedTimer timer("DeviceTreeLearner::Train");
+    // per-tree inputs: root rows, class, feature sampling
+    TreeParams* tp = pin_tp_.Get(1);
+    tp->root_buf = use_bag_ ? 2 : -1;
+    tp->root_count = use_bag_ ? bag_cnt_ : N_;
+    tp->cls = class_id;
+    int gcount = tp->root_count;
+    if (distributed_) gcount = Network::GlobalSyncUpBySum(gcount);
+    tp->root_gcount = gcount;
+    HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
+    col_sampler_.ResetByTree();
+    const auto& used = col_sampler_.is_feature_used_bytree();
+    uint8_t* um = pin_mask_.Get(static_cast<size_t>(F_) * (1 + 2 * L_));
+    for (int f = 0; f < F_; ++f) um[f] = used[f] ? 1 : 0;
+    HIP_CHECK(hipMemcpyAsync(used_bytree_.get(), um, F_, hipMemcpyHostToDevice, stream_));
+    if (use_bynode_) {
+      Tree dummy(2);
+      uint8_t* bm = um + F_;
+      for (int r = 0; r < 2 * L_; ++r) {
+        auto m = col_sampler_.GetByNode(&dummy, 0);
+        for (int f = 0; f < F_; ++f) bm[static_cast<size_t>(r) * F_ + f] = m[f] ? 1 : 0;
+      }
+      HIP_CHECK(hipMemcpyAsync(bynode_.get(), bm, static_cast<size_t>(2 * L_) * F_, hipMemcpyHostToDevice, stream_));
+    }
+    const bool use_graph = config_->device_use_graph && !distributed_;
+    if (use_graph) {
+      if (!graph_exec_) CaptureGraph();
+      HIP_CHECK(hipGraphLaunch(graph_exec_, stream_));
+    } else {
+      EnqueueTree();
+    }
+    // results
+    Ctl* hc = pin_ctl_.Get(1);
+    SplitRec* hr = pin_rec_.Get(L_);
+    LeafRange* hrange = pin_range_.Get(L_);
+    double* hlo = pin_lout_.Get(1);
+    HIP_CHECK(hipMemcpyAsync(hc, ctl_.get(), sizeof(Ctl), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hr, rec_.get(), sizeof(SplitRec) * (L_ - 1), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hrange, range_.get(), sizeof(LeafRange) * L_, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hlo, lout_.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    auto tree = std::make_unique<Tree>(L_, false, false);
+    tree->SetLeafOutput(0, hlo[0]);
+    for (int s = 0; s < hc->num_splits; ++s) {
+      const SplitRec& r = hr[s];
+      const SplitInfo& info = r.info;
+      const FeatureInfo& fi = data_->feature(info.feature);
+      const BinMapper& mapper = data_->inner_mapper(info.feature);
+      const float gain = static_cast<float>(info.gain + config_->min_gain_to_split);
+      if (fi.bin_type == BinType::Numerical) {
+        tree->Split(r.leaf, info.feature, fi.real_index, info.threshold, mapper.BinToValue(info.threshold),
+                    info.left_output, info.right_output, r.left_count, r.right_count, info.left_sum_hessian,
+                    info.right_sum_hessian, gain, fi.missing, info.default_left != 0);
+      } else {
+        int nwords = 0;
+        std::vector<int> cats;
+        for (int w = 0; w < kMaxCatWords; ++w) {
+          if (info.cat_bitset[w]) nwords = w + 1;
+          for (int j = 0; j < 32; ++j) {
+            if ((info.cat_bitset[w] >> j) & 1) cats.push_back(mapper.bin_to_category()[w * 32 + j]);
+          }
+        }
+        std::vector<uint32_t> inner(info.cat_bitset, info.cat_bitset + nwords);
+        std::vector<uint32_t> raw = common::ConstructBitset(cats.data(), static_cast<int>(cats.size()));
+        tree->SplitCategorical(r.leaf, info.feature, fi.real_index, inner.data(), nwords, raw.data(),
+                               static_cast<int>(raw.size()), info.left_output, info.right_output, r.left_count,
+                               r.right_count, info.left_sum_hessian, info.right_sum_hessian, gain, fi.missing);
+      }
+    }
+    h_range_.assign(hrange, hrange + hc->num_leaves);
+    tree->RecomputeMaxDepth();
+    return tree;
+  }
+
+  std::string DeviceName() const override { return device_name_; }
+
+ private:
+  void UploadData() {
+    // packed rows
+    const size_t rb = static_cast<size_t>(N_) * stride_dw_;
+    rowbins_.Resize(std::max<size_t>(rb, 1));
+    rowbins_.Upload(reinterpret_cast<const uint32_t*>(data_->bins()), rb, stream_);
+    // group-major copy
+    const size_t cb = static_cast<size_t>(G_) * N_ * width_;
+    std::vector<uint8_t> col(std::max<size_t>(cb, 1));
+    const uint8_t* bins = data_->bins();
+    const int stride = data_->row_stride();
+#pragma omp parallel for schedule(static)
+    for (int g = 0; g < G_; ++g) {
+      if (width_ == 1) {
+        uint8_t* dst = col.data() + static_cast<size_t>(g) * N_;
+        for (data_size_t i = 0; i < N_; ++i) dst[i] = bins[static_cast<size_t>(i) * stride + g];
+      } else {
+        uint16_t* dst = reinterpret_cast<uint16_t*>(col.data()) + static_cast<size_t>(g) * N_;
+        for (data_size_t i = 0; i < N_; ++i) {
+          dst[i] = reinterpret_cast<const uint16_t*>(bins + static_cast<size_t>(i) * stride)[g];
+        }
+      }
+    }
+    colbins_.Upload(col, stream_);
+    // features / groups
+    std::vector<DevFeature> feats(std::max(F_, 1));
+    max_cat_bin_ = 1;
+    has_cat_ = false;
+    for (int f = 0; f < F_; ++f) {
+      const FeatureInfo& fi = data_->feature(f);
+      DevFeature& d = feats[f];
+      std::memset(&d, 0, sizeof(d));
+      d.group = fi.group;
+      d.offset = fi.offset;
+      d.num_bin = fi.num_bin;
+      d.mfb = static_cast<int>(fi.mfb);
+      d.default_bin = static_cast<int>(fi.default_bin);
+      d.hist_offset = fi.hist_offset;
+      d.missing = static_cast<int8_t>(fi.missing);
+      d.bin_type = static_cast<int8_t>(fi.bin_type);
+      d.monotone = fi.monotone;
+      d.penalty = fi.penalty;
+      if (fi.bin_type == BinType::Categorical) {
+        has_cat_ = true;
+        max_cat_bin_ = std::max(max_cat_bin_, fi.num_bin);
+      }
+    }
+    feat_.Upload(feats, stream_);
+    std::vector<int> gs(std::max(G_, 1));
+    for (int g = 0; g < G_; ++g) gs[g] = data_->group(g).hist_start;
+    gstart_.Upload(gs, stream_);
+    BuildTiles();
+    // labels / weights for the device objectives are uploaded lazily
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  void BuildTiles() {
+    const int per = 4 / width_;
+    const int max_bins = kHistLdsBytes / 8 - 64;
+    const int max_dw = kHistThreads / 2;
+    std::vector<HistTile> tiles;
+    int d = 0;
+    const int nd = DivUp(G_, per);
+    while (d < nd) {
+      HistTile t;
+      t.d0 = d;
+      t.g0 = d * per;
+      t.bin0 = data_->group(t.g0).hist_start;
+      int bins = 0;
+      int e = d;
+      while (e < nd && e - d < max_dw) {
+        int wb = 0;
+        for (int g = e * per; g < std::min(G_, (e + 1) * per); ++g) wb += data_->group(g).num_bin;
+        if (bins + wb > max_bins && e > d) break;
+        bins += wb;
+        ++e;
+      }
+      t.d1 = e;
+      t.g1 = std::min(G_, e * per);
+      t.nbins = bins;
+      tiles.push_back(t);
+      hist_lds_bytes_ = std::max(hist_lds_bytes_, static_cast<size_t>(bins) * 8 + sizeof(int) * (t.g1 - t.g0) + 16);
+      d = e;
+    }
+    if (hist_lds_bytes_ > 64 * 1024) {
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(width_ == 1 ? k_hist<1> : k_hist<2>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
+    }
+    num_tiles_ = static_cast<int>(tiles.size());
+    tiles_.Upload(tiles, stream_);
+  }
+
+  void AllocState() {
+    const size_t L = L_;
+    tparams_.Resize(1);
+    ctl_.Resize(1);
+    range_.Resize(L);
+    lsum_.Resize(L);
+    lout_.Resize(L);
+    gcount_.Resize(L);
+    depth_.Resize(L);
+    slot_.Resize(L);
+    bounds_.Resize(L);
+    best_.Resize(L);
+    rec_.Resize(L);
+    slots_.Resize(L * 2 * static_cast<size_t>(TB_));
+    staging_.Resize(2 * static_cast<size_t>(TB_));
+    staging_.Zero(stream_);
+    splittable_.Resize(L * F_);
+    scan_out_.Resize(2 * static_cast<size_t>(F_));
+    max_tiles_ = std::max(1, DivUp(N_, kTileRows));
+    tile_cnt_.Resize(max_tiles_);
+    tile_off_.Resize(max_tiles_);
+    used_bytree_.Resize(std::max(F_, 1));
+    use_bynode_ = config_->feature_fraction_bynode < 1.0;
+    if (use_bynode_) bynode_.Resize(2 * L * F_);
+    for (int i = 0; i < 3; ++i) {
+      if (i < 2) idx_[i].Resize(std::max(N_, 1));
+    }
+    if (idx_[2].size() == 0) idx_[2].Resize(1);
+    // extra-trees streams: Random(extra_seed + f) per feature, persistent across trees
+    std::vector<unsigned> rs(std::max(F_, 1));
+    for (int f = 0; f < F_; ++f) rs[f] = static_cast<unsigned>(config_->extra_seed + f);
+    rng_.Upload(rs, stream_);
+    if (has_cat_) cat_scratch_.Resize(static_cast<size_t>(F_) * 3 * max_cat_bin_);
+    else cat_scratch_.Resize(1);
+    if (bag_cnt_ == 0) bag_cnt_ = N_;
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  Args MakeArgs() const {
+    Args a;
+    std::memset(&a, 0, sizeof(a));
+    a.rowbins = rowbins_.get();
+    a.colbins = colbins_.get();
+    a.gh = gh_.get();
+    for (int i = 0; i < 3; ++i) a.idx[i] = idx_[i].get();
+    a.N = N_;
+    a.stride_dw = stride_dw_;
+    a.width = width_;
+    a.num_groups = G_;
+    a.TB = TB_;
+    a.F = F_;
+    a.L = L_;
+    a.max_tiles = max_tiles_;
+    a.gstart = gstart_.get();
+    a.feat = feat_.get();
+    a.tiles = tiles_.get();
+    a.used_bytree = used_bytree_.get();
+    a.bynode = use_bynode_ ? bynode_.get() : nullptr;
+    a.tp = tparams_.get();
+    a.ctl = ctl_.get();
+    a.range = range_.get();
+    a.lsum = lsum_.get();
+    a.lout = lout_.get();
+    a.gcount = gcount_.get();
+    a.depth = depth_.get();
+    a.slot = slot_.get();
+    a.bounds = bounds_.get();
+    a.best = best_.get();
+    a.rec = rec_.get();
+    a.slots = slots_.get();
+    a.staging = staging_.get();
+    a.splittable = splittable_.get();
+    a.scan_out = scan_out_.get();
+    a.tile_cnt = tile_cnt_.get();
+    a.tile_off = tile_off_.get();
+    a.rng = rng_.get();
+    a.cat_scratch = cat_scratch_.get();
+    a.max_cat_bin = max_cat_bin_;
+    a.max_depth = config_->max_depth;
+    a.distributed = distributed_ ? 1 : 0;
+    a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
+    a.monotone_penalty = config_->monotone_penalty;
+    SplitParams& p = a.sp;
+    p.lambda_l1 = config_->lambda_l1;
+    p.lambda_l2 = config_->lambda_l2;
+    p.max_delta_step = config_->max_delta_step;
+    p.path_smooth = config_->path_smooth;
+    p.min_gain_to_split = config_->min_gain_to_split;
+    p.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf;
+    p.cat_smooth = config_->cat_smooth;
+    p.cat_l2 = config_->cat_l2;
+    p.min_data_in_leaf = config_->min_data_in_leaf;
+    p.max_cat_threshold = config_->max_cat_threshold;
+    p.max_cat_to_onehot = config_->max_cat_to_onehot;
+    p.min_data_per_group = config_->min_data_per_group;
+    p.extra_trees = config_->extra_trees ? 1 : 0;
+    p.use_monotone = a.use_monotone;
+    return a;
+  }
+
+  // The whole growth of one tree; fixed launch shapes, data-dependent work read on device.
+  void EnqueueTree() {
+    const Args a = MakeArgs();
+    hipStream_t s = stream_;
+    const int hist_blocks = std::max(1, std::min(config_->device_hist_blocks > 0 ? config_->device_hist_blocks : 2 * num_cu_,
+                                                 DivUp(N_, kHistMinRows)));
+    const int part_blocks = std::max(1, std::min(max_tiles_, 4 * num_cu_));
+    const int scan_blocks = std::max(1, DivUp(F_, kScanWaves));
+    const dim3 hgrid(hist_blocks, num_tiles_);
+    auto hist = [&]() {
+      if (width_ == 1) k_hist<1><<<hgrid, kHistThreads, hist_lds_bytes_, s>>>(a);
+      else k_hist<2><<<hgrid, kHistThreads, hist_lds_bytes_, s>>>(a);
+      if (distributed_) AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), s);
+    };
+    k_init_tree<<<1, kNodeThreads, 0, s>>>(a);
+    k_root_sums<<<std::max(1, std::min(DivUp(N_, 256), 4 * num_cu_)), 256, 0, s>>>(a);
+    if (distributed_) AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
+    hist();
+    k_scan<<<scan_blocks, kScanWaves * 64, 0, s>>>(a);
+    for (int it = 0; it < L_ - 1; ++it) {
+      k_select<<<1, kNodeThreads, 0, s>>>(a);
+      k_part_count<<<part_blocks, kPartThreads, 0, s>>>(a);
+      k_part_scan<<<1, 1024, 0, s>>>(a);
+      k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(a);
+      k_post<<<1, kNodeThreads, 0, s>>>(a);
+      if (it < L_ - 2) {
+        hist();
+        k_scan<<<scan_blocks, kScanWaves * 64, 0, s>>>(a);
+      }
+    }
+    HIP_CHECK(hipGetLastError());
+  }
+
+  void CaptureGraph() {
+    InvalidateGraph();
+    hipGraph_t g;
+    HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    EnqueueTree();
+    HIP_CHECK(hipStreamEndCapture(stream_, &g));
+    HIP_CHECK(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(g));
+  }
+
+  void InvalidateGraph() {
+    if (graph_exec_) {
+      (void)hipGraphExecDestroy(graph_exec_);
+      graph_exec_ = nullptr;
+    }
+  }
+
+  void PrepareObjective(const ObjectiveFunction* obj) {
+    if (obj == prepared_obj_) return;
+    prepared_obj_ = obj;
+    const Metadata& md = data_->metadata();
+    const label_t* lab = obj->effective_label() ? obj->effective_label() : md.label();
+    label_.Upload(lab, N_, stream_);
+    if (md.weights()) weight_.Upload(md.weights(), N_, stream_);
+    else weight_.Free();
+    if (obj->aux_weight()) aux_.Upload(obj->aux_weight(), N_, stream_);
+    else aux_.Free();
+    if (obj->device_kind() == DeviceGradKind::kLambdarank) {
+      LambdarankTables t;
+      if (!GetLambdarankTables(obj, &t)) Log::Fatal("lambdarank tables unavailable");
+      rank_table_.Upload(*t.table, stream_);
+      rank_gain_.Upload(*t.label_gain, stream_);
+      rank_inv_dcg_.Upload(*t.inv_max_dcg, stream_);
+      rank_inv_bdcg_.Upload(*t.inv_max_bdcg, stream_);
+      rank_qb_.Upload(md.query_boundaries_vec(), stream_);
+      RankKernelArgs& r = rank_args_;
+      r.target = t.target;
+      r.k = t.k;
+      r.norm = t.norm;
+      r.sigmoid = t.sigmoid;
+      r.gap_weight = t.gap_weight;
+      r.tmin = t.tmin;
+      r.tmax = t.tmax;
+      r.tfactor = t.tfactor;
+      r.table_size = static_cast<int>(t.table->size());
+      r.table = rank_table_.get();
+      r.label_gain = rank_gain_.get();
+      r.num_label_gain = static_cast<int>(t.label_gain->size());
+      r.inv_max_dcg = rank_inv_dcg_.get();
+      r.inv_max_bdcg = rank_inv_bdcg_.get();
+      r.qb = rank_qb_.get();
+      r.num_queries = md.num_queries();
+      r.label = label_.get();
+      r.weight = weight_.size() ? weight_.get() : nullptr;
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  const Config* config_;
+  bool data_parallel_ = false;
+  bool distributed_ = false;
+  const Dataset* data_ = nullptr;
+  int N_ = 0, F_ = 0, G_ = 0, TB_ = 0, width_ = 1, stride_dw_ = 1, L_ = 2, K_ = 1;
+  int device_id_ = 0, num_cu_ = 256, num_tiles_ = 0, max_tiles_ = 1, max_cat_bin_ = 1;
+  bool has_cat_ = false, use_bag_ = false, use_bynode_ = false;
+  data_size_t bag_cnt_ = 0;
+  size_t hist_lds_bytes_ = 0;
+  std::string device_name_;
+  hipStream_t stream_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr;
+  ColSampler col_sampler_;
+  const ObjectiveFunction* prepared_obj_ = nullptr;
+  std::vector<LeafRange> h_range_;
+
+  DevBuf<uint32_t> rowbins_;
+  DevBuf<uint8_t> colbins_;
+  DevBuf<float2> gh_;
+  DevBuf<double> score_;
+  DevBuf<float> label_, weight_, aux_;
+  DevBuf<int> idx_[3];
+  DevBuf<DevFeature> feat_;
+  DevBuf<int> gstart_;
+  DevBuf<HistTile> tiles_;
+  DevBuf<TreeParams> tparams_;
+  DevBuf<Ctl> ctl_;
+  DevBuf<LeafRange> range_;
+  DevBuf<double2> lsum_;
+  DevBuf<double> lout_;
+  DevBuf<int> gcount_, depth_, slot_;
+  DevBuf<LeafBounds> bounds_;
+  DevBuf<SplitInfo> best_;
+  DevBuf<SplitRec> rec_;
+  DevBuf<double> slots_, staging_;
+  DevBuf<uint8_t> splittable_;
+  DevBuf<SplitInfo> scan_out_;
+  DevBuf<int> tile_cnt_, tile_off_;
+  DevBuf<uint8_t> used_bytree_, bynode_;
+  DevBuf<unsigned> rng_;
+  DevBuf<double> cat_scratch_;
+  DevBuf<char> tree_buf_;
+  // lambdarank tables
+  DevBuf<double> rank_table_, rank_gain_, rank_inv_dcg_, rank_inv_bdcg_;
+  DevBuf<int> rank_qb_;
+  RankKernelArgs rank_args_;
+  // pinned staging
+  PinnedBuf<TreeParams> pin_tp_;
+  PinnedBuf<uint8_t> pin_mask_;
+  PinnedBuf<Ctl> pin_ctl_;
+  PinnedBuf<SplitRec> pin_rec_;
+  PinnedBuf<LeafRange> pin_range_;
+  PinnedBuf<double> pin_lout_;
+  PinnedBuf<float2> pin_gh_;
+  PinnedBuf<char> pin_tree_;
+};
+
+}  // namespace
+
+std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const std::string& parallel_mode) {
+  if (parallel_mode == "serial") return std::make_unique<DeviceTreeLearner>(config, false);
+  if (parallel_mode == "data" || parallel_mode == "voting" || parallel_mode == "feature") {
+    if (parallel_mode != "data") {
+      Log::Warning("tree_learner=%s on the HIP learner runs as data-parallel (histogram all-reduce over RCCL)",
+                   parallel_mode.c_str());
+    }
+    return std::make_unique<DeviceTreeLearner>(config, true);
+  }
+  Log::Fatal("Unknown tree learner type %s", parallel_mode.c_str());
+  return nullptr;
+}
+
+}  // namespace device
+}  // namespace lgap

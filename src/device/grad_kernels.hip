@@ -1,0 +1,292 @@
+// Gradient / hessian kernels for the device-resident boosting loop.
+//  * pointwise objectives: one thread per row, formulas shared with the host
+//    objectives through lgap/pointwise.h (so both paths give the same numbers);
+//  * multiclass softmax: one thread per row over the K class scores;
+//  * lambdarank (all 18 `lambdarank_target`s): one 256-thread workgroup per
+//    query. The query's scores are bitonic-sorted in LDS (score desc, index
+//    asc == std::stable_sort), the (i, j) pair space of the target is
+//    flattened with an LDS prefix sum so every lane gets equal work, and the
+//    per-document lambdas/hessians accumulate with LDS float atomics.
+// Reference semantics: rank_objective.hpp:182-560 (targets, pair ranges,
+// delta_pair, normalisation), multiclass_objective.hpp:120-150.
+#include <hip/hip_runtime.h>
+
+#include "device/grad_kernels.h"
+#include "device/hip_common.h"
+#include "lgap/rank_math.h"
+
+namespace lgap {
+namespace device {
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_pointwise(PointwiseParams p, const double* __restrict__ score,
+                                                   const float* __restrict__ label, const float* __restrict__ weight,
+                                                   const float* __restrict__ aux, int n, float2* __restrict__ gh) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double w = weight ? static_cast<double>(weight[i]) : 1.0;
+    const double ax = aux ? static_cast<double>(aux[i]) : 0.0;
+    score_t g, h;
+    PointwiseGradient(p, score[i], static_cast<double>(label[i]), w, weight != nullptr, ax, &g, &h);
+    gh[i] = make_float2(g, h);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_softmax(int K, double factor, const double* __restrict__ score,
+                                                 const float* __restrict__ label, const float* __restrict__ weight,
+                                                 int n, float2* __restrict__ gh) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double mx = score[i];
+    for (int k = 1; k < K; ++k) mx = fmax(mx, score[static_cast<size_t>(k) * n + i]);
+    double den = 0.0;
+    for (int k = 0; k < K; ++k) den += exp(score[static_cast<size_t>(k) * n + i] - mx);
+    const int y = static_cast<int>(label[i]);
+    const double w = weight ? static_cast<double>(weight[i]) : 1.0;
+    for (int k = 0; k < K; ++k) {
+      const double pk = exp(score[static_cast<size_t>(k) * n + i] - mx) / den;
+      float g, h;
+      if (weight) {
+        g = static_cast<float>((y == k ? pk - 1.0f : pk) * w);
+        h = static_cast<float>(factor * pk * (1.0f - pk) * w);
+      } else {
+        g = static_cast<float>(y == k ? pk - 1.0f : pk);
+        h = static_cast<float>(factor * pk * (1.0f - pk));
+      }
+      gh[static_cast<size_t>(k) * n + i] = make_float2(g, h);
+    }
+  }
+}
+
+__global__ void k_add_constant(double* score, int n, double v) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) score[i] += v;
+}
+
+constexpr int kRankThreads = 256;
+
+__device__ __forceinline__ bool RankBefore(double sa, int ia, double sb, int ib, int cnt) {
+  const bool va = ia < cnt, vb = ib < cnt;
+  if (va != vb) return va;
+  if (sa != sb) return sa > sb;
+  return ia < ib;
+}
+
+__device__ __forceinline__ double TableSigmoid(const RankKernelArgs& a, double s) {
+  if (s <= a.tmin) return a.table[0];
+  if (s >= a.tmax) return a.table[a.table_size - 1];
+  return a.table[static_cast<size_t>((s - a.tmin) * a.tfactor)];
+}
+
+__global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a) {
+  __shared__ double s_score[kMaxDeviceQuery];
+  __shared__ int s_idx[kMaxDeviceQuery];
+  __shared__ float s_lab[kMaxDeviceQuery];
+  __shared__ float s_lam[kMaxDeviceQuery];
+  __shared__ float s_hes[kMaxDeviceQuery];
+  __shared__ int s_off[kMaxDeviceQuery + 1];
+  __shared__ double s_red[kRankThreads / kWave];
+  __shared__ int s_redi[kRankThreads / kWave];
+
+  const int q = blockIdx.x;
+  const int t = threadIdx.x;
+  const int start = a.qb[q];
+  const int cnt = a.qb[q + 1] - start;
+  float2* out = a.gh + start;
+  if (cnt <= 1) {
+    for (int i = t; i < cnt; i += blockDim.x) out[i] = make_float2(0.f, 0.f);
+    return;
+  }
+  int P = 1;
+  while (P < cnt) P <<= 1;
+  const bool full_sort = TargetNeedsFullSort(a.target) || a.target == kTgtPrecision;
+  for (int i = t; i < P; i += blockDim.x) {
+    if (i < cnt) {
+      s_score[i] = a.score[start + i];
+      s_lab[i] = a.label[start + i];
+      s_lam[i] = 0.f;
+      s_hes[i] = 0.f;
+    }
+    s_idx[i] = i;
+  }
+  __syncthreads();
+  // scores by original position; s_idx holds the ranking permutation
+  if (full_sort) {
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = t; i < P; i += blockDim.x) {
+          const int l = i ^ j;
+          if (l > i) {
+            const int ai = s_idx[i], al = s_idx[l];
+            const double sa = ai < cnt ? s_score[ai] : 0.0, sl = al < cnt ? s_score[al] : 0.0;
+            const bool asc = (i & k) == 0;
+            // asc segment: keep "before" order at i; desc segment: reversed
+            const bool swap = asc ? RankBefore(sl, al, sa, ai, cnt) : RankBefore(sa, ai, sl, al, cnt);
+            if (swap) {
+              s_idx[i] = al;
+              s_idx[l] = ai;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  // best / worst scores
+  double best, worst;
+  if (TargetNeedsFullSort(a.target)) {
+    best = s_score[s_idx[0]];
+    int wi = cnt - 1;
+    if (wi > 0 && s_score[s_idx[wi]] == kMinScore) wi -= 1;
+    worst = s_score[s_idx[wi]];
+  } else {
+    double mx = -INFINITY, mn = INFINITY;
+    for (int i = t; i < cnt; i += blockDim.x) {
+      mx = fmax(mx, s_score[i]);
+      mn = fmin(mn, s_score[i]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      mx = fmax(mx, __shfl_xor(mx, o, kWave));
+      mn = fmin(mn, __shfl_xor(mn, o, kWave));
+    }
+    if ((t & 63) == 0) s_red[t >> 6] = mx;
+    __syncthreads();
+    mx = s_red[0];
+    for (int w = 1; w < kRankThreads / kWave; ++w) mx = fmax(mx, s_red[w]);
+    __syncthreads();
+    if ((t & 63) == 0) s_red[t >> 6] = mn;
+    __syncthreads();
+    mn = s_red[0];
+    for (int w = 1; w < kRankThreads / kWave; ++w) mn = fmin(mn, s_red[w]);
+    __syncthreads();
+    best = mx;
+    worst = mn;
+  }
+  // identity order for the order-free targets (the host iterates idx = 0..cnt-1)
+  if (!full_sort) {
+    for (int i = t; i < cnt; i += blockDim.x) s_idx[i] = i;
+    __syncthreads();
+  }
+  // flattened pair space: s_off[i] = sum_{i' < i} |J(i')|
+  const int i_end = TargetIEnd(a.target, cnt, a.k);
+  if (t == 0) {
+    int acc = 0;
+    for (int i = 0; i < i_end; ++i) {
+      s_off[i] = acc;
+      int js, je;
+      TargetJRange(a.target, i, cnt, a.k, &js, &je);
+      acc += je > js ? je - js : 0;
+    }
+    s_off[i_end > 0 ? i_end : 0] = acc;
+  }
+  __syncthreads();
+  const int total = i_end > 0 ? s_off[i_end] : 0;
+  const bool binary = TargetIsBinary(a.target);
+  const double inv_dcg = a.inv_max_dcg ? a.inv_max_dcg[q] : 0.0;
+  const double inv_bdcg = a.inv_max_bdcg ? a.inv_max_bdcg[q] : 0.0;
+  double sum_lambdas = 0.0;
+  int count = 0;
+  for (int p = t; p < total; p += blockDim.x) {
+    int lo = 0, hi = i_end - 1;
+    while (lo < hi) {  // last i with s_off[i] <= p
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    const int i = lo;
+    int js, je;
+    TargetJRange(a.target, i, cnt, a.k, &js, &je);
+    const int j = js + (p - s_off[i]);
+    const int di = s_idx[i], dj = s_idx[j];
+    if (s_score[di] == kMinScore || s_score[dj] == kMinScore) continue;
+    const float li = s_lab[di], lj = s_lab[dj];
+    if (li == lj) continue;
+    if (binary && li > 0 && lj > 0) continue;
+    int hr, lr;
+    if (li > lj) {
+      hr = i;
+      lr = j;
+    } else {
+      hr = j;
+      lr = i;
+    }
+    const int high = s_idx[hr], low = s_idx[lr];
+    const double ds = s_score[high] - s_score[low];
+    const int hl = static_cast<int>(s_lab[high]), ll = static_cast<int>(s_lab[low]);
+    const double hg = hl < a.num_label_gain ? a.label_gain[hl] : 0.0;
+    const double lg = ll < a.num_label_gain ? a.label_gain[ll] : 0.0;
+    double dp = TargetDeltaPair(a.target, i, j, hr, lr, hg, lg, s_lab[high], s_lab[low], inv_dcg, inv_bdcg, a.k,
+                                a.gap_weight);
+    if (dp == 0) continue;
+    if (a.norm && best != worst) dp /= (0.01f + fabs(ds));
+    double pl = TableSigmoid(a, ds);
+    double ph = pl * (1.0f - pl);
+    pl *= -a.sigmoid * dp;
+    ph *= a.sigmoid * a.sigmoid * dp;
+    atomicAdd(&s_lam[low], -static_cast<float>(pl));
+    atomicAdd(&s_hes[low], static_cast<float>(ph));
+    atomicAdd(&s_lam[high], static_cast<float>(pl));
+    atomicAdd(&s_hes[high], static_cast<float>(ph));
+    sum_lambdas -= 2 * pl;
+    ++count;
+  }
+  sum_lambdas = WaveSum(sum_lambdas);
+  if ((t & 63) == 0) s_red[t >> 6] = sum_lambdas;
+  __syncthreads();
+  double sl = 0.0;
+  for (int w = 0; w < kRankThreads / kWave; ++w) sl += s_red[w];
+  double f = 1.0;
+  if (a.norm && sl > 0) f = log2(1 + sl) / sl;
+  (void)count;
+  for (int i = t; i < cnt; i += blockDim.x) {
+    float g = s_lam[i], h = s_hes[i];
+    if (a.norm && sl > 0) {
+      g = static_cast<float>(g * f);
+      h = static_cast<float>(h * f);
+    }
+    if (a.weight) {
+      const float w = a.weight[start + i];
+      g = static_cast<float>(g * w);
+      h = static_cast<float>(h * w);
+    }
+    out[i] = make_float2(g, h);
+  }
+  (void)s_redi;
+}
+
+int GridFor(int n) {
+  int g = DivUp(n, 256);
+  return g < 1 ? 1 : (g > 65536 ? 65536 : g);
+}
+
+}  // namespace
+
+void LaunchPointwiseGrad(const PointwiseParams& p, const double* score, const float* label, const float* weight,
+                         const float* aux, int n, float2* gh, hipStream_t s) {
+  if (n <= 0) return;
+  k_pointwise<<<GridFor(n), 256, 0, s>>>(p, score, label, weight, aux, n, gh);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchSoftmaxGrad(int num_class, double factor, const double* score, const float* label, const float* weight,
+                       int n, float2* gh, hipStream_t s) {
+  if (n <= 0) return;
+  k_softmax<<<GridFor(n), 256, 0, s>>>(num_class, factor, score, label, weight, n, gh);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s) {
+  if (a.num_queries <= 0) return;
+  k_lambdarank<<<a.num_queries, kRankThreads, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchAddConstant(double* score, int n, double v, hipStream_t s) {
+  if (n <= 0) return;
+  k_add_constant<<<GridFor(n), 256, 0, s>>>(score, n, v);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace device
+}  // namespace lgap

@@ -1,0 +1,193 @@
+// Device runtime: device discovery and the RCCL communicator (one process per
+// GPU, xGMI transport). The communicator is bootstrapped from an ncclUniqueId
+// that the launcher (torch.distributed / the CLI's socket network) broadcasts.
+//
+// Besides the device learners' histogram all-reduce, the same communicator
+// backs the host collective layer (Network) when no socket mesh is configured:
+// reduce-scatter / allgather of host bytes go through pinned staging buffers
+// and ncclAllGather, so scalar syncs (boost_from_average, distributed bin
+// finding, metric sums) need no second transport.
+// Reference counterpart: src/network/network.cpp:30-75 (external functions).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "device/hip_common.h"
+#include "device/runtime_internal.h"
+#include "lgap/device_api.h"
+#include "lgap/network.h"
+
+namespace lgap {
+namespace device {
+
+namespace {
+
+struct CommState {
+  ncclComm_t comm = nullptr;
+  int rank = 0;
+  int size = 1;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  char* dev_buf = nullptr;
+  size_t dev_cap = 0;
+  std::mutex mu;
+};
+
+CommState& S() {
+  static CommState s;
+  return s;
+}
+
+void NcclCheck(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) Log::Fatal("RCCL error in %s: %s", what, ncclGetErrorString(r));
+}
+
+char* Staging(size_t bytes) {
+  auto& s = S();
+  if (bytes > s.dev_cap) {
+    if (s.dev_buf) HIP_CHECK(hipFree(s.dev_buf));
+    s.dev_cap = std::max<size_t>(bytes, 1 << 20);
+    HIP_CHECK(hipMalloc(&s.dev_buf, s.dev_cap));
+  }
+  return s.dev_buf;
+}
+
+// Equal-size allgather of `bytes` per rank from host memory into host memory.
+void HostAllgatherEqual(const char* in, size_t bytes, char* out) {
+  auto& s = S();
+  std::lock_guard<std::mutex> lk(s.mu);
+  HIP_CHECK(hipSetDevice(s.device));
+  char* d = Staging(bytes * (s.size + 1));
+  char* d_in = d + bytes * s.size;
+  HIP_CHECK(hipMemcpyAsync(d_in, in, bytes, hipMemcpyHostToDevice, s.stream));
+  NcclCheck(ncclAllGather(d_in, d, bytes, ncclChar, s.comm, s.stream), "ncclAllGather");
+  HIP_CHECK(hipMemcpyAsync(out, d, bytes * s.size, hipMemcpyDeviceToHost, s.stream));
+  HIP_CHECK(hipStreamSynchronize(s.stream));
+}
+
+// Network external allgather: variable blocks, padded to the largest block.
+void RcclAllgather(char* input, comm_size_t input_size, const comm_size_t* block_start, const comm_size_t* block_len,
+                   int num_block, char* output, comm_size_t output_size) {
+  (void)input_size;
+  (void)output_size;
+  comm_size_t mx = 0;
+  for (int i = 0; i < num_block; ++i) mx = std::max(mx, block_len[i]);
+  if (mx == 0) return;
+  std::vector<char> pad(mx, 0), all(static_cast<size_t>(mx) * num_block);
+  std::memcpy(pad.data(), input, block_len[S().rank]);
+  HostAllgatherEqual(pad.data(), mx, all.data());
+  for (int i = 0; i < num_block; ++i) {
+    std::memcpy(output + block_start[i], all.data() + static_cast<size_t>(i) * mx, block_len[i]);
+  }
+}
+
+// Network external reduce-scatter with an arbitrary host reducer: gather every
+// rank's full input, then reduce this rank's block locally (inputs here are
+// small host-side syncs; the device histograms use ncclAllReduce directly).
+void RcclReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
+                       const comm_size_t* block_len, int num_block, char* output, comm_size_t output_size,
+                       const ReduceFunction& reducer) {
+  (void)num_block;
+  (void)output_size;
+  const int n = S().size, r = S().rank;
+  std::vector<char> all(static_cast<size_t>(input_size) * n);
+  HostAllgatherEqual(input, input_size, all.data());
+  std::memcpy(output, all.data() + block_start[r], block_len[r]);
+  for (int k = 0; k < n; ++k) {
+    if (k == r) continue;
+    reducer(all.data() + static_cast<size_t>(k) * input_size + block_start[r], output, type_size, block_len[r]);
+  }
+}
+
+std::string ToHex(const char* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s(2 * n, '0');
+  for (size_t i = 0; i < n; ++i) {
+    s[2 * i] = d[(static_cast<unsigned char>(p[i]) >> 4) & 15];
+    s[2 * i + 1] = d[static_cast<unsigned char>(p[i]) & 15];
+  }
+  return s;
+}
+
+int HexVal(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  Log::Fatal("Invalid hex digit in RCCL unique id");
+  return 0;
+}
+
+}  // namespace
+
+int DeviceCount() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+std::string CommGetUniqueId() {
+  ncclUniqueId id;
+  NcclCheck(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return ToHex(id.internal, sizeof(id.internal));
+}
+
+void CommInit(const std::string& unique_id, int num_ranks, int rank, int device_id) {
+  auto& s = S();
+  if (s.comm) CommFree();
+  if (unique_id.size() != 2 * sizeof(ncclUniqueId().internal)) Log::Fatal("Malformed RCCL unique id");
+  ncclUniqueId id;
+  for (size_t i = 0; i < sizeof(id.internal); ++i) {
+    id.internal[i] = static_cast<char>(HexVal(unique_id[2 * i]) * 16 + HexVal(unique_id[2 * i + 1]));
+  }
+  s.device = device_id;
+  HIP_CHECK(hipSetDevice(device_id));
+  HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  NcclCheck(ncclCommInitRank(&s.comm, num_ranks, id, rank), "ncclCommInitRank");
+  s.rank = rank;
+  s.size = num_ranks;
+  // host collectives ride on the same communicator unless a socket mesh exists
+  if (Network::num_machines() <= 1 && num_ranks > 1) {
+    Network::Init(num_ranks, rank, RcclReduceScatter, RcclAllgather);
+  }
+  Log::Info("RCCL communicator ready: rank %d / %d on device %d", rank, num_ranks, device_id);
+}
+
+void CommFree() {
+  auto& s = S();
+  if (s.comm) {
+    (void)ncclCommDestroy(s.comm);
+    s.comm = nullptr;
+  }
+  if (s.stream) {
+    (void)hipStreamDestroy(s.stream);
+    s.stream = nullptr;
+  }
+  if (s.dev_buf) {
+    (void)hipFree(s.dev_buf);
+    s.dev_buf = nullptr;
+    s.dev_cap = 0;
+  }
+  s.rank = 0;
+  s.size = 1;
+}
+
+int CommRank() { return S().rank; }
+int CommSize() { return S().size; }
+bool CommActive() { return S().comm != nullptr && S().size > 1; }
+ncclComm_t ActiveComm() { return S().comm; }
+int CommDevice() { return S().device; }
+
+void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream) {
+  if (!CommActive() || count == 0) return;
+  NcclCheck(ncclAllReduce(dev_ptr, dev_ptr, count, ncclFloat64, ncclSum, S().comm, stream), "ncclAllReduce");
+}
+
+}  // namespace device
+}  // namespace lgap

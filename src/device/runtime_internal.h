@@ -1,0 +1,18 @@
+// Internal accessors of the device runtime shared by the HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstddef>
+
+namespace lgap {
+namespace device {
+
+ncclComm_t ActiveComm();
+int CommDevice();
+// In-place sum all-reduce of device doubles on `stream` (no-op without a communicator).
+void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream);
+
+}  // namespace device
+}  // namespace lgap

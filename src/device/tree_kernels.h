@@ -1,0 +1,76 @@
+// Device-side state of the HIP tree learner. Everything that changes while a
+// tree grows (leaf ranges, best splits, the split about to be applied) lives
+// in device memory so the whole leaf-wise growth loop is a fixed sequence of
+// kernels with fixed launch shapes: it is captured once into a hipGraph and
+// replayed per tree; kernels whose work vanished (tree finished early) exit
+// on the `done` flag.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "lgap/split_math.h"
+
+namespace lgap {
+namespace device {
+
+struct DevFeature {
+  int group;
+  int offset;       // first group bin
+  int num_bin;
+  int mfb;          // most frequent bin (implicit in histograms)
+  int default_bin;
+  int hist_offset;  // global histogram position of group bin `offset`
+  int8_t missing;
+  int8_t bin_type;
+  int8_t monotone;
+  int8_t pad;
+  int pad2;
+  double penalty;
+};
+
+// Histogram tile: a run of whole dwords of the packed row (so whole groups)
+// whose bins fit in the LDS budget of one workgroup.
+struct HistTile {
+  int d0, d1;    // dword range within a row
+  int g0, g1;    // groups [g0, g1)
+  int bin0;      // global histogram index of the first bin of group g0
+  int nbins;     // bins covered
+};
+
+// Rows of a leaf: positions [start, start+count) of index buffer `buf`
+// (buf -1: identity order, i.e. all rows without bagging; 2: the bag list).
+struct LeafRange {
+  int buf, start, count, pad;
+};
+
+// Per-tree inputs written by the host before each replay.
+struct TreeParams {
+  int root_buf;
+  int root_count;
+  int cls;
+  int root_gcount;  // global (all ranks) row count of the root
+};
+
+struct Ctl {
+  int num_leaves, done, smaller, larger;
+  int skip, num_splits, split_leaf, new_leaf;
+  int parent_buf, parent_start, parent_count, target_buf;
+  int left_count, cls, scan_round, pad;
+};
+
+struct SplitRec {
+  int leaf, left_count, right_count, pad;
+  SplitInfo info;
+};
+
+// Device-resident tree for score updates (one tree uploaded at a time).
+struct DevNode {
+  int group, offset, num_bin, mfb;
+  int default_bin, missing, threshold, decision;  // decision: bit0 categorical, bit1 default_left
+  int left, right, cat_begin, cat_nwords;
+};
+
+}  // namespace device
+}  // namespace lgap

@@ -1,0 +1,778 @@
+// Host leaf-wise learner (correctness oracle). Behaviour mirrors the
+// reference's SerialTreeLearner (serial_tree_learner.cpp:179-1114):
+// smaller-child histogram + parent-minus-sibling subtraction, per-feature
+// splittable inheritance, basic monotone constraints, extra-trees thresholds,
+// feature sampling by tree / node, interaction constraints, forced splits,
+// refit and L1/quantile leaf renewal.
+#include "serial_tree_learner.h"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <numeric>
+#include <queue>
+#include <unordered_set>
+
+#include "lgap/common.h"
+#include "lgap/log.h"
+#include "lgap/network.h"
+
+namespace lgap {
+
+// ============================================================================
+// ColSampler (col_sampler.hpp:20-207)
+int ColSampler::GetCnt(size_t total, double fraction) {
+  const int mn = std::min(1, static_cast<int>(total));
+  const int c = common::RoundInt(total * fraction);
+  return std::max(c, mn);
+}
+
+void ColSampler::Init(const Dataset* data, const Config* cfg) {
+  data_ = data;
+  frac_tree_ = cfg->feature_fraction;
+  frac_node_ = cfg->feature_fraction_bynode;
+  if (seed_ != cfg->feature_fraction_seed) {
+    seed_ = cfg->feature_fraction_seed;
+    rand_ = Random(seed_);
+  }
+  valid_.clear();
+  for (int f = 0; f < data->num_features(); ++f) valid_.push_back(data->feature(f).real_index);
+  used_bytree_.assign(data->num_features(), 1);
+  if (frac_tree_ >= 1.0) {
+    need_reset_tree_ = false;
+    used_cnt_tree_ = static_cast<int>(valid_.size());
+  } else {
+    need_reset_tree_ = true;
+    used_cnt_tree_ = GetCnt(valid_.size(), frac_tree_);
+  }
+  interaction_.clear();
+  for (auto& c : cfg->interaction_constraints_vector) interaction_.emplace_back(c.begin(), c.end());
+  ResetByTree();
+}
+
+void ColSampler::ResetByTree() {
+  if (!need_reset_tree_) return;
+  std::fill(used_bytree_.begin(), used_bytree_.end(), 0);
+  used_idx_ = rand_.Sample(static_cast<int>(valid_.size()), used_cnt_tree_);
+  for (int i : used_idx_) used_bytree_[data_->InnerIndex(valid_[i])] = 1;
+}
+
+std::vector<int8_t> ColSampler::GetByNode(const Tree* tree, int leaf) {
+  std::unordered_set<int> allowed;
+  if (!interaction_.empty()) {
+    const auto& bf = tree->branch_features(leaf);
+    allowed.insert(bf.begin(), bf.end());
+    for (auto& c : interaction_) {
+      if (bf.empty()) allowed.insert(c.begin(), c.end());
+      int found = 0;
+      for (int f : bf) {
+        if (c.count(f) == 0) break;
+        if (++found == static_cast<int>(bf.size())) {
+          allowed.insert(c.begin(), c.end());
+          break;
+        }
+      }
+    }
+  }
+  const int nf = data_->num_features();
+  std::vector<int8_t> ret(nf, 0);
+  if (frac_node_ >= 1.0) {
+    if (interaction_.empty()) return std::vector<int8_t>(nf, 1);
+    for (int f : allowed) {
+      if (f < data_->num_total_features()) {
+        int in = data_->InnerIndex(f);
+        if (in >= 0) ret[in] = 1;
+      }
+    }
+    return ret;
+  }
+  std::vector<int> pool;
+  if (need_reset_tree_) {
+    for (int i : used_idx_) if (interaction_.empty() || allowed.count(valid_[i])) pool.push_back(i);
+  } else {
+    for (int i = 0; i < static_cast<int>(valid_.size()); ++i)
+      if (interaction_.empty() || allowed.count(valid_[i])) pool.push_back(i);
+  }
+  int cnt = GetCnt(need_reset_tree_ ? used_idx_.size() : valid_.size(), frac_node_);
+  cnt = std::min(cnt, static_cast<int>(pool.size()));
+  auto s = rand_.Sample(static_cast<int>(pool.size()), cnt);
+  for (int i : s) ret[data_->InnerIndex(valid_[pool[i]])] = 1;
+  return ret;
+}
+
+// ============================================================================
+// DataPartition
+void DataPartition::Init(data_size_t num_data, int num_leaves) {
+  num_data_ = num_data;
+  indices_.resize(num_data);
+  tmp_.resize(num_data);
+  begin_.assign(num_leaves, 0);
+  count_.assign(num_leaves, 0);
+}
+
+void DataPartition::SetUsedIndices(const data_size_t* idx, data_size_t n) {
+  if (idx == nullptr) {
+    use_bag_ = false;
+    used_.clear();
+  } else {
+    use_bag_ = true;
+    used_.assign(idx, idx + n);
+  }
+  bag_cnt_ = n;
+}
+
+void DataPartition::Reset() {
+  std::fill(begin_.begin(), begin_.end(), 0);
+  std::fill(count_.begin(), count_.end(), 0);
+  if (use_bag_) {
+    std::copy(used_.begin(), used_.end(), indices_.begin());
+    count_[0] = static_cast<data_size_t>(used_.size());
+  } else {
+    std::iota(indices_.begin(), indices_.end(), 0);
+    count_[0] = num_data_;
+  }
+}
+
+void DataPartition::ResetByLeafPred(const std::vector<int>& leaf_pred, int num_leaves) {
+  std::vector<std::vector<data_size_t>> lists(num_leaves);
+  for (data_size_t i = 0; i < static_cast<data_size_t>(leaf_pred.size()); ++i) lists[leaf_pred[i]].push_back(i);
+  begin_.assign(std::max<size_t>(begin_.size(), num_leaves), 0);
+  count_.assign(begin_.size(), 0);
+  data_size_t off = 0;
+  for (int l = 0; l < num_leaves; ++l) {
+    begin_[l] = off;
+    count_[l] = static_cast<data_size_t>(lists[l].size());
+    std::copy(lists[l].begin(), lists[l].end(), indices_.begin() + off);
+    off += count_[l];
+  }
+}
+
+// ============================================================================
+SerialTreeLearner::SerialTreeLearner(const Config* config) : config_(config) {}
+
+void SerialTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
+  train_data_ = train_data;
+  num_data_ = train_data->num_data();
+  num_features_ = train_data->num_features();
+  is_constant_hessian_ = is_constant_hessian;
+  partition_.Init(num_data_, config_->num_leaves);
+  col_sampler_.Init(train_data, config_);
+  best_split_per_leaf_.assign(config_->num_leaves, SplitInfo());
+  hist_.assign(config_->num_leaves, {});
+  splittable_.assign(config_->num_leaves, std::vector<char>(num_features_, 1));
+  bounds_.assign(config_->num_leaves, LeafBounds());
+  leaf_count_global_.assign(config_->num_leaves, 0);
+  use_monotone_ = !config_->monotone_constraints.empty();
+  extra_rand_ = Random(config_->extra_seed);
+  feature_mask_.assign(num_features_, 1);
+  hist_begin_ = 0;
+  hist_end_ = train_data->num_total_bin();
+  if (!config_->forcedsplits_filename.empty()) {
+    std::ifstream in(config_->forcedsplits_filename);
+    if (in) forced_json_.assign((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    else Log::Warning("Forced splits file %s cannot be opened", config_->forcedsplits_filename.c_str());
+  }
+  Log::Info("Number of data points in the train set: %d, number of used features: %d", num_data_, num_features_);
+}
+
+void SerialTreeLearner::ResetConfig(const Config* config) {
+  config_ = config;
+  if (static_cast<int>(best_split_per_leaf_.size()) != config->num_leaves) {
+    partition_.Init(num_data_, config->num_leaves);
+    best_split_per_leaf_.assign(config->num_leaves, SplitInfo());
+    hist_.assign(config->num_leaves, {});
+    splittable_.assign(config->num_leaves, std::vector<char>(num_features_, 1));
+    bounds_.assign(config->num_leaves, LeafBounds());
+    leaf_count_global_.assign(config->num_leaves, 0);
+  }
+  col_sampler_.Init(train_data_, config_);
+  use_monotone_ = !config_->monotone_constraints.empty();
+}
+
+void SerialTreeLearner::SetBaggingData(const data_size_t* used_indices, data_size_t num_data) {
+  partition_.SetUsedIndices(used_indices, num_data);
+}
+
+SplitParams SerialTreeLearner::MakeParams() const {
+  SplitParams p;
+  p.lambda_l1 = config_->lambda_l1;
+  p.lambda_l2 = config_->lambda_l2;
+  p.max_delta_step = config_->max_delta_step;
+  p.path_smooth = config_->path_smooth;
+  p.min_gain_to_split = config_->min_gain_to_split;
+  p.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf;
+  p.cat_smooth = config_->cat_smooth;
+  p.cat_l2 = config_->cat_l2;
+  p.min_data_in_leaf = config_->min_data_in_leaf;
+  p.max_cat_threshold = config_->max_cat_threshold;
+  p.max_cat_to_onehot = config_->max_cat_to_onehot;
+  p.min_data_per_group = config_->min_data_per_group;
+  p.extra_trees = config_->extra_trees ? 1 : 0;
+  p.use_monotone = use_monotone_ ? 1 : 0;
+  return p;
+}
+
+std::vector<double>& SerialTreeLearner::HistOf(int leaf) {
+  auto& h = hist_[leaf];
+  if (h.size() != static_cast<size_t>(2 * train_data_->num_total_bin())) h.assign(2 * train_data_->num_total_bin(), 0.0);
+  return h;
+}
+
+void SerialTreeLearner::ComputeLeafSums(const data_size_t* idx, data_size_t n, double* sg, double* sh) const {
+  double g = 0.0, h = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : g, h) if (n >= 4096)
+  for (data_size_t i = 0; i < n; ++i) {
+    g += gradients_[idx[i]];
+    h += hessians_[idx[i]];
+  }
+  *sg = g;
+  *sh = h;
+}
+
+// Row-wise histogram over the packed group bins; group bin 0 (all features at
+// their most-frequent bin) is never accumulated.
+void SerialTreeLearner::BuildHistogram(const data_size_t* idx, data_size_t n, double* hist) const {
+  const int tb = train_data_->num_total_bin();
+  const int ng = train_data_->num_groups();
+  const auto& groups = train_data_->groups();
+  std::vector<int> gstart(ng);
+  for (int g = 0; g < ng; ++g) gstart[g] = groups[g].hist_start;
+  std::memset(hist, 0, sizeof(double) * 2 * tb);
+  const int nt = (n >= 16384) ? omp_get_max_threads() : 1;
+  std::vector<std::vector<double>> local(nt);
+  const uint8_t* bins = train_data_->bins();
+  const int stride = train_data_->row_stride();
+  const bool w1 = train_data_->bin_width() == 1;
+#pragma omp parallel num_threads(nt)
+  {
+    const int tid = omp_get_thread_num();
+    double* hh = hist;
+    if (nt > 1) {
+      local[tid].assign(2 * tb, 0.0);
+      hh = local[tid].data();
+    }
+#pragma omp for schedule(static)
+    for (data_size_t i = 0; i < n; ++i) {
+      const data_size_t r = idx[i];
+      const double g = gradients_[r], h = hessians_[r];
+      const uint8_t* row = bins + static_cast<size_t>(r) * stride;
+      for (int k = 0; k < ng; ++k) {
+        const uint32_t b = w1 ? row[k] : reinterpret_cast<const uint16_t*>(row)[k];
+        if (b == 0) continue;
+        const int o = 2 * (gstart[k] + static_cast<int>(b));
+        hh[o] += g;
+        hh[o + 1] += h;
+      }
+    }
+  }
+  if (nt > 1) {
+#pragma omp parallel for schedule(static)
+    for (int j = 0; j < 2 * tb; ++j) {
+      double s = 0.0;
+      for (int t = 0; t < nt; ++t) s += local[t][j];
+      hist[j] = s;
+    }
+  }
+}
+
+void SerialTreeLearner::InitLeafStat(LeafStat* ls, int leaf, double sg, double sh, double output) {
+  ls->leaf = leaf;
+  ls->sum_g = sg;
+  ls->sum_h = sh;
+  ls->output = output;
+  ls->count = leaf >= 0 ? partition_.count(leaf) : 0;
+  ls->global_count = ls->count;
+  if (leaf >= 0) leaf_count_global_[leaf] = ls->count;
+}
+
+void SerialTreeLearner::BeforeTrain() {
+  col_sampler_.ResetByTree();
+  partition_.Reset();
+  for (auto& s : best_split_per_leaf_) s.Reset();
+  for (auto& b : bounds_) b = LeafBounds();
+  for (auto& s : splittable_) std::fill(s.begin(), s.end(), 1);
+  double sg, sh;
+  ComputeLeafSums(partition_.indices(0), partition_.count(0), &sg, &sh);
+  InitLeafStat(&smaller_, 0, sg, sh, 0.0);
+  larger_ = LeafStat();
+  has_parent_hist_ = false;
+}
+
+double SerialTreeLearner::ParentOutput(const Tree* tree, const LeafStat& ls) const {
+  if (tree->num_leaves() == 1) {
+    SplitParams p = MakeParams();
+    p.path_smooth = 0.0;
+    return LeafOutputRaw(ls.sum_g, ls.sum_h, p, ls.global_count, 0.0);
+  }
+  return ls.output;
+}
+
+double SerialTreeLearner::MonotonePenalty(const Tree* tree, int leaf) const {
+  const double pen = config_->monotone_penalty;
+  const int depth = tree->leaf_depth(leaf);
+  if (pen >= depth + 1.0) return kEpsilon;
+  if (pen <= 1.0) return 1.0 - pen / std::pow(2.0, depth) + kEpsilon;
+  return 1.0 - std::pow(2.0, pen - 1.0 - depth) + kEpsilon;
+}
+
+SplitInfo SerialTreeLearner::BestSplitForFeature(const double* group_hist, int f, const LeafStat& leaf,
+                                                 double parent_output, const LeafBounds& bounds,
+                                                 bool* splittable) const {
+  const FeatureInfo& fi = train_data_->feature(f);
+  std::vector<double> full(2 * fi.num_bin);
+  train_data_->FeatureHistogram(group_hist, f, leaf.sum_g, leaf.sum_h, full.data());
+  FeatureScanMeta m;
+  m.num_bin = fi.num_bin;
+  m.default_bin = fi.default_bin;
+  m.missing_type = static_cast<int8_t>(fi.missing);
+  m.bin_type = static_cast<int8_t>(fi.bin_type);
+  m.monotone = fi.monotone;
+  m.penalty = fi.penalty;
+  SplitParams p = MakeParams();
+  SplitInfo out;
+  out.Reset();
+  if (config_->extra_trees) {
+    // per-feature RNG stream (feature_histogram.hpp:1450): Random(extra_seed + f)
+    Random& r = const_cast<std::vector<Random>&>(extra_rands_)[f];
+    if (fi.bin_type == BinType::Numerical) {
+      if (fi.num_bin - 2 > 0) m.rand_threshold = r.NextInt(0, fi.num_bin - 2);
+    } else if (fi.num_bin <= p.max_cat_to_onehot) {
+      if (fi.num_bin - 1 > 0) m.rand_threshold = r.NextInt(1, fi.num_bin);
+    } else {
+      const double cnt_factor = leaf.global_count / (leaf.sum_h + 2 * kEpsilon);
+      int used = 0;
+      for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(full[2 * b + 1] * cnt_factor) >= p.cat_smooth;
+      const int max_num_cat = std::min(p.max_cat_threshold, (used + 1) / 2);
+      const int max_thr = std::max(std::min(max_num_cat, used) - 1, 0);
+      if (max_thr > 0) m.rand_threshold = r.NextInt(0, max_thr);
+    }
+  }
+  bool sp;
+  if (fi.bin_type == BinType::Numerical) {
+    sp = FindBestNumerical(full.data(), m, p, leaf.sum_g, leaf.sum_h, leaf.global_count, parent_output, bounds, &out);
+  } else {
+    std::vector<int> order(fi.num_bin);
+    sp = FindBestCategorical(full.data(), m, p, leaf.sum_g, leaf.sum_h, leaf.global_count, parent_output, bounds,
+                             order.data(), &out);
+  }
+  *splittable = sp;
+  out.feature = sp ? f : -1;
+  if (!sp) out.gain = kMinScore;
+  return out;
+}
+
+std::unique_ptr<Tree> SerialTreeLearner::Train(const score_t* gradients, const score_t* hessians, bool) {
+  ScopedTimer t("SerialTreeLearner::Train");
+  gradients_ = gradients;
+  hessians_ = hessians;
+  if (extra_rands_.size() != static_cast<size_t>(num_features_)) {
+    extra_rands_.clear();
+    for (int f = 0; f < num_features_; ++f) extra_rands_.emplace_back(config_->extra_seed + f);
+  }
+  BeforeTrain();
+  const bool track = !config_->interaction_constraints_vector.empty();
+  auto tree = std::make_unique<Tree>(config_->num_leaves, track, false);
+  {
+    SplitParams p = MakeParams();
+    p.path_smooth = 0.0;
+    tree->SetLeafOutput(0, LeafOutputRaw(smaller_.sum_g, smaller_.sum_h, p, smaller_.global_count, 0.0));
+    smaller_.output = tree->LeafOutput(0);
+  }
+  int left = 0, right = -1;
+  int init_splits = ForceSplits(tree.get(), &left, &right);
+  for (int s = init_splits; s < config_->num_leaves - 1; ++s) {
+    if (BeforeFindBestSplit(tree.get(), left, right)) FindBestSplits(tree.get());
+    int best = 0;
+    for (int l = 1; l < tree->num_leaves(); ++l) {
+      if (best_split_per_leaf_[l].BetterThan(best_split_per_leaf_[best])) best = l;
+    }
+    const SplitInfo& bs = best_split_per_leaf_[best];
+    if (bs.feature < 0 || bs.gain <= 0.0) {
+      Log::Debug("No further splits with positive gain, best gain: %f", bs.gain);
+      break;
+    }
+    Split(tree.get(), best, &left, &right);
+  }
+  tree->RecomputeMaxDepth();
+  return tree;
+}
+
+bool SerialTreeLearner::BeforeFindBestSplit(const Tree* tree, int left, int right) {
+  if (config_->max_depth > 0 && tree->leaf_depth(left) >= config_->max_depth) {
+    best_split_per_leaf_[left].gain = kMinScore;
+    best_split_per_leaf_[left].feature = -1;
+    if (right >= 0) {
+      best_split_per_leaf_[right].gain = kMinScore;
+      best_split_per_leaf_[right].feature = -1;
+    }
+    return false;
+  }
+  const data_size_t nl = GlobalCount(left), nr = GlobalCount(right);
+  if (nr < config_->min_data_in_leaf * 2 && nl < config_->min_data_in_leaf * 2) {
+    best_split_per_leaf_[left].gain = kMinScore;
+    best_split_per_leaf_[left].feature = -1;
+    if (right >= 0) {
+      best_split_per_leaf_[right].gain = kMinScore;
+      best_split_per_leaf_[right].feature = -1;
+    }
+    return false;
+  }
+  has_parent_hist_ = false;
+  if (right >= 0) {
+    // the parent histogram lives in hist_[left]; hand it to the larger child
+    if (larger_.leaf == right) std::swap(hist_[left], hist_[right]), std::swap(splittable_[left], splittable_[right]);
+    has_parent_hist_ = hist_[larger_.leaf].size() == static_cast<size_t>(2 * train_data_->num_total_bin());
+    // the smaller child inherits the parent's splittable flags too
+    splittable_[smaller_.leaf] = splittable_[larger_.leaf];
+  }
+  return true;
+}
+
+void SerialTreeLearner::FindBestSplits(const Tree* tree) {
+  ConstructHistograms(has_parent_hist_);
+  FindBestSplitsFromHistograms(tree, has_parent_hist_);
+}
+
+void SerialTreeLearner::ConstructHistograms(bool use_subtract) {
+  BuildHistogram(partition_.indices(smaller_.leaf), partition_.count(smaller_.leaf), HistOf(smaller_.leaf).data());
+  if (larger_.leaf >= 0 && !use_subtract) {
+    BuildHistogram(partition_.indices(larger_.leaf), partition_.count(larger_.leaf), HistOf(larger_.leaf).data());
+  }
+}
+
+void SerialTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, bool use_subtract) {
+  const auto& bytree = col_sampler_.is_feature_used_bytree();
+  std::vector<int8_t> node_s = col_sampler_.GetByNode(tree, smaller_.leaf);
+  std::vector<int8_t> node_l;
+  const bool has_larger = larger_.leaf >= 0;
+  if (has_larger) node_l = col_sampler_.GetByNode(tree, larger_.leaf);
+  const double po_s = ParentOutput(tree, smaller_);
+  const double po_l = has_larger ? ParentOutput(tree, larger_) : 0.0;
+  const double* hs = HistOf(smaller_.leaf).data();
+  if (use_subtract && has_larger) {
+    double* hl = HistOf(larger_.leaf).data();
+    const int j0 = 2 * hist_begin_, j1 = 2 * hist_end_;
+#pragma omp parallel for schedule(static) if (j1 - j0 >= 65536)
+    for (int j = j0; j < j1; ++j) hl[j] -= hs[j];
+  }
+  const double* hl = has_larger ? HistOf(larger_.leaf).data() : nullptr;
+  std::vector<SplitInfo> bs(num_features_), bl(num_features_);
+  auto& spl_s = splittable_[smaller_.leaf];
+  std::vector<char>* spl_l = has_larger ? &splittable_[larger_.leaf] : nullptr;
+#pragma omp parallel for schedule(dynamic)
+  for (int f = 0; f < num_features_; ++f) {
+    bs[f].Reset();
+    bl[f].Reset();
+    if (!bytree[f] || !feature_mask_[f]) continue;
+    if (use_subtract && !spl_s[f]) {
+      // the parent could not split on f: neither child tries (feature_histogram is_splittable inheritance)
+      continue;
+    }
+    bool sp = false;
+    SplitInfo s = BestSplitForFeature(hs, f, smaller_, po_s, bounds_[smaller_.leaf], &sp);
+    spl_s[f] = sp;
+    if (s.monotone_type != 0 && s.feature >= 0) s.gain *= MonotonePenalty(tree, smaller_.leaf);
+    if (node_s[f]) bs[f] = s;
+    if (has_larger) {
+      SplitInfo l = BestSplitForFeature(hl, f, larger_, po_l, bounds_[larger_.leaf], &sp);
+      (*spl_l)[f] = sp;
+      if (l.monotone_type != 0 && l.feature >= 0) l.gain *= MonotonePenalty(tree, larger_.leaf);
+      if (node_l[f]) bl[f] = l;
+    }
+  }
+  SplitInfo best_s, best_l;
+  best_s.Reset();
+  best_l.Reset();
+  for (int f = 0; f < num_features_; ++f) {
+    if (bs[f].feature >= 0 && bs[f].BetterThan(best_s)) best_s = bs[f];
+    if (bl[f].feature >= 0 && bl[f].BetterThan(best_l)) best_l = bl[f];
+  }
+  best_split_per_leaf_[smaller_.leaf] = best_s;
+  if (has_larger) best_split_per_leaf_[larger_.leaf] = best_l;
+  SyncBestSplits();
+}
+
+void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) {
+  SplitInfo info = best_split_per_leaf_[best_leaf];
+  const int f = info.feature;
+  const FeatureInfo& fi = train_data_->feature(f);
+  const BinMapper& mapper = train_data_->inner_mapper(f);
+  const int next = tree->num_leaves();
+  *left_leaf = best_leaf;
+  const Dataset* d = train_data_;
+  data_size_t nl;
+  if (fi.bin_type == BinType::Numerical) {
+    const uint32_t thr = info.threshold;
+    const bool dl = info.default_left != 0;
+    const MissingType mt = fi.missing;
+    const uint32_t nan_bin = static_cast<uint32_t>(fi.num_bin - 1);
+    nl = partition_.Split(best_leaf, next, [&](data_size_t r) {
+      const uint32_t b = d->FeatureBin(r, f);
+      if ((mt == MissingType::Zero && b == fi.default_bin) || (mt == MissingType::NaN && b == nan_bin)) return dl;
+      return b <= thr;
+    });
+    if (!global_counts_from_split_) {
+      info.left_count = nl;
+      info.right_count = partition_.count(next);
+    }
+    *right_leaf = tree->Split(best_leaf, f, fi.real_index, thr, mapper.BinToValue(thr), info.left_output,
+                              info.right_output, info.left_count, info.right_count, info.left_sum_hessian,
+                              info.right_sum_hessian, static_cast<float>(info.gain + config_->min_gain_to_split),
+                              mt, dl);
+  } else {
+    const uint32_t* bits = info.cat_bitset;
+    int nwords = 0;
+    std::vector<int> cats;
+    for (int w = 0; w < kMaxCatWords; ++w) {
+      if (bits[w]) nwords = w + 1;
+      for (int j = 0; j < 32; ++j) {
+        if ((bits[w] >> j) & 1) cats.push_back(mapper.bin_to_category()[w * 32 + j]);
+      }
+    }
+    std::vector<uint32_t> inner(bits, bits + nwords);
+    std::vector<uint32_t> raw = common::ConstructBitset(cats.data(), static_cast<int>(cats.size()));
+    nl = partition_.Split(best_leaf, next, [&](data_size_t r) {
+      const uint32_t b = d->FeatureBin(r, f);
+      return common::FindInBitset(inner.data(), nwords, static_cast<int>(b));
+    });
+    if (!global_counts_from_split_) {
+      info.left_count = nl;
+      info.right_count = partition_.count(next);
+    }
+    *right_leaf = tree->SplitCategorical(best_leaf, f, fi.real_index, inner.data(), nwords, raw.data(),
+                                         static_cast<int>(raw.size()), info.left_output, info.right_output,
+                                         info.left_count, info.right_count, info.left_sum_hessian,
+                                         info.right_sum_hessian,
+                                         static_cast<float>(info.gain + config_->min_gain_to_split), fi.missing);
+  }
+  // children statistics; the smaller (by count) child gets the fresh histogram
+  if (info.left_count < info.right_count) {
+    InitLeafStat(&smaller_, *left_leaf, info.left_sum_gradient, info.left_sum_hessian, info.left_output);
+    InitLeafStat(&larger_, *right_leaf, info.right_sum_gradient, info.right_sum_hessian, info.right_output);
+  } else {
+    InitLeafStat(&smaller_, *right_leaf, info.right_sum_gradient, info.right_sum_hessian, info.right_output);
+    InitLeafStat(&larger_, *left_leaf, info.left_sum_gradient, info.left_sum_hessian, info.left_output);
+  }
+  if (global_counts_from_split_) {
+    leaf_count_global_[*left_leaf] = info.left_count;
+    leaf_count_global_[*right_leaf] = info.right_count;
+    smaller_.global_count = leaf_count_global_[smaller_.leaf];
+    larger_.global_count = leaf_count_global_[larger_.leaf];
+  }
+  // basic monotone constraints
+  bounds_[next] = bounds_[best_leaf];
+  if (use_monotone_ && fi.bin_type == BinType::Numerical) {
+    const double mid = (info.left_output + info.right_output) / 2.0f;
+    if (info.monotone_type < 0) {
+      bounds_[best_leaf].min = std::max(bounds_[best_leaf].min, mid);
+      bounds_[next].max = std::min(bounds_[next].max, mid);
+    } else if (info.monotone_type > 0) {
+      bounds_[best_leaf].max = std::min(bounds_[best_leaf].max, mid);
+      bounds_[next].min = std::max(bounds_[next].min, mid);
+    }
+  }
+}
+
+// Forced splits from a JSON file: {"feature": f, "threshold": t, "left": {...}, "right": {...}}.
+namespace {
+struct ForcedNode {
+  int feature = -1;
+  double threshold = 0.0;
+  std::unique_ptr<ForcedNode> left, right;
+};
+std::unique_ptr<ForcedNode> ParseForced(const std::string& s, size_t* pos) {
+  auto skip = [&] { while (*pos < s.size() && std::isspace(static_cast<unsigned char>(s[*pos]))) ++*pos; };
+  skip();
+  if (*pos >= s.size() || s[*pos] != '{') return nullptr;
+  ++*pos;
+  auto node = std::make_unique<ForcedNode>();
+  while (*pos < s.size()) {
+    skip();
+    if (s[*pos] == '}') {
+      ++*pos;
+      break;
+    }
+    if (s[*pos] == ',') {
+      ++*pos;
+      continue;
+    }
+    size_t q1 = s.find('"', *pos), q2 = s.find('"', q1 + 1);
+    std::string key = s.substr(q1 + 1, q2 - q1 - 1);
+    *pos = s.find(':', q2) + 1;
+    skip();
+    if (key == "left" || key == "right") {
+      auto child = ParseForced(s, pos);
+      (key == "left" ? node->left : node->right) = std::move(child);
+    } else {
+      char* e;
+      double v = std::strtod(s.c_str() + *pos, &e);
+      *pos = e - s.c_str();
+      if (key == "feature") node->feature = static_cast<int>(v);
+      else if (key == "threshold") node->threshold = v;
+    }
+  }
+  return node;
+}
+}  // namespace
+
+int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf) {
+  if (forced_json_.empty()) return 0;
+  size_t pos = 0;
+  auto root = ParseForced(forced_json_, &pos);
+  if (!root || root->feature < 0) return 0;
+  int done = 0;
+  std::queue<std::pair<const ForcedNode*, int>> q;
+  q.push({root.get(), 0});
+  while (!q.empty() && done < config_->num_leaves - 1) {
+    auto [node, leaf] = q.front();
+    q.pop();
+    const int inner = train_data_->InnerIndex(node->feature);
+    if (inner < 0) continue;
+    const FeatureInfo& fi = train_data_->feature(inner);
+    if (fi.bin_type != BinType::Numerical) continue;
+    // statistics of `leaf`: build its histogram directly
+    LeafStat ls;
+    double sg, sh;
+    ComputeLeafSums(partition_.indices(leaf), partition_.count(leaf), &sg, &sh);
+    ls.leaf = leaf;
+    ls.sum_g = sg;
+    ls.sum_h = sh;
+    ls.count = ls.global_count = partition_.count(leaf);
+    ls.output = tree->LeafOutput(leaf);
+    auto& h = HistOf(leaf);
+    BuildHistogram(partition_.indices(leaf), partition_.count(leaf), h.data());
+    std::vector<double> full(2 * fi.num_bin);
+    train_data_->FeatureHistogram(h.data(), inner, sg, sh, full.data());
+    const uint32_t thr = train_data_->inner_mapper(inner).ValueToBin(node->threshold);
+    double lg = 0, lh = 0;
+    data_size_t lc = 0;
+    const double cf = ls.count / (sh + 2 * kEpsilon);
+    for (uint32_t b = 0; b <= thr && b < static_cast<uint32_t>(fi.num_bin); ++b) {
+      lg += full[2 * b];
+      lh += full[2 * b + 1];
+      lc += RoundCount(full[2 * b + 1] * cf);
+    }
+    SplitParams p = MakeParams();
+    SplitInfo info;
+    info.Reset();
+    info.feature = inner;
+    info.threshold = thr;
+    info.default_left = 1;
+    info.left_sum_gradient = lg;
+    info.left_sum_hessian = lh;
+    info.right_sum_gradient = sg - lg;
+    info.right_sum_hessian = sh - lh;
+    info.left_output = LeafOutputRaw(lg, lh, p, lc, ls.output);
+    info.right_output = LeafOutputRaw(sg - lg, sh - lh, p, ls.count - lc, ls.output);
+    info.gain = SplitGain(lg, lh, sg - lg, sh - lh, p, 0, lc, ls.count - lc, ls.output, LeafBounds()) -
+                LeafGain(sg, sh, p, ls.count, ls.output) - config_->min_gain_to_split;
+    best_split_per_leaf_[leaf] = info;
+    Split(tree, leaf, left_leaf, right_leaf);
+    ++done;
+    if (node->left) q.push({node->left.get(), *left_leaf});
+    if (node->right) q.push({node->right.get(), *right_leaf});
+  }
+  // fresh start for the regular loop: recompute best splits for all current leaves
+  for (int l = 0; l < tree->num_leaves(); ++l) {
+    double sg, sh;
+    ComputeLeafSums(partition_.indices(l), partition_.count(l), &sg, &sh);
+    LeafStat ls;
+    InitLeafStat(&ls, l, sg, sh, tree->LeafOutput(l));
+    BuildHistogram(partition_.indices(l), partition_.count(l), HistOf(l).data());
+    SplitInfo best;
+    best.Reset();
+    for (int f = 0; f < num_features_; ++f) {
+      if (!col_sampler_.is_feature_used_bytree()[f]) continue;
+      bool sp;
+      SplitInfo s = BestSplitForFeature(HistOf(l).data(), f, ls, ls.output, bounds_[l], &sp);
+      if (s.feature >= 0 && s.BetterThan(best)) best = s;
+    }
+    best_split_per_leaf_[l] = best;
+  }
+  // the main loop resumes with no pending histograms to build
+  *left_leaf = 0;
+  *right_leaf = -1;
+  smaller_.leaf = 0;
+  larger_.leaf = -1;
+  return done;
+}
+
+// ----------------------------------------------------------------------------
+std::unique_ptr<Tree> SerialTreeLearner::FitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
+                                                           const score_t* g, const score_t* h) {
+  auto tree = std::make_unique<Tree>(*old_tree);
+  partition_.ResetByLeafPred(leaf_pred, tree->num_leaves());
+  SplitParams p = MakeParams();
+  for (int i = 0; i < tree->num_leaves(); ++i) {
+    const data_size_t n = partition_.count(i);
+    const data_size_t* idx = partition_.indices(i);
+    double sg = 0.0, sh = kEpsilon;
+    for (data_size_t j = 0; j < n; ++j) {
+      sg += g[idx[j]];
+      sh += h[idx[j]];
+    }
+    double out;
+    if (config_->path_smooth > kEpsilon && i > 0) {
+      out = LeafOutputRaw(sg, sh, p, n, tree->leaf_parent(i));
+    } else {
+      SplitParams q = p;
+      q.path_smooth = 0.0;
+      out = LeafOutputRaw(sg, sh, q, n, 0.0);
+    }
+    const double old_v = tree->LeafOutput(i);
+    const double new_v = out * tree->shrinkage();
+    tree->SetLeafOutput(i, config_->refit_decay_rate * old_v + (1.0 - config_->refit_decay_rate) * new_v);
+  }
+  return tree;
+}
+
+void SerialTreeLearner::AddPredictionToScore(const Tree* tree, double* out_score) const {
+  if (tree->num_leaves() <= 1) {
+    const double v = tree->LeafOutput(0);
+    const data_size_t n = partition_.count(0);
+    const data_size_t* idx = partition_.indices(0);
+#pragma omp parallel for schedule(static)
+    for (data_size_t i = 0; i < n; ++i) out_score[idx[i]] += v;
+    return;
+  }
+#pragma omp parallel for schedule(dynamic)
+  for (int l = 0; l < tree->num_leaves(); ++l) {
+    const double v = tree->LeafOutput(l);
+    const data_size_t n = partition_.count(l);
+    const data_size_t* idx = partition_.indices(l);
+    for (data_size_t i = 0; i < n; ++i) out_score[idx[i]] += v;
+  }
+}
+
+void SerialTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj, const double* score, data_size_t,
+                                        const data_size_t*, data_size_t) const {
+  if (obj == nullptr || !obj->IsRenewTreeOutput()) return;
+  const int nl = tree->num_leaves();
+  std::vector<double> outs(nl, 0.0);
+  std::vector<int> nonzero(nl, 1);
+#pragma omp parallel for schedule(dynamic)
+  for (int l = 0; l < nl; ++l) {
+    const data_size_t n = partition_.count(l);
+    if (n > 0) {
+      outs[l] = obj->RenewTreeOutput(tree->LeafOutput(l), score, partition_.indices(l), n);
+    } else {
+      outs[l] = 0.0;
+      nonzero[l] = 0;
+    }
+  }
+  if (Network::num_machines() > 1) {
+    Network::GlobalSum(&outs);
+    Network::GlobalSum(&nonzero);
+    for (int l = 0; l < nl; ++l) outs[l] = nonzero[l] > 0 ? outs[l] / nonzero[l] : 0.0;
+  }
+  for (int l = 0; l < nl; ++l) tree->SetLeafOutput(l, outs[l]);
+}
+
+std::vector<data_size_t> SerialTreeLearner::LeafIndices(int leaf) const {
+  return std::vector<data_size_t>(partition_.indices(leaf), partition_.indices(leaf) + partition_.count(leaf));
+}
+
+}  // namespace lgap

@@ -1,0 +1,157 @@
+// Host leaf-wise tree learner: the correctness oracle for the HIP learner and
+// the device_type=cpu path. Reference: src/treelearner/serial_tree_learner.{h,cpp},
+// data_partition.hpp, leaf_splits.hpp, col_sampler.hpp, monotone_constraints.hpp
+// (basic method), feature_histogram.hpp (via split_math.h).
+#pragma once
+
+#include <memory>
+#include <set>
+#include <vector>
+
+#include "lgap/random.h"
+#include "lgap/split_math.h"
+#include "lgap/tree_learner.h"
+
+namespace lgap {
+
+// Feature sampling by tree / by node and interaction constraints.
+class ColSampler {
+ public:
+  void Init(const Dataset* data, const Config* cfg);
+  void ResetByTree();
+  std::vector<int8_t> GetByNode(const Tree* tree, int leaf);
+  const std::vector<int8_t>& is_feature_used_bytree() const { return used_bytree_; }
+
+ private:
+  static int GetCnt(size_t total, double fraction);
+  const Dataset* data_ = nullptr;
+  double frac_tree_ = 1.0, frac_node_ = 1.0;
+  bool need_reset_tree_ = false;
+  int used_cnt_tree_ = 0;
+  Random rand_;
+  int seed_ = -1;
+  std::vector<int> valid_;          // real feature indices of used features
+  std::vector<int> used_idx_;       // sampled positions into valid_
+  std::vector<int8_t> used_bytree_;
+  std::vector<std::set<int>> interaction_;
+};
+
+// Contiguous per-leaf index ranges with stable 2-way split.
+class DataPartition {
+ public:
+  void Init(data_size_t num_data, int num_leaves);
+  void SetUsedIndices(const data_size_t* idx, data_size_t n);
+  void Reset();  // all rows (or the bag) into leaf 0
+  // go_left(row) -> bool; returns left count
+  template <typename F>
+  data_size_t Split(int leaf, int right_leaf, F go_left);
+  const data_size_t* indices(int leaf) const { return indices_.data() + begin_[leaf]; }
+  data_size_t count(int leaf) const { return count_[leaf]; }
+  data_size_t begin(int leaf) const { return begin_[leaf]; }
+  void ResetByLeafPred(const std::vector<int>& leaf_pred, int num_leaves);
+  int num_leaves() const { return static_cast<int>(begin_.size()); }
+
+ private:
+  data_size_t num_data_ = 0;
+  std::vector<data_size_t> indices_, tmp_;
+  std::vector<data_size_t> begin_, count_;
+  std::vector<data_size_t> used_;
+  bool use_bag_ = false;
+  data_size_t bag_cnt_ = 0;
+};
+
+struct LeafStat {
+  int leaf = -1;
+  double sum_g = 0.0, sum_h = 0.0;
+  data_size_t count = 0;         // local rows
+  data_size_t global_count = 0;  // all ranks
+  double output = 0.0;           // leaf weight (parent output for path smoothing)
+};
+
+class SerialTreeLearner : public TreeLearner {
+ public:
+  explicit SerialTreeLearner(const Config* config);
+  void Init(const Dataset* train_data, bool is_constant_hessian) override;
+  void ResetConfig(const Config* config) override;
+  void SetBaggingData(const data_size_t* used_indices, data_size_t num_data) override;
+  std::unique_ptr<Tree> Train(const score_t* gradients, const score_t* hessians, bool is_first_tree) override;
+  std::unique_ptr<Tree> FitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
+                                          const score_t* gradients, const score_t* hessians) override;
+  void AddPredictionToScore(const Tree* tree, double* out_score) const override;
+  void RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj, const double* score, data_size_t total_num_data,
+                       const data_size_t* bag_indices, data_size_t bag_cnt) const override;
+  std::vector<data_size_t> LeafIndices(int leaf) const override;
+
+ protected:
+  // ---- hooks for the parallel learners
+  virtual void BeforeTrain();
+  virtual bool BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf);
+  virtual void FindBestSplits(const Tree* tree);
+  virtual void ConstructHistograms(bool use_subtract);
+  virtual void FindBestSplitsFromHistograms(const Tree* tree, bool use_subtract);
+  virtual void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf);
+  virtual data_size_t GlobalCount(int leaf) const { return leaf < 0 ? 0 : leaf_count_global_[leaf]; }
+  // parallel learners: agree on the best split of the two current leaves
+  virtual void SyncBestSplits() {}
+
+  void BuildHistogram(const data_size_t* idx, data_size_t n, double* hist) const;
+  void ComputeLeafSums(const data_size_t* idx, data_size_t n, double* sg, double* sh) const;
+  SplitInfo BestSplitForFeature(const double* group_hist, int f, const LeafStat& leaf, double parent_output,
+                                const LeafBounds& bounds, bool* splittable) const;
+  double ParentOutput(const Tree* tree, const LeafStat& ls) const;
+  double MonotonePenalty(const Tree* tree, int leaf) const;
+  void InitLeafStat(LeafStat* ls, int leaf, double sg, double sh, double output);
+  SplitParams MakeParams() const;
+  std::vector<double>& HistOf(int leaf);
+  int ForceSplits(Tree* tree, int* left_leaf, int* right_leaf);
+
+  const Config* config_;
+  const Dataset* train_data_ = nullptr;
+  data_size_t num_data_ = 0;
+  int num_features_ = 0;
+  const score_t* gradients_ = nullptr;
+  const score_t* hessians_ = nullptr;
+  bool is_constant_hessian_ = false;
+  DataPartition partition_;
+  ColSampler col_sampler_;
+  std::vector<SplitInfo> best_split_per_leaf_;
+  std::vector<std::vector<double>> hist_;            // per leaf, 2*num_total_bin
+  std::vector<std::vector<char>> splittable_;        // per leaf, per feature
+  std::vector<LeafBounds> bounds_;                   // monotone basic constraints
+  std::vector<data_size_t> leaf_count_global_;
+  LeafStat smaller_, larger_;
+  int parent_leaf_ = -1;  // leaf whose histogram became the larger child's (subtraction source)
+  bool has_parent_hist_ = false;
+  Random extra_rand_;
+  bool use_monotone_ = false;
+  std::string forced_json_;
+  std::vector<Random> extra_rands_;
+  // parallel learners
+  std::vector<char> feature_mask_;       // features scanned by this rank
+  int hist_begin_ = 0, hist_end_ = -1;   // histogram entries (bins) owned by this rank; -1 = all
+  bool global_counts_from_split_ = false;
+};
+
+// ---------------------------------------------------------------------------
+template <typename F>
+data_size_t DataPartition::Split(int leaf, int right_leaf, F go_left) {
+  const data_size_t b = begin_[leaf], n = count_[leaf];
+  data_size_t* src = indices_.data() + b;
+  data_size_t* dst = tmp_.data() + b;
+  // two-pass stable partition (left kept in order, right kept in order)
+  data_size_t nl = 0;
+  for (data_size_t i = 0; i < n; ++i) if (go_left(src[i])) dst[nl++] = src[i];
+  data_size_t nr = nl;
+  for (data_size_t i = 0; i < n; ++i) if (!go_left(src[i])) dst[nr++] = src[i];
+  std::copy(dst, dst + n, src);
+  if (right_leaf >= static_cast<int>(begin_.size())) {
+    begin_.resize(right_leaf + 1, 0);
+    count_.resize(right_leaf + 1, 0);
+  }
+  count_[leaf] = nl;
+  begin_[right_leaf] = b + nl;
+  count_[right_leaf] = n - nl;
+  return nl;
+}
+
+}  // namespace lgap
