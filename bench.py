@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Headline benchmark: boosting iterations/sec + AUC on synthetic Higgs-shape
+10M x 28 binary data, 255 bins, 63 leaves (BASELINE.json), HIP learner on MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+
+N>1 runs under torchrun, one process per GPU: the 10M training rows are split
+evenly across ranks (strong scaling: the job always trains on the same 10M x 28
+dataset) and every tree is grown data-parallel with the smaller child's
+histogram all-reduced over RCCL. A "step" is one full boosting iteration
+(gradients, tree growth, score update). W untimed iterations, then exactly K
+timed iterations between barrier + device synchronisation on both sides; the
+max over ranks is reported. AUC is computed after timing on a held-out set.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_IT_S = 4.31  # GTX 1080 OpenCL, Higgs 500 iters (docs/GPU-Performance.rst:99)
+METRIC = "boosting iters/sec + AUC, synthetic Higgs-shape 10M×28, 255 bins, 63 leaves"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--valid-rows", type=int, default=500_000)
+    ap.add_argument("--num-leaves", type=int, default=63)
+    ap.add_argument("--max-bin", type=int, default=255)
+    ap.add_argument("--device", default="gpu")
+    ap.add_argument("--seed", type=int, default=7)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: --gpus N>1 must be launched with torchrun (one process per GPU)", file=sys.stderr)
+            return 2
+
+    import lambdagap_amd as lgb
+    from lambdagap_amd.parallel import device_synchronize, init_device_comm, shard_range
+    from lambdagap_amd.utils import make_higgs_like
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        init_device_comm()
+    t_data = time.time()
+    start, stop = shard_range(args.rows, rank, world)
+    X, y = make_higgs_like(args.rows, seed=args.seed, start=start, stop=stop)
+    params = {
+        "objective": "binary",
+        "num_leaves": args.num_leaves,
+        "max_bin": args.max_bin,
+        "learning_rate": 0.1,
+        "min_data_in_leaf": 1,
+        "min_sum_hessian_in_leaf": 100,
+        "device_type": args.device,
+        "verbosity": -1,
+        "seed": args.seed,
+    }
+    if world > 1:
+        params.update({"tree_learner": "data", "num_machines": world, "pre_partition": True})
+    train_set = lgb.Dataset(X, y, params=params, free_raw_data=True)
+    booster = lgb.Booster(params=params, train_set=train_set)
+    del X
+    t_data = time.time() - t_data
+
+    def barrier_sync():
+        device_synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        booster.update()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        booster.update()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    auc = None
+    if rank == 0:
+        Xv, yv = make_higgs_like(args.valid_rows, seed=args.seed + 1000)
+        pred = booster.predict(Xv)
+        auc = _auc(yv, pred)
+    if rank == 0:
+        it_s = args.steps / elapsed
+        out = {
+            "metric": METRIC,
+            "value": round(it_s, 4),
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(it_s / BASELINE_IT_S, 3),
+            "dtype": "fp32",
+            "data": "synthetic",
+            "auc": round(auc, 6),
+            "config": {
+                "model": f"gbdt binary, {args.num_leaves} leaves, {args.max_bin} bins, lr 0.1",
+                "global_batch": args.rows,
+                "seq_len": 28,
+                "parallelism": f"dp{world}",
+                "device": booster.device_name(),
+                "setup_s": round(t_data, 2),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+    return 0
+
+
+def _auc(y: np.ndarray, p: np.ndarray) -> float:
+    order = np.argsort(p, kind="mergesort")
+    ps = p[order]
+    ys = y[order]
+    # average ranks for ties
+    ranks = np.empty(len(p), dtype=np.float64)
+    i = 0
+    n = len(p)
+    idx = np.flatnonzero(np.diff(ps)) + 1
+    bounds = np.concatenate([[0], idx, [n]])
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        ranks[a:b] = (a + b + 1) / 2.0
+    npos = ys.sum()
+    nneg = n - npos
+    return float((ranks[ys > 0].sum() - npos * (npos + 1) / 2.0) / (npos * nneg))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

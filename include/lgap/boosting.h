@@ -124,6 +124,15 @@ class GBDT {
   void set_objective_for_prediction(std::unique_ptr<ObjectiveFunction> o) { loaded_objective_ = std::move(o); objective_ = loaded_objective_.get(); }
   const std::string& loaded_parameter() const { return loaded_parameter_; }
   TreeLearner* tree_learner() { return learner_.get(); }
+  // Gradients / hessians of the last boosting round (downloaded from the device in device mode).
+  void GetGradients(std::vector<score_t>* g, std::vector<score_t>* h) const {
+    if (device_mode_ && learner_) {
+      learner_->DeviceGetGradients(g, h);
+    } else {
+      *g = gradients_;
+      *h = hessians_;
+    }
+  }
   const Config* config() const { return config_; }
   int best_iteration() const { return best_iter_; }
   std::string parser_config_str_;

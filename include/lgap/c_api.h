@@ -188,6 +188,20 @@ LIGHTGBM_C_EXPORT int LGBM_GetMaxThreads(int* out);
 
 /* ---- MI355X device helpers (LambdaGap extension) */
 LIGHTGBM_C_EXPORT int LGBM_DeviceCount(int* out);
+// Waits for all queued device work of this process (timing brackets).
+LIGHTGBM_C_EXPORT int LGBM_DeviceSynchronize();
+// ---- kernel-level entry points (numerics tests / ops module)
+// Gradients and hessians of the last boosting round (class-major); pass null buffers to query *out_len.
+LIGHTGBM_C_EXPORT int LGBM_BoosterGetGradients(BoosterHandle handle, int64_t* out_len, float* grad, float* hess);
+// Packed group layout: groups, total histogram bins, bytes per group bin, per-group histogram start.
+LIGHTGBM_C_EXPORT int LGBM_DatasetGetGroupLayout(DatasetHandle handle, int* num_groups, int* num_total_bin,
+                                                 int* bin_width, int32_t* hist_start);
+// Row-major [num_data x num_groups] group bins.
+LIGHTGBM_C_EXPORT int LGBM_DatasetGetGroupBins(DatasetHandle handle, uint16_t* out);
+// (grad, hess) histogram over `rows` (null = all rows) built by the HIP histogram kernel:
+// out_hist has 2 * num_total_bin doubles; group bin 0 (all features at their most frequent bin) stays 0.
+LIGHTGBM_C_EXPORT int LGBM_DeviceHistogram(DatasetHandle handle, const float* grad, const float* hess,
+                                           const int32_t* rows, int32_t num_rows, double* out_hist);
 LIGHTGBM_C_EXPORT int LGBM_DeviceCommGetUniqueId(char* out, int64_t buffer_len, int64_t* out_len);
 LIGHTGBM_C_EXPORT int LGBM_DeviceCommInit(const char* unique_id, int64_t id_len, int num_ranks, int rank,
                                           int device_id);

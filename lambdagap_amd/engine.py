@@ -1,0 +1,314 @@
+"""High-level training API: :func:`train`, :func:`cv`, :class:`CVBooster`.
+
+Reference: python-package/lightgbm/engine.py (train loop with callbacks and
+early stopping, k-fold CV with stratification / group folds).
+"""
+from __future__ import annotations
+
+import copy
+from collections import OrderedDict, defaultdict
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple, Union
+
+import numpy as np
+
+from . import callback as cb
+from .basic import Booster, Dataset, LightGBMError, _choose_param_value
+
+__all__ = ["train", "cv", "CVBooster"]
+
+
+def _pop_num_rounds(params: Dict[str, Any], num_boost_round: int) -> Tuple[Dict[str, Any], int]:
+    params = dict(params)
+    for alias in ("num_iterations", "num_iteration", "n_iter", "num_tree", "num_trees", "num_round", "num_rounds",
+                  "nrounds", "num_boost_round", "n_estimators", "max_iter"):
+        if alias in params:
+            num_boost_round = int(params.pop(alias))
+    params["num_iterations"] = num_boost_round
+    return params, num_boost_round
+
+
+def _early_stop_params(params: Dict[str, Any]) -> Tuple[Optional[int], bool, float]:
+    rounds = None
+    for alias in ("early_stopping_round", "early_stopping_rounds", "early_stopping", "n_iter_no_change"):
+        if alias in params and params[alias] is not None:
+            rounds = int(params[alias])
+    first_only = bool(params.get("first_metric_only", False))
+    min_delta = float(params.get("early_stopping_min_delta", 0.0))
+    return rounds, first_only, min_delta
+
+
+def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100,
+          valid_sets: Optional[List[Dataset]] = None, valid_names: Optional[List[str]] = None,
+          feval: Optional[Union[Callable, List[Callable]]] = None, init_model: Optional[Union[str, Booster]] = None,
+          feature_name: Any = "auto", categorical_feature: Any = "auto", keep_training_booster: bool = False,
+          callbacks: Optional[List[Callable]] = None) -> Booster:
+    """Train a booster for ``num_boost_round`` rounds."""
+    if not isinstance(train_set, Dataset):
+        raise TypeError(f"train() only accepts Dataset object, train_set has type '{type(train_set).__name__}'.")
+    params = copy.deepcopy(params) if params else {}
+    fobj = None
+    obj = params.get("objective")
+    if callable(obj):
+        fobj = obj
+        params["objective"] = "none"
+    params, num_boost_round = _pop_num_rounds(params, num_boost_round)
+    if num_boost_round <= 0:
+        raise ValueError("num_boost_round should be greater than zero.")
+    es_rounds, first_only, min_delta = _early_stop_params(params)
+    if feature_name != "auto":
+        train_set.feature_name = feature_name
+    if categorical_feature != "auto":
+        train_set.categorical_feature = categorical_feature
+    if isinstance(init_model, str):
+        predictor = Booster(model_file=init_model)
+    elif isinstance(init_model, Booster):
+        predictor = init_model
+    else:
+        predictor = None
+    init_iteration = predictor.current_iteration() if predictor is not None else 0
+    if predictor is not None:
+        # continue training from the scores of the existing model
+        if train_set.init_score is None and train_set.data is not None and not isinstance(train_set.data, str):
+            train_set.init_score = predictor.predict(train_set.data, raw_score=True)
+    booster = Booster(params=params, train_set=train_set)
+    if predictor is not None:
+        booster.merge_models_from = predictor  # keep alive
+        from .basic import _LIB, _check
+        _check(_LIB.LGBM_BoosterMerge(booster.handle, predictor.handle))
+    valid_sets = valid_sets or []
+    names = valid_names or []
+    is_valid_contain_train = False
+    train_data_name = "training"
+    for i, vs in enumerate(valid_sets):
+        if vs is train_set:
+            is_valid_contain_train = True
+            if i < len(names):
+                train_data_name = names[i]
+            continue
+        name = names[i] if i < len(names) else f"valid_{i}"
+        if vs.reference is None:
+            vs.set_reference(train_set)
+        booster.add_valid(vs, name)
+    booster.set_train_data_name(train_data_name)
+    callbacks = list(callbacks or [])
+    if es_rounds is not None and es_rounds > 0:
+        verbose = int(params.get("verbosity", params.get("verbose", 1))) > 0
+        callbacks.append(cb.early_stopping(es_rounds, first_only, verbose=verbose, min_delta=min_delta))
+    before = sorted([c for c in callbacks if getattr(c, "before_iteration", False)], key=lambda c: getattr(c, "order", 0))
+    after = sorted([c for c in callbacks if not getattr(c, "before_iteration", False)],
+                   key=lambda c: getattr(c, "order", 0))
+    booster.best_iteration = 0
+    evaluation_result_list: List[Any] = []
+    for i in range(init_iteration, init_iteration + num_boost_round):
+        for c in before:
+            c(cb.CallbackEnv(model=booster, params=params, iteration=i, begin_iteration=init_iteration,
+                             end_iteration=init_iteration + num_boost_round, evaluation_result_list=None))
+        finished = booster.update(fobj=fobj)
+        evaluation_result_list = []
+        if valid_sets or feval is not None:
+            if is_valid_contain_train:
+                evaluation_result_list.extend(booster.eval_train(feval))
+            evaluation_result_list.extend(booster.eval_valid(feval))
+        try:
+            for c in after:
+                c(cb.CallbackEnv(model=booster, params=params, iteration=i, begin_iteration=init_iteration,
+                                 end_iteration=init_iteration + num_boost_round,
+                                 evaluation_result_list=evaluation_result_list))
+        except cb.EarlyStopException as e:
+            booster.best_iteration = e.best_iteration + 1
+            evaluation_result_list = e.best_score
+            break
+        if finished:
+            break
+    booster.best_score = defaultdict(OrderedDict)
+    for item in evaluation_result_list:
+        booster.best_score[item[0]][item[1]] = item[2]
+    if not keep_training_booster:
+        booster.free_dataset()
+    return booster
+
+
+class CVBooster:
+    """The boosters of a k-fold cross-validation run."""
+
+    def __init__(self, model_file: Optional[str] = None):
+        self.boosters: List[Booster] = []
+        self.best_iteration = -1
+        if model_file is not None:
+            import json
+
+            with open(model_file) as f:
+                self._from_dict(json.load(f))
+
+    def _append(self, booster: Booster) -> None:
+        self.boosters.append(booster)
+
+    def _from_dict(self, models: Dict[str, Any]) -> None:
+        self.best_iteration = models["best_iteration"]
+        self.boosters = [Booster(model_str=s) for s in models["boosters"]]
+
+    def _to_dict(self, num_iteration: Optional[int], start_iteration: int, importance_type: str) -> Dict[str, Any]:
+        return {"best_iteration": self.best_iteration,
+                "boosters": [b.model_to_string(num_iteration=num_iteration, start_iteration=start_iteration,
+                                               importance_type=importance_type) for b in self.boosters]}
+
+    def model_to_string(self, num_iteration: Optional[int] = None, start_iteration: int = 0,
+                        importance_type: str = "split") -> str:
+        import json
+
+        return json.dumps(self._to_dict(num_iteration, start_iteration, importance_type))
+
+    def model_from_string(self, model_str: str) -> "CVBooster":
+        import json
+
+        self._from_dict(json.loads(model_str))
+        return self
+
+    def save_model(self, filename: str, num_iteration: Optional[int] = None, start_iteration: int = 0,
+                   importance_type: str = "split") -> "CVBooster":
+        with open(filename, "w") as f:
+            f.write(self.model_to_string(num_iteration, start_iteration, importance_type))
+        return self
+
+    def __getattr__(self, name: str) -> Callable:
+        def handler(*args: Any, **kwargs: Any) -> List[Any]:
+            return [getattr(b, name)(*args, **kwargs) for b in self.boosters]
+
+        return handler
+
+
+def _make_folds(full: Dataset, folds, nfold: int, params: Dict[str, Any], seed: int, fpreproc, stratified: bool,
+                shuffle: bool, eval_train_metric: bool):
+    full.construct()
+    num_data = full.num_data()
+    if folds is not None:
+        if hasattr(folds, "split"):
+            group_info = full.get_group()
+            if group_info is not None:
+                group_info = np.asarray(group_info, dtype=np.int32)
+                flatted_group = np.repeat(np.arange(len(group_info)), repeats=group_info)
+            else:
+                flatted_group = np.zeros(num_data, dtype=np.int32)
+            folds = folds.split(X=np.empty(num_data), y=full.get_label(), groups=flatted_group)
+    else:
+        objective = str(params.get("objective", "regression"))
+        if objective in ("lambdarank", "rank_xendcg", "xendcg", "xe_ndcg", "xe_ndcg_mart", "xendcg_mart"):
+            group_info = np.asarray(full.get_group(), dtype=np.int32)
+            if group_info is None:
+                raise LightGBMError("Ranking tasks require query information")
+            rng = np.random.RandomState(seed)
+            nq = len(group_info)
+            order = rng.permutation(nq) if shuffle else np.arange(nq)
+            bounds = np.concatenate([[0], np.cumsum(group_info)])
+            qfolds = np.array_split(order, nfold)
+            folds = []
+            for k in range(nfold):
+                test_q = np.sort(qfolds[k])
+                test_idx = np.concatenate([np.arange(bounds[q], bounds[q + 1]) for q in test_q]) if len(test_q) else \
+                    np.array([], dtype=np.int64)
+                mask = np.ones(num_data, dtype=bool)
+                mask[test_idx] = False
+                folds.append((np.where(mask)[0], test_idx))
+        elif stratified:
+            label = np.asarray(full.get_label())
+            rng = np.random.RandomState(seed)
+            test_of = np.empty(num_data, dtype=np.int64)
+            for cls in np.unique(label):
+                idx = np.where(label == cls)[0]
+                if shuffle:
+                    idx = rng.permutation(idx)
+                for k, part in enumerate(np.array_split(idx, nfold)):
+                    test_of[part] = k
+            folds = [(np.where(test_of != k)[0], np.where(test_of == k)[0]) for k in range(nfold)]
+        else:
+            rng = np.random.RandomState(seed)
+            idx = rng.permutation(num_data) if shuffle else np.arange(num_data)
+            parts = np.array_split(idx, nfold)
+            folds = []
+            for k in range(nfold):
+                test = np.sort(parts[k])
+                train_idx = np.sort(np.concatenate([parts[j] for j in range(nfold) if j != k]))
+                folds.append((train_idx, test))
+    ret = CVBooster()
+    for train_idx, test_idx in folds:
+        train_set = full.subset(sorted(train_idx))
+        valid_set = full.subset(sorted(test_idx))
+        if fpreproc is not None:
+            train_set, valid_set, tparam = fpreproc(train_set, valid_set, params.copy())
+        else:
+            tparam = params
+        b = Booster(tparam, train_set)
+        if eval_train_metric:
+            b.add_valid(train_set, "train")
+        b.add_valid(valid_set, "valid")
+        ret._append(b)
+    return ret
+
+
+def _agg_cv_result(raw_results: List[List[Tuple[str, str, float, bool]]]):
+    cvmap: Dict[str, List[float]] = OrderedDict()
+    metric_type: Dict[str, bool] = {}
+    for one in raw_results:
+        for one_line in one:
+            key = f"{one_line[0]} {one_line[1]}"
+            metric_type[key] = one_line[3]
+            cvmap.setdefault(key, []).append(one_line[2])
+    return [("cv_agg", k, float(np.mean(v)), metric_type[k], float(np.std(v))) for k, v in cvmap.items()]
+
+
+def cv(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100, folds=None, nfold: int = 5,
+       stratified: bool = True, shuffle: bool = True, metrics: Optional[Union[str, List[str]]] = None,
+       feval: Optional[Union[Callable, List[Callable]]] = None, init_model=None, feature_name: Any = "auto",
+       categorical_feature: Any = "auto", fpreproc=None, seed: int = 0, callbacks: Optional[List[Callable]] = None,
+       eval_train_metric: bool = False, return_cvbooster: bool = False) -> Dict[str, Any]:
+    """k-fold cross validation; returns {"valid <metric>-mean": [...], "valid <metric>-stdv": [...]}."""
+    if not isinstance(train_set, Dataset):
+        raise TypeError(f"cv() only accepts Dataset object, train_set has type '{type(train_set).__name__}'.")
+    params = copy.deepcopy(params) if params else {}
+    fobj = None
+    if callable(params.get("objective")):
+        fobj = params["objective"]
+        params["objective"] = "none"
+    params, num_boost_round = _pop_num_rounds(params, num_boost_round)
+    es_rounds, first_only, min_delta = _early_stop_params(params)
+    if metrics is not None:
+        params["metric"] = metrics
+    if feature_name != "auto":
+        train_set.feature_name = feature_name
+    if categorical_feature != "auto":
+        train_set.categorical_feature = categorical_feature
+    train_set._update_params(params)
+    results: Dict[str, List[float]] = defaultdict(list)
+    cvfolds = _make_folds(train_set, folds, nfold, params, seed, fpreproc, stratified, shuffle, eval_train_metric)
+    callbacks = list(callbacks or [])
+    if es_rounds is not None and es_rounds > 0:
+        verbose = int(params.get("verbosity", params.get("verbose", 1))) > 0
+        callbacks.append(cb.early_stopping(es_rounds, first_only, verbose=verbose, min_delta=min_delta))
+    before = sorted([c for c in callbacks if getattr(c, "before_iteration", False)], key=lambda c: getattr(c, "order", 0))
+    after = sorted([c for c in callbacks if not getattr(c, "before_iteration", False)],
+                   key=lambda c: getattr(c, "order", 0))
+    for i in range(num_boost_round):
+        for c in before:
+            c(cb.CallbackEnv(model=cvfolds, params=params, iteration=i, begin_iteration=0,
+                             end_iteration=num_boost_round, evaluation_result_list=None))
+        raw = []
+        for b in cvfolds.boosters:
+            b.update(fobj=fobj)
+            raw.append(b.eval_valid(feval))
+        res = _agg_cv_result(raw)
+        for _, key, mean, _, std in res:
+            results[f"{key}-mean"].append(mean)
+            results[f"{key}-stdv"].append(std)
+        try:
+            for c in after:
+                c(cb.CallbackEnv(model=cvfolds, params=params, iteration=i, begin_iteration=0,
+                                 end_iteration=num_boost_round, evaluation_result_list=res))
+        except cb.EarlyStopException as e:
+            cvfolds.best_iteration = e.best_iteration + 1
+            for k in results:
+                results[k] = results[k][:cvfolds.best_iteration]
+            break
+    out = dict(results)
+    if return_cvbooster:
+        out["cvbooster"] = cvfolds
+    return out

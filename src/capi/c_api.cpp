@@ -1040,6 +1040,53 @@ int LGBM_DeviceCount(int* out) {
   API_END();
 }
 
+int LGBM_BoosterGetGradients(BoosterHandle handle, int64_t* out_len, float* grad, float* hess) {
+  API_BEGIN();
+  std::vector<score_t> g, h;
+  B(handle)->boosting_->GetGradients(&g, &h);
+  *out_len = static_cast<int64_t>(g.size());
+  if (grad) std::copy(g.begin(), g.end(), grad);
+  if (hess) std::copy(h.begin(), h.end(), hess);
+  API_END();
+}
+
+int LGBM_DatasetGetGroupLayout(DatasetHandle handle, int* num_groups, int* num_total_bin, int* bin_width,
+                               int32_t* hist_start) {
+  API_BEGIN();
+  const Dataset* d = D(handle)->ds.get();
+  *num_groups = d->num_groups();
+  *num_total_bin = d->num_total_bin();
+  *bin_width = d->bin_width();
+  if (hist_start) {
+    for (int g = 0; g < d->num_groups(); ++g) hist_start[g] = d->group(g).hist_start;
+  }
+  API_END();
+}
+
+int LGBM_DatasetGetGroupBins(DatasetHandle handle, uint16_t* out) {
+  API_BEGIN();
+  const Dataset* d = D(handle)->ds.get();
+  const int ng = d->num_groups();
+#pragma omp parallel for schedule(static)
+  for (data_size_t i = 0; i < d->num_data(); ++i) {
+    for (int g = 0; g < ng; ++g) out[static_cast<size_t>(i) * ng + g] = static_cast<uint16_t>(d->GroupBin(i, g));
+  }
+  API_END();
+}
+
+int LGBM_DeviceHistogram(DatasetHandle handle, const float* grad, const float* hess, const int32_t* rows,
+                         int32_t num_rows, double* out_hist) {
+  API_BEGIN();
+  device::DeviceHistogram(D(handle)->ds.get(), grad, hess, rows, num_rows, out_hist);
+  API_END();
+}
+
+int LGBM_DeviceSynchronize() {
+  API_BEGIN();
+  device::DeviceSynchronize();
+  API_END();
+}
+
 int LGBM_DeviceCommGetUniqueId(char* out, int64_t buffer_len, int64_t* out_len) {
   API_BEGIN();
   std::string id = device::CommGetUniqueId();

@@ -1319,7 +1319,45 @@ class DeviceTreeLearner : public TreeLearner {
 
   std::string DeviceName() const override { return device_name_; }
 
+  // One histogram of (g, h) over `rows` (identity when null) into `out` (2 * TB doubles).
+  void TestHistogram(const float* g, const float* h, const int* rows, int n, double* out) {
+    K_ = 1;
+    gh_.Resize(static_cast<size_t>(N_));
+    DeviceSetGradients(g, h, 1);
+    if (rows) idx_[2].Upload(rows, n, stream_);
+    Ctl* hc = pin_ctl_.Get(1);
+    std::memset(hc, 0, sizeof(Ctl));
+    hc->num_leaves = 1;
+    hc->larger = -1;
+    LeafRange* hr = pin_range_.Get(L_);
+    hr[0].buf = rows ? 2 : -1;
+    hr[0].start = 0;
+    hr[0].count = rows ? n : N_;
+    hr[0].pad = 0;
+    HIP_CHECK(hipMemcpyAsync(ctl_.get(), hc, sizeof(Ctl), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(range_.get(), hr, sizeof(LeafRange), hipMemcpyHostToDevice, stream_));
+    staging_.Zero(stream_);
+    LaunchHist(MakeArgs());
+    staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    staging_.Zero(stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
  private:
+  int HistBlocks() const {
+    const int want = config_->device_hist_blocks > 0 ? config_->device_hist_blocks : 2 * num_cu_;
+    return std::max(1, std::min(want, DivUp(N_, kHistMinRows)));
+  }
+
+  void LaunchHist(const Args& a) {
+    const dim3 hgrid(HistBlocks(), num_tiles_);
+    if (width_ == 1) k_hist<1><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
+    else k_hist<2><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
+    HIP_CHECK(hipGetLastError());
+    if (distributed_) AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), stream_);
+  }
+
   void UploadData() {
     // packed rows
     const size_t rb = static_cast<size_t>(N_) * stride_dw_;
@@ -1515,16 +1553,9 @@ class DeviceTreeLearner : public TreeLearner {
   void EnqueueTree() {
     const Args a = MakeArgs();
     hipStream_t s = stream_;
-    const int hist_blocks = std::max(1, std::min(config_->device_hist_blocks > 0 ? config_->device_hist_blocks : 2 * num_cu_,
-                                                 DivUp(N_, kHistMinRows)));
     const int part_blocks = std::max(1, std::min(max_tiles_, 4 * num_cu_));
     const int scan_blocks = std::max(1, DivUp(F_, kScanWaves));
-    const dim3 hgrid(hist_blocks, num_tiles_);
-    auto hist = [&]() {
-      if (width_ == 1) k_hist<1><<<hgrid, kHistThreads, hist_lds_bytes_, s>>>(a);
-      else k_hist<2><<<hgrid, kHistThreads, hist_lds_bytes_, s>>>(a);
-      if (distributed_) AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), s);
-    };
+    auto hist = [&]() { LaunchHist(a); };
     k_init_tree<<<1, kNodeThreads, 0, s>>>(a);
     k_root_sums<<<std::max(1, std::min(DivUp(N_, 256), 4 * num_cu_)), 256, 0, s>>>(a);
     if (distributed_) AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
@@ -1672,6 +1703,17 @@ std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const
   }
   Log::Fatal("Unknown tree learner type %s", parallel_mode.c_str());
   return nullptr;
+}
+
+void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, const int* rows, int num_rows,
+                     double* out) {
+  if (DeviceCount() <= 0) Log::Fatal("DeviceHistogram: no AMD GPU visible to HIP");
+  Config cfg;
+  cfg.num_leaves = 2;
+  cfg.verbosity = -1;
+  DeviceTreeLearner learner(&cfg, false);
+  learner.Init(data, false);
+  learner.TestHistogram(grad, hess, rows, num_rows, out);
 }
 
 }  // namespace device

@@ -132,6 +132,10 @@ int DeviceCount() {
   return n;
 }
 
+void DeviceSynchronize() {
+  if (DeviceCount() > 0) HIP_CHECK(hipDeviceSynchronize());
+}
+
 std::string CommGetUniqueId() {
   ncclUniqueId id;
   NcclCheck(ncclGetUniqueId(&id), "ncclGetUniqueId");

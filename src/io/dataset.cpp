@@ -15,6 +15,7 @@
 
 #include "lgap/common.h"
 #include "lgap/log.h"
+#include "lgap/network.h"
 #include "lgap/random.h"
 
 namespace lgap {
@@ -370,6 +371,19 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
                         cat_set.count(j) ? BinType::Categorical : BinType::Numerical, cfg.use_missing,
                         cfg.zero_as_missing, forced[j]);
   }
+  // ---- distributed: every rank adopts the mappers of the feature's owner rank
+  // (features dealt round-robin; reference dataset_loader.cpp:1166-1262 splits
+  // the feature range and allgathers serialized BinMappers the same way).
+  const int nm = Network::num_machines();
+  if (nm > 1) {
+    std::vector<char> mine;
+    for (int j = Network::rank(); j < num_total_features_; j += nm) mappers_[j].Serialize(&mine);
+    auto blobs = Network::AllgatherBlobs(mine);
+    for (int r = 0; r < nm; ++r) {
+      const char* p = blobs[r].data();
+      for (int j = r; j < num_total_features_; j += nm) p += mappers_[j].Deserialize(p);
+    }
+  }
   // ---- used features
   used_map_.assign(num_total_features_, -1);
   features_.clear();
@@ -420,6 +434,31 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
     }
   }
   BuildGroups(cfg, nz, static_cast<data_size_t>(sample_idx.size()));
+  if (nm > 1) {
+    // bundles were decided on local samples: adopt rank 0's so histogram layouts agree
+    std::vector<char> mine;
+    if (Network::rank() == 0) {
+      auto put = [&mine](int v) { mine.insert(mine.end(), reinterpret_cast<char*>(&v), reinterpret_cast<char*>(&v) + 4); };
+      put(static_cast<int>(groups_.size()));
+      for (auto& g : groups_) {
+        put(static_cast<int>(g.features.size()));
+        for (int f : g.features) put(f);
+      }
+    }
+    auto blobs = Network::AllgatherBlobs(mine);
+    const char* p = blobs[0].data();
+    auto get = [&p]() {
+      int v;
+      std::memcpy(&v, p, 4);
+      p += 4;
+      return v;
+    };
+    groups_.assign(get(), FeatureGroup());
+    for (auto& g : groups_) {
+      g.features.resize(get());
+      for (auto& f : g.features) f = get();
+    }
+  }
   FinalizeLayout();
   PackRows(src);
   metadata_.Init(num_data_);

@@ -1,0 +1,34 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD MI355X (gfx950) GPU and the HIP kernels")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(scope="session")
+def lgb():
+    import lambdagap_amd
+
+    return lambdagap_amd
+
+
+@pytest.fixture(scope="session")
+def gpu_required(lgb):
+    """GPU tests fail loudly (never skip) when the device path is unavailable."""
+    n = lgb.device_count()
+    assert n >= 1, "GPU test requested but the native library sees no gfx950 device"
+    return n
+
+
+@pytest.fixture
+def rng():
+    return np.random.default_rng(12345)

@@ -1,0 +1,124 @@
+"""HIP tree learner vs the CPU oracle learner (same data, same parameters)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _auc(y, p):
+    from sklearn.metrics import roc_auc_score
+
+    return roc_auc_score(y, p)
+
+
+def _train(lgb, X, y, device, rounds=1, **kw):
+    params = {"objective": "binary", "num_leaves": 31, "device_type": device, "verbosity": -1,
+              "min_data_in_leaf": 20, "seed": 1, "deterministic": True}
+    params.update(kw)
+    ds = lgb.Dataset(X, y, params=params)
+    return lgb.train(params, ds, rounds)
+
+
+def _trees(b):
+    return b.dump_model()["tree_info"]
+
+
+def _splits(node, out):
+    if "split_index" in node:
+        out.append((node["split_feature"], node["threshold"], node["default_left"]))
+        _splits(node["left_child"], out)
+        _splits(node["right_child"], out)
+    return out
+
+
+@pytest.mark.parametrize("extra", [{}, {"lambda_l1": 1.0, "lambda_l2": 2.0},
+                                   {"max_depth": 4}, {"path_smooth": 5.0},
+                                   {"min_sum_hessian_in_leaf": 5.0, "max_delta_step": 0.7}])
+def test_first_tree_matches_cpu(lgb, gpu_required, rng, extra):
+    from lambdagap_amd.utils import make_higgs_like
+
+    X, y = make_higgs_like(40000, seed=5)
+    bc = _train(lgb, X, y, "cpu", **extra)
+    bg = _train(lgb, X, y, "gpu", **extra)
+    assert "gfx950" in bg.device_name() or "MI3" in bg.device_name()
+    tc, tg = _trees(bc)[0], _trees(bg)[0]
+    assert tc["num_leaves"] == tg["num_leaves"]
+    assert _splits(tc["tree_structure"], []) == _splits(tg["tree_structure"], [])
+    pc, pg = bc.predict(X[:5000], raw_score=True), bg.predict(X[:5000], raw_score=True)
+    np.testing.assert_allclose(pg, pc, rtol=1e-5, atol=1e-6)
+
+
+def test_missing_values_and_categorical(lgb, gpu_required, rng):
+    n = 30000
+    X = rng.standard_normal((n, 6))
+    X[rng.random(n) < 0.2, 0] = np.nan
+    X[rng.random(n) < 0.5, 1] = 0.0
+    X[:, 2] = rng.integers(0, 12, n)
+    y = ((np.nan_to_num(X[:, 0]) > 0.3) ^ (X[:, 2] % 3 == 0) ^ (X[:, 1] > 0.5)).astype(float)
+    kw = {"categorical_feature": [2], "max_cat_to_onehot": 4}
+    bc = _train(lgb, X, y, "cpu", rounds=3, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=3, **kw)
+    for tc, tg in zip(_trees(bc), _trees(bg)):
+        assert _splits(tc["tree_structure"], []) == _splits(tg["tree_structure"], [])
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-5)
+
+
+def test_auc_parity_with_cpu_oracle(lgb, gpu_required):
+    """BASELINE.md accuracy criterion: |AUC_gpu - AUC_cpu| <= 1e-3 on identical synthetic data."""
+    from lambdagap_amd.utils import make_higgs_like
+
+    X, y = make_higgs_like(200000, seed=11)
+    Xv, yv = make_higgs_like(50000, seed=12)
+    kw = {"num_leaves": 63, "learning_rate": 0.1, "min_data_in_leaf": 1, "min_sum_hessian_in_leaf": 100}
+    bc = _train(lgb, X, y, "cpu", rounds=40, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=40, **kw)
+    ac, ag = _auc(yv, bc.predict(Xv)), _auc(yv, bg.predict(Xv))
+    assert abs(ac - ag) <= 1e-3, (ac, ag)
+
+
+@pytest.mark.parametrize("objective,extra", [("regression", {}), ("huber", {"alpha": 0.8}),
+                                             ("poisson", {}), ("multiclass", {"num_class": 3}),
+                                             ("regression_l1", {})])
+def test_objectives_on_device(lgb, gpu_required, rng, objective, extra):
+    n = 20000
+    X = rng.standard_normal((n, 8))
+    if objective == "multiclass":
+        y = (np.digitize(X[:, 0] + 0.3 * X[:, 1], [-0.5, 0.5])).astype(float)
+    elif objective == "poisson":
+        y = rng.poisson(np.exp(0.5 * X[:, 0])).astype(float)
+    else:
+        y = 2 * X[:, 0] - X[:, 1] ** 2 + 0.1 * rng.standard_normal(n)
+    params = {"objective": objective, "num_leaves": 15, "verbosity": -1, **extra}
+    bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y), 5)
+    bg = lgb.train({**params, "device_type": "gpu"}, lgb.Dataset(X, y), 5)
+    np.testing.assert_allclose(bg.predict(X[:2000], raw_score=True), bc.predict(X[:2000], raw_score=True),
+                               rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("target", ["ndcg", "lambdaloss_ndcg", "bndcg", "precision", "arp_k", "ranknet",
+                                    "bin_ranknet", "gap_s", "gap_x_plus_plus", "lambdaloss_arp2"])
+def test_lambdarank_targets_on_device(lgb, gpu_required, rng, target):
+    from lambdagap_amd.utils import make_ranking
+
+    X, y, sizes = make_ranking(300, num_features=20, seed=3)
+    if target in ("bndcg", "precision", "arp_k", "bin_ranknet", "gap_s", "gap_x_plus_plus"):
+        y = (y >= 3).astype(np.float32)
+    params = {"objective": "lambdarank", "lambdarank_target": target, "num_leaves": 15, "verbosity": -1,
+              "lambdarank_truncation_level": 10}
+    bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y, group=sizes), 3)
+    bg = lgb.train({**params, "device_type": "gpu"}, lgb.Dataset(X, y, group=sizes), 3)
+    pc, pg = bc.predict(X, raw_score=True), bg.predict(X, raw_score=True)
+    assert np.corrcoef(pc, pg)[0, 1] > 0.999
+    np.testing.assert_allclose(pg, pc, rtol=5e-3, atol=5e-3)
+
+
+def test_bagging_goss_feature_fraction_on_device(lgb, gpu_required):
+    from lambdagap_amd.utils import make_higgs_like
+
+    X, y = make_higgs_like(60000, seed=21)
+    for kw in ({"bagging_fraction": 0.7, "bagging_freq": 1}, {"data_sample_strategy": "goss"},
+               {"feature_fraction": 0.6}, {"extra_trees": True}):
+        bc = _train(lgb, X, y, "cpu", rounds=5, **kw)
+        bg = _train(lgb, X, y, "gpu", rounds=5, **kw)
+        np.testing.assert_allclose(bg.predict(X[:3000], raw_score=True), bc.predict(X[:3000], raw_score=True),
+                                   rtol=1e-3, atol=1e-4)
