@@ -1,0 +1,34 @@
+#!/bin/bash
+# GPU check sequence for one gpurun call. Every GPU step has its own time limit;
+# the script stops at the first fault / abort / timeout (anything other than a
+# clean exit or an ordinary pytest failure).
+set -u
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <limit-seconds> <cmd...>
+  local name=$1 lim=$2; shift 2
+  echo "=== $name" | tee -a $OUT/steps.log
+  timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -5 $OUT/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    info) step info 300 python -c "import lambdagap_amd as l; print('devices', l.device_count())";;
+    kernels) step kernels 900 python -m pytest tests/test_gpu_kernels.py -q --timeout 300 -p no:cacheprovider;;
+    learner) step learner 1200 python -m pytest tests/test_gpu_learner.py -q --timeout 300 -p no:cacheprovider;;
+    gputests) step gputests 1500 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider;;
+    debugrank) step debugrank 300 python scripts/debug_rank.py ndcg;;
+    debugcat) step debugcat 300 python scripts/debug_cat.py && step debugcatdp 300 python scripts/debug_cat.py dp;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
+    bench1m) step bench1m 400 python bench.py --rows 1000000 --steps 10 --warmup 2;;
+    bench) step bench 900 python bench.py --steps 30 --warmup 3;;
+    timetag) LGAP_TIMETAG=1 step timetag 900 python bench.py --steps 20 --warmup 3;;
+    prof) step prof 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2;;
+  esac
+done
+echo ALLDONE

@@ -92,6 +92,8 @@ struct Args {
   SplitRec* rec;
   double* slots;
   double* staging;
+  void* hist_slab;
+  unsigned* ghmax;  // float bits of max|g|, max|h| over the root rows
   uint8_t* splittable;
   SplitInfo* scan_out;
   int* tile_cnt;
@@ -205,6 +207,8 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     r.pad = 0;
     a.range[0] = r;
     a.lsum[0] = make_double2(0.0, 0.0);
+    a.ghmax[0] = 0u;
+    a.ghmax[1] = 0u;
     a.gcount[0] = tp.root_gcount;
     a.depth[0] = 0;
     a.lout[0] = 0.0;
@@ -222,14 +226,26 @@ __global__ __launch_bounds__(256) void k_root_sums(Args a) {
   const TreeParams tp = *a.tp;
   const float2* gh = a.gh + static_cast<size_t>(tp.cls) * a.N;
   double g = 0.0, h = 0.0;
+  float mg = 0.f, mh = 0.f;
   const int stride = gridDim.x * blockDim.x;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tp.root_count; i += stride) {
     const float2 v = gh[RowAt(a, tp.root_buf, i)];
     g += v.x;
     h += v.y;
+    mg = fmaxf(mg, fabsf(v.x));
+    mh = fmaxf(mh, fabsf(v.y));
   }
   g = WaveSum(g);
   h = WaveSum(h);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
+    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&a.ghmax[0], __float_as_uint(mg));
+    atomicMax(&a.ghmax[1], __float_as_uint(mh));
+  }
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     sh[w] = g;
@@ -248,11 +264,126 @@ __global__ __launch_bounds__(256) void k_root_sums(Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// histogram of the smaller leaf into `staging` (fp64), LDS-privatised per block
+// histogram of the smaller leaf.
+//
+// gfx950 executes LDS float atomics (ds_add_f32/f64) at a small fraction of the
+// integer rate (measured, scripts/hist_micro.hip: 10M x 28 root histogram 2.06 ms
+// with ds_add_f32 vs 0.195 ms with ds_add_u64), so the per-block histogram is
+// accumulated in FIXED POINT:
+//   default    one ds_add_u64 per (row, group): signed g in the high 32 bits,
+//              signed h in the low 32 bits, each scaled by 2^30 / (rows_in_block *
+//              max|.|) so no partial sum can overflow; low-part borrows are undone
+//              when unpacking. Per-value resolution ~2^-30 * rows * max|g|, below
+//              the error of fp32 accumulation for any bin with more than a few
+//              hundred rows.
+//   gpu_use_dp two ds_add_u64 (g, h) at scale 2^62 / (rows * max|.|): ~2^-47
+//              relative, indistinguishable from the CPU's double sums.
+// Each active block unpacks its LDS histogram to real values and stores it into
+// its own slab row (plain coalesced stores); k_hist_reduce sums the rows into
+// `staging` (fp64). No float atomics anywhere on the hot path.
 
-template <int W>
+__device__ __forceinline__ int HistActiveBlocks(int n, int grid) {
+  int nb = (n + kHistMinRows - 1) / kHistMinRows;
+  return nb > grid ? grid : nb;
+}
+
+// MODE 0: packed (g32|h32) in one u64; MODE 1: two u64 (gpu_use_dp)
+template <int W, int MODE>
+__device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& tile, const LeafRange& r, int cls, int rb,
+                                              int re, const int* gst, unsigned long long* hist, float sg, float sh,
+                                              double dsg, double dsh) {
+  const int tpr = tile.d1 - tile.d0;
+  const int rpi = blockDim.x / tpr;
+  const int myr = threadIdx.x / tpr;
+  const int myd = threadIdx.x - myr * tpr;
+  if (myr >= rpi) return;
+  constexpr int per = 4 / W;
+  constexpr int R = 4;  // rows in flight per thread
+  const int dw = tile.d0 + myd;
+  const int gfirst = dw * per;
+  int go[per];
+#pragma unroll
+  for (int k = 0; k < per; ++k) go[k] = gfirst + k < tile.g1 ? gst[gfirst + k - tile.g0] : -1;
+  const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
+  const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf] + r.start;
+  const int base = r.buf < 0 ? r.start : 0;
+  for (int p0 = rb + myr; p0 < re; p0 += rpi * R) {
+    int rows[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = p0 + j * rpi;
+      rows[j] = p < re ? (idx ? idx[p] : base + p) : -1;
+    }
+    uint32_t word[R];
+    float2 v[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
+      v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      unsigned long long pg, ph = 0ull;
+      if (MODE == 0) {
+        const long long ig = __float2int_rn(v[j].x * sg);
+        const long long ih = __float2int_rn(v[j].y * sh);
+        pg = (static_cast<unsigned long long>(ig) << 32) + static_cast<unsigned long long>(ih);
+      } else {
+        pg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v[j].x) * dsg));
+        ph = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v[j].y) * dsh));
+      }
+#pragma unroll
+      for (int k = 0; k < per; ++k) {
+        const uint32_t b = W == 1 ? ((word[j] >> (8 * k)) & 0xFFu) : ((word[j] >> (16 * k)) & 0xFFFFu);
+        if (b != 0u && go[k] >= 0) {
+          const int o = go[k] + static_cast<int>(b);
+          if (MODE == 0) {
+            atomicAdd(&hist[o], pg);
+          } else {
+            atomicAdd(&hist[2 * o], pg);
+            atomicAdd(&hist[2 * o + 1], ph);
+          }
+        }
+      }
+    }
+  }
+}
+
+// Rows of the (rare) tiles whose bins exceed the LDS budget: fp64 atomics into
+// the block's own slab row (global memory, no cross-block contention).
+template <int W, typename Acc>
+__device__ void HistRowsDirect(const Args& a, const HistTile& tile, const LeafRange& r, int cls, int rb, int re,
+                               const int* gst, Acc* hist) {
+  const int tpr = tile.d1 - tile.d0;
+  const int rpi = blockDim.x / tpr;
+  const int myr = threadIdx.x / tpr;
+  const int myd = threadIdx.x - myr * tpr;
+  if (myr >= rpi) return;
+  constexpr int per = 4 / W;
+  const int dw = tile.d0 + myd;
+  const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
+  const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf] + r.start;
+  const int base = r.buf < 0 ? r.start : 0;
+  for (int p = rb + myr; p < re; p += rpi) {
+    const int row = idx ? idx[p] : base + p;
+    const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
+    const float2 v = gh[row];
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+      const uint32_t b = W == 1 ? ((word >> (8 * k)) & 0xFFu) : ((word >> (16 * k)) & 0xFFFFu);
+      const int g = dw * per + k;
+      if (b != 0u && g < tile.g1) {
+        const int o = gst[g - tile.g0] + static_cast<int>(b);
+        atomicAdd(&hist[2 * o], static_cast<Acc>(v.x));
+        atomicAdd(&hist[2 * o + 1], static_cast<Acc>(v.y));
+      }
+    }
+  }
+}
+
+template <int W, int MODE>
 __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
-  extern __shared__ float lds[];
+  extern __shared__ __align__(8) unsigned char lds_raw[];
   const Ctl* cp = a.ctl;
   if (cp->done || cp->skip) return;
   const int leaf = cp->smaller;
@@ -260,50 +391,86 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   const HistTile tile = a.tiles[blockIdx.y];
   const LeafRange r = a.range[leaf];
   const int n = r.count;
-  int nb = (n + kHistMinRows - 1) / kHistMinRows;
-  if (nb > static_cast<int>(gridDim.x)) nb = gridDim.x;
+  const int nb = HistActiveBlocks(n, gridDim.x);
   if (static_cast<int>(blockIdx.x) >= nb) return;
   const int chunk = (n + nb - 1) / nb;
   const int rb = blockIdx.x * chunk;
   const int re = min(n, rb + chunk);
-  int* gst = reinterpret_cast<int*>(lds + 2 * tile.nbins);
-  for (int i = threadIdx.x; i < 2 * tile.nbins; i += blockDim.x) lds[i] = 0.f;
+  double* slab = reinterpret_cast<double*>(a.hist_slab) + (static_cast<size_t>(blockIdx.x) * a.TB + tile.bin0) * 2;
+  float* slabf = reinterpret_cast<float*>(a.hist_slab) + (static_cast<size_t>(blockIdx.x) * a.TB + tile.bin0) * 2;
+  if (tile.direct) {
+    int* gst = reinterpret_cast<int*>(lds_raw);
+    for (int i = threadIdx.x; i < 2 * tile.nbins; i += blockDim.x) {
+      if (MODE == 0) slabf[i] = 0.f;
+      else slab[i] = 0.0;
+    }
+    for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
+    __threadfence_block();
+    __syncthreads();
+    if (MODE == 0) HistRowsDirect<W, float>(a, tile, r, cls, rb, re, gst, slabf);
+    else HistRowsDirect<W, double>(a, tile, r, cls, rb, re, gst, slab);
+    return;
+  }
+  const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
+  const double rows_in_block = static_cast<double>(re - rb > 0 ? re - rb : 1);
+  const double kPk = 1073741824.0;            // 2^30
+  const double kDp = 4611686018427387904.0;   // 2^62
+  const double sgd = gmax > 0.f ? kPk / (rows_in_block * gmax) : 1.0;
+  const double shd = hmax > 0.f ? kPk / (rows_in_block * hmax) : 1.0;
+  const double dsg = gmax > 0.f ? kDp / (rows_in_block * gmax) : 1.0;
+  const double dsh = hmax > 0.f ? kDp / (rows_in_block * hmax) : 1.0;
+  // float scales rounded down so |v * s| never exceeds the bound
+  const float sg = static_cast<float>(sgd) * 0.99999f, sh = static_cast<float>(shd) * 0.99999f;
+  const int words = MODE == 0 ? tile.nbins : 2 * tile.nbins;
+  unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
+  int* gst = reinterpret_cast<int*>(hist + words);
+  for (int i = threadIdx.x; i < words; i += blockDim.x) hist[i] = 0ull;
   for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
   __syncthreads();
-  const int tpr = tile.d1 - tile.d0;
-  const int rpi = blockDim.x / tpr;
-  const int myr = threadIdx.x / tpr;
-  const int myd = threadIdx.x - myr * tpr;
-  if (myr < rpi) {
-    constexpr int per = 4 / W;
-    const int dw = tile.d0 + myd;
-    const int gfirst = dw * per;
-    const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
-    const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf];
-    for (int p = rb + myr; p < re; p += rpi) {
-      const int row = idx ? idx[r.start + p] : r.start + p;
-      const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
-      const float2 v = gh[row];
-#pragma unroll
-      for (int k = 0; k < per; ++k) {
-        const uint32_t b = W == 1 ? ((word >> (8 * k)) & 0xFFu) : ((word >> (16 * k)) & 0xFFFFu);
-        const int g = gfirst + k;
-        if (b != 0u && g < tile.g1) {
-          const int o = gst[g - tile.g0] + static_cast<int>(b);
-          atomicAdd(&lds[2 * o], v.x);
-          atomicAdd(&lds[2 * o + 1], v.y);
-        }
-      }
+  HistRowsFixed<W, MODE>(a, tile, r, cls, rb, re, gst, hist, sg, sh, dsg * 0.99999, dsh * 0.99999);
+  __syncthreads();
+  if (MODE == 0) {
+    const double ig = 1.0 / (static_cast<double>(sg)), ih = 1.0 / (static_cast<double>(sh));
+    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
+      const unsigned long long x = hist[i];
+      const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
+      const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
+      slabf[2 * i] = static_cast<float>(static_cast<double>(gs) * ig);
+      slabf[2 * i + 1] = static_cast<float>(static_cast<double>(hs) * ih);
+    }
+  } else {
+    const double ig = 1.0 / (dsg * 0.99999), ih = 1.0 / (dsh * 0.99999);
+    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
+      slab[2 * i] = static_cast<double>(static_cast<long long>(hist[2 * i])) * ig;
+      slab[2 * i + 1] = static_cast<double>(static_cast<long long>(hist[2 * i + 1])) * ih;
     }
   }
+}
+
+// staging[v] = sum over the active blocks' slab rows (v over 2 * TB values).
+// 64 consecutive values per workgroup, its 16 waves split the slab rows.
+template <typename Acc>
+__global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid) {
+  __shared__ double part[16][64];
+  const Ctl* cp = a.ctl;
+  if (cp->done || cp->skip) return;
+  const int n = a.range[cp->smaller].count;
+  const int nb = HistActiveBlocks(n, hist_grid);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const size_t V = 2 * static_cast<size_t>(a.TB);
+  const size_t v = static_cast<size_t>(blockIdx.x) * 64 + lane;
+  const Acc* slab = reinterpret_cast<const Acc*>(a.hist_slab);
+  double s = 0.0;
+  if (v < V) {
+    for (int p = w; p < nb; p += 16) s += static_cast<double>(slab[static_cast<size_t>(p) * V + v]);
+  }
+  part[w][lane] = s;
   __syncthreads();
-  double* st = a.staging + 2 * static_cast<size_t>(tile.bin0);
-  for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
-    const float g = lds[2 * i], h = lds[2 * i + 1];
-    if (g != 0.f || h != 0.f) {
-      atomicAdd(&st[2 * i], static_cast<double>(g));
-      atomicAdd(&st[2 * i + 1], static_cast<double>(h));
-    }
+  if (w == 0 && v < V) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += part[i][lane];
+    a.staging[v] = t;
   }
 }
 
@@ -514,8 +681,6 @@ __global__ __launch_bounds__(kScanWaves * 64) void k_scan(Args a) {
   double* st = a.staging + 2 * static_cast<size_t>(fi.hist_offset);
   for (int k = lane; k < nst; k += 64) {
     const double g = st[2 * k], h = st[2 * k + 1];
-    st[2 * k] = 0.0;
-    st[2 * k + 1] = 0.0;
     hs[2 * k] = g;
     hs[2 * k + 1] = h;
     if (hl) {
@@ -1011,7 +1176,7 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipSetDevice(device_id_));
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device_id_));
-    device_name_ = std::string(prop.name) + " (" + prop.gcnArchName + ")";
+    device_name_ = std::string(prop.name[0] ? prop.name : "AMD GPU") + " (" + prop.gcnArchName + ")";
     num_cu_ = prop.multiProcessorCount;
     if (!stream_) HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (!config_->interaction_constraints_vector.empty()) {
@@ -1020,6 +1185,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (!config_->forcedsplits_filename.empty()) {
       Log::Fatal("forcedsplits_filename is not supported by the HIP learner yet; use device_type=cpu");
     }
+    use_dp_ = config_->gpu_use_dp;
     UploadData();
     ResetConfig(config_);
     Log::Info("HIP tree learner on %s: %d rows, %d features, %d groups, %d bins%s", device_name_.c_str(), N_, F_, G_,
@@ -1336,6 +1502,16 @@ class DeviceTreeLearner : public TreeLearner {
     hr[0].pad = 0;
     HIP_CHECK(hipMemcpyAsync(ctl_.get(), hc, sizeof(Ctl), hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemcpyAsync(range_.get(), hr, sizeof(LeafRange), hipMemcpyHostToDevice, stream_));
+    float mg = 0.f, mh = 0.f;
+    for (int i = 0; i < (rows ? n : N_); ++i) {
+      const int r = rows ? rows[i] : i;
+      mg = std::max(mg, std::fabs(g[r]));
+      mh = std::max(mh, std::fabs(h[r]));
+    }
+    unsigned* hm = pin_max_.Get(2);
+    std::memcpy(&hm[0], &mg, 4);
+    std::memcpy(&hm[1], &mh, 4);
+    HIP_CHECK(hipMemcpyAsync(ghmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
     staging_.Zero(stream_);
     LaunchHist(MakeArgs());
     staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
@@ -1347,13 +1523,24 @@ class DeviceTreeLearner : public TreeLearner {
  private:
   int HistBlocks() const {
     const int want = config_->device_hist_blocks > 0 ? config_->device_hist_blocks : 2 * num_cu_;
-    return std::max(1, std::min(want, DivUp(N_, kHistMinRows)));
+    // partial-histogram slab: one row of 2 * TB accumulators per block, capped at 4 GiB
+    const size_t row_bytes = 2 * static_cast<size_t>(TB_) * (use_dp_ ? 8 : 4);
+    const int mem_cap = static_cast<int>(std::max<size_t>(1, (size_t(4) << 30) / std::max<size_t>(row_bytes, 1)));
+    return std::max(1, std::min({want, DivUp(N_, kHistMinRows), mem_cap}));
   }
 
   void LaunchHist(const Args& a) {
     const dim3 hgrid(HistBlocks(), num_tiles_);
-    if (width_ == 1) k_hist<1><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
-    else k_hist<2><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
+    if (use_dp_) {
+      if (width_ == 1) k_hist<1, 1><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
+      else k_hist<2, 1><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
+    } else {
+      if (width_ == 1) k_hist<1, 0><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
+      else k_hist<2, 0><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
+    }
+    const int rgrid = DivUp(2 * static_cast<long long>(TB_), 64);
+    if (use_dp_) k_hist_reduce<double><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks());
+    else k_hist_reduce<float><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks());
     HIP_CHECK(hipGetLastError());
     if (distributed_) AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), stream_);
   }
@@ -1415,9 +1602,11 @@ class DeviceTreeLearner : public TreeLearner {
 
   void BuildTiles() {
     const int per = 4 / width_;
-    const int max_bins = kHistLdsBytes / 8 - 64;
+    const size_t acc = use_dp_ ? 16 : 8;  // LDS bytes per bin (grad + hess)
+    const int max_bins = static_cast<int>(kHistLdsBytes / acc) - 64;
     const int max_dw = kHistThreads / 2;
     std::vector<HistTile> tiles;
+    hist_lds_bytes_ = 16;
     int d = 0;
     const int nd = DivUp(G_, per);
     while (d < nd) {
@@ -1437,13 +1626,22 @@ class DeviceTreeLearner : public TreeLearner {
       t.d1 = e;
       t.g1 = std::min(G_, e * per);
       t.nbins = bins;
+      // a single dword of huge bundles that cannot fit: accumulate straight into global memory
+      t.direct = bins > max_bins ? 1 : 0;
       tiles.push_back(t);
-      hist_lds_bytes_ = std::max(hist_lds_bytes_, static_cast<size_t>(bins) * 8 + sizeof(int) * (t.g1 - t.g0) + 16);
+      if (!t.direct) {
+        hist_lds_bytes_ = std::max(hist_lds_bytes_, static_cast<size_t>(bins) * acc + sizeof(int) * (t.g1 - t.g0) + 16);
+      } else {
+        hist_lds_bytes_ = std::max(hist_lds_bytes_, sizeof(int) * (t.g1 - t.g0) + 16);
+      }
       d = e;
     }
     if (hist_lds_bytes_ > 64 * 1024) {
-      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(width_ == 1 ? k_hist<1> : k_hist<2>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
+      const void* fn = use_dp_ ? (width_ == 1 ? reinterpret_cast<const void*>(k_hist<1, 1>)
+                                              : reinterpret_cast<const void*>(k_hist<2, 1>))
+                               : (width_ == 1 ? reinterpret_cast<const void*>(k_hist<1, 0>)
+                                              : reinterpret_cast<const void*>(k_hist<2, 0>));
+      HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
     }
     num_tiles_ = static_cast<int>(tiles.size());
     tiles_.Upload(tiles, stream_);
@@ -1465,6 +1663,8 @@ class DeviceTreeLearner : public TreeLearner {
     slots_.Resize(L * 2 * static_cast<size_t>(TB_));
     staging_.Resize(2 * static_cast<size_t>(TB_));
     staging_.Zero(stream_);
+    ghmax_.Resize(2);
+    hist_slab_.Resize(static_cast<size_t>(HistBlocks()) * 2 * TB_ * (use_dp_ ? 8 : 4));
     splittable_.Resize(L * F_);
     scan_out_.Resize(2 * static_cast<size_t>(F_));
     max_tiles_ = std::max(1, DivUp(N_, kTileRows));
@@ -1520,6 +1720,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.rec = rec_.get();
     a.slots = slots_.get();
     a.staging = staging_.get();
+    a.hist_slab = hist_slab_.get();
+    a.ghmax = ghmax_.get();
     a.splittable = splittable_.get();
     a.scan_out = scan_out_.get();
     a.tile_cnt = tile_cnt_.get();
@@ -1639,7 +1841,7 @@ class DeviceTreeLearner : public TreeLearner {
   const Dataset* data_ = nullptr;
   int N_ = 0, F_ = 0, G_ = 0, TB_ = 0, width_ = 1, stride_dw_ = 1, L_ = 2, K_ = 1;
   int device_id_ = 0, num_cu_ = 256, num_tiles_ = 0, max_tiles_ = 1, max_cat_bin_ = 1;
-  bool has_cat_ = false, use_bag_ = false, use_bynode_ = false;
+  bool has_cat_ = false, use_bag_ = false, use_bynode_ = false, use_dp_ = false;
   data_size_t bag_cnt_ = 0;
   size_t hist_lds_bytes_ = 0;
   std::string device_name_;
@@ -1668,6 +1870,8 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<SplitInfo> best_;
   DevBuf<SplitRec> rec_;
   DevBuf<double> slots_, staging_;
+  DevBuf<char> hist_slab_;
+  DevBuf<unsigned> ghmax_;
   DevBuf<uint8_t> splittable_;
   DevBuf<SplitInfo> scan_out_;
   DevBuf<int> tile_cnt_, tile_off_;
@@ -1688,6 +1892,7 @@ class DeviceTreeLearner : public TreeLearner {
   PinnedBuf<double> pin_lout_;
   PinnedBuf<float2> pin_gh_;
   PinnedBuf<char> pin_tree_;
+  PinnedBuf<unsigned> pin_max_;
 };
 
 }  // namespace

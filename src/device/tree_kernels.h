@@ -37,6 +37,8 @@ struct HistTile {
   int g0, g1;    // groups [g0, g1)
   int bin0;      // global histogram index of the first bin of group g0
   int nbins;     // bins covered
+  int direct;    // 1: bins exceed the LDS budget, accumulate in global memory
+  int pad;
 };
 
 // Rows of a leaf: positions [start, start+count) of index buffer `buf`

@@ -184,8 +184,12 @@ class LambdarankObjective : public RankingBase {
     double best, worst;
     if (target_ == kTgtPrecision) {
       const data_size_t kk = std::min<data_size_t>(k_, cnt);
-      std::nth_element(idx.begin(), idx.begin() + (kk - 1), idx.end(),
-                       [score](data_size_t a, data_size_t b) { return score[a] > score[b]; });
+      // top-k by score with ties to the lower index: a deterministic choice of
+      // the reference's nth_element set (ties there are implementation-defined),
+      // identical to the device kernel's stable-sorted prefix
+      std::nth_element(idx.begin(), idx.begin() + (kk - 1), idx.end(), [score](data_size_t a, data_size_t b) {
+        return score[a] > score[b] || (score[a] == score[b] && a < b);
+      });
       auto mm = std::minmax_element(score, score + cnt);
       worst = *mm.first;
       best = *mm.second;
