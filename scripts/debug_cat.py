@@ -27,9 +27,15 @@ def walk(node, out, depth=0):
     return out
 
 
-bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y, params=params), 1)
-bg = lgb.train({**params, "device_type": "gpu", "gpu_use_dp": dp}, lgb.Dataset(X, y, params=params), 1)
-sc = sorted(walk(bc.dump_model()["tree_info"][0]["tree_structure"], []))
-sg = sorted(walk(bg.dump_model()["tree_info"][0]["tree_structure"], []))
-for a, b in zip(sc, sg):
-    print("SAME" if a[1:4] == b[1:4] else "DIFF", a, "|", b)
+bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y, params=params), 3)
+bg = lgb.train({**params, "device_type": "gpu", "gpu_use_dp": dp}, lgb.Dataset(X, y, params=params), 3)
+for t in range(3):
+    sc = sorted(walk(bc.dump_model()["tree_info"][t]["tree_structure"], []))
+    sg = sorted(walk(bg.dump_model()["tree_info"][t]["tree_structure"], []))
+    nd = 0
+    for a, b in zip(sc, sg):
+        if a[1:3] != b[1:3]:
+            nd += 1
+            if nd <= 4:
+                print("tree", t, "DIFF", a, "|", b)
+    print("tree", t, "splits", len(sc), len(sg), "diffs", nd)

@@ -38,6 +38,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -66,6 +68,7 @@ constexpr int kPartThreads = 256;
 constexpr int kPartIters = 16;
 constexpr int kTileRows = kPartThreads * kPartIters;
 constexpr int kScanWaves = 4;
+constexpr int kScanThreads = 1024;
 constexpr int kNodeThreads = 256;
 
 struct Args {
@@ -99,9 +102,11 @@ struct Args {
   int* tile_cnt;
   int* tile_off;
   unsigned* rng;
-  double* cat_scratch;
   int max_cat_bin;
+  int max_bin;  // largest feature num_bin (LDS sizing of k_reduce_scan)
   int max_depth;
+  int fuse_post;
+  unsigned long long* stamps;  // optional phase timestamps (LGAP_STAMPS=1)
   int distributed;
   int use_monotone;
   double monotone_penalty;
@@ -141,6 +146,14 @@ __device__ __forceinline__ uint32_t ColBin(const Args& a, int g, int row) {
 }
 
 __device__ __forceinline__ int RowAt(const Args& a, int buf, int pos) { return buf < 0 ? pos : a.idx[buf][pos]; }
+
+// Diagnostic phase stamps: [kernel 0..3][split 0..255][block 0..1][stamp 0..7], 100 MHz wall clock.
+__device__ __forceinline__ void Stamp(const Args& a, int kernel, int i) {
+  if (a.stamps != nullptr && blockIdx.x < 2 && blockIdx.y == 0 && threadIdx.x == 0) {
+    const int split = a.ctl->num_splits & 255;
+    a.stamps[((static_cast<size_t>(kernel) * 256 + split) * 2 + blockIdx.x) * 8 + i] = wall_clock64();
+  }
+}
 
 // block = 256 threads: sum of an int
 __device__ int BlockSumInt(int v, int* sh) {
@@ -198,7 +211,7 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     c.left_count = 0;
     c.cls = tp.cls;
     c.scan_round = 0;
-    c.pad = 0;
+    c.max_count = tp.root_count;
     *a.ctl = c;
     LeafRange r;
     r.buf = tp.root_buf;
@@ -298,7 +311,7 @@ __device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& til
   const int myd = threadIdx.x - myr * tpr;
   if (myr >= rpi) return;
   constexpr int per = 4 / W;
-  constexpr int R = 4;  // rows in flight per thread
+  constexpr int R = 16;  // rows in flight per thread
   const int dw = tile.d0 + myd;
   const int gfirst = dw * per;
   int go[per];
@@ -396,6 +409,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   const int chunk = (n + nb - 1) / nb;
   const int rb = blockIdx.x * chunk;
   const int re = min(n, rb + chunk);
+  Stamp(a, 2, 0);
   double* slab = reinterpret_cast<double*>(a.hist_slab) + (static_cast<size_t>(blockIdx.x) * a.TB + tile.bin0) * 2;
   float* slabf = reinterpret_cast<float*>(a.hist_slab) + (static_cast<size_t>(blockIdx.x) * a.TB + tile.bin0) * 2;
   if (tile.direct) {
@@ -427,8 +441,10 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   for (int i = threadIdx.x; i < words; i += blockDim.x) hist[i] = 0ull;
   for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
   __syncthreads();
+  Stamp(a, 2, 1);
   HistRowsFixed<W, MODE>(a, tile, r, cls, rb, re, gst, hist, sg, sh, dsg * 0.99999, dsh * 0.99999);
   __syncthreads();
+  Stamp(a, 2, 2);
   if (MODE == 0) {
     const double ig = 1.0 / (static_cast<double>(sg)), ih = 1.0 / (static_cast<double>(sh));
     for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
@@ -448,7 +464,8 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
 }
 
 // staging[v] = sum over the active blocks' slab rows (v over 2 * TB values).
-// 64 consecutive values per workgroup, its 16 waves split the slab rows.
+// Used where the full histogram must exist in one place: data-parallel
+// training (all-reduced over RCCL before the scan) and the kernel tests.
 template <typename Acc>
 __global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid) {
   __shared__ double part[16][64];
@@ -475,7 +492,7 @@ __global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid) {
 }
 
 // ---------------------------------------------------------------------------
-// split scan: one wave per feature
+// split finding: one workgroup per feature (k_reduce_scan)
 
 struct Cand {
   double gain, lg, lh;
@@ -509,23 +526,14 @@ __device__ __forceinline__ Cand WaveBest(Cand c, bool prefer_high) {
   return r;
 }
 
-__device__ __forceinline__ void BinValue(const double* H, int mfb, int b, double mg, double mh, double* g, double* h) {
-  if (b == mfb) {
-    *g = mg;
-    *h = mh;
-  } else {
-    const int k = b < mfb ? b : b - 1;
-    *g = H[2 * k];
-    *h = H[2 * k + 1];
-  }
-}
-
-// Numerical threshold search over a full feature histogram (implicit mfb),
-// matching FindBestNumerical in split_math.h. Returns splittable; lane 0's
-// `out` holds the result.
+// Numerical threshold search of one wave over a FULL feature histogram H
+// (LDS, num_bin (g, h) pairs, most-frequent bin included). Same semantics as
+// FindBestNumerical (split_math.h / feature_histogram.hpp:830-1057): reverse
+// pass (right side grows from the top bin) and, with missing values, the
+// forward pass; SKIP_DEFAULT_BIN / NA_AS_MISSING as masks; first-max tie rules.
+// Returns splittable; lane 0's `out` holds the result.
 __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const double* H, double sg, double sh_raw,
-                                  int n, double po, const LeafBounds& bounds, int rand_thr, double mg, double mh,
-                                  SplitInfo* out) {
+                                  int n, double po, const LeafBounds& bounds, int rand_thr, SplitInfo* out) {
   const int lane = threadIdx.x & 63;
   const SplitParams& p = a.sp;
   const double sum_h = sh_raw + 2 * kEpsilon;
@@ -538,7 +546,6 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
   const int top = nb - 1 - (na ? 1 : 0);
   const bool use_rand = p.extra_trees != 0;
   const int8_t mono = fi.monotone;
-  // ---- reverse pass (right side accumulates from the top bin down)
   Cand rb;
   rb.gain = kMinScore;
   rb.thr = -1;
@@ -551,13 +558,13 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
     const int b = base - lane;
     double g = 0.0, h = 0.0;
     int c = 0;
-    const bool incl = b >= 0 && !(skip_def && b == fi.default_bin) && !(na && b == nb - 1);
-    if (incl) {
-      BinValue(H, fi.mfb, b, mg, mh, &g, &h);
+    if (b >= 0 && !(skip_def && b == fi.default_bin) && !(na && b == nb - 1)) {
+      g = H[2 * b];
+      h = H[2 * b + 1];
       c = RoundCount(h * cnt_factor);
     }
-    double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
-    int sci = WaveInclusiveScan(c);
+    const double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
+    const int sci = WaveInclusiveScan(c);
     const double rg = cg + sgi, rh_raw = ch + shi;
     const int rc = cc + sci;
     cg += __shfl(sgi, 63, kWave);
@@ -585,7 +592,6 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
       }
     }
   }
-  // ---- forward pass
   Cand fb;
   fb.gain = kMinScore;
   fb.thr = 0x7fffffff;
@@ -598,13 +604,13 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
       const int b = base + lane;
       double g = 0.0, h = 0.0;
       int c = 0;
-      const bool incl = b < nb && !(skip_def && b == fi.default_bin);
-      if (incl) {
-        BinValue(H, fi.mfb, b, mg, mh, &g, &h);
+      if (b < nb && !(skip_def && b == fi.default_bin)) {
+        g = H[2 * b];
+        h = H[2 * b + 1];
         c = RoundCount(h * cnt_factor);
       }
-      double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
-      int sci = WaveInclusiveScan(c);
+      const double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
+      const int sci = WaveInclusiveScan(c);
       const double lg = cg + sgi, lh_raw = ch + shi;
       const int lc = cc + sci;
       cg += __shfl(sgi, 63, kWave);
@@ -666,84 +672,149 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
   return any;
 }
 
-__global__ __launch_bounds__(kScanWaves * 64) void k_scan(Args a) {
-  const int lane = threadIdx.x & 63;
-  const int f = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
+// One workgroup (16 waves) per feature:
+//  1. sum the active histogram blocks' slab rows for this feature's bins (LDS)
+//  2. smaller child's histogram -> its slot; larger child = parent - smaller
+//     (the parent histogram lives in the larger child's slot)
+//  3. reconstruct the most-frequent bin of each child, then wave 0 scans the
+//     smaller child and wave 1 the larger one concurrently, from LDS
+template <typename Acc>
+__global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_grid, int from_staging) {
+  extern __shared__ __align__(16) unsigned char smem[];
   const Ctl c = *a.ctl;
-  if (c.done || c.skip || f >= a.F) return;
+  if (c.done || c.skip) return;
+  const int f = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  Stamp(a, 3, 0);
   const DevFeature fi = a.feat[f];
-  const int nst = fi.num_bin - 1;
+  const int nbin = fi.num_bin;
+  const int nst = nbin - 1;
+  const int nv = 2 * nst;  // stored values of this feature
+  double* hs_full = reinterpret_cast<double*>(smem);                 // 2 * nbin: smaller child, full
+  double* hl_full = hs_full + 2 * a.max_bin;                          // 2 * nbin: larger child, full
+  double* part = hl_full + 2 * a.max_bin;                             // [16][64]
+  int* order = reinterpret_cast<int*>(part + 16 * 64);                // max_bin (categorical scratch)
+  __shared__ int s_skip_both, s_rand[2];
+  __shared__ double s_sum[2][2];
+  __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
+  SplitInfo* s_out = reinterpret_cast<SplitInfo*>(s_out_raw);
+  const int n_small = a.range[c.smaller].count;
+  // single GPU: sum the histogram blocks' slab rows here; data-parallel: the
+  // all-reduced histogram already sits in `staging` (one row of doubles)
+  const int nb = from_staging ? 1 : HistActiveBlocks(n_small, hist_grid);
+  const size_t V = 2 * static_cast<size_t>(a.TB);
+  const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
+  const Acc* slab = from_staging ? reinterpret_cast<const Acc*>(a.staging) : reinterpret_cast<const Acc*>(a.hist_slab);
+  // 1. slab reduction into hs_full at stored positions (mfb filled in step 3):
+  //    each wave owns 32 values, its two half-waves stride over the slab rows;
+  //    no barrier until all values are reduced
+  {
+    const int half = lane >> 5;
+    for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
+      const int v = vbase + (lane & 31);
+      double acc = 0.0;
+      if (v < nv) {
+        const Acc* col = slab + v0 + v;
+#pragma unroll 4
+        for (int p = half; p < nb; p += 2) acc += static_cast<double>(col[static_cast<size_t>(p) * V]);
+      }
+      acc += __shfl_xor(acc, 32, kWave);
+      if (lane < 32 && v < nv) {
+        const int k = v >> 1;
+        const int b = k < fi.mfb ? k : k + 1;
+        hs_full[2 * b + (v & 1)] = acc;
+      }
+    }
+  }
+  __syncthreads();
+  Stamp(a, 3, 1);
+  // 2. slots: smaller <- reduced; larger <- parent - smaller
   const size_t slot_stride = 2 * static_cast<size_t>(a.TB);
   const int s_slot = a.slot[c.smaller];
   const int l_slot = c.larger >= 0 ? a.slot[c.larger] : -1;
-  double* hs = a.slots + s_slot * slot_stride + 2 * static_cast<size_t>(fi.hist_offset);
-  double* hl = l_slot >= 0 ? a.slots + l_slot * slot_stride + 2 * static_cast<size_t>(fi.hist_offset) : nullptr;
-  double* st = a.staging + 2 * static_cast<size_t>(fi.hist_offset);
-  for (int k = lane; k < nst; k += 64) {
-    const double g = st[2 * k], h = st[2 * k + 1];
-    hs[2 * k] = g;
-    hs[2 * k + 1] = h;
-    if (hl) {
-      hl[2 * k] -= g;
-      hl[2 * k + 1] -= h;
+  double* gs = a.slots + s_slot * slot_stride + v0;
+  double* gl = l_slot >= 0 ? a.slots + l_slot * slot_stride + v0 : nullptr;
+  for (int v = t; v < nv; v += blockDim.x) {
+    const int k = v >> 1;
+    const int b = k < fi.mfb ? k : k + 1;
+    const double s = hs_full[2 * b + (v & 1)];
+    gs[v] = s;
+    if (gl) {
+      const double l = gl[v] - s;
+      gl[v] = l;
+      hl_full[2 * b + (v & 1)] = l;
     }
   }
-  __threadfence_block();
-  if (c.num_leaves == 1 && f == 0 && lane == 0) {
-    SplitParams p0 = a.sp;
-    p0.path_smooth = 0.0;
-    a.lout[0] = LeafOutputRaw(a.lsum[0].x, a.lsum[0].y, p0, a.gcount[0], 0.0);
-  }
-  const bool skip_both = !a.used_bytree[f] || (c.larger >= 0 && !a.splittable[static_cast<size_t>(s_slot) * a.F + f]);
-  for (int sel = 0; sel < 2; ++sel) {
-    const int leaf = sel ? c.larger : c.smaller;
-    if (leaf < 0) break;
-    SplitInfo* out = a.scan_out + static_cast<size_t>(sel) * a.F + f;
-    if (skip_both) {
-      if (lane == 0) out->Reset();
-      continue;
+  if (t == 0) {
+    const bool skip_both =
+        !a.used_bytree[f] || (c.larger >= 0 && !a.splittable[static_cast<size_t>(s_slot) * a.F + f]);
+    s_skip_both = skip_both ? 1 : 0;
+    // extra-trees draws in the host learner's order: smaller leaf first, then larger
+    s_rand[0] = s_rand[1] = 0;
+    if (a.sp.extra_trees && !skip_both && fi.bin_type == 0 && fi.num_bin - 2 > 0) {
+      s_rand[0] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
+      if (c.larger >= 0) s_rand[1] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
     }
+    if (c.num_leaves == 1 && f == 0) {
+      SplitParams p0 = a.sp;
+      p0.path_smooth = 0.0;
+      a.lout[0] = LeafOutputRaw(a.lsum[0].x, a.lsum[0].y, p0, a.gcount[0], 0.0);
+    }
+  }
+  __syncthreads();
+  Stamp(a, 3, 2);
+  // 3. most-frequent bin = leaf total - stored bins
+  if (w < 2) {
+    const int leaf = w == 0 ? c.smaller : c.larger;
+    if (leaf >= 0) {
+      double* H = w == 0 ? hs_full : hl_full;
+      double sgs = 0.0, shs = 0.0;
+      for (int b = lane; b < nbin; b += 64) {
+        if (b == fi.mfb) continue;
+        sgs += H[2 * b];
+        shs += H[2 * b + 1];
+      }
+      sgs = WaveSum(sgs);
+      shs = WaveSum(shs);
+      const double2 sums = a.lsum[leaf];
+      if (lane == 0) {
+        H[2 * fi.mfb] = sums.x - sgs;
+        H[2 * fi.mfb + 1] = sums.y - shs;
+        s_sum[w][0] = sums.x;
+        s_sum[w][1] = sums.y;
+      }
+    }
+  }
+  __syncthreads();
+  Stamp(a, 3, 3);
+  if (w >= 2) return;
+  const int sel = w;
+  const int leaf = sel ? c.larger : c.smaller;
+  if (leaf < 0) return;
+  SplitInfo* gout = a.scan_out + static_cast<size_t>(sel) * a.F + f;
+  SplitInfo* out = &s_out[sel];  // built in LDS, then copied out by the wave
+  if (s_skip_both) {
+    if (lane == 0) out->Reset();
+  } else {
+    const double* H = sel ? hl_full : hs_full;
     const int lslot = sel ? l_slot : s_slot;
-    const double* H = sel ? hl : hs;
-    const double2 sums = a.lsum[leaf];
+    const double sg = s_sum[sel][0], sh = s_sum[sel][1];
     const int n = a.gcount[leaf];
     double po;
     if (c.num_leaves == 1) {
       SplitParams p0 = a.sp;
       p0.path_smooth = 0.0;
-      po = LeafOutputRaw(sums.x, sums.y, p0, n, 0.0);
+      po = LeafOutputRaw(sg, sh, p0, n, 0.0);
     } else {
       po = a.lout[leaf];
     }
     const LeafBounds bounds = a.bounds[leaf];
-    // mfb reconstruction
-    double sgs = 0.0, shs = 0.0;
-    for (int k = lane; k < nst; k += 64) {
-      sgs += H[2 * k];
-      shs += H[2 * k + 1];
-    }
-    sgs = WaveSum(sgs);
-    shs = WaveSum(shs);
-    const double mg = sums.x - sgs, mh = sums.y - shs;
+    const int depth = a.depth[leaf];
     bool sp;
     if (fi.bin_type == 0) {
-      int rand_thr = 0;
-      if (a.sp.extra_trees) {
-        if (lane == 0 && fi.num_bin - 2 > 0) rand_thr = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
-        rand_thr = __shfl(rand_thr, 0, kWave);
-      }
-      sp = ScanNumericalWave(a, fi, H, sums.x, sums.y, n, po, bounds, rand_thr, mg, mh, out);
+      sp = ScanNumericalWave(a, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
     } else {
-      // categorical: expand the full histogram into scratch, lane 0 runs the sequential scan
-      double* full = a.cat_scratch + static_cast<size_t>(f) * 3 * a.max_cat_bin;
-      int* order = reinterpret_cast<int*>(full + 2 * a.max_cat_bin);
-      for (int b = lane; b < fi.num_bin; b += 64) {
-        double g, h;
-        BinValue(H, fi.mfb, b, mg, mh, &g, &h);
-        full[2 * b] = g;
-        full[2 * b + 1] = h;
-      }
-      __threadfence_block();
+      // categorical: lane 0 runs the sequential one-hot / ctr-sorted scan (rare, few bins)
       int spi = 0;
       if (lane == 0) {
         FeatureScanMeta m;
@@ -755,21 +826,20 @@ __global__ __launch_bounds__(kScanWaves * 64) void k_scan(Args a) {
         m.penalty = fi.penalty;
         m.rand_threshold = 0;
         if (a.sp.extra_trees) {
+          // (categorical draws happen here; numerical ones were drawn above)
           if (fi.num_bin <= a.sp.max_cat_to_onehot) {
             if (fi.num_bin - 1 > 0) m.rand_threshold = RandNextInt(&a.rng[f], 1, fi.num_bin);
           } else {
-            const double cf = n / (sums.y + 2 * kEpsilon);
+            const double cf = n / (sh + 2 * kEpsilon);
             int used = 0;
-            for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(full[2 * b + 1] * cf) >= a.sp.cat_smooth;
-            int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
-            int max_thr = max(min(max_num_cat, used) - 1, 0);
+            for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(H[2 * b + 1] * cf) >= a.sp.cat_smooth;
+            const int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
+            const int max_thr = max(min(max_num_cat, used) - 1, 0);
             if (max_thr > 0) m.rand_threshold = RandNextInt(&a.rng[f], 0, max_thr);
           }
         }
-        SplitInfo tmp;
-        tmp.Reset();
-        spi = FindBestCategorical(full, m, a.sp, sums.x, sums.y, n, po, bounds, order, &tmp) ? 1 : 0;
-        *out = tmp;
+        out->Reset();
+        spi = FindBestCategorical(H, m, a.sp, sg, sh, n, po, bounds, order + sel * a.max_bin, out) ? 1 : 0;
       }
       sp = __shfl(spi, 0, kWave) != 0;
     }
@@ -779,15 +849,34 @@ __global__ __launch_bounds__(kScanWaves * 64) void k_scan(Args a) {
         out->Reset();
       } else {
         out->feature = f;
-        if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, a.depth[leaf]);
+        if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
         if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
       }
     }
   }
+  // lane 0 built the record in LDS; the whole wave stores it
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    constexpr int kWords = static_cast<int>(sizeof(SplitInfo) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(out);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(gout);
+    for (int i = lane; i < kWords; i += 64) dst[i] = src[i];
+  }
+  Stamp(a, 3, 4);
+}
+
+// Copy a SplitInfo with one dword per thread (no serial per-thread struct copy).
+__device__ __forceinline__ void CopySplitInfoBlock(SplitInfo* dst, const SplitInfo* src) {
+  constexpr int kWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+  for (int i = threadIdx.x; i < kWords; i += blockDim.x) d[i] = s[i];
 }
 
 // ---------------------------------------------------------------------------
-// best split of the new leaves, then the best leaf overall
+// best-leaf selection, replicated in every block of k_part_count
 
 __device__ __forceinline__ bool CandBetter(double ga, int fa, int la, double gb, int fb, int lb) {
   if (ga != gb) return ga > gb;
@@ -795,92 +884,116 @@ __device__ __forceinline__ bool CandBetter(double ga, int fa, int la, double gb,
   return la < lb;
 }
 
-__global__ __launch_bounds__(kNodeThreads) void k_select(Args a) {
-  __shared__ double s_g[kNodeThreads];
-  __shared__ int s_f[kNodeThreads];
-  __shared__ int s_l[kNodeThreads];
-  Ctl* cp = a.ctl;
-  if (cp->done) return;
-  const int t = threadIdx.x;
-  const Ctl c = *cp;
+struct SelState {
+  int done;       // no further split
+  int leaf;       // leaf to split
+  int sel;        // winner source: 0/1 = scan_out row of the smaller/larger child, -1 = best[leaf]
+  int feature;
+  int new_best[2];  // winning feature of the smaller/larger child (-1: none)
+};
+
+__device__ __forceinline__ void WaveArgBest(double* g, int* f, int* l) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(*g, o, kWave);
+    const int of = __shfl_xor(*f, o, kWave);
+    const int ol = __shfl_xor(*l, o, kWave);
+    if (CandBetter(og, of, ol, *g, *f, *l)) {
+      *g = og;
+      *f = of;
+      *l = ol;
+    }
+  }
+}
+
+// Block-wide argmax; a pure function of device state, so every block computes
+// the same decision without communicating. One pass: the two new children's
+// per-feature candidates and the older leaves' stored bests are loaded together
+// (one memory round trip), then three wave-shuffle argmaxes and one barrier.
+__device__ void BlockSelect(const Args& a, const Ctl& c, SelState* st) {
+  constexpr int kW = kPartThreads / 64;
+  __shared__ double s_g[3][kW];
+  __shared__ int s_f[3][kW];
+  __shared__ int s_l[3][kW];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  double g3[3] = {kMinScore, kMinScore, kMinScore};
+  int f3[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};
+  int l3[3] = {0, 0, 0x7fffffff};
   if (!c.skip) {
     for (int sel = 0; sel < 2; ++sel) {
       const int leaf = sel ? c.larger : c.smaller;
       if (leaf < 0) continue;
-      double bg = kMinScore;
-      int bf = 0x7fffffff;
       for (int f = t; f < a.F; f += blockDim.x) {
         const SplitInfo& s = a.scan_out[static_cast<size_t>(sel) * a.F + f];
-        if (s.feature < 0) continue;
-        const double g = SafeGain(s);
-        if (CandBetter(g, f, 0, bg, bf, 0)) {
-          bg = g;
-          bf = f;
+        const int sf = s.feature;
+        const double sg = s.gain;
+        const double g = (sf < 0 || sg != sg) ? kMinScore : sg;
+        if (sf >= 0 && CandBetter(g, f, 0, g3[sel], f3[sel], 0)) {
+          g3[sel] = g;
+          f3[sel] = f;
         }
       }
-      s_g[t] = bg;
-      s_f[t] = bf;
-      __syncthreads();
-      for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
-        if (t < o && CandBetter(s_g[t + o], s_f[t + o], 0, s_g[t], s_f[t], 0)) {
-          s_g[t] = s_g[t + o];
-          s_f[t] = s_f[t + o];
-        }
-        __syncthreads();
-      }
-      if (t == 0) {
-        if (s_f[0] != 0x7fffffff) a.best[leaf] = a.scan_out[static_cast<size_t>(sel) * a.F + s_f[0]];
-        else a.best[leaf].Reset();
-      }
-      __syncthreads();
     }
   }
-  double bg = kMinScore;
-  int bf = 0x7fffffff, bl = 0x7fffffff;
   for (int l = t; l < c.num_leaves; l += blockDim.x) {
+    if (l == c.smaller || l == c.larger) continue;
     const SplitInfo& s = a.best[l];
-    const double g = SafeGain(s);
-    const int f = s.feature < 0 ? 0x7fffffff : s.feature;
-    if (CandBetter(g, f, l, bg, bf, bl)) {
-      bg = g;
-      bf = f;
-      bl = l;
+    const int sf = s.feature;
+    const double sg = s.gain;
+    const double g = (sf < 0 || sg != sg) ? kMinScore : sg;
+    const int f = sf < 0 ? 0x7fffffff : sf;
+    if (CandBetter(g, f, l, g3[2], f3[2], l3[2])) {
+      g3[2] = g;
+      f3[2] = f;
+      l3[2] = l;
     }
   }
-  s_g[t] = bg;
-  s_f[t] = bf;
-  s_l[t] = bl;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    WaveArgBest(&g3[k], &f3[k], &l3[k]);
+    if (lane == 0) {
+      s_g[k][w] = g3[k];
+      s_f[k][w] = f3[k];
+      s_l[k][w] = l3[k];
+    }
+  }
   __syncthreads();
-  for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
-    if (t < o && CandBetter(s_g[t + o], s_f[t + o], s_l[t + o], s_g[t], s_f[t], s_l[t])) {
-      s_g[t] = s_g[t + o];
-      s_f[t] = s_f[t + o];
-      s_l[t] = s_l[t + o];
-    }
-    __syncthreads();
-  }
   if (t == 0) {
-    if (!c.skip) cp->scan_round = c.scan_round + 1;
-    const int l = s_l[0];
-    if (l == 0x7fffffff || a.best[l].feature < 0 || !(a.best[l].gain > 0.0)) {
-      cp->done = 1;
-      return;
+    for (int k = 0; k < 3; ++k) {
+      for (int i = 1; i < kW; ++i) {
+        if (CandBetter(s_g[k][i], s_f[k][i], s_l[k][i], s_g[k][0], s_f[k][0], s_l[k][0])) {
+          s_g[k][0] = s_g[k][i];
+          s_f[k][0] = s_f[k][i];
+          s_l[k][0] = s_l[k][i];
+        }
+      }
     }
-    const LeafRange pr = a.range[l];
-    cp->split_leaf = l;
-    cp->new_leaf = c.num_leaves;
-    cp->parent_buf = pr.buf;
-    cp->parent_start = pr.start;
-    cp->parent_count = pr.count;
-    cp->target_buf = pr.buf == 0 ? 1 : 0;
+    st->new_best[0] = s_f[0][0] == 0x7fffffff ? -1 : s_f[0][0];
+    st->new_best[1] = s_f[1][0] == 0x7fffffff ? -1 : s_f[1][0];
+    // overall: older leaves vs the two children (leaf index breaks full ties)
+    double bg = s_g[2][0];
+    int bf = s_f[2][0], bl = s_l[2][0];
+    for (int sel = 0; sel < 2; ++sel) {
+      const int leaf = sel ? c.larger : c.smaller;
+      if (leaf < 0 || s_f[sel][0] == 0x7fffffff) continue;
+      if (CandBetter(s_g[sel][0], s_f[sel][0], leaf, bg, bf, bl)) {
+        bg = s_g[sel][0];
+        bf = s_f[sel][0];
+        bl = leaf;
+      }
+    }
+    st->leaf = bl;
+    st->feature = bf;
+    st->done = (bl == 0x7fffffff || bf == 0x7fffffff || !(bg > 0.0)) ? 1 : 0;
+    st->sel = (bl == c.smaller) ? 0 : ((bl == c.larger) ? 1 : -1);
   }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
 // stable partition of the split leaf's row indices
 
-__device__ void LoadSplitDesc(const Args& a, int leaf, SplitDesc* d) {
-  const SplitInfo& s = a.best[leaf];
+__device__ void FillSplitDesc(const Args& a, const SplitInfo& s, SplitDesc* d) {
   const DevFeature fi = a.feat[s.feature];
   d->group = fi.group;
   d->offset = fi.offset;
@@ -894,127 +1007,92 @@ __device__ void LoadSplitDesc(const Args& a, int leaf, SplitDesc* d) {
   for (int w = 0; w < kMaxCatWords; ++w) d->bits[w] = d->is_cat ? s.cat_bitset[w] : 0u;
 }
 
+// Select the leaf to split (replicated), persist the decision (block 0), then
+// count the rows going left per 4096-row tile of the parent range.
 __global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
   __shared__ SplitDesc d;
+  __shared__ SelState st;
   __shared__ int sh[8];
-  const Ctl* cp = a.ctl;
-  if (cp->done) return;
-  const int leaf = cp->split_leaf;
-  const int pbuf = cp->parent_buf, pstart = cp->parent_start, pcount = cp->parent_count;
-  if (threadIdx.x == 0) LoadSplitDesc(a, leaf, &d);
-  __syncthreads();
-  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int cnt = 0;
-#pragma unroll 4
-    for (int k = 0; k < kPartIters; ++k) {
-      const int pos = tile * kTileRows + k * kPartThreads + threadIdx.x;
-      if (pos < pcount) {
-        const int row = RowAt(a, pbuf, pstart + pos);
-        cnt += GoLeft(d, ColBin(a, d.group, row)) ? 1 : 0;
-      }
+  Ctl* cp = a.ctl;
+  const Ctl c = *cp;
+  if (c.done) return;
+  // no leaf has more tiles than this: surplus blocks have nothing to count
+  if (blockIdx.x > 0 && static_cast<int>(blockIdx.x) >= (c.max_count + kTileRows - 1) / kTileRows) return;
+  Stamp(a, 0, 0);
+  BlockSelect(a, c, &st);
+  Stamp(a, 0, 1);
+  const SplitInfo* win = st.done ? nullptr
+                                 : (st.sel >= 0 ? &a.scan_out[static_cast<size_t>(st.sel) * a.F + st.feature]
+                                                : &a.best[st.leaf]);
+  if (blockIdx.x == 0) {
+    // persist: per-leaf bests of the two children (invalid when their scan was skipped)
+    if (c.smaller >= 0 && st.new_best[0] >= 0) CopySplitInfoBlock(&a.best[c.smaller], &a.scan_out[st.new_best[0]]);
+    if (c.larger >= 0 && st.new_best[1] >= 0) {
+      CopySplitInfoBlock(&a.best[c.larger], &a.scan_out[static_cast<size_t>(a.F) + st.new_best[1]]);
     }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (c.smaller >= 0 && st.new_best[0] < 0) a.best[c.smaller].Reset();
+    if (c.larger >= 0 && st.new_best[1] < 0) a.best[c.larger].Reset();
+    if (!c.skip) cp->scan_round = c.scan_round + 1;
+    if (st.done) {
+      cp->done = 1;
+    } else {
+      const LeafRange pr = a.range[st.leaf];
+      cp->split_leaf = st.leaf;
+      cp->new_leaf = c.num_leaves;
+      cp->parent_buf = pr.buf;
+      cp->parent_start = pr.start;
+      cp->parent_count = pr.count;
+      cp->target_buf = pr.buf == 0 ? 1 : 0;
+    }
+  }
+  if (st.done) return;
+  if (threadIdx.x == 0) FillSplitDesc(a, *win, &d);
+  const LeafRange pr = a.range[st.leaf];
+  __syncthreads();
+  Stamp(a, 0, 2);
+  const int ntiles = (pr.count + kTileRows - 1) / kTileRows;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // all 16 index loads in flight, then all 16 split-column loads
+    int rows[kPartIters];
+    const int pos0 = tile * kTileRows + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) {
+      const int pos = pos0 + k * kPartThreads;
+      rows[k] = pos < pr.count ? RowAt(a, pr.buf, pr.start + pos) : -1;
+    }
+    uint32_t gb[kPartIters];
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) cnt += (rows[k] >= 0 && GoLeft(d, gb[k])) ? 1 : 0;
     cnt = BlockSumInt(cnt, sh);
     if (threadIdx.x == 0) a.tile_cnt[tile] = cnt;
   }
+  Stamp(a, 0, 3);
 }
 
-__global__ __launch_bounds__(1024) void k_part_scan(Args a) {
-  __shared__ int sh[1024];
-  Ctl* cp = a.ctl;
-  if (cp->done) return;
-  const int pcount = cp->parent_count;
-  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
-  const int t = threadIdx.x;
-  const int per = (ntiles + blockDim.x - 1) / blockDim.x;
-  const int b = t * per, e = min(ntiles, b + per);
-  int s = 0;
-  for (int i = b; i < e; ++i) s += a.tile_cnt[i];
-  sh[t] = s;
-  __syncthreads();
-  for (int o = 1; o < static_cast<int>(blockDim.x); o <<= 1) {
-    const int v = t >= o ? sh[t - o] : 0;
-    __syncthreads();
-    sh[t] += v;
-    __syncthreads();
-  }
-  int run = sh[t] - s;  // exclusive prefix
-  for (int i = b; i < e; ++i) {
-    const int c = a.tile_cnt[i];
-    a.tile_off[i] = run;
-    run += c;
-  }
-  if (t == static_cast<int>(blockDim.x) - 1) cp->left_count = sh[t];
-}
-
-__global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
-  __shared__ SplitDesc d;
-  __shared__ int s_wl[kPartThreads / 64];
-  __shared__ int s_wv[kPartThreads / 64];
-  const Ctl* cp = a.ctl;
-  if (cp->done) return;
-  const int leaf = cp->split_leaf;
-  const int pbuf = cp->parent_buf, pstart = cp->parent_start, pcount = cp->parent_count;
-  const int nl_total = cp->left_count;
-  int* out = a.idx[cp->target_buf] + pstart;
-  if (threadIdx.x == 0) LoadSplitDesc(a, leaf, &d);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int lbase = a.tile_off[tile];
-    int rbase = tile * kTileRows - lbase;
-    for (int k = 0; k < kPartIters; ++k) {
-      const int pos = tile * kTileRows + k * kPartThreads + threadIdx.x;
-      const bool valid = pos < pcount;
-      int row = 0;
-      bool left = false;
-      if (valid) {
-        row = RowAt(a, pbuf, pstart + pos);
-        left = GoLeft(d, ColBin(a, d.group, row));
-      }
-      const unsigned long long ml = __ballot(valid && left);
-      const unsigned long long mv = __ballot(valid);
-      if (lane == 0) {
-        s_wl[w] = __popcll(ml);
-        s_wv[w] = __popcll(mv);
-      }
-      __syncthreads();
-      int pl = 0, pv = 0, tl = 0, tv = 0;
-      for (int i = 0; i < kPartThreads / 64; ++i) {
-        if (i < w) {
-          pl += s_wl[i];
-          pv += s_wv[i];
-        }
-        tl += s_wl[i];
-        tv += s_wv[i];
-      }
-      if (valid) {
-        const int rl = pl + __popcll(ml & lt_mask);
-        const int rv = pv + __popcll(mv & lt_mask);
-        if (left) out[lbase + rl] = row;
-        else out[nl_total + rbase + (rv - rl)] = row;
-      }
-      lbase += tl;
-      rbase += tv - tl;
-      __syncthreads();
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// bookkeeping after a split (BeforeFindBestSplit for the two children)
-
-__global__ __launch_bounds__(kNodeThreads) void k_post(Args a) {
+// Post-split bookkeeping (BeforeFindBestSplit of the two children); run by
+// block 0 of k_part_scatter after its own tiles. Touches only state that no
+// other k_part_scatter block reads. All loads are issued before any store.
+__device__ void PostSplit(const Args& a, const Ctl& c, int left_count) {
   __shared__ int s_skip, s_from, s_to;
-  Ctl* cp = a.ctl;
-  if (cp->done) return;
+  const int l = c.split_leaf, r = c.new_leaf;
   if (threadIdx.x == 0) {
-    Ctl c = *cp;
-    const int l = c.split_leaf, r = c.new_leaf;
-    const SplitInfo info = a.best[l];
-    const int lc = c.left_count, rc = c.parent_count - lc;
+    const SplitInfo& bi = a.best[l];
+    const double lsg = bi.left_sum_gradient, lsh = bi.left_sum_hessian;
+    const double rsg = bi.right_sum_gradient, rsh = bi.right_sum_hessian;
+    const double lo = bi.left_output, ro = bi.right_output;
+    const int ilc = bi.left_count, irc = bi.right_count;
+    const int8_t mono = bi.monotone_type;
+    const int16_t ncat = bi.num_cat_threshold;
+    const int dep = a.depth[l] + 1;
+    LeafBounds bl = a.bounds[l];
+    const int ps = a.slot[l];
+    // ---- stores
+    const int lc = left_count, rc = c.parent_count - lc;
     LeafRange rl, rr;
     rl.buf = rr.buf = c.target_buf;
     rl.start = c.parent_start;
@@ -1024,67 +1102,82 @@ __global__ __launch_bounds__(kNodeThreads) void k_post(Args a) {
     rl.pad = rr.pad = 0;
     a.range[l] = rl;
     a.range[r] = rr;
-    const int glc = a.distributed ? info.left_count : lc;
-    const int grc = a.distributed ? info.right_count : rc;
+    const int glc = a.distributed ? ilc : lc;
+    const int grc = a.distributed ? irc : rc;
     SplitRec& rec = a.rec[c.num_splits];
     rec.leaf = l;
     rec.left_count = glc;
     rec.right_count = grc;
     rec.pad = 0;
-    rec.info = info;
-    c.num_splits += 1;
-    c.num_leaves += 1;
-    a.lsum[l] = make_double2(info.left_sum_gradient, info.left_sum_hessian);
-    a.lsum[r] = make_double2(info.right_sum_gradient, info.right_sum_hessian);
-    a.lout[l] = info.left_output;
-    a.lout[r] = info.right_output;
+    a.lsum[l] = make_double2(lsg, lsh);
+    a.lsum[r] = make_double2(rsg, rsh);
+    a.lout[l] = lo;
+    a.lout[r] = ro;
     a.gcount[l] = glc;
     a.gcount[r] = grc;
-    const int d = a.depth[l] + 1;
-    a.depth[l] = d;
-    a.depth[r] = d;
-    LeafBounds bl = a.bounds[l], br = bl;
-    if (a.use_monotone && info.num_cat_threshold == 0) {
-      const double mid = (info.left_output + info.right_output) / 2.0f;
-      if (info.monotone_type < 0) {
+    a.depth[l] = dep;
+    a.depth[r] = dep;
+    LeafBounds br = bl;
+    if (a.use_monotone && ncat == 0) {
+      const double mid = (lo + ro) / 2.0f;
+      if (mono < 0) {
         bl.min = fmax(bl.min, mid);
         br.max = fmin(br.max, mid);
-      } else if (info.monotone_type > 0) {
+      } else if (mono > 0) {
         bl.max = fmin(bl.max, mid);
         br.min = fmax(br.min, mid);
       }
     }
     a.bounds[l] = bl;
     a.bounds[r] = br;
-    int smaller, larger;
-    if (glc < grc) {
-      smaller = l;
-      larger = r;
-    } else {
-      smaller = r;
-      larger = l;
-    }
+    const int smaller = glc < grc ? l : r;
+    const int larger = glc < grc ? r : l;
     const int md = a.sp.min_data_in_leaf;
-    const bool skip = (a.max_depth > 0 && d >= a.max_depth) || (grc < md * 2 && glc < md * 2);
-    c.smaller = smaller;
-    c.larger = larger;
-    c.skip = skip ? 1 : 0;
-    if (skip) {
-      a.best[l].Reset();
-      a.best[r].Reset();
-    } else {
-      const int ps = a.slot[l];
+    const bool skip = (a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2);
+    Ctl nc = c;
+    nc.num_splits = c.num_splits + 1;
+    nc.num_leaves = c.num_leaves + 1;
+    nc.left_count = lc;
+    nc.smaller = smaller;
+    nc.larger = larger;
+    nc.skip = skip ? 1 : 0;
+    int to = -1;
+    if (!skip) {
       if (larger == r) {
         a.slot[r] = ps;
         a.slot[l] = r;
+        to = r;
       } else {
         a.slot[r] = r;
+        to = r;
       }
-      s_from = ps;
-      s_to = a.slot[smaller];
     }
+    *a.ctl = nc;
+    s_from = ps;
+    s_to = to;
     s_skip = skip ? 1 : 0;
-    *cp = c;
+  }
+  // the split record (dword-parallel copy of the winning SplitInfo)
+  CopySplitInfoBlock(&a.rec[c.num_splits].info, &a.best[l]);
+  // largest leaf after this split (grid bound of the next partition kernels)
+  {
+    __shared__ int s_mx[kPartThreads / 64];
+    int mx = 0;
+    for (int q = threadIdx.x; q <= c.num_leaves; q += blockDim.x) {
+      int cnt;
+      if (q == l) cnt = left_count;
+      else if (q == r) cnt = c.parent_count - left_count;
+      else cnt = a.range[q].count;
+      mx = max(mx, cnt);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, kWave));
+    if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int i = 1; i < static_cast<int>(blockDim.x >> 6); ++i) mx = max(mx, s_mx[i]);
+      a.ctl->max_count = mx;
+    }
   }
   __syncthreads();
   if (!s_skip) {
@@ -1092,6 +1185,98 @@ __global__ __launch_bounds__(kNodeThreads) void k_post(Args a) {
     uint8_t* dst = a.splittable + static_cast<size_t>(s_to) * a.F;
     for (int f = threadIdx.x; f < a.F; f += blockDim.x) dst[f] = src[f];
   }
+}
+
+// Scatter rows into the target index buffer (stable: lefts in order, then
+// rights in order). Each block derives its tiles' offsets from the tile counts
+// itself; block 0 finishes with the post-split bookkeeping.
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
+  __shared__ SplitDesc d;
+  __shared__ int s_wl[kPartIters][kPartThreads / 64];
+  __shared__ int s_wv[kPartIters][kPartThreads / 64];
+  __shared__ int sh[8];
+  const Ctl* cp = a.ctl;
+  const Ctl c = *cp;
+  if (c.done) return;
+  const int pbuf = c.parent_buf, pstart = c.parent_start, pcount = c.parent_count;
+  if (blockIdx.x > 0 && static_cast<int>(blockIdx.x) >= (pcount + kTileRows - 1) / kTileRows) return;
+  int* out = a.idx[c.target_buf] + pstart;
+  Stamp(a, 1, 0);
+  if (threadIdx.x == 0) FillSplitDesc(a, a.best[c.split_leaf], &d);
+  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
+  int nl = 0;
+  for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += a.tile_cnt[i];
+  const int nl_total = BlockSumInt(nl, sh);
+  Stamp(a, 1, 1);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int pre = 0;
+    for (int i = threadIdx.x; i < tile; i += blockDim.x) pre += a.tile_cnt[i];
+    int lbase = BlockSumInt(pre, sh);
+    int rbase = tile * kTileRows - lbase;
+    int rows[kPartIters];
+    const int pos0 = tile * kTileRows + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) {
+      const int pos = pos0 + k * kPartThreads;
+      rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
+    }
+    uint32_t gb[kPartIters];
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) {
+      const bool valid = rows[k] >= 0;
+      const bool left = valid && GoLeft(d, gb[k]);
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      if (lane == 0) {
+        s_wl[k][w] = __popcll(ml);
+        s_wv[k][w] = __popcll(mv);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) {
+      const bool valid = rows[k] >= 0;
+      const bool left = valid && GoLeft(d, gb[k]);
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      int pl = 0, pv = 0, tl = 0, tv = 0;
+#pragma unroll
+      for (int i = 0; i < kPartThreads / 64; ++i) {
+        if (i < w) {
+          pl += s_wl[k][i];
+          pv += s_wv[k][i];
+        }
+        tl += s_wl[k][i];
+        tv += s_wv[k][i];
+      }
+      if (valid) {
+        const int rl = pl + __popcll(ml & lt_mask);
+        const int rv = pv + __popcll(mv & lt_mask);
+        if (left) out[lbase + rl] = rows[k];
+        else out[nl_total + rbase + (rv - rl)] = rows[k];
+      }
+      lbase += tl;
+      rbase += tv - tl;
+    }
+    __syncthreads();
+  }
+  Stamp(a, 1, 2);
+  if (blockIdx.x == 0 && a.fuse_post) PostSplit(a, c, nl_total);
+  Stamp(a, 1, 3);
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_post(Args a) {
+  __shared__ int sh[8];
+  const Ctl c = *a.ctl;
+  if (c.done) return;
+  const int ntiles = (c.parent_count + kTileRows - 1) / kTileRows;
+  int nl = 0;
+  for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += a.tile_cnt[i];
+  PostSplit(a, c, BlockSumInt(nl, sh));
 }
 
 // ---------------------------------------------------------------------------
@@ -1479,11 +1664,39 @@ class DeviceTreeLearner : public TreeLearner {
       }
     }
     h_range_.assign(hrange, hrange + hc->num_leaves);
+    if (stamps_.size() && ++stamp_trees_ == 3) ReportStamps(hc->num_splits);
     tree->RecomputeMaxDepth();
     return tree;
   }
 
   std::string DeviceName() const override { return device_name_; }
+
+  void ReportStamps(int nsplits) {
+    std::vector<unsigned long long> h(stamps_.size());
+    stamps_.Download(h.data(), h.size(), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    static const char* names[4] = {"part_count", "part_scatter", "hist", "reduce_scan"};
+    for (int k = 0; k < 4; ++k) {
+      for (int b = 0; b < 2; ++b) {
+        double acc[8] = {0};
+        int cnt = 0;
+        for (int sp = 1; sp < std::min(nsplits, 255); ++sp) {
+          const unsigned long long* st = &h[((static_cast<size_t>(k) * 256 + sp) * 2 + b) * 8];
+          if (st[0] == 0) continue;
+          ++cnt;
+          for (int i = 1; i < 8; ++i) {
+            if (st[i] >= st[0]) acc[i] += (st[i] - st[0]) * 0.01;  // 100 MHz -> us
+          }
+        }
+        if (!cnt) continue;
+        std::string line;
+        for (int i = 1; i < 8; ++i) {
+          if (acc[i] > 0) line += " t" + std::to_string(i) + "=" + common::FormatG(acc[i] / cnt);
+        }
+        std::fprintf(stderr, "stamps %s block %d (%d splits, us from kernel start):%s\n", names[k], b, cnt, line.c_str());
+      }
+    }
+  }
 
   // One histogram of (g, h) over `rows` (identity when null) into `out` (2 * TB doubles).
   void TestHistogram(const float* g, const float* h, const int* rows, int n, double* out) {
@@ -1513,7 +1726,9 @@ class DeviceTreeLearner : public TreeLearner {
     std::memcpy(&hm[1], &mh, 4);
     HIP_CHECK(hipMemcpyAsync(ghmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
     staging_.Zero(stream_);
-    LaunchHist(MakeArgs());
+    const Args args = MakeArgs();
+    LaunchHist(args);
+    if (!distributed_) LaunchHistReduce(args);
     staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
     staging_.Zero(stream_);
@@ -1538,11 +1753,29 @@ class DeviceTreeLearner : public TreeLearner {
       if (width_ == 1) k_hist<1, 0><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
       else k_hist<2, 0><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
     }
+    HIP_CHECK(hipGetLastError());
+    if (distributed_) {
+      LaunchHistReduce(a);
+      AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), stream_);
+    }
+  }
+
+  void LaunchHistReduce(const Args& a) {
     const int rgrid = DivUp(2 * static_cast<long long>(TB_), 64);
     if (use_dp_) k_hist_reduce<double><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks());
     else k_hist_reduce<float><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks());
     HIP_CHECK(hipGetLastError());
-    if (distributed_) AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), stream_);
+  }
+
+  void LaunchScan(const Args& a) {
+    if (distributed_) {
+      k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 1);
+    } else if (use_dp_) {
+      k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 0);
+    } else {
+      k_reduce_scan<float><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 0);
+    }
+    HIP_CHECK(hipGetLastError());
   }
 
   void UploadData() {
@@ -1591,10 +1824,24 @@ class DeviceTreeLearner : public TreeLearner {
         max_cat_bin_ = std::max(max_cat_bin_, fi.num_bin);
       }
     }
-    feat_.Upload(feats, stream_);
+    h_feats_ = feats;
+    max_bin_ = 2;
+    for (int f = 0; f < F_; ++f) max_bin_ = std::max(max_bin_, data_->feature(f).num_bin);
+    // k_reduce_scan: two full histograms + 16x64 partials + 2 categorical order arrays
+    scan_lds_bytes_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + 16 * 64 * sizeof(double) +
+                      static_cast<size_t>(max_bin_) * 2 * sizeof(int);
+    if (scan_lds_bytes_ > 150 * 1024) {
+      Log::Fatal("A feature with %d bins exceeds the HIP split-scan LDS budget; lower max_bin", max_bin_);
+    }
+    if (scan_lds_bytes_ > 64 * 1024) {
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_reduce_scan<float>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(scan_lds_bytes_)));
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_reduce_scan<double>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(scan_lds_bytes_)));
+    }
     std::vector<int> gs(std::max(G_, 1));
     for (int g = 0; g < G_; ++g) gs[g] = data_->group(g).hist_start;
-    gstart_.Upload(gs, stream_);
+    h_gstart_ = gs;
     BuildTiles();
     // labels / weights for the device objectives are uploaded lazily
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -1644,46 +1891,68 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
     }
     num_tiles_ = static_cast<int>(tiles.size());
-    tiles_.Upload(tiles, stream_);
+    h_tiles_ = tiles;
   }
 
   void AllocState() {
     const size_t L = L_;
-    tparams_.Resize(1);
-    ctl_.Resize(1);
-    range_.Resize(L);
-    lsum_.Resize(L);
-    lout_.Resize(L);
-    gcount_.Resize(L);
-    depth_.Resize(L);
-    slot_.Resize(L);
-    bounds_.Resize(L);
-    best_.Resize(L);
-    rec_.Resize(L);
-    slots_.Resize(L * 2 * static_cast<size_t>(TB_));
-    staging_.Resize(2 * static_cast<size_t>(TB_));
-    staging_.Zero(stream_);
-    ghmax_.Resize(2);
-    hist_slab_.Resize(static_cast<size_t>(HistBlocks()) * 2 * TB_ * (use_dp_ ? 8 : 4));
-    splittable_.Resize(L * F_);
-    scan_out_.Resize(2 * static_cast<size_t>(F_));
     max_tiles_ = std::max(1, DivUp(N_, kTileRows));
-    tile_cnt_.Resize(max_tiles_);
-    tile_off_.Resize(max_tiles_);
-    used_bytree_.Resize(std::max(F_, 1));
     use_bynode_ = config_->feature_fraction_bynode < 1.0;
-    if (use_bynode_) bynode_.Resize(2 * L * F_);
-    for (int i = 0; i < 3; ++i) {
-      if (i < 2) idx_[i].Resize(std::max(N_, 1));
-    }
-    if (idx_[2].size() == 0) idx_[2].Resize(1);
+    // every small per-tree structure + the static feature metadata in one allocation
+    ArenaLayout lay;
+    const size_t o_tp = lay.Add<TreeParams>(1), o_ctl = lay.Add<Ctl>(1), o_range = lay.Add<LeafRange>(L),
+                 o_lsum = lay.Add<double2>(L), o_lout = lay.Add<double>(L), o_gcount = lay.Add<int>(L),
+                 o_depth = lay.Add<int>(L), o_slot = lay.Add<int>(L), o_bounds = lay.Add<LeafBounds>(L),
+                 o_best = lay.Add<SplitInfo>(L), o_rec = lay.Add<SplitRec>(L), o_ghmax = lay.Add<unsigned>(2),
+                 o_spl = lay.Add<uint8_t>(L * F_), o_scan = lay.Add<SplitInfo>(2 * static_cast<size_t>(F_)),
+                 o_tcnt = lay.Add<int>(max_tiles_), o_toff = lay.Add<int>(max_tiles_),
+                 o_used = lay.Add<uint8_t>(std::max(F_, 1)), o_byn = lay.Add<uint8_t>(use_bynode_ ? 2 * L * F_ : 1),
+                 o_rng = lay.Add<unsigned>(std::max(F_, 1)), o_feat = lay.Add<DevFeature>(h_feats_.size()),
+                 o_gst = lay.Add<int>(h_gstart_.size()), o_tiles = lay.Add<HistTile>(h_tiles_.size());
+    arena_.Resize(std::max<size_t>(lay.bytes(), size_t(2) << 20));
+    char* base = arena_.get();
+    tparams_.Attach(reinterpret_cast<TreeParams*>(base + o_tp), 1);
+    ctl_.Attach(reinterpret_cast<Ctl*>(base + o_ctl), 1);
+    range_.Attach(reinterpret_cast<LeafRange*>(base + o_range), L);
+    lsum_.Attach(reinterpret_cast<double2*>(base + o_lsum), L);
+    lout_.Attach(reinterpret_cast<double*>(base + o_lout), L);
+    gcount_.Attach(reinterpret_cast<int*>(base + o_gcount), L);
+    depth_.Attach(reinterpret_cast<int*>(base + o_depth), L);
+    slot_.Attach(reinterpret_cast<int*>(base + o_slot), L);
+    bounds_.Attach(reinterpret_cast<LeafBounds*>(base + o_bounds), L);
+    best_.Attach(reinterpret_cast<SplitInfo*>(base + o_best), L);
+    rec_.Attach(reinterpret_cast<SplitRec*>(base + o_rec), L);
+    ghmax_.Attach(reinterpret_cast<unsigned*>(base + o_ghmax), 2);
+    splittable_.Attach(reinterpret_cast<uint8_t*>(base + o_spl), L * F_);
+    scan_out_.Attach(reinterpret_cast<SplitInfo*>(base + o_scan), 2 * static_cast<size_t>(F_));
+    tile_cnt_.Attach(reinterpret_cast<int*>(base + o_tcnt), max_tiles_);
+    tile_off_.Attach(reinterpret_cast<int*>(base + o_toff), max_tiles_);
+    used_bytree_.Attach(reinterpret_cast<uint8_t*>(base + o_used), std::max(F_, 1));
+    bynode_.Attach(reinterpret_cast<uint8_t*>(base + o_byn), use_bynode_ ? 2 * L * F_ : 1);
+    rng_.Attach(reinterpret_cast<unsigned*>(base + o_rng), std::max(F_, 1));
+    feat_.Attach(reinterpret_cast<DevFeature*>(base + o_feat), h_feats_.size());
+    gstart_.Attach(reinterpret_cast<int*>(base + o_gst), h_gstart_.size());
+    tiles_.Attach(reinterpret_cast<HistTile*>(base + o_tiles), h_tiles_.size());
+    arena_.Zero(stream_);
+    feat_.Upload(h_feats_, stream_);
+    gstart_.Upload(h_gstart_, stream_);
+    tiles_.Upload(h_tiles_, stream_);
     // extra-trees streams: Random(extra_seed + f) per feature, persistent across trees
     std::vector<unsigned> rs(std::max(F_, 1));
     for (int f = 0; f < F_; ++f) rs[f] = static_cast<unsigned>(config_->extra_seed + f);
     rng_.Upload(rs, stream_);
-    if (has_cat_) cat_scratch_.Resize(static_cast<size_t>(F_) * 3 * max_cat_bin_);
-    else cat_scratch_.Resize(1);
+    // large buffers keep their own allocations
+    slots_.Resize(L * 2 * static_cast<size_t>(TB_));
+    staging_.Resize(2 * static_cast<size_t>(TB_));
+    staging_.Zero(stream_);
+    hist_slab_.Resize(static_cast<size_t>(HistBlocks()) * 2 * TB_ * (use_dp_ ? 8 : 4));
+    for (int i = 0; i < 2; ++i) idx_[i].Resize(std::max(N_, 1));
+    if (idx_[2].size() == 0) idx_[2].Resize(1);
     if (bag_cnt_ == 0) bag_cnt_ = N_;
+    if (getenv("LGAP_STAMPS")) {
+      stamps_.Resize(4 * 256 * 2 * 8);
+      stamps_.Zero(stream_);
+    }
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
@@ -1727,9 +1996,11 @@ class DeviceTreeLearner : public TreeLearner {
     a.tile_cnt = tile_cnt_.get();
     a.tile_off = tile_off_.get();
     a.rng = rng_.get();
-    a.cat_scratch = cat_scratch_.get();
     a.max_cat_bin = max_cat_bin_;
+    a.max_bin = max_bin_;
     a.max_depth = config_->max_depth;
+    a.fuse_post = getenv("LGAP_SPLIT_POST") ? 0 : 1;
+    a.stamps = stamps_.size() ? stamps_.get() : nullptr;
     a.distributed = distributed_ ? 1 : 0;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
     a.monotone_penalty = config_->monotone_penalty;
@@ -1756,22 +2027,18 @@ class DeviceTreeLearner : public TreeLearner {
     const Args a = MakeArgs();
     hipStream_t s = stream_;
     const int part_blocks = std::max(1, std::min(max_tiles_, 4 * num_cu_));
-    const int scan_blocks = std::max(1, DivUp(F_, kScanWaves));
-    auto hist = [&]() { LaunchHist(a); };
     k_init_tree<<<1, kNodeThreads, 0, s>>>(a);
     k_root_sums<<<std::max(1, std::min(DivUp(N_, 256), 4 * num_cu_)), 256, 0, s>>>(a);
     if (distributed_) AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
-    hist();
-    k_scan<<<scan_blocks, kScanWaves * 64, 0, s>>>(a);
+    LaunchHist(a);
+    LaunchScan(a);
     for (int it = 0; it < L_ - 1; ++it) {
-      k_select<<<1, kNodeThreads, 0, s>>>(a);
       k_part_count<<<part_blocks, kPartThreads, 0, s>>>(a);
-      k_part_scan<<<1, 1024, 0, s>>>(a);
       k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(a);
-      k_post<<<1, kNodeThreads, 0, s>>>(a);
+      if (!a.fuse_post) k_post<<<1, kPartThreads, 0, s>>>(a);
       if (it < L_ - 2) {
-        hist();
-        k_scan<<<scan_blocks, kScanWaves * 64, 0, s>>>(a);
+        LaunchHist(a);
+        LaunchScan(a);
       }
     }
     HIP_CHECK(hipGetLastError());
@@ -1843,7 +2110,8 @@ class DeviceTreeLearner : public TreeLearner {
   int device_id_ = 0, num_cu_ = 256, num_tiles_ = 0, max_tiles_ = 1, max_cat_bin_ = 1;
   bool has_cat_ = false, use_bag_ = false, use_bynode_ = false, use_dp_ = false;
   data_size_t bag_cnt_ = 0;
-  size_t hist_lds_bytes_ = 0;
+  size_t hist_lds_bytes_ = 0, scan_lds_bytes_ = 0;
+  int max_bin_ = 2;
   std::string device_name_;
   hipStream_t stream_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
@@ -1870,14 +2138,18 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<SplitInfo> best_;
   DevBuf<SplitRec> rec_;
   DevBuf<double> slots_, staging_;
-  DevBuf<char> hist_slab_;
+  DevBuf<char> hist_slab_, arena_;
+  DevBuf<unsigned long long> stamps_;
+  int stamp_trees_ = 0;
+  std::vector<DevFeature> h_feats_;
+  std::vector<int> h_gstart_;
+  std::vector<HistTile> h_tiles_;
   DevBuf<unsigned> ghmax_;
   DevBuf<uint8_t> splittable_;
   DevBuf<SplitInfo> scan_out_;
   DevBuf<int> tile_cnt_, tile_off_;
   DevBuf<uint8_t> used_bytree_, bynode_;
   DevBuf<unsigned> rng_;
-  DevBuf<double> cat_scratch_;
   DevBuf<char> tree_buf_;
   // lambdarank tables
   DevBuf<double> rank_table_, rank_gain_, rank_inv_dcg_, rank_inv_bdcg_;

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -62,14 +63,26 @@ class DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
   void Resize(size_t n) {
     if (n == n_ && ptr_ != nullptr) return;
+    if (!owns_ && ptr_ != nullptr && n <= n_) {  // views never grow in place
+      n_ = n;
+      return;
+    }
     Free();
     n_ = n;
     if (n > 0) HIP_CHECK(hipMalloc(&ptr_, n * sizeof(T)));
   }
   void Free() {
-    if (ptr_ != nullptr) (void)hipFree(ptr_);
+    if (ptr_ != nullptr && owns_) (void)hipFree(ptr_);
     ptr_ = nullptr;
     n_ = 0;
+    owns_ = true;
+  }
+  // Non-owning view into memory carved from a larger allocation (arena).
+  void Attach(T* p, size_t n) {
+    Free();
+    ptr_ = p;
+    n_ = n;
+    owns_ = false;
   }
   T* get() const { return ptr_; }
   size_t size() const { return n_; }
@@ -88,6 +101,24 @@ class DevBuf {
  private:
   T* ptr_ = nullptr;
   size_t n_ = 0;
+  bool owns_ = true;
+};
+
+// Bump allocator laying out many small device buffers inside ONE allocation
+// (one TLB reach for all per-tree state instead of a page per buffer).
+class ArenaLayout {
+ public:
+  template <typename T>
+  size_t Add(size_t count) {
+    off_ = (off_ + 255) & ~static_cast<size_t>(255);
+    const size_t o = off_;
+    off_ += std::max<size_t>(count, 1) * sizeof(T);
+    return o;
+  }
+  size_t bytes() const { return (off_ + 255) & ~static_cast<size_t>(255); }
+
+ private:
+  size_t off_ = 0;
 };
 
 inline int DivUp(long long a, long long b) { return static_cast<int>((a + b - 1) / b); }

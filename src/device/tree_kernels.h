@@ -59,7 +59,7 @@ struct Ctl {
   int num_leaves, done, smaller, larger;
   int skip, num_splits, split_leaf, new_leaf;
   int parent_buf, parent_start, parent_count, target_buf;
-  int left_count, cls, scan_round, pad;
+  int left_count, cls, scan_round, max_count;  // max_count: largest leaf (rows), bounds useful grid size
 };
 
 struct SplitRec {
