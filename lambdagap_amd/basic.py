@@ -124,6 +124,9 @@ def _get_string(fn: Callable, size: int = 1 << 16) -> str:
 
 def _param_value(v: Any) -> str:
     if isinstance(v, (list, tuple, np.ndarray)):
+        if len(v) and isinstance(v[0], (list, tuple, np.ndarray)):
+            # list of lists (interaction_constraints): "[0,1,2],[3,4]"
+            return ",".join("[" + ",".join(_param_value(x) for x in inner) + "]" for inner in v)
         return ",".join(_param_value(x) for x in v)
     if isinstance(v, bool):
         return "true" if v else "false"

@@ -1,0 +1,419 @@
+"""scikit-learn estimators: LGBMModel, LGBMRegressor, LGBMClassifier, LGBMRanker.
+
+Same constructor arguments, fitted attributes and fit/predict signatures as the
+reference (python-package/lightgbm/sklearn.py:486 LGBMModel, :1314 regressor,
+:1424 classifier, :1678 ranker), implemented over :func:`lambdagap_amd.train`.
+"""
+from __future__ import annotations
+
+import copy
+from typing import Any, Callable, Dict, List, Optional, Union
+
+import numpy as np
+
+from .basic import Booster, Dataset, LightGBMError, _choose_param_value
+from .callback import record_evaluation
+from .engine import train
+
+try:
+    from sklearn.base import BaseEstimator, ClassifierMixin, RegressorMixin
+    from sklearn.preprocessing import LabelEncoder
+    from sklearn.utils.multiclass import check_classification_targets
+except ImportError:  # pragma: no cover
+    raise
+
+__all__ = ["LGBMModel", "LGBMRegressor", "LGBMClassifier", "LGBMRanker"]
+
+
+class _ObjectiveFunctionWrapper:
+    """Adapts a sklearn-style objective ``f(y_true, y_pred[, weight[, group]]) -> (grad, hess)``."""
+
+    def __init__(self, func: Callable):
+        self.func = func
+
+    def __call__(self, preds: np.ndarray, dataset: Dataset):
+        labels = dataset.get_label()
+        argc = self.func.__code__.co_argcount
+        if argc == 2:
+            return self.func(labels, preds)
+        if argc == 3:
+            return self.func(labels, preds, dataset.get_weight())
+        return self.func(labels, preds, dataset.get_weight(), dataset.get_group())
+
+
+class _EvalFunctionWrapper:
+    """Adapts ``f(y_true, y_pred[, weight[, group]]) -> (name, value, is_higher_better)``."""
+
+    def __init__(self, func: Callable):
+        self.func = func
+
+    def __call__(self, preds: np.ndarray, dataset: Dataset):
+        labels = dataset.get_label()
+        argc = self.func.__code__.co_argcount
+        if argc == 2:
+            return self.func(labels, preds)
+        if argc == 3:
+            return self.func(labels, preds, dataset.get_weight())
+        return self.func(labels, preds, dataset.get_weight(), dataset.get_group())
+
+
+class LGBMModel(BaseEstimator):
+    """Gradient boosting model with the scikit-learn estimator interface."""
+
+    def __init__(self, boosting_type: str = "gbdt", num_leaves: int = 31, max_depth: int = -1,
+                 learning_rate: float = 0.1, n_estimators: int = 100, subsample_for_bin: int = 200000,
+                 objective: Optional[Union[str, Callable]] = None, class_weight: Optional[Union[Dict, str]] = None,
+                 min_split_gain: float = 0.0, min_child_weight: float = 1e-3, min_child_samples: int = 20,
+                 subsample: float = 1.0, subsample_freq: int = 0, colsample_bytree: float = 1.0,
+                 reg_alpha: float = 0.0, reg_lambda: float = 0.0, random_state: Optional[Union[int, np.random.RandomState]] = None,
+                 n_jobs: Optional[int] = None, importance_type: str = "split", **kwargs: Any):
+        self.boosting_type = boosting_type
+        self.objective = objective
+        self.num_leaves = num_leaves
+        self.max_depth = max_depth
+        self.learning_rate = learning_rate
+        self.n_estimators = n_estimators
+        self.subsample_for_bin = subsample_for_bin
+        self.min_split_gain = min_split_gain
+        self.min_child_weight = min_child_weight
+        self.min_child_samples = min_child_samples
+        self.subsample = subsample
+        self.subsample_freq = subsample_freq
+        self.colsample_bytree = colsample_bytree
+        self.reg_alpha = reg_alpha
+        self.reg_lambda = reg_lambda
+        self.random_state = random_state
+        self.n_jobs = n_jobs
+        self.importance_type = importance_type
+        self.class_weight = class_weight
+        self._other_params: Dict[str, Any] = {}
+        self._Booster: Optional[Booster] = None
+        self._evals_result: Dict[str, Any] = {}
+        self._best_score: Dict[str, Any] = {}
+        self._best_iteration = -1
+        self._n_features = -1
+        self._n_classes = -1
+        self._objective = objective
+        self._class_weight = None
+        self._class_map = None
+        self.fitted_ = False
+        self.set_params(**kwargs)
+
+    # ------------------------------------------------------------------ params
+    def get_params(self, deep: bool = True) -> Dict[str, Any]:
+        params = super().get_params(deep=deep)
+        params.update(self._other_params)
+        return params
+
+    def set_params(self, **params: Any) -> "LGBMModel":
+        for key, value in params.items():
+            setattr(self, key, value)
+            if hasattr(self, f"_{key}"):
+                setattr(self, f"_{key}", value)
+            self._other_params[key] = value
+        return self
+
+    def _more_tags(self) -> Dict[str, Any]:
+        return {"allow_nan": True, "X_types": ["2darray", "sparse", "1dlabels"]}
+
+    def _default_objective(self) -> str:
+        return "regression"
+
+    def _process_params(self, stage: str) -> Dict[str, Any]:
+        params = self.get_params()
+        params.pop("objective", None)
+        for alias in ("class_weight", "importance_type", "n_estimators"):
+            params.pop(alias, None)
+        if isinstance(params.get("random_state"), np.random.RandomState):
+            params["random_state"] = params["random_state"].randint(np.iinfo(np.int32).max)
+        mapping = {"boosting_type": "boosting", "subsample_for_bin": "bin_construct_sample_cnt",
+                   "min_split_gain": "min_gain_to_split", "min_child_weight": "min_sum_hessian_in_leaf",
+                   "min_child_samples": "min_data_in_leaf", "subsample": "bagging_fraction",
+                   "subsample_freq": "bagging_freq", "colsample_bytree": "feature_fraction",
+                   "reg_alpha": "lambda_l1", "reg_lambda": "lambda_l2", "random_state": "seed",
+                   "n_jobs": "num_threads"}
+        out: Dict[str, Any] = {}
+        for k, v in params.items():
+            if v is None:
+                continue
+            out[mapping.get(k, k)] = v
+        if callable(self._objective):
+            out["objective"] = _ObjectiveFunctionWrapper(self._objective)
+        else:
+            out["objective"] = self._objective or self._default_objective()
+        out.setdefault("verbosity", -1)
+        return out
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, X, y, sample_weight=None, init_score=None, group=None, eval_set=None, eval_names=None,
+            eval_sample_weight=None, eval_class_weight=None, eval_init_score=None, eval_group=None,
+            eval_metric=None, feature_name="auto", categorical_feature="auto", callbacks=None,
+            init_model=None, position=None, eval_position=None) -> "LGBMModel":
+        params = self._process_params("fit")
+        feval = None
+        if eval_metric is not None:
+            metrics = eval_metric if isinstance(eval_metric, list) else [eval_metric]
+            names = [m for m in metrics if isinstance(m, str)]
+            funcs = [_EvalFunctionWrapper(m) for m in metrics if callable(m)]
+            if names:
+                base = params.get("metric")
+                base = [] if base is None else (base if isinstance(base, list) else [base])
+                params["metric"] = [*base, *names]
+            feval = funcs or None
+        X_arr = X
+        if hasattr(X, "shape"):
+            self._n_features = X.shape[1]
+        sw = sample_weight
+        if self._class_weight is not None:
+            cw = self._compute_class_weight(y)
+            sw = cw if sw is None else np.asarray(sw) * cw
+        train_set = Dataset(X_arr, label=y, weight=sw, group=group, init_score=init_score, position=position,
+                            feature_name=feature_name, categorical_feature=categorical_feature, params=params)
+        valid_sets: List[Dataset] = []
+        names: List[str] = []
+        if eval_set is not None:
+            if isinstance(eval_set, tuple):
+                eval_set = [eval_set]
+            for i, (vx, vy) in enumerate(eval_set):
+                if vx is X and vy is y:
+                    vs = train_set
+                else:
+                    def _get(coll, i):
+                        if coll is None:
+                            return None
+                        if isinstance(coll, dict):
+                            return coll.get(i)
+                        return coll[i]
+
+                    vw = _get(eval_sample_weight, i)
+                    vcw = _get(eval_class_weight, i)
+                    if vcw is not None:
+                        cw = self._class_weight_from(vcw, vy)
+                        vw = cw if vw is None else np.asarray(vw) * cw
+                    vs = train_set.create_valid(vx, label=vy, weight=vw, group=_get(eval_group, i),
+                                                init_score=_get(eval_init_score, i), position=_get(eval_position, i))
+                valid_sets.append(vs)
+                names.append(eval_names[i] if eval_names is not None and i < len(eval_names) else f"valid_{i}")
+        self._evals_result = {}
+        cbs = list(callbacks or [])
+        cbs.append(record_evaluation(self._evals_result))
+        self._Booster = train(params, train_set, num_boost_round=self.n_estimators, valid_sets=valid_sets,
+                              valid_names=names, feval=feval, init_model=init_model, callbacks=cbs)
+        self._best_iteration = self._Booster.best_iteration
+        self._best_score = self._Booster.best_score
+        self._n_features = self._Booster.num_feature()
+        self.fitted_ = True
+        return self
+
+    def _compute_class_weight(self, y) -> np.ndarray:
+        return self._class_weight_from(self._class_weight, y)
+
+    @staticmethod
+    def _class_weight_from(cw, y) -> np.ndarray:
+        y = np.asarray(y)
+        classes, counts = np.unique(y, return_counts=True)
+        if cw == "balanced":
+            weights = {c: len(y) / (len(classes) * n) for c, n in zip(classes, counts)}
+        else:
+            weights = {c: cw.get(c, 1.0) for c in classes}
+        return np.array([weights[v] for v in y], dtype=np.float64)
+
+    # ------------------------------------------------------------------ predict
+    def predict(self, X, raw_score: bool = False, start_iteration: int = 0, num_iteration: Optional[int] = None,
+                pred_leaf: bool = False, pred_contrib: bool = False, validate_features: bool = False, **kwargs):
+        if self._Booster is None:
+            raise LightGBMError("Estimator not fitted, call fit before exploiting the model.")
+        if hasattr(X, "shape") and X.shape[1] != self._n_features:
+            raise ValueError(f"Number of features of the model must match the input. Model n_features_ is "
+                             f"{self._n_features} and input n_features is {X.shape[1]}")
+        return self._Booster.predict(X, raw_score=raw_score, start_iteration=start_iteration,
+                                     num_iteration=num_iteration, pred_leaf=pred_leaf, pred_contrib=pred_contrib,
+                                     validate_features=validate_features, **kwargs)
+
+    # ------------------------------------------------------------------ attributes
+    def _check_fitted(self) -> None:
+        if self._Booster is None:
+            from sklearn.exceptions import NotFittedError
+
+            raise NotFittedError("No booster found. Need to call fit beforehand.")
+
+    @property
+    def n_features_(self) -> int:
+        self._check_fitted()
+        return self._n_features
+
+    @property
+    def n_features_in_(self) -> int:
+        self._check_fitted()
+        return self._n_features
+
+    @property
+    def best_score_(self):
+        self._check_fitted()
+        return self._best_score
+
+    @property
+    def best_iteration_(self) -> int:
+        self._check_fitted()
+        return self._best_iteration
+
+    @property
+    def objective_(self):
+        self._check_fitted()
+        return self._objective or self._default_objective()
+
+    @property
+    def n_estimators_(self) -> int:
+        self._check_fitted()
+        return self._Booster.current_iteration()
+
+    @property
+    def n_iter_(self) -> int:
+        return self.n_estimators_
+
+    @property
+    def booster_(self) -> Booster:
+        self._check_fitted()
+        return self._Booster
+
+    @property
+    def evals_result_(self):
+        self._check_fitted()
+        return self._evals_result
+
+    @property
+    def feature_importances_(self) -> np.ndarray:
+        self._check_fitted()
+        return self._Booster.feature_importance(importance_type=self.importance_type)
+
+    @property
+    def feature_name_(self) -> List[str]:
+        self._check_fitted()
+        return self._Booster.feature_name()
+
+    @property
+    def feature_names_in_(self) -> np.ndarray:
+        return np.array(self.feature_name_)
+
+
+class LGBMRegressor(RegressorMixin, LGBMModel):
+    """LightGBM regressor."""
+
+    def _default_objective(self) -> str:
+        return "regression"
+
+    def fit(self, X, y, sample_weight=None, init_score=None, eval_set=None, eval_names=None,
+            eval_sample_weight=None, eval_init_score=None, eval_metric=None, feature_name="auto",
+            categorical_feature="auto", callbacks=None, init_model=None):
+        return super().fit(X, y, sample_weight=sample_weight, init_score=init_score, eval_set=eval_set,
+                           eval_names=eval_names, eval_sample_weight=eval_sample_weight,
+                           eval_init_score=eval_init_score, eval_metric=eval_metric, feature_name=feature_name,
+                           categorical_feature=categorical_feature, callbacks=callbacks, init_model=init_model)
+
+
+class LGBMClassifier(ClassifierMixin, LGBMModel):
+    """LightGBM classifier (binary or multiclass; labels of any type)."""
+
+    def _default_objective(self) -> str:
+        return "binary" if self._n_classes <= 2 else "multiclass"
+
+    def fit(self, X, y, sample_weight=None, init_score=None, eval_set=None, eval_names=None,
+            eval_sample_weight=None, eval_class_weight=None, eval_init_score=None, eval_metric=None,
+            feature_name="auto", categorical_feature="auto", callbacks=None, init_model=None):
+        check_classification_targets(y)
+        self._le = LabelEncoder().fit(y)
+        y_enc = self._le.transform(y)
+        self._class_map = dict(zip(self._le.classes_, range(len(self._le.classes_))))
+        if isinstance(self.class_weight, dict):
+            self._class_weight = {self._class_map[k]: v for k, v in self.class_weight.items()}
+        self._classes = self._le.classes_
+        self._n_classes = len(self._classes)
+        if self._n_classes > 2:
+            self._other_params["num_class"] = self._n_classes
+        if not callable(self._objective) and self._objective is not None:
+            obj = str(self._objective)
+            if obj in ("multiclass", "softmax", "multiclassova", "multiclass_ova", "ova", "ovr"):
+                self._other_params["num_class"] = self._n_classes
+        valid = None
+        if eval_set is not None:
+            if isinstance(eval_set, tuple):
+                eval_set = [eval_set]
+            valid = []
+            for vx, vy in eval_set:
+                if vx is X and vy is y:
+                    valid.append((vx, y_enc))
+                else:
+                    valid.append((vx, self._le.transform(vy)))
+        if eval_metric is not None:
+            metrics = eval_metric if isinstance(eval_metric, list) else [eval_metric]
+            fixed = []
+            for m in metrics:
+                if isinstance(m, str) and self._n_classes > 2:
+                    m = {"logloss": "multi_logloss", "binary_logloss": "multi_logloss", "error": "multi_error",
+                         "binary_error": "multi_error"}.get(m, m)
+                elif isinstance(m, str):
+                    m = {"logloss": "binary_logloss", "error": "binary_error"}.get(m, m)
+                fixed.append(m)
+            eval_metric = fixed
+        X_fit = X
+        super().fit(X_fit, y_enc, sample_weight=sample_weight, init_score=init_score, eval_set=valid,
+                    eval_names=eval_names, eval_sample_weight=eval_sample_weight, eval_class_weight=eval_class_weight,
+                    eval_init_score=eval_init_score, eval_metric=eval_metric, feature_name=feature_name,
+                    categorical_feature=categorical_feature, callbacks=callbacks, init_model=init_model)
+        return self
+
+    def predict(self, X, raw_score: bool = False, start_iteration: int = 0, num_iteration: Optional[int] = None,
+                pred_leaf: bool = False, pred_contrib: bool = False, validate_features: bool = False, **kwargs):
+        result = self.predict_proba(X, raw_score, start_iteration, num_iteration, pred_leaf, pred_contrib,
+                                    validate_features, **kwargs)
+        if callable(self._objective) or raw_score or pred_leaf or pred_contrib:
+            return result
+        idx = np.argmax(result, axis=1)
+        return self._le.inverse_transform(idx)
+
+    def predict_proba(self, X, raw_score: bool = False, start_iteration: int = 0,
+                      num_iteration: Optional[int] = None, pred_leaf: bool = False, pred_contrib: bool = False,
+                      validate_features: bool = False, **kwargs):
+        result = super().predict(X, raw_score, start_iteration, num_iteration, pred_leaf, pred_contrib,
+                                 validate_features, **kwargs)
+        if callable(self._objective) and not (raw_score or pred_leaf or pred_contrib):
+            return result
+        if self._n_classes > 2 or raw_score or pred_leaf or pred_contrib:
+            return result
+        return np.vstack((1.0 - result, result)).transpose()
+
+    @property
+    def classes_(self) -> np.ndarray:
+        self._check_fitted()
+        return self._classes
+
+    @property
+    def n_classes_(self) -> int:
+        self._check_fitted()
+        return self._n_classes
+
+
+class LGBMRanker(LGBMModel):
+    """LightGBM ranker (lambdarank by default; all LambdaGap `lambdarank_target`s via kwargs)."""
+
+    def _default_objective(self) -> str:
+        return "lambdarank"
+
+    def fit(self, X, y, sample_weight=None, init_score=None, group=None, eval_set=None, eval_names=None,
+            eval_sample_weight=None, eval_init_score=None, eval_group=None, eval_metric=None, eval_at=(1, 2, 3, 4, 5),
+            feature_name="auto", categorical_feature="auto", callbacks=None, init_model=None, position=None,
+            eval_position=None):
+        if group is None:
+            raise ValueError("Should set group for ranking task")
+        if eval_set is not None:
+            if eval_group is None:
+                raise ValueError("Eval_group cannot be None when eval_set is not None")
+            n = 1 if isinstance(eval_set, tuple) else len(eval_set)
+            if len(eval_group) != n:
+                raise ValueError("Length of eval_group should be equal to eval_set")
+        self._other_params["eval_at"] = list(eval_at)
+        return super().fit(X, y, sample_weight=sample_weight, init_score=init_score, group=group, eval_set=eval_set,
+                           eval_names=eval_names, eval_sample_weight=eval_sample_weight,
+                           eval_init_score=eval_init_score, eval_group=eval_group, eval_metric=eval_metric,
+                           feature_name=feature_name, categorical_feature=categorical_feature, callbacks=callbacks,
+                           init_model=init_model, position=position, eval_position=eval_position)
