@@ -651,9 +651,12 @@ class Booster:
         self._num_class = 1
         self._eval_names: Optional[List[str]] = None
         self.__inner_predict_buffer: Dict[int, np.ndarray] = {}
+        self._network = False
         if train_set is not None:
             if not isinstance(train_set, Dataset):
                 raise TypeError(f"Training data should be Dataset instance, met {type(train_set).__name__}")
+            # the socket mesh must exist before binning: distributed bin finding syncs the mappers
+            self._setup_network()
             train_set._update_params(self.params)
             train_set.construct()
             self.train_set = train_set
@@ -677,8 +680,32 @@ class Booster:
             if self.handle is not None and self.handle.value:
                 _LIB.LGBM_BoosterFree(self.handle)
                 self.handle = None
+            if getattr(self, "_network", False):
+                _LIB.LGBM_NetworkFree()
+                self._network = False
         except Exception:
             pass
+
+    def _setup_network(self) -> None:
+        """Socket mesh from `machines` / `num_machines` params (reference basic.py Booster.set_network)."""
+        p = self.params
+        machines = p.get("machines", p.get("workers", p.get("nodes")))
+        num = int(p.get("num_machines", p.get("num_machine", 1)))
+        if not machines or num <= 1:
+            return
+        if isinstance(machines, (list, tuple, set)):
+            machines = ",".join(machines)
+        port = int(p.get("local_listen_port", p.get("local_port", p.get("port", 12400))))
+        timeout = int(p.get("time_out", 120))
+        _check(_LIB.LGBM_NetworkInit(_c_str(str(machines)), ctypes.c_int(port), ctypes.c_int(timeout),
+                                     ctypes.c_int(num)))
+        self._network = True
+
+    def free_network(self) -> "Booster":
+        if self._network:
+            _check(_LIB.LGBM_NetworkFree())
+            self._network = False
+        return self
 
     def __copy__(self):
         return self.__deepcopy__(None)

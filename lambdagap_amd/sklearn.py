@@ -157,15 +157,20 @@ class LGBMModel(BaseEstimator):
             funcs = [_EvalFunctionWrapper(m) for m in metrics if callable(m)]
             if names:
                 base = params.get("metric")
-                base = [] if base is None else (base if isinstance(base, list) else [base])
-                params["metric"] = [*base, *names]
+                if base is None:
+                    # keep the objective's default metric (objective names are metric aliases)
+                    obj = params.get("objective")
+                    base = [obj] if isinstance(obj, str) else []
+                base = base if isinstance(base, list) else [base]
+                params["metric"] = [*base, *[n for n in names if n not in base]]
             feval = funcs or None
         X_arr = X
         if hasattr(X, "shape"):
             self._n_features = X.shape[1]
         sw = sample_weight
-        if self._class_weight is not None:
-            cw = self._compute_class_weight(y)
+        class_weight = self._class_weight if self._class_weight is not None else self.class_weight
+        if class_weight is not None:
+            cw = self._class_weight_from(class_weight, y)
             sw = cw if sw is None else np.asarray(sw) * cw
         train_set = Dataset(X_arr, label=y, weight=sw, group=group, init_score=init_score, position=position,
                             feature_name=feature_name, categorical_feature=categorical_feature, params=params)

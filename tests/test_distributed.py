@@ -1,0 +1,103 @@
+"""Multi-process distributed training on CPU over the TCP socket mesh (2 ranks, 127.0.0.1).
+
+Covers the three parallel tree learners (data / feature / voting) and the
+distributed bin-finding path, the CPU analogue of the reference's
+examples/parallel_learning setup.
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+DATA = os.path.join(os.path.dirname(__file__), "data")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _worker(rank, ports, learner, rows, out_dir, extra):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import lambdagap_amd as lgb
+
+    mat = np.loadtxt(os.path.join(DATA, "binary.train"))
+    X, y = mat[:, 1:], mat[:, 0]
+    if rows == "split":
+        X, y = X[rank::2], y[rank::2]
+    machines = ",".join(f"127.0.0.1:{p}" for p in ports)
+    params = {"objective": "binary", "tree_learner": learner, "num_machines": 2, "machines": machines,
+              "local_listen_port": ports[rank], "verbosity": -1, "num_leaves": 15, "pre_partition": True,
+              "time_out": 2, **extra}
+    b = lgb.train(params, lgb.Dataset(X, y, params=params), 8)
+    with open(os.path.join(out_dir, f"model{rank}.txt"), "w") as f:
+        f.write(b.model_to_string())
+
+
+def _run(learner, rows, tmp_path, extra=None):
+    ports = _free_ports(2)
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_worker, args=(r, ports, learner, rows, str(tmp_path), extra or {}))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0, 0], codes
+    return [open(tmp_path / f"model{r}.txt").read() for r in range(2)]
+
+
+def _trees(s):
+    return s.split("end of trees")[0]
+
+
+@pytest.mark.parametrize("learner", ["data", "voting"])
+def test_row_sharded_learners(lgb, tmp_path, learner):
+    m0, m1 = _run(learner, "split", tmp_path)
+    # every rank ends with the same model
+    assert _trees(m0) == _trees(m1)
+    b = lgb.Booster(model_str=m0)
+    t = np.loadtxt(os.path.join(DATA, "binary.test"))
+    from sklearn.metrics import roc_auc_score
+
+    assert roc_auc_score(t[:, 0], b.predict(t[:, 1:])) > 0.75
+
+
+def test_data_parallel_matches_serial_on_same_bins(lgb, tmp_path):
+    """Every rank holding ALL rows: data-parallel sums two identical halves of every histogram, which is the
+    serial histogram doubled -> the same splits as serial training with doubled weights."""
+    m0, m1 = _run("data", "all", tmp_path, {"min_data_in_leaf": 20})
+    assert _trees(m0) == _trees(m1)
+    mat = np.loadtxt(os.path.join(DATA, "binary.train"))
+    X, y = mat[:, 1:], mat[:, 0]
+    serial = lgb.train({"objective": "binary", "verbosity": -1, "num_leaves": 15, "min_data_in_leaf": 40},
+                       lgb.Dataset(np.vstack([X, X]), np.concatenate([y, y])), 8)
+    t = np.loadtxt(os.path.join(DATA, "binary.test"))
+    np.testing.assert_allclose(lgb.Booster(model_str=m0).predict(t[:, 1:]), serial.predict(t[:, 1:]), rtol=1e-6,
+                               atol=1e-8)
+
+
+def test_feature_parallel_matches_serial(lgb, tmp_path):
+    m0, m1 = _run("feature", "all", tmp_path)
+    assert _trees(m0) == _trees(m1)
+    mat = np.loadtxt(os.path.join(DATA, "binary.train"))
+    serial = lgb.train({"objective": "binary", "verbosity": -1, "num_leaves": 15}, lgb.Dataset(mat[:, 1:], mat[:, 0]),
+                       8)
+    t = np.loadtxt(os.path.join(DATA, "binary.test"))
+    np.testing.assert_allclose(lgb.Booster(model_str=m0).predict(t[:, 1:]), serial.predict(t[:, 1:]), rtol=1e-9)
