@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Single-GPU rehearsal of the RCCL data-parallel HIP learner.
+
+Creates a one-rank RCCL communicator, trains with LGAP_FORCE_DEVICE_DP=1 (the
+learner then takes the distributed path: fixed-point partials decoded to fp64
+staging, ncclAllReduce, scan from staging, global leaf counts from the split
+records) and compares against the single-device path on the same data.
+Prints one JSON line; tests/test_gpu_learner.py runs this in a subprocess so the
+communicator never outlives it.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    import lambdagap_amd as lgb
+    from lambdagap_amd.parallel import distributed as d
+
+    uid = d.get_unique_id()
+    import ctypes
+
+    d._check(d._LIB.LGBM_DeviceCommInit(d._c_str(uid), ctypes.c_int64(len(uid)), ctypes.c_int(1), ctypes.c_int(0),
+                                        ctypes.c_int(0)))
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((60000, 12))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    y = ((np.nan_to_num(X[:, 0]) + 0.5 * np.nan_to_num(X[:, 3]) ** 2 + 0.3 * rng.standard_normal(60000)) > 0.4)
+    y = y.astype(float)
+    params = {"objective": "binary", "num_leaves": 31, "device_type": "gpu", "verbosity": -1, "seed": 1,
+              "min_data_in_leaf": 20}
+    out = {}
+    for mode in ("single", "dp"):
+        os.environ["LGAP_FORCE_DEVICE_DP"] = "1" if mode == "dp" else "0"
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 8)
+        out[mode] = b
+    pa, pb = out["single"].predict(X), out["dp"].predict(X)
+    ta = [t["tree_structure"].get("split_feature") for t in out["single"].dump_model()["tree_info"]]
+    tb = [t["tree_structure"].get("split_feature") for t in out["dp"].dump_model()["tree_info"]]
+    print(json.dumps({"max_abs_diff": float(np.max(np.abs(pa - pb))), "root_features_equal": ta == tb,
+                      "num_trees": [out["single"].num_trees(), out["dp"].num_trees()]}), flush=True)
+    d.free_device_comm()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1356,7 +1356,10 @@ class DeviceTreeLearner : public TreeLearner {
     if (data_parallel_ && !CommActive() && Network::num_machines() > 1) {
       Log::Fatal("Data-parallel HIP training needs an RCCL communicator (LGBM_DeviceCommInit)");
     }
-    distributed_ = data_parallel_ && CommActive();
+    // LGAP_FORCE_DEVICE_DP=1 routes a single-rank run through the RCCL data-parallel path
+    // (staging reduce + ncclAllReduce + global counts): lets a 1-GPU box test that path.
+    const char* force_dp = std::getenv("LGAP_FORCE_DEVICE_DP");
+    distributed_ = CommActive() && (data_parallel_ || (force_dp && force_dp[0] == '1'));
     device_id_ = CommActive() ? CommDevice() : std::max(0, config_->gpu_device_id);
     HIP_CHECK(hipSetDevice(device_id_));
     hipDeviceProp_t prop;

@@ -166,6 +166,7 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian
   bounds_.assign(config_->num_leaves, LeafBounds());
   leaf_count_global_.assign(config_->num_leaves, 0);
   use_monotone_ = !config_->monotone_constraints.empty();
+  SetupPolicies();
   extra_rand_ = Random(config_->extra_seed);
   feature_mask_.assign(num_features_, 1);
   hist_begin_ = 0;
@@ -190,6 +191,26 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
   }
   col_sampler_.Init(train_data_, config_);
   use_monotone_ = !config_->monotone_constraints.empty();
+  SetupPolicies();
+}
+
+void SerialTreeLearner::SetupPolicies() {
+  intermediate_monotone_ = use_monotone_ && config_->monotone_constraints_method != "basic";
+  if (use_monotone_ && config_->monotone_constraints_method == "advanced") {
+    Log::Warning("monotone_constraints_method=advanced is served by the intermediate method");
+  }
+  if (intermediate_monotone_) mono_.Init(train_data_, config_->num_leaves);
+  if (CegbPenalty::Enabled(config_)) {
+    if (!cegb_) cegb_ = std::make_unique<CegbPenalty>();
+    cegb_->Init(train_data_, config_);
+  } else {
+    cegb_.reset();
+  }
+  if (config_->use_quantized_grad) {
+    quantizer_.Init(num_data_, config_->num_grad_quant_bins, config_->seed, config_->stochastic_rounding);
+    qgrad_.resize(num_data_);
+    qhess_.resize(num_data_);
+  }
 }
 
 void SerialTreeLearner::SetBaggingData(const data_size_t* used_indices, data_size_t num_data) {
@@ -294,6 +315,8 @@ void SerialTreeLearner::BeforeTrain() {
   for (auto& s : best_split_per_leaf_) s.Reset();
   for (auto& b : bounds_) b = LeafBounds();
   for (auto& s : splittable_) std::fill(s.begin(), s.end(), 1);
+  if (intermediate_monotone_) mono_.Reset();
+  if (cegb_) cegb_->BeforeTree();
   double sg, sh;
   ComputeLeafSums(partition_.indices(0), partition_.count(0), &sg, &sh);
   InitLeafStat(&smaller_, 0, sg, sh, 0.0);
@@ -366,8 +389,14 @@ SplitInfo SerialTreeLearner::BestSplitForFeature(const double* group_hist, int f
 
 std::unique_ptr<Tree> SerialTreeLearner::Train(const score_t* gradients, const score_t* hessians, bool) {
   ScopedTimer t("SerialTreeLearner::Train");
-  gradients_ = gradients;
-  hessians_ = hessians;
+  gradients_ = true_gradients_ = gradients;
+  hessians_ = true_hessians_ = hessians;
+  if (config_->use_quantized_grad) {
+    // integer-level (g, h); sums of de-scaled integers are exact in the fp64 histograms
+    quantizer_.Quantize(gradients, hessians, num_data_, is_constant_hessian_, qgrad_.data(), qhess_.data());
+    gradients_ = qgrad_.data();
+    hessians_ = qhess_.data();
+  }
   if (extra_rands_.size() != static_cast<size_t>(num_features_)) {
     extra_rands_.clear();
     for (int f = 0; f < num_features_; ++f) extra_rands_.emplace_back(config_->extra_seed + f);
@@ -396,6 +425,7 @@ std::unique_ptr<Tree> SerialTreeLearner::Train(const score_t* gradients, const s
     }
     Split(tree.get(), best, &left, &right);
   }
+  if (config_->use_quantized_grad && config_->quant_train_renew_leaf) RenewQuantizedLeaves(tree.get());
   tree->RecomputeMaxDepth();
   return tree;
 }
@@ -472,14 +502,12 @@ void SerialTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, bool use_
       continue;
     }
     bool sp = false;
-    SplitInfo s = BestSplitForFeature(hs, f, smaller_, po_s, bounds_[smaller_.leaf], &sp);
+    SplitInfo s = ScoreFeature(tree, hs, f, smaller_, po_s, &sp);
     spl_s[f] = sp;
-    if (s.monotone_type != 0 && s.feature >= 0) s.gain *= MonotonePenalty(tree, smaller_.leaf);
     if (node_s[f]) bs[f] = s;
     if (has_larger) {
-      SplitInfo l = BestSplitForFeature(hl, f, larger_, po_l, bounds_[larger_.leaf], &sp);
+      SplitInfo l = ScoreFeature(tree, hl, f, larger_, po_l, &sp);
       (*spl_l)[f] = sp;
-      if (l.monotone_type != 0 && l.feature >= 0) l.gain *= MonotonePenalty(tree, larger_.leaf);
       if (node_l[f]) bl[f] = l;
     }
   }
@@ -495,7 +523,74 @@ void SerialTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, bool use_
   SyncBestSplits();
 }
 
+SplitInfo SerialTreeLearner::ScoreFeature(const Tree* tree, const double* group_hist, int f, const LeafStat& leaf,
+                                          double parent_output, bool* splittable) {
+  SplitInfo s = BestSplitForFeature(group_hist, f, leaf, parent_output, bounds_[leaf.leaf], splittable);
+  if (s.feature < 0) return s;
+  if (cegb_) s.gain -= cegb_->DeltaGain(f, leaf.leaf, partition_.indices(leaf.leaf), partition_.count(leaf.leaf), s);
+  if (s.monotone_type != 0) s.gain *= MonotonePenalty(tree, leaf.leaf);
+  return s;
+}
+
+// reference serial_tree_learner.cpp RecomputeBestSplitForLeaf: the leaf keeps its
+// histogram; its statistics come from the pending best split
+void SerialTreeLearner::RecomputeBestSplit(const Tree* tree, int leaf) {
+  SplitInfo& cur = best_split_per_leaf_[leaf];
+  if (hist_[leaf].size() != static_cast<size_t>(2 * train_data_->num_total_bin())) return;
+  LeafStat ls;
+  ls.leaf = leaf;
+  ls.sum_g = cur.left_sum_gradient + cur.right_sum_gradient;
+  ls.sum_h = cur.left_sum_hessian + cur.right_sum_hessian;
+  ls.count = ls.global_count = cur.left_count + cur.right_count;
+  double po = 0.0;
+  if (config_->path_smooth > kEpsilon) {
+    SplitParams p = MakeParams();
+    p.path_smooth = 0.0;
+    po = LeafOutputRaw(ls.sum_g, ls.sum_h, p, ls.count, 0.0);
+  }
+  ls.output = po;
+  const auto& bytree = col_sampler_.is_feature_used_bytree();
+  SplitInfo best;
+  best.Reset();
+  for (int f = 0; f < num_features_; ++f) {
+    if (!bytree[f] || !feature_mask_[f] || !splittable_[leaf][f]) continue;
+    bool sp;
+    SplitInfo s = ScoreFeature(tree, hist_[leaf].data(), f, ls, po, &sp);
+    if (s.feature >= 0 && s.BetterThan(best)) best = s;
+  }
+  cur = best;
+}
+
+void SerialTreeLearner::RenewQuantizedLeaves(Tree* tree) const {
+  const int nl = tree->num_leaves();
+  std::vector<double> st(2 * nl, 0.0);
+  for (int l = 0; l < nl; ++l) {
+    const data_size_t n = partition_.count(l);
+    const data_size_t* idx = partition_.indices(l);
+    double g = 0.0, h = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : g, h) if (n >= 4096)
+    for (data_size_t i = 0; i < n; ++i) {
+      g += true_gradients_[idx[i]];
+      h += true_hessians_[idx[i]];
+    }
+    st[2 * l] = g;
+    st[2 * l + 1] = h;
+  }
+  const bool global = config_->tree_learner == "data" && Network::num_machines() > 1;
+  if (global) Network::GlobalSum(&st);
+  SplitParams p = MakeParams();
+  p.path_smooth = 0.0;
+  for (int l = 0; l < nl; ++l) {
+    const data_size_t cnt = global ? GlobalCount(l) : partition_.count(l);
+    tree->SetLeafOutput(l, LeafOutputRaw(st[2 * l], st[2 * l + 1], p, cnt, 0.0));
+  }
+}
+
 void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) {
+  if (cegb_) {
+    cegb_->OnSplit(tree->num_leaves(), best_leaf, best_split_per_leaf_[best_leaf], partition_.indices(best_leaf),
+                   partition_.count(best_leaf), &best_split_per_leaf_);
+  }
   SplitInfo info = best_split_per_leaf_[best_leaf];
   const int f = info.feature;
   const FeatureInfo& fi = train_data_->feature(f);
@@ -504,6 +599,7 @@ void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* ri
   *left_leaf = best_leaf;
   const Dataset* d = train_data_;
   data_size_t nl;
+  if (intermediate_monotone_) mono_.BeforeSplit(tree, best_leaf, next, info.monotone_type);
   if (fi.bin_type == BinType::Numerical) {
     const uint32_t thr = info.threshold;
     const bool dl = info.default_left != 0;
@@ -562,9 +658,13 @@ void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* ri
     smaller_.global_count = leaf_count_global_[smaller_.leaf];
     larger_.global_count = leaf_count_global_[larger_.leaf];
   }
-  // basic monotone constraints
   bounds_[next] = bounds_[best_leaf];
-  if (use_monotone_ && fi.bin_type == BinType::Numerical) {
+  if (intermediate_monotone_) {
+    const auto redo = mono_.AfterSplit(tree, &bounds_, fi.bin_type == BinType::Numerical, best_leaf, next,
+                                       info.monotone_type, info, best_split_per_leaf_);
+    for (int l : redo) RecomputeBestSplit(tree, l);
+  } else if (use_monotone_ && fi.bin_type == BinType::Numerical) {
+    // basic method: both children bounded by the midpoint of their outputs
     const double mid = (info.left_output + info.right_output) / 2.0f;
     if (info.monotone_type < 0) {
       bounds_[best_leaf].min = std::max(bounds_[best_leaf].min, mid);
@@ -687,7 +787,7 @@ int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf) 
     for (int f = 0; f < num_features_; ++f) {
       if (!col_sampler_.is_feature_used_bytree()[f]) continue;
       bool sp;
-      SplitInfo s = BestSplitForFeature(HistOf(l).data(), f, ls, ls.output, bounds_[l], &sp);
+      SplitInfo s = ScoreFeature(tree, HistOf(l).data(), f, ls, ls.output, &sp);
       if (s.feature >= 0 && s.BetterThan(best)) best = s;
     }
     best_split_per_leaf_[l] = best;

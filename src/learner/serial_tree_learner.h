@@ -8,6 +8,7 @@
 #include <set>
 #include <vector>
 
+#include "leaf_constraints.h"
 #include "lgap/random.h"
 #include "lgap/split_math.h"
 #include "lgap/tree_learner.h"
@@ -103,7 +104,15 @@ class SerialTreeLearner : public TreeLearner {
   void InitLeafStat(LeafStat* ls, int leaf, double sg, double sh, double output);
   SplitParams MakeParams() const;
   std::vector<double>& HistOf(int leaf);
+  void SetupPolicies();
   int ForceSplits(Tree* tree, int* left_leaf, int* right_leaf);
+  // BestSplitForFeature + CEGB deduction + monotone split penalty (ComputeBestSplitForFeature)
+  SplitInfo ScoreFeature(const Tree* tree, const double* group_hist, int f, const LeafStat& leaf,
+                         double parent_output, bool* splittable);
+  // intermediate monotone: rescan a leaf whose constraint interval tightened
+  void RecomputeBestSplit(const Tree* tree, int leaf);
+  // quant_train_renew_leaf: leaf outputs from the true (unquantized) gradient sums
+  void RenewQuantizedLeaves(Tree* tree) const;
 
   const Config* config_;
   const Dataset* train_data_ = nullptr;
@@ -124,6 +133,13 @@ class SerialTreeLearner : public TreeLearner {
   bool has_parent_hist_ = false;
   Random extra_rand_;
   bool use_monotone_ = false;
+  bool intermediate_monotone_ = false;
+  IntermediateMonotone mono_;
+  std::unique_ptr<CegbPenalty> cegb_;
+  GradientQuantizer quantizer_;
+  std::vector<score_t> qgrad_, qhess_;
+  const score_t* true_gradients_ = nullptr;
+  const score_t* true_hessians_ = nullptr;
   std::string forced_json_;
   std::vector<Random> extra_rands_;
   // parallel learners

@@ -343,12 +343,14 @@ def test_params_train(lgb, binary_data, extra):
                 assert any(feats <= a for a in allowed), feats
 
 
-def test_monotone_constraints(lgb, rng):
+@pytest.mark.parametrize("method", ["basic", "intermediate", "advanced"])
+@pytest.mark.parametrize("penalty", [0.0, 2.0])
+def test_monotone_constraints(lgb, rng, method, penalty):
     n = 3000
     X = rng.random((n, 3))
     y = 5 * X[:, 0] - 3 * X[:, 1] + np.sin(10 * X[:, 2]) + 0.3 * rng.standard_normal(n)
-    b = lgb.train({"objective": "regression", "monotone_constraints": [1, -1, 0], "verbosity": -1}, lgb.Dataset(X, y),
-                  50)
+    b = lgb.train({"objective": "regression", "monotone_constraints": [1, -1, 0], "verbosity": -1,
+                   "monotone_constraints_method": method, "monotone_penalty": penalty}, lgb.Dataset(X, y), 50)
     grid = np.linspace(0, 1, 50)
     base = rng.random((20, 3))
     for row in base:
