@@ -27,6 +27,21 @@ bool CommActive();
 // variant (tree_learner=data|voting|feature with an RCCL communicator).
 std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const std::string& parallel_mode);
 
+// GPU histogram engine for the host learners (the reference's GPUTreeLearner
+// split, src/treelearner/gpu_tree_learner.cpp: histograms on the device, split
+// policy on the host). Used when a host-side policy (CEGB, forced splits,
+// intermediate/advanced monotone, linear leaves, voting/feature parallel) is
+// requested with device_type=gpu. Gradients are uploaded once per tree.
+class HistogramBackend {
+ public:
+  virtual ~HistogramBackend() = default;
+  virtual void SetGradients(const float* grad, const float* hess, int num_data) = 0;
+  // out: 2 * num_total_bin doubles (group bin 0 left zero, as the host builder)
+  virtual void Histogram(const int* rows, int num_rows, double* out) = 0;
+  virtual std::string DeviceName() const = 0;
+};
+std::unique_ptr<HistogramBackend> CreateHistogramBackend(const Config* config, const Dataset* data);
+
 // Histogram of (grad, hess) over `rows` (all rows when null) with the HIP
 // histogram kernel; out has 2 * num_total_bin doubles.
 void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, const int* rows, int num_rows,

@@ -110,6 +110,10 @@ struct Args {
   int distributed;
   int use_monotone;
   double monotone_penalty;
+  // interaction constraints: bit k of ic_feat[f] = constraint set k holds f;
+  // ic_leaf[leaf] = sets that hold every feature on the leaf's branch
+  const unsigned long long* ic_feat;
+  unsigned long long* ic_leaf;
   SplitParams sp;
 };
 
@@ -189,6 +193,57 @@ __device__ double MonotonePenaltyAt(double pen, int depth) {
 }
 
 // ---------------------------------------------------------------------------
+// quantized-gradient training (reference gradient_discretizer.cpp:66-160):
+// max |g|, |h| over the rows, then integer levels with stochastic rounding,
+// stored de-scaled in place so the fixed-point histograms sum exact integers.
+
+__device__ __forceinline__ float HashUniform(uint32_t seed, uint32_t i) {
+  uint32_t x = i * 0x9E3779B1u + seed * 0x85EBCA77u;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return static_cast<float>(x >> 8) * (1.0f / 16777216.0f);
+}
+
+__global__ __launch_bounds__(256) void k_qmax(const float2* gh, int n, unsigned* qmax) {
+  float mg = 0.f, mh = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float2 v = gh[i];
+    mg = fmaxf(mg, fabsf(v.x));
+    mh = fmaxf(mh, fabsf(v.y));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
+    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&qmax[0], __float_as_uint(mg));  // non-negative floats order as their bits
+    atomicMax(&qmax[1], __float_as_uint(mh));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_quantize(float2* gh, float2* gh_true, int n, const unsigned* qmax, int bins,
+                                                  int const_hess, uint32_t seed, int stochastic) {
+  const double mg = __uint_as_float(qmax[0]), mh = __uint_as_float(qmax[1]);
+  const double gs = mg / (bins / 2), hs = const_hess ? mh : mh / bins;
+  const double ig = gs > 0 ? 1.0 / gs : 0.0, ih = hs > 0 ? 1.0 / hs : 0.0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float2 v = gh[i];
+    if (gh_true) gh_true[i] = v;
+    const double rg = stochastic ? HashUniform(seed, 2u * i) : 0.5;
+    const double rh = stochastic ? HashUniform(seed, 2u * i + 1u) : 0.5;
+    const double x = v.x * ig;
+    const int q = static_cast<int>(v.x >= 0.f ? x + rg : x - rg);  // truncation toward zero
+    float2 o;
+    o.x = static_cast<float>(q * gs);
+    o.y = const_hess ? static_cast<float>(hs) : static_cast<float>(static_cast<int>(v.y * ih + rh) * hs);
+    gh[i] = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // tree setup
 
 __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
@@ -225,6 +280,7 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     a.gcount[0] = tp.root_gcount;
     a.depth[0] = 0;
     a.lout[0] = 0.0;
+    if (a.ic_leaf) a.ic_leaf[0] = ~0ull;
   }
   for (int i = t; i < a.L; i += blockDim.x) {
     a.slot[i] = i;
@@ -851,6 +907,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
         out->feature = f;
         if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
         if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
+        if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
       }
     }
   }
@@ -865,6 +922,34 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     for (int i = lane; i < kWords; i += 64) dst[i] = src[i];
   }
   Stamp(a, 3, 4);
+}
+
+// quant_train_renew_leaf: per-leaf sums of the unquantized (g, h); one block per leaf
+__global__ __launch_bounds__(kNodeThreads) void k_leaf_true_sums(Args a, const float2* gh_true, int num_leaves,
+                                                                  double2* out) {
+  __shared__ double sh[2][kNodeThreads / 64];
+  const int leaf = blockIdx.x;
+  if (leaf >= num_leaves) return;
+  const LeafRange r = a.range[leaf];
+  double g = 0.0, h = 0.0;
+  for (int i = threadIdx.x; i < r.count; i += blockDim.x) {
+    const float2 v = gh_true[RowAt(a, r.buf, r.start + i)];
+    g += v.x;
+    h += v.y;
+  }
+  g = WaveSum(g);
+  h = WaveSum(h);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = g;
+    sh[1][w] = h;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tg = 0.0, th = 0.0;
+    for (int k = 0; k < kNodeThreads / 64; ++k) tg += sh[0][k], th += sh[1][k];
+    out[leaf] = make_double2(tg, th);
+  }
 }
 
 // Copy a SplitInfo with one dword per thread (no serial per-thread struct copy).
@@ -1088,6 +1173,11 @@ __device__ void PostSplit(const Args& a, const Ctl& c, int left_count) {
     const int ilc = bi.left_count, irc = bi.right_count;
     const int8_t mono = bi.monotone_type;
     const int16_t ncat = bi.num_cat_threshold;
+    if (a.ic_leaf) {
+      const unsigned long long m = a.ic_leaf[l] & a.ic_feat[bi.feature];
+      a.ic_leaf[l] = m;
+      a.ic_leaf[r] = m;
+    }
     const int dep = a.depth[l] + 1;
     LeafBounds bl = a.bounds[l];
     const int ps = a.slot[l];
@@ -1345,7 +1435,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void Init(const Dataset* train, bool is_constant_hessian) override {
-    (void)is_constant_hessian;
+    is_const_hess_ = is_constant_hessian;
     data_ = train;
     N_ = train->num_data();
     F_ = train->num_features();
@@ -1367,9 +1457,6 @@ class DeviceTreeLearner : public TreeLearner {
     device_name_ = std::string(prop.name[0] ? prop.name : "AMD GPU") + " (" + prop.gcnArchName + ")";
     num_cu_ = prop.multiProcessorCount;
     if (!stream_) HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    if (!config_->interaction_constraints_vector.empty()) {
-      Log::Fatal("interaction_constraints are not supported by the HIP learner yet; use device_type=cpu");
-    }
     if (!config_->forcedsplits_filename.empty()) {
       Log::Fatal("forcedsplits_filename is not supported by the HIP learner yet; use device_type=cpu");
     }
@@ -1607,6 +1694,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (distributed_) gcount = Network::GlobalSyncUpBySum(gcount);
     tp->root_gcount = gcount;
     HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
+    if (config_->use_quantized_grad) QuantizeGradients(class_id);
     col_sampler_.ResetByTree();
     const auto& used = col_sampler_.is_feature_used_bytree();
     uint8_t* um = pin_mask_.Get(static_cast<size_t>(F_) * (1 + 2 * L_));
@@ -1667,6 +1755,7 @@ class DeviceTreeLearner : public TreeLearner {
       }
     }
     h_range_.assign(hrange, hrange + hc->num_leaves);
+    if (config_->use_quantized_grad && config_->quant_train_renew_leaf) RenewQuantizedLeaves(tree.get());
     if (stamps_.size() && ++stamp_trees_ == 3) ReportStamps(hc->num_splits);
     tree->RecomputeMaxDepth();
     return tree;
@@ -1699,6 +1788,95 @@ class DeviceTreeLearner : public TreeLearner {
         std::fprintf(stderr, "stamps %s block %d (%d splits, us from kernel start):%s\n", names[k], b, cnt, line.c_str());
       }
     }
+  }
+
+  void QuantizeGradients(int class_id) {
+    float2* gh = gh_.get() + static_cast<size_t>(class_id) * N_;
+    const bool renew = config_->quant_train_renew_leaf;
+    if (renew && gh_true_.size() < static_cast<size_t>(N_)) gh_true_.Resize(N_);
+    qmax_.Zero(stream_);
+    const int grid = std::max(1, std::min(DivUp(N_, 256), num_cu_ * 4));
+    k_qmax<<<grid, 256, 0, stream_>>>(gh, N_, qmax_.get());
+    HIP_CHECK(hipGetLastError());
+    if (Network::num_machines() > 1) {
+      unsigned* hm = pin_max_.Get(2);
+      qmax_.Download(hm, 2, stream_);
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      float v[2];
+      std::memcpy(v, hm, 8);
+      v[0] = static_cast<float>(Network::GlobalSyncUpByMax(static_cast<double>(v[0])));
+      v[1] = static_cast<float>(Network::GlobalSyncUpByMax(static_cast<double>(v[1])));
+      std::memcpy(hm, v, 8);
+      HIP_CHECK(hipMemcpyAsync(qmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
+    }
+    const uint32_t seed = static_cast<uint32_t>(config_->seed) * 0x9E3779B9u + (quant_round_++);
+    k_quantize<<<grid, 256, 0, stream_>>>(gh, renew ? gh_true_.get() : nullptr, N_, qmax_.get(),
+                                          std::max(2, config_->num_grad_quant_bins), is_const_hess_ ? 1 : 0, seed,
+                                          config_->stochastic_rounding ? 1 : 0);
+    HIP_CHECK(hipGetLastError());
+  }
+
+  void RenewQuantizedLeaves(Tree* tree) {
+    const int nl = tree->num_leaves();
+    const Args args = MakeArgs();
+    k_leaf_true_sums<<<nl, kNodeThreads, 0, stream_>>>(args, gh_true_.get(), nl, true_sums_.get());
+    HIP_CHECK(hipGetLastError());
+    std::vector<double2> st(nl);
+    true_sums_.Download(st.data(), nl, stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    std::vector<double> flat(2 * nl);
+    for (int l = 0; l < nl; ++l) flat[2 * l] = st[l].x, flat[2 * l + 1] = st[l].y;
+    if (distributed_) Network::GlobalSum(&flat);
+    SplitParams p = MakeArgs().sp;
+    p.path_smooth = 0.0;
+    for (int l = 0; l < nl; ++l) {
+      tree->SetLeafOutput(l, LeafOutputRaw(flat[2 * l], flat[2 * l + 1], p, tree->leaf_count(l), 0.0));
+    }
+  }
+
+  // ---- histogram engine for the host learners (HistogramBackend)
+  void BackendSetGradients(const float* g, const float* h, int n) {
+    if (n != N_) Log::Fatal("HistogramBackend: %d gradients for %d rows", n, N_);
+    K_ = 1;
+    if (gh_.size() < static_cast<size_t>(N_)) gh_.Resize(static_cast<size_t>(N_));
+    DeviceSetGradients(g, h, 1);
+    float mg = 0.f, mh = 0.f;
+    for (int i = 0; i < N_; ++i) {
+      mg = std::max(mg, std::fabs(g[i]));
+      mh = std::max(mh, std::fabs(h[i]));
+    }
+    unsigned* hm = pin_max_.Get(2);
+    std::memcpy(&hm[0], &mg, 4);
+    std::memcpy(&hm[1], &mh, 4);
+    HIP_CHECK(hipMemcpyAsync(ghmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  void BackendHistogram(const int* rows, int n, double* out) {
+    // a full row set is order-free for a histogram: skip the index upload
+    const bool all = rows == nullptr || n == N_;
+    if (n == 0) {
+      std::memset(out, 0, sizeof(double) * 2 * static_cast<size_t>(TB_));
+      return;
+    }
+    if (!all) idx_[2].Upload(rows, n, stream_);
+    Ctl* hc = pin_ctl_.Get(1);
+    std::memset(hc, 0, sizeof(Ctl));
+    hc->num_leaves = 1;
+    hc->larger = -1;
+    LeafRange* hr = pin_range_.Get(L_);
+    hr[0].buf = all ? -1 : 2;
+    hr[0].start = 0;
+    hr[0].count = all ? N_ : n;
+    hr[0].pad = 0;
+    HIP_CHECK(hipMemcpyAsync(ctl_.get(), hc, sizeof(Ctl), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(range_.get(), hr, sizeof(LeafRange), hipMemcpyHostToDevice, stream_));
+    staging_.Zero(stream_);
+    const Args args = MakeArgs();
+    LaunchHist(args);
+    if (!distributed_) LaunchHistReduce(args);
+    staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
   // One histogram of (g, h) over `rows` (identity when null) into `out` (2 * TB doubles).
@@ -1911,7 +2089,9 @@ class DeviceTreeLearner : public TreeLearner {
                  o_tcnt = lay.Add<int>(max_tiles_), o_toff = lay.Add<int>(max_tiles_),
                  o_used = lay.Add<uint8_t>(std::max(F_, 1)), o_byn = lay.Add<uint8_t>(use_bynode_ ? 2 * L * F_ : 1),
                  o_rng = lay.Add<unsigned>(std::max(F_, 1)), o_feat = lay.Add<DevFeature>(h_feats_.size()),
-                 o_gst = lay.Add<int>(h_gstart_.size()), o_tiles = lay.Add<HistTile>(h_tiles_.size());
+                 o_gst = lay.Add<int>(h_gstart_.size()), o_tiles = lay.Add<HistTile>(h_tiles_.size()),
+                 o_icf = lay.Add<unsigned long long>(std::max(F_, 1)), o_icl = lay.Add<unsigned long long>(L),
+                 o_qmax = lay.Add<unsigned>(2), o_tsum = lay.Add<double2>(L);
     arena_.Resize(std::max<size_t>(lay.bytes(), size_t(2) << 20));
     char* base = arena_.get();
     tparams_.Attach(reinterpret_cast<TreeParams*>(base + o_tp), 1);
@@ -1936,7 +2116,24 @@ class DeviceTreeLearner : public TreeLearner {
     feat_.Attach(reinterpret_cast<DevFeature*>(base + o_feat), h_feats_.size());
     gstart_.Attach(reinterpret_cast<int*>(base + o_gst), h_gstart_.size());
     tiles_.Attach(reinterpret_cast<HistTile*>(base + o_tiles), h_tiles_.size());
+    ic_feat_.Attach(reinterpret_cast<unsigned long long*>(base + o_icf), std::max(F_, 1));
+    ic_leaf_.Attach(reinterpret_cast<unsigned long long*>(base + o_icl), L);
+    qmax_.Attach(reinterpret_cast<unsigned*>(base + o_qmax), 2);
+    true_sums_.Attach(reinterpret_cast<double2*>(base + o_tsum), L);
     arena_.Zero(stream_);
+    use_ic_ = !config_->interaction_constraints_vector.empty();
+    if (use_ic_) {
+      const auto& sets = config_->interaction_constraints_vector;
+      if (sets.size() > 64) Log::Fatal("The HIP learner holds at most 64 interaction constraint sets");
+      std::vector<unsigned long long> m(std::max(F_, 1), 0ull);
+      for (int f = 0; f < F_; ++f) {
+        const int real = data_->feature(f).real_index;
+        for (size_t k = 0; k < sets.size(); ++k) {
+          if (std::find(sets[k].begin(), sets[k].end(), real) != sets[k].end()) m[f] |= 1ull << k;
+        }
+      }
+      ic_feat_.Upload(m, stream_);
+    }
     feat_.Upload(h_feats_, stream_);
     gstart_.Upload(h_gstart_, stream_);
     tiles_.Upload(h_tiles_, stream_);
@@ -2007,6 +2204,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.distributed = distributed_ ? 1 : 0;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
     a.monotone_penalty = config_->monotone_penalty;
+    a.ic_feat = use_ic_ ? ic_feat_.get() : nullptr;
+    a.ic_leaf = use_ic_ ? ic_leaf_.get() : nullptr;
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;
@@ -2152,6 +2351,12 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<SplitInfo> scan_out_;
   DevBuf<int> tile_cnt_, tile_off_;
   DevBuf<uint8_t> used_bytree_, bynode_;
+  DevBuf<unsigned long long> ic_feat_, ic_leaf_;
+  DevBuf<unsigned> qmax_;
+  DevBuf<double2> true_sums_;
+  DevBuf<float2> gh_true_;
+  bool use_ic_ = false, is_const_hess_ = false;
+  unsigned quant_round_ = 0;
   DevBuf<unsigned> rng_;
   DevBuf<char> tree_buf_;
   // lambdarank tables
@@ -2183,6 +2388,34 @@ std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const
   }
   Log::Fatal("Unknown tree learner type %s", parallel_mode.c_str());
   return nullptr;
+}
+
+namespace {
+class DeviceHistogramBackend final : public HistogramBackend {
+ public:
+  DeviceHistogramBackend(const Config* user, const Dataset* data) {
+    // private config: only the knobs the histogram kernels read
+    cfg_.num_leaves = 2;
+    cfg_.verbosity = user->verbosity;
+    cfg_.gpu_use_dp = user->gpu_use_dp;
+    cfg_.gpu_device_id = user->gpu_device_id;
+    cfg_.device_hist_blocks = user->device_hist_blocks;
+    learner_ = std::make_unique<DeviceTreeLearner>(&cfg_, false);
+    learner_->Init(data, false);
+  }
+  void SetGradients(const float* g, const float* h, int n) override { learner_->BackendSetGradients(g, h, n); }
+  void Histogram(const int* rows, int n, double* out) override { learner_->BackendHistogram(rows, n, out); }
+  std::string DeviceName() const override { return learner_->DeviceName(); }
+
+ private:
+  Config cfg_;
+  std::unique_ptr<DeviceTreeLearner> learner_;
+};
+}  // namespace
+
+std::unique_ptr<HistogramBackend> CreateHistogramBackend(const Config* config, const Dataset* data) {
+  if (DeviceCount() <= 0) Log::Fatal("HIP histogram backend: no AMD GPU visible to HIP");
+  return std::make_unique<DeviceHistogramBackend>(config, data);
 }
 
 void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, const int* rows, int num_rows,

@@ -176,6 +176,7 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian
     if (in) forced_json_.assign((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
     else Log::Warning("Forced splits file %s cannot be opened", config_->forcedsplits_filename.c_str());
   }
+  if (want_device_hist_) hist_backend_ = device::CreateHistogramBackend(config_, train_data);
   Log::Info("Number of data points in the train set: %d, number of used features: %d", num_data_, num_features_);
 }
 
@@ -256,6 +257,10 @@ void SerialTreeLearner::ComputeLeafSums(const data_size_t* idx, data_size_t n, d
 // Row-wise histogram over the packed group bins; group bin 0 (all features at
 // their most-frequent bin) is never accumulated.
 void SerialTreeLearner::BuildHistogram(const data_size_t* idx, data_size_t n, double* hist) const {
+  if (hist_backend_) {
+    hist_backend_->Histogram(idx, n, hist);
+    return;
+  }
   const int tb = train_data_->num_total_bin();
   const int ng = train_data_->num_groups();
   const auto& groups = train_data_->groups();
@@ -397,6 +402,7 @@ std::unique_ptr<Tree> SerialTreeLearner::Train(const score_t* gradients, const s
     gradients_ = qgrad_.data();
     hessians_ = qhess_.data();
   }
+  if (hist_backend_) hist_backend_->SetGradients(gradients_, hessians_, num_data_);
   if (extra_rands_.size() != static_cast<size_t>(num_features_)) {
     extra_rands_.clear();
     for (int f = 0; f < num_features_; ++f) extra_rands_.emplace_back(config_->extra_seed + f);
@@ -729,6 +735,7 @@ int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf) 
   while (!q.empty() && done < config_->num_leaves - 1) {
     auto [node, leaf] = q.front();
     q.pop();
+    if (node->feature < 0 || node->feature >= train_data_->num_total_features()) continue;
     const int inner = train_data_->InnerIndex(node->feature);
     if (inner < 0) continue;
     const FeatureInfo& fi = train_data_->feature(inner);
@@ -747,14 +754,22 @@ int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf) 
     std::vector<double> full(2 * fi.num_bin);
     train_data_->FeatureHistogram(h.data(), inner, sg, sh, full.data());
     const uint32_t thr = train_data_->inner_mapper(inner).ValueToBin(node->threshold);
-    double lg = 0, lh = 0;
-    data_size_t lc = 0;
-    const double cf = ls.count / (sh + 2 * kEpsilon);
-    for (uint32_t b = 0; b <= thr && b < static_cast<uint32_t>(fi.num_bin); ++b) {
-      lg += full[2 * b];
-      lh += full[2 * b + 1];
-      lc += RoundCount(full[2 * b + 1] * cf);
+    // GatherInfoForThresholdNumerical (feature_histogram.hpp:486-588): the right side
+    // sums bins above the threshold, skipping the zero bin (MissingType::Zero) and
+    // the NaN bin (MissingType::NaN); missing values go left
+    const bool na = fi.missing == MissingType::NaN, zero = fi.missing == MissingType::Zero;
+    double rg = 0.0, rh = 0.0;
+    data_size_t rc = 0;
+    const double cf = ls.count / sh;
+    for (int b = fi.num_bin - 1 - (na ? 1 : 0); b >= 1; --b) {
+      if (static_cast<uint32_t>(b) <= thr) break;
+      if (zero && b == static_cast<int>(fi.default_bin)) continue;
+      rg += full[2 * b];
+      rh += full[2 * b + 1];
+      rc += RoundCount(full[2 * b + 1] * cf);
     }
+    const double lg = sg - rg, lh = sh - rh;
+    const data_size_t lc = ls.count - rc;
     SplitParams p = MakeParams();
     SplitInfo info;
     info.Reset();
@@ -763,12 +778,18 @@ int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf) 
     info.default_left = 1;
     info.left_sum_gradient = lg;
     info.left_sum_hessian = lh;
-    info.right_sum_gradient = sg - lg;
-    info.right_sum_hessian = sh - lh;
+    info.right_sum_gradient = rg;
+    info.right_sum_hessian = rh;
+    info.left_count = lc;
+    info.right_count = rc;
     info.left_output = LeafOutputRaw(lg, lh, p, lc, ls.output);
-    info.right_output = LeafOutputRaw(sg - lg, sh - lh, p, ls.count - lc, ls.output);
-    info.gain = SplitGain(lg, lh, sg - lg, sh - lh, p, 0, lc, ls.count - lc, ls.output, LeafBounds()) -
+    info.right_output = LeafOutputRaw(rg, rh, p, rc, ls.output);
+    info.gain = SplitGain(lg, lh, rg, rh, p, 0, lc, rc, ls.output, LeafBounds()) -
                 LeafGain(sg, sh, p, ls.count, ls.output) - config_->min_gain_to_split;
+    if (!(info.gain > 0.0)) {
+      Log::Warning("'Forced Split' will be ignored since the gain getting worse.");
+      break;
+    }
     best_split_per_leaf_[leaf] = info;
     Split(tree, leaf, left_leaf, right_leaf);
     ++done;
@@ -869,6 +890,10 @@ void SerialTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj
     for (int l = 0; l < nl; ++l) outs[l] = nonzero[l] > 0 ? outs[l] / nonzero[l] : 0.0;
   }
   for (int l = 0; l < nl; ++l) tree->SetLeafOutput(l, outs[l]);
+}
+
+std::string SerialTreeLearner::DeviceName() const {
+  return hist_backend_ ? hist_backend_->DeviceName() + " (HIP histograms, host split policy)" : "cpu";
 }
 
 std::vector<data_size_t> SerialTreeLearner::LeafIndices(int leaf) const {

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "leaf_constraints.h"
+#include "lgap/device_api.h"
 #include "lgap/random.h"
 #include "lgap/split_math.h"
 #include "lgap/tree_learner.h"
@@ -82,6 +83,9 @@ class SerialTreeLearner : public TreeLearner {
   void RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj, const double* score, data_size_t total_num_data,
                        const data_size_t* bag_indices, data_size_t bag_cnt) const override;
   std::vector<data_size_t> LeafIndices(int leaf) const override;
+  std::string DeviceName() const override;
+  // device_type=gpu with a host split policy: histograms are built by the HIP kernels
+  void EnableDeviceHistograms() { want_device_hist_ = true; }
 
  protected:
   // ---- hooks for the parallel learners
@@ -140,6 +144,8 @@ class SerialTreeLearner : public TreeLearner {
   std::vector<score_t> qgrad_, qhess_;
   const score_t* true_gradients_ = nullptr;
   const score_t* true_hessians_ = nullptr;
+  std::unique_ptr<device::HistogramBackend> hist_backend_;
+  bool want_device_hist_ = false;
   std::string forced_json_;
   std::vector<Random> extra_rands_;
   // parallel learners

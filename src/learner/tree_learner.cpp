@@ -1,6 +1,9 @@
 // TreeLearner factory (reference src/treelearner/tree_learner.cpp:15-57).
-// device_type=cpu -> host learners; device_type=gpu|cuda -> the HIP learner
-// (fails loudly when no MI355X is visible: no silent CPU fallback).
+// device_type=cpu -> host learners. device_type=gpu|cuda -> the device-resident
+// HIP learner, or — when a split policy only the host learners implement is
+// requested — the host learner of that type with HIP histograms (the
+// reference's GPUTreeLearner arrangement). Fails loudly when no MI355X is
+// visible: no silent CPU fallback.
 #include "lgap/tree_learner.h"
 
 #include "lgap/device_api.h"
@@ -10,22 +13,52 @@
 
 namespace lgap {
 
-std::unique_ptr<TreeLearner> TreeLearner::Create(const std::string& learner_type, const std::string& device_type,
-                                                 bool linear_tree, const Config* config) {
-  if (device_type == "gpu" || device_type == "cuda") {
-    if (device::DeviceCount() <= 0) {
-      Log::Fatal("device_type=%s requested but no AMD GPU (gfx950) is visible to HIP", device_type.c_str());
-    }
-    if (linear_tree) Log::Fatal("linear_tree is not supported by the HIP learner yet; use device_type=cpu");
-    return device::CreateDeviceTreeLearner(config, learner_type);
-  }
-  if (device_type != "cpu") Log::Fatal("Unknown device type %s", device_type.c_str());
+namespace {
+
+std::unique_ptr<TreeLearner> CreateHost(const std::string& learner_type, bool linear_tree, const Config* config) {
   if (linear_tree) return CreateLinearTreeLearner(config);
   if (learner_type == "serial") return std::make_unique<SerialTreeLearner>(config);
   if (learner_type == "feature") return std::make_unique<FeatureParallelTreeLearner>(config);
   if (learner_type == "data") return std::make_unique<DataParallelTreeLearner>(config);
   if (learner_type == "voting") return std::make_unique<VotingParallelTreeLearner>(config);
   Log::Fatal("Unknown tree learner type %s", learner_type.c_str());
+  return nullptr;
+}
+
+// Why the device-resident learner cannot serve `config` (nullptr = it can).
+const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, const Config* c) {
+  if (linear_tree) return "linear_tree";
+  if (learner_type == "voting") return "voting-parallel election";
+  if (learner_type == "feature") return "feature-parallel ownership";
+  if (CegbPenalty::Enabled(c)) return "cost-effective gradient boosting";
+  if (!c->forcedsplits_filename.empty()) return "forced splits";
+  if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {
+    return "intermediate/advanced monotone constraints";
+  }
+  if (!c->interaction_constraints_vector.empty() &&
+      (c->feature_fraction_bynode < 1.0 || c->interaction_constraints_vector.size() > 64)) {
+    return "interaction constraints with by-node sampling / more than 64 sets";
+  }
+  return nullptr;
+}
+
+}  // namespace
+
+std::unique_ptr<TreeLearner> TreeLearner::Create(const std::string& learner_type, const std::string& device_type,
+                                                 bool linear_tree, const Config* config) {
+  if (device_type == "gpu" || device_type == "cuda") {
+    if (device::DeviceCount() <= 0) {
+      Log::Fatal("device_type=%s requested but no AMD GPU (gfx950) is visible to HIP", device_type.c_str());
+    }
+    const char* why = HostPolicyReason(learner_type, linear_tree, config);
+    if (why == nullptr) return device::CreateDeviceTreeLearner(config, learner_type);
+    Log::Info("%s: host split policy over HIP histograms", why);
+    auto learner = CreateHost(learner_type, linear_tree, config);
+    static_cast<SerialTreeLearner*>(learner.get())->EnableDeviceHistograms();
+    return learner;
+  }
+  if (device_type != "cpu") Log::Fatal("Unknown device type %s", device_type.c_str());
+  return CreateHost(learner_type, linear_tree, config);
 }
 
 }  // namespace lgap

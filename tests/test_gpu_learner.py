@@ -158,3 +158,87 @@ def test_rccl_data_parallel_path_single_rank(lgb, gpu_required):
     assert res["num_trees"] == [8, 8]
     assert res["root_features_equal"]
     assert res["max_abs_diff"] < 1e-3, res
+
+
+def _policy_data(rng, n=20000):
+    X = rng.standard_normal((n, 6))
+    z = 1.5 * X[:, 0] - X[:, 1] + 0.7 * X[:, 2] * X[:, 3] + 0.3 * rng.standard_normal(n)
+    return X, z
+
+
+@pytest.mark.parametrize("extra", [{"interaction_constraints": [[0, 1], [1, 2, 3]]},
+                                   {"interaction_constraints": [[0], [2, 3, 4], [1, 5]], "num_leaves": 15}])
+def test_device_interaction_constraints(lgb, gpu_required, rng, extra):
+    """Device-resident interaction constraints (per-leaf set masks) against the CPU learner."""
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    bc = _train(lgb, X, y, "cpu", rounds=5, **extra)
+    bg = _train(lgb, X, y, "gpu", rounds=5, gpu_use_dp=True, **extra)
+    assert "host split policy" not in bg.device_name()
+    sets = [set(c) for c in extra["interaction_constraints"]]
+
+    def paths(n, acc):
+        if "split_index" in n:
+            f = n["split_feature"]
+            yield from paths(n["left_child"], acc | {f})
+            yield from paths(n["right_child"], acc | {f})
+        else:
+            yield acc
+    for t in _trees(bg):
+        for feats in paths(t["tree_structure"], set()):
+            assert any(feats <= s for s in sets), feats
+    tc, tg = _trees(bc)[0], _trees(bg)[0]
+    assert [s[:2] for s in _splits(tc["tree_structure"], [])][:3] == [s[:2] for s in _splits(tg["tree_structure"], [])][:3]
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=0, atol=5e-2)
+
+
+@pytest.mark.parametrize("renew", [False, True])
+def test_device_quantized_training(lgb, gpu_required, rng, renew):
+    """use_quantized_grad on the device-resident learner: integer-level gradients through the
+    fixed-point histograms; accuracy tracks the full-precision model."""
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    q = {"use_quantized_grad": True, "num_grad_quant_bins": 4, "quant_train_renew_leaf": renew}
+    full = _train(lgb, X, y, "gpu", rounds=30)
+    bq = _train(lgb, X, y, "gpu", rounds=30, **q)
+    bq_cpu = _train(lgb, X, y, "cpu", rounds=30, **q)
+    a_full, a_q, a_qc = _auc(y, full.predict(X)), _auc(y, bq.predict(X)), _auc(y, bq_cpu.predict(X))
+    assert a_q > a_full - 0.01, (a_q, a_full)
+    assert abs(a_q - a_qc) < 0.01, (a_q, a_qc)
+    # deterministic rounding: the first split matches the host quantizer
+    d = dict(q, stochastic_rounding=False)
+    tc = _trees(_train(lgb, X, y, "cpu", rounds=1, **d))[0]["tree_structure"]
+    tg = _trees(_train(lgb, X, y, "gpu", rounds=1, gpu_use_dp=True, **d))[0]["tree_structure"]
+    assert (tc["split_feature"], tc["threshold"]) == (tg["split_feature"], tg["threshold"])
+
+
+@pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05, "cegb_penalty_feature_coupled": [1, 2, 3, 4, 5, 6]},
+                                   {"monotone_constraints": [1, -1, 0, 0, 0, 0],
+                                    "monotone_constraints_method": "intermediate"},
+                                   {"linear_tree": True, "objective": "regression"}])
+def test_host_policy_over_device_histograms(lgb, gpu_required, rng, extra):
+    """Options only the host learners implement run the host split policy over HIP histograms
+    (the reference's GPUTreeLearner arrangement); the model matches the CPU learner."""
+    X, z = _policy_data(rng)
+    y = z if extra.get("objective") == "regression" else (z > 0).astype(float)
+    bc = _train(lgb, X, y, "cpu", rounds=4, **extra)
+    bg = _train(lgb, X, y, "gpu", rounds=4, gpu_use_dp=True, **extra)
+    assert "host split policy" in bg.device_name()
+    tc, tg = _trees(bc)[0], _trees(bg)[0]
+    assert [s[:2] for s in _splits(tc["tree_structure"], [])][:4] == [s[:2] for s in _splits(tg["tree_structure"], [])][:4]
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
+
+
+def test_forced_splits_over_device_histograms(lgb, gpu_required, rng, tmp_path):
+    import json
+
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    f = tmp_path / "forced.json"
+    f.write_text(json.dumps({"feature": 4, "threshold": 0.1, "left": {"feature": 5, "threshold": -0.2}}))
+    bc = _train(lgb, X, y, "cpu", rounds=2, forcedsplits_filename=str(f))
+    bg = _train(lgb, X, y, "gpu", rounds=2, gpu_use_dp=True, forcedsplits_filename=str(f))
+    for b in (bc, bg):
+        root = _trees(b)[0]["tree_structure"]
+        assert root["split_feature"] == 4 and root["left_child"]["split_feature"] == 5
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
