@@ -186,6 +186,76 @@ LIGHTGBM_C_EXPORT int LGBM_NetworkInitWithFunctions(int num_machines, int rank, 
 LIGHTGBM_C_EXPORT int LGBM_SetMaxThreads(int num_threads);
 LIGHTGBM_C_EXPORT int LGBM_GetMaxThreads(int* out);
 
+/* ---- Arrow C data interface (struct ArrowArray / ArrowSchema, see lgap/arrow.h) */
+struct ArrowArray;
+struct ArrowSchema;
+typedef void* ByteBufferHandle;
+#define C_API_MATRIX_TYPE_CSR (0)
+#define C_API_MATRIX_TYPE_CSC (1)
+LIGHTGBM_C_EXPORT int LGBM_DatasetCreateFromArrow(int64_t n_chunks, const struct ArrowArray* chunks,
+                                                  const struct ArrowSchema* schema, const char* parameters,
+                                                  const DatasetHandle reference, DatasetHandle* out);
+LIGHTGBM_C_EXPORT int LGBM_DatasetSetFieldFromArrow(DatasetHandle handle, const char* field_name, int64_t n_chunks,
+                                                    const struct ArrowArray* chunks, const struct ArrowSchema* schema);
+LIGHTGBM_C_EXPORT int LGBM_BoosterPredictForArrow(BoosterHandle handle, int64_t n_chunks,
+                                                  const struct ArrowArray* chunks, const struct ArrowSchema* schema,
+                                                  int predict_type, int start_iteration, int num_iteration,
+                                                  const char* parameter, int64_t* out_len, double* out_result);
+
+/* ---- more dataset constructors */
+// get_row_funptr: std::function<void(int idx, std::vector<std::pair<int, double>>& row)>*
+LIGHTGBM_C_EXPORT int LGBM_DatasetCreateFromCSRFunc(void* get_row_funptr, int num_rows, int64_t num_col,
+                                                    const char* parameters, const DatasetHandle reference,
+                                                    DatasetHandle* out);
+LIGHTGBM_C_EXPORT int LGBM_DatasetCreateFromSampledColumn(double** sample_data, int** sample_indices, int32_t ncol,
+                                                          const int* num_per_col, int32_t num_sample_row,
+                                                          int32_t num_local_row, int64_t num_dist_row,
+                                                          const char* parameters, DatasetHandle* out);
+LIGHTGBM_C_EXPORT int LGBM_DatasetPushRowsByCSRWithMetadata(DatasetHandle dataset, const void* indptr,
+                                                            int indptr_type, const int32_t* indices, const void* data,
+                                                            int data_type, int64_t nindptr, int64_t nelem,
+                                                            int64_t start_row, const float* label, const float* weight,
+                                                            const double* init_score, const int32_t* query,
+                                                            int32_t tid);
+LIGHTGBM_C_EXPORT int LGBM_DatasetSerializeReferenceToBinary(DatasetHandle handle, ByteBufferHandle* out,
+                                                             int32_t* out_len);
+LIGHTGBM_C_EXPORT int LGBM_DatasetCreateFromSerializedReference(const void* ref_buffer, int32_t ref_buffer_size,
+                                                                int64_t num_row, int32_t num_classes,
+                                                                const char* parameters, DatasetHandle* out);
+LIGHTGBM_C_EXPORT int LGBM_ByteBufferGetAt(ByteBufferHandle handle, int32_t index, uint8_t* out_val);
+LIGHTGBM_C_EXPORT int LGBM_ByteBufferFree(ByteBufferHandle handle);
+
+/* ---- single-row fast prediction (config parsed once) */
+LIGHTGBM_C_EXPORT int LGBM_BoosterPredictForMatSingleRowFastInit(BoosterHandle handle, const int predict_type,
+                                                                 const int start_iteration, const int num_iteration,
+                                                                 const int data_type, const int32_t ncol,
+                                                                 const char* parameter,
+                                                                 FastConfigHandle* out_fastConfig);
+LIGHTGBM_C_EXPORT int LGBM_BoosterPredictForMatSingleRowFast(FastConfigHandle fastConfig_handle, const void* data,
+                                                             int64_t* out_len, double* out_result);
+LIGHTGBM_C_EXPORT int LGBM_BoosterPredictForCSRSingleRowFastInit(BoosterHandle handle, const int predict_type,
+                                                                 const int start_iteration, const int num_iteration,
+                                                                 const int data_type, const int64_t num_col,
+                                                                 const char* parameter,
+                                                                 FastConfigHandle* out_fastConfig);
+LIGHTGBM_C_EXPORT int LGBM_BoosterPredictForCSRSingleRowFast(FastConfigHandle fastConfig_handle, const void* indptr,
+                                                             const int indptr_type, const int32_t* indices,
+                                                             const void* data, const int64_t nindptr,
+                                                             const int64_t nelem, int64_t* out_len,
+                                                             double* out_result);
+LIGHTGBM_C_EXPORT int LGBM_FastConfigFree(FastConfigHandle fastConfig);
+
+/* ---- sparse SHAP output */
+LIGHTGBM_C_EXPORT int LGBM_BoosterPredictSparseOutput(BoosterHandle handle, const void* indptr, int indptr_type,
+                                                      const int32_t* indices, const void* data, int data_type,
+                                                      int64_t nindptr, int64_t nelem, int64_t num_col_or_row,
+                                                      int predict_type, int start_iteration, int num_iteration,
+                                                      const char* parameter, int matrix_type, int64_t* out_len,
+                                                      void** out_indptr, int32_t** out_indices, void** out_data);
+LIGHTGBM_C_EXPORT int LGBM_BoosterFreePredictSparse(void* indptr, int32_t* indices, void* data, int indptr_type,
+                                                    int data_type);
+LIGHTGBM_C_EXPORT void LGBM_SetLastError(const char* msg);
+
 /* ---- MI355X device helpers (LambdaGap extension) */
 LIGHTGBM_C_EXPORT int LGBM_DeviceCount(int* out);
 // Waits for all queued device work of this process (timing brackets).

@@ -32,6 +32,10 @@ class Metadata {
   void SetQueryBoundaries(const std::vector<data_size_t>& b);
   void SetPosition(const int32_t* pos, data_size_t len);
   void Subset(const Metadata& src, const data_size_t* idx, data_size_t n);
+  // streaming pushes: rows [start, start + n) (query = per-row query ids; boundaries are
+  // derived once the last row has arrived)
+  void SetRows(data_size_t start, data_size_t n, const float* label, const float* weight, const double* init_score,
+               const int32_t* query);
 
   data_size_t num_data() const { return num_data_; }
   const label_t* label() const { return label_.data(); }
@@ -55,6 +59,7 @@ class Metadata {
 
  private:
   void CalcQueryWeights();
+  std::vector<int32_t> pending_query_ids_;
   data_size_t num_data_ = 0;
   std::vector<label_t> label_;
   std::vector<label_t> weights_;
@@ -109,6 +114,9 @@ class Dataset {
 
   void SaveBinary(const std::string& filename) const;
   static std::unique_ptr<Dataset> LoadBinary(const std::string& filename);
+  // in-memory form of the binary file (LGBM_DatasetSerializeReferenceToBinary)
+  void SerializeBinary(std::vector<char>* out) const;
+  static std::unique_ptr<Dataset> DeserializeBinary(const char* data, size_t size);
   static bool IsBinaryFile(const std::string& filename);
 
   data_size_t num_data() const { return num_data_; }

@@ -213,6 +213,71 @@ def _is_sparse(x: Any) -> bool:
     return sp is not None and sp.issparse(x)
 
 
+class _ArrowSchema(ctypes.Structure):
+    _fields_ = [("format", ctypes.c_char_p), ("name", ctypes.c_char_p), ("metadata", ctypes.c_char_p),
+                ("flags", ctypes.c_int64), ("n_children", ctypes.c_int64), ("children", ctypes.c_void_p),
+                ("dictionary", ctypes.c_void_p), ("release", ctypes.c_void_p), ("private_data", ctypes.c_void_p)]
+
+
+class _ArrowArray(ctypes.Structure):
+    _fields_ = [("length", ctypes.c_int64), ("null_count", ctypes.c_int64), ("offset", ctypes.c_int64),
+                ("n_buffers", ctypes.c_int64), ("n_children", ctypes.c_int64), ("buffers", ctypes.c_void_p),
+                ("children", ctypes.c_void_p), ("dictionary", ctypes.c_void_p), ("release", ctypes.c_void_p),
+                ("private_data", ctypes.c_void_p)]
+
+
+_ARROW_RELEASE = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
+def _is_arrow(x: Any) -> bool:
+    mod = type(x).__module__ or ""
+    if not mod.startswith("pyarrow"):
+        return False
+    import pyarrow as pa
+
+    return isinstance(x, (pa.Table, pa.RecordBatch, pa.Array, pa.ChunkedArray))
+
+
+class _ArrowExport:
+    """Exports a pyarrow Table / RecordBatch / (Chunked)Array through the Arrow C data
+    interface for the native reader (lgap/arrow.h); releases the exported structs on exit."""
+
+    def __init__(self, obj: Any) -> None:
+        import pyarrow as pa
+
+        if isinstance(obj, pa.Table):
+            parts, schema_src = obj.to_batches(), obj.schema
+        elif isinstance(obj, pa.RecordBatch):
+            parts, schema_src = [obj], obj.schema
+        elif isinstance(obj, pa.ChunkedArray):
+            parts, schema_src = list(obj.chunks), obj.type
+        elif isinstance(obj, pa.Array):
+            parts, schema_src = [obj], obj.type
+        else:
+            raise TypeError(f"Unsupported Arrow object {type(obj).__name__}")
+        self.n = len(parts)
+        self.chunks = (_ArrowArray * max(1, self.n))()
+        self.schema = _ArrowSchema()
+        schema_src._export_to_c(ctypes.addressof(self.schema))
+        for i, part in enumerate(parts):
+            tmp = _ArrowSchema()
+            part._export_to_c(ctypes.addressof(self.chunks[i]), ctypes.addressof(tmp))
+            _ArrowExport._release(tmp)
+
+    @staticmethod
+    def _release(struct: ctypes.Structure) -> None:
+        if struct.release:
+            _ARROW_RELEASE(struct.release)(ctypes.addressof(struct))
+
+    def __enter__(self) -> "_ArrowExport":
+        return self
+
+    def __exit__(self, *exc: Any) -> None:
+        for i in range(self.n):
+            _ArrowExport._release(self.chunks[i])
+        _ArrowExport._release(self.schema)
+
+
 def _is_pandas(x: Any) -> bool:
     return pd is not None and isinstance(x, pd.DataFrame)
 
@@ -325,7 +390,13 @@ class Dataset:
         if self.feature_name != "auto" and self.feature_name is not None:
             feature_names = list(self.feature_name)
         out = ctypes.c_void_p()
-        if _is_path(data):
+        if _is_arrow(data):
+            names = list(data.schema.names) if hasattr(data, "schema") else None
+            cat_idx = self._resolve_categorical(feature_names or names, len(names or []))
+            with _ArrowExport(data) as ex:
+                _check(_LIB.LGBM_DatasetCreateFromArrow(ctypes.c_int64(ex.n), ex.chunks, ctypes.byref(ex.schema),
+                                                        _c_str(self._build_params(cat_idx)), ref, ctypes.byref(out)))
+        elif _is_path(data):
             cat_idx = self._resolve_categorical(feature_names, -1)
             _check(_LIB.LGBM_DatasetCreateFromFile(_c_str(str(data)), _c_str(self._build_params(cat_idx)), ref,
                                                    ctypes.byref(out)))
@@ -433,6 +504,12 @@ class Dataset:
         if data is None:
             _check(_LIB.LGBM_DatasetSetField(self.handle, _c_str(field_name), None, ctypes.c_int(0),
                                              ctypes.c_int(C_API_DTYPE_FLOAT32)))
+            return self
+        if _is_arrow(data):
+            with _ArrowExport(data) as ex:
+                _check(_LIB.LGBM_DatasetSetFieldFromArrow(self.handle, _c_str(field_name), ctypes.c_int64(ex.n),
+                                                          ex.chunks, ctypes.byref(ex.schema)))
+            self.version += 1
             return self
         dtype = _FIELD_TYPES.get(field_name, np.float32)
         if field_name == "init_score":
@@ -917,6 +994,23 @@ class Booster:
             return res[:, 0] if res.shape[1] == 1 else res
         if _is_pandas(data):
             data = _pandas_to_numpy(data, "auto", self.pandas_categorical)[0]
+        if _is_arrow(data):
+            nrow = data.num_rows
+            n_pred = ctypes.c_int64(0)
+            _check(_LIB.LGBM_BoosterCalcNumPredict(self.handle, ctypes.c_int(nrow), ctypes.c_int(ptype),
+                                                   ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
+                                                   ctypes.byref(n_pred)))
+            out = np.empty(n_pred.value, dtype=np.float64)
+            out_len = ctypes.c_int64(0)
+            with _ArrowExport(data) as ex:
+                _check(_LIB.LGBM_BoosterPredictForArrow(self.handle, ctypes.c_int64(ex.n), ex.chunks,
+                                                        ctypes.byref(ex.schema), ctypes.c_int(ptype),
+                                                        ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
+                                                        params, ctypes.byref(out_len),
+                                                        out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+            return self._shape_pred(out, nrow, ptype)
+        if _is_sparse(data) and pred_contrib:
+            return self._predict_sparse_contrib(data, start_iteration, num_iteration, params)
         if _is_sparse(data):
             return self._predict_sparse(data, ptype, start_iteration, num_iteration, params)
         mat, dtype = _to_float_matrix(data if not isinstance(data, list) else np.asarray(data))
@@ -954,6 +1048,49 @@ class Booster:
                                               ctypes.c_int(start_iteration), ctypes.c_int(num_iteration), params,
                                               ctypes.byref(out_len), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
         return self._shape_pred(out, nrow, ptype)
+
+    def _predict_sparse_contrib(self, data, start_iteration, num_iteration, params):
+        """SHAP values of sparse input as sparse matrices (one per class when multiclass),
+        in the input's format (reference basic.py __inner_predict_sparse_csr/csc)."""
+        is_csc = data.format == "csc"
+        mat = data if data.format in ("csr", "csc") else data.tocsr()
+        indptr, ip_type = Dataset._indptr(mat.indptr)
+        vals, vtype = Dataset._values(mat.data)
+        indices = np.ascontiguousarray(mat.indices, dtype=np.int32)
+        out_len = (ctypes.c_int64 * 2)()
+        out_ptr, out_idx, out_data = ctypes.c_void_p(), ctypes.POINTER(ctypes.c_int32)(), ctypes.c_void_p()
+        other = mat.shape[0] if is_csc else mat.shape[1]
+        _check(_LIB.LGBM_BoosterPredictSparseOutput(
+            self.handle, indptr.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(ip_type),
+            indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), vals.ctypes.data_as(ctypes.c_void_p),
+            ctypes.c_int(vtype), ctypes.c_int64(indptr.size), ctypes.c_int64(vals.size), ctypes.c_int64(other),
+            ctypes.c_int(C_API_PREDICT_CONTRIB), ctypes.c_int(start_iteration), ctypes.c_int(num_iteration), params,
+            ctypes.c_int(1 if is_csc else 0), out_len, ctypes.byref(out_ptr), ctypes.byref(out_idx),
+            ctypes.byref(out_data)))
+        try:
+            nnz, nptr = out_len[0], out_len[1]
+            pt = ctypes.c_int32 if ip_type == C_API_DTYPE_INT32 else ctypes.c_int64
+            dt = ctypes.c_float if vtype == C_API_DTYPE_FLOAT32 else ctypes.c_double
+            ptr = np.ctypeslib.as_array(ctypes.cast(out_ptr, ctypes.POINTER(pt)), shape=(nptr,)).copy()
+            idx = np.ctypeslib.as_array(out_idx, shape=(max(nnz, 1),))[:nnz].copy()
+            val = np.ctypeslib.as_array(ctypes.cast(out_data, ctypes.POINTER(dt)), shape=(max(nnz, 1),))[:nnz].copy()
+        finally:
+            _check(_LIB.LGBM_BoosterFreePredictSparse(out_ptr, out_idx, out_data, ctypes.c_int(ip_type),
+                                                      ctypes.c_int(vtype)))
+        k = self.num_model_per_iteration()
+        nrow = mat.shape[0]
+        width = self.num_feature() + 1
+        outer = width if is_csc else nrow
+        shape = (nrow, width)
+        mats, off = [], 0
+        for c in range(k):
+            p = ptr[c * (outer + 1):(c + 1) * (outer + 1)]
+            n = int(p[-1])
+            seg_i, seg_v = idx[off:off + n], val[off:off + n]
+            off += n
+            mats.append(sp.csc_matrix((seg_v, seg_i, p), shape=shape) if is_csc else
+                        sp.csr_matrix((seg_v, seg_i, p), shape=shape))
+        return mats[0] if k == 1 else mats
 
     def _shape_pred(self, out: np.ndarray, nrow: int, ptype: int) -> np.ndarray:
         if nrow == 0:

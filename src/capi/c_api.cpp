@@ -6,6 +6,7 @@
 #include <omp.h>
 
 #include <cstring>
+#include <functional>
 #include <fstream>
 #include <memory>
 #include <mutex>
@@ -14,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "lgap/arrow.h"
 #include "lgap/boosting.h"
 #include "lgap/common.h"
 #include "lgap/config.h"
@@ -370,20 +372,7 @@ int LGBM_DatasetPushRowsWithMetadata(DatasetHandle dataset, const void* data, in
   DenseSource src(data, data_type == C_API_DTYPE_FLOAT64, nrow, ncol, true);
   Dataset* ds = D(dataset)->ds.get();
   ds->PushRows(src, start_row);
-  auto& md = ds->metadata();
-  std::vector<float> l(md.label(), md.label() + md.num_data());
-  if (label) {
-    std::copy(label, label + nrow, l.begin() + start_row);
-    md.SetLabel(l.data(), md.num_data());
-  }
-  if (weight) {
-    std::vector<float> w = md.weights_vec();
-    if (w.empty()) w.assign(md.num_data(), 1.0f);
-    std::copy(weight, weight + nrow, w.begin() + start_row);
-    md.SetWeights(w.data(), md.num_data());
-  }
-  (void)init_score;
-  (void)query;
+  ds->metadata().SetRows(start_row, nrow, label, weight, init_score, query);
   API_END();
 }
 
@@ -1104,5 +1093,342 @@ int LGBM_DeviceCommInit(const char* unique_id, int64_t id_len, int num_ranks, in
 int LGBM_DeviceCommFree() {
   API_BEGIN();
   device::CommFree();
+  API_END();
+}
+
+// ============================================================================
+// Arrow, streaming / sampled constructors, serialized references, fast
+// single-row and sparse-output prediction (reference src/c_api.cpp:1245-2960).
+namespace {
+
+class FuncSource : public RowSource {
+ public:
+  using RowFn = std::function<void(int idx, std::vector<std::pair<int, double>>& row)>;
+  FuncSource(RowFn* fn, int nrow, int ncol) : fn_(fn), nrow_(nrow), ncol_(ncol) {}
+  data_size_t num_rows() const override { return nrow_; }
+  int num_cols() const override { return ncol_; }
+  void GetRow(data_size_t i, std::vector<std::pair<int, double>>* out) const override {
+    out->clear();
+    (*fn_)(static_cast<int>(i), *out);
+  }
+
+ private:
+  RowFn* fn_;
+  int nrow_, ncol_;
+};
+
+struct FastConfig {
+  Booster* booster;
+  int predict_type, start_iteration, num_iteration, data_type;
+  int64_t ncol;
+  Config config;
+  std::unique_ptr<PredictionEarlyStop> es;
+};
+
+// One row through the booster without OpenMP or config parsing.
+void PredictOneRow(FastConfig* fc, const std::vector<std::pair<int, double>>& row, int64_t* out_len, double* out) {
+  Booster* b = fc->booster;
+  std::shared_lock<std::shared_mutex> lk(b->mu_);
+  GBDT* g = b->boosting_.get();
+  const bool leaf = fc->predict_type == C_API_PREDICT_LEAF_INDEX;
+  const bool contrib = fc->predict_type == C_API_PREDICT_CONTRIB;
+  g->InitPredict(fc->start_iteration, fc->num_iteration, contrib);
+  const int nf = std::max<int64_t>(g->MaxFeatureIdx() + 1, fc->ncol);
+  thread_local std::vector<double> x;
+  x.assign(nf, 0.0);
+  for (auto& kv : row) if (kv.first < nf) x[kv.first] = kv.second;
+  if (leaf) g->PredictLeafIndex(x.data(), out);
+  else if (contrib) g->PredictContrib(x.data(), out);
+  else if (fc->predict_type == C_API_PREDICT_RAW_SCORE) g->PredictRaw(x.data(), out, fc->es.get());
+  else g->Predict(x.data(), out, fc->es.get());
+  *out_len = g->NumPredictOneRow(fc->start_iteration, fc->num_iteration, leaf, contrib);
+}
+
+FastConfig* MakeFast(BoosterHandle handle, int predict_type, int start_iteration, int num_iteration, int data_type,
+                     int64_t ncol, const char* parameter) {
+  auto fc = std::make_unique<FastConfig>();
+  fc->booster = B(handle);
+  fc->predict_type = predict_type;
+  fc->start_iteration = start_iteration;
+  fc->num_iteration = num_iteration;
+  fc->data_type = data_type;
+  fc->ncol = ncol;
+  fc->config = ParseConfig(parameter);
+  std::string es_type = "none";
+  const GBDT* g = fc->booster->boosting_.get();
+  if (fc->config.pred_early_stop && predict_type != C_API_PREDICT_LEAF_INDEX && predict_type != C_API_PREDICT_CONTRIB &&
+      g->objective()) {
+    const std::string name = g->objective()->GetName();
+    if (name == "binary") es_type = "binary";
+    else if (name.find("multiclass") == 0) es_type = "multiclass";
+  }
+  fc->es = std::make_unique<PredictionEarlyStop>(es_type, fc->config.pred_early_stop_freq,
+                                                 fc->config.pred_early_stop_margin);
+  return fc.release();
+}
+
+struct ByteBuffer {
+  std::vector<char> data;
+};
+
+}  // namespace
+
+void LGBM_SetLastError(const char* msg) { SetLastError(msg); }
+
+int LGBM_DatasetCreateFromArrow(int64_t n_chunks, const struct ArrowArray* chunks, const struct ArrowSchema* schema,
+                                const char* parameters, const DatasetHandle reference, DatasetHandle* out) {
+  API_BEGIN();
+  ArrowTable table(n_chunks, chunks, schema);
+  ArrowSource src(table);
+  *out = BuildFromSource(src, parameters, reference);
+  D(*out)->ds->set_feature_names(table.names());
+  API_END();
+}
+
+int LGBM_DatasetSetFieldFromArrow(DatasetHandle handle, const char* field_name, int64_t n_chunks,
+                                  const struct ArrowArray* chunks, const struct ArrowSchema* schema) {
+  API_BEGIN();
+  ArrowTable table(n_chunks, chunks, schema);
+  if (table.num_columns() != 1) Log::Fatal("Arrow field %s must have exactly one column", field_name);
+  const std::vector<double> v = table.Column(0);
+  const std::string name(field_name);
+  if (name == "group" || name == "query" || name == "position") {
+    std::vector<int32_t> iv(v.begin(), v.end());
+    if (LGBM_DatasetSetField(handle, field_name, iv.data(), static_cast<int>(iv.size()), C_API_DTYPE_INT32) != 0) {
+      throw std::runtime_error(LGBM_GetLastError());
+    }
+  } else if (LGBM_DatasetSetField(handle, field_name, v.data(), static_cast<int>(v.size()), C_API_DTYPE_FLOAT64) != 0) {
+    throw std::runtime_error(LGBM_GetLastError());
+  }
+  API_END();
+}
+
+int LGBM_BoosterPredictForArrow(BoosterHandle handle, int64_t n_chunks, const struct ArrowArray* chunks,
+                                const struct ArrowSchema* schema, int predict_type, int start_iteration,
+                                int num_iteration, const char* parameter, int64_t* out_len, double* out_result) {
+  API_BEGIN();
+  ArrowTable table(n_chunks, chunks, schema);
+  ArrowSource src(table);
+  PredictRows(B(handle), src, predict_type, start_iteration, num_iteration, parameter, out_len, out_result);
+  API_END();
+}
+
+int LGBM_DatasetCreateFromCSRFunc(void* get_row_funptr, int num_rows, int64_t num_col, const char* parameters,
+                                  const DatasetHandle reference, DatasetHandle* out) {
+  API_BEGIN();
+  FuncSource src(static_cast<FuncSource::RowFn*>(get_row_funptr), num_rows, static_cast<int>(num_col));
+  *out = BuildFromSource(src, parameters, reference);
+  API_END();
+}
+
+int LGBM_DatasetCreateFromSampledColumn(double** sample_data, int** sample_indices, int32_t ncol,
+                                        const int* num_per_col, int32_t num_sample_row, int32_t num_local_row,
+                                        int64_t num_dist_row, const char* parameters, DatasetHandle* out) {
+  API_BEGIN();
+  (void)num_dist_row;
+  // bin boundaries come from the sampled non-zero values; rows arrive later via PushRows
+  OwnedSparseSource sample;
+  sample.ncol = ncol;
+  sample.rows.resize(num_sample_row);
+  for (int32_t c = 0; c < ncol; ++c) {
+    for (int k = 0; k < num_per_col[c]; ++k) {
+      const int r = sample_indices[c][k];
+      if (r >= 0 && r < num_sample_row) sample.rows[r].emplace_back(c, sample_data[c][k]);
+    }
+  }
+  Config cfg = ParseConfig(parameters);
+  Dataset ref;
+  ref.Construct(sample, cfg, nullptr, {}, CategoricalIndices(cfg));
+  auto w = std::make_unique<DatasetWrapper>();
+  w->cfg = cfg;
+  w->ds = std::make_unique<Dataset>();
+  w->ds->InitEmptyLike(ref, num_local_row);
+  *out = w.release();
+  API_END();
+}
+
+int LGBM_DatasetPushRowsByCSRWithMetadata(DatasetHandle dataset, const void* indptr, int indptr_type,
+                                          const int32_t* indices, const void* data, int data_type, int64_t nindptr,
+                                          int64_t nelem, int64_t start_row, const float* label, const float* weight,
+                                          const double* init_score, const int32_t* query, int32_t tid) {
+  API_BEGIN();
+  (void)tid;
+  CSRSource src(indptr, indptr_type == C_API_DTYPE_INT64, indices, data, data_type == C_API_DTYPE_FLOAT64, nindptr,
+                nelem, D(dataset)->ds->num_total_features());
+  Dataset* ds = D(dataset)->ds.get();
+  ds->PushRows(src, static_cast<data_size_t>(start_row));
+  const data_size_t n = src.num_rows();
+  ds->metadata().SetRows(static_cast<data_size_t>(start_row), n, label, weight, init_score, query);
+  API_END();
+}
+
+int LGBM_DatasetSerializeReferenceToBinary(DatasetHandle handle, ByteBufferHandle* out, int32_t* out_len) {
+  API_BEGIN();
+  Dataset empty;
+  empty.InitEmptyLike(*D(handle)->ds, 0);
+  auto bb = std::make_unique<ByteBuffer>();
+  empty.SerializeBinary(&bb->data);
+  *out_len = static_cast<int32_t>(bb->data.size());
+  *out = bb.release();
+  API_END();
+}
+
+int LGBM_DatasetCreateFromSerializedReference(const void* ref_buffer, int32_t ref_buffer_size, int64_t num_row,
+                                              int32_t num_classes, const char* parameters, DatasetHandle* out) {
+  API_BEGIN();
+  (void)num_classes;
+  auto ref = Dataset::DeserializeBinary(static_cast<const char*>(ref_buffer), static_cast<size_t>(ref_buffer_size));
+  auto w = std::make_unique<DatasetWrapper>();
+  w->cfg = ParseConfig(parameters);
+  w->ds = std::make_unique<Dataset>();
+  w->ds->InitEmptyLike(*ref, static_cast<data_size_t>(num_row));
+  *out = w.release();
+  API_END();
+}
+
+int LGBM_ByteBufferGetAt(ByteBufferHandle handle, int32_t index, uint8_t* out_val) {
+  API_BEGIN();
+  *out_val = static_cast<uint8_t>(static_cast<ByteBuffer*>(handle)->data.at(index));
+  API_END();
+}
+
+int LGBM_ByteBufferFree(ByteBufferHandle handle) {
+  API_BEGIN();
+  delete static_cast<ByteBuffer*>(handle);
+  API_END();
+}
+
+int LGBM_BoosterPredictForMatSingleRowFastInit(BoosterHandle handle, const int predict_type, const int start_iteration,
+                                               const int num_iteration, const int data_type, const int32_t ncol,
+                                               const char* parameter, FastConfigHandle* out_fastConfig) {
+  API_BEGIN();
+  *out_fastConfig = MakeFast(handle, predict_type, start_iteration, num_iteration, data_type, ncol, parameter);
+  API_END();
+}
+
+int LGBM_BoosterPredictForMatSingleRowFast(FastConfigHandle fastConfig_handle, const void* data, int64_t* out_len,
+                                           double* out_result) {
+  API_BEGIN();
+  auto* fc = static_cast<FastConfig*>(fastConfig_handle);
+  thread_local std::vector<std::pair<int, double>> row;
+  DenseSource src(data, fc->data_type == C_API_DTYPE_FLOAT64, 1, static_cast<int>(fc->ncol), true);
+  src.GetRow(0, &row);
+  PredictOneRow(fc, row, out_len, out_result);
+  API_END();
+}
+
+int LGBM_BoosterPredictForCSRSingleRowFastInit(BoosterHandle handle, const int predict_type, const int start_iteration,
+                                               const int num_iteration, const int data_type, const int64_t num_col,
+                                               const char* parameter, FastConfigHandle* out_fastConfig) {
+  API_BEGIN();
+  *out_fastConfig = MakeFast(handle, predict_type, start_iteration, num_iteration, data_type, num_col, parameter);
+  API_END();
+}
+
+int LGBM_BoosterPredictForCSRSingleRowFast(FastConfigHandle fastConfig_handle, const void* indptr,
+                                           const int indptr_type, const int32_t* indices, const void* data,
+                                           const int64_t nindptr, const int64_t nelem, int64_t* out_len,
+                                           double* out_result) {
+  API_BEGIN();
+  auto* fc = static_cast<FastConfig*>(fastConfig_handle);
+  thread_local std::vector<std::pair<int, double>> row;
+  CSRSource src(indptr, indptr_type == C_API_DTYPE_INT64, indices, data, fc->data_type == C_API_DTYPE_FLOAT64,
+                nindptr, nelem, fc->ncol);
+  src.GetRow(0, &row);
+  PredictOneRow(fc, row, out_len, out_result);
+  API_END();
+}
+
+int LGBM_FastConfigFree(FastConfigHandle fastConfig) {
+  API_BEGIN();
+  delete static_cast<FastConfig*>(fastConfig);
+  API_END();
+}
+
+int LGBM_BoosterPredictSparseOutput(BoosterHandle handle, const void* indptr, int indptr_type, const int32_t* indices,
+                                    const void* data, int data_type, int64_t nindptr, int64_t nelem,
+                                    int64_t num_col_or_row, int predict_type, int start_iteration, int num_iteration,
+                                    const char* parameter, int matrix_type, int64_t* out_len, void** out_indptr,
+                                    int32_t** out_indices, void** out_data) {
+  API_BEGIN();
+  if (predict_type != C_API_PREDICT_CONTRIB) Log::Fatal("Sparse output is only supported for feature contributions");
+  Booster* b = B(handle);
+  std::unique_ptr<RowSource> src;
+  std::unique_ptr<OwnedSparseSource> csc_rows;
+  if (matrix_type == C_API_MATRIX_TYPE_CSR) {
+    src = std::make_unique<CSRSource>(indptr, indptr_type == C_API_DTYPE_INT64, indices, data,
+                                      data_type == C_API_DTYPE_FLOAT64, nindptr, nelem, num_col_or_row);
+  } else if (matrix_type == C_API_MATRIX_TYPE_CSC) {
+    csc_rows = CSCToRows(indptr, indptr_type, indices, data, data_type, nindptr, num_col_or_row);
+  } else {
+    Log::Fatal("Unknown matrix type in LGBM_BoosterPredictSparseOutput");
+  }
+  const RowSource& rows = csc_rows ? static_cast<const RowSource&>(*csc_rows) : *src;
+  const data_size_t nrow = rows.num_rows();
+  const int64_t ncol_in = matrix_type == C_API_MATRIX_TYPE_CSR ? num_col_or_row : nindptr - 1;
+  GBDT* g = b->boosting_.get();
+  const int K = g->NumModelPerIteration();
+  const int width = g->MaxFeatureIdx() + 2;  // contributions + expected value
+  std::vector<double> dense(static_cast<size_t>(nrow) * K * width);
+  int64_t dlen = 0;
+  PredictRows(b, rows, predict_type, start_iteration, num_iteration, parameter, &dlen, dense.data());
+  // per class matrix: non-zero entries of each row (CSR) or column (CSC)
+  const bool i32 = indptr_type == C_API_DTYPE_INT32, f32 = data_type == C_API_DTYPE_FLOAT32;
+  const int64_t outer = matrix_type == C_API_MATRIX_TYPE_CSR ? nrow : width;
+  const int64_t ptr_len = K * (outer + 1);
+  std::vector<int64_t> ptr(ptr_len);
+  std::vector<int32_t> idx;
+  std::vector<double> val;
+  (void)ncol_in;
+  for (int k = 0; k < K; ++k) {
+    const int64_t base = k * (outer + 1);
+    ptr[base] = 0;
+    const int64_t start = static_cast<int64_t>(idx.size());
+    for (int64_t o = 0; o < outer; ++o) {
+      const int64_t inner_n = matrix_type == C_API_MATRIX_TYPE_CSR ? width : nrow;
+      for (int64_t q = 0; q < inner_n; ++q) {
+        const int64_t r = matrix_type == C_API_MATRIX_TYPE_CSR ? o : q;
+        const int64_t c = matrix_type == C_API_MATRIX_TYPE_CSR ? q : o;
+        const double v = dense[(static_cast<size_t>(r) * K + k) * width + c];
+        if (v != 0.0) {
+          idx.push_back(static_cast<int32_t>(q));
+          val.push_back(v);
+        }
+      }
+      ptr[base + o + 1] = static_cast<int64_t>(idx.size()) - start;
+    }
+  }
+  if (i32) {
+    auto* p = new int32_t[ptr_len];
+    for (int64_t i = 0; i < ptr_len; ++i) p[i] = static_cast<int32_t>(ptr[i]);
+    *out_indptr = p;
+  } else {
+    auto* p = new int64_t[ptr_len];
+    std::copy(ptr.begin(), ptr.end(), p);
+    *out_indptr = p;
+  }
+  *out_indices = new int32_t[std::max<size_t>(1, idx.size())];
+  std::copy(idx.begin(), idx.end(), *out_indices);
+  if (f32) {
+    auto* d = new float[std::max<size_t>(1, val.size())];
+    for (size_t i = 0; i < val.size(); ++i) d[i] = static_cast<float>(val[i]);
+    *out_data = d;
+  } else {
+    auto* d = new double[std::max<size_t>(1, val.size())];
+    std::copy(val.begin(), val.end(), d);
+    *out_data = d;
+  }
+  out_len[0] = static_cast<int64_t>(val.size());
+  out_len[1] = ptr_len;
+  API_END();
+}
+
+int LGBM_BoosterFreePredictSparse(void* indptr, int32_t* indices, void* data, int indptr_type, int data_type) {
+  API_BEGIN();
+  if (indptr_type == C_API_DTYPE_INT32) delete[] static_cast<int32_t*>(indptr);
+  else delete[] static_cast<int64_t*>(indptr);
+  delete[] indices;
+  if (data_type == C_API_DTYPE_FLOAT32) delete[] static_cast<float*>(data);
+  else delete[] static_cast<double*>(data);
   API_END();
 }

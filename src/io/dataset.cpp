@@ -591,8 +591,9 @@ bool Dataset::IsBinaryFile(const std::string& filename) {
   return in.gcount() == static_cast<std::streamsize>(tok.size()) && tok == kBinaryToken;
 }
 
-void Dataset::SaveBinary(const std::string& filename) const {
-  std::vector<char> buf(kBinaryToken, kBinaryToken + std::strlen(kBinaryToken));
+void Dataset::SerializeBinary(std::vector<char>* out) const {
+  std::vector<char>& buf = *out;
+  buf.assign(kBinaryToken, kBinaryToken + std::strlen(kBinaryToken));
   Put(&buf, num_data_);
   Put(&buf, num_total_features_);
   Put(&buf, num_total_bin_);
@@ -613,6 +614,11 @@ void Dataset::SaveBinary(const std::string& filename) const {
   PutVec(&buf, categorical_);
   metadata_.Serialize(&buf);
   PutVec(&buf, bins_);
+}
+
+void Dataset::SaveBinary(const std::string& filename) const {
+  std::vector<char> buf;
+  SerializeBinary(&buf);
   std::ofstream out(filename, std::ios::binary);
   if (!out) Log::Fatal("Cannot write binary data to %s", filename.c_str());
   out.write(buf.data(), buf.size());
@@ -623,9 +629,16 @@ std::unique_ptr<Dataset> Dataset::LoadBinary(const std::string& filename) {
   std::ifstream in(filename, std::ios::binary);
   if (!in) Log::Fatal("Cannot open binary file %s", filename.c_str());
   std::vector<char> buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-  const char* p = buf.data();
-  if (buf.size() < std::strlen(kBinaryToken) || std::memcmp(p, kBinaryToken, std::strlen(kBinaryToken)) != 0) {
+  if (buf.size() < std::strlen(kBinaryToken) || std::memcmp(buf.data(), kBinaryToken, std::strlen(kBinaryToken)) != 0) {
     Log::Fatal("File %s is not a LambdaGap binary dataset", filename.c_str());
+  }
+  return DeserializeBinary(buf.data(), buf.size());
+}
+
+std::unique_ptr<Dataset> Dataset::DeserializeBinary(const char* data, size_t size) {
+  const char* p = data;
+  if (size < std::strlen(kBinaryToken) || std::memcmp(p, kBinaryToken, std::strlen(kBinaryToken)) != 0) {
+    Log::Fatal("Buffer is not a serialized LambdaGap dataset");
   }
   p += std::strlen(kBinaryToken);
   auto d = std::make_unique<Dataset>();

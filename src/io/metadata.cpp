@@ -31,6 +31,37 @@ void Metadata::SetLabel(const float* label, data_size_t len) {
   }
 }
 
+void Metadata::SetRows(data_size_t start, data_size_t n, const float* label, const float* weight,
+                       const double* init_score, const int32_t* query) {
+  if (start < 0 || start + n > num_data_) Log::Fatal("Pushed metadata rows exceed the dataset size");
+  if (label) std::copy(label, label + n, label_.begin() + start);
+  if (weight) {
+    if (weights_.empty()) weights_.assign(num_data_, 1.0f);
+    std::copy(weight, weight + n, weights_.begin() + start);
+  }
+  if (init_score) {
+    if (init_score_.empty()) init_score_.assign(num_data_, 0.0);
+    std::copy(init_score, init_score + n, init_score_.begin() + start);
+  }
+  if (query) {
+    if (pending_query_ids_.empty()) pending_query_ids_.assign(num_data_, -1);
+    std::copy(query, query + n, pending_query_ids_.begin() + start);
+  }
+  if (start + n == num_data_) {
+    if (!weights_.empty()) SetWeights(std::vector<float>(weights_).data(), num_data_);
+    if (!pending_query_ids_.empty()) {
+      // consecutive equal ids form one query
+      std::vector<data_size_t> sizes;
+      for (data_size_t i = 0; i < num_data_; ++i) {
+        if (i == 0 || pending_query_ids_[i] != pending_query_ids_[i - 1]) sizes.push_back(0);
+        ++sizes.back();
+      }
+      pending_query_ids_.clear();
+      SetQuery(sizes.data(), static_cast<data_size_t>(sizes.size()));
+    }
+  }
+}
+
 void Metadata::SetWeights(const float* w, data_size_t len) {
   if (w == nullptr || len == 0) {
     weights_.clear();
