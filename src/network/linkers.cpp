@@ -182,9 +182,39 @@ void Linkers::SendRecv(int sp, const char* sd, size_t sl, int rp, char* rd, size
   net_time_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
-void Linkers::Allgather(char* input, const comm_size_t* start, const comm_size_t* len, char* output, comm_size_t) {
+// ---------------------------------------------------------------------------
+// Collectives over the mesh (reference src/network/network.cpp:150-328):
+//   Allgather     ring for large payloads (>= 10 MB, < 64 ranks), recursive
+//                 doubling for power-of-two rank counts, Bruck otherwise;
+//   ReduceScatter recursive halving for power-of-two rank counts with
+//                 contiguous ascending blocks, ring otherwise.
+namespace {
+bool IsPow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+bool Ascending(const comm_size_t* start, const comm_size_t* len, int n) {
+  for (int i = 1; i < n; ++i) {
+    if (start[i] != start[i - 1] + len[i - 1]) return false;
+  }
+  return true;
+}
+constexpr comm_size_t kRingThreshold = 10 * 1024 * 1024;
+}  // namespace
+
+void Linkers::Allgather(char* input, const comm_size_t* start, const comm_size_t* len, char* output,
+                        comm_size_t all_size) {
   const int n = num_machines_;
   std::memcpy(output + start[rank_], input, len[rank_]);
+  const bool contiguous = Ascending(start, len, n);
+  if (all_size >= kRingThreshold && n < 64) {
+    AllgatherRing(start, len, output);
+  } else if (IsPow2(n) && contiguous) {
+    AllgatherRecursiveDoubling(start, len, output);
+  } else {
+    AllgatherBruck(start, len, output);
+  }
+}
+
+void Linkers::AllgatherRing(const comm_size_t* start, const comm_size_t* len, char* output) {
+  const int n = num_machines_;
   const int next = (rank_ + 1) % n, prev = (rank_ - 1 + n) % n;
   for (int s = 0; s < n - 1; ++s) {
     const int sb = (rank_ - s + n) % n;
@@ -193,8 +223,56 @@ void Linkers::Allgather(char* input, const comm_size_t* start, const comm_size_t
   }
 }
 
+// log2(n) steps; at distance d each rank swaps its gathered run of d blocks with rank ^ d
+void Linkers::AllgatherRecursiveDoubling(const comm_size_t* start, const comm_size_t* len, char* output) {
+  const int n = num_machines_;
+  for (int d = 1; d < n; d <<= 1) {
+    const int peer = rank_ ^ d;
+    const int mine = rank_ & ~(d - 1), theirs = peer & ~(d - 1);
+    const comm_size_t sb = start[mine], rb = start[theirs];
+    const comm_size_t sl = start[mine + d - 1] + len[mine + d - 1] - sb;
+    const comm_size_t rl = start[theirs + d - 1] + len[theirs + d - 1] - rb;
+    SendRecv(peer, output + sb, sl, peer, output + rb, rl);
+  }
+}
+
+// ceil(log2(n)) steps for any n: blocks are held in rank-relative order
+// (slot j = rank + j); at distance d the first min(d, n - d) slots go to rank - d
+void Linkers::AllgatherBruck(const comm_size_t* start, const comm_size_t* len, char* output) {
+  const int n = num_machines_;
+  std::vector<char> rel;
+  std::vector<comm_size_t> roff(n + 1, 0);
+  for (int j = 0; j < n; ++j) roff[j + 1] = roff[j] + len[(rank_ + j) % n];
+  rel.resize(std::max<comm_size_t>(roff[n], 1));
+  std::memcpy(rel.data(), output + start[rank_], len[rank_]);
+  for (int d = 1; d < n; d <<= 1) {
+    const int cnt = std::min(d, n - d);
+    const int to = (rank_ - d + n) % n, from = (rank_ + d) % n;
+    // the receiver's slots [d, d + cnt) are the sender's [0, cnt): sizes from the sender's view
+    comm_size_t recv_bytes = 0;
+    for (int j = 0; j < cnt; ++j) recv_bytes += len[(from + j) % n];
+    SendRecv(to, rel.data(), roff[cnt], from, rel.data() + roff[d], recv_bytes);
+  }
+  for (int j = 1; j < n; ++j) {
+    const int r = (rank_ + j) % n;
+    std::memcpy(output + start[r], rel.data() + roff[j], len[r]);
+  }
+}
+
 void Linkers::ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* start,
-                            const comm_size_t* len, char* output, comm_size_t, const ReduceFunction& reducer) {
+                            const comm_size_t* len, char* output, comm_size_t output_size,
+                            const ReduceFunction& reducer) {
+  const int n = num_machines_;
+  if (IsPow2(n) && Ascending(start, len, n)) {
+    ReduceScatterRecursiveHalving(input, input_size, type_size, start, len, output, reducer);
+  } else {
+    ReduceScatterRing(input, input_size, type_size, start, len, output, reducer);
+  }
+  (void)output_size;
+}
+
+void Linkers::ReduceScatterRing(char* input, comm_size_t input_size, int type_size, const comm_size_t* start,
+                                const comm_size_t* len, char* output, const ReduceFunction& reducer) {
   const int n = num_machines_;
   std::vector<char> acc(input, input + input_size);
   const int next = (rank_ + 1) % n, prev = (rank_ - 1 + n) % n;
@@ -205,6 +283,32 @@ void Linkers::ReduceScatter(char* input, comm_size_t input_size, int type_size, 
     tmp.resize(len[rb] > 0 ? len[rb] : 1);
     SendRecv(next, acc.data() + start[sb], len[sb], prev, tmp.data(), len[rb]);
     if (len[rb] > 0) reducer(tmp.data(), acc.data() + start[rb], type_size, len[rb]);
+  }
+  std::memcpy(output, acc.data() + start[rank_], len[rank_]);
+}
+
+// log2(n) steps: the live rank range halves each step; the half that holds the
+// partner's blocks is sent, the own half is received and reduced in place
+void Linkers::ReduceScatterRecursiveHalving(char* input, comm_size_t input_size, int type_size,
+                                            const comm_size_t* start, const comm_size_t* len, char* output,
+                                            const ReduceFunction& reducer) {
+  const int n = num_machines_;
+  std::vector<char> acc(input, input + input_size);
+  std::vector<char> tmp;
+  int lo = 0, hi = n;
+  for (int d = n / 2; d >= 1; d >>= 1) {
+    const int mid = lo + d;
+    const bool upper = rank_ >= mid;
+    const int peer = upper ? rank_ - d : rank_ + d;
+    const int keep_lo = upper ? mid : lo, keep_hi = upper ? hi : mid;
+    const int give_lo = upper ? lo : mid, give_hi = upper ? mid : hi;
+    const comm_size_t kb = start[keep_lo], kl = start[keep_hi - 1] + len[keep_hi - 1] - kb;
+    const comm_size_t gb = start[give_lo], gl = start[give_hi - 1] + len[give_hi - 1] - gb;
+    tmp.resize(std::max<comm_size_t>(kl, 1));
+    SendRecv(peer, acc.data() + gb, gl, peer, tmp.data(), kl);
+    if (kl > 0) reducer(tmp.data(), acc.data() + kb, type_size, kl);
+    lo = keep_lo;
+    hi = keep_hi;
   }
   std::memcpy(output, acc.data() + start[rank_], len[rank_]);
 }

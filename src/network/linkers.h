@@ -2,7 +2,8 @@
 // linkers_socket.cpp, socket_wrapper.hpp): machine list parsing
 // ("ip port" / "ip:port" lines or the `machines` string), lower rank connects
 // to higher rank with exponential backoff, TCP_NODELAY, receive timeout of
-// `time_out` minutes, and ring Allgather / ReduceScatter over the mesh.
+// `time_out` minutes, and ring / recursive-doubling / Bruck Allgather and ring /
+// recursive-halving ReduceScatter over the mesh.
 #pragma once
 
 #include <string>
@@ -31,6 +32,13 @@ class Linkers {
   double network_seconds() const { return net_time_; }
 
  private:
+  void AllgatherRing(const comm_size_t* start, const comm_size_t* len, char* output);
+  void AllgatherRecursiveDoubling(const comm_size_t* start, const comm_size_t* len, char* output);
+  void AllgatherBruck(const comm_size_t* start, const comm_size_t* len, char* output);
+  void ReduceScatterRing(char* input, comm_size_t input_size, int type_size, const comm_size_t* start,
+                         const comm_size_t* len, char* output, const ReduceFunction& reducer);
+  void ReduceScatterRecursiveHalving(char* input, comm_size_t input_size, int type_size, const comm_size_t* start,
+                                     const comm_size_t* len, char* output, const ReduceFunction& reducer);
   void ParseMachines(const Config& config);
   void Construct(int listen_port, int time_out_min);
   int rank_ = 0;

@@ -28,6 +28,7 @@ def _free_ports(n):
 
 
 def _worker(rank, ports, learner, rows, out_dir, extra):
+    world = len(ports)
     import sys
 
     sys.path.insert(0, ROOT)
@@ -36,9 +37,9 @@ def _worker(rank, ports, learner, rows, out_dir, extra):
     mat = np.loadtxt(os.path.join(DATA, "binary.train"))
     X, y = mat[:, 1:], mat[:, 0]
     if rows == "split":
-        X, y = X[rank::2], y[rank::2]
+        X, y = X[rank::world], y[rank::world]
     machines = ",".join(f"127.0.0.1:{p}" for p in ports)
-    params = {"objective": "binary", "tree_learner": learner, "num_machines": 2, "machines": machines,
+    params = {"objective": "binary", "tree_learner": learner, "num_machines": world, "machines": machines,
               "local_listen_port": ports[rank], "verbosity": -1, "num_leaves": 15, "pre_partition": True,
               "time_out": 2, **extra}
     b = lgb.train(params, lgb.Dataset(X, y, params=params), 8)
@@ -46,11 +47,11 @@ def _worker(rank, ports, learner, rows, out_dir, extra):
         f.write(b.model_to_string())
 
 
-def _run(learner, rows, tmp_path, extra=None):
-    ports = _free_ports(2)
+def _run(learner, rows, tmp_path, extra=None, world=2):
+    ports = _free_ports(world)
     ctx = mp.get_context("spawn")
     procs = [ctx.Process(target=_worker, args=(r, ports, learner, rows, str(tmp_path), extra or {}))
-             for r in range(2)]
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -59,19 +60,20 @@ def _run(learner, rows, tmp_path, extra=None):
     for p in procs:
         if p.is_alive():
             p.kill()
-    assert codes == [0, 0], codes
-    return [open(tmp_path / f"model{r}.txt").read() for r in range(2)]
+    assert codes == [0] * world, codes
+    return [open(tmp_path / f"model{r}.txt").read() for r in range(world)]
 
 
 def _trees(s):
     return s.split("end of trees")[0]
 
 
-@pytest.mark.parametrize("learner", ["data", "voting"])
-def test_row_sharded_learners(lgb, tmp_path, learner):
-    m0, m1 = _run(learner, "split", tmp_path)
+@pytest.mark.parametrize("learner,world", [("data", 2), ("voting", 2), ("data", 3), ("voting", 3)])
+def test_row_sharded_learners(lgb, tmp_path, learner, world):
+    ms = _run(learner, "split", tmp_path, world=world)
+    m0 = ms[0]
     # every rank ends with the same model
-    assert _trees(m0) == _trees(m1)
+    assert all(_trees(m) == _trees(m0) for m in ms)
     b = lgb.Booster(model_str=m0)
     t = np.loadtxt(os.path.join(DATA, "binary.test"))
     from sklearn.metrics import roc_auc_score
@@ -79,15 +81,18 @@ def test_row_sharded_learners(lgb, tmp_path, learner):
     assert roc_auc_score(t[:, 0], b.predict(t[:, 1:])) > 0.75
 
 
-def test_data_parallel_matches_serial_on_same_bins(lgb, tmp_path):
-    """Every rank holding ALL rows: data-parallel sums two identical halves of every histogram, which is the
-    serial histogram doubled -> the same splits as serial training with doubled weights."""
-    m0, m1 = _run("data", "all", tmp_path, {"min_data_in_leaf": 20})
-    assert _trees(m0) == _trees(m1)
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_data_parallel_matches_serial_on_same_bins(lgb, tmp_path, world):
+    """Every rank holding ALL rows: data-parallel sums `world` identical copies of every histogram (through
+    recursive halving / doubling for 2 and 4 ranks, ring + Bruck for 3), which is the serial histogram of
+    the rows repeated `world` times -> the same model."""
+    ms = _run("data", "all", tmp_path, {"min_data_in_leaf": 20}, world=world)
+    m0 = ms[0]
+    assert all(_trees(m) == _trees(m0) for m in ms)
     mat = np.loadtxt(os.path.join(DATA, "binary.train"))
     X, y = mat[:, 1:], mat[:, 0]
-    serial = lgb.train({"objective": "binary", "verbosity": -1, "num_leaves": 15, "min_data_in_leaf": 40},
-                       lgb.Dataset(np.vstack([X, X]), np.concatenate([y, y])), 8)
+    serial = lgb.train({"objective": "binary", "verbosity": -1, "num_leaves": 15, "min_data_in_leaf": 20 * world},
+                       lgb.Dataset(np.vstack([X] * world), np.concatenate([y] * world)), 8)
     t = np.loadtxt(os.path.join(DATA, "binary.test"))
     np.testing.assert_allclose(lgb.Booster(model_str=m0).predict(t[:, 1:]), serial.predict(t[:, 1:]), rtol=1e-6,
                                atol=1e-8)
