@@ -65,8 +65,10 @@ def test_missing_values_and_categorical(lgb, gpu_required, rng):
     bc = _train(lgb, X, y, "cpu", rounds=3, **kw)
     bg = _train(lgb, X, y, "gpu", rounds=3, gpu_use_dp=True, **kw)
     tc, tg = _trees(bc)[0], _trees(bg)[0]
-    sc = [s[:2] for s in _splits(tc["tree_structure"], [])][:4]
-    sg = [s[:2] for s in _splits(tg["tree_structure"], [])][:4]
+    # the first three pre-order splits resolve the three effects; deeper splits of the (then
+    # pure) leaves have ~0 gain and are decided by summation-order rounding
+    sc = [s[:2] for s in _splits(tc["tree_structure"], [])][:3]
+    sg = [s[:2] for s in _splits(tg["tree_structure"], [])][:3]
     assert sc == sg
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=0, atol=2e-2)
 
