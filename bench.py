@@ -39,6 +39,8 @@ def main() -> int:
     ap.add_argument("--max-bin", type=int, default=255)
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--rehearse-dp", action="store_true",
+                    help="1 GPU: run the RCCL data-parallel learner path on a one-rank communicator")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -58,6 +60,15 @@ def main() -> int:
         import torch.distributed as dist  # noqa: F811
 
         init_device_comm()
+    elif args.rehearse_dp:
+        import ctypes
+
+        from lambdagap_amd.parallel import distributed as dd
+
+        uid = dd.get_unique_id()
+        dd._check(dd._LIB.LGBM_DeviceCommInit(dd._c_str(uid), ctypes.c_int64(len(uid)), ctypes.c_int(1),
+                                              ctypes.c_int(0), ctypes.c_int(0)))
+        os.environ["LGAP_FORCE_DEVICE_DP"] = "1"
     t_data = time.time()
     start, stop = shard_range(args.rows, rank, world)
     X, y = make_higgs_like(args.rows, seed=args.seed, start=start, stop=stop)

@@ -42,6 +42,8 @@ def main() -> int:
     ta = [t["tree_structure"].get("split_feature") for t in out["single"].dump_model()["tree_info"]]
     tb = [t["tree_structure"].get("split_feature") for t in out["dp"].dump_model()["tree_info"]]
     print(json.dumps({"max_abs_diff": float(np.max(np.abs(pa - pb))), "root_features_equal": ta == tb,
+                      "dp_path": "RCCL data-parallel" in out["dp"].device_name(),
+                      "single_path": "RCCL" not in out["single"].device_name(),
                       "num_trees": [out["single"].num_trees(), out["dp"].num_trees()]}), flush=True)
     d.free_device_comm()
     return 0

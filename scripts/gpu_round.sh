@@ -27,6 +27,8 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
     bench1m) step bench1m 400 python bench.py --rows 1000000 --steps 10 --warmup 2;;
     bench) step bench 900 python bench.py --steps 30 --warmup 3;;
+    benchdp) step benchdp 900 python bench.py --steps 30 --warmup 3 --rehearse-dp;;
+    dpself) step dpself 600 python scripts/dp_selftest.py;;
     timetag) LGAP_TIMETAG=1 step timetag 900 python bench.py --steps 20 --warmup 3;;
     pmc) step pmc 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA --kernel-trace --output-format csv -d $PWD/$OUT/pmc -o pmc -- python3 bench.py --rows 2000000 --steps 3 --warmup 1;;
     profpost) LGAP_SPLIT_POST=1 step profpost 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/profpost -o run -- python3 bench.py --steps 10 --warmup 2;;

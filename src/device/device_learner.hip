@@ -1449,8 +1449,9 @@ class DeviceTreeLearner : public TreeLearner {
     // LGAP_FORCE_DEVICE_DP=1 routes a single-rank run through the RCCL data-parallel path
     // (staging reduce + ncclAllReduce + global counts): lets a 1-GPU box test that path.
     const char* force_dp = std::getenv("LGAP_FORCE_DEVICE_DP");
-    distributed_ = CommActive() && (data_parallel_ || (force_dp && force_dp[0] == '1'));
-    device_id_ = CommActive() ? CommDevice() : std::max(0, config_->gpu_device_id);
+    const bool forced = CommExists() && force_dp && force_dp[0] == '1';
+    distributed_ = (data_parallel_ && CommActive()) || forced;
+    device_id_ = CommExists() ? CommDevice() : std::max(0, config_->gpu_device_id);
     HIP_CHECK(hipSetDevice(device_id_));
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device_id_));
@@ -1761,7 +1762,9 @@ class DeviceTreeLearner : public TreeLearner {
     return tree;
   }
 
-  std::string DeviceName() const override { return device_name_; }
+  std::string DeviceName() const override {
+    return distributed_ ? device_name_ + " [RCCL data-parallel]" : device_name_;
+  }
 
   void ReportStamps(int nsplits) {
     std::vector<unsigned long long> h(stamps_.size());

@@ -185,11 +185,13 @@ void CommFree() {
 int CommRank() { return S().rank; }
 int CommSize() { return S().size; }
 bool CommActive() { return S().comm != nullptr && S().size > 1; }
+bool CommExists() { return S().comm != nullptr; }
 ncclComm_t ActiveComm() { return S().comm; }
 int CommDevice() { return S().device; }
 
 void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream) {
-  if (!CommActive() || count == 0) return;
+  // a one-rank communicator still runs the collective (single-GPU rehearsal of the DP path)
+  if (!CommExists() || count == 0) return;
   NcclCheck(ncclAllReduce(dev_ptr, dev_ptr, count, ncclFloat64, ncclSum, S().comm, stream), "ncclAllReduce");
 }
 

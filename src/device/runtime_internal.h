@@ -11,6 +11,8 @@ namespace device {
 
 ncclComm_t ActiveComm();
 int CommDevice();
+// communicator present (CommActive() additionally requires more than one rank)
+bool CommExists();
 // In-place sum all-reduce of device doubles on `stream` (no-op without a communicator).
 void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream);
 

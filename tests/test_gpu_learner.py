@@ -158,6 +158,7 @@ def test_rccl_data_parallel_path_single_rank(lgb, gpu_required):
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["num_trees"] == [8, 8]
+    assert res["dp_path"] and res["single_path"], res
     assert res["root_features_equal"]
     assert res["max_abs_diff"] < 1e-3, res
 
