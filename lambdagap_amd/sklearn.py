@@ -102,6 +102,13 @@ class LGBMModel(BaseEstimator):
     # ------------------------------------------------------------------ params
     def get_params(self, deep: bool = True) -> Dict[str, Any]:
         params = super().get_params(deep=deep)
+        if type(self) is not LGBMModel and not isinstance(self, (LGBMRegressor, LGBMClassifier)):
+            # subclasses with their own __init__ signature still report the base parameters
+            import inspect
+
+            for name in inspect.signature(LGBMModel.__init__).parameters:
+                if name not in ("self", "kwargs") and name not in params and hasattr(self, name):
+                    params[name] = getattr(self, name)
         params.update(self._other_params)
         return params
 
