@@ -91,6 +91,60 @@ std::vector<int> ResolveColumnList(const std::string& spec, const std::vector<st
   return out;
 }
 
+// One text line -> (feature row, label, weight, group id). Feature indices have
+// the label column removed (CSV/TSV) or are taken as written (LibSVM).
+void ParseLine(const std::string& line, TextFormat fmt, char delim, int label_idx, int weight_idx, int group_idx,
+               std::vector<std::pair<int, double>>* row, float* label, float* weight, double* gid, int* maxcol) {
+  row->clear();
+  if (fmt == TextFormat::LIBSVM) {
+    const char* p = line.c_str();
+    // optional leading label (a token without ':')
+    while (*p == ' ' || *p == '\t') ++p;
+    const char* q = p;
+    while (*q && *q != ' ' && *q != '\t' && *q != ':') ++q;
+    if (*q != ':' && label_idx >= 0) {
+      double v;
+      common::Atof(p, &v);
+      *label = static_cast<float>(v);
+      p = q;
+    }
+    while (*p) {
+      while (*p == ' ' || *p == '\t') ++p;
+      if (!*p) break;
+      char* e;
+      long idx = std::strtol(p, &e, 10);
+      if (*e != ':') break;
+      double v;
+      p = common::Atof(e + 1, &v);
+      if (idx == weight_idx) *weight = static_cast<float>(v);
+      if (idx == group_idx) *gid = v;
+      if (std::isnan(v) || std::fabs(v) > kZeroThreshold) row->emplace_back(static_cast<int>(idx), v);
+      if (idx > *maxcol) *maxcol = static_cast<int>(idx);
+    }
+    return;
+  }
+  const char* p = line.c_str();
+  int col = 0;   // raw column index
+  int fcol = 0;  // feature column index (label removed)
+  while (true) {
+    double v;
+    const char* e = common::Atof(p, &v);
+    if (col == label_idx) {
+      *label = static_cast<float>(v);
+    } else {
+      if (fcol == weight_idx) *weight = static_cast<float>(v);
+      if (fcol == group_idx) *gid = v;
+      if (std::isnan(v) || std::fabs(v) > kZeroThreshold) row->emplace_back(fcol, v);
+      ++fcol;
+    }
+    ++col;
+    while (*e && *e != delim) ++e;
+    if (!*e) break;
+    p = e + 1;
+  }
+  if (fcol - 1 > *maxcol) *maxcol = fcol - 1;
+}
+
 }  // namespace
 
 void ParseTextFile(const std::string& filename, bool header, int label_idx, OwnedSparseSource* rows,
@@ -122,62 +176,18 @@ void ParseTextFile(const std::string& filename, bool header, int label_idx, Owne
   if (out_label_idx) *out_label_idx = label_idx;
 #pragma omp parallel for schedule(static, 1024)
   for (size_t r = 0; r < n; ++r) {
-    const std::string& line = lines[first + r];
-    auto& row = rows->rows[r];
-    int tid = omp_get_thread_num();
-    if (fmt == TextFormat::LIBSVM) {
-      const char* p = line.c_str();
-      // optional leading label (a token without ':')
-      while (*p == ' ' || *p == '\t') ++p;
-      const char* q = p;
-      while (*q && *q != ' ' && *q != '\t' && *q != ':') ++q;
-      if (*q != ':' && label_idx >= 0) {
-        double v;
-        common::Atof(p, &v);
-        (*labels)[r] = static_cast<float>(v);
-        p = q;
-      }
-      while (*p) {
-        while (*p == ' ' || *p == '\t') ++p;
-        if (!*p) break;
-        char* e;
-        long idx = std::strtol(p, &e, 10);
-        if (*e != ':') break;
-        double v;
-        p = common::Atof(e + 1, &v);
-        if (std::isnan(v) || std::fabs(v) > kZeroThreshold) row.emplace_back(static_cast<int>(idx), v);
-        if (idx > maxcol[tid]) maxcol[tid] = static_cast<int>(idx);
-      }
-    } else {
-      const char* p = line.c_str();
-      int col = 0;   // raw column index
-      int fcol = 0;  // feature column index (label removed)
-      while (true) {
-        double v;
-        const char* e = common::Atof(p, &v);
-        if (col == label_idx) {
-          (*labels)[r] = static_cast<float>(v);
-        } else {
-          if (fcol == weight_idx && weights) (*weights)[r] = static_cast<float>(v);
-          if (fcol == group_idx && group_ids) (*group_ids)[r] = v;
-          if (std::isnan(v) || std::fabs(v) > kZeroThreshold) row.emplace_back(fcol, v);
-          ++fcol;
-        }
-        ++col;
-        while (*e && *e != delim) ++e;
-        if (!*e) break;
-        p = e + 1;
-      }
-      if (fcol - 1 > maxcol[tid]) maxcol[tid] = fcol - 1;
-    }
+    const int tid = omp_get_thread_num();
+    float w = 1.0f;
+    double gid = 0.0;
+    ParseLine(lines[first + r], fmt, delim, label_idx, weight_idx, group_idx, &rows->rows[r], &(*labels)[r], &w, &gid,
+              &maxcol[tid]);
+    if (weights && weight_idx >= 0) (*weights)[r] = w;
+    if (group_ids && group_idx >= 0) (*group_ids)[r] = gid;
   }
   int mc = -1;
   for (int m : maxcol) mc = std::max(mc, m);
   rows->ncol = mc + 1;
-  if (fmt == TextFormat::LIBSVM && weights && weight_idx >= 0) {
-    for (size_t r = 0; r < n; ++r)
-      for (auto& kv : rows->rows[r]) if (kv.first == weight_idx) (*weights)[r] = static_cast<float>(kv.second);
-  }
+
   // drop ignored / weight / group columns from the feature values (they remain in the index space)
   std::set<int> drop(ignore_cols.begin(), ignore_cols.end());
   if (weight_idx >= 0) drop.insert(weight_idx);
@@ -191,6 +201,165 @@ void ParseTextFile(const std::string& filename, bool header, int label_idx, Owne
     }
   }
 }
+
+// Two-round loading (reference dataset_loader.cpp two_round / TextReader sampling):
+// pass 1 streams the file once to count rows, reservoir-sample
+// bin_construct_sample_cnt lines for the bin mappers and decide rank membership;
+// pass 2 streams it again and packs rows chunk by chunk, so the parsed text is
+// never resident as a whole (long-data analogue of the reference's design).
+namespace {
+struct TwoRoundSpec {
+  int label_idx, weight_idx, group_idx;
+  std::vector<std::string> feat_names;
+  std::vector<int> cats;
+  Config c2;
+};
+
+bool NextDataLine(std::istream& in, std::string* line) {
+  while (std::getline(in, *line)) {
+    if (!line->empty() && line->back() == '\r') line->pop_back();
+    if (!line->empty()) return true;
+  }
+  return false;
+}
+
+std::unique_ptr<Dataset> LoadTwoRound(const std::string& filename, const Config& cfg, const Dataset* reference,
+                                      int rank, int num_machines, const TwoRoundSpec& sp) {
+  std::ifstream in(filename, std::ios::binary);
+  if (!in) Log::Fatal("Data file %s doesn't exist.", filename.c_str());
+  std::string line;
+  if (cfg.header) NextDataLine(in, &line);
+  std::vector<std::string> head, sample;
+  std::vector<double> gids_all;
+  const size_t want = static_cast<size_t>(std::max(1, cfg.bin_construct_sample_cnt));
+  Random sampler(cfg.data_random_seed);
+  size_t n = 0;
+  TextFormat fmt = TextFormat::INVALID;
+  char delim = '\t';
+  int maxcol = -1;
+  while (NextDataLine(in, &line)) {
+    if (head.size() < 2) {
+      head.push_back(line);
+      if (head.size() == 2) {
+        fmt = Detect(head, 0);
+        delim = fmt == TextFormat::CSV ? ',' : '\t';
+      }
+    }
+    if (!reference) {
+      if (sample.size() < want) {
+        sample.push_back(line);
+      } else {
+        const size_t j = static_cast<size_t>(sampler.NextInt(0, static_cast<int>(std::min<size_t>(n + 1, 0x7fffffff))));
+        if (j < want) sample[j] = line;
+      }
+    }
+    if (sp.group_idx >= 0) {
+      std::vector<std::pair<int, double>> row;
+      float lab = 0.f, w = 1.f;
+      double g = 0.0;
+      if (fmt == TextFormat::INVALID) fmt = Detect(head, 0), delim = fmt == TextFormat::CSV ? ',' : '\t';
+      ParseLine(line, fmt, delim, sp.label_idx, sp.weight_idx, sp.group_idx, &row, &lab, &w, &g, &maxcol);
+      gids_all.push_back(g);
+    }
+    ++n;
+  }
+  if (fmt == TextFormat::INVALID) fmt = Detect(head, 0), delim = fmt == TextFormat::CSV ? ',' : '\t';
+  if (fmt == TextFormat::INVALID) Log::Fatal("Unknown format of training data %s", filename.c_str());
+  // rank membership, drawn in the one-round loader's order (rows, or whole queries)
+  std::vector<char> keep(n, 1);
+  std::vector<data_size_t> qb;
+  if (sp.group_idx >= 0) {
+    qb.push_back(0);
+    for (size_t i = 1; i < n; ++i) if (gids_all[i] != gids_all[i - 1]) qb.push_back(static_cast<data_size_t>(i));
+    qb.push_back(static_cast<data_size_t>(n));
+  }
+  if (num_machines > 1 && !cfg.pre_partition) {
+    Random rnd(cfg.data_random_seed);
+    if (!qb.empty()) {
+      std::vector<data_size_t> nqb = {0};
+      for (size_t q = 0; q + 1 < qb.size(); ++q) {
+        const bool mine = rnd.NextShort(0, num_machines) == rank;
+        for (data_size_t i = qb[q]; i < qb[q + 1]; ++i) keep[i] = mine;
+        if (mine) nqb.push_back(nqb.back() + (qb[q + 1] - qb[q]));
+      }
+      qb = nqb;
+    } else {
+      for (size_t i = 0; i < n; ++i) keep[i] = rnd.NextShort(0, num_machines) == rank;
+    }
+  }
+  data_size_t n_local = 0;
+  for (char k : keep) n_local += k;
+  // bin mappers (and bundles) from the sample, or the reference's
+  auto ds = std::make_unique<Dataset>();
+  if (reference) {
+    ds->InitEmptyLike(*reference, n_local);
+  } else {
+    OwnedSparseSource srows;
+    srows.rows.resize(sample.size());
+    int smax = -1;
+    for (size_t r = 0; r < sample.size(); ++r) {
+      float lab, w;
+      double g;
+      ParseLine(sample[r], fmt, delim, sp.label_idx, sp.weight_idx, sp.group_idx, &srows.rows[r], &lab, &w, &g, &smax);
+    }
+    srows.ncol = std::max(smax, maxcol) + 1;
+    Dataset ref;
+    ref.Construct(srows, sp.c2, nullptr, sp.feat_names, sp.cats);
+    ds->InitEmptyLike(ref, n_local);
+  }
+  sample.clear();
+  sample.shrink_to_fit();
+  // pass 2: parse and pack in chunks
+  in.clear();
+  in.seekg(0);
+  if (cfg.header) NextDataLine(in, &line);
+  constexpr size_t kChunk = 1 << 16;
+  std::vector<std::string> lines;
+  lines.reserve(kChunk);
+  std::vector<float> labels(n_local), weights(sp.weight_idx >= 0 ? n_local : 0);
+  data_size_t filled = 0;
+  size_t row_id = 0;
+  auto flush = [&]() {
+    OwnedSparseSource chunk;
+    chunk.ncol = ds->num_total_features();
+    chunk.rows.resize(lines.size());
+    std::vector<int> mc(omp_get_max_threads(), -1);
+#pragma omp parallel for schedule(static, 256)
+    for (size_t r = 0; r < lines.size(); ++r) {
+      float w = 1.0f;
+      double g = 0.0;
+      ParseLine(lines[r], fmt, delim, sp.label_idx, sp.weight_idx, sp.group_idx, &chunk.rows[r],
+                &labels[filled + r], &w, &g, &mc[omp_get_thread_num()]);
+      if (sp.weight_idx >= 0) weights[filled + r] = w;
+      // weight / group columns are not features
+      if (sp.weight_idx >= 0 || sp.group_idx >= 0) {
+        auto& row = chunk.rows[r];
+        row.erase(std::remove_if(row.begin(), row.end(),
+                                 [&](const std::pair<int, double>& kv) {
+                                   return kv.first == sp.weight_idx || kv.first == sp.group_idx;
+                                 }),
+                  row.end());
+      }
+    }
+    ds->PushRows(chunk, filled);
+    filled += static_cast<data_size_t>(lines.size());
+    lines.clear();
+  };
+  while (NextDataLine(in, &line)) {
+    if (keep[row_id++]) {
+      lines.push_back(line);
+      if (lines.size() == kChunk) flush();
+    }
+  }
+  if (!lines.empty()) flush();
+  ds->metadata().SetLabel(labels.data(), n_local);
+  if (sp.weight_idx >= 0) ds->metadata().SetWeights(weights.data(), n_local);
+  if (!qb.empty()) ds->metadata().SetQueryBoundaries(qb);
+  if (num_machines <= 1 || cfg.pre_partition) ds->metadata().LoadSideFiles(filename);
+  Log::Info("Loaded %d rows x %d features from %s (two-round)", n_local, ds->num_total_features(), filename.c_str());
+  return ds;
+}
+}  // namespace
 
 std::unique_ptr<Dataset> LoadDatasetFromFile(const std::string& filename, const Config& cfg, const Dataset* reference,
                                              int rank, int num_machines) {
@@ -231,6 +400,27 @@ std::unique_ptr<Dataset> LoadDatasetFromFile(const std::string& filename, const 
   std::vector<int> ignore = common::StartsWith(cfg.ignore_column, "name:")
                                 ? ResolveColumnList(cfg.ignore_column, feat_names)
                                 : ResolveColumnList(cfg.ignore_column, {});
+  if (cfg.two_round) {
+    TwoRoundSpec sp;
+    sp.label_idx = label_idx;
+    sp.weight_idx = weight_idx;
+    sp.group_idx = group_idx;
+    sp.feat_names = reference ? std::vector<std::string>() : feat_names;
+    if (!cfg.categorical_feature.empty()) {
+      sp.cats = common::StartsWith(cfg.categorical_feature, "name:")
+                    ? ResolveColumnList(cfg.categorical_feature, feat_names)
+                    : ResolveColumnList(cfg.categorical_feature, {});
+    }
+    sp.c2 = cfg;
+    std::string ig;
+    for (size_t i = 0; i < ignore.size(); ++i) ig += (i ? "," : "") + std::to_string(ignore[i]);
+    if (weight_idx >= 0) ig += (ig.empty() ? "" : ",") + std::to_string(weight_idx);
+    if (group_idx >= 0) ig += (ig.empty() ? "" : ",") + std::to_string(group_idx);
+    sp.c2.ignore_column = ig;
+    auto ds = LoadTwoRound(filename, cfg, reference, rank, num_machines, sp);
+    if (cfg.save_binary) ds->SaveBinary(filename + ".bin");
+    return ds;
+  }
   OwnedSparseSource rows;
   std::vector<float> labels, weights;
   std::vector<double> gids;

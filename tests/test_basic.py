@@ -204,3 +204,15 @@ def test_free_raw_data_and_reference_alignment(lgb, rng):
     b = lgb.train({"verbosity": -1}, ds, 3, valid_sets=[dv])
     assert ds.data is None
     assert b.eval_valid()[0][0] == "valid_0"
+
+
+@pytest.mark.parametrize("name,obj", [("binary", "binary"), ("rank", "lambdarank")])
+def test_two_round_loading_matches_one_round(lgb, name, obj):
+    """two_round streams the file twice (sample for bins, then chunked packing); with the
+    sample covering the file the dataset and model are identical to one-round loading."""
+    path = os.path.join(DATA, f"{name}.train")
+    params = {"objective": obj, "verbosity": -1, "num_leaves": 15}
+    one = lgb.train(params, lgb.Dataset(path, params=dict(params)), 5)
+    two = lgb.train(params, lgb.Dataset(path, params=dict(params, two_round=True)), 5)
+    strip = lambda s: s[:s.index("parameters:")]  # noqa: E731
+    assert strip(one.model_to_string()) == strip(two.model_to_string())
