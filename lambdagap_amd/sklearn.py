@@ -102,7 +102,7 @@ class LGBMModel(BaseEstimator):
     # ------------------------------------------------------------------ params
     def get_params(self, deep: bool = True) -> Dict[str, Any]:
         params = super().get_params(deep=deep)
-        if type(self) is not LGBMModel and not isinstance(self, (LGBMRegressor, LGBMClassifier)):
+        if type(self).__init__ is not LGBMModel.__init__:
             # subclasses with their own __init__ signature still report the base parameters
             import inspect
 

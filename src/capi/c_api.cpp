@@ -998,9 +998,13 @@ int LGBM_NetworkInitWithFunctions(int num_machines, int rank, void* reduce_scatt
     using RSRaw = void (*)(char*, comm_size_t, int, const comm_size_t*, const comm_size_t*, int, char*, comm_size_t,
                            const ReduceFunction&);
     using AGRaw = void (*)(char*, comm_size_t, const comm_size_t*, const comm_size_t*, int, char*, comm_size_t);
-    auto rs = reinterpret_cast<RSRaw>(reduce_scatter_ext_fun);
+    if (allgather_ext_fun == nullptr) Log::Fatal("LGBM_NetworkInitWithFunctions needs an allgather function");
     auto ag = reinterpret_cast<AGRaw>(allgather_ext_fun);
-    Network::Init(num_machines, rank, rs, ag);
+    // a null reduce-scatter (e.g. a Python / torch.distributed allgather-only transport) is
+    // served by allgather + local reduction inside Network
+    ReduceScatterFunction rs = nullptr;
+    if (reduce_scatter_ext_fun != nullptr) rs = reinterpret_cast<RSRaw>(reduce_scatter_ext_fun);
+    Network::Init(num_machines, rank, rs, AllgatherFunction(ag));
   }
   API_END();
 }

@@ -93,6 +93,17 @@ void Network::ReduceScatter(char* input, comm_size_t input_size, int type_size, 
     S().ext_rs(input, input_size, type_size, block_start, block_len, n, output, output_size, reducer);
     return;
   }
+  if (S().ext_ag) {
+    // allgather-only external transport: gather every rank's input, reduce this rank's block
+    std::vector<char> all(static_cast<size_t>(input_size) * n);
+    Allgather(input, input_size, all.data());
+    const int r = S().rank;
+    std::memcpy(output, all.data() + block_start[r], block_len[r]);
+    for (int k = 0; k < n; ++k) {
+      if (k != r) reducer(all.data() + static_cast<size_t>(k) * input_size + block_start[r], output, type_size, block_len[r]);
+    }
+    return;
+  }
   S().linkers->ReduceScatter(input, input_size, type_size, block_start, block_len, output, output_size, reducer);
 }
 
