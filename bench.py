@@ -39,6 +39,7 @@ def main() -> int:
     ap.add_argument("--max-bin", type=int, default=255)
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--graph", type=int, default=None, help="device_use_graph override (1/0)")
     ap.add_argument("--rehearse-dp", action="store_true",
                     help="1 GPU: run the RCCL data-parallel learner path on a one-rank communicator")
     args = ap.parse_args()
@@ -85,6 +86,8 @@ def main() -> int:
     }
     if world > 1:
         params.update({"tree_learner": "data", "num_machines": world, "pre_partition": True})
+    if args.graph is not None:
+        params["device_use_graph"] = bool(args.graph)
     train_set = lgb.Dataset(X, y, params=params, free_raw_data=True)
     booster = lgb.Booster(params=params, train_set=train_set)
     del X

@@ -114,6 +114,7 @@ struct Args {
   // ic_leaf[leaf] = sets that hold every feature on the leaf's branch
   const unsigned long long* ic_feat;
   unsigned long long* ic_leaf;
+  double* root_part;  // per-block (sum g, sum h, max|g|, max|h|) of k_root_sums
   SplitParams sp;
 };
 
@@ -290,8 +291,12 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
   for (int f = t; f < a.F; f += blockDim.x) a.splittable[f] = 1;
 }
 
-__global__ __launch_bounds__(256) void k_root_sums(Args a) {
-  __shared__ double sh[8];
+// Root statistics in two steps: per-block partials (no atomics: 1024 blocks x
+// device-scope fp64 atomics on one address serialised to ~97 us), then one block
+// folds them and writes lsum[0] and the histogram scale maxima.
+constexpr int kRootThreads = 256;
+__global__ __launch_bounds__(kRootThreads) void k_root_sums(Args a) {
+  __shared__ double sh[4][kRootThreads / 64];
   const TreeParams tp = *a.tp;
   const float2* gh = a.gh + static_cast<size_t>(tp.cls) * a.N;
   double g = 0.0, h = 0.0;
@@ -311,24 +316,57 @@ __global__ __launch_bounds__(256) void k_root_sums(Args a) {
     mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
     mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
   }
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    atomicMax(&a.ghmax[0], __float_as_uint(mg));
-    atomicMax(&a.ghmax[1], __float_as_uint(mh));
+    sh[0][w] = g;
+    sh[1][w] = h;
+    sh[2][w] = mg;
+    sh[3][w] = mh;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double v = sh[threadIdx.x][0];
+    for (int i = 1; i < kRootThreads / 64; ++i) {
+      v = threadIdx.x < 2 ? v + sh[threadIdx.x][i] : fmax(v, sh[threadIdx.x][i]);
+    }
+    a.root_part[4 * blockIdx.x + threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(kRootThreads) void k_root_final(Args a, int nblocks) {
+  __shared__ double sh[4][kRootThreads / 64];
+  double g = 0.0, h = 0.0, mg = 0.0, mh = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
+    g += a.root_part[4 * b];
+    h += a.root_part[4 * b + 1];
+    mg = fmax(mg, a.root_part[4 * b + 2]);
+    mh = fmax(mh, a.root_part[4 * b + 3]);
+  }
+  g = WaveSum(g);
+  h = WaveSum(h);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmax(mg, __shfl_xor(mg, o, kWave));
+    mh = fmax(mh, __shfl_xor(mh, o, kWave));
   }
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    sh[w] = g;
-    sh[4 + w] = h;
+    sh[0][w] = g;
+    sh[1][w] = h;
+    sh[2][w] = mg;
+    sh[3][w] = mh;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double sg = 0.0, shh = 0.0;
-    for (int i = 0; i < 4; ++i) {
-      sg += sh[i];
-      shh += sh[4 + i];
+    for (int i = 1; i < kRootThreads / 64; ++i) {
+      g += sh[0][i];
+      h += sh[1][i];
+      mg = fmax(mg, sh[2][i]);
+      mh = fmax(mh, sh[3][i]);
     }
-    atomicAdd(&a.lsum[0].x, sg);
-    atomicAdd(&a.lsum[0].y, shh);
+    a.lsum[0] = make_double2(g, h);
+    a.ghmax[0] = __float_as_uint(static_cast<float>(mg));
+    a.ghmax[1] = __float_as_uint(static_cast<float>(mh));
   }
 }
 
@@ -1289,11 +1327,15 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
   const Ctl c = *cp;
   if (c.done) return;
   const int pbuf = c.parent_buf, pstart = c.parent_start, pcount = c.parent_count;
-  if (blockIdx.x > 0 && static_cast<int>(blockIdx.x) >= (pcount + kTileRows - 1) / kTileRows) return;
+  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
+  // the post-split bookkeeping runs on the first block without tiles (in parallel
+  // with the scatter), or after block 0's tiles when every block has tiles
+  const int post_block = ntiles < static_cast<int>(gridDim.x) ? ntiles : 0;
+  const int bid = static_cast<int>(blockIdx.x);
+  if (bid > 0 && bid >= ntiles && bid != post_block) return;
   int* out = a.idx[c.target_buf] + pstart;
   Stamp(a, 1, 0);
-  if (threadIdx.x == 0) FillSplitDesc(a, a.best[c.split_leaf], &d);
-  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
+  if (threadIdx.x == 0 && bid < ntiles) FillSplitDesc(a, a.best[c.split_leaf], &d);
   int nl = 0;
   for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += a.tile_cnt[i];
   const int nl_total = BlockSumInt(nl, sh);
@@ -1355,7 +1397,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
     __syncthreads();
   }
   Stamp(a, 1, 2);
-  if (blockIdx.x == 0 && a.fuse_post) PostSplit(a, c, nl_total);
+  if (bid == post_block && a.fuse_post) PostSplit(a, c, nl_total);
   Stamp(a, 1, 3);
 }
 
@@ -1920,6 +1962,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
  private:
+  int RootBlocks() const { return std::max(1, std::min(DivUp(N_, kRootThreads), 4 * num_cu_)); }
+
   int HistBlocks() const {
     const int want = config_->device_hist_blocks > 0 ? config_->device_hist_blocks : 2 * num_cu_;
     // partial-histogram slab: one row of 2 * TB accumulators per block, capped at 4 GiB
@@ -2094,7 +2138,8 @@ class DeviceTreeLearner : public TreeLearner {
                  o_rng = lay.Add<unsigned>(std::max(F_, 1)), o_feat = lay.Add<DevFeature>(h_feats_.size()),
                  o_gst = lay.Add<int>(h_gstart_.size()), o_tiles = lay.Add<HistTile>(h_tiles_.size()),
                  o_icf = lay.Add<unsigned long long>(std::max(F_, 1)), o_icl = lay.Add<unsigned long long>(L),
-                 o_qmax = lay.Add<unsigned>(2), o_tsum = lay.Add<double2>(L);
+                 o_qmax = lay.Add<unsigned>(2), o_tsum = lay.Add<double2>(L),
+                 o_rpart = lay.Add<double>(4 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
     arena_.Resize(std::max<size_t>(lay.bytes(), size_t(2) << 20));
     char* base = arena_.get();
     tparams_.Attach(reinterpret_cast<TreeParams*>(base + o_tp), 1);
@@ -2123,6 +2168,7 @@ class DeviceTreeLearner : public TreeLearner {
     ic_leaf_.Attach(reinterpret_cast<unsigned long long*>(base + o_icl), L);
     qmax_.Attach(reinterpret_cast<unsigned*>(base + o_qmax), 2);
     true_sums_.Attach(reinterpret_cast<double2*>(base + o_tsum), L);
+    root_part_.Attach(reinterpret_cast<double*>(base + o_rpart), 4 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
     arena_.Zero(stream_);
     use_ic_ = !config_->interaction_constraints_vector.empty();
     if (use_ic_) {
@@ -2209,6 +2255,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.monotone_penalty = config_->monotone_penalty;
     a.ic_feat = use_ic_ ? ic_feat_.get() : nullptr;
     a.ic_leaf = use_ic_ ? ic_leaf_.get() : nullptr;
+    a.root_part = root_part_.get();
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;
@@ -2233,7 +2280,9 @@ class DeviceTreeLearner : public TreeLearner {
     hipStream_t s = stream_;
     const int part_blocks = std::max(1, std::min(max_tiles_, 4 * num_cu_));
     k_init_tree<<<1, kNodeThreads, 0, s>>>(a);
-    k_root_sums<<<std::max(1, std::min(DivUp(N_, 256), 4 * num_cu_)), 256, 0, s>>>(a);
+    const int root_blocks = RootBlocks();
+    k_root_sums<<<root_blocks, kRootThreads, 0, s>>>(a);
+    k_root_final<<<1, kRootThreads, 0, s>>>(a, root_blocks);
     if (distributed_) AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
     LaunchHist(a);
     LaunchScan(a);
@@ -2357,6 +2406,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<unsigned long long> ic_feat_, ic_leaf_;
   DevBuf<unsigned> qmax_;
   DevBuf<double2> true_sums_;
+  DevBuf<double> root_part_;
   DevBuf<float2> gh_true_;
   bool use_ic_ = false, is_const_hess_ = false;
   unsigned quant_round_ = 0;
