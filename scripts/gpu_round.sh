@@ -28,6 +28,8 @@ for s in "$@"; do
     bench1m) step bench1m 400 python bench.py --rows 1000000 --steps 10 --warmup 2;;
     bench) step bench 900 python bench.py --steps 30 --warmup 3;;
     benchdp) step benchdp 900 python bench.py --steps 30 --warmup 3 --rehearse-dp;;
+    abpost) step abpost10 900 python scripts/ab_bench.py --rows 10000000 --variant device_post_mode=1 --variant device_post_mode=2 --variant device_post_mode=0 && step abpost1 900 python scripts/ab_bench.py --rows 1250000 --variant device_post_mode=1 --variant device_post_mode=2 --variant device_post_mode=0;;
+    abfused) step abfused10 900 python scripts/ab_bench.py --rows 10000000 --variant device_fused_partition=1 --variant device_fused_partition=0 && step abfused1 900 python scripts/ab_bench.py --rows 1250000 --variant device_fused_partition=1 --variant device_fused_partition=0;;
     abgraph) step ab10 900 python scripts/ab_bench.py --rows 10000000 && step ab1 900 python scripts/ab_bench.py --rows 1250000;;
     quad) step q10g 600 python bench.py --steps 30 --warmup 3 --graph 1 && step q10e 600 python bench.py --steps 30 --warmup 3 --graph 0 && step q1g 600 python bench.py --rows 1250000 --steps 50 --warmup 5 --graph 1 && step q1e 600 python bench.py --rows 1250000 --steps 50 --warmup 5 --graph 0;;
     nograph) step nograph 600 python bench.py --steps 30 --warmup 3 --graph 0 && step nographsmall 600 python bench.py --rows 1250000 --steps 50 --warmup 5 --graph 0;;
@@ -37,6 +39,7 @@ for s in "$@"; do
     pmc) step pmc 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA --kernel-trace --output-format csv -d $PWD/$OUT/pmc -o pmc -- python3 bench.py --rows 2000000 --steps 3 --warmup 1;;
     profpost) LGAP_SPLIT_POST=1 step profpost 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/profpost -o run -- python3 bench.py --steps 10 --warmup 2;;
     stamps) LGAP_STAMPS=1 step stamps 600 python bench.py --rows 10000000 --steps 2 --warmup 1;;
+    stampsmall) LGAP_STAMPS=1 step stampsmall 600 python bench.py --rows 1250000 --steps 2 --warmup 1;;
     profsmall) step profsmall 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/profsmall -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 && python scripts/prof_summary.py $OUT/profsmall "1.25M rows, graph path" 22 > $OUT/profsmall_summary.md;;
     profsmalldp) step profsmalldp 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/profsmalldp -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 --rehearse-dp && python scripts/prof_summary.py $OUT/profsmalldp "1.25M rows, DP rehearsal path" 22 > $OUT/profsmalldp_summary.md;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2;;

@@ -115,6 +115,7 @@ struct Args {
   const unsigned long long* ic_feat;
   unsigned long long* ic_leaf;
   double* root_part;  // per-block (sum g, sum h, max|g|, max|h|) of k_root_sums
+  unsigned* bar;      // grid barrier of k_partition: {arrivals, generation, error}
   SplitParams sp;
 };
 
@@ -1330,7 +1331,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
   const int ntiles = (pcount + kTileRows - 1) / kTileRows;
   // the post-split bookkeeping runs on the first block without tiles (in parallel
   // with the scatter), or after block 0's tiles when every block has tiles
-  const int post_block = ntiles < static_cast<int>(gridDim.x) ? ntiles : 0;
+  const int post_block = (a.fuse_post == 2 && ntiles < static_cast<int>(gridDim.x)) ? ntiles : 0;
   const int bid = static_cast<int>(blockIdx.x);
   if (bid > 0 && bid >= ntiles && bid != post_block) return;
   int* out = a.idx[c.target_buf] + pstart;
@@ -1399,6 +1400,198 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
   Stamp(a, 1, 2);
   if (bid == post_block && a.fuse_post) PostSplit(a, c, nl_total);
   Stamp(a, 1, 3);
+}
+
+// ---------------------------------------------------------------------------
+// Fused partition (select + count + scatter in ONE launch). The per-tile left
+// counts are exchanged through a grid barrier among the participating blocks.
+// All of them are co-resident (the host caps the grid at the occupancy limit),
+// and the exchange uses agent-scope atomics only (they bypass the per-XCD L2s),
+// so no L2 writeback / invalidate fences are needed. A bounded spin turns a
+// barrier that cannot complete into an error flag instead of a hang.
+
+__device__ __forceinline__ void AtomicStoreAgent(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int AtomicLoadAgent(const int* p) {
+  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// thread 0 of each participating block; `gen` was read before arriving
+__device__ void GridBarrier(unsigned* bar, unsigned participants, unsigned gen) {
+  __builtin_amdgcn_s_waitcnt(0);  // this block's published tile counts have landed
+  const unsigned old = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == participants - 1) {
+    __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);
+    __hip_atomic_store(&bar[1], gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  unsigned spins = 0;
+  while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 26)) {
+      __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
+  __shared__ SplitDesc d;
+  __shared__ SelState st;
+  __shared__ int sh[8];
+  __shared__ int s_wl[kPartIters][kPartThreads / 64];
+  __shared__ int s_wv[kPartIters][kPartThreads / 64];
+  __shared__ unsigned s_gen;
+  Ctl* cp = a.ctl;
+  const Ctl c = *cp;
+  if (c.done) return;
+  const int bid = static_cast<int>(blockIdx.x);
+  if (bid > 0 && bid >= (c.max_count + kTileRows - 1) / kTileRows) return;
+  if (threadIdx.x == 0) s_gen = __hip_atomic_load(&a.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  Stamp(a, 0, 0);
+  BlockSelect(a, c, &st);
+  Stamp(a, 0, 1);
+  const SplitInfo* win = st.done ? nullptr
+                                 : (st.sel >= 0 ? &a.scan_out[static_cast<size_t>(st.sel) * a.F + st.feature]
+                                                : &a.best[st.leaf]);
+  if (bid == 0) {
+    if (c.smaller >= 0 && st.new_best[0] >= 0) CopySplitInfoBlock(&a.best[c.smaller], &a.scan_out[st.new_best[0]]);
+    if (c.larger >= 0 && st.new_best[1] >= 0) {
+      CopySplitInfoBlock(&a.best[c.larger], &a.scan_out[static_cast<size_t>(a.F) + st.new_best[1]]);
+    }
+    if (threadIdx.x == 0) {
+      if (c.smaller >= 0 && st.new_best[0] < 0) a.best[c.smaller].Reset();
+      if (c.larger >= 0 && st.new_best[1] < 0) a.best[c.larger].Reset();
+      if (!c.skip) cp->scan_round = c.scan_round + 1;
+      if (st.done) cp->done = 1;
+    }
+  }
+  if (st.done) return;
+  const LeafRange pr = a.range[st.leaf];
+  if (threadIdx.x == 0) FillSplitDesc(a, *win, &d);
+  const int ntiles = (pr.count + kTileRows - 1) / kTileRows;
+  const int participants = ntiles < static_cast<int>(gridDim.x) ? ntiles : static_cast<int>(gridDim.x);
+  if (bid >= participants) return;
+  __syncthreads();
+  Stamp(a, 0, 2);
+  const int pbuf = pr.buf, pstart = pr.start, pcount = pr.count;
+  const int tbuf = pbuf == 0 ? 1 : 0;
+  // phase 1: count this block's tiles (the first tile's rows stay in registers)
+  int rows0[kPartIters];
+  uint32_t gb0[kPartIters];
+  for (int tile = bid; tile < ntiles; tile += gridDim.x) {
+    int rows[kPartIters];
+    const int pos0 = tile * kTileRows + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) {
+      const int pos = pos0 + k * kPartThreads;
+      rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
+    }
+    uint32_t gb[kPartIters];
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) cnt += (rows[k] >= 0 && GoLeft(d, gb[k])) ? 1 : 0;
+    cnt = BlockSumInt(cnt, sh);
+    if (threadIdx.x == 0) AtomicStoreAgent(&a.tile_cnt[tile], cnt);
+    if (tile == bid) {
+#pragma unroll
+      for (int k = 0; k < kPartIters; ++k) {
+        rows0[k] = rows[k];
+        gb0[k] = gb[k];
+      }
+    }
+  }
+  Stamp(a, 0, 3);
+  if (threadIdx.x == 0) GridBarrier(a.bar, static_cast<unsigned>(participants), s_gen);
+  __syncthreads();
+  Stamp(a, 1, 0);
+  // phase 2: prefix over the published counts, scatter (lefts from the front, rights after them)
+  int nl = 0;
+  for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += AtomicLoadAgent(&a.tile_cnt[i]);
+  const int nl_total = BlockSumInt(nl, sh);
+  Stamp(a, 1, 1);
+  int* out = a.idx[tbuf] + pstart;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int tile = bid; tile < ntiles; tile += gridDim.x) {
+    int pre = 0;
+    for (int i = threadIdx.x; i < tile; i += blockDim.x) pre += AtomicLoadAgent(&a.tile_cnt[i]);
+    int lbase = BlockSumInt(pre, sh);
+    int rbase = tile * kTileRows - lbase;
+    int rows[kPartIters];
+    uint32_t gb[kPartIters];
+    if (tile == bid) {
+#pragma unroll
+      for (int k = 0; k < kPartIters; ++k) {
+        rows[k] = rows0[k];
+        gb[k] = gb0[k];
+      }
+    } else {
+      const int pos0 = tile * kTileRows + threadIdx.x;
+#pragma unroll
+      for (int k = 0; k < kPartIters; ++k) {
+        const int pos = pos0 + k * kPartThreads;
+        rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) {
+      const bool valid = rows[k] >= 0;
+      const bool left = valid && GoLeft(d, gb[k]);
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      if (lane == 0) {
+        s_wl[k][w] = __popcll(ml);
+        s_wv[k][w] = __popcll(mv);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPartIters; ++k) {
+      const bool valid = rows[k] >= 0;
+      const bool left = valid && GoLeft(d, gb[k]);
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      int pl = 0, pv = 0, tl = 0, tv = 0;
+#pragma unroll
+      for (int i = 0; i < kPartThreads / 64; ++i) {
+        if (i < w) {
+          pl += s_wl[k][i];
+          pv += s_wv[k][i];
+        }
+        tl += s_wl[k][i];
+        tv += s_wv[k][i];
+      }
+      if (valid) {
+        const int rl = pl + __popcll(ml & lt_mask);
+        const int rv = pv + __popcll(mv & lt_mask);
+        if (left) out[lbase + rl] = rows[k];
+        else out[nl_total + rbase + (rv - rl)] = rows[k];
+      }
+      lbase += tl;
+      rbase += tv - tl;
+    }
+    __syncthreads();
+  }
+  Stamp(a, 1, 2);
+  if (bid == 0) {
+    // the post-split bookkeeping reads the parent fields from ctl
+    Ctl pc = c;
+    pc.split_leaf = st.leaf;
+    pc.new_leaf = c.num_leaves;
+    pc.parent_buf = pbuf;
+    pc.parent_start = pstart;
+    pc.parent_count = pcount;
+    pc.target_buf = tbuf;
+    if (!c.skip) pc.scan_round = c.scan_round + 1;
+    PostSplit(a, pc, nl_total);
+  }
 }
 
 __global__ __launch_bounds__(kPartThreads) void k_post(Args a) {
@@ -1768,7 +1961,10 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(hr, rec_.get(), sizeof(SplitRec) * (L_ - 1), hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(hrange, range_.get(), sizeof(LeafRange) * L_, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(hlo, lout_.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
+    unsigned* hbar = pin_bar_.Get(4);
+    HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    if (hbar[2] != 0u) Log::Fatal("k_partition grid barrier timed out (blocks not co-resident?)");
     auto tree = std::make_unique<Tree>(L_, false, false);
     tree->SetLeafOutput(0, hlo[0]);
     for (int s = 0; s < hc->num_splits; ++s) {
@@ -2125,6 +2321,15 @@ class DeviceTreeLearner : public TreeLearner {
   void AllocState() {
     const size_t L = L_;
     max_tiles_ = std::max(1, DivUp(N_, kTileRows));
+    fused_blocks_ = 0;
+    if (config_->device_fused_partition) {
+      // every participating block must be resident at once for the grid barrier
+      int per_cu = 0;
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_partition, kPartThreads, 0));
+      const int cap = per_cu * num_cu_;
+      fused_blocks_ = std::min({max_tiles_, 4 * num_cu_, cap});
+      if (fused_blocks_ < 1) fused_blocks_ = 0;
+    }
     use_bynode_ = config_->feature_fraction_bynode < 1.0;
     // every small per-tree structure + the static feature metadata in one allocation
     ArenaLayout lay;
@@ -2139,7 +2344,8 @@ class DeviceTreeLearner : public TreeLearner {
                  o_gst = lay.Add<int>(h_gstart_.size()), o_tiles = lay.Add<HistTile>(h_tiles_.size()),
                  o_icf = lay.Add<unsigned long long>(std::max(F_, 1)), o_icl = lay.Add<unsigned long long>(L),
                  o_qmax = lay.Add<unsigned>(2), o_tsum = lay.Add<double2>(L),
-                 o_rpart = lay.Add<double>(4 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
+                 o_rpart = lay.Add<double>(4 * static_cast<size_t>(std::max(1, 4 * num_cu_))),
+                 o_bar = lay.Add<unsigned>(4);
     arena_.Resize(std::max<size_t>(lay.bytes(), size_t(2) << 20));
     char* base = arena_.get();
     tparams_.Attach(reinterpret_cast<TreeParams*>(base + o_tp), 1);
@@ -2169,6 +2375,7 @@ class DeviceTreeLearner : public TreeLearner {
     qmax_.Attach(reinterpret_cast<unsigned*>(base + o_qmax), 2);
     true_sums_.Attach(reinterpret_cast<double2*>(base + o_tsum), L);
     root_part_.Attach(reinterpret_cast<double*>(base + o_rpart), 4 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
+    bar_.Attach(reinterpret_cast<unsigned*>(base + o_bar), 4);
     arena_.Zero(stream_);
     use_ic_ = !config_->interaction_constraints_vector.empty();
     if (use_ic_) {
@@ -2248,7 +2455,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.max_cat_bin = max_cat_bin_;
     a.max_bin = max_bin_;
     a.max_depth = config_->max_depth;
-    a.fuse_post = getenv("LGAP_SPLIT_POST") ? 0 : 1;
+    // 0: separate k_post kernel, 1: block 0 after its tiles, 2: first spare block
+    a.fuse_post = getenv("LGAP_SPLIT_POST") ? 0 : config_->device_post_mode;
     a.stamps = stamps_.size() ? stamps_.get() : nullptr;
     a.distributed = distributed_ ? 1 : 0;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
@@ -2256,6 +2464,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.ic_feat = use_ic_ ? ic_feat_.get() : nullptr;
     a.ic_leaf = use_ic_ ? ic_leaf_.get() : nullptr;
     a.root_part = root_part_.get();
+    a.bar = bar_.get();
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;
@@ -2287,9 +2496,13 @@ class DeviceTreeLearner : public TreeLearner {
     LaunchHist(a);
     LaunchScan(a);
     for (int it = 0; it < L_ - 1; ++it) {
-      k_part_count<<<part_blocks, kPartThreads, 0, s>>>(a);
-      k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(a);
-      if (!a.fuse_post) k_post<<<1, kPartThreads, 0, s>>>(a);
+      if (fused_blocks_ > 0) {
+        k_partition<<<fused_blocks_, kPartThreads, 0, s>>>(a);
+      } else {
+        k_part_count<<<part_blocks, kPartThreads, 0, s>>>(a);
+        k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(a);
+        if (!a.fuse_post) k_post<<<1, kPartThreads, 0, s>>>(a);
+      }
       if (it < L_ - 2) {
         LaunchHist(a);
         LaunchScan(a);
@@ -2407,6 +2620,9 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<unsigned> qmax_;
   DevBuf<double2> true_sums_;
   DevBuf<double> root_part_;
+  DevBuf<unsigned> bar_;
+  PinnedBuf<unsigned> pin_bar_;
+  int fused_blocks_ = 0;  // k_partition grid (0: two-kernel partition)
   DevBuf<float2> gh_true_;
   bool use_ic_ = false, is_const_hess_ = false;
   unsigned quant_round_ = 0;
