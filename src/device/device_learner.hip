@@ -269,6 +269,8 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     c.cls = tp.cls;
     c.scan_round = 0;
     c.max_count = tp.root_count;
+    c.hist_nb = 0;
+    c.pad0 = c.pad1 = c.pad2 = 0;
     *a.ctl = c;
     LeafRange r;
     r.buf = tp.root_buf;
@@ -567,7 +569,7 @@ __global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid) {
   const Ctl* cp = a.ctl;
   if (cp->done || cp->skip) return;
   const int n = a.range[cp->smaller].count;
-  const int nb = HistActiveBlocks(n, hist_grid);
+  const int nb = cp->hist_nb > 0 ? cp->hist_nb : HistActiveBlocks(n, hist_grid);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const size_t V = 2 * static_cast<size_t>(a.TB);
   const size_t v = static_cast<size_t>(blockIdx.x) * 64 + lane;
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
   const int n_small = a.range[c.smaller].count;
   // single GPU: sum the histogram blocks' slab rows here; data-parallel: the
   // all-reduced histogram already sits in `staging` (one row of doubles)
-  const int nb = from_staging ? 1 : HistActiveBlocks(n_small, hist_grid);
+  const int nb = from_staging ? 1 : (c.hist_nb > 0 ? c.hist_nb : HistActiveBlocks(n_small, hist_grid));
   const size_t V = 2 * static_cast<size_t>(a.TB);
   const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
   const Acc* slab = from_staging ? reinterpret_cast<const Acc*>(a.staging) : reinterpret_cast<const Acc*>(a.hist_slab);
@@ -1437,7 +1439,12 @@ __device__ void GridBarrier(unsigned* bar, unsigned participants, unsigned gen) 
   }
 }
 
+// HIST: also build the smaller child's histogram while scattering (whole-row
+// fixed-point accumulation into LDS, one slab row per participating block), so
+// no separate k_hist launch is needed for this split.
+template <int W, bool HIST>
 __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
+  extern __shared__ __align__(8) unsigned char part_lds[];
   __shared__ SplitDesc d;
   __shared__ SelState st;
   __shared__ int sh[8];
@@ -1514,6 +1521,39 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += AtomicLoadAgent(&a.tile_cnt[i]);
   const int nl_total = BlockSumInt(nl, sh);
   Stamp(a, 1, 1);
+  // smaller child and whether its histogram is needed at all (PostSplit's rule, replicated)
+  bool do_hist = false, hist_left = false;
+  unsigned long long* lhist = reinterpret_cast<unsigned long long*>(part_lds);
+  int* lgst = nullptr;
+  float hsg = 1.f, hsh = 1.f;
+  if (HIST) {
+    const int glc = a.distributed ? win->left_count : nl_total;
+    const int grc = a.distributed ? win->right_count : pcount - nl_total;
+    const int dep = a.depth[st.leaf] + 1;
+    const int md = a.sp.min_data_in_leaf;
+    do_hist = !((a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2));
+    hist_left = glc < grc;
+    const HistTile tile = a.tiles[0];
+    lgst = reinterpret_cast<int*>(lhist + tile.nbins);
+    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) lhist[i] = 0ull;
+    for (int g = threadIdx.x; g < a.num_groups; g += blockDim.x) lgst[g] = a.gstart[g];
+    // rows of the smaller child in this block's tiles bound the fixed-point scale
+    int mine = 0;
+    for (int tile_i = bid; tile_i < ntiles; tile_i += gridDim.x) {
+      if (threadIdx.x == 0) {
+        const int tl = AtomicLoadAgent(&a.tile_cnt[tile_i]);
+        const int trows = min(kTileRows, pcount - tile_i * kTileRows);
+        mine += hist_left ? tl : trows - tl;
+      }
+    }
+    if (threadIdx.x == 0) sh[7] = mine;
+    __syncthreads();
+    const double rows_in_block = static_cast<double>(sh[7] > 0 ? sh[7] : 1);
+    const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
+    const double kPk = 1073741824.0;  // 2^30
+    hsg = static_cast<float>(gmax > 0.f ? kPk / (rows_in_block * gmax) : 1.0) * 0.99999f;
+    hsh = static_cast<float>(hmax > 0.f ? kPk / (rows_in_block * hmax) : 1.0) * 0.99999f;
+  }
   int* out = a.idx[tbuf] + pstart;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1577,7 +1617,56 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
       lbase += tl;
       rbase += tv - tl;
     }
+    if (HIST && do_hist) {
+      // whole rows of the smaller child: 4 rows' packed words in flight per step
+      const float2* gh = a.gh + static_cast<size_t>(c.cls) * a.N;
+      constexpr int per = 4 / W;
+      const int nd = (a.num_groups + per - 1) / per;
+#pragma unroll
+      for (int k0 = 0; k0 < kPartIters; k0 += 4) {
+        int hr[4];
+        float2 hv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + j;
+          const bool take = rows[k] >= 0 && (GoLeft(d, gb[k]) == hist_left);
+          hr[j] = take ? rows[k] : -1;
+          hv[j] = take ? gh[rows[k]] : make_float2(0.f, 0.f);
+        }
+        for (int dw = 0; dw < nd; ++dw) {
+          uint32_t wd[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wd[j] = hr[j] >= 0 ? a.rowbins[static_cast<size_t>(hr[j]) * a.stride_dw + dw] : 0u;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (hr[j] < 0) continue;
+            const long long ig = __float2int_rn(hv[j].x * hsg);
+            const long long ih = __float2int_rn(hv[j].y * hsh);
+            const unsigned long long pg = (static_cast<unsigned long long>(ig) << 32) + static_cast<unsigned long long>(ih);
+#pragma unroll
+            for (int q = 0; q < per; ++q) {
+              const int g = dw * per + q;
+              const uint32_t b = W == 1 ? ((wd[j] >> (8 * q)) & 0xFFu) : ((wd[j] >> (16 * q)) & 0xFFFFu);
+              if (b != 0u && g < a.num_groups) atomicAdd(&lhist[lgst[g] + static_cast<int>(b)], pg);
+            }
+          }
+        }
+      }
+    }
     __syncthreads();
+  }
+  if (HIST) {
+    // this block's slab row (zeros when the split needs no histogram: the scan is skipped then)
+    const HistTile tile = a.tiles[0];
+    float* slabf = reinterpret_cast<float*>(a.hist_slab) + static_cast<size_t>(bid) * a.TB * 2;
+    const double ig = 1.0 / static_cast<double>(hsg), ih = 1.0 / static_cast<double>(hsh);
+    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
+      const unsigned long long x = lhist[i];
+      const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
+      const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
+      slabf[2 * i] = static_cast<float>(static_cast<double>(gs) * ig);
+      slabf[2 * i + 1] = static_cast<float>(static_cast<double>(hs) * ih);
+    }
   }
   Stamp(a, 1, 2);
   if (bid == 0) {
@@ -1590,6 +1679,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     pc.parent_count = pcount;
     pc.target_buf = tbuf;
     if (!c.skip) pc.scan_round = c.scan_round + 1;
+    pc.hist_nb = HIST ? participants : 0;
     PostSplit(a, pc, nl_total);
   }
 }
@@ -2322,14 +2412,29 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t L = L_;
     max_tiles_ = std::max(1, DivUp(N_, kTileRows));
     fused_blocks_ = 0;
+    // the histogram rides in the partition kernel when one LDS tile covers every
+    // group in packed fixed point (the common case: <= ~7K total bins)
+    fused_hist_ = config_->device_fused_partition && config_->device_fused_hist && !use_dp_ && num_tiles_ == 1 &&
+                  !h_tiles_[0].direct;
     if (config_->device_fused_partition) {
       // every participating block must be resident at once for the grid barrier
       int per_cu = 0;
-      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_partition, kPartThreads, 0));
+      if (fused_hist_) {
+        const void* fn = width_ == 1 ? reinterpret_cast<const void*>(k_partition<1, true>)
+                                     : reinterpret_cast<const void*>(k_partition<2, true>);
+        if (hist_lds_bytes_ > 64 * 1024) {
+          HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
+        }
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kPartThreads, hist_lds_bytes_));
+      } else {
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_partition<1, false>, kPartThreads, 0));
+      }
       const int cap = per_cu * num_cu_;
       fused_blocks_ = std::min({max_tiles_, 4 * num_cu_, cap});
       if (fused_blocks_ < 1) fused_blocks_ = 0;
+      if (fused_hist_) fused_blocks_ = std::min(fused_blocks_, HistBlocks());  // slab rows
     }
+    if (fused_blocks_ == 0) fused_hist_ = false;
     use_bynode_ = config_->feature_fraction_bynode < 1.0;
     // every small per-tree structure + the static feature metadata in one allocation
     ArenaLayout lay;
@@ -2497,14 +2602,27 @@ class DeviceTreeLearner : public TreeLearner {
     LaunchScan(a);
     for (int it = 0; it < L_ - 1; ++it) {
       if (fused_blocks_ > 0) {
-        k_partition<<<fused_blocks_, kPartThreads, 0, s>>>(a);
+        if (fused_hist_) {
+          if (width_ == 1) k_partition<1, true><<<fused_blocks_, kPartThreads, hist_lds_bytes_, s>>>(a);
+          else k_partition<2, true><<<fused_blocks_, kPartThreads, hist_lds_bytes_, s>>>(a);
+        } else {
+          k_partition<1, false><<<fused_blocks_, kPartThreads, 0, s>>>(a);
+        }
       } else {
         k_part_count<<<part_blocks, kPartThreads, 0, s>>>(a);
         k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(a);
         if (!a.fuse_post) k_post<<<1, kPartThreads, 0, s>>>(a);
       }
       if (it < L_ - 2) {
-        LaunchHist(a);
+        if (fused_hist_) {
+          // the partition kernel left the smaller child's histogram in the slab
+          if (distributed_) {
+            LaunchHistReduce(a);
+            AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), stream_);
+          }
+        } else {
+          LaunchHist(a);
+        }
         LaunchScan(a);
       }
     }
@@ -2623,6 +2741,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<unsigned> bar_;
   PinnedBuf<unsigned> pin_bar_;
   int fused_blocks_ = 0;  // k_partition grid (0: two-kernel partition)
+  bool fused_hist_ = false;
   DevBuf<float2> gh_true_;
   bool use_ic_ = false, is_const_hess_ = false;
   unsigned quant_round_ = 0;

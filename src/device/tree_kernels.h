@@ -60,6 +60,8 @@ struct Ctl {
   int skip, num_splits, split_leaf, new_leaf;
   int parent_buf, parent_start, parent_count, target_buf;
   int left_count, cls, scan_round, max_count;  // max_count: largest leaf (rows), bounds useful grid size
+  int hist_nb;  // slab rows holding the smaller child's histogram when k_partition built it (0: k_hist did)
+  int pad0, pad1, pad2;
 };
 
 struct SplitRec {
