@@ -2412,8 +2412,9 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t L = L_;
     max_tiles_ = std::max(1, DivUp(N_, kTileRows));
     fused_blocks_ = 0;
-    // the histogram rides in the partition kernel when one LDS tile covers every
-    // group in packed fixed point (the common case: <= ~7K total bins)
+    // optionally the histogram rides in the partition kernel (one LDS tile, packed
+    // fixed point). Measured slower than k_hist (whole-row threads, half the lanes
+    // idle on the larger child, 2 blocks/CU): off by default, kept for A/B runs.
     fused_hist_ = config_->device_fused_partition && config_->device_fused_hist && !use_dp_ && num_tiles_ == 1 &&
                   !h_tiles_[0].direct;
     if (config_->device_fused_partition) {
