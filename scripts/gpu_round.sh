@@ -31,6 +31,7 @@ for s in "$@"; do
     abpost) step abpost10 900 python scripts/ab_bench.py --rows 10000000 --variant device_post_mode=1 --variant device_post_mode=2 --variant device_post_mode=0 && step abpost1 900 python scripts/ab_bench.py --rows 1250000 --variant device_post_mode=1 --variant device_post_mode=2 --variant device_post_mode=0;;
     abfused) step abfused10 900 python scripts/ab_bench.py --rows 10000000 --variant device_fused_partition=1 --variant device_fused_partition=0 && step abfused1 900 python scripts/ab_bench.py --rows 1250000 --variant device_fused_partition=1 --variant device_fused_partition=0;;
     abhist) step abhist10 900 python scripts/ab_bench.py --rows 10000000 --variant device_fused_hist=1 --variant device_fused_hist=0 && step abhist1 900 python scripts/ab_bench.py --rows 1250000 --variant device_fused_hist=1 --variant device_fused_hist=0;;
+    abminrows) step abmr10 900 python scripts/ab_bench.py --rows 10000000 --variant device_hist_min_rows=2048 --variant device_hist_min_rows=1024 --variant device_hist_min_rows=512 --variant device_hist_min_rows=4096 && step abmr1 900 python scripts/ab_bench.py --rows 1250000 --variant device_hist_min_rows=2048 --variant device_hist_min_rows=1024 --variant device_hist_min_rows=512;;
     abgraph) step ab10 900 python scripts/ab_bench.py --rows 10000000 && step ab1 900 python scripts/ab_bench.py --rows 1250000;;
     quad) step q10g 600 python bench.py --steps 30 --warmup 3 --graph 1 && step q10e 600 python bench.py --steps 30 --warmup 3 --graph 0 && step q1g 600 python bench.py --rows 1250000 --steps 50 --warmup 5 --graph 1 && step q1e 600 python bench.py --rows 1250000 --steps 50 --warmup 5 --graph 0;;
     nograph) step nograph 600 python bench.py --steps 30 --warmup 3 --graph 0 && step nographsmall 600 python bench.py --rows 1250000 --steps 50 --warmup 5 --graph 0;;

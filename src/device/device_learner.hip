@@ -116,6 +116,7 @@ struct Args {
   unsigned long long* ic_leaf;
   double* root_part;  // per-block (sum g, sum h, max|g|, max|h|) of k_root_sums
   unsigned* bar;      // grid barrier of k_partition: {arrivals, generation, error}
+  int hist_min_rows;  // rows per k_hist block (fewer rows: more blocks and slab rows)
   SplitParams sp;
 };
 
@@ -392,8 +393,8 @@ __global__ __launch_bounds__(kRootThreads) void k_root_final(Args a, int nblocks
 // its own slab row (plain coalesced stores); k_hist_reduce sums the rows into
 // `staging` (fp64). No float atomics anywhere on the hot path.
 
-__device__ __forceinline__ int HistActiveBlocks(int n, int grid) {
-  int nb = (n + kHistMinRows - 1) / kHistMinRows;
+__device__ __forceinline__ int HistActiveBlocks(int n, int grid, int min_rows) {
+  int nb = (n + min_rows - 1) / min_rows;
   return nb > grid ? grid : nb;
 }
 
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   const HistTile tile = a.tiles[blockIdx.y];
   const LeafRange r = a.range[leaf];
   const int n = r.count;
-  const int nb = HistActiveBlocks(n, gridDim.x);
+  const int nb = HistActiveBlocks(n, gridDim.x, a.hist_min_rows);
   if (static_cast<int>(blockIdx.x) >= nb) return;
   const int chunk = (n + nb - 1) / nb;
   const int rb = blockIdx.x * chunk;
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid) {
   const Ctl* cp = a.ctl;
   if (cp->done || cp->skip) return;
   const int n = a.range[cp->smaller].count;
-  const int nb = cp->hist_nb > 0 ? cp->hist_nb : HistActiveBlocks(n, hist_grid);
+  const int nb = cp->hist_nb > 0 ? cp->hist_nb : HistActiveBlocks(n, hist_grid, a.hist_min_rows);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const size_t V = 2 * static_cast<size_t>(a.TB);
   const size_t v = static_cast<size_t>(blockIdx.x) * 64 + lane;
@@ -798,7 +799,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
   const int n_small = a.range[c.smaller].count;
   // single GPU: sum the histogram blocks' slab rows here; data-parallel: the
   // all-reduced histogram already sits in `staging` (one row of doubles)
-  const int nb = from_staging ? 1 : (c.hist_nb > 0 ? c.hist_nb : HistActiveBlocks(n_small, hist_grid));
+  const int nb = from_staging ? 1 : (c.hist_nb > 0 ? c.hist_nb : HistActiveBlocks(n_small, hist_grid, a.hist_min_rows));
   const size_t V = 2 * static_cast<size_t>(a.TB);
   const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
   const Acc* slab = from_staging ? reinterpret_cast<const Acc*>(a.staging) : reinterpret_cast<const Acc*>(a.hist_slab);
@@ -1695,6 +1696,21 @@ __global__ __launch_bounds__(kPartThreads) void k_post(Args a) {
 }
 
 // ---------------------------------------------------------------------------
+// score update of the tree just grown: its final leaf ranges already list every
+// row (no bagging), so each leaf adds its value to its rows — one pass over the
+// row indices instead of a per-row tree traversal (serial_tree_learner
+// AddPredictionToScore via the data partition).
+__global__ __launch_bounds__(256) void k_add_leaves(Args a, const double* __restrict__ leaf_value,
+                                                    double* __restrict__ score) {
+  const int leaf = blockIdx.y;
+  const LeafRange r = a.range[leaf];
+  const double v = leaf_value[leaf];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < r.count; i += gridDim.x * blockDim.x) {
+    score[RowAt(a, r.buf, r.start + i)] += v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // score update: traverse one uploaded tree over the packed rows
 
 __global__ __launch_bounds__(256) void k_add_tree(const uint32_t* __restrict__ rowbins, int stride_dw, int width,
@@ -1958,6 +1974,24 @@ class DeviceTreeLearner : public TreeLearner {
       return;
     }
     if (tree->is_linear()) Log::Fatal("Linear trees cannot be applied on the device");
+    if (tree == last_trained_ && !use_bag_ && tree->num_leaves() == static_cast<int>(h_range_.size())) {
+      last_trained_ = nullptr;
+      const int nl = tree->num_leaves();
+      double* lv = reinterpret_cast<double*>(pin_tree_.Get(sizeof(double) * nl));
+      int mx = 1;
+      for (int l = 0; l < nl; ++l) {
+        lv[l] = tree->LeafOutput(l);
+        mx = std::max(mx, h_range_[l].count);
+      }
+      tree_buf_.Resize(std::max(tree_buf_.size(), sizeof(double) * nl));
+      HIP_CHECK(hipMemcpyAsync(tree_buf_.get(), lv, sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
+      const dim3 grid(std::max(1, std::min(DivUp(mx, 256), 4 * num_cu_ / std::max(1, nl) + 1)), nl);
+      k_add_leaves<<<grid, 256, 0, stream_>>>(MakeArgs(), reinterpret_cast<const double*>(tree_buf_.get()), s);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      return;
+    }
+    last_trained_ = nullptr;
     const int nn = tree->num_leaves() - 1;
     const auto& cb = tree->cat_boundaries_inner();
     const auto& ct = tree->cat_threshold_inner();
@@ -2087,6 +2121,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (config_->use_quantized_grad && config_->quant_train_renew_leaf) RenewQuantizedLeaves(tree.get());
     if (stamps_.size() && ++stamp_trees_ == 3) ReportStamps(hc->num_splits);
     tree->RecomputeMaxDepth();
+    last_trained_ = tree.get();
     return tree;
   }
 
@@ -2248,6 +2283,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
  private:
+  int HistMinRows() const { return config_->device_hist_min_rows > 0 ? config_->device_hist_min_rows : kHistMinRows; }
+
   int RootBlocks() const { return std::max(1, std::min(DivUp(N_, kRootThreads), 4 * num_cu_)); }
 
   int HistBlocks() const {
@@ -2255,7 +2292,7 @@ class DeviceTreeLearner : public TreeLearner {
     // partial-histogram slab: one row of 2 * TB accumulators per block, capped at 4 GiB
     const size_t row_bytes = 2 * static_cast<size_t>(TB_) * (use_dp_ ? 8 : 4);
     const int mem_cap = static_cast<int>(std::max<size_t>(1, (size_t(4) << 30) / std::max<size_t>(row_bytes, 1)));
-    return std::max(1, std::min({want, DivUp(N_, kHistMinRows), mem_cap}));
+    return std::max(1, std::min({want, DivUp(N_, HistMinRows()), mem_cap}));
   }
 
   void LaunchHist(const Args& a) {
@@ -2571,6 +2608,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.ic_leaf = use_ic_ ? ic_leaf_.get() : nullptr;
     a.root_part = root_part_.get();
     a.bar = bar_.get();
+    a.hist_min_rows = HistMinRows();
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;
@@ -2743,6 +2781,7 @@ class DeviceTreeLearner : public TreeLearner {
   PinnedBuf<unsigned> pin_bar_;
   int fused_blocks_ = 0;  // k_partition grid (0: two-kernel partition)
   bool fused_hist_ = false;
+  const Tree* last_trained_ = nullptr;  // DeviceTrain's tree: its leaf ranges are still on the device
   DevBuf<float2> gh_true_;
   bool use_ic_ = false, is_const_hess_ = false;
   unsigned quant_round_ = 0;
