@@ -62,7 +62,7 @@ namespace device {
 namespace {
 
 constexpr int kHistThreads = 512;
-constexpr int kHistMinRows = 2048;
+constexpr int kHistMinRows = 1024;  // A/B on MI355X: 1024 beats 2048 / 512 / 4096 at 1.25M and 10M rows
 constexpr int kHistLdsBytes = 56 * 1024;
 constexpr int kPartThreads = 256;
 constexpr int kPartIters = 16;
@@ -1481,7 +1481,12 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   if (threadIdx.x == 0) FillSplitDesc(a, *win, &d);
   const int ntiles = (pr.count + kTileRows - 1) / kTileRows;
   const int participants = ntiles < static_cast<int>(gridDim.x) ? ntiles : static_cast<int>(gridDim.x);
-  if (bid >= participants) return;
+  // a spare block (if any) joins the barrier only to run the post-split bookkeeping
+  // concurrently with the scatter; otherwise block 0 runs it after its tiles
+  const bool has_post_block = participants < static_cast<int>(gridDim.x);
+  const int post_block = has_post_block ? participants : 0;
+  const int arrivals = participants + (has_post_block ? 1 : 0);
+  if (bid >= participants && bid != post_block) return;
   __syncthreads();
   Stamp(a, 0, 2);
   const int pbuf = pr.buf, pstart = pr.start, pcount = pr.count;
@@ -1514,7 +1519,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     }
   }
   Stamp(a, 0, 3);
-  if (threadIdx.x == 0) GridBarrier(a.bar, static_cast<unsigned>(participants), s_gen);
+  if (threadIdx.x == 0) GridBarrier(a.bar, static_cast<unsigned>(arrivals), s_gen);
   __syncthreads();
   Stamp(a, 1, 0);
   // phase 2: prefix over the published counts, scatter (lefts from the front, rights after them)
@@ -1670,7 +1675,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     }
   }
   Stamp(a, 1, 2);
-  if (bid == 0) {
+  if (bid == post_block) {
     // the post-split bookkeeping reads the parent fields from ctl
     Ctl pc = c;
     pc.split_leaf = st.leaf;
