@@ -1433,7 +1433,10 @@ __device__ void GridBarrier(unsigned* bar, unsigned participants, unsigned gen) 
   unsigned spins = 0;
   while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 26)) {
+    // a barrier that cannot complete (or an earlier failure) ends the wait: the
+    // host sees the sticky error flag after the tree and fails loudly
+    if ((++spins & 1023u) == 0u &&
+        (spins > (1u << 22) || __hip_atomic_load(&bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
       __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
@@ -1456,7 +1459,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   const Ctl c = *cp;
   if (c.done) return;
   const int bid = static_cast<int>(blockIdx.x);
-  if (bid > 0 && bid >= (c.max_count + kTileRows - 1) / kTileRows) return;
+  // no leaf has more tiles than this; one block beyond may be the post-split block
+  if (bid > (c.max_count + kTileRows - 1) / kTileRows) return;
   if (threadIdx.x == 0) s_gen = __hip_atomic_load(&a.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   Stamp(a, 0, 0);
   BlockSelect(a, c, &st);
