@@ -1204,11 +1204,14 @@ __global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
 // Post-split bookkeeping (BeforeFindBestSplit of the two children); run by
 // block 0 of k_part_scatter after its own tiles. Touches only state that no
 // other k_part_scatter block reads. All loads are issued before any store.
-__device__ void PostSplit(const Args& a, const Ctl& c, int left_count) {
+// `win` is the applied split: best[split_leaf] in the two-kernel path, or the
+// record the fused kernel selected from (visible to every block: written by an
+// earlier kernel, unlike best[] entries persisted by block 0 in the same launch).
+__device__ void PostSplit(const Args& a, const Ctl& c, int left_count, const SplitInfo* win) {
   __shared__ int s_skip, s_from, s_to;
   const int l = c.split_leaf, r = c.new_leaf;
   if (threadIdx.x == 0) {
-    const SplitInfo& bi = a.best[l];
+    const SplitInfo& bi = *win;
     const double lsg = bi.left_sum_gradient, lsh = bi.left_sum_hessian;
     const double rsg = bi.right_sum_gradient, rsh = bi.right_sum_hessian;
     const double lo = bi.left_output, ro = bi.right_output;
@@ -1290,7 +1293,7 @@ __device__ void PostSplit(const Args& a, const Ctl& c, int left_count) {
     s_skip = skip ? 1 : 0;
   }
   // the split record (dword-parallel copy of the winning SplitInfo)
-  CopySplitInfoBlock(&a.rec[c.num_splits].info, &a.best[l]);
+  CopySplitInfoBlock(&a.rec[c.num_splits].info, win);
   // largest leaf after this split (grid bound of the next partition kernels)
   {
     __shared__ int s_mx[kPartThreads / 64];
@@ -1401,7 +1404,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
     __syncthreads();
   }
   Stamp(a, 1, 2);
-  if (bid == post_block && a.fuse_post) PostSplit(a, c, nl_total);
+  if (bid == post_block && a.fuse_post) PostSplit(a, c, nl_total, &a.best[c.split_leaf]);
   Stamp(a, 1, 3);
 }
 
@@ -1690,7 +1693,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     pc.target_buf = tbuf;
     if (!c.skip) pc.scan_round = c.scan_round + 1;
     pc.hist_nb = HIST ? participants : 0;
-    PostSplit(a, pc, nl_total);
+    PostSplit(a, pc, nl_total, win);
   }
 }
 
@@ -1701,7 +1704,7 @@ __global__ __launch_bounds__(kPartThreads) void k_post(Args a) {
   const int ntiles = (c.parent_count + kTileRows - 1) / kTileRows;
   int nl = 0;
   for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += a.tile_cnt[i];
-  PostSplit(a, c, BlockSumInt(nl, sh));
+  PostSplit(a, c, BlockSumInt(nl, sh), &a.best[c.split_leaf]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2100,9 +2103,13 @@ class DeviceTreeLearner : public TreeLearner {
     if (hbar[2] != 0u) Log::Fatal("k_partition grid barrier timed out (blocks not co-resident?)");
     auto tree = std::make_unique<Tree>(L_, false, false);
     tree->SetLeafOutput(0, hlo[0]);
+    if (hc->num_splits < 0 || hc->num_splits > L_ - 1) Log::Fatal("device tree: invalid split count %d", hc->num_splits);
     for (int s = 0; s < hc->num_splits; ++s) {
       const SplitRec& r = hr[s];
       const SplitInfo& info = r.info;
+      if (r.leaf < 0 || r.leaf > s || info.feature < 0 || info.feature >= F_) {
+        Log::Fatal("device tree: invalid split record %d (leaf %d, feature %d)", s, r.leaf, info.feature);
+      }
       const FeatureInfo& fi = data_->feature(info.feature);
       const BinMapper& mapper = data_->inner_mapper(info.feature);
       const float gain = static_cast<float>(info.gain + config_->min_gain_to_split);
