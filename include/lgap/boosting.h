@@ -25,6 +25,9 @@ class SampleStrategy {
   void ResetConfig(const Config* cfg);
   // returns true if a new bag was drawn this iteration
   bool Bagging(int iter, score_t* gradients, score_t* hessians);
+  // The same decision as Bagging() for a learner that draws the sample on the
+  // device: returns a DeviceSamplePlan (kSampleHost when only the host can).
+  int PlanDevice(int iter);
   bool is_hessian_change() const { return goss_; }
   bool active() const { return bag_cnt_ < num_data_; }
   data_size_t bag_cnt() const { return bag_cnt_; }
@@ -33,7 +36,7 @@ class SampleStrategy {
 
  private:
   data_size_t BagBlock(data_size_t start, data_size_t cnt, data_size_t* out, bool balanced);
-  data_size_t GossBlock(data_size_t start, data_size_t cnt, data_size_t* out, score_t* g, score_t* h);
+  data_size_t GossBlock(data_size_t start, data_size_t cnt, data_size_t* out, score_t* g, score_t* h, uint32_t seed);
   const Config* cfg_;
   const Dataset* data_;
   const ObjectiveFunction* obj_;

@@ -272,6 +272,15 @@ LIGHTGBM_C_EXPORT int LGBM_DatasetGetGroupBins(DatasetHandle handle, uint16_t* o
 // out_hist has 2 * num_total_bin doubles; group bin 0 (all features at their most frequent bin) stays 0.
 LIGHTGBM_C_EXPORT int LGBM_DeviceHistogram(DatasetHandle handle, const float* grad, const float* hess,
                                            const int32_t* rows, int32_t num_rows, double* out_hist);
+// One device row-sampling pass (the HIP bagging / GOSS kernels) over host arrays: mode 1 bagging,
+// 2 balanced bagging, 3 GOSS; `rounds` > 1 re-bags with the advanced streams and reports the last.
+// grad/hess (num_class * num_rows, class-major) are scaled in place by GOSS. Returns the kept
+// rows (ascending) in out_rows and their count in out_count.
+LIGHTGBM_C_EXPORT int LGBM_DeviceSampleRows(int mode, int32_t num_rows, int num_class, float* grad, float* hess,
+                                            const float* label, double fraction, double pos_fraction,
+                                            double neg_fraction, double top_rate, double other_rate,
+                                            int bagging_seed, uint32_t goss_seed, int rounds, int32_t* out_rows,
+                                            int32_t* out_count);
 LIGHTGBM_C_EXPORT int LGBM_DeviceCommGetUniqueId(char* out, int64_t buffer_len, int64_t* out_len);
 LIGHTGBM_C_EXPORT int LGBM_DeviceCommInit(const char* unique_id, int64_t id_len, int num_ranks, int rank,
                                           int device_id);

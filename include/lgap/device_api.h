@@ -2,6 +2,7 @@
 // Kept free of HIP headers so plain C++ translation units can include it.
 #pragma once
 
+#include <cstdint>
 #include <memory>
 #include <string>
 
@@ -46,6 +47,12 @@ std::unique_ptr<HistogramBackend> CreateHistogramBackend(const Config* config, c
 // histogram kernel; out has 2 * num_total_bin doubles.
 void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, const int* rows, int num_rows,
                      double* out);
+
+// One pass of the device row-sampling kernels over host arrays (LGBM_DeviceSampleRows):
+// returns the kept-row count, rows in out_rows, GOSS scaling applied to grad / hess.
+int SampleRowsOnDevice(int mode, int num_rows, int num_class, float* grad, float* hess, const float* label,
+                       double fraction, double pos_fraction, double neg_fraction, double top_rate, double other_rate,
+                       int bagging_seed, uint32_t goss_seed, int rounds, int* out_rows);
 
 }  // namespace device
 }  // namespace lgap

@@ -59,4 +59,21 @@ class Random {
   unsigned int x_;
 };
 
+// Counter-based hash draw shared by the host and device GOSS samplers: the key of
+// row i in iteration `iter` does not depend on thread count or visiting order.
+LGAP_HD inline uint32_t Hash32(uint32_t seed, uint32_t i) {
+  uint32_t x = i * 0x9E3779B1u ^ (seed * 0x85EBCA77u + 0x165667B1u);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+LGAP_HD inline uint32_t GossSeed(int bagging_seed, int iter) {
+  return static_cast<uint32_t>(bagging_seed) * 0x9E3779B9u + static_cast<uint32_t>(iter) * 0x85EBCA6Bu;
+}
+// GOSS works on fixed row tiles (host and device alike).
+constexpr int kGossTile = 4096;
+
 }  // namespace lgap

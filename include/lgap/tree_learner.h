@@ -17,6 +17,17 @@
 
 namespace lgap {
 
+// What the boosting loop asks a device learner to do with the row sample of
+// this iteration (SampleStrategy::PlanDevice).
+enum DeviceSamplePlan {
+  kSampleHost = -2,      // the host SampleStrategy draws it (bagging by query)
+  kSampleAll = -1,       // train on all rows
+  kSampleKeep = 0,       // keep the current bag
+  kSampleBag = 1,        // uniform bagging (bagging_fraction)
+  kSampleBalanced = 2,   // balanced bagging (pos/neg_bagging_fraction)
+  kSampleGoss = 3,       // GOSS (top_rate / other_rate)
+};
+
 class TreeLearner {
  public:
   virtual ~TreeLearner() = default;
@@ -48,6 +59,9 @@ class TreeLearner {
   virtual void DeviceAddConstant(double, int class_id) { (void)class_id; }
   virtual void DeviceGetScore(std::vector<double>*) const {}
   virtual void DeviceGetGradients(std::vector<score_t>*, std::vector<score_t>*) const {}
+  // Row sampling drawn on the device from the device-resident gradients.
+  virtual bool SupportsDeviceSampling() const { return false; }
+  virtual void DeviceSample(int plan, int iter) { (void)plan; (void)iter; }
   virtual std::string DeviceName() const { return "cpu"; }
 
   static std::unique_ptr<TreeLearner> Create(const std::string& learner_type, const std::string& device_type,

@@ -13,7 +13,7 @@ import numpy as np
 
 from ..basic import _LIB, Booster, Dataset, _check
 
-__all__ = ["group_layout", "group_bins", "device_histogram", "booster_gradients"]
+__all__ = ["group_layout", "group_bins", "device_histogram", "device_sample_rows", "booster_gradients"]
 
 
 def group_layout(ds: Dataset) -> Tuple[int, int, int, np.ndarray]:
@@ -52,6 +52,33 @@ def device_histogram(ds: Dataset, grad: np.ndarray, hess: np.ndarray, rows: Opti
                                      h.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), rp, ctypes.c_int32(n),
                                      out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
     return out.reshape(tb, 2)
+
+
+_SAMPLE_MODES = {"bagging": 1, "balanced": 2, "goss": 3}
+
+
+def device_sample_rows(mode: str, grad: np.ndarray, hess: np.ndarray, label: Optional[np.ndarray] = None,
+                       num_class: int = 1, fraction: float = 1.0, pos_fraction: float = 1.0,
+                       neg_fraction: float = 1.0, top_rate: float = 0.2, other_rate: float = 0.1,
+                       bagging_seed: int = 3, goss_seed: int = 0, rounds: int = 1
+                       ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Run the HIP bagging / GOSS sampling kernels once (``rounds`` re-bags for bagging).
+
+    Returns (kept rows ascending, grad, hess) where GOSS has scaled the sampled rows."""
+    g = np.array(grad, dtype=np.float32, copy=True).ravel()
+    h = np.array(hess, dtype=np.float32, copy=True).ravel()
+    n = g.size // num_class
+    lab = None if label is None else np.ascontiguousarray(label, dtype=np.float32)
+    rows = np.zeros(max(n, 1), dtype=np.int32)
+    cnt = ctypes.c_int32(0)
+    fp = ctypes.POINTER(ctypes.c_float)
+    _check(_LIB.LGBM_DeviceSampleRows(
+        ctypes.c_int(_SAMPLE_MODES[mode]), ctypes.c_int32(n), ctypes.c_int(num_class), g.ctypes.data_as(fp),
+        h.ctypes.data_as(fp), None if lab is None else lab.ctypes.data_as(fp), ctypes.c_double(fraction),
+        ctypes.c_double(pos_fraction), ctypes.c_double(neg_fraction), ctypes.c_double(top_rate),
+        ctypes.c_double(other_rate), ctypes.c_int(bagging_seed), ctypes.c_uint32(goss_seed), ctypes.c_int(rounds),
+        rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.byref(cnt)))
+    return rows[:cnt.value].copy(), g, h
 
 
 def booster_gradients(booster: Booster) -> Tuple[np.ndarray, np.ndarray]:

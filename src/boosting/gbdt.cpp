@@ -224,8 +224,13 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
     std::copy(hessians, hessians + hessians_.size(), hessians_.begin());
     if (device_mode_) learner_->DeviceSetGradients(gradients_.data(), hessians_.data(), num_tree_per_iteration_);
   }
-  // bagging / GOSS (GOSS rescales gradients of sampled rows, so it needs them on host)
-  {
+  // bagging / GOSS: drawn on the device from the device-resident gradients when the
+  // learner can; otherwise on the host (GOSS then round-trips the gradients)
+  int plan = kSampleHost;
+  if (device_mode_ && config_->device_sampling && learner_->SupportsDeviceSampling()) plan = sampler_->PlanDevice(iter_);
+  if (plan != kSampleHost) {
+    learner_->DeviceSample(plan, iter_);
+  } else {
     const bool need_host_grads = sampler_->is_hessian_change() && device_mode_ && !custom &&
                                  learner_->SupportsDeviceGradients(objective_);
     if (need_host_grads) learner_->DeviceGetGradients(&gradients_, &hessians_);

@@ -57,7 +57,16 @@ data_size_t SampleStrategy::BagBlock(data_size_t start, data_size_t cnt, data_si
   return nl;
 }
 
-data_size_t SampleStrategy::GossBlock(data_size_t start, data_size_t cnt, data_size_t* out, score_t* g, score_t* h) {
+// One GOSS tile (goss.hpp:118-167 Helper): keep every row whose sum_k |g_k h_k| reaches the
+// top_k-th largest, sample other_k of the rest and scale their (g, h) by (cnt - top_k) / other_k.
+// Deliberate difference from the reference: the reference's blocks are one per thread and it
+// draws the rest with a sequential adaptive-probability scan of per-1024-row LCG streams, so
+// its bag depends on the thread count. Here tiles are fixed (kGossTile rows) and the rest
+// sample is the other_k smallest Hash32(seed, row) keys (an exact-size uniform sample): the
+// bag depends only on the data, the seed and the iteration, and the HIP sampler
+// (src/device/sample_kernels.hip) draws the identical bag.
+data_size_t SampleStrategy::GossBlock(data_size_t start, data_size_t cnt, data_size_t* out, score_t* g, score_t* h,
+                                      uint32_t seed) {
   if (cnt <= 0) return 0;
   std::vector<score_t> imp(cnt, 0.0f);
   for (data_size_t i = 0; i < cnt; ++i)
@@ -65,34 +74,57 @@ data_size_t SampleStrategy::GossBlock(data_size_t start, data_size_t cnt, data_s
       const size_t idx = static_cast<size_t>(k) * num_data_ + start + i;
       imp[i] += std::fabs(g[idx] * h[idx]);
     }
-  data_size_t top_k = std::max<data_size_t>(1, static_cast<data_size_t>(cnt * cfg_->top_rate));
+  const data_size_t top_k = std::max<data_size_t>(1, static_cast<data_size_t>(cnt * cfg_->top_rate));
   const data_size_t other_k = static_cast<data_size_t>(cnt * cfg_->other_rate);
   std::vector<score_t> sorted = imp;
   std::nth_element(sorted.begin(), sorted.begin() + (top_k - 1), sorted.end(), std::greater<score_t>());
   const score_t threshold = sorted[top_k - 1];
+  std::vector<uint32_t> keys;
+  for (data_size_t i = 0; i < cnt; ++i) {
+    if (!(imp[i] >= threshold)) keys.push_back(Hash32(seed, static_cast<uint32_t>(start + i)));
+  }
+  const data_size_t rest = static_cast<data_size_t>(keys.size());
+  // 0: sample none, 1: all of the rest, 2: keys <= kthr
+  int mode = 0;
+  uint32_t kthr = 0;
+  if (other_k > 0 && rest > 0) {
+    if (other_k >= rest) {
+      mode = 1;
+    } else {
+      std::nth_element(keys.begin(), keys.begin() + (other_k - 1), keys.end());
+      kthr = keys[other_k - 1];
+      mode = 2;
+    }
+  }
   const score_t multiply = other_k > 0 ? static_cast<score_t>(cnt - top_k) / other_k : 1.0f;
-  data_size_t nl = 0, big = 0;
+  data_size_t nl = 0;
   for (data_size_t i = 0; i < cnt; ++i) {
     const data_size_t idx = start + i;
     if (imp[i] >= threshold) {
       out[nl++] = idx;
-      ++big;
-    } else {
-      const data_size_t sampled = nl - big;
-      const data_size_t need = other_k - sampled;
-      const data_size_t rest = (cnt - i) - (top_k - big);
-      const double prob = rest > 0 ? need / static_cast<double>(rest) : 0.0;
-      if (rands_[idx / kRandBlock].NextFloat() < prob) {
-        out[nl++] = idx;
-        for (int k = 0; k < ntpi_; ++k) {
-          const size_t j = static_cast<size_t>(k) * num_data_ + idx;
-          g[j] *= multiply;
-          h[j] *= multiply;
-        }
+    } else if (mode == 1 || (mode == 2 && Hash32(seed, static_cast<uint32_t>(idx)) <= kthr)) {
+      out[nl++] = idx;
+      for (int k = 0; k < ntpi_; ++k) {
+        const size_t j = static_cast<size_t>(k) * num_data_ + idx;
+        g[j] *= multiply;
+        h[j] *= multiply;
       }
     }
   }
   return nl;
+}
+
+int SampleStrategy::PlanDevice(int iter) {
+  if (goss_) {
+    if (iter < static_cast<int>(1.0f / cfg_->learning_rate)) return iter == 0 ? kSampleAll : kSampleKeep;
+    return kSampleGoss;
+  }
+  const bool bagging = cfg_->bagging_freq > 0 && (cfg_->bagging_fraction < 1.0 || balanced_);
+  if (!bagging) return kSampleKeep;
+  if (by_query_) return kSampleHost;
+  if (!(need_rebag_ || iter % cfg_->bagging_freq == 0)) return kSampleKeep;
+  need_rebag_ = false;
+  return balanced_ ? kSampleBalanced : kSampleBag;
 }
 
 bool SampleStrategy::Bagging(int iter, score_t* g, score_t* h) {
@@ -101,16 +133,16 @@ bool SampleStrategy::Bagging(int iter, score_t* g, score_t* h) {
     if (iter < static_cast<int>(1.0f / cfg_->learning_rate)) {
       return iter == 0;
     }
-    // blocks sized like the reference's thread partition (>= 1024 rows)
-    const int nt = omp_get_max_threads();
-    const data_size_t block = std::max<data_size_t>(kRandBlock, (num_data_ + nt - 1) / nt);
+    // fixed tiles: the bag does not depend on the thread count (see GossBlock)
+    const data_size_t block = kGossTile;
     const int nb = static_cast<int>((num_data_ + block - 1) / block);
+    const uint32_t seed = GossSeed(cfg_->bagging_seed, iter);
     std::vector<std::vector<data_size_t>> left(nb);
-#pragma omp parallel for schedule(static, 1)
+#pragma omp parallel for schedule(static)
     for (int b = 0; b < nb; ++b) {
       const data_size_t s = b * block, c = std::min(block, num_data_ - s);
       left[b].resize(c);
-      left[b].resize(GossBlock(s, c, left[b].data(), g, h));
+      left[b].resize(GossBlock(s, c, left[b].data(), g, h, seed));
     }
     std::vector<char> in(num_data_, 0);
     data_size_t p = 0;

@@ -1074,6 +1074,17 @@ int LGBM_DeviceHistogram(DatasetHandle handle, const float* grad, const float* h
   API_END();
 }
 
+int LGBM_DeviceSampleRows(int mode, int32_t num_rows, int num_class, float* grad, float* hess, const float* label,
+                          double fraction, double pos_fraction, double neg_fraction, double top_rate,
+                          double other_rate, int bagging_seed, uint32_t goss_seed, int rounds, int32_t* out_rows,
+                          int32_t* out_count) {
+  API_BEGIN();
+  *out_count = device::SampleRowsOnDevice(mode, num_rows, num_class, grad, hess, label, fraction, pos_fraction,
+                                          neg_fraction, top_rate, other_rate, bagging_seed, goss_seed, rounds,
+                                          out_rows);
+  API_END();
+}
+
 int LGBM_DeviceSynchronize() {
   API_BEGIN();
   device::DeviceSynchronize();

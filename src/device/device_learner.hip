@@ -48,6 +48,7 @@
 #include "device/grad_kernels.h"
 #include "device/hip_common.h"
 #include "device/runtime_internal.h"
+#include "device/sample_kernels.h"
 #include "device/tree_kernels.h"
 #include "learner/serial_tree_learner.h"
 #include "lgap/common.h"
@@ -154,12 +155,16 @@ __device__ __forceinline__ uint32_t ColBin(const Args& a, int g, int row) {
 
 __device__ __forceinline__ int RowAt(const Args& a, int buf, int pos) { return buf < 0 ? pos : a.idx[buf][pos]; }
 
-// Diagnostic phase stamps: [kernel 0..3][split 0..255][block 0..1][stamp 0..7], 100 MHz wall clock.
+// Diagnostic phase stamps: [kernel 0..4][split 0..255][block 0..1][stamp 0..7], 100 MHz wall clock.
 __device__ __forceinline__ void Stamp(const Args& a, int kernel, int i) {
   if (a.stamps != nullptr && blockIdx.x < 2 && blockIdx.y == 0 && threadIdx.x == 0) {
     const int split = a.ctl->num_splits & 255;
     a.stamps[((static_cast<size_t>(kernel) * 256 + split) * 2 + blockIdx.x) * 8 + i] = wall_clock64();
   }
+}
+// A stamp of a given block role (slot 0) for a given split, with an explicit clock value.
+__device__ __forceinline__ void StampAt(const Args& a, int kernel, int split, int i, unsigned long long v) {
+  if (a.stamps != nullptr && threadIdx.x == 0) a.stamps[((static_cast<size_t>(kernel) * 256 + (split & 255)) * 2) * 8 + i] = v;
 }
 
 // block = 256 threads: sum of an int
@@ -1465,6 +1470,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   // no leaf has more tiles than this; one block beyond may be the post-split block
   if (bid > (c.max_count + kTileRows - 1) / kTileRows) return;
   if (threadIdx.x == 0) s_gen = __hip_atomic_load(&a.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long t_start = a.stamps ? wall_clock64() : 0ull;
   Stamp(a, 0, 0);
   BlockSelect(a, c, &st);
   Stamp(a, 0, 1);
@@ -1528,6 +1534,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   Stamp(a, 0, 3);
   if (threadIdx.x == 0) GridBarrier(a.bar, static_cast<unsigned>(arrivals), s_gen);
   __syncthreads();
+  const unsigned long long t_bar = a.stamps ? wall_clock64() : 0ull;
+  Stamp(a, 0, 4);
   Stamp(a, 1, 0);
   // phase 2: prefix over the published counts, scatter (lefts from the front, rights after them)
   int nl = 0;
@@ -1694,6 +1702,11 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     if (!c.skip) pc.scan_round = c.scan_round + 1;
     pc.hist_nb = HIST ? participants : 0;
     PostSplit(a, pc, nl_total, win);
+    if (a.stamps) {
+      StampAt(a, 4, c.num_splits, 0, t_start);
+      StampAt(a, 4, c.num_splits, 1, t_bar);
+      StampAt(a, 4, c.num_splits, 2, wall_clock64());
+    }
   }
 }
 
@@ -1838,6 +1851,61 @@ class DeviceTreeLearner : public TreeLearner {
       use_bag_ = true;
       idx_[2].Upload(used, n, stream_);
     }
+  }
+
+  // ---- row sampling on the device (sample_kernels.hip): the bag goes straight into idx_[2]
+  bool SupportsDeviceSampling() const override { return true; }
+
+  void DeviceSample(int plan, int iter) override {
+    if (plan == kSampleKeep) return;
+    if (plan == kSampleAll) {
+      SetBaggingData(nullptr, N_);
+      return;
+    }
+    const int nt = SampleTiles(N_);
+    if (samp_jump_.size() == 0) {
+      std::vector<uint2> jt(kSampleRandBlock);
+      BuildLcgJumpTable(jt.data());
+      samp_jump_.Upload(jt, stream_);
+      // Random(bagging_seed + block) per 1024-row block, as SampleStrategy seeds them
+      std::vector<unsigned> st(std::max(1, DivUp(N_, kSampleRandBlock)));
+      for (size_t b = 0; b < st.size(); ++b) st[b] = static_cast<unsigned>(config_->bagging_seed + static_cast<int>(b));
+      samp_rng_.Upload(st, stream_);
+      samp_cnt_.Resize(std::max(nt, 1));
+      samp_sel_.Resize(4 * static_cast<size_t>(std::max(nt, 1)));
+      samp_total_.Resize(1);
+    }
+    SampleArgs a;
+    a.mode = plan == kSampleGoss ? 3 : (plan == kSampleBalanced ? 2 : 1);
+    a.N = N_;
+    a.K = K_;
+    a.fraction = config_->bagging_fraction;
+    a.pos_fraction = config_->pos_bagging_fraction;
+    a.neg_fraction = config_->neg_bagging_fraction;
+    a.top_rate = config_->top_rate;
+    a.other_rate = config_->other_rate;
+    a.seed = GossSeed(config_->bagging_seed, iter);  // the host sampler's seed: identical GOSS bags
+    if (a.mode == 2) {
+      if (bag_label_.size() == 0) bag_label_.Upload(data_->metadata().label(), N_, stream_);
+      a.label = bag_label_.get();
+    }
+    a.gh = gh_.get();
+    a.rng = samp_rng_.get();
+    a.jump = samp_jump_.get();
+    a.tile_cnt = samp_cnt_.get();
+    a.tile_sel = samp_sel_.get();
+    a.out = idx_[2].get();
+    a.total = samp_total_.get();
+    LaunchSampleCount(a, stream_);
+    LaunchSampleScatter(a, stream_);
+    int* cnt = pin_cnt_.Get(1);
+    samp_total_.Download(cnt, 1, stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (*cnt < 0 || *cnt > N_) Log::Fatal("device sampling: invalid bag size %d", *cnt);
+    bag_cnt_ = *cnt;
+    use_bag_ = bag_cnt_ < N_;
+    if (!use_bag_) bag_cnt_ = N_;
+    Log::Debug("Device %s, using %d data to train", a.mode == 3 ? "GOSS" : "bagging", bag_cnt_);
   }
 
   std::unique_ptr<Tree> Train(const score_t* g, const score_t* h, bool is_first_tree) override {
@@ -2149,8 +2217,26 @@ class DeviceTreeLearner : public TreeLearner {
     std::vector<unsigned long long> h(stamps_.size());
     stamps_.Download(h.data(), h.size(), stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
-    static const char* names[4] = {"part_count", "part_scatter", "hist", "reduce_scan"};
-    for (int k = 0; k < 4; ++k) {
+    static const char* names[5] = {"part_count", "part_scatter", "hist", "reduce_scan", "post"};
+    auto at = [&](int k, int sp, int b, int i) { return h[((static_cast<size_t>(k) * 256 + sp) * 2 + b) * 8 + i]; };
+    {
+      // start-to-start of block 0 along the per-split chain hist(j) -> scan(j) -> partition(j) -> hist(j+1)
+      double hs = 0, sp_ = 0, ph = 0;
+      int cnt = 0;
+      for (int j = 1; j + 1 < std::min(nsplits, 255); ++j) {
+        const unsigned long long H = at(2, j, 0, 0), S = at(3, j, 0, 0), P = at(0, j, 0, 0), H2 = at(2, j + 1, 0, 0);
+        if (!H || !S || !P || !H2 || !(H < S && S < P && P < H2)) continue;
+        hs += (S - H) * 0.01;
+        sp_ += (P - S) * 0.01;
+        ph += (H2 - P) * 0.01;
+        ++cnt;
+      }
+      if (cnt) {
+        std::fprintf(stderr, "stamps chain (%d splits, block-0 start to start, us): hist->scan %.2f scan->partition %.2f "
+                     "partition->hist %.2f\n", cnt, hs / cnt, sp_ / cnt, ph / cnt);
+      }
+    }
+    for (int k = 0; k < 5; ++k) {
       for (int b = 0; b < 2; ++b) {
         double acc[8] = {0};
         int cnt = 0;
@@ -2561,11 +2647,12 @@ class DeviceTreeLearner : public TreeLearner {
     staging_.Resize(2 * static_cast<size_t>(TB_));
     staging_.Zero(stream_);
     hist_slab_.Resize(static_cast<size_t>(HistBlocks()) * 2 * TB_ * (use_dp_ ? 8 : 4));
-    for (int i = 0; i < 2; ++i) idx_[i].Resize(std::max(N_, 1));
-    if (idx_[2].size() == 0) idx_[2].Resize(1);
+    // all three index buffers hold N rows up front: a captured graph keeps their
+    // addresses, so a later bag (host upload or device draw) must not reallocate
+    for (int i = 0; i < 3; ++i) idx_[i].Resize(std::max(N_, 1));
     if (bag_cnt_ == 0) bag_cnt_ = N_;
     if (getenv("LGAP_STAMPS")) {
-      stamps_.Resize(4 * 256 * 2 * 8);
+      stamps_.Resize(5 * 256 * 2 * 8);
       stamps_.Zero(stream_);
     }
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -2817,6 +2904,12 @@ class DeviceTreeLearner : public TreeLearner {
   PinnedBuf<float2> pin_gh_;
   PinnedBuf<char> pin_tree_;
   PinnedBuf<unsigned> pin_max_;
+  // device row sampling
+  DevBuf<uint2> samp_jump_;
+  DevBuf<unsigned> samp_rng_, samp_sel_;
+  DevBuf<int> samp_cnt_, samp_total_;
+  DevBuf<float> bag_label_;
+  PinnedBuf<int> pin_cnt_;
 };
 
 }  // namespace

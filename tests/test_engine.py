@@ -571,6 +571,21 @@ def test_goss_and_bagging_by_query(lgb, rank_data):
               lgb.Dataset(X, y, group=q), 5)
 
 
+def test_goss_independent_of_thread_count(lgb):
+    """GOSS tiles are fixed (not one block per thread as in the reference): the model does not
+    change with num_threads, also when several boosters run in one process."""
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((30000, 6))
+    y = (X[:, 0] + 0.5 * X[:, 1] ** 2 + 0.3 * rng.standard_normal(30000) > 0.4).astype(float)
+    preds = []
+    for nt in (1, 3, 1):
+        p = {"objective": "binary", "verbosity": -1, "data_sample_strategy": "goss", "learning_rate": 0.5,
+             "num_threads": nt, "num_leaves": 15}
+        preds.append(lgb.train(p, lgb.Dataset(X, y), 6).predict(X[:2000], raw_score=True))
+    np.testing.assert_array_equal(preds[0], preds[1])
+    np.testing.assert_array_equal(preds[0], preds[2])
+
+
 def test_position_bias(lgb, rank_data):
     X, y, q, *_ = rank_data
     pos = np.concatenate([np.arange(c) for c in q]).astype(np.int32) % 10

@@ -153,3 +153,77 @@ def test_lambdarank_gradient_kernel_matches_torch(lgb, gpu_required, rng):
     # the kernel uses the 1M-entry sigmoid lookup table of the host objective
     np.testing.assert_allclose(g, tg, rtol=2e-3, atol=2e-4)
     np.testing.assert_allclose(h, th, rtol=2e-3, atol=2e-4)
+
+
+def _lcg_bags(n, seed, rounds, decide):
+    """Host reference of the bagging streams: Random(seed + b) per 1024-row block, one
+    NextFloat per row, continued across re-bags (sample_strategy.cpp / bagging.hpp)."""
+    nb = (n + 1023) // 1024
+    states = (seed + np.arange(nb, dtype=np.int64)) & 0xFFFFFFFF
+    keep = None
+    for _ in range(rounds):
+        draws = np.zeros((nb, 1024), dtype=np.float32)
+        s = states.copy()
+        for j in range(1024):
+            s = (214013 * s + 2531011) & 0xFFFFFFFF
+            draws[:, j] = ((s >> 16) & 0x7FFF).astype(np.float32) / np.float32(32768.0)
+        rows_per = np.minimum(1024, n - 1024 * np.arange(nb))
+        # each block's stream advances by its own row count
+        for b in range(nb):
+            t = states[b]
+            for _ in range(int(rows_per[b])):
+                t = (214013 * t + 2531011) & 0xFFFFFFFF
+            states[b] = t
+        r = draws.reshape(-1)[:n].astype(np.float64)
+        keep = decide(r)
+    return np.flatnonzero(keep)
+
+
+@pytest.mark.parametrize("rounds", [1, 3])
+def test_device_bagging_matches_host_streams(lgb, gpu_required, rng, rounds):
+    from lambdagap_amd import ops
+
+    n = 50_000 + 123
+    g = rng.standard_normal(n).astype(np.float32)
+    h = np.ones(n, np.float32)
+    rows, _, _ = ops.device_sample_rows("bagging", g, h, fraction=0.37, bagging_seed=11, rounds=rounds)
+    ref = _lcg_bags(n, 11, rounds, lambda r: r < 0.37)
+    np.testing.assert_array_equal(rows, ref)
+    label = (rng.random(n) < 0.3).astype(np.float32)
+    rows, _, _ = ops.device_sample_rows("balanced", g, h, label=label, pos_fraction=0.9, neg_fraction=0.2,
+                                        bagging_seed=5, rounds=rounds)
+    ref = _lcg_bags(n, 5, rounds, lambda r: np.where(label > 0, r < 0.9, r < 0.2))
+    np.testing.assert_array_equal(rows, ref)
+
+
+@pytest.mark.parametrize("num_class", [1, 3])
+def test_device_goss_selection(lgb, gpu_required, rng, num_class):
+    """Per 4096-row tile: every row with sum_k |g_k h_k| >= the top_k-th largest is kept, exactly
+    min(other_k, rest) others are sampled and only those are scaled by (cnt - top_k) / other_k."""
+    from lambdagap_amd import ops
+
+    n = 3 * 4096 + 1000
+    g = rng.standard_normal(num_class * n).astype(np.float32)
+    h = rng.random(num_class * n).astype(np.float32) + 0.1
+    g[:50] = 0.0  # ties at zero importance
+    top, other = 0.2, 0.1
+    rows, g2, h2 = ops.device_sample_rows("goss", g, h, num_class=num_class, top_rate=top, other_rate=other,
+                                          goss_seed=99)
+    assert np.all(np.diff(rows) > 0)
+    imp = np.abs(g * h).reshape(num_class, n).sum(0, dtype=np.float32)
+    kept = np.zeros(n, bool)
+    kept[rows] = True
+    for t0 in range(0, n, 4096):
+        sl = slice(t0, min(n, t0 + 4096))
+        cnt = sl.stop - sl.start
+        top_k, other_k = max(1, int(cnt * top)), int(cnt * other)
+        thr = np.sort(imp[sl])[::-1][top_k - 1]
+        big = imp[sl] >= thr
+        assert kept[sl][big].all()
+        sampled = kept[sl] & ~big
+        assert sampled.sum() == min(other_k, cnt - big.sum())
+        mul = np.float32(cnt - top_k) / np.float32(other_k)
+        for k in range(num_class):
+            gk, gk2 = g.reshape(num_class, n)[k, sl], g2.reshape(num_class, n)[k, sl]
+            np.testing.assert_allclose(gk2[sampled], gk[sampled] * mul, rtol=1e-6)
+            np.testing.assert_array_equal(gk2[~sampled], gk[~sampled])

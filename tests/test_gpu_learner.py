@@ -136,12 +136,33 @@ def test_bagging_goss_feature_fraction_on_device(lgb, gpu_required):
     from lambdagap_amd.utils import make_higgs_like
 
     X, y = make_higgs_like(60000, seed=21)
-    for kw in ({"bagging_fraction": 0.7, "bagging_freq": 1}, {"data_sample_strategy": "goss"},
+    # device bagging draws the host's bags bit for bit (same per-1024-row LCG streams, also
+    # across re-bags); GOSS with device_sampling=false runs the host sampler
+    for kw in ({"bagging_fraction": 0.7, "bagging_freq": 1},
+               {"pos_bagging_fraction": 0.8, "neg_bagging_fraction": 0.5, "bagging_freq": 2},
+               {"data_sample_strategy": "goss", "learning_rate": 0.5, "device_sampling": False},
                {"feature_fraction": 0.6}, {"extra_trees": True}):
         bc = _train(lgb, X, y, "cpu", rounds=5, **kw)
         bg = _train(lgb, X, y, "gpu", rounds=5, **kw)
         np.testing.assert_allclose(bg.predict(X[:3000], raw_score=True), bc.predict(X[:3000], raw_score=True),
                                    rtol=1e-3, atol=1e-4)
+
+
+def test_device_goss(lgb, gpu_required):
+    """GOSS drawn on the device (fixed 4096-row tiles: exact top-k by |g*h| + the other_k smallest
+    hash keys of the rest, rescaled) draws the host sampler's bag: same models either way."""
+    from lambdagap_amd.utils import make_higgs_like
+
+    X, y = make_higgs_like(100000, seed=23)
+    Xv, yv = make_higgs_like(40000, seed=24)
+    kw = {"data_sample_strategy": "goss", "learning_rate": 0.25, "top_rate": 0.2, "other_rate": 0.1}
+    bc = _train(lgb, X, y, "cpu", rounds=20, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=20, **kw)
+    bh = _train(lgb, X, y, "gpu", rounds=20, device_sampling=False, **kw)
+    pg, ph = bg.predict(Xv, raw_score=True), bh.predict(Xv, raw_score=True)
+    np.testing.assert_allclose(pg, ph, rtol=1e-5, atol=1e-5)
+    ac, ag = _auc(yv, bc.predict(Xv)), _auc(yv, bg.predict(Xv))
+    assert abs(ag - ac) < 1e-3, (ag, ac)
 
 
 def test_rccl_data_parallel_path_single_rank(lgb, gpu_required):
