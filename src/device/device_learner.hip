@@ -84,7 +84,8 @@ struct Args {
   const uint8_t* used_bytree;
   const uint8_t* bynode;
   const TreeParams* tp;
-  Ctl* ctl;
+  Ctl* ctl;       // control block this launch reads (never written while the launch runs)
+  Ctl* ctl_next;  // k_partition writes the post-split control block here (double buffer)
   LeafRange* range;
   double2* lsum;
   double* lout;
@@ -116,7 +117,10 @@ struct Args {
   const unsigned long long* ic_feat;
   unsigned long long* ic_leaf;
   double* root_part;  // per-block (sum g, sum h, max|g|, max|h|) of k_root_sums
-  unsigned* bar;      // grid barrier of k_partition: {arrivals, generation, error}
+  unsigned* bar;      // {-, -, error flag of k_partition's bounded waits}
+  SplitKey* scan_key;  // [2][F] compact candidates of the last scan (next to scan_out)
+  SplitKey* leaf_key;  // [L] compact best split per leaf (next to best)
+  unsigned long long* tile_pub;  // k_partition tile counts tagged with the split epoch
   int hist_min_rows;  // rows per k_hist block (fewer rows: more blocks and slab rows)
   SplitParams sp;
 };
@@ -160,6 +164,13 @@ __device__ __forceinline__ void Stamp(const Args& a, int kernel, int i) {
   if (a.stamps != nullptr && blockIdx.x < 2 && blockIdx.y == 0 && threadIdx.x == 0) {
     const int split = a.ctl->num_splits & 255;
     a.stamps[((static_cast<size_t>(kernel) * 256 + split) * 2 + blockIdx.x) * 8 + i] = wall_clock64();
+  }
+}
+// Latest exit over all blocks of a kernel (slot 0, stamp 7), for kernel-span / gap analysis.
+__device__ __forceinline__ void StampEnd(const Args& a, int kernel) {
+  if (a.stamps != nullptr && threadIdx.x == 0) {
+    const int split = a.ctl->num_splits & 255;
+    atomicMax(&a.stamps[((static_cast<size_t>(kernel) * 256 + split) * 2) * 8 + 7], wall_clock64());
   }
 }
 // A stamp of a given block role (slot 0) for a given split, with an explicit clock value.
@@ -276,7 +287,10 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     c.scan_round = 0;
     c.max_count = tp.root_count;
     c.hist_nb = 0;
-    c.pad0 = c.pad1 = c.pad2 = 0;
+    // the split epoch keeps increasing across trees (tile_pub tags must never repeat)
+    const unsigned e0 = a.ctl->epoch, e1 = a.ctl_next ? a.ctl_next->epoch : 0u;
+    c.epoch = (e0 > e1 ? e0 : e1) + 1u;
+    c.pad1 = c.pad2 = 0;
     *a.ctl = c;
     LeafRange r;
     r.buf = tp.root_buf;
@@ -296,6 +310,8 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     a.slot[i] = i;
     a.bounds[i] = LeafBounds();
     a.best[i].Reset();
+    a.leaf_key[i].feature = -1;
+    a.leaf_key[i].gain = kMinScore;
   }
   for (int f = t; f < a.F; f += blockDim.x) a.splittable[f] = 1;
 }
@@ -564,6 +580,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
       slab[2 * i + 1] = static_cast<double>(static_cast<long long>(hist[2 * i + 1])) * ih;
     }
   }
+  StampEnd(a, 2);
 }
 
 // staging[v] = sum over the active blocks' slab rows (v over 2 * TB values).
@@ -968,7 +985,28 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     uint32_t* dst = reinterpret_cast<uint32_t*>(gout);
     for (int i = lane; i < kWords; i += 64) dst[i] = src[i];
   }
+  if (lane == 0) {
+    // the compact candidate the partition's select reads
+    SplitKey k;
+    k.feature = out->feature;
+    k.gain = SafeGain(*out);
+    k.threshold = out->threshold;
+    k.group = fi.group;
+    k.offset = fi.offset;
+    k.num_bin = fi.num_bin;
+    k.mfb = fi.mfb;
+    k.default_bin = fi.default_bin;
+    k.missing = fi.missing;
+    k.default_left = out->default_left;
+    k.is_cat = fi.bin_type != 0 ? 1 : 0;
+    k.pad0 = 0;
+    k.pad1 = k.pad2 = 0;
+    a.scan_key[static_cast<size_t>(sel) * a.F + f] = k;
+  }
   Stamp(a, 3, 4);
+  if (lane == 0 && a.stamps) {
+    atomicMax(&a.stamps[((static_cast<size_t>(3) * 256 + (a.ctl->num_splits & 255)) * 2) * 8 + 7], wall_clock64());
+  }
 }
 
 // quant_train_renew_leaf: per-leaf sums of the unquantized (g, h); one block per leaf
@@ -1169,6 +1207,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
     if (!c.skip) cp->scan_round = c.scan_round + 1;
     if (st.done) {
       cp->done = 1;
+      a.ctl_next->done = 1;
     } else {
       const LeafRange pr = a.range[st.leaf];
       cp->split_leaf = st.leaf;
@@ -1281,6 +1320,7 @@ __device__ void PostSplit(const Args& a, const Ctl& c, int left_count, const Spl
     nc.smaller = smaller;
     nc.larger = larger;
     nc.skip = skip ? 1 : 0;
+    nc.epoch = c.epoch + 1u;
     int to = -1;
     if (!skip) {
       if (larger == r) {
@@ -1292,7 +1332,7 @@ __device__ void PostSplit(const Args& a, const Ctl& c, int left_count, const Spl
         to = r;
       }
     }
-    *a.ctl = nc;
+    *a.ctl_next = nc;
     s_from = ps;
     s_to = to;
     s_skip = skip ? 1 : 0;
@@ -1316,7 +1356,7 @@ __device__ void PostSplit(const Args& a, const Ctl& c, int left_count, const Spl
     __syncthreads();
     if (threadIdx.x == 0) {
       for (int i = 1; i < static_cast<int>(blockDim.x >> 6); ++i) mx = max(mx, s_mx[i]);
-      a.ctl->max_count = mx;
+      a.ctl_next->max_count = mx;
     }
   }
   __syncthreads();
@@ -1414,97 +1454,247 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// Fused partition (select + count + scatter in ONE launch). The per-tile left
-// counts are exchanged through a grid barrier among the participating blocks.
-// All of them are co-resident (the host caps the grid at the occupancy limit),
-// and the exchange uses agent-scope atomics only (they bypass the per-XCD L2s),
-// so no L2 writeback / invalidate fences are needed. A bounded spin turns a
-// barrier that cannot complete into an error flag instead of a hang.
+// Fused partition (select + count + scatter + post-split in ONE launch), with no
+// grid barrier:
+//  * select reads only compact SplitKeys (children's per-feature candidates, the
+//    older leaves' bests) and the leaf ranges in one round of independent loads;
+//    the winner's key is the partition predicate, no dependent descriptor loads;
+//  * every block publishes its tiles' left counts as 64-bit {epoch, count}
+//    granules (one agent-scope store each, no fences needed);
+//  * a tile waits only for its PREDECESSORS' counts (decoupled look-back): lefts go
+//    to [0, nl) in order, rights are placed from the END of the range in reverse
+//    order, which needs the rights before the tile, not the global left total;
+//  * a spare block (or block 0) gathers all counts for the total and runs the
+//    post-split bookkeeping concurrently with the scatter.
+// The control block it reads (a.ctl) is never written during the launch: the
+// post-split state goes to a.ctl_next (double buffer), so no block can observe a
+// half-updated split. Histograms are order independent (fixed point), so the
+// reversed right child changes no result. Every wait is bounded: a timeout raises
+// the sticky error flag bar[2] that the host checks after the tree.
 
-__device__ __forceinline__ void AtomicStoreAgent(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int AtomicLoadAgent(const int* p) {
-  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// thread 0 of each participating block; `gen` was read before arriving
-__device__ void GridBarrier(unsigned* bar, unsigned participants, unsigned gen) {
-  __builtin_amdgcn_s_waitcnt(0);  // this block's published tile counts have landed
-  const unsigned old = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (old == participants - 1) {
-    __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);
-    __hip_atomic_store(&bar[1], gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  unsigned spins = 0;
-  while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-    __builtin_amdgcn_s_sleep(1);
-    // a barrier that cannot complete (or an earlier failure) ends the wait: the
-    // host sees the sticky error flag after the tree and fails loudly
-    if ((++spins & 1023u) == 0u &&
-        (spins > (1u << 22) || __hip_atomic_load(&bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-      __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
+__device__ __forceinline__ void WaveArgBest4(double* g, int* f, int* l, int* o) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    const double og = __shfl_xor(*g, s, kWave);
+    const int of = __shfl_xor(*f, s, kWave);
+    const int ol = __shfl_xor(*l, s, kWave);
+    const int oo = __shfl_xor(*o, s, kWave);
+    if (CandBetter(og, of, ol, *g, *f, *l)) {
+      *g = og;
+      *f = of;
+      *l = ol;
+      *o = oo;
     }
   }
 }
 
-// HIST: also build the smaller child's histogram while scattering (whole-row
-// fixed-point accumulation into LDS, one slab row per participating block), so
-// no separate k_hist launch is needed for this split.
-template <int W, bool HIST>
+struct SelOut {
+  SelState st;
+  SplitDesc d;
+  LeafRange pr;
+  SplitKey key[2];  // the two children's winning keys (persisted by block 0)
+};
+
+__device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
+  constexpr int kW = kPartThreads / 64;
+  constexpr int kNone = 0x7fffffff;
+  __shared__ double s_g[3][kW];
+  __shared__ int s_f[3][kW], s_l[3][kW], s_o[3][kW];
+  __shared__ int s_owner[3], s_win_cat;
+  __shared__ LeafRange s_rng[kPartThreads];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  double g3[3] = {kMinScore, kMinScore, kMinScore};
+  int f3[3] = {kNone, kNone, kNone};
+  int l3[3] = {0, 0, kNone};
+  SplitKey k3[3];
+  if (!c.skip) {
+#pragma unroll
+    for (int sel = 0; sel < 2; ++sel) {
+      const int leaf = sel ? c.larger : c.smaller;
+      if (leaf < 0) continue;
+      for (int f = t; f < a.F; f += blockDim.x) {
+        const SplitKey k = a.scan_key[static_cast<size_t>(sel) * a.F + f];
+        if (k.feature >= 0 && CandBetter(k.gain, f, 0, g3[sel], f3[sel], 0)) {
+          g3[sel] = k.gain;
+          f3[sel] = f;
+          k3[sel] = k;
+        }
+      }
+    }
+  }
+  for (int l = t; l < c.num_leaves; l += blockDim.x) {
+    if (l == c.smaller || l == c.larger) continue;
+    const SplitKey k = a.leaf_key[l];
+    const double g = k.feature < 0 ? kMinScore : k.gain;
+    const int f = k.feature < 0 ? kNone : k.feature;
+    if (CandBetter(g, f, l, g3[2], f3[2], l3[2])) {
+      g3[2] = g;
+      f3[2] = f;
+      l3[2] = l;
+      k3[2] = k;
+    }
+  }
+  if (t <= c.num_leaves && t < kPartThreads) s_rng[t] = a.range[t];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    int o = t;
+    WaveArgBest4(&g3[k], &f3[k], &l3[k], &o);
+    if (lane == 0) {
+      s_g[k][w] = g3[k];
+      s_f[k][w] = f3[k];
+      s_l[k][w] = l3[k];
+      s_o[k][w] = o;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int k = 0; k < 3; ++k) {
+      for (int i = 1; i < kW; ++i) {
+        if (CandBetter(s_g[k][i], s_f[k][i], s_l[k][i], s_g[k][0], s_f[k][0], s_l[k][0])) {
+          s_g[k][0] = s_g[k][i];
+          s_f[k][0] = s_f[k][i];
+          s_l[k][0] = s_l[k][i];
+          s_o[k][0] = s_o[k][i];
+        }
+      }
+      s_owner[k] = s_f[k][0] == kNone ? -1 : s_o[k][0];
+    }
+    SelState& st = so->st;
+    st.new_best[0] = s_f[0][0] == kNone ? -1 : s_f[0][0];
+    st.new_best[1] = s_f[1][0] == kNone ? -1 : s_f[1][0];
+    double bg = s_g[2][0];
+    int bf = s_f[2][0], bl = s_l[2][0], cat = 2;
+    for (int sel = 0; sel < 2; ++sel) {
+      const int leaf = sel ? c.larger : c.smaller;
+      if (leaf < 0 || s_f[sel][0] == kNone) continue;
+      if (CandBetter(s_g[sel][0], s_f[sel][0], leaf, bg, bf, bl)) {
+        bg = s_g[sel][0];
+        bf = s_f[sel][0];
+        bl = leaf;
+        cat = sel;
+      }
+    }
+    st.leaf = bl;
+    st.feature = bf;
+    st.done = (bl == kNone || bf == kNone || !(bg > 0.0)) ? 1 : 0;
+    st.sel = cat == 2 ? -1 : cat;
+    s_win_cat = st.done ? -1 : cat;
+  }
+  __syncthreads();
+  if (t == s_owner[0]) so->key[0] = k3[0];
+  if (t == s_owner[1]) so->key[1] = k3[1];
+  const int wc = s_win_cat;
+  if (wc >= 0 && t == s_owner[wc]) {
+    const SplitKey& k = k3[wc];
+    SplitDesc& d = so->d;
+    d.group = k.group;
+    d.offset = k.offset;
+    d.num_bin = k.num_bin;
+    d.mfb = k.mfb;
+    d.default_bin = k.default_bin;
+    d.missing = k.missing;
+    d.thr = static_cast<int>(k.threshold);
+    d.default_left = k.default_left;
+    d.is_cat = k.is_cat;
+    if (k.is_cat) {
+      const SplitInfo* win = wc < 2 ? &a.scan_out[static_cast<size_t>(wc) * a.F + k.feature] : &a.best[so->st.leaf];
+      for (int i = 0; i < kMaxCatWords; ++i) d.bits[i] = win->cat_bitset[i];
+    }
+    const int leaf = so->st.leaf;
+    so->pr = leaf < kPartThreads ? s_rng[leaf] : a.range[leaf];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void PublishCount(unsigned long long* p, unsigned epoch, int cnt) {
+  const unsigned long long v = (static_cast<unsigned long long>(epoch) << 32) | static_cast<unsigned>(cnt);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// count of tile i of this split (bounded spin; on timeout raise the error flag and use 0)
+__device__ __forceinline__ int AwaitCount(const Args& a, int i, unsigned epoch) {
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned long long v = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (static_cast<unsigned>(v >> 32) == epoch) return static_cast<int>(static_cast<unsigned>(v));
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 1023u) == 0u &&
+        (spins > (1u << 22) || __hip_atomic_load(&a.bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+      __hip_atomic_store(&a.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0;
+    }
+  }
+}
+
+// sum of the published counts of tiles [0, n)
+__device__ int SumCounts(const Args& a, int n, unsigned epoch, int* sh) {
+  int s = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += AwaitCount(a, i, epoch);
+  return BlockSumInt(s, sh);
+}
+
 __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
-  extern __shared__ __align__(8) unsigned char part_lds[];
-  __shared__ SplitDesc d;
-  __shared__ SelState st;
+  __shared__ SelOut so;
   __shared__ int sh[8];
   __shared__ int s_wl[kPartIters][kPartThreads / 64];
   __shared__ int s_wv[kPartIters][kPartThreads / 64];
-  __shared__ unsigned s_gen;
-  Ctl* cp = a.ctl;
-  const Ctl c = *cp;
+  const unsigned long long t_start = a.stamps ? wall_clock64() : 0ull;
+  const Ctl c = *a.ctl;
   if (c.done) return;
   const int bid = static_cast<int>(blockIdx.x);
   // no leaf has more tiles than this; one block beyond may be the post-split block
   if (bid > (c.max_count + kTileRows - 1) / kTileRows) return;
-  if (threadIdx.x == 0) s_gen = __hip_atomic_load(&a.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t_start = a.stamps ? wall_clock64() : 0ull;
   Stamp(a, 0, 0);
-  BlockSelect(a, c, &st);
+  SelectFromKeys(a, c, &so);
   Stamp(a, 0, 1);
-  const SplitInfo* win = st.done ? nullptr
-                                 : (st.sel >= 0 ? &a.scan_out[static_cast<size_t>(st.sel) * a.F + st.feature]
-                                                : &a.best[st.leaf]);
+  const SelState& st = so.st;
   if (bid == 0) {
+    // persist the two children's bests (full record + compact key) for later selects
     if (c.smaller >= 0 && st.new_best[0] >= 0) CopySplitInfoBlock(&a.best[c.smaller], &a.scan_out[st.new_best[0]]);
     if (c.larger >= 0 && st.new_best[1] >= 0) {
       CopySplitInfoBlock(&a.best[c.larger], &a.scan_out[static_cast<size_t>(a.F) + st.new_best[1]]);
     }
     if (threadIdx.x == 0) {
-      if (c.smaller >= 0 && st.new_best[0] < 0) a.best[c.smaller].Reset();
-      if (c.larger >= 0 && st.new_best[1] < 0) a.best[c.larger].Reset();
-      if (!c.skip) cp->scan_round = c.scan_round + 1;
-      if (st.done) cp->done = 1;
+      if (c.smaller >= 0) {
+        if (st.new_best[0] >= 0) {
+          a.leaf_key[c.smaller] = so.key[0];
+        } else {
+          a.best[c.smaller].Reset();
+          a.leaf_key[c.smaller].feature = -1;
+          a.leaf_key[c.smaller].gain = kMinScore;
+        }
+      }
+      if (c.larger >= 0) {
+        if (st.new_best[1] >= 0) {
+          a.leaf_key[c.larger] = so.key[1];
+        } else {
+          a.best[c.larger].Reset();
+          a.leaf_key[c.larger].feature = -1;
+          a.leaf_key[c.larger].gain = kMinScore;
+        }
+      }
+      if (st.done) {
+        // both control buffers: later launches read either
+        a.ctl->done = 1;
+        a.ctl_next->done = 1;
+      }
     }
   }
   if (st.done) return;
-  const LeafRange pr = a.range[st.leaf];
-  if (threadIdx.x == 0) FillSplitDesc(a, *win, &d);
+  const SplitInfo* win = st.sel >= 0 ? &a.scan_out[static_cast<size_t>(st.sel) * a.F + st.feature] : &a.best[st.leaf];
+  const LeafRange pr = so.pr;
+  const SplitDesc& d = so.d;
+  const unsigned epoch = c.epoch;
   const int ntiles = (pr.count + kTileRows - 1) / kTileRows;
   const int participants = ntiles < static_cast<int>(gridDim.x) ? ntiles : static_cast<int>(gridDim.x);
-  // a spare block (if any) joins the barrier only to run the post-split bookkeeping
-  // concurrently with the scatter; otherwise block 0 runs it after its tiles
   const bool has_post_block = participants < static_cast<int>(gridDim.x);
   const int post_block = has_post_block ? participants : 0;
-  const int arrivals = participants + (has_post_block ? 1 : 0);
   if (bid >= participants && bid != post_block) return;
-  __syncthreads();
   Stamp(a, 0, 2);
   const int pbuf = pr.buf, pstart = pr.start, pcount = pr.count;
   const int tbuf = pbuf == 0 ? 1 : 0;
-  // phase 1: count this block's tiles (the first tile's rows stay in registers)
+  int* out = a.idx[tbuf] + pstart;
+  // phase 1: count this block's tiles and publish them (the first tile's rows stay in registers)
   int rows0[kPartIters];
   uint32_t gb0[kPartIters];
   for (int tile = bid; tile < ntiles; tile += gridDim.x) {
@@ -1522,7 +1712,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
 #pragma unroll
     for (int k = 0; k < kPartIters; ++k) cnt += (rows[k] >= 0 && GoLeft(d, gb[k])) ? 1 : 0;
     cnt = BlockSumInt(cnt, sh);
-    if (threadIdx.x == 0) AtomicStoreAgent(&a.tile_cnt[tile], cnt);
+    if (threadIdx.x == 0) PublishCount(&a.tile_pub[tile], epoch, cnt);
     if (tile == bid) {
 #pragma unroll
       for (int k = 0; k < kPartIters; ++k) {
@@ -1532,57 +1722,34 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     }
   }
   Stamp(a, 0, 3);
-  if (threadIdx.x == 0) GridBarrier(a.bar, static_cast<unsigned>(arrivals), s_gen);
-  __syncthreads();
-  const unsigned long long t_bar = a.stamps ? wall_clock64() : 0ull;
-  Stamp(a, 0, 4);
-  Stamp(a, 1, 0);
-  // phase 2: prefix over the published counts, scatter (lefts from the front, rights after them)
-  int nl = 0;
-  for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += AtomicLoadAgent(&a.tile_cnt[i]);
-  const int nl_total = BlockSumInt(nl, sh);
-  Stamp(a, 1, 1);
-  // smaller child and whether its histogram is needed at all (PostSplit's rule, replicated)
-  bool do_hist = false, hist_left = false;
-  unsigned long long* lhist = reinterpret_cast<unsigned long long*>(part_lds);
-  int* lgst = nullptr;
-  float hsg = 1.f, hsh = 1.f;
-  if (HIST) {
-    const int glc = a.distributed ? win->left_count : nl_total;
-    const int grc = a.distributed ? win->right_count : pcount - nl_total;
-    const int dep = a.depth[st.leaf] + 1;
-    const int md = a.sp.min_data_in_leaf;
-    do_hist = !((a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2));
-    hist_left = glc < grc;
-    const HistTile tile = a.tiles[0];
-    lgst = reinterpret_cast<int*>(lhist + tile.nbins);
-    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) lhist[i] = 0ull;
-    for (int g = threadIdx.x; g < a.num_groups; g += blockDim.x) lgst[g] = a.gstart[g];
-    // rows of the smaller child in this block's tiles bound the fixed-point scale
-    int mine = 0;
-    for (int tile_i = bid; tile_i < ntiles; tile_i += gridDim.x) {
-      if (threadIdx.x == 0) {
-        const int tl = AtomicLoadAgent(&a.tile_cnt[tile_i]);
-        const int trows = min(kTileRows, pcount - tile_i * kTileRows);
-        mine += hist_left ? tl : trows - tl;
-      }
+  // the post-split block: total lefts from every tile, bookkeeping next to the scatter
+  if (has_post_block && bid == post_block) {
+    const int nl_total = SumCounts(a, ntiles, epoch, sh);
+    const unsigned long long t_cnt = a.stamps ? wall_clock64() : 0ull;
+    Ctl pc = c;
+    pc.split_leaf = st.leaf;
+    pc.new_leaf = c.num_leaves;
+    pc.parent_buf = pbuf;
+    pc.parent_start = pstart;
+    pc.parent_count = pcount;
+    pc.target_buf = tbuf;
+    if (!c.skip) pc.scan_round = c.scan_round + 1;
+    pc.hist_nb = 0;
+    PostSplit(a, pc, nl_total, win);
+    if (a.stamps) {
+      StampAt(a, 4, c.num_splits, 0, t_start);
+      StampAt(a, 4, c.num_splits, 1, t_cnt);
+      StampAt(a, 4, c.num_splits, 2, wall_clock64());
     }
-    if (threadIdx.x == 0) sh[7] = mine;
-    __syncthreads();
-    const double rows_in_block = static_cast<double>(sh[7] > 0 ? sh[7] : 1);
-    const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
-    const double kPk = 1073741824.0;  // 2^30
-    hsg = static_cast<float>(gmax > 0.f ? kPk / (rows_in_block * gmax) : 1.0) * 0.99999f;
-    hsh = static_cast<float>(hmax > 0.f ? kPk / (rows_in_block * hmax) : 1.0) * 0.99999f;
+    return;
   }
-  int* out = a.idx[tbuf] + pstart;
+  // phase 2: per tile, lefts before it (look-back) -> scatter
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int tile = bid; tile < ntiles; tile += gridDim.x) {
-    int pre = 0;
-    for (int i = threadIdx.x; i < tile; i += blockDim.x) pre += AtomicLoadAgent(&a.tile_cnt[i]);
-    int lbase = BlockSumInt(pre, sh);
-    int rbase = tile * kTileRows - lbase;
+    int lbase = SumCounts(a, tile, epoch, sh);
+    if (tile == bid) Stamp(a, 1, 0);
+    int rbase = tile * kTileRows - lbase;  // rights before this tile
     int rows[kPartIters];
     uint32_t gb[kPartIters];
     if (tile == bid) {
@@ -1633,65 +1800,17 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
         if (left) out[lbase + rl] = rows[k];
-        else out[nl_total + rbase + (rv - rl)] = rows[k];
+        else out[pcount - 1 - (rbase + (rv - rl))] = rows[k];  // rights fill the range from its end
       }
       lbase += tl;
       rbase += tv - tl;
     }
-    if (HIST && do_hist) {
-      // whole rows of the smaller child: 4 rows' packed words in flight per step
-      const float2* gh = a.gh + static_cast<size_t>(c.cls) * a.N;
-      constexpr int per = 4 / W;
-      const int nd = (a.num_groups + per - 1) / per;
-#pragma unroll
-      for (int k0 = 0; k0 < kPartIters; k0 += 4) {
-        int hr[4];
-        float2 hv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = k0 + j;
-          const bool take = rows[k] >= 0 && (GoLeft(d, gb[k]) == hist_left);
-          hr[j] = take ? rows[k] : -1;
-          hv[j] = take ? gh[rows[k]] : make_float2(0.f, 0.f);
-        }
-        for (int dw = 0; dw < nd; ++dw) {
-          uint32_t wd[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) wd[j] = hr[j] >= 0 ? a.rowbins[static_cast<size_t>(hr[j]) * a.stride_dw + dw] : 0u;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (hr[j] < 0) continue;
-            const long long ig = __float2int_rn(hv[j].x * hsg);
-            const long long ih = __float2int_rn(hv[j].y * hsh);
-            const unsigned long long pg = (static_cast<unsigned long long>(ig) << 32) + static_cast<unsigned long long>(ih);
-#pragma unroll
-            for (int q = 0; q < per; ++q) {
-              const int g = dw * per + q;
-              const uint32_t b = W == 1 ? ((wd[j] >> (8 * q)) & 0xFFu) : ((wd[j] >> (16 * q)) & 0xFFFFu);
-              if (b != 0u && g < a.num_groups) atomicAdd(&lhist[lgst[g] + static_cast<int>(b)], pg);
-            }
-          }
-        }
-      }
-    }
     __syncthreads();
   }
-  if (HIST) {
-    // this block's slab row (zeros when the split needs no histogram: the scan is skipped then)
-    const HistTile tile = a.tiles[0];
-    float* slabf = reinterpret_cast<float*>(a.hist_slab) + static_cast<size_t>(bid) * a.TB * 2;
-    const double ig = 1.0 / static_cast<double>(hsg), ih = 1.0 / static_cast<double>(hsh);
-    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
-      const unsigned long long x = lhist[i];
-      const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
-      const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
-      slabf[2 * i] = static_cast<float>(static_cast<double>(gs) * ig);
-      slabf[2 * i + 1] = static_cast<float>(static_cast<double>(hs) * ih);
-    }
-  }
   Stamp(a, 1, 2);
-  if (bid == post_block) {
-    // the post-split bookkeeping reads the parent fields from ctl
+  if (!has_post_block && bid == 0) {
+    // every block has tiles: block 0 runs the post-split after its own
+    const int nl_total = SumCounts(a, ntiles, epoch, sh);
     Ctl pc = c;
     pc.split_leaf = st.leaf;
     pc.new_leaf = c.num_leaves;
@@ -1700,13 +1819,11 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     pc.parent_count = pcount;
     pc.target_buf = tbuf;
     if (!c.skip) pc.scan_round = c.scan_round + 1;
-    pc.hist_nb = HIST ? participants : 0;
+    pc.hist_nb = 0;
     PostSplit(a, pc, nl_total, win);
-    if (a.stamps) {
-      StampAt(a, 4, c.num_splits, 0, t_start);
-      StampAt(a, 4, c.num_splits, 1, t_bar);
-      StampAt(a, 4, c.num_splits, 2, wall_clock64());
-    }
+  }
+  if (a.stamps && threadIdx.x == 0) {
+    atomicMax(&a.stamps[((static_cast<size_t>(0) * 256 + (c.num_splits & 255)) * 2) * 8 + 7], wall_clock64());
   }
 }
 
@@ -2157,18 +2274,20 @@ class DeviceTreeLearner : public TreeLearner {
       EnqueueTree();
     }
     // results
-    Ctl* hc = pin_ctl_.Get(1);
+    Ctl* hc2 = pin_ctl_.Get(2);
     SplitRec* hr = pin_rec_.Get(L_);
     LeafRange* hrange = pin_range_.Get(L_);
     double* hlo = pin_lout_.Get(1);
-    HIP_CHECK(hipMemcpyAsync(hc, ctl_.get(), sizeof(Ctl), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hc2, ctl_.get(), 2 * sizeof(Ctl), hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(hr, rec_.get(), sizeof(SplitRec) * (L_ - 1), hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(hrange, range_.get(), sizeof(LeafRange) * L_, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(hlo, lout_.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
     unsigned* hbar = pin_bar_.Get(4);
     HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-    if (hbar[2] != 0u) Log::Fatal("k_partition grid barrier timed out (blocks not co-resident?)");
+    if (hbar[2] != 0u) Log::Fatal("k_partition: a wait on published tile counts timed out (blocks not co-resident?)");
+    // the control buffer written last holds the final tree state
+    const Ctl* hc = hc2[1].num_splits > hc2[0].num_splits ? &hc2[1] : &hc2[0];
     auto tree = std::make_unique<Tree>(L_, false, false);
     tree->SetLeafOutput(0, hlo[0]);
     if (hc->num_splits < 0 || hc->num_splits > L_ - 1) Log::Fatal("device tree: invalid split count %d", hc->num_splits);
@@ -2230,6 +2349,21 @@ class DeviceTreeLearner : public TreeLearner {
         sp_ += (P - S) * 0.01;
         ph += (H2 - P) * 0.01;
         ++cnt;
+      }
+      double e_h = 0, e_s = 0, e_p = 0;
+      int ce = 0;
+      for (int j = 1; j + 1 < std::min(nsplits, 255); ++j) {
+        const unsigned long long H = at(2, j, 0, 0), S = at(3, j, 0, 0), P = at(0, j, 0, 0), H2 = at(2, j + 1, 0, 0);
+        const unsigned long long He = at(2, j, 0, 7), Se = at(3, j, 0, 7), Pe = at(0, j, 0, 7);
+        if (!H || !S || !P || !H2 || !He || !Se || !Pe) continue;
+        e_h += (static_cast<double>(He) - H) * 0.01;
+        e_s += (static_cast<double>(Se) - S) * 0.01;
+        e_p += (static_cast<double>(Pe) - P) * 0.01;
+        ++ce;
+      }
+      if (ce) {
+        std::fprintf(stderr, "stamps kernel spans (%d splits, block-0 start to last block exit, us): hist %.2f scan %.2f "
+                     "partition %.2f\n", ce, e_h / ce, e_s / ce, e_p / ce);
       }
       if (cnt) {
         std::fprintf(stderr, "stamps chain (%d splits, block-0 start to start, us): hist->scan %.2f scan->partition %.2f "
@@ -2554,31 +2688,18 @@ class DeviceTreeLearner : public TreeLearner {
     // optionally the histogram rides in the partition kernel (one LDS tile, packed
     // fixed point). Measured slower than k_hist (whole-row threads, half the lanes
     // idle on the larger child, 2 blocks/CU): off by default, kept for A/B runs.
-    fused_hist_ = config_->device_fused_partition && config_->device_fused_hist && !use_dp_ && num_tiles_ == 1 &&
-                  !h_tiles_[0].direct;
     if (config_->device_fused_partition) {
-      // every participating block must be resident at once for the grid barrier
+      // k_partition waits on other blocks' published counts: every block must be resident at once
       int per_cu = 0;
-      if (fused_hist_) {
-        const void* fn = width_ == 1 ? reinterpret_cast<const void*>(k_partition<1, true>)
-                                     : reinterpret_cast<const void*>(k_partition<2, true>);
-        if (hist_lds_bytes_ > 64 * 1024) {
-          HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
-        }
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kPartThreads, hist_lds_bytes_));
-      } else {
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_partition<1, false>, kPartThreads, 0));
-      }
-      const int cap = per_cu * num_cu_;
-      fused_blocks_ = std::min({max_tiles_, 4 * num_cu_, cap});
-      if (fused_blocks_ < 1) fused_blocks_ = 0;
-      if (fused_hist_) fused_blocks_ = std::min(fused_blocks_, HistBlocks());  // slab rows
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_partition, kPartThreads, 0));
+      // the occupancy API can overstate residency by one block per CU (MI355X_MICROARCH.md): keep a margin
+      per_cu = std::max(1, per_cu - 1);
+      fused_blocks_ = std::min({max_tiles_ + 1, 4 * num_cu_, per_cu * num_cu_});
     }
-    if (fused_blocks_ == 0) fused_hist_ = false;
     use_bynode_ = config_->feature_fraction_bynode < 1.0;
     // every small per-tree structure + the static feature metadata in one allocation
     ArenaLayout lay;
-    const size_t o_tp = lay.Add<TreeParams>(1), o_ctl = lay.Add<Ctl>(1), o_range = lay.Add<LeafRange>(L),
+    const size_t o_tp = lay.Add<TreeParams>(1), o_ctl = lay.Add<Ctl>(2), o_range = lay.Add<LeafRange>(L),
                  o_lsum = lay.Add<double2>(L), o_lout = lay.Add<double>(L), o_gcount = lay.Add<int>(L),
                  o_depth = lay.Add<int>(L), o_slot = lay.Add<int>(L), o_bounds = lay.Add<LeafBounds>(L),
                  o_best = lay.Add<SplitInfo>(L), o_rec = lay.Add<SplitRec>(L), o_ghmax = lay.Add<unsigned>(2),
@@ -2590,11 +2711,12 @@ class DeviceTreeLearner : public TreeLearner {
                  o_icf = lay.Add<unsigned long long>(std::max(F_, 1)), o_icl = lay.Add<unsigned long long>(L),
                  o_qmax = lay.Add<unsigned>(2), o_tsum = lay.Add<double2>(L),
                  o_rpart = lay.Add<double>(4 * static_cast<size_t>(std::max(1, 4 * num_cu_))),
-                 o_bar = lay.Add<unsigned>(4);
+                 o_bar = lay.Add<unsigned>(4), o_skey = lay.Add<SplitKey>(2 * static_cast<size_t>(F_)),
+                 o_lkey = lay.Add<SplitKey>(L), o_tpub = lay.Add<unsigned long long>(max_tiles_);
     arena_.Resize(std::max<size_t>(lay.bytes(), size_t(2) << 20));
     char* base = arena_.get();
     tparams_.Attach(reinterpret_cast<TreeParams*>(base + o_tp), 1);
-    ctl_.Attach(reinterpret_cast<Ctl*>(base + o_ctl), 1);
+    ctl_.Attach(reinterpret_cast<Ctl*>(base + o_ctl), 2);
     range_.Attach(reinterpret_cast<LeafRange*>(base + o_range), L);
     lsum_.Attach(reinterpret_cast<double2*>(base + o_lsum), L);
     lout_.Attach(reinterpret_cast<double*>(base + o_lout), L);
@@ -2621,6 +2743,9 @@ class DeviceTreeLearner : public TreeLearner {
     true_sums_.Attach(reinterpret_cast<double2*>(base + o_tsum), L);
     root_part_.Attach(reinterpret_cast<double*>(base + o_rpart), 4 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
     bar_.Attach(reinterpret_cast<unsigned*>(base + o_bar), 4);
+    scan_key_.Attach(reinterpret_cast<SplitKey*>(base + o_skey), 2 * static_cast<size_t>(F_));
+    leaf_key_.Attach(reinterpret_cast<SplitKey*>(base + o_lkey), L);
+    tile_pub_.Attach(reinterpret_cast<unsigned long long*>(base + o_tpub), max_tiles_);
     arena_.Zero(stream_);
     use_ic_ = !config_->interaction_constraints_vector.empty();
     if (use_ic_) {
@@ -2658,7 +2783,9 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
-  Args MakeArgs() const {
+  // Args of a launch in split round `it`: the partition of round it reads control
+  // buffer it % 2 and writes the other; the histogram / scan after it read the new one.
+  Args MakeArgs(int it = 0) const {
     Args a;
     std::memset(&a, 0, sizeof(a));
     a.rowbins = rowbins_.get();
@@ -2679,7 +2806,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.used_bytree = used_bytree_.get();
     a.bynode = use_bynode_ ? bynode_.get() : nullptr;
     a.tp = tparams_.get();
-    a.ctl = ctl_.get();
+    a.ctl = ctl_.get() + (it & 1);
+    a.ctl_next = ctl_.get() + ((it + 1) & 1);
     a.range = range_.get();
     a.lsum = lsum_.get();
     a.lout = lout_.get();
@@ -2711,6 +2839,9 @@ class DeviceTreeLearner : public TreeLearner {
     a.ic_leaf = use_ic_ ? ic_leaf_.get() : nullptr;
     a.root_part = root_part_.get();
     a.bar = bar_.get();
+    a.scan_key = scan_key_.get();
+    a.leaf_key = leaf_key_.get();
+    a.tile_pub = tile_pub_.get();
     a.hist_min_rows = HistMinRows();
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
@@ -2732,7 +2863,7 @@ class DeviceTreeLearner : public TreeLearner {
 
   // The whole growth of one tree; fixed launch shapes, data-dependent work read on device.
   void EnqueueTree() {
-    const Args a = MakeArgs();
+    const Args a = MakeArgs(0);
     hipStream_t s = stream_;
     const int part_blocks = std::max(1, std::min(max_tiles_, 4 * num_cu_));
     k_init_tree<<<1, kNodeThreads, 0, s>>>(a);
@@ -2743,29 +2874,18 @@ class DeviceTreeLearner : public TreeLearner {
     LaunchHist(a);
     LaunchScan(a);
     for (int it = 0; it < L_ - 1; ++it) {
+      const Args ap = MakeArgs(it);
       if (fused_blocks_ > 0) {
-        if (fused_hist_) {
-          if (width_ == 1) k_partition<1, true><<<fused_blocks_, kPartThreads, hist_lds_bytes_, s>>>(a);
-          else k_partition<2, true><<<fused_blocks_, kPartThreads, hist_lds_bytes_, s>>>(a);
-        } else {
-          k_partition<1, false><<<fused_blocks_, kPartThreads, 0, s>>>(a);
-        }
+        k_partition<<<fused_blocks_, kPartThreads, 0, s>>>(ap);
       } else {
-        k_part_count<<<part_blocks, kPartThreads, 0, s>>>(a);
-        k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(a);
-        if (!a.fuse_post) k_post<<<1, kPartThreads, 0, s>>>(a);
+        k_part_count<<<part_blocks, kPartThreads, 0, s>>>(ap);
+        k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(ap);
+        if (!ap.fuse_post) k_post<<<1, kPartThreads, 0, s>>>(ap);
       }
       if (it < L_ - 2) {
-        if (fused_hist_) {
-          // the partition kernel left the smaller child's histogram in the slab
-          if (distributed_) {
-            LaunchHistReduce(a);
-            AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), stream_);
-          }
-        } else {
-          LaunchHist(a);
-        }
-        LaunchScan(a);
+        const Args an = MakeArgs(it + 1);
+        LaunchHist(an);
+        LaunchScan(an);
       }
     }
     HIP_CHECK(hipGetLastError());
@@ -2881,9 +3001,10 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<double2> true_sums_;
   DevBuf<double> root_part_;
   DevBuf<unsigned> bar_;
+  DevBuf<SplitKey> scan_key_, leaf_key_;
+  DevBuf<unsigned long long> tile_pub_;
   PinnedBuf<unsigned> pin_bar_;
   int fused_blocks_ = 0;  // k_partition grid (0: two-kernel partition)
-  bool fused_hist_ = false;
   const Tree* last_trained_ = nullptr;  // DeviceTrain's tree: its leaf ranges are still on the device
   DevBuf<float2> gh_true_;
   bool use_ic_ = false, is_const_hess_ = false;

@@ -61,7 +61,21 @@ struct Ctl {
   int parent_buf, parent_start, parent_count, target_buf;
   int left_count, cls, scan_round, max_count;  // max_count: largest leaf (rows), bounds useful grid size
   int hist_nb;  // slab rows holding the smaller child's histogram when k_partition built it (0: k_hist did)
-  int pad0, pad1, pad2;
+  unsigned epoch;  // split sequence number (never reset): tags k_partition's published tile counts
+  int pad1, pad2;
+};
+
+// Compact record of a split candidate: everything the best-leaf select and the
+// partition predicate need, written by k_reduce_scan next to each SplitInfo and
+// persisted per leaf, so the select is one round of 48-byte loads.
+struct SplitKey {
+  double gain;  // kMinScore: no split
+  int feature;  // -1: no split
+  uint32_t threshold;
+  int group, offset, num_bin, mfb;
+  int default_bin;
+  int8_t missing, default_left, is_cat, pad0;
+  int pad1, pad2;
 };
 
 struct SplitRec {
