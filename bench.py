@@ -42,6 +42,9 @@ def main() -> int:
     ap.add_argument("--graph", type=int, default=None, help="device_use_graph override (1/0)")
     ap.add_argument("--rehearse-dp", action="store_true",
                     help="1 GPU: run the RCCL data-parallel learner path on a one-rank communicator")
+    ap.add_argument("--dp-host-transport", action="store_true",
+                    help="N>1 ranks sharing one GPU: stage the data-parallel collectives through host "
+                         "memory over gloo (multi-rank rehearsal; not a performance configuration)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -57,7 +60,15 @@ def main() -> int:
     from lambdagap_amd.utils import make_higgs_like
 
     dist = None
-    if world > 1:
+    if world > 1 and args.dp_host_transport:
+        import torch.distributed as dist  # noqa: F811
+
+        from lambdagap_amd.parallel.torch_network import init_torch_network
+
+        dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+        init_torch_network()
+        os.environ["LGAP_DEVICE_DP_TRANSPORT"] = "host"
+    elif world > 1:
         import torch.distributed as dist  # noqa: F811
 
         init_device_comm()
@@ -141,6 +152,7 @@ def main() -> int:
                 "parallelism": f"dp{world}",
                 "device": booster.device_name(),
                 "setup_s": round(t_data, 2),
+                "transport": ("host-staged (rehearsal)" if args.dp_host_transport else "rccl") if world > 1 else None,
             },
         }
         print(json.dumps(out), flush=True)

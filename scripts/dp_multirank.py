@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Multi-rank rehearsal of the data-parallel HIP learner on ONE GPU.
+
+Launched with ``torchrun --standalone --nproc-per-node P`` (P ranks share
+cuda:0). The device learner's collectives are staged through host memory over
+gloo (``LGAP_DEVICE_DP_TRANSPORT=host``) so that everything the 8-GPU RCCL run
+depends on besides RCCL itself is exercised with P > 1 ranks: row sharding
+with ``pre_partition``, distributed bin finding, root-sum and histogram
+all-reduce, global leaf counts, identical split decisions on every rank, and
+the score / metric bookkeeping. The same ranks then train the host
+data-parallel learner on the same bins; both models must agree.
+
+Rank 0 prints one JSON line.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    import torch.distributed as dist
+
+    import lambdagap_amd as lgb
+    from lambdagap_amd.parallel import shard_range
+    from lambdagap_amd.parallel.torch_network import init_torch_network
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+    init_torch_network()
+    os.environ["LGAP_DEVICE_DP_TRANSPORT"] = "host"
+    n = int(os.environ.get("DP_ROWS", "120000"))
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((n, 10))
+    X[rng.random(X.shape) < 0.03] = np.nan
+    y = ((np.nan_to_num(X[:, 0]) - 0.8 * np.nan_to_num(X[:, 2]) + 0.4 * np.nan_to_num(X[:, 5]) ** 2
+          + 0.3 * rng.standard_normal(n)) > 0.3).astype(float)
+    a, b = shard_range(n, rank, world)
+    base = {"objective": "binary", "num_leaves": 31, "verbosity": -1, "seed": 1, "min_data_in_leaf": 20,
+            "tree_learner": "data", "num_machines": world, "pre_partition": True, "deterministic": True}
+    ds = lgb.Dataset(X[a:b], y[a:b], params=dict(base, device_type="cpu"), free_raw_data=False).construct()
+    models = {}
+    devs = os.environ.get("DP_DEVICES", "gpu,cpu").split(",")
+    for dev in devs:
+        models[dev] = lgb.train(dict(base, device_type=dev), ds, 10)
+    first = models[devs[0]]
+    name = first.device_name()
+    text = first.model_to_string()
+    texts = [None] * world
+    dist.all_gather_object(texts, text)
+    pg, pc = first.predict(X), models[devs[-1]].predict(X)
+    if rank == 0:
+        from sklearn.metrics import roc_auc_score
+
+        print(json.dumps({"world": world, "device_name": name,
+                          "ranks_identical": all(t == texts[0] for t in texts),
+                          "num_trees": first.num_trees(),
+                          "max_abs_diff_vs_cpu_dp": float(np.max(np.abs(pg - pc))),
+                          "auc_gpu": float(roc_auc_score(y, pg)), "auc_cpu": float(roc_auc_score(y, pc))}),
+              flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

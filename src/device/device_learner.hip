@@ -1926,14 +1926,14 @@ class DeviceTreeLearner : public TreeLearner {
     TB_ = train->num_total_bin();
     width_ = train->bin_width();
     stride_dw_ = train->row_stride() / 4;
-    if (data_parallel_ && !CommActive() && Network::num_machines() > 1) {
+    if (data_parallel_ && !CommActive() && !HostStagedDP() && Network::num_machines() > 1) {
       Log::Fatal("Data-parallel HIP training needs an RCCL communicator (LGBM_DeviceCommInit)");
     }
     // LGAP_FORCE_DEVICE_DP=1 routes a single-rank run through the RCCL data-parallel path
     // (staging reduce + ncclAllReduce + global counts): lets a 1-GPU box test that path.
     const char* force_dp = std::getenv("LGAP_FORCE_DEVICE_DP");
     const bool forced = CommExists() && force_dp && force_dp[0] == '1';
-    distributed_ = (data_parallel_ && CommActive()) || forced;
+    distributed_ = (data_parallel_ && (CommActive() || HostStagedDP())) || forced;
     device_id_ = CommExists() ? CommDevice() : std::max(0, config_->gpu_device_id);
     HIP_CHECK(hipSetDevice(device_id_));
     hipDeviceProp_t prop;
@@ -2329,7 +2329,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   std::string DeviceName() const override {
-    return distributed_ ? device_name_ + " [RCCL data-parallel]" : device_name_;
+    if (!distributed_) return device_name_;
+    return device_name_ + (HostStagedDP() ? " [host-staged data-parallel]" : " [RCCL data-parallel]");
   }
 
   void ReportStamps(int nsplits) {

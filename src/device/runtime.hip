@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -189,9 +190,31 @@ bool CommExists() { return S().comm != nullptr; }
 ncclComm_t ActiveComm() { return S().comm; }
 int CommDevice() { return S().device; }
 
+bool HostStagedDP() {
+  static const bool on = [] {
+    const char* e = std::getenv("LGAP_DEVICE_DP_TRANSPORT");
+    return e != nullptr && std::strcmp(e, "host") == 0;
+  }();
+  return on && S().comm == nullptr && Network::num_machines() > 1;
+}
+
 void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream) {
+  if (count == 0) return;
+  if (HostStagedDP()) {
+    // Rehearsal transport (several ranks sharing one GPU, host Network underneath):
+    // device -> pinned host -> Network allreduce -> device. Not for production runs.
+    thread_local std::vector<double> h;
+    h.resize(count);
+    HIP_CHECK(hipMemcpyAsync(h.data(), dev_ptr, count * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    Network::Allreduce(reinterpret_cast<char*>(h.data()), static_cast<comm_size_t>(count * sizeof(double)),
+                       sizeof(double), reinterpret_cast<char*>(h.data()), Network::SumReducer<double>());
+    HIP_CHECK(hipMemcpyAsync(dev_ptr, h.data(), count * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    return;
+  }
   // a one-rank communicator still runs the collective (single-GPU rehearsal of the DP path)
-  if (!CommExists() || count == 0) return;
+  if (!CommExists()) return;
   NcclCheck(ncclAllReduce(dev_ptr, dev_ptr, count, ncclFloat64, ncclSum, S().comm, stream), "ncclAllReduce");
 }
 

@@ -13,6 +13,10 @@ ncclComm_t ActiveComm();
 int CommDevice();
 // communicator present (CommActive() additionally requires more than one rank)
 bool CommExists();
+// LGAP_DEVICE_DP_TRANSPORT=host with a multi-rank host Network and no RCCL
+// communicator: the device data-parallel learner stages its collectives through
+// host memory (lets several ranks share one GPU to rehearse the multi-rank path).
+bool HostStagedDP();
 // In-place sum all-reduce of device doubles on `stream` (no-op without a communicator).
 void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream);
 

@@ -184,6 +184,31 @@ def test_rccl_data_parallel_path_single_rank(lgb, gpu_required):
     assert res["max_abs_diff"] < 1e-3, res
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world):
+    """P ranks share the one GPU; the device data-parallel learner's collectives are staged
+    through host memory (gloo). Every rank must grow the identical model, and it must match
+    the host data-parallel learner trained by the same ranks on the same bins."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+                        "--nproc-per-node", str(world), os.path.join(root, "scripts", "dp_multirank.py")],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["world"] == world
+    assert "data-parallel" in res["device_name"], res
+    assert res["ranks_identical"], res
+    assert res["num_trees"] == 10
+    assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
+    assert abs(res["auc_gpu"] - res["auc_cpu"]) < 1e-3, res
+
+
 def _policy_data(rng, n=20000):
     X = rng.standard_normal((n, 6))
     z = 1.5 * X[:, 0] - X[:, 1] + 0.7 * X[:, 2] * X[:, 3] + 0.3 * rng.standard_normal(n)
