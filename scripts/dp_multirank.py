@@ -39,7 +39,11 @@ def main() -> int:
     y = ((np.nan_to_num(X[:, 0]) - 0.8 * np.nan_to_num(X[:, 2]) + 0.4 * np.nan_to_num(X[:, 5]) ** 2
           + 0.3 * rng.standard_normal(n)) > 0.3).astype(float)
     a, b = shard_range(n, rank, world)
-    base = {"objective": "binary", "num_leaves": 31, "verbosity": -1, "seed": 1, "min_data_in_leaf": 20,
+    # l2 regression: unit hessians make every histogram hessian sum and count estimate exact,
+    # so no min_data / min_hessian boundary can flip between the fixed-point device sums
+    # and the host's doubles; any model difference is then a transport or split-sync bug
+    objective = os.environ.get("DP_OBJECTIVE", "regression")
+    base = {"objective": objective, "num_leaves": 31, "verbosity": -1, "seed": 1, "min_data_in_leaf": 20,
             "tree_learner": "data", "num_machines": world, "pre_partition": True, "deterministic": True}
     ds = lgb.Dataset(X[a:b], y[a:b], params=dict(base, device_type="cpu"), free_raw_data=False).construct()
     models = {}
@@ -52,6 +56,26 @@ def main() -> int:
     texts = [None] * world
     dist.all_gather_object(texts, text)
     pg, pc = first.predict(X), models[devs[-1]].predict(X)
+    def splits(node, out):
+        if "split_index" in node:
+            out.append((node["split_feature"], round(node["threshold"], 6), node["split_gain"],
+                        node["internal_count"]))
+            splits(node["left_child"], out)
+            splits(node["right_child"], out)
+        return out
+
+    ta = [splits(t["tree_structure"], []) for t in first.dump_model()["tree_info"]]
+    tb = [splits(t["tree_structure"], []) for t in models[devs[-1]].dump_model()["tree_info"]]
+    same = 0
+    while same < min(len(ta), len(tb)) and [x[:2] for x in ta[same]] == [x[:2] for x in tb[same]]:
+        same += 1
+    if rank == 0 and os.environ.get("DP_DIAG"):
+        for i, (u, v) in enumerate(zip(ta, tb)):
+            if [x[:2] for x in u] != [x[:2] for x in v]:
+                print("first differing tree", i, file=sys.stderr)
+                for x, z in zip(u, v):
+                    print("  ", x, z, file=sys.stderr)
+                break
     if rank == 0:
         from sklearn.metrics import roc_auc_score
 
@@ -59,6 +83,8 @@ def main() -> int:
                           "ranks_identical": all(t == texts[0] for t in texts),
                           "num_trees": first.num_trees(),
                           "max_abs_diff_vs_cpu_dp": float(np.max(np.abs(pg - pc))),
+                          "mean_abs_diff_vs_cpu_dp": float(np.mean(np.abs(pg - pc))),
+                          "identical_leading_trees": same,
                           "auc_gpu": float(roc_auc_score(y, pg)), "auc_cpu": float(roc_auc_score(y, pc))}),
               flush=True)
     dist.barrier()

@@ -1838,10 +1838,12 @@ __global__ __launch_bounds__(kPartThreads) void k_post(Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// score update of the tree just grown: its final leaf ranges already list every
-// row (no bagging), so each leaf adds its value to its rows — one pass over the
-// row indices instead of a per-row tree traversal (serial_tree_learner
-// AddPredictionToScore via the data partition).
+// score update of the tree just grown from its final leaf ranges (every row, no
+// bagging): each leaf adds its value to its rows (serial_tree_learner
+// AddPredictionToScore via the data partition). Opt-in (LGAP_SCORE_PATH=leaves):
+// the scattered 8 B score updates touch one cache line per row, and the
+// LDS-staged traversal below measured faster on MI355X (10M rows: 374 us -> see
+// profiles/README.md).
 __global__ __launch_bounds__(256) void k_add_leaves(Args a, const double* __restrict__ leaf_value,
                                                     double* __restrict__ score) {
   const int leaf = blockIdx.y;
@@ -1855,32 +1857,58 @@ __global__ __launch_bounds__(256) void k_add_leaves(Args a, const double* __rest
 // ---------------------------------------------------------------------------
 // score update: traverse one uploaded tree over the packed rows
 
-__global__ __launch_bounds__(256) void k_add_tree(const uint32_t* __restrict__ rowbins, int stride_dw, int width,
-                                                  int N, const DevNode* __restrict__ nodes, int num_nodes,
-                                                  const uint32_t* __restrict__ cat_bits,
-                                                  const double* __restrict__ leaf_value, double* __restrict__ score) {
-  extern __shared__ DevNode s_nodes[];
+// One row per thread. A block first stages its 256 contiguous packed rows in LDS
+// with coalesced dword loads (rows are stride_dw dwords, not 16 B aligned), so
+// the per-level bin reads of the traversal are LDS hits instead of dependent
+// global loads; rows wider than kTraverseMaxDw read global memory directly.
+constexpr int kTraverseThreads = 256;
+constexpr int kTraverseMaxDw = 16;
+
+__device__ __forceinline__ bool NodeGoLeft(const DevNode& nd, uint32_t gb, const uint32_t* __restrict__ cat_bits) {
+  const uint32_t b = DecodeBin(nd.offset, nd.num_bin, nd.mfb, gb);
+  if (nd.decision & 1) {
+    const uint32_t wd = b >> 5;
+    return static_cast<int>(wd) < nd.cat_nwords && ((cat_bits[nd.cat_begin + wd] >> (b & 31u)) & 1u);
+  }
+  if ((nd.missing == 1 && b == static_cast<uint32_t>(nd.default_bin)) ||
+      (nd.missing == 2 && b == static_cast<uint32_t>(nd.num_bin - 1))) {
+    return (nd.decision & 2) != 0;
+  }
+  return b <= static_cast<uint32_t>(nd.threshold);
+}
+
+__global__ __launch_bounds__(kTraverseThreads) void k_add_tree(const uint32_t* __restrict__ rowbins, int stride_dw,
+                                                               int width, int N, const DevNode* __restrict__ nodes,
+                                                               int num_nodes, const uint32_t* __restrict__ cat_bits,
+                                                               const double* __restrict__ leaf_value,
+                                                               double* __restrict__ score) {
+  extern __shared__ uint32_t s_dyn[];
+  DevNode* s_nodes = reinterpret_cast<DevNode*>(s_dyn);
+  uint32_t* s_rows = s_dyn + num_nodes * (sizeof(DevNode) / 4);
   for (int i = threadIdx.x; i < num_nodes; i += blockDim.x) s_nodes[i] = nodes[i];
-  __syncthreads();
-  const int stride = gridDim.x * blockDim.x;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
-    const uint8_t* row = reinterpret_cast<const uint8_t*>(rowbins + static_cast<size_t>(i) * stride_dw);
+  const bool staged = stride_dw <= kTraverseMaxDw;
+  for (long long base = static_cast<long long>(blockIdx.x) * kTraverseThreads; base < N;
+       base += static_cast<long long>(gridDim.x) * kTraverseThreads) {
+    const int rows = static_cast<int>(min(static_cast<long long>(kTraverseThreads), N - base));
+    const int i = static_cast<int>(base) + threadIdx.x;
+    const uint8_t* row;
+    if (staged) {
+      __syncthreads();  // previous chunk's readers are done (and the nodes are in place)
+      const uint32_t* src = rowbins + base * stride_dw;
+      const int ndw = rows * stride_dw;
+      for (int k = threadIdx.x; k < ndw; k += kTraverseThreads) s_rows[k] = src[k];
+      __syncthreads();
+      row = reinterpret_cast<const uint8_t*>(s_rows + threadIdx.x * stride_dw);
+    } else {
+      if (base == static_cast<long long>(blockIdx.x) * kTraverseThreads) __syncthreads();
+      row = reinterpret_cast<const uint8_t*>(rowbins + static_cast<size_t>(i) * stride_dw);
+    }
+    if (threadIdx.x >= rows) continue;
     int node = 0;
     while (node >= 0) {
       const DevNode& nd = s_nodes[node];
       const uint32_t gb = width == 1 ? row[nd.group] : reinterpret_cast<const uint16_t*>(row)[nd.group];
-      const uint32_t b = DecodeBin(nd.offset, nd.num_bin, nd.mfb, gb);
-      bool left;
-      if (nd.decision & 1) {
-        const uint32_t wd = b >> 5;
-        left = static_cast<int>(wd) < nd.cat_nwords && ((cat_bits[nd.cat_begin + wd] >> (b & 31u)) & 1u);
-      } else if ((nd.missing == 1 && b == static_cast<uint32_t>(nd.default_bin)) ||
-                 (nd.missing == 2 && b == static_cast<uint32_t>(nd.num_bin - 1))) {
-        left = (nd.decision & 2) != 0;
-      } else {
-        left = b <= static_cast<uint32_t>(nd.threshold);
-      }
-      node = left ? nd.left : nd.right;
+      node = NodeGoLeft(nd, gb, cat_bits) ? nd.left : nd.right;
     }
     score[i] += leaf_value[~node];
   }
@@ -2171,7 +2199,11 @@ class DeviceTreeLearner : public TreeLearner {
       return;
     }
     if (tree->is_linear()) Log::Fatal("Linear trees cannot be applied on the device");
-    if (tree == last_trained_ && !use_bag_ && tree->num_leaves() == static_cast<int>(h_range_.size())) {
+    static const int score_path = [] {
+      const char* e = std::getenv("LGAP_SCORE_PATH");
+      return e == nullptr ? 0 : (std::strcmp(e, "leaves") == 0 ? 1 : (std::strcmp(e, "traverse") == 0 ? 2 : 0));
+    }();
+    if (score_path == 1 && tree == last_trained_ && !use_bag_ && tree->num_leaves() == static_cast<int>(h_range_.size())) {
       last_trained_ = nullptr;
       const int nl = tree->num_leaves();
       double* lv = reinterpret_cast<double*>(pin_tree_.Get(sizeof(double) * nl));
@@ -2232,8 +2264,10 @@ class DeviceTreeLearner : public TreeLearner {
     const DevNode* dn = reinterpret_cast<const DevNode*>(tree_buf_.get());
     const double* dl = reinterpret_cast<const double*>(tree_buf_.get() + node_bytes);
     const uint32_t* dc = reinterpret_cast<const uint32_t*>(tree_buf_.get() + node_bytes + leaf_bytes);
-    const int grid = std::min(DivUp(N_, 256), num_cu_ * 8);
-    k_add_tree<<<std::max(grid, 1), 256, node_bytes, stream_>>>(rowbins_.get(), stride_dw_, width_, N_, dn, nn, dc, dl, s);
+    const int grid = std::min(DivUp(N_, kTraverseThreads), num_cu_ * 8);
+    const size_t lds = node_bytes + (stride_dw_ <= kTraverseMaxDw ? sizeof(uint32_t) * kTraverseThreads * stride_dw_ : 0);
+    k_add_tree<<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins_.get(), stride_dw_, width_, N_, dn, nn, dc,
+                                                                      dl, s);
     HIP_CHECK(hipGetLastError());
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_CHECK(hipStreamSynchronize(stream_));

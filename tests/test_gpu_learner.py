@@ -205,6 +205,8 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world):
     assert "data-parallel" in res["device_name"], res
     assert res["ranks_identical"], res
     assert res["num_trees"] == 10
+    # unit hessians (l2): the split structure must match the host learner tree for tree
+    assert res["identical_leading_trees"] == 10, res
     assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
     assert abs(res["auc_gpu"] - res["auc_cpu"]) < 1e-3, res
 
