@@ -13,7 +13,7 @@ CXXFLAGS ?= -O3 -g0 -std=c++17 -fPIC -fopenmp -Wall -Wno-unused-function -Wno-si
             -D__HIP_PLATFORM_AMD__=1 -I$(ROCM)/include
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Isrc -munsafe-fp-atomics \
             -Wno-unused-result -ffp-contract=fast
-LDFLAGS ?= -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
+LDFLAGS ?= -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 
 CPP_SRCS := $(shell find src -name '*.cpp' ! -path 'src/cli/*' | sort)
 HIP_SRCS := $(shell find src -name '*.hip' | sort)

@@ -4,6 +4,7 @@
 // reference's fmt "{:g}"/"{:.17g}" output for the model text format.
 #pragma once
 
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -292,12 +293,17 @@ class PhaseTimer {
   std::map<std::string, std::pair<double, long long>> stats_;
 };
 
+// Every ScopedTimer phase is also a roctx range ("lgap:<phase>"), so
+// `rocprofv3 --marker-trace` lines the phases up with the kernel trace
+// (SURVEY.md 5.1). roctx calls are no-ops unless a profiler is attached.
 class ScopedTimer {
  public:
   explicit ScopedTimer(const char* name) : name_(name) {
+    roctxRangePushA(name);
     if (PhaseTimer::Global().enabled()) start_ = std::chrono::steady_clock::now();
   }
   ~ScopedTimer() {
+    roctxRangePop();
     if (PhaseTimer::Global().enabled()) {
       auto d = std::chrono::duration<double>(std::chrono::steady_clock::now() - start_).count();
       PhaseTimer::Global().Add(name_, d);

@@ -45,6 +45,8 @@ for s in "$@"; do
     stampsmall) LGAP_STAMPS=1 step stampsmall 600 python bench.py --rows 1250000 --steps 2 --warmup 1;;
     profsmall) step profsmall 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/profsmall -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 && python scripts/prof_summary.py $OUT/profsmall "1.25M rows, graph path" 22 > $OUT/profsmall_summary.md;;
     profsmalldp) step profsmalldp 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/profsmalldp -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 --rehearse-dp && python scripts/prof_summary.py $OUT/profsmalldp "1.25M rows, DP rehearsal path" 22 > $OUT/profsmalldp_summary.md;;
+    marker) step marker 900 rocprofv3 --marker-trace --kernel-trace --stats -d $PWD/$OUT/marker -o run -- python3 bench.py --rows 1250000 --steps 10 --warmup 2 --rehearse-dp;;
+    watchdog) step watchdog 300 python scripts/watchdog_selftest.py;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run -- python3 bench.py --steps 20 --warmup 2 && python scripts/prof_summary.py $OUT/prof "10M rows x 28, 63 leaves" 22 > $OUT/prof_summary.md;;
   esac
 done

@@ -9,9 +9,12 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <thread>
 
 #include "lgap/common.h"
 #include "lgap/log.h"
@@ -211,8 +214,35 @@ void GBDT::UpdateScore(const Tree* tree, int k) {
   }
 }
 
+// Fault injection for failure-detection tests (no reference counterpart: the
+// reference has none). LGAP_FAULT_INJECT="<rank>:<iter>:<mode>"
+// makes machine <rank> fail when it starts boosting iteration <iter>:
+// mode "exit" ends the process at once (no cleanup, sockets / communicator
+// dropped), "hang" stops it in place so its peers' timeouts / the collective
+// watchdog must notice, "throw" raises a fatal error through the normal path.
+static void MaybeInjectFault(int iter) {
+  static const char* spec = std::getenv("LGAP_FAULT_INJECT");
+  if (spec == nullptr || *spec == '\0') return;
+  int rank = -1, at = -1;
+  char mode[16] = {0};
+  if (std::sscanf(spec, "%d:%d:%15s", &rank, &at, mode) != 3) Log::Fatal("Malformed LGAP_FAULT_INJECT=%s", spec);
+  if (iter != at || rank != std::max(0, Network::rank())) return;
+  if (std::strcmp(mode, "exit") == 0) {
+    std::fprintf(stderr, "[fault-inject] rank %d exits at iteration %d\n", rank, iter);
+    std::fflush(stderr);
+    std::_Exit(3);
+  } else if (std::strcmp(mode, "hang") == 0) {
+    std::fprintf(stderr, "[fault-inject] rank %d hangs at iteration %d\n", rank, iter);
+    std::fflush(stderr);
+    for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+  } else {
+    Log::Fatal("[fault-inject] rank %d fails at iteration %d", rank, iter);
+  }
+}
+
 bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
   ScopedTimer timer("GBDT::TrainOneIter");
+  MaybeInjectFault(iter_);
   std::vector<double> init_scores(num_tree_per_iteration_, 0.0);
   const bool custom = gradients != nullptr && hessians != nullptr;
   if (!custom) {

@@ -2002,6 +2002,7 @@ class DeviceTreeLearner : public TreeLearner {
   bool SupportsDeviceSampling() const override { return true; }
 
   void DeviceSample(int plan, int iter) override {
+    ScopedTimer timer("Device::Sample");
     if (plan == kSampleKeep) return;
     if (plan == kSampleAll) {
       SetBaggingData(nullptr, N_);
@@ -2138,6 +2139,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceComputeGradients(const ObjectiveFunction* obj) override {
+    ScopedTimer timer("Device::ComputeGradients");
     PrepareObjective(obj);
     switch (obj->device_kind()) {
       case DeviceGradKind::kPointwise:
@@ -2193,6 +2195,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceAddTreeToScore(const Tree* tree, int k) override {
+    ScopedTimer timer("Device::AddTreeToScore");
     double* s = score_.get() + static_cast<size_t>(k) * N_;
     if (tree->num_leaves() <= 1) {
       if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, N_, tree->LeafOutput(0), stream_);
@@ -2318,7 +2321,13 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(hlo, lout_.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
     unsigned* hbar = pin_bar_.Get(4);
     HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (distributed_) {
+      // the tree's histogram all-reduces ride on this stream: a lost peer must not hang us
+      static const double timeout_s = CommTimeoutSeconds(config_->time_out);
+      WatchedStreamSync(stream_, timeout_s, "device tree growth (RCCL histogram all-reduce)");
+    } else {
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
     if (hbar[2] != 0u) Log::Fatal("k_partition: a wait on published tile counts timed out (blocks not co-resident?)");
     // the control buffer written last holds the final tree state
     const Ctl* hc = hc2[1].num_splits > hc2[0].num_splits ? &hc2[1] : &hc2[0];

@@ -11,10 +11,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "device/hip_common.h"
@@ -216,6 +218,50 @@ void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream) {
   // a one-rank communicator still runs the collective (single-GPU rehearsal of the DP path)
   if (!CommExists()) return;
   NcclCheck(ncclAllReduce(dev_ptr, dev_ptr, count, ncclFloat64, ncclSum, S().comm, stream), "ncclAllReduce");
+}
+
+// Collective watchdog (the reference only has socket timeouts; a lost
+// worker hangs its peers). Waits for `stream` while polling the communicator's
+// asynchronous error state; on an RCCL error, or when the wait outlives
+// `timeout_s` (a peer stopped joining the collectives, so the RCCL kernels on
+// this stream wait forever), the communicator is aborted — which releases
+// those kernels — and the failure is raised as a fatal error on this rank.
+void WatchedStreamSync(hipStream_t stream, double timeout_s, const char* what) {
+  auto& s = S();
+  if (s.comm == nullptr) {  // (a one-rank communicator is watched too: the rehearsal path)
+    HIP_CHECK(hipStreamSynchronize(stream));
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long long polls = 0;; ++polls) {
+    const hipError_t r = hipStreamQuery(stream);
+    if (r == hipSuccess) return;
+    if (r != hipErrorNotReady) HIP_CHECK(r);
+    ncclResult_t ae = ncclSuccess;
+    if (ncclCommGetAsyncError(s.comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+      (void)ncclCommAbort(s.comm);
+      s.comm = nullptr;
+      Log::Fatal("RCCL asynchronous error during %s on rank %d: %s", what, s.rank, ncclGetErrorString(ae));
+    }
+    if ((polls & 255) == 0 && timeout_s > 0) {
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s) {
+        (void)ncclCommAbort(s.comm);
+        s.comm = nullptr;
+        Log::Fatal("%s did not finish within %.1f s on rank %d: a peer stopped joining the collectives; "
+                   "RCCL communicator aborted",
+                   what, timeout_s, s.rank);
+      }
+    }
+    // spin for the first milliseconds (a tree takes a few), then back off
+    if (polls > 4096) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+double CommTimeoutSeconds(int time_out_minutes) {
+  const char* e = std::getenv("LGAP_COMM_TIMEOUT_S");
+  if (e != nullptr && *e != '\0') return std::atof(e);
+  return 60.0 * std::max(1, time_out_minutes);
 }
 
 }  // namespace device

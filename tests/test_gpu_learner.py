@@ -293,3 +293,20 @@ def test_forced_splits_over_device_histograms(lgb, gpu_required, rng, tmp_path):
         root = _trees(b)[0]["tree_structure"]
         assert root["split_feature"] == 4 and root["left_child"]["split_feature"] == 5
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
+
+
+def test_collective_watchdog_aborts_on_timeout(lgb, gpu_required):
+    """The RCCL watchdog (runtime.hip WatchedStreamSync): a collective wait that outlives the
+    timeout aborts the communicator and raises on the rank instead of hanging."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "watchdog_selftest.py")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["raised"], res
+    assert "communicator aborted" in res["message"], res
