@@ -52,6 +52,32 @@ def main(path, title, steps=None):
         short = short.split("(")[0]
         print(f"| `{short[:70]}` | {n} | {tot / 1e6:.2f} | {avg / 1e3:.2f} | {mn / 1e3:.2f} | {mx / 1e3:.2f} | "
               f"{100.0 * tot / total:.1f} |")
+    _phases(c)
+
+
+def _phases(c):
+    """roctx phase ranges (ScopedTimer -> roctxRangePushA, rocprofv3 --marker-trace), host wall time."""
+    import json
+
+    try:
+        rows = c.execute("select extdata, end - start from regions where category like 'MARKER%'").fetchall()
+    except sqlite3.OperationalError:
+        return
+    agg = {}
+    for ext, dur in rows:
+        try:
+            name = json.loads(ext).get("message", "?")
+        except (TypeError, ValueError):
+            name = "?"
+        n, t = agg.get(name, (0, 0))
+        agg[name] = (n + 1, t + dur)
+    if not agg:
+        return
+    print("\nroctx phases (host wall time between push and pop; `rocprofv3 --marker-trace`):\n")
+    print("| phase | calls | total ms | avg us |")
+    print("|---|---:|---:|---:|")
+    for name, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"| `{name}` | {n} | {t / 1e6:.2f} | {t / 1e3 / n:.1f} |")
 
 
 if __name__ == "__main__":
