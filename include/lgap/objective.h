@@ -68,6 +68,8 @@ struct LambdarankTables {
   const std::vector<double>* table;
 };
 bool GetLambdarankTables(const ObjectiveFunction* obj, LambdarankTables* out);
+// objective_seed of a rank_xendcg objective (its per-query Random streams start at seed + q)
+bool GetXendcgSeed(const ObjectiveFunction* obj, int* seed);
 
 double Percentile(std::vector<double> v, double alpha);
 double WeightedPercentile(const std::vector<double>& v, const std::vector<double>& w, double alpha);

@@ -2115,7 +2115,8 @@ class DeviceTreeLearner : public TreeLearner {
         return obj->pointwise() != nullptr && obj->effective_label() != nullptr;
       case DeviceGradKind::kSoftmax:
         return obj->effective_label() != nullptr;
-      case DeviceGradKind::kLambdarank: {
+      case DeviceGradKind::kLambdarank:
+      case DeviceGradKind::kXendcg: {
         const Metadata& md = data_->metadata();
         if (md.positions() != nullptr || md.num_queries() == 0) return false;
         const data_size_t* qb = md.query_boundaries();
@@ -2155,6 +2156,13 @@ class DeviceTreeLearner : public TreeLearner {
         ra.score = score_.get();
         ra.gh = gh_.get();
         LaunchLambdarankGrad(ra, stream_);
+        break;
+      }
+      case DeviceGradKind::kXendcg: {
+        XendcgArgs xa = xendcg_args_;
+        xa.score = score_.get();
+        xa.gh = gh_.get();
+        LaunchXendcgGrad(xa, stream_);
         break;
       }
       default:
@@ -2990,6 +2998,21 @@ class DeviceTreeLearner : public TreeLearner {
       r.label = label_.get();
       r.weight = weight_.size() ? weight_.get() : nullptr;
     }
+    if (obj->device_kind() == DeviceGradKind::kXendcg) {
+      int seed = 0;
+      if (!GetXendcgSeed(obj, &seed)) Log::Fatal("rank_xendcg state unavailable");
+      const int nq = md.num_queries();
+      std::vector<unsigned> st(std::max(nq, 1));
+      for (int q = 0; q < nq; ++q) st[q] = static_cast<unsigned>(seed + q);  // Random(seed + q)
+      xendcg_state_.Upload(st, stream_);
+      rank_qb_.Upload(md.query_boundaries_vec(), stream_);
+      XendcgArgs& x = xendcg_args_;
+      x.qb = rank_qb_.get();
+      x.num_queries = nq;
+      x.label = label_.get();
+      x.weight = weight_.size() ? weight_.get() : nullptr;
+      x.state = xendcg_state_.get();
+    }
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
@@ -3059,6 +3082,8 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<double> rank_table_, rank_gain_, rank_inv_dcg_, rank_inv_bdcg_;
   DevBuf<int> rank_qb_;
   RankKernelArgs rank_args_;
+  DevBuf<unsigned> xendcg_state_;
+  XendcgArgs xendcg_args_;
   // pinned staging
   PinnedBuf<TreeParams> pin_tp_;
   PinnedBuf<uint8_t> pin_mask_;

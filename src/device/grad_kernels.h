@@ -39,6 +39,17 @@ struct RankKernelArgs {
 constexpr int kMaxDeviceQuery = 2048;
 void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s);
 
+struct XendcgArgs {
+  const int* qb = nullptr;  // query boundaries (num_queries + 1)
+  int num_queries = 0;
+  const float* label = nullptr;
+  const float* weight = nullptr;
+  const double* score = nullptr;
+  unsigned* state = nullptr;  // per-query LCG state (Random(objective_seed + q))
+  float2* gh = nullptr;
+};
+void LaunchXendcgGrad(const XendcgArgs& a, hipStream_t s);
+
 void LaunchAddConstant(double* score, int n, double v, hipStream_t s);
 
 }  // namespace device

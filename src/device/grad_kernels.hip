@@ -260,6 +260,88 @@ int GridFor(int n) {
   return g < 1 ? 1 : (g > 65536 ? 65536 : g);
 }
 
+// rank_xendcg (rank_objective.hpp:620-700; host twin RankXENDCG::OneQuery): one
+// workgroup per query. The order-dependent parts (softmax max / denominator,
+// the query's LCG draws, the three sums) run on lane 0 in document order so
+// the lambdas match the host objective's sequential sums; the per-document
+// terms run on all lanes from LDS. state[q] is the query's Random, advanced by
+// cnt draws per call exactly like the host's rands_[q].
+__global__ __launch_bounds__(kRankThreads) void k_xendcg(XendcgArgs a) {
+  __shared__ double s_rho[kMaxDeviceQuery];
+  __shared__ double s_p[kMaxDeviceQuery];
+  __shared__ float s_lam[kMaxDeviceQuery];
+  __shared__ double s_v[3];
+  const int q = blockIdx.x;
+  const int t = threadIdx.x;
+  const int start = a.qb[q];
+  const int cnt = a.qb[q + 1] - start;
+  float2* out = a.gh + start;
+  const double* score = a.score + start;
+  const float* label = a.label + start;
+  if (cnt <= 1) {  // the host returns before drawing
+    for (int i = t; i < cnt; i += blockDim.x) out[i] = make_float2(0.f, 0.f);
+    return;
+  }
+  if (t == 0) {
+    double wmax = score[0];
+    for (int i = 1; i < cnt; ++i) wmax = fmax(wmax, score[i]);
+    s_v[0] = wmax;
+  }
+  __syncthreads();
+  for (int i = t; i < cnt; i += blockDim.x) s_rho[i] = exp(score[i] - s_v[0]);
+  __syncthreads();
+  if (t == 0) {
+    double den = 0.0;
+    for (int i = 0; i < cnt; ++i) den += s_rho[i];
+    unsigned x = a.state[q];
+    double sp = 0.0;
+    for (int i = 0; i < cnt; ++i) {
+      x = 214013u * x + 2531011u;
+      const float r = static_cast<float>(static_cast<int>((x >> 16) & 0x7FFF)) / 32768.0f;
+      const double pi = pow(2.0, static_cast<int>(label[i])) - r;
+      s_p[i] = pi;
+      sp += pi;
+    }
+    a.state[q] = x;
+    s_v[1] = den;
+    s_v[2] = 1.0 / fmax(kEpsilon, sp);
+  }
+  __syncthreads();
+  const double den = s_v[1], inv_den = s_v[2];
+  for (int i = t; i < cnt; i += blockDim.x) {
+    const double rho = s_rho[i] / den;
+    s_rho[i] = rho;
+    const double term = -s_p[i] * inv_den + rho;
+    s_lam[i] = static_cast<float>(term);
+    s_p[i] = term / (1. - rho);
+  }
+  __syncthreads();
+  for (int pass = 0; pass < 2; ++pass) {
+    if (t == 0) {
+      double sum = 0.0;
+      for (int i = 0; i < cnt; ++i) sum += s_p[i];
+      s_v[0] = sum;
+    }
+    __syncthreads();
+    const double sum = s_v[0];
+    for (int i = t; i < cnt; i += blockDim.x) {
+      const double term = s_rho[i] * (sum - s_p[i]);
+      s_lam[i] += static_cast<float>(term);
+      if (pass == 0) s_p[i] = term / (1. - s_rho[i]);
+    }
+    __syncthreads();
+  }
+  for (int i = t; i < cnt; i += blockDim.x) {
+    float g = s_lam[i];
+    float h = static_cast<float>(s_rho[i] * (1.0 - s_rho[i]));
+    if (a.weight) {
+      g = static_cast<float>(g * a.weight[start + i]);
+      h = static_cast<float>(h * a.weight[start + i]);
+    }
+    out[i] = make_float2(g, h);
+  }
+}
+
 }  // namespace
 
 void LaunchPointwiseGrad(const PointwiseParams& p, const double* score, const float* label, const float* weight,
@@ -279,6 +361,12 @@ void LaunchSoftmaxGrad(int num_class, double factor, const double* score, const 
 void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s) {
   if (a.num_queries <= 0) return;
   k_lambdarank<<<a.num_queries, kRankThreads, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchXendcgGrad(const XendcgArgs& a, hipStream_t s) {
+  if (a.num_queries <= 0) return;
+  k_xendcg<<<a.num_queries, kRankThreads, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 

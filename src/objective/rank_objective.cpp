@@ -345,6 +345,8 @@ class RankXENDCG : public RankingBase {
     }
   }
   const char* GetName() const override { return "rank_xendcg"; }
+  DeviceGradKind device_kind() const override { return DeviceGradKind::kXendcg; }
+  int objective_seed() const { return seed_; }
 
  private:
   mutable std::vector<Random> rands_;
@@ -364,6 +366,13 @@ std::unique_ptr<ObjectiveFunction> CreateRankObjectiveFromString(const std::stri
 }
 
 // Device learners need the lambdarank tables; expose a narrow accessor.
+bool GetXendcgSeed(const ObjectiveFunction* obj, int* seed) {
+  auto* x = dynamic_cast<const RankXENDCG*>(obj);
+  if (!x) return false;
+  *seed = x->objective_seed();
+  return true;
+}
+
 bool GetLambdarankTables(const ObjectiveFunction* obj, LambdarankTables* out) {
   auto* l = dynamic_cast<const LambdarankObjective*>(obj);
   if (!l) return false;
