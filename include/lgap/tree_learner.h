@@ -20,12 +20,13 @@ namespace lgap {
 // What the boosting loop asks a device learner to do with the row sample of
 // this iteration (SampleStrategy::PlanDevice).
 enum DeviceSamplePlan {
-  kSampleHost = -2,      // the host SampleStrategy draws it (bagging by query)
+  kSampleHost = -2,      // the host SampleStrategy draws it
   kSampleAll = -1,       // train on all rows
   kSampleKeep = 0,       // keep the current bag
   kSampleBag = 1,        // uniform bagging (bagging_fraction)
   kSampleBalanced = 2,   // balanced bagging (pos/neg_bagging_fraction)
   kSampleGoss = 3,       // GOSS (top_rate / other_rate)
+  kSampleBagQuery = 4,   // bagging by query (whole queries kept or dropped)
 };
 
 class TreeLearner {

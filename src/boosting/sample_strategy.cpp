@@ -121,9 +121,9 @@ int SampleStrategy::PlanDevice(int iter) {
   }
   const bool bagging = cfg_->bagging_freq > 0 && (cfg_->bagging_fraction < 1.0 || balanced_);
   if (!bagging) return kSampleKeep;
-  if (by_query_) return kSampleHost;
   if (!(need_rebag_ || iter % cfg_->bagging_freq == 0)) return kSampleKeep;
   need_rebag_ = false;
+  if (by_query_) return kSampleBagQuery;
   return balanced_ ? kSampleBalanced : kSampleBag;
 }
 

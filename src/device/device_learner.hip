@@ -2013,8 +2013,10 @@ class DeviceTreeLearner : public TreeLearner {
       std::vector<uint2> jt(kSampleRandBlock);
       BuildLcgJumpTable(jt.data());
       samp_jump_.Upload(jt, stream_);
-      // Random(bagging_seed + block) per 1024-row block, as SampleStrategy seeds them
-      std::vector<unsigned> st(std::max(1, DivUp(N_, kSampleRandBlock)));
+      // Random(bagging_seed + block) per 1024-unit block (rows, or queries when bagging
+      // by query), as SampleStrategy seeds them
+      const int units = plan == kSampleBagQuery ? data_->metadata().num_queries() : N_;
+      std::vector<unsigned> st(std::max(1, DivUp(units, kSampleRandBlock)));
       for (size_t b = 0; b < st.size(); ++b) st[b] = static_cast<unsigned>(config_->bagging_seed + static_cast<int>(b));
       samp_rng_.Upload(st, stream_);
       samp_cnt_.Resize(std::max(nt, 1));
@@ -2022,7 +2024,19 @@ class DeviceTreeLearner : public TreeLearner {
       samp_total_.Resize(1);
     }
     SampleArgs a;
-    a.mode = plan == kSampleGoss ? 3 : (plan == kSampleBalanced ? 2 : 1);
+    a.mode = plan == kSampleGoss ? 3 : (plan == kSampleBalanced ? 2 : (plan == kSampleBagQuery ? 4 : 1));
+    if (a.mode == 4) {
+      const Metadata& md = data_->metadata();
+      if (row_query_.size() == 0) {
+        std::vector<int> rq(std::max(N_, 1));
+        const data_size_t* qb = md.query_boundaries();
+        for (data_size_t q = 0; q < md.num_queries(); ++q)
+          for (data_size_t i = qb[q]; i < qb[q + 1]; ++i) rq[i] = q;
+        row_query_.Upload(rq, stream_);
+      }
+      a.row_unit = row_query_.get();
+      a.num_units = md.num_queries();
+    }
     a.N = N_;
     a.K = K_;
     a.fraction = config_->bagging_fraction;
@@ -2044,6 +2058,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.total = samp_total_.get();
     LaunchSampleCount(a, stream_);
     LaunchSampleScatter(a, stream_);
+    if (a.mode == 4) LaunchSampleAdvanceUnits(a, stream_);
     int* cnt = pin_cnt_.Get(1);
     samp_total_.Download(cnt, 1, stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -3083,6 +3098,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<int> rank_qb_;
   RankKernelArgs rank_args_;
   DevBuf<unsigned> xendcg_state_;
+  DevBuf<int> row_query_;  // bagging by query: query of each row
   XendcgArgs xendcg_args_;
   // pinned staging
   PinnedBuf<TreeParams> pin_tp_;

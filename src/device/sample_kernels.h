@@ -26,7 +26,7 @@ constexpr int kSampleTile = 4096;       // rows per workgroup (256 threads x 16 
 constexpr int kSampleRandBlock = 1024;  // rows per bagging Random stream (SampleStrategy kRandBlock)
 
 struct SampleArgs {
-  int mode = 0;  // 1 bagging, 2 balanced bagging, 3 GOSS
+  int mode = 0;  // 1 bagging, 2 balanced bagging, 3 GOSS, 4 bagging by query
   int N = 0;
   int K = 1;  // classes (GOSS sums |g*h| over them and scales all of them)
   double fraction = 1.0, pos_fraction = 1.0, neg_fraction = 1.0;
@@ -35,6 +35,9 @@ struct SampleArgs {
   const float* label = nullptr;  // balanced bagging
   float2* gh = nullptr;          // GOSS: class-major (g, h), scaled in place
   unsigned* rng = nullptr;       // bagging: one LCG state per 1024-row block (advanced by the scatter)
+                                 // (by query: per 1024-query block, advanced by LaunchSampleAdvanceUnits)
+  const int* row_unit = nullptr; // bagging by query: query of each row
+  int num_units = 0;             // bagging by query: number of queries
   const uint2* jump = nullptr;   // bagging: state after j + 1 steps = jump[j].x * s + jump[j].y
   int* tile_cnt = nullptr;       // kept rows per tile
   unsigned* tile_sel = nullptr;  // GOSS, 4 words per tile: top threshold bits, key threshold, key mode, multiplier bits
@@ -48,6 +51,9 @@ inline int SampleTiles(int n) { return (n + kSampleTile - 1) / kSampleTile; }
 void LaunchSampleCount(const SampleArgs& a, hipStream_t s);
 // stable compaction of the kept rows (+ GOSS scaling, + bagging stream advance); writes *total
 void LaunchSampleScatter(const SampleArgs& a, hipStream_t s);
+// bagging by query: advance the per-1024-query streams past this bag's draws
+// (a separate launch: every row tile reads the shared query streams)
+void LaunchSampleAdvanceUnits(const SampleArgs& a, hipStream_t s);
 // (a^j, c_j) of the reference LCG for j = 1..1024 (host side)
 void BuildLcgJumpTable(uint2* out);
 

@@ -26,6 +26,8 @@ constexpr int kWaves = kThreads / kWave;
 
 // Bagging decision of row i: SampleStrategy::BagBlock's draw, jumped to directly.
 __device__ __forceinline__ bool BagKeep(const SampleArgs& a, int i) {
+  // by query: every row of query u shares the query's draw (u-th unit of the streams)
+  if (a.mode == 4) i = a.row_unit[i];
   const unsigned s = a.rng[i / kSampleRandBlock];
   const uint2 j = a.jump[i % kSampleRandBlock];
   const unsigned x = j.x * s + j.y;
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(kThreads) void k_sample_scatter(SampleArgs a, int n
         v.y *= mul;
       }
     }
-  } else {
+  } else if (a.mode != 4) {
     // every draw of this tile's streams is consumed: advance them (this block alone owns them)
     __syncthreads();
     constexpr int kStreams = kSampleTile / kSampleRandBlock;
@@ -254,7 +256,23 @@ __global__ __launch_bounds__(kThreads) void k_sample_scatter(SampleArgs a, int n
   }
 }
 
+__global__ __launch_bounds__(kThreads) void k_sample_advance_units(SampleArgs a) {
+  const int b = blockIdx.x * kThreads + threadIdx.x;
+  const int units = min(kSampleRandBlock, a.num_units - b * kSampleRandBlock);
+  if (units > 0) {
+    const uint2 j = a.jump[units - 1];
+    a.rng[b] = j.x * a.rng[b] + j.y;
+  }
+}
+
 }  // namespace
+
+void LaunchSampleAdvanceUnits(const SampleArgs& a, hipStream_t s) {
+  const int streams = (a.num_units + kSampleRandBlock - 1) / kSampleRandBlock;
+  if (streams <= 0) return;
+  k_sample_advance_units<<<(streams + kThreads - 1) / kThreads, kThreads, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
 
 void LaunchSampleCount(const SampleArgs& a, hipStream_t s) {
   const int nt = SampleTiles(a.N);

@@ -4,6 +4,12 @@ import sys
 import numpy as np
 import pytest
 
+# pytest-xdist: N workers x (all cores) OpenMP threads spin against each other and
+# slow the CPU learner tests down ~100x; give each worker a fair share instead
+if os.environ.get("PYTEST_XDIST_WORKER") and "OMP_NUM_THREADS" not in os.environ:
+    _n = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1"))
+    os.environ["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // max(1, _n)))
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -310,3 +310,26 @@ def test_collective_watchdog_aborts_on_timeout(lgb, gpu_required):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["raised"], res
     assert "communicator aborted" in res["message"], res
+
+
+def test_device_bagging_by_query_matches_host(lgb, gpu_required):
+    """bagging_by_query drawn on the device (one draw per query from the per-1024-query LCG
+    streams, every row of a kept query kept, streams advanced across re-bags) trains the
+    host sampler's model."""
+    from lambdagap_amd.utils import make_ranking
+
+    X, y, sizes = make_ranking(400, num_features=20, seed=9)
+    params = {"objective": "lambdarank", "num_leaves": 15, "verbosity": -1, "bagging_by_query": True,
+              "bagging_fraction": 0.6, "bagging_freq": 2, "bagging_seed": 5}
+    bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y, group=sizes), 6)
+    bg = lgb.train({**params, "device_type": "gpu"}, lgb.Dataset(X, y, group=sizes), 6)
+    bh = lgb.train({**params, "device_type": "gpu", "device_sampling": False}, lgb.Dataset(X, y, group=sizes), 6)
+    pc, pg, ph = (b.predict(X, raw_score=True) for b in (bc, bg, bh))
+    # device draw == host draw: the device-sampled model has the host-sampled device model's
+    # splits (leaf values agree to float rounding)
+    def splits(b):
+        return [ln for ln in b.model_to_string().splitlines() if ln.startswith(("split_feature=", "threshold="))]
+
+    assert splits(bg) == splits(bh)
+    np.testing.assert_allclose(pg, ph, rtol=1e-4, atol=1e-5)
+    assert np.corrcoef(pc, pg)[0, 1] > 0.999
