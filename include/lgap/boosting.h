@@ -147,6 +147,9 @@ class GBDT {
   void AddScoreConstant(double v, int cur_tree_id);
   void SyncTrainScoreFromDevice();
   void ResetGradientBuffers();
+  std::vector<double> EvalTraining(const Metric* m, const double** score);
+  // DART drops trees when the training score is first read in an iteration: keep that read
+  virtual bool DeviceMetricsAllowed() const { return true; }
   std::vector<double> EvalOne(const Metric* m, const double* score) const;
 
   const Config* config_ = nullptr;
@@ -194,6 +197,7 @@ class DART : public GBDT {
             const std::vector<const Metric*>& training_metrics) override;
   bool TrainOneIter(const score_t* gradients, const score_t* hessians) override;
   const double* GetTrainingScore(int64_t* out_len) override;
+  bool DeviceMetricsAllowed() const override { return false; }
   const char* SubModelName() const override { return "tree"; }
 
  private:

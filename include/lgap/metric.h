@@ -11,6 +11,7 @@
 #include "lgap/dataset.h"
 #include "lgap/meta.h"
 #include "lgap/objective.h"
+#include "lgap/pointwise_metric.h"
 
 namespace lgap {
 
@@ -24,6 +25,11 @@ class Metric {
   // score: raw scores [num_class x num_data] class-major
   virtual std::vector<double> Eval(const double* score, const ObjectiveFunction* objective) const = 0;
   static std::unique_ptr<Metric> Create(const std::string& type, const Config& config);
+  // Pointwise metrics that a device learner can evaluate from its device-resident
+  // score: fill the row-loss description (objective output transform included)
+  // and turn the device's weighted loss sum into the metric value.
+  virtual bool DevicePointwise(const ObjectiveFunction*, PwMetricParams*) const { return false; }
+  virtual std::vector<double> FinishSum(double) const { return {}; }
 };
 
 class DCGCalculator {

@@ -13,6 +13,7 @@
 #include "lgap/dataset.h"
 #include "lgap/meta.h"
 #include "lgap/pointwise.h"
+#include "lgap/pointwise_metric.h"
 
 namespace lgap {
 
@@ -70,6 +71,9 @@ struct LambdarankTables {
 bool GetLambdarankTables(const ObjectiveFunction* obj, LambdarankTables* out);
 // objective_seed of a rank_xendcg objective (its per-query Random streams start at seed + q)
 bool GetXendcgSeed(const ObjectiveFunction* obj, int* seed);
+// output transform of a pointwise objective as a PwOutput code (lgap/pointwise_metric.h);
+// false for objectives whose ConvertOutput is not pointwise
+bool PointwiseOutputTransform(const ObjectiveFunction* obj, int* output, double* sigmoid);
 
 double Percentile(std::vector<double> v, double alpha);
 double WeightedPercentile(const std::vector<double>& v, const std::vector<double>& w, double alpha);

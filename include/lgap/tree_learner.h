@@ -57,6 +57,8 @@ class TreeLearner {
   virtual void DeviceSetGradients(const score_t*, const score_t*, int) {}
   virtual std::unique_ptr<Tree> DeviceTrain(int class_id, bool is_first_tree) { (void)class_id; (void)is_first_tree; return nullptr; }
   virtual void DeviceAddTreeToScore(const Tree*, int class_id) { (void)class_id; }
+  // training metric from the device-resident score of class k (false: evaluate on the host)
+  virtual bool DeviceEvalPointwise(const PwMetricParams&, int /*k*/, double* /*sum*/) { return false; }
   virtual void DeviceAddConstant(double, int class_id) { (void)class_id; }
   virtual void DeviceGetScore(std::vector<double>*) const {}
   virtual void DeviceGetGradients(std::vector<score_t>*, std::vector<score_t>*) const {}

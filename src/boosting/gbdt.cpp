@@ -339,6 +339,25 @@ void GBDT::RollbackOneIter() {
 
 std::vector<double> GBDT::EvalOne(const Metric* m, const double* score) const { return m->Eval(score, objective_); }
 
+// Training metrics: pointwise metrics are evaluated where the score lives (the
+// device learner's HBM copy, no N-double download); everything else reads the
+// training score on the host. `*score` is fetched lazily and reused.
+std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
+  PwMetricParams p;
+  const char* off = std::getenv("LGAP_DEVICE_METRICS");  // "0": always evaluate on the host (A/B, tests)
+  const bool allow = off == nullptr || std::strcmp(off, "0") != 0;
+  if (allow && device_mode_ && num_tree_per_iteration_ == 1 && DeviceMetricsAllowed() &&
+      m->DevicePointwise(objective_, &p)) {
+    double sum = 0.0;
+    if (learner_->DeviceEvalPointwise(p, 0, &sum)) return m->FinishSum(sum);
+  }
+  if (*score == nullptr) {
+    int64_t len;
+    *score = GetTrainingScore(&len);
+  }
+  return EvalOne(m, *score);
+}
+
 std::vector<std::string> GBDT::GetEvalNames() const {
   std::vector<std::string> out;
   for (auto* m : training_metrics_) for (auto& n : m->GetName()) out.push_back(n);
@@ -351,11 +370,10 @@ std::string GBDT::OutputMetric(int iter) {
   std::stringstream msg;
   std::vector<std::pair<size_t, size_t>> improved;
   if (need_output && !training_metrics_.empty()) {
-    int64_t len;
-    const double* score = GetTrainingScore(&len);
+    const double* score = nullptr;
     for (auto* m : training_metrics_) {
       auto names = m->GetName();
-      auto vals = EvalOne(m, score);
+      auto vals = EvalTraining(m, &score);
       for (size_t k = 0; k < names.size(); ++k) {
         std::stringstream line;
         line << "Iteration:" << iter << ", training " << names[k] << " : " << vals[k];
@@ -406,9 +424,8 @@ bool GBDT::EvalAndCheckEarlyStopping() {
 std::vector<double> GBDT::GetEvalAt(int data_idx) {
   std::vector<double> ret;
   if (data_idx == 0) {
-    int64_t len;
-    const double* score = GetTrainingScore(&len);
-    for (auto* m : training_metrics_) for (double v : EvalOne(m, score)) ret.push_back(v);
+    const double* score = nullptr;
+    for (auto* m : training_metrics_) for (double v : EvalTraining(m, &score)) ret.push_back(v);
   } else {
     const size_t i = static_cast<size_t>(data_idx - 1);
     if (i >= valid_score_.size()) Log::Fatal("Invalid data index %d", data_idx);

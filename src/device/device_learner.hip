@@ -2217,6 +2217,25 @@ class DeviceTreeLearner : public TreeLearner {
     LaunchAddConstant(score_.get() + static_cast<size_t>(k) * N_, N_, v, stream_);
   }
 
+  bool DeviceEvalPointwise(const PwMetricParams& p, int k, double* sum) override {
+    if (score_.size() < static_cast<size_t>(k + 1) * N_ || N_ <= 0) return false;
+    ScopedTimer timer("Device::EvalMetric");
+    const Metadata& md = data_->metadata();
+    if (metric_label_.size() == 0) {
+      metric_label_.Upload(md.label(), N_, stream_);  // the raw labels (objectives may relabel theirs)
+      if (md.weights()) metric_weight_.Upload(md.weights(), N_, stream_);
+      metric_partial_.Resize(kMetricBlocks + 1);
+    }
+    LaunchPointwiseMetric(p, score_.get() + static_cast<size_t>(k) * N_, metric_label_.get(),
+                          metric_weight_.size() ? metric_weight_.get() : nullptr, N_, metric_partial_.get(),
+                          kMetricBlocks, metric_partial_.get() + kMetricBlocks, stream_);
+    double* h = pin_lout_.Get(1);
+    HIP_CHECK(hipMemcpyAsync(h, metric_partial_.get() + kMetricBlocks, sizeof(double), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    *sum = h[0];
+    return true;
+  }
+
   void DeviceAddTreeToScore(const Tree* tree, int k) override {
     ScopedTimer timer("Device::AddTreeToScore");
     double* s = score_.get() + static_cast<size_t>(k) * N_;
@@ -3099,6 +3118,10 @@ class DeviceTreeLearner : public TreeLearner {
   RankKernelArgs rank_args_;
   DevBuf<unsigned> xendcg_state_;
   DevBuf<int> row_query_;  // bagging by query: query of each row
+  // device training metrics
+  static constexpr int kMetricBlocks = 1024;
+  DevBuf<float> metric_label_, metric_weight_;
+  DevBuf<double> metric_partial_;
   XendcgArgs xendcg_args_;
   // pinned staging
   PinnedBuf<TreeParams> pin_tp_;

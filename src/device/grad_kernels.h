@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "lgap/pointwise.h"
+#include "lgap/pointwise_metric.h"
 
 namespace lgap {
 namespace device {
@@ -51,6 +52,11 @@ struct XendcgArgs {
 void LaunchXendcgGrad(const XendcgArgs& a, hipStream_t s);
 
 void LaunchAddConstant(double* score, int n, double v, hipStream_t s);
+
+// sum over rows of the pointwise metric's weighted row loss (PmRowTerm) -> *out (device);
+// `partial` holds max_blocks doubles
+void LaunchPointwiseMetric(const PwMetricParams& p, const double* score, const float* label, const float* weight, int n,
+                           double* partial, int max_blocks, double* out, hipStream_t s);
 
 }  // namespace device
 }  // namespace lgap

@@ -11,8 +11,11 @@
 // delta_pair, normalisation), multiclass_objective.hpp:120-150.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "device/grad_kernels.h"
 #include "device/hip_common.h"
+#include "lgap/pointwise_metric.h"
 #include "lgap/rank_math.h"
 
 namespace lgap {
@@ -342,6 +345,40 @@ __global__ __launch_bounds__(kRankThreads) void k_xendcg(XendcgArgs a) {
   }
 }
 
+// Pointwise training metric from the device-resident score (reference CUDA
+// EvalKernel, cuda_pointwise_metric.cu:20): per-block fp64 partial sums of
+// PmRowTerm (the host metric's row term), then one wave folds the partials in
+// a fixed order, so the value is run-to-run deterministic.
+constexpr int kMetricThreads = 256;
+
+__global__ __launch_bounds__(kMetricThreads) void k_metric_partial(PwMetricParams p, const double* __restrict__ score,
+                                                                   const float* __restrict__ label,
+                                                                   const float* __restrict__ weight, int n,
+                                                                   double* __restrict__ partial) {
+  __shared__ double s_w[kMetricThreads / kWave];
+  double acc = 0.0;
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    acc += PmRowTerm(p, static_cast<double>(label[i]), score[i], weight != nullptr,
+                     weight ? static_cast<double>(weight[i]) : 1.0);
+  }
+  acc = WaveSum(acc);
+  if ((threadIdx.x & (kWave - 1)) == 0) s_w[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kMetricThreads / kWave; ++w) t += s_w[w];
+    partial[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_metric_fold(const double* __restrict__ partial, int nb, double* out) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += kWave) acc += partial[i];
+  acc = WaveSum(acc);
+  if (threadIdx.x == 0) *out = acc;
+}
+
 }  // namespace
 
 void LaunchPointwiseGrad(const PointwiseParams& p, const double* score, const float* label, const float* weight,
@@ -367,6 +404,15 @@ void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s) {
 void LaunchXendcgGrad(const XendcgArgs& a, hipStream_t s) {
   if (a.num_queries <= 0) return;
   k_xendcg<<<a.num_queries, kRankThreads, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchPointwiseMetric(const PwMetricParams& p, const double* score, const float* label, const float* weight, int n,
+                           double* partial, int max_blocks, double* out, hipStream_t s) {
+  const int nb = std::max(1, std::min(max_blocks, (n + kMetricThreads - 1) / kMetricThreads));
+  k_metric_partial<<<nb, kMetricThreads, 0, s>>>(p, score, label, weight, n, partial);
+  HIP_CHECK(hipGetLastError());
+  k_metric_fold<<<1, kWave, 0, s>>>(partial, nb, out);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -14,6 +14,7 @@
 #include "lgap/common.h"
 #include "lgap/log.h"
 #include "lgap/metric.h"
+#include "lgap/pointwise_metric.h"
 
 namespace lgap {
 
@@ -130,6 +131,10 @@ class PointwiseMetric : public Metric {
   enum Kind { L2, RMSE, L1, QUANTILE, HUBER, FAIR, POISSON, MAPE, GAMMA, GAMMA_DEV, TWEEDIE, BIN_LOGLOSS, BIN_ERROR,
               XENT, XENT_LAMBDA, KLDIV };
   PointwiseMetric(Kind k, const Config& c) : k_(k), cfg_(c) {
+    pm_.kind = static_cast<int>(k);  // Kind and PwMetricKind list the metrics in the same order
+    pm_.alpha = c.alpha;
+    pm_.fair_c = c.fair_c;
+    pm_.tweedie_rho = c.tweedie_variance_power;
     static const char* names[] = {"l2", "rmse", "l1", "quantile", "huber", "fair", "poisson", "mape", "gamma",
                                   "gamma_deviance", "tweedie", "binary_logloss", "binary_error", "cross_entropy",
                                   "cross_entropy_lambda", "kullback_leibler"};
@@ -154,12 +159,6 @@ class PointwiseMetric : public Metric {
   const std::vector<std::string>& GetName() const override { return name_; }
   double factor_to_bigger_better() const override { return -1.0; }
 
-  static double Xent(double y, double p) {
-    const double eps = 1.0e-12;
-    double a = y * (p > eps ? std::log(p) : std::log(eps));
-    double b = (1.0f - y) * (1.0f - p > eps ? std::log(1.0f - p) : std::log(eps));
-    return -(a + b);
-  }
   static double Yent(double p) {
     double h = 0.0;
     if (p > 0) h += p * std::log(p);
@@ -168,66 +167,29 @@ class PointwiseMetric : public Metric {
     return h;
   }
 
-  double Loss(label_t y, double s, double w) const {
-    switch (k_) {
-      case L2:
-      case RMSE:
-        return (s - y) * (s - y);
-      case L1:
-        return std::fabs(s - y);
-      case QUANTILE: {
-        double d = y - s;
-        return d < 0 ? (cfg_.alpha - 1.0f) * d : cfg_.alpha * d;
-      }
-      case HUBER: {
-        double d = s - y;
-        return std::abs(d) <= cfg_.alpha ? 0.5f * d * d : cfg_.alpha * (std::abs(d) - 0.5f * cfg_.alpha);
-      }
-      case FAIR: {
-        double x = std::fabs(s - y), c = cfg_.fair_c;
-        return c * x - c * c * std::log1p(x / c);
-      }
-      case POISSON: {
-        if (s < 1e-10f) s = 1e-10f;
-        return s - y * std::log(s);
-      }
-      case MAPE:
-        return std::fabs(y - s) / std::max(1.0f, std::fabs(y));
-      case GAMMA: {
-        const double theta = -1.0 / s;
-        const double b = -SafeLog(-theta);
-        const double c = SafeLog(y) - SafeLog(y);
-        return -((y * theta - b) + c);
-      }
-      case GAMMA_DEV: {
-        const double t = y / (s + 1.0e-9);
-        return t - SafeLog(t) - 1;
-      }
-      case TWEEDIE: {
-        const double rho = cfg_.tweedie_variance_power;
-        if (s < 1e-10f) s = 1e-10f;
-        const double a = y * std::exp((1 - rho) * std::log(s)) / (1 - rho);
-        const double b = std::exp((2 - rho) * std::log(s)) / (2 - rho);
-        return -a + b;
-      }
-      case BIN_LOGLOSS:
-        if (y <= 0) {
-          if (1.0f - s > kEpsilon) return -std::log(1.0f - s);
-        } else if (s > kEpsilon) {
-          return -std::log(s);
-        }
-        return -std::log(kEpsilon);
-      case BIN_ERROR:
-        return s <= 0.5f ? (y > 0) : (y <= 0);
-      case XENT:
-      case KLDIV:
-        return Xent(y, s);
-      case XENT_LAMBDA:
-        return Xent(y, 1.0f - std::exp(-w * s));
+  // the row loss is shared with the device metric kernel (lgap/pointwise_metric.h)
+  double Loss(label_t y, double s, double w) const { return PmLoss(pm_, y, s, w); }
+
+  bool DevicePointwise(const ObjectiveFunction* obj, PwMetricParams* out) const override {
+    PwMetricParams p = pm_;
+    if (obj == nullptr) {
+      p.output = k_ == XENT_LAMBDA ? kOutLog1pExp : kOutIdentity;
+    } else if (!PointwiseOutputTransform(obj, &p.output, &p.sigmoid)) {
+      return false;
     }
-    return 0.0;
+    *out = p;
+    return true;
   }
-  static double SafeLog(double x) { return x > 0 ? std::log(x) : -INFINITY; }
+
+  std::vector<double> FinishSum(double sum) const override {
+    double v;
+    if (k_ == RMSE) v = std::sqrt(sum / sumw_);
+    else if (k_ == GAMMA_DEV) v = sum * 2;
+    else if (k_ == XENT_LAMBDA) v = sum / static_cast<double>(n_);
+    else if (k_ == KLDIV) v = ent_ + sum / sumw_;
+    else v = sum / sumw_;
+    return {v};
+  }
 
   std::vector<double> Eval(const double* score, const ObjectiveFunction* obj) const override {
     double sum = 0.0;
@@ -243,13 +205,7 @@ class PointwiseMetric : public Metric {
       if (obj) obj->ConvertOutput(&score[i], &s);
       sum += w_ ? Loss(label_[i], s, 1.0) * w_[i] : Loss(label_[i], s, 1.0);
     }
-    double v;
-    if (k_ == RMSE) v = std::sqrt(sum / sumw_);
-    else if (k_ == GAMMA_DEV) v = sum * 2;
-    else if (k_ == XENT_LAMBDA) v = sum / static_cast<double>(n_);
-    else if (k_ == KLDIV) v = ent_ + sum / sumw_;
-    else v = sum / sumw_;
-    return {v};
+    return FinishSum(sum);
   }
 
  private:
@@ -260,6 +216,7 @@ class PointwiseMetric : public Metric {
   const label_t* label_ = nullptr;
   const label_t* w_ = nullptr;
   double sumw_ = 0.0, ent_ = 0.0;
+  PwMetricParams pm_;
 };
 
 // AUC with tied-score groups (binary_metric.hpp:194-251).

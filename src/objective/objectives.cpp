@@ -281,6 +281,25 @@ class PointwiseObjective : public ObjectiveFunction {
 
   DeviceGradKind device_kind() const override { return DeviceGradKind::kPointwise; }
   const PointwiseParams* pointwise() const override { return &p_; }
+  // ConvertOutput above as a PwOutput code (device metrics)
+  int OutputTransform(double* sigmoid) const {
+    *sigmoid = p_.sigmoid;
+    switch (p_.kind) {
+      case kPwPoisson:
+      case kPwGamma:
+      case kPwTweedie:
+        return kOutExp;
+      case kPwBinary:
+        return kOutSigmoid;
+      case kPwXent:
+        *sigmoid = 1.0;
+        return kOutSigmoid;
+      case kPwXentLambda:
+        return kOutLog1pExp;
+      default:
+        return sqrt_ ? kOutSignedSquare : kOutIdentity;
+    }
+  }
   const label_t* effective_label() const override { return label_; }
   const label_t* aux_weight() const override { return aux_.empty() ? nullptr : aux_.data(); }
   double sigmoid() const override { return p_.sigmoid; }
@@ -475,6 +494,13 @@ std::unique_ptr<ObjectiveFunction> ObjectiveFunction::CreateFromString(const std
   }
   if (type == "lambdarank" || type == "rank_xendcg") return CreateRankObjectiveFromString(type, strs);
   Log::Fatal("Unknown objective type name: %s", type.c_str());
+}
+
+bool PointwiseOutputTransform(const ObjectiveFunction* obj, int* output, double* sigmoid) {
+  auto* p = dynamic_cast<const PointwiseObjective*>(obj);
+  if (p == nullptr) return false;
+  *output = p->OutputTransform(sigmoid);
+  return true;
 }
 
 }  // namespace lgap

@@ -333,3 +333,45 @@ def test_device_bagging_by_query_matches_host(lgb, gpu_required):
     assert splits(bg) == splits(bh)
     np.testing.assert_allclose(pg, ph, rtol=1e-4, atol=1e-5)
     assert np.corrcoef(pc, pg)[0, 1] > 0.999
+
+
+@pytest.mark.parametrize("objective,metrics,extra", [
+    ("binary", ["binary_logloss", "binary_error", "l2", "l1", "mape"], {}),
+    ("regression", ["l2", "rmse", "l1", "huber", "fair", "quantile", "mape"], {"reg_sqrt": True}),
+    ("poisson", ["poisson", "l2", "gamma", "gamma_deviance", "tweedie"], {}),
+    ("cross_entropy", ["cross_entropy", "kullback_leibler", "cross_entropy_lambda"], {}),
+    ("cross_entropy_lambda", ["cross_entropy_lambda", "cross_entropy"], {}),
+])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_device_training_metrics_match_host(lgb, gpu_required, objective, metrics, extra, weighted):
+    """Pointwise training metrics evaluated on the device score (k_metric_partial + fold, row loss
+    shared with the host metric through lgap/pointwise_metric.h) equal the host evaluation of the
+    same booster (LGAP_DEVICE_METRICS=0 forces the host path)."""
+    import os
+
+    rng = np.random.default_rng(31)
+    n = 50000
+    X = rng.standard_normal((n, 8))
+    if objective == "binary":
+        y = (X[:, 0] + 0.5 * rng.standard_normal(n) > 0).astype(float)
+    elif objective == "regression":
+        y = X[:, 0] * 3 + rng.standard_normal(n)
+    elif objective == "poisson":
+        y = rng.poisson(np.exp(0.3 * X[:, 0] + 0.5)).astype(float) + 0.5
+    else:
+        y = 1 / (1 + np.exp(-X[:, 0] - 0.3 * rng.standard_normal(n)))
+    w = rng.uniform(0.5, 2.0, n) if weighted else None
+    params = {"objective": objective, "metric": metrics, "device_type": "gpu", "verbosity": -1, "num_leaves": 15,
+              **extra}
+    b = lgb.Booster(params, lgb.Dataset(X, y, weight=w, params=params))
+    for _ in range(3):
+        b.update()
+    dev = b.eval_train()
+    os.environ["LGAP_DEVICE_METRICS"] = "0"
+    try:
+        host = b.eval_train()
+    finally:
+        del os.environ["LGAP_DEVICE_METRICS"]
+    assert [r[1] for r in dev] == [r[1] for r in host]
+    for d, h in zip(dev, host):
+        assert d[2] == pytest.approx(h[2], rel=1e-9, abs=1e-12), (d, h)
