@@ -97,6 +97,7 @@ struct Args {
   SplitRec* rec;
   double* slots;
   double* staging;
+  float* staging_f;  // data-parallel all-reduce row of the fp32 (default) histogram path
   void* hist_slab;
   unsigned* ghmax;  // float bits of max|g|, max|h| over the root rows
   uint8_t* splittable;
@@ -583,11 +584,12 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   StampEnd(a, 2);
 }
 
-// staging[v] = sum over the active blocks' slab rows (v over 2 * TB values).
-// Used where the full histogram must exist in one place: data-parallel
-// training (all-reduced over RCCL before the scan) and the kernel tests.
-template <typename Acc>
-__global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid) {
+// out[v] = sum over the active blocks' slab rows (v over 2 * TB values), folded
+// in fp64. Used where the full histogram must exist in one place: data-parallel
+// training (all-reduced over RCCL before the scan; fp32 rows unless gpu_use_dp,
+// half the bytes on the wire) and the kernel tests (fp64 staging).
+template <typename Acc, typename Out>
+__global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid, Out* __restrict__ out) {
   __shared__ double part[16][64];
   const Ctl* cp = a.ctl;
   if (cp->done || cp->skip) return;
@@ -607,7 +609,7 @@ __global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid) {
     double t = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += part[i][lane];
-    a.staging[v] = t;
+    out[v] = static_cast<Out>(t);
   }
 }
 
@@ -824,7 +826,9 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
   const int nb = from_staging ? 1 : (c.hist_nb > 0 ? c.hist_nb : HistActiveBlocks(n_small, hist_grid, a.hist_min_rows));
   const size_t V = 2 * static_cast<size_t>(a.TB);
   const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
-  const Acc* slab = from_staging ? reinterpret_cast<const Acc*>(a.staging) : reinterpret_cast<const Acc*>(a.hist_slab);
+  // (the all-reduced row has the slab element type: fp32 staging_f, or fp64 staging with gpu_use_dp)
+  const void* srow = sizeof(Acc) == sizeof(float) ? static_cast<const void*>(a.staging_f) : static_cast<const void*>(a.staging);
+  const Acc* slab = from_staging ? reinterpret_cast<const Acc*>(srow) : reinterpret_cast<const Acc*>(a.hist_slab);
   // 1. slab reduction into hs_full at stored positions (mfb filled in step 3):
   //    each wave owns 32 values, its two half-waves stride over the slab rows;
   //    no barrier until all values are reduced
@@ -2561,8 +2565,8 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(range_.get(), hr, sizeof(LeafRange), hipMemcpyHostToDevice, stream_));
     staging_.Zero(stream_);
     const Args args = MakeArgs();
-    LaunchHist(args);
-    if (!distributed_) LaunchHistReduce(args);
+    LaunchHist(args, /*collective=*/false);
+    LaunchHistReduce(args);
     staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
@@ -2596,8 +2600,8 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(ghmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
     staging_.Zero(stream_);
     const Args args = MakeArgs();
-    LaunchHist(args);
-    if (!distributed_) LaunchHistReduce(args);
+    LaunchHist(args, /*collective=*/false);
+    LaunchHistReduce(args);
     staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
     staging_.Zero(stream_);
@@ -2620,7 +2624,7 @@ class DeviceTreeLearner : public TreeLearner {
     return std::max(1, std::min({want, DivUp(N_, HistMinRows()), mem_cap}));
   }
 
-  void LaunchHist(const Args& a) {
+  void LaunchHist(const Args& a, bool collective = true) {
     const dim3 hgrid(HistBlocks(), num_tiles_);
     if (use_dp_) {
       if (width_ == 1) k_hist<1, 1><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
@@ -2630,22 +2634,34 @@ class DeviceTreeLearner : public TreeLearner {
       else k_hist<2, 0><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
     }
     HIP_CHECK(hipGetLastError());
-    if (distributed_) {
-      LaunchHistReduce(a);
-      AllreduceSumF64(staging_.get(), 2 * static_cast<size_t>(TB_), stream_);
+    if (distributed_ && collective) {
+      const size_t n = 2 * static_cast<size_t>(TB_);
+      const int rgrid = DivUp(2 * static_cast<long long>(TB_), 64);
+      if (use_dp_) {
+        k_hist_reduce<double, double><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks(), staging_.get());
+        HIP_CHECK(hipGetLastError());
+        AllreduceSumF64(staging_.get(), n, stream_);
+      } else {
+        k_hist_reduce<float, float><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks(), staging_f_.get());
+        HIP_CHECK(hipGetLastError());
+        AllreduceSumF32(staging_f_.get(), n, stream_);
+      }
     }
   }
 
+  // rank-local fp64 histogram into `staging` (kernel test hooks, host split policies)
   void LaunchHistReduce(const Args& a) {
     const int rgrid = DivUp(2 * static_cast<long long>(TB_), 64);
-    if (use_dp_) k_hist_reduce<double><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks());
-    else k_hist_reduce<float><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks());
+    if (use_dp_) k_hist_reduce<double, double><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks(), staging_.get());
+    else k_hist_reduce<float, double><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks(), staging_.get());
     HIP_CHECK(hipGetLastError());
   }
 
   void LaunchScan(const Args& a) {
-    if (distributed_) {
+    if (distributed_ && use_dp_) {
       k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 1);
+    } else if (distributed_) {
+      k_reduce_scan<float><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 1);
     } else if (use_dp_) {
       k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 0);
     } else {
@@ -2860,6 +2876,7 @@ class DeviceTreeLearner : public TreeLearner {
     slots_.Resize(L * 2 * static_cast<size_t>(TB_));
     staging_.Resize(2 * static_cast<size_t>(TB_));
     staging_.Zero(stream_);
+    staging_f_.Resize(2 * static_cast<size_t>(TB_));
     hist_slab_.Resize(static_cast<size_t>(HistBlocks()) * 2 * TB_ * (use_dp_ ? 8 : 4));
     // all three index buffers hold N rows up front: a captured graph keeps their
     // addresses, so a later bag (host upload or device draw) must not reallocate
@@ -2908,6 +2925,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.rec = rec_.get();
     a.slots = slots_.get();
     a.staging = staging_.get();
+    a.staging_f = staging_f_.get();
     a.hist_slab = hist_slab_.get();
     a.ghmax = ghmax_.get();
     a.splittable = splittable_.get();
@@ -3089,6 +3107,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<SplitInfo> best_;
   DevBuf<SplitRec> rec_;
   DevBuf<double> slots_, staging_;
+  DevBuf<float> staging_f_;
   DevBuf<char> hist_slab_, arena_;
   DevBuf<unsigned long long> stamps_;
   int stamp_trees_ = 0;

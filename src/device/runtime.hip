@@ -200,24 +200,33 @@ bool HostStagedDP() {
   return on && S().comm == nullptr && Network::num_machines() > 1;
 }
 
-void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream) {
+template <typename T>
+void AllreduceSum(T* dev_ptr, size_t count, hipStream_t stream, ncclDataType_t type) {
   if (count == 0) return;
   if (HostStagedDP()) {
     // Rehearsal transport (several ranks sharing one GPU, host Network underneath):
     // device -> pinned host -> Network allreduce -> device. Not for production runs.
-    thread_local std::vector<double> h;
+    thread_local std::vector<T> h;
     h.resize(count);
-    HIP_CHECK(hipMemcpyAsync(h.data(), dev_ptr, count * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipMemcpyAsync(h.data(), dev_ptr, count * sizeof(T), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
-    Network::Allreduce(reinterpret_cast<char*>(h.data()), static_cast<comm_size_t>(count * sizeof(double)),
-                       sizeof(double), reinterpret_cast<char*>(h.data()), Network::SumReducer<double>());
-    HIP_CHECK(hipMemcpyAsync(dev_ptr, h.data(), count * sizeof(double), hipMemcpyHostToDevice, stream));
+    Network::Allreduce(reinterpret_cast<char*>(h.data()), static_cast<comm_size_t>(count * sizeof(T)), sizeof(T),
+                       reinterpret_cast<char*>(h.data()), Network::SumReducer<T>());
+    HIP_CHECK(hipMemcpyAsync(dev_ptr, h.data(), count * sizeof(T), hipMemcpyHostToDevice, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
     return;
   }
   // a one-rank communicator still runs the collective (single-GPU rehearsal of the DP path)
   if (!CommExists()) return;
-  NcclCheck(ncclAllReduce(dev_ptr, dev_ptr, count, ncclFloat64, ncclSum, S().comm, stream), "ncclAllReduce");
+  NcclCheck(ncclAllReduce(dev_ptr, dev_ptr, count, type, ncclSum, S().comm, stream), "ncclAllReduce");
+}
+
+void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream) {
+  AllreduceSum(dev_ptr, count, stream, ncclFloat64);
+}
+
+void AllreduceSumF32(float* dev_ptr, size_t count, hipStream_t stream) {
+  AllreduceSum(dev_ptr, count, stream, ncclFloat32);
 }
 
 // Collective watchdog (the reference only has socket timeouts; a lost

@@ -19,6 +19,7 @@ bool CommExists();
 bool HostStagedDP();
 // In-place sum all-reduce of device doubles on `stream` (no-op without a communicator).
 void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream);
+void AllreduceSumF32(float* dev_ptr, size_t count, hipStream_t stream);
 // hipStreamSynchronize for streams carrying collectives: polls the communicator's
 // async error and aborts it after timeout_s (<= 0: no limit), raising a fatal error.
 void WatchedStreamSync(hipStream_t stream, double timeout_s, const char* what);
