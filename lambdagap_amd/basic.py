@@ -612,6 +612,16 @@ class Dataset:
         self.reference = reference
         return self
 
+    def get_ref_chain(self, ref_limit: int = 100) -> set:
+        """This Dataset, its reference, the reference's reference, ... (stops at ref_limit or a loop)."""
+        head, chain = self, set()
+        while len(chain) < ref_limit and isinstance(head, Dataset):
+            chain.add(head)
+            if head.reference is None or head.reference in chain:
+                break
+            head = head.reference
+        return chain
+
     def set_categorical_feature(self, categorical_feature: Any) -> "Dataset":
         if self.categorical_feature == categorical_feature:
             return self
@@ -777,6 +787,16 @@ class Booster:
         _check(_LIB.LGBM_NetworkInit(_c_str(str(machines)), ctypes.c_int(port), ctypes.c_int(timeout),
                                      ctypes.c_int(num)))
         self._network = True
+
+    def set_network(self, machines: Union[List[str], set, str], local_listen_port: int = 12400,
+                    listen_time_out: int = 120, num_machines: int = 1) -> "Booster":
+        """Join the TCP socket mesh of the host parallel learners (reference Booster.set_network)."""
+        if isinstance(machines, (list, set)):
+            machines = ",".join(machines)
+        _check(_LIB.LGBM_NetworkInit(_c_str(machines), ctypes.c_int(local_listen_port),
+                                     ctypes.c_int(listen_time_out), ctypes.c_int(num_machines)))
+        self._network = True
+        return self
 
     def free_network(self) -> "Booster":
         if self._network:

@@ -216,3 +216,16 @@ def test_two_round_loading_matches_one_round(lgb, name, obj):
     two = lgb.train(params, lgb.Dataset(path, params=dict(params, two_round=True)), 5)
     strip = lambda s: s[:s.index("parameters:")]  # noqa: E731
     assert strip(one.model_to_string()) == strip(two.model_to_string())
+
+
+def test_ref_chain_and_set_network_api(lgb):
+    """Reference Dataset.get_ref_chain / Booster.set_network surface."""
+    X = np.random.default_rng(0).random((300, 4))
+    y = X[:, 0]
+    a = lgb.Dataset(X, y)
+    b = lgb.Dataset(X, y, reference=a)
+    c = lgb.Dataset(X, y, reference=b)
+    assert c.get_ref_chain() == {a, b, c}
+    assert c.get_ref_chain(ref_limit=2) == {b, c}
+    bst = lgb.train({"verbosity": -1}, a, 1)
+    assert callable(bst.set_network) and callable(bst.free_network)
