@@ -98,7 +98,8 @@ void Network::ReduceScatter(char* input, comm_size_t input_size, int type_size, 
     std::vector<char> all(static_cast<size_t>(input_size) * n);
     Allgather(input, input_size, all.data());
     const int r = S().rank;
-    std::memcpy(output, all.data() + block_start[r], block_len[r]);
+    // start from this rank's own block, then add every other rank's
+    std::memcpy(output, all.data() + static_cast<size_t>(r) * input_size + block_start[r], block_len[r]);
     for (int k = 0; k < n; ++k) {
       if (k != r) reducer(all.data() + static_cast<size_t>(k) * input_size + block_start[r], output, type_size, block_len[r]);
     }

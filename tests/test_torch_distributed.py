@@ -91,3 +91,22 @@ def test_distributed_sklearn_estimator(lgb, tmp_path):
     from sklearn.metrics import roc_auc_score
 
     assert roc_auc_score(t[:, 0], lgb.Booster(model_str=m).predict(t[:, 1:])) > 0.68
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_torch_network_sharded_matches_socket_mesh(lgb, tmp_path, world):
+    """Different rows on every rank: the allgather-derived reduce-scatter must reduce each rank's own
+    block (identical shards, as in the "all" test above, cannot tell whose block is whose). The
+    socket mesh's native reduce-scatter on the same shards is the reference."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_distributed import _run as socket_run
+
+    (tmp_path / "t").mkdir()
+    (tmp_path / "s").mkdir()
+    m = _run(world, "shard", "data", tmp_path / "t")
+    ms = socket_run("data", "split", tmp_path / "s", {"min_data_in_leaf": 20}, world=world)
+    t = np.loadtxt(os.path.join(DATA, "binary.test"))
+    np.testing.assert_allclose(lgb.Booster(model_str=m).predict(t[:, 1:]),
+                               lgb.Booster(model_str=ms[0]).predict(t[:, 1:], num_iteration=6), rtol=1e-6, atol=1e-8)
