@@ -4,8 +4,8 @@
 //
 // Besides the device learners' histogram all-reduce, the same communicator
 // backs the host collective layer (Network) when no socket mesh is configured:
-// reduce-scatter / allgather of host bytes go through pinned staging buffers
-// and ncclAllGather, so scalar syncs (boost_from_average, distributed bin
+// allgather of host bytes goes through a device staging buffer and
+// ncclAllGather (Network derives reduce-scatter from it), so scalar syncs (boost_from_average, distributed bin
 // finding, metric sums) need no second transport.
 // Reference counterpart: src/network/network.cpp:30-75 (external functions).
 #include <hip/hip_runtime.h>
@@ -88,25 +88,6 @@ void RcclAllgather(char* input, comm_size_t input_size, const comm_size_t* block
   }
 }
 
-// Network external reduce-scatter with an arbitrary host reducer: gather every
-// rank's full input, then reduce this rank's block locally (inputs here are
-// small host-side syncs; the device histograms use ncclAllReduce directly).
-void RcclReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
-                       const comm_size_t* block_len, int num_block, char* output, comm_size_t output_size,
-                       const ReduceFunction& reducer) {
-  (void)num_block;
-  (void)output_size;
-  const int n = S().size, r = S().rank;
-  std::vector<char> all(static_cast<size_t>(input_size) * n);
-  HostAllgatherEqual(input, input_size, all.data());
-  // start from this rank's own block, then add every other rank's
-  std::memcpy(output, all.data() + static_cast<size_t>(r) * input_size + block_start[r], block_len[r]);
-  for (int k = 0; k < n; ++k) {
-    if (k == r) continue;
-    reducer(all.data() + static_cast<size_t>(k) * input_size + block_start[r], output, type_size, block_len[r]);
-  }
-}
-
 std::string ToHex(const char* p, size_t n) {
   static const char* d = "0123456789abcdef";
   std::string s(2 * n, '0');
@@ -162,7 +143,9 @@ void CommInit(const std::string& unique_id, int num_ranks, int rank, int device_
   s.size = num_ranks;
   // host collectives ride on the same communicator unless a socket mesh exists
   if (Network::num_machines() <= 1 && num_ranks > 1) {
-    Network::Init(num_ranks, rank, RcclReduceScatter, RcclAllgather);
+    // allgather only: Network derives reduce-scatter from it (the path the torch.distributed
+    // transport exercises in the multi-rank CPU tests)
+    Network::Init(num_ranks, rank, nullptr, RcclAllgather);
   }
   Log::Info("RCCL communicator ready: rank %d / %d on device %d", rank, num_ranks, device_id);
 }
