@@ -3050,6 +3050,10 @@ class DeviceTreeLearner : public TreeLearner {
       r.inv_max_bdcg = rank_inv_bdcg_.get();
       r.qb = rank_qb_.get();
       r.num_queries = md.num_queries();
+      r.max_query = 1;
+      for (data_size_t q = 0; q < md.num_queries(); ++q) {
+        r.max_query = std::max(r.max_query, md.query_boundaries()[q + 1] - md.query_boundaries()[q]);
+      }
       r.label = label_.get();
       r.weight = weight_.size() ? weight_.get() : nullptr;
     }

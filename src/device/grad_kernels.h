@@ -16,6 +16,7 @@ void LaunchPointwiseGrad(const PointwiseParams& p, const double* score, const fl
 void LaunchSoftmaxGrad(int num_class, double factor, const double* score, const float* label, const float* weight,
                        int n, float2* gh, hipStream_t s);
 
+constexpr int kMaxDeviceQueryDecl = 2048;
 struct RankKernelArgs {
   int target = 0;
   int k = 30;
@@ -31,6 +32,7 @@ struct RankKernelArgs {
   const double* inv_max_bdcg = nullptr;
   const int* qb = nullptr;              // query boundaries (num_queries + 1)
   int num_queries = 0;
+  int max_query = kMaxDeviceQueryDecl;  // largest query (documents): sizes the LDS
   const float* label = nullptr;
   const float* weight = nullptr;
   const double* score = nullptr;
