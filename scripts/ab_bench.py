@@ -26,15 +26,25 @@ def main() -> int:
     ap.add_argument("--block", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--preset", default="higgs", choices=["higgs", "ltr"])
+    ap.add_argument("--features", type=int, default=300)
     args = ap.parse_args()
     import lambdagap_amd as lgb
     from lambdagap_amd.parallel import device_synchronize
     from lambdagap_amd.utils import make_higgs_like
 
-    X, y = make_higgs_like(args.rows, seed=7)
-    base = {"objective": "binary", "num_leaves": 63, "max_bin": 255, "learning_rate": 0.1, "min_data_in_leaf": 1,
-            "min_sum_hessian_in_leaf": 100, "device_type": "gpu", "verbosity": -1, "seed": 7}
-    ds = lgb.Dataset(X, y, params=base, free_raw_data=False).construct()
+    if args.preset == "ltr":
+        from lambdagap_amd.models import preset
+        from lambdagap_amd.utils import make_ranking
+
+        X, y, g = make_ranking(max(1, args.rows // 120), num_features=args.features, docs_per_query=(60, 180), seed=7)
+        base = preset("ltr", verbosity=-1, seed=7)
+        ds = lgb.Dataset(X, y, group=g, params=base, free_raw_data=False).construct()
+    else:
+        X, y = make_higgs_like(args.rows, seed=7)
+        base = {"objective": "binary", "num_leaves": 63, "max_bin": 255, "learning_rate": 0.1, "min_data_in_leaf": 1,
+                "min_sum_hessian_in_leaf": 100, "device_type": "gpu", "verbosity": -1, "seed": 7}
+        ds = lgb.Dataset(X, y, params=base, free_raw_data=False).construct()
     variants = args.variant or ["device_use_graph=1", "device_use_graph=0"]
     boosters = []
     for v in variants:

@@ -2617,7 +2617,12 @@ class DeviceTreeLearner : public TreeLearner {
     // one block per CU: A/B on MI355X (10M rows) 256 blocks 4.68-4.74 ms/iter vs 512: 4.85,
     // 384: 4.85, 320: 4.91, 768: 4.93 (fewer slab rows for the scan to fold; an uneven
     // multiple of the CU count leaves a tail); 1.25M rows: flat within 0.6%
-    const int want = config_->device_hist_blocks > 0 ? config_->device_hist_blocks : num_cu_;
+    // Wide data (many LDS feature tiles): the grid is row blocks x tiles, so fewer row blocks
+    // still fill the chip while the slab rows the scan folds (each one 8 B x all bins) shrink:
+    // LambdaRank 1M x 300 (11 tiles) 17.7 -> 16.4 ms/iter at 46 row blocks instead of 256.
+    const int want = config_->device_hist_blocks > 0
+                         ? config_->device_hist_blocks
+                         : std::min(num_cu_, std::max(1, 2 * num_cu_ / std::max(1, num_tiles_)));
     // partial-histogram slab: one row of 2 * TB accumulators per block, capped at 4 GiB
     const size_t row_bytes = 2 * static_cast<size_t>(TB_) * (use_dp_ ? 8 : 4);
     const int mem_cap = static_cast<int>(std::max<size_t>(1, (size_t(4) << 30) / std::max<size_t>(row_bytes, 1)));
