@@ -42,7 +42,27 @@ $(CLI): src/cli/main.cpp $(LIB) $(HEADERS)
 	@mkdir -p $(OUT)
 	$(CXX) $(CXXFLAGS) -o $@ src/cli/main.cpp -L$(OUT) -l_lambdagap -Wl,-rpath,'$$ORIGIN' -fopenmp
 
+# native unit tests (reference tests/cpp_tests analogue), linked against the library
+CPPTEST := $(BUILD)/test_native
+cpptest: $(CPPTEST)
+$(CPPTEST): tests/cpp/test_native.cpp $(LIB) $(HEADERS)
+	$(CXX) $(CXXFLAGS) -o $@ tests/cpp/test_native.cpp -L$(OUT) -l_lambdagap -Wl,-rpath,$(abspath $(OUT)) -fopenmp
+
+# host code under AddressSanitizer + UBSan: every .cpp of the core and
+# the test are rebuilt with the sanitizers; the HIP objects are linked as built (device
+# code is never sanitized: GPU ASan / XNACK runs are unavailable on the target pool)
+ASAN_DIR := $(BUILD)/asan
+SANFLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined
+ASAN_OBJS := $(patsubst src/%.cpp,$(ASAN_DIR)/%.o,$(CPP_SRCS))
+$(ASAN_DIR)/%.o: src/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -O1 $(SANFLAGS) -c $< -o $@
+asan: $(ASAN_DIR)/test_native
+$(ASAN_DIR)/test_native: tests/cpp/test_native.cpp $(ASAN_OBJS) $(HIP_OBJS) $(HEADERS)
+	$(CXX) $(CXXFLAGS) -O1 $(SANFLAGS) -o $@ tests/cpp/test_native.cpp $(ASAN_OBJS) $(HIP_OBJS) \
+	  -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
+
 clean:
 	rm -rf $(BUILD) $(LIB) $(CLI)
 
-.PHONY: all clean
+.PHONY: all clean cpptest asan
