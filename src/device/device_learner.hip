@@ -66,7 +66,7 @@ constexpr int kHistThreads = 512;
 constexpr int kHistMinRows = 1024;  // A/B on MI355X: 1024 beats 2048 / 512 / 4096 at 1.25M and 10M rows
 constexpr int kHistLdsBytes = 56 * 1024;
 constexpr int kPartThreads = 256;
-constexpr int kPartIters = 16;
+constexpr int kPartIters = 16;  // rows per thread of the two-kernel partition (k_part_count / k_part_scatter)
 constexpr int kTileRows = kPartThreads * kPartIters;
 constexpr int kScanWaves = 4;
 constexpr int kScanThreads = 1024;
@@ -1637,17 +1637,22 @@ __device__ int SumCounts(const Args& a, int n, unsigned epoch, int* sh) {
   return BlockSumInt(s, sh);
 }
 
+// ITERS rows per thread: tiles of 256 * ITERS rows. Smaller tiles spread a leaf over more
+// blocks (more loads in flight, shorter look-back chains per block); A/B on MI355X:
+// 10M rows 8 > 16 (+6%) and 4, 1.25M rows 4 > 8 > 16 (+18% over 16). See PartIters().
+template <int ITERS>
 __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
+  constexpr int kTile = kPartThreads * ITERS;
   __shared__ SelOut so;
   __shared__ int sh[8];
-  __shared__ int s_wl[kPartIters][kPartThreads / 64];
-  __shared__ int s_wv[kPartIters][kPartThreads / 64];
+  __shared__ int s_wl[ITERS][kPartThreads / 64];
+  __shared__ int s_wv[ITERS][kPartThreads / 64];
   const unsigned long long t_start = a.stamps ? wall_clock64() : 0ull;
   const Ctl c = *a.ctl;
   if (c.done) return;
   const int bid = static_cast<int>(blockIdx.x);
   // no leaf has more tiles than this; one block beyond may be the post-split block
-  if (bid > (c.max_count + kTileRows - 1) / kTileRows) return;
+  if (bid > (c.max_count + kTile - 1) / kTile) return;
   Stamp(a, 0, 0);
   SelectFromKeys(a, c, &so);
   Stamp(a, 0, 1);
@@ -1689,7 +1694,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   const LeafRange pr = so.pr;
   const SplitDesc& d = so.d;
   const unsigned epoch = c.epoch;
-  const int ntiles = (pr.count + kTileRows - 1) / kTileRows;
+  const int ntiles = (pr.count + kTile - 1) / kTile;
   const int participants = ntiles < static_cast<int>(gridDim.x) ? ntiles : static_cast<int>(gridDim.x);
   const bool has_post_block = participants < static_cast<int>(gridDim.x);
   const int post_block = has_post_block ? participants : 0;
@@ -1699,27 +1704,27 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   const int tbuf = pbuf == 0 ? 1 : 0;
   int* out = a.idx[tbuf] + pstart;
   // phase 1: count this block's tiles and publish them (the first tile's rows stay in registers)
-  int rows0[kPartIters];
-  uint32_t gb0[kPartIters];
+  int rows0[ITERS];
+  uint32_t gb0[ITERS];
   for (int tile = bid; tile < ntiles; tile += gridDim.x) {
-    int rows[kPartIters];
-    const int pos0 = tile * kTileRows + threadIdx.x;
+    int rows[ITERS];
+    const int pos0 = tile * kTile + threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < kPartIters; ++k) {
+    for (int k = 0; k < ITERS; ++k) {
       const int pos = pos0 + k * kPartThreads;
       rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
     }
-    uint32_t gb[kPartIters];
+    uint32_t gb[ITERS];
 #pragma unroll
-    for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
+    for (int k = 0; k < ITERS; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
     int cnt = 0;
 #pragma unroll
-    for (int k = 0; k < kPartIters; ++k) cnt += (rows[k] >= 0 && GoLeft(d, gb[k])) ? 1 : 0;
+    for (int k = 0; k < ITERS; ++k) cnt += (rows[k] >= 0 && GoLeft(d, gb[k])) ? 1 : 0;
     cnt = BlockSumInt(cnt, sh);
     if (threadIdx.x == 0) PublishCount(&a.tile_pub[tile], epoch, cnt);
     if (tile == bid) {
 #pragma unroll
-      for (int k = 0; k < kPartIters; ++k) {
+      for (int k = 0; k < ITERS; ++k) {
         rows0[k] = rows[k];
         gb0[k] = gb[k];
       }
@@ -1753,27 +1758,27 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   for (int tile = bid; tile < ntiles; tile += gridDim.x) {
     int lbase = SumCounts(a, tile, epoch, sh);
     if (tile == bid) Stamp(a, 1, 0);
-    int rbase = tile * kTileRows - lbase;  // rights before this tile
-    int rows[kPartIters];
-    uint32_t gb[kPartIters];
+    int rbase = tile * kTile - lbase;  // rights before this tile
+    int rows[ITERS];
+    uint32_t gb[ITERS];
     if (tile == bid) {
 #pragma unroll
-      for (int k = 0; k < kPartIters; ++k) {
+      for (int k = 0; k < ITERS; ++k) {
         rows[k] = rows0[k];
         gb[k] = gb0[k];
       }
     } else {
-      const int pos0 = tile * kTileRows + threadIdx.x;
+      const int pos0 = tile * kTile + threadIdx.x;
 #pragma unroll
-      for (int k = 0; k < kPartIters; ++k) {
+      for (int k = 0; k < ITERS; ++k) {
         const int pos = pos0 + k * kPartThreads;
         rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
       }
 #pragma unroll
-      for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
+      for (int k = 0; k < ITERS; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < kPartIters; ++k) {
+    for (int k = 0; k < ITERS; ++k) {
       const bool valid = rows[k] >= 0;
       const bool left = valid && GoLeft(d, gb[k]);
       const unsigned long long ml = __ballot(left);
@@ -1785,7 +1790,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kPartIters; ++k) {
+    for (int k = 0; k < ITERS; ++k) {
       const bool valid = rows[k] >= 0;
       const bool left = valid && GoLeft(d, gb[k]);
       const unsigned long long ml = __ballot(left);
@@ -2609,6 +2614,22 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
  private:
+  // Fused-partition tile: 8 rows per thread from 4M rows per GPU up, 4 below (A/B:
+  // 10M 227 it/s at 8 vs 225 at 4 vs 214 at 16; 1.25M 390 at 4 vs 368 at 8 vs 330 at 16).
+  // LGAP_PART_ITERS (4 / 8 / 16) overrides.
+  int PartIters() const {
+    if (const char* e = std::getenv("LGAP_PART_ITERS")) {
+      const int v = std::atoi(e);
+      if (v == 4 || v == 8 || v == 16) return v;
+    }
+    return N_ >= 4000000 ? 8 : 4;
+  }
+
+  typedef void (*PartitionFn)(Args);
+  PartitionFn PartitionKernel() const {
+    return part_iters_ == 16 ? k_partition<16> : (part_iters_ == 8 ? k_partition<8> : k_partition<4>);
+  }
+
   int HistMinRows() const { return config_->device_hist_min_rows > 0 ? config_->device_hist_min_rows : kHistMinRows; }
 
   int RootBlocks() const { return std::max(1, std::min(DivUp(N_, kRootThreads), 4 * num_cu_)); }
@@ -2793,7 +2814,10 @@ class DeviceTreeLearner : public TreeLearner {
 
   void AllocState() {
     const size_t L = L_;
-    max_tiles_ = std::max(1, DivUp(N_, kTileRows));
+    part_iters_ = PartIters();
+    // tile bookkeeping sized for the smaller of the fused (256 * part_iters_) and
+    // two-kernel (kTileRows) tiles
+    max_tiles_ = std::max(1, DivUp(N_, kPartThreads * std::min(part_iters_, kPartIters)));
     fused_blocks_ = 0;
     // optionally the histogram rides in the partition kernel (one LDS tile, packed
     // fixed point). Measured slower than k_hist (whole-row threads, half the lanes
@@ -2801,7 +2825,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (config_->device_fused_partition) {
       // k_partition waits on other blocks' published counts: every block must be resident at once
       int per_cu = 0;
-      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_partition, kPartThreads, 0));
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, PartitionKernel(), kPartThreads, 0));
       // the occupancy API can overstate residency by one block per CU (MI355X_MICROARCH.md): keep a margin
       per_cu = std::max(1, per_cu - 1);
       fused_blocks_ = std::min({max_tiles_ + 1, 4 * num_cu_, per_cu * num_cu_});
@@ -2988,7 +3012,7 @@ class DeviceTreeLearner : public TreeLearner {
     for (int it = 0; it < L_ - 1; ++it) {
       const Args ap = MakeArgs(it);
       if (fused_blocks_ > 0) {
-        k_partition<<<fused_blocks_, kPartThreads, 0, s>>>(ap);
+        hipLaunchKernelGGL(PartitionKernel(), dim3(fused_blocks_), dim3(kPartThreads), 0, s, ap);
       } else {
         k_part_count<<<part_blocks, kPartThreads, 0, s>>>(ap);
         k_part_scatter<<<part_blocks, kPartThreads, 0, s>>>(ap);
@@ -3137,6 +3161,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<unsigned long long> tile_pub_;
   PinnedBuf<unsigned> pin_bar_;
   int fused_blocks_ = 0;  // k_partition grid (0: two-kernel partition)
+  int part_iters_ = 8;    // rows per thread of the fused partition (PartIters())
   const Tree* last_trained_ = nullptr;  // DeviceTrain's tree: its leaf ranges are still on the device
   DevBuf<float2> gh_true_;
   bool use_ic_ = false, is_const_hess_ = false;
