@@ -49,10 +49,21 @@ def main() -> int:
     boosters = []
     for v in variants:
         p = dict(base)
+        envs = {}
         for kv in v.split(","):
             k, val = kv.split("=")
-            p[k] = val
+            if k.startswith("env."):  # environment knobs read when the learner is set up
+                envs[k[4:]] = val
+            else:
+                p[k] = val
+        saved = {k: os.environ.get(k) for k in envs}
+        os.environ.update(envs)
         boosters.append(lgb.Booster(params=p, train_set=ds))
+        for k, old_v in saved.items():
+            if old_v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = old_v
     for b in boosters:
         for _ in range(args.warmup):
             b.update()

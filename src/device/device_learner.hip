@@ -2614,15 +2614,16 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
  private:
-  // Fused-partition tile: 8 rows per thread from 4M rows per GPU up, 4 below (A/B:
-  // 10M 227 it/s at 8 vs 225 at 4 vs 214 at 16; 1.25M 390 at 4 vs 368 at 8 vs 330 at 16).
+  // Fused-partition tile: 8 rows per thread from 8M rows per GPU up, 4 below (A/B:
+  // 10M 227 it/s at 8 vs 225 at 4 vs 214 at 16; 5M 3.42 ms/iter at 4 vs 3.48 at 8;
+  // 2.5M 2.83 vs 2.92; 1.25M 390 it/s at 4 vs 368 at 8 vs 330 at 16).
   // LGAP_PART_ITERS (4 / 8 / 16) overrides.
   int PartIters() const {
     if (const char* e = std::getenv("LGAP_PART_ITERS")) {
       const int v = std::atoi(e);
       if (v == 4 || v == 8 || v == 16) return v;
     }
-    return N_ >= 4000000 ? 8 : 4;
+    return N_ >= 8000000 ? 8 : 4;
   }
 
   typedef void (*PartitionFn)(Args);
