@@ -2829,7 +2829,9 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, PartitionKernel(), kPartThreads, 0));
       // the occupancy API can overstate residency by one block per CU (MI355X_MICROARCH.md): keep a margin
       per_cu = std::max(1, per_cu - 1);
-      fused_blocks_ = std::min({max_tiles_ + 1, 4 * num_cu_, per_cu * num_cu_});
+      const char* cap_env = std::getenv("LGAP_PART_BLOCKS_PER_CU");  // A/B knob (default 4)
+      const int cap = cap_env ? std::max(1, std::atoi(cap_env)) : 4;
+      fused_blocks_ = std::min({max_tiles_ + 1, cap * num_cu_, per_cu * num_cu_});
     }
     use_bynode_ = config_->feature_fraction_bynode < 1.0;
     // every small per-tree structure + the static feature metadata in one allocation
