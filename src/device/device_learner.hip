@@ -1886,65 +1886,40 @@ __device__ __forceinline__ bool NodeGoLeft(const DevNode& nd, uint32_t gb, const
   return b <= static_cast<uint32_t>(nd.threshold);
 }
 
-// ROWS rows per thread (rows t, t + 256, ... of a staged chunk) are walked down the
-// tree together: ROWS independent LDS lookups in flight per step instead of one
-// dependent chain per thread.
-template <int ROWS>
 __global__ __launch_bounds__(kTraverseThreads) void k_add_tree(const uint32_t* __restrict__ rowbins, int stride_dw,
                                                                int width, int N, const DevNode* __restrict__ nodes,
                                                                int num_nodes, const uint32_t* __restrict__ cat_bits,
                                                                const double* __restrict__ leaf_value,
                                                                double* __restrict__ score) {
-  constexpr int kChunk = kTraverseThreads * ROWS;
   extern __shared__ uint32_t s_dyn[];
   DevNode* s_nodes = reinterpret_cast<DevNode*>(s_dyn);
   uint32_t* s_rows = s_dyn + num_nodes * (sizeof(DevNode) / 4);
   for (int i = threadIdx.x; i < num_nodes; i += blockDim.x) s_nodes[i] = nodes[i];
   const bool staged = stride_dw <= kTraverseMaxDw;
-  for (long long base = static_cast<long long>(blockIdx.x) * kChunk; base < N;
-       base += static_cast<long long>(gridDim.x) * kChunk) {
-    const int rows = static_cast<int>(min(static_cast<long long>(kChunk), N - base));
-    const uint8_t* row[ROWS];
+  for (long long base = static_cast<long long>(blockIdx.x) * kTraverseThreads; base < N;
+       base += static_cast<long long>(gridDim.x) * kTraverseThreads) {
+    const int rows = static_cast<int>(min(static_cast<long long>(kTraverseThreads), N - base));
+    const int i = static_cast<int>(base) + threadIdx.x;
+    const uint8_t* row;
     if (staged) {
       __syncthreads();  // previous chunk's readers are done (and the nodes are in place)
       const uint32_t* src = rowbins + base * stride_dw;
       const int ndw = rows * stride_dw;
       for (int k = threadIdx.x; k < ndw; k += kTraverseThreads) s_rows[k] = src[k];
       __syncthreads();
-#pragma unroll
-      for (int r = 0; r < ROWS; ++r) {
-        row[r] = reinterpret_cast<const uint8_t*>(s_rows + (threadIdx.x + r * kTraverseThreads) * stride_dw);
-      }
+      row = reinterpret_cast<const uint8_t*>(s_rows + threadIdx.x * stride_dw);
     } else {
-      if (base == static_cast<long long>(blockIdx.x) * kChunk) __syncthreads();
-#pragma unroll
-      for (int r = 0; r < ROWS; ++r) {
-        const long long i = base + threadIdx.x + r * kTraverseThreads;
-        row[r] = reinterpret_cast<const uint8_t*>(rowbins + static_cast<size_t>(i < N ? i : 0) * stride_dw);
-      }
+      if (base == static_cast<long long>(blockIdx.x) * kTraverseThreads) __syncthreads();
+      row = reinterpret_cast<const uint8_t*>(rowbins + static_cast<size_t>(i) * stride_dw);
     }
-    int node[ROWS];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) node[r] = threadIdx.x + r * kTraverseThreads < rows ? 0 : -1;
-    bool more = true;
-    while (more) {
-      more = false;
-#pragma unroll
-      for (int r = 0; r < ROWS; ++r) {
-        if (node[r] >= 0) {
-          const DevNode& nd = s_nodes[node[r]];
-          const uint32_t gb = width == 1 ? row[r][nd.group] : reinterpret_cast<const uint16_t*>(row[r])[nd.group];
-          node[r] = NodeGoLeft(nd, gb, cat_bits) ? nd.left : nd.right;
-          more |= node[r] >= 0;
-        }
-      }
+    if (threadIdx.x >= rows) continue;
+    int node = 0;
+    while (node >= 0) {
+      const DevNode& nd = s_nodes[node];
+      const uint32_t gb = width == 1 ? row[nd.group] : reinterpret_cast<const uint16_t*>(row)[nd.group];
+      node = NodeGoLeft(nd, gb, cat_bits) ? nd.left : nd.right;
     }
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-      const int j = threadIdx.x + r * kTraverseThreads;
-      // rows that started inactive stay at -1 == ~0: only real rows write
-      if (j < rows) score[base + j] += leaf_value[~node[r]];
-    }
+    score[i] += leaf_value[~node];
   }
 }
 
@@ -2343,19 +2318,10 @@ class DeviceTreeLearner : public TreeLearner {
     const DevNode* dn = reinterpret_cast<const DevNode*>(tree_buf_.get());
     const double* dl = reinterpret_cast<const double*>(tree_buf_.get() + node_bytes);
     const uint32_t* dc = reinterpret_cast<const uint32_t*>(tree_buf_.get() + node_bytes + leaf_bytes);
-    // 4 rows per thread when a 1024-row chunk of packed rows fits the LDS budget
-    const size_t lds4 = node_bytes + sizeof(uint32_t) * kTraverseThreads * 4 * stride_dw_;
-    const bool four = stride_dw_ <= kTraverseMaxDw && lds4 <= 60 * 1024;
-    const int rows_per_block = kTraverseThreads * (four ? 4 : 1);
-    const int grid = std::min(DivUp(N_, rows_per_block), num_cu_ * 8);
-    if (four) {
-      k_add_tree<4><<<std::max(grid, 1), kTraverseThreads, lds4, stream_>>>(rowbins_.get(), stride_dw_, width_, N_, dn,
-                                                                          nn, dc, dl, s);
-    } else {
-      const size_t lds = node_bytes + (stride_dw_ <= kTraverseMaxDw ? sizeof(uint32_t) * kTraverseThreads * stride_dw_ : 0);
-      k_add_tree<1><<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins_.get(), stride_dw_, width_, N_, dn,
-                                                                         nn, dc, dl, s);
-    }
+    const int grid = std::min(DivUp(N_, kTraverseThreads), num_cu_ * 8);
+    const size_t lds = node_bytes + (stride_dw_ <= kTraverseMaxDw ? sizeof(uint32_t) * kTraverseThreads * stride_dw_ : 0);
+    k_add_tree<<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins_.get(), stride_dw_, width_, N_, dn, nn, dc,
+                                                                      dl, s);
     HIP_CHECK(hipGetLastError());
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_CHECK(hipStreamSynchronize(stream_));
