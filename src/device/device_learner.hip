@@ -62,7 +62,13 @@ namespace lgap {
 namespace device {
 namespace {
 
-constexpr int kHistThreads = 512;
+#ifndef LGAP_HIST_THREADS
+#define LGAP_HIST_THREADS 512
+#endif
+#ifndef LGAP_HIST_R
+#define LGAP_HIST_R 16
+#endif
+constexpr int kHistThreads = LGAP_HIST_THREADS;
 constexpr int kHistMinRows = 1024;  // A/B on MI355X: 1024 beats 2048 / 512 / 4096 at 1.25M and 10M rows
 constexpr int kHistLdsBytes = 56 * 1024;
 constexpr int kPartThreads = 256;
@@ -431,7 +437,7 @@ __device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& til
   const int myd = threadIdx.x - myr * tpr;
   if (myr >= rpi) return;
   constexpr int per = 4 / W;
-  constexpr int R = 16;  // rows in flight per thread
+  constexpr int R = LGAP_HIST_R;  // rows in flight per thread
   const int dw = tile.d0 + myd;
   const int gfirst = dw * per;
   int go[per];
