@@ -11,6 +11,10 @@ import socket
 import numpy as np
 import pytest
 
+# socket meshes and gloo rendezvous pick free localhost ports: under pytest-xdist run these
+# modules in one worker (--dist loadgroup) so two tests never race for the same port
+pytestmark = pytest.mark.xdist_group("localhost-network")
+
 DATA = os.path.join(os.path.dirname(__file__), "data")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
