@@ -1505,15 +1505,7 @@ struct SelOut {
   SplitKey key[2];  // the two children's winning keys (persisted by block 0)
 };
 
-// Keys / ranges a thread loaded before the control block (see k_partition): with
-// `pre` set, thread t holds scan_key[t] (t < 2F), leaf_key[t] and range[t] (t < L).
-struct SelPre {
-  bool pre;
-  SplitKey sk, lk;
-  LeafRange rg;
-};
-
-__device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so, const SelPre& pl) {
+__device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
   constexpr int kW = kPartThreads / 64;
   constexpr int kNone = 0x7fffffff;
   __shared__ double s_g[3][kW];
@@ -1526,37 +1518,23 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so, const Se
   int l3[3] = {0, 0, kNone};
   SplitKey k3[3];
   if (!c.skip) {
-    if (pl.pre) {
-      // thread t holds candidate (sel = t / F, f = t % F)
-      if (t < 2 * a.F) {
-        const int sel = t >= a.F ? 1 : 0, f = t - sel * a.F;
-        const int leaf = sel ? c.larger : c.smaller;
-        const SplitKey& k = pl.sk;
-        if (leaf >= 0 && k.feature >= 0 && CandBetter(k.gain, f, 0, g3[sel], f3[sel], 0)) {
+#pragma unroll
+    for (int sel = 0; sel < 2; ++sel) {
+      const int leaf = sel ? c.larger : c.smaller;
+      if (leaf < 0) continue;
+      for (int f = t; f < a.F; f += blockDim.x) {
+        const SplitKey k = a.scan_key[static_cast<size_t>(sel) * a.F + f];
+        if (k.feature >= 0 && CandBetter(k.gain, f, 0, g3[sel], f3[sel], 0)) {
           g3[sel] = k.gain;
           f3[sel] = f;
           k3[sel] = k;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int sel = 0; sel < 2; ++sel) {
-        const int leaf = sel ? c.larger : c.smaller;
-        if (leaf < 0) continue;
-        for (int f = t; f < a.F; f += blockDim.x) {
-          const SplitKey k = a.scan_key[static_cast<size_t>(sel) * a.F + f];
-          if (k.feature >= 0 && CandBetter(k.gain, f, 0, g3[sel], f3[sel], 0)) {
-            g3[sel] = k.gain;
-            f3[sel] = f;
-            k3[sel] = k;
-          }
         }
       }
     }
   }
   for (int l = t; l < c.num_leaves; l += blockDim.x) {
     if (l == c.smaller || l == c.larger) continue;
-    const SplitKey k = pl.pre ? pl.lk : a.leaf_key[l];
+    const SplitKey k = a.leaf_key[l];
     const double g = k.feature < 0 ? kMinScore : k.gain;
     const int f = k.feature < 0 ? kNone : k.feature;
     if (CandBetter(g, f, l, g3[2], f3[2], l3[2])) {
@@ -1566,7 +1544,7 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so, const Se
       k3[2] = k;
     }
   }
-  if (t <= c.num_leaves && t < kPartThreads) s_rng[t] = pl.pre ? pl.rg : a.range[t];
+  if (t <= c.num_leaves && t < kPartThreads) s_rng[t] = a.range[t];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     int o = t;
@@ -1676,25 +1654,13 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   __shared__ int s_wl[ITERS][kPartThreads / 64];
   __shared__ int s_wv[ITERS][kPartThreads / 64];
   const unsigned long long t_start = a.stamps ? wall_clock64() : 0ull;
-  // The select's inputs do not depend on the control block: issue their loads first so
-  // they travel with the control-block load (one dependent hop instead of two).
-  SelPre pl;
-  pl.pre = 2 * a.F <= kPartThreads && a.L <= kPartThreads;
-  if (pl.pre) {
-    const int t = threadIdx.x;
-    if (t < 2 * a.F) pl.sk = a.scan_key[t];
-    if (t < a.L) {
-      pl.lk = a.leaf_key[t];
-      pl.rg = a.range[t];
-    }
-  }
   const Ctl c = *a.ctl;
   if (c.done) return;
   const int bid = static_cast<int>(blockIdx.x);
   // no leaf has more tiles than this; one block beyond may be the post-split block
   if (bid > (c.max_count + kTile - 1) / kTile) return;
   Stamp(a, 0, 0);
-  SelectFromKeys(a, c, &so, pl);
+  SelectFromKeys(a, c, &so);
   Stamp(a, 0, 1);
   const SelState& st = so.st;
   if (bid == 0) {
