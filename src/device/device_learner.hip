@@ -2360,8 +2360,14 @@ class DeviceTreeLearner : public TreeLearner {
       }
       HIP_CHECK(hipMemcpyAsync(bynode_.get(), bm, static_cast<size_t>(2 * L_) * F_, hipMemcpyHostToDevice, stream_));
     }
-    const bool use_graph = config_->device_use_graph && !distributed_;
+    // LGAP_DP_GRAPH=1 also captures the RCCL data-parallel tree (the per-split ncclAllReduce
+    // calls replay from the graph). Off by default: on a one-rank communicator it measured
+    // 358 it/s captured vs 368 eager at 1.25M rows (profiles/README.md), and the eager host
+    // enqueue stays ahead of the ~40 us splits. The host-staged rehearsal transport
+    // synchronises inside its all-reduce and is never captured.
+    const bool use_graph = config_->device_use_graph && (!distributed_ || (DPGraphEnabled() && !HostStagedDP()));
     if (use_graph) {
+      if (graph_exec_ && distributed_ && graph_comm_ != ActiveComm()) InvalidateGraph();
       if (!graph_exec_) CaptureGraph();
       HIP_CHECK(hipGraphLaunch(graph_exec_, stream_));
     } else {
@@ -3044,6 +3050,15 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipStreamEndCapture(stream_, &g));
     HIP_CHECK(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     HIP_CHECK(hipGraphDestroy(g));
+    graph_comm_ = distributed_ ? ActiveComm() : nullptr;  // the captured collectives' communicator
+  }
+
+  static bool DPGraphEnabled() {
+    static const bool on = [] {
+      const char* e = std::getenv("LGAP_DP_GRAPH");
+      return e != nullptr && std::strcmp(e, "1") == 0;
+    }();
+    return on;
   }
 
   void InvalidateGraph() {
@@ -3126,6 +3141,7 @@ class DeviceTreeLearner : public TreeLearner {
   std::string device_name_;
   hipStream_t stream_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
+  ncclComm_t graph_comm_ = nullptr;
   ColSampler col_sampler_;
   const ObjectiveFunction* prepared_obj_ = nullptr;
   std::vector<LeafRange> h_range_;
