@@ -65,6 +65,9 @@ namespace {
 #ifndef LGAP_HIST_THREADS
 #define LGAP_HIST_THREADS 512
 #endif
+#ifndef LGAP_SCAN_UNROLL
+#define LGAP_SCAN_UNROLL 8  // slab rows in flight per lane in the k_reduce_scan fold
+#endif
 #ifndef LGAP_HIST_R
 #define LGAP_HIST_R 16
 #endif
@@ -845,7 +848,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
       double acc = 0.0;
       if (v < nv) {
         const Acc* col = slab + v0 + v;
-#pragma unroll 4
+#pragma unroll LGAP_SCAN_UNROLL
         for (int p = half; p < nb; p += 2) acc += static_cast<double>(col[static_cast<size_t>(p) * V]);
       }
       acc += __shfl_xor(acc, 32, kWave);
