@@ -78,7 +78,10 @@ constexpr int kPartThreads = 256;
 constexpr int kPartIters = 16;  // rows per thread of the two-kernel partition (k_part_count / k_part_scatter)
 constexpr int kTileRows = kPartThreads * kPartIters;
 constexpr int kScanWaves = 4;
-constexpr int kScanThreads = 1024;
+#ifndef LGAP_SCAN_THREADS
+#define LGAP_SCAN_THREADS 1024  // k_reduce_scan block size (the fold and the slot update use all waves)
+#endif
+constexpr int kScanThreads = LGAP_SCAN_THREADS;
 constexpr int kNodeThreads = 256;
 
 struct Args {
