@@ -78,6 +78,9 @@ constexpr int kPartThreads = 256;
 constexpr int kPartIters = 16;  // rows per thread of the two-kernel partition (k_part_count / k_part_scatter)
 constexpr int kTileRows = kPartThreads * kPartIters;
 constexpr int kScanWaves = 4;
+#ifndef LGAP_SCAN_FOLD
+#define LGAP_SCAN_FOLD 1  // 1: half-wave row streams, one value per lane; 2: quarter-wave streams, value pairs
+#endif
 #ifndef LGAP_SCAN_THREADS
 #define LGAP_SCAN_THREADS 1024  // k_reduce_scan block size (the fold and the slot update use all waves)
 #endif
@@ -844,6 +847,36 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
   // 1. slab reduction into hs_full at stored positions (mfb filled in step 3):
   //    each wave owns 32 values, its two half-waves stride over the slab rows;
   //    no barrier until all values are reduced
+#if LGAP_SCAN_FOLD == 2
+  // 16-lane quarter-waves each own 32 values as 16 pairs (one 2-element load per row) and
+  // stride over the slab rows 4 apart: half the dependent loads per lane of the half-wave form
+  {
+    const int quarter = lane >> 4, q = lane & 15;
+    for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
+      const int v = vbase + 2 * q;  // nv is even, so v < nv implies v + 1 < nv
+      double acc0 = 0.0, acc1 = 0.0;
+      if (v < nv) {
+        const Acc* col = slab + v0 + v;
+#pragma unroll LGAP_SCAN_UNROLL
+        for (int p = quarter; p < nb; p += 4) {
+          const Acc* e = col + static_cast<size_t>(p) * V;
+          acc0 += static_cast<double>(e[0]);
+          acc1 += static_cast<double>(e[1]);
+        }
+      }
+      acc0 += __shfl_xor(acc0, 16, kWave);
+      acc1 += __shfl_xor(acc1, 16, kWave);
+      acc0 += __shfl_xor(acc0, 32, kWave);
+      acc1 += __shfl_xor(acc1, 32, kWave);
+      if (lane < 16 && v < nv) {
+        const int k = v >> 1;  // (v, v + 1) are the (grad, hess) of stored bin k
+        const int b = k < fi.mfb ? k : k + 1;
+        hs_full[2 * b] = acc0;
+        hs_full[2 * b + 1] = acc1;
+      }
+    }
+  }
+#else
   {
     const int half = lane >> 5;
     for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
@@ -862,6 +895,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
       }
     }
   }
+#endif
   __syncthreads();
   Stamp(a, 3, 1);
   // 2. slots: smaller <- reduced; larger <- parent - smaller
