@@ -38,13 +38,15 @@ def main() -> int:
     X[rng.random(X.shape) < 0.03] = np.nan
     y = ((np.nan_to_num(X[:, 0]) - 0.8 * np.nan_to_num(X[:, 2]) + 0.4 * np.nan_to_num(X[:, 5]) ** 2
           + 0.3 * rng.standard_normal(n)) > 0.3).astype(float)
-    a, b = shard_range(n, rank, world)
+    learner = os.environ.get("DP_LEARNER", "data")
+    # data parallel: each rank holds a row shard; feature parallel: every rank holds all rows
+    a, b = shard_range(n, rank, world) if learner == "data" else (0, n)
     # l2 regression: unit hessians make every histogram hessian sum and count estimate exact,
     # so no min_data / min_hessian boundary can flip between the fixed-point device sums
     # and the host's doubles; any model difference is then a transport or split-sync bug
     objective = os.environ.get("DP_OBJECTIVE", "regression")
     base = {"objective": objective, "num_leaves": 31, "verbosity": -1, "seed": 1, "min_data_in_leaf": 20,
-            "tree_learner": "data", "num_machines": world, "pre_partition": True, "deterministic": True}
+            "tree_learner": learner, "num_machines": world, "pre_partition": True, "deterministic": True}
     ds = lgb.Dataset(X[a:b], y[a:b], params=dict(base, device_type="cpu"), free_raw_data=False).construct()
     models = {}
     devs = os.environ.get("DP_DEVICES", "gpu,cpu").split(",")

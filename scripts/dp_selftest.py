@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
-"""Single-GPU rehearsal of the RCCL data-parallel HIP learner.
+"""Single-GPU rehearsal of the data-parallel HIP learner.
 
 Creates a one-rank RCCL communicator, trains with LGAP_FORCE_DEVICE_DP=1 (the
-learner then takes the distributed path: fixed-point partials decoded to fp64
-staging, ncclAllReduce, scan from staging, global leaf counts from the split
-records) and compares against the single-device path on the same data.
+learner then takes the owner-computes distributed path: slab rows folded into the
+owner-permuted row, the owner exchange — ncclReduceScatter / ncclAllGather, or the
+xGMI in-kernel exchange with LGAP_DP_TRANSPORT=xgmi —, scan of the owned features
+from the exchanged rows, global leaf counts from the split records) and compares
+against the single-device path on the same data.
 Prints one JSON line; tests/test_gpu_learner.py runs this in a subprocess so the
 communicator never outlives it.
 """
@@ -42,8 +44,9 @@ def main() -> int:
     ta = [t["tree_structure"].get("split_feature") for t in out["single"].dump_model()["tree_info"]]
     tb = [t["tree_structure"].get("split_feature") for t in out["dp"].dump_model()["tree_info"]]
     print(json.dumps({"max_abs_diff": float(np.max(np.abs(pa - pb))), "root_features_equal": ta == tb,
-                      "dp_path": "RCCL data-parallel" in out["dp"].device_name(),
-                      "single_path": "RCCL" not in out["single"].device_name(),
+                      "dp_path": "data-parallel" in out["dp"].device_name(),
+                      "dp_name": out["dp"].device_name(),
+                      "single_path": "parallel" not in out["single"].device_name(),
                       "num_trees": [out["single"].num_trees(), out["dp"].num_trees()]}), flush=True)
     d.free_device_comm()
     return 0

@@ -20,6 +20,8 @@ for s in "$@"; do
   case $s in
     info) step info 300 python -c "import lambdagap_amd as l; print('devices', l.device_count())";;
     kernels) step kernels 900 python -m pytest tests/test_gpu_kernels.py -q --timeout 300 -p no:cacheprovider;;
+    dp1) step dp1 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "single_rank";;
+    dpmulti) step dpmulti 1100 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank";;
     learnerx) step learnerx 400 python -m pytest tests/test_gpu_learner.py -x -q --timeout 60 -p no:cacheprovider;;
     learner) step learner 1200 python -m pytest tests/test_gpu_learner.py -q --timeout 300 -p no:cacheprovider;;
     gputests) step gputests 1500 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider;;

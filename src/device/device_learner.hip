@@ -116,7 +116,6 @@ struct Args {
   void* hist_slab;
   unsigned* ghmax;  // float bits of max|g|, max|h| over the root rows
   uint8_t* splittable;
-  SplitInfo* scan_out;
   int* tile_cnt;
   int* tile_off;
   unsigned* rng;
@@ -134,12 +133,42 @@ struct Args {
   unsigned long long* ic_leaf;
   double* root_part;  // per-block (sum g, sum h, max|g|, max|h|) of k_root_sums
   unsigned* bar;      // {-, -, error flag of k_partition's bounded waits}
-  SplitKey* scan_key;  // [2][F] compact candidates of the last scan (next to scan_out)
   SplitKey* leaf_key;  // [L] compact best split per leaf (next to best)
   unsigned long long* tile_pub;  // k_partition tile counts tagged with the split epoch
   int hist_min_rows;  // rows per k_hist block (fewer rows: more blocks and slab rows)
+  // ---- owner-computes split finding (tree_learner=data|feature); single GPU: P = 1, Fmax = F
+  int P, rank, Fmax;  // ranks, this rank, candidate block width (most features any rank owns)
+  const int* own_feat;  // [Fmax] features of the groups this rank owns (-1: padding); nullptr: identity
+  char* cand;           // candidate table [P] blocks of cand_stride bytes (tree_kernels.h)
+  int cand_stride;
+  int cand_key_bytes;   // SplitKey part of a block (SplitInfo part follows)
+  int scan_src;         // 0: fold the k_hist slab rows; 1: sum the `nparts` owner rows of `rx`
+  int nparts;
+  const void* rx;       // owner rows: nparts x (2 * bbin) values of the bins this rank owns
+  int own_bin0;         // first histogram bin this rank owns
+  int bbin;             // owner block width (bins, padded to the largest block)
+  const int* bin_lo;    // [P + 1] owner bin bounds (k_hist_owner permutation)
+  int transport;        // 0: collectives between kernels (RCCL / host-staged), 2: xGMI in-kernel exchange
+  const XPeers* xp;     // xGMI: every rank's exchange buffer
+  int x_off_hist, x_off_cand, x_off_flag, x_off_root;  // offsets inside an exchange buffer
+  unsigned* xcnt;       // local arrival counters of the exchanges [4]
+  unsigned xsession;    // high word of the exchange tags (new per learner state)
+  unsigned long long xtimeout;  // bound of an exchange wait (wall_clock64 ticks, 100 MHz)
   SplitParams sp;
 };
+
+__device__ __forceinline__ SplitKey* CandKey(const Args& a, int r, int sel, int j) {
+  return reinterpret_cast<SplitKey*>(a.cand + static_cast<size_t>(r) * a.cand_stride) + sel * a.Fmax + j;
+}
+__device__ __forceinline__ SplitInfo* CandInfo(const Args& a, int r, int sel, int j) {
+  return reinterpret_cast<SplitInfo*>(a.cand + static_cast<size_t>(r) * a.cand_stride + a.cand_key_bytes) +
+         sel * a.Fmax + j;
+}
+// full record of the candidate at table position `pos` (SplitKey::pos) of child `sel`
+__device__ __forceinline__ SplitInfo* CandInfoPos(const Args& a, int sel, int pos) {
+  const int r = pos / a.Fmax;
+  return CandInfo(a, r, sel, pos - r * a.Fmax);
+}
 
 // ---------------------------------------------------------------------------
 // small device helpers
@@ -629,6 +658,163 @@ __global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid, Out
 }
 
 // ---------------------------------------------------------------------------
+// Owner-computes data parallelism (reference data_parallel_tree_learner.cpp:225-302,
+// 305-450 and parallel_tree_learner.h:209-232, redesigned for one node of MI355X):
+// ranks own contiguous, bin-balanced ranges of feature groups; per split the
+// smaller child's histogram is reduce-scattered by ownership, each rank scans only
+// the features it owns, and the per-feature candidates are all-gathered into the
+// candidate table every rank's select reads (so every rank applies the same split).
+//
+// Two transports carry the two exchanges:
+//  * collectives between kernels (transport 0): k_hist_owner writes the owner-permuted
+//    histogram row, ncclReduceScatter delivers this rank's block, k_reduce_scan writes
+//    its candidate block, ncclAllGather completes the table (host-staged for the
+//    one-GPU multi-process rehearsal);
+//  * xGMI in-kernel exchange (transport 2): the same kernels PUSH their payloads into
+//    the peers' IPC-mapped exchange buffers (uncached device memory) and complete the
+//    exchange inside the launch: every block makes its stores visible system-wide and
+//    arrives on a local counter; the last block to arrive tags flag[kind][me] in every
+//    peer and waits until all ranks tagged its own flags. The consumer is the next
+//    kernel on the stream, so no collective call, host round trip or extra launch sits
+//    in the split chain, and the whole tree still replays as one hipGraph.
+// Tags are (session << 32) | split epoch: strictly increasing, never reset, so a flag
+// is only ever compared for "reached". Every wait is bounded (error bar[3]).
+
+constexpr int kXKindHist = 0, kXKindCand = 1, kXKindRoot = 2;
+
+__device__ __forceinline__ unsigned long long XTag(const Args& a, unsigned epoch) {
+  return (static_cast<unsigned long long>(a.xsession) << 32) | epoch;
+}
+
+// flag[kind][src] inside rank `owner`'s exchange buffer
+__device__ __forceinline__ unsigned long long* XFlag(const Args& a, int owner, int kind, int src) {
+  return reinterpret_cast<unsigned long long*>(a.xp->base[owner] + a.x_off_flag) + kind * kMaxXRanks + src;
+}
+
+// spin until every rank has tagged flag[kind][*] of this rank with `tag` (one lane)
+__device__ bool XWaitAll(const Args& a, int kind, unsigned long long tag) {
+  const unsigned long long t0 = wall_clock64();
+  for (int q = 0; q < a.P; ++q) {
+    unsigned long long* f = XFlag(a, a.rank, kind, q);
+    unsigned spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < tag) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 255u) == 0u &&
+          (wall_clock64() - t0 > a.xtimeout || __hip_atomic_load(&a.bar[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(&a.bar[3], 1u + kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return true;
+}
+
+// Called by every thread of every block after the block's pushes to the peers.
+__device__ void XArriveAndExchange(const Args& a, int kind, unsigned long long tag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();  // this block's peer stores are complete before it arrives
+    const unsigned nb = gridDim.x * gridDim.y;
+    if (atomicAdd(&a.xcnt[kind], 1u) == nb - 1u) {
+      atomicExch(&a.xcnt[kind], 0u);  // every block of this launch has arrived
+      __threadfence_system();
+      for (int q = 0; q < a.P; ++q) {
+        __hip_atomic_store(XFlag(a, q, kind, a.rank), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      XWaitAll(a, kind, tag);
+    }
+  }
+}
+
+// Fold the smaller child's slab rows into the owner-permuted layout: destination q of
+// [P][2 * bbin] takes value 2 * bin_lo[r] + l of the local histogram (r = q / (2 bbin),
+// l = q % (2 bbin)); padding positions carry zeros. Transport 0 writes the row to
+// `stage` (then ncclReduceScatter); transport 2 pushes block r straight into rank r's
+// receive row `me` and completes the exchange in-kernel.
+template <typename Acc>
+__global__ __launch_bounds__(1024) void k_hist_owner(Args a, int hist_grid, Acc* __restrict__ stage) {
+  __shared__ double part[16][64];
+  const Ctl* cp = a.ctl;
+  if (cp->done || cp->skip) return;
+  const int n = a.range[cp->smaller].count;
+  const int nb = cp->hist_nb > 0 ? cp->hist_nb : HistActiveBlocks(n, hist_grid, a.hist_min_rows);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int V2 = 2 * a.bbin;
+  const int q = blockIdx.x * 64 + lane;
+  const int r = q / V2;
+  const int l = q - r * V2;
+  const bool valid = r < a.P && l < 2 * (a.bin_lo[r + 1] - a.bin_lo[r]);
+  const size_t V = 2 * static_cast<size_t>(a.TB);
+  const size_t v = valid ? 2 * static_cast<size_t>(a.bin_lo[r]) + l : 0;
+  const Acc* slab = reinterpret_cast<const Acc*>(a.hist_slab);
+  double s = 0.0;
+  if (valid) {
+    for (int p = w; p < nb; p += 16) s += static_cast<double>(slab[static_cast<size_t>(p) * V + v]);
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && r < a.P) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += part[i][lane];
+    if (a.transport == 2) {
+      if (valid) reinterpret_cast<Acc*>(a.xp->base[r] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + l] = static_cast<Acc>(t);
+    } else {
+      stage[q] = valid ? static_cast<Acc>(t) : static_cast<Acc>(0);
+    }
+  }
+  if (a.transport == 2) XArriveAndExchange(a, kXKindHist, XTag(a, cp->epoch));
+}
+
+// Root sums across ranks on the xGMI transport (one block): push (sum g, sum h) into
+// every rank's root rows, exchange, then every rank folds the rows in rank order (the
+// same fp64 result everywhere).
+__global__ __launch_bounds__(64) void k_x_root(Args a) {
+  const Ctl* cp = a.ctl;
+  if (threadIdx.x == 0) {
+    const double2 mine = a.lsum[0];
+    for (int q = 0; q < a.P; ++q) reinterpret_cast<double2*>(a.xp->base[q] + a.x_off_root)[a.rank] = mine;
+  }
+  XArriveAndExchange(a, kXKindRoot, XTag(a, cp->epoch));
+  if (threadIdx.x == 0) {
+    const double2* rows = reinterpret_cast<const double2*>(a.xp->base[a.rank] + a.x_off_root);
+    double g = 0.0, h = 0.0;
+    for (int q = 0; q < a.P; ++q) {
+      const double2 x = rows[q];
+      g += x.x;
+      h += x.y;
+    }
+    a.lsum[0] = make_double2(g, h);
+  }
+}
+
+// Transport self-test (run once when the exchange is set up): `rounds` exchanges of a
+// known pattern through the histogram rows; counts mismatching values into err[0].
+__global__ __launch_bounds__(256) void k_x_selftest(Args a, int round, int nvals, unsigned* err) {
+  const int V2 = 2 * a.bbin;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
+    for (int q = 0; q < a.P; ++q) {
+      reinterpret_cast<float*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + i] =
+          static_cast<float>(a.rank * 131 + round * 7 + (i & 1023));
+    }
+  }
+  XArriveAndExchange(a, kXKindHist, XTag(a, static_cast<unsigned>(round + 1)));
+}
+
+__global__ __launch_bounds__(256) void k_x_selfcheck(Args a, int round, int nvals, unsigned* err) {
+  const int V2 = 2 * a.bbin;
+  const float* rows = reinterpret_cast<const float*>(a.xp->base[a.rank] + a.x_off_hist);
+  unsigned bad = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
+    for (int q = 0; q < a.P; ++q) {
+      bad += rows[static_cast<size_t>(q) * V2 + i] != static_cast<float>(q * 131 + round * 7 + (i & 1023)) ? 1u : 0u;
+    }
+  }
+  if (bad) atomicAdd(err, bad);
+}
+
+// ---------------------------------------------------------------------------
 // split finding: one workgroup per feature (k_reduce_scan)
 
 struct Cand {
@@ -809,252 +995,289 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
   return any;
 }
 
-// One workgroup (16 waves) per feature:
-//  1. sum the active histogram blocks' slab rows for this feature's bins (LDS)
+// One workgroup (16 waves) per feature this rank owns (every feature on one GPU):
+//  1. the smaller child's histogram of the feature into LDS: the sum of the active
+//     histogram blocks' slab rows (single GPU / feature parallel), or of the owner rows
+//     the data-parallel exchange delivered (scan_src 1)
 //  2. smaller child's histogram -> its slot; larger child = parent - smaller
 //     (the parent histogram lives in the larger child's slot)
 //  3. reconstruct the most-frequent bin of each child, then wave 0 scans the
 //     smaller child and wave 1 the larger one concurrently, from LDS
+//  4. the block writes both candidates into this rank's block of the candidate table
+//     (on the xGMI transport: into every rank's table, then the in-kernel exchange)
 template <typename Acc>
-__global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_grid, int from_staging) {
+__global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_grid) {
   extern __shared__ __align__(16) unsigned char smem[];
   const Ctl c = *a.ctl;
   if (c.done || c.skip) return;
-  const int f = blockIdx.x;
+  const int j = blockIdx.x;
+  const int f = a.own_feat ? a.own_feat[j] : j;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   Stamp(a, 3, 0);
-  const DevFeature fi = a.feat[f];
-  const int nbin = fi.num_bin;
-  const int nst = nbin - 1;
-  const int nv = 2 * nst;  // stored values of this feature
-  double* hs_full = reinterpret_cast<double*>(smem);                 // 2 * nbin: smaller child, full
-  double* hl_full = hs_full + 2 * a.max_bin;                          // 2 * nbin: larger child, full
-  double* part = hl_full + 2 * a.max_bin;                             // [16][64]
-  int* order = reinterpret_cast<int*>(part + 16 * 64);                // max_bin (categorical scratch)
   __shared__ int s_skip_both, s_rand[2];
   __shared__ double s_sum[2][2];
   __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
+  __shared__ SplitKey s_key[2];
   SplitInfo* s_out = reinterpret_cast<SplitInfo*>(s_out_raw);
-  const int n_small = a.range[c.smaller].count;
-  // single GPU: sum the histogram blocks' slab rows here; data-parallel: the
-  // all-reduced histogram already sits in `staging` (one row of doubles)
-  const int nb = from_staging ? 1 : (c.hist_nb > 0 ? c.hist_nb : HistActiveBlocks(n_small, hist_grid, a.hist_min_rows));
-  const size_t V = 2 * static_cast<size_t>(a.TB);
-  const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
-  // (the all-reduced row has the slab element type: fp32 staging_f, or fp64 staging with gpu_use_dp)
-  const void* srow = sizeof(Acc) == sizeof(float) ? static_cast<const void*>(a.staging_f) : static_cast<const void*>(a.staging);
-  const Acc* slab = from_staging ? reinterpret_cast<const Acc*>(srow) : reinterpret_cast<const Acc*>(a.hist_slab);
-  // 1. slab reduction into hs_full at stored positions (mfb filled in step 3):
-  //    each wave owns 32 values, its two half-waves stride over the slab rows;
-  //    no barrier until all values are reduced
-#if LGAP_SCAN_FOLD == 2
-  // 16-lane quarter-waves each own 32 values as 16 pairs (one 2-element load per row) and
-  // stride over the slab rows 4 apart: half the dependent loads per lane of the half-wave form
-  {
-    const int quarter = lane >> 4, q = lane & 15;
-    for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
-      const int v = vbase + 2 * q;  // nv is even, so v < nv implies v + 1 < nv
-      double acc0 = 0.0, acc1 = 0.0;
-      if (v < nv) {
-        const Acc* col = slab + v0 + v;
-#pragma unroll LGAP_SCAN_UNROLL
-        for (int p = quarter; p < nb; p += 4) {
-          const Acc* e = col + static_cast<size_t>(p) * V;
-          acc0 += static_cast<double>(e[0]);
-          acc1 += static_cast<double>(e[1]);
-        }
-      }
-      acc0 += __shfl_xor(acc0, 16, kWave);
-      acc1 += __shfl_xor(acc1, 16, kWave);
-      acc0 += __shfl_xor(acc0, 32, kWave);
-      acc1 += __shfl_xor(acc1, 32, kWave);
-      if (lane < 16 && v < nv) {
-        const int k = v >> 1;  // (v, v + 1) are the (grad, hess) of stored bin k
-        const int b = k < fi.mfb ? k : k + 1;
-        hs_full[2 * b] = acc0;
-        hs_full[2 * b + 1] = acc1;
-      }
-    }
+  if (t < 2) {
+    s_out[t].Reset();
+    SplitKey k;
+    k.gain = kMinScore;
+    k.feature = -1;
+    k.threshold = 0;
+    k.group = k.offset = k.num_bin = k.mfb = k.default_bin = 0;
+    k.missing = k.default_left = k.is_cat = k.pad0 = 0;
+    k.pos = a.rank * a.Fmax + j;
+    k.pad2 = 0;
+    s_key[t] = k;
   }
-#else
-  {
-    const int half = lane >> 5;
-    for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
-      const int v = vbase + (lane & 31);
-      double acc = 0.0;
-      if (v < nv) {
-        const Acc* col = slab + v0 + v;
-#pragma unroll LGAP_SCAN_UNROLL
-        for (int p = half; p < nb; p += 2) acc += static_cast<double>(col[static_cast<size_t>(p) * V]);
-      }
-      acc += __shfl_xor(acc, 32, kWave);
-      if (lane < 32 && v < nv) {
+  if (t == 0 && j == 0 && c.num_leaves == 1) {
+    // root output (every rank: the host reads it back with the tree)
+    SplitParams p0 = a.sp;
+    p0.path_smooth = 0.0;
+    a.lout[0] = LeafOutputRaw(a.lsum[0].x, a.lsum[0].y, p0, a.gcount[0], 0.0);
+  }
+  if (f >= 0) {
+    const DevFeature fi = a.feat[f];
+    const int nbin = fi.num_bin;
+    const int nst = nbin - 1;
+    const int nv = 2 * nst;  // stored values of this feature
+    double* hs_full = reinterpret_cast<double*>(smem);                 // 2 * nbin: smaller child, full
+    double* hl_full = hs_full + 2 * a.max_bin;                          // 2 * nbin: larger child, full
+    double* part = hl_full + 2 * a.max_bin;                             // [16][64]
+    int* order = reinterpret_cast<int*>(part + 16 * 64);                // max_bin (categorical scratch)
+    (void)part;
+    const int n_small = a.range[c.smaller].count;
+    // 1. smaller child's histogram into hs_full at stored positions (mfb filled in step 3)
+    if (a.scan_src == 1) {
+      // owner rows of the data-parallel exchange: nparts rows of 2 * bbin values
+      const Acc* rows = reinterpret_cast<const Acc*>(a.rx) + 2 * static_cast<size_t>(fi.hist_offset - a.own_bin0);
+      const size_t stride = 2 * static_cast<size_t>(a.bbin);
+      for (int v = t; v < nv; v += blockDim.x) {
+        double acc = 0.0;
+        for (int p = 0; p < a.nparts; ++p) acc += static_cast<double>(rows[static_cast<size_t>(p) * stride + v]);
         const int k = v >> 1;
         const int b = k < fi.mfb ? k : k + 1;
         hs_full[2 * b + (v & 1)] = acc;
       }
-    }
-  }
-#endif
-  __syncthreads();
-  Stamp(a, 3, 1);
-  // 2. slots: smaller <- reduced; larger <- parent - smaller
-  const size_t slot_stride = 2 * static_cast<size_t>(a.TB);
-  const int s_slot = a.slot[c.smaller];
-  const int l_slot = c.larger >= 0 ? a.slot[c.larger] : -1;
-  double* gs = a.slots + s_slot * slot_stride + v0;
-  double* gl = l_slot >= 0 ? a.slots + l_slot * slot_stride + v0 : nullptr;
-  for (int v = t; v < nv; v += blockDim.x) {
-    const int k = v >> 1;
-    const int b = k < fi.mfb ? k : k + 1;
-    const double s = hs_full[2 * b + (v & 1)];
-    gs[v] = s;
-    if (gl) {
-      const double l = gl[v] - s;
-      gl[v] = l;
-      hl_full[2 * b + (v & 1)] = l;
-    }
-  }
-  if (t == 0) {
-    const bool skip_both =
-        !a.used_bytree[f] || (c.larger >= 0 && !a.splittable[static_cast<size_t>(s_slot) * a.F + f]);
-    s_skip_both = skip_both ? 1 : 0;
-    // extra-trees draws in the host learner's order: smaller leaf first, then larger
-    s_rand[0] = s_rand[1] = 0;
-    if (a.sp.extra_trees && !skip_both && fi.bin_type == 0 && fi.num_bin - 2 > 0) {
-      s_rand[0] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
-      if (c.larger >= 0) s_rand[1] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
-    }
-    if (c.num_leaves == 1 && f == 0) {
-      SplitParams p0 = a.sp;
-      p0.path_smooth = 0.0;
-      a.lout[0] = LeafOutputRaw(a.lsum[0].x, a.lsum[0].y, p0, a.gcount[0], 0.0);
-    }
-  }
-  __syncthreads();
-  Stamp(a, 3, 2);
-  // 3. most-frequent bin = leaf total - stored bins
-  if (w < 2) {
-    const int leaf = w == 0 ? c.smaller : c.larger;
-    if (leaf >= 0) {
-      double* H = w == 0 ? hs_full : hl_full;
-      double sgs = 0.0, shs = 0.0;
-      for (int b = lane; b < nbin; b += 64) {
-        if (b == fi.mfb) continue;
-        sgs += H[2 * b];
-        shs += H[2 * b + 1];
-      }
-      sgs = WaveSum(sgs);
-      shs = WaveSum(shs);
-      const double2 sums = a.lsum[leaf];
-      if (lane == 0) {
-        H[2 * fi.mfb] = sums.x - sgs;
-        H[2 * fi.mfb + 1] = sums.y - shs;
-        s_sum[w][0] = sums.x;
-        s_sum[w][1] = sums.y;
-      }
-    }
-  }
-  __syncthreads();
-  Stamp(a, 3, 3);
-  if (w >= 2) return;
-  const int sel = w;
-  const int leaf = sel ? c.larger : c.smaller;
-  if (leaf < 0) return;
-  SplitInfo* gout = a.scan_out + static_cast<size_t>(sel) * a.F + f;
-  SplitInfo* out = &s_out[sel];  // built in LDS, then copied out by the wave
-  if (s_skip_both) {
-    if (lane == 0) out->Reset();
-  } else {
-    const double* H = sel ? hl_full : hs_full;
-    const int lslot = sel ? l_slot : s_slot;
-    const double sg = s_sum[sel][0], sh = s_sum[sel][1];
-    const int n = a.gcount[leaf];
-    double po;
-    if (c.num_leaves == 1) {
-      SplitParams p0 = a.sp;
-      p0.path_smooth = 0.0;
-      po = LeafOutputRaw(sg, sh, p0, n, 0.0);
     } else {
-      po = a.lout[leaf];
-    }
-    const LeafBounds bounds = a.bounds[leaf];
-    const int depth = a.depth[leaf];
-    bool sp;
-    if (fi.bin_type == 0) {
-      sp = ScanNumericalWave(a, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
-    } else {
-      // categorical: lane 0 runs the sequential one-hot / ctr-sorted scan (rare, few bins)
-      int spi = 0;
-      if (lane == 0) {
-        FeatureScanMeta m;
-        m.num_bin = fi.num_bin;
-        m.default_bin = static_cast<uint32_t>(fi.default_bin);
-        m.missing_type = fi.missing;
-        m.bin_type = fi.bin_type;
-        m.monotone = fi.monotone;
-        m.penalty = fi.penalty;
-        m.rand_threshold = 0;
-        if (a.sp.extra_trees) {
-          // (categorical draws happen here; numerical ones were drawn above)
-          if (fi.num_bin <= a.sp.max_cat_to_onehot) {
-            if (fi.num_bin - 1 > 0) m.rand_threshold = RandNextInt(&a.rng[f], 1, fi.num_bin);
-          } else {
-            const double cf = n / (sh + 2 * kEpsilon);
-            int used = 0;
-            for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(H[2 * b + 1] * cf) >= a.sp.cat_smooth;
-            const int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
-            const int max_thr = max(min(max_num_cat, used) - 1, 0);
-            if (max_thr > 0) m.rand_threshold = RandNextInt(&a.rng[f], 0, max_thr);
+      const int nb = c.hist_nb > 0 ? c.hist_nb : HistActiveBlocks(n_small, hist_grid, a.hist_min_rows);
+      const size_t V = 2 * static_cast<size_t>(a.TB);
+      const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
+      const Acc* slab = reinterpret_cast<const Acc*>(a.hist_slab);
+      // each wave owns 32 values, its two half-waves stride over the slab rows;
+      // no barrier until all values are reduced
+#if LGAP_SCAN_FOLD == 2
+      // 16-lane quarter-waves each own 32 values as 16 pairs (one 2-element load per row) and
+      // stride over the slab rows 4 apart: half the dependent loads per lane of the half-wave form
+      const int quarter = lane >> 4, q = lane & 15;
+      for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
+        const int v = vbase + 2 * q;  // nv is even, so v < nv implies v + 1 < nv
+        double acc0 = 0.0, acc1 = 0.0;
+        if (v < nv) {
+          const Acc* col = slab + v0 + v;
+#pragma unroll LGAP_SCAN_UNROLL
+          for (int p = quarter; p < nb; p += 4) {
+            const Acc* e = col + static_cast<size_t>(p) * V;
+            acc0 += static_cast<double>(e[0]);
+            acc1 += static_cast<double>(e[1]);
           }
         }
-        out->Reset();
-        spi = FindBestCategorical(H, m, a.sp, sg, sh, n, po, bounds, order + sel * a.max_bin, out) ? 1 : 0;
+        acc0 += __shfl_xor(acc0, 16, kWave);
+        acc1 += __shfl_xor(acc1, 16, kWave);
+        acc0 += __shfl_xor(acc0, 32, kWave);
+        acc1 += __shfl_xor(acc1, 32, kWave);
+        if (lane < 16 && v < nv) {
+          const int k = v >> 1;  // (v, v + 1) are the (grad, hess) of stored bin k
+          const int b = k < fi.mfb ? k : k + 1;
+          hs_full[2 * b] = acc0;
+          hs_full[2 * b + 1] = acc1;
+        }
       }
-      sp = __shfl(spi, 0, kWave) != 0;
+#else
+      const int half = lane >> 5;
+      for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
+        const int v = vbase + (lane & 31);
+        double acc = 0.0;
+        if (v < nv) {
+          const Acc* col = slab + v0 + v;
+#pragma unroll LGAP_SCAN_UNROLL
+          for (int p = half; p < nb; p += 2) acc += static_cast<double>(col[static_cast<size_t>(p) * V]);
+        }
+        acc += __shfl_xor(acc, 32, kWave);
+        if (lane < 32 && v < nv) {
+          const int k = v >> 1;
+          const int b = k < fi.mfb ? k : k + 1;
+          hs_full[2 * b + (v & 1)] = acc;
+        }
+      }
+#endif
     }
-    if (lane == 0) {
-      a.splittable[static_cast<size_t>(lslot) * a.F + f] = sp ? 1 : 0;
-      if (!sp) {
-        out->Reset();
-      } else {
-        out->feature = f;
-        if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
-        if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
-        if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
+    __syncthreads();
+    Stamp(a, 3, 1);
+    // 2. slots: smaller <- reduced; larger <- parent - smaller
+    const size_t slot_stride = 2 * static_cast<size_t>(a.TB);
+    const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
+    const int s_slot = a.slot[c.smaller];
+    const int l_slot = c.larger >= 0 ? a.slot[c.larger] : -1;
+    double* gs = a.slots + s_slot * slot_stride + v0;
+    double* gl = l_slot >= 0 ? a.slots + l_slot * slot_stride + v0 : nullptr;
+    for (int v = t; v < nv; v += blockDim.x) {
+      const int k = v >> 1;
+      const int b = k < fi.mfb ? k : k + 1;
+      const double sv = hs_full[2 * b + (v & 1)];
+      gs[v] = sv;
+      if (gl) {
+        const double lv = gl[v] - sv;
+        gl[v] = lv;
+        hl_full[2 * b + (v & 1)] = lv;
+      }
+    }
+    if (t == 0) {
+      const bool skip_both =
+          !a.used_bytree[f] || (c.larger >= 0 && !a.splittable[static_cast<size_t>(s_slot) * a.F + f]);
+      s_skip_both = skip_both ? 1 : 0;
+      // extra-trees draws in the host learner's order: smaller leaf first, then larger
+      s_rand[0] = s_rand[1] = 0;
+      if (a.sp.extra_trees && !skip_both && fi.bin_type == 0 && fi.num_bin - 2 > 0) {
+        s_rand[0] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
+        if (c.larger >= 0) s_rand[1] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
+      }
+    }
+    __syncthreads();
+    Stamp(a, 3, 2);
+    // 3. most-frequent bin = leaf total - stored bins
+    if (w < 2) {
+      const int leaf = w == 0 ? c.smaller : c.larger;
+      if (leaf >= 0) {
+        double* H = w == 0 ? hs_full : hl_full;
+        double sgs = 0.0, shs = 0.0;
+        for (int b = lane; b < nbin; b += 64) {
+          if (b == fi.mfb) continue;
+          sgs += H[2 * b];
+          shs += H[2 * b + 1];
+        }
+        sgs = WaveSum(sgs);
+        shs = WaveSum(shs);
+        const double2 sums = a.lsum[leaf];
+        if (lane == 0) {
+          H[2 * fi.mfb] = sums.x - sgs;
+          H[2 * fi.mfb + 1] = sums.y - shs;
+          s_sum[w][0] = sums.x;
+          s_sum[w][1] = sums.y;
+        }
+      }
+    }
+    __syncthreads();
+    Stamp(a, 3, 3);
+    const int sel = w;
+    const int leaf = sel == 0 ? c.smaller : c.larger;
+    if (w < 2 && leaf >= 0) {
+      SplitInfo* out = &s_out[sel];  // built in LDS, published by the whole block below
+      if (!s_skip_both) {
+        const double* H = sel ? hl_full : hs_full;
+        const int lslot = sel ? l_slot : s_slot;
+        const double sg = s_sum[sel][0], sh = s_sum[sel][1];
+        const int n = a.gcount[leaf];
+        double po;
+        if (c.num_leaves == 1) {
+          SplitParams p0 = a.sp;
+          p0.path_smooth = 0.0;
+          po = LeafOutputRaw(sg, sh, p0, n, 0.0);
+        } else {
+          po = a.lout[leaf];
+        }
+        const LeafBounds bounds = a.bounds[leaf];
+        const int depth = a.depth[leaf];
+        bool sp;
+        if (fi.bin_type == 0) {
+          sp = ScanNumericalWave(a, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
+        } else {
+          // categorical: lane 0 runs the sequential one-hot / ctr-sorted scan (rare, few bins)
+          int spi = 0;
+          if (lane == 0) {
+            FeatureScanMeta m;
+            m.num_bin = fi.num_bin;
+            m.default_bin = static_cast<uint32_t>(fi.default_bin);
+            m.missing_type = fi.missing;
+            m.bin_type = fi.bin_type;
+            m.monotone = fi.monotone;
+            m.penalty = fi.penalty;
+            m.rand_threshold = 0;
+            if (a.sp.extra_trees) {
+              // (categorical draws happen here; numerical ones were drawn above)
+              if (fi.num_bin <= a.sp.max_cat_to_onehot) {
+                if (fi.num_bin - 1 > 0) m.rand_threshold = RandNextInt(&a.rng[f], 1, fi.num_bin);
+              } else {
+                const double cf = n / (sh + 2 * kEpsilon);
+                int used = 0;
+                for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(H[2 * b + 1] * cf) >= a.sp.cat_smooth;
+                const int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
+                const int max_thr = max(min(max_num_cat, used) - 1, 0);
+                if (max_thr > 0) m.rand_threshold = RandNextInt(&a.rng[f], 0, max_thr);
+              }
+            }
+            out->Reset();
+            spi = FindBestCategorical(H, m, a.sp, sg, sh, n, po, bounds, order + sel * a.max_bin, out) ? 1 : 0;
+          }
+          sp = __shfl(spi, 0, kWave) != 0;
+        }
+        if (lane == 0) {
+          a.splittable[static_cast<size_t>(lslot) * a.F + f] = sp ? 1 : 0;
+          if (!sp) {
+            out->Reset();
+          } else {
+            out->feature = f;
+            if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
+            if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
+            if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
+          }
+        }
+      }
+      if (lane == 0) {
+        // the compact candidate the partition's select reads
+        SplitKey& k = s_key[sel];
+        k.feature = out->feature;
+        k.gain = SafeGain(*out);
+        k.threshold = out->threshold;
+        k.group = fi.group;
+        k.offset = fi.offset;
+        k.num_bin = fi.num_bin;
+        k.mfb = fi.mfb;
+        k.default_bin = fi.default_bin;
+        k.missing = fi.missing;
+        k.default_left = out->default_left;
+        k.is_cat = fi.bin_type != 0 ? 1 : 0;
       }
     }
   }
-  // lane 0 built the record in LDS; the whole wave stores it
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __syncthreads();
+  // 4. publish the two candidates (dword-parallel copies of the LDS records)
   {
-    constexpr int kWords = static_cast<int>(sizeof(SplitInfo) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(out);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(gout);
-    for (int i = lane; i < kWords; i += 64) dst[i] = src[i];
-  }
-  if (lane == 0) {
-    // the compact candidate the partition's select reads
-    SplitKey k;
-    k.feature = out->feature;
-    k.gain = SafeGain(*out);
-    k.threshold = out->threshold;
-    k.group = fi.group;
-    k.offset = fi.offset;
-    k.num_bin = fi.num_bin;
-    k.mfb = fi.mfb;
-    k.default_bin = fi.default_bin;
-    k.missing = fi.missing;
-    k.default_left = out->default_left;
-    k.is_cat = fi.bin_type != 0 ? 1 : 0;
-    k.pad0 = 0;
-    k.pad1 = k.pad2 = 0;
-    a.scan_key[static_cast<size_t>(sel) * a.F + f] = k;
+    constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+    constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+    constexpr int kWords = 2 * (kKeyWords + kInfoWords);
+    const int q0 = a.transport == 2 ? 0 : a.rank;
+    const int q1 = a.transport == 2 ? a.P : a.rank + 1;
+    for (int q = q0; q < q1; ++q) {
+      char* tbl = a.transport == 2 ? a.xp->base[q] + a.x_off_cand : a.cand;
+      for (int i = t; i < kWords; i += blockDim.x) {
+        const int sel = i / (kKeyWords + kInfoWords);
+        const int o = i - sel * (kKeyWords + kInfoWords);
+        char* blk = tbl + static_cast<size_t>(a.rank) * a.cand_stride;
+        if (o < kKeyWords) {
+          reinterpret_cast<uint32_t*>(reinterpret_cast<SplitKey*>(blk) + sel * a.Fmax + j)[o] =
+              reinterpret_cast<const uint32_t*>(&s_key[sel])[o];
+        } else {
+          reinterpret_cast<uint32_t*>(reinterpret_cast<SplitInfo*>(blk + a.cand_key_bytes) + sel * a.Fmax + j)[o - kKeyWords] =
+              reinterpret_cast<const uint32_t*>(&s_out[sel])[o - kKeyWords];
+        }
+      }
+    }
   }
   Stamp(a, 3, 4);
-  if (lane == 0 && a.stamps) {
+  if (a.transport == 2) XArriveAndExchange(a, kXKindCand, XTag(a, c.epoch));
+  if (t == 0 && a.stamps) {
     atomicMax(&a.stamps[((static_cast<size_t>(3) * 256 + (a.ctl->num_splits & 255)) * 2) * 8 + 7], wall_clock64());
   }
 }
@@ -1107,108 +1330,10 @@ __device__ __forceinline__ bool CandBetter(double ga, int fa, int la, double gb,
 struct SelState {
   int done;       // no further split
   int leaf;       // leaf to split
-  int sel;        // winner source: 0/1 = scan_out row of the smaller/larger child, -1 = best[leaf]
+  int sel;        // winner source: 0/1 = candidate table row of the smaller/larger child, -1 = best[leaf]
   int feature;
-  int new_best[2];  // winning feature of the smaller/larger child (-1: none)
+  int new_best[2];  // candidate-table position of the smaller/larger child's best (-1: none)
 };
-
-__device__ __forceinline__ void WaveArgBest(double* g, int* f, int* l) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double og = __shfl_xor(*g, o, kWave);
-    const int of = __shfl_xor(*f, o, kWave);
-    const int ol = __shfl_xor(*l, o, kWave);
-    if (CandBetter(og, of, ol, *g, *f, *l)) {
-      *g = og;
-      *f = of;
-      *l = ol;
-    }
-  }
-}
-
-// Block-wide argmax; a pure function of device state, so every block computes
-// the same decision without communicating. One pass: the two new children's
-// per-feature candidates and the older leaves' stored bests are loaded together
-// (one memory round trip), then three wave-shuffle argmaxes and one barrier.
-__device__ void BlockSelect(const Args& a, const Ctl& c, SelState* st) {
-  constexpr int kW = kPartThreads / 64;
-  __shared__ double s_g[3][kW];
-  __shared__ int s_f[3][kW];
-  __shared__ int s_l[3][kW];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  double g3[3] = {kMinScore, kMinScore, kMinScore};
-  int f3[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};
-  int l3[3] = {0, 0, 0x7fffffff};
-  if (!c.skip) {
-    for (int sel = 0; sel < 2; ++sel) {
-      const int leaf = sel ? c.larger : c.smaller;
-      if (leaf < 0) continue;
-      for (int f = t; f < a.F; f += blockDim.x) {
-        const SplitInfo& s = a.scan_out[static_cast<size_t>(sel) * a.F + f];
-        const int sf = s.feature;
-        const double sg = s.gain;
-        const double g = (sf < 0 || sg != sg) ? kMinScore : sg;
-        if (sf >= 0 && CandBetter(g, f, 0, g3[sel], f3[sel], 0)) {
-          g3[sel] = g;
-          f3[sel] = f;
-        }
-      }
-    }
-  }
-  for (int l = t; l < c.num_leaves; l += blockDim.x) {
-    if (l == c.smaller || l == c.larger) continue;
-    const SplitInfo& s = a.best[l];
-    const int sf = s.feature;
-    const double sg = s.gain;
-    const double g = (sf < 0 || sg != sg) ? kMinScore : sg;
-    const int f = sf < 0 ? 0x7fffffff : sf;
-    if (CandBetter(g, f, l, g3[2], f3[2], l3[2])) {
-      g3[2] = g;
-      f3[2] = f;
-      l3[2] = l;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    WaveArgBest(&g3[k], &f3[k], &l3[k]);
-    if (lane == 0) {
-      s_g[k][w] = g3[k];
-      s_f[k][w] = f3[k];
-      s_l[k][w] = l3[k];
-    }
-  }
-  __syncthreads();
-  if (t == 0) {
-    for (int k = 0; k < 3; ++k) {
-      for (int i = 1; i < kW; ++i) {
-        if (CandBetter(s_g[k][i], s_f[k][i], s_l[k][i], s_g[k][0], s_f[k][0], s_l[k][0])) {
-          s_g[k][0] = s_g[k][i];
-          s_f[k][0] = s_f[k][i];
-          s_l[k][0] = s_l[k][i];
-        }
-      }
-    }
-    st->new_best[0] = s_f[0][0] == 0x7fffffff ? -1 : s_f[0][0];
-    st->new_best[1] = s_f[1][0] == 0x7fffffff ? -1 : s_f[1][0];
-    // overall: older leaves vs the two children (leaf index breaks full ties)
-    double bg = s_g[2][0];
-    int bf = s_f[2][0], bl = s_l[2][0];
-    for (int sel = 0; sel < 2; ++sel) {
-      const int leaf = sel ? c.larger : c.smaller;
-      if (leaf < 0 || s_f[sel][0] == 0x7fffffff) continue;
-      if (CandBetter(s_g[sel][0], s_f[sel][0], leaf, bg, bf, bl)) {
-        bg = s_g[sel][0];
-        bf = s_f[sel][0];
-        bl = leaf;
-      }
-    }
-    st->leaf = bl;
-    st->feature = bf;
-    st->done = (bl == 0x7fffffff || bf == 0x7fffffff || !(bg > 0.0)) ? 1 : 0;
-    st->sel = (bl == c.smaller) ? 0 : ((bl == c.larger) ? 1 : -1);
-  }
-  __syncthreads();
-}
 
 // ---------------------------------------------------------------------------
 // stable partition of the split leaf's row indices
@@ -1227,11 +1352,187 @@ __device__ void FillSplitDesc(const Args& a, const SplitInfo& s, SplitDesc* d) {
   for (int w = 0; w < kMaxCatWords; ++w) d->bits[w] = d->is_cat ? s.cat_bitset[w] : 0u;
 }
 
+__device__ __forceinline__ void WaveArgBest4(double* g, int* f, int* l, int* o) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    const double og = __shfl_xor(*g, s, kWave);
+    const int of = __shfl_xor(*f, s, kWave);
+    const int ol = __shfl_xor(*l, s, kWave);
+    const int oo = __shfl_xor(*o, s, kWave);
+    if (CandBetter(og, of, ol, *g, *f, *l)) {
+      *g = og;
+      *f = of;
+      *l = ol;
+      *o = oo;
+    }
+  }
+}
+
+struct SelOut {
+  SelState st;
+  SplitDesc d;
+  LeafRange pr;
+  SplitKey key[2];  // the two children's winning keys (persisted by block 0)
+};
+
+__device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
+  constexpr int kW = kPartThreads / 64;
+  constexpr int kNone = 0x7fffffff;
+  __shared__ double s_g[3][kW];
+  __shared__ int s_f[3][kW], s_l[3][kW], s_o[3][kW];
+  __shared__ int s_owner[3], s_win_cat;
+  __shared__ LeafRange s_rng[kPartThreads];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  double g3[3] = {kMinScore, kMinScore, kMinScore};
+  int f3[3] = {kNone, kNone, kNone};
+  int l3[3] = {0, 0, kNone};
+  SplitKey k3[3];
+  if (!c.skip) {
+    // the two children's candidates: every position of the table (all ranks' blocks)
+    const int np = a.P * a.Fmax;
+#pragma unroll
+    for (int sel = 0; sel < 2; ++sel) {
+      const int leaf = sel ? c.larger : c.smaller;
+      if (leaf < 0) continue;
+      for (int p = t; p < np; p += blockDim.x) {
+        const int r = p / a.Fmax;
+        const SplitKey k = *CandKey(a, r, sel, p - r * a.Fmax);
+        if (k.feature >= 0 && CandBetter(k.gain, k.feature, 0, g3[sel], f3[sel], 0)) {
+          g3[sel] = k.gain;
+          f3[sel] = k.feature;
+          k3[sel] = k;
+        }
+      }
+    }
+  }
+  for (int l = t; l < c.num_leaves; l += blockDim.x) {
+    if (l == c.smaller || l == c.larger) continue;
+    const SplitKey k = a.leaf_key[l];
+    const double g = k.feature < 0 ? kMinScore : k.gain;
+    const int f = k.feature < 0 ? kNone : k.feature;
+    if (CandBetter(g, f, l, g3[2], f3[2], l3[2])) {
+      g3[2] = g;
+      f3[2] = f;
+      l3[2] = l;
+      k3[2] = k;
+    }
+  }
+  if (t <= c.num_leaves && t < kPartThreads) s_rng[t] = a.range[t];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    int o = t;
+    WaveArgBest4(&g3[k], &f3[k], &l3[k], &o);
+    if (lane == 0) {
+      s_g[k][w] = g3[k];
+      s_f[k][w] = f3[k];
+      s_l[k][w] = l3[k];
+      s_o[k][w] = o;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int k = 0; k < 3; ++k) {
+      for (int i = 1; i < kW; ++i) {
+        if (CandBetter(s_g[k][i], s_f[k][i], s_l[k][i], s_g[k][0], s_f[k][0], s_l[k][0])) {
+          s_g[k][0] = s_g[k][i];
+          s_f[k][0] = s_f[k][i];
+          s_l[k][0] = s_l[k][i];
+          s_o[k][0] = s_o[k][i];
+        }
+      }
+      s_owner[k] = s_f[k][0] == kNone ? -1 : s_o[k][0];
+    }
+    SelState& st = so->st;
+    st.new_best[0] = -1;  // positions: filled in by the owning threads below
+    st.new_best[1] = -1;
+    double bg = s_g[2][0];
+    int bf = s_f[2][0], bl = s_l[2][0], cat = 2;
+    for (int sel = 0; sel < 2; ++sel) {
+      const int leaf = sel ? c.larger : c.smaller;
+      if (leaf < 0 || s_f[sel][0] == kNone) continue;
+      if (CandBetter(s_g[sel][0], s_f[sel][0], leaf, bg, bf, bl)) {
+        bg = s_g[sel][0];
+        bf = s_f[sel][0];
+        bl = leaf;
+        cat = sel;
+      }
+    }
+    st.leaf = bl;
+    st.feature = bf;
+    st.done = (bl == kNone || bf == kNone || !(bg > 0.0)) ? 1 : 0;
+    st.sel = cat == 2 ? -1 : cat;
+    s_win_cat = st.done ? -1 : cat;
+  }
+  __syncthreads();
+  if (t == s_owner[0]) {
+    so->key[0] = k3[0];
+    so->st.new_best[0] = k3[0].pos;
+  }
+  if (t == s_owner[1]) {
+    so->key[1] = k3[1];
+    so->st.new_best[1] = k3[1].pos;
+  }
+  const int wc = s_win_cat;
+  if (wc >= 0 && t == s_owner[wc]) {
+    const SplitKey& k = k3[wc];
+    SplitDesc& d = so->d;
+    d.group = k.group;
+    d.offset = k.offset;
+    d.num_bin = k.num_bin;
+    d.mfb = k.mfb;
+    d.default_bin = k.default_bin;
+    d.missing = k.missing;
+    d.thr = static_cast<int>(k.threshold);
+    d.default_left = k.default_left;
+    d.is_cat = k.is_cat;
+    if (k.is_cat) {
+      const SplitInfo* win = wc < 2 ? CandInfoPos(a, wc, k.pos) : &a.best[so->st.leaf];
+      for (int i = 0; i < kMaxCatWords; ++i) d.bits[i] = win->cat_bitset[i];
+    }
+    const int leaf = so->st.leaf;
+    so->pr = leaf < kPartThreads ? s_rng[leaf] : a.range[leaf];
+  }
+  __syncthreads();
+}
+
+
+// Block 0 of the partition: persist the two children's bests (full record + compact
+// key) for later selects, and the `done` decision in both control buffers.
+__device__ void PersistChildBests(const Args& a, const Ctl& c, const SelOut& so) {
+  const SelState& st = so.st;
+  if (c.smaller >= 0 && st.new_best[0] >= 0) CopySplitInfoBlock(&a.best[c.smaller], CandInfoPos(a, 0, st.new_best[0]));
+  if (c.larger >= 0 && st.new_best[1] >= 0) CopySplitInfoBlock(&a.best[c.larger], CandInfoPos(a, 1, st.new_best[1]));
+  if (threadIdx.x == 0) {
+    if (c.smaller >= 0) {
+      if (st.new_best[0] >= 0) {
+        a.leaf_key[c.smaller] = so.key[0];
+      } else {
+        a.best[c.smaller].Reset();
+        a.leaf_key[c.smaller].feature = -1;
+        a.leaf_key[c.smaller].gain = kMinScore;
+      }
+    }
+    if (c.larger >= 0) {
+      if (st.new_best[1] >= 0) {
+        a.leaf_key[c.larger] = so.key[1];
+      } else {
+        a.best[c.larger].Reset();
+        a.leaf_key[c.larger].feature = -1;
+        a.leaf_key[c.larger].gain = kMinScore;
+      }
+    }
+    if (st.done) {
+      // both control buffers: later launches read either
+      a.ctl->done = 1;
+      a.ctl_next->done = 1;
+    }
+  }
+}
+
 // Select the leaf to split (replicated), persist the decision (block 0), then
 // count the rows going left per 4096-row tile of the parent range.
 __global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
-  __shared__ SplitDesc d;
-  __shared__ SelState st;
+  __shared__ SelOut so;
   __shared__ int sh[8];
   Ctl* cp = a.ctl;
   const Ctl c = *cp;
@@ -1239,27 +1540,14 @@ __global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
   // no leaf has more tiles than this: surplus blocks have nothing to count
   if (blockIdx.x > 0 && static_cast<int>(blockIdx.x) >= (c.max_count + kTileRows - 1) / kTileRows) return;
   Stamp(a, 0, 0);
-  BlockSelect(a, c, &st);
+  SelectFromKeys(a, c, &so);
   Stamp(a, 0, 1);
-  const SplitInfo* win = st.done ? nullptr
-                                 : (st.sel >= 0 ? &a.scan_out[static_cast<size_t>(st.sel) * a.F + st.feature]
-                                                : &a.best[st.leaf]);
-  if (blockIdx.x == 0) {
-    // persist: per-leaf bests of the two children (invalid when their scan was skipped)
-    if (c.smaller >= 0 && st.new_best[0] >= 0) CopySplitInfoBlock(&a.best[c.smaller], &a.scan_out[st.new_best[0]]);
-    if (c.larger >= 0 && st.new_best[1] >= 0) {
-      CopySplitInfoBlock(&a.best[c.larger], &a.scan_out[static_cast<size_t>(a.F) + st.new_best[1]]);
-    }
-  }
+  const SelState& st = so.st;
+  if (blockIdx.x == 0) PersistChildBests(a, c, so);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (c.smaller >= 0 && st.new_best[0] < 0) a.best[c.smaller].Reset();
-    if (c.larger >= 0 && st.new_best[1] < 0) a.best[c.larger].Reset();
     if (!c.skip) cp->scan_round = c.scan_round + 1;
-    if (st.done) {
-      cp->done = 1;
-      a.ctl_next->done = 1;
-    } else {
-      const LeafRange pr = a.range[st.leaf];
+    if (!st.done) {
+      const LeafRange pr = so.pr;
       cp->split_leaf = st.leaf;
       cp->new_leaf = c.num_leaves;
       cp->parent_buf = pr.buf;
@@ -1269,9 +1557,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
     }
   }
   if (st.done) return;
-  if (threadIdx.x == 0) FillSplitDesc(a, *win, &d);
-  const LeafRange pr = a.range[st.leaf];
-  __syncthreads();
+  const SplitDesc& d = so.d;
+  const LeafRange pr = so.pr;
   Stamp(a, 0, 2);
   const int ntiles = (pr.count + kTileRows - 1) / kTileRows;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -1522,140 +1809,6 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
 // reversed right child changes no result. Every wait is bounded: a timeout raises
 // the sticky error flag bar[2] that the host checks after the tree.
 
-__device__ __forceinline__ void WaveArgBest4(double* g, int* f, int* l, int* o) {
-#pragma unroll
-  for (int s = 32; s > 0; s >>= 1) {
-    const double og = __shfl_xor(*g, s, kWave);
-    const int of = __shfl_xor(*f, s, kWave);
-    const int ol = __shfl_xor(*l, s, kWave);
-    const int oo = __shfl_xor(*o, s, kWave);
-    if (CandBetter(og, of, ol, *g, *f, *l)) {
-      *g = og;
-      *f = of;
-      *l = ol;
-      *o = oo;
-    }
-  }
-}
-
-struct SelOut {
-  SelState st;
-  SplitDesc d;
-  LeafRange pr;
-  SplitKey key[2];  // the two children's winning keys (persisted by block 0)
-};
-
-__device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
-  constexpr int kW = kPartThreads / 64;
-  constexpr int kNone = 0x7fffffff;
-  __shared__ double s_g[3][kW];
-  __shared__ int s_f[3][kW], s_l[3][kW], s_o[3][kW];
-  __shared__ int s_owner[3], s_win_cat;
-  __shared__ LeafRange s_rng[kPartThreads];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  double g3[3] = {kMinScore, kMinScore, kMinScore};
-  int f3[3] = {kNone, kNone, kNone};
-  int l3[3] = {0, 0, kNone};
-  SplitKey k3[3];
-  if (!c.skip) {
-#pragma unroll
-    for (int sel = 0; sel < 2; ++sel) {
-      const int leaf = sel ? c.larger : c.smaller;
-      if (leaf < 0) continue;
-      for (int f = t; f < a.F; f += blockDim.x) {
-        const SplitKey k = a.scan_key[static_cast<size_t>(sel) * a.F + f];
-        if (k.feature >= 0 && CandBetter(k.gain, f, 0, g3[sel], f3[sel], 0)) {
-          g3[sel] = k.gain;
-          f3[sel] = f;
-          k3[sel] = k;
-        }
-      }
-    }
-  }
-  for (int l = t; l < c.num_leaves; l += blockDim.x) {
-    if (l == c.smaller || l == c.larger) continue;
-    const SplitKey k = a.leaf_key[l];
-    const double g = k.feature < 0 ? kMinScore : k.gain;
-    const int f = k.feature < 0 ? kNone : k.feature;
-    if (CandBetter(g, f, l, g3[2], f3[2], l3[2])) {
-      g3[2] = g;
-      f3[2] = f;
-      l3[2] = l;
-      k3[2] = k;
-    }
-  }
-  if (t <= c.num_leaves && t < kPartThreads) s_rng[t] = a.range[t];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    int o = t;
-    WaveArgBest4(&g3[k], &f3[k], &l3[k], &o);
-    if (lane == 0) {
-      s_g[k][w] = g3[k];
-      s_f[k][w] = f3[k];
-      s_l[k][w] = l3[k];
-      s_o[k][w] = o;
-    }
-  }
-  __syncthreads();
-  if (t == 0) {
-    for (int k = 0; k < 3; ++k) {
-      for (int i = 1; i < kW; ++i) {
-        if (CandBetter(s_g[k][i], s_f[k][i], s_l[k][i], s_g[k][0], s_f[k][0], s_l[k][0])) {
-          s_g[k][0] = s_g[k][i];
-          s_f[k][0] = s_f[k][i];
-          s_l[k][0] = s_l[k][i];
-          s_o[k][0] = s_o[k][i];
-        }
-      }
-      s_owner[k] = s_f[k][0] == kNone ? -1 : s_o[k][0];
-    }
-    SelState& st = so->st;
-    st.new_best[0] = s_f[0][0] == kNone ? -1 : s_f[0][0];
-    st.new_best[1] = s_f[1][0] == kNone ? -1 : s_f[1][0];
-    double bg = s_g[2][0];
-    int bf = s_f[2][0], bl = s_l[2][0], cat = 2;
-    for (int sel = 0; sel < 2; ++sel) {
-      const int leaf = sel ? c.larger : c.smaller;
-      if (leaf < 0 || s_f[sel][0] == kNone) continue;
-      if (CandBetter(s_g[sel][0], s_f[sel][0], leaf, bg, bf, bl)) {
-        bg = s_g[sel][0];
-        bf = s_f[sel][0];
-        bl = leaf;
-        cat = sel;
-      }
-    }
-    st.leaf = bl;
-    st.feature = bf;
-    st.done = (bl == kNone || bf == kNone || !(bg > 0.0)) ? 1 : 0;
-    st.sel = cat == 2 ? -1 : cat;
-    s_win_cat = st.done ? -1 : cat;
-  }
-  __syncthreads();
-  if (t == s_owner[0]) so->key[0] = k3[0];
-  if (t == s_owner[1]) so->key[1] = k3[1];
-  const int wc = s_win_cat;
-  if (wc >= 0 && t == s_owner[wc]) {
-    const SplitKey& k = k3[wc];
-    SplitDesc& d = so->d;
-    d.group = k.group;
-    d.offset = k.offset;
-    d.num_bin = k.num_bin;
-    d.mfb = k.mfb;
-    d.default_bin = k.default_bin;
-    d.missing = k.missing;
-    d.thr = static_cast<int>(k.threshold);
-    d.default_left = k.default_left;
-    d.is_cat = k.is_cat;
-    if (k.is_cat) {
-      const SplitInfo* win = wc < 2 ? &a.scan_out[static_cast<size_t>(wc) * a.F + k.feature] : &a.best[so->st.leaf];
-      for (int i = 0; i < kMaxCatWords; ++i) d.bits[i] = win->cat_bitset[i];
-    }
-    const int leaf = so->st.leaf;
-    so->pr = leaf < kPartThreads ? s_rng[leaf] : a.range[leaf];
-  }
-  __syncthreads();
-}
-
 __device__ __forceinline__ void PublishCount(unsigned long long* p, unsigned epoch, int cnt) {
   const unsigned long long v = (static_cast<unsigned long long>(epoch) << 32) | static_cast<unsigned>(cnt);
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1703,40 +1856,9 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
   SelectFromKeys(a, c, &so);
   Stamp(a, 0, 1);
   const SelState& st = so.st;
-  if (bid == 0) {
-    // persist the two children's bests (full record + compact key) for later selects
-    if (c.smaller >= 0 && st.new_best[0] >= 0) CopySplitInfoBlock(&a.best[c.smaller], &a.scan_out[st.new_best[0]]);
-    if (c.larger >= 0 && st.new_best[1] >= 0) {
-      CopySplitInfoBlock(&a.best[c.larger], &a.scan_out[static_cast<size_t>(a.F) + st.new_best[1]]);
-    }
-    if (threadIdx.x == 0) {
-      if (c.smaller >= 0) {
-        if (st.new_best[0] >= 0) {
-          a.leaf_key[c.smaller] = so.key[0];
-        } else {
-          a.best[c.smaller].Reset();
-          a.leaf_key[c.smaller].feature = -1;
-          a.leaf_key[c.smaller].gain = kMinScore;
-        }
-      }
-      if (c.larger >= 0) {
-        if (st.new_best[1] >= 0) {
-          a.leaf_key[c.larger] = so.key[1];
-        } else {
-          a.best[c.larger].Reset();
-          a.leaf_key[c.larger].feature = -1;
-          a.leaf_key[c.larger].gain = kMinScore;
-        }
-      }
-      if (st.done) {
-        // both control buffers: later launches read either
-        a.ctl->done = 1;
-        a.ctl_next->done = 1;
-      }
-    }
-  }
+  if (bid == 0) PersistChildBests(a, c, so);
   if (st.done) return;
-  const SplitInfo* win = st.sel >= 0 ? &a.scan_out[static_cast<size_t>(st.sel) * a.F + st.feature] : &a.best[st.leaf];
+  const SplitInfo* win = st.sel >= 0 ? CandInfoPos(a, st.sel, st.new_best[st.sel]) : &a.best[st.leaf];
   const LeafRange pr = so.pr;
   const SplitDesc& d = so.d;
   const unsigned epoch = c.epoch;
@@ -1991,12 +2113,18 @@ class PinnedBuf {
   size_t n_ = 0;
 };
 
+// Parallel modes of the device learner (tree_learner=serial|data|feature).
+enum class DevParallel { kSerial, kData, kFeature };
+
 class DeviceTreeLearner : public TreeLearner {
  public:
-  DeviceTreeLearner(const Config* config, bool data_parallel) : config_(config), data_parallel_(data_parallel) {}
+  DeviceTreeLearner(const Config* config, DevParallel mode)
+      : config_(config), mode_(mode), data_parallel_(mode == DevParallel::kData) {}
 
   ~DeviceTreeLearner() override {
     if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+    if (!x_peers_.empty()) XgmiClose(x_local_, &x_peers_);
+    if (x_local_) (void)hipFree(x_local_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
 
@@ -2009,14 +2137,20 @@ class DeviceTreeLearner : public TreeLearner {
     TB_ = train->num_total_bin();
     width_ = train->bin_width();
     stride_dw_ = train->row_stride() / 4;
-    if (data_parallel_ && !CommActive() && !HostStagedDP() && Network::num_machines() > 1) {
-      Log::Fatal("Data-parallel HIP training needs an RCCL communicator (LGBM_DeviceCommInit)");
+    const bool parallel = mode_ != DevParallel::kSerial;
+    if (parallel && !CommActive() && !HostStagedDP() && Network::num_machines() > 1) {
+      Log::Fatal("Parallel HIP training needs an RCCL communicator (LGBM_DeviceCommInit)");
     }
-    // LGAP_FORCE_DEVICE_DP=1 routes a single-rank run through the RCCL data-parallel path
-    // (staging reduce + ncclAllReduce + global counts): lets a 1-GPU box test that path.
+    // LGAP_FORCE_DEVICE_DP=1 routes a single-rank run through the data-parallel path
+    // (owner histogram exchange, candidate table, global counts): lets a 1-GPU box test it.
     const char* force_dp = std::getenv("LGAP_FORCE_DEVICE_DP");
     const bool forced = CommExists() && force_dp && force_dp[0] == '1';
-    distributed_ = (data_parallel_ && (CommActive() || HostStagedDP())) || forced;
+    if (forced && mode_ == DevParallel::kSerial) {
+      mode_ = DevParallel::kData;
+      data_parallel_ = true;
+    }
+    owner_scan_ = (mode_ != DevParallel::kSerial) && (CommActive() || HostStagedDP() || forced);
+    distributed_ = owner_scan_ && data_parallel_;
     device_id_ = CommExists() ? CommDevice() : std::max(0, config_->gpu_device_id);
     HIP_CHECK(hipSetDevice(device_id_));
     hipDeviceProp_t prop;
@@ -2029,9 +2163,159 @@ class DeviceTreeLearner : public TreeLearner {
     }
     use_dp_ = config_->gpu_use_dp;
     UploadData();
+    SetupOwnership();
     ResetConfig(config_);
+    SetupTransport();
     Log::Info("HIP tree learner on %s: %d rows, %d features, %d groups, %d bins%s", device_name_.c_str(), N_, F_, G_,
-              TB_, distributed_ ? " (data-parallel over RCCL)" : "");
+              TB_, owner_scan_ ? (" (" + ParallelDesc() + ")").c_str() : "");
+  }
+
+  // Feature-group ownership of the owner-computes modes: contiguous group ranges with
+  // ~equal bins per rank (the host DataParallelTreeLearner's assignment), so rank r's
+  // block of the histogram is the contiguous bin range [bin_lo[r], bin_lo[r + 1]).
+  void SetupOwnership() {
+    P_ = owner_scan_ ? DpSize() : 1;
+    rank_ = owner_scan_ ? DpRank() : 0;
+    h_bin_lo_.assign(P_ + 1, TB_);
+    std::vector<int> owner(G_);
+    for (int g = 0; g < G_; ++g) {
+      const auto& grp = data_->group(g);
+      const long long mid = grp.hist_start + grp.num_bin / 2;
+      owner[g] = std::min(P_ - 1, static_cast<int>(mid * P_ / std::max(1, TB_)));
+    }
+    // owners are non-decreasing in g: rank r owns groups [first_r, first_{r+1})
+    for (int r = P_ - 1; r >= 0; --r) {
+      int lo = h_bin_lo_[r + 1];
+      for (int g = 0; g < G_; ++g) {
+        if (owner[g] == r) {
+          lo = data_->group(g).hist_start;
+          break;
+        }
+      }
+      h_bin_lo_[r] = std::min(lo, h_bin_lo_[r + 1]);
+    }
+    h_bin_lo_[0] = 0;
+    bbin_ = 1;
+    for (int r = 0; r < P_; ++r) bbin_ = std::max(bbin_, h_bin_lo_[r + 1] - h_bin_lo_[r]);
+    std::vector<int> cnt(P_, 0);
+    h_own_feat_.clear();
+    for (int f = 0; f < F_; ++f) {
+      const int r = owner_scan_ ? owner[data_->feature(f).group] : 0;
+      ++cnt[r];
+      if (r == rank_) h_own_feat_.push_back(f);
+    }
+    Fmax_ = 1;
+    for (int r = 0; r < P_; ++r) Fmax_ = std::max(Fmax_, cnt[r]);
+    if (!owner_scan_) Fmax_ = std::max(1, F_);
+    h_own_feat_.resize(Fmax_, -1);
+    const size_t kb = Round256(2 * static_cast<size_t>(Fmax_) * sizeof(SplitKey));
+    const size_t ib = Round256(2 * static_cast<size_t>(Fmax_) * sizeof(SplitInfo));
+    cand_key_bytes_ = static_cast<int>(kb);
+    cand_stride_ = static_cast<int>(kb + ib);
+  }
+
+  static size_t Round256(size_t x) { return (x + 255) & ~static_cast<size_t>(255); }
+
+  // Transport of the owner-computes exchanges. LGAP_DP_TRANSPORT = auto (default: xGMI
+  // in-kernel exchange when every rank maps every peer and the self-test passes, else
+  // collectives) | xgmi | collective.
+  void SetupTransport() {
+    transport_ = 0;
+    if (!owner_scan_) return;
+    const char* e = std::getenv("LGAP_DP_TRANSPORT");
+    const std::string want = e ? e : "auto";
+    if (want != "auto" && want != "xgmi" && want != "collective") Log::Fatal("LGAP_DP_TRANSPORT=%s: expected auto|xgmi|collective", want.c_str());
+    if (want == "collective" || P_ > kMaxXRanks) return;
+    const size_t es = use_dp_ ? sizeof(double) : sizeof(float);
+    ArenaLayout lay;
+    x_off_hist_ = static_cast<int>(lay.Add<char>(static_cast<size_t>(P_) * 2 * bbin_ * es));
+    x_off_cand_ = static_cast<int>(lay.Add<char>(static_cast<size_t>(P_) * cand_stride_));
+    x_off_flag_ = static_cast<int>(lay.Add<unsigned long long>(4 * kMaxXRanks));
+    x_off_root_ = static_cast<int>(lay.Add<double2>(kMaxXRanks));
+    x_bytes_ = lay.bytes();
+    // uncached device memory: peers' pushes land in HBM and every read of it is fresh
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, x_bytes_, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      if (hipExtMallocWithFlags(&p, x_bytes_, hipDeviceMallocFinegrained) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+      }
+    }
+    int ok = p != nullptr ? 1 : 0;
+    if (ok) HIP_CHECK(hipMemset(p, 0, x_bytes_));
+    if (P_ > 1) ok = Network::GlobalSyncUpByMin(ok);
+    if (!ok) {
+      if (p) (void)hipFree(p);
+      if (want == "xgmi") Log::Fatal("xGMI transport: cannot allocate the uncached exchange buffer");
+      Log::Warning("xGMI transport unavailable (exchange buffer); using collectives");
+      return;
+    }
+    x_local_ = static_cast<char*>(p);
+    if (!XgmiOpen(x_local_, &x_peers_)) {
+      (void)hipFree(x_local_);
+      x_local_ = nullptr;
+      if (want == "xgmi") Log::Fatal("xGMI transport: peer exchange buffers could not be mapped");
+      Log::Warning("xGMI transport unavailable (IPC mapping); using collectives");
+      return;
+    }
+    XPeers xp;
+    std::memset(&xp, 0, sizeof(xp));
+    for (int q = 0; q < P_; ++q) xp.base[q] = x_peers_[q];
+    xpeers_.Resize(1);
+    xpeers_.Upload(&xp, 1, stream_);
+    transport_ = 2;
+    const bool good = XgmiSelfTest();
+    int all_good = good ? 1 : 0;
+    if (P_ > 1) all_good = Network::GlobalSyncUpByMin(all_good);
+    if (!all_good) {
+      transport_ = 0;
+      XgmiClose(x_local_, &x_peers_);
+      (void)hipFree(x_local_);
+      x_local_ = nullptr;
+      if (want == "xgmi") Log::Fatal("xGMI transport: self-test failed");
+      Log::Warning("xGMI transport self-test failed; using collectives");
+      return;
+    }
+    InvalidateGraph();
+  }
+
+  // Three exchanges of a known pattern through the histogram rows (session 0 tags,
+  // below every training tag), checked value by value on every rank.
+  bool XgmiSelfTest() {
+    Args a = MakeArgs(0);
+    a.xsession = 0;
+    const double saved = a.xtimeout;
+    a.xtimeout = static_cast<unsigned long long>(100e6 * std::min(30.0, std::max(1.0, saved / 100e6)));
+    DevBuf<unsigned> err(1);
+    err.Zero(stream_);
+    const int nvals = std::min(2 * bbin_, 4096);
+    for (int round = 0; round < 3; ++round) {
+      k_x_selftest<<<4, 256, 0, stream_>>>(a, round, nvals, err.get());
+      k_x_selfcheck<<<4, 256, 0, stream_>>>(a, round, nvals, err.get());
+    }
+    HIP_CHECK(hipGetLastError());
+    unsigned h[4] = {0, 0, 0, 0};
+    err.Download(h, 1, stream_);
+    unsigned* hb = pin_bar_.Get(4);
+    HIP_CHECK(hipMemcpyAsync(hb, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    const bool ok = h[0] == 0u && hb[3] == 0u;
+    if (!ok) {
+      Log::Warning("xGMI self-test on rank %d: %u wrong values, wait status %u", rank_, h[0], hb[3]);
+      bar_.Zero(stream_);
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    return ok;
+  }
+
+  std::string ParallelDesc() const {
+    std::string m = mode_ == DevParallel::kFeature ? "feature-parallel" : "data-parallel";
+    m += ", " + std::to_string(P_) + " ranks, ";
+    if (transport_ == 2) return m + "xGMI in-kernel exchange";
+    if (HostStagedDP()) return m + "host-staged collectives";
+    return m + "RCCL reduce-scatter/all-gather";
   }
 
   void ResetConfig(const Config* config) override {
@@ -2382,7 +2666,14 @@ class DeviceTreeLearner : public TreeLearner {
     tp->root_count = use_bag_ ? bag_cnt_ : N_;
     tp->cls = class_id;
     int gcount = tp->root_count;
-    if (distributed_) gcount = Network::GlobalSyncUpBySum(gcount);
+    if (distributed_) {
+      // the global root count changes only with the bag: one host collective per new bag
+      if (gcount != cached_gcount_local_) {
+        cached_gcount_local_ = gcount;
+        cached_gcount_ = Network::num_machines() > 1 ? Network::GlobalSyncUpBySum(gcount) : gcount;
+      }
+      gcount = cached_gcount_;
+    }
     tp->root_gcount = gcount;
     HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
     if (config_->use_quantized_grad) QuantizeGradients(class_id);
@@ -2405,7 +2696,9 @@ class DeviceTreeLearner : public TreeLearner {
     // 358 it/s captured vs 368 eager at 1.25M rows (profiles/README.md), and the eager host
     // enqueue stays ahead of the ~40 us splits. The host-staged rehearsal transport
     // synchronises inside its all-reduce and is never captured.
-    const bool use_graph = config_->device_use_graph && (!distributed_ || (DPGraphEnabled() && !HostStagedDP()));
+    // the xGMI transport keeps every exchange inside the kernels: the tree replays as one graph
+    const bool collectives = owner_scan_ && transport_ != 2;
+    const bool use_graph = config_->device_use_graph && (!collectives || (DPGraphEnabled() && !HostStagedDP()));
     if (use_graph) {
       if (graph_exec_ && distributed_ && graph_comm_ != ActiveComm()) InvalidateGraph();
       if (!graph_exec_) CaptureGraph();
@@ -2424,14 +2717,18 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(hlo, lout_.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
     unsigned* hbar = pin_bar_.Get(4);
     HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
-    if (distributed_) {
-      // the tree's histogram all-reduces ride on this stream: a lost peer must not hang us
+    if (collectives && !HostStagedDP()) {
+      // the tree's collectives ride on this stream: a lost peer must not hang us
       static const double timeout_s = CommTimeoutSeconds(config_->time_out);
-      WatchedStreamSync(stream_, timeout_s, "device tree growth (RCCL histogram all-reduce)");
+      WatchedStreamSync(stream_, timeout_s, "device tree growth (RCCL histogram reduce-scatter)");
     } else {
       HIP_CHECK(hipStreamSynchronize(stream_));
     }
     if (hbar[2] != 0u) Log::Fatal("k_partition: a wait on published tile counts timed out (blocks not co-resident?)");
+    if (hbar[3] != 0u) {
+      Log::Fatal("xGMI exchange (%s) timed out on rank %d after %.0f s: a peer stopped training",
+                 hbar[3] == 1u ? "histogram" : (hbar[3] == 2u ? "split candidates" : "root sums"), rank_, XTimeoutSeconds());
+    }
     // the control buffer written last holds the final tree state
     const Ctl* hc = hc2[1].num_splits > hc2[0].num_splits ? &hc2[1] : &hc2[0];
     auto tree = std::make_unique<Tree>(L_, false, false);
@@ -2475,8 +2772,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   std::string DeviceName() const override {
-    if (!distributed_) return device_name_;
-    return device_name_ + (HostStagedDP() ? " [host-staged data-parallel]" : " [RCCL data-parallel]");
+    if (!owner_scan_) return device_name_;
+    return device_name_ + " [" + ParallelDesc() + "]";
   }
 
   void ReportStamps(int nsplits) {
@@ -2714,17 +3011,15 @@ class DeviceTreeLearner : public TreeLearner {
     }
     HIP_CHECK(hipGetLastError());
     if (distributed_ && collective) {
-      const size_t n = 2 * static_cast<size_t>(TB_);
-      const int rgrid = DivUp(2 * static_cast<long long>(TB_), 64);
+      // owner reduce-scatter of the smaller child's histogram (xGMI: inside k_hist_owner)
+      const int ogrid = DivUp(static_cast<long long>(P_) * 2 * bbin_, 64);
       if (use_dp_) {
-        k_hist_reduce<double, double><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks(), staging_.get());
-        HIP_CHECK(hipGetLastError());
-        AllreduceSumF64(staging_.get(), n, stream_);
+        k_hist_owner<double><<<ogrid, 1024, 0, stream_>>>(a, HistBlocks(), reinterpret_cast<double*>(stage_.get()));
       } else {
-        k_hist_reduce<float, float><<<rgrid, 1024, 0, stream_>>>(a, HistBlocks(), staging_f_.get());
-        HIP_CHECK(hipGetLastError());
-        AllreduceSumF32(staging_f_.get(), n, stream_);
+        k_hist_owner<float><<<ogrid, 1024, 0, stream_>>>(a, HistBlocks(), reinterpret_cast<float*>(stage_.get()));
       }
+      HIP_CHECK(hipGetLastError());
+      if (transport_ != 2) ReduceScatterSum(stage_.get(), rx_.get(), 2 * static_cast<size_t>(bbin_), use_dp_, stream_);
     }
   }
 
@@ -2737,16 +3032,19 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void LaunchScan(const Args& a) {
-    if (distributed_ && use_dp_) {
-      k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 1);
-    } else if (distributed_) {
-      k_reduce_scan<float><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 1);
-    } else if (use_dp_) {
-      k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 0);
-    } else {
-      k_reduce_scan<float><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks(), 0);
-    }
+    if (use_dp_) k_reduce_scan<double><<<Fmax_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks());
+    else k_reduce_scan<float><<<Fmax_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks());
     HIP_CHECK(hipGetLastError());
+    // complete the candidate table (xGMI: inside k_reduce_scan)
+    if (owner_scan_ && transport_ != 2 && P_ > 1) AllGatherInPlace(cand_.get(), cand_stride_, stream_);
+  }
+
+  static double XTimeoutSeconds() {
+    static const double t = [] {
+      const char* e = std::getenv("LGAP_XGMI_TIMEOUT_S");
+      return e != nullptr && *e ? std::max(0.1, std::atof(e)) : 60.0;
+    }();
+    return t;
   }
 
   void UploadData() {
@@ -2892,16 +3190,16 @@ class DeviceTreeLearner : public TreeLearner {
                  o_lsum = lay.Add<double2>(L), o_lout = lay.Add<double>(L), o_gcount = lay.Add<int>(L),
                  o_depth = lay.Add<int>(L), o_slot = lay.Add<int>(L), o_bounds = lay.Add<LeafBounds>(L),
                  o_best = lay.Add<SplitInfo>(L), o_rec = lay.Add<SplitRec>(L), o_ghmax = lay.Add<unsigned>(2),
-                 o_spl = lay.Add<uint8_t>(L * F_), o_scan = lay.Add<SplitInfo>(2 * static_cast<size_t>(F_)),
-                 o_tcnt = lay.Add<int>(max_tiles_), o_toff = lay.Add<int>(max_tiles_),
+                 o_spl = lay.Add<uint8_t>(L * F_), o_tcnt = lay.Add<int>(max_tiles_), o_toff = lay.Add<int>(max_tiles_),
                  o_used = lay.Add<uint8_t>(std::max(F_, 1)), o_byn = lay.Add<uint8_t>(use_bynode_ ? 2 * L * F_ : 1),
                  o_rng = lay.Add<unsigned>(std::max(F_, 1)), o_feat = lay.Add<DevFeature>(h_feats_.size()),
                  o_gst = lay.Add<int>(h_gstart_.size()), o_tiles = lay.Add<HistTile>(h_tiles_.size()),
                  o_icf = lay.Add<unsigned long long>(std::max(F_, 1)), o_icl = lay.Add<unsigned long long>(L),
                  o_qmax = lay.Add<unsigned>(2), o_tsum = lay.Add<double2>(L),
                  o_rpart = lay.Add<double>(4 * static_cast<size_t>(std::max(1, 4 * num_cu_))),
-                 o_bar = lay.Add<unsigned>(4), o_skey = lay.Add<SplitKey>(2 * static_cast<size_t>(F_)),
-                 o_lkey = lay.Add<SplitKey>(L), o_tpub = lay.Add<unsigned long long>(max_tiles_);
+                 o_bar = lay.Add<unsigned>(4), o_lkey = lay.Add<SplitKey>(L),
+                 o_tpub = lay.Add<unsigned long long>(max_tiles_), o_xcnt = lay.Add<unsigned>(4),
+                 o_own = lay.Add<int>(Fmax_), o_binlo = lay.Add<int>(P_ + 1);
     arena_.Resize(std::max<size_t>(lay.bytes(), size_t(2) << 20));
     char* base = arena_.get();
     tparams_.Attach(reinterpret_cast<TreeParams*>(base + o_tp), 1);
@@ -2917,7 +3215,6 @@ class DeviceTreeLearner : public TreeLearner {
     rec_.Attach(reinterpret_cast<SplitRec*>(base + o_rec), L);
     ghmax_.Attach(reinterpret_cast<unsigned*>(base + o_ghmax), 2);
     splittable_.Attach(reinterpret_cast<uint8_t*>(base + o_spl), L * F_);
-    scan_out_.Attach(reinterpret_cast<SplitInfo*>(base + o_scan), 2 * static_cast<size_t>(F_));
     tile_cnt_.Attach(reinterpret_cast<int*>(base + o_tcnt), max_tiles_);
     tile_off_.Attach(reinterpret_cast<int*>(base + o_toff), max_tiles_);
     used_bytree_.Attach(reinterpret_cast<uint8_t*>(base + o_used), std::max(F_, 1));
@@ -2932,10 +3229,21 @@ class DeviceTreeLearner : public TreeLearner {
     true_sums_.Attach(reinterpret_cast<double2*>(base + o_tsum), L);
     root_part_.Attach(reinterpret_cast<double*>(base + o_rpart), 4 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
     bar_.Attach(reinterpret_cast<unsigned*>(base + o_bar), 4);
-    scan_key_.Attach(reinterpret_cast<SplitKey*>(base + o_skey), 2 * static_cast<size_t>(F_));
     leaf_key_.Attach(reinterpret_cast<SplitKey*>(base + o_lkey), L);
     tile_pub_.Attach(reinterpret_cast<unsigned long long*>(base + o_tpub), max_tiles_);
+    xcnt_.Attach(reinterpret_cast<unsigned*>(base + o_xcnt), 4);
+    own_feat_.Attach(reinterpret_cast<int*>(base + o_own), Fmax_);
+    bin_lo_.Attach(reinterpret_cast<int*>(base + o_binlo), P_ + 1);
     arena_.Zero(stream_);
+    own_feat_.Upload(h_own_feat_, stream_);
+    bin_lo_.Upload(h_bin_lo_, stream_);
+    // candidate table: P blocks (a local copy; the xGMI transport uses the table inside
+    // the exchange buffer that the peers push into)
+    cand_.Resize(static_cast<size_t>(P_) * cand_stride_);
+    cand_.Zero(stream_);
+    rx_.Resize(std::max<size_t>(1, 2 * static_cast<size_t>(bbin_) * (use_dp_ ? 8 : 4)));
+    stage_.Resize(owner_scan_ ? static_cast<size_t>(P_) * 2 * bbin_ * (use_dp_ ? 8 : 4) : 1);
+    ++xsession_;  // exchange tags of this state start above every earlier one
     use_ic_ = !config_->interaction_constraints_vector.empty();
     if (use_ic_) {
       const auto& sets = config_->interaction_constraints_vector;
@@ -3013,7 +3321,6 @@ class DeviceTreeLearner : public TreeLearner {
     a.hist_slab = hist_slab_.get();
     a.ghmax = ghmax_.get();
     a.splittable = splittable_.get();
-    a.scan_out = scan_out_.get();
     a.tile_cnt = tile_cnt_.get();
     a.tile_off = tile_off_.get();
     a.rng = rng_.get();
@@ -3030,10 +3337,33 @@ class DeviceTreeLearner : public TreeLearner {
     a.ic_leaf = use_ic_ ? ic_leaf_.get() : nullptr;
     a.root_part = root_part_.get();
     a.bar = bar_.get();
-    a.scan_key = scan_key_.get();
     a.leaf_key = leaf_key_.get();
     a.tile_pub = tile_pub_.get();
     a.hist_min_rows = HistMinRows();
+    a.P = P_;
+    a.rank = rank_;
+    a.Fmax = Fmax_;
+    a.own_feat = owner_scan_ ? own_feat_.get() : nullptr;
+    a.cand = transport_ == 2 ? x_local_ + x_off_cand_ : cand_.get();
+    a.cand_stride = cand_stride_;
+    a.cand_key_bytes = cand_key_bytes_;
+    // data parallel: the scan sums owner rows (xGMI: every rank's pushed row; collectives:
+    // the reduce-scattered row); single GPU / feature parallel: the local slab rows
+    a.scan_src = distributed_ ? 1 : 0;
+    a.nparts = transport_ == 2 ? P_ : 1;
+    a.rx = transport_ == 2 ? static_cast<const void*>(x_local_ + x_off_hist_) : static_cast<const void*>(rx_.get());
+    a.own_bin0 = h_bin_lo_.empty() ? 0 : h_bin_lo_[rank_];
+    a.bbin = bbin_;
+    a.bin_lo = bin_lo_.get();
+    a.transport = transport_;
+    a.xp = transport_ == 2 ? xpeers_.get() : nullptr;
+    a.x_off_hist = x_off_hist_;
+    a.x_off_cand = x_off_cand_;
+    a.x_off_flag = x_off_flag_;
+    a.x_off_root = x_off_root_;
+    a.xcnt = xcnt_.get();
+    a.xsession = xsession_;
+    a.xtimeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;
@@ -3061,7 +3391,10 @@ class DeviceTreeLearner : public TreeLearner {
     const int root_blocks = RootBlocks();
     k_root_sums<<<root_blocks, kRootThreads, 0, s>>>(a);
     k_root_final<<<1, kRootThreads, 0, s>>>(a, root_blocks);
-    if (distributed_) AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
+    if (distributed_) {
+      if (transport_ == 2) k_x_root<<<1, 64, 0, s>>>(a);
+      else AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
+    }
     LaunchHist(a);
     LaunchScan(a);
     for (int it = 0; it < L_ - 1; ++it) {
@@ -3214,7 +3547,6 @@ class DeviceTreeLearner : public TreeLearner {
   std::vector<HistTile> h_tiles_;
   DevBuf<unsigned> ghmax_;
   DevBuf<uint8_t> splittable_;
-  DevBuf<SplitInfo> scan_out_;
   DevBuf<int> tile_cnt_, tile_off_;
   DevBuf<uint8_t> used_bytree_, bynode_;
   DevBuf<unsigned long long> ic_feat_, ic_leaf_;
@@ -3222,7 +3554,24 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<double2> true_sums_;
   DevBuf<double> root_part_;
   DevBuf<unsigned> bar_;
-  DevBuf<SplitKey> scan_key_, leaf_key_;
+  DevBuf<SplitKey> leaf_key_;
+  // owner-computes parallel modes
+  DevParallel mode_ = DevParallel::kSerial;
+  bool owner_scan_ = false;
+  int P_ = 1, rank_ = 0, Fmax_ = 1, bbin_ = 1, cand_stride_ = 0, cand_key_bytes_ = 0;
+  std::vector<int> h_bin_lo_, h_own_feat_;
+  DevBuf<int> own_feat_, bin_lo_;
+  DevBuf<char> cand_, rx_, stage_;
+  DevBuf<unsigned> xcnt_;
+  // xGMI transport
+  int transport_ = 0;
+  char* x_local_ = nullptr;
+  std::vector<char*> x_peers_;
+  size_t x_bytes_ = 0;
+  int x_off_hist_ = 0, x_off_cand_ = 0, x_off_flag_ = 0, x_off_root_ = 0;
+  DevBuf<XPeers> xpeers_;
+  unsigned xsession_ = 0;
+  int cached_gcount_ = -1, cached_gcount_local_ = -1;
   DevBuf<unsigned long long> tile_pub_;
   PinnedBuf<unsigned> pin_bar_;
   int fused_blocks_ = 0;  // k_partition grid (0: two-kernel partition)
@@ -3265,14 +3614,9 @@ class DeviceTreeLearner : public TreeLearner {
 }  // namespace
 
 std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const std::string& parallel_mode) {
-  if (parallel_mode == "serial") return std::make_unique<DeviceTreeLearner>(config, false);
-  if (parallel_mode == "data" || parallel_mode == "voting" || parallel_mode == "feature") {
-    if (parallel_mode != "data") {
-      Log::Warning("tree_learner=%s on the HIP learner runs as data-parallel (histogram all-reduce over RCCL)",
-                   parallel_mode.c_str());
-    }
-    return std::make_unique<DeviceTreeLearner>(config, true);
-  }
+  if (parallel_mode == "serial") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kSerial);
+  if (parallel_mode == "data") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kData);
+  if (parallel_mode == "feature") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kFeature);
   Log::Fatal("Unknown tree learner type %s", parallel_mode.c_str());
   return nullptr;
 }
@@ -3287,7 +3631,7 @@ class DeviceHistogramBackend final : public HistogramBackend {
     cfg_.gpu_use_dp = user->gpu_use_dp;
     cfg_.gpu_device_id = user->gpu_device_id;
     cfg_.device_hist_blocks = user->device_hist_blocks;
-    learner_ = std::make_unique<DeviceTreeLearner>(&cfg_, false);
+    learner_ = std::make_unique<DeviceTreeLearner>(&cfg_, DevParallel::kSerial);
     learner_->Init(data, false);
   }
   void SetGradients(const float* g, const float* h, int n) override { learner_->BackendSetGradients(g, h, n); }
@@ -3311,7 +3655,7 @@ void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, 
   Config cfg;
   cfg.num_leaves = 2;
   cfg.verbosity = -1;
-  DeviceTreeLearner learner(&cfg, false);
+  DeviceTreeLearner learner(&cfg, DevParallel::kSerial);
   learner.Init(data, false);
   learner.TestHistogram(grad, hess, rows, num_rows, out);
 }

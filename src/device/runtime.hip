@@ -213,6 +213,109 @@ void AllreduceSumF32(float* dev_ptr, size_t count, hipStream_t stream) {
   AllreduceSum(dev_ptr, count, stream, ncclFloat32);
 }
 
+int DpSize() { return Network::num_machines() > 1 ? Network::num_machines() : std::max(1, S().size); }
+int DpRank() { return Network::num_machines() > 1 ? Network::rank() : S().rank; }
+
+// Owner reduce-scatter of the data-parallel histogram: `send` holds DpSize() blocks of
+// `count` elements (block r = the bins rank r owns); `recv` gets this rank's block summed
+// over ranks (reference data_parallel_tree_learner.cpp:284-297, HistogramSumReducer).
+void ReduceScatterSum(const void* send, void* recv, size_t count, bool f64, hipStream_t stream) {
+  if (count == 0) return;
+  const size_t es = f64 ? sizeof(double) : sizeof(float);
+  if (HostStagedDP()) {
+    const int n = Network::num_machines();
+    thread_local std::vector<char> h, o;
+    h.resize(es * count * n);
+    o.resize(es * count);
+    HIP_CHECK(hipMemcpyAsync(h.data(), send, h.size(), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    std::vector<comm_size_t> start(n), len(n, static_cast<comm_size_t>(es * count));
+    for (int i = 0; i < n; ++i) start[i] = static_cast<comm_size_t>(es * count * i);
+    Network::ReduceScatter(h.data(), static_cast<comm_size_t>(h.size()), static_cast<int>(es), start.data(),
+                           len.data(), o.data(), static_cast<comm_size_t>(o.size()),
+                           f64 ? Network::SumReducer<double>() : Network::SumReducer<float>());
+    HIP_CHECK(hipMemcpyAsync(recv, o.data(), o.size(), hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    return;
+  }
+  if (!CommExists()) {
+    HIP_CHECK(hipMemcpyAsync(recv, send, es * count, hipMemcpyDeviceToDevice, stream));
+    return;
+  }
+  NcclCheck(ncclReduceScatter(send, recv, count, f64 ? ncclFloat64 : ncclFloat32, ncclSum, S().comm, stream),
+            "ncclReduceScatter");
+}
+
+// In-place allgather: `buf` holds DpSize() blocks of `bytes` each, this rank's block filled.
+void AllGatherInPlace(void* buf, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return;
+  if (HostStagedDP()) {
+    const int n = Network::num_machines(), r = Network::rank();
+    thread_local std::vector<char> h;
+    h.resize(bytes * n);
+    char* mine = h.data() + bytes * r;
+    HIP_CHECK(hipMemcpyAsync(mine, static_cast<char*>(buf) + bytes * r, bytes, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    std::vector<char> in(mine, mine + bytes);
+    Network::Allgather(in.data(), static_cast<comm_size_t>(bytes), h.data());
+    HIP_CHECK(hipMemcpyAsync(buf, h.data(), h.size(), hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    return;
+  }
+  if (!CommExists() || S().size <= 1) return;
+  char* base = static_cast<char*>(buf);
+  NcclCheck(ncclAllGather(base + bytes * S().rank, base, bytes, ncclChar, S().comm, stream), "ncclAllGather");
+}
+
+// xGMI peer mapping (collective over the DpSize() ranks): every rank exports `local`
+// (one allocation of identical size and layout on every rank) with hipIpcGetMemHandle,
+// the handles are all-gathered over the host collectives, and each rank maps its peers'
+// buffers. Returns false on every rank when any rank failed (the caller then keeps the
+// collective transport); no HIP error is fatal here.
+bool XgmiOpen(char* local, std::vector<char*>* peers) {
+  const int n = DpSize(), r = DpRank();
+  struct Rec {
+    int ok, pad;
+    hipIpcMemHandle_t h;
+  };
+  Rec mine;
+  std::memset(&mine, 0, sizeof(mine));
+  mine.ok = hipIpcGetMemHandle(&mine.h, local) == hipSuccess ? 1 : 0;
+  if (!mine.ok) (void)hipGetLastError();
+  std::vector<Rec> all(n);
+  if (n > 1) {
+    Network::Allgather(reinterpret_cast<char*>(&mine), sizeof(Rec), reinterpret_cast<char*>(all.data()));
+  } else {
+    all[0] = mine;
+  }
+  int ok = 1;
+  for (const Rec& x : all) ok &= x.ok;
+  peers->assign(n, nullptr);
+  for (int q = 0; q < n && ok; ++q) {
+    if (q == r) {
+      (*peers)[q] = local;
+      continue;
+    }
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, all[q].h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      (void)hipGetLastError();
+      ok = 0;
+    } else {
+      (*peers)[q] = static_cast<char*>(p);
+    }
+  }
+  if (n > 1) ok = Network::GlobalSyncUpByMin(ok);
+  if (!ok) XgmiClose(local, peers);
+  return ok != 0;
+}
+
+void XgmiClose(char* local, std::vector<char*>* peers) {
+  for (char* p : *peers) {
+    if (p != nullptr && p != local) (void)hipIpcCloseMemHandle(p);
+  }
+  peers->clear();
+}
+
 // Collective watchdog (the reference only has socket timeouts; a lost
 // worker hangs its peers). Waits for `stream` while polling the communicator's
 // asynchronous error state; on an RCCL error, or when the wait outlives

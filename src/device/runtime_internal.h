@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <cstddef>
+#include <vector>
 
 namespace lgap {
 namespace device {
@@ -25,6 +26,21 @@ void AllreduceSumF32(float* dev_ptr, size_t count, hipStream_t stream);
 void WatchedStreamSync(hipStream_t stream, double timeout_s, const char* what);
 // collective timeout: LGAP_COMM_TIMEOUT_S, else the `time_out` parameter (minutes)
 double CommTimeoutSeconds(int time_out_minutes);
+
+// ---- owner-computes data parallelism (device learner)
+// ranks / this rank of the data-parallel group (host Network when it spans several
+// processes, else the RCCL communicator)
+int DpSize();
+int DpRank();
+// `send`: DpSize() blocks of `count` fp32 (fp64 with f64) values; recv: this rank's block
+// summed over ranks (ncclReduceScatter, or host-staged for the rehearsal transport)
+void ReduceScatterSum(const void* send, void* recv, size_t count, bool f64, hipStream_t stream);
+// in-place allgather of DpSize() blocks of `bytes` (this rank's block filled)
+void AllGatherInPlace(void* buf, size_t bytes, hipStream_t stream);
+// map every rank's exchange buffer (same size / layout on all ranks) into this process
+// over IPC (xGMI transport); collective; false on every rank if any rank failed
+bool XgmiOpen(char* local, std::vector<char*>* peers);
+void XgmiClose(char* local, std::vector<char*>* peers);
 
 }  // namespace device
 }  // namespace lgap

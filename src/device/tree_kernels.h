@@ -75,7 +75,21 @@ struct SplitKey {
   int group, offset, num_bin, mfb;
   int default_bin;
   int8_t missing, default_left, is_cat, pad0;
-  int pad1, pad2;
+  int pos;  // candidate position (rank * Fmax + owned index): where the full SplitInfo sits
+  int pad2;
+};
+
+// Owner-computes data parallelism: every rank scans the features of the groups it
+// owns and publishes its candidates as one block; the blocks of all ranks form the
+// candidate table [P][ SplitKey[2][Fmax] | SplitInfo[2][Fmax] ] that every rank's
+// best-leaf select reads (single GPU: P = 1, Fmax = F).
+constexpr int kMaxXRanks = 16;  // xGMI transport: ranks of one node
+
+// xGMI transport: each rank's exchange buffer (IPC-mapped, uncached device memory)
+// holds [histogram receive rows][candidate table][flags][root rows] at identical
+// offsets on every rank; base[q] is rank q's buffer in this process's address space.
+struct XPeers {
+  char* base[kMaxXRanks];
 };
 
 struct SplitRec {

@@ -29,7 +29,6 @@ std::unique_ptr<TreeLearner> CreateHost(const std::string& learner_type, bool li
 const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, const Config* c) {
   if (linear_tree) return "linear_tree";
   if (learner_type == "voting") return "voting-parallel election";
-  if (learner_type == "feature") return "feature-parallel ownership";
   if (CegbPenalty::Enabled(c)) return "cost-effective gradient boosting";
   if (!c->forcedsplits_filename.empty()) return "forced splits";
   if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {

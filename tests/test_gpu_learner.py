@@ -165,37 +165,44 @@ def test_device_goss(lgb, gpu_required):
     assert abs(ag - ac) < 1e-3, (ag, ac)
 
 
-def test_rccl_data_parallel_path_single_rank(lgb, gpu_required):
-    """The RCCL data-parallel learner path (fp64 staging + ncclAllReduce + global counts) on a
-    one-rank communicator must reproduce the single-device model."""
+@pytest.mark.parametrize("transport", ["collective", "xgmi"])
+def test_data_parallel_path_single_rank(lgb, gpu_required, transport):
+    """The owner-computes data-parallel learner path (owner exchange of the histogram, owned-feature
+    scan, candidate table, global counts) on a one-rank communicator must reproduce the
+    single-device model, over RCCL collectives and over the xGMI in-kernel exchange."""
     import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20")
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "dp_selftest.py")], capture_output=True,
-                       text=True, timeout=600)
+                       text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["num_trees"] == [8, 8]
     assert res["dp_path"] and res["single_path"], res
+    assert ("xGMI" in res["dp_name"]) == (transport == "xgmi"), res
     assert res["root_features_equal"]
     assert res["max_abs_diff"] < 1e-3, res
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world):
-    """P ranks share the one GPU; the device data-parallel learner's collectives are staged
-    through host memory (gloo). Every rank must grow the identical model, and it must match
-    the host data-parallel learner trained by the same ranks on the same bins."""
+@pytest.mark.parametrize("world,transport", [(2, "collective"), (3, "collective"), (2, "xgmi"), (3, "xgmi"),
+                                             (4, "xgmi")])
+def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
+    """P ranks share the one GPU. The device data-parallel learner exchanges owner histograms and
+    split candidates either through host-staged collectives (gloo) or through the xGMI in-kernel
+    exchange over IPC-mapped buffers (here all on one device). Every rank must grow the identical
+    model, and it must match the host data-parallel learner trained by the same ranks on the
+    same bins."""
     import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
                         "--nproc-per-node", str(world), os.path.join(root, "scripts", "dp_multirank.py")],
                        capture_output=True, text=True, timeout=600, env=env, cwd=root)
@@ -203,12 +210,37 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["world"] == world
     assert "data-parallel" in res["device_name"], res
+    assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
     assert res["ranks_identical"], res
     assert res["num_trees"] == 10
     # unit hessians (l2): the split structure must match the host learner tree for tree
     assert res["identical_leading_trees"] == 10, res
     assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
     assert abs(res["auc_gpu"] - res["auc_cpu"]) < 1e-3, res
+
+
+@pytest.mark.parametrize("transport", ["collective", "xgmi"])
+def test_feature_parallel_multirank_rehearsal(lgb, gpu_required, transport):
+    """Device feature-parallel (every rank holds all rows, scans the features of the groups it
+    owns, candidates exchanged into one table) on 3 ranks sharing the GPU: identical models on all
+    ranks, equal to the host feature-parallel learner tree for tree."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20",
+               DP_LEARNER="feature")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+                        "--nproc-per-node", "3", os.path.join(root, "scripts", "dp_multirank.py")],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "feature-parallel" in res["device_name"], res
+    assert res["ranks_identical"], res
+    assert res["identical_leading_trees"] == 10, res
+    assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
 
 
 def _policy_data(rng, n=20000):
