@@ -66,3 +66,13 @@ clean:
 	rm -rf $(BUILD) $(LIB) $(CLI)
 
 .PHONY: all clean cpptest asan
+
+# A/B variant of the library with extra compile-time flags on the device learner:
+#   make variant NAME=k1 VFLAGS=-DLGAP_SCAN_K=1   ->  variants/lib_k1.so (LAMBDAGAP_LIB=...)
+VARIANT_DIR := variants
+variant: $(CPP_OBJS) $(HIP_OBJS)
+	@mkdir -p $(BUILD)/variant_$(NAME) $(VARIANT_DIR)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c src/device/device_learner.hip -o $(BUILD)/variant_$(NAME)/device_learner.hip.o
+	$(CXX) -o $(VARIANT_DIR)/lib_$(NAME).so $(CPP_OBJS) $(filter-out $(BUILD)/device/device_learner.hip.o,$(HIP_OBJS)) \
+	  $(BUILD)/variant_$(NAME)/device_learner.hip.o $(LDFLAGS)
+.PHONY: variant

@@ -22,11 +22,19 @@ for s in "$@"; do
     kernels) step kernels 900 python -m pytest tests/test_gpu_kernels.py -q --timeout 300 -p no:cacheprovider;;
     dp1) step dp1 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "single_rank";;
     dpmulti) step dpmulti 1100 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank";;
+    fp) step fp 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "feature_parallel";;
+    dpbench) step b1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_DP_TRANSPORT=xgmi step b1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=collective step b1coll 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && step b10single 300 python bench.py --steps 30 --warmup 3 && LGAP_DP_TRANSPORT=xgmi step b10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp;;
+    profdpx) LGAP_DP_TRANSPORT=xgmi step profdpx 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/profdpx -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 --rehearse-dp && python scripts/prof_summary.py $OUT/profdpx "1.25M rows, DP xGMI path (1 rank)" 22 > $OUT/profdpx_summary.md;;
+    pmc10) for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" "FETCH_SIZE TCC_HIT_sum" "WRITE_SIZE TCC_MISS_sum"; do
+             n=$(echo $pass | cut -c1-8 | tr -d ' '); step pmc_$n 240 timeout -s KILL 200 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d $PWD/$OUT/pmc10_$n -o run -- python3 bench.py --steps 3 --warmup 1;
+           done; python scripts/pmc_summary.py "10M x 28, 63 leaves (bench.py --steps 3 --warmup 1)" $OUT/pmc10_* > $OUT/pmc10_summary.md;;
+    stampsdp) LGAP_STAMPS=1 LGAP_DP_TRANSPORT=xgmi step stampsdp 300 python bench.py --rows 1250000 --steps 3 --warmup 1 --rehearse-dp;;
+    quick) step b10 300 python bench.py --steps 30 --warmup 3 && step b1 300 python bench.py --rows 1250000 --steps 50 --warmup 5;;
+    diagrank) step diagrank 300 python scripts/diag_rank.py ${DIAG_TARGET:-lambdagap-s} && step diagrank_dp 300 python scripts/diag_rank.py ${DIAG_TARGET:-lambdagap-s} gpu_use_dp=true;;
+    dpfix) step dpfix 900 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank or watchdog or xgmi_exchange";;
     learnerx) step learnerx 400 python -m pytest tests/test_gpu_learner.py -x -q --timeout 60 -p no:cacheprovider;;
     learner) step learner 1200 python -m pytest tests/test_gpu_learner.py -q --timeout 300 -p no:cacheprovider;;
     gputests) step gputests 1500 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider;;
-    debugrank) step debugrank 300 python scripts/debug_rank.py ndcg;;
-    debugcat) step debugcat 300 python scripts/debug_cat.py && step debugcatdp 300 python scripts/debug_cat.py dp;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
     bench1m) step bench1m 400 python bench.py --rows 1000000 --steps 10 --warmup 2;;
     bench) step bench 900 python bench.py --steps 30 --warmup 3;;

@@ -1,0 +1,87 @@
+"""Summarise rocprofv3 --pmc passes (csv output) per kernel into one markdown table.
+
+usage: pmc_summary.py <title> <pass dir> [<pass dir> ...]
+
+Each pass directory holds the csv files of one `rocprofv3 --pmc ... --kernel-trace
+--output-format csv` run. Counter values are averaged per dispatch of a kernel and
+joined with the mean dispatch duration of the same run. Derived columns:
+  HBM GB/s   (2 x FETCH_SIZE + WRITE_SIZE) / duration; FETCH_SIZE is doubled because on
+             gfx950 it reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md,
+             HBM) -- an upper estimate for narrower access patterns
+  L2 hit %   TCC_HIT / (TCC_HIT + TCC_MISS)
+  LDS confl  SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (extra LDS cycles per LDS instruction)
+  wait %     SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
+  issue %    SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (waves stalled issuing)
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def _short(name):
+    for pre in ("lgap::device::(anonymous namespace)::", "(anonymous namespace)::", "lgap::device::", "void "):
+        name = name.replace(pre, "")
+    return name.split("(")[0].strip()
+
+
+def load(dirpath):
+    counters = defaultdict(lambda: defaultdict(list))
+    durations = defaultdict(list)
+    for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
+        per_dispatch = defaultdict(lambda: defaultdict(float))
+        names = {}
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                d = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                names[d] = _short(row["Kernel_Name"])
+                per_dispatch[d][row["Counter_Name"]] += float(row["Counter_Value"])
+        for d, cs in per_dispatch.items():
+            for c, v in cs.items():
+                counters[names[d]][c].append(v)
+    for f in glob.glob(os.path.join(dirpath, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                durations[_short(row["Kernel_Name"])].append(
+                    (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1000.0)
+    return counters, durations
+
+
+def main():
+    title, dirs = sys.argv[1], sys.argv[2:]
+    merged = defaultdict(dict)
+    dur = defaultdict(list)
+    for d in dirs:
+        cs, ds = load(d)
+        for k, m in cs.items():
+            for c, vals in m.items():
+                merged[k][c] = sum(vals) / len(vals)
+        for k, v in ds.items():
+            dur[k].extend(v)
+    print(f"# {title}\n")
+    print("Per-dispatch means over the profiled run(s): " + ", ".join(f"`{d}`" for d in dirs) + "\n")
+    cols = ["calls", "avg us", "FETCH KB", "WRITE KB", "HBM GB/s", "L2 hit %", "LDS confl", "wait %", "issue %"]
+    print("| kernel | " + " | ".join(cols) + " |")
+    print("|---|" + "---:|" * len(cols))
+    rows = []
+    for k in merged:
+        m = merged[k]
+        t = sum(dur[k]) / len(dur[k]) if dur.get(k) else float("nan")
+        fetch, write = m.get("FETCH_SIZE", float("nan")), m.get("WRITE_SIZE", float("nan"))
+        bw = (2 * fetch + write) * 1024 / (t * 1e-6) / 1e9 if t == t and t > 0 else float("nan")
+        hit, miss = m.get("TCC_HIT_sum", float("nan")), m.get("TCC_MISS_sum", float("nan"))
+        l2 = 100.0 * hit / (hit + miss) if hit + miss > 0 else float("nan")
+        lds = m.get("SQ_ACTIVE_INST_LDS", 0.0)
+        confl = m.get("SQ_LDS_BANK_CONFLICT", float("nan")) / lds if lds > 0 else float("nan")
+        cyc = m.get("SQ_WAVE_CYCLES", 0.0)
+        wait = 100.0 * m.get("SQ_WAIT_ANY", float("nan")) / cyc if cyc > 0 else float("nan")
+        issue = 100.0 * m.get("SQ_WAIT_INST_ANY", float("nan")) / cyc if cyc > 0 else float("nan")
+        rows.append((t * len(dur.get(k, [])), k, [len(dur.get(k, [])), t, fetch, write, bw, l2, confl, wait, issue]))
+    for _, k, v in sorted(rows, key=lambda r: -r[0] if r[0] == r[0] else 0):
+        cells = [str(v[0])] + [("%.1f" % x) if x == x else "-" for x in v[1:]]
+        print(f"| `{k}` | " + " | ".join(cells) + " |")
+
+
+if __name__ == "__main__":
+    main()

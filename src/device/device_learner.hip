@@ -78,6 +78,10 @@ constexpr int kPartThreads = 256;
 constexpr int kPartIters = 16;  // rows per thread of the two-kernel partition (k_part_count / k_part_scatter)
 constexpr int kTileRows = kPartThreads * kPartIters;
 constexpr int kScanWaves = 4;
+#ifndef LGAP_SCAN_K
+#define LGAP_SCAN_K 4
+#endif
+constexpr int kScanK = LGAP_SCAN_K;  // consecutive bins per lane in the numerical threshold scan
 #ifndef LGAP_SCAN_FOLD
 #define LGAP_SCAN_FOLD 1  // 1: half-wave row streams, one value per lane; 2: quarter-wave streams, value pairs
 #endif
@@ -154,6 +158,7 @@ struct Args {
   unsigned* xcnt;       // local arrival counters of the exchanges [4]
   unsigned xsession;    // high word of the exchange tags (new per learner state)
   unsigned long long xtimeout;  // bound of an exchange wait (wall_clock64 ticks, 100 MHz)
+  int xfault;           // LGAP_XGMI_FAULT=1: never signal (failure-detection tests)
   SplitParams sp;
 };
 
@@ -719,7 +724,7 @@ __device__ void XArriveAndExchange(const Args& a, int kind, unsigned long long t
     if (atomicAdd(&a.xcnt[kind], 1u) == nb - 1u) {
       atomicExch(&a.xcnt[kind], 0u);  // every block of this launch has arrived
       __threadfence_system();
-      for (int q = 0; q < a.P; ++q) {
+      for (int q = 0; q < a.P && !(a.xfault && a.xsession > 0); ++q) {
         __hip_atomic_store(XFlag(a, q, kind, a.rank), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       XWaitAll(a, kind, tag);
@@ -791,11 +796,14 @@ __global__ __launch_bounds__(64) void k_x_root(Args a) {
 
 // Transport self-test (run once when the exchange is set up): `rounds` exchanges of a
 // known pattern through the histogram rows; counts mismatching values into err[0].
+// Rounds alternate between the two halves of the rows (nvals <= bbin): a rank that has
+// finished round r may already push round r + 1 while a peer still checks round r.
 __global__ __launch_bounds__(256) void k_x_selftest(Args a, int round, int nvals, unsigned* err) {
   const int V2 = 2 * a.bbin;
+  const int half = (round & 1) * nvals;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
     for (int q = 0; q < a.P; ++q) {
-      reinterpret_cast<float*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + i] =
+      reinterpret_cast<float*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + half + i] =
           static_cast<float>(a.rank * 131 + round * 7 + (i & 1023));
     }
   }
@@ -804,11 +812,12 @@ __global__ __launch_bounds__(256) void k_x_selftest(Args a, int round, int nvals
 
 __global__ __launch_bounds__(256) void k_x_selfcheck(Args a, int round, int nvals, unsigned* err) {
   const int V2 = 2 * a.bbin;
+  const int half = (round & 1) * nvals;
   const float* rows = reinterpret_cast<const float*>(a.xp->base[a.rank] + a.x_off_hist);
   unsigned bad = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
     for (int q = 0; q < a.P; ++q) {
-      bad += rows[static_cast<size_t>(q) * V2 + i] != static_cast<float>(q * 131 + round * 7 + (i & 1023)) ? 1u : 0u;
+      bad += rows[static_cast<size_t>(q) * V2 + half + i] != static_cast<float>(q * 131 + round * 7 + (i & 1023)) ? 1u : 0u;
     }
   }
   if (bad) atomicAdd(err, bad);
@@ -869,6 +878,13 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
   const int top = nb - 1 - (na ? 1 : 0);
   const bool use_rand = p.extra_trees != 0;
   const int8_t mono = fi.monotone;
+  // Each lane owns kScanK consecutive positions of a 64 * kScanK chunk: a serial
+  // prefix over its own bins, ONE wave scan of the lane totals per chunk, then the
+  // kScanK thresholds are evaluated independently (one 256-bin chunk covers max_bin
+  // 255: one wave scan per pass instead of four). Position order = scan order; within
+  // a lane the first (strict >) best is kept, across lanes WaveBest applies the same
+  // tie rule, so the winner is the scan's first maximum as in the host scan.
+  constexpr int K = kScanK;
   Cand rb;
   rb.gain = kMinScore;
   rb.thr = -1;
@@ -877,39 +893,67 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
   bool sp = false;
   double cg = 0.0, ch = 0.0;
   int cc = 0;
-  for (int base = nb - 1; base >= 0; base -= 64) {
-    const int b = base - lane;
-    double g = 0.0, h = 0.0;
-    int c = 0;
-    if (b >= 0 && !(skip_def && b == fi.default_bin) && !(na && b == nb - 1)) {
-      g = H[2 * b];
-      h = H[2 * b + 1];
-      c = RoundCount(h * cnt_factor);
+  // An empty bin leaves the prefix unchanged: the threshold after it has the same partition
+  // and gain as the one before, and the host scan keeps the first of such exact ties. The
+  // parallel prefix may round the two positions differently, so empty-bin positions after
+  // the first evaluated one are skipped (the host rule, independent of summation order).
+  const int first_rev = (skip_def && top == fi.default_bin) ? top - 1 : top;
+  const int first_fwd = (skip_def && fi.default_bin == 0) ? 1 : 0;
+  // reverse pass: position i <-> bin nb - 1 - i (the right side grows from the top bin)
+  for (int base = 0; base < nb; base += 64 * K) {
+    double pg[K], ph[K];
+    int pc[K];
+    bool empty[K];
+    double tg = 0.0, th = 0.0;
+    int tc = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int b = nb - 1 - (base + lane * K + k);
+      double g = 0.0, h = 0.0;
+      int c = 0;
+      if (b >= 0 && !(skip_def && b == fi.default_bin) && !(na && b == nb - 1)) {
+        g = H[2 * b];
+        h = H[2 * b + 1];
+        c = RoundCount(h * cnt_factor);
+      }
+      empty[k] = g == 0.0 && h == 0.0;
+      tg += g;
+      th += h;
+      tc += c;
+      pg[k] = tg;
+      ph[k] = th;
+      pc[k] = tc;
     }
-    const double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
-    const int sci = WaveInclusiveScan(c);
-    const double rg = cg + sgi, rh_raw = ch + shi;
-    const int rc = cc + sci;
-    cg += __shfl(sgi, 63, kWave);
-    ch += __shfl(shi, 63, kWave);
-    cc += __shfl(sci, 63, kWave);
-    if (b >= 1 && b <= top && !(skip_def && b == fi.default_bin)) {
-      const int thr = b - 1;
-      const double rh = kEpsilon + rh_raw;
-      const int lc = n - rc;
-      const double lh = sum_h - rh;
-      if (rc >= p.min_data_in_leaf && rh >= p.min_sum_hessian_in_leaf && lc >= p.min_data_in_leaf &&
-          lh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
-        const double lg = sg - rg;
-        const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
-        if (gain > shift) {
-          sp = true;
-          if (gain > rb.gain) {
-            rb.gain = gain;
-            rb.thr = thr;
-            rb.lg = lg;
-            rb.lh = lh;
-            rb.lc = lc;
+    const double ig = WaveInclusiveScan(tg), ih = WaveInclusiveScan(th);
+    const int ic = WaveInclusiveScan(tc);
+    const double eg = cg + ig - tg, eh = ch + ih - th;
+    const int ec = cc + ic - tc;
+    cg += __shfl(ig, 63, kWave);
+    ch += __shfl(ih, 63, kWave);
+    cc += __shfl(ic, 63, kWave);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int b = nb - 1 - (base + lane * K + k);
+      if (b >= 1 && b <= top && !(skip_def && b == fi.default_bin) && !(b < first_rev && empty[k])) {
+        const int thr = b - 1;
+        const double rg = eg + pg[k];
+        const double rh = kEpsilon + eh + ph[k];
+        const int rc = ec + pc[k];
+        const int lc = n - rc;
+        const double lh = sum_h - rh;
+        if (rc >= p.min_data_in_leaf && rh >= p.min_sum_hessian_in_leaf && lc >= p.min_data_in_leaf &&
+            lh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
+          const double lg = sg - rg;
+          const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
+          if (gain > shift) {
+            sp = true;
+            if (gain > rb.gain) {
+              rb.gain = gain;
+              rb.thr = thr;
+              rb.lg = lg;
+              rb.lh = lh;
+              rb.lc = lc;
+            }
           }
         }
       }
@@ -921,41 +965,63 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
   fb.lg = fb.lh = 0.0;
   fb.lc = 0;
   if (two_dir) {
+    // forward pass: position i <-> bin i (the left side grows from bin 0)
     cg = ch = 0.0;
     cc = 0;
-    for (int base = 0; base < nb; base += 64) {
-      const int b = base + lane;
-      double g = 0.0, h = 0.0;
-      int c = 0;
-      if (b < nb && !(skip_def && b == fi.default_bin)) {
-        g = H[2 * b];
-        h = H[2 * b + 1];
-        c = RoundCount(h * cnt_factor);
+    for (int base = 0; base < nb; base += 64 * K) {
+      double pg[K], ph[K];
+      int pc[K];
+      bool empty[K];
+      double tg = 0.0, th = 0.0;
+      int tc = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int b = base + lane * K + k;
+        double g = 0.0, h = 0.0;
+        int c = 0;
+        if (b < nb && !(skip_def && b == fi.default_bin)) {
+          g = H[2 * b];
+          h = H[2 * b + 1];
+          c = RoundCount(h * cnt_factor);
+        }
+        empty[k] = g == 0.0 && h == 0.0;
+        tg += g;
+        th += h;
+        tc += c;
+        pg[k] = tg;
+        ph[k] = th;
+        pc[k] = tc;
       }
-      const double sgi = WaveInclusiveScan(g), shi = WaveInclusiveScan(h);
-      const int sci = WaveInclusiveScan(c);
-      const double lg = cg + sgi, lh_raw = ch + shi;
-      const int lc = cc + sci;
-      cg += __shfl(sgi, 63, kWave);
-      ch += __shfl(shi, 63, kWave);
-      cc += __shfl(sci, 63, kWave);
-      if (b <= nb - 2 && !(skip_def && b == fi.default_bin)) {
-        const int thr = b;
-        const double lh = kEpsilon + lh_raw;
-        const int rc = n - lc;
-        const double rh = sum_h - lh;
-        if (lc >= p.min_data_in_leaf && lh >= p.min_sum_hessian_in_leaf && rc >= p.min_data_in_leaf &&
-            rh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
-          const double rg = sg - lg;
-          const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
-          if (gain > shift) {
-            sp = true;
-            if (gain > fb.gain) {
-              fb.gain = gain;
-              fb.thr = thr;
-              fb.lg = lg;
-              fb.lh = lh;
-              fb.lc = lc;
+      const double ig = WaveInclusiveScan(tg), ih = WaveInclusiveScan(th);
+      const int ic = WaveInclusiveScan(tc);
+      const double eg = cg + ig - tg, eh = ch + ih - th;
+      const int ec = cc + ic - tc;
+      cg += __shfl(ig, 63, kWave);
+      ch += __shfl(ih, 63, kWave);
+      cc += __shfl(ic, 63, kWave);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int b = base + lane * K + k;
+        if (b <= nb - 2 && !(skip_def && b == fi.default_bin) && !(b > first_fwd && empty[k])) {
+          const int thr = b;
+          const double lg = eg + pg[k];
+          const double lh = kEpsilon + eh + ph[k];
+          const int lc = ec + pc[k];
+          const int rc = n - lc;
+          const double rh = sum_h - lh;
+          if (lc >= p.min_data_in_leaf && lh >= p.min_sum_hessian_in_leaf && rc >= p.min_data_in_leaf &&
+              rh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
+            const double rg = sg - lg;
+            const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
+            if (gain > shift) {
+              sp = true;
+              if (gain > fb.gain) {
+                fb.gain = gain;
+                fb.thr = thr;
+                fb.lg = lg;
+                fb.lh = lh;
+                fb.lc = lc;
+              }
             }
           }
         }
@@ -2290,8 +2356,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.xtimeout = static_cast<unsigned long long>(100e6 * std::min(30.0, std::max(1.0, saved / 100e6)));
     DevBuf<unsigned> err(1);
     err.Zero(stream_);
-    const int nvals = std::min(2 * bbin_, 4096);
-    for (int round = 0; round < 3; ++round) {
+    const int nvals = std::min(bbin_, 2048);
+    for (int round = 0; round < 4; ++round) {
       k_x_selftest<<<4, 256, 0, stream_>>>(a, round, nvals, err.get());
       k_x_selfcheck<<<4, 256, 0, stream_>>>(a, round, nvals, err.get());
     }
@@ -3364,6 +3430,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.xcnt = xcnt_.get();
     a.xsession = xsession_;
     a.xtimeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
+    a.xfault = std::getenv("LGAP_XGMI_FAULT") != nullptr && std::getenv("LGAP_XGMI_FAULT")[0] == '1';
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;

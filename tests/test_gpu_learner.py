@@ -126,10 +126,11 @@ def test_lambdarank_targets_on_device(lgb, gpu_required, rng, target):
     bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y, group=sizes), 3)
     bg = lgb.train({**params, "device_type": "gpu"}, lgb.Dataset(X, y, group=sizes), 3)
     pc, pg = bc.predict(X, raw_score=True), bg.predict(X, raw_score=True)
-    assert np.corrcoef(pc, pg)[0, 1] > 0.999
-    # lambdas accumulate in a different order on the device: a rare near-tie split may flip
-    close = np.isclose(pg, pc, rtol=5e-3, atol=5e-3)
-    assert close.mean() > 0.995, close.mean()
+    # exact ties (empty bins) are broken as on the host; what remains is a rare near-tie (gains
+    # ~1e-7 apart) flipped by 1-ulp float differences of the device lambdas
+    # (test_gpu_kernels.py pins the gradients of all 18 targets against torch)
+    assert np.corrcoef(pc, pg)[0, 1] > 0.9999
+    assert np.mean(np.abs(pc - pg)) < 1e-3 * np.mean(np.abs(pc)), (np.mean(np.abs(pc - pg)), np.mean(np.abs(pc)))
 
 
 def test_bagging_goss_feature_fraction_on_device(lgb, gpu_required):
@@ -336,12 +337,34 @@ def test_collective_watchdog_aborts_on_timeout(lgb, gpu_required):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LGAP_DP_TRANSPORT="collective")
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "watchdog_selftest.py")], capture_output=True,
+                       env=env,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["raised"], res
     assert "communicator aborted" in res["message"], res
+
+
+def test_xgmi_exchange_timeout_raises(lgb, gpu_required):
+    """xGMI transport failure detection: a rank that stops signalling (LGAP_XGMI_FAULT=1 drops
+    every flag after the set-up self-test) makes the in-kernel exchange wait run into its bound;
+    the learner raises instead of hanging the GPU."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LGAP_DP_TRANSPORT="xgmi", LGAP_XGMI_FAULT="1", LGAP_XGMI_TIMEOUT_S="0.5",
+               LGAP_COMM_TIMEOUT_S="120")
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "watchdog_selftest.py")], capture_output=True,
+                       env=env, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["raised"], res
+    assert "xGMI exchange" in res["message"] and "timed out" in res["message"], res
 
 
 def test_device_bagging_by_query_matches_host(lgb, gpu_required):
