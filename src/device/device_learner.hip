@@ -79,7 +79,7 @@ constexpr int kPartIters = 16;  // rows per thread of the two-kernel partition (
 constexpr int kTileRows = kPartThreads * kPartIters;
 constexpr int kScanWaves = 4;
 #ifndef LGAP_SCAN_K
-#define LGAP_SCAN_K 4
+#define LGAP_SCAN_K 2
 #endif
 constexpr int kScanK = LGAP_SCAN_K;  // consecutive bins per lane in the numerical threshold scan
 #ifndef LGAP_SCAN_FOLD
@@ -833,28 +833,13 @@ struct Cand {
 
 // wave argmax; prefer_high: ties go to the larger threshold
 __device__ __forceinline__ Cand WaveBest(Cand c, bool prefer_high) {
-  int src = threadIdx.x & 63;
-  double bg = c.gain;
-  int bt = c.thr;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double og = __shfl_xor(bg, o, kWave);
-    const int ot = __shfl_xor(bt, o, kWave);
-    const int os = __shfl_xor(src, o, kWave);
-    bool take = og > bg;
-    if (og == bg) take = prefer_high ? (ot > bt) : (ot < bt);
-    if (take) {
-      bg = og;
-      bt = ot;
-      src = os;
-    }
-  }
+  const int src = WaveArgBestLane(c.gain, prefer_high ? -c.thr : c.thr, 0);
   Cand r;
-  r.gain = bg;
-  r.thr = bt;
-  r.lg = __shfl(c.lg, src, kWave);
-  r.lh = __shfl(c.lh, src, kWave);
-  r.lc = __shfl(c.lc, src, kWave);
+  r.gain = ReadLane(c.gain, src);
+  r.thr = ReadLane(c.thr, src);
+  r.lg = ReadLane(c.lg, src);
+  r.lh = ReadLane(c.lh, src);
+  r.lc = ReadLane(c.lc, src);
   return r;
 }
 
@@ -924,13 +909,13 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
       ph[k] = th;
       pc[k] = tc;
     }
-    const double ig = WaveInclusiveScan(tg), ih = WaveInclusiveScan(th);
-    const int ic = WaveInclusiveScan(tc);
+    const double ig = WaveInclusiveSumDpp(tg), ih = WaveInclusiveSumDpp(th);
+    const int ic = WaveInclusiveSumDpp(tc);
     const double eg = cg + ig - tg, eh = ch + ih - th;
     const int ec = cc + ic - tc;
-    cg += __shfl(ig, 63, kWave);
-    ch += __shfl(ih, 63, kWave);
-    cc += __shfl(ic, 63, kWave);
+    cg += ReadLane(ig, 63);
+    ch += ReadLane(ih, 63);
+    cc += ReadLane(ic, 63);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int b = nb - 1 - (base + lane * K + k);
@@ -959,6 +944,7 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
       }
     }
   }
+  Stamp(a, 3, 5);
   Cand fb;
   fb.gain = kMinScore;
   fb.thr = 0x7fffffff;
@@ -992,13 +978,13 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
         ph[k] = th;
         pc[k] = tc;
       }
-      const double ig = WaveInclusiveScan(tg), ih = WaveInclusiveScan(th);
-      const int ic = WaveInclusiveScan(tc);
+      const double ig = WaveInclusiveSumDpp(tg), ih = WaveInclusiveSumDpp(th);
+      const int ic = WaveInclusiveSumDpp(tc);
       const double eg = cg + ig - tg, eh = ch + ih - th;
       const int ec = cc + ic - tc;
-      cg += __shfl(ig, 63, kWave);
-      ch += __shfl(ih, 63, kWave);
-      cc += __shfl(ic, 63, kWave);
+      cg += ReadLane(ig, 63);
+      ch += ReadLane(ih, 63);
+      cc += ReadLane(ic, 63);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int b = base + lane * K + k;
@@ -1028,6 +1014,7 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
       }
     }
   }
+  Stamp(a, 3, 6);
   const bool any = __any(sp) != 0;
   const Cand r = WaveBest(rb, true);
   const Cand f = two_dir ? WaveBest(fb, false) : fb;
@@ -1104,10 +1091,44 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     a.lout[0] = LeafOutputRaw(a.lsum[0].x, a.lsum[0].y, p0, a.gcount[0], 0.0);
   }
   if (f >= 0) {
+    // Loads that do not depend on the histogram are issued first so their latency hides
+    // under the fold: slots of the two children, the parent (larger child's slot) values
+    // this thread subtracts, the leaf statistics the scanning waves read (held by lane 0
+    // of waves 0 / 1 until used) and the feature masks.
+    const int s_slot = a.slot[c.smaller];
+    const int l_slot = c.larger >= 0 ? a.slot[c.larger] : -1;
     const DevFeature fi = a.feat[f];
     const int nbin = fi.num_bin;
     const int nst = nbin - 1;
     const int nv = 2 * nst;  // stored values of this feature
+    const size_t slot_stride = 2 * static_cast<size_t>(a.TB);
+    const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
+    double* gs = a.slots + s_slot * slot_stride + v0;
+    double* gl = l_slot >= 0 ? a.slots + l_slot * slot_stride + v0 : nullptr;
+    constexpr int kPre = 2;  // parent values per thread held in registers (nv <= kPre * blockDim)
+    double parent[kPre];
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int v = t + k * kScanThreads;
+      parent[k] = (gl && v < nv) ? gl[v] : 0.0;
+    }
+    const int my_leaf = (w == 0) ? c.smaller : (w == 1 ? c.larger : -1);
+    double2 pre_sum = make_double2(0.0, 0.0);
+    int pre_n = 0, pre_depth = 0;
+    double pre_out = 0.0;
+    LeafBounds pre_bounds;
+    if (lane == 0 && my_leaf >= 0) {
+      pre_sum = a.lsum[my_leaf];
+      pre_n = a.gcount[my_leaf];
+      pre_out = a.lout[my_leaf];
+      pre_bounds = a.bounds[my_leaf];
+      pre_depth = a.depth[my_leaf];
+    }
+    int pre_used = 1, pre_spl = 1;
+    if (t == 0) {
+      pre_used = a.used_bytree[f];
+      pre_spl = c.larger >= 0 ? a.splittable[static_cast<size_t>(s_slot) * a.F + f] : 1;
+    }
     double* hs_full = reinterpret_cast<double*>(smem);                 // 2 * nbin: smaller child, full
     double* hl_full = hs_full + 2 * a.max_bin;                          // 2 * nbin: larger child, full
     double* part = hl_full + 2 * a.max_bin;                             // [16][64]
@@ -1182,26 +1203,25 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     __syncthreads();
     Stamp(a, 3, 1);
     // 2. slots: smaller <- reduced; larger <- parent - smaller
-    const size_t slot_stride = 2 * static_cast<size_t>(a.TB);
-    const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
-    const int s_slot = a.slot[c.smaller];
-    const int l_slot = c.larger >= 0 ? a.slot[c.larger] : -1;
-    double* gs = a.slots + s_slot * slot_stride + v0;
-    double* gl = l_slot >= 0 ? a.slots + l_slot * slot_stride + v0 : nullptr;
-    for (int v = t; v < nv; v += blockDim.x) {
+    auto slot_update = [&](int v, double pv) {
       const int k = v >> 1;
       const int b = k < fi.mfb ? k : k + 1;
       const double sv = hs_full[2 * b + (v & 1)];
       gs[v] = sv;
       if (gl) {
-        const double lv = gl[v] - sv;
+        const double lv = pv - sv;
         gl[v] = lv;
         hl_full[2 * b + (v & 1)] = lv;
       }
+    };
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int v = t + k * kScanThreads;
+      if (v < nv) slot_update(v, parent[k]);
     }
+    for (int v = t + kPre * kScanThreads; v < nv; v += kScanThreads) slot_update(v, gl ? gl[v] : 0.0);
     if (t == 0) {
-      const bool skip_both =
-          !a.used_bytree[f] || (c.larger >= 0 && !a.splittable[static_cast<size_t>(s_slot) * a.F + f]);
+      const bool skip_both = !pre_used || !pre_spl;
       s_skip_both = skip_both ? 1 : 0;
       // extra-trees draws in the host learner's order: smaller leaf first, then larger
       s_rand[0] = s_rand[1] = 0;
@@ -1225,7 +1245,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
         }
         sgs = WaveSum(sgs);
         shs = WaveSum(shs);
-        const double2 sums = a.lsum[leaf];
+        const double2 sums = pre_sum;  // lane 0's prefetched leaf sums (only lane 0 uses them)
         if (lane == 0) {
           H[2 * fi.mfb] = sums.x - sgs;
           H[2 * fi.mfb + 1] = sums.y - shs;
@@ -1244,17 +1264,19 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
         const double* H = sel ? hl_full : hs_full;
         const int lslot = sel ? l_slot : s_slot;
         const double sg = s_sum[sel][0], sh = s_sum[sel][1];
-        const int n = a.gcount[leaf];
+        const int n = __shfl(pre_n, 0, kWave);
         double po;
         if (c.num_leaves == 1) {
           SplitParams p0 = a.sp;
           p0.path_smooth = 0.0;
           po = LeafOutputRaw(sg, sh, p0, n, 0.0);
         } else {
-          po = a.lout[leaf];
+          po = __shfl(pre_out, 0, kWave);
         }
-        const LeafBounds bounds = a.bounds[leaf];
-        const int depth = a.depth[leaf];
+        LeafBounds bounds;
+        bounds.min = __shfl(pre_bounds.min, 0, kWave);
+        bounds.max = __shfl(pre_bounds.max, 0, kWave);
+        const int depth = __shfl(pre_depth, 0, kWave);
         bool sp;
         if (fi.bin_type == 0) {
           sp = ScanNumericalWave(a, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
@@ -1419,19 +1441,11 @@ __device__ void FillSplitDesc(const Args& a, const SplitInfo& s, SplitDesc* d) {
 }
 
 __device__ __forceinline__ void WaveArgBest4(double* g, int* f, int* l, int* o) {
-#pragma unroll
-  for (int s = 32; s > 0; s >>= 1) {
-    const double og = __shfl_xor(*g, s, kWave);
-    const int of = __shfl_xor(*f, s, kWave);
-    const int ol = __shfl_xor(*l, s, kWave);
-    const int oo = __shfl_xor(*o, s, kWave);
-    if (CandBetter(og, of, ol, *g, *f, *l)) {
-      *g = og;
-      *f = of;
-      *l = ol;
-      *o = oo;
-    }
-  }
+  const int src = WaveArgBestLane(*g, *f, *l);
+  *g = ReadLane(*g, src);
+  *f = ReadLane(*f, src);
+  *l = ReadLane(*l, src);
+  *o = ReadLane(*o, src);
 }
 
 struct SelOut {
@@ -1452,7 +1466,7 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
   double g3[3] = {kMinScore, kMinScore, kMinScore};
   int f3[3] = {kNone, kNone, kNone};
   int l3[3] = {0, 0, kNone};
-  SplitKey k3[3];
+  SplitKey k3_0, k3_1, k3_2;  // (named: a runtime-indexed array would live in scratch)
   if (!c.skip) {
     // the two children's candidates: every position of the table (all ranks' blocks)
     const int np = a.P * a.Fmax;
@@ -1466,7 +1480,8 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
         if (k.feature >= 0 && CandBetter(k.gain, k.feature, 0, g3[sel], f3[sel], 0)) {
           g3[sel] = k.gain;
           f3[sel] = k.feature;
-          k3[sel] = k;
+          if (sel == 0) k3_0 = k;
+          else k3_1 = k;
         }
       }
     }
@@ -1480,10 +1495,11 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
       g3[2] = g;
       f3[2] = f;
       l3[2] = l;
-      k3[2] = k;
+      k3_2 = k;
     }
   }
   if (t <= c.num_leaves && t < kPartThreads) s_rng[t] = a.range[t];
+  Stamp(a, 0, 4);
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     int o = t;
@@ -1496,6 +1512,7 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
     }
   }
   __syncthreads();
+  Stamp(a, 0, 5);
   if (t == 0) {
     for (int k = 0; k < 3; ++k) {
       for (int i = 1; i < kW; ++i) {
@@ -1531,16 +1548,16 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
   }
   __syncthreads();
   if (t == s_owner[0]) {
-    so->key[0] = k3[0];
-    so->st.new_best[0] = k3[0].pos;
+    so->key[0] = k3_0;
+    so->st.new_best[0] = k3_0.pos;
   }
   if (t == s_owner[1]) {
-    so->key[1] = k3[1];
-    so->st.new_best[1] = k3[1].pos;
+    so->key[1] = k3_1;
+    so->st.new_best[1] = k3_1.pos;
   }
   const int wc = s_win_cat;
   if (wc >= 0 && t == s_owner[wc]) {
-    const SplitKey& k = k3[wc];
+    const SplitKey k = wc == 0 ? k3_0 : (wc == 1 ? k3_1 : k3_2);
     SplitDesc& d = so->d;
     d.group = k.group;
     d.offset = k.offset;
@@ -1558,6 +1575,7 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
     const int leaf = so->st.leaf;
     so->pr = leaf < kPartThreads ? s_rng[leaf] : a.range[leaf];
   }
+  Stamp(a, 0, 6);
   __syncthreads();
 }
 

@@ -24,32 +24,82 @@ namespace device {
 
 constexpr int kWave = 64;
 
-// ---- wave64 primitives
-__device__ __forceinline__ double WaveSum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+// ---- DPP wave64 primitives (gfx9 data-parallel-primitive moves: row_shr:n = 0x110 + n,
+// row_bcast:15 = 0x142, row_bcast:31 = 0x143). A DPP move is a VALU operand modifier:
+// a few cycles per step instead of a ds_bpermute round trip through the LDS crossbar.
+template <int kCtrl>
+__device__ __forceinline__ int DppMove(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xf, 0xf, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ float DppMove(float v) {
+  return __int_as_float(DppMove<kCtrl>(__float_as_int(v)));
+}
+template <int kCtrl>
+__device__ __forceinline__ double DppMove(double v) {
+  const int lo = DppMove<kCtrl>(__double2loint(v));
+  const int hi = DppMove<kCtrl>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double ReadLane(double v, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                          __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+__device__ __forceinline__ int ReadLane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+// Inclusive wave scan with an associative op: Hillis-Steele inside each 16-lane row
+// (row_shr 1, 2, 4, 8), then row 15 -> rows 1 and 3 (row_bcast:15) and lane 31 -> rows 2
+// and 3 (row_bcast:31).
+template <typename T, typename Op>
+__device__ __forceinline__ T WaveScanDpp(T v, Op op) {
+  const int lane = threadIdx.x & 63, rl = lane & 15;
+  T t = DppMove<0x111>(v);
+  if (rl >= 1) v = op(v, t);
+  t = DppMove<0x112>(v);
+  if (rl >= 2) v = op(v, t);
+  t = DppMove<0x114>(v);
+  if (rl >= 4) v = op(v, t);
+  t = DppMove<0x118>(v);
+  if (rl >= 8) v = op(v, t);
+  t = DppMove<0x142>(v);
+  if (lane & 16) v = op(v, t);
+  t = DppMove<0x143>(v);
+  if (lane >= 32) v = op(v, t);
   return v;
 }
+template <typename T>
+__device__ __forceinline__ T WaveInclusiveSumDpp(T v) {
+  return WaveScanDpp(v, [](T x, T y) { return x + y; });
+}
+// wave maximum, the same value in every lane
+__device__ __forceinline__ double WaveMaxDpp(double v) {
+  return ReadLane(WaveScanDpp(v, [](double x, double y) { return x > y ? x : y; }), 63);
+}
+__device__ __forceinline__ int WaveMaxDpp(int v) {
+  return ReadLane(WaveScanDpp(v, [](int x, int y) { return x > y ? x : y; }), 63);
+}
+// Lane of the wave's best (g descending, then x ascending, then y ascending): one DPP
+// max per key and a ballot, the winner's payload is then read with ReadLane.
+__device__ __forceinline__ int WaveArgBestLane(double g, int x, int y) {
+  const double mg = WaveMaxDpp(g);
+  const bool t1 = g == mg;
+  const int mx = -WaveMaxDpp(t1 ? -x : -0x7fffffff - 1);
+  const bool t2 = t1 && x == mx;
+  const int my = -WaveMaxDpp(t2 ? -y : -0x7fffffff - 1);
+  const unsigned long long m = __ballot(t2 && y == my);
+  return m ? __ffsll(static_cast<long long>(m)) - 1 : 0;
+}
+
+// ---- wave64 reductions / scans (on the DPP primitives above)
+__device__ __forceinline__ double WaveSum(double v) { return ReadLane(WaveInclusiveSumDpp(v), 63); }
 __device__ __forceinline__ float WaveSum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+  return __int_as_float(ReadLane(__float_as_int(WaveScanDpp(v, [](float x, float y) { return x + y; })), 63));
 }
-__device__ __forceinline__ int WaveSum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
-}
+__device__ __forceinline__ int WaveSum(int v) { return ReadLane(WaveInclusiveSumDpp(v), 63); }
 // inclusive prefix sum across the 64 lanes
 template <typename T>
 __device__ __forceinline__ T WaveInclusiveScan(T v) {
-  const int lane = threadIdx.x & (kWave - 1);
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    T u = __shfl_up(v, o, kWave);
-    if (lane >= o) v += u;
-  }
-  return v;
+  return WaveInclusiveSumDpp(v);
 }
 
 // ---- owning device buffer
