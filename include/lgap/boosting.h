@@ -176,6 +176,7 @@ class GBDT {
   int label_idx_ = 0;
   data_size_t num_data_ = 0;
   int iter_ = 0;
+  int num_init_models_ = 0;  // leading trees merged from an init model (MergeFrom)
   double shrinkage_rate_ = 0.1;
   bool average_output_ = false;
   bool has_init_score_ = false;

@@ -353,8 +353,18 @@ class Dataset:
                                               ctypes.c_int32(idx.size), _c_str(param_dict_to_str(self.params)),
                                               ctypes.byref(out)))
             self.handle = out
+            # the native subset inherits the reference's init score; a different model needs
+            # the reference's raw rows
+            if self._predictor is not None and self._predictor is not self.reference._predictor:
+                if self.reference.data is None:
+                    raise LightGBMError("Cannot set predictor after freed raw data, "
+                                        "set free_raw_data=False when construct Dataset to avoid this.")
+                self.init_score = self._init_score_from_predictor(self._predictor, self.reference.data,
+                                                                  self.used_indices)
             self._set_metadata()
             return self
+        if self._predictor is not None:  # the continued model's scores replace any init_score
+            self.init_score = self._init_score_from_predictor(self._predictor, self.data)
         self._lazy_init(self.data)
         return self
 
@@ -495,6 +505,7 @@ class Dataset:
                       params=params if params is not None else self.params, free_raw_data=self.free_raw_data)
         ret.used_indices = np.sort(np.asarray(used_indices, dtype=np.int32))
         ret.pandas_categorical = self.pandas_categorical
+        ret._predictor = self._predictor
         return ret
 
     # ------------------------------------------------------------------ fields
@@ -610,6 +621,45 @@ class Dataset:
 
     def set_reference(self, reference: "Dataset") -> "Dataset":
         self.reference = reference
+        # a validation set continues from the same model as its training set
+        if reference is not None and reference._predictor is not None:
+            self._set_predictor(reference._predictor)
+        return self
+
+    # ------------------------------------------------------------------ continued training
+    def _init_score_from_predictor(self, predictor: "Booster", data: Any,
+                                   used_indices: Optional[np.ndarray] = None) -> Optional[np.ndarray]:
+        """Raw scores of ``predictor`` on ``data`` (array / frame / sparse / file path), restricted to
+        ``used_indices`` for a subset (reference basic.py ``_set_init_score_by_predictor``)."""
+        if data is None:
+            return None
+        if _is_path(data):
+            header = str(self.params.get("header", self.params.get("has_header", False))).lower() in ("true", "1")
+            raw = predictor.predict(str(data), raw_score=True, data_has_header=header)
+        else:
+            raw = predictor.predict(data, raw_score=True)
+        raw = np.asarray(raw, dtype=np.float64)
+        if used_indices is not None:
+            raw = raw[np.asarray(used_indices, dtype=np.int64)]
+        return raw
+
+    def _set_predictor(self, predictor: Optional["Booster"]) -> "Dataset":
+        """Attach the model training continues from; its raw scores become this Dataset's init
+        score (now when constructed, else at construction). Reference: basic.py ``_set_predictor``."""
+        if predictor is self._predictor:
+            return self
+        self._predictor = predictor
+        if predictor is None or self.handle is None:
+            return self  # construct() applies it
+        if self.data is not None:
+            self.set_init_score(self._init_score_from_predictor(predictor, self.data))
+        elif self.used_indices is not None and self.reference is not None and self.reference._predictor is predictor:
+            pass  # inherited from the reference at subset construction
+        elif self.used_indices is not None and self.reference is not None and self.reference.data is not None:
+            self.set_init_score(self._init_score_from_predictor(predictor, self.reference.data, self.used_indices))
+        else:
+            raise LightGBMError("Cannot set predictor after freed raw data, "
+                                "set free_raw_data=False when construct Dataset to avoid this.")
         return self
 
     def get_ref_chain(self, ref_limit: int = 100) -> set:
@@ -749,6 +799,10 @@ class Booster:
             self.train_set = train_set
             _check(_LIB.LGBM_BoosterCreate(train_set.handle, _c_str(param_dict_to_str(self.params)),
                                            ctypes.byref(self.handle)))
+            if train_set._predictor is not None:
+                # continued training: the init model's trees go first, its scores are the init score
+                self._init_predictor = train_set._predictor
+                _check(_LIB.LGBM_BoosterMerge(self.handle, self._init_predictor.handle))
             self.pandas_categorical = train_set.pandas_categorical
             self._num_class = self._get_num_class()
         elif model_file is not None:

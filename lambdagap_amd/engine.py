@@ -6,6 +6,7 @@ early stopping, k-fold CV with stratification / group folds).
 from __future__ import annotations
 
 import copy
+import os
 from collections import OrderedDict, defaultdict
 from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple, Union
 
@@ -66,15 +67,11 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
     else:
         predictor = None
     init_iteration = predictor.current_iteration() if predictor is not None else 0
-    if predictor is not None:
-        # continue training from the scores of the existing model
-        if train_set.init_score is None and train_set.data is not None and not isinstance(train_set.data, str):
-            train_set.init_score = predictor.predict(train_set.data, raw_score=True)
+    # continued training: the init model's raw scores become the init score of the training
+    # and validation sets (also for file data / constructed Datasets), and the Booster puts the
+    # init model's trees first (reference engine.py train -> Dataset._set_predictor)
+    train_set._update_params(params)._set_predictor(predictor)
     booster = Booster(params=params, train_set=train_set)
-    if predictor is not None:
-        booster.merge_models_from = predictor  # keep alive
-        from .basic import _LIB, _check
-        _check(_LIB.LGBM_BoosterMerge(booster.handle, predictor.handle))
     valid_sets = valid_sets or []
     names = valid_names or []
     is_valid_contain_train = False
@@ -88,6 +85,7 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
         name = names[i] if i < len(names) else f"valid_{i}"
         if vs.reference is None:
             vs.set_reference(train_set)
+        vs._set_predictor(predictor)
         booster.add_valid(vs, name)
     booster.set_train_data_name(train_data_name)
     callbacks = list(callbacks or [])
@@ -277,7 +275,15 @@ def cv(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100, f
         train_set.feature_name = feature_name
     if categorical_feature != "auto":
         train_set.categorical_feature = categorical_feature
-    train_set._update_params(params)
+    if isinstance(init_model, (str, os.PathLike)):
+        predictor = Booster(model_file=str(init_model))
+    elif isinstance(init_model, Booster):
+        predictor = init_model
+    else:
+        predictor = None
+    # every fold continues from init_model: the full set's init score is the model's raw score,
+    # fold subsets inherit it, and each fold Booster merges the model's trees
+    train_set._update_params(params)._set_predictor(predictor)
     results: Dict[str, List[float]] = defaultdict(list)
     cvfolds = _make_folds(train_set, folds, nfold, params, seed, fpreproc, stratified, shuffle, eval_train_metric)
     callbacks = list(callbacks or [])

@@ -95,8 +95,9 @@ void GBDT::AddValidDataset(const Dataset* valid, const std::vector<const Metric*
   std::vector<double> s(total, 0.0);
   const auto& md = valid->metadata();
   if (md.init_score() != nullptr && md.init_score_size() == total) std::copy(md.init_score(), md.init_score() + total, s.begin());
-  // existing models (continued training / added mid-training)
-  for (size_t i = 0; i < models_.size(); ++i) {
+  // models trained by this booster before the set was added; merged init-model trees reach
+  // the set through its init score (reference gbdt.cpp AddValidDataset loops over iter_ only)
+  for (size_t i = static_cast<size_t>(num_init_models_); i < models_.size(); ++i) {
     const int k = static_cast<int>(i % num_tree_per_iteration_);
     models_[i]->AddPredictionToScore(*valid, valid->num_data(), s.data() + static_cast<size_t>(k) * valid->num_data());
   }
@@ -503,6 +504,7 @@ void GBDT::MergeFrom(const GBDT* other) {
   for (auto& t : other->models_) merged.push_back(std::make_unique<Tree>(*t));
   for (auto& t : models_) merged.push_back(std::move(t));
   models_ = std::move(merged);
+  num_init_models_ += static_cast<int>(other->models_.size());
 }
 
 void GBDT::ShuffleModels(int start_iter, int end_iter) {

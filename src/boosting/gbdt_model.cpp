@@ -123,7 +123,8 @@ std::vector<double> GBDT::FeatureImportance(int num_iteration, int importance_ty
   for (int i = 0; i < used; ++i) {
     const Tree* t = models_[i].get();
     for (int n = 0; n < t->num_leaves() - 1; ++n) {
-      if (t->split_gain(n) > 0 || importance_type == 0) {
+      // only splits that gained count, for both types (reference gbdt_model_text.cpp:635-653)
+      if (t->split_gain(n) > 0) {
         if (importance_type == 0) imp[t->split_feature(n)] += 1.0;
         else imp[t->split_feature(n)] += t->split_gain(n);
       }

@@ -1,6 +1,7 @@
 // LGBM_* C ABI (reference: src/c_api.cpp:47-3000). The Booster wrapper guards
 // training with a unique lock and prediction / evaluation with a shared lock
 // (c_api.cpp:54-58). Exceptions become -1 + LGBM_GetLastError.
+#include "lgap/omp_errors.h"
 #include "lgap/c_api.h"
 
 #include <omp.h>
@@ -230,22 +231,26 @@ void PredictRows(Booster* b, const RowSource& src, int predict_type, int start_i
     else if (g->objective() && std::string(g->objective()->GetName()).find("multiclass") == 0) es_type = "multiclass";
   }
   PredictionEarlyStop es(es_type, pc.pred_early_stop_freq, pc.pred_early_stop_margin);
+  OmpErrors errs;  // a failing row source (Arrow / Python callback) must return -1, not abort
 #pragma omp parallel
   {
     std::vector<double> x(nf);
     std::vector<std::pair<int, double>> row;
 #pragma omp for schedule(static)
     for (data_size_t i = 0; i < n; ++i) {
-      src.GetRow(i, &row);
-      std::fill(x.begin(), x.end(), 0.0);
-      for (auto& kv : row) if (kv.first < nf) x[kv.first] = kv.second;
-      double* o = out + static_cast<size_t>(i) * per_row;
-      if (leaf) g->PredictLeafIndex(x.data(), o);
-      else if (contrib) g->PredictContrib(x.data(), o);
-      else if (raw) g->PredictRaw(x.data(), o, &es);
-      else g->Predict(x.data(), o, &es);
+      errs.Run([&] {
+        src.GetRow(i, &row);
+        std::fill(x.begin(), x.end(), 0.0);
+        for (auto& kv : row) if (kv.first < nf) x[kv.first] = kv.second;
+        double* o = out + static_cast<size_t>(i) * per_row;
+        if (leaf) g->PredictLeafIndex(x.data(), o);
+        else if (contrib) g->PredictContrib(x.data(), o);
+        else if (raw) g->PredictRaw(x.data(), o, &es);
+        else g->Predict(x.data(), o, &es);
+      });
     }
   }
+  errs.Rethrow();
   *out_len = static_cast<int64_t>(n) * per_row;
 }
 

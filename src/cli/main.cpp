@@ -11,6 +11,7 @@
 #include <sstream>
 #include <vector>
 
+#include "lgap/omp_errors.h"
 #include "lgap/boosting.h"
 #include "lgap/common.h"
 #include "lgap/config.h"
@@ -80,20 +81,24 @@ void Predict(const Config& c) {
   const int nf = std::max(boosting->MaxFeatureIdx() + 1, rows.ncol);
   std::vector<double> out(rows.rows.size() * static_cast<size_t>(per));
   PredictionEarlyStop es(c.pred_early_stop ? "binary" : "none", c.pred_early_stop_freq, c.pred_early_stop_margin);
+  OmpErrors errs;
 #pragma omp parallel
   {
     std::vector<double> x(nf);
 #pragma omp for schedule(static)
     for (size_t i = 0; i < rows.rows.size(); ++i) {
-      std::fill(x.begin(), x.end(), 0.0);
-      for (auto& kv : rows.rows[i]) if (kv.first < nf) x[kv.first] = kv.second;
-      double* o = out.data() + i * per;
-      if (leaf) boosting->PredictLeafIndex(x.data(), o);
-      else if (contrib) boosting->PredictContrib(x.data(), o);
-      else if (raw) boosting->PredictRaw(x.data(), o, nullptr);
-      else boosting->Predict(x.data(), o, &es);
+      errs.Run([&] {
+        std::fill(x.begin(), x.end(), 0.0);
+        for (auto& kv : rows.rows[i]) if (kv.first < nf) x[kv.first] = kv.second;
+        double* o = out.data() + i * per;
+        if (leaf) boosting->PredictLeafIndex(x.data(), o);
+        else if (contrib) boosting->PredictContrib(x.data(), o);
+        else if (raw) boosting->PredictRaw(x.data(), o, nullptr);
+        else boosting->Predict(x.data(), o, &es);
+      });
     }
   }
+  errs.Rethrow();
   std::ofstream fo(c.output_result);
   for (size_t i = 0; i < rows.rows.size(); ++i) {
     for (int k = 0; k < per; ++k) fo << (k ? "\t" : "") << common::Format17(out[i * per + k]);

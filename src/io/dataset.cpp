@@ -3,6 +3,7 @@
 // Reference behaviour: src/io/dataset.cpp (FindGroups :107-244,
 // FastFeatureBundling :246-323, Construct :325-441, SaveBinary :1018-1187) and
 // dataset_loader.cpp:593 (ConstructFromSampleData).
+#include "lgap/omp_errors.h"
 #include "lgap/dataset.h"
 
 #include <omp.h>
@@ -271,28 +272,32 @@ void Dataset::PackRows(const RowSource& src, data_size_t start_row, bool reset) 
     }
   }
   const int nthreads = omp_get_max_threads();
+  OmpErrors errs;  // row sources (Arrow, Python sequences through the C API) may raise
 #pragma omp parallel num_threads(nthreads)
   {
     std::vector<std::pair<int, double>> row;
 #pragma omp for schedule(static, 4096)
     for (data_size_t i = 0; i < nrows; ++i) {
-      uint8_t* r = bins_.data() + static_cast<size_t>(i + start_row) * row_stride_;
-      std::memcpy(r, tmpl.data(), row_stride_);
-      src.GetRow(i, &row);
-      for (auto& kv : row) {
-        if (kv.first >= num_total_features_) continue;
-        int f = used_map_[kv.first];
-        if (f < 0) continue;
-        const auto& fi = features_[f];
-        if (store_raw) raw_[static_cast<size_t>(i + start_row) * nfeat + f] = static_cast<float>(kv.second);
-        uint32_t b = mappers_[kv.first].ValueToBin(kv.second);
-        int gb = EncodeBin(fi, b);
-        if (gb == 0 && owner[fi.group] != f) continue;
-        if (bin_width_ == 1) r[fi.group] = static_cast<uint8_t>(gb);
-        else reinterpret_cast<uint16_t*>(r)[fi.group] = static_cast<uint16_t>(gb);
-      }
+      errs.Run([&] {
+        uint8_t* r = bins_.data() + static_cast<size_t>(i + start_row) * row_stride_;
+        std::memcpy(r, tmpl.data(), row_stride_);
+        src.GetRow(i, &row);
+        for (auto& kv : row) {
+          if (kv.first >= num_total_features_) continue;
+          int f = used_map_[kv.first];
+          if (f < 0) continue;
+          const auto& fi = features_[f];
+          if (store_raw) raw_[static_cast<size_t>(i + start_row) * nfeat + f] = static_cast<float>(kv.second);
+          uint32_t b = mappers_[kv.first].ValueToBin(kv.second);
+          int gb = EncodeBin(fi, b);
+          if (gb == 0 && owner[fi.group] != f) continue;
+          if (bin_width_ == 1) r[fi.group] = static_cast<uint8_t>(gb);
+          else reinterpret_cast<uint16_t*>(r)[fi.group] = static_cast<uint16_t>(gb);
+        }
+      });
     }
   }
+  errs.Rethrow();
 }
 
 void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* reference,
@@ -354,9 +359,11 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
       }
     }
   }
+  OmpErrors errs;  // FindBin rejects invalid bin settings with Log::Fatal
 #pragma omp parallel for schedule(dynamic)
   for (int j = 0; j < num_total_features_; ++j) {
-    if (ignore[j]) continue;
+    if (ignore[j] || errs.failed()) continue;
+    try {
     int mb = cfg.max_bin;
     if (!cfg.max_bin_by_feature.empty()) {
       if (static_cast<int>(cfg.max_bin_by_feature.size()) != num_total_features_) {
@@ -370,7 +377,11 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
                         cfg.min_data_in_leaf, cfg.feature_pre_filter,
                         cat_set.count(j) ? BinType::Categorical : BinType::Numerical, cfg.use_missing,
                         cfg.zero_as_missing, forced[j]);
+    } catch (...) {
+      errs.Capture();
+    }
   }
+  errs.Rethrow();
   // ---- distributed: every rank adopts the mappers of the feature's owner rank
   // (features dealt round-robin; reference dataset_loader.cpp:1166-1262 splits
   // the feature range and allgathers serialized BinMappers the same way).

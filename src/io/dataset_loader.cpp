@@ -11,6 +11,7 @@
 #include <sstream>
 #include <unordered_map>
 
+#include "lgap/omp_errors.h"
 #include "lgap/common.h"
 #include "lgap/dataset.h"
 #include "lgap/log.h"
@@ -174,16 +175,20 @@ void ParseTextFile(const std::string& filename, bool header, int label_idx, Owne
   std::vector<int> maxcol(omp_get_max_threads(), -1);
   const char delim = fmt == TextFormat::CSV ? ',' : '\t';
   if (out_label_idx) *out_label_idx = label_idx;
+  OmpErrors errs;  // a malformed line raises from ParseLine inside the region
 #pragma omp parallel for schedule(static, 1024)
   for (size_t r = 0; r < n; ++r) {
-    const int tid = omp_get_thread_num();
-    float w = 1.0f;
-    double gid = 0.0;
-    ParseLine(lines[first + r], fmt, delim, label_idx, weight_idx, group_idx, &rows->rows[r], &(*labels)[r], &w, &gid,
-              &maxcol[tid]);
-    if (weights && weight_idx >= 0) (*weights)[r] = w;
-    if (group_ids && group_idx >= 0) (*group_ids)[r] = gid;
+    errs.Run([&] {
+      const int tid = omp_get_thread_num();
+      float w = 1.0f;
+      double gid = 0.0;
+      ParseLine(lines[first + r], fmt, delim, label_idx, weight_idx, group_idx, &rows->rows[r], &(*labels)[r], &w,
+                &gid, &maxcol[tid]);
+      if (weights && weight_idx >= 0) (*weights)[r] = w;
+      if (group_ids && group_idx >= 0) (*group_ids)[r] = gid;
+    });
   }
+  errs.Rethrow();
   int mc = -1;
   for (int m : maxcol) mc = std::max(mc, m);
   rows->ncol = mc + 1;
@@ -324,23 +329,27 @@ std::unique_ptr<Dataset> LoadTwoRound(const std::string& filename, const Config&
     chunk.ncol = ds->num_total_features();
     chunk.rows.resize(lines.size());
     std::vector<int> mc(omp_get_max_threads(), -1);
+    OmpErrors errs;
 #pragma omp parallel for schedule(static, 256)
     for (size_t r = 0; r < lines.size(); ++r) {
-      float w = 1.0f;
-      double g = 0.0;
-      ParseLine(lines[r], fmt, delim, sp.label_idx, sp.weight_idx, sp.group_idx, &chunk.rows[r],
-                &labels[filled + r], &w, &g, &mc[omp_get_thread_num()]);
-      if (sp.weight_idx >= 0) weights[filled + r] = w;
-      // weight / group columns are not features
-      if (sp.weight_idx >= 0 || sp.group_idx >= 0) {
-        auto& row = chunk.rows[r];
-        row.erase(std::remove_if(row.begin(), row.end(),
-                                 [&](const std::pair<int, double>& kv) {
-                                   return kv.first == sp.weight_idx || kv.first == sp.group_idx;
-                                 }),
-                  row.end());
-      }
+      errs.Run([&] {
+        float w = 1.0f;
+        double g = 0.0;
+        ParseLine(lines[r], fmt, delim, sp.label_idx, sp.weight_idx, sp.group_idx, &chunk.rows[r],
+                  &labels[filled + r], &w, &g, &mc[omp_get_thread_num()]);
+        if (sp.weight_idx >= 0) weights[filled + r] = w;
+        // weight / group columns are not features
+        if (sp.weight_idx >= 0 || sp.group_idx >= 0) {
+          auto& row = chunk.rows[r];
+          row.erase(std::remove_if(row.begin(), row.end(),
+                                   [&](const std::pair<int, double>& kv) {
+                                     return kv.first == sp.weight_idx || kv.first == sp.group_idx;
+                                   }),
+                    row.end());
+        }
+      });
     }
+    errs.Rethrow();
     ds->PushRows(chunk, filled);
     filled += static_cast<data_size_t>(lines.size());
     lines.clear();

@@ -12,6 +12,7 @@
 #include <map>
 #include <numeric>
 
+#include "lgap/omp_errors.h"
 #include "lgap/common.h"
 #include "lgap/log.h"
 #include "lgap/metric.h"
@@ -71,25 +72,29 @@ class RankingBase : public ObjectiveFunction {
     effective_pairs_.assign(num_queries_, 0.0);
   }
   void GetGradients(const double* score, score_t* g, score_t* h) const override {
+    OmpErrors errs;  // label / target checks inside OneQuery raise
 #pragma omp parallel for schedule(guided)
     for (data_size_t q = 0; q < num_queries_; ++q) {
-      const data_size_t start = qb_[q];
-      const data_size_t cnt = qb_[q + 1] - qb_[q];
-      std::vector<double> adj;
-      const double* s = score + start;
-      if (num_position_ids_ > 0) {
-        adj.resize(cnt);
-        for (data_size_t j = 0; j < cnt; ++j) adj[j] = score[start + j] + pos_biases_[positions_[start + j]];
-        s = adj.data();
-      }
-      OneQuery(q, cnt, label_ + start, s, g + start, h + start);
-      if (weights_) {
-        for (data_size_t j = 0; j < cnt; ++j) {
-          g[start + j] = static_cast<score_t>(g[start + j] * weights_[start + j]);
-          h[start + j] = static_cast<score_t>(h[start + j] * weights_[start + j]);
+      errs.Run([&] {
+        const data_size_t start = qb_[q];
+        const data_size_t cnt = qb_[q + 1] - qb_[q];
+        std::vector<double> adj;
+        const double* s = score + start;
+        if (num_position_ids_ > 0) {
+          adj.resize(cnt);
+          for (data_size_t j = 0; j < cnt; ++j) adj[j] = score[start + j] + pos_biases_[positions_[start + j]];
+          s = adj.data();
         }
-      }
+        OneQuery(q, cnt, label_ + start, s, g + start, h + start);
+        if (weights_) {
+          for (data_size_t j = 0; j < cnt; ++j) {
+            g[start + j] = static_cast<score_t>(g[start + j] * weights_[start + j]);
+            h[start + j] = static_cast<score_t>(h[start + j] * weights_[start + j]);
+          }
+        }
+      });
     }
+    errs.Rethrow();
     if (Log::Level() >= LogLevel::Debug) {
       double avg = 0.0;
       for (auto e : effective_pairs_) if (!std::isnan(e)) avg += e;

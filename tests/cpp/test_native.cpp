@@ -164,6 +164,47 @@ void TestTrainPredictRoundTrip(const std::string& data) {
   CHECK_API(LGBM_DatasetFree(ds));
 }
 
+// Errors raised inside OpenMP regions (parsing) must come back as -1 + LGBM_GetLastError,
+// never std::terminate (reference utils/openmp_wrapper.h:80-131).
+void TestParallelErrorsReturnMinusOne() {
+  const std::string dir = "/tmp";
+  const std::string bad_csv = dir + "/lgap_native_bad.csv";
+  {
+    std::ofstream f(bad_csv);
+    for (int i = 0; i < 20000; ++i) {
+      if (i == 12345) f << "1,2.5,oops,4\n";
+      else f << (i % 2) << "," << i * 0.5 << "," << (i % 7) << "," << (i % 3) << "\n";
+    }
+  }
+  DatasetHandle ds = nullptr;
+  EXPECT(LGBM_DatasetCreateFromFile(bad_csv.c_str(), "verbosity=-1", nullptr, &ds) == -1);
+  EXPECT(std::strstr(LGBM_GetLastError(), "oops") != nullptr);
+  EXPECT(LGBM_DatasetCreateFromFile(bad_csv.c_str(), "verbosity=-1 two_round=true", nullptr, &ds) == -1);
+  EXPECT(std::strstr(LGBM_GetLastError(), "oops") != nullptr);
+  // a bad label token (label column parsed inside the same region)
+  const std::string bad_label = dir + "/lgap_native_badlabel.csv";
+  {
+    std::ofstream f(bad_label);
+    for (int i = 0; i < 20000; ++i) f << (i == 777 ? "yes" : (i % 2 ? "1" : "0")) << "," << i << "," << i % 5 << "\n";
+  }
+  EXPECT(LGBM_DatasetCreateFromFile(bad_label.c_str(), "verbosity=-1", nullptr, &ds) == -1);
+  EXPECT(std::strstr(LGBM_GetLastError(), "yes") != nullptr);
+  // a query file whose sizes do not add up to the row count
+  const std::string good = dir + "/lgap_native_rank.csv";
+  {
+    std::ofstream f(good);
+    for (int i = 0; i < 1000; ++i) f << (i % 3) << "," << i << "," << i % 5 << "\n";
+    std::ofstream q(good + ".query");
+    q << "500\n400\n";
+  }
+  EXPECT(LGBM_DatasetCreateFromFile(good.c_str(), "verbosity=-1", nullptr, &ds) == -1);
+  EXPECT(std::strlen(LGBM_GetLastError()) > 0);
+  std::remove(bad_csv.c_str());
+  std::remove(bad_label.c_str());
+  std::remove(good.c_str());
+  std::remove((good + ".query").c_str());
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -172,6 +213,7 @@ int main(int argc, char** argv) {
   TestCommon();
   TestPointwiseMetric();
   TestTrainPredictRoundTrip(data);
+  TestParallelErrorsReturnMinusOne();
   if (g_failures) {
     std::fprintf(stderr, "%d expectation(s) failed\n", g_failures);
     return 1;

@@ -229,3 +229,31 @@ def test_ref_chain_and_set_network_api(lgb):
     assert c.get_ref_chain(ref_limit=2) == {b, c}
     bst = lgb.train({"verbosity": -1}, a, 1)
     assert callable(bst.set_network) and callable(bst.free_network)
+
+
+@pytest.mark.parametrize("two_round", [False, True])
+def test_parse_errors_in_parallel_regions_raise(lgb, tmp_path, two_round):
+    """A malformed CSV value, a bad label token and an inconsistent query file are raised as
+    LightGBMError from inside the OpenMP parse regions; the process must not abort
+    (reference utils/openmp_wrapper.h:80-131)."""
+    bad = tmp_path / "bad.csv"
+    lines = [f"{i % 2},{i * 0.5},{i % 7}" for i in range(30000)]
+    lines[17001] = "1,2.5,notanumber"
+    bad.write_text("\n".join(lines) + "\n")
+    params = {"verbosity": -1, "two_round": two_round}
+    with pytest.raises(lgb.LightGBMError, match="notanumber"):
+        lgb.Dataset(str(bad), params=params).construct()
+    badlab = tmp_path / "badlab.csv"
+    lines = [f"{i % 2},{i * 0.5},{i % 7}" for i in range(30000)]
+    lines[29999] = "maybe,1.0,2.0"
+    badlab.write_text("\n".join(lines) + "\n")
+    with pytest.raises(lgb.LightGBMError, match="maybe"):
+        lgb.Dataset(str(badlab), params=params).construct()
+    good = tmp_path / "rank.csv"
+    good.write_text("\n".join(f"{i % 3},{i},{i % 5}" for i in range(1000)) + "\n")
+    (tmp_path / "rank.csv.query").write_text("600\n300\n")
+    with pytest.raises(lgb.LightGBMError, match="query"):
+        lgb.Dataset(str(good), params=params).construct()
+    # the library is still usable afterwards
+    ok = lgb.Dataset(np.arange(200.0).reshape(100, 2), np.arange(100) % 2)
+    assert lgb.train({"objective": "binary", "verbosity": -1}, ok, 2).num_trees() == 2

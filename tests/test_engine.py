@@ -249,6 +249,70 @@ def test_continue_training(lgb, binary_data):
                                atol=1e-6)
 
 
+def test_continue_training_constructed_and_file_datasets(lgb, binary_data, tmp_path):
+    """Continued training from a pre-constructed Dataset and from a file-backed Dataset must start
+    from the init model's scores (reference engine.py -> Dataset._set_predictor), so that 10 + 10
+    rounds equal 20 rounds in one go, also in the validation-set metric."""
+    X, y, Xt, yt, _ = binary_data
+    params = {"objective": "regression", "verbosity": -1, "metric": "l2"}
+    full = lgb.train(params, lgb.Dataset(X, y), 20)
+    b1 = lgb.train(params, lgb.Dataset(X, y), 10)
+    ds = lgb.Dataset(X, y, free_raw_data=False).construct()
+    evals = {}
+    b2 = lgb.train(params, ds, 10, init_model=b1, valid_sets=[ds.create_valid(Xt, yt)], valid_names=["v"],
+                   callbacks=[lgb.record_evaluation(evals)])
+    np.testing.assert_allclose(b2.predict(Xt, raw_score=True), full.predict(Xt, raw_score=True), atol=1e-6)
+    l2_full = float(np.mean((full.predict(Xt) - yt) ** 2))
+    assert abs(evals["v"]["l2"][-1] - l2_full) < 1e-6
+    # constructed and raw data freed: the reference raises rather than silently train from zero
+    gone = lgb.Dataset(X, y).construct()
+    with pytest.raises(lgb.basic.LightGBMError, match="freed raw data"):
+        lgb.train(params, gone, 10, init_model=b1)
+    # file data: the init score comes from predicting on the file
+    path = os.path.join(DATA, "binary.train")
+    b1f = lgb.train(params, lgb.Dataset(path), 10)
+    b3 = lgb.train(params, lgb.Dataset(path), 10, init_model=b1f)
+    full_f = lgb.train(params, lgb.Dataset(path), 20)
+    np.testing.assert_allclose(b3.predict(Xt, raw_score=True), full_f.predict(Xt, raw_score=True), atol=1e-6)
+    # init model from a saved file
+    model_file = str(tmp_path / "m.txt")
+    b1.save_model(model_file)
+    b4 = lgb.train(params, lgb.Dataset(X, y), 10, init_model=model_file)
+    np.testing.assert_allclose(b4.predict(Xt, raw_score=True), full.predict(Xt, raw_score=True), atol=1e-6)
+
+
+def test_cv_init_model(lgb, binary_data):
+    """cv(init_model=...) continues every fold from the model (reference engine.py cv)."""
+    X, y, *_ = binary_data
+    params = {"objective": "binary", "metric": "binary_logloss", "verbosity": -1}
+    b1 = lgb.train(params, lgb.Dataset(X, y), 20)
+    cold = lgb.cv(params, lgb.Dataset(X, y), 5, nfold=3, seed=2)
+    warm = lgb.cv(params, lgb.Dataset(X, y), 5, nfold=3, seed=2, init_model=b1, return_cvbooster=True)
+    assert warm["valid binary_logloss-mean"][0] < cold["valid binary_logloss-mean"][-1]
+    assert all(b.current_iteration() == 25 for b in warm["cvbooster"].boosters)
+
+
+def test_split_importance_counts_positive_gain_only(lgb, binary_data):
+    """Split importance counts only splits with positive gain, as gain importance does
+    (reference gbdt_model_text.cpp:635-653)."""
+    X, y, *_ = binary_data
+    b = lgb.train({"objective": "binary", "verbosity": -1, "num_leaves": 4}, lgb.Dataset(X, y), 3)
+    d = b.dump_model()
+    gains = {}
+
+    def walk(n):
+        if "split_index" in n:
+            gains.setdefault(n["split_feature"], []).append(n["split_gain"])
+            walk(n["left_child"])
+            walk(n["right_child"])
+
+    for t in d["tree_info"]:
+        walk(t["tree_structure"])
+    split = b.feature_importance("split")
+    for f, gs in gains.items():
+        assert split[f] == sum(1 for g in gs if g > 0)
+
+
 def test_cv(lgb, binary_data):
     X, y, *_ = binary_data
     res = lgb.cv({"objective": "binary", "metric": "auc", "verbosity": -1}, lgb.Dataset(X, y), 10, nfold=3,
