@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Multi-rank rehearsal of the data-parallel HIP learner on ONE GPU.
+"""Multi-rank rehearsal of the parallel HIP learners (data / feature / voting) on ONE GPU.
 
 Launched with ``torchrun --standalone --nproc-per-node P`` (P ranks share
 cuda:0). The device learner's collectives are staged through host memory over
@@ -40,13 +40,14 @@ def main() -> int:
           + 0.3 * rng.standard_normal(n)) > 0.3).astype(float)
     learner = os.environ.get("DP_LEARNER", "data")
     # data parallel: each rank holds a row shard; feature parallel: every rank holds all rows
-    a, b = shard_range(n, rank, world) if learner == "data" else (0, n)
+    a, b = shard_range(n, rank, world) if learner in ("data", "voting") else (0, n)
     # l2 regression: unit hessians make every histogram hessian sum and count estimate exact,
     # so no min_data / min_hessian boundary can flip between the fixed-point device sums
     # and the host's doubles; any model difference is then a transport or split-sync bug
     objective = os.environ.get("DP_OBJECTIVE", "regression")
     base = {"objective": objective, "num_leaves": 31, "verbosity": -1, "seed": 1, "min_data_in_leaf": 20,
-            "tree_learner": learner, "num_machines": world, "pre_partition": True, "deterministic": True}
+            "tree_learner": learner, "num_machines": world, "pre_partition": True, "deterministic": True,
+            "top_k": int(os.environ.get("DP_TOPK", "20"))}
     ds = lgb.Dataset(X[a:b], y[a:b], params=dict(base, device_type="cpu"), free_raw_data=False).construct()
     models = {}
     devs = os.environ.get("DP_DEVICES", "gpu,cpu").split(",")

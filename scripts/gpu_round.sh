@@ -32,6 +32,7 @@ for s in "$@"; do
     quick) step b10 300 python bench.py --steps 30 --warmup 3 && step b1 300 python bench.py --rows 1250000 --steps 50 --warmup 5;;
     diagrank) step diagrank 300 python scripts/diag_rank.py ${DIAG_TARGET:-lambdagap-s} && step diagrank_dp 300 python scripts/diag_rank.py ${DIAG_TARGET:-lambdagap-s} gpu_use_dp=true;;
     dpfix) step dpfix 900 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank or watchdog or xgmi_exchange";;
+    vote) step vote 900 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "voting or multirank";;
     learnerx) step learnerx 400 python -m pytest tests/test_gpu_learner.py -x -q --timeout 60 -p no:cacheprovider;;
     learner) step learner 1200 python -m pytest tests/test_gpu_learner.py -q --timeout 300 -p no:cacheprovider;;
     gputests) step gputests 1500 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider;;

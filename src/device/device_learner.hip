@@ -142,6 +142,7 @@ struct Args {
   int hist_min_rows;  // rows per k_hist block (fewer rows: more blocks and slab rows)
   // ---- owner-computes split finding (tree_learner=data|feature); single GPU: P = 1, Fmax = F
   int P, rank, Fmax;  // ranks, this rank, candidate block width (most features any rank owns)
+  int cand_rows;        // blocks of the candidate table the select reads (P for data / feature parallel)
   const int* own_feat;  // [Fmax] features of the groups this rank owns (-1: padding); nullptr: identity
   char* cand;           // candidate table [P] blocks of cand_stride bytes (tree_kernels.h)
   int cand_stride;
@@ -159,6 +160,17 @@ struct Args {
   unsigned xsession;    // high word of the exchange tags (new per learner state)
   unsigned long long xtimeout;  // bound of an exchange wait (wall_clock64 ticks, 100 MHz)
   int xfault;           // LGAP_XGMI_FAULT=1: never signal (failure-detection tests)
+  // ---- voting parallel (tree_learner=voting): local scan, top-k vote, elected histograms
+  int vote;             // 1: k_reduce_scan is the LOCAL pass (local sums / counts, no masks or penalties)
+  double2* hsum_part;   // [hist blocks] local (sum g, sum h) of the smaller child's rows per k_hist block
+  double2* lsum_loc;    // [L] local leaf sums
+  int topk;             // elected features per child (min(top_k, F))
+  const char* lcand;    // local candidate table (keys [2][F], infos [2][F] at lcand_key_bytes)
+  int lcand_key_bytes;
+  VoteRec* vrec;        // collective transport: gathered local top-k records [P][2 * topk]
+  void* vhist;          // collective transport: packed elected histograms (all-reduced in place)
+  int vcap;             // values of one packed row (2 * topk * 2 * (max_bin - 1))
+  int* elect;           // [2][topk + 2]: count, first-value offset, then the elected features (ascending)
   SplitParams sp;
 };
 
@@ -341,6 +353,7 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     const unsigned e0 = a.ctl->epoch, e1 = a.ctl_next ? a.ctl_next->epoch : 0u;
     c.epoch = (e0 > e1 ? e0 : e1) + 1u;
     c.pad1 = c.pad2 = 0;
+    c.plg = c.plh = 0.0;
     *a.ctl = c;
     LeafRange r;
     r.buf = tp.root_buf;
@@ -473,11 +486,13 @@ __device__ __forceinline__ int HistActiveBlocks(int n, int grid, int min_rows) {
 template <int W, int MODE>
 __device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& tile, const LeafRange& r, int cls, int rb,
                                               int re, const int* gst, unsigned long long* hist, float sg, float sh,
-                                              double dsg, double dsh) {
+                                              double dsg, double dsh, double* rsum_g, double* rsum_h) {
   const int tpr = tile.d1 - tile.d0;
   const int rpi = blockDim.x / tpr;
   const int myr = threadIdx.x / tpr;
   const int myd = threadIdx.x - myr * tpr;
+  *rsum_g = 0.0;
+  *rsum_h = 0.0;
   if (myr >= rpi) return;
   constexpr int per = 4 / W;
   constexpr int R = LGAP_HIST_R;  // rows in flight per thread
@@ -489,6 +504,9 @@ __device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& til
   const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
   const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf] + r.start;
   const int base = r.buf < 0 ? r.start : 0;
+  // voting: the first dword's thread of each row also sums the row's (g, h) (local leaf sums)
+  const bool sums = a.hsum_part != nullptr && myd == 0;
+  double tg = 0.0, th = 0.0;
   for (int p0 = rb + myr; p0 < re; p0 += rpi * R) {
     int rows[R];
 #pragma unroll
@@ -502,6 +520,13 @@ __device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& til
     for (int j = 0; j < R; ++j) {
       word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
       v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
+    }
+    if (sums) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        tg += v[j].x;
+        th += v[j].y;
+      }
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -529,27 +554,37 @@ __device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& til
       }
     }
   }
+  *rsum_g = tg;
+  *rsum_h = th;
 }
 
 // Rows of the (rare) tiles whose bins exceed the LDS budget: fp64 atomics into
 // the block's own slab row (global memory, no cross-block contention).
 template <int W, typename Acc>
 __device__ void HistRowsDirect(const Args& a, const HistTile& tile, const LeafRange& r, int cls, int rb, int re,
-                               const int* gst, Acc* hist) {
+                               const int* gst, Acc* hist, double* rsum_g, double* rsum_h) {
   const int tpr = tile.d1 - tile.d0;
   const int rpi = blockDim.x / tpr;
   const int myr = threadIdx.x / tpr;
   const int myd = threadIdx.x - myr * tpr;
+  *rsum_g = 0.0;
+  *rsum_h = 0.0;
   if (myr >= rpi) return;
   constexpr int per = 4 / W;
   const int dw = tile.d0 + myd;
   const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
   const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf] + r.start;
   const int base = r.buf < 0 ? r.start : 0;
+  const bool sums = a.hsum_part != nullptr && myd == 0;
+  double tg = 0.0, th = 0.0;
   for (int p = rb + myr; p < re; p += rpi) {
     const int row = idx ? idx[p] : base + p;
     const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
     const float2 v = gh[row];
+    if (sums) {
+      tg += v.x;
+      th += v.y;
+    }
 #pragma unroll
     for (int k = 0; k < per; ++k) {
       const uint32_t b = W == 1 ? ((word >> (8 * k)) & 0xFFu) : ((word >> (16 * k)) & 0xFFFFu);
@@ -560,6 +595,27 @@ __device__ void HistRowsDirect(const Args& a, const HistTile& tile, const LeafRa
         atomicAdd(&hist[2 * o + 1], static_cast<Acc>(v.y));
       }
     }
+  }
+  *rsum_g = tg;
+  *rsum_h = th;
+}
+
+// voting: block sum of the per-thread row sums -> hsum_part[blockIdx.x] (first tile's blocks)
+__device__ void PublishRowSums(const Args& a, double tg, double th) {
+  if (a.hsum_part == nullptr || blockIdx.y != 0) return;
+  __shared__ double s_rs[2][kHistThreads / 64];
+  tg = WaveSum(tg);
+  th = WaveSum(th);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_rs[0][w] = tg;
+    s_rs[1][w] = th;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double g = 0.0, h = 0.0;
+    for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) g += s_rs[0][i], h += s_rs[1][i];
+    a.hsum_part[blockIdx.x] = make_double2(g, h);
   }
 }
 
@@ -590,8 +646,10 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
     for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
     __threadfence_block();
     __syncthreads();
-    if (MODE == 0) HistRowsDirect<W, float>(a, tile, r, cls, rb, re, gst, slabf);
-    else HistRowsDirect<W, double>(a, tile, r, cls, rb, re, gst, slab);
+    double tg, th;
+    if (MODE == 0) HistRowsDirect<W, float>(a, tile, r, cls, rb, re, gst, slabf, &tg, &th);
+    else HistRowsDirect<W, double>(a, tile, r, cls, rb, re, gst, slab, &tg, &th);
+    PublishRowSums(a, tg, th);
     return;
   }
   const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
@@ -611,8 +669,10 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
   __syncthreads();
   Stamp(a, 2, 1);
-  HistRowsFixed<W, MODE>(a, tile, r, cls, rb, re, gst, hist, sg, sh, dsg * 0.99999, dsh * 0.99999);
+  double tg, th;
+  HistRowsFixed<W, MODE>(a, tile, r, cls, rb, re, gst, hist, sg, sh, dsg * 0.99999, dsh * 0.99999, &tg, &th);
   __syncthreads();
+  PublishRowSums(a, tg, th);
   Stamp(a, 2, 2);
   if (MODE == 0) {
     const double ig = 1.0 / (static_cast<double>(sg)), ih = 1.0 / (static_cast<double>(sh));
@@ -1119,7 +1179,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     LeafBounds pre_bounds;
     if (lane == 0 && my_leaf >= 0) {
       pre_sum = a.lsum[my_leaf];
-      pre_n = a.gcount[my_leaf];
+      pre_n = a.vote ? a.range[my_leaf].count : a.gcount[my_leaf];
       pre_out = a.lout[my_leaf];
       pre_bounds = a.bounds[my_leaf];
       pre_depth = a.depth[my_leaf];
@@ -1127,7 +1187,8 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     int pre_used = 1, pre_spl = 1;
     if (t == 0) {
       pre_used = a.used_bytree[f];
-      pre_spl = c.larger >= 0 ? a.splittable[static_cast<size_t>(s_slot) * a.F + f] : 1;
+      // the voting learner's local pass tries every feature (no splittable inheritance)
+      pre_spl = (c.larger >= 0 && !a.vote) ? a.splittable[static_cast<size_t>(s_slot) * a.F + f] : 1;
     }
     double* hs_full = reinterpret_cast<double*>(smem);                 // 2 * nbin: smaller child, full
     double* hl_full = hs_full + 2 * a.max_bin;                          // 2 * nbin: larger child, full
@@ -1245,7 +1306,22 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
         }
         sgs = WaveSum(sgs);
         shs = WaveSum(shs);
-        const double2 sums = pre_sum;  // lane 0's prefetched leaf sums (only lane 0 uses them)
+        double2 sums = pre_sum;  // lane 0's prefetched leaf sums (only lane 0 uses them)
+        if (a.vote) {
+          // voting local pass: the smaller child's local sums are the k_hist row sums; the
+          // larger child's are the split leaf's local sums (Ctl) minus them
+          const int nbp = HistActiveBlocks(n_small, hist_grid, a.hist_min_rows);
+          double pg = 0.0, ph = 0.0;
+          for (int p = lane; p < nbp; p += 64) {
+            const double2 x = a.hsum_part[p];
+            pg += x.x;
+            ph += x.y;
+          }
+          pg = WaveSum(pg);
+          ph = WaveSum(ph);
+          sums = w == 0 ? make_double2(pg, ph) : make_double2(c.plg - pg, c.plh - ph);
+          if (j == 0 && lane == 0) a.lsum_loc[leaf] = sums;
+        }
         if (lane == 0) {
           H[2 * fi.mfb] = sums.x - sgs;
           H[2 * fi.mfb + 1] = sums.y - shs;
@@ -1311,14 +1387,18 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
           sp = __shfl(spi, 0, kWave) != 0;
         }
         if (lane == 0) {
-          a.splittable[static_cast<size_t>(lslot) * a.F + f] = sp ? 1 : 0;
+          if (!a.vote) a.splittable[static_cast<size_t>(lslot) * a.F + f] = sp ? 1 : 0;
           if (!sp) {
             out->Reset();
           } else {
             out->feature = f;
-            if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
-            if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
-            if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
+            // (the voting learner's local pass ranks raw gains: penalties and node masks
+            // apply in its global pass, k_vote_scan)
+            if (!a.vote) {
+              if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
+              if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
+              if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
+            }
           }
         }
       }
@@ -1367,6 +1447,308 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
   if (a.transport == 2) XArriveAndExchange(a, kXKindCand, XTag(a, c.epoch));
   if (t == 0 && a.stamps) {
     atomicMax(&a.stamps[((static_cast<size_t>(3) * 256 + (a.ctl->num_splits & 255)) * 2) * 8 + 7], wall_clock64());
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Voting parallel (PV-Tree; reference voting_parallel_tree_learner.cpp:243-399), on the
+// device. Rows are sharded like data parallel, but the per-split exchange carries only
+// what the vote needs:
+//   k_hist        local histogram of the smaller child (+ its local (sum g, sum h))
+//   k_reduce_scan LOCAL pass over every feature: local sums / counts, min_data and
+//                 min_sum_hessian divided by the ranks -> local candidate table
+//   k_vote_local  this rank's top-k per child -> VoteRec rows, all-gathered (xGMI push
+//                 + in-kernel exchange, or ncclAllGather)
+//   k_vote_pack   every block elects the same <= top_k features per child from the
+//                 gathered rows (GlobalVoting: gain weighted by count / mean leaf count,
+//                 best record per feature, top_k), and packs this rank's local histogram
+//                 of one elected feature; the packed rows are summed over the ranks
+//                 (xGMI push + in-kernel exchange, or ncclAllReduce)
+//   k_vote_scan   GLOBAL pass over the elected features only (global sums and counts,
+//                 split penalties, node masks) -> the candidate table the partition's
+//                 select reads. Every rank computes the same table: no further exchange.
+// The local histograms stay in the slots (parent - smaller subtraction stays local).
+
+constexpr int kVoteThreads = 256;
+
+// best record first: higher gain, then smaller feature (SplitInfo::BetterThan)
+__device__ __forceinline__ bool VoteBetter(double ga, int fa, double gb, int fb) {
+  return ga != gb ? ga > gb : fa < fb;
+}
+
+__global__ __launch_bounds__(kVoteThreads) void k_vote_local(Args a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const Ctl c = *a.ctl;
+  if (c.done || c.skip) return;
+  const int F = a.F, K = a.topk, t = threadIdx.x;
+  double* s_gain = reinterpret_cast<double*>(smem);
+  int* s_cnt = reinterpret_cast<int*>(s_gain + F);
+  __shared__ int s_n[kVoteThreads / 64];
+  const SplitKey* keys = reinterpret_cast<const SplitKey*>(a.lcand);
+  const SplitInfo* infos = reinterpret_cast<const SplitInfo*>(a.lcand + a.lcand_key_bytes);
+  for (int sel = 0; sel < 2; ++sel) {
+    const int leaf = sel ? c.larger : c.smaller;
+    int nv = 0;
+    for (int f = t; f < F; f += blockDim.x) {
+      const SplitKey k = keys[sel * F + f];
+      const bool valid = leaf >= 0 && k.feature >= 0;
+      s_gain[f] = valid ? k.gain : kMinScore;
+      s_cnt[f] = valid ? infos[sel * F + f].left_count + infos[sel * F + f].right_count : -1;
+      nv += valid ? 1 : 0;
+    }
+    const int nvalid = BlockSumInt(nv, s_n);  // (barrier inside: the LDS arrays are complete)
+    for (int f = t; f < F; f += blockDim.x) {
+      if (s_cnt[f] < 0) continue;
+      const double g = s_gain[f];
+      int rank = 0;
+      for (int j = 0; j < F && rank < K; ++j) rank += (s_cnt[j] >= 0 && VoteBetter(s_gain[j], j, g, f)) ? 1 : 0;
+      if (rank < K) {
+        VoteRec r;
+        r.gain = g;
+        r.feature = f;
+        r.count = s_cnt[f];
+        const size_t o = static_cast<size_t>(a.rank) * 2 * K + sel * K + rank;
+        if (a.transport == 2) {
+          for (int q = 0; q < a.P; ++q) reinterpret_cast<VoteRec*>(a.xp->base[q] + a.x_off_cand)[o] = r;
+        } else {
+          a.vrec[o] = r;
+        }
+      }
+    }
+    for (int i = nvalid + t; i < K; i += blockDim.x) {
+      VoteRec r;
+      r.gain = kMinScore;
+      r.feature = -1;
+      r.count = 0;
+      const size_t o = static_cast<size_t>(a.rank) * 2 * K + sel * K + i;
+      if (a.transport == 2) {
+        for (int q = 0; q < a.P; ++q) reinterpret_cast<VoteRec*>(a.xp->base[q] + a.x_off_cand)[o] = r;
+      } else {
+        a.vrec[o] = r;
+      }
+    }
+    __syncthreads();
+  }
+  if (a.transport == 2) XArriveAndExchange(a, kXKindCand, XTag(a, c.epoch));
+}
+
+// GlobalVoting of child `sel` over the gathered rows (same result in every block and on
+// every rank): s_list[0..n) = the elected features in ascending order; returns n.
+__device__ int ElectChild(const Args& a, const Ctl& c, int sel, const VoteRec* recs, double* s_w, int* s_f,
+                          int* s_flag, int* s_list, int* s_tmp) {
+  const int K = a.topk, R = a.P * K, t = threadIdx.x;
+  const int leaf = sel ? c.larger : c.smaller;
+  // mean leaf count per rank in float, as the reference's score_t mean_num_data
+  const float mean = leaf >= 0 ? static_cast<float>(a.gcount[leaf]) / static_cast<float>(a.P) : 1.f;
+  for (int i = t; i < R; i += blockDim.x) {
+    const int r = i / K, k = i - r * K;
+    const VoteRec v = recs[static_cast<size_t>(r) * 2 * K + sel * K + k];
+    const double w = v.gain * v.count / static_cast<double>(mean);
+    const bool valid = leaf >= 0 && v.feature >= 0 && w > kMinScore;
+    s_w[i] = w;
+    s_f[i] = valid ? v.feature : -1;
+  }
+  __syncthreads();
+  // the best record of each feature (first in gather order on equal weighted gain)
+  for (int i = t; i < R; i += blockDim.x) {
+    int best = s_f[i] >= 0 ? 1 : 0;
+    for (int j = 0; j < R && best; ++j) {
+      if (j != i && s_f[j] == s_f[i] && (s_w[j] > s_w[i] || (s_w[j] == s_w[i] && j < i))) best = 0;
+    }
+    s_flag[i] = best;
+  }
+  __syncthreads();
+  // elected: feature-best records ranked < K by (weighted gain desc, feature asc)
+  int ne = 0;
+  for (int i = t; i < R; i += blockDim.x) {
+    int el = 0;
+    if (s_flag[i]) {
+      int rank = 0;
+      for (int j = 0; j < R && rank < K; ++j) rank += (s_flag[j] && VoteBetter(s_w[j], s_f[j], s_w[i], s_f[i])) ? 1 : 0;
+      el = rank < K ? 1 : 0;
+    }
+    ne += el;
+    s_tmp[i] = el;
+  }
+  __syncthreads();
+  for (int i = t; i < R; i += blockDim.x) s_flag[i] = s_tmp[i];
+  const int n = BlockSumInt(ne, s_tmp + R);
+  for (int i = t; i < R; i += blockDim.x) {
+    if (!s_flag[i]) continue;
+    int pos = 0;
+    for (int j = 0; j < R; ++j) pos += (s_flag[j] && s_f[j] < s_f[i]) ? 1 : 0;
+    s_list[pos] = s_f[i];
+  }
+  __syncthreads();
+  return n;
+}
+
+__device__ __forceinline__ int VoteValues(const Args& a, int f) { return 2 * (a.feat[f].num_bin - 1); }
+
+// One block per (child, elected rank): elect (redundantly per block), then pack this
+// rank's local histogram of the block's feature into the packed row at its offset.
+template <typename Acc>
+__global__ __launch_bounds__(kVoteThreads) void k_vote_pack(Args a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const Ctl c = *a.ctl;
+  if (c.done || c.skip) return;
+  const int K = a.topk, R = a.P * K, t = threadIdx.x;
+  double* s_w = reinterpret_cast<double*>(smem);
+  int* s_f = reinterpret_cast<int*>(s_w + R);
+  int* s_flag = s_f + R;
+  int* s_tmp = s_flag + R;                     // R + kVoteThreads / 64
+  int* s_list = s_tmp + R + kVoteThreads / 64;  // [2][K]
+  __shared__ int s_n[2];
+  const VoteRec* recs = a.transport == 2 ? reinterpret_cast<const VoteRec*>(a.xp->base[a.rank] + a.x_off_cand) : a.vrec;
+  for (int sel = 0; sel < 2; ++sel) {
+    const int n = ElectChild(a, c, sel, recs, s_w, s_f, s_flag, s_list + sel * K, s_tmp);
+    if (t == 0) s_n[sel] = n;
+    __syncthreads();
+  }
+  const int sel = blockIdx.x / K, k = blockIdx.x - sel * K;
+  int base0 = 0;
+  for (int i = 0; i < s_n[0]; ++i) base0 += VoteValues(a, s_list[i]);
+  if (blockIdx.x == 0 && t < 2) {
+    int* e = a.elect + t * (K + 2);
+    e[0] = s_n[t];
+    e[1] = t == 0 ? 0 : base0;
+  }
+  if (blockIdx.x == 0) {
+    for (int i = t; i < 2 * K; i += blockDim.x) {
+      const int sl = i / K, kk = i - sl * K;
+      a.elect[sl * (K + 2) + 2 + kk] = kk < s_n[sl] ? s_list[sl * K + kk] : -1;
+    }
+  }
+  const int leaf = sel ? c.larger : c.smaller;
+  if (k < s_n[sel] && leaf >= 0) {
+    const int f = s_list[sel * K + k];
+    int off = sel ? base0 : 0;
+    for (int i = 0; i < k; ++i) off += VoteValues(a, s_list[sel * K + i]);
+    const int nv = VoteValues(a, f);
+    const double* src = a.slots + static_cast<size_t>(a.slot[leaf]) * 2 * a.TB + 2 * static_cast<size_t>(a.feat[f].hist_offset);
+    for (int v = t; v < nv; v += blockDim.x) {
+      const Acc x = static_cast<Acc>(src[v]);
+      if (a.transport == 2) {
+        for (int q = 0; q < a.P; ++q) {
+          reinterpret_cast<Acc*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * a.vcap + off + v] = x;
+        }
+      } else {
+        reinterpret_cast<Acc*>(a.vhist)[off + v] = x;
+      }
+    }
+  }
+  if (a.transport == 2) XArriveAndExchange(a, kXKindHist, XTag(a, c.epoch));
+}
+
+// Global pass: block k, wave `sel` scans elected feature k of child sel from the summed
+// packed rows with the GLOBAL leaf statistics; writes the candidate table (one row of
+// 2 x top_k positions) that the partition's select reads.
+template <typename Acc>
+__global__ __launch_bounds__(128) void k_vote_scan(Args a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const Ctl c = *a.ctl;
+  if (c.done || c.skip) return;
+  const int K = a.topk, k = blockIdx.x, t = threadIdx.x, lane = t & 63, sel = t >> 6;
+  __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
+  SplitInfo* out = reinterpret_cast<SplitInfo*>(s_out_raw) + sel;
+  double* H = reinterpret_cast<double*>(smem) + sel * 2 * a.max_bin;
+  int* order = reinterpret_cast<int*>(reinterpret_cast<double*>(smem) + 4 * a.max_bin) + sel * a.max_bin;
+  const int* e = a.elect + sel * (K + 2);
+  const int leaf = sel ? c.larger : c.smaller;
+  SplitKey key;
+  key.gain = kMinScore;
+  key.feature = -1;
+  key.threshold = 0;
+  key.group = key.offset = key.num_bin = key.mfb = key.default_bin = 0;
+  key.missing = key.default_left = key.is_cat = key.pad0 = 0;
+  key.pos = k;  // table row 0, column k of child sel (CandInfoPos(a, sel, k))
+  key.pad2 = 0;
+  if (lane == 0) out->Reset();
+  if (leaf >= 0 && k < e[0]) {
+    const int f = e[2 + k];
+    const DevFeature fi = a.feat[f];
+    int off = e[1];
+    for (int i = 0; i < k; ++i) off += VoteValues(a, e[2 + i]);
+    const int nv = 2 * (fi.num_bin - 1);
+    const Acc* rows = a.transport == 2 ? reinterpret_cast<const Acc*>(a.xp->base[a.rank] + a.x_off_hist)
+                                       : reinterpret_cast<const Acc*>(a.vhist);
+    const int nparts = a.transport == 2 ? a.P : 1;
+    double sgs = 0.0, shs = 0.0;
+    for (int v = lane; v < nv; v += 64) {
+      double acc = 0.0;
+      for (int p = 0; p < nparts; ++p) acc += static_cast<double>(rows[static_cast<size_t>(p) * a.vcap + off + v]);
+      const int kb = v >> 1;
+      const int b = kb < fi.mfb ? kb : kb + 1;
+      H[2 * b + (v & 1)] = acc;
+      if (v & 1) shs += acc;
+      else sgs += acc;
+    }
+    sgs = WaveSum(sgs);
+    shs = WaveSum(shs);
+    const double2 sums = a.lsum[leaf];
+    const int n = a.gcount[leaf];
+    if (lane == 0) {
+      H[2 * fi.mfb] = sums.x - sgs;
+      H[2 * fi.mfb + 1] = sums.y - shs;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    double po;
+    if (c.num_leaves == 1) {
+      SplitParams p0 = a.sp;
+      p0.path_smooth = 0.0;
+      po = LeafOutputRaw(sums.x, sums.y, p0, n, 0.0);
+    } else {
+      po = a.lout[leaf];
+    }
+    const LeafBounds bounds = a.bounds[leaf];
+    bool sp;
+    if (fi.bin_type == 0) {
+      sp = ScanNumericalWave(a, fi, H, sums.x, sums.y, n, po, bounds, 0, out);
+    } else {
+      int spi = 0;
+      if (lane == 0) {
+        FeatureScanMeta m;
+        m.num_bin = fi.num_bin;
+        m.default_bin = static_cast<uint32_t>(fi.default_bin);
+        m.missing_type = fi.missing;
+        m.bin_type = fi.bin_type;
+        m.monotone = fi.monotone;
+        m.penalty = fi.penalty;
+        m.rand_threshold = 0;
+        out->Reset();
+        spi = FindBestCategorical(H, m, a.sp, sums.x, sums.y, n, po, bounds, order, out) ? 1 : 0;
+      }
+      sp = __shfl(spi, 0, kWave) != 0;
+    }
+    if (lane == 0) {
+      if (!sp) {
+        out->Reset();
+      } else {
+        out->feature = f;
+        if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, a.depth[leaf]);
+        if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
+        if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
+      }
+      key.feature = out->feature;
+      key.gain = SafeGain(*out);
+      key.threshold = out->threshold;
+      key.group = fi.group;
+      key.offset = fi.offset;
+      key.num_bin = fi.num_bin;
+      key.mfb = fi.mfb;
+      key.default_bin = fi.default_bin;
+      key.missing = fi.missing;
+      key.default_left = out->default_left;
+      key.is_cat = fi.bin_type != 0 ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) *CandKey(a, 0, sel, k) = key;
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  for (int i = lane; i < kInfoWords; i += 64) {
+    reinterpret_cast<uint32_t*>(CandInfo(a, 0, sel, k))[i] = reinterpret_cast<const uint32_t*>(out)[i];
   }
 }
 
@@ -1469,7 +1851,7 @@ __device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
   SplitKey k3_0, k3_1, k3_2;  // (named: a runtime-indexed array would live in scratch)
   if (!c.skip) {
     // the two children's candidates: every position of the table (all ranks' blocks)
-    const int np = a.P * a.Fmax;
+    const int np = a.cand_rows * a.Fmax;
 #pragma unroll
     for (int sel = 0; sel < 2; ++sel) {
       const int leaf = sel ? c.larger : c.smaller;
@@ -1735,6 +2117,12 @@ __device__ void PostSplit(const Args& a, const Ctl& c, int left_count, const Spl
     const int md = a.sp.min_data_in_leaf;
     const bool skip = (a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2);
     Ctl nc = c;
+    if (a.lsum_loc) {
+      // voting: the split leaf's local sums, for the larger child's local pass
+      const double2 pl = a.lsum_loc[l];
+      nc.plg = pl.x;
+      nc.plh = pl.y;
+    }
     nc.num_splits = c.num_splits + 1;
     nc.num_leaves = c.num_leaves + 1;
     nc.left_count = lc;
@@ -2197,8 +2585,8 @@ class PinnedBuf {
   size_t n_ = 0;
 };
 
-// Parallel modes of the device learner (tree_learner=serial|data|feature).
-enum class DevParallel { kSerial, kData, kFeature };
+// Parallel modes of the device learner (tree_learner=serial|data|feature|voting).
+enum class DevParallel { kSerial, kData, kFeature, kVoting };
 
 class DeviceTreeLearner : public TreeLearner {
  public:
@@ -2233,8 +2621,11 @@ class DeviceTreeLearner : public TreeLearner {
       mode_ = DevParallel::kData;
       data_parallel_ = true;
     }
-    owner_scan_ = (mode_ != DevParallel::kSerial) && (CommActive() || HostStagedDP() || forced);
-    distributed_ = owner_scan_ && data_parallel_;
+    const bool multi = CommActive() || HostStagedDP() || forced;
+    // voting: a one-rank communicator also runs the voting path (single-GPU rehearsal)
+    voting_ = mode_ == DevParallel::kVoting && (multi || CommExists());
+    owner_scan_ = (mode_ == DevParallel::kData || mode_ == DevParallel::kFeature) && multi;
+    distributed_ = (owner_scan_ && data_parallel_) || voting_;
     device_id_ = CommExists() ? CommDevice() : std::max(0, config_->gpu_device_id);
     HIP_CHECK(hipSetDevice(device_id_));
     hipDeviceProp_t prop;
@@ -2251,15 +2642,15 @@ class DeviceTreeLearner : public TreeLearner {
     ResetConfig(config_);
     SetupTransport();
     Log::Info("HIP tree learner on %s: %d rows, %d features, %d groups, %d bins%s", device_name_.c_str(), N_, F_, G_,
-              TB_, owner_scan_ ? (" (" + ParallelDesc() + ")").c_str() : "");
+              TB_, (owner_scan_ || voting_) ? (" (" + ParallelDesc() + ")").c_str() : "");
   }
 
   // Feature-group ownership of the owner-computes modes: contiguous group ranges with
   // ~equal bins per rank (the host DataParallelTreeLearner's assignment), so rank r's
   // block of the histogram is the contiguous bin range [bin_lo[r], bin_lo[r + 1]).
   void SetupOwnership() {
-    P_ = owner_scan_ ? DpSize() : 1;
-    rank_ = owner_scan_ ? DpRank() : 0;
+    P_ = (owner_scan_ || voting_) ? DpSize() : 1;
+    rank_ = (owner_scan_ || voting_) ? DpRank() : 0;
     h_bin_lo_.assign(P_ + 1, TB_);
     std::vector<int> owner(G_);
     for (int g = 0; g < G_; ++g) {
@@ -2296,16 +2687,35 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t ib = Round256(2 * static_cast<size_t>(Fmax_) * sizeof(SplitInfo));
     cand_key_bytes_ = static_cast<int>(kb);
     cand_stride_ = static_cast<int>(kb + ib);
+    if (voting_) SetupVoting();
   }
 
   static size_t Round256(size_t x) { return (x + 255) & ~static_cast<size_t>(255); }
+
+  // Voting: top-k width, the packed elected-histogram row, and the global candidate table
+  // (one row of 2 x top_k positions). The xGMI exchange buffer reuses the histogram receive
+  // rows (P x vcap values) and the candidate region (P x 2 top_k VoteRecs).
+  void SetupVoting() {
+    topk_ = std::max(1, std::min(config_->top_k, F_));
+    if (topk_ > 1024 || F_ > 12000) {
+      Log::Fatal("The HIP voting-parallel learner supports top_k <= 1024 and up to 12000 features "
+                 "(top_k=%d, %d features); use device_type=cpu", config_->top_k, F_);
+    }
+    vcap_ = 2 * topk_ * 2 * std::max(1, max_bin_ - 1);
+    bbin_ = vcap_ / 2;
+    vcand_key_bytes_ = static_cast<int>(Round256(2 * static_cast<size_t>(topk_) * sizeof(SplitKey)));
+    vcand_stride_ = vcand_key_bytes_ + static_cast<int>(Round256(2 * static_cast<size_t>(topk_) * sizeof(SplitInfo)));
+    if (static_cast<size_t>(cand_stride_) < 2 * static_cast<size_t>(topk_) * sizeof(VoteRec)) {
+      cand_stride_ = static_cast<int>(Round256(2 * static_cast<size_t>(topk_) * sizeof(VoteRec)));
+    }
+  }
 
   // Transport of the owner-computes exchanges. LGAP_DP_TRANSPORT = auto (default: xGMI
   // in-kernel exchange when every rank maps every peer and the self-test passes, else
   // collectives) | xgmi | collective.
   void SetupTransport() {
     transport_ = 0;
-    if (!owner_scan_) return;
+    if (!owner_scan_ && !voting_) return;
     const char* e = std::getenv("LGAP_DP_TRANSPORT");
     const std::string want = e ? e : "auto";
     if (want != "auto" && want != "xgmi" && want != "collective") Log::Fatal("LGAP_DP_TRANSPORT=%s: expected auto|xgmi|collective", want.c_str());
@@ -2395,7 +2805,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   std::string ParallelDesc() const {
-    std::string m = mode_ == DevParallel::kFeature ? "feature-parallel" : "data-parallel";
+    std::string m = mode_ == DevParallel::kFeature ? "feature-parallel"
+                                                   : (voting_ ? "voting-parallel" : "data-parallel");
     m += ", " + std::to_string(P_) + " ranks, ";
     if (transport_ == 2) return m + "xGMI in-kernel exchange";
     if (HostStagedDP()) return m + "host-staged collectives";
@@ -2781,7 +3192,7 @@ class DeviceTreeLearner : public TreeLearner {
     // enqueue stays ahead of the ~40 us splits. The host-staged rehearsal transport
     // synchronises inside its all-reduce and is never captured.
     // the xGMI transport keeps every exchange inside the kernels: the tree replays as one graph
-    const bool collectives = owner_scan_ && transport_ != 2;
+    const bool collectives = (owner_scan_ || voting_) && transport_ != 2;
     const bool use_graph = config_->device_use_graph && (!collectives || (DPGraphEnabled() && !HostStagedDP()));
     if (use_graph) {
       if (graph_exec_ && distributed_ && graph_comm_ != ActiveComm()) InvalidateGraph();
@@ -2856,7 +3267,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   std::string DeviceName() const override {
-    if (!owner_scan_) return device_name_;
+    if (!owner_scan_ && !voting_) return device_name_;
     return device_name_ + " [" + ParallelDesc() + "]";
   }
 
@@ -3094,7 +3505,7 @@ class DeviceTreeLearner : public TreeLearner {
       else k_hist<2, 0><<<hgrid, kHistThreads, hist_lds_bytes_, stream_>>>(a);
     }
     HIP_CHECK(hipGetLastError());
-    if (distributed_ && collective) {
+    if (owner_scan_ && data_parallel_ && collective) {
       // owner reduce-scatter of the smaller child's histogram (xGMI: inside k_hist_owner)
       const int ogrid = DivUp(static_cast<long long>(P_) * 2 * bbin_, 64);
       if (use_dp_) {
@@ -3116,11 +3527,48 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void LaunchScan(const Args& a) {
+    if (voting_) {
+      LaunchVoting(a);
+      return;
+    }
     if (use_dp_) k_reduce_scan<double><<<Fmax_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks());
     else k_reduce_scan<float><<<Fmax_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks());
     HIP_CHECK(hipGetLastError());
     // complete the candidate table (xGMI: inside k_reduce_scan)
     if (owner_scan_ && transport_ != 2 && P_ > 1) AllGatherInPlace(cand_.get(), cand_stride_, stream_);
+  }
+
+  // The voting learner's per-split chain after k_hist (see k_vote_local).
+  void LaunchVoting(const Args& a) {
+    Args al = a;  // local pass: every feature, local sums / counts, divided thresholds, local table
+    al.vote = 1;
+    al.cand = cand_.get();
+    al.Fmax = F_;
+    al.cand_rows = 1;
+    al.cand_key_bytes = cand_key_bytes_;
+    al.cand_stride = cand_stride_;
+    al.rank = 0;
+    al.P = 1;
+    al.transport = 0;
+    al.own_feat = nullptr;
+    al.sp.min_data_in_leaf = config_->min_data_in_leaf / P_;  // integer division (reference :61-63)
+    al.sp.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf / P_;
+    if (use_dp_) k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(al, HistBlocks());
+    else k_reduce_scan<float><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(al, HistBlocks());
+    HIP_CHECK(hipGetLastError());
+    k_vote_local<<<1, kVoteThreads, vote_local_lds_, stream_>>>(a);
+    HIP_CHECK(hipGetLastError());
+    if (transport_ != 2) AllGatherInPlace(vrec_.get(), 2 * static_cast<size_t>(topk_) * sizeof(VoteRec), stream_);
+    if (use_dp_) k_vote_pack<double><<<2 * topk_, kVoteThreads, vote_pack_lds_, stream_>>>(a);
+    else k_vote_pack<float><<<2 * topk_, kVoteThreads, vote_pack_lds_, stream_>>>(a);
+    HIP_CHECK(hipGetLastError());
+    if (transport_ != 2) {
+      if (use_dp_) AllreduceSumF64(reinterpret_cast<double*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
+      else AllreduceSumF32(reinterpret_cast<float*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
+    }
+    if (use_dp_) k_vote_scan<double><<<topk_, 128, vote_scan_lds_, stream_>>>(a);
+    else k_vote_scan<float><<<topk_, 128, vote_scan_lds_, stream_>>>(a);
+    HIP_CHECK(hipGetLastError());
   }
 
   static double XTimeoutSeconds() {
@@ -3325,6 +3773,37 @@ class DeviceTreeLearner : public TreeLearner {
     // the exchange buffer that the peers push into)
     cand_.Resize(static_cast<size_t>(P_) * cand_stride_);
     cand_.Zero(stream_);
+    if (voting_) {
+      const size_t es = use_dp_ ? 8 : 4;
+      vcand_.Resize(static_cast<size_t>(vcand_stride_));
+      vcand_.Zero(stream_);
+      vrec_.Resize(static_cast<size_t>(P_) * 2 * topk_);
+      vhist_.Resize(static_cast<size_t>(vcap_) * es);
+      vhist_.Zero(stream_);
+      elect_.Resize(2 * static_cast<size_t>(topk_ + 2));
+      elect_.Zero(stream_);
+      hsum_part_.Resize(static_cast<size_t>(std::max(1, HistBlocks())));
+      lsum_loc_.Resize(L);
+      const int R = P_ * topk_;
+      vote_local_lds_ = static_cast<size_t>(F_) * (sizeof(double) + sizeof(int));
+      vote_pack_lds_ = static_cast<size_t>(R) * (sizeof(double) + 3 * sizeof(int)) + sizeof(int) * (kVoteThreads / 64) +
+                       2 * sizeof(int) * topk_;
+      vote_scan_lds_ = static_cast<size_t>(max_bin_) * (4 * sizeof(double) + 2 * sizeof(int));
+      auto big = [](const void* fn, size_t bytes) {
+        if (bytes > 64 * 1024) {
+          HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes)));
+        }
+      };
+      if (vote_local_lds_ > 150 * 1024 || vote_pack_lds_ > 150 * 1024) {
+        Log::Fatal("HIP voting learner: %d features x top_k %d x %d ranks exceed the LDS budget; use device_type=cpu",
+                   F_, topk_, P_);
+      }
+      big(reinterpret_cast<const void*>(k_vote_local), vote_local_lds_);
+      big(reinterpret_cast<const void*>(k_vote_pack<float>), vote_pack_lds_);
+      big(reinterpret_cast<const void*>(k_vote_pack<double>), vote_pack_lds_);
+      big(reinterpret_cast<const void*>(k_vote_scan<float>), vote_scan_lds_);
+      big(reinterpret_cast<const void*>(k_vote_scan<double>), vote_scan_lds_);
+    }
     rx_.Resize(std::max<size_t>(1, 2 * static_cast<size_t>(bbin_) * (use_dp_ ? 8 : 4)));
     stage_.Resize(owner_scan_ ? static_cast<size_t>(P_) * 2 * bbin_ * (use_dp_ ? 8 : 4) : 1);
     ++xsession_;  // exchange tags of this state start above every earlier one
@@ -3427,13 +3906,30 @@ class DeviceTreeLearner : public TreeLearner {
     a.P = P_;
     a.rank = rank_;
     a.Fmax = Fmax_;
+    a.cand_rows = owner_scan_ ? P_ : 1;
     a.own_feat = owner_scan_ ? own_feat_.get() : nullptr;
-    a.cand = transport_ == 2 ? x_local_ + x_off_cand_ : cand_.get();
+    a.cand = transport_ == 2 && owner_scan_ ? x_local_ + x_off_cand_ : cand_.get();
     a.cand_stride = cand_stride_;
     a.cand_key_bytes = cand_key_bytes_;
+    if (voting_) {
+      // the partition's select and k_vote_scan use the global (elected) table
+      a.cand = vcand_.get();
+      a.Fmax = topk_;
+      a.cand_stride = vcand_stride_;
+      a.cand_key_bytes = vcand_key_bytes_;
+      a.hsum_part = hsum_part_.get();
+      a.lsum_loc = lsum_loc_.get();
+      a.topk = topk_;
+      a.lcand = cand_.get();
+      a.lcand_key_bytes = cand_key_bytes_;
+      a.vrec = vrec_.get();
+      a.vhist = vhist_.get();
+      a.vcap = vcap_;
+      a.elect = elect_.get();
+    }
     // data parallel: the scan sums owner rows (xGMI: every rank's pushed row; collectives:
     // the reduce-scattered row); single GPU / feature parallel: the local slab rows
-    a.scan_src = distributed_ ? 1 : 0;
+    a.scan_src = (owner_scan_ && data_parallel_) ? 1 : 0;
     a.nparts = transport_ == 2 ? P_ : 1;
     a.rx = transport_ == 2 ? static_cast<const void*>(x_local_ + x_off_hist_) : static_cast<const void*>(rx_.get());
     a.own_bin0 = h_bin_lo_.empty() ? 0 : h_bin_lo_[rank_];
@@ -3648,6 +4144,14 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<int> own_feat_, bin_lo_;
   DevBuf<char> cand_, rx_, stage_;
   DevBuf<unsigned> xcnt_;
+  // voting parallel
+  bool voting_ = false;
+  int topk_ = 1, vcap_ = 2, vcand_key_bytes_ = 0, vcand_stride_ = 0;
+  size_t vote_local_lds_ = 0, vote_pack_lds_ = 0, vote_scan_lds_ = 0;
+  DevBuf<char> vcand_, vhist_;
+  DevBuf<VoteRec> vrec_;
+  DevBuf<int> elect_;
+  DevBuf<double2> hsum_part_, lsum_loc_;
   // xGMI transport
   int transport_ = 0;
   char* x_local_ = nullptr;
@@ -3702,6 +4206,7 @@ std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const
   if (parallel_mode == "serial") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kSerial);
   if (parallel_mode == "data") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kData);
   if (parallel_mode == "feature") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kFeature);
+  if (parallel_mode == "voting") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kVoting);
   Log::Fatal("Unknown tree learner type %s", parallel_mode.c_str());
   return nullptr;
 }

@@ -63,6 +63,7 @@ struct Ctl {
   int hist_nb;  // slab rows holding the smaller child's histogram when k_partition built it (0: k_hist did)
   unsigned epoch;  // split sequence number (never reset): tags k_partition's published tile counts
   int pad1, pad2;
+  double plg, plh;  // voting-parallel: this rank's local (sum g, sum h) of the leaf just split
 };
 
 // Compact record of a split candidate: everything the best-leaf select and the
@@ -90,6 +91,14 @@ constexpr int kMaxXRanks = 16;  // xGMI transport: ranks of one node
 // offsets on every rank; base[q] is rank q's buffer in this process's address space.
 struct XPeers {
   char* base[kMaxXRanks];
+};
+
+// Voting-parallel: one rank's local top-k candidate of one child (LightSplitInfo,
+// split_info.hpp:199-262): best local gain of a feature and its left + right count.
+struct VoteRec {
+  double gain;
+  int feature;  // -1: empty
+  int count;
 };
 
 struct SplitRec {

@@ -115,6 +115,36 @@ void DataParallelTreeLearner::SyncBestSplits() {
 }
 
 // ============================================================================
+// Global voting of voting_parallel_tree_learner.cpp:150-181 (GlobalVoting): every rank's
+// local top-k records are weighted by (left + right count) / (global leaf count / P); each
+// feature keeps its best weighted record (first in gather order on ties); the top_k
+// features by (weighted gain desc, feature asc) are elected. Returned sorted by feature.
+// Shared with the device learner, which evaluates the same rule in k_vote_pack.
+std::vector<int> ElectFeatures(const VoteRecord* recs, int num_recs, int top_k, data_size_t global_count,
+                               int num_machines) {
+  const float mean = static_cast<float>(global_count) / static_cast<float>(num_machines);
+  std::vector<std::pair<double, int>> best;  // (weighted gain, feature), first-seen order
+  for (int i = 0; i < num_recs; ++i) {
+    const VoteRecord& r = recs[i];
+    if (r.feature < 0) continue;
+    const double w = r.gain * r.count / mean;
+    auto it = std::find_if(best.begin(), best.end(), [&](const std::pair<double, int>& b) { return b.second == r.feature; });
+    if (it == best.end()) {
+      if (w > kMinScore) best.emplace_back(w, r.feature);
+    } else if (w > it->first) {
+      it->first = w;
+    }
+  }
+  std::stable_sort(best.begin(), best.end(), [](const std::pair<double, int>& a, const std::pair<double, int>& b) {
+    if (a.first != b.first) return a.first > b.first;
+    return a.second < b.second;
+  });
+  std::vector<int> out;
+  for (size_t i = 0; i < best.size() && static_cast<int>(i) < top_k; ++i) out.push_back(best[i].second);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
 void VotingParallelTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
   SerialTreeLearner::Init(train_data, is_constant_hessian);
   global_counts_from_split_ = true;
@@ -132,40 +162,22 @@ void VotingParallelTreeLearner::BeforeTrain() {
   leaf_count_global_[0] = smaller_.global_count;
 }
 
-std::vector<int> VotingParallelTreeLearner::Vote(const std::vector<SplitInfo>& local_best, int top_k) {
-  // local top-k features by gain
+std::vector<int> VotingParallelTreeLearner::Vote(const std::vector<SplitInfo>& local_best, int top_k,
+                                                data_size_t global_count) {
+  const int n = Network::num_machines();
+  // local top-k by (gain desc, feature asc): ArrayArgs::MaxK of voting_parallel_tree_learner.cpp:354
   std::vector<int> order(num_features_);
   std::iota(order.begin(), order.end(), 0);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return local_best[a].BetterThan(local_best[b]); });
-  struct Cand {
-    int feature;
-    double gain;
-  };
-  std::vector<Cand> mine(top_k, Cand{-1, kMinScore});
-  for (int i = 0; i < top_k && i < num_features_; ++i) {
-    if (local_best[order[i]].feature >= 0) mine[i] = {order[i], local_best[order[i]].gain};
+  std::vector<VoteRecord> mine(top_k);
+  for (int i = 0; i < top_k; ++i) {
+    const SplitInfo& s = local_best[order[i]];
+    if (s.feature >= 0) mine[i] = VoteRecord{s.gain, s.feature, s.left_count + s.right_count, 0};
   }
-  const int n = Network::num_machines();
-  std::vector<Cand> all(static_cast<size_t>(top_k) * n);
-  Network::Allgather(reinterpret_cast<char*>(mine.data()), static_cast<comm_size_t>(sizeof(Cand) * top_k),
+  std::vector<VoteRecord> all(static_cast<size_t>(top_k) * n);
+  Network::Allgather(reinterpret_cast<char*>(mine.data()), static_cast<comm_size_t>(sizeof(VoteRecord) * top_k),
                      reinterpret_cast<char*>(all.data()));
-  // global voting: number of votes, ties broken by summed gain then feature index
-  std::vector<double> votes(num_features_, 0.0), gains(num_features_, 0.0);
-  for (auto& c : all) {
-    if (c.feature < 0) continue;
-    votes[c.feature] += 1.0;
-    gains[c.feature] += c.gain;
-  }
-  std::vector<int> cand;
-  for (int f = 0; f < num_features_; ++f) if (votes[f] > 0) cand.push_back(f);
-  std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) {
-    if (votes[a] != votes[b]) return votes[a] > votes[b];
-    if (gains[a] != gains[b]) return gains[a] > gains[b];
-    return a < b;
-  });
-  if (static_cast<int>(cand.size()) > 2 * top_k) cand.resize(2 * top_k);
-  std::sort(cand.begin(), cand.end());
-  return cand;
+  return ElectFeatures(all.data(), static_cast<int>(all.size()), top_k, global_count, n);
 }
 
 void VotingParallelTreeLearner::ReduceGroups(const std::vector<int>& features, int leaf) {
@@ -210,9 +222,10 @@ void VotingParallelTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, b
   };
   LeafStat ls = local_stat(smaller_);
   LeafStat ll = has_larger ? local_stat(larger_) : LeafStat();
-  // local scan with min_data / min_hessian scaled by 1/num_machines
+  // local scan with min_data / min_hessian divided by num_machines (voting_parallel_tree_learner.cpp:61-63;
+  // integer division as in the reference); no split penalties in the local pass
   Config local_cfg = *config_;
-  local_cfg.min_data_in_leaf = std::max(1, config_->min_data_in_leaf / n);
+  local_cfg.min_data_in_leaf = config_->min_data_in_leaf / n;
   local_cfg.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf / n;
   const Config* saved = config_;
   config_ = &local_cfg;
@@ -223,14 +236,14 @@ void VotingParallelTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, b
     bl[f].Reset();
     if (!bytree[f]) continue;
     bool sp;
-    bs[f] = BestSplitForFeature(hs, f, ls, ParentOutput(tree, smaller_), bounds_[smaller_.leaf], &sp);
-    if (has_larger) bl[f] = BestSplitForFeature(HistOf(larger_.leaf).data(), f, ll, ParentOutput(tree, larger_),
+    bs[f] = BestSplitForFeature(hs, f, ls, ParentOutput(tree, ls), bounds_[smaller_.leaf], &sp);
+    if (has_larger) bl[f] = BestSplitForFeature(HistOf(larger_.leaf).data(), f, ll, ParentOutput(tree, ll),
                                                 bounds_[larger_.leaf], &sp);
   }
   config_ = saved;
   const int top_k = std::min(config_->top_k, num_features_);
-  std::vector<int> elected_s = Vote(bs, top_k);
-  std::vector<int> elected_l = has_larger ? Vote(bl, top_k) : std::vector<int>();
+  std::vector<int> elected_s = Vote(bs, top_k, smaller_.global_count);
+  std::vector<int> elected_l = has_larger ? Vote(bl, top_k, larger_.global_count) : std::vector<int>();
   // global histograms of the elected features only (copies, local ones stay for subtraction)
   std::vector<double> local_s = hist_[smaller_.leaf];
   std::vector<double> local_l = has_larger ? hist_[larger_.leaf] : std::vector<double>();
@@ -240,18 +253,18 @@ void VotingParallelTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, b
   best_s.Reset();
   best_l.Reset();
   std::vector<int8_t> node_s = col_sampler_.GetByNode(tree, smaller_.leaf);
+  // global pass over the elected features: global sums and counts, split penalties applied
+  // (FindBestSplitsFromHistograms of the reference's voting learner)
   for (int f : elected_s) {
     bool sp;
-    SplitInfo s = BestSplitForFeature(HistOf(smaller_.leaf).data(), f, smaller_, ParentOutput(tree, smaller_),
-                                      bounds_[smaller_.leaf], &sp);
+    SplitInfo s = ScoreFeature(tree, HistOf(smaller_.leaf).data(), f, smaller_, ParentOutput(tree, smaller_), &sp);
     if (node_s[f] && s.feature >= 0 && s.BetterThan(best_s)) best_s = s;
   }
   if (has_larger) {
     std::vector<int8_t> node_l = col_sampler_.GetByNode(tree, larger_.leaf);
     for (int f : elected_l) {
       bool sp;
-      SplitInfo s = BestSplitForFeature(HistOf(larger_.leaf).data(), f, larger_, ParentOutput(tree, larger_),
-                                        bounds_[larger_.leaf], &sp);
+      SplitInfo s = ScoreFeature(tree, HistOf(larger_.leaf).data(), f, larger_, ParentOutput(tree, larger_), &sp);
       if (node_l[f] && s.feature >= 0 && s.BetterThan(best_l)) best_l = s;
     }
   }

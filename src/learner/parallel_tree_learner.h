@@ -47,9 +47,20 @@ class VotingParallelTreeLearner : public SerialTreeLearner {
  protected:
   void BeforeTrain() override;
   void FindBestSplitsFromHistograms(const Tree* tree, bool use_subtract) override;
-  std::vector<int> Vote(const std::vector<SplitInfo>& local_best, int top_k);
+  std::vector<int> Vote(const std::vector<SplitInfo>& local_best, int top_k, data_size_t global_count);
   void ReduceGroups(const std::vector<int>& features, int leaf);
 };
+
+// One rank's local top-k candidate of the voting learner (LightSplitInfo analogue,
+// split_info.hpp:199-262): gain and left + right count of a feature's best local split.
+struct VoteRecord {
+  double gain = kMinScore;
+  int feature = -1;
+  int count = 0;
+  int pad = 0;
+};
+std::vector<int> ElectFeatures(const VoteRecord* recs, int num_recs, int top_k, data_size_t global_count,
+                               int num_machines);
 
 // Piecewise-linear leaves (linear_tree_learner.cpp): serial tree structure,
 // then a ridge fit of each leaf on its branch's numerical features.

@@ -28,7 +28,8 @@ std::unique_ptr<TreeLearner> CreateHost(const std::string& learner_type, bool li
 // Why the device-resident learner cannot serve `config` (nullptr = it can).
 const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, const Config* c) {
   if (linear_tree) return "linear_tree";
-  if (learner_type == "voting") return "voting-parallel election";
+  // (voting runs on the device; its global pass redraws no extra-trees thresholds)
+  if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
   if (CegbPenalty::Enabled(c)) return "cost-effective gradient boosting";
   if (!c->forcedsplits_filename.empty()) return "forced splits";
   if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {

@@ -244,6 +244,33 @@ def test_feature_parallel_multirank_rehearsal(lgb, gpu_required, transport):
     assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
 
 
+@pytest.mark.parametrize("world,transport,topk", [(2, "collective", 3), (3, "xgmi", 3), (2, "xgmi", 20),
+                                                  (4, "xgmi", 2)])
+def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport, topk):
+    """Device voting-parallel (PV-Tree: local scan, top-k vote all-gathered, elected features'
+    histograms summed, global scan of the elected features only), P ranks sharing the GPU: every
+    rank grows the identical model, equal to the host voting learner tree for tree."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20",
+               DP_LEARNER="voting", DP_TOPK=str(topk))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+                        "--nproc-per-node", str(world), os.path.join(root, "scripts", "dp_multirank.py")],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "voting-parallel" in res["device_name"], res
+    assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
+    assert res["ranks_identical"], res
+    assert res["num_trees"] == 10
+    assert res["identical_leading_trees"] == 10, res
+    assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
+
+
 def _policy_data(rng, n=20000):
     X = rng.standard_normal((n, 6))
     z = 1.5 * X[:, 0] - X[:, 1] + 0.7 * X[:, 2] * X[:, 3] + 0.3 * rng.standard_normal(n)
