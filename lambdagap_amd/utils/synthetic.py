@@ -96,9 +96,12 @@ def make_ranking(num_queries: int, num_features: int = 300, docs_per_query: Tupl
     return X, y, sizes
 
 
-def make_regression(n: int, num_features: int = 500, density: float = 0.1, seed: int = 0
+def make_regression(n: int, num_features: int = 500, density: float = 0.1, seed: int = 0, function_seed: int = 0
                     ) -> Tuple[np.ndarray, np.ndarray]:
-    """Wide regression data where most columns are mostly zero (exclusive-feature-bundling friendly)."""
+    """Wide regression data where most columns are mostly zero (exclusive-feature-bundling friendly).
+
+    ``seed`` draws the rows; ``function_seed`` the target's coefficients, so a held-out set drawn
+    with another ``seed`` follows the same function."""
     rng = np.random.default_rng(seed)
     X = np.zeros((n, num_features), dtype=np.float32)
     dense = min(20, num_features)
@@ -106,6 +109,7 @@ def make_regression(n: int, num_features: int = 500, density: float = 0.1, seed:
     for j in range(dense, num_features):
         mask = rng.random(n) < density
         X[mask, j] = rng.standard_normal(int(mask.sum())).astype(np.float32)
-    w = rng.standard_normal(num_features).astype(np.float32) / np.sqrt(num_features)
+    w = np.random.default_rng([function_seed, num_features]).standard_normal(num_features).astype(np.float32)
+    w /= np.sqrt(num_features)
     y = X @ w + np.sin(X[:, 0]) * X[:, 1] + 0.1 * rng.standard_normal(n).astype(np.float32)
     return X, y.astype(np.float32)

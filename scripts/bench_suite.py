@@ -28,7 +28,20 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--device", default="gpu")
+    ap.add_argument("--learner", choices=["serial", "data", "voting"], default="serial",
+                    help="data / voting on ONE GPU run through a one-rank RCCL communicator (the parallel "
+                         "learner's kernels and exchanges, single rank)")
     args = ap.parse_args()
+    if args.learner != "serial":
+        import ctypes
+
+        from lambdagap_amd.parallel import distributed as dd
+
+        uid = dd.get_unique_id()
+        dd._check(dd._LIB.LGBM_DeviceCommInit(dd._c_str(uid), ctypes.c_int64(len(uid)), ctypes.c_int(1),
+                                              ctypes.c_int(0), ctypes.c_int(0)))
+        if args.learner == "data":
+            os.environ["LGAP_FORCE_DEVICE_DP"] = "1"
 
     import numpy as np
 
@@ -49,6 +62,8 @@ def main() -> int:
         Xv, yv = make_regression(args.valid_rows, num_features=nf, seed=8)
         g = gv = None
         params = preset("regression_goss", device_type=args.device, verbosity=-1, metric="l2")
+    if args.learner == "voting":
+        params["tree_learner"] = "voting"
     gen_s = time.time() - t0
     t0 = time.time()
     train = lgb.Dataset(X, y, group=g, params=params, free_raw_data=True)
@@ -69,7 +84,7 @@ def main() -> int:
     ev = {name: round(v, 6) for _, name, v, _ in booster.eval_valid()}
     print(json.dumps({"config": args.config, "rows": rows, "features": nf, "value": round(args.steps / el, 3),
                       "unit": "iters/s", "ms_per_step": round(1000 * el / args.steps, 3), "steps": args.steps,
-                      "warmup": args.warmup, "device": booster.device_name(), "valid": ev,
+                      "warmup": args.warmup, "device": booster.device_name(), "valid": ev, "learner": args.learner,
                       "num_leaves": params["num_leaves"], "max_bin": params["max_bin"],
                       "data_gen_s": round(gen_s, 1), "construct_s": round(construct_s, 1), "data": "synthetic"}),
           flush=True)

@@ -466,16 +466,24 @@ __global__ __launch_bounds__(kRootThreads) void k_root_final(Args a, int nblocks
 // with ds_add_f32 vs 0.195 ms with ds_add_u64), so the per-block histogram is
 // accumulated in FIXED POINT:
 //   default    one ds_add_u64 per (row, group): signed g in the high 32 bits,
-//              signed h in the low 32 bits, each scaled by 2^30 / (rows_in_block *
-//              max|.|) so no partial sum can overflow; low-part borrows are undone
+//              signed h in the low 32 bits, each scaled by the largest power of two
+//              <= 2^30 / (rows_in_block * max|.|) so no partial sum can overflow (and
+//              constant hessians are exact); low-part borrows are undone
 //              when unpacking. Per-value resolution ~2^-30 * rows * max|g|, below
 //              the error of fp32 accumulation for any bin with more than a few
 //              hundred rows.
-//   gpu_use_dp two ds_add_u64 (g, h) at scale 2^62 / (rows * max|.|): ~2^-47
+//   gpu_use_dp two ds_add_u64 (g, h) at scale ~2^62 / (rows * max|.|): ~2^-47
 //              relative, indistinguishable from the CPU's double sums.
 // Each active block unpacks its LDS histogram to real values and stores it into
 // its own slab row (plain coalesced stores); k_hist_reduce sums the rows into
 // `staging` (fp64). No float atomics anywhere on the hot path.
+
+// largest power of two <= x (x > 0)
+__device__ __forceinline__ double Pow2AtMost(double x) {
+  int e;
+  (void)frexp(x, &e);  // x = m * 2^e, m in [0.5, 1)
+  return ldexp(1.0, e - 1);
+}
 
 __device__ __forceinline__ int HistActiveBlocks(int n, int grid, int min_rows) {
   int nb = (n + min_rows - 1) / min_rows;
@@ -656,12 +664,17 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   const double rows_in_block = static_cast<double>(re - rb > 0 ? re - rb : 1);
   const double kPk = 1073741824.0;            // 2^30
   const double kDp = 4611686018427387904.0;   // 2^62
-  const double sgd = gmax > 0.f ? kPk / (rows_in_block * gmax) : 1.0;
-  const double shd = hmax > 0.f ? kPk / (rows_in_block * hmax) : 1.0;
-  const double dsg = gmax > 0.f ? kDp / (rows_in_block * gmax) : 1.0;
-  const double dsh = hmax > 0.f ? kDp / (rows_in_block * hmax) : 1.0;
-  // float scales rounded down so |v * s| never exceeds the bound
-  const float sg = static_cast<float>(sgd) * 0.99999f, sh = static_cast<float>(shd) * 0.99999f;
+  // Scales are POWERS OF TWO (the largest not above the overflow bound): scaling is then an
+  // exponent shift, de-scaling is exact, and a value with few significant bits (a constant
+  // hessian: l2, quantile, ...) is quantized exactly. A non-power-of-two scale rounded every
+  // h = 1 the same way: a systematic relative bias of up to 0.5 / scale that the
+  // parent - smaller subtraction carried, as an absolute error of the root-size bins, into
+  // small deep leaves (near-zero or negative hessian sums, exploding outputs at ~8M rows).
+  const double sgd = gmax > 0.f ? Pow2AtMost(kPk / (rows_in_block * gmax)) : 1.0;
+  const double shd = hmax > 0.f ? Pow2AtMost(kPk / (rows_in_block * hmax)) : 1.0;
+  const double dsg = gmax > 0.f ? Pow2AtMost(kDp / (rows_in_block * gmax)) : 1.0;
+  const double dsh = hmax > 0.f ? Pow2AtMost(kDp / (rows_in_block * hmax)) : 1.0;
+  const float sg = static_cast<float>(sgd), sh = static_cast<float>(shd);
   const int words = MODE == 0 ? tile.nbins : 2 * tile.nbins;
   unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
   int* gst = reinterpret_cast<int*>(hist + words);
@@ -670,7 +683,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
   __syncthreads();
   Stamp(a, 2, 1);
   double tg, th;
-  HistRowsFixed<W, MODE>(a, tile, r, cls, rb, re, gst, hist, sg, sh, dsg * 0.99999, dsh * 0.99999, &tg, &th);
+  HistRowsFixed<W, MODE>(a, tile, r, cls, rb, re, gst, hist, sg, sh, dsg, dsh, &tg, &th);
   __syncthreads();
   PublishRowSums(a, tg, th);
   Stamp(a, 2, 2);
@@ -684,7 +697,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
       slabf[2 * i + 1] = static_cast<float>(static_cast<double>(hs) * ih);
     }
   } else {
-    const double ig = 1.0 / (dsg * 0.99999), ih = 1.0 / (dsh * 0.99999);
+    const double ig = 1.0 / dsg, ih = 1.0 / dsh;
     for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
       slab[2 * i] = static_cast<double>(static_cast<long long>(hist[2 * i])) * ig;
       slab[2 * i + 1] = static_cast<double>(static_cast<long long>(hist[2 * i + 1])) * ih;

@@ -136,13 +136,24 @@ class DevBuf {
   }
   T* get() const { return ptr_; }
   size_t size() const { return n_; }
+  // Copies are issued in chunks of at most kCopyChunk bytes: a single pageable copy of more
+  // than 4 GiB (rowbins / colbins of a wide 10M-row dataset) arrived incomplete on MI355X.
+  static constexpr size_t kCopyChunk = size_t(1) << 30;
   void Upload(const T* host, size_t n, hipStream_t s = 0) {
     if (n > n_) Resize(n);
-    if (n) HIP_CHECK(hipMemcpyAsync(ptr_, host, n * sizeof(T), hipMemcpyHostToDevice, s));
+    const char* src = reinterpret_cast<const char*>(host);
+    char* dst = reinterpret_cast<char*>(ptr_);
+    for (size_t off = 0, bytes = n * sizeof(T); off < bytes; off += kCopyChunk) {
+      HIP_CHECK(hipMemcpyAsync(dst + off, src + off, std::min(kCopyChunk, bytes - off), hipMemcpyHostToDevice, s));
+    }
   }
   void Upload(const std::vector<T>& v, hipStream_t s = 0) { Upload(v.data(), v.size(), s); }
   void Download(T* host, size_t n, hipStream_t s = 0) const {
-    if (n) HIP_CHECK(hipMemcpyAsync(host, ptr_, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    char* dst = reinterpret_cast<char*>(host);
+    const char* src = reinterpret_cast<const char*>(ptr_);
+    for (size_t off = 0, bytes = n * sizeof(T); off < bytes; off += kCopyChunk) {
+      HIP_CHECK(hipMemcpyAsync(dst + off, src + off, std::min(kCopyChunk, bytes - off), hipMemcpyDeviceToHost, s));
+    }
   }
   void Zero(hipStream_t s = 0) {
     if (n_) HIP_CHECK(hipMemsetAsync(ptr_, 0, n_ * sizeof(T), s));

@@ -44,6 +44,29 @@ def test_histogram_kernel_matches_torch(lgb, gpu_required, rng, max_bin):
     np.testing.assert_allclose(out2, ref2, rtol=2e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("n", [300_007, 1_234_567])
+def test_histogram_constant_hessian_is_exact(lgb, gpu_required, rng, n):
+    """Constant hessians (l2, quantile, ...) must histogram EXACTLY: the fixed-point scales are
+    powers of two, so h = 1 quantizes without rounding and every bin's hessian is its row
+    count. A non-power-of-two scale biased every row alike, and parent - smaller subtraction
+    carried the root's error into small deep leaves (diverging l2 training at ~8M rows)."""
+    from lambdagap_amd import ops
+
+    X = rng.standard_normal((n, 6)).astype(np.float32)
+    ds = lgb.Dataset(X, params={"max_bin": 63, "verbosity": -1}).construct()
+    ng, tb, bw, starts = ops.group_layout(ds)
+    bins = ops.group_bins(ds)
+    g = rng.standard_normal(n).astype(np.float32)
+    h = np.ones(n, dtype=np.float32)
+    for rows in (None, np.sort(rng.choice(n, n // 3, replace=False)).astype(np.int32)):
+        out = ops.device_histogram(ds, g, h, rows)
+        b = bins if rows is None else bins[rows]
+        for k in range(ng):
+            cnt = np.bincount(b[:, k], minlength=64)
+            nb = (starts[k + 1] if k + 1 < ng else tb) - starts[k]
+            np.testing.assert_array_equal(out[starts[k] + 1:starts[k] + nb, 1], cnt[1:nb])
+
+
 def test_binary_gradient_kernel_matches_torch(lgb, gpu_required, rng):
     import torch
     from lambdagap_amd import ops

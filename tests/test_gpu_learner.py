@@ -86,6 +86,27 @@ def test_auc_parity_with_cpu_oracle(lgb, gpu_required):
     assert abs(ac - ag) <= 1e-3, (ac, ag)
 
 
+def test_fixed_point_vs_fp64_histograms_auc_1m(lgb, gpu_required):
+    """Precision of the default fixed-point histograms at scale: 1M Higgs-shape rows, 63 leaves,
+    30 iterations; held-out AUC of the fixed-point learner, of gpu_use_dp=true (fp64) and of the
+    CPU oracle on the same bins agree within 1e-3 (docs/GPU-Performance.rst:136 tolerance)."""
+    from lambdagap_amd.utils import make_higgs_like
+
+    X, y = make_higgs_like(1_000_000, seed=21)
+    Xv, yv = make_higgs_like(200_000, seed=22)
+    base = {"objective": "binary", "num_leaves": 63, "learning_rate": 0.1, "min_data_in_leaf": 1,
+            "min_sum_hessian_in_leaf": 100, "verbosity": -1}
+    ds = lgb.Dataset(X, y, params=dict(base, device_type="cpu"), free_raw_data=False).construct()
+    aucs = {}
+    for name, extra in (("fixed", {"device_type": "gpu"}), ("fp64", {"device_type": "gpu", "gpu_use_dp": True}),
+                        ("cpu", {"device_type": "cpu"})):
+        b = lgb.train(dict(base, **extra), ds, 30, keep_training_booster=True)
+        aucs[name] = _auc(yv, b.predict(Xv))
+    assert abs(aucs["fixed"] - aucs["fp64"]) < 1e-3, aucs
+    assert abs(aucs["fixed"] - aucs["cpu"]) < 1e-3, aucs
+    assert abs(aucs["fp64"] - aucs["cpu"]) < 1e-3, aucs
+
+
 @pytest.mark.parametrize("objective,extra", [("regression", {}), ("huber", {"alpha": 0.8}),
                                              ("poisson", {}), ("multiclass", {"num_class": 3}),
                                              ("regression_l1", {})])
