@@ -48,6 +48,8 @@ class ObjectiveFunction {
   virtual DeviceGradKind device_kind() const { return DeviceGradKind::kHostOnly; }
   // pointwise objectives: formula parameters, (possibly transformed) labels, MAPE label weights
   virtual const PointwiseParams* pointwise() const { return nullptr; }
+  // per-class pointwise parameters (multiclassova: class k's binary objective)
+  virtual const PointwiseParams* pointwise_class(int k) const { return k == 0 ? pointwise() : nullptr; }
   virtual const label_t* effective_label() const { return nullptr; }
   virtual const label_t* aux_weight() const { return nullptr; }
   virtual int num_class() const { return 1; }
@@ -67,6 +69,7 @@ struct LambdarankTables {
   const std::vector<double>* inv_max_dcg;
   const std::vector<double>* inv_max_bdcg;
   const std::vector<double>* table;
+  double pos_lr, pos_reg;  // position-bias Newton step (learning_rate, lambdarank_position_bias_regularization)
 };
 bool GetLambdarankTables(const ObjectiveFunction* obj, LambdarankTables* out);
 // objective_seed of a rank_xendcg objective (its per-query Random streams start at seed + q)

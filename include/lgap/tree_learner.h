@@ -63,6 +63,15 @@ class TreeLearner {
   virtual void DeviceGetScore(std::vector<double>*) const {}
   virtual void DeviceGetGradients(std::vector<score_t>*, std::vector<score_t>*) const {}
   // Row sampling drawn on the device from the device-resident gradients.
+  // L1 / quantile / MAPE leaf renewal from the device-resident score and partition
+  // (false: not handled, the host renews from a downloaded score)
+  virtual bool DeviceRenewTreeOutput(Tree*, const ObjectiveFunction*, int /*class_id*/) { return false; }
+  // Refit of an existing tree from the device-resident gradients of class k; also updates the
+  // device score by the change of the leaf outputs (nullptr: not handled)
+  virtual std::unique_ptr<Tree> DeviceFitByExistingTree(const Tree*, const std::vector<int>& /*leaf_pred*/,
+                                                        int /*class_id*/) {
+    return nullptr;
+  }
   virtual bool SupportsDeviceSampling() const { return false; }
   virtual void DeviceSample(int plan, int iter) { (void)plan; (void)iter; }
   virtual std::string DeviceName() const { return "cpu"; }

@@ -285,7 +285,8 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
     }
     if (tree->num_leaves() > 1) {
       should_continue = true;
-      if (objective_ && objective_->IsRenewTreeOutput()) {
+      if (objective_ && objective_->IsRenewTreeOutput() &&
+          !(device_mode_ && learner_->DeviceRenewTreeOutput(tree.get(), objective_, k))) {
         int64_t len;
         const double* score = GetTrainingScore(&len);
         learner_->RenewTreeOutput(tree.get(), objective_, score + off, num_data_, sampler_->bag_indices().data(),
@@ -490,10 +491,28 @@ void GBDT::RefitTree(const std::vector<std::vector<int>>& leaf_preds) {
       const int m = it * num_tree_per_iteration_ + k;
       for (data_size_t i = 0; i < num_data_; ++i) leaf_pred[i] = leaf_preds[i][m];
       const size_t off = static_cast<size_t>(k) * num_data_;
+      if (device_mode_) {
+        // device-resident gradients and score (Boosting() left the gradients on the device)
+        auto nt = learner_->DeviceFitByExistingTree(models_[m].get(), leaf_pred, k);
+        if (nt) {
+          models_[m] = std::move(nt);
+          train_score_stale_ = true;
+          continue;
+        }
+        learner_->DeviceGetGradients(&gradients_, &hessians_);
+      }
       auto nt = learner_->FitByExistingTree(models_[m].get(), leaf_pred, gradients_.data() + off, hessians_.data() + off);
       // train score: refit tree replaces the old one
-      double* s = train_score_.data() + off;
-      for (data_size_t i = 0; i < num_data_; ++i) s[i] += nt->LeafOutput(leaf_pred[i]) - models_[m]->LeafOutput(leaf_pred[i]);
+      if (device_mode_) {
+        learner_->DeviceAddTreeToScore(nt.get(), k);
+        Tree neg(*models_[m]);
+        neg.Shrinkage(-1.0);
+        learner_->DeviceAddTreeToScore(&neg, k);
+        train_score_stale_ = true;
+      } else {
+        double* s = train_score_.data() + off;
+        for (data_size_t i = 0; i < num_data_; ++i) s[i] += nt->LeafOutput(leaf_pred[i]) - models_[m]->LeafOutput(leaf_pred[i]);
+      }
       models_[m] = std::move(nt);
     }
   }

@@ -47,6 +47,7 @@
 
 #include "device/grad_kernels.h"
 #include "device/hip_common.h"
+#include "device/leaf_kernels.h"
 #include "device/runtime_internal.h"
 #include "device/sample_kernels.h"
 #include "device/tree_kernels.h"
@@ -2929,6 +2930,106 @@ class DeviceTreeLearner : public TreeLearner {
     return host.FitByExistingTree(old_tree, leaf_pred, g, h);
   }
 
+  // Refit on the device (reference cuda_single_gpu_tree_learner.cu:19-78): leaf sums of the
+  // device gradients over the leaf assignment, the host's output formula, and the score
+  // delta of the new outputs applied on the device.
+  std::unique_ptr<Tree> DeviceFitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
+                                                int class_id) override {
+    ScopedTimer timer("Device::Refit");
+    if (static_cast<data_size_t>(leaf_pred.size()) != N_ || gh_.size() < static_cast<size_t>(class_id + 1) * N_) {
+      return nullptr;
+    }
+    const int L = old_tree->num_leaves();
+    leaf_pred_dev_.Upload(leaf_pred, stream_);
+    refit_partial_.Resize(static_cast<size_t>(RefitPartialBlocks(N_)) * 3 * L);
+    refit_sums_.Resize(3 * static_cast<size_t>(L));
+    LaunchRefitLeafSums(gh_.get() + static_cast<size_t>(class_id) * N_, leaf_pred_dev_.get(), N_, L,
+                        refit_partial_.get(), refit_sums_.get(), stream_);
+    std::vector<double> sums(3 * static_cast<size_t>(L));
+    refit_sums_.Download(sums.data(), sums.size(), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    auto tree = std::make_unique<Tree>(*old_tree);
+    SplitParams p = MakeArgs().sp;
+    std::vector<double> delta(L);
+    for (int i = 0; i < L; ++i) {
+      const double sg = sums[3 * i], sh = kEpsilon + sums[3 * i + 1];
+      const data_size_t n = static_cast<data_size_t>(sums[3 * i + 2] + 0.5);
+      double out;
+      if (config_->path_smooth > kEpsilon && i > 0) {
+        out = LeafOutputRaw(sg, sh, p, n, tree->leaf_parent(i));  // (the reference passes leaf_parent)
+      } else {
+        SplitParams q = p;
+        q.path_smooth = 0.0;
+        out = LeafOutputRaw(sg, sh, q, n, 0.0);
+      }
+      const double old_v = tree->LeafOutput(i);
+      const double new_v = config_->refit_decay_rate * old_v + (1.0 - config_->refit_decay_rate) * out * tree->shrinkage();
+      tree->SetLeafOutput(i, new_v);
+      delta[i] = new_v - old_v;
+    }
+    refit_delta_.Upload(delta, stream_);
+    LaunchAddLeafDelta(score_.get() + static_cast<size_t>(class_id) * N_, leaf_pred_dev_.get(), refit_delta_.get(), N_,
+                       stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return tree;
+  }
+
+  // L1 / quantile / MAPE leaf renewal on the device: residual percentiles over the final leaf
+  // ranges of the tree just grown (bagged rows only, as the partition holds them).
+  bool DeviceRenewTreeOutput(Tree* tree, const ObjectiveFunction* obj, int class_id) override {
+    if (obj == nullptr || !obj->IsRenewTreeOutput()) return true;
+    const PointwiseParams* pp = obj->pointwise();
+    const int nl = tree->num_leaves();
+    if (pp == nullptr || obj->effective_label() == nullptr || static_cast<int>(h_range_.size()) != nl) return false;
+    ScopedTimer timer("Device::RenewTreeOutput");
+    PrepareObjective(obj);
+    std::vector<LeafSeg> segs(nl);
+    std::vector<int> off(nl + 1, 0);
+    for (int l = 0; l < nl; ++l) {
+      segs[l].buf = h_range_[l].buf;
+      segs[l].start = h_range_[l].start;
+      segs[l].count = h_range_[l].count;
+      segs[l].pad = 0;
+      off[l + 1] = off[l] + h_range_[l].count;
+    }
+    const int total = off[nl];
+    renew_segs_.Upload(segs, stream_);
+    renew_off_.Upload(off, stream_);
+    RenewArgs ra;
+    ra.score = score_.get() + static_cast<size_t>(class_id) * N_;
+    ra.label = label_.get();
+    ra.weight = pp->kind == kPwMape ? aux_.get() : (weight_.size() ? weight_.get() : nullptr);
+    ra.idx0 = idx_[0].get();
+    ra.idx1 = idx_[1].get();
+    ra.idx2 = idx_[2].get();
+    ra.segs = renew_segs_.get();
+    ra.seg_off = renew_off_.get();
+    ra.num_leaves = nl;
+    ra.alpha = pp->kind == kPwQuantile ? pp->alpha : 0.5;
+    const size_t bytes = RenewScratchBytes(total, nl);
+    if (renew_scratch_.size() < bytes) renew_scratch_.Resize(bytes);
+    renew_out_.Resize(std::max<size_t>(renew_out_.size(), nl));
+    renew_nz_.Resize(std::max<size_t>(renew_nz_.size(), nl));
+    LaunchRenewLeaves(ra, total, renew_scratch_.get(), renew_scratch_.size(), renew_out_.get(), renew_nz_.get(),
+                      stream_);
+    std::vector<double> outs(nl);
+    std::vector<int> nonzero(nl);
+    renew_out_.Download(outs.data(), nl, stream_);
+    renew_nz_.Download(nonzero.data(), nl, stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int l = 0; l < nl; ++l) {
+      if (!nonzero[l]) outs[l] = 0.0;
+    }
+    if (Network::num_machines() > 1) {
+      // the reference averages the per-machine renewed outputs (serial_tree_learner.cpp:947-960)
+      Network::GlobalSum(&outs);
+      Network::GlobalSum(&nonzero);
+      for (int l = 0; l < nl; ++l) outs[l] = nonzero[l] > 0 ? outs[l] / nonzero[l] : 0.0;
+    }
+    for (int l = 0; l < nl; ++l) tree->SetLeafOutput(l, outs[l]);
+    return true;
+  }
+
   void AddPredictionToScore(const Tree* tree, double* out_score) const override {
     tree->AddPredictionToScore(*data_, N_, out_score);
   }
@@ -2977,16 +3078,14 @@ class DeviceTreeLearner : public TreeLearner {
         return obj->pointwise() != nullptr && obj->effective_label() != nullptr;
       case DeviceGradKind::kSoftmax:
         return obj->effective_label() != nullptr;
+      case DeviceGradKind::kOVA:
+        return obj->effective_label() != nullptr && obj->pointwise_class(0) != nullptr;
       case DeviceGradKind::kLambdarank:
-      case DeviceGradKind::kXendcg: {
-        const Metadata& md = data_->metadata();
-        if (md.positions() != nullptr || md.num_queries() == 0) return false;
-        const data_size_t* qb = md.query_boundaries();
-        for (data_size_t q = 0; q < md.num_queries(); ++q) {
-          if (qb[q + 1] - qb[q] > kMaxDeviceQuery) return false;
-        }
-        return true;
-      }
+        // any query length (long queries in global scratch), position bias included
+        return data_->metadata().num_queries() > 0;
+      case DeviceGradKind::kXendcg:
+        // (position-biased rank_xendcg stays on the host)
+        return data_->metadata().num_queries() > 0 && data_->metadata().positions() == nullptr;
       default:
         return false;
     }
@@ -3013,11 +3112,19 @@ class DeviceTreeLearner : public TreeLearner {
         LaunchSoftmaxGrad(K_, static_cast<double>(K_) / (K_ - 1.0), score_.get(), label_.get(),
                           weight_.size() ? weight_.get() : nullptr, N_, gh_.get(), stream_);
         break;
+      case DeviceGradKind::kOVA:
+        LaunchOvaGrad(K_, ova_params_.get(), score_.get(), label_.get(), weight_.size() ? weight_.get() : nullptr, N_,
+                      gh_.get(), stream_);
+        break;
       case DeviceGradKind::kLambdarank: {
         RankKernelArgs ra = rank_args_;
         ra.score = score_.get();
         ra.gh = gh_.get();
         LaunchLambdarankGrad(ra, stream_);
+        if (ra.positions) {
+          LaunchPositionBiasUpdate(gh_.get(), ra.positions, N_, num_pos_ids_, pos_lr_, pos_reg_, pos_acc_.get(),
+                                   pos_bias_.get(), stream_);
+        }
         break;
       }
       case DeviceGradKind::kXendcg: {
@@ -4035,6 +4142,35 @@ class DeviceTreeLearner : public TreeLearner {
     }
   }
 
+  // Queries longer than kMaxDeviceQuery: their list and per-query slices of global scratch.
+  void SetupLongQueries(const Metadata& md, bool xendcg, int* num, const int** list, const long long** off,
+                        char** scratch) {
+    std::vector<int> lq;
+    std::vector<long long> lo;
+    long long bytes = 0;
+    const data_size_t* qb = md.query_boundaries();
+    for (data_size_t q = 0; q < md.num_queries(); ++q) {
+      const int cnt = qb[q + 1] - qb[q];
+      if (cnt <= kMaxDeviceQuery) continue;
+      lq.push_back(q);
+      lo.push_back(bytes);
+      bytes += static_cast<long long>(xendcg ? XendcgGlobalBytes(cnt) : RankGlobalBytes(cnt));
+    }
+    *num = static_cast<int>(lq.size());
+    *list = nullptr;
+    *off = nullptr;
+    *scratch = nullptr;
+    if (lq.empty()) return;
+    long_q_.Upload(lq, stream_);
+    long_off_.Upload(lo, stream_);
+    long_scratch_.Resize(static_cast<size_t>(bytes));
+    *list = long_q_.get();
+    *off = long_off_.get();
+    *scratch = long_scratch_.get();
+    Log::Debug("HIP %s: %d queries longer than %d documents use %lld bytes of global scratch",
+               xendcg ? "rank_xendcg" : "lambdarank", *num, kMaxDeviceQuery, bytes);
+  }
+
   void PrepareObjective(const ObjectiveFunction* obj) {
     if (obj == prepared_obj_) return;
     prepared_obj_ = obj;
@@ -4045,6 +4181,11 @@ class DeviceTreeLearner : public TreeLearner {
     else weight_.Free();
     if (obj->aux_weight()) aux_.Upload(obj->aux_weight(), N_, stream_);
     else aux_.Free();
+    if (obj->device_kind() == DeviceGradKind::kOVA) {
+      std::vector<PointwiseParams> pp(std::max(1, obj->num_class()));
+      for (int k = 0; k < obj->num_class(); ++k) pp[k] = *obj->pointwise_class(k);
+      ova_params_.Upload(pp, stream_);
+    }
     if (obj->device_kind() == DeviceGradKind::kLambdarank) {
       LambdarankTables t;
       if (!GetLambdarankTables(obj, &t)) Log::Fatal("lambdarank tables unavailable");
@@ -4076,6 +4217,23 @@ class DeviceTreeLearner : public TreeLearner {
       }
       r.label = label_.get();
       r.weight = weight_.size() ? weight_.get() : nullptr;
+      // unbiased LTR: positions and the learned biases live on the device
+      r.positions = nullptr;
+      r.pos_bias = nullptr;
+      if (md.positions() != nullptr && md.num_position_ids() > 0) {
+        num_pos_ids_ = md.num_position_ids();
+        pos_lr_ = t.pos_lr;
+        pos_reg_ = t.pos_reg;
+        std::vector<int> pos(md.positions(), md.positions() + N_);
+        positions_.Upload(pos, stream_);
+        pos_bias_.Resize(num_pos_ids_);
+        pos_bias_.Zero(stream_);
+        pos_acc_.Resize(3 * static_cast<size_t>(num_pos_ids_));
+        pos_acc_.Zero(stream_);
+        r.positions = positions_.get();
+        r.pos_bias = pos_bias_.get();
+      }
+      SetupLongQueries(md, /*xendcg=*/false, &r.num_large, &r.large_q, &r.large_off, &r.large_scratch);
     }
     if (obj->device_kind() == DeviceGradKind::kXendcg) {
       int seed = 0;
@@ -4091,6 +4249,7 @@ class DeviceTreeLearner : public TreeLearner {
       x.label = label_.get();
       x.weight = weight_.size() ? weight_.get() : nullptr;
       x.state = xendcg_state_.get();
+      SetupLongQueries(md, /*xendcg=*/true, &x.num_large, &x.large_q, &x.large_off, &x.large_scratch);
     }
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
@@ -4190,6 +4349,19 @@ class DeviceTreeLearner : public TreeLearner {
   RankKernelArgs rank_args_;
   DevBuf<unsigned> xendcg_state_;
   DevBuf<int> row_query_;  // bagging by query: query of each row
+  // refit / leaf renewal
+  DevBuf<int> leaf_pred_dev_, renew_off_, renew_nz_;
+  DevBuf<double> refit_partial_, refit_sums_, refit_delta_, renew_out_;
+  DevBuf<LeafSeg> renew_segs_;
+  DevBuf<char> renew_scratch_;
+  // multiclassova / unbiased LTR / long queries
+  DevBuf<PointwiseParams> ova_params_;
+  DevBuf<int> positions_, long_q_;
+  DevBuf<float> pos_bias_;
+  DevBuf<long long> pos_acc_, long_off_;
+  DevBuf<char> long_scratch_;
+  int num_pos_ids_ = 0;
+  double pos_lr_ = 0.0, pos_reg_ = 0.0;
   // device training metrics
   static constexpr int kMetricBlocks = 1024;
   DevBuf<float> metric_label_, metric_weight_;

@@ -16,6 +16,11 @@ void LaunchPointwiseGrad(const PointwiseParams& p, const double* score, const fl
 void LaunchSoftmaxGrad(int num_class, double factor, const double* score, const float* label, const float* weight,
                        int n, float2* gh, hipStream_t s);
 
+// multiclassova: one binary objective per class over the one-hot labels (label == k);
+// params[k] carries class k's label weights (is_unbalance / scale_pos_weight)
+void LaunchOvaGrad(int num_class, const PointwiseParams* params_dev, const double* score, const float* label,
+                   const float* weight, int n, float2* gh, hipStream_t s);
+
 constexpr int kMaxDeviceQueryDecl = 2048;
 struct RankKernelArgs {
   int target = 0;
@@ -37,10 +42,27 @@ struct RankKernelArgs {
   const float* weight = nullptr;
   const double* score = nullptr;
   float2* gh = nullptr;
+  // unbiased LambdaRank (rank_objective.hpp:554-591): score + bias[position] ranks the documents
+  const int* positions = nullptr;  // per row, nullptr: no position bias
+  const float* pos_bias = nullptr;
+  // queries longer than kMaxDeviceQuery: their block works in global scratch
+  int num_large = 0;
+  const int* large_q = nullptr;          // the long queries
+  const long long* large_off = nullptr;  // byte offset of each one's scratch
+  char* large_scratch = nullptr;
 };
-// Largest query the block-per-query kernel handles (LDS-resident sort).
+// Largest query whose sort / accumulators live in LDS (longer ones use global scratch).
 constexpr int kMaxDeviceQuery = 2048;
+// global scratch bytes of one long query of `cnt` documents (lambdarank / xendcg)
+size_t RankGlobalBytes(int cnt);
+size_t XendcgGlobalBytes(int cnt);
 void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s);
+
+// Position-bias Newton step after the lambdas (rank_objective.hpp UpdatePositionBias):
+// per position d1 -= g, d2 -= h, cnt += 1, then bias += lr * (d1 - bias * reg * cnt) /
+// (|d2 - reg * cnt| + 0.001). `acc` holds 3 * num_pos int64 fixed-point sums.
+void LaunchPositionBiasUpdate(const float2* gh, const int* positions, int n, int num_pos, double lr, double reg,
+                              long long* acc, float* bias, hipStream_t s);
 
 struct XendcgArgs {
   const int* qb = nullptr;  // query boundaries (num_queries + 1)
@@ -50,6 +72,10 @@ struct XendcgArgs {
   const double* score = nullptr;
   unsigned* state = nullptr;  // per-query LCG state (Random(objective_seed + q))
   float2* gh = nullptr;
+  int num_large = 0;  // queries longer than kMaxDeviceQuery (global scratch, as RankKernelArgs)
+  const int* large_q = nullptr;
+  const long long* large_off = nullptr;
+  char* large_scratch = nullptr;
 };
 void LaunchXendcgGrad(const XendcgArgs& a, hipStream_t s);
 

@@ -2,8 +2,10 @@
 //  * pointwise objectives: one thread per row, formulas shared with the host
 //    objectives through lgap/pointwise.h (so both paths give the same numbers);
 //  * multiclass softmax: one thread per row over the K class scores;
-//  * lambdarank (all 18 `lambdarank_target`s): one 256-thread workgroup per
-//    query. The query's scores are bitonic-sorted in LDS (score desc, index
+//  * multiclassova: one binary objective per class over one-hot labels;
+//  * lambdarank (all 18 `lambdarank_target`s, position-biased scores for unbiased
+//    LTR): one 256-thread workgroup per query (queries beyond kMaxDeviceQuery
+//    documents in global scratch). The query's scores are bitonic-sorted in LDS (score desc, index
 //    asc == std::stable_sort), the (i, j) pair space of the target is
 //    flattened with an LDS prefix sum so every lane gets equal work, and the
 //    per-document lambdas/hessians accumulate with LDS float atomics.
@@ -62,6 +64,22 @@ __global__ __launch_bounds__(256) void k_softmax(int K, double factor, const dou
   }
 }
 
+__global__ __launch_bounds__(256) void k_ova(int K, const PointwiseParams* __restrict__ params,
+                                             const double* __restrict__ score, const float* __restrict__ label,
+                                             const float* __restrict__ weight, int n, float2* __restrict__ gh) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int y = static_cast<int>(label[i]);
+    const double w = weight ? static_cast<double>(weight[i]) : 1.0;
+    for (int k = 0; k < K; ++k) {
+      score_t g, h;
+      PointwiseGradient(params[k], score[static_cast<size_t>(k) * n + i], y == k ? 1.0 : 0.0, w, weight != nullptr,
+                        0.0, &g, &h);
+      gh[static_cast<size_t>(k) * n + i] = make_float2(g, h);
+    }
+  }
+}
+
 __global__ void k_add_constant(double* score, int n, double v) {
   const int stride = gridDim.x * blockDim.x;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) score[i] += v;
@@ -104,23 +122,21 @@ inline size_t RankLdsBytes(int max_cnt) {
          static_cast<size_t>(P + 1) * sizeof(int);
 }
 
+// kGlobal = false: one block per query, arrays in LDS sized by the dataset's largest query up
+// to kMaxDeviceQuery (short queries then fit many blocks per CU); longer queries are skipped
+// and handled by the kGlobal = true launch (one block per long query, the same arrays in its
+// own slice of global scratch; the integer accumulators become global atomics).
+template <bool kGlobal>
 __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, int Pmax) {
-  // dynamic LDS sized by the dataset's largest query (not kMaxDeviceQuery): short queries
-  // then fit many blocks per CU
   extern __shared__ __align__(8) unsigned char s_dyn[];
-  double* s_score = reinterpret_cast<double*>(s_dyn);
-  unsigned long long* s_lam = reinterpret_cast<unsigned long long*>(s_score + Pmax);
-  unsigned long long* s_hes = s_lam + Pmax;
-  int* s_idx = reinterpret_cast<int*>(s_hes + Pmax);
-  float* s_lab = reinterpret_cast<float*>(s_idx + Pmax);
-  int* s_off = reinterpret_cast<int*>(s_lab + Pmax);
   __shared__ double s_red[kRankThreads / kWave];
   __shared__ int s_redi[kRankThreads / kWave];
 
-  const int q = blockIdx.x;
+  const int q = kGlobal ? a.large_q[blockIdx.x] : static_cast<int>(blockIdx.x);
   const int t = threadIdx.x;
   const int start = a.qb[q];
   const int cnt = a.qb[q + 1] - start;
+  if (!kGlobal && cnt > kMaxDeviceQuery) return;
   float2* out = a.gh + start;
   if (cnt <= 1) {
     for (int i = t; i < cnt; i += blockDim.x) out[i] = make_float2(0.f, 0.f);
@@ -128,10 +144,19 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
   }
   int P = 1;
   while (P < cnt) P <<= 1;
+  const int Pa = kGlobal ? P : Pmax;  // array length
+  unsigned char* base = kGlobal ? reinterpret_cast<unsigned char*>(a.large_scratch + a.large_off[blockIdx.x]) : s_dyn;
+  double* s_score = reinterpret_cast<double*>(base);
+  unsigned long long* s_lam = reinterpret_cast<unsigned long long*>(s_score + Pa);
+  unsigned long long* s_hes = s_lam + Pa;
+  int* s_idx = reinterpret_cast<int*>(s_hes + Pa);
+  float* s_lab = reinterpret_cast<float*>(s_idx + Pa);
+  int* s_off = reinterpret_cast<int*>(s_lab + Pa);
   const bool full_sort = TargetNeedsFullSort(a.target) || a.target == kTgtPrecision;
   for (int i = t; i < P; i += blockDim.x) {
     if (i < cnt) {
-      s_score[i] = a.score[start + i];
+      // unbiased LTR ranks by score + the position's learned bias (host: adj[j])
+      s_score[i] = a.positions ? a.score[start + i] + a.pos_bias[a.positions[start + i]] : a.score[start + i];
       s_lab[i] = a.label[start + i];
       s_lam[i] = 0ull;
       s_hes[i] = 0ull;
@@ -294,15 +319,25 @@ int GridFor(int n) {
 // the lambdas match the host objective's sequential sums; the per-document
 // terms run on all lanes from LDS. state[q] is the query's Random, advanced by
 // cnt draws per call exactly like the host's rands_[q].
+template <bool kGlobal>
 __global__ __launch_bounds__(kRankThreads) void k_xendcg(XendcgArgs a) {
-  __shared__ double s_rho[kMaxDeviceQuery];
-  __shared__ double s_p[kMaxDeviceQuery];
-  __shared__ float s_lam[kMaxDeviceQuery];
+  __shared__ double l_rho[kGlobal ? 1 : kMaxDeviceQuery];
+  __shared__ double l_p[kGlobal ? 1 : kMaxDeviceQuery];
+  __shared__ float l_lam[kGlobal ? 1 : kMaxDeviceQuery];
   __shared__ double s_v[3];
-  const int q = blockIdx.x;
+  const int q = kGlobal ? a.large_q[blockIdx.x] : static_cast<int>(blockIdx.x);
   const int t = threadIdx.x;
   const int start = a.qb[q];
   const int cnt = a.qb[q + 1] - start;
+  if (!kGlobal && cnt > kMaxDeviceQuery) return;  // the long-query launch handles it
+  double* s_rho = l_rho;
+  double* s_p = l_p;
+  float* s_lam = l_lam;
+  if (kGlobal) {
+    s_rho = reinterpret_cast<double*>(a.large_scratch + a.large_off[blockIdx.x]);
+    s_p = s_rho + cnt;
+    s_lam = reinterpret_cast<float*>(s_p + cnt);
+  }
   float2* out = a.gh + start;
   const double* score = a.score + start;
   const float* label = a.label + start;
@@ -404,7 +439,75 @@ __global__ __launch_bounds__(kWave) void k_metric_fold(const double* __restrict_
   if (threadIdx.x == 0) *out = acc;
 }
 
+// Position-bias statistics: per-position (-sum g, -sum h, count) as int64 fixed point
+// (order independent), then one block applies the Newton step.
+constexpr double kPosScale = 4294967296.0;  // 2^32
+constexpr int kPosLds = 1024;
+
+__global__ __launch_bounds__(256) void k_pos_accum(const float2* __restrict__ gh, const int* __restrict__ positions, int n,
+                                                   int num_pos, long long* __restrict__ acc) {
+  __shared__ unsigned long long s[3 * kPosLds];
+  const bool lds = num_pos <= kPosLds;
+  if (lds) {
+    for (int i = threadIdx.x; i < 3 * num_pos; i += blockDim.x) s[i] = 0ull;
+    __syncthreads();
+  }
+  unsigned long long* dst = lds ? s : reinterpret_cast<unsigned long long*>(acc);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int p = positions[i];
+    const float2 v = gh[i];
+    atomicAdd(&dst[3 * p], static_cast<unsigned long long>(__double2ll_rn(-static_cast<double>(v.x) * kPosScale)));
+    atomicAdd(&dst[3 * p + 1], static_cast<unsigned long long>(__double2ll_rn(-static_cast<double>(v.y) * kPosScale)));
+    atomicAdd(&dst[3 * p + 2], 1ull);
+  }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * num_pos; i += blockDim.x) {
+      if (s[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[i]), s[i]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pos_update(long long* __restrict__ acc, int num_pos, double lr, double reg,
+                                                    float* __restrict__ bias) {
+  for (int p = threadIdx.x; p < num_pos; p += blockDim.x) {
+    const double d1 = static_cast<double>(acc[3 * p]) / kPosScale;
+    const double d2 = static_cast<double>(acc[3 * p + 1]) / kPosScale;
+    const double cnt = static_cast<double>(acc[3 * p + 2]);
+    const double av = d1 - bias[p] * reg * cnt;
+    const double bv = d2 - reg * cnt;
+    bias[p] += static_cast<float>(lr * av / (fabs(bv) + 0.001));
+    acc[3 * p] = acc[3 * p + 1] = acc[3 * p + 2] = 0;
+  }
+}
+
 }  // namespace
+
+size_t RankGlobalBytes(int cnt) {
+  int P = 1;
+  while (P < cnt) P <<= 1;
+  return (RankLdsBytes(P) + 255) & ~static_cast<size_t>(255);
+}
+
+size_t XendcgGlobalBytes(int cnt) {
+  return (static_cast<size_t>(cnt) * (2 * sizeof(double) + sizeof(float)) + 255) & ~static_cast<size_t>(255);
+}
+
+void LaunchOvaGrad(int num_class, const PointwiseParams* params_dev, const double* score, const float* label,
+                   const float* weight, int n, float2* gh, hipStream_t s) {
+  if (n <= 0) return;
+  k_ova<<<GridFor(n), 256, 0, s>>>(num_class, params_dev, score, label, weight, n, gh);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchPositionBiasUpdate(const float2* gh, const int* positions, int n, int num_pos, double lr, double reg,
+                              long long* acc, float* bias, hipStream_t s) {
+  if (n <= 0 || num_pos <= 0) return;
+  k_pos_accum<<<std::min(GridFor(n), 1024), 256, 0, s>>>(gh, positions, n, num_pos, acc);
+  HIP_CHECK(hipGetLastError());
+  k_pos_update<<<1, 256, 0, s>>>(acc, num_pos, lr, reg, bias);
+  HIP_CHECK(hipGetLastError());
+}
 
 void LaunchPointwiseGrad(const PointwiseParams& p, const double* score, const float* label, const float* weight,
                          const float* aux, int n, float2* gh, hipStream_t s) {
@@ -423,20 +526,28 @@ void LaunchSoftmaxGrad(int num_class, double factor, const double* score, const 
 void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s) {
   if (a.num_queries <= 0) return;
   int Pmax = 1;
-  while (Pmax < std::max(2, a.max_query)) Pmax <<= 1;
+  while (Pmax < std::max(2, std::min(a.max_query, kMaxDeviceQuery))) Pmax <<= 1;
   const size_t lds = RankLdsBytes(Pmax);
   if (lds > 64 * 1024) {
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_lambdarank),
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_lambdarank<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   }
-  k_lambdarank<<<a.num_queries, kRankThreads, lds, s>>>(a, Pmax);
+  k_lambdarank<false><<<a.num_queries, kRankThreads, lds, s>>>(a, Pmax);
   HIP_CHECK(hipGetLastError());
+  if (a.num_large > 0) {
+    k_lambdarank<true><<<a.num_large, kRankThreads, 0, s>>>(a, 0);
+    HIP_CHECK(hipGetLastError());
+  }
 }
 
 void LaunchXendcgGrad(const XendcgArgs& a, hipStream_t s) {
   if (a.num_queries <= 0) return;
-  k_xendcg<<<a.num_queries, kRankThreads, 0, s>>>(a);
+  k_xendcg<false><<<a.num_queries, kRankThreads, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
+  if (a.num_large > 0) {
+    k_xendcg<true><<<a.num_large, kRankThreads, 0, s>>>(a);
+    HIP_CHECK(hipGetLastError());
+  }
 }
 
 void LaunchPointwiseMetric(const PwMetricParams& p, const double* score, const float* label, const float* weight, int n,

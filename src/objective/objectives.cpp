@@ -403,6 +403,7 @@ class MulticlassOVA : public ObjectiveFunction {
   }
   void Init(const Metadata& md, data_size_t num_data) override {
     num_data_ = num_data;
+    label_ = md.label();
     bin_.clear();
     onehot_.assign(num_class_, std::vector<label_t>(num_data));
     for (int k = 0; k < num_class_; ++k) {
@@ -437,10 +438,17 @@ class MulticlassOVA : public ObjectiveFunction {
   bool ClassNeedTrain(int k) const override { return bin_[k]->ClassNeedTrain(0); }
   int num_class() const override { return num_class_; }
   double sigmoid() const override { return sigmoid_; }
+  // device: one binary kernel pass per class over the original labels (label == k)
+  DeviceGradKind device_kind() const override { return DeviceGradKind::kOVA; }
+  const PointwiseParams* pointwise_class(int k) const override {
+    return k >= 0 && k < static_cast<int>(bin_.size()) ? bin_[k]->pointwise() : nullptr;
+  }
+  const label_t* effective_label() const override { return label_; }
 
  private:
   int num_class_;
   double sigmoid_;
+  const label_t* label_ = nullptr;
   Config cfg_;
   data_size_t num_data_ = 0;
   std::vector<std::unique_ptr<PointwiseObjective>> bin_;

@@ -108,6 +108,8 @@ class RankingBase : public ObjectiveFunction {
   bool NeedAccuratePrediction() const override { return false; }
   bool IsRanking() const override { return true; }
   const std::vector<label_t>& position_biases() const { return pos_biases_; }
+  double position_learning_rate() const { return learning_rate_; }
+  double position_regularization() const { return pos_reg_; }
   const std::vector<double>& effective_pairs() const { return effective_pairs_; }
 
  protected:
@@ -393,6 +395,8 @@ bool GetLambdarankTables(const ObjectiveFunction* obj, LambdarankTables* out) {
   out->inv_max_dcg = &l->inv_max_dcg();
   out->inv_max_bdcg = &l->inv_max_bdcg();
   out->table = &l->sigmoid_table();
+  out->pos_lr = l->position_learning_rate();
+  out->pos_reg = l->position_regularization();
   return true;
 }
 

@@ -178,6 +178,45 @@ def test_lambdarank_gradient_kernel_matches_torch(lgb, gpu_required, rng):
     np.testing.assert_allclose(h, th, rtol=2e-3, atol=2e-4)
 
 
+LTR_TARGETS = ["ndcg", "lambdaloss-ndcg", "lambdaloss-ndcg-plus-plus", "bndcg", "lambdaloss-bndcg",
+               "lambdaloss-bndcg-plus-plus", "precision", "arpk", "lambdaloss-arp1", "lambdaloss-arp2", "ranknet",
+               "bin-ranknet", "lambdagap-s", "lambdagap-x", "lambdagap-s-plus", "lambdagap-x-plus",
+               "lambdagap-s-plus-plus", "lambdagap-x-plus-plus"]
+
+
+@pytest.mark.parametrize("target", LTR_TARGETS)
+@pytest.mark.parametrize("variant", ["plain", "long_queries_positions"])
+def test_lambdarank_gradient_kernel_all_targets(lgb, gpu_required, rng, target, variant):
+    """Device lambdas / hessians of every LambdaGap target against the host objective (the
+    correctness oracle of the 18 targets) on the same scores: short queries in LDS, queries over
+    2048 documents in global scratch, and position-biased (unbiased LTR) scores."""
+    from lambdagap_amd import ops
+
+    if variant == "plain":
+        sizes = rng.integers(2, 60, 80)
+    else:
+        sizes = np.array([30, 2500, 7, 4100, 90], dtype=np.int64)
+    n = int(sizes.sum())
+    X = rng.standard_normal((n, 5)).astype(np.float32)
+    y = rng.integers(0, 5, n).astype(np.float32)
+    if target in ("bndcg", "lambdaloss-bndcg", "lambdaloss-bndcg-plus-plus", "precision", "arpk", "bin-ranknet") or \
+            target.startswith("lambdagap"):
+        y = (y >= 3).astype(np.float32)
+    init = rng.standard_normal(n)
+    pos = np.concatenate([np.arange(s) % 7 for s in sizes]).astype(np.int32) if variant != "plain" else None
+    grads = {}
+    for dev in ("cpu", "gpu"):
+        params = {"objective": "lambdarank", "device_type": dev, "verbosity": -1, "num_leaves": 7,
+                  "lambdarank_target": target, "lambdarank_truncation_level": 12, "lambdagap_weight": 0.5}
+        b = lgb.Booster(params, lgb.Dataset(X, y, group=sizes, init_score=init, position=pos, params=params))
+        b.update()
+        grads[dev] = ops.booster_gradients(b)
+    (gc, hc), (gg, hg) = grads["cpu"], grads["gpu"]
+    scale_g, scale_h = np.abs(gc).max() + 1e-12, np.abs(hc).max() + 1e-12
+    np.testing.assert_allclose(gg, gc, rtol=1e-4, atol=1e-5 * scale_g)
+    np.testing.assert_allclose(hg, hc, rtol=1e-4, atol=1e-5 * scale_h)
+
+
 def _lcg_bags(n, seed, rounds, decide):
     """Host reference of the bagging streams: Random(seed + b) per 1024-row block, one
     NextFloat per row, continued across re-bags (sample_strategy.cpp / bagging.hpp)."""
