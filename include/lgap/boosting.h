@@ -162,6 +162,10 @@ class GBDT {
   std::vector<const Dataset*> valid_data_;
   std::vector<std::vector<const Metric*>> valid_metrics_;
   std::vector<std::vector<double>> valid_score_;
+  std::vector<int> valid_dev_;     // device handle of each validation set (-1: scored on the host)
+  std::vector<char> valid_stale_;  // host copy behind the device score
+  const double* ValidScore(size_t d);
+  std::vector<double> EvalValid(size_t d, const Metric* m);
   std::vector<double> train_score_;   // [num_tree_per_iteration x num_data]
   bool train_score_stale_ = false;    // device owns the score and the host copy is out of date
   bool device_mode_ = false;

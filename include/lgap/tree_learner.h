@@ -72,6 +72,14 @@ class TreeLearner {
                                                         int /*class_id*/) {
     return nullptr;
   }
+  // Validation sets scored on the device (training-layout packed rows): returns a handle, or
+  // -1 when the learner keeps validation scores on the host.
+  virtual int DeviceAddValidSet(const Dataset*, const std::vector<double>& /*init_score*/) { return -1; }
+  virtual void DeviceAddTreeToValid(int /*id*/, const Tree*, int /*class_id*/) {}
+  virtual void DeviceValidAddConstant(int /*id*/, double, int /*class_id*/) {}
+  virtual void DeviceGetValidScore(int /*id*/, std::vector<double>*) {}
+  virtual void DeviceSetValidScore(int /*id*/, const std::vector<double>&) {}
+  virtual bool DeviceEvalPointwiseValid(int /*id*/, const PwMetricParams&, int /*k*/, double* /*sum*/) { return false; }
   virtual bool SupportsDeviceSampling() const { return false; }
   virtual void DeviceSample(int plan, int iter) { (void)plan; (void)iter; }
   virtual std::string DeviceName() const { return "cpu"; }

@@ -102,6 +102,15 @@ void GBDT::AddValidDataset(const Dataset* valid, const std::vector<const Metric*
     models_[i]->AddPredictionToScore(*valid, valid->num_data(), s.data() + static_cast<size_t>(k) * valid->num_data());
   }
   valid_score_.push_back(std::move(s));
+  // device mode: the set's packed rows and score live on the device; trees are added and
+  // pointwise metrics evaluated there, the host copy is refreshed only when read
+  int dev = -1;
+  const char* ev = std::getenv("LGAP_DEVICE_VALID");  // "0": score validation sets on the host
+  if (device_mode_ && DeviceMetricsAllowed() && !(ev && std::strcmp(ev, "0") == 0)) {
+    dev = learner_->DeviceAddValidSet(valid, valid_score_.back());
+  }
+  valid_dev_.push_back(dev);
+  valid_stale_.push_back(0);
   valid_metrics_.push_back(metrics);
   best_score_.emplace_back(metrics.size(), kMinScore);
   best_iter_vec_.emplace_back(metrics.size(), 0);
@@ -140,6 +149,14 @@ void GBDT::SyncTrainScoreFromDevice() {
   }
 }
 
+const double* GBDT::ValidScore(size_t d) {
+  if (valid_dev_[d] >= 0 && valid_stale_[d]) {
+    learner_->DeviceGetValidScore(valid_dev_[d], &valid_score_[d]);
+    valid_stale_[d] = 0;
+  }
+  return valid_score_[d].data();
+}
+
 const double* GBDT::GetTrainingScore(int64_t* out_len) {
   SyncTrainScoreFromDevice();
   *out_len = static_cast<int64_t>(train_score_.size());
@@ -156,6 +173,11 @@ void GBDT::AddScoreConstant(double v, int k) {
     for (data_size_t i = 0; i < num_data_; ++i) s[i] += v;
   }
   for (size_t d = 0; d < valid_score_.size(); ++d) {
+    if (valid_dev_[d] >= 0) {
+      learner_->DeviceValidAddConstant(valid_dev_[d], v, k);
+      valid_stale_[d] = 1;
+      continue;
+    }
     const data_size_t n = valid_data_[d]->num_data();
     double* s = valid_score_[d].data() + static_cast<size_t>(k) * n;
     for (data_size_t i = 0; i < n; ++i) s[i] += v;
@@ -210,6 +232,11 @@ void GBDT::UpdateScore(const Tree* tree, int k) {
     }
   }
   for (size_t d = 0; d < valid_score_.size(); ++d) {
+    if (valid_dev_[d] >= 0) {
+      learner_->DeviceAddTreeToValid(valid_dev_[d], tree, k);
+      valid_stale_[d] = 1;
+      continue;
+    }
     const data_size_t n = valid_data_[d]->num_data();
     tree->AddPredictionToScore(*valid_data_[d], n, valid_score_[d].data() + static_cast<size_t>(k) * n);
   }
@@ -331,6 +358,11 @@ void GBDT::RollbackOneIter() {
       models_[t]->AddPredictionToScore(*train_data_, num_data_, train_score_.data() + static_cast<size_t>(k) * num_data_);
     }
     for (size_t d = 0; d < valid_score_.size(); ++d) {
+      if (valid_dev_[d] >= 0) {
+        learner_->DeviceAddTreeToValid(valid_dev_[d], models_[t].get(), k);
+        valid_stale_[d] = 1;
+        continue;
+      }
       const data_size_t n = valid_data_[d]->num_data();
       models_[t]->AddPredictionToScore(*valid_data_[d], n, valid_score_[d].data() + static_cast<size_t>(k) * n);
     }
@@ -360,6 +392,17 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
   return EvalOne(m, *score);
 }
 
+// Validation metrics: pointwise ones on the device-resident validation score, the rest
+// (AUC, NDCG, ...) on the host copy, refreshed once when stale.
+std::vector<double> GBDT::EvalValid(size_t d, const Metric* m) {
+  PwMetricParams p;
+  if (valid_dev_[d] >= 0 && num_tree_per_iteration_ == 1 && m->DevicePointwise(objective_, &p)) {
+    double sum = 0.0;
+    if (learner_->DeviceEvalPointwiseValid(valid_dev_[d], p, 0, &sum)) return m->FinishSum(sum);
+  }
+  return EvalOne(m, ValidScore(d));
+}
+
 std::vector<std::string> GBDT::GetEvalNames() const {
   std::vector<std::string> out;
   for (auto* m : training_metrics_) for (auto& n : m->GetName()) out.push_back(n);
@@ -387,7 +430,7 @@ std::string GBDT::OutputMetric(int iter) {
   if (need_output || early_stopping_round_ > 0) {
     for (size_t i = 0; i < valid_metrics_.size(); ++i) {
       for (size_t j = 0; j < valid_metrics_[i].size(); ++j) {
-        auto vals = EvalOne(valid_metrics_[i][j], valid_score_[i].data());
+        auto vals = EvalValid(i, valid_metrics_[i][j]);
         auto names = valid_metrics_[i][j]->GetName();
         for (size_t k = 0; k < names.size(); ++k) {
           std::stringstream line;
@@ -431,7 +474,7 @@ std::vector<double> GBDT::GetEvalAt(int data_idx) {
   } else {
     const size_t i = static_cast<size_t>(data_idx - 1);
     if (i >= valid_score_.size()) Log::Fatal("Invalid data index %d", data_idx);
-    for (auto* m : valid_metrics_[i]) for (double v : EvalOne(m, valid_score_[i].data())) ret.push_back(v);
+    for (auto* m : valid_metrics_[i]) for (double v : EvalValid(i, m)) ret.push_back(v);
   }
   return ret;
 }
@@ -449,7 +492,7 @@ void GBDT::GetPredictAt(int data_idx, double* out, int64_t* out_len) {
     raw = GetTrainingScore(&len);
     n = num_data_;
   } else {
-    raw = valid_score_[data_idx - 1].data();
+    raw = ValidScore(static_cast<size_t>(data_idx - 1));
     n = valid_data_[data_idx - 1]->num_data();
   }
   *out_len = static_cast<int64_t>(n) * num_class_;

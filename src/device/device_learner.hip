@@ -3220,6 +3220,15 @@ class DeviceTreeLearner : public TreeLearner {
       return;
     }
     last_trained_ = nullptr;
+    TraverseTree(tree, rowbins_.get(), N_, s);
+  }
+
+  // score[i] += tree(row i) over packed rows of the training layout (training or validation set)
+  void TraverseTree(const Tree* tree, const uint32_t* rowbins, int n, double* s) {
+    if (tree->num_leaves() <= 1) {
+      if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, n, tree->LeafOutput(0), stream_);
+      return;
+    }
     const int nn = tree->num_leaves() - 1;
     const auto& cb = tree->cat_boundaries_inner();
     const auto& ct = tree->cat_threshold_inner();
@@ -3263,13 +3272,61 @@ class DeviceTreeLearner : public TreeLearner {
     const DevNode* dn = reinterpret_cast<const DevNode*>(tree_buf_.get());
     const double* dl = reinterpret_cast<const double*>(tree_buf_.get() + node_bytes);
     const uint32_t* dc = reinterpret_cast<const uint32_t*>(tree_buf_.get() + node_bytes + leaf_bytes);
-    const int grid = std::min(DivUp(N_, kTraverseThreads), num_cu_ * 8);
+    const int grid = std::min(DivUp(n, kTraverseThreads), num_cu_ * 8);
     const size_t lds = node_bytes + (stride_dw_ <= kTraverseMaxDw ? sizeof(uint32_t) * kTraverseThreads * stride_dw_ : 0);
-    k_add_tree<<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins_.get(), stride_dw_, width_, N_, dn, nn, dc,
-                                                                      dl, s);
+    k_add_tree<<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins, stride_dw_, width_, n, dn, nn, dc, dl, s);
     HIP_CHECK(hipGetLastError());
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  // ---- validation sets on the device: packed rows (training layout), score, labels / weights
+  int DeviceAddValidSet(const Dataset* v, const std::vector<double>& score) override {
+    if (v->row_stride() != data_->row_stride() || v->bin_width() != width_ || v->num_data() <= 0) return -1;
+    ScopedTimer timer("Device::AddValidSet");
+    auto dv = std::make_unique<DevValid>();
+    dv->n = v->num_data();
+    dv->rowbins.Upload(reinterpret_cast<const uint32_t*>(v->bins()), static_cast<size_t>(dv->n) * stride_dw_, stream_);
+    dv->score.Upload(score, stream_);
+    const Metadata& md = v->metadata();
+    if (md.label()) dv->label.Upload(md.label(), dv->n, stream_);
+    if (md.weights()) dv->weight.Upload(md.weights(), dv->n, stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    valid_.push_back(std::move(dv));
+    return static_cast<int>(valid_.size()) - 1;
+  }
+  void DeviceAddTreeToValid(int id, const Tree* tree, int k) override {
+    ScopedTimer timer("Device::AddTreeToValid");
+    DevValid& v = *valid_[id];
+    TraverseTree(tree, v.rowbins.get(), v.n, v.score.get() + static_cast<size_t>(k) * v.n);
+  }
+  void DeviceValidAddConstant(int id, double c, int k) override {
+    DevValid& v = *valid_[id];
+    LaunchAddConstant(v.score.get() + static_cast<size_t>(k) * v.n, v.n, c, stream_);
+  }
+  void DeviceGetValidScore(int id, std::vector<double>* out) override {
+    DevValid& v = *valid_[id];
+    out->resize(v.score.size());
+    v.score.Download(out->data(), out->size(), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  void DeviceSetValidScore(int id, const std::vector<double>& in) override {
+    valid_[id]->score.Upload(in, stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  bool DeviceEvalPointwiseValid(int id, const PwMetricParams& p, int k, double* sum) override {
+    DevValid& v = *valid_[id];
+    if (v.label.size() == 0) return false;
+    ScopedTimer timer("Device::EvalValid");
+    if (metric_partial_.size() < static_cast<size_t>(kMetricBlocks + 1)) metric_partial_.Resize(kMetricBlocks + 1);
+    LaunchPointwiseMetric(p, v.score.get() + static_cast<size_t>(k) * v.n, v.label.get(),
+                          v.weight.size() ? v.weight.get() : nullptr, v.n, metric_partial_.get(), kMetricBlocks,
+                          metric_partial_.get() + kMetricBlocks, stream_);
+    double* h = pin_lout_.Get(1);
+    HIP_CHECK(hipMemcpyAsync(h, metric_partial_.get() + kMetricBlocks, sizeof(double), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    *sum = h[0];
+    return true;
   }
 
   std::unique_ptr<Tree> DeviceTrain(int class_id, bool is_first_tree) override {
@@ -4349,6 +4406,13 @@ class DeviceTreeLearner : public TreeLearner {
   RankKernelArgs rank_args_;
   DevBuf<unsigned> xendcg_state_;
   DevBuf<int> row_query_;  // bagging by query: query of each row
+  struct DevValid {
+    int n = 0;
+    DevBuf<uint32_t> rowbins;
+    DevBuf<double> score;
+    DevBuf<float> label, weight;
+  };
+  std::vector<std::unique_ptr<DevValid>> valid_;
   // refit / leaf renewal
   DevBuf<int> leaf_pred_dev_, renew_off_, renew_nz_;
   DevBuf<double> refit_partial_, refit_sums_, refit_delta_, renew_out_;

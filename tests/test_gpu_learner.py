@@ -540,3 +540,51 @@ def test_device_training_metrics_match_host(lgb, gpu_required, objective, metric
     assert [r[1] for r in dev] == [r[1] for r in host]
     for d, h in zip(dev, host):
         assert d[2] == pytest.approx(h[2], rel=1e-9, abs=1e-12), (d, h)
+
+
+@pytest.mark.parametrize("objective,metrics", [("binary", ["binary_logloss", "auc", "binary_error"]),
+                                               ("regression", ["l2", "l1", "huber"]),
+                                               ("multiclass", ["multi_logloss", "multi_error"])])
+def test_device_validation_scoring(lgb, gpu_required, rng, objective, metrics):
+    """Validation sets scored on the device (packed rows uploaded once, each tree traversed on
+    the device, pointwise metrics reduced there; AUC / multiclass read the refreshed host copy):
+    every recorded metric, early stopping and predictions equal the host-scored run."""
+    import os
+    import subprocess
+    import sys
+    import json
+
+    code = f"""
+import json, os, sys, numpy as np
+sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+import lambdagap_amd as lgb
+rng = np.random.default_rng(5)
+X = rng.standard_normal((30000, 8)); Xv = rng.standard_normal((7000, 8))
+def lab(X):
+    z = X[:, 0] - 0.7 * X[:, 1] + 0.3 * X[:, 2] * X[:, 3]
+    if {objective!r} == "binary": return (z + 0.3 * rng.standard_normal(len(X)) > 0).astype(float)
+    if {objective!r} == "multiclass": return np.digitize(z, [-0.5, 0.5]).astype(float)
+    return z + 0.2 * rng.standard_normal(len(X))
+y, yv = lab(X), lab(Xv)
+p = {{"objective": {objective!r}, "metric": {metrics!r}, "num_leaves": 15, "device_type": "gpu", "verbosity": -1,
+     "early_stopping_round": 5}}
+if {objective!r} == "multiclass": p["num_class"] = 3
+ds = lgb.Dataset(X, y); dv = ds.create_valid(Xv, yv)
+ev = {{}}
+b = lgb.train(p, ds, 40, valid_sets=[dv], valid_names=["v"], callbacks=[lgb.record_evaluation(ev)],
+              keep_training_booster=True)
+print(json.dumps({{"ev": ev["v"], "best": b.best_iteration, "pred": b.predict(Xv[:500]).ravel().tolist(),
+                  "inner": b._Booster__inner_predict(1).ravel()[:500].tolist()}}))
+"""
+    runs = {}
+    for mode in ("1", "0"):
+        env = dict(os.environ, LGAP_DEVICE_VALID=mode)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        runs[mode] = json.loads(r.stdout.strip().splitlines()[-1])
+    dev, host = runs["1"], runs["0"]
+    assert dev["best"] == host["best"]
+    for name in host["ev"]:
+        np.testing.assert_allclose(dev["ev"][name], host["ev"][name], rtol=1e-9, atol=1e-12, err_msg=name)
+    np.testing.assert_allclose(dev["pred"], host["pred"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(dev["inner"], host["inner"], rtol=1e-9, atol=1e-12)
