@@ -103,6 +103,11 @@ struct RowSource {
 class Dataset {
  public:
   Dataset() = default;
+  ~Dataset();
+  Dataset(const Dataset&) = default;
+  Dataset& operator=(const Dataset&) = default;
+  Dataset(Dataset&&) = default;
+  Dataset& operator=(Dataset&&) = default;
 
   // Build bin mappers from a sample + pack all rows (c_api.cpp:1322 / dataset_loader.cpp:593 analogue).
   void Construct(const RowSource& src, const Config& cfg, const Dataset* reference,
@@ -199,6 +204,7 @@ class Dataset {
   std::vector<uint8_t> bins_;
   std::vector<float> raw_;
   bool keep_raw_ = false;
+  bool device_pack_ = false;  // device_type=gpu + device_binning: PackRows runs on the GPU
   Metadata metadata_;
   std::vector<int8_t> monotone_;
   std::vector<double> feature_penalty_;
@@ -211,6 +217,9 @@ class DenseSource : public RowSource {
       : data_(data), f64_(dtype_f64), nrow_(nrow), ncol_(ncol), row_major_(row_major) {}
   data_size_t num_rows() const override { return nrow_; }
   int num_cols() const override { return ncol_; }
+  const void* data() const { return data_; }
+  bool is_f64() const { return f64_ != 0; }
+  bool row_major() const { return row_major_; }
   inline double At(data_size_t i, int j) const {
     size_t k = row_major_ ? static_cast<size_t>(i) * ncol_ + j : static_cast<size_t>(j) * nrow_ + i;
     return f64_ ? static_cast<const double*>(data_)[k] : static_cast<const float*>(data_)[k];

@@ -54,5 +54,17 @@ int SampleRowsOnDevice(int mode, int num_rows, int num_class, float* grad, float
                        double fraction, double pos_fraction, double neg_fraction, double top_rate, double other_rate,
                        int bagging_seed, uint32_t goss_seed, int rounds, int* out_rows);
 
+// Feature binning on the device (bin_kernels.hip): packs `nrow` rows of a dense row-major
+// matrix (fp32 / fp64) into `ds`'s packed group-bin layout (its mappers and EFB groups),
+// writing host_out (nrow x row_stride bytes). With keep_device_copy the device rows stay
+// registered for the HIP learner of `ds` (TakeDeviceRows). False: not supported here (the
+// caller bins on the host).
+bool DevicePackDense(const Dataset& ds, const void* data, bool f64, int nrow, int ncol, uint8_t* host_out,
+                     bool keep_device_copy);
+// the device copy of `ds`'s packed rows (ownership moves to the caller; hipFree), or nullptr
+// when none matches `bytes`
+void* TakeDeviceRows(const Dataset* ds, size_t bytes);
+void ReleaseDeviceRows(const Dataset* ds);
+
 }  // namespace device
 }  // namespace lgap

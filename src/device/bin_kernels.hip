@@ -1,0 +1,274 @@
+// Feature binning on the device: a dense row-major matrix (fp32 / fp64) becomes the
+// Dataset's packed group-bin rows (EFB bundles included) on the GPU.
+//
+// The host keeps only what needs a sample: BinMapper::FindBin and the bundle plan
+// (Dataset::Construct). The per-value work — BinMapper::ValueToBin (reference
+// include/LightGBM/bin.h:612-650: NaN / zero handling, binary search over the upper
+// bounds, categorical lookup) and the bundle packing of Dataset::PackRows (reference
+// src/io/dataset.cpp:325-441) — runs here, one thread per (row, group), so a row's
+// group bytes are written by consecutive lanes. Bundled features are applied in
+// ascending column order with the host's rule (a value whose encoded bin is the
+// group's zero only writes when its feature owns the group's default), so the
+// result is bit-identical to the host packer.
+//
+// The packed rows are downloaded into the host Dataset (which stays the canonical
+// container) and the device copy is kept for the HIP learner to adopt, so the
+// training upload of the row-major bins is skipped.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "device/hip_common.h"
+#include "lgap/common.h"
+#include "lgap/dataset.h"
+#include "lgap/device_api.h"
+#include "lgap/log.h"
+
+namespace lgap {
+namespace device {
+
+namespace {
+
+struct BinFeat {
+  int col;          // column of the input matrix
+  int num_bin;
+  int missing;      // MissingType
+  int is_cat;
+  int mfb, offset;  // EncodeBin
+  int bounds;       // first upper bound in the flat bounds array
+  int lut;          // first entry of the categorical lookup (category -> bin), -1: none
+  int lut_size;
+  int owner;        // this feature owns the group's template value
+};
+
+struct BinGroup {
+  int first, count;  // features of the group (ascending column)
+  int tmpl;          // group bin of an all-zero row
+  int pad;
+};
+
+__device__ __forceinline__ uint32_t DevValueToBin(const BinFeat& f, const double* __restrict__ bounds,
+                                                  const int* __restrict__ lut, double v) {
+  if (v != v) {
+    if (f.is_cat) return 0u;
+    if (f.missing == static_cast<int>(MissingType::NaN)) return static_cast<uint32_t>(f.num_bin - 1);
+    v = 0.0;
+  }
+  if (!f.is_cat) {
+    int l = 0, r = f.num_bin - 1;
+    if (f.missing == static_cast<int>(MissingType::NaN)) r -= 1;
+    const double* ub = bounds + f.bounds;
+    while (l < r) {
+      const int m = (r + l - 1) / 2;
+      if (v <= ub[m]) r = m;
+      else l = m + 1;
+    }
+    return static_cast<uint32_t>(l);
+  }
+  const int iv = static_cast<int>(v);
+  if (iv < 0 || iv >= f.lut_size) return 0u;
+  return static_cast<uint32_t>(lut[f.lut + iv]);
+}
+
+template <typename T, int W>
+__global__ __launch_bounds__(256) void k_pack_rows(const T* __restrict__ x, int nrow, int ncol, int num_groups,
+                                                   const BinGroup* __restrict__ groups, const BinFeat* __restrict__ feats,
+                                                   const double* __restrict__ bounds, const int* __restrict__ lut,
+                                                   int stride, uint8_t* __restrict__ out) {
+  const long long total = static_cast<long long>(nrow) * num_groups;
+  for (long long idx = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int row = static_cast<int>(idx / num_groups);
+    const int g = static_cast<int>(idx - static_cast<long long>(row) * num_groups);
+    const BinGroup gr = groups[g];
+    int gb = gr.tmpl;
+    const T* xr = x + static_cast<size_t>(row) * ncol;
+    for (int k = 0; k < gr.count; ++k) {
+      const BinFeat f = feats[gr.first + k];
+      const double v = static_cast<double>(xr[f.col]);
+      if (!(v != v || fabs(v) > kZeroThreshold)) continue;  // zeros keep the template (host GetRow skips them)
+      const uint32_t b = DevValueToBin(f, bounds, lut, v);
+      const int e = b == static_cast<uint32_t>(f.mfb) ? 0 : f.offset + static_cast<int>(b) - (b > static_cast<uint32_t>(f.mfb) ? 1 : 0);
+      if (e == 0 && !f.owner) continue;
+      gb = e;
+    }
+    uint8_t* o = out + static_cast<size_t>(row) * stride;
+    if (W == 1) o[g] = static_cast<uint8_t>(gb);
+    else reinterpret_cast<uint16_t*>(o)[g] = static_cast<uint16_t>(gb);
+  }
+}
+
+// padding bytes of each packed row (stride beyond num_groups * width) are zero
+__global__ void k_zero_pad(uint8_t* out, int nrow, int stride, int used) {
+  const int pad = stride - used;
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < static_cast<long long>(nrow) * pad;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long r = i / pad;
+    out[r * stride + used + (i - r * pad)] = 0;
+  }
+}
+
+// Device packed rows kept for the learner, keyed by the Dataset they belong to.
+struct KeptRows {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_kept_mu;
+std::map<const Dataset*, KeptRows> g_kept;
+
+}  // namespace
+
+bool DevicePackDense(const Dataset& ds, const void* data, bool f64, int nrow, int ncol, uint8_t* host_out,
+                     bool keep_device_copy) {
+  if (DeviceCount() <= 0 || nrow <= 0) return false;
+  ScopedTimer timer("Device::PackRows");
+  const int G = ds.num_groups();
+  const int W = ds.bin_width();
+  const int stride = ds.row_stride();
+  // plan: groups -> features in ascending column order, flat bounds, categorical lookups
+  std::vector<BinGroup> groups(std::max(G, 1));
+  std::vector<BinFeat> feats;
+  std::vector<double> bounds;
+  std::vector<int> lut;
+  std::vector<int> owner(G, -1);
+  std::vector<int> tmpl(G, 0);
+  for (int f = 0; f < ds.num_features(); ++f) {
+    const FeatureInfo& fi = ds.feature(f);
+    if (fi.default_bin != fi.mfb) {
+      tmpl[fi.group] = Dataset::EncodeBin(fi, fi.default_bin);
+      owner[fi.group] = f;
+    }
+  }
+  for (int g = 0; g < G; ++g) {
+    std::vector<int> fs = ds.group(g).features;
+    std::sort(fs.begin(), fs.end(), [&](int a, int b) { return ds.feature(a).real_index < ds.feature(b).real_index; });
+    groups[g].first = static_cast<int>(feats.size());
+    groups[g].count = static_cast<int>(fs.size());
+    groups[g].tmpl = tmpl[g];
+    groups[g].pad = 0;
+    for (int f : fs) {
+      const FeatureInfo& fi = ds.feature(f);
+      const BinMapper& m = ds.inner_mapper(f);
+      if (fi.real_index >= ncol) return false;
+      BinFeat b;
+      b.col = fi.real_index;
+      b.num_bin = m.num_bin();
+      b.missing = static_cast<int>(m.missing_type());
+      b.is_cat = m.bin_type() == BinType::Categorical ? 1 : 0;
+      b.mfb = static_cast<int>(fi.mfb);
+      b.offset = fi.offset;
+      b.bounds = static_cast<int>(bounds.size());
+      b.lut = -1;
+      b.lut_size = 0;
+      b.owner = owner[g] == f ? 1 : 0;
+      if (b.is_cat) {
+        const auto& b2c = m.bin_to_category();
+        int mx = 0;
+        for (int c : b2c) mx = std::max(mx, c);
+        if (mx > (1 << 22)) return false;  // sparse huge category ids: the host map handles them
+        b.lut = static_cast<int>(lut.size());
+        b.lut_size = mx + 1;
+        lut.resize(lut.size() + mx + 1, 0);
+        for (size_t k = 0; k < b2c.size(); ++k) {
+          if (b2c[k] >= 0) lut[b.lut + b2c[k]] = static_cast<int>(k);
+        }
+        // bins absent from bin_to_category map to 0 as the host's cat_2_bin miss
+      } else {
+        const auto& ub = m.upper_bounds();
+        bounds.insert(bounds.end(), ub.begin(), ub.end());
+      }
+      feats.push_back(b);
+    }
+  }
+  if (feats.empty()) feats.resize(1);
+  if (bounds.empty()) bounds.resize(1);
+  if (lut.empty()) lut.resize(1);
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  DevBuf<BinGroup> d_groups;
+  DevBuf<BinFeat> d_feats;
+  DevBuf<double> d_bounds;
+  DevBuf<int> d_lut;
+  d_groups.Upload(groups, s);
+  d_feats.Upload(feats, s);
+  d_bounds.Upload(bounds, s);
+  d_lut.Upload(lut, s);
+  const size_t out_bytes = static_cast<size_t>(nrow) * stride;
+  void* d_out = nullptr;
+  HIP_CHECK(hipMalloc(&d_out, std::max<size_t>(out_bytes, 1)));
+  // the matrix in row chunks of <= 1 GiB
+  const size_t es = f64 ? 8 : 4;
+  const size_t row_bytes = es * static_cast<size_t>(ncol);
+  const int chunk = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nrow, (size_t(1) << 30) / std::max<size_t>(row_bytes, 1))));
+  // (one stream: each chunk's upload follows the previous chunk's kernel)
+  DevBuf<char> d_in[2];
+  d_in[0].Resize(row_bytes * chunk);
+  if (nrow > chunk) d_in[1].Resize(row_bytes * chunk);
+  int slot = 0;
+  for (int r0 = 0; r0 < nrow; r0 += chunk, slot ^= 1) {
+    const int rows = std::min(chunk, nrow - r0);
+    const char* src = static_cast<const char*>(data) + row_bytes * r0;
+    HIP_CHECK(hipMemcpyAsync(d_in[slot].get(), src, row_bytes * rows, hipMemcpyHostToDevice, s));
+    uint8_t* dst = static_cast<uint8_t*>(d_out) + static_cast<size_t>(r0) * stride;
+    const long long work = static_cast<long long>(rows) * G;
+    const int grid = static_cast<int>(std::max<long long>(1, std::min<long long>(65536, (work + 255) / 256)));
+    if (f64) {
+      if (W == 1) k_pack_rows<double, 1><<<grid, 256, 0, s>>>(reinterpret_cast<const double*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
+      else k_pack_rows<double, 2><<<grid, 256, 0, s>>>(reinterpret_cast<const double*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
+    } else {
+      if (W == 1) k_pack_rows<float, 1><<<grid, 256, 0, s>>>(reinterpret_cast<const float*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
+      else k_pack_rows<float, 2><<<grid, 256, 0, s>>>(reinterpret_cast<const float*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
+    }
+    HIP_CHECK(hipGetLastError());
+  }
+  if (stride > G * W) {
+    k_zero_pad<<<1024, 256, 0, s>>>(static_cast<uint8_t*>(d_out), nrow, stride, G * W);
+    HIP_CHECK(hipGetLastError());
+  }
+  for (size_t off = 0; off < out_bytes; off += size_t(1) << 30) {
+    HIP_CHECK(hipMemcpyAsync(host_out + off, static_cast<uint8_t*>(d_out) + off, std::min(size_t(1) << 30, out_bytes - off),
+                             hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipStreamDestroy(s));
+  if (keep_device_copy) {
+    std::lock_guard<std::mutex> lock(g_kept_mu);
+    KeptRows& k = g_kept[&ds];
+    if (k.ptr) (void)hipFree(k.ptr);
+    k.ptr = d_out;
+    k.bytes = out_bytes;
+  } else {
+    HIP_CHECK(hipFree(d_out));
+  }
+  return true;
+}
+
+void* TakeDeviceRows(const Dataset* ds, size_t bytes) {
+  std::lock_guard<std::mutex> lock(g_kept_mu);
+  auto it = g_kept.find(ds);
+  if (it == g_kept.end()) return nullptr;
+  void* p = it->second.ptr;
+  const size_t b = it->second.bytes;
+  g_kept.erase(it);
+  if (b != bytes) {  // the dataset changed after packing: not usable
+    (void)hipFree(p);
+    return nullptr;
+  }
+  return p;
+}
+
+void ReleaseDeviceRows(const Dataset* ds) {
+  std::lock_guard<std::mutex> lock(g_kept_mu);
+  auto it = g_kept.find(ds);
+  if (it == g_kept.end()) return;
+  (void)hipFree(it->second.ptr);
+  g_kept.erase(it);
+}
+
+}  // namespace device
+}  // namespace lgap

@@ -2577,6 +2577,21 @@ __global__ __launch_bounds__(kTraverseThreads) void k_add_tree(const uint32_t* _
   }
 }
 
+// group-major copy of the packed rows: col[g * N + i] = group bin g of row i (coalesced writes;
+// each row's dword run is read by consecutive groups' threads of other waves through L2)
+template <typename T>
+__global__ __launch_bounds__(256) void k_transpose_bins(const uint32_t* __restrict__ rowbins, int stride_dw, int N, int G,
+                                                        uint8_t* __restrict__ colbins) {
+  const long long total = static_cast<long long>(G) * N;
+  for (long long idx = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(idx / N);
+    const int i = static_cast<int>(idx - static_cast<long long>(g) * N);
+    const T* row = reinterpret_cast<const T*>(rowbins + static_cast<size_t>(i) * stride_dw);
+    reinterpret_cast<T*>(colbins)[idx] = row[g];
+  }
+}
+
 // ---------------------------------------------------------------------------
 
 template <typename T>
@@ -3759,26 +3774,24 @@ class DeviceTreeLearner : public TreeLearner {
   void UploadData() {
     // packed rows
     const size_t rb = static_cast<size_t>(N_) * stride_dw_;
-    rowbins_.Resize(std::max<size_t>(rb, 1));
-    rowbins_.Upload(reinterpret_cast<const uint32_t*>(data_->bins()), rb, stream_);
-    // group-major copy
-    const size_t cb = static_cast<size_t>(G_) * N_ * width_;
-    std::vector<uint8_t> col(std::max<size_t>(cb, 1));
-    const uint8_t* bins = data_->bins();
-    const int stride = data_->row_stride();
-#pragma omp parallel for schedule(static)
-    for (int g = 0; g < G_; ++g) {
-      if (width_ == 1) {
-        uint8_t* dst = col.data() + static_cast<size_t>(g) * N_;
-        for (data_size_t i = 0; i < N_; ++i) dst[i] = bins[static_cast<size_t>(i) * stride + g];
-      } else {
-        uint16_t* dst = reinterpret_cast<uint16_t*>(col.data()) + static_cast<size_t>(g) * N_;
-        for (data_size_t i = 0; i < N_; ++i) {
-          dst[i] = reinterpret_cast<const uint16_t*>(bins + static_cast<size_t>(i) * stride)[g];
-        }
-      }
+    // rows binned on the device (bin_kernels.hip) are adopted instead of uploaded again
+    void* adopted = rb > 0 ? TakeDeviceRows(data_, rb * sizeof(uint32_t)) : nullptr;
+    if (adopted != nullptr) {
+      rowbins_.Adopt(static_cast<uint32_t*>(adopted), rb);
+      Log::Debug("HIP learner: adopted the device-binned rows (%zu bytes)", rb * sizeof(uint32_t));
+    } else {
+      rowbins_.Resize(std::max<size_t>(rb, 1));
+      rowbins_.Upload(reinterpret_cast<const uint32_t*>(data_->bins()), rb, stream_);
     }
-    colbins_.Upload(col, stream_);
+    // group-major copy, transposed on the device from the packed rows
+    const size_t cb = static_cast<size_t>(G_) * N_ * width_;
+    colbins_.Resize(std::max<size_t>(cb, 1));
+    if (cb > 0) {
+      const int grid = std::max(1, std::min(DivUp(static_cast<long long>(G_) * N_, 256), 65536));
+      if (width_ == 1) k_transpose_bins<uint8_t><<<grid, 256, 0, stream_>>>(rowbins_.get(), stride_dw_, N_, G_, colbins_.get());
+      else k_transpose_bins<uint16_t><<<grid, 256, 0, stream_>>>(rowbins_.get(), stride_dw_, N_, G_, colbins_.get());
+      HIP_CHECK(hipGetLastError());
+    }
     // features / groups
     std::vector<DevFeature> feats(std::max(F_, 1));
     max_cat_bin_ = 1;

@@ -127,6 +127,13 @@ class DevBuf {
     n_ = 0;
     owns_ = true;
   }
+  // Take ownership of a device allocation of n elements (hipMalloc'd elsewhere).
+  void Adopt(T* p, size_t n) {
+    Free();
+    ptr_ = p;
+    n_ = n;
+    owns_ = true;
+  }
   // Non-owning view into memory carved from a larger allocation (arena).
   void Attach(T* p, size_t n) {
     Free();

@@ -3,6 +3,7 @@
 // Reference behaviour: src/io/dataset.cpp (FindGroups :107-244,
 // FastFeatureBundling :246-323, Construct :325-441, SaveBinary :1018-1187) and
 // dataset_loader.cpp:593 (ConstructFromSampleData).
+#include "lgap/device_api.h"
 #include "lgap/omp_errors.h"
 #include "lgap/dataset.h"
 
@@ -250,12 +251,22 @@ void Dataset::PushRows(const RowSource& src, data_size_t start_row) {
   PackRows(src, start_row, false);
 }
 
+Dataset::~Dataset() { device::ReleaseDeviceRows(this); }
+
 void Dataset::PackRows(const RowSource& src, data_size_t start_row, bool reset) {
   const data_size_t nrows = src.num_rows();
   if (reset) {
     num_data_ = nrows;
     bins_.assign(static_cast<size_t>(num_data_) * row_stride_, 0);
     if (keep_raw_) raw_.assign(static_cast<size_t>(num_data_) * features_.size(), 0.0f);
+  }
+  // device binning of a dense row-major matrix (bin_kernels.hip); the device rows are kept
+  // for the HIP learner. Anything else (sparse / Arrow / streaming / raw values) bins here.
+  const auto* dense = dynamic_cast<const DenseSource*>(&src);
+  if (device_pack_ && reset && start_row == 0 && !keep_raw_ && dense != nullptr && dense->row_major() &&
+      device::DeviceCount() > 0 &&
+      device::DevicePackDense(*this, dense->data(), dense->is_f64(), nrows, dense->num_cols(), bins_.data(), true)) {
+    return;
   }
   const size_t nfeat = features_.size();
   const bool store_raw = keep_raw_ && !raw_.empty();
@@ -306,6 +317,7 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
   num_data_ = src.num_rows();
   num_total_features_ = src.num_cols();
   keep_raw_ = cfg.linear_tree || (reference != nullptr && reference->keep_raw_);
+  device_pack_ = (cfg.device_type == "gpu" || cfg.device_type == "cuda") && cfg.device_binning;
   if (reference != nullptr) {
     if (reference->num_total_features_ != num_total_features_) {
       Log::Fatal("The number of features in data (%d) is not the same as it was in training data (%d).",

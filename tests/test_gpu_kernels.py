@@ -67,6 +67,61 @@ def test_histogram_constant_hessian_is_exact(lgb, gpu_required, rng, n):
             np.testing.assert_array_equal(out[starts[k] + 1:starts[k] + nb, 1], cnt[1:nb])
 
 
+@pytest.mark.parametrize("dtype,max_bin", [(np.float32, 255), (np.float64, 63), (np.float32, 1023)])
+def test_device_binning_matches_host_bit_for_bit(lgb, gpu_required, rng, dtype, max_bin):
+    """Device feature binning (ValueToBin + EFB bundle packing on the GPU) produces exactly the
+    host packer's group bins: NaN (missing as NaN and as zero), exact zeros and values under the
+    zero threshold, categorical codes (incl. unseen / negative), and sparse bundled columns."""
+    from lambdagap_amd import ops
+
+    n = 120_000
+    X = rng.standard_normal((n, 12))
+    X[rng.random(n) < 0.1, 0] = np.nan                  # NaN -> missing bin
+    X[rng.random(n) < 0.3, 1] = 0.0                     # zero-heavy
+    X[rng.random(n) < 0.05, 1] = 1e-40                  # below the zero threshold
+    X[:, 2] = rng.integers(-1, 40, n)                   # categorical (negative -> bin 0)
+    X[rng.random(n) < 0.02, 2] = np.nan
+    X[:, 3] = np.round(X[:, 3] * 3)                     # few distinct values
+    for j in range(6, 12):                              # sparse columns EFB bundles together
+        X[rng.random(n) < 0.93, j] = 0.0
+    X[rng.random(n) < 0.05, 5] = np.nan
+    X = X.astype(dtype)
+    params = {"max_bin": max_bin, "verbosity": -1, "categorical_feature": [2], "enable_bundle": True,
+              "use_missing": True}
+    host = lgb.Dataset(X, params=dict(params, device_type="cpu")).construct()
+    dev = lgb.Dataset(X, params=dict(params, device_type="gpu")).construct()
+    assert ops.group_layout(host)[:3] == ops.group_layout(dev)[:3]
+    np.testing.assert_array_equal(ops.group_bins(dev), ops.group_bins(host))
+    # zero_as_missing routes zeros through the missing path
+    host_z = lgb.Dataset(X, params=dict(params, device_type="cpu", zero_as_missing=True)).construct()
+    dev_z = lgb.Dataset(X, params=dict(params, device_type="gpu", zero_as_missing=True)).construct()
+    np.testing.assert_array_equal(ops.group_bins(dev_z), ops.group_bins(host_z))
+
+
+def test_device_binned_dataset_trains_like_host_binned(lgb, gpu_required, rng):
+    """The HIP learner adopts the device-binned rows (no second upload) and grows the same model
+    as from host-binned rows."""
+    from lambdagap_amd.utils import make_higgs_like
+
+    X, y = make_higgs_like(200_000, seed=9)
+    p = {"objective": "binary", "num_leaves": 31, "device_type": "gpu", "verbosity": -1}
+    b_dev = lgb.train(p, lgb.Dataset(X, y, params=p), 5)
+    b_host = lgb.train(p, lgb.Dataset(X, y, params=dict(p, device_binning=False)), 5)
+    np.testing.assert_array_equal(b_dev.predict(X[:5000], raw_score=True), b_host.predict(X[:5000], raw_score=True))
+    # the device packer ran (phase timer), not a silent host fallback
+    import os
+    import subprocess
+    import sys
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import lambdagap_amd as lgb; "
+            "X = np.random.default_rng(1).standard_normal((50000, 8)).astype(np.float32); "
+            "lgb.Dataset(X, params={'device_type': 'gpu', 'verbosity': -1}).construct(); "
+            "print(lgb.phase_timer_report())") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, LGAP_TIMETAG="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Device::PackRows" in r.stdout + r.stderr
+
+
 def test_binary_gradient_kernel_matches_torch(lgb, gpu_required, rng):
     import torch
     from lambdagap_amd import ops
