@@ -126,6 +126,9 @@ struct Args {
   unsigned* rng;
   int max_cat_bin;
   int max_bin;  // largest feature num_bin (LDS sizing of k_reduce_scan)
+  int cat_p2;   // power of two >= the largest categorical num_bin (categorical sort scratch), 1 without
+  char* scan_scratch;        // global-memory scan scratch (features wider than the LDS budget), else null
+  size_t scan_scratch_stride;  // bytes per block
   int max_depth;
   int fuse_post;
   unsigned long long* stamps;  // optional phase timestamps (LGAP_STAMPS=1)
@@ -1122,6 +1125,186 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
   return any;
 }
 
+// Wave-parallel FindBestCategorical (split_math.h:262-386, the host oracle; reference
+// cuda_best_split_finder.cu:639 sorts the categories in-block): the one-hot candidates are
+// evaluated one bin per lane with a wave arg-max (first maximum in bin order), and the
+// many-vs-many path compacts the used bins with a ballot scan, bitonic-sorts them in LDS by
+// (ctr, bin) — the order of the host's stable insertion sort — and lane 0 walks the at most
+// max_cat_threshold prefix positions of both directions. `order` / `key` hold cat_p2 entries.
+__device__ bool ScanCategoricalWave(const SplitParams& p_in, const FeatureScanMeta& m, const double* H, double sum_g,
+                                    double sum_h_raw, int n, double po, const LeafBounds& bounds, int cat_p2,
+                                    int* order, double* key, SplitInfo* out) {
+  const int lane = threadIdx.x & 63;
+  const double sum_h = sum_h_raw + 2 * kEpsilon;
+  SplitParams p = p_in;
+  p.use_monotone = 0;
+  double gain_shift;
+  if (p.path_smooth > kEpsilon) {
+    gain_shift = LeafGainGivenOutput(sum_g, sum_h, p, po);
+  } else {
+    SplitParams q = p;
+    q.path_smooth = 0.0;
+    gain_shift = LeafGain(sum_g, sum_h, q, n, 0.0);
+  }
+  const double min_gain_shift = gain_shift + p.min_gain_to_split;
+  const double cnt_factor = n / sum_h;
+  const bool use_rand = p.extra_trees != 0;
+  bool sp = false;
+  double best_gain = kMinScore, best_lg = 0.0, best_lh = 0.0;
+  int best_lc = 0, best_t = -1, best_dir = 1, used = 0;
+  const bool onehot = m.num_bin <= p.max_cat_to_onehot;
+  if (onehot) {
+    double lg = kMinScore, llg = 0.0, llh = 0.0;
+    int lt = 0x7fffffff, llc = 0;
+    bool lsp = false;
+    for (int t = 1 + lane; t < m.num_bin; t += 64) {
+      const double g = H[2 * t], h = H[2 * t + 1];
+      const int c = RoundCount(h * cnt_factor);
+      if (c < p.min_data_in_leaf || h < p.min_sum_hessian_in_leaf) continue;
+      const int oc = n - c;
+      if (oc < p.min_data_in_leaf) continue;
+      const double oh = sum_h - h - kEpsilon;
+      if (oh < p.min_sum_hessian_in_leaf) continue;
+      const double og = sum_g - g;
+      if (use_rand && t != m.rand_threshold) continue;
+      const double gain = SplitGain(og, oh, g, h + kEpsilon, p, 0, oc, c, po, bounds);
+      if (gain <= min_gain_shift) continue;
+      lsp = true;
+      if (gain > lg) {
+        lg = gain;
+        lt = t;
+        llg = g;
+        llh = h + kEpsilon;
+        llc = c;
+      }
+    }
+    sp = __any(lsp) != 0;
+    const int src = WaveArgBestLane(lg, lt, 0);
+    best_gain = ReadLane(lg, src);
+    best_t = ReadLane(lt, src);
+    best_lg = ReadLane(llg, src);
+    best_lh = ReadLane(llh, src);
+    best_lc = ReadLane(llc, src);
+  } else {
+    // used bins in ascending order (ballot compaction)
+    const unsigned long long lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int base = 0; base < m.num_bin; base += 64) {
+      const int i = base + lane;
+      const bool v = i >= 1 && i < m.num_bin && RoundCount(H[2 * i + 1] * cnt_factor) >= p.cat_smooth;
+      const unsigned long long b = __ballot(v);
+      if (v) order[used + __popcll(b & lt_mask)] = i;
+      used += __popcll(b);
+    }
+    int P2 = 1;
+    while (P2 < used) P2 <<= 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int j = lane; j < P2; j += 64) {
+      if (j < used) {
+        const int b = order[j];
+        key[j] = H[2 * b] / (H[2 * b + 1] + p.cat_smooth);
+      } else {
+        key[j] = INFINITY;
+        order[j] = 0x7fffffff;
+      }
+    }
+    // bitonic sort ascending by (ctr, bin): the stable order of the host's insertion sort
+    for (int k = 2; k <= P2; k <<= 1) {
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int i = lane; i < P2; i += 64) {
+          const int l = i ^ jj;
+          if (l <= i) continue;
+          const double ka = key[i], kb = key[l];
+          const int ba = order[i], bb = order[l];
+          const bool a_gt = ka != kb ? ka > kb : ba > bb;
+          if (a_gt == ((i & k) == 0)) {
+            key[i] = kb;
+            key[l] = ka;
+            order[i] = bb;
+            order[l] = ba;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    p.lambda_l2 += p.cat_l2;
+    if (lane == 0) {
+      const int max_num_cat = p.max_cat_threshold < (used + 1) / 2 ? p.max_cat_threshold : (used + 1) / 2;
+      for (int dir_i = 0; dir_i < 2; ++dir_i) {
+        const int dir = dir_i == 0 ? 1 : -1;
+        int pos = dir_i == 0 ? 0 : used - 1;
+        int cur_group = 0, lc = 0;
+        double lg = 0.0, lh = kEpsilon;
+        for (int i = 0; i < used && i < max_num_cat; ++i) {
+          const int t = order[pos];
+          pos += dir;
+          const double g = H[2 * t], h = H[2 * t + 1];
+          const int c = RoundCount(h * cnt_factor);
+          lg += g;
+          lh += h;
+          lc += c;
+          cur_group += c;
+          if (lc < p.min_data_in_leaf || lh < p.min_sum_hessian_in_leaf) continue;
+          const int rc = n - lc;
+          if (rc < p.min_data_in_leaf || rc < p.min_data_per_group) break;
+          const double rh = sum_h - lh;
+          if (rh < p.min_sum_hessian_in_leaf) break;
+          if (cur_group < p.min_data_per_group) continue;
+          cur_group = 0;
+          const double rg = sum_g - lg;
+          if (use_rand && i != m.rand_threshold) continue;
+          const double gain = SplitGain(lg, lh, rg, rh, p, 0, lc, rc, po, bounds);
+          if (gain <= min_gain_shift) continue;
+          sp = true;
+          if (gain > best_gain) {
+            best_lc = lc;
+            best_lg = lg;
+            best_lh = lh;
+            best_t = i;
+            best_gain = gain;
+            best_dir = dir;
+          }
+        }
+      }
+    }
+    sp = __shfl(sp ? 1 : 0, 0, kWave) != 0;
+  }
+  if (lane == 0) {
+    out->Reset();
+    out->default_left = 0;
+    if (sp) {
+      out->left_output = LeafOutput(best_lg, best_lh, p, best_lc, po, bounds);
+      out->left_count = best_lc;
+      out->left_sum_gradient = best_lg;
+      out->left_sum_hessian = best_lh - kEpsilon;
+      out->right_output = LeafOutput(sum_g - best_lg, sum_h - best_lh, p, n - best_lc, po, bounds);
+      out->right_count = n - best_lc;
+      out->right_sum_gradient = sum_g - best_lg;
+      out->right_sum_hessian = sum_h - best_lh - kEpsilon;
+      out->gain = (best_gain - min_gain_shift) * m.penalty;
+      for (int w = 0; w < kMaxCatWords; ++w) out->cat_bitset[w] = 0u;
+      if (onehot) {
+        out->num_cat_threshold = 1;
+        out->cat_bitset[best_t / 32] |= (1u << (best_t % 32));
+      } else {
+        out->num_cat_threshold = static_cast<int16_t>(best_t + 1);
+        for (int i = 0; i <= best_t; ++i) {
+          const int b = best_dir == 1 ? order[i] : order[used - 1 - i];
+          out->cat_bitset[b / 32] |= (1u << (b % 32));
+        }
+      }
+      out->monotone_type = 0;
+    }
+  }
+  return sp;
+}
+
 // One workgroup (16 waves) per feature this rank owns (every feature on one GPU):
 //  1. the smaller child's histogram of the feature into LDS: the sum of the active
 //     histogram blocks' slab rows (single GPU / feature parallel), or of the owner rows
@@ -1132,9 +1315,14 @@ __device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const dou
 //     smaller child and wave 1 the larger one concurrently, from LDS
 //  4. the block writes both candidates into this rank's block of the candidate table
 //     (on the xGMI transport: into every rank's table, then the in-kernel exchange)
-template <typename Acc>
+// kGlobal: the block's scratch (histograms, partials, categorical sort) lives in its slice of
+// global memory instead of LDS — features wider than the LDS budget (max_bin in the thousands;
+// reference cuda_best_split_finder.cu:1561 global-memory variant).
+template <typename Acc, bool kGlobal>
 __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_grid) {
-  extern __shared__ __align__(16) unsigned char smem[];
+  extern __shared__ __align__(16) unsigned char smem_dyn[];
+  unsigned char* smem = kGlobal ? reinterpret_cast<unsigned char*>(a.scan_scratch) + blockIdx.x * a.scan_scratch_stride
+                                : smem_dyn;
   const Ctl c = *a.ctl;
   if (c.done || c.skip) return;
   const int j = blockIdx.x;
@@ -1207,7 +1395,8 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     double* hs_full = reinterpret_cast<double*>(smem);                 // 2 * nbin: smaller child, full
     double* hl_full = hs_full + 2 * a.max_bin;                          // 2 * nbin: larger child, full
     double* part = hl_full + 2 * a.max_bin;                             // [16][64]
-    int* order = reinterpret_cast<int*>(part + 16 * 64);                // max_bin (categorical scratch)
+    int* order = reinterpret_cast<int*>(part + 16 * 64);                // [2][cat_p2] categorical scratch
+    double* ckey = reinterpret_cast<double*>(order + 2 * a.cat_p2);     // [2][cat_p2] ctr sort keys
     (void)part;
     const int n_small = a.range[c.smaller].count;
     // 1. smaller child's histogram into hs_full at stored positions (mfb filled in step 3)
@@ -1371,34 +1560,32 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
         if (fi.bin_type == 0) {
           sp = ScanNumericalWave(a, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
         } else {
-          // categorical: lane 0 runs the sequential one-hot / ctr-sorted scan (rare, few bins)
-          int spi = 0;
-          if (lane == 0) {
-            FeatureScanMeta m;
-            m.num_bin = fi.num_bin;
-            m.default_bin = static_cast<uint32_t>(fi.default_bin);
-            m.missing_type = fi.missing;
-            m.bin_type = fi.bin_type;
-            m.monotone = fi.monotone;
-            m.penalty = fi.penalty;
-            m.rand_threshold = 0;
-            if (a.sp.extra_trees) {
-              // (categorical draws happen here; numerical ones were drawn above)
-              if (fi.num_bin <= a.sp.max_cat_to_onehot) {
-                if (fi.num_bin - 1 > 0) m.rand_threshold = RandNextInt(&a.rng[f], 1, fi.num_bin);
-              } else {
-                const double cf = n / (sh + 2 * kEpsilon);
-                int used = 0;
-                for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(H[2 * b + 1] * cf) >= a.sp.cat_smooth;
-                const int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
-                const int max_thr = max(min(max_num_cat, used) - 1, 0);
-                if (max_thr > 0) m.rand_threshold = RandNextInt(&a.rng[f], 0, max_thr);
-              }
+          // categorical: the wave-parallel one-hot / ctr-sorted scan
+          FeatureScanMeta m;
+          m.num_bin = fi.num_bin;
+          m.default_bin = static_cast<uint32_t>(fi.default_bin);
+          m.missing_type = fi.missing;
+          m.bin_type = fi.bin_type;
+          m.monotone = fi.monotone;
+          m.penalty = fi.penalty;
+          int rt = 0;
+          if (a.sp.extra_trees && lane == 0) {
+            // (categorical draws happen here; numerical ones were drawn above)
+            if (fi.num_bin <= a.sp.max_cat_to_onehot) {
+              if (fi.num_bin - 1 > 0) rt = RandNextInt(&a.rng[f], 1, fi.num_bin);
+            } else {
+              const double cf = n / (sh + 2 * kEpsilon);
+              int used = 0;
+              for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(H[2 * b + 1] * cf) >= a.sp.cat_smooth;
+              const int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
+              const int max_thr = max(min(max_num_cat, used) - 1, 0);
+              if (max_thr > 0) rt = RandNextInt(&a.rng[f], 0, max_thr);
             }
-            out->Reset();
-            spi = FindBestCategorical(H, m, a.sp, sg, sh, n, po, bounds, order + sel * a.max_bin, out) ? 1 : 0;
           }
-          sp = __shfl(spi, 0, kWave) != 0;
+          m.rand_threshold = __shfl(rt, 0, kWave);
+          if (lane == 0) out->Reset();
+          sp = ScanCategoricalWave(a.sp, m, H, sg, sh, n, po, bounds, a.cat_p2, order + sel * a.cat_p2,
+                                   ckey + sel * a.cat_p2, out);
         }
         if (lane == 0) {
           if (!a.vote) a.splittable[static_cast<size_t>(lslot) * a.F + f] = sp ? 1 : 0;
@@ -1657,16 +1844,20 @@ __global__ __launch_bounds__(kVoteThreads) void k_vote_pack(Args a) {
 // Global pass: block k, wave `sel` scans elected feature k of child sel from the summed
 // packed rows with the GLOBAL leaf statistics; writes the candidate table (one row of
 // 2 x top_k positions) that the partition's select reads.
-template <typename Acc>
+template <typename Acc, bool kGlobal>
 __global__ __launch_bounds__(128) void k_vote_scan(Args a) {
-  extern __shared__ __align__(16) unsigned char smem[];
+  extern __shared__ __align__(16) unsigned char smem_dyn[];
+  unsigned char* smem = kGlobal ? reinterpret_cast<unsigned char*>(a.scan_scratch) + blockIdx.x * a.scan_scratch_stride
+                                : smem_dyn;
   const Ctl c = *a.ctl;
   if (c.done || c.skip) return;
   const int K = a.topk, k = blockIdx.x, t = threadIdx.x, lane = t & 63, sel = t >> 6;
   __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
   SplitInfo* out = reinterpret_cast<SplitInfo*>(s_out_raw) + sel;
   double* H = reinterpret_cast<double*>(smem) + sel * 2 * a.max_bin;
-  int* order = reinterpret_cast<int*>(reinterpret_cast<double*>(smem) + 4 * a.max_bin) + sel * a.max_bin;
+  int* order = reinterpret_cast<int*>(reinterpret_cast<double*>(smem) + 4 * a.max_bin) + sel * a.cat_p2;
+  double* ckey = reinterpret_cast<double*>(reinterpret_cast<int*>(reinterpret_cast<double*>(smem) + 4 * a.max_bin) +
+                                           2 * a.cat_p2) + sel * a.cat_p2;
   const int* e = a.elect + sel * (K + 2);
   const int leaf = sel ? c.larger : c.smaller;
   SplitKey key;
@@ -1721,20 +1912,16 @@ __global__ __launch_bounds__(128) void k_vote_scan(Args a) {
     if (fi.bin_type == 0) {
       sp = ScanNumericalWave(a, fi, H, sums.x, sums.y, n, po, bounds, 0, out);
     } else {
-      int spi = 0;
-      if (lane == 0) {
-        FeatureScanMeta m;
-        m.num_bin = fi.num_bin;
-        m.default_bin = static_cast<uint32_t>(fi.default_bin);
-        m.missing_type = fi.missing;
-        m.bin_type = fi.bin_type;
-        m.monotone = fi.monotone;
-        m.penalty = fi.penalty;
-        m.rand_threshold = 0;
-        out->Reset();
-        spi = FindBestCategorical(H, m, a.sp, sums.x, sums.y, n, po, bounds, order, out) ? 1 : 0;
-      }
-      sp = __shfl(spi, 0, kWave) != 0;
+      FeatureScanMeta m;
+      m.num_bin = fi.num_bin;
+      m.default_bin = static_cast<uint32_t>(fi.default_bin);
+      m.missing_type = fi.missing;
+      m.bin_type = fi.bin_type;
+      m.monotone = fi.monotone;
+      m.penalty = fi.penalty;
+      m.rand_threshold = 0;
+      if (lane == 0) out->Reset();
+      sp = ScanCategoricalWave(a.sp, m, H, sums.x, sums.y, n, po, bounds, a.cat_p2, order, ckey, out);
     }
     if (lane == 0) {
       if (!sp) {
@@ -3723,11 +3910,22 @@ class DeviceTreeLearner : public TreeLearner {
       LaunchVoting(a);
       return;
     }
-    if (use_dp_) k_reduce_scan<double><<<Fmax_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks());
-    else k_reduce_scan<float><<<Fmax_, kScanThreads, scan_lds_bytes_, stream_>>>(a, HistBlocks());
+    LaunchReduceScan(a, Fmax_);
     HIP_CHECK(hipGetLastError());
     // complete the candidate table (xGMI: inside k_reduce_scan)
     if (owner_scan_ && transport_ != 2 && P_ > 1) AllGatherInPlace(cand_.get(), cand_stride_, stream_);
+  }
+
+  void LaunchReduceScan(const Args& a, int grid) {
+    const int hg = HistBlocks();
+    if (use_dp_) {
+      if (scan_global_) k_reduce_scan<double, true><<<grid, kScanThreads, 0, stream_>>>(a, hg);
+      else k_reduce_scan<double, false><<<grid, kScanThreads, scan_lds_bytes_, stream_>>>(a, hg);
+    } else {
+      if (scan_global_) k_reduce_scan<float, true><<<grid, kScanThreads, 0, stream_>>>(a, hg);
+      else k_reduce_scan<float, false><<<grid, kScanThreads, scan_lds_bytes_, stream_>>>(a, hg);
+    }
+    HIP_CHECK(hipGetLastError());
   }
 
   // The voting learner's per-split chain after k_hist (see k_vote_local).
@@ -3745,8 +3943,7 @@ class DeviceTreeLearner : public TreeLearner {
     al.own_feat = nullptr;
     al.sp.min_data_in_leaf = config_->min_data_in_leaf / P_;  // integer division (reference :61-63)
     al.sp.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf / P_;
-    if (use_dp_) k_reduce_scan<double><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(al, HistBlocks());
-    else k_reduce_scan<float><<<F_, kScanThreads, scan_lds_bytes_, stream_>>>(al, HistBlocks());
+    LaunchReduceScan(al, F_);
     HIP_CHECK(hipGetLastError());
     k_vote_local<<<1, kVoteThreads, vote_local_lds_, stream_>>>(a);
     HIP_CHECK(hipGetLastError());
@@ -3758,8 +3955,14 @@ class DeviceTreeLearner : public TreeLearner {
       if (use_dp_) AllreduceSumF64(reinterpret_cast<double*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
       else AllreduceSumF32(reinterpret_cast<float*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
     }
-    if (use_dp_) k_vote_scan<double><<<topk_, 128, vote_scan_lds_, stream_>>>(a);
-    else k_vote_scan<float><<<topk_, 128, vote_scan_lds_, stream_>>>(a);
+    const size_t vlds = scan_global_ ? 0 : vote_scan_lds_;
+    if (use_dp_) {
+      if (scan_global_) k_vote_scan<double, true><<<topk_, 128, 0, stream_>>>(a);
+      else k_vote_scan<double, false><<<topk_, 128, vlds, stream_>>>(a);
+    } else {
+      if (scan_global_) k_vote_scan<float, true><<<topk_, 128, 0, stream_>>>(a);
+      else k_vote_scan<float, false><<<topk_, 128, vlds, stream_>>>(a);
+    }
     HIP_CHECK(hipGetLastError());
   }
 
@@ -3818,16 +4021,24 @@ class DeviceTreeLearner : public TreeLearner {
     h_feats_ = feats;
     max_bin_ = 2;
     for (int f = 0; f < F_; ++f) max_bin_ = std::max(max_bin_, data_->feature(f).num_bin);
-    // k_reduce_scan: two full histograms + 16x64 partials + 2 categorical order arrays
-    scan_lds_bytes_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + 16 * 64 * sizeof(double) +
-                      static_cast<size_t>(max_bin_) * 2 * sizeof(int);
-    if (scan_lds_bytes_ > 150 * 1024) {
-      Log::Fatal("A feature with %d bins exceeds the HIP split-scan LDS budget; lower max_bin", max_bin_);
+    // k_reduce_scan: two full histograms + 16x64 partials + 2 categorical sort arrays (bin, ctr)
+    cat_p2_ = 1;
+    if (has_cat_) {
+      while (cat_p2_ < max_cat_bin_) cat_p2_ <<= 1;
     }
-    if (scan_lds_bytes_ > 64 * 1024) {
-      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_reduce_scan<float>),
+    scan_lds_bytes_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + 16 * 64 * sizeof(double) +
+                      static_cast<size_t>(cat_p2_) * 2 * (sizeof(int) + sizeof(double));
+    // wider than the LDS budget: the scan kernels work in global scratch (one slice per block)
+    scan_global_ = scan_lds_bytes_ > 150 * 1024 || std::getenv("LGAP_SCAN_GLOBAL") != nullptr;
+    scan_scratch_stride_ = Round256(scan_lds_bytes_);
+    if (scan_global_) {
+      scan_scratch_.Resize(scan_scratch_stride_ * static_cast<size_t>(std::max(F_, 1)));
+      Log::Debug("HIP split scan: %d-bin features use %zu bytes of global scratch per block", max_bin_,
+                 scan_scratch_stride_);
+    } else if (scan_lds_bytes_ > 64 * 1024) {
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_reduce_scan<float, false>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(scan_lds_bytes_)));
-      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_reduce_scan<double>),
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_reduce_scan<double, false>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(scan_lds_bytes_)));
     }
     std::vector<int> gs(std::max(G_, 1));
@@ -3978,7 +4189,8 @@ class DeviceTreeLearner : public TreeLearner {
       vote_local_lds_ = static_cast<size_t>(F_) * (sizeof(double) + sizeof(int));
       vote_pack_lds_ = static_cast<size_t>(R) * (sizeof(double) + 3 * sizeof(int)) + sizeof(int) * (kVoteThreads / 64) +
                        2 * sizeof(int) * topk_;
-      vote_scan_lds_ = static_cast<size_t>(max_bin_) * (4 * sizeof(double) + 2 * sizeof(int));
+      vote_scan_lds_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) +
+                       static_cast<size_t>(cat_p2_) * 2 * (sizeof(int) + sizeof(double));
       auto big = [](const void* fn, size_t bytes) {
         if (bytes > 64 * 1024) {
           HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes)));
@@ -3991,8 +4203,10 @@ class DeviceTreeLearner : public TreeLearner {
       big(reinterpret_cast<const void*>(k_vote_local), vote_local_lds_);
       big(reinterpret_cast<const void*>(k_vote_pack<float>), vote_pack_lds_);
       big(reinterpret_cast<const void*>(k_vote_pack<double>), vote_pack_lds_);
-      big(reinterpret_cast<const void*>(k_vote_scan<float>), vote_scan_lds_);
-      big(reinterpret_cast<const void*>(k_vote_scan<double>), vote_scan_lds_);
+      if (!scan_global_) {
+        big(reinterpret_cast<const void*>(k_vote_scan<float, false>), vote_scan_lds_);
+        big(reinterpret_cast<const void*>(k_vote_scan<double, false>), vote_scan_lds_);
+      }
     }
     rx_.Resize(std::max<size_t>(1, 2 * static_cast<size_t>(bbin_) * (use_dp_ ? 8 : 4)));
     stage_.Resize(owner_scan_ ? static_cast<size_t>(P_) * 2 * bbin_ * (use_dp_ ? 8 : 4) : 1);
@@ -4079,6 +4293,9 @@ class DeviceTreeLearner : public TreeLearner {
     a.rng = rng_.get();
     a.max_cat_bin = max_cat_bin_;
     a.max_bin = max_bin_;
+    a.cat_p2 = cat_p2_;
+    a.scan_scratch = scan_global_ ? scan_scratch_.get() : nullptr;
+    a.scan_scratch_stride = scan_scratch_stride_;
     a.max_depth = config_->max_depth;
     // 0: separate k_post kernel, 1: block 0 after its tiles, 2: first spare block
     a.fuse_post = getenv("LGAP_SPLIT_POST") ? 0 : config_->device_post_mode;
@@ -4333,7 +4550,10 @@ class DeviceTreeLearner : public TreeLearner {
   bool has_cat_ = false, use_bag_ = false, use_bynode_ = false, use_dp_ = false;
   data_size_t bag_cnt_ = 0;
   size_t hist_lds_bytes_ = 0, scan_lds_bytes_ = 0;
-  int max_bin_ = 2;
+  int max_bin_ = 2, cat_p2_ = 1;
+  bool scan_global_ = false;
+  size_t scan_scratch_stride_ = 0;
+  DevBuf<char> scan_scratch_;
   std::string device_name_;
   hipStream_t stream_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;

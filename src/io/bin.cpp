@@ -2,6 +2,7 @@
 // bin, optional NaN bin, forced bounds) and categorical (frequency ordered,
 // 99% coverage) binning. Reference semantics: src/io/bin.cpp:78-508.
 #include "lgap/bin.h"
+#include "lgap/split_math.h"
 
 #include <algorithm>
 #include <cstring>
@@ -293,7 +294,16 @@ void BinMapper::FindBin(double* values, int num_values, size_t total_sample_cnt,
       num_bin_ = 1;
       int used = 0;
       size_t k = 0;
+      // categorical splits carry their left-bin set as a kMaxCatWords-word bitset (host and
+      // device share SplitInfo): at most 1024 category bins; rarer categories fold into bin 0
+      // (the reference has no cap; it only binds for > 1024 frequent categories)
+      constexpr int kMaxCatBins = kMaxCatWords * 32;
       while (k < order.size() && (used < cut_cnt || num_bin_ < max_bin)) {
+        if (num_bin_ >= kMaxCatBins) {
+          Log::Warning("Categorical feature has more than %d frequent categories; the rarest ones share bin 0",
+                       kMaxCatBins - 1);
+          break;
+        }
         int c = order[k];
         if (ic[c] < min_data_in_bin && k > 1) break;
         bin_2_cat_.push_back(iv[c]);

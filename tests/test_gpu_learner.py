@@ -588,3 +588,58 @@ print(json.dumps({{"ev": ev["v"], "best": b.best_iteration, "pred": b.predict(Xv
         np.testing.assert_allclose(dev["ev"][name], host["ev"][name], rtol=1e-9, atol=1e-12, err_msg=name)
     np.testing.assert_allclose(dev["pred"], host["pred"], rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(dev["inner"], host["inner"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("ncat,onehot", [(1500, 4), (40, 64), (300, 4)])
+def test_device_categorical_wide(lgb, gpu_required, rng, ncat, onehot):
+    """Categorical features between max_cat_to_onehot and the 1024-bin bitset cap (1500 distinct
+    categories fold their rarest into bin 0): the wave-parallel one-hot / bitonic ctr-sorted device
+    scan picks the CPU learner's splits."""
+    n = 200_000
+    X = rng.standard_normal((n, 4))
+    X[:, 0] = rng.integers(0, ncat, n)
+    eff = rng.standard_normal(ncat)
+    y = (eff[X[:, 0].astype(int)] + 0.5 * X[:, 1] + 0.3 * rng.standard_normal(n) > 0).astype(float)
+    kw = {"categorical_feature": [0], "max_cat_to_onehot": onehot, "max_bin": 2047, "min_data_per_group": 20,
+          "cat_smooth": 5.0, "max_cat_threshold": 64, "num_leaves": 15}
+    bc = _train(lgb, X, y, "cpu", rounds=3, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=3, gpu_use_dp=True, **kw)
+    nb = lgb.Dataset(X, y, params={"categorical_feature": [0], "max_bin": 2047, "verbosity": -1}).construct() \
+        .feature_num_bin(0)
+    assert nb <= 1024 and (nb > onehot) == (ncat > onehot), nb  # ctr-sorted vs one-hot path
+    sc = [s[:2] for s in _splits(_trees(bc)[0]["tree_structure"], [])][:4]
+    sg = [s[:2] for s in _splits(_trees(bg)[0]["tree_structure"], [])][:4]
+    assert sc == sg
+    np.testing.assert_allclose(bg.predict(X[:5000], raw_score=True), bc.predict(X[:5000], raw_score=True),
+                               rtol=0, atol=2e-3)
+
+
+def test_device_max_bin_8191_global_scan(lgb, gpu_required, rng):
+    """max_bin=8191: the split scan works in global scratch (features wider than the LDS budget)
+    and matches the CPU learner; the same global path forced on ordinary bins (LGAP_SCAN_GLOBAL)
+    grows the model of the LDS path."""
+    import os
+    import subprocess
+    import sys
+
+    n = 300_000
+    X = rng.standard_normal((n, 5))
+    y = (X[:, 0] + 0.5 * np.sin(3 * X[:, 1]) + 0.2 * rng.standard_normal(n) > 0).astype(float)
+    kw = {"max_bin": 8191, "num_leaves": 15, "min_data_in_bin": 1}
+    bc = _train(lgb, X, y, "cpu", rounds=2, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=2, gpu_use_dp=True, **kw)
+    assert _splits(_trees(bc)[0]["tree_structure"], []) == _splits(_trees(bg)[0]["tree_structure"], [])
+    np.testing.assert_allclose(bg.predict(X[:5000], raw_score=True), bc.predict(X[:5000], raw_score=True),
+                               rtol=0, atol=1e-6)
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import lambdagap_amd as lgb; "
+            "from lambdagap_amd.utils import make_higgs_like; X, y = make_higgs_like(100000, seed=2); "
+            "p = {'objective': 'binary', 'num_leaves': 31, 'device_type': 'gpu', 'verbosity': -1}; "
+            "print(lgb.train(p, lgb.Dataset(X, y, params=p), 5).model_to_string().split('end of trees')[0])"
+            ) % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for env in ({}, {"LGAP_SCAN_GLOBAL": "1"}):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, **env))
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout)
+    assert outs[0] == outs[1]
