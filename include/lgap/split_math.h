@@ -51,6 +51,20 @@ struct LeafBounds {
   double max = INFINITY;
 };
 
+// Threshold-dependent bounds of one feature of one leaf (the "advanced" monotone
+// method, reference monotone_constraints.hpp:145-257 CumulativeFeatureConstraint).
+// Arrays of num_bin entries: for a reverse-pass threshold whose right side starts
+// at bin t, the left child is bounded by [lmin[t], lmax[t]] (extremes over bins
+// < t) and the right child by [rmin[t], rmax[t]] (extremes over bins >= t). The
+// forward pass keeps the reference's fixed cursor: left bounded by bin 0's
+// constraint (lmin[1], lmax[1]), right by the whole feature's (rmin[0], rmax[0]).
+struct ThresholdBounds {
+  const double* lmin;
+  const double* lmax;
+  const double* rmin;
+  const double* rmax;
+};
+
 // Fixed-size POD split record; also the on-wire record of the parallel learners
 // (reference split_info.hpp:22-294 / LightSplitInfo).
 struct SplitInfo {
@@ -129,15 +143,22 @@ LGAP_HD inline double LeafGain(double g, double h, const SplitParams& p, data_si
   return LeafGainGivenOutput(g, h, p, out);
 }
 
-LGAP_HD inline double SplitGain(double lg, double lh, double rg, double rh, const SplitParams& p, int8_t monotone,
-                                data_size_t lc, data_size_t rc, double parent_output, const LeafBounds& b) {
+// Gain of a split whose children are bounded by `lb` / `rb` (feature_histogram.hpp:755-796).
+LGAP_HD inline double SplitGain2(double lg, double lh, double rg, double rh, const SplitParams& p, int8_t monotone,
+                                 data_size_t lc, data_size_t rc, double parent_output, const LeafBounds& lb,
+                                 const LeafBounds& rb) {
   if (!p.use_monotone) {
     return LeafGain(lg, lh, p, lc, parent_output) + LeafGain(rg, rh, p, rc, parent_output);
   }
-  const double lo = LeafOutput(lg, lh, p, lc, parent_output, b);
-  const double ro = LeafOutput(rg, rh, p, rc, parent_output, b);
+  const double lo = LeafOutput(lg, lh, p, lc, parent_output, lb);
+  const double ro = LeafOutput(rg, rh, p, rc, parent_output, rb);
   if ((monotone > 0 && lo > ro) || (monotone < 0 && lo < ro)) return 0.0;
   return LeafGainGivenOutput(lg, lh, p, lo) + LeafGainGivenOutput(rg, rh, p, ro);
+}
+
+LGAP_HD inline double SplitGain(double lg, double lh, double rg, double rh, const SplitParams& p, int8_t monotone,
+                                data_size_t lc, data_size_t rc, double parent_output, const LeafBounds& b) {
+  return SplitGain2(lg, lh, rg, rh, p, monotone, lc, rc, parent_output, b, b);
 }
 
 LGAP_HD inline int RoundCount(double x) { return static_cast<int>(x + 0.5f); }
@@ -145,15 +166,24 @@ LGAP_HD inline int RoundCount(double x) { return static_cast<int>(x + 0.5f); }
 // ----------------------------------------------------------------------------
 // Sequential numerical scan over one full feature histogram (`hist` = 2*num_bin doubles).
 // `out` must be Reset by the caller; the best of REVERSE / forward passes is kept.
+// `tb` (advanced monotone) replaces `bounds` with per-threshold child bounds.
 LGAP_HD inline void ScanNumericalPass(const double* hist, const FeatureScanMeta& m, const SplitParams& p,
                                       double sum_g, double sum_h, data_size_t num_data, double min_gain_shift,
                                       double parent_output, const LeafBounds& bounds, bool reverse, bool skip_default,
-                                      bool na_as_missing, bool* splittable, SplitInfo* out) {
+                                      bool na_as_missing, bool* splittable, SplitInfo* out,
+                                      const ThresholdBounds* tb = nullptr) {
   const double cnt_factor = num_data / sum_h;
   double best_lg = NAN, best_lh = NAN, best_gain = kMinScore;
   data_size_t best_lc = 0;
   uint32_t best_t = static_cast<uint32_t>(m.num_bin);
   const bool use_rand = p.extra_trees != 0;
+  LeafBounds lb = bounds, rb = bounds, best_lb = bounds, best_rb = bounds;
+  if (tb != nullptr && !reverse) {
+    lb.min = tb->lmin[1];
+    lb.max = tb->lmax[1];
+    rb.min = tb->rmin[0];
+    rb.max = tb->rmax[0];
+  }
   if (reverse) {
     double rg = 0.0, rh = kEpsilon;
     data_size_t rc = 0;
@@ -170,10 +200,20 @@ LGAP_HD inline void ScanNumericalPass(const double* hist, const FeatureScanMeta&
       if (lh < p.min_sum_hessian_in_leaf) break;
       const double lg = sum_g - rg;
       if (use_rand && t - 1 != m.rand_threshold) continue;
-      const double gain = SplitGain(lg, lh, rg, rh, p, m.monotone, lc, rc, parent_output, bounds);
+      if (tb != nullptr) {
+        lb.min = tb->lmin[t];
+        lb.max = tb->lmax[t];
+        rb.min = tb->rmin[t];
+        rb.max = tb->rmax[t];
+      }
+      const double gain = SplitGain2(lg, lh, rg, rh, p, m.monotone, lc, rc, parent_output, lb, rb);
       if (gain <= min_gain_shift) continue;
       *splittable = true;
       if (gain > best_gain) {
+        // a threshold whose child bounds cross cannot be taken (feature_histogram.hpp:920-926)
+        if (p.use_monotone && (lb.min > lb.max || rb.min > rb.max)) continue;
+        best_lb = lb;
+        best_rb = rb;
         best_lc = lc;
         best_lg = lg;
         best_lh = lh;
@@ -198,10 +238,13 @@ LGAP_HD inline void ScanNumericalPass(const double* hist, const FeatureScanMeta&
       if (rh < p.min_sum_hessian_in_leaf) break;
       const double rg = sum_g - lg;
       if (use_rand && t != m.rand_threshold) continue;
-      const double gain = SplitGain(lg, lh, rg, rh, p, m.monotone, lc, rc, parent_output, bounds);
+      const double gain = SplitGain2(lg, lh, rg, rh, p, m.monotone, lc, rc, parent_output, lb, rb);
       if (gain <= min_gain_shift) continue;
       *splittable = true;
       if (gain > best_gain) {
+        if (p.use_monotone && (lb.min > lb.max || rb.min > rb.max)) continue;
+        best_lb = lb;
+        best_rb = rb;
         best_lc = lc;
         best_lg = lg;
         best_lh = lh;
@@ -212,11 +255,11 @@ LGAP_HD inline void ScanNumericalPass(const double* hist, const FeatureScanMeta&
   }
   if (*splittable && best_gain > out->gain + min_gain_shift) {
     out->threshold = best_t;
-    out->left_output = LeafOutput(best_lg, best_lh, p, best_lc, parent_output, bounds);
+    out->left_output = LeafOutput(best_lg, best_lh, p, best_lc, parent_output, best_lb);
     out->left_count = best_lc;
     out->left_sum_gradient = best_lg;
     out->left_sum_hessian = best_lh - kEpsilon;
-    out->right_output = LeafOutput(sum_g - best_lg, sum_h - best_lh, p, num_data - best_lc, parent_output, bounds);
+    out->right_output = LeafOutput(sum_g - best_lg, sum_h - best_lh, p, num_data - best_lc, parent_output, best_rb);
     out->right_count = num_data - best_lc;
     out->right_sum_gradient = sum_g - best_lg;
     out->right_sum_hessian = sum_h - best_lh - kEpsilon;
@@ -229,7 +272,7 @@ LGAP_HD inline void ScanNumericalPass(const double* hist, const FeatureScanMeta&
 // sum_h must already include the +2*kEpsilon of the reference (caller passes raw sums).
 LGAP_HD inline bool FindBestNumerical(const double* hist, const FeatureScanMeta& m, const SplitParams& p,
                                       double sum_g, double sum_h_raw, data_size_t num_data, double parent_output,
-                                      const LeafBounds& bounds, SplitInfo* out) {
+                                      const LeafBounds& bounds, SplitInfo* out, const ThresholdBounds* tb = nullptr) {
   const double sum_h = sum_h_raw + 2 * kEpsilon;
   out->default_left = 1;
   out->gain = kMinScore;
@@ -240,18 +283,18 @@ LGAP_HD inline bool FindBestNumerical(const double* hist, const FeatureScanMeta&
   if (m.num_bin > 2 && mt != static_cast<int8_t>(MissingType::None)) {
     if (mt == static_cast<int8_t>(MissingType::Zero)) {
       ScanNumericalPass(hist, m, p, sum_g, sum_h, num_data, min_gain_shift, parent_output, bounds, true, true, false,
-                        &splittable, out);
+                        &splittable, out, tb);
       ScanNumericalPass(hist, m, p, sum_g, sum_h, num_data, min_gain_shift, parent_output, bounds, false, true, false,
-                        &splittable, out);
+                        &splittable, out, tb);
     } else {
       ScanNumericalPass(hist, m, p, sum_g, sum_h, num_data, min_gain_shift, parent_output, bounds, true, false, true,
-                        &splittable, out);
+                        &splittable, out, tb);
       ScanNumericalPass(hist, m, p, sum_g, sum_h, num_data, min_gain_shift, parent_output, bounds, false, false, true,
-                        &splittable, out);
+                        &splittable, out, tb);
     }
   } else {
     ScanNumericalPass(hist, m, p, sum_g, sum_h, num_data, min_gain_shift, parent_output, bounds, true, false, false,
-                      &splittable, out);
+                      &splittable, out, tb);
     if (mt == static_cast<int8_t>(MissingType::NaN)) out->default_left = 0;
   }
   out->gain *= m.penalty;
@@ -265,8 +308,9 @@ LGAP_HD inline bool FindBestCategorical(const double* hist, const FeatureScanMet
   const double sum_h = sum_h_raw + 2 * kEpsilon;
   out->default_left = 0;
   out->gain = kMinScore;
+  // monotone bounds still clamp the outputs (monotone type 0: no order check),
+  // feature_histogram.cpp:195-199
   SplitParams p = p_in;
-  p.use_monotone = 0;
   double gain_shift;
   if (p.path_smooth > kEpsilon) {
     gain_shift = LeafGainGivenOutput(sum_g, sum_h, p, parent_output);

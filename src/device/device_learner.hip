@@ -1136,8 +1136,7 @@ __device__ bool ScanCategoricalWave(const SplitParams& p_in, const FeatureScanMe
                                     int* order, double* key, SplitInfo* out) {
   const int lane = threadIdx.x & 63;
   const double sum_h = sum_h_raw + 2 * kEpsilon;
-  SplitParams p = p_in;
-  p.use_monotone = 0;
+  SplitParams p = p_in;  // monotone bounds clamp categorical outputs too (type 0: no order check)
   double gain_shift;
   if (p.path_smooth > kEpsilon) {
     gain_shift = LeafGainGivenOutput(sum_g, sum_h, p, po);

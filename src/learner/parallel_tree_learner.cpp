@@ -236,9 +236,9 @@ void VotingParallelTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, b
     bl[f].Reset();
     if (!bytree[f]) continue;
     bool sp;
-    bs[f] = BestSplitForFeature(hs, f, ls, ParentOutput(tree, ls), bounds_[smaller_.leaf], &sp);
+    bs[f] = BestSplitForFeature(hs, f, ls, ParentOutput(tree, ls), bounds_[smaller_.leaf], nullptr, &sp);
     if (has_larger) bl[f] = BestSplitForFeature(HistOf(larger_.leaf).data(), f, ll, ParentOutput(tree, ll),
-                                                bounds_[larger_.leaf], &sp);
+                                                bounds_[larger_.leaf], nullptr, &sp);
   }
   config_ = saved;
   const int top_k = std::min(config_->top_k, num_features_);

@@ -161,7 +161,7 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian
   partition_.Init(num_data_, config_->num_leaves);
   col_sampler_.Init(train_data, config_);
   best_split_per_leaf_.assign(config_->num_leaves, SplitInfo());
-  hist_.assign(config_->num_leaves, {});
+  ResetHistPool();
   splittable_.assign(config_->num_leaves, std::vector<char>(num_features_, 1));
   bounds_.assign(config_->num_leaves, LeafBounds());
   leaf_count_global_.assign(config_->num_leaves, 0);
@@ -185,11 +185,11 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
   if (static_cast<int>(best_split_per_leaf_.size()) != config->num_leaves) {
     partition_.Init(num_data_, config->num_leaves);
     best_split_per_leaf_.assign(config->num_leaves, SplitInfo());
-    hist_.assign(config->num_leaves, {});
     splittable_.assign(config->num_leaves, std::vector<char>(num_features_, 1));
     bounds_.assign(config->num_leaves, LeafBounds());
     leaf_count_global_.assign(config->num_leaves, 0);
   }
+  if (train_data_ != nullptr) ResetHistPool();
   col_sampler_.Init(train_data_, config_);
   use_monotone_ = !config_->monotone_constraints.empty();
   SetupPolicies();
@@ -197,10 +197,9 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
 
 void SerialTreeLearner::SetupPolicies() {
   intermediate_monotone_ = use_monotone_ && config_->monotone_constraints_method != "basic";
-  if (use_monotone_ && config_->monotone_constraints_method == "advanced") {
-    Log::Warning("monotone_constraints_method=advanced is served by the intermediate method");
+  if (intermediate_monotone_) {
+    mono_.Init(train_data_, config_->num_leaves, config_->monotone_constraints_method == "advanced");
   }
-  if (intermediate_monotone_) mono_.Init(train_data_, config_->num_leaves);
   if (CegbPenalty::Enabled(config_)) {
     if (!cegb_) cegb_ = std::make_unique<CegbPenalty>();
     cegb_->Init(train_data_, config_);
@@ -237,9 +236,39 @@ SplitParams SerialTreeLearner::MakeParams() const {
   return p;
 }
 
+void SerialTreeLearner::ResetHistPool() {
+  const int L = config_->num_leaves;
+  int cap = L;
+  if (config_->histogram_pool_size > 0) {
+    const double per_leaf = 16.0 * train_data_->num_total_bin();  // (grad, hess) doubles per bin
+    cap = static_cast<int>(config_->histogram_pool_size * 1024 * 1024 / per_leaf);
+  }
+  hist_cap_ = std::min(std::max(2, cap), L);
+  Log::Debug("Histogram pool: %d of %d leaves", hist_cap_, L);
+  hist_.assign(L, {});
+  hist_stamp_.assign(L, 0);
+  hist_live_ = 0;
+}
+
 std::vector<double>& SerialTreeLearner::HistOf(int leaf) {
   auto& h = hist_[leaf];
-  if (h.size() != static_cast<size_t>(2 * train_data_->num_total_bin())) h.assign(2 * train_data_->num_total_bin(), 0.0);
+  const size_t want = static_cast<size_t>(2 * train_data_->num_total_bin());
+  if (h.size() == want) return h;
+  if (hist_live_ >= hist_cap_) {
+    // drop the oldest histogram not in use by the two current leaves
+    int victim = -1;
+    for (int l = 0; l < static_cast<int>(hist_.size()); ++l) {
+      if (l == leaf || l == smaller_.leaf || l == larger_.leaf || hist_[l].size() != want) continue;
+      if (victim < 0 || hist_stamp_[l] < hist_stamp_[victim]) victim = l;
+    }
+    if (victim >= 0) {
+      std::vector<double>().swap(hist_[victim]);
+      --hist_live_;
+    }
+  }
+  h.assign(want, 0.0);
+  ++hist_live_;
+  hist_stamp_[leaf] = ++hist_clock_;
   return h;
 }
 
@@ -348,7 +377,7 @@ double SerialTreeLearner::MonotonePenalty(const Tree* tree, int leaf) const {
 
 SplitInfo SerialTreeLearner::BestSplitForFeature(const double* group_hist, int f, const LeafStat& leaf,
                                                  double parent_output, const LeafBounds& bounds,
-                                                 bool* splittable) const {
+                                                 const ThresholdBounds* tb, bool* splittable) const {
   const FeatureInfo& fi = train_data_->feature(f);
   std::vector<double> full(2 * fi.num_bin);
   train_data_->FeatureHistogram(group_hist, f, leaf.sum_g, leaf.sum_h, full.data());
@@ -380,7 +409,8 @@ SplitInfo SerialTreeLearner::BestSplitForFeature(const double* group_hist, int f
   }
   bool sp;
   if (fi.bin_type == BinType::Numerical) {
-    sp = FindBestNumerical(full.data(), m, p, leaf.sum_g, leaf.sum_h, leaf.global_count, parent_output, bounds, &out);
+    sp = FindBestNumerical(full.data(), m, p, leaf.sum_g, leaf.sum_h, leaf.global_count, parent_output, bounds, &out,
+                           tb);
   } else {
     std::vector<int> order(fi.num_bin);
     sp = FindBestCategorical(full.data(), m, p, leaf.sum_g, leaf.sum_h, leaf.global_count, parent_output, bounds,
@@ -459,7 +489,12 @@ bool SerialTreeLearner::BeforeFindBestSplit(const Tree* tree, int left, int righ
   has_parent_hist_ = false;
   if (right >= 0) {
     // the parent histogram lives in hist_[left]; hand it to the larger child
-    if (larger_.leaf == right) std::swap(hist_[left], hist_[right]), std::swap(splittable_[left], splittable_[right]);
+    if (larger_.leaf == right) {
+      std::swap(hist_[left], hist_[right]);
+      std::swap(hist_stamp_[left], hist_stamp_[right]);
+      std::swap(splittable_[left], splittable_[right]);
+    }
+    hist_stamp_[larger_.leaf] = ++hist_clock_;
     has_parent_hist_ = hist_[larger_.leaf].size() == static_cast<size_t>(2 * train_data_->num_total_bin());
     // the smaller child inherits the parent's splittable flags too
     splittable_[smaller_.leaf] = splittable_[larger_.leaf];
@@ -531,7 +566,17 @@ void SerialTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, bool use_
 
 SplitInfo SerialTreeLearner::ScoreFeature(const Tree* tree, const double* group_hist, int f, const LeafStat& leaf,
                                           double parent_output, bool* splittable) {
-  SplitInfo s = BestSplitForFeature(group_hist, f, leaf, parent_output, bounds_[leaf.leaf], splittable);
+  SplitInfo s;
+  if (intermediate_monotone_ && mono_.advanced() && train_data_->feature(f).bin_type == BinType::Numerical) {
+    // advanced monotone: the bounds of this feature's thresholds (serial_tree_learner.cpp:970-974)
+    std::vector<double> scratch;
+    ThresholdBounds tb;
+    LeafBounds flat;
+    const bool varies = mono_.ThresholdBoundsFor(tree, f, leaf.leaf, &scratch, &tb, &flat);
+    s = BestSplitForFeature(group_hist, f, leaf, parent_output, flat, varies ? &tb : nullptr, splittable);
+  } else {
+    s = BestSplitForFeature(group_hist, f, leaf, parent_output, bounds_[leaf.leaf], nullptr, splittable);
+  }
   if (s.feature < 0) return s;
   if (cegb_) s.gain -= cegb_->DeltaGain(f, leaf.leaf, partition_.indices(leaf.leaf), partition_.count(leaf.leaf), s);
   if (s.monotone_type != 0) s.gain *= MonotonePenalty(tree, leaf.leaf);
@@ -542,7 +587,12 @@ SplitInfo SerialTreeLearner::ScoreFeature(const Tree* tree, const double* group_
 // histogram; its statistics come from the pending best split
 void SerialTreeLearner::RecomputeBestSplit(const Tree* tree, int leaf) {
   SplitInfo& cur = best_split_per_leaf_[leaf];
-  if (hist_[leaf].size() != static_cast<size_t>(2 * train_data_->num_total_bin())) return;
+  if (hist_[leaf].size() != static_cast<size_t>(2 * train_data_->num_total_bin())) {
+    // dropped from the histogram pool: rebuilt from the leaf's rows (the reference skips the
+    // rescan here, serial_tree_learner.cpp:1025-1031, leaving a split that may break the
+    // tightened bounds)
+    BuildHistogram(partition_.indices(leaf), partition_.count(leaf), HistOf(leaf).data());
+  }
   LeafStat ls;
   ls.leaf = leaf;
   ls.sum_g = cur.left_sum_gradient + cur.right_sum_gradient;
@@ -556,13 +606,15 @@ void SerialTreeLearner::RecomputeBestSplit(const Tree* tree, int leaf) {
   }
   ls.output = po;
   const auto& bytree = col_sampler_.is_feature_used_bytree();
+  // node-level sampling and interaction constraints of this leaf (serial_tree_learner.cpp:1050)
+  const std::vector<int8_t> node_used = col_sampler_.GetByNode(tree, leaf);
   SplitInfo best;
   best.Reset();
   for (int f = 0; f < num_features_; ++f) {
     if (!bytree[f] || !feature_mask_[f] || !splittable_[leaf][f]) continue;
     bool sp;
     SplitInfo s = ScoreFeature(tree, hist_[leaf].data(), f, ls, po, &sp);
-    if (s.feature >= 0 && s.BetterThan(best)) best = s;
+    if (node_used[f] && s.feature >= 0 && s.BetterThan(best)) best = s;
   }
   cur = best;
 }

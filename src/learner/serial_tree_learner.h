@@ -102,12 +102,13 @@ class SerialTreeLearner : public TreeLearner {
   void BuildHistogram(const data_size_t* idx, data_size_t n, double* hist) const;
   void ComputeLeafSums(const data_size_t* idx, data_size_t n, double* sg, double* sh) const;
   SplitInfo BestSplitForFeature(const double* group_hist, int f, const LeafStat& leaf, double parent_output,
-                                const LeafBounds& bounds, bool* splittable) const;
+                                const LeafBounds& bounds, const ThresholdBounds* tb, bool* splittable) const;
   double ParentOutput(const Tree* tree, const LeafStat& ls) const;
   double MonotonePenalty(const Tree* tree, int leaf) const;
   void InitLeafStat(LeafStat* ls, int leaf, double sg, double sh, double output);
   SplitParams MakeParams() const;
   std::vector<double>& HistOf(int leaf);
+  void ResetHistPool();
   void SetupPolicies();
   int ForceSplits(Tree* tree, int* left_leaf, int* right_leaf);
   // BestSplitForFeature + CEGB deduction + monotone split penalty (ComputeBestSplitForFeature)
@@ -129,6 +130,12 @@ class SerialTreeLearner : public TreeLearner {
   ColSampler col_sampler_;
   std::vector<SplitInfo> best_split_per_leaf_;
   std::vector<std::vector<double>> hist_;            // per leaf, 2*num_total_bin
+  // histogram_pool_size: at most hist_cap_ leaf histograms live at once; the one
+  // produced longest ago is dropped first (reference HistogramPool LRU,
+  // feature_histogram.hpp:1367-1594)
+  int hist_cap_ = 0, hist_live_ = 0;
+  int64_t hist_clock_ = 0;
+  std::vector<int64_t> hist_stamp_;
   std::vector<std::vector<char>> splittable_;        // per leaf, per feature
   std::vector<LeafBounds> bounds_;                   // monotone basic constraints
   std::vector<data_size_t> leaf_count_global_;
@@ -138,7 +145,7 @@ class SerialTreeLearner : public TreeLearner {
   Random extra_rand_;
   bool use_monotone_ = false;
   bool intermediate_monotone_ = false;
-  IntermediateMonotone mono_;
+  MonotoneLeafConstraints mono_;
   std::unique_ptr<CegbPenalty> cegb_;
   GradientQuantizer quantizer_;
   std::vector<score_t> qgrad_, qhess_;

@@ -19,6 +19,7 @@
 #include "lgap/pointwise_metric.h"
 #include "lgap/random.h"
 #include "lgap/split_math.h"
+#include "learner/leaf_constraints.h"
 
 namespace {
 
@@ -207,6 +208,36 @@ void TestParallelErrorsReturnMinusOne() {
 
 }  // namespace
 
+// Piecewise per-bin bounds of the advanced monotone method against a dense per-bin
+// model (reference monotone_constraints.hpp:872-965 UpdateConstraints semantics:
+// a leaf output tightens the bound on the bin range [b, e) it shares).
+void TestBinPiecesMatchDenseBounds() {
+  lgap::Random r(7);
+  for (int trial = 0; trial < 400; ++trial) {
+    const int nb = 2 + r.NextShort(0, 60);
+    const bool raise = trial & 1;
+    lgap::BinPieces p;
+    p.Reset(raise ? -INFINITY : INFINITY);
+    std::vector<double> dense(nb, raise ? -INFINITY : INFINITY);
+    for (int op = 0; op < 12; ++op) {
+      const double v = r.NextShort(-8, 8) * 0.25;
+      if (r.NextShort(0, 5) == 0) {
+        p.TightenAll(v, raise);
+        for (double& x : dense) x = raise ? std::max(x, v) : std::min(x, v);
+        continue;
+      }
+      const uint32_t b = r.NextShort(0, nb), e = b + 1 + r.NextShort(0, nb);
+      p.TightenRange(v, raise, b, e, nb);
+      for (uint32_t t = b; t < std::min<uint32_t>(e, nb); ++t) dense[t] = raise ? std::max(dense[t], v) : std::min(dense[t], v);
+    }
+    std::vector<double> got(nb);
+    p.Expand(nb, got.data());
+    for (int t = 0; t < nb; ++t) EXPECT(got[t] == dense[t]);
+    EXPECT(p.start[0] == 0);
+    for (size_t i = 1; i < p.size(); ++i) EXPECT(p.start[i] > p.start[i - 1] && p.val[i] != p.val[i - 1]);
+  }
+}
+
 int main(int argc, char** argv) {
   const std::string data = argc > 1 ? argv[1] : "tests/data";
   TestRandom();
@@ -214,6 +245,7 @@ int main(int argc, char** argv) {
   TestPointwiseMetric();
   TestTrainPredictRoundTrip(data);
   TestParallelErrorsReturnMinusOne();
+  TestBinPiecesMatchDenseBounds();
   if (g_failures) {
     std::fprintf(stderr, "%d expectation(s) failed\n", g_failures);
     return 1;

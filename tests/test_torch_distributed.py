@@ -27,6 +27,9 @@ def _port():
 def _worker(rank, world, port, mode, learner, out_dir):
     import sys
 
+    # keep each rank's native stderr (gloo / runtime aborts) for the failure report
+    err = os.open(os.path.join(out_dir, f"err{rank}.txt"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+    os.dup2(err, 2)
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     sys.path.insert(0, ROOT)
@@ -61,7 +64,10 @@ def _run(world, mode, learner, tmp_path):
     for p in ps:
         if p.is_alive():
             p.kill()
-    assert codes == [0] * world, codes
+    if codes != [0] * world:
+        logs = {r: open(tmp_path / f"err{r}.txt").read()[-3000:] for r in range(world)
+                if os.path.exists(tmp_path / f"err{r}.txt")}
+        raise AssertionError(f"exit codes {codes}; stderr tails {logs}")
     ms = [open(tmp_path / f"m{r}.txt").read() for r in range(world)]
     trees = [m.split("end of trees")[0] for m in ms]
     assert all(t == trees[0] for t in trees)
