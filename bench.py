@@ -166,7 +166,20 @@ def main() -> int:
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
+        # orderly teardown: the device learner, then the native collectives, then the process
+        # group (left to static destructors, gloo's threads can abort the exiting process)
         dist.barrier()
+        del booster, train_set
+        if args.dp_host_transport:
+            from lambdagap_amd.parallel.torch_network import free_torch_network
+
+            free_torch_network()
+        else:
+            from lambdagap_amd.parallel.distributed import free_device_comm
+
+            free_device_comm()
+        dist.barrier()
+        dist.destroy_process_group()
     return 0
 
 

@@ -8,6 +8,7 @@ own row shard; ranks are wired together with RCCL (GPU, ``device_type=gpu``) or
 """
 from __future__ import annotations
 
+import atexit
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -15,8 +16,8 @@ import numpy as np
 from .. import basic
 from ..engine import train as _train
 from ..sklearn import LGBMClassifier, LGBMRanker, LGBMRegressor
-from .distributed import DistContext, env_context, init_device_comm
-from .torch_network import init_torch_network
+from .distributed import DistContext, env_context, free_device_comm, init_device_comm
+from .torch_network import free_torch_network, init_torch_network
 
 _WIRED: Dict[str, Any] = {}
 
@@ -35,12 +36,36 @@ def setup_network(device_type: str = "cpu", tree_learner: str = "data", backend:
 
     if not dist.is_initialized():
         dist.init_process_group(backend=backend, rank=ctx.rank, world_size=ctx.world_size)
+        _WIRED["own_group"] = True
     if device_type in ("gpu", "cuda", "hip", "rocm"):
         ctx = init_device_comm(ctx)
     else:
         init_torch_network()
     _WIRED["ctx"] = ctx
+    atexit.register(teardown_network)
     return ctx
+
+
+def teardown_network() -> None:
+    """Undo :func:`setup_network` (also run at interpreter exit): release the native
+    collectives, then the process group this module created. Without it the gloo
+    process group is torn down by static destructors while its threads still run, which
+    can abort the process after training has finished."""
+    ctx = _WIRED.pop("ctx", None)
+    if ctx is None:
+        return
+    try:
+        if getattr(ctx, "device_comm", False):
+            free_device_comm()
+        else:
+            free_torch_network()
+    finally:
+        if _WIRED.pop("own_group", False):
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.barrier()
+                dist.destroy_process_group()
 
 
 def distributed_params(params: Dict[str, Any], tree_learner: str = "data") -> Dict[str, Any]:

@@ -2,6 +2,7 @@
 // training with a unique lock and prediction / evaluation with a shared lock
 // (c_api.cpp:54-58). Exceptions become -1 + LGBM_GetLastError.
 #include "lgap/omp_errors.h"
+#include "lgap/threading.h"
 #include "lgap/c_api.h"
 
 #include <omp.h>
@@ -68,6 +69,7 @@ void CopyStrings(const std::vector<std::string>& v, int len, int* out_len, size_
 Config ParseConfig(const char* params) {
   Config c;
   c.Set(Config::Str2Map(params ? params : ""));
+  SetDefaultNumThreads(c.num_threads);  // reference c_api.cpp OMP_SET_NUM_THREADS(config.num_threads)
   return c;
 }
 
@@ -129,6 +131,7 @@ class Booster {
   Booster(DatasetWrapper* train, const char* params) : train_(train) {
     auto pm = Config::Str2Map(params);
     config_.Set(pm);
+    SetDefaultNumThreads(config_.num_threads);
     if (config_.num_machines > 1 && Network::num_machines() <= 1 && !config_.machines.empty()) {
       Network::Init(config_);
     }
@@ -188,6 +191,7 @@ class Booster {
     if (pm.count("boosting") && pm["boosting"] != config_.boosting) Log::Fatal("Cannot change boosting during training");
     if (pm.count("metric")) Log::Fatal("Cannot change metric during training");
     config_.Set(pm);
+    SetDefaultNumThreads(config_.num_threads);
     if (pm.count("objective")) {
       objective_ = ObjectiveFunction::Create(config_.objective, config_);
       if (objective_) objective_->Init(train_->ds->metadata(), train_->ds->num_data());
@@ -1016,13 +1020,13 @@ int LGBM_NetworkInitWithFunctions(int num_machines, int rank, void* reduce_scatt
 
 int LGBM_SetMaxThreads(int num_threads) {
   API_BEGIN();
-  if (num_threads > 0) omp_set_num_threads(num_threads);
+  SetMaxNumThreads(num_threads);
   API_END();
 }
 
 int LGBM_GetMaxThreads(int* out) {
   API_BEGIN();
-  *out = omp_get_max_threads();
+  *out = MaxNumThreadsSetting();
   API_END();
 }
 

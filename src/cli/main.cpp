@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "lgap/omp_errors.h"
+#include "lgap/threading.h"
 #include "lgap/boosting.h"
 #include "lgap/common.h"
 #include "lgap/config.h"
@@ -192,7 +193,7 @@ int main(int argc, char** argv) {
     ParamMap params = LoadParameters(argc, argv);
     Config c;
     c.Set(params);
-    if (c.num_threads > 0) omp_set_num_threads(c.num_threads);
+    SetDefaultNumThreads(c.num_threads);
     if (c.task == "train") Train(c);
     else if (c.task == "predict") Predict(c);
     else if (c.task == "convert_model") ConvertModel(c);

@@ -152,6 +152,11 @@ struct Args {
   int cand_stride;
   int cand_key_bytes;   // SplitKey part of a block (SplitInfo part follows)
   int scan_src;         // 0: fold the k_hist slab rows; 1: sum the `nparts` owner rows of `rx`
+  // split slab fold (scan_src 0): fold_chunks blocks per feature each fold a run of the slab
+  // rows into fold_part; the last to arrive on fold_cnt[j] sums the runs and scans
+  int fold_chunks, fold_feats;
+  double* fold_part;   // [fold_chunks][2 * TB]
+  unsigned* fold_cnt;  // [F]: a multiple of fold_chunks between launches
   int nparts;
   const void* rx;       // owner rows: nparts x (2 * bbin) values of the bins this rank owns
   int own_bin0;         // first histogram bin this rank owns
@@ -381,6 +386,9 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     a.leaf_key[i].gain = kMinScore;
   }
   for (int f = t; f < a.F; f += blockDim.x) a.splittable[f] = 1;
+  if (a.fold_cnt) {
+    for (int f = t; f < a.F; f += blockDim.x) a.fold_cnt[f] = 0u;
+  }
 }
 
 // Root statistics in two steps: per-block partials (no atomics: 1024 blocks x
@@ -1320,11 +1328,22 @@ __device__ bool ScanCategoricalWave(const SplitParams& p_in, const FeatureScanMe
 template <typename Acc, bool kGlobal>
 __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_grid) {
   extern __shared__ __align__(16) unsigned char smem_dyn[];
+  // (kGlobal launches never split the fold: blockIdx.x is the feature slot)
   unsigned char* smem = kGlobal ? reinterpret_cast<unsigned char*>(a.scan_scratch) + blockIdx.x * a.scan_scratch_stride
                                 : smem_dyn;
   const Ctl c = *a.ctl;
   if (c.done || c.skip) return;
-  const int j = blockIdx.x;
+  const int C = a.fold_chunks;
+  int j = blockIdx.x, ch = 0;
+  if (C > 1) {
+    // the C chunk blocks of a feature take consecutive places in XCD order (blocks b and b + 8
+    // usually share an XCD, so the last arriver reads its partners' runs from its own L2;
+    // speed only): the grid is padded to a multiple of 8
+    const int q = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    j = q / C;
+    ch = q - j * C;
+    if (j >= a.fold_feats) return;
+  }
   const int f = a.own_feat ? a.own_feat[j] : j;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   Stamp(a, 3, 0);
@@ -1446,16 +1465,53 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
       }
 #else
       const int half = lane >> 5;
+      // this block's run of slab rows (all of them unless the fold is split)
+      const int p0 = C > 1 ? static_cast<int>((static_cast<long long>(ch) * nb) / C) : 0;
+      const int p1 = C > 1 ? static_cast<int>((static_cast<long long>(ch + 1) * nb) / C) : nb;
+      double* run = C > 1 ? a.fold_part + static_cast<size_t>(ch) * V + v0 : nullptr;
       for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
         const int v = vbase + (lane & 31);
         double acc = 0.0;
         if (v < nv) {
           const Acc* col = slab + v0 + v;
 #pragma unroll LGAP_SCAN_UNROLL
-          for (int p = half; p < nb; p += 2) acc += static_cast<double>(col[static_cast<size_t>(p) * V]);
+          for (int p = p0 + half; p < p1; p += 2) acc += static_cast<double>(col[static_cast<size_t>(p) * V]);
         }
         acc += __shfl_xor(acc, 32, kWave);
         if (lane < 32 && v < nv) {
+          if (run) {
+            run[v] = acc;
+          } else {
+            const int k = v >> 1;
+            const int b = k < fi.mfb ? k : k + 1;
+            hs_full[2 * b + (v & 1)] = acc;
+          }
+        }
+      }
+      if (C > 1) {
+        // in-launch combine (one agent release per block, one acquire in the last arriver):
+        // runs stored -> release -> ticket; the block drawing the last ticket of this launch
+        // acquires and sums the C runs in chunk order (deterministic)
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const unsigned old = __hip_atomic_fetch_add(&a.fold_cnt[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_last = (old % static_cast<unsigned>(C)) == static_cast<unsigned>(C - 1) ? 1 : 0;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        if (t == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        const double* runs = a.fold_part + v0;
+        for (int v = t; v < nv; v += blockDim.x) {
+          double acc = 0.0;
+          for (int r = 0; r < C; ++r) acc += runs[static_cast<size_t>(r) * V + v];
           const int k = v >> 1;
           const int b = k < fi.mfb ? k : k + 1;
           hs_full[2 * b + (v & 1)] = acc;
@@ -1846,6 +1902,7 @@ __global__ __launch_bounds__(kVoteThreads) void k_vote_pack(Args a) {
 template <typename Acc, bool kGlobal>
 __global__ __launch_bounds__(128) void k_vote_scan(Args a) {
   extern __shared__ __align__(16) unsigned char smem_dyn[];
+  // (kGlobal launches never split the fold: blockIdx.x is the feature slot)
   unsigned char* smem = kGlobal ? reinterpret_cast<unsigned char*>(a.scan_scratch) + blockIdx.x * a.scan_scratch_stride
                                 : smem_dyn;
   const Ctl c = *a.ctl;
@@ -3915,8 +3972,16 @@ class DeviceTreeLearner : public TreeLearner {
     if (owner_scan_ && transport_ != 2 && P_ > 1) AllGatherInPlace(cand_.get(), cand_stride_, stream_);
   }
 
-  void LaunchReduceScan(const Args& a, int grid) {
+  void LaunchReduceScan(const Args& a0, int grid) {
     const int hg = HistBlocks();
+    Args a = a0;
+    // slab rows folded by fold_chunks_ blocks per feature (single GPU / feature parallel /
+    // voting local pass); the exchange transport counts its blocks, so it keeps one per feature
+    if (fold_chunks_ > 1 && a.scan_src == 0 && !scan_global_ && a.transport != 2 && a.fold_cnt) {
+      a.fold_chunks = fold_chunks_;
+      a.fold_feats = grid;
+      grid = (grid * fold_chunks_ + 7) & ~7;
+    }
     if (use_dp_) {
       if (scan_global_) k_reduce_scan<double, true><<<grid, kScanThreads, 0, stream_>>>(a, hg);
       else k_reduce_scan<double, false><<<grid, kScanThreads, scan_lds_bytes_, stream_>>>(a, hg);
@@ -4236,6 +4301,19 @@ class DeviceTreeLearner : public TreeLearner {
     staging_.Zero(stream_);
     staging_f_.Resize(2 * static_cast<size_t>(TB_));
     hist_slab_.Resize(static_cast<size_t>(HistBlocks()) * 2 * TB_ * (use_dp_ ? 8 : 4));
+    // split slab fold (LGAP_SCAN_CHUNKS=C: C blocks per feature, in-launch combine). Off: A/B on
+    // MI355X, 10M rows C=8 222 it/s, C=4 229, C=1 232; 1.25M C=8 348, C=1 386 -- the release /
+    // ticket / acquire hand-off costs more than the shorter fold saves
+    fold_chunks_ = 1;
+    if (const char* e = std::getenv("LGAP_SCAN_CHUNKS")) fold_chunks_ = std::max(1, std::min(16, std::atoi(e)));
+#if LGAP_SCAN_FOLD == 2
+    fold_chunks_ = 1;
+#endif
+    if (fold_chunks_ > 1) {
+      fold_part_.Resize(static_cast<size_t>(fold_chunks_) * 2 * TB_);
+      fold_cnt_.Resize(std::max(F_, 1));
+      fold_cnt_.Zero(stream_);
+    }
     // all three index buffers hold N rows up front: a captured graph keeps their
     // addresses, so a later bag (host upload or device draw) must not reallocate
     for (int i = 0; i < 3; ++i) idx_[i].Resize(std::max(N_, 1));
@@ -4294,6 +4372,9 @@ class DeviceTreeLearner : public TreeLearner {
     a.max_bin = max_bin_;
     a.cat_p2 = cat_p2_;
     a.scan_scratch = scan_global_ ? scan_scratch_.get() : nullptr;
+    a.fold_chunks = 1;  // LaunchReduceScan splits the fold where it applies
+    a.fold_part = fold_chunks_ > 1 ? fold_part_.get() : nullptr;
+    a.fold_cnt = fold_chunks_ > 1 ? fold_cnt_.get() : nullptr;
     a.scan_scratch_stride = scan_scratch_stride_;
     a.max_depth = config_->max_depth;
     // 0: separate k_post kernel, 1: block 0 after its tiles, 2: first spare block
@@ -4553,6 +4634,9 @@ class DeviceTreeLearner : public TreeLearner {
   bool scan_global_ = false;
   size_t scan_scratch_stride_ = 0;
   DevBuf<char> scan_scratch_;
+  int fold_chunks_ = 1;
+  DevBuf<double> fold_part_;
+  DevBuf<unsigned> fold_cnt_;
   std::string device_name_;
   hipStream_t stream_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;

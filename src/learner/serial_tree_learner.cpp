@@ -285,6 +285,34 @@ void SerialTreeLearner::ComputeLeafSums(const data_size_t* idx, data_size_t n, d
 
 // Row-wise histogram over the packed group bins; group bin 0 (all features at
 // their most-frequent bin) is never accumulated.
+namespace {
+template <typename BinT>
+void HistRows(const data_size_t* idx, data_size_t i0, data_size_t i1, const uint8_t* bins, int stride, int ng,
+              const int* gstart, const score_t* grad, const score_t* hess, double* hh) {
+  // rows of a deep leaf are scattered: prefetch the bin row and the gradients kPf rows
+  // ahead so the misses overlap (reference dense_bin.hpp ConstructHistogram prefetch)
+  constexpr data_size_t kPf = 32;
+  for (data_size_t i = i0; i < i1; ++i) {
+    if (i + kPf < i1) {
+      const data_size_t rp = idx[i + kPf];
+      __builtin_prefetch(bins + static_cast<size_t>(rp) * stride);
+      __builtin_prefetch(grad + rp);
+      __builtin_prefetch(hess + rp);
+    }
+    const data_size_t r = idx[i];
+    const double g = grad[r], h = hess[r];
+    const BinT* row = reinterpret_cast<const BinT*>(bins + static_cast<size_t>(r) * stride);
+    for (int k = 0; k < ng; ++k) {
+      const uint32_t bv = row[k];
+      if (bv == 0) continue;
+      double* e = hh + 2 * (gstart[k] + static_cast<int>(bv));
+      e[0] += g;
+      e[1] += h;
+    }
+  }
+}
+}  // namespace
+
 void SerialTreeLearner::BuildHistogram(const data_size_t* idx, data_size_t n, double* hist) const {
   if (hist_backend_) {
     hist_backend_->Histogram(idx, n, hist);
@@ -296,40 +324,33 @@ void SerialTreeLearner::BuildHistogram(const data_size_t* idx, data_size_t n, do
   std::vector<int> gstart(ng);
   for (int g = 0; g < ng; ++g) gstart[g] = groups[g].hist_start;
   std::memset(hist, 0, sizeof(double) * 2 * tb);
-  const int nt = (n >= 16384) ? omp_get_max_threads() : 1;
-  std::vector<std::vector<double>> local(nt);
+  // one private histogram per thread above ~8k rows each (kept across calls), folded after
+  const int nt = static_cast<int>(std::max<data_size_t>(1, std::min<data_size_t>(omp_get_max_threads(), n / 8192)));
   const uint8_t* bins = train_data_->bins();
   const int stride = train_data_->row_stride();
   const bool w1 = train_data_->bin_width() == 1;
-#pragma omp parallel num_threads(nt)
-  {
-    const int tid = omp_get_thread_num();
-    double* hh = hist;
-    if (nt > 1) {
-      local[tid].assign(2 * tb, 0.0);
-      hh = local[tid].data();
-    }
-#pragma omp for schedule(static)
-    for (data_size_t i = 0; i < n; ++i) {
-      const data_size_t r = idx[i];
-      const double g = gradients_[r], h = hessians_[r];
-      const uint8_t* row = bins + static_cast<size_t>(r) * stride;
-      for (int k = 0; k < ng; ++k) {
-        const uint32_t b = w1 ? row[k] : reinterpret_cast<const uint16_t*>(row)[k];
-        if (b == 0) continue;
-        const int o = 2 * (gstart[k] + static_cast<int>(b));
-        hh[o] += g;
-        hh[o + 1] += h;
-      }
-    }
+  auto run = [&](data_size_t i0, data_size_t i1, double* hh) {
+    if (w1) HistRows<uint8_t>(idx, i0, i1, bins, stride, ng, gstart.data(), gradients_, hessians_, hh);
+    else HistRows<uint16_t>(idx, i0, i1, bins, stride, ng, gstart.data(), gradients_, hessians_, hh);
+  };
+  if (nt == 1) {
+    run(0, n, hist);
+    return;
   }
-  if (nt > 1) {
-#pragma omp parallel for schedule(static)
-    for (int j = 0; j < 2 * tb; ++j) {
-      double s = 0.0;
-      for (int t = 0; t < nt; ++t) s += local[t][j];
-      hist[j] = s;
-    }
+  if (static_cast<int>(tls_hist_.size()) < nt) tls_hist_.resize(nt);
+  const data_size_t per = (n + nt - 1) / nt;
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+  for (int t = 0; t < nt; ++t) {
+    auto& buf = tls_hist_[t];
+    buf.assign(2 * static_cast<size_t>(tb), 0.0);
+    const data_size_t i0 = std::min(n, t * per);
+    run(i0, std::min(n, i0 + per), buf.data());
+  }
+#pragma omp parallel for schedule(static) num_threads(nt) if (2 * tb >= 16384)
+  for (int j = 0; j < 2 * tb; ++j) {
+    double s = 0.0;
+    for (int t = 0; t < nt; ++t) s += tls_hist_[t][j];
+    hist[j] = s;
   }
 }
 
@@ -508,6 +529,7 @@ void SerialTreeLearner::FindBestSplits(const Tree* tree) {
 }
 
 void SerialTreeLearner::ConstructHistograms(bool use_subtract) {
+  ScopedTimer timer("SerialTreeLearner::ConstructHistograms");
   BuildHistogram(partition_.indices(smaller_.leaf), partition_.count(smaller_.leaf), HistOf(smaller_.leaf).data());
   if (larger_.leaf >= 0 && !use_subtract) {
     BuildHistogram(partition_.indices(larger_.leaf), partition_.count(larger_.leaf), HistOf(larger_.leaf).data());
@@ -515,6 +537,7 @@ void SerialTreeLearner::ConstructHistograms(bool use_subtract) {
 }
 
 void SerialTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, bool use_subtract) {
+  ScopedTimer timer("SerialTreeLearner::FindBestSplitsFromHistograms");
   const auto& bytree = col_sampler_.is_feature_used_bytree();
   std::vector<int8_t> node_s = col_sampler_.GetByNode(tree, smaller_.leaf);
   std::vector<int8_t> node_l;
@@ -645,6 +668,7 @@ void SerialTreeLearner::RenewQuantizedLeaves(Tree* tree) const {
 }
 
 void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) {
+  ScopedTimer timer("SerialTreeLearner::Split");
   if (cegb_) {
     cegb_->OnSplit(tree->num_leaves(), best_leaf, best_split_per_leaf_[best_leaf], partition_.indices(best_leaf),
                    partition_.count(best_leaf), &best_split_per_leaf_);
@@ -663,11 +687,14 @@ void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* ri
     const bool dl = info.default_left != 0;
     const MissingType mt = fi.missing;
     const uint32_t nan_bin = static_cast<uint32_t>(fi.num_bin - 1);
+    const uint8_t* bins = d->bins();
+    const size_t stride = static_cast<size_t>(d->row_stride());
+    auto pf = [&](data_size_t r) { __builtin_prefetch(bins + r * stride); };
     nl = partition_.Split(best_leaf, next, [&](data_size_t r) {
       const uint32_t b = d->FeatureBin(r, f);
       if ((mt == MissingType::Zero && b == fi.default_bin) || (mt == MissingType::NaN && b == nan_bin)) return dl;
       return b <= thr;
-    });
+    }, pf);
     if (!global_counts_from_split_) {
       info.left_count = nl;
       info.right_count = partition_.count(next);

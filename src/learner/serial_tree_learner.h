@@ -4,6 +4,8 @@
 // (basic method), feature_histogram.hpp (via split_math.h).
 #pragma once
 
+#include <omp.h>
+
 #include <memory>
 #include <set>
 #include <vector>
@@ -44,9 +46,14 @@ class DataPartition {
   void Init(data_size_t num_data, int num_leaves);
   void SetUsedIndices(const data_size_t* idx, data_size_t n);
   void Reset();  // all rows (or the bag) into leaf 0
-  // go_left(row) -> bool; returns left count
+  // go_left(row) -> bool; returns left count. prefetch(row) is called a few rows ahead of
+  // go_left on the same row (the rows of a deep leaf are scattered)
+  template <typename F, typename P>
+  data_size_t Split(int leaf, int right_leaf, F go_left, P prefetch);
   template <typename F>
-  data_size_t Split(int leaf, int right_leaf, F go_left);
+  data_size_t Split(int leaf, int right_leaf, F go_left) {
+    return Split(leaf, right_leaf, go_left, [](data_size_t) {});
+  }
   const data_size_t* indices(int leaf) const { return indices_.data() + begin_[leaf]; }
   data_size_t count(int leaf) const { return count_[leaf]; }
   data_size_t begin(int leaf) const { return begin_[leaf]; }
@@ -130,6 +137,7 @@ class SerialTreeLearner : public TreeLearner {
   ColSampler col_sampler_;
   std::vector<SplitInfo> best_split_per_leaf_;
   std::vector<std::vector<double>> hist_;            // per leaf, 2*num_total_bin
+  mutable std::vector<std::vector<double>> tls_hist_;  // per-thread partial histograms (BuildHistogram)
   // histogram_pool_size: at most hist_cap_ leaf histograms live at once; the one
   // produced longest ago is dropped first (reference HistogramPool LRU,
   // feature_histogram.hpp:1367-1594)
@@ -162,17 +170,47 @@ class SerialTreeLearner : public TreeLearner {
 };
 
 // ---------------------------------------------------------------------------
-template <typename F>
-data_size_t DataPartition::Split(int leaf, int right_leaf, F go_left) {
+template <typename F, typename P>
+data_size_t DataPartition::Split(int leaf, int right_leaf, F go_left, P prefetch) {
   const data_size_t b = begin_[leaf], n = count_[leaf];
   data_size_t* src = indices_.data() + b;
   data_size_t* dst = tmp_.data() + b;
-  // two-pass stable partition (left kept in order, right kept in order)
-  data_size_t nl = 0;
-  for (data_size_t i = 0; i < n; ++i) if (go_left(src[i])) dst[nl++] = src[i];
-  data_size_t nr = nl;
-  for (data_size_t i = 0; i < n; ++i) if (!go_left(src[i])) dst[nr++] = src[i];
-  std::copy(dst, dst + n, src);
+  // Stable partition in one predicate pass (reference data_partition.hpp:104-160 splits the
+  // leaf into per-thread blocks the same way): each block writes its lefts forward from its
+  // start and its rights backward from its end in `dst`, then every block copies its lefts
+  // and (re-reversed) rights to their final offsets in `src`.
+  constexpr data_size_t kMinPerBlock = 8192;
+  const int nblk = static_cast<int>(std::max<data_size_t>(1, std::min<data_size_t>(
+      static_cast<data_size_t>(omp_get_max_threads()), n / kMinPerBlock)));
+  const data_size_t per = (n + nblk - 1) / nblk;
+  std::vector<data_size_t> lcnt(nblk + 1, 0), rcnt(nblk + 1, 0);
+#pragma omp parallel for schedule(static, 1) num_threads(nblk) if (nblk > 1)
+  for (int t = 0; t < nblk; ++t) {
+    const data_size_t s0 = std::min(n, t * per), s1 = std::min(n, s0 + per);
+    data_size_t l = s0, r = s1;
+    constexpr data_size_t kPf = 32;
+    for (data_size_t i = s0; i < s1; ++i) {
+      if (i + kPf < s1) prefetch(src[i + kPf]);
+      const data_size_t row = src[i];
+      if (go_left(row)) dst[l++] = row;
+      else dst[--r] = row;
+    }
+    lcnt[t + 1] = l - s0;
+    rcnt[t + 1] = s1 - r;
+  }
+  for (int t = 0; t < nblk; ++t) {
+    lcnt[t + 1] += lcnt[t];
+    rcnt[t + 1] += rcnt[t];
+  }
+  const data_size_t nl = lcnt[nblk];
+#pragma omp parallel for schedule(static, 1) num_threads(nblk) if (nblk > 1)
+  for (int t = 0; t < nblk; ++t) {
+    const data_size_t s0 = std::min(n, t * per), s1 = std::min(n, s0 + per);
+    const data_size_t nlt = lcnt[t + 1] - lcnt[t], nrt = rcnt[t + 1] - rcnt[t];
+    std::copy(dst + s0, dst + s0 + nlt, src + lcnt[t]);
+    data_size_t* rout = src + nl + rcnt[t];
+    for (data_size_t k = 0; k < nrt; ++k) rout[k] = dst[s1 - 1 - k];
+  }
   if (right_leaf >= static_cast<int>(begin_.size())) {
     begin_.resize(right_leaf + 1, 0);
     count_.resize(right_leaf + 1, 0);
