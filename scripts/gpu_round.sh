@@ -35,6 +35,7 @@ for s in "$@"; do
     vote) step vote 900 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "voting or multirank";;
     evidence) step parity1m 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 500 --timeout-method thread -p no:cacheprovider -k "fixed_point_vs_fp64" && step b255 600 python bench.py --num-leaves 255 --steps 500 --warmup 5 && step b63dp 600 python bench.py --use-dp --steps 30 --warmup 3 && step vote12 900 python scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --learner voting --steps 20 --warmup 3 && step serial12 900 python scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --steps 20 --warmup 3 && step parity10 1000 python scripts/auc_parity.py --rows 10000000 --iters 50;;
     abchunks) step c10a 300 python bench.py --steps 30 --warmup 3 && LGAP_SCAN_CHUNKS=1 step c10b 300 python bench.py --steps 30 --warmup 3 && step c1a 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_SCAN_CHUNKS=1 step c1b 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_SCAN_CHUNKS=4 step c10c 300 python bench.py --steps 30 --warmup 3;;
+    rehearse2) step rehearse2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dp-host-transport --rows 1250000 --steps 5 --warmup 2;;
     learnerx) step learnerx 400 python -m pytest tests/test_gpu_learner.py -x -q --timeout 60 -p no:cacheprovider;;
     learner) step learner 1200 python -m pytest tests/test_gpu_learner.py -q --timeout 300 -p no:cacheprovider;;
     gputests) step gputests 1500 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider;;
