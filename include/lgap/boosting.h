@@ -113,6 +113,8 @@ class GBDT {
   int NumberOfTotalModel() const { return static_cast<int>(models_.size()); }
   int NumModelPerIteration() const { return num_tree_per_iteration_; }
   int NumberOfClasses() const { return num_class_; }
+  // prediction early stopping applies only when this is false (reference gbdt.h:229-235)
+  virtual bool NeedAccuratePrediction() const { return objective() == nullptr || objective()->NeedAccuratePrediction(); }
   int GetCurrentIteration() const { return static_cast<int>(models_.size()) / std::max(1, num_tree_per_iteration_); }
   int MaxFeatureIdx() const { return max_feature_idx_; }
   const std::vector<std::string>& FeatureNames() const { return feature_names_; }
@@ -221,6 +223,7 @@ class RF : public GBDT {
             const std::vector<const Metric*>& training_metrics) override;
   bool TrainOneIter(const score_t* gradients, const score_t* hessians) override;
   void RollbackOneIter() override;
+  bool NeedAccuratePrediction() const override { return true; }  // rf.hpp:224: no early stopping
 
  private:
   std::vector<double> init_scores_;

@@ -8,6 +8,7 @@ through ctypes without copies where the input is already contiguous.
 from __future__ import annotations
 
 import ctypes
+import warnings
 import json
 import os
 from copy import deepcopy
@@ -68,23 +69,43 @@ def _c_str(s: str) -> ctypes.c_char_p:
     return ctypes.c_char_p(s.encode("utf-8"))
 
 
+def _log_info(msg: str) -> None:
+    if _LOGGER is not None:
+        _LOGGER.info(msg)
+    else:
+        print(msg, flush=True)
+
+
+def _log_warning(msg: str) -> None:
+    """Python-side warnings: the registered logger's warning method, else ``warnings.warn``
+    (reference basic.py _DummyLogger / _log_warning)."""
+    if _LOGGER is not None:
+        _LOGGER.warning(msg)
+    else:
+        warnings.warn(msg, stacklevel=3)
+
+
 def _log_sink(msg: bytes) -> None:
     text = msg.decode("utf-8").rstrip("\n")
     if not text:
         return
-    if _LOGGER is not None:
-        _LOGGER.info(text)
-    else:
-        print(text, flush=True)
+    _log_info(text)
 
 
 def register_logger(logger: Any, info_method_name: str = "info", warning_method_name: str = "warning") -> None:
-    """Route native log lines to a logger object (``logger.info``)."""
+    """Route native log lines (``info_method_name``) and Python-side warnings
+    (``warning_method_name``) to a logger object."""
     global _LOGGER
+    for name in (info_method_name, warning_method_name):
+        if not callable(getattr(logger, name, None)):
+            raise TypeError(f"Logger must provide '{name}' method")
 
     class _Wrap:
         def info(self, m):
             getattr(logger, info_method_name)(m)
+
+        def warning(self, m):
+            getattr(logger, warning_method_name)(m)
 
     _LOGGER = _Wrap()
 
@@ -760,8 +781,8 @@ def _get_names(fn: Callable, n: int) -> List[str]:
     return [bufs[i].value.decode("utf-8") for i in range(out_len.value)]
 
 
-_HIGHER_BETTER_PREFIX = ("auc", "ndcg@", "map@", "average_precision", "precision@", "auc_mu", "ndcg", "map",
-                         "precision")
+# reference basic.py:5268-5270 ("map@", not "map": "mape" is a loss); precision@k is a gain too
+_HIGHER_BETTER_PREFIX = ("auc", "ndcg@", "map@", "average_precision", "precision@")
 
 
 def _is_higher_better(name: str) -> bool:

@@ -135,15 +135,17 @@ def reset_parameter(**kwargs: Union[list, Callable]) -> Callable:
 class _EarlyStopping:
     def __init__(self, stopping_rounds: int, first_metric_only: bool, verbose: bool,
                  min_delta: Union[float, List[float]]):
-        if not isinstance(stopping_rounds, int) or stopping_rounds <= 0:
-            raise ValueError(f"stopping_rounds should be an integer and greater than 0. got: {stopping_rounds}")
+        # a non-positive count leaves the callback disabled; a non-integer is an error
+        # (reference callback.py _should_enable_early_stopping)
+        if not isinstance(stopping_rounds, int) or isinstance(stopping_rounds, bool):
+            raise TypeError(f"early_stopping_round should be an integer. Got '{type(stopping_rounds).__name__}'")
         self.order = 30
         self.before_iteration = False
         self.stopping_rounds = stopping_rounds
         self.first_metric_only = first_metric_only
         self.verbose = verbose
         self.min_delta = min_delta
-        self.enabled = True
+        self.enabled = stopping_rounds > 0
         self._reset()
 
     def _reset(self) -> None:
@@ -156,6 +158,18 @@ class _EarlyStopping:
     def _init(self, env: CallbackEnv) -> None:
         if not env.evaluation_result_list:
             raise ValueError("For early stopping, at least one dataset and eval metric is required for evaluation")
+        from .basic import _log_warning
+
+        if any(env.params.get(a, "") == "dart" for a in ("boosting", "boosting_type", "boost")):
+            self.enabled = False
+            _log_warning("Early stopping is not available in dart mode")
+            return
+        first_name = env.evaluation_result_list[0][0]
+        if len(env.evaluation_result_list) == 1 and self._is_train_set(first_name, env) and \
+                not isinstance(env.model, dict) and hasattr(env.model, "_train_data_name"):
+            self.enabled = False
+            _log_warning("Only training set found, disabling early stopping.")
+            return
         self._reset()
         self.first_metric = env.evaluation_result_list[0][1].split(" ")[-1]
         n = len(env.evaluation_result_list)
@@ -192,6 +206,8 @@ class _EarlyStopping:
         return data_name == "train"
 
     def __call__(self, env: CallbackEnv) -> None:
+        if not self.enabled:
+            return
         if env.iteration == env.begin_iteration:
             self._init(env)
         if not self.enabled:

@@ -19,20 +19,42 @@ __all__ = ["train", "cv", "CVBooster"]
 
 
 def _pop_num_rounds(params: Dict[str, Any], num_boost_round: int) -> Tuple[Dict[str, Any], int]:
+    """num_iterations from params beats the argument; the main name beats its aliases, then the
+    first alias given (reference engine.py _choose_num_iterations)."""
     params = dict(params)
-    for alias in ("num_iterations", "num_iteration", "n_iter", "num_tree", "num_trees", "num_round", "num_rounds",
-                  "nrounds", "num_boost_round", "n_estimators", "max_iter"):
-        if alias in params:
-            num_boost_round = int(params.pop(alias))
+    given = [a for a in params if a in ("num_iterations", "num_iteration", "n_iter", "num_tree", "num_trees",
+                                        "num_round", "num_rounds", "nrounds", "num_boost_round", "n_estimators",
+                                        "max_iter")]
+    if given:
+        main = "num_iterations" if "num_iterations" in given else given[0]
+        values = {a: params[a] for a in given}
+        num_boost_round = int(values[main])
+        if len(set(str(v) for v in values.values())) > 1:
+            import warnings
+
+            warnings.warn(f"Found conflicting values for num_iterations provided via 'params': "
+                          f"{', '.join(f'{a}={v}' for a, v in values.items())}. "
+                          f"LightGBM will perform up to {num_boost_round} boosting rounds.")
+        for a in given:
+            params.pop(a)
     params["num_iterations"] = num_boost_round
     return params, num_boost_round
 
 
 def _early_stop_params(params: Dict[str, Any]) -> Tuple[Optional[int], bool, float]:
+    """early_stopping_round from params under its main name (aliases folded into it); None
+    removes it, a non-integer is a TypeError, <= 0 keeps it but stops nothing (reference
+    engine.py train + callback._should_enable_early_stopping)."""
     rounds = None
-    for alias in ("early_stopping_round", "early_stopping_rounds", "early_stopping", "n_iter_no_change"):
-        if alias in params and params[alias] is not None:
-            rounds = int(params[alias])
+    for alias in ("early_stopping_rounds", "early_stopping", "n_iter_no_change", "early_stopping_round"):
+        if alias in params:
+            rounds = params.pop(alias)
+            if alias == "early_stopping_round":
+                break
+    if rounds is not None:
+        if not isinstance(rounds, int) or isinstance(rounds, bool):
+            raise TypeError(f"early_stopping_round should be an integer. Got '{type(rounds).__name__}'")
+        params["early_stopping_round"] = rounds
     first_only = bool(params.get("first_metric_only", False))
     min_delta = float(params.get("early_stopping_min_delta", 0.0))
     return rounds, first_only, min_delta
@@ -46,6 +68,17 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
     """Train a booster for ``num_boost_round`` rounds."""
     if not isinstance(train_set, Dataset):
         raise TypeError(f"train() only accepts Dataset object, train_set has type '{type(train_set).__name__}'.")
+    if isinstance(valid_sets, Dataset):
+        valid_sets = [valid_sets]
+    if isinstance(valid_names, str):
+        valid_names = [valid_names]
+    if isinstance(valid_sets, list):
+        for i, item in enumerate(valid_sets):
+            if not isinstance(item, Dataset):
+                raise TypeError("Every item in valid_sets must be a Dataset object. "
+                                f"Item {i} has type '{type(item).__name__}'.")
+    if params is not None and not isinstance(params, dict):
+        raise TypeError(f"params must be a dict, got '{type(params).__name__}'.")
     params = copy.deepcopy(params) if params else {}
     fobj = None
     obj = params.get("objective")
@@ -83,8 +116,7 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
                 train_data_name = names[i]
             continue
         name = names[i] if i < len(names) else f"valid_{i}"
-        if vs.reference is None:
-            vs.set_reference(train_set)
+        vs._update_params(params).set_reference(train_set)
         vs._set_predictor(predictor)
         booster.add_valid(vs, name)
     booster.set_train_data_name(train_data_name)

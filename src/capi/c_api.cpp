@@ -229,10 +229,11 @@ void PredictRows(Booster* b, const RowSource& src, int predict_type, int start_i
                "You can set ``predict_disable_shape_check=true`` to discard this error, but please be aware what you are doing.",
                src.num_cols(), g->MaxFeatureIdx() + 1);
   }
+  // reference predictor.hpp:46-58: any objective that needs no accurate raw scores (binary,
+  // multiclass, ranking) stops early; "binary" margins for one class, "multiclass" otherwise
   std::string es_type = "none";
-  if (pc.pred_early_stop && !leaf && !contrib) {
-    if (g->objective() && std::string(g->objective()->GetName()) == "binary") es_type = "binary";
-    else if (g->objective() && std::string(g->objective()->GetName()).find("multiclass") == 0) es_type = "multiclass";
+  if (pc.pred_early_stop && !leaf && !contrib && !g->NeedAccuratePrediction()) {
+    es_type = g->NumberOfClasses() == 1 ? "binary" : "multiclass";
   }
   PredictionEarlyStop es(es_type, pc.pred_early_stop_freq, pc.pred_early_stop_margin);
   OmpErrors errs;  // a failing row source (Arrow / Python callback) must return -1, not abort
@@ -1181,10 +1182,8 @@ FastConfig* MakeFast(BoosterHandle handle, int predict_type, int start_iteration
   std::string es_type = "none";
   const GBDT* g = fc->booster->boosting_.get();
   if (fc->config.pred_early_stop && predict_type != C_API_PREDICT_LEAF_INDEX && predict_type != C_API_PREDICT_CONTRIB &&
-      g->objective()) {
-    const std::string name = g->objective()->GetName();
-    if (name == "binary") es_type = "binary";
-    else if (name.find("multiclass") == 0) es_type = "multiclass";
+      !g->NeedAccuratePrediction()) {
+    es_type = g->NumberOfClasses() == 1 ? "binary" : "multiclass";
   }
   fc->es = std::make_unique<PredictionEarlyStop>(es_type, fc->config.pred_early_stop_freq,
                                                  fc->config.pred_early_stop_margin);

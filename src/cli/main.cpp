@@ -81,7 +81,11 @@ void Predict(const Config& c) {
   const int per = boosting->NumPredictOneRow(c.start_iteration_predict, c.num_iteration_predict, leaf, contrib);
   const int nf = std::max(boosting->MaxFeatureIdx() + 1, rows.ncol);
   std::vector<double> out(rows.rows.size() * static_cast<size_t>(per));
-  PredictionEarlyStop es(c.pred_early_stop ? "binary" : "none", c.pred_early_stop_freq, c.pred_early_stop_margin);
+  std::string es_type = "none";
+  if (c.pred_early_stop && !leaf && !contrib && !boosting->NeedAccuratePrediction()) {
+    es_type = boosting->NumberOfClasses() == 1 ? "binary" : "multiclass";
+  }
+  PredictionEarlyStop es(es_type, c.pred_early_stop_freq, c.pred_early_stop_margin);
   OmpErrors errs;
 #pragma omp parallel
   {

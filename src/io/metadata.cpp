@@ -224,7 +224,11 @@ void Metadata::LoadSideFiles(const std::string& fn) {
     }
   }
   auto pos = read_lines(fn + ".position");
-  if (!pos.empty() && static_cast<data_size_t>(pos.size()) == num_data_) {
+  if (!pos.empty() && static_cast<data_size_t>(pos.size()) != num_data_) {
+    // reference metadata.cpp:223-226 / 268-272
+    Log::Fatal("Positions size (%d) doesn't match data size (%d)", static_cast<int>(pos.size()), num_data_);
+  }
+  if (!pos.empty()) {
     std::unordered_map<std::string, int32_t> id;
     position_ids_.clear();
     positions_.resize(num_data_);
