@@ -48,6 +48,8 @@ struct Config {
   static std::string DumpParameterTypes();
   static const std::unordered_map<std::string, std::string>& AliasTable();
   static bool IsKnownParameter(const std::string& name);
+  // kind of a parameter in config_params.def (INT, DBL, BOOL, STR, VINT, ...), "" if unknown
+  static std::string ParameterKind(const std::string& name);
 
  private:
   void GetMembersFromString(const ParamMap& params);

@@ -390,10 +390,18 @@ class Dataset:
         return self
 
     def _build_params(self, categorical_indices: List[int]) -> str:
-        params = dict(self.params)
+        # the resolved categorical columns become a Dataset parameter (categorical_column), which
+        # the Booster inherits and the model text records (reference basic.py Dataset._lazy_init)
         if categorical_indices:
-            params["categorical_feature"] = ",".join(str(i) for i in categorical_indices)
-        return param_dict_to_str(params)
+            want = sorted(set(categorical_indices))
+            for alias in ["categorical_feature"] + _aliases().get("categorical_feature", []):
+                if alias in self.params:
+                    cur = self.params[alias]
+                    if not (isinstance(cur, list) and set(cur) == set(want)):
+                        _log_warning(f"{alias} in param dict is overridden.")
+                    self.params.pop(alias, None)
+            self.params["categorical_column"] = want
+        return param_dict_to_str(self.params)
 
     def _resolve_categorical(self, feature_names: Optional[List[str]], ncol: int) -> List[int]:
         cf = self.categorical_feature
@@ -637,8 +645,22 @@ class Dataset:
     def get_data(self):
         return self.data
 
+    _DATASET_PARAMS = ("bin_construct_sample_cnt", "categorical_feature", "data_random_seed", "enable_bundle",
+                       "feature_pre_filter", "forcedbins_filename", "group_column", "header", "ignore_column",
+                       "is_enable_sparse", "label_column", "linear_tree", "max_bin", "max_bin_by_feature",
+                       "min_data_in_bin", "pre_partition", "precise_float_parser", "two_round", "use_missing",
+                       "weight_column", "zero_as_missing")
+
     def get_params(self) -> Dict[str, Any]:
-        return dict(self.params)
+        """The Dataset-level parameters among ``params`` (binning / loading; aliases included),
+        reference basic.py Dataset.get_params."""
+        if not self.params:
+            return {}
+        names = set()
+        for k in self._DATASET_PARAMS:
+            names.add(k)
+            names.update(_aliases().get(k, []))
+        return {k: v for k, v in self.params.items() if k in names}
 
     def set_reference(self, reference: "Dataset") -> "Dataset":
         self.reference = reference
@@ -818,6 +840,7 @@ class Booster:
             train_set._update_params(self.params)
             train_set.construct()
             self.train_set = train_set
+            self.params.update(train_set.get_params())
             _check(_LIB.LGBM_BoosterCreate(train_set.handle, _c_str(param_dict_to_str(self.params)),
                                            ctypes.byref(self.handle)))
             if train_set._predictor is not None:
@@ -832,10 +855,21 @@ class Booster:
                                                         ctypes.byref(self.handle)))
             self._num_class = self._get_num_class()
             self.pandas_categorical = _load_pandas_categorical(Path(model_file).read_text())
+            self._params_from_model(params, "file")
         elif model_str is not None:
             self.model_from_string(model_str)
+            self._params_from_model(params, "string")
         else:
             raise TypeError("Need at least one training dataset or model file or model string to create Booster instance")
+
+    def _params_from_model(self, params: Optional[Dict[str, Any]], source: str) -> None:
+        """Booster.params of a loaded model are the model's own parameters section (reference
+        basic.py Booster.__init__ / _get_loaded_param); constructor params are ignored."""
+        if params:
+            _log_warning(f"Ignoring params argument, using parameters from model {source}.")
+        s = _get_string(lambda n, ol, buf: _LIB.LGBM_BoosterGetLoadedParam(self.handle, ctypes.c_int64(n), ol, buf),
+                        size=1 << 16)
+        self.params = json.loads(s)
 
     def __del__(self):
         try:

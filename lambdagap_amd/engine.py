@@ -201,10 +201,21 @@ class CVBooster:
         return self
 
     def __getattr__(self, name: str) -> Callable:
+        # only public Booster methods are broadcast (dunder / private lookups, e.g. by pickle
+        # before `boosters` exists, must fail normally)
+        if name.startswith("_"):
+            raise AttributeError(name)
+
         def handler(*args: Any, **kwargs: Any) -> List[Any]:
             return [getattr(b, name)(*args, **kwargs) for b in self.boosters]
 
         return handler
+
+    def __getstate__(self) -> Dict[str, Any]:
+        return vars(self)
+
+    def __setstate__(self, state: Dict[str, Any]) -> None:
+        vars(self).update(state)
 
 
 def _make_folds(full: Dataset, folds, nfold: int, params: Dict[str, Any], seed: int, fpreproc, stratified: bool,
@@ -221,44 +232,27 @@ def _make_folds(full: Dataset, folds, nfold: int, params: Dict[str, Any], seed: 
                 flatted_group = np.zeros(num_data, dtype=np.int32)
             folds = folds.split(X=np.empty(num_data), y=full.get_label(), groups=flatted_group)
     else:
-        objective = str(params.get("objective", "regression"))
-        if objective in ("lambdarank", "rank_xendcg", "xendcg", "xe_ndcg", "xe_ndcg_mart", "xendcg_mart"):
-            group_info = np.asarray(full.get_group(), dtype=np.int32)
+        # reference engine.py _make_n_folds: GroupKFold over queries for ranking objectives,
+        # StratifiedKFold when stratified, else nfold contiguous chunks of num_data // nfold rows
+        # of a (seeded) permutation
+        from sklearn.model_selection import GroupKFold, StratifiedKFold
+
+        ranking = {"lambdarank", "rank_xendcg", "xendcg", "xe_ndcg", "xe_ndcg_mart", "xendcg_mart"}
+        if any(params.get(a, "") in ranking for a in ("objective", "objective_type", "app", "application", "loss")):
+            group_info = full.get_group()
             if group_info is None:
                 raise LightGBMError("Ranking tasks require query information")
-            rng = np.random.RandomState(seed)
-            nq = len(group_info)
-            order = rng.permutation(nq) if shuffle else np.arange(nq)
-            bounds = np.concatenate([[0], np.cumsum(group_info)])
-            qfolds = np.array_split(order, nfold)
-            folds = []
-            for k in range(nfold):
-                test_q = np.sort(qfolds[k])
-                test_idx = np.concatenate([np.arange(bounds[q], bounds[q + 1]) for q in test_q]) if len(test_q) else \
-                    np.array([], dtype=np.int64)
-                mask = np.ones(num_data, dtype=bool)
-                mask[test_idx] = False
-                folds.append((np.where(mask)[0], test_idx))
+            group_info = np.asarray(group_info, dtype=np.int32)
+            flatted_group = np.repeat(np.arange(len(group_info)), repeats=group_info)
+            folds = GroupKFold(n_splits=nfold).split(X=np.empty(num_data), groups=flatted_group)
         elif stratified:
-            label = np.asarray(full.get_label())
-            rng = np.random.RandomState(seed)
-            test_of = np.empty(num_data, dtype=np.int64)
-            for cls in np.unique(label):
-                idx = np.where(label == cls)[0]
-                if shuffle:
-                    idx = rng.permutation(idx)
-                for k, part in enumerate(np.array_split(idx, nfold)):
-                    test_of[part] = k
-            folds = [(np.where(test_of != k)[0], np.where(test_of == k)[0]) for k in range(nfold)]
+            skf = StratifiedKFold(n_splits=nfold, shuffle=shuffle, random_state=seed if shuffle else None)
+            folds = skf.split(X=np.empty(num_data), y=full.get_label())
         else:
-            rng = np.random.RandomState(seed)
-            idx = rng.permutation(num_data) if shuffle else np.arange(num_data)
-            parts = np.array_split(idx, nfold)
-            folds = []
-            for k in range(nfold):
-                test = np.sort(parts[k])
-                train_idx = np.sort(np.concatenate([parts[j] for j in range(nfold) if j != k]))
-                folds.append((train_idx, test))
+            order = np.random.RandomState(seed).permutation(num_data) if shuffle else np.arange(num_data)
+            kstep = int(num_data / nfold)
+            test_id = [order[i:i + kstep] for i in range(0, num_data, kstep)]
+            folds = [(np.concatenate([test_id[j] for j in range(nfold) if j != k]), test_id[k]) for k in range(nfold)]
     ret = CVBooster()
     for train_idx, test_idx in folds:
         train_set = full.subset(sorted(train_idx))
@@ -343,6 +337,8 @@ def cv(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100, f
                                  end_iteration=num_boost_round, evaluation_result_list=res))
         except cb.EarlyStopException as e:
             cvfolds.best_iteration = e.best_iteration + 1
+            for b in cvfolds.boosters:
+                b.best_iteration = cvfolds.best_iteration
             for k in results:
                 results[k] = results[k][:cvfolds.best_iteration]
             break

@@ -603,9 +603,29 @@ int LGBM_BoosterLoadModelFromString(const char* model_str, int* out_num_iteratio
   API_END();
 }
 
+namespace {
+std::string JsonQuote(const std::string& v) {
+  std::string o = "\"";
+  for (char ch : v) {
+    if (ch == '"' || ch == '\\') o += '\\';
+    o += ch;
+  }
+  return o + "\"";
+}
+
+bool AllInts(const std::vector<std::string>& parts) {
+  for (auto& t : parts) {
+    if (t.empty() || t.find_first_not_of("-0123456789") != std::string::npos) return false;
+  }
+  return !parts.empty();
+}
+}  // namespace
+
+// The model's "parameters:" section as a typed JSON object (reference GBDT::GetLoadedParam,
+// gbdt.h): values typed by the parameter table, empty values skipped, unknown keys warned
+// about and dropped.
 int LGBM_BoosterGetLoadedParam(BoosterHandle handle, int64_t buffer_len, int64_t* out_len, char* out_str) {
   API_BEGIN();
-  // JSON object of the loaded "[key: value]" lines
   std::string p = B(handle)->boosting_->loaded_parameter();
   std::stringstream ss;
   ss << "{";
@@ -614,8 +634,33 @@ int LGBM_BoosterGetLoadedParam(BoosterHandle handle, int64_t buffer_len, int64_t
     if (line.size() < 4 || line.front() != '[' || line.back() != ']') continue;
     size_t c = line.find(": ");
     if (c == std::string::npos) continue;
-    std::string k = line.substr(1, c - 1), v = line.substr(c + 2, line.size() - c - 3);
-    ss << (first ? "" : ", ") << "\"" << k << "\": \"" << v << "\"";
+    const std::string k = line.substr(1, c - 1), v = line.substr(c + 2, line.size() - c - 3);
+    if (v.empty()) continue;
+    const std::string kind = Config::ParameterKind(k);
+    if (kind.empty()) {
+      Log::Warning("Ignoring unrecognized parameter '%s' found in model string.", k.c_str());
+      continue;
+    }
+    std::string js;
+    const auto parts = common::Split(v, ',');
+    if (k == "interaction_constraints") {
+      js = "[" + v + "]";
+    } else if (k == "categorical_feature" && AllInts(parts)) {
+      js = "[" + v + "]";
+    } else if (kind == "STR") {
+      js = JsonQuote(v);
+    } else if (kind == "BOOL") {
+      js = (v == "1" || v == "true") ? "true" : "false";
+    } else if (kind == "INT" || kind == "DBL") {
+      js = v;
+    } else if (kind == "VSTR") {
+      js = "[";
+      for (size_t i = 0; i < parts.size(); ++i) js += (i ? "," : "") + JsonQuote(parts[i]);
+      js += "]";
+    } else {
+      js = "[" + v + "]";
+    }
+    ss << (first ? "" : ", ") << JsonQuote(k) << ": " << js;
     first = false;
   }
   ss << "}";

@@ -433,6 +433,13 @@ std::string Config::DumpAliases() {
   return ss.str();
 }
 
+std::string Config::ParameterKind(const std::string& name) {
+  for (auto& p : ParamTable()) {
+    if (name == p.name) return p.kind;
+  }
+  return "";
+}
+
 std::string Config::DumpParameterTypes() {
   std::stringstream ss;
   ss << "{";

@@ -544,3 +544,256 @@ def test_continue_train_dart_mae_bound(lgb):
     ret = mean_absolute_error(y_te, b.predict(X_te))
     assert ret < 13.6
     assert rec["valid_0"]["l1"][-1] == pytest.approx(ret)
+
+
+# ---------------------------------------------------------------------------
+# cv / CVBooster / serialization (test_engine.py:1175-1690)
+import copy  # noqa: E402
+import pickle  # noqa: E402
+
+from sklearn.model_selection import GroupKFold, TimeSeriesSplit  # noqa: E402
+
+
+def test_continue_train_multiclass_bound(lgb):
+    """test_continue_train_multiclass."""
+    from sklearn.datasets import load_iris
+
+    X_tr, X_te, y_tr, y_te = _split(*load_iris(return_X_y=True))
+    params = {"objective": "multiclass", "metric": "multi_logloss", "num_class": 3, "verbose": -1}
+    tr = lgb.Dataset(X_tr, y_tr, params=params, free_raw_data=False)
+    va = lgb.Dataset(X_te, y_te, reference=tr, params=params, free_raw_data=False)
+    init = lgb.train(params, tr, num_boost_round=20)
+    rec = {}
+    b = lgb.train(params, tr, num_boost_round=30, valid_sets=va, callbacks=[lgb.record_evaluation(rec)],
+                  init_model=init)
+    ret = _multi_logloss(y_te, b.predict(X_te))
+    assert ret < 0.1
+    assert rec["valid_0"]["multi_logloss"][-1] == pytest.approx(ret)
+
+
+def test_cv_metrics_folds_and_ranking(lgb):
+    """test_cv."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    ds = lgb.Dataset(X, y)
+    with_metric = {"metric": "l2", "verbose": -1}
+    r = lgb.cv(with_metric, ds, num_boost_round=10, nfold=3, stratified=False, shuffle=False, metrics="l1")
+    assert "valid l1-mean" in r and "valid l2-mean" not in r and len(r["valid l1-mean"]) == 10
+    r = lgb.cv({"verbose": -1}, ds, num_boost_round=10, nfold=3, stratified=False, shuffle=True, metrics="l1",
+               callbacks=[lgb.reset_parameter(learning_rate=lambda i: 0.1 - 0.001 * i)])
+    assert len(r["valid l1-mean"]) == 10
+    r = lgb.cv(with_metric, ds, num_boost_round=10, nfold=3, stratified=False, shuffle=False, metrics="l1",
+               eval_train_metric=True)
+    assert {"train l1-mean", "valid l1-mean"} <= set(r) and not ({"train l2-mean", "valid l2-mean"} & set(r))
+    assert len(r["train l1-mean"]) == 10
+    tss = TimeSeriesSplit(3)
+    gen = lgb.cv(with_metric, ds, num_boost_round=10, folds=tss.split(X))
+    obj = lgb.cv(with_metric, ds, num_boost_round=10, folds=tss)
+    np.testing.assert_allclose(gen["valid l2-mean"], obj["valid l2-mean"])
+    Xr, yr = load_svmlight_file(os.path.join(DATA, "rank.train"))
+    q = np.loadtxt(os.path.join(DATA, "rank.train.query"))
+    prm = {"objective": "lambdarank", "verbose": -1, "eval_at": 3}
+    rds = lgb.Dataset(Xr, yr, group=q)
+    r = lgb.cv(prm, rds, num_boost_round=10, nfold=3, metrics="l2")
+    assert len(r) == 2 and not np.isnan(r["valid l2-mean"]).any()
+    r = lgb.cv(prm, rds, num_boost_round=10, nfold=3)
+    assert len(r) == 2 and not np.isnan(r["valid ndcg@3-mean"]).any()
+    r2 = lgb.cv(prm, rds, num_boost_round=10, folds=GroupKFold(n_splits=3))
+    np.testing.assert_allclose(r["valid ndcg@3-mean"], r2["valid ndcg@3-mean"])
+
+
+def test_cv_with_init_model_booster_and_file(lgb, tmp_path):
+    """test_cv_works_with_init_model."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    params = {"objective": "regression", "verbose": -1}
+    ds = lgb.Dataset(X, y, free_raw_data=False)
+    bst = lgb.train(params=params, train_set=ds, num_boost_round=2)
+    raw = bst.predict(X, raw_score=True)
+    bst.save_model(str(tmp_path / "lgb.model"))
+    kw = {"num_boost_round": 5, "nfold": 3, "stratified": False, "shuffle": False, "seed": 708,
+          "return_cvbooster": True, "params": params}
+    cvs = []
+    for init in (bst, str(tmp_path / "lgb.model")):
+        cvb = lgb.cv(train_set=ds, init_model=init, **kw)["cvbooster"]
+        assert cvb.current_iteration() == [7] * 3
+        for b in cvb.boosters:
+            np.testing.assert_allclose(raw, b.predict(X, raw_score=True, num_iteration=2))
+        cvs.append(cvb)
+    for i in range(3):
+        np.testing.assert_allclose(cvs[0].boosters[i].predict(X), cvs[1].boosters[i].predict(X))
+
+
+def _cancer_train(lgb):
+    X, y = load_breast_cancer(return_X_y=True)
+    X_tr, X_te, y_tr, y_te = _split(X, y)
+    return lgb.Dataset(X_tr, y_tr), X_te, y_te
+
+
+_BIN_LOGLOSS = {"objective": "binary", "metric": "binary_logloss", "verbose": -1}
+
+
+def test_cvbooster_best_iteration_and_fold_average(lgb):
+    """test_cvbooster."""
+    ds, X_te, y_te = _cancer_train(lgb)
+    cvb = lgb.cv(_BIN_LOGLOSS, ds, num_boost_round=25, nfold=3, callbacks=[lgb.early_stopping(stopping_rounds=5)],
+                 return_cvbooster=True)["cvbooster"]
+    assert isinstance(cvb, lgb.CVBooster) and len(cvb.boosters) == 3 and cvb.best_iteration > 0
+    preds = cvb.predict(X_te)
+    assert isinstance(preds, list) and len(preds) == 3
+    for p, b in zip(preds, cvb.boosters):
+        assert b.best_iteration == cvb.best_iteration
+        np.testing.assert_allclose(p, b.predict(X_te, num_iteration=cvb.best_iteration))
+    assert log_loss(y_te, np.mean(preds, axis=0)) < 0.13
+    cvb = lgb.cv(_BIN_LOGLOSS, ds, num_boost_round=20, nfold=3, return_cvbooster=True)["cvbooster"]
+    assert cvb.best_iteration == -1
+    assert log_loss(y_te, np.mean(cvb.predict(X_te), axis=0)) < 0.15
+
+
+def test_cvbooster_save_load_and_pickle(lgb, tmp_path):
+    """test_cvbooster_save_load, test_cvbooster_picklable (pickle / joblib / cloudpickle)."""
+    import cloudpickle
+    import joblib
+
+    ds, X_te, _ = _cancer_train(lgb)
+    cvb = lgb.cv(_BIN_LOGLOSS, ds, num_boost_round=10, nfold=3, callbacks=[lgb.early_stopping(stopping_rounds=5)],
+                 return_cvbooster=True)["cvbooster"]
+    preds, best = cvb.predict(X_te), cvb.best_iteration
+    cvb.save_model(str(tmp_path / "lgb.model"))
+    text = cvb.model_to_string()
+    loaded = [lgb.CVBooster(model_file=str(tmp_path / "lgb.model")), lgb.CVBooster().model_from_string(text),
+              pickle.loads(pickle.dumps(cvb)), cloudpickle.loads(cloudpickle.dumps(cvb))]
+    joblib.dump(cvb, tmp_path / "cvb.joblib")
+    loaded.append(joblib.load(tmp_path / "cvb.joblib"))
+    for c in loaded:
+        assert c.best_iteration == best
+        np.testing.assert_array_equal(preds, c.predict(X_te))
+
+
+def test_feature_names_whitespace_and_non_ascii(lgb, tmp_path):
+    """test_feature_name, test_feature_name_with_non_ascii."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    names = [f"f_{i}" for i in range(4)]
+    ds = lgb.Dataset(X, y, feature_name=names)
+    assert lgb.train({"verbose": -1}, ds, num_boost_round=5).feature_name() == names
+    ds.set_feature_name([f"f {i}" for i in range(4)])
+    assert lgb.train({"verbose": -1}, ds, num_boost_round=5).feature_name() == names
+    uni = ["F_零", "F_一", "F_二", "F_三"]
+    b = lgb.train({"verbose": -1}, lgb.Dataset(X, y, feature_name=uni), num_boost_round=5)
+    assert b.feature_name() == uni
+    b.save_model(str(tmp_path / "lgb.model"))
+    assert lgb.Booster(model_file=str(tmp_path / "lgb.model")).feature_name() == uni
+
+
+def test_parameters_loaded_from_model_file(lgb, tmp_path, capsys):
+    """test_parameters_are_loaded_from_model_file: the model's parameters section comes back as
+    Booster.params (unknown entries warned about and ignored), constructor params are ignored
+    with a warning, predictions unchanged."""
+    rng = np.random.default_rng(11)
+    X = np.hstack([rng.uniform(size=(100, 1)), rng.integers(0, 5, size=(100, 2))])
+    y = rng.uniform(size=(100,))
+    ds = lgb.Dataset(X, y, categorical_feature=[1, 2])
+    params = {"bagging_fraction": 0.8, "bagging_freq": 2, "boosting": "rf", "feature_contri": [0.5, 0.5, 0.5],
+              "feature_fraction": 0.7, "boost_from_average": False, "interaction_constraints": [[0, 1], [0]],
+              "metric": ["l2", "rmse"], "num_leaves": 5, "num_threads": 1, "verbosity": 0}
+    orig = lgb.train(params, ds, num_boost_round=1)
+    path = tmp_path / "model.txt"
+    orig.save_model(path)
+    lines = path.read_text().splitlines(keepends=True)
+    lines.insert(lines.index("parameters:\n") + 1, "[max_conflict_rate: 0]\n")
+    path.write_text("".join(lines))
+    b = lgb.Booster(model_file=path)
+    out = capsys.readouterr().out
+    assert "Ignoring unrecognized parameter 'max_conflict_rate' found in model string." in out
+    assert {k: b.params[k] for k in params} == params
+    assert b.params["categorical_feature"] == [1, 2]
+    with pytest.warns(UserWarning, match="Ignoring params argument, using parameters from model file."):
+        b2 = lgb.Booster(params={"num_leaves": 7}, model_file=path)
+    assert b.params == b2.params
+    np.testing.assert_allclose(b.predict(X), orig.predict(X))
+
+
+def test_params_from_model_string(lgb):
+    """test_string_serialized_params_retrieval."""
+    rng = np.random.default_rng(5)
+    X, y = rng.random((500, 3)), rng.integers(0, 1, 500)
+    params = {"boosting": "gbdt", "deterministic": True, "feature_contri": [0.5] * 3,
+              "interaction_constraints": [[0, 1], [0]], "objective": "binary", "metric": ["auc"], "num_leaves": 7,
+              "learning_rate": 0.05, "feature_fraction": 0.9, "bagging_fraction": 0.8, "bagging_freq": 5,
+              "verbosity": -100}
+    s = lgb.train(params, lgb.Dataset(X, y), num_boost_round=2).model_to_string()
+    with pytest.warns(UserWarning, match="Ignoring params argument, using parameters from model string."):
+        m = lgb.Booster(params={"num_leaves": 32}, model_str=s)
+    for k, v in params.items():
+        assert m.params[k] == v, k
+    assert m.params["deterministic"] is True
+
+
+def test_continue_from_saved_copied_and_pickled_models(lgb, tmp_path):
+    """test_save_load_copy_pickle: continuing from the model in memory, from its file, from a
+    copy / deepcopy and from a pickle gives the same test error."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    X_tr, X_te, y_tr, y_te = _split(X, y)
+    params = {"objective": "regression", "metric": "l2", "verbose": -1}
+
+    def fit(init=None):
+        return lgb.train(params, lgb.Dataset(X_tr, y_tr), num_boost_round=10, init_model=init)
+
+    gbm = fit()
+    want = mean_squared_error(y_te, fit(gbm).predict(X_te))
+    path = str(tmp_path / "lgb.model")
+    gbm.save_model(path)
+    assert "[num_iterations: 10]" in open(path).read()
+    for init in (path, lgb.Booster(model_file=path), copy.copy(gbm), copy.deepcopy(gbm),
+                 pickle.loads(pickle.dumps(gbm))):
+        assert mean_squared_error(y_te, fit(init).predict(X_te)) == pytest.approx(want)
+
+
+_DEFAULT_PARAM_ENTRIES = [
+    "[boosting: gbdt]", "[tree_learner: serial]", "[data: ]", "[valid: ]", "[learning_rate: 0.1]",
+    "[num_leaves: 31]", "[num_threads: 0]", "[deterministic: 0]", "[histogram_pool_size: -1]", "[max_depth: -1]",
+    "[min_data_in_leaf: 20]", "[min_sum_hessian_in_leaf: 0.001]", "[pos_bagging_fraction: 1]",
+    "[neg_bagging_fraction: 1]", "[bagging_freq: 0]", "[bagging_seed: 15415]", "[feature_fraction: 1]",
+    "[feature_fraction_bynode: 1]", "[feature_fraction_seed: 32671]", "[extra_trees: 0]", "[extra_seed: 6642]",
+    "[early_stopping_round: 0]", "[early_stopping_min_delta: 0]", "[first_metric_only: 0]", "[max_delta_step: 0]",
+    "[lambda_l1: 0]", "[lambda_l2: 0]", "[linear_lambda: 0]", "[min_gain_to_split: 0]", "[drop_rate: 0.1]",
+    "[max_drop: 50]", "[skip_drop: 0.5]", "[xgboost_dart_mode: 0]", "[uniform_drop: 0]", "[drop_seed: 20623]",
+    "[top_rate: 0.2]", "[other_rate: 0.1]", "[min_data_per_group: 100]", "[max_cat_threshold: 32]", "[cat_l2: 10]",
+    "[cat_smooth: 10]", "[max_cat_to_onehot: 4]", "[top_k: 20]", "[monotone_constraints: ]",
+    "[monotone_constraints_method: basic]", "[monotone_penalty: 0]", "[feature_contri: ]",
+    "[forcedsplits_filename: ]", "[refit_decay_rate: 0.9]", "[cegb_tradeoff: 1]", "[cegb_penalty_split: 0]",
+    "[cegb_penalty_feature_lazy: ]", "[cegb_penalty_feature_coupled: ]", "[path_smooth: 0]",
+    "[interaction_constraints: ]", "[verbosity: -1]", "[saved_feature_importance_type: 0]",
+    "[use_quantized_grad: 0]", "[num_grad_quant_bins: 4]", "[quant_train_renew_leaf: 0]",
+    "[stochastic_rounding: 1]", "[linear_tree: 0]", "[max_bin: 255]", "[max_bin_by_feature: ]",
+    "[min_data_in_bin: 3]", "[bin_construct_sample_cnt: 200000]", "[data_random_seed: 2350]",
+    "[is_enable_sparse: 1]", "[enable_bundle: 1]", "[use_missing: 1]", "[zero_as_missing: 0]",
+    "[feature_pre_filter: 1]", "[pre_partition: 0]", "[two_round: 0]", "[header: 0]", "[label_column: ]",
+    "[weight_column: ]", "[group_column: ]", "[ignore_column: ]", "[categorical_feature: ]",
+    "[forcedbins_filename: ]", "[precise_float_parser: 0]", "[parser_config_file: ]", "[objective_seed: 4309]",
+    "[num_class: 1]", "[is_unbalance: 0]", "[scale_pos_weight: 1]", "[sigmoid: 1]", "[boost_from_average: 1]",
+    "[reg_sqrt: 0]", "[alpha: 0.9]", "[fair_c: 1]", "[poisson_max_delta_step: 0.7]",
+    "[tweedie_variance_power: 1.5]", "[lambdarank_truncation_level: 30]", "[lambdarank_norm: 1]", "[label_gain: ]",
+    "[lambdarank_position_bias_regularization: 0]", "[eval_at: ]", "[multi_error_top_k: 1]", "[auc_mu_weights: ]",
+    "[num_machines: 1]", "[local_listen_port: 12400]", "[time_out: 120]", "[machine_list_filename: ]",
+    "[machines: ]", "[gpu_platform_id: -1]", "[gpu_device_id: -1]", "[num_gpu: 1]",
+    "[force_col_wise: 0]", "[force_row_wise: 0]", "[device_type: cpu]", "[gpu_use_dp: 0]",
+]
+
+
+def test_all_expected_params_written_to_model_text(lgb, tmp_path):
+    """test_all_expected_params_are_written_out_to_model_text (CPU device entries)."""
+    import joblib
+
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    params = {"objective": "mape", "metric": ["l2", "mae"], "seed": 708, "data_sample_strategy": "bagging",
+              "sub_row": 0.8234, "verbose": -1}
+    gbm = lgb.train(params=params, train_set=lgb.Dataset(data=X, label=y), num_boost_round=3)
+    mem = gbm.model_to_string()
+    gbm.save_model(filename=tmp_path / "out.model")
+    assert mem == (tmp_path / "out.model").read_text()
+    want = ["[objective: mape]", "[metric: l2,l1]", "[data_sample_strategy: bagging]", "[seed: 708]",
+            "[bagging_fraction: 0.8234]", "[num_iterations: 3]"] + _DEFAULT_PARAM_ENTRIES
+    joblib.dump(gbm, tmp_path / "gbm.joblib")
+    again = joblib.load(tmp_path / "gbm.joblib").model_to_string()
+    for entry in want:
+        assert entry in mem, entry
+        assert entry in again, entry
