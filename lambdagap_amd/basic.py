@@ -216,6 +216,7 @@ def _pandas_to_numpy(df: Any, categorical_feature: Any, pandas_categorical: Opti
     else:
         if len(cat_cols) != len(pandas_categorical):
             raise ValueError("train and valid dataset categorical_feature do not match.")
+    ordered = [bool(df[c].cat.ordered) for c in cat_cols]
     df = df.copy() if cat_cols else df
     for col, cats in zip(cat_cols, pandas_categorical):
         if list(df[col].cat.categories) != list(cats):
@@ -223,9 +224,9 @@ def _pandas_to_numpy(df: Any, categorical_feature: Any, pandas_categorical: Opti
         df[col] = df[col].cat.codes.replace({-1: np.nan}).astype(np.float64)
     feature_names = [str(c) for c in df.columns]
     if categorical_feature == "auto":
-        categorical_feature = [str(c) for c in cat_cols]
-    elif cat_cols:
-        categorical_feature = list(categorical_feature) + [str(c) for c in cat_cols if str(c) not in categorical_feature]
+        # unordered category columns only (reference basic.py _data_from_pandas); an explicit
+        # list is taken as given
+        categorical_feature = [str(c) for c, o in zip(cat_cols, ordered) if not o]
     values = df.to_numpy(dtype=np.float64, na_value=np.nan) if hasattr(df, "to_numpy") else df.values.astype(np.float64)
     return values, feature_names, categorical_feature, pandas_categorical
 
@@ -404,7 +405,11 @@ class Dataset:
         return param_dict_to_str(self.params)
 
     def _resolve_categorical(self, feature_names: Optional[List[str]], ncol: int) -> List[int]:
-        cf = self.categorical_feature
+        # a DataFrame's "auto" resolves to its unordered category columns without changing the
+        # user-facing categorical_feature (reference basic.py _lazy_init)
+        cf = getattr(self, "_frame_categorical", None)
+        if cf is None:
+            cf = self.categorical_feature
         if cf is None or cf == "auto" or (isinstance(cf, (list, tuple)) and len(cf) == 0):
             return []
         out = []
@@ -423,7 +428,7 @@ class Dataset:
         if _is_pandas(data):
             pc = self.reference.pandas_categorical if self.reference is not None else None
             data, feature_names, cat, self.pandas_categorical = _pandas_to_numpy(data, self.categorical_feature, pc)
-            self.categorical_feature = cat
+            self._frame_categorical = cat
         elif self.reference is not None:
             self.pandas_categorical = self.reference.pandas_categorical
         if self.feature_name != "auto" and self.feature_name is not None:
@@ -643,6 +648,28 @@ class Dataset:
         return self.position
 
     def get_data(self):
+        """The raw data of the Dataset; a subset slices its reference's raw data on first use
+        (reference basic.py Dataset.get_data)."""
+        if self.handle is None:
+            raise Exception("Cannot get data before construct Dataset")
+        if self.used_indices is not None and self.reference is not None and not getattr(self, "_sliced", False):
+            self.data = self.reference.data
+            if self.data is not None:
+                if isinstance(self.data, np.ndarray) or _is_sparse(self.data):
+                    self.data = self.data[self.used_indices, :]
+                elif _is_pandas(self.data):
+                    self.data = self.data.iloc[self.used_indices].copy()
+                elif isinstance(self.data, Sequence):
+                    self.data = self.data[self.used_indices]
+                elif _is_arrow(self.data):
+                    self.data = self.data.take(self.used_indices)
+                elif not _is_path(self.data):
+                    _log_warning(f"Cannot subset {type(self.data).__name__} type of raw data.\n"
+                                 "Returning original raw data")
+            self._sliced = True
+        if self.data is None:
+            raise LightGBMError("Cannot call `get_data` after freed raw data, "
+                                "set free_raw_data=False when construct Dataset to avoid this.")
         return self.data
 
     _DATASET_PARAMS = ("bin_construct_sample_cnt", "categorical_feature", "data_random_seed", "enable_bundle",

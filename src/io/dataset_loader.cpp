@@ -164,7 +164,9 @@ void ParseTextFile(const std::string& filename, bool header, int label_idx, Owne
     }
   }
   TextFormat fmt = Detect(lines, first);
-  if (fmt == TextFormat::INVALID) {
+  // a binary Dataset file is not text (reference parser.cpp:265 on the same input)
+  const bool binary = first < lines.size() && lines[first].rfind("______LambdaGap_Binary_File_Token______", 0) == 0;
+  if (fmt == TextFormat::INVALID || binary) {
     Log::Fatal("Unknown format of training data. Only CSV, TSV, and LibSVM (zero-based) formatted text files are supported.");
   }
   const size_t n = lines.size() - first;

@@ -797,3 +797,173 @@ def test_all_expected_params_written_to_model_text(lgb, tmp_path):
     for entry in want:
         assert entry in mem, entry
         assert entry in again, entry
+
+
+# ---------------------------------------------------------------------------
+# pandas / contributions / slicing / subsets (test_engine.py:1690-2116)
+def test_pandas_categorical_handling(lgb, tmp_path):
+    """test_pandas_categorical: category dtype columns are categorical by default, ordered
+    categoricals are not, explicit lists override, the category lists are stored with the
+    model and survive save / load / model strings."""
+    pd = pytest.importorskip("pandas")
+    rng = np.random.default_rng(42)
+    X = pd.DataFrame({"A": rng.permutation(["a", "b", "c", "d"] * 75), "B": rng.permutation([1, 2, 3] * 100),
+                      "C": rng.permutation([0.1, 0.2, -0.1, -0.1, 0.2] * 60),
+                      "D": rng.permutation([True, False] * 150),
+                      "E": pd.Categorical(rng.permutation(["z", "y", "x", "w", "v"] * 60), ordered=True)})
+    y = rng.permutation([0, 1] * 150)
+    Xt = pd.DataFrame({"A": rng.permutation(["a", "b", "e"] * 20), "B": rng.permutation([1, 3] * 30),
+                       "C": rng.permutation([0.1, -0.1, 0.2, 0.2] * 15), "D": rng.permutation([True, False] * 30),
+                       "E": pd.Categorical(rng.permutation(["z", "y"] * 30), ordered=True)})
+    cats = ["A", "B", "C", "D"]
+    X[cats] = X[cats].astype("category")
+    Xt[cats] = Xt[cats].astype("category")
+    cat_values = [X[c].cat.categories.tolist() for c in cats + ["E"]]
+    params = {"objective": "binary", "metric": "binary_logloss", "verbose": -1}
+
+    def fit(ds):
+        return lgb.train(params, ds, num_boost_round=10)
+
+    ds0 = lgb.Dataset(X, y)
+    g0 = fit(ds0)
+    assert ds0.categorical_feature == "auto"
+    ds1 = lgb.Dataset(X, pd.DataFrame(y), categorical_feature=[0])
+    g1 = fit(ds1)
+    assert ds1.categorical_feature == [0]
+    ds2 = lgb.Dataset(X, pd.Series(y), categorical_feature=["A"])
+    g2 = fit(ds2)
+    g3 = fit(lgb.Dataset(X, y, categorical_feature=cats))
+    g3.save_model(tmp_path / "categorical.model")
+    g4 = lgb.Booster(model_file=tmp_path / "categorical.model")
+    p4 = g4.predict(Xt)
+    s = g4.model_to_string()
+    g4.model_from_string(s)
+    p5 = g4.predict(Xt)
+    g5 = lgb.Booster(model_str=s)
+    g6 = fit(lgb.Dataset(X, y, categorical_feature=cats + ["E"]))
+    g7 = fit(lgb.Dataset(X, y, categorical_feature=[]))
+    p0 = g0.predict(Xt)
+    assert not np.allclose(p0, g1.predict(Xt))
+    assert not np.allclose(p0, g2.predict(Xt))
+    np.testing.assert_allclose(g1.predict(Xt), g2.predict(Xt))
+    for p in (g3.predict(Xt), p4, p5, g5.predict(Xt)):
+        np.testing.assert_allclose(p0, p)
+    assert not np.allclose(p0, g6.predict(Xt))   # ordered categoricals are not categorical by default
+    assert not np.allclose(p0, g7.predict(Xt))
+    for g in (g0, g1, g2, g3, g4, g5, g6, g7):
+        assert g.pandas_categorical == cat_values
+
+
+def test_pandas_sparse_columns_predict_like_dense(lgb):
+    """test_pandas_sparse."""
+    pd = pytest.importorskip("pandas")
+    rng = np.random.default_rng(9)
+    sa = pd.arrays.SparseArray
+    X = pd.DataFrame({"A": sa(rng.permutation([0, 1, 2] * 100)), "B": sa(rng.permutation([0.0, 0.1, 0.2, -0.1, 0.2] * 60)),
+                      "C": sa(rng.permutation([True, False] * 150))})
+    y = pd.Series(sa(rng.permutation([0, 1] * 150)))
+    Xt = pd.DataFrame({"A": sa(rng.permutation([0, 2] * 30)), "B": sa(rng.permutation([0.0, 0.1, 0.2, -0.1] * 15)),
+                       "C": sa(rng.permutation([True, False] * 30))})
+    b = lgb.train({"objective": "binary", "verbose": -1}, lgb.Dataset(X, y), num_boost_round=10)
+    np.testing.assert_allclose(b.predict(Xt, raw_score=True), b.predict(Xt.sparse.to_dense(), raw_score=True))
+
+
+def test_subset_of_subset_as_validation(lgb):
+    """test_reference_chain."""
+    rng = np.random.default_rng(2)
+    ds = lgb.Dataset(rng.normal(size=(100, 2)), rng.normal(size=(100,)))
+    tr = ds.subset(np.arange(80))
+    va = ds.subset(np.arange(80, 100)).subset(np.arange(18))
+    rec = {}
+    lgb.train({"objective": "regression_l2", "metric": "rmse"}, tr, num_boost_round=20, valid_sets=[tr, va],
+              callbacks=[lgb.record_evaluation(rec)])
+    assert len(rec["training"]["rmse"]) == 20 and len(rec["valid_1"]["rmse"]) == 20
+
+
+def test_contributions_sum_to_raw_score(lgb):
+    """test_contribs."""
+    ds, X_te, _ = _cancer_train(lgb)
+    b = lgb.train(_BIN_LOGLOSS, ds, num_boost_round=20)
+    assert np.linalg.norm(b.predict(X_te, raw_score=True) - b.predict(X_te, pred_contrib=True).sum(axis=1)) < 1e-4
+
+
+@pytest.mark.parametrize("n_labels", [2, 4])
+def test_sparse_contributions_match_dense(lgb, n_labels):
+    """test_contribs_sparse / test_contribs_sparse_multiclass: CSR and CSC inputs give CSR / CSC
+    contributions (a list per class for multiclass) equal to the dense ones."""
+    from scipy.sparse import isspmatrix_csc, isspmatrix_csr
+    from sklearn.datasets import make_multilabel_classification
+
+    X, y = make_multilabel_classification(n_samples=100, sparse=True, n_features=20, n_classes=1, n_labels=n_labels,
+                                          random_state=0)
+    X_tr, X_te, y_tr, _ = _split(X, y.flatten())
+    params = {"objective": "binary", "verbose": -1} if n_labels == 2 else \
+        {"objective": "multiclass", "num_class": n_labels, "verbose": -1}
+    b = lgb.train(params, lgb.Dataset(X_tr, y_tr), num_boost_round=20)
+    dense = b.predict(X_te.toarray(), pred_contrib=True)
+    for fmt, check in ((X_te, isspmatrix_csr), (X_te.tocsc(), isspmatrix_csc)):
+        out = b.predict(fmt, pred_contrib=True)
+        if n_labels == 2:
+            assert check(out)
+            np.testing.assert_allclose(out.toarray(), dense)
+        else:
+            assert isinstance(out, list) and all(check(m) for m in out)
+            arr = np.swapaxes(np.array([m.toarray() for m in out]), 0, 1)
+            np.testing.assert_allclose(arr.reshape(arr.shape[0], -1), dense)
+    if n_labels == 2:
+        assert np.linalg.norm(b.predict(X_te, raw_score=True) - dense.sum(axis=1)) < 1e-4
+    else:
+        per = dense.reshape(dense.shape[0], n_labels, -1)
+        assert np.linalg.norm(b.predict(X_te, raw_score=True) - per.sum(axis=2)) < 1e-4
+
+
+def test_sliced_labels_matrices_and_csr(lgb):
+    """test_sliced_data: strided label views, sliced 2-d arrays and sliced CSR train the same model."""
+    from scipy.sparse import csr_matrix
+
+    rng = np.random.default_rng(4)
+    feats = rng.uniform(size=(100, 5))
+    labels = np.append(np.ones(25, dtype=np.float32), np.zeros(75, dtype=np.float32))
+
+    def fit_predict(f, lab):
+        b = lgb.train({"application": "binary", "verbose": -1, "min_data": 5}, lgb.Dataset(f, label=lab), 10)
+        return b.predict(f)
+
+    base = fit_predict(feats, labels)
+    sliced_labels = np.column_stack((labels, np.ones(100, dtype=np.float32)))[:, 0]
+    np.testing.assert_allclose(base, fit_predict(feats, sliced_labels))
+    big = np.ones((104, 9), dtype=np.float64)
+    big[2:102, 2:7] = feats
+    np.testing.assert_allclose(base, fit_predict(big[2:102, 2:7], sliced_labels))
+    np.testing.assert_allclose(base, fit_predict(csr_matrix(big)[2:102, 2:7], sliced_labels))
+
+
+def test_subsets_of_array_and_binary_file_datasets(lgb, tmp_path):
+    """test_init_with_subset: continuing on another subset of an in-memory Dataset works; for a
+    Dataset loaded from a binary file it fails with 'Unknown format of training data'."""
+    rng = np.random.default_rng(6)
+    data = rng.uniform(size=(50, 2))
+    y = [1] * 25 + [0] * 25
+    full = lgb.Dataset(data, y, free_raw_data=False)
+    i1, i2 = rng.choice(50, 30, replace=False), rng.choice(50, 20, replace=False)
+    s1, s2 = full.subset(i1), full.subset(i2)
+    params = {"objective": "binary", "verbose": -1}
+    init = lgb.train(params=params, train_set=s1, num_boost_round=10, keep_training_booster=True)
+    lgb.train(params=params, train_set=s2, num_boost_round=10, init_model=init)
+    assert full.get_data().shape[0] == 50 and s1.get_data().shape[0] == 30 and s2.get_data().shape[0] == 20
+    path = str(tmp_path / "lgb_train_data.bin")
+    full.save_binary(path)
+    ffile = lgb.Dataset(path, free_raw_data=False)
+    s3, s4 = ffile.subset(i1), ffile.subset(i2)
+    init2 = lgb.train(params=params, train_set=s3, num_boost_round=10, keep_training_booster=True)
+    with pytest.raises(lgb.basic.LightGBMError, match="Unknown format of training data"):
+        lgb.train(params=params, train_set=s4, num_boost_round=10, init_model=init2)
+    assert ffile.get_data() == path and s3.get_data() == path and s4.get_data() == path
+
+
+def test_constructed_subset_without_params(lgb):
+    """test_training_on_constructed_subset_without_params."""
+    rng = np.random.default_rng(8)
+    sub = lgb.Dataset(rng.uniform(size=(100, 10)), rng.uniform(size=(100,))).subset([1, 2, 3, 4]).construct()
+    b = lgb.train({}, sub, num_boost_round=1)
+    assert sub.get_params() == {} and sub.num_data() == 4 and b.current_iteration() == 1
