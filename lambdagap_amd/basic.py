@@ -384,6 +384,11 @@ class Dataset:
                 self.init_score = self._init_score_from_predictor(self._predictor, self.reference.data,
                                                                   self.used_indices)
             self._set_metadata()
+            # reference basic.py construct: a kept subset materialises its rows and label
+            if not self.free_raw_data and self.reference.data is not None:
+                self.get_data()
+            if self.get_label() is None:
+                raise ValueError("Label should not be None.")
             return self
         if self._predictor is not None:  # the continued model's scores replace any init_score
             self.init_score = self._init_score_from_predictor(self._predictor, self.data)
@@ -805,14 +810,26 @@ class Dataset:
         return self
 
     def _update_params(self, params: Optional[Dict[str, Any]]) -> "Dataset":
+        """Merge ``params`` before construction. Once constructed, the Dataset keeps the
+        parameters it was built with: new ones are only checked for changes to binning
+        parameters, which rebuild the Dataset when its raw data is still held, else raise
+        (reference basic.py Dataset._update_params)."""
         if not params:
             return self
-        if self.handle is not None:
-            ret = _LIB.LGBM_DatasetUpdateParamChecking(_c_str(param_dict_to_str(self.params)),
-                                                       _c_str(param_dict_to_str({**self.params, **params})))
-            if ret != 0:
+        params = deepcopy(params)
+        if self.handle is None:
+            self._params_back_up = deepcopy(self.params)
+            self.params.update(params)
+            return self
+        ret = _LIB.LGBM_DatasetUpdateParamChecking(_c_str(param_dict_to_str(self.params)),
+                                                   _c_str(param_dict_to_str(params)))
+        if ret != 0:
+            if self.data is not None:
+                self._params_back_up = deepcopy(self.params)
+                self.params.update(params)
+                self._free_handle()
+            else:
                 raise LightGBMError(_LIB.LGBM_GetLastError().decode("utf-8"))
-        self.params.update(params)
         return self
 
 

@@ -535,17 +535,40 @@ int LGBM_DatasetGetField(DatasetHandle handle, const char* field_name, int* out_
 
 int LGBM_DatasetUpdateParamChecking(const char* old_parameters, const char* new_parameters) {
   API_BEGIN();
+  // only the binning / loading parameters given in `new_parameters` are compared, against the
+  // values the Dataset was built with (reference Booster::CheckDatasetResetConfig)
   auto o = Config::Str2Map(old_parameters), n = Config::Str2Map(new_parameters);
+  Config::KeyAliasTransform(&o);
+  Config::KeyAliasTransform(&n);
   static const char* kDatasetParams[] = {"max_bin", "max_bin_by_feature", "bin_construct_sample_cnt", "min_data_in_bin",
                                          "use_missing", "zero_as_missing", "categorical_feature", "feature_pre_filter",
                                          "enable_bundle", "data_random_seed", "is_enable_sparse", "header",
                                          "two_round", "label_column", "weight_column", "group_column",
                                          "ignore_column", "forcedbins_filename", "linear_tree", "precise_float_parser"};
+  // typed comparison of the dataset keys only (the other parameters may legitimately change)
+  ParamMap ob, nb;
   for (const char* k : kDatasetParams) {
-    std::string a = o.count(k) ? o[k] : "", b = n.count(k) ? n[k] : "";
-    if (a != b) {
-      Log::Fatal("Cannot change %s after constructed Dataset handle.", k);
+    if (o.count(k)) ob[k] = o[k];
+  }
+  nb = ob;
+  for (const char* k : kDatasetParams) {
+    if (n.count(k)) nb[k] = n[k];
+  }
+  Config before, after;
+  before.Set(ob);
+  after.Set(nb);
+  auto lines = [](const std::string& dump) {
+    std::unordered_map<std::string, std::string> m;
+    for (auto& l : common::SplitLines(dump.c_str())) {
+      const size_t c = l.find(": ");
+      if (l.size() > 3 && l.front() == '[' && c != std::string::npos) m[l.substr(1, c - 1)] = l.substr(c + 2);
     }
+    return m;
+  };
+  auto bm = lines(before.ToString()), am = lines(after.ToString());
+  for (const char* k : kDatasetParams) {
+    if (!n.count(k)) continue;
+    if (bm[k] != am[k]) Log::Fatal("Cannot change %s after constructed Dataset handle.", k);
   }
   API_END();
 }

@@ -967,3 +967,344 @@ def test_constructed_subset_without_params(lgb):
     sub = lgb.Dataset(rng.uniform(size=(100, 10)), rng.uniform(size=(100,))).subset([1, 2, 3, 4]).construct()
     b = lgb.train({}, sub, num_boost_round=1)
     assert sub.get_params() == {} and sub.num_data() == 4 and b.current_iteration() == 1
+
+
+# ---------------------------------------------------------------------------
+# bins / refit / constant features / metric selection / custom objectives
+# (test_engine.py:2310-3090)
+from sklearn.datasets import load_iris, make_blobs  # noqa: E402
+
+
+def test_max_bin_by_feature_controls_distinct_outputs(lgb):
+    """test_max_bin_by_feature."""
+    X = np.column_stack([np.arange(100), np.r_[np.zeros(20), np.ones(80)]]).astype(float)
+    y = np.arange(100, dtype=float)
+    params = {"objective": "regression_l2", "verbose": -1, "num_leaves": 100, "min_data_in_leaf": 1,
+              "min_sum_hessian_in_leaf": 0, "min_data_in_bin": 1, "max_bin_by_feature": [100, 2]}
+    assert len(np.unique(lgb.train(params, lgb.Dataset(X, label=y), 1).predict(X))) == 100
+    params["max_bin_by_feature"] = [2, 100]
+    assert len(np.unique(lgb.train(params, lgb.Dataset(X, label=y), 1).predict(X))) == 3
+
+
+def test_small_max_bin_trains(lgb):
+    """test_small_max_bin."""
+    rng = np.random.default_rng(42)
+    y = rng.choice([0, 1], 100)
+    x = np.ones((100, 1))
+    x[:30, 0], x[60:, 0] = -1, 2
+    params = {"objective": "binary", "seed": 0, "min_data_in_leaf": 1, "verbose": -1, "max_bin": 2}
+    lgb.train(params, lgb.Dataset(x, label=y), num_boost_round=5)
+    x[0, 0] = np.nan
+    lgb.train(dict(params, max_bin=3), lgb.Dataset(x, label=y), num_boost_round=5)
+
+
+def test_refit_lowers_test_logloss(lgb):
+    """test_refit."""
+    X_tr, X_te, y_tr, y_te = _split(*load_breast_cancer(return_X_y=True))
+    b = lgb.train({"objective": "binary", "metric": "binary_logloss", "verbose": -1, "min_data": 10},
+                  lgb.Dataset(X_tr, y_tr), num_boost_round=20)
+    assert log_loss(y_te, b.predict(X_te)) > log_loss(y_te, b.refit(X_te, y_te).predict(X_te))
+
+
+@pytest.mark.parametrize("case", ["regression", "binary", "multiclass"])
+def test_refit_single_tree_models(lgb, case):
+    """test_refit_with_one_tree_{regression,binary_classification,multiclass_classification}."""
+    if case == "regression":
+        X, y = make_regression(n_samples=1000, n_features=2, n_informative=2, random_state=42)
+        params = {"objective": "regression", "verbosity": -1}
+    elif case == "binary":
+        X, y = load_breast_cancer(return_X_y=True)
+        params = {"objective": "binary", "verbosity": -1}
+    else:
+        X, y = load_iris(return_X_y=True)
+        params = {"objective": "multiclass", "num_class": 3, "verbose": -1}
+    model = lgb.train(params, lgb.Dataset(X, label=y), num_boost_round=1)
+    assert isinstance(model.refit(X, y), lgb.Booster)
+
+
+def test_refit_with_dataset_params_and_weights(lgb):
+    """test_refit_dataset_params."""
+    X, y = load_breast_cancer(return_X_y=True)
+    b = lgb.train({"objective": "binary", "verbose": -1, "seed": 123}, lgb.Dataset(X, y, init_score=np.zeros(y.size)),
+                  num_boost_round=10)
+    base = log_loss(y, b.predict(X))
+    w = np.random.default_rng(1).uniform(size=(y.shape[0],))
+    nb = b.refit(data=X, label=y, weight=w, dataset_params={"max_bin": 260, "min_data_in_bin": 5,
+                                                             "data_random_seed": 123}, decay_rate=0.0)
+    assert log_loss(y, nb.predict(X)) != base
+    p = nb.train_set.get_params()
+    assert p["max_bin"] == 260 and p["min_data_in_bin"] == 5 and p["data_random_seed"] == 123
+    np.testing.assert_allclose(nb.train_set.get_weight(), w)
+
+
+@pytest.mark.parametrize("boosting", ["rf", "dart"])
+def test_mape_with_rf_and_dart_predicts_outside_unit_range(lgb, boosting):
+    """test_mape_for_specific_boosting_types."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    params = {"boosting_type": boosting, "objective": "mape", "verbose": -1, "bagging_freq": 1,
+              "bagging_fraction": 0.8, "feature_fraction": 0.8, "boost_from_average": True}
+    assert lgb.train(params, lgb.Dataset(X, np.abs(y)), num_boost_round=20).predict(X).mean() > 8
+
+
+@pytest.mark.parametrize("objective,y,expected", [
+    ("regression", [0.0, 10.0, 0.0, 10.0], 5.0), ("regression", [0.0, 1.0, 2.0, 3.0], 1.5),
+    ("regression", [-1.0, 1.0, -2.0, 2.0], 0.0), ("binary", [0.0, 10.0, 0.0, 10.0], 0.5),
+    ("binary", [0.0, 1.0, 2.0, 3.0], 0.75),
+    ("multiclass", [0.0, 1.0, 2.0, 0.0], [0.5, 0.25, 0.25]), ("multiclass", [0.0, 1.0, 2.0, 1.0], [0.25, 0.5, 0.25]),
+    ("multiclassova", [0.0, 1.0, 2.0, 0.0], [0.5, 0.25, 0.25]),
+    ("multiclassova", [0.0, 1.0, 2.0, 1.0], [0.25, 0.5, 0.25]),
+])
+def test_constant_feature_predicts_boost_from_average(lgb, objective, y, expected):
+    """test_constant_features_{regression,binary,multiclass,multiclassova}."""
+    params = {"objective": objective, "num_class": 3 if objective.startswith("multiclass") else 1, "verbose": -1,
+              "min_data": 1, "num_leaves": 2, "learning_rate": 1, "min_data_in_bin": 1, "boost_from_average": True}
+    X = np.ones((len(y), 1))
+    b = lgb.train(params, lgb.Dataset(X, np.array(y), params=params), num_boost_round=2)
+    assert np.allclose(b.predict(X), expected)
+
+
+def test_fpreproc_rewrites_folds(lgb):
+    """test_fpreproc."""
+    def prep(dtrain, dtest, params):
+        tr, te = dtrain.construct().get_data(), dtest.construct().get_data()
+        tr[:, 0] += 1
+        te[:, 0] += 1
+        dtrain.label[-5:] = 3
+        dtest.label[-5:] = 3
+        dtrain2 = lgb.Dataset(tr, dtrain.label)
+        return dtrain2, lgb.Dataset(te, dtest.label, reference=dtrain2), dict(params, num_class=4)
+
+    X, y = load_iris(return_X_y=True)
+    res = lgb.cv({"objective": "multiclass", "num_class": 3, "verbose": -1}, lgb.Dataset(X, y, free_raw_data=False),
+                 num_boost_round=10, fpreproc=prep)
+    assert len(res["valid multi_logloss-mean"]) == 10
+
+
+def _dummy_obj(preds, data):
+    return np.ones(preds.shape), np.ones(preds.shape)
+
+
+def _constant_metric_multi(preds, data):
+    return [("important_metric", 1.5, False), ("irrelevant_metric", 7.8, False)]
+
+
+def test_metric_selection_matrix(lgb):
+    """test_metrics: which metrics cv() / train() report for every combination of objective
+    (built-in / custom), metric in params / arguments / aliases / 'None', and feval."""
+    X, y = load_digits(n_class=2, return_X_y=True)
+    X_tr, X_te, y_tr, y_te = _split(X, y)
+    tr = lgb.Dataset(X_tr, y_tr)
+    va = lgb.Dataset(X_te, y_te, reference=tr)
+    obj = {"objective": "binary", "verbose": -1}
+    dobj = {"objective": _dummy_obj, "verbose": -1}
+
+    def cvkeys(params=obj, **kw):
+        return set(lgb.cv(params, tr, num_boost_round=2, **kw))
+
+    def m(*names):
+        return {f"valid {n}-{s}" for n in names for s in ("mean", "stdv")}
+
+    cases = [
+        ({}, m("binary_logloss")),
+        ({"params": dict(obj, metric="binary_error")}, m("binary_error")),
+        ({"metrics": "binary_logloss"}, m("binary_logloss")),
+        ({"metrics": "binary_error"}, m("binary_error")),
+        ({"params": dict(obj, metric="invalid_metric"), "metrics": "binary_error"}, m("binary_error")),
+        ({"params": {"objective": "regression", "metric": "quantile", "verbose": 2}}, m("quantile")),
+        ({"params": dict(obj, metric=["binary_logloss", "binary_error"])}, m("binary_logloss", "binary_error")),
+        ({"metrics": ["binary_logloss", "binary_error"]}, m("binary_logloss", "binary_error")),
+        ({"metrics": ["None"]}, set()),
+        ({"params": dobj}, set()),
+        ({"params": dict(dobj, metric="binary_error")}, m("binary_error")),
+        ({"params": dobj, "metrics": "binary_error"}, m("binary_error")),
+        ({"params": dict(dobj, metric_types="invalid_metric"), "metrics": "binary_error"}, m("binary_error")),
+        ({"params": dict(dobj, metric=["binary_logloss", "binary_error"])}, m("binary_logloss", "binary_error")),
+        ({"params": dobj, "metrics": ["binary_logloss", "binary_error"]}, m("binary_logloss", "binary_error")),
+        ({"feval": _constant_metric}, m("binary_logloss", "error")),
+        ({"params": dict(obj, metric="binary_error"), "feval": _constant_metric}, m("binary_error", "error")),
+        ({"metrics": "binary_logloss", "feval": _constant_metric_multi},
+         m("binary_logloss", "important_metric", "irrelevant_metric")),
+        ({"params": dict(obj, metric="invalid_metric"), "metrics": "binary_error", "feval": _constant_metric},
+         m("binary_error", "error")),
+        ({"metrics": ["binary_logloss", "binary_error"], "feval": _constant_metric},
+         m("binary_logloss", "binary_error", "error")),
+        ({"metrics": ["None"], "feval": _constant_metric}, m("error")),
+        ({"params": dobj, "feval": _constant_metric}, m("error")),
+        ({"params": dict(dobj, metric="binary_error"), "feval": _constant_metric}, m("binary_error", "error")),
+        ({"params": dict(dobj, metric="None"), "feval": _constant_metric}, m("error")),
+    ]
+    for na in ("None", "na", "null", "custom"):
+        cases.append(({"metrics": na}, set()))
+    for kw, want in cases:
+        assert cvkeys(**kw) == want, kw
+    r = lgb.cv(obj, tr, num_boost_round=2, metrics="binary_logloss", feval=_constant_metric_multi)
+    assert r["valid important_metric-mean"] == [1.5, 1.5] and r["valid irrelevant_metric-mean"] == [7.8, 7.8]
+
+    def trkeys(params=obj, **kw):
+        rec = {}
+        lgb.train(params, tr, num_boost_round=2, valid_sets=[va], callbacks=[lgb.record_evaluation(rec)], **kw)
+        return rec
+
+    assert set(trkeys()["valid_0"]) == {"binary_logloss"}
+    assert set(trkeys(dict(obj, metric="binary_error"))["valid_0"]) == {"binary_error"}
+    assert set(trkeys(dict(obj, metric=["binary_logloss", "binary_error"]))["valid_0"]) == \
+        {"binary_logloss", "binary_error"}
+    for na in ("None", "na", "null", "custom"):
+        assert trkeys(dict(obj, metric=na)) == {}
+    assert trkeys(dobj) == {}
+    assert set(trkeys(dict(dobj, metric="binary_logloss"))["valid_0"]) == {"binary_logloss"}
+    assert set(trkeys(feval=_constant_metric)["valid_0"]) == {"binary_logloss", "error"}
+    rec = trkeys(dict(obj, metric="binary_logloss"), feval=_constant_metric_multi)["valid_0"]
+    assert rec["important_metric"] == [1.5, 1.5] and rec["irrelevant_metric"] == [7.8, 7.8] and len(rec) == 3
+    assert set(trkeys(dict(obj, metric="None"), feval=_constant_metric)["valid_0"]) == {"error"}
+    assert set(trkeys(dobj, feval=_constant_metric)["valid_0"]) == {"error"}
+
+    # multiclass objective aliases and num_class checks
+    Xm, ym = load_digits(n_class=3, return_X_y=True)
+    trm = lgb.Dataset(Xm, ym)
+
+    def mkeys(params, **kw):
+        return set(lgb.cv(params, trm, num_boost_round=2, **kw))
+
+    d3 = {"objective": _dummy_obj, "num_class": 3, "verbose": -1}
+    d1 = {"objective": _dummy_obj, "num_class": 1, "verbose": -1}
+    aliases = ["multiclass", "softmax", "multiclassova", "multiclass_ova", "ova", "ovr"]
+    for a in aliases:
+        c3 = {"objective": a, "num_class": 3, "verbose": -1}
+        assert mkeys(c3) == m("multi_logloss")
+        assert mkeys(c3, feval=_constant_metric) == m("multi_logloss", "error")
+        assert mkeys(d3, feval=_constant_metric) == m("error")
+        assert mkeys(d1) == set()
+        assert mkeys(d1, feval=_constant_metric) == m("error")
+        with pytest.raises(lgb.basic.LightGBMError, match="Multiclass objective and metrics don't match"):
+            mkeys(d1, metrics=a, feval=_constant_metric)
+        with pytest.raises(lgb.basic.LightGBMError,
+                           match="Number of classes should be specified and greater than 1 for multiclass training"):
+            mkeys({"objective": a, "verbose": -1})
+        for ma in aliases + ["multi_logloss"]:
+            assert mkeys(c3, metrics=ma) == m("multi_logloss")
+        assert mkeys(c3, metrics="multi_error") == m("multi_error")
+        with pytest.raises(lgb.basic.LightGBMError, match="Multiclass objective and metrics don't match"):
+            mkeys(c3, metrics="binary_logloss")
+    with pytest.raises(lgb.basic.LightGBMError, match="Number of classes must be 1 for non-multiclass training"):
+        mkeys({"num_class": 3, "verbose": -1})
+    assert mkeys(d3) == set()
+    for ma in aliases + ["multi_logloss"]:
+        assert mkeys(d3, metrics=ma) == m("multi_logloss")
+    assert mkeys(d3, metrics="multi_error") == m("multi_error")
+    with pytest.raises(lgb.basic.LightGBMError, match="Multiclass objective and metrics don't match"):
+        mkeys(d3, metrics="binary_error")
+
+
+def test_multiple_feval_train_and_cv(lgb):
+    """test_multiple_feval_train, test_multiple_feval_cv."""
+    X, y = load_breast_cancer(return_X_y=True)
+    params = {"verbose": -1, "objective": "binary", "metric": "binary_logloss"}
+    X_tr, X_va, y_tr, y_va = train_test_split(X, y, test_size=0.2, random_state=0)
+    tr = lgb.Dataset(X_tr, y_tr)
+    rec = {}
+    lgb.train(params, tr, valid_sets=lgb.Dataset(X_va, y_va, reference=tr), num_boost_round=5,
+              feval=[_constant_metric, _decreasing_metric], callbacks=[lgb.record_evaluation(rec)])
+    assert set(rec["valid_0"]) == {"binary_logloss", "error", "decreasing_metric"}
+    r = lgb.cv(params, lgb.Dataset(X, y), num_boost_round=5, feval=[_constant_metric, _decreasing_metric])
+    assert set(r) == {f"valid {n}-{s}" for n in ("binary_logloss", "error", "decreasing_metric")
+                      for s in ("mean", "stdv")}
+
+
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def _logloss_obj(preds, data):
+    p = _sigmoid(preds)
+    return p - data.get_label(), p * (1.0 - p)
+
+
+def _mse_obj(preds, data):
+    return preds - data.get_label(), np.ones(len(preds))
+
+
+def test_callable_objective_exact_values(lgb):
+    """test_objective_callable_train_binary_classification / _regression: the reference's exact
+    training-set log loss, AUC and MSE after 20 rounds with a Python objective."""
+    X, y = load_breast_cancer(return_X_y=True)
+    b = lgb.train({"verbose": -1, "objective": _logloss_obj, "learning_rate": 0.01}, lgb.Dataset(X, y), 20)
+    p = _sigmoid(b.predict(X))
+    assert b.params["objective"] == "none"
+    assert log_loss(y, p) == pytest.approx(0.547907)
+    assert roc_auc_score(y, p) == pytest.approx(0.995944)
+    Xr, yr = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    b = lgb.train({"verbose": -1, "objective": _mse_obj}, lgb.Dataset(Xr, yr), 20)
+    assert b.params["objective"] == "none"
+    assert mean_squared_error(yr, b.predict(Xr)) == pytest.approx(286.724194)
+
+
+def test_callable_objective_in_cv(lgb):
+    """test_objective_callable_cv_binary_classification / _regression."""
+    X, y = load_breast_cancer(return_X_y=True)
+    cvb = lgb.cv({"verbose": -1, "objective": _logloss_obj, "learning_rate": 0.01}, lgb.Dataset(X, y),
+                 num_boost_round=20, nfold=3, return_cvbooster=True)["cvbooster"].boosters
+    assert all(b.params["objective"] == "none" for b in cvb)
+    assert all(log_loss(y, _sigmoid(b.predict(X))) < 0.56 for b in cvb)
+    Xr, yr = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    cvb = lgb.cv({"verbose": -1, "objective": _mse_obj}, lgb.Dataset(Xr, yr), num_boost_round=20, nfold=3,
+                 stratified=False, return_cvbooster=True)["cvbooster"].boosters
+    assert all(b.params["objective"] == "none" for b in cvb)
+    assert all(mean_squared_error(yr, b.predict(Xr)) < 463 for b in cvb)
+
+
+def test_default_objective_is_regression_with_l2(lgb):
+    """test_default_objective_and_metric."""
+    X, y = load_breast_cancer(return_X_y=True)
+    X_tr, X_te, y_tr, y_te = train_test_split(X, y, test_size=0.2, random_state=0)
+    tr = lgb.Dataset(X_tr, y_tr)
+    rec = {}
+    lgb.train({"verbose": -1}, tr, valid_sets=lgb.Dataset(X_te, y_te, reference=tr), num_boost_round=5,
+              callbacks=[lgb.record_evaluation(rec)])
+    assert set(rec["valid_0"]) == {"l2"} and len(rec["valid_0"]["l2"]) == 5
+
+
+def _softmax(x):
+    e = np.exp(x - x.max(axis=1, keepdims=True))
+    return e / e.sum(axis=1, keepdims=True)
+
+
+@pytest.mark.parametrize("use_weight", [True, False])
+def test_multiclass_custom_objective_and_eval(lgb, use_weight):
+    """test_multiclass_custom_objective, test_multiclass_custom_eval."""
+    def custom_obj(preds, ds):
+        yt, w = ds.get_label(), ds.get_weight()
+        prob = _softmax(preds)
+        g = prob.copy()
+        g[np.arange(len(yt)), yt.astype(int)] -= 1.0
+        h = preds.shape[1] / (preds.shape[1] - 1) * prob * (1 - prob)
+        if w is not None:
+            g, h = g * w.reshape(-1, 1), h * w.reshape(-1, 1)
+        return g, h
+
+    def custom_eval(preds, ds):
+        return "custom_logloss", log_loss(ds.get_label(), preds, sample_weight=ds.get_weight()), False
+
+    X, y = make_blobs(n_samples=1000, centers=[[-4, -4], [4, 4], [-4, 4]], random_state=42)
+    ds = lgb.Dataset(X, y)
+    if use_weight:
+        ds.set_weight(np.full_like(y, 2))
+    params = {"objective": "multiclass", "num_class": 3, "num_leaves": 7}
+    builtin = lgb.train(params, ds, num_boost_round=10).predict(X)
+    custom = _softmax(lgb.train(dict(params, objective=custom_obj), ds, num_boost_round=10).predict(X))
+    np.testing.assert_allclose(builtin, custom, rtol=0.01)
+    w = np.full_like(y, 2)
+    X_tr, X_va, y_tr, y_va, w_tr, w_va = train_test_split(X, y, w, test_size=0.2, random_state=0)
+    tr, va = lgb.Dataset(X_tr, y_tr), None
+    va = lgb.Dataset(X_va, y_va, reference=tr)
+    if use_weight:
+        tr.set_weight(w_tr)
+        va.set_weight(w_va)
+    rec = {}
+    b = lgb.train(params, tr, num_boost_round=10, valid_sets=[tr, va], valid_names=["train", "valid"],
+                  feval=custom_eval, callbacks=[lgb.record_evaluation(rec)], keep_training_booster=True)
+    for key, d in (("train", tr), ("valid", va)):
+        np.testing.assert_allclose(rec[key]["multi_logloss"], rec[key]["custom_logloss"])
+        _, metric, value, _ = b.eval(d, key, feval=custom_eval)[1]
+        assert metric == "custom_logloss"
+        np.testing.assert_allclose(value, rec[key][metric][-1])
