@@ -367,6 +367,14 @@ class Dataset:
             return self
         if self.reference is not None:
             self.reference.construct()
+            # a validation set / subset is binned like its reference (reference basic.py construct)
+            ref_params, own = self.reference.get_params(), self.get_params()
+            if own != ref_params:
+                cat_keys = {"categorical_feature"} | set(_aliases().get("categorical_feature", []))
+                strip = lambda d: {k: v for k, v in d.items() if k not in cat_keys}  # noqa: E731
+                if strip(own) != strip(ref_params):
+                    _log_warning("Overriding the parameters from Reference Dataset.")
+                self._update_params(ref_params)
         if self.used_indices is not None and self.reference is not None:
             # subset of a constructed dataset
             idx = np.ascontiguousarray(self.used_indices, dtype=np.int32)

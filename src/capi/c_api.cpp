@@ -544,7 +544,7 @@ int LGBM_DatasetUpdateParamChecking(const char* old_parameters, const char* new_
                                          "use_missing", "zero_as_missing", "categorical_feature", "feature_pre_filter",
                                          "enable_bundle", "data_random_seed", "is_enable_sparse", "header",
                                          "two_round", "label_column", "weight_column", "group_column",
-                                         "ignore_column", "forcedbins_filename", "linear_tree", "precise_float_parser"};
+                                         "ignore_column", "linear_tree", "precise_float_parser"};
   // typed comparison of the dataset keys only (the other parameters may legitimately change)
   ParamMap ob, nb;
   for (const char* k : kDatasetParams) {
@@ -566,9 +566,30 @@ int LGBM_DatasetUpdateParamChecking(const char* old_parameters, const char* new_
     return m;
   };
   auto bm = lines(before.ToString()), am = lines(after.ToString());
+  if (n.count("forcedbins_filename")) Log::Fatal("Cannot change forced bins after constructed Dataset handle.");
   for (const char* k : kDatasetParams) {
     if (!n.count(k)) continue;
     if (bm[k] != am[k]) Log::Fatal("Cannot change %s after constructed Dataset handle.", k);
+  }
+  if (n.count("pre_partition") && (o.count("pre_partition") ? o["pre_partition"] : "false") != n["pre_partition"]) {
+    Config a, b;
+    a.Set({{"pre_partition", o.count("pre_partition") ? o["pre_partition"] : "false"}});
+    b.Set({{"pre_partition", n["pre_partition"]}});
+    if (a.pre_partition != b.pre_partition) Log::Fatal("Cannot change pre_partition after constructed Dataset handle.");
+  }
+  if (n.count("min_data_in_leaf")) {
+    Config a, b;
+    ParamMap ao;
+    for (const char* k : {"min_data_in_leaf", "feature_pre_filter"}) {
+      if (o.count(k)) ao[k] = o[k];
+    }
+    a.Set(ao);
+    b.Set({{"min_data_in_leaf", n["min_data_in_leaf"]}});
+    if (b.min_data_in_leaf < a.min_data_in_leaf && a.feature_pre_filter) {
+      Log::Fatal("Reducing `min_data_in_leaf` with `feature_pre_filter=true` may cause unexpected behaviour for "
+                 "features that were pre-filtered by the larger `min_data_in_leaf`.\nYou need to set "
+                 "`feature_pre_filter=false` to dynamically change the `min_data_in_leaf`.");
+    }
   }
   API_END();
 }

@@ -175,6 +175,7 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian
     std::ifstream in(config_->forcedsplits_filename);
     if (in) forced_json_.assign((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
     else Log::Warning("Forced splits file %s cannot be opened", config_->forcedsplits_filename.c_str());
+    CheckForcedSplitFeatures();
   }
   if (want_device_hist_) hist_backend_ = device::CreateHistogramBackend(config_, train_data);
   Log::Info("Number of data points in the train set: %d, number of used features: %d", num_data_, num_features_);
@@ -802,6 +803,26 @@ std::unique_ptr<ForcedNode> ParseForced(const std::string& s, size_t* pos) {
   return node;
 }
 }  // namespace
+
+// reference gbdt.cpp CheckForcedSplitFeatures: every node's feature must exist in the data
+void SerialTreeLearner::CheckForcedSplitFeatures() const {
+  if (forced_json_.empty()) return;
+  size_t pos = 0;
+  auto root = ParseForced(forced_json_, &pos);
+  const int max_idx = train_data_->num_total_features() - 1;
+  std::queue<const ForcedNode*> q;
+  if (root) q.push(root.get());
+  while (!q.empty()) {
+    const ForcedNode* n = q.front();
+    q.pop();
+    if (n->feature > max_idx) {
+      Log::Fatal("Forced splits file includes feature index %d, but maximum feature index in dataset is %d",
+                 n->feature, max_idx);
+    }
+    if (n->left) q.push(n->left.get());
+    if (n->right) q.push(n->right.get());
+  }
+}
 
 int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf) {
   if (forced_json_.empty()) return 0;

@@ -118,6 +118,7 @@ class SerialTreeLearner : public TreeLearner {
   void ResetHistPool();
   void SetupPolicies();
   int ForceSplits(Tree* tree, int* left_leaf, int* right_leaf);
+  void CheckForcedSplitFeatures() const;
   // BestSplitForFeature + CEGB deduction + monotone split penalty (ComputeBestSplitForFeature)
   SplitInfo ScoreFeature(const Tree* tree, const double* group_hist, int f, const LeafStat& leaf,
                          double parent_output, bool* splittable);

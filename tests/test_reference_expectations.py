@@ -1308,3 +1308,223 @@ def test_multiclass_custom_objective_and_eval(lgb, use_weight):
         _, metric, value, _ = b.eval(d, key, feval=custom_eval)[1]
         assert metric == "custom_logloss"
         np.testing.assert_allclose(value, rec[key][metric][-1])
+
+
+# ---------------------------------------------------------------------------
+# split value histogram, early stopping on the first metric (test_engine.py:3117-3350)
+def test_split_value_histogram_shapes(lgb):
+    """test_get_split_value_histogram: the reference's exact bin counts (12 distinct split values
+    of feature 0 after 20 trees), numpy / xgboost styles, names vs indices, categorical refusal."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    X, y = np.repeat(X, 3, axis=0), np.repeat(y, 3, axis=0)
+    X[:, 2] = np.random.default_rng(0).integers(0, 20, size=X.shape[0])
+    g = lgb.train({"verbose": -1}, lgb.Dataset(X, y, categorical_feature=[2]), num_boost_round=20)
+    kw = {"feature": 0, "xgboost_style": True}
+    for bins, rows in ((None, 12), (999, 12), (-1, 1), (0, 1), (1, 1), (2, 2), (6, 6), (7, 7)):
+        out = g.get_split_value_histogram(**kw) if bins is None else g.get_split_value_histogram(bins=bins, **kw)
+        assert out.shape == (rows, 2), bins
+    for f in (0, X.shape[-1] - 1):
+        np.testing.assert_allclose(g.get_split_value_histogram(f, xgboost_style=True).values,
+                                   g.get_split_value_histogram(g.feature_name()[f], xgboost_style=True).values)
+    hist, edges = g.get_split_value_histogram(0)
+    assert len(hist) == 20 and len(edges) == 21
+    for bins in (999, 1, 2, 6, 7):
+        hist, edges = g.get_split_value_histogram(0, bins=bins)
+        assert len(hist) == bins and len(edges) == bins + 1
+    for bad in (-1, 0):
+        with pytest.raises(ValueError, match="`bins` must be positive, when an integer"):
+            g.get_split_value_histogram(0, bins=bad)
+    for f in (0, X.shape[-1] - 1):
+        hi, bi = g.get_split_value_histogram(f)
+        hn, bn = g.get_split_value_histogram(g.feature_name()[f])
+        np.testing.assert_array_equal(hi, hn)
+        np.testing.assert_allclose(bi, bn)
+    vals, edges = g.get_split_value_histogram(0, bins="auto")
+    xs = g.get_split_value_histogram(0, bins="auto", xgboost_style=True)
+    mask = vals > 0
+    np.testing.assert_array_equal(vals[mask], xs["Count"].values)
+    np.testing.assert_allclose(edges[1:][mask], xs["SplitValue"].values)
+    with pytest.raises(lgb.basic.LightGBMError, match="Cannot compute split value histogram for the categorical"):
+        g.get_split_value_histogram(2)
+
+
+def test_early_stopping_first_metric_only_exact_iterations(lgb):
+    """test_early_stopping_for_only_first_metric: the reference's exact best iterations (train:
+    l1 / l2 best at 3 on the first validation set, l2 at 15 on the second; cv: l1 15, l2 13)."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    X_tr, X_te, y_tr, y_te = train_test_split(X, y, test_size=0.2, random_state=42)
+    X1, X2, y1, y2 = train_test_split(X_te, y_te, test_size=0.5, random_state=73)
+    tr = lgb.Dataset(X_tr, y_tr)
+    v1, v2 = lgb.Dataset(X1, y1, reference=tr), lgb.Dataset(X2, y2, reference=tr)
+
+    def run_train(valid, metric, want, first_only, feval=None):
+        params = {"objective": "regression", "learning_rate": 1.1, "num_leaves": 10, "metric": metric, "verbose": -1,
+                  "seed": 123}
+        b = lgb.train(params, tr, num_boost_round=25, valid_sets=valid, feval=feval,
+                      callbacks=[lgb.early_stopping(stopping_rounds=5, first_metric_only=first_only)])
+        assert b.best_iteration == want, (metric, first_only)
+
+    def run_cv(metric, want, first_only, train_metric, feval=None):
+        params = {"objective": "regression", "learning_rate": 0.9, "num_leaves": 10, "metric": metric, "verbose": -1,
+                  "seed": 123, "gpu_use_dp": True}
+        r = lgb.cv(params, train_set=tr, num_boost_round=25, stratified=False, feval=feval,
+                   callbacks=[lgb.early_stopping(stopping_rounds=5, first_metric_only=first_only)],
+                   eval_train_metric=train_metric)
+        assert len(r[list(r.keys())[0]]) == want, (metric, first_only, train_metric)
+
+    for metric, want, fo in (([], 3, False), ([], 3, True), (None, 3, False), (None, 3, True), ("l2", 3, True),
+                             ("l1", 3, True), (["l2", "l1"], 3, True), (["l1", "l2"], 3, True),
+                             (["l2", "l1"], 3, False), (["l1", "l2"], 3, False)):
+        run_train(v1, metric, want, fo)
+
+    def dec_then_const(p, d):
+        return [_decreasing_metric(p, d), _constant_metric(p, d)]
+
+    def const_then_dec(p, d):
+        return [_constant_metric(p, d), _decreasing_metric(p, d)]
+
+    run_train(v1, "None", 1, False, feval=dec_then_const)
+    run_train(v1, "None", 25, True, feval=dec_then_const)
+    run_train(v1, "None", 1, True, feval=const_then_dec)
+    run_train([v1, v2], ["l2", "l1"], 3, True)
+    run_train([v2, v1], ["l2", "l1"], 3, True)
+    run_train([v1, v2], ["l1", "l2"], 3, True)
+    run_train([v2, v1], ["l1", "l2"], 3, True)
+    for tm in (False, True):
+        for metric, want, fo in ((None, 13, True), ("l2", 13, True), ("l1", 15, True), (["l2", "l1"], 13, True),
+                                 (["l1", "l2"], 15, True), (["l2", "l1"], 13, False), (["l1", "l2"], 13, False)):
+            run_cv(metric, want, fo, tm)
+    run_cv("None", 1, False, False, feval=dec_then_const)
+    run_cv("None", 25, True, False, feval=dec_then_const)
+    run_cv("None", 1, True, False, feval=const_then_dec)
+
+
+# ---------------------------------------------------------------------------
+# node sampling, forced splits / bins, binning, dataset param updates, regularisers
+# (test_engine.py:3353-3640)
+import json  # noqa: E402
+
+
+def test_feature_fraction_bynode(lgb):
+    """test_node_level_subcol."""
+    X_tr, X_te, y_tr, y_te = _split(*load_breast_cancer(return_X_y=True))
+    params = {"objective": "binary", "metric": "binary_logloss", "feature_fraction_bynode": 0.8,
+              "feature_fraction": 1.0, "verbose": -1}
+    b, rec = _train_with_record(lgb, params, X_tr, y_tr, X_te, y_te, 25)
+    ret = log_loss(y_te, b.predict(X_te))
+    assert ret < 0.14 and rec["binary_logloss"][-1] == pytest.approx(ret)
+    b2 = lgb.train(dict(params, feature_fraction=0.5), lgb.Dataset(X_tr, y_tr), 25)
+    assert ret != log_loss(y_te, b2.predict(X_te))
+
+
+def test_forced_split_with_out_of_range_feature(lgb, tmp_path):
+    """test_forced_split_feature_indices."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    f = tmp_path / "forced_split.json"
+    f.write_text(json.dumps({"feature": 0, "threshold": 0.5, "left": {"feature": X.shape[1], "threshold": 0.5}}))
+    with pytest.raises(lgb.basic.LightGBMError, match="Forced splits file includes feature index"):
+        lgb.train({"objective": "regression", "forcedsplits_filename": f}, lgb.Dataset(X, y))
+
+
+def test_forced_bins_files(lgb):
+    """test_forced_bins (examples/regression/forced_bins*.json)."""
+    ex = os.path.join(DATA, "examples", "regression")
+    x = np.empty((100, 2))
+    x[:, 0] = np.arange(0, 1, 0.01)
+    x[:, 1] = -np.arange(0, 1, 0.01)
+    y = np.arange(0, 1, 0.01)
+    params = {"objective": "regression_l1", "max_bin": 5, "forcedbins_filename": os.path.join(ex, "forced_bins.json"),
+              "num_leaves": 2, "min_data_in_leaf": 1, "verbose": -1}
+    est = lgb.train(params, lgb.Dataset(x, label=y), num_boost_round=20)
+    nx = np.zeros((3, 2))
+    nx[:, 0] = [0.31, 0.37, 0.41]
+    assert len(np.unique(est.predict(nx))) == 3
+    nx[:, 0] = 0
+    nx[:, 1] = [-0.9, -0.6, -0.3]
+    assert len(np.unique(est.predict(nx))) == 1
+    est = lgb.train(dict(params, forcedbins_filename=""), lgb.Dataset(x, label=y), num_boost_round=20)
+    assert len(np.unique(est.predict(nx))) == 3
+    p2 = dict(params, forcedbins_filename=os.path.join(ex, "forced_bins2.json"), max_bin=11)
+    est = lgb.train(p2, lgb.Dataset(x[:, :1], label=y), num_boost_round=50)
+    _, counts = np.unique(est.predict(x[1:, :1]), return_counts=True)
+    assert min(counts) >= 9 and max(counts) <= 11
+
+
+def test_binning_one_signed_features(lgb):
+    """test_binning_same_sign: zero falls with the negative side for a positive-only feature and
+    with the positive side for a negative-only one."""
+    x = np.empty((99, 2))
+    x[:, 0] = np.arange(0.01, 1, 0.01)
+    x[:, 1] = -np.arange(0.01, 1, 0.01)
+    y = np.arange(0.01, 1, 0.01)
+    est = lgb.train({"objective": "regression_l1", "max_bin": 5, "num_leaves": 2, "min_data_in_leaf": 1,
+                     "verbose": -1, "seed": 0}, lgb.Dataset(x, label=y), num_boost_round=20)
+    nx = np.zeros((3, 2))
+    nx[:, 0] = [-1, 0, 1]
+    p = est.predict(nx)
+    assert p[0] == pytest.approx(p[1]) and p[1] != pytest.approx(p[2])
+    nx = np.zeros((3, 2))
+    nx[:, 1] = [-1, 0, 1]
+    p = est.predict(nx)
+    assert p[0] != pytest.approx(p[1]) and p[1] == pytest.approx(p[2])
+
+
+def test_dataset_param_updates_allowed_and_refused(lgb):
+    """test_dataset_update_params."""
+    rng = np.random.default_rng(12)
+    base = {"max_bin": 100, "max_bin_by_feature": [20, 10], "bin_construct_sample_cnt": 10000, "min_data_in_bin": 1,
+            "use_missing": False, "zero_as_missing": False, "categorical_feature": [0], "feature_pre_filter": True,
+            "pre_partition": False, "enable_bundle": True, "data_random_seed": 0, "is_enable_sparse": True,
+            "header": True, "two_round": True, "label_column": 0, "weight_column": 0, "group_column": 0,
+            "ignore_column": 0, "min_data_in_leaf": 10, "linear_tree": False, "precise_float_parser": True,
+            "verbose": -1}
+    changed = {"max_bin": 150, "max_bin_by_feature": [30, 5], "bin_construct_sample_cnt": 5000, "min_data_in_bin": 2,
+               "use_missing": True, "zero_as_missing": True, "categorical_feature": [0, 1],
+               "feature_pre_filter": False, "pre_partition": True, "enable_bundle": False, "data_random_seed": 1,
+               "is_enable_sparse": False, "header": False, "two_round": False, "label_column": 1,
+               "weight_column": 1, "group_column": 1, "ignore_column": 1,
+               "forcedbins_filename": "/some/path/forcedbins.json", "min_data_in_leaf": 2, "linear_tree": True,
+               "precise_float_parser": False}
+    X, y = rng.uniform(size=(100, 2)), rng.uniform(size=(100,))
+    p = dict(base)
+    ds = lgb.Dataset(X, y, params=p, free_raw_data=False).construct()
+    p["min_data_in_leaf"] -= 1
+    lgb.train(p, ds, num_boost_round=3)
+    ds = lgb.Dataset(X, y, params=p)
+    p["min_data_in_leaf"] -= 1
+    lgb.train(p, ds, num_boost_round=3)
+    p["min_data_in_leaf"] += 2
+    lgb.train(p, ds, num_boost_round=3)
+    p["feature_pre_filter"] = False
+    ds = lgb.Dataset(X, y, params=p).construct()
+    p["min_data_in_leaf"] -= 4
+    lgb.train(p, ds, num_boost_round=3)
+    p["feature_pre_filter"] = True
+    ds = lgb.Dataset(X, y, params=p).construct()
+    for key, value in changed.items():
+        q = dict(p, **{key: value})
+        name = "forced bins" if key == "forcedbins_filename" else key
+        msg = ("Reducing `min_data_in_leaf` with `feature_pre_filter=true` may cause *" if key == "min_data_in_leaf"
+               else f"Cannot change {name} *")
+        with pytest.raises(lgb.basic.LightGBMError, match=msg):
+            lgb.train(q, ds, num_boost_round=3)
+
+
+def test_dataset_params_with_reference_dataset(lgb):
+    """test_dataset_params_with_reference."""
+    rng = np.random.default_rng(13)
+    prm = {"max_bin": 100}
+    tr = lgb.Dataset(rng.uniform(size=(100, 2)), rng.uniform(size=(100,)), params=prm, free_raw_data=False).construct()
+    va = lgb.Dataset(rng.uniform(size=(100, 2)), rng.uniform(size=(100,)), reference=tr, free_raw_data=False).construct()
+    assert tr.get_params() == prm and va.get_params() == prm
+    lgb.train(prm, tr, valid_sets=[va])
+
+
+@pytest.mark.parametrize("extra", [{"extra_trees": True}, {"path_smooth": 1}])
+def test_extra_trees_and_path_smoothing_regularise(lgb, extra):
+    """test_extra_trees, test_path_smoothing."""
+    X, y = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    params = {"objective": "regression", "num_leaves": 32, "verbose": -1, "seed": 0}
+    err = mean_squared_error(y, lgb.train(params, lgb.Dataset(X, label=y), 10).predict(X))
+    err2 = mean_squared_error(y, lgb.train(dict(params, **extra), lgb.Dataset(X, label=y), 10).predict(X))
+    assert err < err2
