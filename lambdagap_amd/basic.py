@@ -1443,6 +1443,10 @@ class Booster:
                    "value": node["internal_value"] if is_split else node["leaf_value"],
                    "weight": node["internal_weight"] if is_split else node.get("leaf_weight"),
                    "count": node["internal_count"] if is_split else node.get("leaf_count")}
+            if not is_split and "leaf_weight" not in node:
+                # a single-leaf tree has no weight record; the reference leaves both unset
+                # (basic.py trees_to_dataframe _is_single_node_tree)
+                row["weight"] = row["count"] = None
             rows.append(row)
             if is_split:
                 lrow = walk(node["left_child"], tree_index, depth + 1, nid)

@@ -545,16 +545,14 @@ void GBDT::RefitTree(const std::vector<std::vector<int>>& leaf_preds) {
         learner_->DeviceGetGradients(&gradients_, &hessians_);
       }
       auto nt = learner_->FitByExistingTree(models_[m].get(), leaf_pred, gradients_.data() + off, hessians_.data() + off);
-      // train score: refit tree replaces the old one
+      // The refit booster's training score starts from the init score alone (MergeFrom adds
+      // no score), so each refit tree is added on top of the refit trees before it
+      // (reference gbdt.cpp RefitTree:293-294, AddScore of the new tree only).
       if (device_mode_) {
         learner_->DeviceAddTreeToScore(nt.get(), k);
-        Tree neg(*models_[m]);
-        neg.Shrinkage(-1.0);
-        learner_->DeviceAddTreeToScore(&neg, k);
         train_score_stale_ = true;
       } else {
-        double* s = train_score_.data() + off;
-        for (data_size_t i = 0; i < num_data_; ++i) s[i] += nt->LeafOutput(leaf_pred[i]) - models_[m]->LeafOutput(leaf_pred[i]);
+        learner_->AddPredictionToScore(nt.get(), train_score_.data() + off);
       }
       models_[m] = std::move(nt);
     }

@@ -3189,8 +3189,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   // Refit on the device (reference cuda_single_gpu_tree_learner.cu:19-78): leaf sums of the
-  // device gradients over the leaf assignment, the host's output formula, and the score
-  // delta of the new outputs applied on the device.
+  // device gradients over the leaf assignment, the host's output formula, and the new
+  // outputs added to the device score.
   std::unique_ptr<Tree> DeviceFitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
                                                 int class_id) override {
     ScopedTimer timer("Device::Refit");
@@ -3223,7 +3223,7 @@ class DeviceTreeLearner : public TreeLearner {
       const double old_v = tree->LeafOutput(i);
       const double new_v = config_->refit_decay_rate * old_v + (1.0 - config_->refit_decay_rate) * out * tree->shrinkage();
       tree->SetLeafOutput(i, new_v);
-      delta[i] = new_v - old_v;
+      delta[i] = new_v;  // the refit score holds only the refit trees so far (GBDT::RefitTree)
     }
     refit_delta_.Upload(delta, stream_);
     LaunchAddLeafDelta(score_.get() + static_cast<size_t>(class_id) * N_, leaf_pred_dev_.get(), refit_delta_.get(), N_,

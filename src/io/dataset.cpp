@@ -637,6 +637,10 @@ void Dataset::SerializeBinary(std::vector<char>* out) const {
   PutVec(&buf, categorical_);
   metadata_.Serialize(&buf);
   PutVec(&buf, bins_);
+  // raw feature values (linear_tree): the reference's binary format stores them too
+  // (dataset.cpp SaveBinaryFile, raw_data_ section)
+  Put(&buf, static_cast<int32_t>(keep_raw_ ? 1 : 0));
+  PutVec(&buf, raw_);
 }
 
 void Dataset::SaveBinary(const std::string& filename) const {
@@ -688,6 +692,10 @@ std::unique_ptr<Dataset> Dataset::DeserializeBinary(const char* data, size_t siz
   d->categorical_ = GetVec<int>(p);
   p += d->metadata_.Deserialize(p);
   d->bins_ = GetVec<uint8_t>(p);
+  if (p < data + size) {
+    d->keep_raw_ = Get<int32_t>(p) != 0;
+    d->raw_ = GetVec<float>(p);
+  }
   return d;
 }
 

@@ -3,6 +3,7 @@
 //   min_b sum_i h_i (g_i/h_i + x_i.b)^2 + linear_lambda |b|^2
 // on the numerical features used on the leaf's branch (Newton step on the
 // second-order approximation), solved by Cholesky.
+#include <algorithm>
 #include <cmath>
 
 #include "lgap/log.h"
@@ -21,6 +22,10 @@ class LinearTreeLearner : public SerialTreeLearner {
     if (!train_data->has_raw()) {
       Log::Fatal("linear_tree requires the Dataset to keep raw feature values (construct it with linear_tree=true)");
     }
+    has_nan_ = false;
+    for (data_size_t i = 0; i < train_data->num_data() && !has_nan_; ++i) {
+      for (int f = 0; f < train_data->num_features() && !has_nan_; ++f) has_nan_ = std::isnan(train_data->raw(i, f));
+    }
   }
 
   std::unique_ptr<Tree> Train(const score_t* g, const score_t* h, bool first) override {
@@ -30,12 +35,77 @@ class LinearTreeLearner : public SerialTreeLearner {
     tree->SetIsLinear(true);
     tree->InitLinear();
     const int nl = tree->num_leaves();
-    for (int l = 0; l < nl; ++l) {
-      FitLeaf(tree.get(), base.get(), l, g, h);
+    if (first) {
+      // the first tree only carries constants (reference CalculateLinear is_first_tree, :184-189)
+      for (int l = 0; l < nl; ++l) tree->SetLeafConst(l, tree->LeafOutput(l));
+      return tree;
     }
-    last_ = std::move(tree);
-    // keep the inner (binned) structure for score updates
-    return std::make_unique<Tree>(*last_);
+#pragma omp parallel for schedule(dynamic) if (nl > 1)
+    for (int l = 0; l < nl; ++l) {
+      const std::vector<int> feats = BranchFeatures(base.get(), l);
+      std::vector<double> z;
+      if (!SolveLeaf(feats, l, g, h, &z)) {
+        tree->SetLeafConst(l, tree->LeafOutput(l));
+        continue;
+      }
+      // coefficients that round to zero are dropped (reference :365-369)
+      std::vector<double> coef;
+      std::vector<int> inner, real;
+      for (size_t j = 0; j < feats.size(); ++j) {
+        if (Tree::IsZero(z[j])) continue;
+        coef.push_back(z[j]);
+        inner.push_back(feats[j]);
+        real.push_back(train_data_->feature(feats[j]).real_index);
+      }
+      tree->SetLeafConst(l, z[feats.size()]);
+      tree->SetLeafCoeffs(l, coef);
+      tree->SetLeafFeatures(l, real);
+      tree->SetLeafFeaturesInner(l, inner);
+    }
+    return tree;
+  }
+
+  // refit: the leaf outputs are refit by the serial learner, then each leaf's linear model
+  // is re-solved on the new rows over the features it already uses and blended with
+  //   new = decay * old + (1 - decay) * solved * shrinkage
+  // (reference FitByExistingTree :136-160 and CalculateLinear is_refit, :330-385). A leaf
+  // with too few usable rows keeps zeroed coefficients and blends its constant towards the
+  // (already refit) leaf output.
+  std::unique_ptr<Tree> FitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
+                                          const score_t* g, const score_t* h) override {
+    auto tree = SerialTreeLearner::FitByExistingTree(old_tree, leaf_pred, g, h);
+    tree->SetIsLinear(true);
+    const double decay = config_->refit_decay_rate, shrink = tree->shrinkage();
+    const int nl = tree->num_leaves();
+#pragma omp parallel for schedule(dynamic) if (nl > 1)
+    for (int l = 0; l < nl; ++l) {
+      std::vector<int> feats;
+      for (int rf : tree->LeafFeatures(l)) {
+        const int f = train_data_->InnerIndex(rf);
+        if (f >= 0 && train_data_->feature(f).bin_type == BinType::Numerical) feats.push_back(f);
+      }
+      std::sort(feats.begin(), feats.end());
+      feats.erase(std::unique(feats.begin(), feats.end()), feats.end());
+      const std::vector<double> old_coef = tree->LeafCoeffs(l);
+      const double old_const = tree->LeafConst(l);
+      std::vector<int> real(feats.size());
+      for (size_t j = 0; j < feats.size(); ++j) real[j] = train_data_->feature(feats[j]).real_index;
+      std::vector<double> z;
+      std::vector<double> coef(feats.size(), 0.0);
+      if (!SolveLeaf(feats, l, g, h, &z)) {
+        tree->SetLeafConst(l, decay * old_const + (1.0 - decay) * tree->LeafOutput(l) * shrink);
+      } else {
+        for (size_t j = 0; j < feats.size(); ++j) {
+          const double o = j < old_coef.size() ? old_coef[j] : 0.0;
+          coef[j] = decay * o + (1.0 - decay) * z[j] * shrink;
+        }
+        tree->SetLeafConst(l, decay * old_const + (1.0 - decay) * z[feats.size()] * shrink);
+      }
+      tree->SetLeafCoeffs(l, coef);
+      tree->SetLeafFeatures(l, real);
+      tree->SetLeafFeaturesInner(l, feats);
+    }
+    return tree;
   }
 
   void AddPredictionToScore(const Tree* tree, double* out) const override {
@@ -62,73 +132,71 @@ class LinearTreeLearner : public SerialTreeLearner {
   }
 
  private:
-  void FitLeaf(Tree* tree, const Tree* base, int leaf, const score_t* g, const score_t* h) {
-    // numerical features on the branch (inner indices)
+  // distinct numerical features split on along the leaf's branch, sorted (inner indices)
+  std::vector<int> BranchFeatures(const Tree* base, int leaf) const {
+    std::vector<int> parent(std::max(1, base->num_leaves() - 1), -1);
+    for (int p = 0; p < base->num_leaves() - 1; ++p) {
+      if (base->left_child(p) >= 0) parent[base->left_child(p)] = p;
+      if (base->right_child(p) >= 0) parent[base->right_child(p)] = p;
+    }
     std::vector<int> feats;
-    int node = base->leaf_parent(leaf);
-    while (node >= 0) {
+    for (int node = base->leaf_parent(leaf); node >= 0; node = parent[node]) {
       const int f = base->split_feature_inner(node);
-      if (train_data_->feature(f).bin_type == BinType::Numerical &&
-          std::find(feats.begin(), feats.end(), f) == feats.end()) {
-        feats.push_back(f);
-      }
-      // walk up
-      int parent = -1;
-      for (int p = 0; p < base->num_leaves() - 1; ++p) {
-        if (base->left_child(p) == node || base->right_child(p) == node) {
-          parent = p;
-          break;
-        }
-      }
-      node = parent;
+      if (train_data_->feature(f).bin_type == BinType::Numerical) feats.push_back(f);
     }
     std::sort(feats.begin(), feats.end());
-    const int k = static_cast<int>(feats.size());
+    feats.erase(std::unique(feats.begin(), feats.end()), feats.end());
+    return feats;
+  }
+
+  // Newton step of the leaf's rows on [x, 1]: z = -(X'HX + lambda I_x)^-1 X'g (reference
+  // CalculateLinear :191-356; Eq. 3 of arXiv:1802.05640). Rows with a NaN in any of the
+  // features are left out. False when fewer usable rows than unknowns or the system is not
+  // positive definite.
+  bool SolveLeaf(const std::vector<int>& feats, int leaf, const score_t* g, const score_t* h,
+                 std::vector<double>* out) const {
+    const int k = static_cast<int>(feats.size()), m = k + 1;
     const data_size_t n = partition_.count(leaf);
     const data_size_t* idx = partition_.indices(leaf);
-    // normal equations of [x, 1]
-    const int m = k + 1;
-    std::vector<double> A(static_cast<size_t>(m) * m, 0.0), b(m, 0.0);
-    std::vector<double> x(m);
+    std::vector<double> A(static_cast<size_t>(m) * m, 0.0), b(m, 0.0), x(m);
+    // "enough data" follows the reference's count (CalculateLinear :266-324): with NaNs in
+    // the dataset it counts the non-NaN values read (so a leaf without features never has
+    // enough and keeps its constant output), otherwise the leaf's rows
+    int64_t usable = has_nan_ ? 0 : n;
     for (data_size_t i = 0; i < n; ++i) {
       bool nan = false;
-      for (int j = 0; j < k; ++j) {
+      for (int j = 0; j < k && !nan; ++j) {
         x[j] = train_data_->raw(idx[i], feats[j]);
-        if (std::isnan(x[j])) nan = true;
+        nan = std::isnan(x[j]);
+        if (has_nan_ && !nan) ++usable;
       }
       if (nan) continue;
       x[k] = 1.0;
       const double hh = h[idx[i]], gg = g[idx[i]];
       for (int a = 0; a < m; ++a) {
         b[a] -= gg * x[a];
-        for (int c = 0; c < m; ++c) A[a * m + c] += hh * x[a] * x[c];
+        const double hx = hh * x[a];
+        for (int c = 0; c <= a; ++c) A[a * m + c] += hx * x[c];
       }
     }
+    if (usable < m) return false;
     for (int j = 0; j < k; ++j) A[j * m + j] += config_->linear_lambda;
-    // Cholesky solve (A is SPD after ridge; fall back to constant leaf on failure)
+    // Cholesky on the lower triangle
     std::vector<double> L(A.size(), 0.0);
-    bool ok = true;
-    for (int i = 0; i < m && ok; ++i) {
+    for (int i = 0; i < m; ++i) {
       for (int j = 0; j <= i; ++j) {
         double s = A[i * m + j];
         for (int t = 0; t < j; ++t) s -= L[i * m + t] * L[j * m + t];
         if (i == j) {
-          if (s <= 1e-12) ok = false;
-          else L[i * m + i] = std::sqrt(s);
+          if (!(s > 1e-12)) return false;
+          L[i * m + i] = std::sqrt(s);
         } else {
           L[i * m + j] = s / L[j * m + j];
         }
       }
     }
-    const double shrink = config_->learning_rate;
-    if (!ok || n < m) {
-      tree->SetLeafConst(leaf, base->LeafOutput(leaf));
-      tree->SetLeafCoeffs(leaf, {});
-      tree->SetLeafFeatures(leaf, {});
-      tree->SetLeafFeaturesInner(leaf, {});
-      return;
-    }
-    std::vector<double> y(m), z(m);
+    std::vector<double> y(m);
+    out->assign(m, 0.0);
     for (int i = 0; i < m; ++i) {
       double s = b[i];
       for (int t = 0; t < i; ++t) s -= L[i * m + t] * y[t];
@@ -136,19 +204,12 @@ class LinearTreeLearner : public SerialTreeLearner {
     }
     for (int i = m - 1; i >= 0; --i) {
       double s = y[i];
-      for (int t = i + 1; t < m; ++t) s -= L[t * m + i] * z[t];
-      z[i] = s / L[i * m + i];
+      for (int t = i + 1; t < m; ++t) s -= L[t * m + i] * (*out)[t];
+      (*out)[i] = s / L[i * m + i];
     }
-    (void)shrink;
-    std::vector<double> coef(z.begin(), z.begin() + k);
-    std::vector<int> real(k);
-    for (int j = 0; j < k; ++j) real[j] = train_data_->feature(feats[j]).real_index;
-    tree->SetLeafConst(leaf, z[k]);
-    tree->SetLeafCoeffs(leaf, coef);
-    tree->SetLeafFeatures(leaf, real);
-    tree->SetLeafFeaturesInner(leaf, feats);
+    return true;
   }
-  std::unique_ptr<Tree> last_;
+  bool has_nan_ = false;
 };
 
 }  // namespace

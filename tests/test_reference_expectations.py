@@ -1528,3 +1528,129 @@ def test_extra_trees_and_path_smoothing_regularise(lgb, extra):
     err = mean_squared_error(y, lgb.train(params, lgb.Dataset(X, label=y), 10).predict(X))
     err2 = mean_squared_error(y, lgb.train(dict(params, **extra), lgb.Dataset(X, label=y), 10).predict(X))
     assert err < err2
+
+
+# ---------------------------------------------------------------------------
+# trees_to_dataframe, interaction constraints, linear trees (test_engine.py:3601-3860)
+def test_trees_to_dataframe_matches_importances(lgb):
+    """test_trees_to_dataframe."""
+    pytest.importorskip("pandas")
+    X, y = load_breast_cancer(return_X_y=True)
+    b = lgb.train({"objective": "binary", "verbose": -1}, lgb.Dataset(X, label=y), 10)
+    df = b.trees_to_dataframe()
+    cols = [f"Column_{i}" for i in range(X.shape[1])]
+    split = df[~df["split_gain"].isnull()].groupby("split_feature").size().to_dict()
+    gains = df.groupby("split_feature")["split_gain"].sum().to_dict()
+    np.testing.assert_equal([split.get(c, 0.0) for c in cols], b.feature_importance("split"))
+    np.testing.assert_allclose([gains.get(c, 0.0) for c in cols], b.feature_importance("gain"))
+    assert df["tree_index"].nunique() == 10
+    np.testing.assert_equal(df.loc[df["node_depth"] == 1, "count"].values, len(y))
+    b = lgb.train({"objective": "binary", "verbose": -1},
+                  lgb.Dataset(np.ones((10, 2)), label=np.random.default_rng(1).uniform(size=(10,))), 10)
+    df = b.trees_to_dataframe()
+    assert len(df) == 1
+    assert df.loc[0, "tree_index"] == 0 and df.loc[0, "node_depth"] == 1 and df.loc[0, "node_index"] == "0-L0"
+    assert df.loc[0, "value"] is not None
+    for c in ("left_child", "right_child", "parent_index", "split_feature", "split_gain", "threshold",
+              "decision_type", "missing_direction", "missing_type", "weight", "count"):
+        assert df.loc[0, c] is None, c
+
+
+def test_interaction_constraints_accuracy_ordering(lgb):
+    """test_interaction_constraints."""
+    X, y = make_regression(n_samples=200, n_features=4, n_informative=2, random_state=42)
+    ds = lgb.Dataset(X, label=y)
+    params = {"verbose": -1, "seed": 0}
+    p1 = lgb.train(params, ds, 10).predict(X)
+    np.testing.assert_allclose(p1, lgb.train(dict(params, interaction_constraints=[list(range(4))]), ds, 10).predict(X))
+    p3 = lgb.train(dict(params, interaction_constraints=[[0, 2], [1, 3]]), ds, 10).predict(X)
+    assert mean_squared_error(y, p1) < mean_squared_error(y, p3)
+    p4 = lgb.train(dict(params, interaction_constraints=[[i] for i in range(4)]), ds, 10).predict(X)
+    assert mean_squared_error(y, p3) < mean_squared_error(y, p4)
+    X2 = np.concatenate([np.zeros((X.shape[0], 1)), X], axis=1)
+    lgb.train(dict(params, interaction_constraints=[[0] + list(range(2, 5)), [1] + list(range(2, 5))]),
+              lgb.Dataset(X2, label=y), 10)
+
+
+def test_linear_trees_thread_independent(lgb):
+    """test_linear_trees_num_threads."""
+    rng = np.random.default_rng(42)
+    x = np.arange(0, 1000, 0.1)
+    y = 2 * x + rng.normal(0, 0.1, size=(len(x),))
+    params = {"verbose": -1, "objective": "regression", "seed": 0, "linear_tree": True, "num_threads": 2}
+    p1 = lgb.train(params, lgb.Dataset(x[:, None], label=y), 100).predict(x[:, None])
+    p2 = lgb.train(dict(params, num_threads=4), lgb.Dataset(x[:, None], label=y), 100).predict(x[:, None])
+    np.testing.assert_allclose(p1, p2)
+
+
+def test_linear_trees_fit_and_refit(lgb, tmp_path):
+    """test_linear_trees."""
+    rng = np.random.default_rng(42)
+    x = np.arange(0, 100, 0.1)
+    y = 2 * x + rng.normal(0, 0.1, len(x))
+    x = x[:, None]
+    params = {"verbose": -1, "metric": "mse", "seed": 0, "num_leaves": 2}
+
+    def compare(xx, extra=None):
+        p1 = lgb.train(params, lgb.Dataset(xx, label=y), 10).predict(xx)
+        res = {}
+        d = lgb.Dataset(xx, label=y)
+        est = lgb.train(dict(params, linear_tree=True, **(extra or {})), d, 10, valid_sets=[d], valid_names=["train"],
+                        callbacks=[lgb.record_evaluation(res)])
+        p2 = est.predict(xx)
+        assert res["train"]["l2"][-1] == pytest.approx(mean_squared_error(y, p2), abs=1e-1)
+        return p1, p2
+
+    p1, p2 = compare(x)
+    assert mean_squared_error(y, p2) < mean_squared_error(y, p1)
+    x[:10] = np.nan
+    p1, p2 = compare(x)
+    assert mean_squared_error(y, p2) < mean_squared_error(y, p1)
+    compare(x, {"subsample": 0.8, "bagging_freq": 1})
+    x = np.concatenate([np.ones([x.shape[0], 1]), x], 1)
+    x[500:, 1] = np.nan
+    y[500:] += 10
+    compare(x, {"subsample": 0.8, "bagging_freq": 1})
+    x[:250, 0] = 0
+    y[:250] += 10
+    est = lgb.train(dict(params, linear_tree=True, subsample=0.8, bagging_freq=1),
+                    lgb.Dataset(x, label=y, categorical_feature=[0]), 10)
+    p1 = est.predict(x)
+    assert np.mean(np.abs(p1 - est.refit(x, label=y).predict(x))) < 2
+    est.save_model(str(tmp_path / "temp_model.txt"))
+    p2 = lgb.Booster(model_file=str(tmp_path / "temp_model.txt")).refit(x, label=y).predict(x)
+    assert np.mean(np.abs(p1 - p2)) < 2
+    p3 = est.refit(x[:100, :], label=y[:100]).predict(x)
+    assert np.mean(np.abs(p2 - p1)) > np.abs(np.max(p3 - p1))
+    X_tr, _, y_tr, _ = train_test_split(*load_breast_cancer(return_X_y=True), test_size=0.1, random_state=2)
+    prm = {"linear_tree": True, "verbose": -1, "metric": "mse", "seed": 0}
+    for nl in (2, 60):
+        lgb.train(prm, lgb.Dataset(X_tr, label=y_tr, params=dict(prm, num_leaves=nl), categorical_feature=[0]), 10)
+
+
+def test_linear_trees_save_load(lgb, tmp_path):
+    """test_save_and_load_linear."""
+    X_tr, _, y_tr, _ = train_test_split(*load_breast_cancer(return_X_y=True), test_size=0.1, random_state=2)
+    X_tr = np.concatenate([np.ones((X_tr.shape[0], 1)), X_tr], 1)
+    X_tr[: X_tr.shape[0] // 2, 0] = 0
+    y_tr[: X_tr.shape[0] // 2] = 1
+    params = {"linear_tree": True}
+    d1 = lgb.Dataset(X_tr, label=y_tr, params=params, categorical_feature=[0])
+    p1 = lgb.train(params, d1, 10).predict(X_tr)
+    d1.save_binary(str(tmp_path / "temp_dataset.bin"))
+    e2 = lgb.train(params, lgb.Dataset(str(tmp_path / "temp_dataset.bin")), 10)
+    np.testing.assert_allclose(p1, e2.predict(X_tr))
+    e2.save_model(str(tmp_path / "model.txt"))
+    np.testing.assert_allclose(e2.predict(X_tr), lgb.Booster(model_file=str(tmp_path / "model.txt")).predict(X_tr))
+
+
+def test_linear_single_leaf_and_unsupported_params(lgb):
+    """test_linear_single_leaf, test_linear_raises_informative_errors_on_unsupported_params."""
+    X, y = load_breast_cancer(return_X_y=True)
+    b = lgb.train({"objective": "binary", "linear_tree": True, "min_sum_hessian": 5000}, lgb.Dataset(X, label=y), 5)
+    assert log_loss(y, b.predict(X)) < 0.661
+    Xr, yr = make_regression(n_samples=100, n_features=4, n_informative=2, random_state=42)
+    with pytest.raises(lgb.basic.LightGBMError, match="Cannot use regression_l1 objective when fitting linear trees"):
+        lgb.train({"linear_tree": True, "objective": "regression_l1"}, lgb.Dataset(Xr, label=yr), 1)
+    with pytest.raises(lgb.basic.LightGBMError, match="zero_as_missing must be false when fitting linear trees"):
+        lgb.train({"linear_tree": True, "zero_as_missing": True}, lgb.Dataset(Xr, label=yr), 1)
