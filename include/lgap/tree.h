@@ -54,6 +54,16 @@ class Tree {
   void Shrinkage(double rate);
   void AddBias(double val);
   void SetLeafOutput(int leaf, double v) { leaf_value_[leaf] = MaybeRoundToZero(v); }
+  // a one-leaf tree holding `count` rows (reference tree.h AsConstantTree)
+  void AsConstantTree(double v, int count, bool linear) {
+    SetLeafOutput(0, v);
+    leaf_count_[0] = count;
+    if (linear) {
+      is_linear_ = true;
+      InitLinear();
+      SetLeafConst(0, v);
+    }
+  }
   void SetShrinkage(double s) { shrinkage_ = s; }
   void RecomputeMaxDepth();
   void RecomputeLeafDepths();

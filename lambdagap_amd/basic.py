@@ -1174,6 +1174,10 @@ class Booster:
                 os.unlink(tmp)
             return res[:, 0] if res.shape[1] == 1 else res
         if _is_pandas(data):
+            if validate_features:
+                names = [str(c) for c in data.columns]
+                arr = (ctypes.c_char_p * len(names))(*[n.encode("utf-8") for n in names])
+                _check(_LIB.LGBM_BoosterValidateFeatureNames(self.handle, arr, ctypes.c_int(len(names))))
             data = _pandas_to_numpy(data, "auto", self.pandas_categorical)[0]
         if _is_arrow(data):
             nrow = data.num_rows
@@ -1277,7 +1281,8 @@ class Booster:
         if nrow == 0:
             return out
         per = out.size // nrow
-        if per == 1:
+        # leaf indices and contributions are always (nrow, k) (reference _InnerPredictor)
+        if per == 1 and ptype not in (C_API_PREDICT_LEAF_INDEX, C_API_PREDICT_CONTRIB):
             return out
         res = out.reshape(nrow, per)
         if ptype == C_API_PREDICT_LEAF_INDEX:
@@ -1345,8 +1350,9 @@ class Booster:
 
     def refit(self, data: Any, label: Any, decay_rate: float = 0.9, reference: Optional[Dataset] = None,
               weight: Any = None, group: Any = None, init_score: Any = None, dataset_params: Optional[Dict] = None,
-              free_raw_data: bool = True, **kwargs: Any) -> "Booster":
-        leaf_preds = self.predict(data, start_iteration=0, num_iteration=-1, pred_leaf=True)
+              free_raw_data: bool = True, validate_features: bool = False, **kwargs: Any) -> "Booster":
+        leaf_preds = self.predict(data, start_iteration=0, num_iteration=-1, pred_leaf=True,
+                                  validate_features=validate_features)
         nrow = leaf_preds.shape[0]
         leaf_preds = np.ascontiguousarray(leaf_preds.reshape(nrow, -1), dtype=np.int32)
         params = dict(self.params)

@@ -68,6 +68,8 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
     """Train a booster for ``num_boost_round`` rounds."""
     if not isinstance(train_set, Dataset):
         raise TypeError(f"train() only accepts Dataset object, train_set has type '{type(train_set).__name__}'.")
+    if num_boost_round <= 0:
+        raise ValueError(f"Number of boosting rounds must be greater than 0. Got {num_boost_round}.")
     if isinstance(valid_sets, Dataset):
         valid_sets = [valid_sets]
     if isinstance(valid_names, str):
@@ -86,8 +88,6 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
         fobj = obj
         params["objective"] = "none"
     params, num_boost_round = _pop_num_rounds(params, num_boost_round)
-    if num_boost_round <= 0:
-        raise ValueError("num_boost_round should be greater than zero.")
     es_rounds, first_only, min_delta = _early_stop_params(params)
     if feature_name != "auto":
         train_set.feature_name = feature_name
@@ -154,7 +154,9 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
     for item in evaluation_result_list:
         booster.best_score[item[0]][item[1]] = item[2]
     if not keep_training_booster:
-        booster.free_dataset()
+        # the returned model is the saved one: trees past best_iteration are dropped
+        # (reference engine.py train: model_from_string(model_to_string()))
+        booster.model_from_string(booster.model_to_string()).free_dataset()
     return booster
 
 
@@ -270,14 +272,15 @@ def _make_folds(full: Dataset, folds, nfold: int, params: Dict[str, Any], seed: 
 
 
 def _agg_cv_result(raw_results: List[List[Tuple[str, str, float, bool]]]):
-    cvmap: Dict[str, List[float]] = OrderedDict()
-    metric_type: Dict[str, bool] = {}
+    """(dataset, metric, mean, is_higher_better, stdv) per (dataset, metric) over the folds
+    (reference engine.py _agg_cv_result)."""
+    values: Dict[Tuple[str, str], List[float]] = OrderedDict()
+    higher: Dict[Tuple[str, str], bool] = {}
     for one in raw_results:
-        for one_line in one:
-            key = f"{one_line[0]} {one_line[1]}"
-            metric_type[key] = one_line[3]
-            cvmap.setdefault(key, []).append(one_line[2])
-    return [("cv_agg", k, float(np.mean(v)), metric_type[k], float(np.std(v))) for k, v in cvmap.items()]
+        for data_name, metric, value, hib in one:
+            higher[(data_name, metric)] = hib
+            values.setdefault((data_name, metric), []).append(value)
+    return [(k[0], k[1], float(np.mean(v)), higher[k], float(np.std(v))) for k, v in values.items()]
 
 
 def cv(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100, folds=None, nfold: int = 5,
@@ -288,6 +291,8 @@ def cv(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100, f
     """k-fold cross validation; returns {"valid <metric>-mean": [...], "valid <metric>-stdv": [...]}."""
     if not isinstance(train_set, Dataset):
         raise TypeError(f"cv() only accepts Dataset object, train_set has type '{type(train_set).__name__}'.")
+    if num_boost_round <= 0:
+        raise ValueError(f"Number of boosting rounds must be greater than 0. Got {num_boost_round}.")
     params = copy.deepcopy(params) if params else {}
     fobj = None
     if callable(params.get("objective")):
@@ -328,9 +333,9 @@ def cv(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100, f
             b.update(fobj=fobj)
             raw.append(b.eval_valid(feval))
         res = _agg_cv_result(raw)
-        for _, key, mean, _, std in res:
-            results[f"{key}-mean"].append(mean)
-            results[f"{key}-stdv"].append(std)
+        for data_name, metric, mean, _, std in res:
+            results[f"{data_name} {metric}-mean"].append(mean)
+            results[f"{data_name} {metric}-stdv"].append(std)
         try:
             for c in after:
                 c(cb.CallbackEnv(model=cvfolds, params=params, iteration=i, begin_iteration=0,

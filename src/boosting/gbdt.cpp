@@ -28,10 +28,9 @@ double AutomaticInitScore(const ObjectiveFunction* obj, int class_id) {
   if (Network::num_machines() > 1) v = Network::GlobalSyncUpByMean(v);
   return v;
 }
-std::unique_ptr<Tree> ConstantTree(double v, data_size_t n) {
+std::unique_ptr<Tree> ConstantTree(double v, data_size_t n, bool linear) {
   auto t = std::make_unique<Tree>(2);
-  t->SetLeafOutput(0, v);
-  (void)n;
+  t->AsConstantTree(v, n, linear);
   return t;
 }
 }  // namespace
@@ -328,9 +327,9 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
           init_scores[k] = AutomaticInitScore(objective_, k);
           AddScoreConstant(init_scores[k], k);
         }
-        tree = ConstantTree(init_scores[k], num_data_);
+        tree = ConstantTree(init_scores[k], num_data_, config_->linear_tree);
       } else {
-        tree = ConstantTree(0.0, num_data_);
+        tree = ConstantTree(0.0, num_data_, config_->linear_tree);
       }
     }
     models_.push_back(std::move(tree));
@@ -603,15 +602,19 @@ void DART::Init(const Config* config, const Dataset* train_data, const Objective
 
 void DART::DroppingTrees() {
   drop_index_.clear();
+  // only this session's iterations are dropped; merged init-model trees stay fixed
+  // (dart.hpp DroppingTrees: num_init_iteration_ + i)
+  const int init_iter = num_init_models_ / num_tree_per_iteration_;
   const bool skip = random_for_drop_.NextFloat() < config_->skip_drop;
   if (!skip) {
     double rate = config_->drop_rate;
     if (!config_->uniform_drop) {
       const double inv_avg = static_cast<double>(tree_weight_.size()) / sum_weight_;
       if (config_->max_drop > 0) rate = std::min(rate, config_->max_drop * inv_avg / sum_weight_);
-      for (int i = 0; i < iter_; ++i) {
+      const int n = std::min(iter_, static_cast<int>(tree_weight_.size()));
+      for (int i = 0; i < n; ++i) {
         if (random_for_drop_.NextFloat() < rate * tree_weight_[i] * inv_avg) {
-          drop_index_.push_back(i);
+          drop_index_.push_back(init_iter + i);
           if (drop_index_.size() >= static_cast<size_t>(config_->max_drop)) break;
         }
       }
@@ -619,7 +622,7 @@ void DART::DroppingTrees() {
       if (config_->max_drop > 0) rate = std::min(rate, config_->max_drop / static_cast<double>(iter_));
       for (int i = 0; i < iter_; ++i) {
         if (random_for_drop_.NextFloat() < rate) {
-          drop_index_.push_back(i);
+          drop_index_.push_back(init_iter + i);
           if (drop_index_.size() >= static_cast<size_t>(config_->max_drop)) break;
         }
       }
@@ -658,12 +661,13 @@ void DART::Normalize() {
       t->AddPredictionToScore(*train_data_, num_data_, train_score_.data() + static_cast<size_t>(c) * num_data_);
     }
     if (!config_->uniform_drop) {
+      const int w = i - num_init_models_ / num_tree_per_iteration_;
       if (!config_->xgboost_dart_mode) {
-        sum_weight_ -= tree_weight_[i] * (1.0 / (k + 1.0));
-        tree_weight_[i] *= (k / (k + 1.0));
+        sum_weight_ -= tree_weight_[w] * (1.0 / (k + 1.0));
+        tree_weight_[w] *= (k / (k + 1.0));
       } else {
-        sum_weight_ -= tree_weight_[i] * (1.0 / (k + config_->learning_rate));
-        tree_weight_[i] *= (k / (k + config_->learning_rate));
+        sum_weight_ -= tree_weight_[w] * (1.0 / (k + config_->learning_rate));
+        tree_weight_[w] *= (k / (k + config_->learning_rate));
       }
     }
   }
@@ -750,7 +754,7 @@ bool RF::TrainOneIter(const score_t*, const score_t*) {
     } else if (models_.size() < static_cast<size_t>(num_tree_per_iteration_)) {
       double out = 0.0;
       if (!class_need_train_[k]) out = objective_->BoostFromScore(k);
-      tree = ConstantTree(out, num_data_);
+      tree = ConstantTree(out, num_data_, config_->linear_tree);
       mult(k, iter_);
       UpdateScore(tree.get(), k);
       mult(k, 1.0 / (iter_ + 1));

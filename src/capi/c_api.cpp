@@ -188,8 +188,12 @@ class Booster {
     if (pm.count("num_class") && common::AtoiOrDie(pm["num_class"]) != config_.num_class) {
       Log::Fatal("Cannot change num_class during training");
     }
-    if (pm.count("boosting") && pm["boosting"] != config_.boosting) Log::Fatal("Cannot change boosting during training");
-    if (pm.count("metric")) Log::Fatal("Cannot change metric during training");
+    // compared after parsing, so restating the current values is allowed (reference
+    // c_api.cpp Booster::ResetConfig)
+    Config next = config_;
+    next.Set(pm);
+    if (pm.count("boosting") && next.boosting != config_.boosting) Log::Fatal("Cannot change boosting during training");
+    if (pm.count("metric") && next.metric != config_.metric) Log::Fatal("Cannot change metric during training");
     config_.Set(pm);
     SetDefaultNumThreads(config_.num_threads);
     if (pm.count("objective")) {

@@ -2,6 +2,8 @@
 // flags and conflict resolution. Behaviour mirrors src/io/config.cpp of the
 // reference; the tables are generated from config_params.def instead of a
 // separate code generator.
+#include <limits>
+#include <map>
 #include "lgap/config.h"
 
 #include <algorithm>
@@ -112,28 +114,51 @@ void Config::KV2Map(std::unordered_map<std::string, std::vector<std::string>>* p
   (*params)[key].push_back(value);
 }
 
+// Reference config.h ParameterAlias::KeyAliasTransform: among several aliases of one
+// parameter the shortest (then alphabetically first) name wins; a canonical name wins over
+// any alias. Every loser is reported.
 void Config::KeyAliasTransform(ParamMap* params) {
   const auto& alias = AliasTable();
+  auto sort_alias = [](const std::string& x, const std::string& y) {
+    return x.size() < y.size() || (x.size() == y.size() && x < y);
+  };
+  std::vector<std::string> keys;
+  for (auto& kv : *params) keys.push_back(kv.first);
+  std::sort(keys.begin(), keys.end());
+  std::map<std::string, std::string> chosen;  // canonical -> winning alias key
+  for (const auto& k : keys) {
+    auto it = alias.find(k);
+    if (it == alias.end()) {
+      if (!IsKnownParameter(k)) Log::Warning("Unknown parameter: %s", k.c_str());
+      continue;
+    }
+    auto c = chosen.find(it->second);
+    if (c == chosen.end()) {
+      chosen.emplace(it->second, k);
+    } else if (sort_alias(c->second, k)) {
+      Log::Warning("%s is set with %s=%s, %s=%s will be ignored. Current value: %s=%s", it->second.c_str(),
+                   c->second.c_str(), params->at(c->second).c_str(), k.c_str(), params->at(k).c_str(),
+                   it->second.c_str(), params->at(c->second).c_str());
+    } else {
+      Log::Warning("%s is set with %s=%s, will be overridden by %s=%s. Current value: %s=%s", it->second.c_str(),
+                   c->second.c_str(), params->at(c->second).c_str(), k.c_str(), params->at(k).c_str(),
+                   it->second.c_str(), params->at(k).c_str());
+      c->second = k;
+    }
+  }
   ParamMap out;
-  // canonical names first, so that they win over aliases
   for (auto& kv : *params) {
     if (alias.count(kv.first) == 0) out[kv.first] = kv.second;
   }
-  for (auto& kv : *params) {
-    auto it = alias.find(kv.first);
-    if (it == alias.end()) continue;
-    if (out.count(it->second)) {
-      if (out[it->second] != kv.second) {
-        Log::Warning("%s is set with %s=%s, %s=%s will be ignored. Current value: %s=%s", it->second.c_str(),
-                     it->second.c_str(), out[it->second].c_str(), kv.first.c_str(), kv.second.c_str(),
-                     it->second.c_str(), out[it->second].c_str());
-      }
+  for (auto& kv : chosen) {
+    auto canon = out.find(kv.first);
+    if (canon == out.end()) {
+      out[kv.first] = params->at(kv.second);
     } else {
-      out[it->second] = kv.second;
+      Log::Warning("%s is set=%s, %s=%s will be ignored. Current value: %s=%s", kv.first.c_str(),
+                   canon->second.c_str(), kv.second.c_str(), params->at(kv.second).c_str(), kv.first.c_str(),
+                   canon->second.c_str());
     }
-  }
-  for (auto& kv : out) {
-    if (!IsKnownParameter(kv.first)) Log::Warning("Unknown parameter: %s", kv.first.c_str());
   }
   *params = std::move(out);
 }
@@ -141,8 +166,26 @@ void Config::KeyAliasTransform(ParamMap* params) {
 ParamMap Config::Str2Map(const char* parameters) {
   std::unordered_map<std::string, std::vector<std::string>> all;
   for (auto& arg : common::SplitAny(parameters ? parameters : "", " \t\n\r")) KV2Map(&all, arg.c_str());
+  // the log level follows verbose / verbosity before any alias is reported (reference
+  // config.cpp SetVerbosity: verbosity over verbose)
+  int verbosity = Config().verbosity;
+  for (const char* key : {"verbose", "verbosity"}) {
+    auto it = all.find(key);
+    if (it != all.end()) verbosity = std::atoi(it->second[0].c_str());
+  }
+  if (verbosity < 0) Log::ResetLevel(LogLevel::Fatal);
+  else if (verbosity == 0) Log::ResetLevel(LogLevel::Warning);
+  else if (verbosity == 1) Log::ResetLevel(LogLevel::Info);
+  else Log::ResetLevel(LogLevel::Debug);
   ParamMap params;
-  for (auto& kv : all) params[kv.first] = kv.second[0];
+  for (auto& kv : all) {
+    params[kv.first] = kv.second[0];
+    for (size_t i = 1; i < kv.second.size(); ++i) {
+      Log::Warning("%s is set=%s, %s=%s will be ignored. Current value: %s=%s", kv.first.c_str(),
+                   kv.second[0].c_str(), kv.first.c_str(), kv.second[i].c_str(), kv.first.c_str(),
+                   kv.second[0].c_str());
+    }
+  }
   KeyAliasTransform(&params);
   return params;
 }
@@ -177,6 +220,33 @@ std::string ParseMetricAlias(const std::string& t) {
   return it == m.end() ? t : it->second;
 }
 
+namespace {
+// typed parameter values must be the whole string (reference config.h GetInt / GetDouble)
+double ParseDblParam(const char* name, const std::string& v) {
+  const std::string t = common::Trim(v);
+  char* end = nullptr;
+  const double d = std::strtod(t.c_str(), &end);
+  if (t.empty() || *end != '\0') {
+    const std::string l = common::ToLower(t);
+    if (l == "inf" || l == "+inf" || l == "infinity") return std::numeric_limits<double>::infinity();
+    if (l == "-inf" || l == "-infinity") return -std::numeric_limits<double>::infinity();
+    Log::Fatal("Parameter %s should be of type double, got \"%s\"", name, v.c_str());
+  }
+  return d;
+}
+int ParseIntParam(const char* name, const std::string& v) {
+  const std::string t = common::Trim(v);
+  char* end = nullptr;
+  const long long i = std::strtoll(t.c_str(), &end, 10);
+  if (!t.empty() && *end == '\0') return static_cast<int>(i);
+  const double d = std::strtod(t.c_str(), &end);  // integral spellings such as 1e3 or 31.0
+  if (t.empty() || *end != '\0' || d != std::floor(d)) {
+    Log::Fatal("Parameter %s should be of type int, got \"%s\"", name, v.c_str());
+  }
+  return static_cast<int>(d);
+}
+}  // namespace
+
 void Config::GetMembersFromString(const ParamMap& params) {
   auto get = [&](const char* n, std::string* v) {
     auto it = params.find(n);
@@ -187,9 +257,9 @@ void Config::GetMembersFromString(const ParamMap& params) {
   std::string v;
 #define LGAP_PARSE_STR(name, check) if (get(#name, &v)) name = v;
 #define LGAP_PARSE_INT(name, check) \
-  if (get(#name, &v) && !v.empty()) { name = static_cast<int>(common::AtofOrDie(v)); CheckRange(#name, name, check); }
+  if (get(#name, &v) && !v.empty()) { name = ParseIntParam(#name, v); CheckRange(#name, name, check); }
 #define LGAP_PARSE_DBL(name, check) \
-  if (get(#name, &v) && !v.empty()) { name = common::AtofOrDie(v); CheckRange(#name, name, check); }
+  if (get(#name, &v) && !v.empty()) { name = ParseDblParam(#name, v); CheckRange(#name, name, check); }
 #define LGAP_PARSE_BOOL(name, check) if (get(#name, &v)) name = ParseBool(#name, v);
 #define LGAP_PARSE_VSTR(name, check) if (get(#name, &v)) name = common::Split(v, ',');
 #define LGAP_PARSE_VINT(name, check) if (get(#name, &v)) name = ParseNumVec<int>(v);

@@ -19,7 +19,7 @@ class LinearTreeLearner : public SerialTreeLearner {
 
   void Init(const Dataset* train_data, bool is_constant_hessian) override {
     SerialTreeLearner::Init(train_data, is_constant_hessian);
-    if (!train_data->has_raw()) {
+    if (!train_data->has_raw() && train_data->num_features() > 0) {
       Log::Fatal("linear_tree requires the Dataset to keep raw feature values (construct it with linear_tree=true)");
     }
     has_nan_ = false;

@@ -469,9 +469,12 @@ std::unique_ptr<Tree> SerialTreeLearner::Train(const score_t* gradients, const s
     smaller_.output = tree->LeafOutput(0);
   }
   int left = 0, right = -1;
+  forced_rescored_ = false;
   int init_splits = ForceSplits(tree.get(), &left, &right);
   for (int s = init_splits; s < config_->num_leaves - 1; ++s) {
-    if (BeforeFindBestSplit(tree.get(), left, right)) FindBestSplits(tree.get());
+    // after forced splits every leaf already has its best split (ForceSplits rescored them)
+    if (forced_rescored_) forced_rescored_ = false;
+    else if (BeforeFindBestSplit(tree.get(), left, right)) FindBestSplits(tree.get());
     int best = 0;
     for (int l = 1; l < tree->num_leaves(); ++l) {
       if (best_split_per_leaf_[l].BetterThan(best_split_per_leaf_[best])) best = l;
@@ -914,6 +917,7 @@ int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf) 
     best_split_per_leaf_[l] = best;
   }
   // the main loop resumes with no pending histograms to build
+  forced_rescored_ = true;
   *left_leaf = 0;
   *right_leaf = -1;
   smaller_.leaf = 0;

@@ -163,6 +163,7 @@ class SerialTreeLearner : public TreeLearner {
   std::unique_ptr<device::HistogramBackend> hist_backend_;
   bool want_device_hist_ = false;
   std::string forced_json_;
+  bool forced_rescored_ = false;  // ForceSplits left every leaf's best split current
   std::vector<Random> extra_rands_;
   // parallel learners
   std::vector<char> feature_mask_;       // features scanned by this rank

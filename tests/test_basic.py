@@ -201,7 +201,7 @@ def test_free_raw_data_and_reference_alignment(lgb, rng):
     y = rng.random(500)
     ds = lgb.Dataset(X, y)
     dv = ds.create_valid(X[:100], y[:100])
-    b = lgb.train({"verbosity": -1}, ds, 3, valid_sets=[dv])
+    b = lgb.train({"verbosity": -1}, ds, 3, valid_sets=[dv], keep_training_booster=True)
     assert ds.data is None
     assert b.eval_valid()[0][0] == "valid_0"
 

@@ -1654,3 +1654,494 @@ def test_linear_single_leaf_and_unsupported_params(lgb):
         lgb.train({"linear_tree": True, "objective": "regression_l1"}, lgb.Dataset(Xr, label=yr), 1)
     with pytest.raises(lgb.basic.LightGBMError, match="zero_as_missing must be false when fitting linear trees"):
         lgb.train({"linear_tree": True, "zero_as_missing": True}, lgb.Dataset(Xr, label=yr), 1)
+
+
+# ---------------------------------------------------------------------------------------------
+# prediction ranges / shapes, dump_model, sampling strategies, verbosity, informative errors
+
+
+def _synth(n_samples=100, n_features=4, n_informative=2, random_state=42):
+    """tests/python_package_test/utils.py make_synthetic_regression."""
+    return make_regression(n_samples=n_samples, n_features=n_features, n_informative=n_informative,
+                           random_state=random_state)
+
+
+def _assert_silent(capsys):
+    out = capsys.readouterr()
+    assert out.out == "" and out.err == "", out
+
+
+@pytest.mark.parametrize("case", ["regression", "multiclass", "binary"])
+@pytest.mark.parametrize("es_rounds", [1, 5, None])
+def test_predict_with_start_iteration(lgb, case, es_rounds):
+    """test_predict_with_start_iteration: sums of iteration windows equal the whole model."""
+    from sklearn.datasets import load_iris
+    if case == "regression":
+        X, y = _synth()
+        params = {"objective": "regression", "verbose": -1, "metric": "l2", "learning_rate": 0.5}
+    elif case == "multiclass":
+        X, y = load_iris(return_X_y=True)
+        params = {"objective": "multiclass", "num_class": 3, "verbose": -1, "metric": "multi_error"}
+    else:
+        X, y = load_breast_cancer(return_X_y=True)
+        params = {"objective": "binary", "verbose": -1, "metric": "auc"}
+    X_tr, X_te, y_tr, y_te = _split(X, y)
+    cbs = [lgb.early_stopping(es_rounds, verbose=False)] if es_rounds is not None else []
+    b = lgb.train(params, lgb.Dataset(X_tr, label=y_tr), num_boost_round=50,
+                  valid_sets=[lgb.Dataset(X_te, label=y_te)], callbacks=cbs)
+    all_pred = b.predict(X, raw_score=True)
+    all_contrib = b.predict(X, pred_contrib=True)
+    for step in (10, 12):
+        pred = np.zeros_like(all_pred)
+        contrib = np.zeros_like(all_contrib)
+        for start in range(0, 50, step):
+            pred += b.predict(X, start_iteration=start, num_iteration=step, raw_score=True)
+            contrib += b.predict(X, start_iteration=start, num_iteration=step, pred_contrib=True)
+        np.testing.assert_allclose(all_pred, pred)
+        np.testing.assert_allclose(all_contrib, contrib)
+    np.testing.assert_allclose(b.predict(X, start_iteration=-1), b.predict(X, num_iteration=b.best_iteration))
+    for kw, n in (({}, 90), ({"pred_leaf": True}, 40), ({"pred_contrib": True}, 40)):
+        p4 = b.predict(X, start_iteration=10, num_iteration=-1, **kw)
+        np.testing.assert_allclose(p4, b.predict(X, start_iteration=10, num_iteration=n, **kw))
+        np.testing.assert_allclose(p4, b.predict(X, start_iteration=10, num_iteration=0, **kw))
+
+
+@pytest.mark.parametrize("use_init_score", [False, True])
+def test_predict_stump(lgb, use_init_score):
+    """test_predict_stump: n stumps predict the initial score once, not n times."""
+    X, y = load_breast_cancer(return_X_y=True)
+    kw = {"data": X, "label": y}
+    if use_init_score:
+        kw["init_score"] = np.random.default_rng(1).uniform(size=y.shape)
+    b = lgb.train(train_set=lgb.Dataset(**kw), params={"objective": "binary", "min_data_in_leaf": X.shape[0],
+                                                       "verbose": -1}, num_boost_round=5)
+    p1 = b.predict(X, raw_score=True, num_iteration=1)
+    pa = b.predict(X, raw_score=True)
+    expect = 0.0 if use_init_score else np.log(y.mean() / (1.0 - y.mean()))
+    np.testing.assert_allclose(p1, np.full_like(p1, expect), atol=1e-12)
+    np.testing.assert_allclose(pa, np.full_like(pa, expect), atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["regression", "binary", "multiclass"])
+def test_predict_output_shapes(lgb, kind):
+    """test_predict_{regression,binary_classification,multiclass_classification}_output_shape."""
+    from sklearn.datasets import make_classification
+    n = 1000
+    if kind == "regression":
+        X, y = _synth(n_samples=n, n_features=4)
+        params, k, f = {"objective": "regression", "verbosity": -1}, 1, 4
+    elif kind == "binary":
+        X, y = make_classification(n_samples=n, n_features=4, n_classes=2, random_state=0)
+        params, k, f = {"objective": "binary", "verbosity": -1}, 1, 4
+    else:
+        X, y = make_classification(n_samples=n, n_features=10, n_classes=3, n_informative=6, random_state=0)
+        params, k, f = {"objective": "multiclass", "verbosity": -1, "num_class": 3}, 3, 10
+    for rounds in (1, 2):
+        b = lgb.train(params, lgb.Dataset(X, label=y), num_boost_round=rounds)
+        flat = (n,) if k == 1 else (n, k)
+        assert b.predict(X).shape == flat
+        assert b.predict(X, raw_score=True).shape == flat
+        assert b.predict(X, pred_contrib=True).shape == (n, k * (f + 1))
+        assert b.predict(X, pred_leaf=True).shape == (n, k * rounds)
+
+
+def test_reset_params_works_with_metric_num_class_and_boosting(lgb):
+    """test_reset_params_works_with_metric_num_class_and_boosting."""
+    X, y = load_breast_cancer(return_X_y=True)
+    dataset_params = {"max_bin": 150}
+    booster_params = {"objective": "multiclass", "max_depth": 4, "bagging_fraction": 0.8,
+                      "metric": ["multi_logloss", "multi_error"], "boosting": "gbdt", "num_class": 5}
+    bst = lgb.Booster(params=booster_params, train_set=lgb.Dataset(X, y, params=dataset_params))
+    assert bst.params == dict(dataset_params, **booster_params)
+    booster_params["bagging_fraction"] += 0.1
+    new = bst.reset_parameter(booster_params)
+    assert bst.params == dict(dataset_params, **booster_params)
+    assert new.params == dict(dataset_params, **booster_params)
+
+
+def _assert_subtree_valid(node):
+    """utils.py assert_subtree_valid: counts / weights add up at every split."""
+    if "leaf_count" in node:
+        return node["leaf_count"], node["leaf_weight"]
+    lc, lw = _assert_subtree_valid(node["left_child"])
+    rc, rw = _assert_subtree_valid(node["right_child"])
+    assert node["internal_count"] == lc + rc
+    assert abs(node["internal_weight"] - (lw + rw)) <= 1e-3
+    return node["internal_count"], node["internal_weight"]
+
+
+def _assert_all_trees_valid(model):
+    for i, t in enumerate(model["tree_info"]):
+        assert t["tree_index"] == i
+        _assert_subtree_valid(t["tree_structure"])
+
+
+@pytest.mark.parametrize("linear_tree", [False, True])
+def test_dump_model_stump(lgb, linear_tree):
+    """test_dump_model_stump."""
+    X, y = load_breast_cancer(return_X_y=True)
+    b = lgb.train({"objective": "binary", "verbose": -1, "linear_tree": linear_tree, "min_data_in_leaf": len(y)},
+                  lgb.Dataset(X, label=y), num_boost_round=5)
+    d = b.dump_model(num_iteration=5, start_iteration=0)
+    assert len(d["tree_info"]) == 1
+    ts = d["tree_info"][0]["tree_structure"]
+    assert "leaf_value" in ts and ts["leaf_count"] == len(y)
+
+
+def test_dump_model(lgb):
+    """test_dump_model: constant-leaf dump, boost_from_average folded into the first tree."""
+    X, y = _synth()
+    b = lgb.train({"objective": "regression", "verbose": -1, "boost_from_average": True},
+                  lgb.Dataset(X, label=y + 57.5), num_boost_round=5)
+    d = b.dump_model(num_iteration=5, start_iteration=0)
+    s = str(d)
+    for k in ("leaf_features", "leaf_coeff", "leaf_const"):
+        assert k not in s
+    assert "leaf_value" in s and "leaf_count" in s
+    assert all(t["tree_structure"]["internal_value"] != 0 for t in d["tree_info"])
+    assert d["tree_info"][0]["tree_structure"]["internal_value"] == pytest.approx(57.5, abs=1)
+    _assert_all_trees_valid(d)
+
+
+def test_dump_model_linear(lgb):
+    """test_dump_model_linear."""
+    X, y = load_breast_cancer(return_X_y=True)
+    b = lgb.train({"objective": "binary", "verbose": -1, "linear_tree": True}, lgb.Dataset(X, label=y), 5)
+    d = b.dump_model(num_iteration=5, start_iteration=0)
+    _assert_all_trees_valid(d)
+    s = str(d)
+    for k in ("leaf_features", "leaf_coeff", "leaf_const", "leaf_value", "leaf_count"):
+        assert k in s
+
+
+def test_dump_model_hook(lgb):
+    """test_dump_model_hook."""
+    def hook(obj):
+        if "leaf_value" in obj:
+            obj["LV"] = obj.pop("leaf_value")
+        return obj
+
+    X, y = load_breast_cancer(return_X_y=True)
+    b = lgb.train({"objective": "binary", "verbose": -1}, lgb.Dataset(X, label=y), 5)
+    s = str(b.dump_model(5, 0, object_hook=hook))
+    assert "leaf_value" not in s and "LV" in s
+
+
+def test_force_split_with_feature_fraction(lgb, tmp_path):
+    """test_force_split_with_feature_fraction: the forced root split survives feature sampling."""
+    import json
+    from sklearn.metrics import mean_absolute_error
+    X_tr, X_te, y_tr, y_te = _split(*_synth())
+    f = tmp_path / "forced_split.json"
+    f.write_text(json.dumps({"feature": 0, "threshold": 0.5, "right": {"feature": 2, "threshold": 10.0}}))
+    b = lgb.train({"objective": "regression", "feature_fraction": 0.6, "force_col_wise": True,
+                   "feature_fraction_seed": 1, "forcedsplits_filename": f, "verbose": -1}, lgb.Dataset(X_tr, y_tr))
+    assert mean_absolute_error(y_te, b.predict(X_te)) < 15.7
+    info = b.dump_model()["tree_info"]
+    assert len(info) > 1
+    assert all(t["tree_structure"]["split_feature"] == 0 for t in info)
+
+
+_SAMPLE_BASE = {"metric": "l2", "verbose": -1, "num_threads": 1, "force_row_wise": True, "gpu_use_dp": True}
+
+
+def _sample_run(lgb, extra):
+    X, y = _synth(n_samples=10_000, n_features=10, n_informative=5, random_state=42)
+    X_tr, X_te, y_tr, y_te = _split(X, y)
+    tr = lgb.Dataset(X_tr, y_tr)
+    ev = lgb.Dataset(X_te, y_te, reference=tr)
+    rec = {}
+    b = lgb.train({**_SAMPLE_BASE, **extra}, tr, num_boost_round=10, valid_sets=ev,
+                  callbacks=[lgb.record_evaluation(rec)])
+    return rec["valid_0"]["l2"], mean_squared_error(y_te, b.predict(X_te))
+
+
+def test_goss_boosting_and_strategy_equivalent(lgb):
+    """test_goss_boosting_and_strategy_equivalent."""
+    extra = {"bagging_seed": 0, "learning_rate": 0.05}
+    assert _sample_run(lgb, {**extra, "boosting": "goss"})[0] == _sample_run(lgb, {**extra,
+                                                                                   "data_sample_strategy": "goss"})[0]
+
+
+def test_sample_strategy_with_boosting(lgb):
+    """test_sample_strategy_with_boosting: the reference's values for each boosting x sampling pair
+    (GOSS / bagging random streams and DART drops reproduced; all seven pinned at abs 1.0)."""
+    res = {}
+    for name, extra in {"dart_goss": {"boosting": "dart", "data_sample_strategy": "goss"},
+                        "gbdt_goss": {"boosting": "gbdt", "data_sample_strategy": "goss"},
+                        "goss_goss": {"boosting": "goss", "data_sample_strategy": "goss"},
+                        "rf_goss": {"boosting": "rf", "data_sample_strategy": "goss"},
+                        "dart_bag": {"boosting": "dart", "data_sample_strategy": "bagging", "bagging_freq": 1,
+                                     "bagging_fraction": 0.5},
+                        "gbdt_bag": {"boosting": "gbdt", "data_sample_strategy": "bagging", "bagging_freq": 1,
+                                     "bagging_fraction": 0.5},
+                        "rf_bag": {"boosting": "rf", "data_sample_strategy": "bagging", "bagging_freq": 1,
+                                   "bagging_fraction": 0.5}}.items():
+        ev, te = _sample_run(lgb, extra)
+        assert ev[-1] == pytest.approx(te)
+        res[name] = te
+    reference = {"dart_goss": 3149.393862, "gbdt_goss": 2547.715968, "goss_goss": 2547.715968,
+                 "rf_goss": 2095.538735, "dart_bag": 3134.866931, "gbdt_bag": 2539.792378, "rf_bag": 1518.704481}
+    assert res["gbdt_goss"] == res["goss_goss"]
+    assert res["dart_goss"] != res["gbdt_goss"] and res["rf_goss"] != res["dart_goss"]
+    assert res["rf_goss"] != res["gbdt_goss"]
+    assert len({res["dart_bag"], res["gbdt_bag"], res["rf_bag"]}) == 3
+    for k, v in res.items():
+        assert v == pytest.approx(reference[k], abs=1.0), k
+
+
+def test_record_evaluation_with_train(lgb):
+    """test_record_evaluation_with_train."""
+    X, y = _synth()
+    ds = lgb.Dataset(X, y)
+    rec = {}
+    b = lgb.train({"objective": "l2", "num_leaves": 3, "verbose": -1}, ds, num_boost_round=5, valid_sets=[ds],
+                  callbacks=[lgb.record_evaluation(rec)])
+    assert list(rec.keys()) == ["training"]
+    np.testing.assert_allclose(rec["training"]["l2"],
+                               [mean_squared_error(y, b.predict(X, num_iteration=i + 1)) for i in range(5)])
+
+
+@pytest.mark.parametrize("train_metric", [False, True])
+def test_record_evaluation_with_cv(lgb, train_metric):
+    """test_record_evaluation_with_cv."""
+    X, y = _synth()
+    rec = {}
+    metrics = ["l2", "rmse"]
+    hist = lgb.cv({"objective": "l2", "num_leaves": 3, "metric": metrics, "verbose": -1}, lgb.Dataset(X, y),
+                  num_boost_round=5, stratified=False, callbacks=[lgb.record_evaluation(rec)],
+                  eval_train_metric=train_metric)
+    sets = {"valid"} | ({"train"} if train_metric else set())
+    assert set(rec.keys()) == sets
+    for s in sets:
+        for m in metrics:
+            for agg in ("mean", "stdv"):
+                np.testing.assert_allclose(hist[f"{s} {m}-{agg}"], rec[s][f"{m}-{agg}"])
+
+
+def test_pandas_with_numpy_regular_dtypes(lgb):
+    """test_pandas_with_numpy_regular_dtypes: every integer / bool / float dtype gives the same model."""
+    pd = pytest.importorskip("pandas")
+    rng = np.random.default_rng(seed=42)
+    n = 100
+    df = pd.DataFrame({"x1": rng.integers(0, 2, n), "x2": rng.integers(1, 3, n),
+                       "x3": 10 * rng.integers(1, 3, n), "x4": 100 * rng.integers(1, 3, n)}).astype(np.float64)
+    y = df["x1"] * (df["x2"] + df["x3"] + df["x4"])
+    params = {"objective": "l2", "num_leaves": 31, "min_child_samples": 1, "verbose": -1}
+    b = lgb.train(params, lgb.Dataset(df, y), num_boost_round=5)
+    preds = b.predict(df)
+    assert b.trees_to_dataframe()["split_feature"].nunique() == df.shape[1]
+    assert mean_squared_error(y, preds) < mean_squared_error(y, np.full_like(y, y.mean()))
+    for dts in (["uint8", "uint16", "uint32", "uint64"], ["int8", "int16", "int32", "int64"],
+                ["bool", "float16", "float32", "float64"]):
+        df2 = df.astype({f"x{i}": dt for i, dt in enumerate(dts, start=1)})
+        assert df2.dtypes.tolist() == dts
+        b2 = lgb.train(params, lgb.Dataset(df2, y), num_boost_round=5)
+        np.testing.assert_allclose(preds, b2.predict(df2))
+
+
+def test_pandas_nullable_dtypes(lgb):
+    """test_pandas_nullable_dtypes: Int32 / Float64 / boolean / sparse columns train like numpy ones."""
+    pd = pytest.importorskip("pandas")
+    rng = np.random.default_rng(seed=42)
+    df = pd.DataFrame({"x1": rng.integers(1, 3, 100), "x2": np.linspace(-1, 1, 100),
+                       "x3": pd.arrays.SparseArray(rng.integers(0, 11, 100)),
+                       "x4": rng.uniform(size=(100,)) < 0.5})
+    df.loc[1, "x1"] = np.nan
+    df.loc[2, "x2"] = np.nan
+    df["x4"] = df["x4"].astype(np.float64)
+    df.loc[3, "x4"] = np.nan
+    y = (df["x1"] * df["x2"] + df["x3"] * (1 + df["x4"])).fillna(0)
+    params = {"objective": "l2", "num_leaves": 31, "min_child_samples": 1, "verbose": -1}
+    preds = lgb.train(params, lgb.Dataset(df, y), num_boost_round=5).predict(df)
+    df2 = df.copy()
+    df2["x1"] = df2["x1"].astype("Int32")
+    df2["x2"] = df2["x2"].astype("Float64")
+    df2["x4"] = df2["x4"].astype("boolean")
+    b2 = lgb.train(params, lgb.Dataset(df2, y), num_boost_round=5)
+    assert b2.trees_to_dataframe()["split_feature"].nunique() == df.shape[1]
+    assert mean_squared_error(y, preds) < mean_squared_error(y, np.full_like(y, y.mean()))
+    np.testing.assert_allclose(preds, b2.predict(df2))
+
+
+def test_boost_from_average_with_single_leaf_trees(lgb):
+    """test_boost_from_average_with_single_leaf_trees (upstream issue 4708 data)."""
+    X = np.array([[1021.0589, 1018.9578], [1023.85754, 1018.7854], [1024.5468, 1018.88513],
+                  [1019.02954, 1018.88513], [1016.79926, 1018.88513], [1007.6, 1018.88513]], dtype=np.float32)
+    y = np.array([1023.8, 1024.6, 1024.4, 1023.8, 1022.0, 1014.4], dtype=np.float32)
+    params = {"extra_trees": True, "min_data_in_bin": 1, "extra_seed": 7, "objective": "regression",
+              "verbose": -1, "boost_from_average": True, "min_data_in_leaf": 1}
+    m = np.mean(lgb.train(params, lgb.Dataset(X, y), num_boost_round=10).predict(X))
+    assert y.min() <= m <= y.max()
+
+
+def test_cegb_split_buffer_clean(lgb):
+    """test_cegb_split_buffer_clean: CEGB per-leaf split buffers are reset between trees."""
+    rng = np.random.default_rng(seed=42)
+    R, C = 1000, 100
+    data = rng.standard_normal(size=(R, C))
+    for i in range(1, C):
+        data[i] += data[0] * rng.standard_normal()
+    N = int(0.8 * R)
+    tr_y, te_y = data[:N].sum(axis=1), data[N:].sum(axis=1)
+    params = {"boosting_type": "gbdt", "objective": "regression", "max_bin": 255, "num_leaves": 31, "seed": 0,
+              "learning_rate": 0.1, "min_data_in_leaf": 0, "verbose": -1, "min_split_gain": 1000.0,
+              "cegb_penalty_feature_coupled": 5 * np.arange(C), "cegb_penalty_split": 0.0002,
+              "cegb_tradeoff": 10.0, "force_col_wise": True}
+    b = lgb.train(params, lgb.Dataset(data[:N], tr_y), num_boost_round=10)
+    assert np.sqrt(mean_squared_error(te_y, b.predict(data[N:]))) < 10.0
+
+
+def test_verbosity_and_verbose(lgb, capsys):
+    """test_verbosity_and_verbose: verbosity wins over its alias, and says so."""
+    X, y = _synth()
+    lgb.train({"num_leaves": 3, "verbose": 1, "verbosity": 0}, lgb.Dataset(X, y), num_boost_round=1)
+    assert ("[Warning] verbosity is set=0, verbose=1 will be ignored. Current value: verbosity=0"
+            in capsys.readouterr().out)
+
+
+def test_verbosity_is_respected_when_using_custom_objective(lgb, capsys):
+    """test_verbosity_is_respected_when_using_custom_objective."""
+    def mse_obj(y_pred, dtrain):
+        return y_pred - dtrain.get_label(), np.ones(len(y_pred))
+
+    X, y = _synth()
+    ds = lgb.Dataset(X, y)
+    params = {"objective": mse_obj, "nonsense": 123, "num_leaves": 3}
+    lgb.train({**params, "verbosity": -1}, ds, num_boost_round=1)
+    _assert_silent(capsys)
+    lgb.train({**params, "verbosity": 0}, ds, num_boost_round=1)
+    assert "[Warning] Unknown parameter: nonsense" in capsys.readouterr().out
+
+
+@pytest.mark.parametrize("verbosity_param", ["verbosity", "verbose"])
+@pytest.mark.parametrize("verbosity", [-1, 0])
+def test_verbosity_can_suppress_alias_warnings(lgb, capsys, verbosity_param, verbosity):
+    """test_verbosity_can_suppress_alias_warnings."""
+    X, y = _synth()
+    lgb.train({"num_leaves": 3, "subsample": 0.75, "bagging_fraction": 0.8, "force_col_wise": True,
+               verbosity_param: verbosity}, lgb.Dataset(X, y), num_boost_round=1)
+    out = capsys.readouterr().out
+    msg = "bagging_fraction is set=0.8, subsample=0.75 will be ignored. Current value: bagging_fraction=0.8"
+    if verbosity >= 0:
+        assert msg in out
+    else:
+        assert "[Warning]" not in out and "[Info]" not in out
+
+
+@pytest.mark.parametrize("use_cv", [False, True])
+def test_num_rounds_warning_only_when_expected(lgb, capsys, use_cv):
+    """test_{train,cv}_only_raises_num_rounds_warning_when_expected."""
+    import warnings
+    X, y = _synth()
+    ds = lgb.Dataset(X, y)
+    base = {"num_leaves": 5, "objective": "regression", "verbosity": -1}
+
+    def trees(params, **kw):
+        if use_cv:
+            out = lgb.cv(params, ds, return_cvbooster=True, stratified=False, **kw)["cvbooster"].num_trees()
+            assert len(set(out)) == 1
+            return out[0]
+        return lgb.train(params, ds, **kw).num_trees()
+
+    quiet = [({}, {}, 100), ({}, {"num_boost_round": 2}, 2), ({"n_iter": 3}, {"num_boost_round": 3}, 3),
+             ({"n_iter": 4}, {"num_boost_round": 3}, 4), ({"n_iter": 3, "num_iterations": 3}, {}, 3),
+             ({"n_iter": 3, "num_trees": 3, "nrounds": 3, "max_iter": 3}, {}, 3)]
+    for extra, kw, n in quiet:
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")
+            assert trees({**base, **extra}, **kw) == n
+        _assert_silent(capsys)
+    with pytest.warns(UserWarning, match="will perform up to 5 boosting rounds"):
+        assert trees({**base, "n_iter": 6, "num_iterations": 5}) == 5
+    _assert_silent(capsys)
+    with pytest.warns(UserWarning, match="will perform up to 4 boosting rounds"):
+        assert trees({**base, "n_iter": 4, "max_iter": 5}) == 4
+    _assert_silent(capsys)
+
+
+def test_validate_features(lgb):
+    """test_validate_features: predict / refit check the column names when asked to."""
+    pd = pytest.importorskip("pandas")
+    X, y = _synth()
+    df = pd.DataFrame(X, columns=["x1", "x2", "x3", "x4"])
+    b = lgb.train({"num_leaves": 15, "verbose": -1}, lgb.Dataset(df, y), num_boost_round=10)
+    assert b.feature_name() == ["x1", "x2", "x3", "x4"]
+    df2 = df.rename(columns={"x3": "z"})
+    with pytest.raises(lgb.basic.LightGBMError, match="Expected 'x3' at position 2 but found 'z'"):
+        b.predict(df2, validate_features=True)
+    b.predict(df2, validate_features=False)
+    with pytest.raises(lgb.basic.LightGBMError, match="Expected 'x3' at position 2 but found 'z'"):
+        b.refit(df2, y, validate_features=True)
+    b.refit(df2, y, validate_features=False)
+
+
+def test_train_and_cv_raise_informative_errors(lgb):
+    """test_train_and_cv_raise_informative_error_for_{train_set_of_wrong_type,impossible_num_boost_round},
+    test_train_raises_informative_error_{if_any_valid_sets_are_not_dataset_objects,for_params_of_wrong_type}."""
+    with pytest.raises(TypeError, match=r"train\(\) only accepts Dataset object, train_set has type 'list'\."):
+        lgb.train({}, train_set=[])
+    with pytest.raises(TypeError, match=r"cv\(\) only accepts Dataset object, train_set has type 'list'\."):
+        lgb.cv({}, train_set=[])
+    X, y = _synth()
+    for n in (-7, -1, 0):
+        msg = rf"Number of boosting rounds must be greater than 0\. Got {n}\."
+        with pytest.raises(ValueError, match=msg):
+            lgb.train({}, train_set=lgb.Dataset(X, y), num_boost_round=n)
+        with pytest.raises(ValueError, match=msg):
+            lgb.cv({}, train_set=lgb.Dataset(X, y), num_boost_round=n)
+    with pytest.raises(TypeError, match=r"Every item in valid_sets must be a Dataset object\. Item 1 has type 'tuple'\."):
+        lgb.train(params={}, train_set=lgb.Dataset(X, y),
+                  valid_sets=[lgb.Dataset(X * 2.0, y), ([1.0], [2.0]), [5.6, 5.7, 5.8]])
+    with pytest.raises(lgb.basic.LightGBMError, match='Parameter num_leaves should be of type int, got "too-many"'):
+        lgb.train({"num_leaves": "too-many"}, lgb.Dataset(X, label=y))
+
+
+def test_bagging_by_query_in_lambdarank(lgb):
+    """test_bagging_by_query_in_lambdarank (reference examples/lambdarank data)."""
+    import os
+    from sklearn.datasets import load_svmlight_file
+    d = os.path.join(os.path.dirname(__file__), "data", "examples", "lambdarank")
+    if not os.path.exists(os.path.join(d, "rank.train")):
+        d = "/root/reference/examples/lambdarank"
+    X_tr, y_tr = load_svmlight_file(os.path.join(d, "rank.train"))
+    X_te, y_te = load_svmlight_file(os.path.join(d, "rank.test"))
+    q_tr = np.loadtxt(os.path.join(d, "rank.train.query"))
+    q_te = np.loadtxt(os.path.join(d, "rank.test.query"))
+    params = {"objective": "lambdarank", "verbose": -1, "metric": "ndcg", "ndcg_eval_at": [5]}
+    tr = lgb.Dataset(X_tr, y_tr, group=q_tr, params=params)
+    te = lgb.Dataset(X_te, y_te, group=q_te, params=params)
+    base = lgb.train(params, tr, num_boost_round=50, valid_sets=[te]).best_score["valid_0"]["ndcg@5"]
+    for by_query in (True, False):
+        p = dict(params, bagging_by_query=by_query, bagging_fraction=0.1, bagging_freq=1)
+        s = lgb.train(p, tr, num_boost_round=50, valid_sets=[te]).best_score["valid_0"]["ndcg@5"]
+        assert s >= base - 0.1
+
+
+def test_equal_predict_from_row_major_and_col_major_data(lgb):
+    """test_equal_predict_from_row_major_and_col_major_data."""
+    X, y = _synth()
+    assert X.flags["C_CONTIGUOUS"]
+    b = lgb.train({"num_leaves": 8, "verbose": -1}, lgb.Dataset(X, y), num_boost_round=5)
+    Xc = np.asfortranarray(X)
+    assert Xc.flags["F_CONTIGUOUS"] and not Xc.flags["C_CONTIGUOUS"]
+    np.testing.assert_allclose(b.predict(X), b.predict(Xc))
+
+
+@pytest.mark.parametrize("use_cv", [False, True])
+def test_objective_callable_regression(lgb, use_cv):
+    """test_objective_callable_{train,cv}_regression (train value 286.724194 pinned)."""
+    def mse_obj(y_pred, dtrain):
+        return y_pred - dtrain.get_label(), np.ones(len(y_pred))
+
+    X, y = _synth()
+    params = {"verbose": -1, "objective": mse_obj}
+    if not use_cv:
+        b = lgb.train(params, lgb.Dataset(X, y), num_boost_round=20)
+        assert b.params["objective"] == "none"
+        assert mean_squared_error(y, b.predict(X)) == pytest.approx(286.724194)
+        return
+    res = lgb.cv(params, lgb.Dataset(X, y), num_boost_round=20, nfold=3, stratified=False, return_cvbooster=True)
+    for cb in res["cvbooster"].boosters:
+        assert cb.params["objective"] == "none"
+        assert mean_squared_error(y, cb.predict(X)) < 463
