@@ -52,7 +52,7 @@ def main() -> int:
     models = {}
     devs = os.environ.get("DP_DEVICES", "gpu,cpu").split(",")
     for dev in devs:
-        models[dev] = lgb.train(dict(base, device_type=dev), ds, 10)
+        models[dev] = lgb.train(dict(base, device_type=dev), ds, 10, keep_training_booster=True)
     first = models[devs[0]]
     name = first.device_name()
     text = first.model_to_string()

@@ -38,7 +38,7 @@ def main() -> int:
     out = {}
     for mode in ("single", "dp"):
         os.environ["LGAP_FORCE_DEVICE_DP"] = "1" if mode == "dp" else "0"
-        b = lgb.train(params, lgb.Dataset(X, y, params=params), 8)
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 8, keep_training_booster=True)
         out[mode] = b
     pa, pb = out["single"].predict(X), out["dp"].predict(X)
     ta = [t["tree_structure"].get("split_feature") for t in out["single"].dump_model()["tree_info"]]

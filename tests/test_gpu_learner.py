@@ -16,7 +16,7 @@ def _train(lgb, X, y, device, rounds=1, **kw):
               "min_data_in_leaf": 20, "seed": 1, "deterministic": True}
     params.update(kw)
     ds = lgb.Dataset(X, y, params=params)
-    return lgb.train(params, ds, rounds)
+    return lgb.train(params, ds, rounds, keep_training_booster=True)  # device_name() needs the live learner
 
 
 def _trees(b):
