@@ -12,6 +12,7 @@
 // applied uniformly. EFB bundles (dataset.cpp:107-323) share one group.
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <vector>
@@ -130,9 +131,29 @@ class Dataset {
   int num_groups() const { return static_cast<int>(groups_.size()); }
   int num_total_bin() const { return num_total_bin_; }
   int bin_width() const { return bin_width_; }
-  int row_stride() const { return row_stride_; }
-  const uint8_t* bins() const { return bins_.data(); }
-  const std::vector<uint8_t>& bins_vec() const { return bins_; }
+  // stride of a row with EVERY group packed (the device kernels' record; MaterializeRows)
+  int row_stride() const { return FullStride(num_groups(), bin_width_); }
+  // the stored dense part: groups [0, num_dense_groups()) packed row-major at dense_stride()
+  int num_dense_groups() const { return num_dense_groups_; }
+  int dense_stride() const { return row_stride_; }
+  const uint8_t* dense_bins() const { return bins_.data(); }
+  const uint8_t* dense_row(data_size_t i) const { return bins_.data() + static_cast<size_t>(i) * row_stride_; }
+  // multi-value sparse part (reference multi_val_sparse_bin.hpp, MI355X-first as one CSR of
+  // global histogram bins): row i's non-zero sparse groups are sp_bins()[sp_ptr()[i] ..
+  // sp_ptr()[i + 1]), each entry hist_start(group) + group bin, ascending
+  bool has_sparse() const { return num_dense_groups_ < num_groups(); }
+  const uint64_t* sp_ptr() const { return sp_ptr_.data(); }
+  const uint32_t* sp_bins() const { return sp_bin_.data(); }
+  size_t sparse_nnz() const { return sp_bin_.size(); }
+  // every group packed row-major at row_stride() (device upload of a sparse-stored dataset)
+  const uint8_t* RowsForDevice(std::vector<uint8_t>* scratch) const;
+  void MaterializeRows(std::vector<uint8_t>* out) const;
+  // sparse groups back into the dense matrix (AddFeaturesFrom, device packing)
+  void Densify();
+  static int FullStride(int ngroups, int width) {
+    const int s = (ngroups * width + 3) / 4 * 4;
+    return s == 0 ? 4 : s;
+  }
   const FeatureInfo& feature(int inner) const { return features_[inner]; }
   const std::vector<FeatureInfo>& features() const { return features_; }
   const FeatureGroup& group(int g) const { return groups_[g]; }
@@ -152,8 +173,16 @@ class Dataset {
 
   // Raw group bin of row i in group g.
   inline uint32_t GroupBin(data_size_t i, int g) const {
+    if (g >= num_dense_groups_) return SparseGroupBin(i, g);
     const uint8_t* r = bins_.data() + static_cast<size_t>(i) * row_stride_;
     return bin_width_ == 1 ? r[g] : reinterpret_cast<const uint16_t*>(r)[g];
+  }
+  inline uint32_t SparseGroupBin(data_size_t i, int g) const {
+    const uint32_t lo = static_cast<uint32_t>(groups_[g].hist_start);
+    const uint32_t* b = sp_bin_.data() + sp_ptr_[i];
+    const uint32_t* e = sp_bin_.data() + sp_ptr_[i + 1];
+    const uint32_t* p = std::lower_bound(b, e, lo);
+    return (p != e && *p < lo + static_cast<uint32_t>(groups_[g].num_bin)) ? *p - lo : 0u;
   }
   // Feature bin of row i for inner feature f (decoding the group bin).
   inline uint32_t FeatureBin(data_size_t i, int f) const {
@@ -189,6 +218,8 @@ class Dataset {
                    data_size_t sample_cnt);
   void PackRows(const RowSource& src, data_size_t start_row = 0, bool reset = true);
   void FinalizeLayout();
+  // moves groups whose rows are mostly at group bin 0 into the sparse CSR (sparse groups last)
+  void CompressSparseGroups(double zero_threshold);
 
   data_size_t num_data_ = 0;
   int num_total_features_ = 0;
@@ -200,8 +231,11 @@ class Dataset {
   std::vector<int> categorical_;
   int num_total_bin_ = 0;
   int bin_width_ = 1;
-  int row_stride_ = 0;
+  int row_stride_ = 0;            // stride of bins_ (dense groups only)
+  int num_dense_groups_ = 0;
   std::vector<uint8_t> bins_;
+  std::vector<uint64_t> sp_ptr_;  // num_data_ + 1 (empty: every group dense)
+  std::vector<uint32_t> sp_bin_;
   std::vector<float> raw_;
   bool keep_raw_ = false;
   bool device_pack_ = false;  // device_type=gpu + device_binning: PackRows runs on the GPU

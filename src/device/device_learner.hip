@@ -3544,7 +3544,10 @@ class DeviceTreeLearner : public TreeLearner {
     ScopedTimer timer("Device::AddValidSet");
     auto dv = std::make_unique<DevValid>();
     dv->n = v->num_data();
-    dv->rowbins.Upload(reinterpret_cast<const uint32_t*>(v->bins()), static_cast<size_t>(dv->n) * stride_dw_, stream_);
+    std::vector<uint8_t> full;  // a sparse-stored set is materialized to full rows for the upload
+    dv->rowbins.Upload(reinterpret_cast<const uint32_t*>(v->RowsForDevice(&full)), static_cast<size_t>(dv->n) * stride_dw_,
+                       stream_);
+    if (!full.empty()) HIP_CHECK(hipStreamSynchronize(stream_));  // the scratch dies here
     dv->score.Upload(score, stream_);
     const Metadata& md = v->metadata();
     if (md.label()) dv->label.Upload(md.label(), dv->n, stream_);
@@ -4048,7 +4051,9 @@ class DeviceTreeLearner : public TreeLearner {
       Log::Debug("HIP learner: adopted the device-binned rows (%zu bytes)", rb * sizeof(uint32_t));
     } else {
       rowbins_.Resize(std::max<size_t>(rb, 1));
-      rowbins_.Upload(reinterpret_cast<const uint32_t*>(data_->bins()), rb, stream_);
+      std::vector<uint8_t> full;  // a sparse-stored (host-constructed) set becomes full rows
+      rowbins_.Upload(reinterpret_cast<const uint32_t*>(data_->RowsForDevice(&full)), rb, stream_);
+      if (!full.empty()) HIP_CHECK(hipStreamSynchronize(stream_));
     }
     // group-major copy, transposed on the device from the packed rows
     const size_t cb = static_cast<size_t>(G_) * N_ * width_;

@@ -24,6 +24,10 @@ namespace lgap {
 
 namespace {
 const char* kBinaryToken = "______LambdaGap_Binary_File_Token______\n";
+// zero rate from which a feature group is stored as multi-value sparse rows: an entry
+// is 4 bytes against 1-2 per row densely, so this sits above the reference's
+// kSparseThreshold (bin.h:43, 0.7)
+constexpr double kSparseZeroRate = 0.8;
 
 template <typename T>
 void Put(std::vector<char>* out, const T& v) {
@@ -226,8 +230,120 @@ void Dataset::FinalizeLayout() {
     num_total_bin_ += fg.num_bin;
   }
   // pad each row to a multiple of 4 bytes (dword-aligned records for the device kernels)
-  row_stride_ = (num_groups() * bin_width_ + 3) / 4 * 4;
-  if (row_stride_ == 0) row_stride_ = 4;
+  row_stride_ = FullStride(num_groups(), bin_width_);
+  num_dense_groups_ = num_groups();
+  sp_ptr_.clear();
+  sp_bin_.clear();
+}
+
+// Multi-value sparse storage (reference src/io/multi_val_sparse_bin.hpp and the
+// is_multi_val feature groups of dataset.cpp:219-242 / feature_group.h:216). A group whose
+// rows are at least `zero_threshold` at group bin 0 moves out of the dense matrix into one
+// CSR of global histogram bins; the host row-wise histogram then walks only its non-zeros.
+// Sparse groups are moved to the end of the group order (dense groups keep their order),
+// so a dense row keeps the layout the device kernels expect for its leading groups and a
+// full row (MaterializeRows) is the dense row followed by the sparse groups' bins.
+// Per-bin sums are accumulated in the same row order either way: models are identical.
+void Dataset::CompressSparseGroups(double zero_threshold) {
+  const int ng = num_groups();
+  if (ng == 0 || num_data_ <= 0 || has_sparse()) return;
+  std::vector<data_size_t> nnz(ng, 0);
+#pragma omp parallel
+  {
+    std::vector<data_size_t> local(ng, 0);
+#pragma omp for schedule(static)
+    for (data_size_t i = 0; i < num_data_; ++i) {
+      for (int g = 0; g < ng; ++g) local[g] += GroupBin(i, g) != 0u;
+    }
+#pragma omp critical
+    for (int g = 0; g < ng; ++g) nnz[g] += local[g];
+  }
+  std::vector<int> order, sparse;
+  for (int g = 0; g < ng; ++g) {
+    const double zero_rate = 1.0 - static_cast<double>(nnz[g]) / num_data_;
+    (zero_rate >= zero_threshold ? sparse : order).push_back(g);
+  }
+  if (sparse.empty()) return;
+  const int nd = static_cast<int>(order.size());
+  order.insert(order.end(), sparse.begin(), sparse.end());
+  const std::vector<uint8_t> old_bins = std::move(bins_);
+  const int old_stride = row_stride_, width = bin_width_;
+  std::vector<FeatureGroup> ng_groups;
+  for (int g : order) ng_groups.push_back(groups_[g]);
+  groups_.swap(ng_groups);
+  FinalizeLayout();
+  bin_width_ = width;
+  num_dense_groups_ = nd;
+  row_stride_ = FullStride(nd, width);
+  auto old_bin = [&](data_size_t i, int g) -> uint32_t {
+    const uint8_t* r = old_bins.data() + static_cast<size_t>(i) * old_stride;
+    return width == 1 ? r[g] : reinterpret_cast<const uint16_t*>(r)[g];
+  };
+  bins_.assign(static_cast<size_t>(num_data_) * row_stride_, 0);
+  sp_ptr_.assign(static_cast<size_t>(num_data_) + 1, 0);
+#pragma omp parallel for schedule(static)
+  for (data_size_t i = 0; i < num_data_; ++i) {
+    uint8_t* r = bins_.data() + static_cast<size_t>(i) * row_stride_;
+    for (int j = 0; j < nd; ++j) {
+      const uint32_t v = old_bin(i, order[j]);
+      if (width == 1) r[j] = static_cast<uint8_t>(v);
+      else reinterpret_cast<uint16_t*>(r)[j] = static_cast<uint16_t>(v);
+    }
+    uint64_t c = 0;
+    for (int j = nd; j < ng; ++j) c += old_bin(i, order[j]) != 0u;
+    sp_ptr_[static_cast<size_t>(i) + 1] = c;
+  }
+  for (data_size_t i = 0; i < num_data_; ++i) sp_ptr_[static_cast<size_t>(i) + 1] += sp_ptr_[i];
+  sp_bin_.resize(sp_ptr_.back());
+#pragma omp parallel for schedule(static)
+  for (data_size_t i = 0; i < num_data_; ++i) {
+    uint64_t k = sp_ptr_[i];
+    for (int j = nd; j < ng; ++j) {  // hist_start ascends with j: entries stay sorted
+      const uint32_t v = old_bin(i, order[j]);
+      if (v != 0u) sp_bin_[k++] = static_cast<uint32_t>(groups_[j].hist_start) + v;
+    }
+  }
+  Log::Info("Sparse storage: %d of %d feature groups as multi-value sparse rows (%.2f non-zeros per row)",
+            ng - nd, ng, static_cast<double>(sp_bin_.size()) / num_data_);
+}
+
+void Dataset::MaterializeRows(std::vector<uint8_t>* out) const {
+  const int fs = row_stride(), ng = num_groups(), nd = num_dense_groups_;
+  out->assign(static_cast<size_t>(num_data_) * fs, 0);
+  std::vector<uint32_t> sstart;
+  for (int g = nd; g < ng; ++g) sstart.push_back(static_cast<uint32_t>(groups_[g].hist_start));
+  const int dense_bytes = nd * bin_width_;
+#pragma omp parallel for schedule(static)
+  for (data_size_t i = 0; i < num_data_; ++i) {
+    uint8_t* r = out->data() + static_cast<size_t>(i) * fs;
+    std::memcpy(r, bins_.data() + static_cast<size_t>(i) * row_stride_, dense_bytes);
+    if (sp_ptr_.empty()) continue;
+    for (uint64_t k = sp_ptr_[i]; k < sp_ptr_[static_cast<size_t>(i) + 1]; ++k) {
+      const uint32_t e = sp_bin_[k];
+      const int j = static_cast<int>(std::upper_bound(sstart.begin(), sstart.end(), e) - sstart.begin()) - 1;
+      const int g = nd + j;
+      const uint32_t v = e - sstart[j];
+      if (bin_width_ == 1) r[g] = static_cast<uint8_t>(v);
+      else reinterpret_cast<uint16_t*>(r)[g] = static_cast<uint16_t>(v);
+    }
+  }
+}
+
+const uint8_t* Dataset::RowsForDevice(std::vector<uint8_t>* scratch) const {
+  if (!has_sparse()) return bins_.data();
+  MaterializeRows(scratch);
+  return scratch->data();
+}
+
+void Dataset::Densify() {
+  if (!has_sparse()) return;
+  std::vector<uint8_t> full;
+  MaterializeRows(&full);
+  bins_.swap(full);
+  row_stride_ = FullStride(num_groups(), bin_width_);
+  num_dense_groups_ = num_groups();
+  sp_ptr_.clear();
+  sp_bin_.clear();
 }
 
 void Dataset::InitEmptyLike(const Dataset& ref, data_size_t n) {
@@ -241,7 +357,8 @@ void Dataset::InitEmptyLike(const Dataset& ref, data_size_t n) {
   categorical_ = ref.categorical_;
   num_total_bin_ = ref.num_total_bin_;
   bin_width_ = ref.bin_width_;
-  row_stride_ = ref.row_stride_;
+  row_stride_ = FullStride(num_groups(), bin_width_);  // streamed rows are stored dense
+  num_dense_groups_ = num_groups();
   bins_.assign(static_cast<size_t>(n) * row_stride_, 0);
   metadata_.Init(n);
 }
@@ -331,7 +448,8 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
     feature_names_ = reference->feature_names_;
     num_total_bin_ = reference->num_total_bin_;
     bin_width_ = reference->bin_width_;
-    row_stride_ = reference->row_stride_;
+    row_stride_ = FullStride(num_groups(), bin_width_);  // the reference's groups, stored dense
+    num_dense_groups_ = num_groups();
     PackRows(src);
     metadata_.Init(num_data_);
     return;
@@ -485,6 +603,11 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
   FinalizeLayout();
   PackRows(src);
   metadata_.Init(num_data_);
+  // single-process host training only: ranks would choose different sparse sets (their own
+  // rows) and the device kernels stream dense rows
+  if (cfg.is_enable_sparse && !device_pack_ && nm == 1 && cfg.device_type == "cpu" && cfg.num_machines <= 1) {
+    CompressSparseGroups(kSparseZeroRate);
+  }
 }
 
 void Dataset::ConstructFromMappers(std::vector<BinMapper> mappers, const RowSource& src, const Config& cfg,
@@ -555,11 +678,24 @@ std::unique_ptr<Dataset> Dataset::Subset(const std::vector<data_size_t>& idx) co
   d->num_total_bin_ = num_total_bin_;
   d->bin_width_ = bin_width_;
   d->row_stride_ = row_stride_;
+  d->num_dense_groups_ = num_dense_groups_;
   d->bins_.resize(static_cast<size_t>(d->num_data_) * row_stride_);
 #pragma omp parallel for schedule(static)
   for (data_size_t i = 0; i < d->num_data_; ++i) {
     std::memcpy(d->bins_.data() + static_cast<size_t>(i) * row_stride_,
                 bins_.data() + static_cast<size_t>(idx[i]) * row_stride_, row_stride_);
+  }
+  if (!sp_ptr_.empty()) {
+    d->sp_ptr_.assign(static_cast<size_t>(d->num_data_) + 1, 0);
+    for (data_size_t i = 0; i < d->num_data_; ++i) {
+      d->sp_ptr_[static_cast<size_t>(i) + 1] = d->sp_ptr_[i] + sp_ptr_[static_cast<size_t>(idx[i]) + 1] - sp_ptr_[idx[i]];
+    }
+    d->sp_bin_.resize(d->sp_ptr_.back());
+#pragma omp parallel for schedule(static)
+    for (data_size_t i = 0; i < d->num_data_; ++i) {
+      std::copy(sp_bin_.begin() + sp_ptr_[idx[i]], sp_bin_.begin() + sp_ptr_[static_cast<size_t>(idx[i]) + 1],
+                d->sp_bin_.begin() + d->sp_ptr_[i]);
+    }
   }
   d->metadata_.Subset(metadata_, idx.data(), d->num_data_);
   return d;
@@ -567,6 +703,7 @@ std::unique_ptr<Dataset> Dataset::Subset(const std::vector<data_size_t>& idx) co
 
 void Dataset::AddFeaturesFrom(const Dataset& o) {
   if (o.num_data_ != num_data_) Log::Fatal("Cannot add features from other Dataset with a different number of rows");
+  Densify();
   const int old_groups = num_groups();
   const int old_stride = row_stride_;
   const int old_width = bin_width_;
@@ -641,6 +778,10 @@ void Dataset::SerializeBinary(std::vector<char>* out) const {
   // (dataset.cpp SaveBinaryFile, raw_data_ section)
   Put(&buf, static_cast<int32_t>(keep_raw_ ? 1 : 0));
   PutVec(&buf, raw_);
+  // multi-value sparse groups (absent in files written before the sparse storage)
+  Put(&buf, static_cast<int32_t>(num_dense_groups_));
+  PutVec(&buf, sp_ptr_);
+  PutVec(&buf, sp_bin_);
 }
 
 void Dataset::SaveBinary(const std::string& filename) const {
@@ -692,9 +833,15 @@ std::unique_ptr<Dataset> Dataset::DeserializeBinary(const char* data, size_t siz
   d->categorical_ = GetVec<int>(p);
   p += d->metadata_.Deserialize(p);
   d->bins_ = GetVec<uint8_t>(p);
+  d->num_dense_groups_ = ng;
   if (p < data + size) {
     d->keep_raw_ = Get<int32_t>(p) != 0;
     d->raw_ = GetVec<float>(p);
+  }
+  if (p < data + size) {
+    d->num_dense_groups_ = Get<int32_t>(p);
+    d->sp_ptr_ = GetVec<uint64_t>(p);
+    d->sp_bin_ = GetVec<uint32_t>(p);
   }
   return d;
 }

@@ -5,10 +5,12 @@
 // feature sampling by tree / node, interaction constraints, forced splits,
 // refit and L1/quantile leaf renewal.
 #include "serial_tree_learner.h"
+#include "lgap/omp_errors.h"
 
 #include <omp.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -289,7 +291,8 @@ void SerialTreeLearner::ComputeLeafSums(const data_size_t* idx, data_size_t n, d
 namespace {
 template <typename BinT>
 void HistRows(const data_size_t* idx, data_size_t i0, data_size_t i1, const uint8_t* bins, int stride, int ng,
-              const int* gstart, const score_t* grad, const score_t* hess, double* hh) {
+              const int* gstart, const uint64_t* sp_ptr, const uint32_t* sp_bin, const score_t* grad,
+              const score_t* hess, double* hh) {
   // rows of a deep leaf are scattered: prefetch the bin row and the gradients kPf rows
   // ahead so the misses overlap (reference dense_bin.hpp ConstructHistogram prefetch)
   constexpr data_size_t kPf = 32;
@@ -299,6 +302,7 @@ void HistRows(const data_size_t* idx, data_size_t i0, data_size_t i1, const uint
       __builtin_prefetch(bins + static_cast<size_t>(rp) * stride);
       __builtin_prefetch(grad + rp);
       __builtin_prefetch(hess + rp);
+      if (sp_ptr) __builtin_prefetch(sp_ptr + rp);
     }
     const data_size_t r = idx[i];
     const double g = grad[r], h = hess[r];
@@ -310,6 +314,14 @@ void HistRows(const data_size_t* idx, data_size_t i0, data_size_t i1, const uint
       e[0] += g;
       e[1] += h;
     }
+    if (sp_ptr) {
+      // multi-value sparse groups: only the row's non-zero entries (global bins)
+      for (uint64_t k = sp_ptr[r], ke = sp_ptr[r + 1]; k < ke; ++k) {
+        double* e = hh + 2 * static_cast<size_t>(sp_bin[k]);
+        e[0] += g;
+        e[1] += h;
+      }
+    }
   }
 }
 }  // namespace
@@ -319,20 +331,143 @@ void SerialTreeLearner::BuildHistogram(const data_size_t* idx, data_size_t n, do
     hist_backend_->Histogram(idx, n, hist);
     return;
   }
+  if (hist_layout_ == HistLayout::kAuto) {
+    if (config_->force_col_wise && config_->force_row_wise) {
+      Log::Fatal("Cannot set both `force_col_wise` and `force_row_wise` to `true` at the same time");
+    }
+    if (config_->force_col_wise) {
+      hist_layout_ = HistLayout::kColWise;
+    } else if (config_->force_row_wise || train_data_->num_dense_groups() <= 1 || omp_get_max_threads() == 1) {
+      hist_layout_ = HistLayout::kRowWise;
+    } else {
+      // time both on this (root-sized) histogram; the results are identical, keep the faster
+      std::vector<double> probe(2 * static_cast<size_t>(train_data_->num_total_bin()));
+      const auto t0 = std::chrono::steady_clock::now();
+      BuildHistogramRowWise(idx, n, hist);
+      const auto t1 = std::chrono::steady_clock::now();
+      BuildHistogramColWise(idx, n, probe.data());
+      const auto t2 = std::chrono::steady_clock::now();
+      const double row_s = std::chrono::duration<double>(t1 - t0).count();
+      const double col_s = std::chrono::duration<double>(t2 - t1).count();
+      const bool col = col_s < row_s;
+      hist_layout_ = col ? HistLayout::kColWise : HistLayout::kRowWise;
+      if (!col) std::vector<uint8_t>().swap(colbins_);
+      Log::Info("Auto-choosing %s-wise multi-threading, the overhead of testing was %f seconds.\n"
+                "You can set `force_%s_wise=true` to remove the overhead.",
+                col ? "col" : "row", std::min(row_s, col_s) + (col ? row_s : col_s), col ? "col" : "row");
+      if (col) std::memcpy(hist, probe.data(), probe.size() * sizeof(double));
+      return;
+    }
+  }
+  if (hist_layout_ == HistLayout::kColWise) BuildHistogramColWise(idx, n, hist);
+  else BuildHistogramRowWise(idx, n, hist);
+}
+
+namespace {
+// rows per histogram thread chunk: shared by both layouts so their sums associate alike
+inline int HistChunks(data_size_t n) {
+  return static_cast<int>(std::max<data_size_t>(1, std::min<data_size_t>(omp_get_max_threads(), n / 8192)));
+}
+
+template <typename BinT>
+void HistColumn(const BinT* col, const data_size_t* idx, data_size_t i0, data_size_t i1, const score_t* grad,
+                const score_t* hess, double* buf) {
+  for (data_size_t i = i0; i < i1; ++i) {
+    const data_size_t r = idx[i];
+    const uint32_t b = col[r];
+    if (b == 0) continue;
+    buf[2 * b] += grad[r];
+    buf[2 * b + 1] += hess[r];
+  }
+}
+}  // namespace
+
+void SerialTreeLearner::BuildHistogramColWise(const data_size_t* idx, data_size_t n, double* hist) const {
+  const Dataset* d = train_data_;
+  const int tb = d->num_total_bin();
+  const int nd = d->num_dense_groups();
+  const int width = d->bin_width();
+  const size_t N = static_cast<size_t>(d->num_data());
+  if (colbins_.size() != N * nd * width) {
+    colbins_.resize(N * nd * width);
+#pragma omp parallel for schedule(static)
+    for (int g = 0; g < nd; ++g) {
+      uint8_t* c = colbins_.data() + static_cast<size_t>(g) * N * width;
+      for (size_t i = 0; i < N; ++i) {
+        const uint32_t v = d->GroupBin(static_cast<data_size_t>(i), g);
+        if (width == 1) c[i] = static_cast<uint8_t>(v);
+        else reinterpret_cast<uint16_t*>(c)[i] = static_cast<uint16_t>(v);
+      }
+    }
+  }
+  std::memset(hist, 0, sizeof(double) * 2 * tb);
+  const int nt = HistChunks(n);
+  const data_size_t per = (n + nt - 1) / nt;
+  // dense groups: one thread per group, chunk partials folded in chunk order
+  OmpErrors errs;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int g = 0; g < nd; ++g) {
+    errs.Run([&] {
+      const FeatureGroup& fg = d->group(g);
+      std::vector<double> buf(2 * static_cast<size_t>(fg.num_bin));
+      double* out = hist + 2 * static_cast<size_t>(fg.hist_start);
+      const uint8_t* c = colbins_.data() + static_cast<size_t>(g) * N * width;
+      for (int t = 0; t < nt; ++t) {
+        const data_size_t i0 = std::min(n, t * per), i1 = std::min(n, i0 + per);
+        std::fill(buf.begin(), buf.end(), 0.0);
+        if (width == 1) HistColumn<uint8_t>(c, idx, i0, i1, gradients_, hessians_, buf.data());
+        else HistColumn<uint16_t>(reinterpret_cast<const uint16_t*>(c), idx, i0, i1, gradients_, hessians_, buf.data());
+        for (int b = 2; b < 2 * fg.num_bin; ++b) out[b] += buf[b];
+      }
+    });
+  }
+  errs.Rethrow();
+  if (!d->has_sparse()) return;
+  // multi-value sparse groups: row chunks over the CSR into the sparse bin range
+  const int s0 = d->group(nd).hist_start;
+  const size_t sw = 2 * static_cast<size_t>(tb - s0);
+  if (static_cast<int>(tls_hist_.size()) < nt) tls_hist_.resize(nt);
+  const uint64_t* sp_ptr = d->sp_ptr();
+  const uint32_t* sp_bin = d->sp_bins();
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+  for (int t = 0; t < nt; ++t) {
+    auto& buf = tls_hist_[t];
+    buf.assign(sw, 0.0);
+    const data_size_t i0 = std::min(n, t * per), i1 = std::min(n, i0 + per);
+    for (data_size_t i = i0; i < i1; ++i) {
+      const data_size_t r = idx[i];
+      const double gr = gradients_[r], hs = hessians_[r];
+      for (uint64_t k = sp_ptr[r], ke = sp_ptr[r + 1]; k < ke; ++k) {
+        double* e = buf.data() + 2 * (static_cast<size_t>(sp_bin[k]) - s0);
+        e[0] += gr;
+        e[1] += hs;
+      }
+    }
+  }
+  double* out = hist + 2 * static_cast<size_t>(s0);
+  for (int t = 0; t < nt; ++t) {
+    const double* b = tls_hist_[t].data();
+    for (size_t j = 0; j < sw; ++j) out[j] += b[j];
+  }
+}
+
+void SerialTreeLearner::BuildHistogramRowWise(const data_size_t* idx, data_size_t n, double* hist) const {
   const int tb = train_data_->num_total_bin();
-  const int ng = train_data_->num_groups();
+  const int ng = train_data_->num_dense_groups();
   const auto& groups = train_data_->groups();
   std::vector<int> gstart(ng);
   for (int g = 0; g < ng; ++g) gstart[g] = groups[g].hist_start;
+  const uint64_t* sp_ptr = train_data_->has_sparse() ? train_data_->sp_ptr() : nullptr;
+  const uint32_t* sp_bin = train_data_->sp_bins();
   std::memset(hist, 0, sizeof(double) * 2 * tb);
   // one private histogram per thread above ~8k rows each (kept across calls), folded after
-  const int nt = static_cast<int>(std::max<data_size_t>(1, std::min<data_size_t>(omp_get_max_threads(), n / 8192)));
-  const uint8_t* bins = train_data_->bins();
-  const int stride = train_data_->row_stride();
+  const int nt = HistChunks(n);
+  const uint8_t* bins = train_data_->dense_bins();
+  const int stride = train_data_->dense_stride();
   const bool w1 = train_data_->bin_width() == 1;
   auto run = [&](data_size_t i0, data_size_t i1, double* hh) {
-    if (w1) HistRows<uint8_t>(idx, i0, i1, bins, stride, ng, gstart.data(), gradients_, hessians_, hh);
-    else HistRows<uint16_t>(idx, i0, i1, bins, stride, ng, gstart.data(), gradients_, hessians_, hh);
+    if (w1) HistRows<uint8_t>(idx, i0, i1, bins, stride, ng, gstart.data(), sp_ptr, sp_bin, gradients_, hessians_, hh);
+    else HistRows<uint16_t>(idx, i0, i1, bins, stride, ng, gstart.data(), sp_ptr, sp_bin, gradients_, hessians_, hh);
   };
   if (nt == 1) {
     run(0, n, hist);
@@ -691,9 +826,7 @@ void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* ri
     const bool dl = info.default_left != 0;
     const MissingType mt = fi.missing;
     const uint32_t nan_bin = static_cast<uint32_t>(fi.num_bin - 1);
-    const uint8_t* bins = d->bins();
-    const size_t stride = static_cast<size_t>(d->row_stride());
-    auto pf = [&](data_size_t r) { __builtin_prefetch(bins + r * stride); };
+    auto pf = [&](data_size_t r) { __builtin_prefetch(d->dense_row(r)); };
     nl = partition_.Split(best_leaf, next, [&](data_size_t r) {
       const uint32_t b = d->FeatureBin(r, f);
       if ((mt == MissingType::Zero && b == fi.default_bin) || (mt == MissingType::NaN && b == nan_bin)) return dl;

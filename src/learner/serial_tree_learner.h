@@ -107,6 +107,8 @@ class SerialTreeLearner : public TreeLearner {
   virtual void SyncBestSplits() {}
 
   void BuildHistogram(const data_size_t* idx, data_size_t n, double* hist) const;
+  void BuildHistogramRowWise(const data_size_t* idx, data_size_t n, double* hist) const;
+  void BuildHistogramColWise(const data_size_t* idx, data_size_t n, double* hist) const;
   void ComputeLeafSums(const data_size_t* idx, data_size_t n, double* sg, double* sh) const;
   SplitInfo BestSplitForFeature(const double* group_hist, int f, const LeafStat& leaf, double parent_output,
                                 const LeafBounds& bounds, const ThresholdBounds* tb, bool* splittable) const;
@@ -139,6 +141,15 @@ class SerialTreeLearner : public TreeLearner {
   std::vector<SplitInfo> best_split_per_leaf_;
   std::vector<std::vector<double>> hist_;            // per leaf, 2*num_total_bin
   mutable std::vector<std::vector<double>> tls_hist_;  // per-thread partial histograms (BuildHistogram)
+  // TrainingShareStates analogue (reference dataset.cpp TestMultiThreadingMethod,
+  // train_share_states.h): histogram threads split the leaf's ROWS (per-thread histograms,
+  // folded) or the feature GROUPS (over a column-major copy of the dense groups). Both sum
+  // the same row chunks and fold the chunk partials in the same order, so the choice never
+  // changes a model; force_col_wise / force_row_wise pin it, otherwise the first root
+  // histogram times both and keeps the faster.
+  enum class HistLayout { kAuto, kRowWise, kColWise };
+  mutable HistLayout hist_layout_ = HistLayout::kAuto;
+  mutable std::vector<uint8_t> colbins_;  // dense groups column-major (col-wise only)
   // histogram_pool_size: at most hist_cap_ leaf histograms live at once; the one
   // produced longest ago is dropped first (reference HistogramPool LRU,
   // feature_histogram.hpp:1367-1594)
