@@ -13,7 +13,7 @@ import json
 import os
 from copy import deepcopy
 from pathlib import Path
-from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple, Union
+from typing import Set, Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -183,6 +183,33 @@ def _aliases() -> Dict[str, List[str]]:
     if _ALIASES is None:
         _ALIASES = dump_param_aliases()
     return _ALIASES
+
+
+class _ConfigAliases:
+    """Parameter alias lookup (reference basic.py ``_ConfigAliases``), backed by the native
+    parameter table (``LGBM_DumpParamAliases``)."""
+
+    @staticmethod
+    def get(*args: str) -> Set[str]:
+        out: Set[str] = set()
+        for name in args:
+            out.add(name)
+            out.update(_aliases().get(name, []))
+        return out
+
+    @staticmethod
+    def get_sorted(name: str) -> List[str]:
+        return [name] + [a for a in _aliases().get(name, []) if a != name]
+
+    @staticmethod
+    def get_by_alias(*args: str) -> Set[str]:
+        out: Set[str] = set(args)
+        for arg in args:
+            for main, al in _aliases().items():
+                if arg == main or arg in al:
+                    out.add(main)
+                    out.update(al)
+        return out
 
 
 def _choose_param_value(main: str, params: Dict[str, Any], default: Any) -> Dict[str, Any]:

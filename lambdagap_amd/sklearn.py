@@ -11,7 +11,9 @@ from typing import Any, Callable, Dict, List, Optional, Union
 
 import numpy as np
 
-from .basic import Booster, Dataset, LightGBMError, _choose_param_value
+import warnings
+
+from .basic import Booster, Dataset, LightGBMError, _choose_param_value, _ConfigAliases
 from .callback import record_evaluation
 from .engine import train
 
@@ -129,6 +131,21 @@ class LGBMModel(BaseEstimator):
     def _process_params(self, stage: str) -> Dict[str, Any]:
         params = self.get_params()
         params.pop("objective", None)
+        # objective aliases given as keyword arguments win over `objective` (reference
+        # sklearn.py _process_params, with the same warning)
+        for alias in sorted(_ConfigAliases.get("objective") - {"objective"}):
+            if alias in params:
+                obj = params.pop(alias)
+                warnings.warn(f"Found '{alias}' in params. Will use it instead of 'objective' argument", UserWarning)
+                if stage == "fit":
+                    self._objective = obj
+        if hasattr(self, "_eval_at"):
+            eval_at = self._eval_at
+            for alias in sorted(_ConfigAliases.get("eval_at")):
+                if alias in params:
+                    warnings.warn(f"Found '{alias}' in params. Will use it instead of 'eval_at' argument", UserWarning)
+                    eval_at = params.pop(alias)
+            params["eval_at"] = eval_at
         for alias in ("class_weight", "importance_type", "n_estimators"):
             params.pop(alias, None)
         if isinstance(params.get("random_state"), np.random.RandomState):
@@ -148,6 +165,13 @@ class LGBMModel(BaseEstimator):
             out["objective"] = _ObjectiveFunctionWrapper(self._objective)
         else:
             out["objective"] = self._objective or self._default_objective()
+        # the default metric is registered explicitly (a custom objective still reports the
+        # estimator's natural metric: l2 / binary_logloss / multi_logloss / ndcg)
+        default_metric = out["objective"] if isinstance(out["objective"], str) else {
+            "regression": "l2", "binary": "binary_logloss", "multiclass": "multi_logloss",
+            "lambdarank": "ndcg"}.get(self._default_objective())
+        if default_metric is not None:
+            out = _choose_param_value("metric", out, default_metric)
         out.setdefault("verbosity", -1)
         return out
 
@@ -205,7 +229,10 @@ class LGBMModel(BaseEstimator):
                     vs = train_set.create_valid(vx, label=vy, weight=vw, group=_get(eval_group, i),
                                                 init_score=_get(eval_init_score, i), position=_get(eval_position, i))
                 valid_sets.append(vs)
-                names.append(eval_names[i] if eval_names is not None and i < len(eval_names) else f"valid_{i}")
+                if eval_names is not None and i < len(eval_names):
+                    names.append(eval_names[i])
+                else:  # the training data passed as an eval set is reported as "training"
+                    names.append("training" if vs is train_set else f"valid_{i}")
         self._evals_result = {}
         cbs = list(callbacks or [])
         cbs.append(record_evaluation(self._evals_result))
@@ -238,9 +265,19 @@ class LGBMModel(BaseEstimator):
         if hasattr(X, "shape") and X.shape[1] != self._n_features:
             raise ValueError(f"Number of features of the model must match the input. Model n_features_ is "
                              f"{self._n_features} and input n_features is {X.shape[1]}")
+        # constructor / set_params parameters reach prediction too (pred_early_stop, ...), those
+        # passed to predict() win (reference sklearn.py predict: _process_params("predict"))
+        predict_params = self._process_params("predict")
+        if not isinstance(predict_params.get("objective"), str):
+            predict_params.pop("objective", None)  # a custom objective: raw scores, nothing to pass
+        for alias in _ConfigAliases.get_by_alias("metric", "eval_at", "data", "X", "raw_score",
+                                                 "start_iteration", "num_iteration", "pred_leaf", "pred_contrib",
+                                                 *kwargs.keys()):
+            predict_params.pop(alias, None)
+        predict_params.update(kwargs)
         return self._Booster.predict(X, raw_score=raw_score, start_iteration=start_iteration,
                                      num_iteration=num_iteration, pred_leaf=pred_leaf, pred_contrib=pred_contrib,
-                                     validate_features=validate_features, **kwargs)
+                                     validate_features=validate_features, **predict_params)
 
     # ------------------------------------------------------------------ attributes
     def _check_fitted(self) -> None:
@@ -390,8 +427,8 @@ class LGBMClassifier(ClassifierMixin, LGBMModel):
                                  validate_features, **kwargs)
         if callable(self._objective) and not (raw_score or pred_leaf or pred_contrib):
             return result
-        if self._n_classes > 2 or raw_score or pred_leaf or pred_contrib:
-            return result
+        if self._n_classes > 2 or raw_score or pred_leaf or pred_contrib or np.ndim(result) == 2:
+            return result  # (a multiclass objective on two classes already gives both columns)
         return np.vstack((1.0 - result, result)).transpose()
 
     @property
@@ -423,7 +460,7 @@ class LGBMRanker(LGBMModel):
             n = 1 if isinstance(eval_set, tuple) else len(eval_set)
             if len(eval_group) != n:
                 raise ValueError("Length of eval_group should be equal to eval_set")
-        self._other_params["eval_at"] = list(eval_at)
+        self._eval_at = list(eval_at)
         return super().fit(X, y, sample_weight=sample_weight, init_score=init_score, group=group, eval_set=eval_set,
                            eval_names=eval_names, eval_sample_weight=eval_sample_weight,
                            eval_init_score=eval_init_score, eval_group=eval_group, eval_metric=eval_metric,

@@ -51,7 +51,7 @@ def test_ranker(lgb, rng):
     rk = lgb.LGBMRanker(n_estimators=20, verbose=-1, lambdarank_target="lambdagap-s", lambdagap_weight=0.5,
                         lambdarank_truncation_level=3)
     rk.fit(X, y, group=group, eval_set=[(X, y)], eval_group=[group], eval_at=[3, 5])
-    assert "ndcg@3" in rk.evals_result_["valid_0"]
+    assert "ndcg@3" in rk.evals_result_["training"]  # the training data as an eval set
     s = rk.predict(X)
     assert np.corrcoef(s, y)[0, 1] > 0.5
     with pytest.raises(ValueError):
