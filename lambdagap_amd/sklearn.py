@@ -128,6 +128,9 @@ class LGBMModel(BaseEstimator):
     def _default_objective(self) -> str:
         return "regression"
 
+    def __sklearn_is_fitted__(self) -> bool:
+        return getattr(self, "_Booster", None) is not None
+
     def _process_params(self, stage: str) -> Dict[str, Any]:
         params = self.get_params()
         params.pop("objective", None)
@@ -223,6 +226,8 @@ class LGBMModel(BaseEstimator):
 
                     vw = _get(eval_sample_weight, i)
                     vcw = _get(eval_class_weight, i)
+                    if isinstance(vcw, dict) and getattr(self, "_class_map", None) is not None:
+                        vcw = {self._class_map[k]: v for k, v in vcw.items()}  # original labels -> encoded
                     if vcw is not None:
                         cw = self._class_weight_from(vcw, vy)
                         vw = cw if vw is None else np.asarray(vw) * cw
@@ -233,6 +238,8 @@ class LGBMModel(BaseEstimator):
                     names.append(eval_names[i])
                 else:  # the training data passed as an eval set is reported as "training"
                     names.append("training" if vs is train_set else f"valid_{i}")
+        if isinstance(init_model, LGBMModel):
+            init_model = init_model.booster_
         self._evals_result = {}
         cbs = list(callbacks or [])
         cbs.append(record_evaluation(self._evals_result))
@@ -394,14 +401,19 @@ class LGBMClassifier(ClassifierMixin, LGBMModel):
                 else:
                     valid.append((vx, self._le.transform(vy)))
         if eval_metric is not None:
+            # binary / multiclass metric names follow the task (reference LGBMClassifier.fit): a
+            # multiclass objective stays multiclass even on two classes
+            multiclass = self._n_classes > 2 or (isinstance(self._objective, str) and self._objective in (
+                "multiclass", "softmax", "multiclassova", "multiclass_ova", "ova", "ovr"))
             metrics = eval_metric if isinstance(eval_metric, list) else [eval_metric]
             fixed = []
             for m in metrics:
-                if isinstance(m, str) and self._n_classes > 2:
+                if isinstance(m, str) and multiclass:
                     m = {"logloss": "multi_logloss", "binary_logloss": "multi_logloss", "error": "multi_error",
                          "binary_error": "multi_error"}.get(m, m)
                 elif isinstance(m, str):
-                    m = {"logloss": "binary_logloss", "error": "binary_error"}.get(m, m)
+                    m = {"logloss": "binary_logloss", "multi_logloss": "binary_logloss", "error": "binary_error",
+                         "multi_error": "binary_error"}.get(m, m)
                 fixed.append(m)
             eval_metric = fixed
         X_fit = X
