@@ -7,6 +7,7 @@ reference (python-package/lightgbm/sklearn.py:486 LGBMModel, :1314 regressor,
 from __future__ import annotations
 
 import copy
+import functools
 from typing import Any, Callable, Dict, List, Optional, Union
 
 import numpy as np
@@ -57,6 +58,23 @@ class _EvalFunctionWrapper:
         if argc == 3:
             return self.func(labels, preds, dataset.get_weight())
         return self.func(labels, preds, dataset.get_weight(), dataset.get_group())
+
+
+@functools.lru_cache(maxsize=None)
+def _cpu_count(physical: bool) -> int:
+    import joblib
+
+    return joblib.cpu_count(only_physical_cores=physical)
+
+
+def _ravel_column(y):
+    """A (n, 1) label is accepted with sklearn's column-vector warning and flattened."""
+    shape = getattr(y, "shape", None)
+    if shape is not None and len(shape) == 2 and shape[1] == 1:
+        warnings.warn("A column-vector y was passed when a 1d array was expected. Please change the shape of y "
+                      "to (n_samples,), for example using ravel().", UserWarning)
+        return np.asarray(y).ravel()
+    return y
 
 
 class LGBMModel(BaseEstimator):
@@ -160,10 +178,20 @@ class LGBMModel(BaseEstimator):
                    "reg_alpha": "lambda_l1", "reg_lambda": "lambda_l2", "random_state": "seed",
                    "n_jobs": "num_threads"}
         out: Dict[str, Any] = {}
+        n_jobs = params.pop("n_jobs", None)
         for k, v in params.items():
             if v is None:
                 continue
             out[mapping.get(k, k)] = v
+        # joblib conventions for n_jobs (None: physical cores, -k: all but k - 1 threads);
+        # an explicit num_threads alias wins (reference sklearn.py _process_n_jobs)
+        out = _choose_param_value("num_threads", out, n_jobs)
+        nt = out["num_threads"]
+        if nt is None:
+            nt = _cpu_count(True)
+        elif nt < 0:
+            nt = max(_cpu_count(False) + 1 + nt, 1)
+        out["num_threads"] = nt
         if callable(self._objective):
             out["objective"] = _ObjectiveFunctionWrapper(self._objective)
         else:
@@ -183,6 +211,7 @@ class LGBMModel(BaseEstimator):
             eval_sample_weight=None, eval_class_weight=None, eval_init_score=None, eval_group=None,
             eval_metric=None, feature_name="auto", categorical_feature="auto", callbacks=None,
             init_model=None, position=None, eval_position=None) -> "LGBMModel":
+        y = _ravel_column(y)
         params = self._process_params("fit")
         feval = None
         if eval_metric is not None:
@@ -270,13 +299,13 @@ class LGBMModel(BaseEstimator):
         if self._Booster is None:
             raise LightGBMError("Estimator not fitted, call fit before exploiting the model.")
         if hasattr(X, "shape") and X.shape[1] != self._n_features:
-            raise ValueError(f"Number of features of the model must match the input. Model n_features_ is "
-                             f"{self._n_features} and input n_features is {X.shape[1]}")
+            raise ValueError(f"X has {X.shape[1]} features, but {type(self).__name__} is expecting "
+                             f"{self._n_features} features as input")
         # constructor / set_params parameters reach prediction too (pred_early_stop, ...), those
         # passed to predict() win (reference sklearn.py predict: _process_params("predict"))
         predict_params = self._process_params("predict")
         if not isinstance(predict_params.get("objective"), str):
-            predict_params.pop("objective", None)  # a custom objective: raw scores, nothing to pass
+            predict_params["objective"] = "none"  # a custom objective: raw scores (num_class kept)
         for alias in _ConfigAliases.get_by_alias("metric", "eval_at", "data", "X", "raw_score",
                                                  "start_iteration", "num_iteration", "pred_leaf", "pred_contrib",
                                                  *kwargs.keys()):
@@ -376,6 +405,7 @@ class LGBMClassifier(ClassifierMixin, LGBMModel):
     def fit(self, X, y, sample_weight=None, init_score=None, eval_set=None, eval_names=None,
             eval_sample_weight=None, eval_class_weight=None, eval_init_score=None, eval_metric=None,
             feature_name="auto", categorical_feature="auto", callbacks=None, init_model=None):
+        y = _ravel_column(y)
         check_classification_targets(y)
         self._le = LabelEncoder().fit(y)
         y_enc = self._le.transform(y)

@@ -397,7 +397,8 @@ void Config::Set(const ParamMap& params) {
 
 void Config::CheckParamConflict(const ParamMap& params) {
   auto is_multi = [](const std::string& o) { return o == "multiclass" || o == "multiclassova"; };
-  bool obj_multi = is_multi(objective) || (objective == "custom" && num_class > 1);
+  const bool custom = objective == "custom" || objective == "none" || objective == "null" || objective == "na";
+  bool obj_multi = is_multi(objective) || (custom && num_class > 1);
   if (obj_multi) {
     if (num_class <= 1) Log::Fatal("Number of classes should be specified and greater than 1 for multiclass training");
   } else if (task == "train" && num_class != 1) {
