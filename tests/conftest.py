@@ -9,6 +9,9 @@ import pytest
 if os.environ.get("PYTEST_XDIST_WORKER") and "OMP_NUM_THREADS" not in os.environ:
     _n = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1"))
     os.environ["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // max(1, _n)))
+    # estimators that pin num_threads (sklearn n_jobs=None -> physical cores) still
+    # oversubscribe: idle OpenMP threads must sleep, not spin
+    os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
