@@ -624,8 +624,12 @@ class Dataset:
         ct = {C_API_DTYPE_FLOAT32: ctypes.c_float, C_API_DTYPE_FLOAT64: ctypes.c_double,
               C_API_DTYPE_INT32: ctypes.c_int32}[out_type.value]
         arr = np.ctypeslib.as_array(ctypes.cast(out_ptr, ctypes.POINTER(ct)), shape=(out_len.value,)).copy()
-        if field_name == "group":
-            return np.diff(arr)
+        if field_name == "init_score":
+            n = self.num_data()
+            if n > 0 and arr.size > n and arr.size % n == 0:  # multiclass: stored class-major
+                arr = arr.reshape(arr.size // n, n).T.copy()
+        # "group" is returned as query boundaries (reference basic.py get_field); get_group()
+        # gives the sizes
         return arr
 
     def set_label(self, label: Any) -> "Dataset":
@@ -634,6 +638,7 @@ class Dataset:
             if pd is not None and isinstance(label, (pd.Series, pd.DataFrame)):
                 label = np.asarray(label).ravel()
             self.set_field("label", label)
+            self.label = self.get_field("label")  # the stored (float32) values
         return self
 
     def set_weight(self, weight: Any) -> "Dataset":
@@ -642,12 +647,14 @@ class Dataset:
         self.weight = weight
         if self.handle is not None and weight is not None:
             self.set_field("weight", weight)
+            self.weight = self.get_field("weight")
         return self
 
     def set_init_score(self, init_score: Any) -> "Dataset":
         self.init_score = init_score
         if self.handle is not None and init_score is not None:
             self.set_field("init_score", init_score)
+            self.init_score = self.get_field("init_score")
         return self
 
     def set_group(self, group: Any) -> "Dataset":
@@ -679,7 +686,8 @@ class Dataset:
 
     def get_group(self):
         if self.group is None and self.handle is not None:
-            self.group = self.get_field("group")
+            b = self.get_field("group")
+            self.group = None if b is None else np.diff(b)
         return self.group
 
     def get_position(self):

@@ -1305,9 +1305,17 @@ int LGBM_DatasetSetFieldFromArrow(DatasetHandle handle, const char* field_name, 
                                   const struct ArrowArray* chunks, const struct ArrowSchema* schema) {
   API_BEGIN();
   ArrowTable table(n_chunks, chunks, schema);
-  if (table.num_columns() != 1) Log::Fatal("Arrow field %s must have exactly one column", field_name);
-  const std::vector<double> v = table.Column(0);
   const std::string name(field_name);
+  // a multi-column table is accepted for init_score only: one column per class, which is
+  // the class-major layout the field stores
+  if (table.num_columns() != 1 && !(name == "init_score" && table.num_columns() > 1)) {
+    Log::Fatal("Arrow field %s must have exactly one column", field_name);
+  }
+  std::vector<double> v;
+  for (int c = 0; c < table.num_columns(); ++c) {
+    const std::vector<double> col = table.Column(c);
+    v.insert(v.end(), col.begin(), col.end());
+  }
   if (name == "group" || name == "query" || name == "position") {
     std::vector<int32_t> iv(v.begin(), v.end());
     if (LGBM_DatasetSetField(handle, field_name, iv.data(), static_cast<int>(iv.size()), C_API_DTYPE_INT32) != 0) {

@@ -69,10 +69,7 @@ void Metadata::SetWeights(const float* w, data_size_t len) {
     return;
   }
   if (len != num_data_) Log::Fatal("Length of weights is not same with #data");
-  weights_.assign(w, w + len);
-  for (auto v : weights_) {
-    if (v < 0 || std::isnan(v)) Log::Fatal("Weights should be non-negative");
-  }
+  weights_.assign(w, w + len);  // no sign check: the reference's SetWeights takes any value
   CalcQueryWeights();
 }
 

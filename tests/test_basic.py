@@ -46,7 +46,8 @@ def test_dataset_group_and_position(lgb, rng):
     X = rng.standard_normal((60, 3))
     y = rng.integers(0, 3, 60)
     ds = lgb.Dataset(X, y, group=[10, 20, 30], position=np.arange(60) % 5).construct()
-    np.testing.assert_array_equal(ds.get_field("group"), [10, 20, 30])
+    np.testing.assert_array_equal(ds.get_field("group"), [0, 10, 30, 60])  # boundaries
+    np.testing.assert_array_equal(ds.get_group(), [10, 20, 30])
     np.testing.assert_array_equal(ds.get_field("position"), np.arange(60) % 5)
 
 
