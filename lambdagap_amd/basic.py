@@ -847,9 +847,57 @@ class Dataset:
         return self
 
     def add_features_from(self, other: "Dataset") -> "Dataset":
-        self.construct()
-        other.construct()
+        """Append other's feature columns (both constructed; reference basic.py
+        add_features_from). Raw data is merged where the two types allow it, else freed."""
+        if self.handle is None or other.handle is None:
+            raise ValueError("Both source and target Datasets must be constructed before adding features")
         _check(_LIB.LGBM_DatasetAddFeaturesFrom(self.handle, other.handle))
+        was_none = self.data is None
+        old_type = type(self.data).__name__
+        od = other.data
+        if od is None or _is_path(od):
+            self.data = None
+        elif self.data is not None:
+            import scipy.sparse as _sp
+
+            sd = self.data
+            if isinstance(sd, np.ndarray):
+                if isinstance(od, np.ndarray):
+                    self.data = np.hstack((sd, od))
+                elif _sp.issparse(od):
+                    self.data = np.hstack((sd, od.toarray()))
+                elif _is_pandas(od):
+                    self.data = np.hstack((sd, od.values))
+                else:
+                    self.data = None
+            elif _sp.issparse(sd):
+                fmt = sd.getformat()
+                if isinstance(od, np.ndarray) or _sp.issparse(od):
+                    self.data = _sp.hstack((sd, od), format=fmt)
+                elif _is_pandas(od):
+                    self.data = _sp.hstack((sd, od.values), format=fmt)
+                else:
+                    self.data = None
+            elif _is_pandas(sd):
+                if isinstance(od, np.ndarray):
+                    self.data = pd.concat((sd, pd.DataFrame(od)), axis=1, ignore_index=True)
+                elif _sp.issparse(od):
+                    self.data = pd.concat((sd, pd.DataFrame(od.toarray())), axis=1, ignore_index=True)
+                elif _is_pandas(od):
+                    self.data = pd.concat((sd, od), axis=1, ignore_index=True)
+                else:
+                    self.data = None
+            else:
+                self.data = None
+        if self.data is None:
+            msg = (f"Cannot add features from {type(od).__name__} type of raw data to {old_type} type of raw data.\n")
+            msg += "Set free_raw_data=False when construct Dataset to avoid this" if was_none else "Freeing raw data"
+            _log_warning(msg)
+        self.feature_name = self.get_feature_name()
+        _log_warning("Reseting categorical features.\n"
+                     "You can set new categorical features via ``set_categorical_feature`` method")
+        self.categorical_feature = "auto"
+        self.pandas_categorical = None
         return self
 
     def _update_params(self, params: Optional[Dict[str, Any]]) -> "Dataset":

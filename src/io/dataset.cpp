@@ -707,9 +707,18 @@ void Dataset::AddFeaturesFrom(const Dataset& o) {
   const int old_groups = num_groups();
   const int old_stride = row_stride_;
   const int old_width = bin_width_;
+  std::set<std::string> taken(feature_names_.begin(), feature_names_.end());
   for (int j = 0; j < o.num_total_features_; ++j) {
     mappers_.push_back(o.mappers_[j]);
-    feature_names_.push_back(o.feature_names_[j]);
+    // a clashing name becomes D<k>_<name> with the first free k >= 2 (as the reference)
+    std::string name = o.feature_names_[j];
+    for (int k = 2; taken.count(name); ++k) name = "D" + std::to_string(k) + "_" + o.feature_names_[j];
+    if (name != o.feature_names_[j]) {
+      Log::Warning("Find the same feature name (%s) in Dataset::AddFeaturesFrom, change its name to (%s)",
+                   o.feature_names_[j].c_str(), name.c_str());
+    }
+    taken.insert(name);
+    feature_names_.push_back(name);
     used_map_.push_back(o.used_map_[j] < 0 ? -1 : o.used_map_[j] + static_cast<int>(features_.size()));
   }
   const int fbase = static_cast<int>(features_.size());
