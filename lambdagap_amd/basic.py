@@ -98,7 +98,7 @@ def register_logger(logger: Any, info_method_name: str = "info", warning_method_
     global _LOGGER
     for name in (info_method_name, warning_method_name):
         if not callable(getattr(logger, name, None)):
-            raise TypeError(f"Logger must provide '{name}' method")
+            raise TypeError(f"Logger must provide '{info_method_name}' and '{warning_method_name}' method")
 
     class _Wrap:
         def info(self, m):

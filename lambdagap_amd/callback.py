@@ -9,6 +9,8 @@ from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Tuple, Union
 
+from .basic import _log_info
+
 __all__ = ["EarlyStopException", "CallbackEnv", "early_stopping", "log_evaluation", "record_evaluation",
            "reset_parameter"]
 
@@ -54,7 +56,7 @@ class _LogEvaluation:
     def __call__(self, env: CallbackEnv) -> None:
         if self.period > 0 and env.evaluation_result_list and (env.iteration + 1) % self.period == 0:
             msg = "\t".join(_format_eval(x, self.show_stdv) for x in env.evaluation_result_list)
-            print(f"[{env.iteration + 1}]\t{msg}", flush=True)
+            _log_info(f"[{env.iteration + 1}]\t{msg}")
 
 
 def log_evaluation(period: int = 1, show_stdv: bool = True) -> Callable:
@@ -197,7 +199,7 @@ class _EarlyStopping:
                 self.cmp_op.append(lambda cur, best, d=delta: cur < best - d)
             self.best_score_list.append(None)
         if self.verbose:
-            print(f"Training until validation scores don't improve for {self.stopping_rounds} rounds", flush=True)
+            _log_info(f"Training until validation scores don't improve for {self.stopping_rounds} rounds")
 
     def _is_train_set(self, data_name: str, env: CallbackEnv) -> bool:
         model = env.model
@@ -226,13 +228,12 @@ class _EarlyStopping:
             if env.iteration - self.best_iter[i] >= self.stopping_rounds:
                 if self.verbose:
                     msg = "\t".join(_format_eval(x, True) for x in self.best_score_list[i])
-                    print(f"Early stopping, best iteration is:\n[{self.best_iter[i] + 1}]\t{msg}", flush=True)
+                    _log_info(f"Early stopping, best iteration is:\n[{self.best_iter[i] + 1}]\t{msg}")
                 raise EarlyStopException(self.best_iter[i], self.best_score_list[i])
             if env.iteration == env.end_iteration - 1:
                 if self.verbose:
                     msg = "\t".join(_format_eval(x, True) for x in self.best_score_list[i])
-                    print(f"Did not meet early stopping. Best iteration is:\n[{self.best_iter[i] + 1}]\t{msg}",
-                          flush=True)
+                    _log_info(f"Did not meet early stopping. Best iteration is:\n[{self.best_iter[i] + 1}]\t{msg}")
                 raise EarlyStopException(self.best_iter[i], self.best_score_list[i])
 
 

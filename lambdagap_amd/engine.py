@@ -133,7 +133,9 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
         for c in before:
             c(cb.CallbackEnv(model=booster, params=params, iteration=i, begin_iteration=init_iteration,
                              end_iteration=init_iteration + num_boost_round, evaluation_result_list=None))
-        finished = booster.update(fobj=fobj)
+        # like the reference, a finished update (no split possible) does not end the loop:
+        # later iterations retry, evaluate and run the callbacks
+        booster.update(fobj=fobj)
         evaluation_result_list = []
         if valid_sets or feval is not None:
             if is_valid_contain_train:
@@ -147,8 +149,6 @@ def train(params: Dict[str, Any], train_set: Dataset, num_boost_round: int = 100
         except cb.EarlyStopException as e:
             booster.best_iteration = e.best_iteration + 1
             evaluation_result_list = e.best_score
-            break
-        if finished:
             break
     booster.best_score = defaultdict(OrderedDict)
     for item in evaluation_result_list:
