@@ -5,6 +5,8 @@ matplotlib draws importance / split histograms / metric curves / trees;
 """
 from __future__ import annotations
 
+import math
+
 from copy import deepcopy
 from typing import Any, Dict, List, Optional, Tuple, Union
 
@@ -228,35 +230,110 @@ def plot_tree(booster: Any, ax=None, tree_index: int = 0, figsize=None, dpi=None
     return ax
 
 
+_ZERO_THRESHOLD = 1e-35
+
+
+def _determine_direction_for_numeric_split(fval: float, threshold: float, missing_type_str: str,
+                                           default_left: bool) -> str:
+    """Which child a value takes at a numerical split: the tree's decision rule (NaN is
+    zero unless the split tracks NaN; the tracked missing value follows default_left)."""
+    if math.isnan(fval) and missing_type_str != "NaN":
+        fval = 0.0
+    if (missing_type_str == "Zero" and abs(fval) <= _ZERO_THRESHOLD) or (
+            missing_type_str == "NaN" and math.isnan(fval)):
+        return "left" if default_left else "right"
+    return "left" if fval <= threshold else "right"
+
+
+def _determine_direction_for_categorical_split(fval: float, thresholds: str) -> str:
+    """Categories listed in the split ("a||b||c") go left; NaN and negatives go right."""
+    if math.isnan(fval) or int(fval) < 0:
+        return "right"
+    return "left" if int(fval) in {int(t) for t in str(thresholds).split("||")} else "right"
+
+
 def create_tree_digraph(booster: Any, tree_index: int = 0, show_info=None, precision: Optional[int] = 3,
                         orientation: str = "horizontal", example_case=None, max_category_values: int = 10,
                         **kwargs: Any):
-    """graphviz.Digraph of one tree (requires the optional graphviz package)."""
-    try:
-        from graphviz import Digraph
-    except ImportError as e:
-        raise ImportError("You must install graphviz and restart your session to plot tree.") from e
+    """graphviz.Digraph of one tree (requires the optional graphviz package), reference
+    plotting.py create_tree_digraph: ``show_info`` adds split_gain / internal_value /
+    internal_count / internal_weight / leaf_count / leaf_weight / data_percentage, an
+    ``example_case`` row is traced in blue, categorical splits list at most
+    ``max_category_values`` categories."""
     b = _booster_of(booster)
     model = b.dump_model()
     trees = model["tree_info"]
     if tree_index >= len(trees):
         raise IndexError("tree_index is out of range.")
     names = model.get("feature_names", [])
+    monotone = model.get("monotone_constraints") or []
+    show_info = list(show_info or [])
+    if example_case is not None:
+        try:
+            import pandas as pd
+        except ImportError:  # pragma: no cover
+            pd = None
+        is_df = pd is not None and isinstance(example_case, pd.DataFrame)
+        if not (isinstance(example_case, np.ndarray) or is_df) or example_case.ndim != 2:
+            raise ValueError("example_case must be a numpy array or a pandas DataFrame")
+        if example_case.shape[0] != 1:
+            raise ValueError("example_case must have a single row.")
+        example_case = np.asarray(example_case.to_numpy(dtype=np.float64) if is_df else example_case,
+                                  dtype=np.float64)[0]
+    try:
+        from graphviz import Digraph
+    except ImportError as e:
+        raise ImportError("You must install graphviz and restart your session to plot tree.") from e
+    total_count = trees[tree_index]["tree_structure"].get("internal_count", 0) or 1
     graph = Digraph(**kwargs)
     graph.attr("graph", nodesep="0.05", ranksep="0.3", rankdir="LR" if orientation == "horizontal" else "TB")
 
-    def add(node, parent=None, decision=None):
+    def fmt(v):
+        return f"{v:.{precision}f}" if precision is not None and isinstance(v, float) else str(v)
+
+    def add(node, parent=None, decision=None, highlight=False):
         if "split_index" in node:
             name = f"split{node['split_index']}"
             f = node["split_feature"]
-            graph.node(name, label=f"{names[f] if f < len(names) else f} <= {node['threshold']}")
-            add(node["left_child"], name, "yes")
-            add(node["right_child"], name, "no")
+            fname = names[f] if f < len(names) else f"feature_{f}"
+            if node["decision_type"] == "<=":
+                lte = "&#8804;"
+                label = f"<B>{fname}</B> {lte} {fmt(node['threshold'])}"
+                direction = None
+                if example_case is not None and highlight:
+                    direction = _determine_direction_for_numeric_split(example_case[f], node["threshold"],
+                                                                       node["missing_type"], node["default_left"])
+            else:
+                cats = str(node["threshold"]).split("||")
+                shown = "||".join(cats[:max_category_values]) + ("||...||" + cats[-1]
+                                                                  if len(cats) > max_category_values else "")
+                label = f"<B>{fname}</B> in {shown}"
+                direction = None
+                if example_case is not None and highlight:
+                    direction = _determine_direction_for_categorical_split(example_case[f], node["threshold"])
+            if f < len(monotone) and monotone[f] != 0:
+                label += " (increasing)" if monotone[f] > 0 else " (decreasing)"
+            for info in ("split_gain", "internal_value", "internal_weight", "internal_count"):
+                if info in show_info and info in node:
+                    label += f"<br/>{info.split('_')[-1]}: {fmt(node[info])}"
+            if "data_percentage" in show_info:
+                label += f"<br/>{node.get('internal_count', 0) / total_count:.2%} of data"
+            color = "blue" if highlight and example_case is not None else "black"
+            graph.node(name, label=f"<{label}>", shape="rectangle", color=color)
+            add(node["left_child"], name, "yes", highlight and direction == "left")
+            add(node["right_child"], name, "no", highlight and direction == "right")
         else:
             name = f"leaf{node.get('leaf_index', 0)}"
-            graph.node(name, label=f"leaf {node.get('leaf_index', 0)}: {node['leaf_value']:.{precision or 3}f}")
+            label = f"leaf {node.get('leaf_index', 0)}: <B>{fmt(node['leaf_value'])}</B>"
+            for info in ("leaf_weight", "leaf_count"):
+                if info in show_info and info in node:
+                    label += f"<br/>{info.split('_')[-1]}: {fmt(node[info])}"
+            if "data_percentage" in show_info:
+                label += f"<br/>{node.get('leaf_count', 0) / total_count:.2%} of data"
+            color = "blue" if highlight and example_case is not None else "black"
+            graph.node(name, label=f"<{label}>", color=color)
         if parent is not None:
-            graph.edge(parent, name, decision)
+            graph.edge(parent, name, decision, color="blue" if highlight and example_case is not None else "black")
 
-    add(trees[tree_index]["tree_structure"])
+    add(trees[tree_index]["tree_structure"], highlight=True)
     return graph
