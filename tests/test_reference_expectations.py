@@ -2145,3 +2145,25 @@ def test_objective_callable_regression(lgb, use_cv):
     for cb in res["cvbooster"].boosters:
         assert cb.params["objective"] == "none"
         assert mean_squared_error(y, cb.predict(X)) < 463
+
+
+def test_missing_value_handle_more_na():
+    """test_engine.py::test_missing_value_handle_more_na: 80 % NaN rows of a constant
+    column are learned apart from the rest (l2 < 0.005 after 20 rounds, no average boost)."""
+    import random
+
+    import lambdagap_amd as lgb
+    from sklearn.metrics import mean_squared_error
+
+    X_train = np.ones((100, 1))
+    y_train = np.ones(100)
+    for idx in random.Random(0).sample(range(100), 80):
+        X_train[idx, 0] = np.nan
+        y_train[idx] = 0
+    evals_result = {}
+    gbm = lgb.train({"metric": "l2", "verbose": -1, "boost_from_average": False}, lgb.Dataset(X_train, y_train),
+                    num_boost_round=20, valid_sets=lgb.Dataset(X_train, y_train),
+                    callbacks=[lgb.record_evaluation(evals_result)])
+    ret = mean_squared_error(y_train, gbm.predict(X_train))
+    assert ret < 0.005
+    assert evals_result["valid_0"]["l2"][-1] == pytest.approx(ret)
