@@ -143,6 +143,14 @@ class LGBMModel(BaseEstimator):
     def _more_tags(self) -> Dict[str, Any]:
         return {"allow_nan": True, "X_types": ["2darray", "sparse", "1dlabels"]}
 
+    def __sklearn_tags__(self):
+        """scikit-learn >= 1.6 tags (the same facts as ``_more_tags``)."""
+        tags = super().__sklearn_tags__()
+        tags.input_tags.allow_nan = True
+        tags.input_tags.sparse = True
+        tags.target_tags.one_d_labels = True
+        return tags
+
     def _default_objective(self) -> str:
         return "regression"
 
@@ -402,6 +410,13 @@ class LGBMClassifier(ClassifierMixin, LGBMModel):
     def _default_objective(self) -> str:
         return "binary" if self._n_classes <= 2 else "multiclass"
 
+    def __sklearn_tags__(self):
+        tags = super().__sklearn_tags__()
+        if tags.classifier_tags is not None:
+            tags.classifier_tags.multi_class = True
+            tags.classifier_tags.multi_label = False
+        return tags
+
     def fit(self, X, y, sample_weight=None, init_score=None, eval_set=None, eval_names=None,
             eval_sample_weight=None, eval_class_weight=None, eval_init_score=None, eval_metric=None,
             feature_name="auto", categorical_feature="auto", callbacks=None, init_model=None):
@@ -414,12 +429,16 @@ class LGBMClassifier(ClassifierMixin, LGBMModel):
             self._class_weight = {self._class_map[k]: v for k, v in self.class_weight.items()}
         self._classes = self._le.classes_
         self._n_classes = len(self._classes)
-        if self._n_classes > 2:
+        # num_class follows the classes of THIS fit: a value set by an earlier fit is dropped
+        prev = getattr(self, "_auto_num_class", None)
+        if prev is not None and self._other_params.get("num_class") == prev:
+            self._other_params.pop("num_class", None)
+        self._auto_num_class = None
+        multiclass_obj = not callable(self._objective) and self._objective is not None and str(self._objective) in (
+            "multiclass", "softmax", "multiclassova", "multiclass_ova", "ova", "ovr")
+        if self._n_classes > 2 or multiclass_obj:
             self._other_params["num_class"] = self._n_classes
-        if not callable(self._objective) and self._objective is not None:
-            obj = str(self._objective)
-            if obj in ("multiclass", "softmax", "multiclassova", "multiclass_ova", "ova", "ovr"):
-                self._other_params["num_class"] = self._n_classes
+            self._auto_num_class = self._n_classes
         valid = None
         if eval_set is not None:
             if isinstance(eval_set, tuple):

@@ -225,3 +225,32 @@ def test_predict_rejects_inputs_with_incorrect_number_of_features(predict_disabl
     assert model.predict(X[:, :-1], predict_disable_shape_check=predict_disable_shape_check).shape == y.shape
     if name == "LGBMClassifier":
         assert model.predict_proba(X[:, :-1], predict_disable_shape_check=predict_disable_shape_check).shape[0] == len(y)
+
+
+@pytest.mark.parametrize("estimator_class", ESTIMATORS)
+def test_sklearn_tags_should_correctly_reflect_lightgbm_specific_values(estimator_class):
+    est = estimator_class()
+    assert est._more_tags()["X_types"] == ["2darray", "sparse", "1dlabels"]
+    tags = est.__sklearn_tags__()  # scikit-learn >= 1.6 here
+    assert tags.input_tags.allow_nan is True
+    assert tags.input_tags.sparse is True
+    assert tags.target_tags.one_d_labels is True
+    if estimator_class is lgb.LGBMClassifier:
+        assert tags.estimator_type == "classifier"
+        assert tags.classifier_tags.multi_class is True
+        assert tags.classifier_tags.multi_label is False
+    elif estimator_class is lgb.LGBMRegressor:
+        assert tags.estimator_type == "regressor"
+
+
+def test_classifier_fit_detects_classes_every_time():
+    rng = np.random.default_rng(seed=123)
+    X = rng.standard_normal(size=(1000, 20))
+    y_bin = (rng.random(size=1000) <= 0.3).astype(np.float64)
+    y_multi = rng.integers(4, size=1000)
+    model = lgb.LGBMClassifier(verbose=-1)
+    for _ in range(2):
+        model.fit(X, y_multi)
+        assert model.objective_ == "multiclass"
+        model.fit(X, y_bin)
+        assert model.objective_ == "binary"
