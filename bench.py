@@ -54,18 +54,28 @@ def main() -> int:
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world == 1 and args.gpus > 1 and "RANK" not in os.environ:
+        # `python bench.py --gpus N` outside torchrun: launch the N rank processes here, before
+        # this process touches the GPU, and relay their output (rank 0 prints the JSON line)
+        return _spawn_ranks(args.gpus)
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: --gpus N>1 must be launched with torchrun (one process per GPU)", file=sys.stderr)
-            return 2
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
 
     import lambdagap_amd as lgb
     from lambdagap_amd.parallel import device_synchronize, init_device_comm, shard_range
     from lambdagap_amd.utils import make_higgs_like
 
     dist = None
-    if world > 1 and args.dp_host_transport:
+    if world > 1 and args.device == "cpu":
+        # host learners: data-parallel over the torch (gloo) collectives
+        import torch.distributed as dist  # noqa: F811
+
+        from lambdagap_amd.parallel.torch_network import init_torch_network
+
+        dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+        init_torch_network()
+    elif world > 1 and args.dp_host_transport:
         import torch.distributed as dist  # noqa: F811
 
         from lambdagap_amd.parallel.torch_network import init_torch_network
@@ -161,7 +171,7 @@ def main() -> int:
                 "parallelism": f"dp{world}",
                 "device": booster.device_name(),
                 "setup_s": round(t_data, 2),
-                "transport": ("host-staged (rehearsal)" if args.dp_host_transport else "rccl") if world > 1 else None,
+                "transport": _transport(booster.device_name(), args) if world > 1 else None,
             },
         }
         print(json.dumps(out), flush=True)
@@ -170,7 +180,7 @@ def main() -> int:
         # group (left to static destructors, gloo's threads can abort the exiting process)
         dist.barrier()
         del booster, train_set
-        if args.dp_host_transport:
+        if args.dp_host_transport or args.device == "cpu":
             from lambdagap_amd.parallel.torch_network import free_torch_network
 
             free_torch_network()
@@ -181,6 +191,31 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _spawn_ranks(n: int) -> int:
+    """Run this benchmark as N ranks under torch.distributed.run (one process per GPU)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _transport(device_name: str, args) -> str:
+    """The exchange the learner actually selected (from its device_name())."""
+    if args.device == "cpu":
+        return "gloo (host collectives)"
+    if "xGMI" in device_name:
+        return "xgmi (in-kernel IPC exchange)"
+    if "host-staged" in device_name or args.dp_host_transport:
+        return "host-staged (rehearsal)"
+    return "rccl"
 
 
 def _auc(y: np.ndarray, p: np.ndarray) -> float:

@@ -41,6 +41,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -49,7 +50,9 @@
 #include "device/hip_common.h"
 #include "device/leaf_kernels.h"
 #include "device/runtime_internal.h"
+#include "device/frontier.h"
 #include "device/sample_kernels.h"
+#include "device/split_scan.h"
 #include "device/tree_kernels.h"
 #include "learner/serial_tree_learner.h"
 #include "lgap/common.h"
@@ -79,10 +82,6 @@ constexpr int kPartThreads = 256;
 constexpr int kPartIters = 16;  // rows per thread of the two-kernel partition (k_part_count / k_part_scatter)
 constexpr int kTileRows = kPartThreads * kPartIters;
 constexpr int kScanWaves = 4;
-#ifndef LGAP_SCAN_K
-#define LGAP_SCAN_K 2
-#endif
-constexpr int kScanK = LGAP_SCAN_K;  // consecutive bins per lane in the numerical threshold scan
 #ifndef LGAP_SCAN_FOLD
 #define LGAP_SCAN_FOLD 1  // 1: half-wave row streams, one value per lane; 2: quarter-wave streams, value pairs
 #endif
@@ -96,7 +95,7 @@ struct Args {
   const uint32_t* rowbins;
   const uint8_t* colbins;
   const float2* gh;
-  int* idx[3];
+  int* idx[5];  // 0/1 ping-pong (frontier: depth buffers 0, 1), 2 bag, 3/4 frontier depth buffers 2, 3
   int N, stride_dw, width, num_groups, TB, F, L, max_tiles;
   const int* gstart;
   const DevFeature* feat;
@@ -199,30 +198,6 @@ __device__ __forceinline__ SplitInfo* CandInfoPos(const Args& a, int sel, int po
 // ---------------------------------------------------------------------------
 // small device helpers
 
-__device__ __forceinline__ uint32_t DecodeBin(int offset, int num_bin, int mfb, uint32_t gb) {
-  const int local = static_cast<int>(gb) - offset;
-  if (local < 0 || local >= num_bin - 1) return static_cast<uint32_t>(mfb);
-  return static_cast<uint32_t>(local < mfb ? local : local + 1);
-}
-
-struct SplitDesc {
-  int group, offset, num_bin, mfb, default_bin, missing, thr, default_left, is_cat;
-  uint32_t bits[kMaxCatWords];
-};
-
-__device__ __forceinline__ bool GoLeft(const SplitDesc& d, uint32_t gb) {
-  const uint32_t b = DecodeBin(d.offset, d.num_bin, d.mfb, gb);
-  if (d.is_cat) {
-    const uint32_t w = b >> 5;
-    return w < static_cast<uint32_t>(kMaxCatWords) && ((d.bits[w] >> (b & 31u)) & 1u);
-  }
-  if ((d.missing == 1 && b == static_cast<uint32_t>(d.default_bin)) ||
-      (d.missing == 2 && b == static_cast<uint32_t>(d.num_bin - 1))) {
-    return d.default_left != 0;
-  }
-  return b <= static_cast<uint32_t>(d.thr);
-}
-
 __device__ __forceinline__ uint32_t ColBin(const Args& a, int g, int row) {
   const size_t o = static_cast<size_t>(g) * a.N + row;
   return a.width == 1 ? a.colbins[o] : reinterpret_cast<const uint16_t*>(a.colbins)[o];
@@ -247,39 +222,6 @@ __device__ __forceinline__ void StampEnd(const Args& a, int kernel) {
 // A stamp of a given block role (slot 0) for a given split, with an explicit clock value.
 __device__ __forceinline__ void StampAt(const Args& a, int kernel, int split, int i, unsigned long long v) {
   if (a.stamps != nullptr && threadIdx.x == 0) a.stamps[((static_cast<size_t>(kernel) * 256 + (split & 255)) * 2) * 8 + i] = v;
-}
-
-// block = 256 threads: sum of an int
-__device__ int BlockSumInt(int v, int* sh) {
-  v = WaveSum(v);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[w] = v;
-  __syncthreads();
-  int s = 0;
-  for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) s += sh[i];
-  return s;
-}
-
-__device__ __forceinline__ double SafeGain(const SplitInfo& s) {
-  double g = s.gain;
-  if (g != g) g = kMinScore;
-  return s.feature < 0 ? kMinScore : g;
-}
-
-__device__ __forceinline__ unsigned LcgNext(unsigned* x) {
-  *x = 214013u * *x + 2531011u;
-  return *x;
-}
-__device__ __forceinline__ int RandNextInt(unsigned* x, int lo, int hi) {
-  const int v = static_cast<int>(LcgNext(x) & 0x7FFFFFFFu);
-  return v % (hi - lo) + lo;
-}
-
-__device__ double MonotonePenaltyAt(double pen, int depth) {
-  if (pen >= depth + 1.0) return kEpsilon;
-  if (pen <= 1.0) return 1.0 - pen / pow(2.0, static_cast<double>(depth)) + kEpsilon;
-  return 1.0 - pow(2.0, pen - 1.0 - depth) + kEpsilon;
 }
 
 // ---------------------------------------------------------------------------
@@ -489,13 +431,6 @@ __global__ __launch_bounds__(kRootThreads) void k_root_final(Args a, int nblocks
 // Each active block unpacks its LDS histogram to real values and stores it into
 // its own slab row (plain coalesced stores); k_hist_reduce sums the rows into
 // `staging` (fp64). No float atomics anywhere on the hot path.
-
-// largest power of two <= x (x > 0)
-__device__ __forceinline__ double Pow2AtMost(double x) {
-  int e;
-  (void)frexp(x, &e);  // x = m * 2^e, m in [0.5, 1)
-  return ldexp(1.0, e - 1);
-}
 
 __device__ __forceinline__ int HistActiveBlocks(int n, int grid, int min_rows) {
   int nb = (n + min_rows - 1) / min_rows;
@@ -908,410 +843,6 @@ __global__ __launch_bounds__(256) void k_x_selfcheck(Args a, int round, int nval
   if (bad) atomicAdd(err, bad);
 }
 
-// ---------------------------------------------------------------------------
-// split finding: one workgroup per feature (k_reduce_scan)
-
-struct Cand {
-  double gain, lg, lh;
-  int lc, thr;
-};
-
-// wave argmax; prefer_high: ties go to the larger threshold
-__device__ __forceinline__ Cand WaveBest(Cand c, bool prefer_high) {
-  const int src = WaveArgBestLane(c.gain, prefer_high ? -c.thr : c.thr, 0);
-  Cand r;
-  r.gain = ReadLane(c.gain, src);
-  r.thr = ReadLane(c.thr, src);
-  r.lg = ReadLane(c.lg, src);
-  r.lh = ReadLane(c.lh, src);
-  r.lc = ReadLane(c.lc, src);
-  return r;
-}
-
-// Numerical threshold search of one wave over a FULL feature histogram H
-// (LDS, num_bin (g, h) pairs, most-frequent bin included). Same semantics as
-// FindBestNumerical (split_math.h / feature_histogram.hpp:830-1057): reverse
-// pass (right side grows from the top bin) and, with missing values, the
-// forward pass; SKIP_DEFAULT_BIN / NA_AS_MISSING as masks; first-max tie rules.
-// Returns splittable; lane 0's `out` holds the result.
-__device__ bool ScanNumericalWave(const Args& a, const DevFeature& fi, const double* H, double sg, double sh_raw,
-                                  int n, double po, const LeafBounds& bounds, int rand_thr, SplitInfo* out) {
-  const int lane = threadIdx.x & 63;
-  const SplitParams& p = a.sp;
-  const double sum_h = sh_raw + 2 * kEpsilon;
-  const double cnt_factor = n / sum_h;
-  const double shift = LeafGain(sg, sum_h, p, n, po) + p.min_gain_to_split;
-  const int nb = fi.num_bin;
-  const bool two_dir = nb > 2 && fi.missing != 0;
-  const bool skip_def = two_dir && fi.missing == 1;
-  const bool na = two_dir && fi.missing == 2;
-  const int top = nb - 1 - (na ? 1 : 0);
-  const bool use_rand = p.extra_trees != 0;
-  const int8_t mono = fi.monotone;
-  // Each lane owns kScanK consecutive positions of a 64 * kScanK chunk: a serial
-  // prefix over its own bins, ONE wave scan of the lane totals per chunk, then the
-  // kScanK thresholds are evaluated independently (one 256-bin chunk covers max_bin
-  // 255: one wave scan per pass instead of four). Position order = scan order; within
-  // a lane the first (strict >) best is kept, across lanes WaveBest applies the same
-  // tie rule, so the winner is the scan's first maximum as in the host scan.
-  constexpr int K = kScanK;
-  Cand rb;
-  rb.gain = kMinScore;
-  rb.thr = -1;
-  rb.lg = rb.lh = 0.0;
-  rb.lc = 0;
-  bool sp = false;
-  double cg = 0.0, ch = 0.0;
-  int cc = 0;
-  // An empty bin leaves the prefix unchanged: the threshold after it has the same partition
-  // and gain as the one before, and the host scan keeps the first of such exact ties. The
-  // parallel prefix may round the two positions differently, so empty-bin positions after
-  // the first evaluated one are skipped (the host rule, independent of summation order).
-  const int first_rev = (skip_def && top == fi.default_bin) ? top - 1 : top;
-  const int first_fwd = (skip_def && fi.default_bin == 0) ? 1 : 0;
-  // reverse pass: position i <-> bin nb - 1 - i (the right side grows from the top bin)
-  for (int base = 0; base < nb; base += 64 * K) {
-    double pg[K], ph[K];
-    int pc[K];
-    bool empty[K];
-    double tg = 0.0, th = 0.0;
-    int tc = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int b = nb - 1 - (base + lane * K + k);
-      double g = 0.0, h = 0.0;
-      int c = 0;
-      if (b >= 0 && !(skip_def && b == fi.default_bin) && !(na && b == nb - 1)) {
-        g = H[2 * b];
-        h = H[2 * b + 1];
-        c = RoundCount(h * cnt_factor);
-      }
-      empty[k] = g == 0.0 && h == 0.0;
-      tg += g;
-      th += h;
-      tc += c;
-      pg[k] = tg;
-      ph[k] = th;
-      pc[k] = tc;
-    }
-    const double ig = WaveInclusiveSumDpp(tg), ih = WaveInclusiveSumDpp(th);
-    const int ic = WaveInclusiveSumDpp(tc);
-    const double eg = cg + ig - tg, eh = ch + ih - th;
-    const int ec = cc + ic - tc;
-    cg += ReadLane(ig, 63);
-    ch += ReadLane(ih, 63);
-    cc += ReadLane(ic, 63);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int b = nb - 1 - (base + lane * K + k);
-      if (b >= 1 && b <= top && !(skip_def && b == fi.default_bin) && !(b < first_rev && empty[k])) {
-        const int thr = b - 1;
-        const double rg = eg + pg[k];
-        const double rh = kEpsilon + eh + ph[k];
-        const int rc = ec + pc[k];
-        const int lc = n - rc;
-        const double lh = sum_h - rh;
-        if (rc >= p.min_data_in_leaf && rh >= p.min_sum_hessian_in_leaf && lc >= p.min_data_in_leaf &&
-            lh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
-          const double lg = sg - rg;
-          const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
-          if (gain > shift) {
-            sp = true;
-            if (gain > rb.gain) {
-              rb.gain = gain;
-              rb.thr = thr;
-              rb.lg = lg;
-              rb.lh = lh;
-              rb.lc = lc;
-            }
-          }
-        }
-      }
-    }
-  }
-  Stamp(a, 3, 5);
-  Cand fb;
-  fb.gain = kMinScore;
-  fb.thr = 0x7fffffff;
-  fb.lg = fb.lh = 0.0;
-  fb.lc = 0;
-  if (two_dir) {
-    // forward pass: position i <-> bin i (the left side grows from bin 0)
-    cg = ch = 0.0;
-    cc = 0;
-    for (int base = 0; base < nb; base += 64 * K) {
-      double pg[K], ph[K];
-      int pc[K];
-      bool empty[K];
-      double tg = 0.0, th = 0.0;
-      int tc = 0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int b = base + lane * K + k;
-        double g = 0.0, h = 0.0;
-        int c = 0;
-        if (b < nb && !(skip_def && b == fi.default_bin)) {
-          g = H[2 * b];
-          h = H[2 * b + 1];
-          c = RoundCount(h * cnt_factor);
-        }
-        empty[k] = g == 0.0 && h == 0.0;
-        tg += g;
-        th += h;
-        tc += c;
-        pg[k] = tg;
-        ph[k] = th;
-        pc[k] = tc;
-      }
-      const double ig = WaveInclusiveSumDpp(tg), ih = WaveInclusiveSumDpp(th);
-      const int ic = WaveInclusiveSumDpp(tc);
-      const double eg = cg + ig - tg, eh = ch + ih - th;
-      const int ec = cc + ic - tc;
-      cg += ReadLane(ig, 63);
-      ch += ReadLane(ih, 63);
-      cc += ReadLane(ic, 63);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int b = base + lane * K + k;
-        if (b <= nb - 2 && !(skip_def && b == fi.default_bin) && !(b > first_fwd && empty[k])) {
-          const int thr = b;
-          const double lg = eg + pg[k];
-          const double lh = kEpsilon + eh + ph[k];
-          const int lc = ec + pc[k];
-          const int rc = n - lc;
-          const double rh = sum_h - lh;
-          if (lc >= p.min_data_in_leaf && lh >= p.min_sum_hessian_in_leaf && rc >= p.min_data_in_leaf &&
-              rh >= p.min_sum_hessian_in_leaf && (!use_rand || thr == rand_thr)) {
-            const double rg = sg - lg;
-            const double gain = SplitGain(lg, lh, rg, rh, p, mono, lc, rc, po, bounds);
-            if (gain > shift) {
-              sp = true;
-              if (gain > fb.gain) {
-                fb.gain = gain;
-                fb.thr = thr;
-                fb.lg = lg;
-                fb.lh = lh;
-                fb.lc = lc;
-              }
-            }
-          }
-        }
-      }
-    }
-  }
-  Stamp(a, 3, 6);
-  const bool any = __any(sp) != 0;
-  const Cand r = WaveBest(rb, true);
-  const Cand f = two_dir ? WaveBest(fb, false) : fb;
-  if (lane == 0) {
-    out->Reset();
-    out->monotone_type = fi.monotone;
-    out->default_left = 1;
-    if (any) {
-      Cand w = r;
-      int dl = 1;
-      if (two_dir && f.gain > r.gain) {
-        w = f;
-        dl = 0;
-      }
-      if (w.gain > kMinScore) {
-        out->threshold = static_cast<uint32_t>(w.thr);
-        out->left_output = LeafOutput(w.lg, w.lh, p, w.lc, po, bounds);
-        out->left_count = w.lc;
-        out->left_sum_gradient = w.lg;
-        out->left_sum_hessian = w.lh - kEpsilon;
-        out->right_output = LeafOutput(sg - w.lg, sum_h - w.lh, p, n - w.lc, po, bounds);
-        out->right_count = n - w.lc;
-        out->right_sum_gradient = sg - w.lg;
-        out->right_sum_hessian = sum_h - w.lh - kEpsilon;
-        out->gain = (w.gain - shift) * fi.penalty;
-        out->default_left = dl;
-      }
-    }
-    if (!two_dir && fi.missing == 2) out->default_left = 0;
-  }
-  return any;
-}
-
-// Wave-parallel FindBestCategorical (split_math.h:262-386, the host oracle; reference
-// cuda_best_split_finder.cu:639 sorts the categories in-block): the one-hot candidates are
-// evaluated one bin per lane with a wave arg-max (first maximum in bin order), and the
-// many-vs-many path compacts the used bins with a ballot scan, bitonic-sorts them in LDS by
-// (ctr, bin) — the order of the host's stable insertion sort — and lane 0 walks the at most
-// max_cat_threshold prefix positions of both directions. `order` / `key` hold cat_p2 entries.
-__device__ bool ScanCategoricalWave(const SplitParams& p_in, const FeatureScanMeta& m, const double* H, double sum_g,
-                                    double sum_h_raw, int n, double po, const LeafBounds& bounds, int cat_p2,
-                                    int* order, double* key, SplitInfo* out) {
-  const int lane = threadIdx.x & 63;
-  const double sum_h = sum_h_raw + 2 * kEpsilon;
-  SplitParams p = p_in;  // monotone bounds clamp categorical outputs too (type 0: no order check)
-  double gain_shift;
-  if (p.path_smooth > kEpsilon) {
-    gain_shift = LeafGainGivenOutput(sum_g, sum_h, p, po);
-  } else {
-    SplitParams q = p;
-    q.path_smooth = 0.0;
-    gain_shift = LeafGain(sum_g, sum_h, q, n, 0.0);
-  }
-  const double min_gain_shift = gain_shift + p.min_gain_to_split;
-  const double cnt_factor = n / sum_h;
-  const bool use_rand = p.extra_trees != 0;
-  bool sp = false;
-  double best_gain = kMinScore, best_lg = 0.0, best_lh = 0.0;
-  int best_lc = 0, best_t = -1, best_dir = 1, used = 0;
-  const bool onehot = m.num_bin <= p.max_cat_to_onehot;
-  if (onehot) {
-    double lg = kMinScore, llg = 0.0, llh = 0.0;
-    int lt = 0x7fffffff, llc = 0;
-    bool lsp = false;
-    for (int t = 1 + lane; t < m.num_bin; t += 64) {
-      const double g = H[2 * t], h = H[2 * t + 1];
-      const int c = RoundCount(h * cnt_factor);
-      if (c < p.min_data_in_leaf || h < p.min_sum_hessian_in_leaf) continue;
-      const int oc = n - c;
-      if (oc < p.min_data_in_leaf) continue;
-      const double oh = sum_h - h - kEpsilon;
-      if (oh < p.min_sum_hessian_in_leaf) continue;
-      const double og = sum_g - g;
-      if (use_rand && t != m.rand_threshold) continue;
-      const double gain = SplitGain(og, oh, g, h + kEpsilon, p, 0, oc, c, po, bounds);
-      if (gain <= min_gain_shift) continue;
-      lsp = true;
-      if (gain > lg) {
-        lg = gain;
-        lt = t;
-        llg = g;
-        llh = h + kEpsilon;
-        llc = c;
-      }
-    }
-    sp = __any(lsp) != 0;
-    const int src = WaveArgBestLane(lg, lt, 0);
-    best_gain = ReadLane(lg, src);
-    best_t = ReadLane(lt, src);
-    best_lg = ReadLane(llg, src);
-    best_lh = ReadLane(llh, src);
-    best_lc = ReadLane(llc, src);
-  } else {
-    // used bins in ascending order (ballot compaction)
-    const unsigned long long lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (int base = 0; base < m.num_bin; base += 64) {
-      const int i = base + lane;
-      const bool v = i >= 1 && i < m.num_bin && RoundCount(H[2 * i + 1] * cnt_factor) >= p.cat_smooth;
-      const unsigned long long b = __ballot(v);
-      if (v) order[used + __popcll(b & lt_mask)] = i;
-      used += __popcll(b);
-    }
-    int P2 = 1;
-    while (P2 < used) P2 <<= 1;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int j = lane; j < P2; j += 64) {
-      if (j < used) {
-        const int b = order[j];
-        key[j] = H[2 * b] / (H[2 * b + 1] + p.cat_smooth);
-      } else {
-        key[j] = INFINITY;
-        order[j] = 0x7fffffff;
-      }
-    }
-    // bitonic sort ascending by (ctr, bin): the stable order of the host's insertion sort
-    for (int k = 2; k <= P2; k <<= 1) {
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int i = lane; i < P2; i += 64) {
-          const int l = i ^ jj;
-          if (l <= i) continue;
-          const double ka = key[i], kb = key[l];
-          const int ba = order[i], bb = order[l];
-          const bool a_gt = ka != kb ? ka > kb : ba > bb;
-          if (a_gt == ((i & k) == 0)) {
-            key[i] = kb;
-            key[l] = ka;
-            order[i] = bb;
-            order[l] = ba;
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    p.lambda_l2 += p.cat_l2;
-    if (lane == 0) {
-      const int max_num_cat = p.max_cat_threshold < (used + 1) / 2 ? p.max_cat_threshold : (used + 1) / 2;
-      for (int dir_i = 0; dir_i < 2; ++dir_i) {
-        const int dir = dir_i == 0 ? 1 : -1;
-        int pos = dir_i == 0 ? 0 : used - 1;
-        int cur_group = 0, lc = 0;
-        double lg = 0.0, lh = kEpsilon;
-        for (int i = 0; i < used && i < max_num_cat; ++i) {
-          const int t = order[pos];
-          pos += dir;
-          const double g = H[2 * t], h = H[2 * t + 1];
-          const int c = RoundCount(h * cnt_factor);
-          lg += g;
-          lh += h;
-          lc += c;
-          cur_group += c;
-          if (lc < p.min_data_in_leaf || lh < p.min_sum_hessian_in_leaf) continue;
-          const int rc = n - lc;
-          if (rc < p.min_data_in_leaf || rc < p.min_data_per_group) break;
-          const double rh = sum_h - lh;
-          if (rh < p.min_sum_hessian_in_leaf) break;
-          if (cur_group < p.min_data_per_group) continue;
-          cur_group = 0;
-          const double rg = sum_g - lg;
-          if (use_rand && i != m.rand_threshold) continue;
-          const double gain = SplitGain(lg, lh, rg, rh, p, 0, lc, rc, po, bounds);
-          if (gain <= min_gain_shift) continue;
-          sp = true;
-          if (gain > best_gain) {
-            best_lc = lc;
-            best_lg = lg;
-            best_lh = lh;
-            best_t = i;
-            best_gain = gain;
-            best_dir = dir;
-          }
-        }
-      }
-    }
-    sp = __shfl(sp ? 1 : 0, 0, kWave) != 0;
-  }
-  if (lane == 0) {
-    out->Reset();
-    out->default_left = 0;
-    if (sp) {
-      out->left_output = LeafOutput(best_lg, best_lh, p, best_lc, po, bounds);
-      out->left_count = best_lc;
-      out->left_sum_gradient = best_lg;
-      out->left_sum_hessian = best_lh - kEpsilon;
-      out->right_output = LeafOutput(sum_g - best_lg, sum_h - best_lh, p, n - best_lc, po, bounds);
-      out->right_count = n - best_lc;
-      out->right_sum_gradient = sum_g - best_lg;
-      out->right_sum_hessian = sum_h - best_lh - kEpsilon;
-      out->gain = (best_gain - min_gain_shift) * m.penalty;
-      for (int w = 0; w < kMaxCatWords; ++w) out->cat_bitset[w] = 0u;
-      if (onehot) {
-        out->num_cat_threshold = 1;
-        out->cat_bitset[best_t / 32] |= (1u << (best_t % 32));
-      } else {
-        out->num_cat_threshold = static_cast<int16_t>(best_t + 1);
-        for (int i = 0; i <= best_t; ++i) {
-          const int b = best_dir == 1 ? order[i] : order[used - 1 - i];
-          out->cat_bitset[b / 32] |= (1u << (b % 32));
-        }
-      }
-      out->monotone_type = 0;
-    }
-  }
-  return sp;
-}
-
 // One workgroup (16 waves) per feature this rank owns (every feature on one GPU):
 //  1. the smaller child's histogram of the feature into LDS: the sum of the active
 //     histogram blocks' slab rows (single GPU / feature parallel), or of the owner rows
@@ -1613,7 +1144,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
         const int depth = __shfl(pre_depth, 0, kWave);
         bool sp;
         if (fi.bin_type == 0) {
-          sp = ScanNumericalWave(a, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
+          sp = ScanNumericalWave(a.sp, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
         } else {
           // categorical: the wave-parallel one-hot / ctr-sorted scan
           FeatureScanMeta m;
@@ -1966,7 +1497,7 @@ __global__ __launch_bounds__(128) void k_vote_scan(Args a) {
     const LeafBounds bounds = a.bounds[leaf];
     bool sp;
     if (fi.bin_type == 0) {
-      sp = ScanNumericalWave(a, fi, H, sums.x, sums.y, n, po, bounds, 0, out);
+      sp = ScanNumericalWave(a.sp, fi, H, sums.x, sums.y, n, po, bounds, 0, out);
     } else {
       FeatureScanMeta m;
       m.num_bin = fi.num_bin;
@@ -2867,6 +2398,8 @@ class DeviceTreeLearner : public TreeLearner {
 
   ~DeviceTreeLearner() override {
     if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+    for (auto& kv : fgraphs_) (void)hipGraphExecDestroy(kv.second);
+    if (fcont_) (void)hipGraphExecDestroy(fcont_);
     if (!x_peers_.empty()) XgmiClose(x_local_, &x_peers_);
     if (x_local_) (void)hipFree(x_local_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -3260,6 +2793,8 @@ class DeviceTreeLearner : public TreeLearner {
     ra.idx0 = idx_[0].get();
     ra.idx1 = idx_[1].get();
     ra.idx2 = idx_[2].get();
+    ra.idx3 = idx_[3].get();
+    ra.idx4 = idx_[4].get();
     ra.segs = renew_segs_.get();
     ra.seg_off = renew_off_.get();
     ra.num_leaves = nl;
@@ -3624,50 +3159,19 @@ class DeviceTreeLearner : public TreeLearner {
       }
       HIP_CHECK(hipMemcpyAsync(bynode_.get(), bm, static_cast<size_t>(2 * L_) * F_, hipMemcpyHostToDevice, stream_));
     }
-    // LGAP_DP_GRAPH=1 also captures the RCCL data-parallel tree (the per-split ncclAllReduce
-    // calls replay from the graph). Off by default: on a one-rank communicator it measured
-    // 358 it/s captured vs 368 eager at 1.25M rows (profiles/README.md), and the eager host
-    // enqueue stays ahead of the ~40 us splits. The host-staged rehearsal transport
-    // synchronises inside its all-reduce and is never captured.
-    // the xGMI transport keeps every exchange inside the kernels: the tree replays as one graph
-    const bool collectives = (owner_scan_ || voting_) && transport_ != 2;
-    const bool use_graph = config_->device_use_graph && (!collectives || (DPGraphEnabled() && !HostStagedDP()));
-    if (use_graph) {
-      if (graph_exec_ && distributed_ && graph_comm_ != ActiveComm()) InvalidateGraph();
-      if (!graph_exec_) CaptureGraph();
-      HIP_CHECK(hipGraphLaunch(graph_exec_, stream_));
-    } else {
-      EnqueueTree();
-    }
-    // results
-    Ctl* hc2 = pin_ctl_.Get(2);
     SplitRec* hr = pin_rec_.Get(L_);
     LeafRange* hrange = pin_range_.Get(L_);
     double* hlo = pin_lout_.Get(1);
-    HIP_CHECK(hipMemcpyAsync(hc2, ctl_.get(), 2 * sizeof(Ctl), hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(hr, rec_.get(), sizeof(SplitRec) * (L_ - 1), hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(hrange, range_.get(), sizeof(LeafRange) * L_, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(hlo, lout_.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
-    unsigned* hbar = pin_bar_.Get(4);
-    HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
-    if (collectives && !HostStagedDP()) {
-      // the tree's collectives ride on this stream: a lost peer must not hang us
-      static const double timeout_s = CommTimeoutSeconds(config_->time_out);
-      WatchedStreamSync(stream_, timeout_s, "device tree growth (RCCL histogram reduce-scatter)");
+    int num_splits = 0, num_leaves = 1;
+    if (frontier_) {
+      FrontierGrow(&num_splits, &num_leaves, hr, hrange, hlo);
     } else {
-      HIP_CHECK(hipStreamSynchronize(stream_));
+      SequentialGrow(&num_splits, &num_leaves, hr, hrange, hlo);
     }
-    if (hbar[2] != 0u) Log::Fatal("k_partition: a wait on published tile counts timed out (blocks not co-resident?)");
-    if (hbar[3] != 0u) {
-      Log::Fatal("xGMI exchange (%s) timed out on rank %d after %.0f s: a peer stopped training",
-                 hbar[3] == 1u ? "histogram" : (hbar[3] == 2u ? "split candidates" : "root sums"), rank_, XTimeoutSeconds());
-    }
-    // the control buffer written last holds the final tree state
-    const Ctl* hc = hc2[1].num_splits > hc2[0].num_splits ? &hc2[1] : &hc2[0];
     auto tree = std::make_unique<Tree>(L_, false, false);
     tree->SetLeafOutput(0, hlo[0]);
-    if (hc->num_splits < 0 || hc->num_splits > L_ - 1) Log::Fatal("device tree: invalid split count %d", hc->num_splits);
-    for (int s = 0; s < hc->num_splits; ++s) {
+    if (num_splits < 0 || num_splits > L_ - 1) Log::Fatal("device tree: invalid split count %d", num_splits);
+    for (int s = 0; s < num_splits; ++s) {
       const SplitRec& r = hr[s];
       const SplitInfo& info = r.info;
       if (r.leaf < 0 || r.leaf > s || info.feature < 0 || info.feature >= F_) {
@@ -3696,12 +3200,286 @@ class DeviceTreeLearner : public TreeLearner {
                                r.right_count, info.left_sum_hessian, info.right_sum_hessian, gain, fi.missing);
       }
     }
-    h_range_.assign(hrange, hrange + hc->num_leaves);
+    h_range_.assign(hrange, hrange + num_leaves);
     if (config_->use_quantized_grad && config_->quant_train_renew_leaf) RenewQuantizedLeaves(tree.get());
-    if (stamps_.size() && ++stamp_trees_ == 3) ReportStamps(hc->num_splits);
+    if (stamps_.size() && !frontier_ && ++stamp_trees_ == 3) ReportStamps(num_splits);
     tree->RecomputeMaxDepth();
     last_trained_ = tree.get();
     return tree;
+  }
+
+  // ---- frontier tree growth (frontier.h): batched rounds, replayed best-first order
+
+  // The frontier engine covers the single-device learner; bynode sampling and extra-trees
+  // draw per split in sequential order, the global-memory scan has no frontier variant, and
+  // the computed-node image of the select must fit its LDS. LGAP_FRONTIER=0 forces the
+  // sequential chain (A/B runs).
+  bool FrontierEligible() const {
+    const char* e = std::getenv("LGAP_FRONTIER");
+    if (e != nullptr && e[0] == '0') return false;
+    if (mode_ != DevParallel::kSerial || owner_scan_ || voting_ || distributed_) return false;
+    if (use_bynode_ || config_->extra_trees || scan_global_) return false;
+    if (FrontierCapacity() > kFrontierMaxNodes || F_ <= 0) return false;
+    return FrontierSelectLds(FrontierCapacity(), L_) <= 150 * 1024;
+  }
+  int FrontierKmax() const {
+    int k = kFrontierKmax;
+    if (const char* e = std::getenv("LGAP_FRONTIER_K")) k = std::max(1, std::min(kFrontierKmax, std::atoi(e)));
+    return std::max(1, std::min(k, L_ - 1));
+  }
+  // computed nodes of one tree: every committed node (2 L - 1) plus room for speculation
+  int FrontierCapacity() const { return 4 * L_ + 2 * kFrontierKmax; }
+
+  void AllocFrontier() {
+    frontier_ = FrontierEligible();
+    if (!frontier_) return;
+    fkmax_ = FrontierKmax();
+    fC_ = FrontierCapacity();
+    const size_t C = fC_, K = fkmax_, F = std::max(F_, 1);
+    ArenaLayout lay;
+    const size_t o_st = lay.Add<FState>(1), o_nodes = lay.Add<FNode>(C), o_exps = lay.Add<FExp>(K),
+                 o_bits = lay.Add<uint32_t>(K * kMaxCatWords), o_lsum = lay.Add<double2>(C), o_lout = lay.Add<double>(C),
+                 o_bounds = lay.Add<LeafBounds>(C), o_key = lay.Add<SplitKey>(C), o_best = lay.Add<SplitInfo>(C),
+                 o_spl = lay.Add<uint8_t>(C * F), o_ic = lay.Add<unsigned long long>(C), o_nst = lay.Add<uint8_t>(C),
+                 o_lcid = lay.Add<int>(L_), o_ckey = lay.Add<SplitKey>(K * 2 * F), o_cinfo = lay.Add<SplitInfo>(K * 2 * F);
+    farena_.Resize(lay.bytes());
+    farena_.Zero(stream_);
+    char* b = farena_.get();
+    fst_ = reinterpret_cast<FState*>(b + o_st);
+    fnodes_ = reinterpret_cast<FNode*>(b + o_nodes);
+    fexps_ = reinterpret_cast<FExp*>(b + o_exps);
+    fbits_ = reinterpret_cast<uint32_t*>(b + o_bits);
+    flsum_ = reinterpret_cast<double2*>(b + o_lsum);
+    flout_ = reinterpret_cast<double*>(b + o_lout);
+    fbounds_ = reinterpret_cast<LeafBounds*>(b + o_bounds);
+    fkey_ = reinterpret_cast<SplitKey*>(b + o_key);
+    fbest_ = reinterpret_cast<SplitInfo*>(b + o_best);
+    fspl_ = reinterpret_cast<uint8_t*>(b + o_spl);
+    fic_ = reinterpret_cast<unsigned long long*>(b + o_ic);
+    fnst_ = reinterpret_cast<uint8_t*>(b + o_nst);
+    flcid_ = reinterpret_cast<int*>(b + o_lcid);
+    fckey_ = reinterpret_cast<SplitKey*>(b + o_ckey);
+    fcinfo_ = reinterpret_cast<SplitInfo*>(b + o_cinfo);
+    fslots_.Resize(C * 2 * static_cast<size_t>(TB_));
+    facc_.Resize(K * 2 * static_cast<size_t>(TB_));
+    facc_.Zero(stream_);  // the scan re-zeroes what it consumes: zero between rounds from here on
+    fpart_tile_ = kPartThreads * part_iters_;
+    ftile_cap_ = DivUp(N_, fpart_tile_) + fkmax_ + 1;
+    ftile_pub_.Resize(ftile_cap_);
+    ftile_pub_.Zero(stream_);
+    for (int i = 3; i < 5; ++i) idx_[i].Resize(std::max(N_, 1));
+    // the partition's look-back needs all of its blocks resident: occupancy minus a margin
+    int per_cu = FrontierPartitionBlocksPerCU(part_iters_);
+    per_cu = std::max(1, std::min(4, per_cu - 1));
+    fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
+    fscan_lds_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + static_cast<size_t>(cat_p2_) * 2 * (sizeof(int) + sizeof(double));
+    FrontierSetLds(hist_lds_bytes_, fscan_lds_, use_dp_, width_);
+    fspec_cap_ = 0;
+    if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
+    for (auto& kv : fgraphs_) (void)hipGraphExecDestroy(kv.second);
+    fgraphs_.clear();
+    if (fcont_) (void)hipGraphExecDestroy(fcont_);
+    fcont_ = nullptr;
+  }
+
+  FArgs MakeFArgs() const {
+    FArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.rowbins = rowbins_.get();
+    a.colbins = colbins_.get();
+    a.gh = gh_.get();
+    for (int i = 0; i < kFrontierIdx; ++i) a.idx[i] = idx_[i].get();
+    a.N = N_;
+    a.stride_dw = stride_dw_;
+    a.width = width_;
+    a.num_groups = G_;
+    a.TB = TB_;
+    a.F = F_;
+    a.L = L_;
+    a.C = fC_;
+    a.kmax = fkmax_;
+    a.gstart = gstart_.get();
+    a.feat = feat_.get();
+    a.tiles = tiles_.get();
+    a.num_tiles = num_tiles_;
+    a.used_bytree = used_bytree_.get();
+    a.tp = tparams_.get();
+    a.st = fst_;
+    a.nodes = fnodes_;
+    a.exps = fexps_;
+    a.exp_bits = fbits_;
+    a.lsum = flsum_;
+    a.lout = flout_;
+    a.bounds = fbounds_;
+    a.key = fkey_;
+    a.best = fbest_;
+    a.spl = fspl_;
+    a.ic = use_ic_ ? fic_ : nullptr;
+    a.ic_feat = use_ic_ ? ic_feat_.get() : nullptr;
+    a.nstate = fnst_;
+    a.leaf_cid = flcid_;
+    a.rec = rec_.get();
+    a.range_out = range_.get();
+    a.slots = fslots_.get();
+    a.acc = reinterpret_cast<unsigned long long*>(facc_.get());
+    a.ghmax = ghmax_.get();
+    a.ckey = fckey_;
+    a.cinfo = fcinfo_;
+    a.tile_pub = ftile_pub_.get();
+    a.bar = bar_.get();
+    a.hist_min_rows = HistMinRows();
+    a.hist_grid = HistBlocks();
+    a.part_tile = fpart_tile_;
+    a.max_depth = config_->max_depth;
+    a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
+    a.monotone_penalty = config_->monotone_penalty;
+    a.max_bin = max_bin_;
+    a.cat_p2 = cat_p2_;
+    a.use_dp = use_dp_ ? 1 : 0;
+    a.spec_cap = fspec_cap_;
+    a.distributed = 0;
+    a.sp = MakeArgs().sp;
+    return a;
+  }
+
+  // One round: partition -> histograms -> scans -> select.
+  void EnqueueFrontierRound(const FArgs& fa) {
+    LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    LaunchFrontierHist(fa, hist_lds_bytes_, stream_);
+    LaunchFrontierScan(fa, fscan_lds_, stream_);
+    LaunchFrontierSelect(fa, stream_);
+  }
+
+  // The root round (setup, root sums, root histogram and scan, first select), then `rounds`
+  // rounds; a finished tree turns the remaining launches into early exits.
+  void EnqueueFrontier(int rounds, bool prologue) {
+    const FArgs fa = MakeFArgs();
+    if (prologue) {
+      LaunchFrontierInit(fa, stream_);
+      Args ra = MakeArgs(0);
+      ra.lsum = flsum_;  // root sums -> the root node; ghmax -> the fixed-point scales
+      const int root_blocks = RootBlocks();
+      k_root_sums<<<root_blocks, kRootThreads, 0, stream_>>>(ra);
+      k_root_final<<<1, kRootThreads, 0, stream_>>>(ra, root_blocks);
+      HIP_CHECK(hipGetLastError());
+      LaunchFrontierHist(fa, hist_lds_bytes_, stream_);
+      LaunchFrontierScan(fa, fscan_lds_, stream_);
+      LaunchFrontierSelect(fa, stream_);
+    }
+    for (int r = 0; r < rounds; ++r) EnqueueFrontierRound(fa);
+  }
+
+  hipGraphExec_t CaptureFrontier(int rounds, bool prologue) {
+    hipGraph_t g;
+    hipGraphExec_t ex = nullptr;
+    HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    EnqueueFrontier(rounds, prologue);
+    HIP_CHECK(hipStreamEndCapture(stream_, &g));
+    HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(g));
+    return ex;
+  }
+
+  // Grow one tree: the root round plus a predicted number of rounds (the previous trees'
+  // count) in one replay; if the tree is not finished, continuation replays of a few rounds
+  // each until it is. Results: the committed splits, the final leaf ranges, the root output.
+  void FrontierGrow(int* num_splits, int* num_leaves, SplitRec* hr, LeafRange* hrange, double* hlo) {
+    const bool use_graph = config_->device_use_graph;
+    const int pred = std::max(1, std::min(fpred_rounds_, L_));
+    FState* hs = pin_fst_.Get(1);
+    if (fgraph_gh_ != gh_.get()) {  // captured launches hold the gradient buffer's address
+      InvalidateGraph();
+      fgraph_gh_ = gh_.get();
+    }
+    if (use_graph) {
+      auto it = fgraphs_.find(pred);
+      if (it == fgraphs_.end()) it = fgraphs_.emplace(pred, CaptureFrontier(pred, true)).first;
+      HIP_CHECK(hipGraphLaunch(it->second, stream_));
+    } else {
+      EnqueueFrontier(pred, true);
+    }
+    constexpr int kCont = 4;
+    int launched = pred;
+    for (;;) {
+      HIP_CHECK(hipMemcpyAsync(hs, fst_, sizeof(FState), hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      if (hs->done) break;
+      if (launched > L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
+      if (use_graph) {
+        if (!fcont_) fcont_ = CaptureFrontier(kCont, false);
+        HIP_CHECK(hipGraphLaunch(fcont_, stream_));
+      } else {
+        EnqueueFrontier(kCont, false);
+      }
+      launched += kCont;
+    }
+    // rounds the tree needed (selects run after the root's) -> next tree's replay length
+    const int used = std::max(1, hs->round - 1);
+    frounds_hist_[frounds_pos_++ % 4] = used;
+    int mx = 1;
+    for (int v : frounds_hist_) mx = std::max(mx, v);
+    fpred_rounds_ = mx;
+    fstat_rounds_ += used;
+    fstat_spec_ += hs->spec;
+    fstat_trees_ += 1;
+    *num_splits = hs->num_splits;
+    *num_leaves = hs->num_leaves;
+    if (*num_splits > 0) HIP_CHECK(hipMemcpyAsync(hr, rec_.get(), sizeof(SplitRec) * *num_splits, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hrange, range_.get(), sizeof(LeafRange) * *num_leaves, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hlo, flout_, sizeof(double), hipMemcpyDeviceToHost, stream_));
+    unsigned* hbar = pin_bar_.Get(4);
+    HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (hbar[2] != 0u) Log::Fatal("k_f_partition: a wait on published tile counts timed out (blocks not co-resident?)");
+    if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {
+      std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max)\n", fstat_trees_,
+                   static_cast<double>(fstat_rounds_) / fstat_trees_, static_cast<double>(fstat_spec_) / fstat_trees_, L_);
+    }
+  }
+
+  // The one-split-at-a-time device tree (one fixed kernel chain per split, replayed from a
+  // hipGraph): the path of the distributed learners and of the options the frontier engine
+  // does not cover (feature_fraction_bynode, extra_trees, global-memory scans).
+  void SequentialGrow(int* num_splits, int* num_leaves, SplitRec* hr, LeafRange* hrange, double* hlo) {
+    // LGAP_DP_GRAPH=1 also captures the RCCL data-parallel tree (the per-split ncclAllReduce
+    // calls replay from the graph). Off by default: on a one-rank communicator it measured
+    // 358 it/s captured vs 368 eager at 1.25M rows (profiles/README.md), and the eager host
+    // enqueue stays ahead of the ~40 us splits. The host-staged rehearsal transport
+    // synchronises inside its all-reduce and is never captured.
+    // the xGMI transport keeps every exchange inside the kernels: the tree replays as one graph
+    const bool collectives = (owner_scan_ || voting_) && transport_ != 2;
+    const bool use_graph = config_->device_use_graph && (!collectives || (DPGraphEnabled() && !HostStagedDP()));
+    if (use_graph) {
+      if (graph_exec_ && distributed_ && graph_comm_ != ActiveComm()) InvalidateGraph();
+      if (!graph_exec_) CaptureGraph();
+      HIP_CHECK(hipGraphLaunch(graph_exec_, stream_));
+    } else {
+      EnqueueTree();
+    }
+    // results
+    Ctl* hc2 = pin_ctl_.Get(2);
+    HIP_CHECK(hipMemcpyAsync(hc2, ctl_.get(), 2 * sizeof(Ctl), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hr, rec_.get(), sizeof(SplitRec) * (L_ - 1), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hrange, range_.get(), sizeof(LeafRange) * L_, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hlo, lout_.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
+    unsigned* hbar = pin_bar_.Get(4);
+    HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
+    if (collectives && !HostStagedDP()) {
+      // the tree's collectives ride on this stream: a lost peer must not hang us
+      static const double timeout_s = CommTimeoutSeconds(config_->time_out);
+      WatchedStreamSync(stream_, timeout_s, "device tree growth (RCCL histogram reduce-scatter)");
+    } else {
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    if (hbar[2] != 0u) Log::Fatal("k_partition: a wait on published tile counts timed out (blocks not co-resident?)");
+    if (hbar[3] != 0u) {
+      Log::Fatal("xGMI exchange (%s) timed out on rank %d after %.0f s: a peer stopped training",
+                 hbar[3] == 1u ? "histogram" : (hbar[3] == 2u ? "split candidates" : "root sums"), rank_, XTimeoutSeconds());
+    }
+    // the control buffer written last holds the final tree state
+    const Ctl* hc = hc2[1].num_splits > hc2[0].num_splits ? &hc2[1] : &hc2[0];
+    *num_splits = hc->num_splits;
+    *num_leaves = hc->num_leaves;
   }
 
   std::string DeviceName() const override {
@@ -4327,6 +4105,7 @@ class DeviceTreeLearner : public TreeLearner {
       stamps_.Resize(5 * 256 * 2 * 8);
       stamps_.Zero(stream_);
     }
+    AllocFrontier();
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
@@ -4338,7 +4117,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.rowbins = rowbins_.get();
     a.colbins = colbins_.get();
     a.gh = gh_.get();
-    for (int i = 0; i < 3; ++i) a.idx[i] = idx_[i].get();
+    for (int i = 0; i < 5; ++i) a.idx[i] = idx_[i].get();
     a.N = N_;
     a.stride_dw = stride_dw_;
     a.width = width_;
@@ -4512,6 +4291,10 @@ class DeviceTreeLearner : public TreeLearner {
       (void)hipGraphExecDestroy(graph_exec_);
       graph_exec_ = nullptr;
     }
+    for (auto& kv : fgraphs_) (void)hipGraphExecDestroy(kv.second);
+    fgraphs_.clear();
+    if (fcont_) (void)hipGraphExecDestroy(fcont_);
+    fcont_ = nullptr;
   }
 
   // Queries longer than kMaxDeviceQuery: their list and per-query slices of global scratch.
@@ -4626,6 +4409,36 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
+  // frontier engine (frontier.h)
+  bool frontier_ = false;
+  int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0;
+  size_t fscan_lds_ = 0;
+  DevBuf<char> farena_;
+  FState* fst_ = nullptr;
+  FNode* fnodes_ = nullptr;
+  FExp* fexps_ = nullptr;
+  uint32_t* fbits_ = nullptr;
+  double2* flsum_ = nullptr;
+  double* flout_ = nullptr;
+  LeafBounds* fbounds_ = nullptr;
+  SplitKey* fkey_ = nullptr;
+  SplitInfo* fbest_ = nullptr;
+  uint8_t* fspl_ = nullptr;
+  unsigned long long* fic_ = nullptr;
+  uint8_t* fnst_ = nullptr;
+  int* flcid_ = nullptr;
+  SplitKey* fckey_ = nullptr;
+  SplitInfo* fcinfo_ = nullptr;
+  DevBuf<double> fslots_;
+  DevBuf<unsigned long long> facc_;
+  DevBuf<unsigned long long> ftile_pub_;
+  std::map<int, hipGraphExec_t> fgraphs_;
+  hipGraphExec_t fcont_ = nullptr;
+  int fpred_rounds_ = 16, frounds_hist_[4] = {1, 1, 1, 1}, frounds_pos_ = 0;
+  long long fstat_rounds_ = 0, fstat_spec_ = 0;
+  int fstat_trees_ = 0;
+  PinnedBuf<FState> pin_fst_;
+  const float2* fgraph_gh_ = nullptr;
   const Config* config_;
   bool data_parallel_ = false;
   bool distributed_ = false;
@@ -4655,7 +4468,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<float2> gh_;
   DevBuf<double> score_;
   DevBuf<float> label_, weight_, aux_;
-  DevBuf<int> idx_[3];
+  DevBuf<int> idx_[5];
   DevBuf<DevFeature> feat_;
   DevBuf<int> gstart_;
   DevBuf<HistTile> tiles_;

@@ -1,0 +1,162 @@
+// Frontier tree growth: leaf-wise (best-first) trees built in batched ROUNDS.
+//
+// Leaf-wise growth splits, at every step, the leaf whose best split has the largest
+// gain. A leaf's best split is a pure function of its rows, so the split of ANY leaf
+// can be computed before best-first order reaches it. The frontier engine exploits
+// that: each round expands a batch of open nodes at once (partition their rows,
+// histogram their smaller children, parent - smaller subtraction, threshold scans of
+// both children), and a replay of the sequential best-first order over the computed
+// nodes commits splits in exactly the order (and with exactly the leaf numbering) of
+// the one-split-at-a-time learner. A round's batch always holds the node the replay is
+// blocked on (the highest-gain unexpanded leaf), plus speculative expansions of the
+// next-best open nodes; speculation that the budget (num_leaves) never commits is
+// simply dropped. Rounds ~ depth of the tree instead of num_leaves - 1 sequential
+// splits, so the per-launch latency floor is paid ~4-5x less often, and each round's
+// kernels get several leaves' worth of parallel work.
+//
+// Per round (all device-resident, fixed launch shapes, replayed from a hipGraph):
+//   k_f_partition  stable 2-way partition of every expanded parent's rows (decoupled
+//                  look-back per expansion), post-split bookkeeping of the children
+//   k_f_hist       LDS fixed-point histograms of every expansion's smaller child,
+//                  flushed with integer atomics into one per-expansion accumulator at
+//                  the tree's global fixed-point scale (deterministic, no slab)
+//   k_f_scan       one workgroup per (expansion, feature): accumulator -> smaller
+//                  child's histogram, larger = parent - smaller, both children scanned
+//   k_f_select     one workgroup: per-child best split, replay of best-first order,
+//                  choice of the next round's expansions
+//
+// Row lists: a node at depth d >= 1 keeps its row indices in depth buffer (d - 1) % 4
+// (the root: the bag or identity order). Children of depth-d nodes never overwrite
+// their parent's list, and a speculative expansion is only allowed where the list it
+// would overwrite (the ancestor 4 levels up) belongs to an already committed split, so
+// every final leaf's list stays intact for the score update and leaf renewal.
+//
+// Reference parity: serial_tree_learner.cpp:179-245 (Train loop), :477-622
+// (FindBestSplitsFromHistograms), :766-922 (SplitInner bookkeeping);
+// cuda_single_gpu_tree_learner.cpp:158-345 (the reference's device loop, one split per
+// step); data_partition.hpp:101 (Split); leaf numbering of Tree::Split (tree.cpp:61).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device/tree_kernels.h"
+#include "lgap/split_math.h"
+
+namespace lgap {
+namespace device {
+
+constexpr int kFrontierKmax = 64;   // expansions per round (compile-time cap)
+constexpr int kFrontierBufs = 4;    // depth-indexed row-index buffers
+constexpr int kFrontierIdx = 5;     // index buffers addressed by id: depth buffers {0, 1, 3, 4}, bag 2
+constexpr int kFrontierMaxNodes = 4096;  // computed-node capacity of the select's LDS image
+
+// index-buffer id of depth buffer j (0..3)
+__host__ __device__ inline int FrontierDepthBuf(int j) { return j < 2 ? j : j + 1; }
+
+// node state bits (FArgs::nstate)
+constexpr uint8_t kNodeExpanded = 1;   // children computed
+constexpr uint8_t kNodeCommitted = 2;  // its split is part of the tree (replay)
+
+struct FNode {
+  int buf, start, count;  // local rows: positions [start, start + count) of index buffer `buf`
+  int gcount;             // global row count (data parallel: estimated from the split) / = count
+  int depth, parent;
+  int left;               // first child cid (right = left + 1), -1: not expanded
+  int pad;
+};
+
+// One expansion (the split of node `parent`) of the current round.
+struct FExp {
+  int parent, left, depth;  // cids (right = left + 1); depth of the parent
+  int tile0, ntiles;        // partition tiles [tile0, tile0 + ntiles)
+  int src_buf, start, count;
+  int dst_buf;
+  // split predicate (the parent's SplitKey)
+  int group, offset, num_bin, mfb, default_bin, missing, thr, default_left, is_cat;
+  // written by the partition's post-split block
+  int skip;                  // the children cannot split: no histogram / scan
+  int smaller, larger;       // cids
+  int h_buf, h_start, h_count;  // the smaller child's local rows
+  int pad;
+};
+
+struct FState {
+  int round;        // rounds run (including the root round)
+  int k;            // expansions of the current round
+  int total_tiles;  // partition tiles of the current round
+  int done;
+  unsigned epoch;   // never reset: tags the partition's published tile counts
+  int num_leaves, num_splits;
+  int cid_next;
+  int blocked;      // cid the replay waits for (-1: none)
+  int spec;         // speculative expansions started so far (diagnostics)
+  int pad[6];
+};
+
+// Arguments of the frontier kernels (device pointers into the learner's buffers).
+struct FArgs {
+  const uint32_t* rowbins;
+  const uint8_t* colbins;
+  const float2* gh;  // class-major (cls from tp)
+  int* idx[kFrontierIdx];
+  int N, stride_dw, width, num_groups, TB, F, L, C, kmax;
+  const int* gstart;
+  const DevFeature* feat;
+  const HistTile* tiles;
+  int num_tiles;
+  const uint8_t* used_bytree;
+  const TreeParams* tp;
+  // tree state
+  FState* st;
+  FNode* nodes;         // [C]
+  FExp* exps;           // [kmax]
+  uint32_t* exp_bits;   // [kmax][kMaxCatWords]: categorical left sets of the expansions
+  double2* lsum;        // [C] (sum g, sum h)
+  double* lout;         // [C] leaf outputs
+  LeafBounds* bounds;   // [C]
+  SplitKey* key;        // [C] best split (compact)
+  SplitInfo* best;      // [C] best split (full)
+  uint8_t* spl;         // [C][F] feature still splittable below this node
+  unsigned long long* ic;        // [C] interaction-constraint sets (null: none)
+  const unsigned long long* ic_feat;
+  uint8_t* nstate;      // [C]
+  int* leaf_cid;        // [L] committed leaf -> cid
+  SplitRec* rec;        // [L - 1] committed splits in order
+  LeafRange* range_out; // [L] final leaf ranges (written when done)
+  // histograms
+  double* slots;              // [C][2 TB] per-node histograms (stored bins, fp64)
+  unsigned long long* acc;    // [kmax][2 TB] per-expansion fixed-point accumulators (zero between rounds)
+  const unsigned* ghmax;      // float bits of max|g|, max|h| over the root rows
+  // candidates of the current round: [kmax][2][F]
+  SplitKey* ckey;
+  SplitInfo* cinfo;
+  // partition look-back
+  unsigned long long* tile_pub;
+  unsigned* bar;  // bar[2]: bounded-wait error flag
+  int hist_min_rows, hist_grid;
+  int part_tile;  // rows per partition tile (256 x rows per thread)
+  int max_depth, use_monotone;
+  double monotone_penalty;
+  int max_bin, cat_p2;
+  int use_dp;       // gpu_use_dp: 64-bit LDS accumulators
+  int spec_cap;     // speculative expansions per round beyond the budget (policy knob)
+  int distributed;  // children counts from the split record (global) instead of the partition
+  SplitParams sp;
+};
+
+// launchers (frontier_kernels.hip)
+void LaunchFrontierInit(const FArgs& a, hipStream_t s);
+void LaunchFrontierHist(const FArgs& a, size_t lds_bytes, hipStream_t s);
+void LaunchFrontierScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
+void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
+void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s);
+// resident 256-thread partition blocks per CU (the look-back needs every block resident)
+int FrontierPartitionBlocksPerCU(int iters);
+// one-time kernel attributes (dynamic LDS above 64 KiB)
+void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width);
+size_t FrontierSelectLds(int C, int L);
+
+}  // namespace device
+}  // namespace lgap

@@ -1,0 +1,1157 @@
+// Frontier tree-growth kernels for MI355X (gfx950): see frontier.h for the algorithm.
+//
+// Launch shapes (fixed per learner; the work of a round is read on the device):
+//   k_f_init        1 x 256
+//   k_f_partition   resident grid x 256 (decoupled look-back needs co-residency)
+//   k_f_hist        (hist_grid + kmax) x LDS tiles, 512 threads
+//   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature))
+//   k_f_select      1 x 1024
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "device/frontier.h"
+#include "device/hip_common.h"
+#include "device/split_scan.h"
+#include "lgap/split_math.h"
+
+namespace lgap {
+namespace device {
+namespace {
+
+constexpr int kFPartThreads = 256;
+constexpr int kFHistThreads = 512;
+constexpr int kFScanThreads = 256;
+constexpr int kFSelThreads = 1024;
+#ifndef LGAP_FHIST_R
+#define LGAP_FHIST_R 16
+#endif
+
+__device__ __forceinline__ int FRowAt(const FArgs& a, int buf, int pos) { return buf < 0 ? pos : a.idx[buf][pos]; }
+
+__device__ __forceinline__ uint32_t FColBin(const FArgs& a, int g, int row) {
+  const size_t o = static_cast<size_t>(g) * a.N + row;
+  return a.width == 1 ? a.colbins[o] : reinterpret_cast<const uint16_t*>(a.colbins)[o];
+}
+
+// exponent k of the largest power of two <= x (x > 0): 2^k <= x < 2^(k+1)
+__device__ __forceinline__ int Pow2Exp(double x) {
+  int e;
+  (void)frexp(x, &e);
+  return e - 1;
+}
+
+// Global fixed-point exponents of the tree: every accumulator holds value * 2^E with
+// 2^E <= 2^62 / (root rows * max|value|), so no sum over any subset of the root's rows can
+// overflow an int64 and every partial of every block, expansion and rank is EXACT integer
+// arithmetic at one shared scale (deterministic and order free).
+__device__ __forceinline__ void GlobalScaleExp(const FArgs& a, int* eg, int* eh) {
+  const double n = static_cast<double>(a.tp->root_gcount > 0 ? a.tp->root_gcount : 1);
+  const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
+  constexpr double k62 = 4611686018427387904.0;
+  *eg = gmax > 0.f ? Pow2Exp(k62 / (n * gmax)) : 0;
+  *eh = hmax > 0.f ? Pow2Exp(k62 / (n * hmax)) : 0;
+}
+
+// ---------------------------------------------------------------------------
+// tree setup: the root node, the root "round" (one pseudo-expansion whose smaller child
+// is the root), the committed-leaf table and the node states.
+__global__ __launch_bounds__(256) void k_f_init(FArgs a) {
+  const TreeParams tp = *a.tp;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    FState s;
+    s.round = 0;
+    s.k = 1;
+    s.total_tiles = 0;
+    s.done = 0;
+    s.epoch = a.st->epoch + 1u;
+    s.num_leaves = 1;
+    s.num_splits = 0;
+    s.cid_next = 1;
+    s.blocked = -1;
+    s.spec = 0;
+    for (int i = 0; i < 6; ++i) s.pad[i] = 0;
+    *a.st = s;
+    FNode r;
+    r.buf = tp.root_buf;
+    r.start = 0;
+    r.count = tp.root_count;
+    r.gcount = tp.root_gcount;
+    r.depth = 0;
+    r.parent = -1;
+    r.left = -1;
+    r.pad = 0;
+    a.nodes[0] = r;
+    FExp x;
+    x.parent = -1;
+    x.left = -1;
+    x.depth = -1;
+    x.tile0 = x.ntiles = 0;
+    x.src_buf = tp.root_buf;
+    x.start = 0;
+    x.count = tp.root_count;
+    x.dst_buf = 0;
+    x.group = x.offset = x.num_bin = x.mfb = x.default_bin = x.missing = x.thr = x.default_left = x.is_cat = 0;
+    x.skip = 0;
+    x.smaller = 0;
+    x.larger = -1;
+    x.h_buf = tp.root_buf;
+    x.h_start = 0;
+    x.h_count = tp.root_count;
+    x.pad = 0;
+    a.exps[0] = x;
+    a.bounds[0] = LeafBounds();
+    if (a.ic) a.ic[0] = ~0ull;
+    a.leaf_cid[0] = 0;
+    a.lout[0] = 0.0;
+  }
+  for (int i = t; i < a.C; i += blockDim.x) a.nstate[i] = 0;
+  for (int f = t; f < a.F; f += blockDim.x) a.spl[f] = 1;
+}
+
+// ---------------------------------------------------------------------------
+// k_f_hist: histograms of every expansion's smaller child.
+//
+// The round's smaller-child rows are cut into chunks of >= hist_min_rows rows, at most
+// ~hist_grid chunks in all; block (b, tile) builds the histogram of its chunk for the LDS
+// tile's feature groups and flushes it into the expansion's accumulator with 64-bit
+// integer atomics at the tree's global scale. LDS accumulation:
+//   MODE 0  one ds_add_u64 per (row, group): signed g in the high 32 bits, signed h in the
+//           low 32 bits, at a per-block power-of-two scale (2^30 / (block rows * max));
+//           the flush shifts each block sum up to the global scale (an exact shift);
+//   MODE 1  (gpu_use_dp) two ds_add_u64 per (row, group) at the global scale itself.
+// Zero bins are skipped by the flush (most of a small leaf's histogram).
+template <int W, int MODE>
+__device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
+                                          const int* gst, unsigned long long* hist, float sg, float sh, double dsg,
+                                          double dsh) {
+  const int tpr = tile.d1 - tile.d0;
+  const int rpi = blockDim.x / tpr;
+  const int myr = threadIdx.x / tpr;
+  const int myd = threadIdx.x - myr * tpr;
+  if (myr >= rpi) return;
+  constexpr int per = 4 / W;
+  constexpr int R = LGAP_FHIST_R;
+  const int dw = tile.d0 + myd;
+  const int gfirst = dw * per;
+  int go[per];
+#pragma unroll
+  for (int k = 0; k < per; ++k) go[k] = gfirst + k < tile.g1 ? gst[gfirst + k - tile.g0] : -1;
+  const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
+  const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
+  const int base = buf < 0 ? start : 0;
+  for (int p0 = rb + myr; p0 < re; p0 += rpi * R) {
+    int rows[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = p0 + j * rpi;
+      rows[j] = p < re ? (idx ? idx[p] : base + p) : -1;
+    }
+    uint32_t word[R];
+    float2 v[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
+      v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      unsigned long long pg, ph = 0ull;
+      if (MODE == 0) {
+        const long long ig = __float2int_rn(v[j].x * sg);
+        const long long ih = __float2int_rn(v[j].y * sh);
+        pg = (static_cast<unsigned long long>(ig) << 32) + static_cast<unsigned long long>(ih);
+      } else {
+        pg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v[j].x) * dsg));
+        ph = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v[j].y) * dsh));
+      }
+#pragma unroll
+      for (int k = 0; k < per; ++k) {
+        const uint32_t b = W == 1 ? ((word[j] >> (8 * k)) & 0xFFu) : ((word[j] >> (16 * k)) & 0xFFFFu);
+        if (b != 0u && go[k] >= 0) {
+          const int o = go[k] + static_cast<int>(b);
+          if (MODE == 0) {
+            atomicAdd(&hist[o], pg);
+          } else {
+            atomicAdd(&hist[2 * o], pg);
+            atomicAdd(&hist[2 * o + 1], ph);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int W, int MODE>
+__global__ __launch_bounds__(kFHistThreads) void k_f_hist(FArgs a) {
+  extern __shared__ __align__(8) unsigned char lds_raw[];
+  __shared__ int s_e, s_rb, s_re, s_buf, s_start;
+  const FState* sp = a.st;
+  if (sp->done) return;
+  const int k = sp->k;
+  const int t = threadIdx.x;
+  if (t < 64) {
+    // per-expansion chunking (identical in every block): chunk rows c for the whole round,
+    // nb_e chunks of expansion e, blocks [pre_e, pre_e + nb_e)
+    int cnt = 0, hb = -1, hs = 0;
+    if (t < k) {
+      const FExp& x = a.exps[t];
+      if (!x.skip) {
+        cnt = x.h_count;
+        hb = x.h_buf;
+        hs = x.h_start;
+      }
+    }
+    const int total = WaveSum(cnt);
+    const int c = max(a.hist_min_rows, (total + a.hist_grid - 1) / max(1, a.hist_grid));
+    const int nb = (cnt + c - 1) / c;
+    const int inc = WaveInclusiveScan(nb);
+    const int bx = static_cast<int>(blockIdx.x);
+    const bool mine = t < k && nb > 0 && bx >= inc - nb && bx < inc;
+    const unsigned long long m = __ballot(mine);
+    if (mine) {
+      const int j = bx - (inc - nb);
+      const int chunk = (cnt + nb - 1) / nb;
+      s_e = t;
+      s_rb = j * chunk;
+      s_re = min(cnt, (j + 1) * chunk);
+      s_buf = hb;
+      s_start = hs;
+    }
+    if (t == 0 && m == 0ull) s_e = -1;
+  }
+  __syncthreads();
+  const int e = s_e;
+  if (e < 0) return;
+  const int rb = s_rb, re = s_re, buf = s_buf, start = s_start;
+  const HistTile tile = a.tiles[blockIdx.y];
+  unsigned long long* acc = a.acc + static_cast<size_t>(e) * 2 * a.TB;
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
+  const double dsg = ldexp(1.0, EG), dsh = ldexp(1.0, EH);
+  if (tile.direct) {
+    // groups too wide for LDS: each row's fixed-point value straight into the accumulator
+    int* gst = reinterpret_cast<int*>(lds_raw);
+    for (int g = tile.g0 + t; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g];
+    __syncthreads();
+    const int tpr = tile.d1 - tile.d0;
+    const int rpi = blockDim.x / tpr;
+    const int myr = t / tpr, myd = t - myr * tpr;
+    if (myr >= rpi) return;
+    constexpr int per = 4 / W;
+    const int dw = tile.d0 + myd;
+    const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
+    for (int p = rb + myr; p < re; p += rpi) {
+      const int row = FRowAt(a, buf, start + p);
+      const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
+      const float2 v = gh[row];
+      const unsigned long long qg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.x) * dsg));
+      const unsigned long long qh = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.y) * dsh));
+#pragma unroll
+      for (int kk = 0; kk < per; ++kk) {
+        const uint32_t b = W == 1 ? ((word >> (8 * kk)) & 0xFFu) : ((word >> (16 * kk)) & 0xFFFFu);
+        const int g = dw * per + kk;
+        if (b != 0u && g < tile.g1) {
+          const int o = gst[g - tile.g0] + static_cast<int>(b);
+          atomicAdd(&acc[2 * o], qg);
+          atomicAdd(&acc[2 * o + 1], qh);
+        }
+      }
+    }
+    return;
+  }
+  const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
+  const double rows_in_block = static_cast<double>(re - rb > 0 ? re - rb : 1);
+  constexpr double k30 = 1073741824.0;
+  const int bg = gmax > 0.f ? Pow2Exp(k30 / (rows_in_block * gmax)) : 0;
+  const int bh = hmax > 0.f ? Pow2Exp(k30 / (rows_in_block * hmax)) : 0;
+  const float sg = ldexpf(1.f, bg), sh = ldexpf(1.f, bh);
+  const int words = MODE == 0 ? tile.nbins : 2 * tile.nbins;
+  unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
+  int* gst = reinterpret_cast<int*>(hist + words);
+  for (int i = t; i < words; i += blockDim.x) hist[i] = 0ull;
+  for (int g = tile.g0 + t; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
+  __syncthreads();
+  FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh);
+  __syncthreads();
+  unsigned long long* out = acc + 2 * static_cast<size_t>(tile.bin0);
+  if (MODE == 0) {
+    // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
+    // GlobalScaleExp; the guard keeps a degenerate max of 0 harmless)
+    const int shg = max(0, EG - bg), shh = max(0, EH - bh);
+    for (int i = t; i < tile.nbins; i += blockDim.x) {
+      const unsigned long long x = hist[i];
+      if (x == 0ull) continue;
+      const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
+      const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
+      const long long qg = gs * (1ll << shg);
+      const long long qh = static_cast<long long>(hs) * (1ll << shh);
+      if (qg) atomicAdd(&out[2 * i], static_cast<unsigned long long>(qg));
+      if (qh) atomicAdd(&out[2 * i + 1], static_cast<unsigned long long>(qh));
+    }
+  } else {
+    for (int i = t; i < 2 * tile.nbins; i += blockDim.x) {
+      const unsigned long long x = hist[i];
+      if (x) atomicAdd(&out[i], x);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_f_scan: one workgroup per (expansion, feature), grid-stride.
+//  1. accumulator -> the smaller child's histogram (fp64, LDS + its node slot), the
+//     accumulator words re-zeroed for the next round; larger = parent - smaller
+//  2. most-frequent bins from the leaf sums; wave 0 scans the smaller child, wave 1 the
+//     larger one (split_scan.h), both from LDS
+//  3. the two candidates -> the round's candidate table [e][sel][f]
+__global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ int s_skip, s_splp;
+  __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
+  __shared__ SplitKey s_key[2];
+  SplitInfo* s_out = reinterpret_cast<SplitInfo*>(s_out_raw);
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int k = stp->k, F = a.F;
+  const int total = k * F;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
+  const double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
+  const size_t TB2 = 2 * static_cast<size_t>(a.TB);
+  double* hs_full = reinterpret_cast<double*>(smem);
+  double* hl_full = hs_full + 2 * a.max_bin;
+  int* order = reinterpret_cast<int*>(hl_full + 2 * a.max_bin);
+  double* ckey = reinterpret_cast<double*>(order + 2 * a.cat_p2);
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    const int e = item / F, f = item - e * F;
+    const FExp& xr = a.exps[e];
+    if (xr.skip) continue;
+    const int cs = xr.smaller, cl = xr.larger, p = xr.parent;
+    const DevFeature fi = a.feat[f];
+    const int nbin = fi.num_bin;
+    const int nv = 2 * (nbin - 1);
+    const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
+    unsigned long long* acc = a.acc + static_cast<size_t>(e) * TB2 + v0;
+    const double* gp = (p >= 0 && cl >= 0) ? a.slots + static_cast<size_t>(p) * TB2 + v0 : nullptr;
+    double* gs = a.slots + static_cast<size_t>(cs) * TB2 + v0;
+    double* gl = cl >= 0 ? a.slots + static_cast<size_t>(cl) * TB2 + v0 : nullptr;
+    // leaf statistics the scanning waves use (lane 0 of waves 0 / 1)
+    const int my = w == 0 ? cs : (w == 1 ? cl : -1);
+    double2 pre_sum = make_double2(0.0, 0.0);
+    int pre_n = 0, pre_depth = 0;
+    double pre_out = 0.0;
+    LeafBounds pre_bounds;
+    if (lane == 0 && my >= 0) {
+      pre_sum = a.lsum[my];
+      pre_n = a.nodes[my].gcount;
+      pre_depth = a.nodes[my].depth;
+      pre_out = a.lout[my];
+      pre_bounds = a.bounds[my];
+    }
+    if (t == 0) {
+      s_skip = !a.used_bytree[f];
+      s_splp = p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1;
+    }
+    for (int v = t; v < nv; v += blockDim.x) {
+      const long long q = static_cast<long long>(acc[v]);
+      acc[v] = 0ull;
+      const double sv = static_cast<double>(q) * ((v & 1) ? inv_h : inv_g);
+      const int kk = v >> 1;
+      const int b = kk < fi.mfb ? kk : kk + 1;
+      hs_full[2 * b + (v & 1)] = sv;
+      gs[v] = sv;
+      if (gl) {
+        const double lv = gp[v] - sv;
+        hl_full[2 * b + (v & 1)] = lv;
+        gl[v] = lv;
+      }
+    }
+    if (t < 2) {
+      s_out[t].Reset();
+      SplitKey kz;
+      kz.gain = kMinScore;
+      kz.feature = -1;
+      kz.threshold = 0;
+      kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
+      kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
+      kz.pos = f;
+      kz.pad2 = 0;
+      s_key[t] = kz;
+    }
+    __syncthreads();
+    const bool skip_both = s_skip || !s_splp;
+    // most-frequent bin = leaf total - stored bins
+    if (w < 2 && my >= 0) {
+      double* H = w == 0 ? hs_full : hl_full;
+      double sgs = 0.0, shs = 0.0;
+      for (int b = lane; b < nbin; b += 64) {
+        if (b == fi.mfb) continue;
+        sgs += H[2 * b];
+        shs += H[2 * b + 1];
+      }
+      sgs = WaveSum(sgs);
+      shs = WaveSum(shs);
+      if (lane == 0) {
+        H[2 * fi.mfb] = pre_sum.x - sgs;
+        H[2 * fi.mfb + 1] = pre_sum.y - shs;
+      }
+    }
+    __syncthreads();
+    if (w < 2 && my >= 0) {
+      SplitInfo* out = &s_out[w];
+      const double sg = __shfl(pre_sum.x, 0, kWave), sh = __shfl(pre_sum.y, 0, kWave);
+      const int n = __shfl(pre_n, 0, kWave);
+      const int depth = __shfl(pre_depth, 0, kWave);
+      if (!skip_both) {
+        const double* H = w ? hl_full : hs_full;
+        double po;
+        if (p < 0) {
+          SplitParams p0 = a.sp;
+          p0.path_smooth = 0.0;
+          po = LeafOutputRaw(sg, sh, p0, n, 0.0);
+          if (f == 0 && lane == 0) a.lout[0] = po;
+        } else {
+          po = __shfl(pre_out, 0, kWave);
+        }
+        LeafBounds bounds;
+        bounds.min = __shfl(pre_bounds.min, 0, kWave);
+        bounds.max = __shfl(pre_bounds.max, 0, kWave);
+        bool spl;
+        if (fi.bin_type == 0) {
+          spl = ScanNumericalWave(a.sp, fi, H, sg, sh, n, po, bounds, 0, out);
+        } else {
+          FeatureScanMeta m;
+          m.num_bin = fi.num_bin;
+          m.default_bin = static_cast<uint32_t>(fi.default_bin);
+          m.missing_type = fi.missing;
+          m.bin_type = fi.bin_type;
+          m.monotone = fi.monotone;
+          m.penalty = fi.penalty;
+          m.rand_threshold = 0;
+          if (lane == 0) out->Reset();
+          spl = ScanCategoricalWave(a.sp, m, H, sg, sh, n, po, bounds, a.cat_p2, order + w * a.cat_p2,
+                                    ckey + w * a.cat_p2, out);
+        }
+        if (lane == 0) {
+          a.spl[static_cast<size_t>(my) * F + f] = spl ? 1 : 0;
+          if (!spl) {
+            out->Reset();
+          } else {
+            out->feature = f;
+            if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
+            if (a.ic && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
+          }
+        }
+      } else if (lane == 0) {
+        // feature not tried: the children inherit the parent's flag
+        a.spl[static_cast<size_t>(my) * F + f] = static_cast<uint8_t>(s_splp);
+        if (p < 0 && f == 0) {
+          SplitParams p0 = a.sp;
+          p0.path_smooth = 0.0;
+          a.lout[0] = LeafOutputRaw(sg, sh, p0, n, 0.0);
+        }
+      }
+      if (lane == 0) {
+        SplitKey& kk = s_key[w];
+        kk.feature = out->feature;
+        kk.gain = SafeGain(*out);
+        kk.threshold = out->threshold;
+        kk.group = fi.group;
+        kk.offset = fi.offset;
+        kk.num_bin = fi.num_bin;
+        kk.mfb = fi.mfb;
+        kk.default_bin = fi.default_bin;
+        kk.missing = fi.missing;
+        kk.default_left = out->default_left;
+        kk.is_cat = fi.bin_type != 0 ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    // publish the candidates (dword-parallel copies of the LDS records)
+    constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+    constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+    const int nsel = cl >= 0 ? 2 : 1;
+    for (int i = t; i < nsel * (kKeyWords + kInfoWords); i += blockDim.x) {
+      const int sel = i / (kKeyWords + kInfoWords);
+      const int o = i - sel * (kKeyWords + kInfoWords);
+      const size_t q = (static_cast<size_t>(e) * 2 + sel) * F + f;
+      if (o < kKeyWords) {
+        reinterpret_cast<uint32_t*>(a.ckey + q)[o] = reinterpret_cast<const uint32_t*>(&s_key[sel])[o];
+      } else {
+        reinterpret_cast<uint32_t*>(a.cinfo + q)[o - kKeyWords] = reinterpret_cast<const uint32_t*>(&s_out[sel])[o - kKeyWords];
+      }
+    }
+    __syncthreads();  // LDS reused by the next item
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_f_partition: stable 2-way partition of every expanded parent (reference
+// data_partition.hpp:101 / cuda_data_partition.cu:290-937, as one launch).
+// Tiles of all expansions are numbered globally ([tile0_e, tile0_e + ntiles_e) for
+// expansion e). Every block first counts all of its tiles and publishes each count as a
+// 64-bit {epoch, count} granule, then scatters its tiles: a tile waits only for the
+// counts of the earlier tiles OF ITS EXPANSION (decoupled look-back); lefts go to the
+// front of the parent's range in order, rights fill it from the end. The block that
+// scatters an expansion's last tile knows its total left count and writes the two
+// children (post-split bookkeeping of serial_tree_learner.cpp:766-922).
+
+__device__ __forceinline__ void FPublish(unsigned long long* p, unsigned epoch, int cnt) {
+  const unsigned long long v = (static_cast<unsigned long long>(epoch) << 32) | static_cast<unsigned>(cnt);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int FAwait(const FArgs& a, int i, unsigned epoch) {
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned long long v = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (static_cast<unsigned>(v >> 32) == epoch) return static_cast<int>(static_cast<unsigned>(v));
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 1023u) == 0u &&
+        (spins > (1u << 22) || __hip_atomic_load(&a.bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+      __hip_atomic_store(&a.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0;
+    }
+  }
+}
+
+// sum of the published counts of tiles [i0, i1)
+__device__ int FSumCounts(const FArgs& a, int i0, int i1, unsigned epoch, int* sh) {
+  int s = 0;
+  for (int i = i0 + static_cast<int>(threadIdx.x); i < i1; i += blockDim.x) s += FAwait(a, i, epoch);
+  return BlockSumInt(s, sh);
+}
+
+// children of expansion x (one thread)
+__device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
+  const SplitInfo& bi = a.best[x.parent];
+  const double lsg = bi.left_sum_gradient, lsh = bi.left_sum_hessian;
+  const double rsg = bi.right_sum_gradient, rsh = bi.right_sum_hessian;
+  const double lo = bi.left_output, ro = bi.right_output;
+  const int ilc = bi.left_count, irc = bi.right_count;
+  const int8_t mono = bi.monotone_type;
+  const int16_t ncat = bi.num_cat_threshold;
+  const int feature = bi.feature;
+  LeafBounds bl = a.bounds[x.parent];
+  const unsigned long long icm = a.ic ? (a.ic[x.parent] & a.ic_feat[feature]) : 0ull;
+  const int rc = x.count - lc;
+  const int glc = a.distributed ? ilc : lc;
+  const int grc = a.distributed ? irc : rc;
+  const int l = x.left, r = x.left + 1;
+  const int dep = x.depth + 1;
+  FNode nl, nr;
+  nl.buf = nr.buf = x.dst_buf;
+  nl.start = x.start;
+  nl.count = lc;
+  nl.gcount = glc;
+  nr.start = x.start + lc;
+  nr.count = rc;
+  nr.gcount = grc;
+  nl.depth = nr.depth = dep;
+  nl.parent = nr.parent = x.parent;
+  nl.left = nr.left = -1;
+  nl.pad = nr.pad = 0;
+  a.nodes[l] = nl;
+  a.nodes[r] = nr;
+  a.lsum[l] = make_double2(lsg, lsh);
+  a.lsum[r] = make_double2(rsg, rsh);
+  a.lout[l] = lo;
+  a.lout[r] = ro;
+  LeafBounds br = bl;
+  if (a.use_monotone && ncat == 0) {
+    const double mid = (lo + ro) / 2.0f;
+    if (mono < 0) {
+      bl.min = fmax(bl.min, mid);
+      br.max = fmin(br.max, mid);
+    } else if (mono > 0) {
+      bl.max = fmin(bl.max, mid);
+      br.min = fmax(br.min, mid);
+    }
+  }
+  a.bounds[l] = bl;
+  a.bounds[r] = br;
+  if (a.ic) {
+    a.ic[l] = icm;
+    a.ic[r] = icm;
+  }
+  const int md = a.sp.min_data_in_leaf;
+  const bool skip = (a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2);
+  const bool left_smaller = glc < grc;
+  FExp* xo = a.exps + e;
+  xo->skip = skip ? 1 : 0;
+  xo->smaller = left_smaller ? l : r;
+  xo->larger = left_smaller ? r : l;
+  xo->h_buf = x.dst_buf;
+  xo->h_start = left_smaller ? x.start : x.start + lc;
+  xo->h_count = left_smaller ? lc : rc;
+}
+
+template <int ITERS>
+__global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
+  constexpr int kTile = kFPartThreads * ITERS;
+  __shared__ int s_t0[kFrontierKmax + 1];
+  __shared__ FExp s_x[kFrontierKmax];
+  __shared__ uint32_t s_bits[kFrontierKmax][kMaxCatWords];
+  __shared__ int sh[8];
+  __shared__ int s_wl[ITERS][kFPartThreads / 64];
+  __shared__ int s_wv[ITERS][kFPartThreads / 64];
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int k = stp->k, T = stp->total_tiles;
+  const unsigned epoch = stp->epoch;
+  const int bid = static_cast<int>(blockIdx.x), G = static_cast<int>(gridDim.x);
+  if (bid >= T) return;
+  const int t = threadIdx.x;
+  // the round's expansions (dword-parallel copy) and their categorical sets
+  constexpr int kXWords = static_cast<int>(sizeof(FExp) / 4);
+  for (int i = t; i < k * kXWords; i += blockDim.x) {
+    reinterpret_cast<uint32_t*>(s_x)[i] = reinterpret_cast<const uint32_t*>(a.exps)[i];
+  }
+  for (int i = t; i < k * kMaxCatWords; i += blockDim.x) s_bits[i / kMaxCatWords][i % kMaxCatWords] = a.exp_bits[i];
+  __syncthreads();
+  if (t <= k) s_t0[t] = t < k ? s_x[t].tile0 : T;
+  __syncthreads();
+  auto find = [&](int tile) {
+    int lo = 0, hi = k - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_t0[mid] <= tile) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  // split predicate of expansion e (GoLeft of split_scan.h, categorical set read from LDS)
+  auto go_left = [&](int e, uint32_t gb) {
+    const FExp& x = s_x[e];
+    const uint32_t b = DecodeBin(x.offset, x.num_bin, x.mfb, gb);
+    if (x.is_cat) {
+      const uint32_t wd = b >> 5;
+      return wd < static_cast<uint32_t>(kMaxCatWords) && ((s_bits[e][wd] >> (b & 31u)) & 1u);
+    }
+    if ((x.missing == 1 && b == static_cast<uint32_t>(x.default_bin)) ||
+        (x.missing == 2 && b == static_cast<uint32_t>(x.num_bin - 1))) {
+      return x.default_left != 0;
+    }
+    return b <= static_cast<uint32_t>(x.thr);
+  };
+  // phase 1: count every own tile and publish (the first tile's rows stay in registers)
+  int rows0[ITERS];
+  uint32_t gb0[ITERS];
+  for (int tile = bid; tile < T; tile += G) {
+    const int e = find(tile);
+    const FExp& x = s_x[e];
+    const int pos0 = (tile - x.tile0) * kTile + t;
+    int rows[ITERS];
+#pragma unroll
+    for (int j = 0; j < ITERS; ++j) {
+      const int pos = pos0 + j * kFPartThreads;
+      rows[j] = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
+    }
+    uint32_t gb[ITERS];
+#pragma unroll
+    for (int j = 0; j < ITERS; ++j) gb[j] = rows[j] >= 0 ? FColBin(a, x.group, rows[j]) : 0u;
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < ITERS; ++j) cnt += (rows[j] >= 0 && go_left(e, gb[j])) ? 1 : 0;
+    cnt = BlockSumInt(cnt, sh);
+    if (t == 0) FPublish(&a.tile_pub[tile], epoch, cnt);
+    if (tile == bid) {
+#pragma unroll
+      for (int j = 0; j < ITERS; ++j) {
+        rows0[j] = rows[j];
+        gb0[j] = gb[j];
+      }
+    }
+  }
+  // phase 2: scatter
+  const int lane = t & 63, w = t >> 6;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int tile = bid; tile < T; tile += G) {
+    const int e = find(tile);
+    const FExp& x = s_x[e];
+    int lbase = FSumCounts(a, x.tile0, tile, epoch, sh);
+    const int tt = tile - x.tile0;
+    int rbase = tt * kTile - lbase;
+    int rows[ITERS];
+    uint32_t gb[ITERS];
+    if (tile == bid) {
+#pragma unroll
+      for (int j = 0; j < ITERS; ++j) {
+        rows[j] = rows0[j];
+        gb[j] = gb0[j];
+      }
+    } else {
+      const int pos0 = tt * kTile + t;
+#pragma unroll
+      for (int j = 0; j < ITERS; ++j) {
+        const int pos = pos0 + j * kFPartThreads;
+        rows[j] = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
+      }
+#pragma unroll
+      for (int j = 0; j < ITERS; ++j) gb[j] = rows[j] >= 0 ? FColBin(a, x.group, rows[j]) : 0u;
+    }
+    int* out = a.idx[x.dst_buf] + x.start;
+#pragma unroll
+    for (int j = 0; j < ITERS; ++j) {
+      const bool valid = rows[j] >= 0;
+      const bool left = valid && go_left(e, gb[j]);
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      if (lane == 0) {
+        s_wl[j][w] = __popcll(ml);
+        s_wv[j][w] = __popcll(mv);
+      }
+    }
+    __syncthreads();
+    int tile_left = 0;
+#pragma unroll
+    for (int j = 0; j < ITERS; ++j) {
+      const bool valid = rows[j] >= 0;
+      const bool left = valid && go_left(e, gb[j]);
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      int pl = 0, pv = 0, tl = 0, tv = 0;
+#pragma unroll
+      for (int i = 0; i < kFPartThreads / 64; ++i) {
+        if (i < w) {
+          pl += s_wl[j][i];
+          pv += s_wv[j][i];
+        }
+        tl += s_wl[j][i];
+        tv += s_wv[j][i];
+      }
+      if (valid) {
+        const int rl = pl + __popcll(ml & lt_mask);
+        const int rv = pv + __popcll(mv & lt_mask);
+        if (left) out[lbase + rl] = rows[j];
+        else out[x.count - 1 - (rbase + (rv - rl))] = rows[j];
+      }
+      lbase += tl;
+      rbase += tv - tl;
+      tile_left += tl;
+    }
+    __syncthreads();
+    if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_f_select: one workgroup.
+//  A. per-child best split of the last round's children: arg-max over the features'
+//     candidates (gain desc, feature asc: SplitInfo::BetterThan), full record -> best[c]
+//  B. replay of best-first order over the committed leaves (wave 0, all in LDS): the leaf
+//     with the largest gain (ties: smaller feature, then smaller leaf, as the sequential
+//     select) is split if its node has been expanded, else the replay stops there
+//  C. the committed splits -> SplitRec[] (tree order), leaf -> node table
+//  D. the next round's expansions: the blocked node first, then the open nodes by gain,
+//     as many as the remaining split budget can still use (+ spec_cap), under the
+//     row-list rule (the list a child overwrites belongs to a committed split)
+__device__ __forceinline__ bool FBetter(double ga, int fa, int la, double gb, int fb, int lb) {
+  if (ga != gb) return ga > gb;
+  if (fa != fb) return fa < fb;
+  return la < lb;
+}
+
+__global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int C = a.C, L = a.L, F = a.F;
+  double* s_gain = reinterpret_cast<double*>(smem);          // [C]
+  int* s_feat = reinterpret_cast<int*>(s_gain + C);          // [C]
+  int* s_left = s_feat + C;                                  // [C]
+  int* s_par = s_left + C;                                   // [C]
+  int* s_dep = s_par + C;                                    // [C]
+  int* s_rank = s_dep + C;                                   // [C] eligible: rank key, else -1
+  int* s_lcid = s_rank + C;                                  // [L]
+  int* s_c0 = s_lcid + L;                                    // [L] committed leaves of this launch
+  int* s_c1 = s_c0 + L;                                      // [L] their cids
+  uint8_t* s_st = reinterpret_cast<uint8_t*>(s_c1 + L);      // [C]
+  __shared__ int s_cpos[2 * kFrontierKmax];                  // winning candidate position of this round's children
+  __shared__ int s_child[2 * kFrontierKmax];                 // their cids (-1: none)
+  __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_nelig, s_eunc, s_k, s_tiles;
+  __shared__ int s_exp[kFrontierKmax];                       // chosen expansions (cids) by order
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const FState st = *a.st;
+  if (st.done) return;
+  const int kprev = st.k;
+  const int cid_next = st.cid_next;
+  // ---- image of the computed nodes
+  for (int c = t; c < cid_next; c += blockDim.x) {
+    const SplitKey& kk = a.key[c];
+    const FNode nd = a.nodes[c];
+    s_gain[c] = kk.feature < 0 ? kMinScore : kk.gain;
+    s_feat[c] = kk.feature;
+    s_left[c] = nd.left;
+    s_par[c] = nd.parent;
+    s_dep[c] = nd.depth;
+    s_st[c] = a.nstate[c];
+    s_rank[c] = -1;
+  }
+  for (int l = t; l < st.num_leaves; l += blockDim.x) s_lcid[l] = a.leaf_cid[l];
+  if (t < 2 * kFrontierKmax) {
+    s_child[t] = -1;
+    s_cpos[t] = -1;
+  }
+  // this round's children are cids [base, base + 2 kprev) (the root round: cid 0)
+  const int base = cid_next - 2 * kprev;
+  __syncthreads();
+  // ---- A. children of the last round: best over features
+  for (int q = w; q < 2 * kprev; q += kFSelThreads / 64) {
+    const int e = q >> 1, sel = q & 1;
+    const FExp& x = a.exps[e];
+    const int c = sel ? x.larger : x.smaller;
+    if (c < 0) continue;
+    double bg = kMinScore;
+    int bf = 0x7fffffff, bpos = -1;
+    if (!x.skip) {
+      for (int f = lane; f < F; f += 64) {
+        const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+        const double g = kk.feature < 0 ? kMinScore : kk.gain;
+        const int ff = kk.feature < 0 ? 0x7fffffff : kk.feature;
+        if (FBetter(g, ff, 0, bg, bf, 0)) {
+          bg = g;
+          bf = ff;
+          bpos = f;
+        }
+      }
+    }
+    const int src = WaveArgBestLane(bg, bf, 0);
+    bg = ReadLane(bg, src);
+    bf = ReadLane(bf, src);
+    bpos = ReadLane(bpos, src);
+    const bool valid = bf != 0x7fffffff && bpos >= 0;
+    // full record -> best[c], compact key -> key[c]
+    constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+    constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+    if (valid) {
+      const size_t pos = static_cast<size_t>(q) * F + bpos;
+      for (int i = lane; i < kInfoWords; i += 64) {
+        reinterpret_cast<uint32_t*>(a.best + c)[i] = reinterpret_cast<const uint32_t*>(a.cinfo + pos)[i];
+      }
+      for (int i = lane; i < kKeyWords; i += 64) {
+        reinterpret_cast<uint32_t*>(a.key + c)[i] = reinterpret_cast<const uint32_t*>(a.ckey + pos)[i];
+      }
+    } else if (lane == 0) {
+      a.best[c].Reset();
+      SplitKey kz;
+      kz.gain = kMinScore;
+      kz.feature = -1;
+      kz.threshold = 0;
+      kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
+      kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
+      kz.pos = -1;
+      kz.pad2 = 0;
+      a.key[c] = kz;
+    }
+    if (lane == 0) {
+      s_gain[c] = valid ? bg : kMinScore;
+      s_feat[c] = valid ? bf : -1;
+      s_child[q] = c;
+      // (keys / records written above are read back by LATER launches only; this launch
+      // reads the candidate table, which an earlier launch wrote)
+      s_cpos[c - base] = valid ? q * F + bpos : -1;
+    }
+  }
+  __syncthreads();
+  // ---- B. replay (wave 0)
+  if (w == 0) {
+    int nl = st.num_leaves, ns = st.num_splits, done = 0, blocked = -1, nc = 0;
+    for (;;) {
+      if (nl >= L) {
+        done = 1;
+        break;
+      }
+      double bg = kMinScore;
+      int bf = 0x7fffffff, bl = 0x7fffffff;
+      for (int l = lane; l < nl; l += 64) {
+        const int c = s_lcid[l];
+        const int f = s_feat[c];
+        const double g = f < 0 ? kMinScore : s_gain[c];
+        const int ff = f < 0 ? 0x7fffffff : f;
+        if (FBetter(g, ff, l, bg, bf, bl)) {
+          bg = g;
+          bf = ff;
+          bl = l;
+        }
+      }
+      const int src = WaveArgBestLane(bg, bf, bl);
+      bg = ReadLane(bg, src);
+      bf = ReadLane(bf, src);
+      bl = ReadLane(bl, src);
+      if (bl == 0x7fffffff || bf == 0x7fffffff || !(bg > 0.0)) {
+        done = 1;
+        break;
+      }
+      const int c = s_lcid[bl];
+      const int left = s_left[c];
+      if (left < 0) {
+        blocked = c;
+        break;
+      }
+      if (lane == 0) {
+        s_c0[nc] = bl;
+        s_c1[nc] = c;
+        s_lcid[bl] = left;
+        s_lcid[nl] = left + 1;
+        s_st[c] |= kNodeCommitted;
+      }
+      ++nc;
+      ++nl;
+      ++ns;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    if (lane == 0) {
+      s_nl = nl;
+      s_ns = ns;
+      s_done = done;
+      s_blocked = blocked;
+      s_ncommit = nc;
+    }
+  }
+  __syncthreads();
+  const int nl = s_nl, ns = s_ns, ncommit = s_ncommit;
+  int done = s_done;
+  // ---- C. committed splits -> records (one wave per split), leaf table, node states
+  for (int i = w; i < ncommit; i += kFSelThreads / 64) {
+    const int leaf = s_c0[i], c = s_c1[i];
+    const int sidx = st.num_splits + i;
+    SplitRec* r = a.rec + sidx;
+    constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+    for (int j = lane; j < kInfoWords; j += 64) {
+      reinterpret_cast<uint32_t*>(&r->info)[j] = reinterpret_cast<const uint32_t*>(a.best + c)[j];
+    }
+    if (lane == 0) {
+      const int left = s_left[c];
+      r->leaf = leaf;
+      r->left_count = a.nodes[left].gcount;
+      r->right_count = a.nodes[left + 1].gcount;
+      r->pad = 0;
+      a.nstate[c] = s_st[c];
+    }
+  }
+  for (int l = t; l < nl; l += blockDim.x) a.leaf_cid[l] = s_lcid[l];
+  // ---- D. next round
+  if (!done) {
+    // eligible open nodes: unexpanded, a positive-gain split, and the row list their children
+    // overwrite (the ancestor kFrontierBufs - 1 levels up) belongs to a committed split
+    for (int c = t; c < cid_next; c += blockDim.x) {
+      bool ok = !(s_st[c] & kNodeExpanded) && s_feat[c] >= 0 && s_gain[c] > 0.0;
+      if (ok) {
+        const int target = s_dep[c] + 1 - kFrontierBufs;
+        if (target >= 1) {
+          int an = c;
+          for (int i = 0; i < kFrontierBufs - 1; ++i) an = s_par[an];
+          ok = (s_st[an] & kNodeCommitted) != 0;
+        }
+      }
+      s_rank[c] = ok ? 0 : -1;
+    }
+    if (t == 0) {
+      s_nelig = 0;
+      s_eunc = 0;
+    }
+    __syncthreads();
+    int ne = 0, eu = 0;
+    for (int c = t; c < cid_next; c += blockDim.x) {
+      ne += s_rank[c] >= 0 ? 1 : 0;
+      eu += ((s_st[c] & kNodeExpanded) && !(s_st[c] & kNodeCommitted)) ? 1 : 0;
+    }
+    ne = WaveSum(ne);
+    eu = WaveSum(eu);
+    if (lane == 0) {
+      atomicAdd(&s_nelig, ne);
+      atomicAdd(&s_eunc, eu);
+    }
+    __syncthreads();
+    const int blocked = s_blocked;
+    // rank: the blocked node first, then gain desc, then cid asc
+    for (int c = t; c < cid_next; c += blockDim.x) {
+      if (s_rank[c] < 0) continue;
+      int r = 0;
+      if (c != blocked) {
+        const double g = s_gain[c];
+        r = blocked >= 0 ? 1 : 0;
+        for (int j = 0; j < cid_next; ++j) {
+          if (j == c || j == blocked || s_rank[j] < 0) continue;
+          const double gj = s_gain[j];
+          r += (gj > g || (gj == g && j < c)) ? 1 : 0;
+        }
+      }
+      s_rank[c] = r;
+    }
+    __syncthreads();
+    const int R = L - 1 - ns;  // splits the tree may still make
+    const int need = R - s_eunc;
+    const int cap_nodes = (C - cid_next) / 2 - (R - 1);
+    int K = min(a.kmax, max(1, need + a.spec_cap));
+    K = min(K, max(1, cap_nodes));
+    K = min(K, s_nelig);
+    if (t == 0) s_k = K;
+    for (int c = t; c < cid_next; c += blockDim.x) {
+      if (s_rank[c] >= 0 && s_rank[c] < K) s_exp[s_rank[c]] = c;
+    }
+    __syncthreads();
+    K = s_k;
+    if (K <= 0) done = 1;  // nothing can be expanded: (only reachable without a blocked node)
+    if (!done && w == 0) {
+      // expansion records, tiles prefix (wave 0; K <= 64)
+      const int kTile = a.part_tile;
+      int ntiles = 0, cnt = 0;
+      FNode nd;
+      int p = -1;
+      if (lane < K) {
+        p = s_exp[lane];
+        nd = a.nodes[p];
+        cnt = nd.count;
+        ntiles = (cnt + kTile - 1) / kTile;
+      }
+      const int inc = WaveInclusiveScan(ntiles);
+      if (lane < K) {
+        FExp x;
+        x.parent = p;
+        x.left = cid_next + 2 * lane;
+        x.depth = nd.depth;
+        x.tile0 = inc - ntiles;
+        x.ntiles = ntiles;
+        x.src_buf = nd.buf;
+        x.start = nd.start;
+        x.count = nd.count;
+        x.dst_buf = FrontierDepthBuf(nd.depth % kFrontierBufs);
+        const int cpos = (p >= base && p - base < 2 * kFrontierKmax) ? s_cpos[p - base] : -1;
+        const SplitKey kk = cpos >= 0 ? a.ckey[cpos] : a.key[p];
+        x.group = kk.group;
+        x.offset = kk.offset;
+        x.num_bin = kk.num_bin;
+        x.mfb = kk.mfb;
+        x.default_bin = kk.default_bin;
+        x.missing = kk.missing;
+        x.thr = static_cast<int>(kk.threshold);
+        x.default_left = kk.default_left;
+        x.is_cat = kk.is_cat;
+        x.skip = 0;
+        x.smaller = x.larger = -1;
+        x.h_buf = x.h_start = x.h_count = 0;
+        x.pad = 0;
+        a.exps[lane] = x;
+        a.nodes[p].left = cid_next + 2 * lane;
+        a.nstate[p] = s_st[p] | kNodeExpanded;
+      }
+      if (lane == 63) s_tiles = inc;
+    }
+    __syncthreads();
+    if (!done) {
+      // categorical left sets of the expansions
+      for (int i = t; i < K * kMaxCatWords; i += blockDim.x) {
+        const int e = i / kMaxCatWords, wd = i - e * kMaxCatWords;
+        const int p = s_exp[e];
+        const int cpos = (p >= base && p - base < 2 * kFrontierKmax) ? s_cpos[p - base] : -1;
+        a.exp_bits[i] = cpos >= 0 ? a.cinfo[cpos].cat_bitset[wd] : a.best[p].cat_bitset[wd];
+      }
+    }
+  }
+  if (t == 0) {
+    FState ns_;
+    ns_ = st;
+    ns_.round = st.round + 1;
+    ns_.num_leaves = nl;
+    ns_.num_splits = ns;
+    ns_.done = done;
+    ns_.blocked = s_blocked;
+    if (!done) {
+      ns_.k = s_k;
+      ns_.total_tiles = s_tiles;
+      ns_.epoch = st.epoch + 1u;
+      ns_.cid_next = cid_next + 2 * s_k;
+      ns_.spec = st.spec + s_k;
+    } else {
+      ns_.k = 0;
+      ns_.total_tiles = 0;
+    }
+    *a.st = ns_;
+  }
+  if (done) {
+    for (int l = t; l < nl; l += blockDim.x) {
+      const FNode nd = a.nodes[s_lcid[l]];
+      LeafRange r;
+      r.buf = nd.buf;
+      r.start = nd.start;
+      r.count = nd.count;
+      r.pad = 0;
+      a.range_out[l] = r;
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launchers
+
+void LaunchFrontierInit(const FArgs& a, hipStream_t s) {
+  k_f_init<<<1, 256, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
+  const dim3 grid(a.hist_grid + a.kmax, a.num_tiles);
+  if (a.use_dp) {
+    if (a.width == 1) k_f_hist<1, 1><<<grid, kFHistThreads, lds, s>>>(a);
+    else k_f_hist<2, 1><<<grid, kFHistThreads, lds, s>>>(a);
+  } else {
+    if (a.width == 1) k_f_hist<1, 0><<<grid, kFHistThreads, lds, s>>>(a);
+    else k_f_hist<2, 0><<<grid, kFHistThreads, lds, s>>>(a);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
+  const int grid = std::max(1, std::min(a.kmax * a.F, 4096));
+  k_f_scan<<<grid, kFScanThreads, lds, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+size_t FrontierSelectLds(int C, int L) {
+  return static_cast<size_t>(C) * (sizeof(double) + 5 * sizeof(int) + 1) + 3 * static_cast<size_t>(L) * sizeof(int) + 64;
+}
+
+void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
+  k_f_select<<<1, kFSelThreads, FrontierSelectLds(a.C, a.L), s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s) {
+  if (iters == 4) k_f_partition<4><<<grid, kFPartThreads, 0, s>>>(a);
+  else if (iters == 16) k_f_partition<16><<<grid, kFPartThreads, 0, s>>>(a);
+  else k_f_partition<8><<<grid, kFPartThreads, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+int FrontierPartitionBlocksPerCU(int iters) {
+  int per_cu = 0;
+  const void* fn = iters == 4 ? reinterpret_cast<const void*>(k_f_partition<4>)
+                              : (iters == 16 ? reinterpret_cast<const void*>(k_f_partition<16>)
+                                             : reinterpret_cast<const void*>(k_f_partition<8>));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kFPartThreads, 0));
+  return per_cu;
+}
+
+void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
+  if (hist_lds > 64 * 1024) {
+    const void* fn = use_dp ? (width == 1 ? reinterpret_cast<const void*>(k_f_hist<1, 1>)
+                                          : reinterpret_cast<const void*>(k_f_hist<2, 1>))
+                            : (width == 1 ? reinterpret_cast<const void*>(k_f_hist<1, 0>)
+                                          : reinterpret_cast<const void*>(k_f_hist<2, 0>));
+    HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds)));
+  }
+  if (scan_lds > 64 * 1024) {
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(scan_lds)));
+  }
+}
+
+}  // namespace device
+}  // namespace lgap

@@ -32,6 +32,8 @@ struct RenewArgs {
   const int* idx0;
   const int* idx1;
   const int* idx2;
+  const int* idx3;  // frontier depth buffers 2 and 3
+  const int* idx4;
   const LeafSeg* segs;  // [num_leaves]
   const int* seg_off;   // [num_leaves + 1] offsets of the leaves in the gathered arrays
   int num_leaves;
