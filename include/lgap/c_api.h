@@ -185,6 +185,7 @@ LIGHTGBM_C_EXPORT int LGBM_NetworkInitWithFunctions(int num_machines, int rank, 
                                                     void* allgather_ext_fun);
 LIGHTGBM_C_EXPORT int LGBM_SetMaxThreads(int num_threads);
 LIGHTGBM_C_EXPORT int LGBM_GetMaxThreads(int* out);
+LIGHTGBM_C_EXPORT int LGBM_GetEffectiveThreads(int* out);
 
 /* ---- Arrow C data interface (struct ArrowArray / ArrowSchema, see lgap/arrow.h) */
 struct ArrowArray;

@@ -11,5 +11,6 @@ void SetDefaultNumThreads(int num_threads);
 void SetMaxNumThreads(int num_threads);
 int MaxNumThreadsSetting();  // LGBM_GetMaxThreads: the cap, -1 when none
 int NumThreads();            // effective team size
+void ApplyNumThreads();      // the effective team size -> the calling thread's OpenMP setting
 
 }  // namespace lgap

@@ -121,7 +121,17 @@ void GBDT::ResetTrainingData(const Dataset* train_data, const ObjectiveFunction*
   auto models = std::move(models_);
   models_.clear();
   const int iter = iter_;
+  // Init builds a new tree learner: validation sets scored on the old learner's device come
+  // back to the host first (their device handles die with it), and early-stopping state
+  // survives the reset
+  for (size_t d = 0; d < valid_dev_.size(); ++d) (void)ValidScore(d);
+  auto best_score = std::move(best_score_);
+  auto best_iter = std::move(best_iter_vec_);
+  auto best_msg = std::move(best_msg_);
   Init(config_, train_data, objective, training_metrics);
+  best_score_ = std::move(best_score);
+  best_iter_vec_ = std::move(best_iter);
+  best_msg_ = std::move(best_msg);
   models_ = std::move(models);
   iter_ = iter;
   // recompute training score from the existing trees
@@ -130,6 +140,13 @@ void GBDT::ResetTrainingData(const Dataset* train_data, const ObjectiveFunction*
     models_[i]->AddPredictionToScore(*train_data_, num_data_, train_score_.data() + static_cast<size_t>(k) * num_data_);
   }
   if (device_mode_) learner_->DeviceInitScore(train_score_, num_tree_per_iteration_);
+  // register the validation sets with the new learner (device scoring where it applies)
+  const char* ev = std::getenv("LGAP_DEVICE_VALID");
+  const bool dev_ok = device_mode_ && DeviceMetricsAllowed() && !(ev && std::strcmp(ev, "0") == 0);
+  for (size_t d = 0; d < valid_dev_.size(); ++d) {
+    valid_dev_[d] = dev_ok ? learner_->DeviceAddValidSet(valid_data_[d], valid_score_[d]) : -1;
+    valid_stale_[d] = 0;
+  }
 }
 
 void GBDT::ResetConfig(const Config* config) {

@@ -35,7 +35,13 @@ namespace {
 thread_local std::string g_last_error = "Everything is fine";
 void SetLastError(const char* msg) { g_last_error = msg; }
 
-#define API_BEGIN() try {
+// Every entry point applies the library's thread setting to the CALLING thread's OpenMP team
+// size (omp_set_num_threads is per-thread state): a Booster's num_threads and
+// LGBM_SetMaxThreads hold whichever host thread trains or predicts (Python threads, joblib,
+// Dask workers), as the reference's num_threads(OMP_NUM_THREADS()) on every region does.
+#define API_BEGIN() \
+  try {             \
+    ::lgap::ApplyNumThreads();
 #define API_END()                      \
   }                                    \
   catch (std::exception & ex) {        \
@@ -1121,6 +1127,14 @@ int LGBM_SetMaxThreads(int num_threads) {
 int LGBM_GetMaxThreads(int* out) {
   API_BEGIN();
   *out = MaxNumThreadsSetting();
+  API_END();
+}
+
+// OpenMP team size a parallel region entered from the calling thread would use (diagnostic:
+// the effective num_threads / LGBM_SetMaxThreads setting as applied on this thread)
+int LGBM_GetEffectiveThreads(int* out) {
+  API_BEGIN();
+  *out = omp_get_max_threads();
   API_END();
 }
 

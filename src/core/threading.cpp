@@ -34,6 +34,16 @@ void SetMaxNumThreads(int num_threads) {
   omp_set_num_threads(Effective());
 }
 
+void ApplyNumThreads() {
+  int n;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_default <= 0 && g_max <= 0) return;  // nothing set: OpenMP's own default stays
+    n = Effective();
+  }
+  if (omp_get_max_threads() != n) omp_set_num_threads(n);
+}
+
 int MaxNumThreadsSetting() {
   std::lock_guard<std::mutex> lk(g_mu);
   return g_max;

@@ -3228,7 +3228,14 @@ class DeviceTreeLearner : public TreeLearner {
     return std::max(1, std::min(k, L_ - 1));
   }
   // computed nodes of one tree: every committed node (2 L - 1) plus room for speculation
-  int FrontierCapacity() const { return 4 * L_ + 2 * kFrontierKmax; }
+  // (8 L + 2 kmax, fewer when the per-node fp64 histograms would exceed ~8 GiB)
+  int FrontierCapacity() const {
+    const long long lo = 4LL * L_ + 2 * kFrontierKmax, hi = 8LL * L_ + 2 * kFrontierKmax;
+    const long long slot_bytes = 16LL * std::max(TB_, 1);
+    const long long fit = (8LL << 30) / slot_bytes;
+    const long long c = std::max(lo, std::min({hi, fit, static_cast<long long>(kFrontierMaxNodes)}));
+    return static_cast<int>(c);
+  }
 
   void AllocFrontier() {
     frontier_ = FrontierEligible();
@@ -3276,6 +3283,8 @@ class DeviceTreeLearner : public TreeLearner {
     FrontierSetLds(hist_lds_bytes_, fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
+    fpolicy_ = 1;
+    if (const char* e = std::getenv("LGAP_FRONTIER_POLICY")) fpolicy_ = std::atoi(e) == 0 ? 0 : 1;
     for (auto& kv : fgraphs_) (void)hipGraphExecDestroy(kv.second);
     fgraphs_.clear();
     if (fcont_) (void)hipGraphExecDestroy(fcont_);
@@ -3337,6 +3346,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.cat_p2 = cat_p2_;
     a.use_dp = use_dp_ ? 1 : 0;
     a.spec_cap = fspec_cap_;
+    a.policy = fpolicy_;
     a.distributed = 0;
     a.sp = MakeArgs().sp;
     return a;
@@ -4411,7 +4421,7 @@ class DeviceTreeLearner : public TreeLearner {
 
   // frontier engine (frontier.h)
   bool frontier_ = false;
-  int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0;
+  int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
   FState* fst_ = nullptr;

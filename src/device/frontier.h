@@ -142,6 +142,7 @@ struct FArgs {
   int max_bin, cat_p2;
   int use_dp;       // gpu_use_dp: 64-bit LDS accumulators
   int spec_cap;     // speculative expansions per round beyond the budget (policy knob)
+  int policy;       // 1: budget by global gain rank (default), 0: budget minus uncommitted expansions
   int distributed;  // children counts from the split record (global) instead of the partition
   SplitParams sp;
 };

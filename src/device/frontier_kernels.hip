@@ -739,7 +739,8 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_f_select: one workgroup.
+// k_f_select: one workgroup. Every phase is ONE round of independent global loads (the
+// select sits on the critical path of every round: its latency, not its work, matters).
 //  A. per-child best split of the last round's children: arg-max over the features'
 //     candidates (gain desc, feature asc: SplitInfo::BetterThan), full record -> best[c]
 //  B. replay of best-first order over the committed leaves (wave 0, all in LDS): the leaf
@@ -755,6 +756,9 @@ __device__ __forceinline__ bool FBetter(double ga, int fa, int la, double gb, in
   return la < lb;
 }
 
+constexpr int kSelWaves = kFSelThreads / 64;
+constexpr int kSelPairs = 2 * kFrontierKmax / kSelWaves;  // (expansion, child) pairs per wave
+
 __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int C = a.C, L = a.L, F = a.F;
@@ -763,95 +767,120 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   int* s_left = s_feat + C;                                  // [C]
   int* s_par = s_left + C;                                   // [C]
   int* s_dep = s_par + C;                                    // [C]
-  int* s_rank = s_dep + C;                                   // [C] eligible: rank key, else -1
+  int* s_rank = s_dep + C;                                   // [C] eligible: rank, else -1
   int* s_lcid = s_rank + C;                                  // [L]
   int* s_c0 = s_lcid + L;                                    // [L] committed leaves of this launch
   int* s_c1 = s_c0 + L;                                      // [L] their cids
   uint8_t* s_st = reinterpret_cast<uint8_t*>(s_c1 + L);      // [C]
-  __shared__ int s_cpos[2 * kFrontierKmax];                  // winning candidate position of this round's children
-  __shared__ int s_child[2 * kFrontierKmax];                 // their cids (-1: none)
+  __shared__ int s_cpos[2 * kFrontierKmax];  // this round's children: winning candidate position
+  __shared__ int s_pc[2 * kFrontierKmax];    // pair -> child cid (-1: none / skipped)
   __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_nelig, s_eunc, s_k, s_tiles;
-  __shared__ int s_exp[kFrontierKmax];                       // chosen expansions (cids) by order
+  __shared__ int s_exp[kFrontierKmax];       // chosen expansions (cids) by order
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
   if (st.done) return;
   const int kprev = st.k;
   const int cid_next = st.cid_next;
-  // ---- image of the computed nodes
+  const int np = 2 * kprev;
+  // this round's children are cids [base, base + 2 kprev) (the root round: cid 0)
+  const int base = cid_next - 2 * kprev;
+  // ---- image of the computed nodes + the pairs of the last round (one load round)
   for (int c = t; c < cid_next; c += blockDim.x) {
     const SplitKey& kk = a.key[c];
-    const FNode nd = a.nodes[c];
-    s_gain[c] = kk.feature < 0 ? kMinScore : kk.gain;
-    s_feat[c] = kk.feature;
+    const FNode& nd = a.nodes[c];
+    const int kf = kk.feature;
+    const double kg = kk.gain;
     s_left[c] = nd.left;
     s_par[c] = nd.parent;
     s_dep[c] = nd.depth;
     s_st[c] = a.nstate[c];
+    s_gain[c] = kf < 0 ? kMinScore : kg;
+    s_feat[c] = kf;
     s_rank[c] = -1;
   }
   for (int l = t; l < st.num_leaves; l += blockDim.x) s_lcid[l] = a.leaf_cid[l];
   if (t < 2 * kFrontierKmax) {
-    s_child[t] = -1;
+    int c = -1;
+    if (t < np) {
+      const FExp& x = a.exps[t >> 1];
+      c = x.skip ? -1 : ((t & 1) ? x.larger : x.smaller);
+      if (x.skip && !(t & 1)) c = -2 - x.smaller;  // skipped: children get empty records
+      if (x.skip && (t & 1)) c = -2 - x.larger;
+    }
+    s_pc[t] = c;
     s_cpos[t] = -1;
   }
-  // this round's children are cids [base, base + 2 kprev) (the root round: cid 0)
-  const int base = cid_next - 2 * kprev;
   __syncthreads();
-  // ---- A. children of the last round: best over features
-  for (int q = w; q < 2 * kprev; q += kFSelThreads / 64) {
-    const int e = q >> 1, sel = q & 1;
-    const FExp& x = a.exps[e];
-    const int c = sel ? x.larger : x.smaller;
-    if (c < 0) continue;
-    double bg = kMinScore;
-    int bf = 0x7fffffff, bpos = -1;
-    if (!x.skip) {
-      for (int f = lane; f < F; f += 64) {
-        const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
-        const double g = kk.feature < 0 ? kMinScore : kk.gain;
-        const int ff = kk.feature < 0 ? 0x7fffffff : kk.feature;
-        if (FBetter(g, ff, 0, bg, bf, 0)) {
-          bg = g;
-          bf = ff;
-          bpos = f;
+  // ---- A. children of the last round: best over features (all pairs' keys in flight)
+  {
+    double bg[kSelPairs];
+    int bf[kSelPairs], bp[kSelPairs];
+#pragma unroll
+    for (int j = 0; j < kSelPairs; ++j) {
+      bg[j] = kMinScore;
+      bf[j] = 0x7fffffff;
+      bp[j] = -1;
+    }
+    for (int f0 = 0; f0 < F; f0 += 64) {
+      const int f = f0 + lane;
+#pragma unroll
+      for (int j = 0; j < kSelPairs; ++j) {
+        const int q = w + j * kSelWaves;
+        if (q < np && f < F && s_pc[q] >= 0) {
+          const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+          const int kf = kk.feature;
+          const double g = kf < 0 ? kMinScore : kk.gain;
+          const int ff = kf < 0 ? 0x7fffffff : kf;
+          if (FBetter(g, ff, 0, bg[j], bf[j], 0)) {
+            bg[j] = g;
+            bf[j] = ff;
+            bp[j] = f;
+          }
         }
       }
     }
-    const int src = WaveArgBestLane(bg, bf, 0);
-    bg = ReadLane(bg, src);
-    bf = ReadLane(bf, src);
-    bpos = ReadLane(bpos, src);
-    const bool valid = bf != 0x7fffffff && bpos >= 0;
-    // full record -> best[c], compact key -> key[c]
     constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
     constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
-    if (valid) {
-      const size_t pos = static_cast<size_t>(q) * F + bpos;
-      for (int i = lane; i < kInfoWords; i += 64) {
-        reinterpret_cast<uint32_t*>(a.best + c)[i] = reinterpret_cast<const uint32_t*>(a.cinfo + pos)[i];
-      }
-      for (int i = lane; i < kKeyWords; i += 64) {
-        reinterpret_cast<uint32_t*>(a.key + c)[i] = reinterpret_cast<const uint32_t*>(a.ckey + pos)[i];
-      }
-    } else if (lane == 0) {
-      a.best[c].Reset();
-      SplitKey kz;
-      kz.gain = kMinScore;
-      kz.feature = -1;
-      kz.threshold = 0;
-      kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
-      kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
-      kz.pos = -1;
-      kz.pad2 = 0;
-      a.key[c] = kz;
-    }
-    if (lane == 0) {
-      s_gain[c] = valid ? bg : kMinScore;
-      s_feat[c] = valid ? bf : -1;
-      s_child[q] = c;
-      // (keys / records written above are read back by LATER launches only; this launch
+#pragma unroll
+    for (int j = 0; j < kSelPairs; ++j) {
+      const int q = w + j * kSelWaves;
+      if (q >= np) continue;
+      const int pc = s_pc[q];
+      if (pc == -1) continue;  // no child (root round's second pair)
+      const int c = pc >= 0 ? pc : -2 - pc;
+      const int src = WaveArgBestLane(bg[j], bf[j], 0);
+      const double g = ReadLane(bg[j], src);
+      const int ff = ReadLane(bf[j], src);
+      const int fpos = ReadLane(bp[j], src);
+      const bool valid = pc >= 0 && ff != 0x7fffffff && fpos >= 0;
+      // (keys / records written here are read back by LATER launches only; this launch
       // reads the candidate table, which an earlier launch wrote)
-      s_cpos[c - base] = valid ? q * F + bpos : -1;
+      if (valid) {
+        const size_t pos = static_cast<size_t>(q) * F + fpos;
+        for (int i = lane; i < kInfoWords + kKeyWords; i += 64) {
+          if (i < kInfoWords) {
+            reinterpret_cast<uint32_t*>(a.best + c)[i] = reinterpret_cast<const uint32_t*>(a.cinfo + pos)[i];
+          } else {
+            reinterpret_cast<uint32_t*>(a.key + c)[i - kInfoWords] = reinterpret_cast<const uint32_t*>(a.ckey + pos)[i - kInfoWords];
+          }
+        }
+      } else if (lane == 0) {
+        a.best[c].Reset();
+        SplitKey kz;
+        kz.gain = kMinScore;
+        kz.feature = -1;
+        kz.threshold = 0;
+        kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
+        kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
+        kz.pos = -1;
+        kz.pad2 = 0;
+        a.key[c] = kz;
+      }
+      if (lane == 0) {
+        s_gain[c] = valid ? g : kMinScore;
+        s_feat[c] = valid ? ff : -1;
+        s_cpos[c - base] = valid ? static_cast<int>(static_cast<size_t>(q) * F + fpos) : -1;
+      }
     }
   }
   __syncthreads();
@@ -915,18 +944,19 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   __syncthreads();
   const int nl = s_nl, ns = s_ns, ncommit = s_ncommit;
   int done = s_done;
-  // ---- C. committed splits -> records (one wave per split), leaf table, node states
-  for (int i = w; i < ncommit; i += kFSelThreads / 64) {
-    const int leaf = s_c0[i], c = s_c1[i];
-    const int sidx = st.num_splits + i;
-    SplitRec* r = a.rec + sidx;
+  // ---- C. committed splits -> records (all threads: one load round), leaf table, states
+  {
     constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-    for (int j = lane; j < kInfoWords; j += 64) {
-      reinterpret_cast<uint32_t*>(&r->info)[j] = reinterpret_cast<const uint32_t*>(a.best + c)[j];
+    for (int i = t; i < ncommit * kInfoWords; i += blockDim.x) {
+      const int k = i / kInfoWords, j = i - k * kInfoWords;
+      reinterpret_cast<uint32_t*>(&a.rec[st.num_splits + k].info)[j] =
+          reinterpret_cast<const uint32_t*>(a.best + s_c1[k])[j];
     }
-    if (lane == 0) {
+    for (int k = t; k < ncommit; k += blockDim.x) {
+      const int c = s_c1[k];
       const int left = s_left[c];
-      r->leaf = leaf;
+      SplitRec* r = a.rec + st.num_splits + k;
+      r->leaf = s_c0[k];
       r->left_count = a.nodes[left].gcount;
       r->right_count = a.nodes[left + 1].gcount;
       r->pad = 0;
@@ -938,8 +968,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   if (!done) {
     // eligible open nodes: unexpanded, a positive-gain split, and the row list their children
     // overwrite (the ancestor kFrontierBufs - 1 levels up) belongs to a committed split
+    int ne = 0, eu = 0;
     for (int c = t; c < cid_next; c += blockDim.x) {
-      bool ok = !(s_st[c] & kNodeExpanded) && s_feat[c] >= 0 && s_gain[c] > 0.0;
+      const uint8_t sc = s_st[c];
+      bool ok = !(sc & kNodeExpanded) && s_feat[c] >= 0 && s_gain[c] > 0.0;
       if (ok) {
         const int target = s_dep[c] + 1 - kFrontierBufs;
         if (target >= 1) {
@@ -949,50 +981,87 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         }
       }
       s_rank[c] = ok ? 0 : -1;
+      ne += ok ? 1 : 0;
+      eu += ((sc & kNodeExpanded) && !(sc & kNodeCommitted)) ? 1 : 0;
     }
     if (t == 0) {
       s_nelig = 0;
       s_eunc = 0;
     }
-    __syncthreads();
-    int ne = 0, eu = 0;
-    for (int c = t; c < cid_next; c += blockDim.x) {
-      ne += s_rank[c] >= 0 ? 1 : 0;
-      eu += ((s_st[c] & kNodeExpanded) && !(s_st[c] & kNodeCommitted)) ? 1 : 0;
-    }
     ne = WaveSum(ne);
     eu = WaveSum(eu);
+    __syncthreads();
     if (lane == 0) {
       atomicAdd(&s_nelig, ne);
       atomicAdd(&s_eunc, eu);
     }
     __syncthreads();
     const int blocked = s_blocked;
-    // rank: the blocked node first, then gain desc, then cid asc
+    const int R = L - 1 - ns;  // splits the tree may still make
+    // Rank of each eligible node: the blocked node first, then gain desc, then cid asc. The
+    // policy also needs, for an eligible node, how many ALIVE UNCOMMITTED nodes (expanded or
+    // not, anywhere in the computed tree) have a better gain: best-first order can commit at
+    // most R more splits, and it takes them roughly by gain, so a node ranked beyond R + spec
+    // among all of them is unlikely to be used (policy 1, default). Policy 0 budgets R minus
+    // every expanded-but-uncommitted node instead.
+    __shared__ int s_gr[kFrontierMaxNodes / 4];
     for (int c = t; c < cid_next; c += blockDim.x) {
       if (s_rank[c] < 0) continue;
-      int r = 0;
-      if (c != blocked) {
-        const double g = s_gain[c];
-        r = blocked >= 0 ? 1 : 0;
-        for (int j = 0; j < cid_next; ++j) {
-          if (j == c || j == blocked || s_rank[j] < 0) continue;
-          const double gj = s_gain[j];
-          r += (gj > g || (gj == g && j < c)) ? 1 : 0;
-        }
+      int r = 0, ga = 0;
+      const double g = s_gain[c];
+      r = (blocked >= 0 && c != blocked) ? 1 : 0;
+      for (int j = 0; j < cid_next; ++j) {
+        if (j == c) continue;
+        const double gj = s_gain[j];
+        const bool better = gj > g || (gj == g && j < c);
+        if (s_rank[j] >= 0 && j != blocked && c != blocked) r += better ? 1 : 0;
+        const uint8_t sj = s_st[j];
+        if (!(sj & kNodeCommitted) && s_feat[j] >= 0 && gj > 0.0) ga += better ? 1 : 0;
       }
-      s_rank[c] = r;
+      s_rank[c] = c == blocked ? 0 : r;
+      if (c < kFrontierMaxNodes / 4) s_gr[c] = ga;
     }
     __syncthreads();
-    const int R = L - 1 - ns;  // splits the tree may still make
-    const int need = R - s_eunc;
     const int cap_nodes = (C - cid_next) / 2 - (R - 1);
-    int K = min(a.kmax, max(1, need + a.spec_cap));
-    K = min(K, max(1, cap_nodes));
-    K = min(K, s_nelig);
-    if (t == 0) s_k = K;
-    for (int c = t; c < cid_next; c += blockDim.x) {
-      if (s_rank[c] >= 0 && s_rank[c] < K) s_exp[s_rank[c]] = c;
+    int K;
+    if (a.policy == 0) {
+      K = min(a.kmax, max(1, R - s_eunc + a.spec_cap));
+      K = min(K, max(1, cap_nodes));
+      K = min(K, s_nelig);
+      if (t == 0) s_k = K;
+      for (int c = t; c < cid_next; c += blockDim.x) {
+        if (s_rank[c] >= 0 && s_rank[c] < K) s_exp[s_rank[c]] = c;
+      }
+    } else {
+      // eligible nodes within the budget by global gain rank, taken in eligible-rank order
+      if (t == 0) s_k = 0;
+      __syncthreads();
+      const int lim = min(a.kmax, max(1, cap_nodes));
+      for (int c = t; c < cid_next; c += blockDim.x) {
+        if (s_rank[c] < 0) continue;
+        const int ga = c < kFrontierMaxNodes / 4 ? s_gr[c] : 0x7fffffff;
+        const bool take = c == blocked || (ga < R + a.spec_cap);
+        if (!take) s_rank[c] = -1;
+      }
+      __syncthreads();
+      // compact by eligible rank among the taken ones
+      for (int c = t; c < cid_next; c += blockDim.x) {
+        if (s_rank[c] < 0) continue;
+        int r = 0;
+        const double g = s_gain[c];
+        if (c != blocked) {
+          r = blocked >= 0 ? 1 : 0;
+          for (int j = 0; j < cid_next; ++j) {
+            if (j == c || j == blocked || s_rank[j] < 0) continue;
+            const double gj = s_gain[j];
+            r += (gj > g || (gj == g && j < c)) ? 1 : 0;
+          }
+        }
+        if (r < lim) {
+          s_exp[r] = c;
+          atomicMax(&s_k, r + 1);
+        }
+      }
     }
     __syncthreads();
     K = s_k;
@@ -1000,14 +1069,16 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     if (!done && w == 0) {
       // expansion records, tiles prefix (wave 0; K <= 64)
       const int kTile = a.part_tile;
-      int ntiles = 0, cnt = 0;
+      int ntiles = 0;
       FNode nd;
       int p = -1;
+      SplitKey kk;
       if (lane < K) {
         p = s_exp[lane];
+        const int cpos = (p >= base && p - base < 2 * kFrontierKmax) ? s_cpos[p - base] : -1;
         nd = a.nodes[p];
-        cnt = nd.count;
-        ntiles = (cnt + kTile - 1) / kTile;
+        kk = cpos >= 0 ? a.ckey[cpos] : a.key[p];
+        ntiles = max(1, (nd.count + kTile - 1) / kTile);
       }
       const int inc = WaveInclusiveScan(ntiles);
       if (lane < K) {
@@ -1021,8 +1092,6 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         x.start = nd.start;
         x.count = nd.count;
         x.dst_buf = FrontierDepthBuf(nd.depth % kFrontierBufs);
-        const int cpos = (p >= base && p - base < 2 * kFrontierKmax) ? s_cpos[p - base] : -1;
-        const SplitKey kk = cpos >= 0 ? a.ckey[cpos] : a.key[p];
         x.group = kk.group;
         x.offset = kk.offset;
         x.num_bin = kk.num_bin;
@@ -1041,21 +1110,19 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         a.nstate[p] = s_st[p] | kNodeExpanded;
       }
       if (lane == 63) s_tiles = inc;
-    }
-    __syncthreads();
-    if (!done) {
-      // categorical left sets of the expansions
-      for (int i = t; i < K * kMaxCatWords; i += blockDim.x) {
+    } else if (!done) {
+      // categorical left sets of the expansions (the other waves, concurrently)
+      for (int i = t - 64; i < K * kMaxCatWords; i += blockDim.x - 64) {
         const int e = i / kMaxCatWords, wd = i - e * kMaxCatWords;
         const int p = s_exp[e];
         const int cpos = (p >= base && p - base < 2 * kFrontierKmax) ? s_cpos[p - base] : -1;
         a.exp_bits[i] = cpos >= 0 ? a.cinfo[cpos].cat_bitset[wd] : a.best[p].cat_bitset[wd];
       }
     }
+    __syncthreads();
   }
   if (t == 0) {
-    FState ns_;
-    ns_ = st;
+    FState ns_ = st;
     ns_.round = st.round + 1;
     ns_.num_leaves = nl;
     ns_.num_splits = ns;

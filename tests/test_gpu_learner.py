@@ -643,3 +643,30 @@ def test_device_max_bin_8191_global_scan(lgb, gpu_required, rng):
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(r.stdout)
     assert outs[0] == outs[1]
+
+
+def test_reset_training_data_keeps_device_validation(lgb, gpu_required, rng):
+    """ResetTrainingData builds a new device learner: validation sets scored on the old one are
+    pulled back and registered again, so training and evaluation continue."""
+    X = rng.standard_normal((20000, 6))
+    y = (X[:, 0] - 0.5 * X[:, 1] > 0).astype(float)
+    Xv = rng.standard_normal((5000, 6))
+    yv = (Xv[:, 0] - 0.5 * Xv[:, 1] > 0).astype(float)
+    p = {"objective": "binary", "metric": "binary_logloss", "num_leaves": 15, "device_type": "gpu",
+         "verbosity": -1}
+    outs = []
+    for dev in ("gpu", "cpu"):
+        q = dict(p, device_type=dev)
+        ds = lgb.Dataset(X, y, params=q, free_raw_data=False)
+        b = lgb.Booster(q, ds)
+        b.add_valid(ds.create_valid(Xv, yv), "v")
+        for _ in range(3):
+            b.update()
+        ds2 = lgb.Dataset(X[:15000], y[:15000], params=q, reference=ds)
+        b.update(train_set=ds2)
+        for _ in range(2):
+            b.update()
+        outs.append((b.eval_valid()[0][2], b.predict(Xv[:1000], raw_score=True)))
+    assert np.isfinite(outs[0][0])
+    assert abs(outs[0][0] - outs[1][0]) < 1e-3, (outs[0][0], outs[1][0])
+    np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-3, atol=1e-3)
