@@ -57,6 +57,8 @@ def grow(finder, n, L, policy, spec=0, kmax=64, M=4):
     ns = 0
     rounds = 0
     exps = 0
+    hist_rows = n  # root histogram
+    part_rows = 0
     while True:
         rounds += 1
         # replay
@@ -76,7 +78,9 @@ def grow(finder, n, L, policy, spec=0, kmax=64, M=4):
             leaves.append(l + 1)
             ns += 1
         if blocked is None:
-            return rounds, exps, ns
+            committed_hist = sum(min(len(nodes[d["left"]]["rows"]), len(nodes[d["left"] + 1]["rows"]))
+                                 for d in nodes.values() if d["committed"])
+            return rounds, exps, ns, round(hist_rows / n, 2), round((n + committed_hist) / n, 2), round(part_rows / n, 2)
         R = L - 1 - ns
         alive = [c for c, d in nodes.items() if d["gain"] > 0 and not d["committed"]]
 
@@ -113,6 +117,8 @@ def grow(finder, n, L, policy, spec=0, kmax=64, M=4):
                 nodes[cid] = dict(rows=sub, depth=d["depth"] + 1, parent=c, left=None, committed=False)
                 nodes[cid]["gain"], nodes[cid]["feat"], nodes[cid]["thr"] = finder.best(sub)
             d["left"] = nxt
+            hist_rows += min(len(nodes[nxt]["rows"]), len(nodes[nxt + 1]["rows"]))
+            part_rows += len(rows)
             nxt += 2
             exps += 1
 
@@ -131,7 +137,7 @@ def main():
         g, h = p - y, p * (1 - p)
         f = Finder(B, g, h)
         res = {}
-        for pol, spec in ((0, 0), (1, 0), (1, 8), (1, 32)):
+        for pol, spec in ((0, 0), (1, 0)):
             res[(pol, spec)] = grow(f, n, L, pol, spec)
         print(it, {f"p{k[0]}s{k[1]}": v for k, v in res.items()}, flush=True)
         # advance the score with a crude tree of the root split (keeps gradients moving)

@@ -51,6 +51,7 @@
 #include "device/leaf_kernels.h"
 #include "device/runtime_internal.h"
 #include "device/frontier.h"
+#include "device/traverse_kernels.h"
 #include "device/sample_kernels.h"
 #include "device/split_scan.h"
 #include "device/tree_kernels.h"
@@ -3022,6 +3023,10 @@ class DeviceTreeLearner : public TreeLearner {
       if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, n, tree->LeafOutput(0), stream_);
       return;
     }
+    if (tree->num_leaves() <= 32767 && !std::getenv("LGAP_OLD_TRAVERSE")) {
+      TraverseTreeCompact(tree, rowbins, n, s);
+      return;
+    }
     const int nn = tree->num_leaves() - 1;
     const auto& cb = tree->cat_boundaries_inner();
     const auto& ct = tree->cat_threshold_inner();
@@ -3069,6 +3074,68 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t lds = node_bytes + (stride_dw_ <= kTraverseMaxDw ? sizeof(uint32_t) * kTraverseThreads * stride_dw_ : 0);
     k_add_tree<<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins, stride_dw_, width_, n, dn, nn, dc, dl, s);
     HIP_CHECK(hipGetLastError());
+    // the pinned staging buffer is reused by the next call: wait for the copy
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  // Compact traversal (traverse_kernels.h): node predicates precomputed in group-bin space.
+  void TraverseTreeCompact(const Tree* tree, const uint32_t* rowbins, int n, double* s) {
+    const int nn = tree->num_leaves() - 1, nl = tree->num_leaves();
+    const auto& cb = tree->cat_boundaries_inner();
+    const auto& ct = tree->cat_threshold_inner();
+    const size_t node_bytes = Round256(sizeof(TNode) * nn), cat_bytes = Round256(sizeof(TCat) * nn);
+    const size_t leaf_bytes = Round256(sizeof(double) * nl), bit_bytes = sizeof(uint32_t) * std::max<size_t>(1, ct.size());
+    const size_t total = node_bytes + cat_bytes + leaf_bytes + bit_bytes;
+    char* hp = pin_tree_.Get(total);
+    TNode* nodes = reinterpret_cast<TNode*>(hp);
+    TCat* cats = reinterpret_cast<TCat*>(hp + node_bytes);
+    for (int i = 0; i < nn; ++i) {
+      const FeatureInfo& fi = data_->feature(tree->split_feature_inner(i));
+      const int8_t dt = tree->decision_type(i);
+      const int missing = Tree::GetMissingType(dt);
+      const bool dleft = Tree::GetDecisionType(dt, kDefaultLeftMask);
+      const int offset = fi.offset, nb = fi.num_bin, mfb = static_cast<int>(fi.mfb);
+      TNode& d = nodes[i];
+      std::memset(&d, 0, sizeof(d));
+      d.group = static_cast<uint16_t>(fi.group);
+      d.left = static_cast<int16_t>(tree->left_child(i));
+      d.right = static_cast<int16_t>(tree->right_child(i));
+      d.gmiss = -1;
+      if (Tree::GetDecisionType(dt, kCategoricalMask)) {
+        const int ci = static_cast<int>(tree->threshold_in_bin(i));
+        d.flags = kTCat;
+        TCat& c = cats[i];
+        c.offset = offset;
+        c.num_bin = nb;
+        c.mfb = mfb;
+        c.begin = cb[ci];
+        c.nwords = cb[ci + 1] - cb[ci];
+        c.pad = 0;
+        continue;
+      }
+      const int thr = static_cast<int>(tree->threshold_in_bin(i));
+      const int bmiss = missing == 1 ? static_cast<int>(fi.default_bin) : (missing == 2 ? nb - 1 : -1);
+      // stored feature bins k = 0 .. nb - 2 sit at group bins offset + k (the mfb is implicit)
+      d.lo = static_cast<uint16_t>(offset);
+      d.hi = static_cast<uint16_t>(offset + nb - 2);
+      const bool out_left = bmiss == mfb ? dleft : (mfb <= thr);
+      if (bmiss >= 0 && bmiss != mfb) d.gmiss = static_cast<int16_t>(offset + (bmiss < mfb ? bmiss : bmiss - 1));
+      // last group bin whose feature bin is <= thr; below `offset` (thr == mfb == 0) no stored bin
+      // goes left, and tg = 0 makes `gb <= tg` false for every in-range bin (offset >= 1)
+      const int tg = offset + (thr < mfb ? thr : thr - 1);
+      d.tg = static_cast<uint16_t>(tg < offset ? 0 : tg);
+      d.flags = static_cast<uint8_t>((out_left ? kTOutLeft : 0) | (dleft ? kTDefaultLeft : 0));
+    }
+    double* lv = reinterpret_cast<double*>(hp + node_bytes + cat_bytes);
+    for (int l = 0; l < nl; ++l) lv[l] = tree->LeafOutput(l);
+    uint32_t* cw = reinterpret_cast<uint32_t*>(hp + node_bytes + cat_bytes + leaf_bytes);
+    for (size_t i = 0; i < ct.size(); ++i) cw[i] = ct[i];
+    tree_buf_.Resize(std::max(tree_buf_.size(), total));
+    HIP_CHECK(hipMemcpyAsync(tree_buf_.get(), hp, total, hipMemcpyHostToDevice, stream_));
+    const char* db = tree_buf_.get();
+    LaunchTraverse(rowbins, stride_dw_, width_, n, reinterpret_cast<const TNode*>(db), nn,
+                   reinterpret_cast<const TCat*>(db + node_bytes), reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
+                   reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
@@ -3277,7 +3344,9 @@ class DeviceTreeLearner : public TreeLearner {
     for (int i = 3; i < 5; ++i) idx_[i].Resize(std::max(N_, 1));
     // the partition's look-back needs all of its blocks resident: occupancy minus a margin
     int per_cu = FrontierPartitionBlocksPerCU(part_iters_);
-    per_cu = std::max(1, std::min(4, per_cu - 1));
+    int cap = 8;  // A/B knob LGAP_FPART_BPC (10M rows: 4 -> 327.9, 6 -> 334.7, 8 -> 337.3 it/s)
+    if (const char* e = std::getenv("LGAP_FPART_BPC")) cap = std::max(1, std::atoi(e));
+    per_cu = std::max(1, std::min(cap, per_cu - 1));
     fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
     fscan_lds_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + static_cast<size_t>(cat_p2_) * 2 * (sizeof(int) + sizeof(double));
     FrontierSetLds(hist_lds_bytes_, fscan_lds_, use_dp_, width_);
@@ -3285,6 +3354,10 @@ class DeviceTreeLearner : public TreeLearner {
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
     fpolicy_ = 1;
     if (const char* e = std::getenv("LGAP_FRONTIER_POLICY")) fpolicy_ = std::atoi(e) == 0 ? 0 : 1;
+    if (std::getenv("LGAP_FSTAMPS")) {
+      fstamps_.Resize(256 * 4 * kFStampSlots);
+      fstamps_.Zero(stream_);
+    }
     for (auto& kv : fgraphs_) (void)hipGraphExecDestroy(kv.second);
     fgraphs_.clear();
     if (fcont_) (void)hipGraphExecDestroy(fcont_);
@@ -3347,6 +3420,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.use_dp = use_dp_ ? 1 : 0;
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
+    a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
     a.distributed = 0;
     a.sp = MakeArgs().sp;
     return a;
@@ -3441,9 +3515,55 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     if (hbar[2] != 0u) Log::Fatal("k_f_partition: a wait on published tile counts timed out (blocks not co-resident?)");
+    if (fstamps_.size() && fstat_trees_ == 3) ReportFrontierStamps(hs->round);
     if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {
       std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max)\n", fstat_trees_,
                    static_cast<double>(fstat_rounds_) / fstat_trees_, static_cast<double>(fstat_spec_) / fstat_trees_, L_);
+    }
+  }
+
+  // Mean phase offsets (us from each kernel's block-0 start) over the rounds of the last
+  // tree, and the round chain: select -> partition -> hist -> scan -> next select.
+  void ReportFrontierStamps(int rounds) {
+    std::vector<unsigned long long> h(fstamps_.size());
+    fstamps_.Download(h.data(), h.size(), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    static const char* names[4] = {"partition", "hist", "scan", "select"};
+    auto at = [&](int r, int k, int i) { return h[(static_cast<size_t>(r) * 4 + k) * kFStampSlots + i]; };
+    for (int k = 0; k < 4; ++k) {
+      double acc[kFStampSlots] = {0};
+      int cnt = 0;
+      for (int r = 0; r < std::min(rounds + 1, 256); ++r) {
+        const unsigned long long s0 = at(r, k, 0);
+        if (!s0) continue;
+        ++cnt;
+        for (int i = 1; i < kFStampSlots; ++i) {
+          const unsigned long long v = at(r, k, i);
+          if (v >= s0) acc[i] += (v - s0) * 0.01;
+        }
+      }
+      if (!cnt) continue;
+      std::string line;
+      for (int i = 1; i < kFStampSlots; ++i) {
+        if (acc[i] > 0) line += " t" + std::to_string(i) + "=" + common::FormatG(acc[i] / cnt);
+      }
+      std::fprintf(stderr, "fstamps %s (%d rounds, us from block-0 start; t7 = last block exit):%s\n", names[k], cnt,
+                   line.c_str());
+    }
+    double gap[4] = {0};
+    int cnt = 0;
+    for (int r = 1; r + 1 < std::min(rounds, 255); ++r) {
+      const unsigned long long P = at(r, 0, 0), H = at(r, 1, 0), S = at(r, 2, 0), Q = at(r, 3, 0), P2 = at(r + 1, 0, 0);
+      if (!P || !H || !S || !Q || !P2 || !(P < H && H < S && S < Q && Q < P2)) continue;
+      gap[0] += (H - P) * 0.01;
+      gap[1] += (S - H) * 0.01;
+      gap[2] += (Q - S) * 0.01;
+      gap[3] += (P2 - Q) * 0.01;
+      ++cnt;
+    }
+    if (cnt) {
+      std::fprintf(stderr, "fstamps chain (%d rounds, start to start, us): partition->hist %.2f hist->scan %.2f "
+                   "scan->select %.2f select->partition %.2f\n", cnt, gap[0] / cnt, gap[1] / cnt, gap[2] / cnt, gap[3] / cnt);
     }
   }
 
@@ -3701,7 +3821,14 @@ class DeviceTreeLearner : public TreeLearner {
     return part_iters_ == 16 ? k_partition<16> : (part_iters_ == 8 ? k_partition<8> : k_partition<4>);
   }
 
-  int HistMinRows() const { return config_->device_hist_min_rows > 0 ? config_->device_hist_min_rows : kHistMinRows; }
+  int HistMinRows() const {
+    static const int env_rows = [] {
+      const char* e = std::getenv("LGAP_HIST_MIN_ROWS");  // A/B knob
+      return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    if (config_->device_hist_min_rows > 0) return config_->device_hist_min_rows;
+    return env_rows > 0 ? env_rows : kHistMinRows;
+  }
 
   int RootBlocks() const { return std::max(1, std::min(DivUp(N_, kRootThreads), 4 * num_cu_)); }
 
@@ -3712,9 +3839,13 @@ class DeviceTreeLearner : public TreeLearner {
     // Wide data (many LDS feature tiles): the grid is row blocks x tiles, so fewer row blocks
     // still fill the chip while the slab rows the scan folds (each one 8 B x all bins) shrink:
     // LambdaRank 1M x 300 (11 tiles) 17.7 -> 16.4 ms/iter at 46 row blocks instead of 256.
-    const int want = config_->device_hist_blocks > 0
-                         ? config_->device_hist_blocks
-                         : std::min(num_cu_, std::max(1, 2 * num_cu_ / std::max(1, num_tiles_)));
+    static const int env_blocks = [] {
+      const char* e = std::getenv("LGAP_HIST_BLOCKS");  // A/B knob
+      return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    const int want = config_->device_hist_blocks > 0 ? config_->device_hist_blocks
+                     : env_blocks > 0                ? env_blocks
+                                                     : std::min(num_cu_, std::max(1, 2 * num_cu_ / std::max(1, num_tiles_)));
     // partial-histogram slab: one row of 2 * TB accumulators per block, capped at 4 GiB
     const size_t row_bytes = 2 * static_cast<size_t>(TB_) * (use_dp_ ? 8 : 4);
     const int mem_cap = static_cast<int>(std::max<size_t>(1, (size_t(4) << 30) / std::max<size_t>(row_bytes, 1)));
@@ -4448,6 +4579,7 @@ class DeviceTreeLearner : public TreeLearner {
   long long fstat_rounds_ = 0, fstat_spec_ = 0;
   int fstat_trees_ = 0;
   PinnedBuf<FState> pin_fst_;
+  DevBuf<unsigned long long> fstamps_;
   const float2* fgraph_gh_ = nullptr;
   const Config* config_;
   bool data_parallel_ = false;

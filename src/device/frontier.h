@@ -58,6 +58,8 @@ __host__ __device__ inline int FrontierDepthBuf(int j) { return j < 2 ? j : j + 
 // node state bits (FArgs::nstate)
 constexpr uint8_t kNodeExpanded = 1;   // children computed
 constexpr uint8_t kNodeCommitted = 2;  // its split is part of the tree (replay)
+// stamp slots: kernel ids and the per-kernel slot count (slot 7: latest block exit)
+constexpr int kFStampPart = 0, kFStampHist = 1, kFStampScan = 2, kFStampSel = 3, kFStampSlots = 8;
 
 struct FNode {
   int buf, start, count;  // local rows: positions [start, start + count) of index buffer `buf`
@@ -144,6 +146,7 @@ struct FArgs {
   int spec_cap;     // speculative expansions per round beyond the budget (policy knob)
   int policy;       // 1: budget by global gain rank (default), 0: budget minus uncommitted expansions
   int distributed;  // children counts from the split record (global) instead of the partition
+  unsigned long long* stamps;  // diagnostics (LGAP_FSTAMPS=1): [round & 255][kernel 0..3][8] wall clock
   SplitParams sp;
 };
 

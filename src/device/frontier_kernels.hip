@@ -35,6 +35,19 @@ __device__ __forceinline__ uint32_t FColBin(const FArgs& a, int g, int row) {
   return a.width == 1 ? a.colbins[o] : reinterpret_cast<const uint16_t*>(a.colbins)[o];
 }
 
+// Diagnostic phase stamps (100 MHz wall clock): block 0 / thread 0 records slot i of kernel
+// `kern` in round `r`; FStampEnd keeps the latest exit over all blocks in slot 7.
+__device__ __forceinline__ void FStamp(const FArgs& a, int r, int kern, int i) {
+  if (a.stamps != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    a.stamps[((static_cast<size_t>(r & 255) * 4 + kern) * kFStampSlots) + i] = wall_clock64();
+  }
+}
+__device__ __forceinline__ void FStampEnd(const FArgs& a, int r, int kern) {
+  if (a.stamps != nullptr && threadIdx.x == 0) {
+    atomicMax(&a.stamps[((static_cast<size_t>(r & 255) * 4 + kern) * kFStampSlots) + 7], wall_clock64());
+  }
+}
+
 // exponent k of the largest power of two <= x (x > 0): 2^k <= x < 2^(k+1)
 __device__ __forceinline__ int Pow2Exp(double x) {
   int e;
@@ -192,6 +205,8 @@ __global__ __launch_bounds__(kFHistThreads) void k_f_hist(FArgs a) {
   if (sp->done) return;
   const int k = sp->k;
   const int t = threadIdx.x;
+  const int rnd = sp->round;
+  FStamp(a, rnd, kFStampHist, 0);
   if (t < 64) {
     // per-expansion chunking (identical in every block): chunk rows c for the whole round,
     // nb_e chunks of expansion e, blocks [pre_e, pre_e + nb_e)
@@ -274,8 +289,10 @@ __global__ __launch_bounds__(kFHistThreads) void k_f_hist(FArgs a) {
   for (int i = t; i < words; i += blockDim.x) hist[i] = 0ull;
   for (int g = tile.g0 + t; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
   __syncthreads();
+  FStamp(a, rnd, kFStampHist, 1);
   FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh);
   __syncthreads();
+  FStamp(a, rnd, kFStampHist, 2);
   unsigned long long* out = acc + 2 * static_cast<size_t>(tile.bin0);
   if (MODE == 0) {
     // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
@@ -297,6 +314,8 @@ __global__ __launch_bounds__(kFHistThreads) void k_f_hist(FArgs a) {
       if (x) atomicAdd(&out[i], x);
     }
   }
+  FStamp(a, rnd, kFStampHist, 3);
+  FStampEnd(a, rnd, kFStampHist);
 }
 
 // ---------------------------------------------------------------------------
@@ -316,6 +335,8 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   if (stp->done) return;
   const int k = stp->k, F = a.F;
   const int total = k * F;
+  const int rnd = stp->round;
+  FStamp(a, rnd, kFStampScan, 0);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
@@ -486,6 +507,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     }
     __syncthreads();  // LDS reused by the next item
   }
+  FStampEnd(a, rnd, kFStampScan);
 }
 
 // ---------------------------------------------------------------------------
@@ -602,6 +624,8 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
   if (stp->done) return;
   const int k = stp->k, T = stp->total_tiles;
   const unsigned epoch = stp->epoch;
+  const int rnd = stp->round;
+  FStamp(a, rnd, kFStampPart, 0);
   const int bid = static_cast<int>(blockIdx.x), G = static_cast<int>(gridDim.x);
   if (bid >= T) return;
   const int t = threadIdx.x;
@@ -637,6 +661,7 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
     }
     return b <= static_cast<uint32_t>(x.thr);
   };
+  FStamp(a, rnd, kFStampPart, 1);
   // phase 1: count every own tile and publish (the first tile's rows stay in registers)
   int rows0[ITERS];
   uint32_t gb0[ITERS];
@@ -666,6 +691,7 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
       }
     }
   }
+  FStamp(a, rnd, kFStampPart, 2);
   // phase 2: scatter
   const int lane = t & 63, w = t >> 6;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -736,6 +762,8 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
     __syncthreads();
     if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
   }
+  FStamp(a, rnd, kFStampPart, 3);
+  FStampEnd(a, rnd, kFStampPart);
 }
 
 // ---------------------------------------------------------------------------
@@ -771,10 +799,12 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   int* s_lcid = s_rank + C;                                  // [L]
   int* s_c0 = s_lcid + L;                                    // [L] committed leaves of this launch
   int* s_c1 = s_c0 + L;                                      // [L] their cids
-  uint8_t* s_st = reinterpret_cast<uint8_t*>(s_c1 + L);      // [C]
+  int* s_ga = s_c1 + L;                                      // [C] policy: better-gain alive count
+  int* s_er = s_ga + C;                                      // [C] policy: better-gain eligible count
+  uint8_t* s_st = reinterpret_cast<uint8_t*>(s_er + C);      // [C]
   __shared__ int s_cpos[2 * kFrontierKmax];  // this round's children: winning candidate position
   __shared__ int s_pc[2 * kFrontierKmax];    // pair -> child cid (-1: none / skipped)
-  __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_nelig, s_eunc, s_k, s_tiles;
+  __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_k, s_tiles;
   __shared__ int s_exp[kFrontierKmax];       // chosen expansions (cids) by order
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
@@ -782,6 +812,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   const int kprev = st.k;
   const int cid_next = st.cid_next;
   const int np = 2 * kprev;
+  const int rnd = st.round;
+  FStamp(a, rnd, kFStampSel, 0);
   // this round's children are cids [base, base + 2 kprev) (the root round: cid 0)
   const int base = cid_next - 2 * kprev;
   // ---- image of the computed nodes + the pairs of the last round (one load round)
@@ -811,6 +843,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     s_cpos[t] = -1;
   }
   __syncthreads();
+  FStamp(a, rnd, kFStampSel, 1);
   // ---- A. children of the last round: best over features (all pairs' keys in flight)
   {
     double bg[kSelPairs];
@@ -884,7 +917,19 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
   }
   __syncthreads();
-  // ---- B. replay (wave 0)
+  FStamp(a, rnd, kFStampSel, 2);
+  // ---- B. replay (wave 0): per-leaf (gain, feature) cached in LDS, one max scan per step
+  // (the full three-key tie-break only when two leaves share the best gain)
+  double* s_lg = reinterpret_cast<double*>(smem + ((reinterpret_cast<uintptr_t>(s_st + C) -
+                                                     reinterpret_cast<uintptr_t>(smem) + 15) & ~uintptr_t(15)));  // [L]
+  int* s_lf = reinterpret_cast<int*>(s_lg + L);                        // [L]
+  for (int l = t; l < st.num_leaves; l += blockDim.x) {
+    const int c = s_lcid[l];
+    const int f = s_feat[c];
+    s_lg[l] = f < 0 ? kMinScore : s_gain[c];
+    s_lf[l] = f < 0 ? 0x7fffffff : f;
+  }
+  __syncthreads();
   if (w == 0) {
     int nl = st.num_leaves, ns = st.num_splits, done = 0, blocked = -1, nc = 0;
     for (;;) {
@@ -895,17 +940,19 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       double bg = kMinScore;
       int bf = 0x7fffffff, bl = 0x7fffffff;
       for (int l = lane; l < nl; l += 64) {
-        const int c = s_lcid[l];
-        const int f = s_feat[c];
-        const double g = f < 0 ? kMinScore : s_gain[c];
-        const int ff = f < 0 ? 0x7fffffff : f;
+        const double g = s_lg[l];
+        const int ff = s_lf[l];
         if (FBetter(g, ff, l, bg, bf, bl)) {
           bg = g;
           bf = ff;
           bl = l;
         }
       }
-      const int src = WaveArgBestLane(bg, bf, bl);
+      const double mg = WaveMaxDpp(bg);
+      const unsigned long long tie = __ballot(bg == mg);
+      int src;
+      if (__popcll(tie) == 1) src = __ffsll(static_cast<long long>(tie)) - 1;
+      else src = WaveArgBestLane(bg, bf, bl);
       bg = ReadLane(bg, src);
       bf = ReadLane(bf, src);
       bl = ReadLane(bl, src);
@@ -925,6 +972,11 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         s_lcid[bl] = left;
         s_lcid[nl] = left + 1;
         s_st[c] |= kNodeCommitted;
+        const int fl = s_feat[left], fr = s_feat[left + 1];
+        s_lg[bl] = fl < 0 ? kMinScore : s_gain[left];
+        s_lf[bl] = fl < 0 ? 0x7fffffff : fl;
+        s_lg[nl] = fr < 0 ? kMinScore : s_gain[left + 1];
+        s_lf[nl] = fr < 0 ? 0x7fffffff : fr;
       }
       ++nc;
       ++nl;
@@ -942,6 +994,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
   }
   __syncthreads();
+  FStamp(a, rnd, kFStampSel, 3);
   const int nl = s_nl, ns = s_ns, ncommit = s_ncommit;
   int done = s_done;
   // ---- C. committed splits -> records (all threads: one load round), leaf table, states
@@ -964,107 +1017,97 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
   }
   for (int l = t; l < nl; l += blockDim.x) a.leaf_cid[l] = s_lcid[l];
+  FStamp(a, rnd, kFStampSel, 4);
   // ---- D. next round
   if (!done) {
-    // eligible open nodes: unexpanded, a positive-gain split, and the row list their children
+    // ALIVE uncommitted nodes (a positive-gain split, not part of the tree yet) are compacted
+    // into a list; ELIGIBLE ones among them are unexpanded and the row list their children
     // overwrite (the ancestor kFrontierBufs - 1 levels up) belongs to a committed split
-    int ne = 0, eu = 0;
-    for (int c = t; c < cid_next; c += blockDim.x) {
-      const uint8_t sc = s_st[c];
-      bool ok = !(sc & kNodeExpanded) && s_feat[c] >= 0 && s_gain[c] > 0.0;
-      if (ok) {
-        const int target = s_dep[c] + 1 - kFrontierBufs;
-        if (target >= 1) {
-          int an = c;
-          for (int i = 0; i < kFrontierBufs - 1; ++i) an = s_par[an];
-          ok = (s_st[an] & kNodeCommitted) != 0;
-        }
-      }
-      s_rank[c] = ok ? 0 : -1;
-      ne += ok ? 1 : 0;
-      eu += ((sc & kNodeExpanded) && !(sc & kNodeCommitted)) ? 1 : 0;
-    }
+    __shared__ int s_na, s_ne, s_eu;
     if (t == 0) {
-      s_nelig = 0;
-      s_eunc = 0;
+      s_na = 0;
+      s_ne = 0;
+      s_eu = 0;
     }
-    ne = WaveSum(ne);
-    eu = WaveSum(eu);
     __syncthreads();
-    if (lane == 0) {
-      atomicAdd(&s_nelig, ne);
-      atomicAdd(&s_eunc, eu);
+    int* s_ac = s_rank;  // [C] compacted alive cids, ~cid when not eligible (reuses s_rank)
+    const int cap_list = C;
+    for (int c0 = 0; c0 < cid_next; c0 += blockDim.x) {
+      const int c = c0 + t;
+      bool alive = false, elig = false, unc = false;
+      if (c < cid_next) {
+        const uint8_t sc = s_st[c];
+        alive = !(sc & kNodeCommitted) && s_feat[c] >= 0 && s_gain[c] > 0.0;
+        elig = alive && !(sc & kNodeExpanded);
+        if (elig) {
+          const int target = s_dep[c] + 1 - kFrontierBufs;
+          if (target >= 1) {
+            int an = c;
+            for (int i = 0; i < kFrontierBufs - 1; ++i) an = s_par[an];
+            elig = (s_st[an] & kNodeCommitted) != 0;
+          }
+        }
+        unc = (sc & kNodeExpanded) && !(sc & kNodeCommitted);
+      }
+      const unsigned long long ma = __ballot(alive);
+      const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+      int basea = 0;
+      if (lane == 0 && ma) basea = atomicAdd(&s_na, __popcll(ma));
+      basea = __shfl(basea, 0, kWave);
+      const int ne = __popcll(__ballot(elig)), eu = __popcll(__ballot(unc));
+      if (lane == 0) {
+        if (ne) atomicAdd(&s_ne, ne);
+        if (eu) atomicAdd(&s_eu, eu);
+      }
+      if (alive) {
+        const int pos = basea + __popcll(ma & lt);
+        if (pos < cap_list) s_ac[pos] = elig ? c : ~c;
+      }
+    }
+    __syncthreads();
+    const int na = min(s_na, cap_list);
+    for (int i = t; i < na; i += blockDim.x) {
+      s_ga[i] = 0;
+      s_er[i] = 0;
     }
     __syncthreads();
     const int blocked = s_blocked;
     const int R = L - 1 - ns;  // splits the tree may still make
-    // Rank of each eligible node: the blocked node first, then gain desc, then cid asc. The
-    // policy also needs, for an eligible node, how many ALIVE UNCOMMITTED nodes (expanded or
-    // not, anywhere in the computed tree) have a better gain: best-first order can commit at
-    // most R more splits, and it takes them roughly by gain, so a node ranked beyond R + spec
-    // among all of them is unlikely to be used (policy 1, default). Policy 0 budgets R minus
-    // every expanded-but-uncommitted node instead.
-    __shared__ int s_gr[kFrontierMaxNodes / 4];
-    for (int c = t; c < cid_next; c += blockDim.x) {
-      if (s_rank[c] < 0) continue;
-      int r = 0, ga = 0;
-      const double g = s_gain[c];
-      r = (blocked >= 0 && c != blocked) ? 1 : 0;
-      for (int j = 0; j < cid_next; ++j) {
-        if (j == c) continue;
-        const double gj = s_gain[j];
-        const bool better = gj > g || (gj == g && j < c);
-        if (s_rank[j] >= 0 && j != blocked && c != blocked) r += better ? 1 : 0;
-        const uint8_t sj = s_st[j];
-        if (!(sj & kNodeCommitted) && s_feat[j] >= 0 && gj > 0.0) ga += better ? 1 : 0;
+    // Pairwise order over the alive list (all threads): s_ga[i] = alive nodes with a better
+    // (gain desc, cid asc) key; s_er[i] = such ELIGIBLE nodes other than the blocked one.
+    // Policy 1 (default) takes an eligible node when it ranks within the remaining budget R
+    // (+ spec_cap) among ALL alive uncommitted nodes: best-first order commits at most R more
+    // splits and takes them roughly by gain. Policy 0 budgets R minus every expanded but
+    // uncommitted node. The blocked node always goes first.
+    for (int q = t; q < na * na; q += blockDim.x) {
+      const int i = q / na, jj = q - i * na;
+      if (i == jj) continue;
+      const int ci = s_ac[i] >= 0 ? s_ac[i] : ~s_ac[i];
+      const int cj = s_ac[jj] >= 0 ? s_ac[jj] : ~s_ac[jj];
+      const double gi = s_gain[ci], gj = s_gain[cj];
+      if (gj > gi || (gj == gi && cj < ci)) {
+        atomicAdd(&s_ga[i], 1);
+        if (s_ac[jj] >= 0 && cj != blocked) atomicAdd(&s_er[i], 1);
       }
-      s_rank[c] = c == blocked ? 0 : r;
-      if (c < kFrontierMaxNodes / 4) s_gr[c] = ga;
     }
+    if (t == 0) s_k = 0;
     __syncthreads();
     const int cap_nodes = (C - cid_next) / 2 - (R - 1);
-    int K;
-    if (a.policy == 0) {
-      K = min(a.kmax, max(1, R - s_eunc + a.spec_cap));
-      K = min(K, max(1, cap_nodes));
-      K = min(K, s_nelig);
-      if (t == 0) s_k = K;
-      for (int c = t; c < cid_next; c += blockDim.x) {
-        if (s_rank[c] >= 0 && s_rank[c] < K) s_exp[s_rank[c]] = c;
-      }
-    } else {
-      // eligible nodes within the budget by global gain rank, taken in eligible-rank order
-      if (t == 0) s_k = 0;
-      __syncthreads();
-      const int lim = min(a.kmax, max(1, cap_nodes));
-      for (int c = t; c < cid_next; c += blockDim.x) {
-        if (s_rank[c] < 0) continue;
-        const int ga = c < kFrontierMaxNodes / 4 ? s_gr[c] : 0x7fffffff;
-        const bool take = c == blocked || (ga < R + a.spec_cap);
-        if (!take) s_rank[c] = -1;
-      }
-      __syncthreads();
-      // compact by eligible rank among the taken ones
-      for (int c = t; c < cid_next; c += blockDim.x) {
-        if (s_rank[c] < 0) continue;
-        int r = 0;
-        const double g = s_gain[c];
-        if (c != blocked) {
-          r = blocked >= 0 ? 1 : 0;
-          for (int j = 0; j < cid_next; ++j) {
-            if (j == c || j == blocked || s_rank[j] < 0) continue;
-            const double gj = s_gain[j];
-            r += (gj > g || (gj == g && j < c)) ? 1 : 0;
-          }
-        }
-        if (r < lim) {
-          s_exp[r] = c;
-          atomicMax(&s_k, r + 1);
-        }
+    const int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
+                                  : min(a.kmax, max(1, cap_nodes));
+    for (int i = t; i < na; i += blockDim.x) {
+      if (s_ac[i] < 0) continue;  // not eligible
+      const int c = s_ac[i];
+      const int r = c == blocked ? 0 : s_er[i] + (blocked >= 0 ? 1 : 0);
+      const bool take = a.policy == 0 || c == blocked || s_ga[i] < R + a.spec_cap;
+      if (take && r < lim) {
+        s_exp[r] = c;
+        atomicMax(&s_k, r + 1);
       }
     }
     __syncthreads();
-    K = s_k;
+    FStamp(a, rnd, kFStampSel, 5);
+    int K = s_k;
     if (K <= 0) done = 1;  // nothing can be expanded: (only reachable without a blocked node)
     if (!done && w == 0) {
       // expansion records, tiles prefix (wave 0; K <= 64)
@@ -1140,6 +1183,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
     *a.st = ns_;
   }
+  FStamp(a, rnd, kFStampSel, 6);
+  FStampEnd(a, rnd, kFStampSel);
   if (done) {
     for (int l = t; l < nl; l += blockDim.x) {
       const FNode nd = a.nodes[s_lcid[l]];
@@ -1182,7 +1227,8 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 }
 
 size_t FrontierSelectLds(int C, int L) {
-  return static_cast<size_t>(C) * (sizeof(double) + 5 * sizeof(int) + 1) + 3 * static_cast<size_t>(L) * sizeof(int) + 64;
+  return static_cast<size_t>(C) * (sizeof(double) + 7 * sizeof(int) + 1) + 32 +
+         static_cast<size_t>(L) * (3 * sizeof(int) + sizeof(double) + sizeof(int)) + 64;
 }
 
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {

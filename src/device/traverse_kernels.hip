@@ -1,0 +1,122 @@
+// Tree traversal score update (see traverse_kernels.h).
+//
+// One block stages kRows contiguous packed rows in LDS with coalesced dword loads, then each
+// thread walks kRows / 256 rows through the LDS-resident nodes; the walks of a thread's rows
+// are interleaved level by level so their LDS reads overlap. Leaf values live in LDS too.
+#include "device/traverse_kernels.h"
+
+#include <algorithm>
+
+#include "device/hip_common.h"
+
+namespace lgap {
+namespace device {
+namespace {
+
+constexpr int kTThreads = 256;
+constexpr int kTRowsPerThread = 2;
+constexpr int kTRows = kTThreads * kTRowsPerThread;
+constexpr int kTMaxDw = 16;  // wider rows read global memory directly
+
+template <int W>
+__device__ __forceinline__ uint32_t GroupBin(const uint8_t* row, int g) {
+  return W == 1 ? row[g] : reinterpret_cast<const uint16_t*>(row)[g];
+}
+
+__device__ __forceinline__ bool CatLeft(const TCat& c, const uint32_t* bits, uint32_t gb) {
+  const int local = static_cast<int>(gb) - c.offset;
+  uint32_t b;
+  if (local < 0 || local >= c.num_bin - 1) b = static_cast<uint32_t>(c.mfb);
+  else b = static_cast<uint32_t>(local < c.mfb ? local : local + 1);
+  const uint32_t w = b >> 5;
+  return static_cast<int>(w) < c.nwords && ((bits[c.begin + w] >> (b & 31u)) & 1u);
+}
+
+template <int W>
+__global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restrict__ rowbins, int stride_dw, int n,
+                                                        const TNode* __restrict__ nodes, int num_nodes,
+                                                        const TCat* __restrict__ cats, const uint32_t* __restrict__ cat_bits,
+                                                        const double* __restrict__ leaf_value, int num_leaves,
+                                                        double* __restrict__ score) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  TNode* s_nodes = reinterpret_cast<TNode*>(lds);
+  double* s_leaf = reinterpret_cast<double*>(lds + ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)));
+  uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_leaf + num_leaves);
+  const int t = threadIdx.x;
+  for (int i = t; i < num_nodes * static_cast<int>(sizeof(TNode) / 4); i += kTThreads) {
+    reinterpret_cast<uint32_t*>(s_nodes)[i] = reinterpret_cast<const uint32_t*>(nodes)[i];
+  }
+  for (int i = t; i < num_leaves; i += kTThreads) s_leaf[i] = leaf_value[i];
+  const bool staged = stride_dw <= kTMaxDw;
+  for (long long base = static_cast<long long>(blockIdx.x) * kTRows; base < n;
+       base += static_cast<long long>(gridDim.x) * kTRows) {
+    const int rows = static_cast<int>(min(static_cast<long long>(kTRows), n - base));
+    if (staged) {
+      __syncthreads();  // the previous chunk's walks are done (first pass: nodes / leaves in place)
+      const uint32_t* src = rowbins + base * stride_dw;
+      const int ndw = rows * stride_dw;
+      for (int k = t; k < ndw; k += kTThreads) s_rows[k] = src[k];
+      __syncthreads();
+    } else if (base == static_cast<long long>(blockIdx.x) * kTRows) {
+      __syncthreads();
+    }
+    const uint8_t* row[kTRowsPerThread];
+    int node[kTRowsPerThread];
+#pragma unroll
+    for (int j = 0; j < kTRowsPerThread; ++j) {
+      const int r = t + j * kTThreads;
+      node[j] = r < rows ? 0 : ~0;
+      row[j] = staged ? reinterpret_cast<const uint8_t*>(s_rows + static_cast<size_t>(r) * stride_dw)
+                      : reinterpret_cast<const uint8_t*>(rowbins + static_cast<size_t>(base + r) * stride_dw);
+    }
+    bool live = true;
+    while (live) {
+      live = false;
+#pragma unroll
+      for (int j = 0; j < kTRowsPerThread; ++j) {
+        if (node[j] < 0) continue;
+        const TNode nd = s_nodes[node[j]];
+        const uint32_t gb = GroupBin<W>(row[j], nd.group);
+        bool left;
+        if (nd.flags & kTCat) {
+          left = CatLeft(cats[node[j]], cat_bits, gb);
+        } else if (gb < nd.lo || gb > nd.hi) {
+          left = (nd.flags & kTOutLeft) != 0;
+        } else if (static_cast<int>(gb) == nd.gmiss) {
+          left = (nd.flags & kTDefaultLeft) != 0;
+        } else {
+          left = gb <= nd.tg;
+        }
+        node[j] = left ? nd.left : nd.right;
+        live |= node[j] >= 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kTRowsPerThread; ++j) {
+      const int r = t + j * kTThreads;
+      if (r < rows) score[base + r] += s_leaf[~node[j]];
+    }
+  }
+}
+
+}  // namespace
+
+void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
+                    const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,
+                    int num_cu, hipStream_t s) {
+  if (n <= 0) return;
+  const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + sizeof(double) * num_leaves +
+                     (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
+  const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
+  if (width == 1) {
+    k_traverse<1><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                              num_leaves, score);
+  } else {
+    k_traverse<2><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                              num_leaves, score);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace device
+}  // namespace lgap
