@@ -3352,6 +3352,10 @@ class DeviceTreeLearner : public TreeLearner {
     FrontierSetLds(hist_lds_bytes_, fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
+    // 512 (default) / 1024 threads per histogram block: 1024 measured 322.9 vs 331.0 it/s at 10M
+    // (a longer tail: blocks finish further apart), 621 vs 738 at 1.25M
+    fhist_threads_ = 512;
+    if (const char* e = std::getenv("LGAP_FHIST_THREADS")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
     fpolicy_ = 1;
     if (const char* e = std::getenv("LGAP_FRONTIER_POLICY")) fpolicy_ = std::atoi(e) == 0 ? 0 : 1;
     if (std::getenv("LGAP_FSTAMPS")) {
@@ -3411,6 +3415,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.bar = bar_.get();
     a.hist_min_rows = HistMinRows();
     a.hist_grid = HistBlocks();
+    a.hist_threads = fhist_threads_;
     a.part_tile = fpart_tile_;
     a.max_depth = config_->max_depth;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
@@ -4552,6 +4557,7 @@ class DeviceTreeLearner : public TreeLearner {
 
   // frontier engine (frontier.h)
   bool frontier_ = false;
+  int fhist_threads_ = 512;
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;

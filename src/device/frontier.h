@@ -138,6 +138,7 @@ struct FArgs {
   unsigned long long* tile_pub;
   unsigned* bar;  // bar[2]: bounded-wait error flag
   int hist_min_rows, hist_grid;
+  int hist_threads;  // 512 or 1024 threads per histogram block
   int part_tile;  // rows per partition tile (256 x rows per thread)
   int max_depth, use_monotone;
   double monotone_penalty;

@@ -21,7 +21,6 @@ namespace device {
 namespace {
 
 constexpr int kFPartThreads = 256;
-constexpr int kFHistThreads = 512;
 constexpr int kFScanThreads = 256;
 constexpr int kFSelThreads = 1024;
 #ifndef LGAP_FHIST_R
@@ -197,8 +196,8 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   }
 }
 
-template <int W, int MODE>
-__global__ __launch_bounds__(kFHistThreads) void k_f_hist(FArgs a) {
+template <int W, int MODE, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   extern __shared__ __align__(8) unsigned char lds_raw[];
   __shared__ int s_e, s_rb, s_re, s_buf, s_start;
   const FState* sp = a.st;
@@ -540,11 +539,32 @@ __device__ __forceinline__ int FAwait(const FArgs& a, int i, unsigned epoch) {
   }
 }
 
+// this thread's share of the published counts of tiles [i0, i1): the loads of a batch are
+// issued together (one round trip per batch of 8), only tiles not yet published are re-polled
+__device__ __forceinline__ int FThreadCounts(const FArgs& a, int i0, int i1, unsigned epoch) {
+  constexpr int B = 8;
+  const int stride = static_cast<int>(blockDim.x);
+  int s = 0;
+  for (int base = i0 + static_cast<int>(threadIdx.x); base < i1; base += B * stride) {
+    unsigned long long v[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int i = base + b * stride;
+      v[b] = i < i1 ? __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : (static_cast<unsigned long long>(epoch) << 32);
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int i = base + b * stride;
+      s += static_cast<unsigned>(v[b] >> 32) == epoch ? static_cast<int>(static_cast<unsigned>(v[b])) : FAwait(a, i, epoch);
+    }
+  }
+  return s;
+}
+
 // sum of the published counts of tiles [i0, i1)
 __device__ int FSumCounts(const FArgs& a, int i0, int i1, unsigned epoch, int* sh) {
-  int s = 0;
-  for (int i = i0 + static_cast<int>(threadIdx.x); i < i1; i += blockDim.x) s += FAwait(a, i, epoch);
-  return BlockSumInt(s, sh);
+  return BlockSumInt(FThreadCounts(a, i0, i1, epoch), sh);
 }
 
 // children of expansion x (one thread)
@@ -611,15 +631,38 @@ __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
   xo->h_count = left_smaller ? lc : rc;
 }
 
-template <int ITERS>
+// block sums of M values at once (one barrier pair for all of them)
+template <int M>
+__device__ __forceinline__ void BlockSumMulti(int* v, int* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int m = 0; m < M; ++m) v[m] = WaveSum(v[m]);
+  __syncthreads();  // sh is reused
+  if (lane == 0) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) sh[m * 4 + w] = v[m];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < M; ++m) v[m] = sh[m * 4] + sh[m * 4 + 1] + sh[m * 4 + 2] + sh[m * 4 + 3];
+}
+
+// A block owns tiles bid + j * G. The first MAXT of them live in registers for the whole
+// launch: their loads are issued together (row ids, then bins), their counts reduced in one
+// block sum, their look-back sums loaded in one round, their scatter ballots published in one
+// LDS barrier, so a block pays a few memory round trips instead of a few per tile. Tiles
+// beyond MAXT (a grid smaller than the round's tiles / MAXT) take the per-tile path.
+template <int ITERS, int MAXT>
 __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
+  static_assert(kFPartThreads == 256, "4 waves per block");
+  static_assert(MAXT * ITERS <= 32, "left / valid bits of a thread fit one word");
   constexpr int kTile = kFPartThreads * ITERS;
   __shared__ int s_t0[kFrontierKmax + 1];
   __shared__ FExp s_x[kFrontierKmax];
   __shared__ uint32_t s_bits[kFrontierKmax][kMaxCatWords];
-  __shared__ int sh[8];
-  __shared__ int s_wl[ITERS][kFPartThreads / 64];
-  __shared__ int s_wv[ITERS][kFPartThreads / 64];
+  __shared__ int sh[MAXT * 4];
+  __shared__ int s_wl[MAXT][ITERS][kFPartThreads / 64];
+  __shared__ int s_wv[MAXT][ITERS][kFPartThreads / 64];
   const FState* stp = a.st;
   if (stp->done) return;
   const int k = stp->k, T = stp->total_tiles;
@@ -662,102 +705,185 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
     return b <= static_cast<uint32_t>(x.thr);
   };
   FStamp(a, rnd, kFStampPart, 1);
-  // phase 1: count every own tile and publish (the first tile's rows stay in registers)
-  int rows0[ITERS];
-  uint32_t gb0[ITERS];
-  for (int tile = bid; tile < T; tile += G) {
-    const int e = find(tile);
+  const int lane = t & 63, w = t >> 6;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // ---- register tiles: counts
+  int ex[MAXT], rows[MAXT][ITERS];
+  unsigned lbits = 0u, vbits = 0u;  // bit j * ITERS + i: row valid / goes left
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    const int tile = bid + j * G;
+    ex[j] = tile < T ? find(tile) : -1;
+    const int e = ex[j] < 0 ? 0 : ex[j];
     const FExp& x = s_x[e];
     const int pos0 = (tile - x.tile0) * kTile + t;
-    int rows[ITERS];
 #pragma unroll
-    for (int j = 0; j < ITERS; ++j) {
-      const int pos = pos0 + j * kFPartThreads;
-      rows[j] = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
+    for (int i = 0; i < ITERS; ++i) {
+      const int pos = pos0 + i * kFPartThreads;
+      rows[j][i] = (ex[j] >= 0 && pos < x.count) ? FRowAt(a, x.src_buf, x.start + pos) : -1;
     }
-    uint32_t gb[ITERS];
+  }
+  int cnt[MAXT];
+  {
+    uint32_t gb[MAXT][ITERS];
 #pragma unroll
-    for (int j = 0; j < ITERS; ++j) gb[j] = rows[j] >= 0 ? FColBin(a, x.group, rows[j]) : 0u;
-    int cnt = 0;
+    for (int j = 0; j < MAXT; ++j) {
+      const int g = s_x[ex[j] < 0 ? 0 : ex[j]].group;
 #pragma unroll
-    for (int j = 0; j < ITERS; ++j) cnt += (rows[j] >= 0 && go_left(e, gb[j])) ? 1 : 0;
-    cnt = BlockSumInt(cnt, sh);
-    if (t == 0) FPublish(&a.tile_pub[tile], epoch, cnt);
-    if (tile == bid) {
+      for (int i = 0; i < ITERS; ++i) gb[j][i] = rows[j][i] >= 0 ? FColBin(a, g, rows[j][i]) : 0u;
+    }
 #pragma unroll
-      for (int j = 0; j < ITERS; ++j) {
-        rows0[j] = rows[j];
-        gb0[j] = gb[j];
+    for (int j = 0; j < MAXT; ++j) {
+      cnt[j] = 0;
+#pragma unroll
+      for (int i = 0; i < ITERS; ++i) {
+        const bool valid = rows[j][i] >= 0;
+        const bool left = valid && go_left(ex[j], gb[j][i]);
+        vbits |= (valid ? 1u : 0u) << (j * ITERS + i);
+        lbits |= (left ? 1u : 0u) << (j * ITERS + i);
+        cnt[j] += left ? 1 : 0;
       }
     }
   }
-  FStamp(a, rnd, kFStampPart, 2);
-  // phase 2: scatter
-  const int lane = t & 63, w = t >> 6;
-  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int tile = bid; tile < T; tile += G) {
+  BlockSumMulti<MAXT>(cnt, sh);
+  if (t == 0) {
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      if (ex[j] >= 0) FPublish(&a.tile_pub[bid + j * G], epoch, cnt[j]);
+    }
+  }
+  // ---- tiles beyond MAXT: count and publish one by one
+  for (int tile = bid + MAXT * G; tile < T; tile += G) {
     const int e = find(tile);
     const FExp& x = s_x[e];
-    int lbase = FSumCounts(a, x.tile0, tile, epoch, sh);
-    const int tt = tile - x.tile0;
-    int rbase = tt * kTile - lbase;
-    int rows[ITERS];
-    uint32_t gb[ITERS];
-    if (tile == bid) {
+    const int pos0 = (tile - x.tile0) * kTile + t;
+    int c = 0;
 #pragma unroll
-      for (int j = 0; j < ITERS; ++j) {
-        rows[j] = rows0[j];
-        gb[j] = gb0[j];
-      }
-    } else {
-      const int pos0 = tt * kTile + t;
-#pragma unroll
-      for (int j = 0; j < ITERS; ++j) {
-        const int pos = pos0 + j * kFPartThreads;
-        rows[j] = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
-      }
-#pragma unroll
-      for (int j = 0; j < ITERS; ++j) gb[j] = rows[j] >= 0 ? FColBin(a, x.group, rows[j]) : 0u;
+    for (int i = 0; i < ITERS; ++i) {
+      const int pos = pos0 + i * kFPartThreads;
+      const int row = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
+      c += (row >= 0 && go_left(e, FColBin(a, x.group, row))) ? 1 : 0;
     }
+    int cc[1] = {c};
+    BlockSumMulti<1>(cc, sh);
+    if (t == 0) FPublish(&a.tile_pub[tile], epoch, cc[0]);
+  }
+  FStamp(a, rnd, kFStampPart, 2);
+  // ---- register tiles: look-back sums of all of them in one round, then one ballot barrier
+  int lb[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    lb[j] = 0;
+    if (ex[j] < 0) continue;
+    lb[j] = FThreadCounts(a, s_x[ex[j]].tile0, bid + j * G, epoch);
+  }
+  BlockSumMulti<MAXT>(lb, sh);
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const unsigned long long ml = __ballot((lbits >> (j * ITERS + i)) & 1u);
+      const unsigned long long mv = __ballot((vbits >> (j * ITERS + i)) & 1u);
+      if (lane == 0) {
+        s_wl[j][i][w] = __popcll(ml);
+        s_wv[j][i][w] = __popcll(mv);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    if (ex[j] < 0) continue;
+    const int e = ex[j];
+    const FExp& x = s_x[e];
+    const int tile = bid + j * G;
+    const int tt = tile - x.tile0;
+    int lbase = lb[j];
+    int rbase = tt * kTile - lbase;
     int* out = a.idx[x.dst_buf] + x.start;
 #pragma unroll
-    for (int j = 0; j < ITERS; ++j) {
-      const bool valid = rows[j] >= 0;
-      const bool left = valid && go_left(e, gb[j]);
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      if (lane == 0) {
-        s_wl[j][w] = __popcll(ml);
-        s_wv[j][w] = __popcll(mv);
-      }
-    }
-    __syncthreads();
-    int tile_left = 0;
-#pragma unroll
-    for (int j = 0; j < ITERS; ++j) {
-      const bool valid = rows[j] >= 0;
-      const bool left = valid && go_left(e, gb[j]);
+    for (int i = 0; i < ITERS; ++i) {
+      const bool valid = (vbits >> (j * ITERS + i)) & 1u;
+      const bool left = (lbits >> (j * ITERS + i)) & 1u;
       const unsigned long long ml = __ballot(left);
       const unsigned long long mv = __ballot(valid);
       int pl = 0, pv = 0, tl = 0, tv = 0;
 #pragma unroll
-      for (int i = 0; i < kFPartThreads / 64; ++i) {
-        if (i < w) {
-          pl += s_wl[j][i];
-          pv += s_wv[j][i];
+      for (int q = 0; q < kFPartThreads / 64; ++q) {
+        if (q < w) {
+          pl += s_wl[j][i][q];
+          pv += s_wv[j][i][q];
         }
-        tl += s_wl[j][i];
-        tv += s_wv[j][i];
+        tl += s_wl[j][i][q];
+        tv += s_wv[j][i][q];
       }
       if (valid) {
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
-        if (left) out[lbase + rl] = rows[j];
-        else out[x.count - 1 - (rbase + (rv - rl))] = rows[j];
+        if (left) out[lbase + rl] = rows[j][i];
+        else out[x.count - 1 - (rbase + (rv - rl))] = rows[j][i];
       }
       lbase += tl;
       rbase += tv - tl;
-      tile_left += tl;
+    }
+    if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
+  }
+  // ---- tiles beyond MAXT: look-back and scatter one by one
+  for (int tile = bid + MAXT * G; tile < T; tile += G) {
+    const int e = find(tile);
+    const FExp& x = s_x[e];
+    int lcur[1] = {FThreadCounts(a, x.tile0, tile, epoch)};
+    BlockSumMulti<1>(lcur, sh);
+    const int tt = tile - x.tile0;
+    int lbase = lcur[0];
+    int rbase = tt * kTile - lbase;
+    int rr[ITERS];
+    unsigned lb1 = 0u, vb1 = 0u;
+    const int pos0 = tt * kTile + t;
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int pos = pos0 + i * kFPartThreads;
+      rr[i] = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const bool valid = rr[i] >= 0;
+      const bool left = valid && go_left(e, FColBin(a, x.group, rr[i]));
+      vb1 |= (valid ? 1u : 0u) << i;
+      lb1 |= (left ? 1u : 0u) << i;
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      if (lane == 0) {
+        s_wl[0][i][w] = __popcll(ml);
+        s_wv[0][i][w] = __popcll(mv);
+      }
+    }
+    __syncthreads();
+    int* out = a.idx[x.dst_buf] + x.start;
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const bool valid = (vb1 >> i) & 1u;
+      const bool left = (lb1 >> i) & 1u;
+      const unsigned long long ml = __ballot(left);
+      const unsigned long long mv = __ballot(valid);
+      int pl = 0, pv = 0, tl = 0, tv = 0;
+#pragma unroll
+      for (int q = 0; q < kFPartThreads / 64; ++q) {
+        if (q < w) {
+          pl += s_wl[0][i][q];
+          pv += s_wv[0][i][q];
+        }
+        tl += s_wl[0][i][q];
+        tv += s_wv[0][i][q];
+      }
+      if (valid) {
+        const int rl = pl + __popcll(ml & lt_mask);
+        const int rv = pv + __popcll(mv & lt_mask);
+        if (left) out[lbase + rl] = rr[i];
+        else out[x.count - 1 - (rbase + (rv - rl))] = rr[i];
+      }
+      lbase += tl;
+      rbase += tv - tl;
     }
     __syncthreads();
     if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
@@ -1208,16 +1334,22 @@ void LaunchFrontierInit(const FArgs& a, hipStream_t s) {
   HIP_CHECK(hipGetLastError());
 }
 
-void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
+template <int THREADS>
+void LaunchHistT(const FArgs& a, size_t lds, hipStream_t s) {
   const dim3 grid(a.hist_grid + a.kmax, a.num_tiles);
   if (a.use_dp) {
-    if (a.width == 1) k_f_hist<1, 1><<<grid, kFHistThreads, lds, s>>>(a);
-    else k_f_hist<2, 1><<<grid, kFHistThreads, lds, s>>>(a);
+    if (a.width == 1) k_f_hist<1, 1, THREADS><<<grid, THREADS, lds, s>>>(a);
+    else k_f_hist<2, 1, THREADS><<<grid, THREADS, lds, s>>>(a);
   } else {
-    if (a.width == 1) k_f_hist<1, 0><<<grid, kFHistThreads, lds, s>>>(a);
-    else k_f_hist<2, 0><<<grid, kFHistThreads, lds, s>>>(a);
+    if (a.width == 1) k_f_hist<1, 0, THREADS><<<grid, THREADS, lds, s>>>(a);
+    else k_f_hist<2, 0, THREADS><<<grid, THREADS, lds, s>>>(a);
   }
   HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
+  if (a.hist_threads == 1024) LaunchHistT<1024>(a, lds, s);
+  else LaunchHistT<512>(a, lds, s);
 }
 
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
@@ -1237,28 +1369,32 @@ void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
 }
 
 void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s) {
-  if (iters == 4) k_f_partition<4><<<grid, kFPartThreads, 0, s>>>(a);
-  else if (iters == 16) k_f_partition<16><<<grid, kFPartThreads, 0, s>>>(a);
-  else k_f_partition<8><<<grid, kFPartThreads, 0, s>>>(a);
+  if (iters == 4) k_f_partition<4, 4><<<grid, kFPartThreads, 0, s>>>(a);
+  else if (iters == 16) k_f_partition<16, 1><<<grid, kFPartThreads, 0, s>>>(a);
+  else k_f_partition<8, 2><<<grid, kFPartThreads, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 
 int FrontierPartitionBlocksPerCU(int iters) {
   int per_cu = 0;
-  const void* fn = iters == 4 ? reinterpret_cast<const void*>(k_f_partition<4>)
-                              : (iters == 16 ? reinterpret_cast<const void*>(k_f_partition<16>)
-                                             : reinterpret_cast<const void*>(k_f_partition<8>));
+  const void* fn = iters == 4 ? reinterpret_cast<const void*>(k_f_partition<4, 4>)
+                              : (iters == 16 ? reinterpret_cast<const void*>(k_f_partition<16, 1>)
+                                             : reinterpret_cast<const void*>(k_f_partition<8, 2>));
   HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kFPartThreads, 0));
   return per_cu;
 }
 
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
   if (hist_lds > 64 * 1024) {
-    const void* fn = use_dp ? (width == 1 ? reinterpret_cast<const void*>(k_f_hist<1, 1>)
-                                          : reinterpret_cast<const void*>(k_f_hist<2, 1>))
-                            : (width == 1 ? reinterpret_cast<const void*>(k_f_hist<1, 0>)
-                                          : reinterpret_cast<const void*>(k_f_hist<2, 0>));
-    HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds)));
+    const void* fns[8] = {reinterpret_cast<const void*>(k_f_hist<1, 1, 512>), reinterpret_cast<const void*>(k_f_hist<2, 1, 512>),
+                          reinterpret_cast<const void*>(k_f_hist<1, 0, 512>), reinterpret_cast<const void*>(k_f_hist<2, 0, 512>),
+                          reinterpret_cast<const void*>(k_f_hist<1, 1, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 1, 1024>),
+                          reinterpret_cast<const void*>(k_f_hist<1, 0, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 0, 1024>)};
+    (void)use_dp;
+    (void)width;
+    for (const void* fn : fns) {
+      HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds)));
+    }
   }
   if (scan_lds > 64 * 1024) {
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -617,7 +617,7 @@ def test_device_categorical_wide(lgb, gpu_required, rng, ncat, onehot):
 def test_device_max_bin_8191_global_scan(lgb, gpu_required, rng):
     """max_bin=8191: the split scan works in global scratch (features wider than the LDS budget)
     and matches the CPU learner; the same global path forced on ordinary bins (LGAP_SCAN_GLOBAL)
-    grows the model of the LDS path."""
+    grows the model of the sequential chain's LDS path."""
     import os
     import subprocess
     import sys
@@ -637,7 +637,9 @@ def test_device_max_bin_8191_global_scan(lgb, gpu_required, rng):
             "print(lgb.train(p, lgb.Dataset(X, y, params=p), 5).model_to_string().split('end of trees')[0])"
             ) % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = []
-    for env in ({}, {"LGAP_SCAN_GLOBAL": "1"}):
+    # the global-memory scan is a variant of the sequential device chain (the frontier engine has
+    # no global-scan variant): compare it with that chain's LDS scan
+    for env in ({"LGAP_FRONTIER": "0"}, {"LGAP_FRONTIER": "0", "LGAP_SCAN_GLOBAL": "1"}):
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                            env=dict(os.environ, **env))
         assert r.returncode == 0, r.stderr[-2000:]
@@ -670,3 +672,38 @@ def test_reset_training_data_keeps_device_validation(lgb, gpu_required, rng):
     assert np.isfinite(outs[0][0])
     assert abs(outs[0][0] - outs[1][0]) < 1e-3, (outs[0][0], outs[1][0])
     np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("extra", [{}, {"max_depth": 6}, {"monotone_constraints": [1, -1, 0, 0, 0, 0]},
+                                   {"interaction_constraints": [[0, 1], [1, 2, 3]]},
+                                   {"categorical_feature": [4], "max_cat_to_onehot": 4},
+                                   {"bagging_fraction": 0.7, "bagging_freq": 1}, {"num_leaves": 255, "min_data_in_leaf": 5}])
+def test_frontier_engine_matches_sequential_chain(lgb, gpu_required, rng, extra):
+    """The frontier engine (batched rounds + replay of best-first order, src/device/frontier.h)
+    grows the trees of the one-split-at-a-time device chain: identical split structure with fp64
+    histograms, for the options the frontier covers."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, json, numpy as np; sys.path.insert(0, %r); import lambdagap_amd as lgb; "
+            "rng = np.random.default_rng(3); X = rng.standard_normal((60000, 6)); "
+            "X[:, 4] = rng.integers(0, 9, 60000); X[rng.random(60000) < 0.1, 0] = np.nan; "
+            "y = (X[:, 0] - 0.7 * X[:, 1] + 0.4 * X[:, 2] * X[:, 3] + 0.3 * (X[:, 4] %% 3) + 0.3 * rng.standard_normal(60000) > 0).astype(float); "
+            "p = dict({'objective': 'binary', 'num_leaves': 31, 'device_type': 'gpu', 'verbosity': -1, 'gpu_use_dp': True, "
+            "'seed': 2}, **json.loads(sys.argv[1])); "
+            "b = lgb.train(p, lgb.Dataset(X, y, params=p), 6, keep_training_booster=True); "
+            "print(json.dumps({'model': b.model_to_string().split('end of trees')[0], 'name': b.device_name()}))") % root
+    outs = []
+    for fr in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", code, json.dumps(extra)], capture_output=True, text=True,
+                           timeout=300, env=dict(os.environ, LGAP_FRONTIER=fr))
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+
+    def structure(model):
+        return [ln for ln in model.splitlines() if ln.startswith(("split_feature=", "threshold=", "left_child=",
+                                                                   "right_child=", "decision_type=", "num_leaves="))]
+    assert structure(outs[0]["model"]) == structure(outs[1]["model"])
