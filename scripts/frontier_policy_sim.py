@@ -48,8 +48,9 @@ class Finder:
         return best
 
 
-def grow(finder, n, L, policy, spec=0, kmax=64, M=4):
-    """Returns (rounds, expansions, committed splits, node table)."""
+def grow(finder, n, L, policy, spec=0, kmax=64, M=4, alpha=1.0):
+    """Returns (rounds, expansions, committed splits, hist rows / n, committed-only hist rows / n,
+    partitioned rows / n)."""
     nodes = {0: dict(rows=np.arange(n), depth=0, parent=-1, left=None, committed=False)}
     nodes[0]["gain"], nodes[0]["feat"], nodes[0]["thr"] = finder.best(nodes[0]["rows"])
     nxt = 1
@@ -105,7 +106,7 @@ def grow(finder, n, L, policy, spec=0, kmax=64, M=4):
             chosen = []
             for c in el:
                 rank = sum(1 for x in gains if x > nodes[c]["gain"])
-                if c == blocked or rank < R + spec:
+                if c == blocked or rank < int(alpha * R) + spec:
                     chosen.append(c)
             chosen = chosen[:kmax]
         for c in chosen:
@@ -137,9 +138,9 @@ def main():
         g, h = p - y, p * (1 - p)
         f = Finder(B, g, h)
         res = {}
-        for pol, spec in ((0, 0), (1, 0)):
-            res[(pol, spec)] = grow(f, n, L, pol, spec)
-        print(it, {f"p{k[0]}s{k[1]}": v for k, v in res.items()}, flush=True)
+        for pol, spec, alpha in ((1, 0, 1.0), (1, 0, 0.5), (1, 0, 0.25)):
+            res[(pol, spec, alpha)] = grow(f, n, L, pol, spec, alpha=alpha)
+        print(it, {f"p{k[0]}s{k[1]}a{k[2]}": v for k, v in res.items()}, flush=True)
         # advance the score with a crude tree of the root split (keeps gradients moving)
         gain, j, t = f.best(np.arange(n))
         left = B[:, j] <= t

@@ -3133,6 +3133,14 @@ class DeviceTreeLearner : public TreeLearner {
     tree_buf_.Resize(std::max(tree_buf_.size(), total));
     HIP_CHECK(hipMemcpyAsync(tree_buf_.get(), hp, total, hipMemcpyHostToDevice, stream_));
     const char* db = tree_buf_.get();
+    if (rowbins == rowbins_.get() && n == N_ && stride_dw_ > 16 && colbins_.size() >= static_cast<size_t>(G_) * N_ * width_) {
+      LaunchTraverseCols(colbins_.get(), width_, n, reinterpret_cast<const TNode*>(db), nn,
+                         reinterpret_cast<const TCat*>(db + node_bytes),
+                         reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
+                         reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      return;
+    }
     LaunchTraverse(rowbins, stride_dw_, width_, n, reinterpret_cast<const TNode*>(db), nn,
                    reinterpret_cast<const TCat*>(db + node_bytes), reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                    reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
@@ -3210,6 +3218,8 @@ class DeviceTreeLearner : public TreeLearner {
       gcount = cached_gcount_;
     }
     tp->root_gcount = gcount;
+    tp->spec_alpha = static_cast<float>(fspec_alpha_);
+    tp->pad[0] = tp->pad[1] = tp->pad[2] = 0;
     HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
     if (config_->use_quantized_grad) QuantizeGradients(class_id);
     col_sampler_.ResetByTree();
@@ -3246,6 +3256,10 @@ class DeviceTreeLearner : public TreeLearner {
       }
       const FeatureInfo& fi = data_->feature(info.feature);
       const BinMapper& mapper = data_->inner_mapper(info.feature);
+      if (fi.bin_type == BinType::Numerical && info.threshold >= static_cast<uint32_t>(std::max(1, fi.num_bin))) {
+        Log::Fatal("device tree: invalid split record %d (feature %d, threshold %u of %d bins)", s, info.feature,
+                   info.threshold, fi.num_bin);
+      }
       const float gain = static_cast<float>(info.gain + config_->min_gain_to_split);
       if (fi.bin_type == BinType::Numerical) {
         tree->Split(r.leaf, info.feature, fi.real_index, info.threshold, mapper.BinToValue(info.threshold),
@@ -3358,6 +3372,12 @@ class DeviceTreeLearner : public TreeLearner {
     if (const char* e = std::getenv("LGAP_FHIST_THREADS")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
     fpolicy_ = 1;
     if (const char* e = std::getenv("LGAP_FRONTIER_POLICY")) fpolicy_ = std::atoi(e) == 0 ? 0 : 1;
+    fspec_alpha_ = 1.0;
+    fspec_fixed_ = false;
+    if (const char* e = std::getenv("LGAP_FRONTIER_ALPHA")) {  // fixed speculation depth (A/B)
+      fspec_alpha_ = std::max(0.01, std::min(1.0, std::atof(e)));
+      fspec_fixed_ = true;
+    }
     if (std::getenv("LGAP_FSTAMPS")) {
       fstamps_.Resize(256 * 4 * kFStampSlots);
       fstamps_.Zero(stream_);
@@ -3502,6 +3522,15 @@ class DeviceTreeLearner : public TreeLearner {
       }
       launched += kCont;
     }
+    // speculation feedback: the fraction of partitioned rows spent on expansions the tree never
+    // committed steers the next tree's speculation depth (deep, chain-like trees waste more)
+    const double rows_all = static_cast<double>(hs->used_rows + hs->waste_rows);
+    if (rows_all > 0 && !fspec_fixed_) {
+      const double waste = static_cast<double>(hs->waste_rows) / rows_all;
+      if (waste > 0.12) fspec_alpha_ = std::max(0.15, fspec_alpha_ * 0.75);
+      else if (waste < 0.04) fspec_alpha_ = std::min(1.0, fspec_alpha_ * 1.2);
+    }
+    fstat_waste_ += rows_all > 0 ? static_cast<double>(hs->waste_rows) / rows_all : 0.0;
     // rounds the tree needed (selects run after the root's) -> next tree's replay length
     const int used = std::max(1, hs->round - 1);
     frounds_hist_[frounds_pos_++ % 4] = used;
@@ -3522,8 +3551,9 @@ class DeviceTreeLearner : public TreeLearner {
     if (hbar[2] != 0u) Log::Fatal("k_f_partition: a wait on published tile counts timed out (blocks not co-resident?)");
     if (fstamps_.size() && fstat_trees_ == 3) ReportFrontierStamps(hs->round);
     if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {
-      std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max)\n", fstat_trees_,
-                   static_cast<double>(fstat_rounds_) / fstat_trees_, static_cast<double>(fstat_spec_) / fstat_trees_, L_);
+      std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max), wasted rows %.1f%%, "
+                   "alpha %.3f\n", fstat_trees_, static_cast<double>(fstat_rounds_) / fstat_trees_,
+                   static_cast<double>(fstat_spec_) / fstat_trees_, L_, 100.0 * fstat_waste_ / fstat_trees_, fspec_alpha_);
     }
   }
 
@@ -4583,6 +4613,8 @@ class DeviceTreeLearner : public TreeLearner {
   hipGraphExec_t fcont_ = nullptr;
   int fpred_rounds_ = 16, frounds_hist_[4] = {1, 1, 1, 1}, frounds_pos_ = 0;
   long long fstat_rounds_ = 0, fstat_spec_ = 0;
+  double fstat_waste_ = 0.0, fspec_alpha_ = 1.0;
+  bool fspec_fixed_ = false;
   int fstat_trees_ = 0;
   PinnedBuf<FState> pin_fst_;
   DevBuf<unsigned long long> fstamps_;

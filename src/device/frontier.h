@@ -52,6 +52,13 @@ constexpr int kFrontierBufs = 4;    // depth-indexed row-index buffers
 constexpr int kFrontierIdx = 5;     // index buffers addressed by id: depth buffers {0, 1, 3, 4}, bag 2
 constexpr int kFrontierMaxNodes = 4096;  // computed-node capacity of the select's LDS image
 
+// entries of the select's sort of the alive nodes: a power of two >= C (C <= kFrontierMaxNodes)
+__host__ __device__ inline int FrontierSortCap(int C) {
+  int p = 64;
+  while (p < C) p <<= 1;
+  return p;
+}
+
 // index-buffer id of depth buffer j (0..3)
 __host__ __device__ inline int FrontierDepthBuf(int j) { return j < 2 ? j : j + 1; }
 
@@ -93,8 +100,9 @@ struct FState {
   int num_leaves, num_splits;
   int cid_next;
   int blocked;      // cid the replay waits for (-1: none)
-  int spec;         // speculative expansions started so far (diagnostics)
-  int pad[6];
+  int spec;         // expansions started so far
+  long long used_rows, waste_rows;  // (when done) rows partitioned by committed / uncommitted expansions
+  int pad[2];
 };
 
 // Arguments of the frontier kernels (device pointers into the learner's buffers).

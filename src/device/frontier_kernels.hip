@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
     s.cid_next = 1;
     s.blocked = -1;
     s.spec = 0;
-    for (int i = 0; i < 6; ++i) s.pad[i] = 0;
+    s.used_rows = s.waste_rows = 0;
+    s.pad[0] = s.pad[1] = 0;
     *a.st = s;
     FNode r;
     r.buf = tp.root_buf;
@@ -925,9 +926,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   int* s_lcid = s_rank + C;                                  // [L]
   int* s_c0 = s_lcid + L;                                    // [L] committed leaves of this launch
   int* s_c1 = s_c0 + L;                                      // [L] their cids
-  int* s_ga = s_c1 + L;                                      // [C] policy: better-gain alive count
-  int* s_er = s_ga + C;                                      // [C] policy: better-gain eligible count
-  uint8_t* s_st = reinterpret_cast<uint8_t*>(s_er + C);      // [C]
+  uint8_t* s_st = reinterpret_cast<uint8_t*>(s_c1 + L);      // [C]
   __shared__ int s_cpos[2 * kFrontierKmax];  // this round's children: winning candidate position
   __shared__ int s_pc[2 * kFrontierKmax];    // pair -> child cid (-1: none / skipped)
   __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_k, s_tiles;
@@ -1049,6 +1048,9 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   double* s_lg = reinterpret_cast<double*>(smem + ((reinterpret_cast<uintptr_t>(s_st + C) -
                                                      reinterpret_cast<uintptr_t>(smem) + 15) & ~uintptr_t(15)));  // [L]
   int* s_lf = reinterpret_cast<int*>(s_lg + L);                        // [L]
+  double* s_sg = reinterpret_cast<double*>(smem + ((reinterpret_cast<uintptr_t>(s_lf + L) -
+                                                    reinterpret_cast<uintptr_t>(smem) + 15) & ~uintptr_t(15)));  // [P2max]
+  int* s_sc = reinterpret_cast<int*>(s_sg + FrontierSortCap(C));      // [P2max]
   for (int l = t; l < st.num_leaves; l += blockDim.x) {
     const int c = s_lcid[l];
     const int f = s_feat[c];
@@ -1192,44 +1194,85 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
     __syncthreads();
     const int na = min(s_na, cap_list);
-    for (int i = t; i < na; i += blockDim.x) {
-      s_ga[i] = 0;
-      s_er[i] = 0;
-    }
-    __syncthreads();
     const int blocked = s_blocked;
     const int R = L - 1 - ns;  // splits the tree may still make
-    // Pairwise order over the alive list (all threads): s_ga[i] = alive nodes with a better
-    // (gain desc, cid asc) key; s_er[i] = such ELIGIBLE nodes other than the blocked one.
-    // Policy 1 (default) takes an eligible node when it ranks within the remaining budget R
-    // (+ spec_cap) among ALL alive uncommitted nodes: best-first order commits at most R more
+    // Order of the alive list by (gain desc, cid asc): a bitonic sort in LDS. Position p in the
+    // sorted list = alive nodes with a better key; the eligible rank = eligible nodes (other
+    // than the blocked one) before p. Policy 1 (default) takes an eligible node when its
+    // position is within the speculation budget: best-first order commits at most R more
     // splits and takes them roughly by gain. Policy 0 budgets R minus every expanded but
     // uncommitted node. The blocked node always goes first.
-    for (int q = t; q < na * na; q += blockDim.x) {
-      const int i = q / na, jj = q - i * na;
-      if (i == jj) continue;
-      const int ci = s_ac[i] >= 0 ? s_ac[i] : ~s_ac[i];
-      const int cj = s_ac[jj] >= 0 ? s_ac[jj] : ~s_ac[jj];
-      const double gi = s_gain[ci], gj = s_gain[cj];
-      if (gj > gi || (gj == gi && cj < ci)) {
-        atomicAdd(&s_ga[i], 1);
-        if (s_ac[jj] >= 0 && cj != blocked) atomicAdd(&s_er[i], 1);
+    int P2 = 64;
+    while (P2 < na) P2 <<= 1;
+    for (int i = t; i < P2; i += blockDim.x) {
+      if (i < na) {
+        const int c = s_ac[i] >= 0 ? s_ac[i] : ~s_ac[i];
+        s_sg[i] = s_gain[c];
+        s_sc[i] = s_ac[i];
+      } else {
+        s_sg[i] = -INFINITY;  // padding sorts last
+        s_sc[i] = 0x7fffffff;
       }
     }
+    __syncthreads();
+    for (int kk = 2; kk <= P2; kk <<= 1) {
+      for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+        for (int i = t; i < P2; i += blockDim.x) {
+          const int l = i ^ jj;
+          if (l <= i) continue;
+          const double gi = s_sg[i], gl = s_sg[l];
+          const int ri = s_sc[i], rl = s_sc[l];
+          const int ci = ri >= 0 ? ri : ~ri, cl = rl >= 0 ? rl : ~rl;
+          // does l belong before i (gain desc, cid asc; padding cid INT_MAX)
+          const bool l_first = gl > gi || (gl == gi && cl < ci);
+          if (l_first == ((i & kk) == 0)) {
+            s_sg[i] = gl;
+            s_sg[l] = gi;
+            s_sc[i] = rl;
+            s_sc[l] = ri;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // eligible ranks: exclusive scan of the eligible (non-blocked) flags in sorted order
+    constexpr int kPer = kFrontierMaxNodes / kFSelThreads;  // <= 4 positions per thread
+    int fl[kPer], loc = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int p = t * kPer + q;
+      const int r = p < na ? s_sc[p] : -1;
+      fl[q] = (r >= 0 && r != blocked) ? 1 : 0;
+      loc += fl[q];
+    }
+    const int incl = WaveInclusiveScan(loc);
+    __shared__ int s_wsum[kFSelThreads / 64];
+    if (lane == 63) s_wsum[w] = incl;
     if (t == 0) s_k = 0;
     __syncthreads();
+    int woff = 0;
+    for (int q = 0; q < w; ++q) woff += s_wsum[q];
+    int ex = woff + incl - loc;
     const int cap_nodes = (C - cid_next) / 2 - (R - 1);
+    // policy 1 budget: the best `alpha` fraction of the remaining splits (alpha tuned per tree by
+    // the host from the rows the previous trees' uncommitted expansions cost)
+    const float alpha = a.tp->spec_alpha > 0.f ? a.tp->spec_alpha : 1.f;
+    const int budget = static_cast<int>(alpha * static_cast<float>(R)) + a.spec_cap;
     const int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
                                   : min(a.kmax, max(1, cap_nodes));
-    for (int i = t; i < na; i += blockDim.x) {
-      if (s_ac[i] < 0) continue;  // not eligible
-      const int c = s_ac[i];
-      const int r = c == blocked ? 0 : s_er[i] + (blocked >= 0 ? 1 : 0);
-      const bool take = a.policy == 0 || c == blocked || s_ga[i] < R + a.spec_cap;
-      if (take && r < lim) {
-        s_exp[r] = c;
-        atomicMax(&s_k, r + 1);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int p = t * kPer + q;
+      const int rc = p < na ? s_sc[p] : -1;
+      if (rc >= 0) {  // eligible
+        const int r = rc == blocked ? 0 : ex + (blocked >= 0 ? 1 : 0);
+        const bool take = a.policy == 0 || rc == blocked || p < budget;
+        if (take && r < lim) {
+          s_exp[r] = rc;
+          atomicMax(&s_k, r + 1);
+        }
       }
+      ex += fl[q];
     }
     __syncthreads();
     FStamp(a, rnd, kFStampSel, 5);
@@ -1312,6 +1355,28 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   FStamp(a, rnd, kFStampSel, 6);
   FStampEnd(a, rnd, kFStampSel);
   if (done) {
+    // rows partitioned by committed vs uncommitted expansions (the host's speculation feedback)
+    __shared__ unsigned long long s_used, s_waste;
+    if (t == 0) {
+      s_used = 0ull;
+      s_waste = 0ull;
+    }
+    __syncthreads();
+    unsigned long long u = 0ull, wst = 0ull;
+    for (int c = t; c < cid_next; c += blockDim.x) {
+      const uint8_t sc = s_st[c];
+      if (!(sc & kNodeExpanded)) continue;
+      const unsigned long long cnt = static_cast<unsigned long long>(a.nodes[c].count);
+      if (sc & kNodeCommitted) u += cnt;
+      else wst += cnt;
+    }
+    if (u) atomicAdd(&s_used, u);
+    if (wst) atomicAdd(&s_waste, wst);
+    __syncthreads();
+    if (t == 0) {
+      a.st->used_rows = static_cast<long long>(s_used);
+      a.st->waste_rows = static_cast<long long>(s_waste);
+    }
     for (int l = t; l < nl; l += blockDim.x) {
       const FNode nd = a.nodes[s_lcid[l]];
       LeafRange r;
@@ -1359,8 +1424,9 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 }
 
 size_t FrontierSelectLds(int C, int L) {
-  return static_cast<size_t>(C) * (sizeof(double) + 7 * sizeof(int) + 1) + 32 +
-         static_cast<size_t>(L) * (3 * sizeof(int) + sizeof(double) + sizeof(int)) + 64;
+  return static_cast<size_t>(C) * (sizeof(double) + 5 * sizeof(int) + 1) + 64 +
+         static_cast<size_t>(L) * (3 * sizeof(int) + sizeof(double) + sizeof(int)) + 64 +
+         static_cast<size_t>(FrontierSortCap(C)) * (sizeof(double) + sizeof(int));
 }
 
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {

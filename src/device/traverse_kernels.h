@@ -39,5 +39,10 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
                     const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,
                     int num_cu, hipStream_t s);
 
+// the same over the group-major copy colbins[g * n + row] (wide training rows)
+void LaunchTraverseCols(const uint8_t* colbins, int width, int n, const TNode* nodes, int num_nodes, const TCat* cats,
+                        const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score, int num_cu,
+                        hipStream_t s);
+
 }  // namespace device
 }  // namespace lgap

@@ -99,7 +99,79 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
   }
 }
 
+// Wide rows of the TRAINING set: walk over the group-major copy (colbins[g * n + row]), so lanes
+// at the same node read one contiguous run of a column instead of one cache line per row.
+template <int W>
+__global__ __launch_bounds__(kTThreads) void k_traverse_col(const uint8_t* __restrict__ colbins, int n,
+                                                            const TNode* __restrict__ nodes, int num_nodes,
+                                                            const TCat* __restrict__ cats, const uint32_t* __restrict__ cat_bits,
+                                                            const double* __restrict__ leaf_value, int num_leaves,
+                                                            double* __restrict__ score) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  TNode* s_nodes = reinterpret_cast<TNode*>(lds);
+  double* s_leaf = reinterpret_cast<double*>(lds + ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)));
+  const int t = threadIdx.x;
+  for (int i = t; i < num_nodes * static_cast<int>(sizeof(TNode) / 4); i += kTThreads) {
+    reinterpret_cast<uint32_t*>(s_nodes)[i] = reinterpret_cast<const uint32_t*>(nodes)[i];
+  }
+  for (int i = t; i < num_leaves; i += kTThreads) s_leaf[i] = leaf_value[i];
+  __syncthreads();
+  for (long long base = static_cast<long long>(blockIdx.x) * kTRows; base < n;
+       base += static_cast<long long>(gridDim.x) * kTRows) {
+    long long row[kTRowsPerThread];
+    int node[kTRowsPerThread];
+#pragma unroll
+    for (int j = 0; j < kTRowsPerThread; ++j) {
+      row[j] = base + t + j * kTThreads;
+      node[j] = row[j] < n ? 0 : ~0;
+    }
+    bool live = true;
+    while (live) {
+      live = false;
+#pragma unroll
+      for (int j = 0; j < kTRowsPerThread; ++j) {
+        if (node[j] < 0) continue;
+        const TNode nd = s_nodes[node[j]];
+        const size_t o = static_cast<size_t>(nd.group) * n + row[j];
+        const uint32_t gb = W == 1 ? colbins[o] : reinterpret_cast<const uint16_t*>(colbins)[o];
+        bool left;
+        if (nd.flags & kTCat) {
+          left = CatLeft(cats[node[j]], cat_bits, gb);
+        } else if (gb < nd.lo || gb > nd.hi) {
+          left = (nd.flags & kTOutLeft) != 0;
+        } else if (static_cast<int>(gb) == nd.gmiss) {
+          left = (nd.flags & kTDefaultLeft) != 0;
+        } else {
+          left = gb <= nd.tg;
+        }
+        node[j] = left ? nd.left : nd.right;
+        live |= node[j] >= 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kTRowsPerThread; ++j) {
+      if (row[j] < n) score[row[j]] += s_leaf[~node[j]];
+    }
+  }
+}
+
 }  // namespace
+
+void LaunchTraverseCols(const uint8_t* colbins, int width, int n, const TNode* nodes, int num_nodes, const TCat* cats,
+                        const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score, int num_cu,
+                        hipStream_t s) {
+  if (n <= 0) return;
+  const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + sizeof(double) * num_leaves;
+  const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
+  if (width == 1) {
+    k_traverse_col<1><<<grid, kTThreads, lds, s>>>(colbins, n, nodes, num_nodes, cats, cat_bits, leaf_value, num_leaves,
+                                                  score);
+  } else {
+    k_traverse_col<2><<<grid, kTThreads, lds, s>>>(colbins, n, nodes, num_nodes, cats, cat_bits, leaf_value, num_leaves,
+                                                  score);
+  }
+  HIP_CHECK(hipGetLastError());
+}
 
 void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
                     const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,

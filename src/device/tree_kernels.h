@@ -53,6 +53,8 @@ struct TreeParams {
   int root_count;
   int cls;
   int root_gcount;  // global (all ranks) row count of the root
+  float spec_alpha;  // frontier engine: speculation depth, fraction of the remaining budget (host-tuned per tree)
+  int pad[3];
 };
 
 struct Ctl {

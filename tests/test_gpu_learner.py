@@ -707,3 +707,17 @@ def test_frontier_engine_matches_sequential_chain(lgb, gpu_required, rng, extra)
         return [ln for ln in model.splitlines() if ln.startswith(("split_feature=", "threshold=", "left_child=",
                                                                    "right_child=", "decision_type=", "num_leaves="))]
     assert structure(outs[0]["model"]) == structure(outs[1]["model"])
+
+
+def test_wide_rows_training_score(lgb, gpu_required, rng):
+    """Rows wider than 16 dwords (120 features): the training score update walks the group-major
+    copy (traverse_kernels.hip, k_traverse_col); the boosted model tracks the CPU learner's."""
+    n, f = 30000, 120
+    X = rng.standard_normal((n, f))
+    X[:, 3] = rng.integers(0, 7, n)
+    y = X[:, 0] - 0.5 * X[:, 1] + 0.3 * X[:, 2] * X[:, 5] + 0.2 * (X[:, 3] == 2) + 0.1 * rng.standard_normal(n)
+    params = {"objective": "regression", "num_leaves": 31, "verbosity": -1, "categorical_feature": [3],
+              "min_data_in_leaf": 40}
+    bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y), 8)
+    bg = lgb.train({**params, "device_type": "gpu", "gpu_use_dp": True}, lgb.Dataset(X, y), 8)
+    np.testing.assert_allclose(bg.predict(X[:3000]), bc.predict(X[:3000]), rtol=1e-4, atol=1e-4)
