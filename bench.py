@@ -45,6 +45,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--graph", type=int, default=None, help="device_use_graph override (1/0)")
     ap.add_argument("--use-dp", action="store_true", help="gpu_use_dp=true: fp64 histogram accumulation")
+    ap.add_argument("--quantized", action="store_true",
+                    help="use_quantized_grad=true (4 gradient levels, integer histograms); a secondary line")
     ap.add_argument("--rehearse-dp", action="store_true",
                     help="1 GPU: run the RCCL data-parallel learner path on a one-rank communicator")
     ap.add_argument("--dp-host-transport", action="store_true",
@@ -114,6 +116,9 @@ def main() -> int:
         params.update({"tree_learner": "data", "num_machines": world, "pre_partition": True})
     if args.use_dp:
         params["gpu_use_dp"] = True
+    if args.quantized:
+        params["use_quantized_grad"] = True
+        params["num_grad_quant_bins"] = 4
     if args.graph is not None:
         params["device_use_graph"] = bool(args.graph)
     train_set = lgb.Dataset(X, y, params=params, free_raw_data=True)
@@ -165,7 +170,8 @@ def main() -> int:
             "auc": round(auc, 6),
             "config": {
                 "model": f"gbdt binary, {args.num_leaves} leaves, {args.max_bin} bins, lr 0.1"
-                         + (", gpu_use_dp" if args.use_dp else ""),
+                         + (", gpu_use_dp" if args.use_dp else "")
+                         + (", use_quantized_grad (4 levels)" if args.quantized else ""),
                 "global_batch": args.rows,
                 "seq_len": 28,
                 "parallelism": f"dp{world}",

@@ -28,6 +28,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--device", default="gpu")
+    ap.add_argument("--quantized", action="store_true", help="use_quantized_grad=true, 4 gradient levels")
     ap.add_argument("--learner", choices=["serial", "data", "voting"], default="serial",
                     help="data / voting on ONE GPU run through a one-rank RCCL communicator (the parallel "
                          "learner's kernels and exchanges, single rank)")
@@ -64,6 +65,9 @@ def main() -> int:
         params = preset("regression_goss", device_type=args.device, verbosity=-1, metric="l2")
     if args.learner == "voting":
         params["tree_learner"] = "voting"
+    if args.quantized:
+        params["use_quantized_grad"] = True
+        params["num_grad_quant_bins"] = 4
     gen_s = time.time() - t0
     t0 = time.time()
     train = lgb.Dataset(X, y, group=g, params=params, free_raw_data=True)
@@ -84,7 +88,7 @@ def main() -> int:
     ev = {name: round(v, 6) for _, name, v, _ in booster.eval_valid()}
     print(json.dumps({"config": args.config, "rows": rows, "features": nf, "value": round(args.steps / el, 3),
                       "unit": "iters/s", "ms_per_step": round(1000 * el / args.steps, 3), "steps": args.steps,
-                      "warmup": args.warmup, "device": booster.device_name(), "valid": ev, "learner": args.learner,
+                      "warmup": args.warmup, "device": booster.device_name(), "valid": ev, "learner": args.learner, "quantized": args.quantized,
                       "num_leaves": params["num_leaves"], "max_bin": params["max_bin"],
                       "data_gen_s": round(gen_s, 1), "construct_s": round(construct_s, 1), "data": "synthetic"}),
           flush=True)

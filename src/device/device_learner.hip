@@ -9,26 +9,46 @@
 //   gh       K x N float2        (gradient, hessian), class-major
 //   idx[0/1] N ints              ping-pong row-index buffers (stable partition)
 //   idx[2]   bag list            root rows when bagging
+//   idx[3/4] N ints              frontier engine: depth-indexed buffers 2 and 3
 //
-// Growth of one tree is a FIXED kernel sequence (no host round trips):
-//   init, root_sums, hist(root), scan(root),
-//   repeat num_leaves-1 times:
-//     select   best leaf (argmax over leaves of the per-leaf best split)
-//     p_count  per-4096-row-tile left counts of the parent range
-//     p_scan   exclusive scan of tile counts
-//     p_scatter  stable partition of row indices into the other buffer
-//     post     leaf bookkeeping: ranges, sums, depth, monotone bounds,
-//              smaller/larger child, histogram-slot handoff, min_data/max_depth
-//     hist     LDS-privatised histogram of the smaller child (fp32 LDS atomics,
-//              fp64 global accumulation), most-frequent bins never touched
-//     scan     one wave per feature: larger = parent - smaller (subtraction
-//              trick), mfb reconstruction, both-direction threshold scan with
-//              wave prefix sums, categorical scan, extra-trees draws
-// Every launch has a fixed grid; kernels exit early when the tree is done, so
-// the sequence is captured once into a hipGraph and replayed per tree.
-// Data-parallel training all-reduces the smaller child's histogram (and the
-// root sums) over RCCL between `hist` and `scan`; every rank then scans all
-// features redundantly, so no best-split exchange is needed.
+// Two growth engines share the data layout, the split scan (split_scan.h) and the
+// tree-building / score-update tail:
+//
+// FRONTIER engine (default for serial training; frontier.h, frontier_kernels.hip).
+// A tree grows in batched ROUNDS; one round is four launches:
+//   partition  stable partition of up to kFrontierKmax expansions at once (one
+//              grid, decoupled look-back over 4096-row tiles, children written to
+//              depth-indexed row buffers so a speculative expansion never
+//              overwrites rows a committed node still owns)
+//   hist       LDS fixed-point histograms of every expansion's smaller child,
+//              flushed with int64 atomics at one global scale per tree
+//   scan       larger = parent - smaller, best split of both children per feature
+//   select     one block replays sequential best-first order EXACTLY (gain desc,
+//              feature asc, leaf asc) over every computed node, commits what the
+//              replay reaches, and picks the next round's expansions: the replay's
+//              blocking leaf plus speculative candidates ranked by gain (adaptive
+//              depth alpha from the rows the previous tree wasted)
+// The result is bit-identical in structure to sequential growth; a tree takes
+// ~log2(num_leaves)+a few rounds instead of num_leaves-1 split steps. The rounds
+// are captured into hipGraphs (main graph for the predicted round count plus a
+// 4-round continuation graph replayed until the tree is done).
+//
+// SEQUENTIAL engine (data/voting-parallel, bynode sampling, extra-trees, the
+// global-scan path for very wide bins): a FIXED kernel sequence per split:
+//   select     best leaf (argmax over leaves of the per-leaf best split)
+//   p_count / p_scan / p_scatter   stable partition of the parent range
+//   post       leaf bookkeeping: ranges, sums, depth, monotone bounds, smaller /
+//              larger child, histogram-slot handoff, min_data / max_depth
+//   hist       LDS-privatised histogram of the smaller child
+//   scan       one wave per feature: subtraction trick, mfb reconstruction,
+//              both-direction threshold scans, categorical scan, extra-trees draws
+// Every launch has a fixed grid and exits early when the tree is done, so the
+// sequence is captured once into a hipGraph and replayed per tree. Data-parallel
+// training all-reduces the smaller child's histogram (and the root sums) over
+// RCCL between `hist` and `scan`; every rank then scans all features redundantly.
+//
+// After either engine: leaf outputs / renew (leaf_kernels.hip), then the score
+// update walks the new tree in group-bin space (traverse_kernels.hip).
 //
 // Reference parity: serial_tree_learner.cpp:170-680 (growth loop, smaller /
 // larger handling, BeforeFindBestSplit), feature_histogram.hpp:830-1057
@@ -257,8 +277,9 @@ __global__ __launch_bounds__(256) void k_qmax(const float2* gh, int n, unsigned*
   }
 }
 
-__global__ __launch_bounds__(256) void k_quantize(float2* gh, float2* gh_true, int n, const unsigned* qmax, int bins,
-                                                  int const_hess, uint32_t seed, int stochastic) {
+// ghq (frontier engine, hist MODE 2): the same levels as int8 g << 8 | uint8 h
+__global__ __launch_bounds__(256) void k_quantize(float2* gh, float2* gh_true, uint16_t* ghq, int n, const unsigned* qmax,
+                                                  int bins, int const_hess, uint32_t seed, int stochastic) {
   const double mg = __uint_as_float(qmax[0]), mh = __uint_as_float(qmax[1]);
   const double gs = mg / (bins / 2), hs = const_hess ? mh : mh / bins;
   const double ig = gs > 0 ? 1.0 / gs : 0.0, ih = hs > 0 ? 1.0 / hs : 0.0;
@@ -269,10 +290,13 @@ __global__ __launch_bounds__(256) void k_quantize(float2* gh, float2* gh_true, i
     const double rh = stochastic ? HashUniform(seed, 2u * i + 1u) : 0.5;
     const double x = v.x * ig;
     const int q = static_cast<int>(v.x >= 0.f ? x + rg : x - rg);  // truncation toward zero
+    const int qh = const_hess ? 1 : static_cast<int>(v.y * ih + rh);
     float2 o;
     o.x = static_cast<float>(q * gs);
-    o.y = const_hess ? static_cast<float>(hs) : static_cast<float>(static_cast<int>(v.y * ih + rh) * hs);
+    o.y = static_cast<float>(qh * hs);
     gh[i] = o;
+    if (ghq) ghq[i] = static_cast<uint16_t>((static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(q))) << 8) |
+                                            static_cast<uint32_t>(qh & 0xFF));
   }
 }
 
@@ -3434,8 +3458,9 @@ class DeviceTreeLearner : public TreeLearner {
     a.tile_pub = ftile_pub_.get();
     a.bar = bar_.get();
     a.hist_min_rows = HistMinRows();
-    a.hist_grid = HistBlocks();
+    a.hist_grid = FrontierHistBlocks();
     a.hist_threads = fhist_threads_;
+    a.debug_noflush = std::getenv("LGAP_DEBUG_NOFLUSH") != nullptr ? 1 : 0;
     a.part_tile = fpart_tile_;
     a.max_depth = config_->max_depth;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
@@ -3443,6 +3468,17 @@ class DeviceTreeLearner : public TreeLearner {
     a.max_bin = max_bin_;
     a.cat_p2 = cat_p2_;
     a.use_dp = use_dp_ ? 1 : 0;
+    a.ghq = ghq_.get();
+    a.qmax = qmax_.get();
+    a.quant = QuantHist() && ghq_.size() >= static_cast<size_t>(K_) * N_ ? 1 : 0;
+    a.qbins = std::max(2, config_->num_grad_quant_bins);
+    a.qconst = is_const_hess_ ? 1 : 0;
+    {
+      // one packed g32|h32 word per bin when no expansion's level sums can leave 32 bits
+      const double rows = static_cast<double>(N_);
+      const double gl = a.qbins / 2, hl = a.qconst ? 1 : a.qbins;
+      a.qpack = rows * gl < 2147483647.0 && rows * hl < 4294967295.0 ? 1 : 0;
+    }
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
@@ -3648,7 +3684,10 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   std::string DeviceName() const override {
-    if (!owner_scan_ && !voting_) return device_name_;
+    if (!owner_scan_ && !voting_) {
+      if (!FrontierEligible()) return device_name_;
+      return device_name_ + (QuantHist() ? " [frontier engine, int8-level histograms]" : " [frontier engine]");
+    }
     return device_name_ + " [" + ParallelDesc() + "]";
   }
 
@@ -3732,10 +3771,25 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipMemcpyAsync(qmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
     }
     const uint32_t seed = static_cast<uint32_t>(config_->seed) * 0x9E3779B9u + (quant_round_++);
-    k_quantize<<<grid, 256, 0, stream_>>>(gh, renew ? gh_true_.get() : nullptr, N_, qmax_.get(),
+    uint16_t* ghq = nullptr;
+    if (QuantHist()) {
+      if (ghq_.size() < static_cast<size_t>(K_) * N_) {
+        ghq_.Resize(static_cast<size_t>(K_) * N_);
+        InvalidateGraph();  // captured frontier rounds hold the buffer's address
+      }
+      ghq = ghq_.get() + static_cast<size_t>(class_id) * N_;
+    }
+    k_quantize<<<grid, 256, 0, stream_>>>(gh, renew ? gh_true_.get() : nullptr, ghq, N_, qmax_.get(),
                                           std::max(2, config_->num_grad_quant_bins), is_const_hess_ ? 1 : 0, seed,
                                           config_->stochastic_rounding ? 1 : 0);
     HIP_CHECK(hipGetLastError());
+  }
+
+  // Integer-level histograms for quantized training (frontier hist MODE 2): int8 g and
+  // uint8 h levels, i.e. num_grad_quant_bins <= 254.
+  bool QuantHist() const {
+    return config_->use_quantized_grad && std::max(2, config_->num_grad_quant_bins) <= 254 &&
+           std::getenv("LGAP_QUANT_HIST") == nullptr;  // LGAP_QUANT_HIST=off: A/B against float histograms
   }
 
   void RenewQuantizedLeaves(Tree* tree) {
@@ -3885,6 +3939,14 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t row_bytes = 2 * static_cast<size_t>(TB_) * (use_dp_ ? 8 : 4);
     const int mem_cap = static_cast<int>(std::max<size_t>(1, (size_t(4) << 30) / std::max<size_t>(row_bytes, 1)));
     return std::max(1, std::min({want, DivUp(N_, HistMinRows()), mem_cap}));
+  }
+
+  // Frontier histogram grid: every working block on its own CU (k_f_hist caps the chunk
+  // count at the grid), 7/8 of the CUs: A/B at 10M rows 224 blocks 363 it/s, 192: 361,
+  // 256: 355, 384: 346, 512: 327 (the per-block flush of a full LDS tile is the fixed cost)
+  int FrontierHistBlocks() const {
+    if (config_->device_hist_blocks > 0 || std::getenv("LGAP_HIST_BLOCKS") != nullptr) return HistBlocks();
+    return std::max(1, HistBlocks() * 7 / 8);
   }
 
   void LaunchHist(const Args& a, bool collective = true) {
@@ -4710,6 +4772,7 @@ class DeviceTreeLearner : public TreeLearner {
   int part_iters_ = 8;    // rows per thread of the fused partition (PartIters())
   const Tree* last_trained_ = nullptr;  // DeviceTrain's tree: its leaf ranges are still on the device
   DevBuf<float2> gh_true_;
+  DevBuf<uint16_t> ghq_;  // quantized levels for the frontier's integer histograms
   bool use_ic_ = false, is_const_hess_ = false;
   unsigned quant_round_ = 0;
   DevBuf<unsigned> rng_;

@@ -139,6 +139,12 @@ struct FArgs {
   double* slots;              // [C][2 TB] per-node histograms (stored bins, fp64)
   unsigned long long* acc;    // [kmax][2 TB] per-expansion fixed-point accumulators (zero between rounds)
   const unsigned* ghmax;      // float bits of max|g|, max|h| over the root rows
+  // quantized training (use_quantized_grad): per-row int8 levels, integer histograms
+  const uint16_t* ghq;        // class-major: (g level int8) << 8 | (h level uint8)
+  const unsigned* qmax;       // float bits of the quantizer's max|g|, max|h| (k_qmax)
+  int quant;                  // 1: integer-level histograms (hist MODE 2)
+  int qpack;                  // 1: one packed g32|h32 word per bin in the accumulator
+  int qbins, qconst;          // num_grad_quant_bins, constant hessian
   // candidates of the current round: [kmax][2][F]
   SplitKey* ckey;
   SplitInfo* cinfo;
@@ -147,6 +153,7 @@ struct FArgs {
   unsigned* bar;  // bar[2]: bounded-wait error flag
   int hist_min_rows, hist_grid;
   int hist_threads;  // 512 or 1024 threads per histogram block
+  int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int part_tile;  // rows per partition tile (256 x rows per thread)
   int max_depth, use_monotone;
   double monotone_penalty;

@@ -3,7 +3,7 @@
 // Launch shapes (fixed per learner; the work of a round is read on the device):
 //   k_f_init        1 x 256
 //   k_f_partition   resident grid x 256 (decoupled look-back needs co-residency)
-//   k_f_hist        (hist_grid + kmax) x LDS tiles, 512 threads
+//   k_f_hist        max(hist_grid, kmax) x LDS tiles, 512 threads
 //   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature))
 //   k_f_select      1 x 1024
 #include <hip/hip_runtime.h>
@@ -64,6 +64,14 @@ __device__ __forceinline__ void GlobalScaleExp(const FArgs& a, int* eg, int* eh)
   constexpr double k62 = 4611686018427387904.0;
   *eg = gmax > 0.f ? Pow2Exp(k62 / (n * gmax)) : 0;
   *eh = hmax > 0.f ? Pow2Exp(k62 / (n * hmax)) : 0;
+}
+
+// Quantized training: the value of one g / h level (must match k_quantize in
+// device_learner.hip, which stores float(level * scale) in gh for everything else).
+__device__ __forceinline__ void QuantScales(const FArgs& a, double* gs, double* hs) {
+  const double mg = __uint_as_float(a.qmax[0]), mh = __uint_as_float(a.qmax[1]);
+  *gs = mg / (a.qbins / 2);
+  *hs = a.qconst ? mh : mh / a.qbins;
 }
 
 // ---------------------------------------------------------------------------
@@ -135,6 +143,11 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
 //           low 32 bits, at a per-block power-of-two scale (2^30 / (block rows * max));
 //           the flush shifts each block sum up to the global scale (an exact shift);
 //   MODE 1  (gpu_use_dp) two ds_add_u64 per (row, group) at the global scale itself.
+//   MODE 2  (use_quantized_grad) the row's int8 g / uint8 h levels (2 bytes per row instead
+//           of 8) packed g32|h32 into one ds_add_u64; integer sums need no scale, and the
+//           flush adds each bin as ONE packed 64-bit word when the whole expansion's sums
+//           fit 32 bits (qpack: root rows x max level < 2^31), halving the global atomics.
+//           Reference: cuda_histogram_constructor.cu:251-450 (int16 / int32 packed bins).
 // Zero bins are skipped by the flush (most of a small leaf's histogram).
 template <int W, int MODE>
 __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
@@ -153,6 +166,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
 #pragma unroll
   for (int k = 0; k < per; ++k) go[k] = gfirst + k < tile.g1 ? gst[gfirst + k - tile.g0] : -1;
   const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
+  const uint16_t* ghq = MODE == 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
   const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
   const int base = buf < 0 ? start : 0;
   for (int p0 = rb + myr; p0 < re; p0 += rpi * R) {
@@ -164,15 +178,20 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
     }
     uint32_t word[R];
     float2 v[R];
+    uint32_t q[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
-      v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
+      if (MODE == 2) q[j] = rows[j] >= 0 ? ghq[rows[j]] : 0u;
+      else v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       unsigned long long pg, ph = 0ull;
-      if (MODE == 0) {
+      if (MODE == 2) {
+        const long long ig = static_cast<int8_t>(q[j] >> 8);
+        pg = (static_cast<unsigned long long>(ig) << 32) + (q[j] & 0xFFu);
+      } else if (MODE == 0) {
         const long long ig = __float2int_rn(v[j].x * sg);
         const long long ih = __float2int_rn(v[j].y * sh);
         pg = (static_cast<unsigned long long>(ig) << 32) + static_cast<unsigned long long>(ih);
@@ -185,7 +204,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
         const uint32_t b = W == 1 ? ((word[j] >> (8 * k)) & 0xFFu) : ((word[j] >> (16 * k)) & 0xFFFFu);
         if (b != 0u && go[k] >= 0) {
           const int o = go[k] + static_cast<int>(b);
-          if (MODE == 0) {
+          if (MODE != 1) {
             atomicAdd(&hist[o], pg);
           } else {
             atomicAdd(&hist[2 * o], pg);
@@ -219,8 +238,13 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         hs = x.h_start;
       }
     }
+    // sum over e of ceil(cnt_e / c) <= total / c + ke <= gridDim.x: every working block gets a
+    // CU of its own (a grid above the CU count doubles some CUs' work and the round waits on
+    // them: A/B at 10M, 256 + k blocks 330 it/s vs 192 + k blocks 363 it/s)
     const int total = WaveSum(cnt);
-    const int c = max(a.hist_min_rows, (total + a.hist_grid - 1) / max(1, a.hist_grid));
+    const int ke = WaveSum(cnt > 0 ? 1 : 0);
+    const int slots = max(1, static_cast<int>(gridDim.x) - ke);
+    const int c = max(a.hist_min_rows, (total + slots - 1) / slots);
     const int nb = (cnt + c - 1) / c;
     const int inc = WaveInclusiveScan(nb);
     const int bx = static_cast<int>(blockIdx.x);
@@ -261,17 +285,25 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     for (int p = rb + myr; p < re; p += rpi) {
       const int row = FRowAt(a, buf, start + p);
       const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
-      const float2 v = gh[row];
-      const unsigned long long qg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.x) * dsg));
-      const unsigned long long qh = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.y) * dsh));
+      unsigned long long qg, qh;
+      if (MODE == 2) {
+        const uint32_t qv = a.ghq[static_cast<size_t>(a.tp->cls) * a.N + row];
+        qg = static_cast<unsigned long long>(static_cast<long long>(static_cast<int8_t>(qv >> 8)));
+        qh = qv & 0xFFu;
+        if (a.qpack) qg = (qg << 32) + qh, qh = 0ull;
+      } else {
+        const float2 v = gh[row];
+        qg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.x) * dsg));
+        qh = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.y) * dsh));
+      }
 #pragma unroll
       for (int kk = 0; kk < per; ++kk) {
         const uint32_t b = W == 1 ? ((word >> (8 * kk)) & 0xFFu) : ((word >> (16 * kk)) & 0xFFFFu);
         const int g = dw * per + kk;
         if (b != 0u && g < tile.g1) {
           const int o = gst[g - tile.g0] + static_cast<int>(b);
-          atomicAdd(&acc[2 * o], qg);
-          atomicAdd(&acc[2 * o + 1], qh);
+          if (qg) atomicAdd(&acc[2 * o], qg);
+          if (qh) atomicAdd(&acc[2 * o + 1], qh);
         }
       }
     }
@@ -283,7 +315,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   const int bg = gmax > 0.f ? Pow2Exp(k30 / (rows_in_block * gmax)) : 0;
   const int bh = hmax > 0.f ? Pow2Exp(k30 / (rows_in_block * hmax)) : 0;
   const float sg = ldexpf(1.f, bg), sh = ldexpf(1.f, bh);
-  const int words = MODE == 0 ? tile.nbins : 2 * tile.nbins;
+  const int words = MODE != 1 ? tile.nbins : 2 * tile.nbins;
   unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
   int* gst = reinterpret_cast<int*>(hist + words);
   for (int i = t; i < words; i += blockDim.x) hist[i] = 0ull;
@@ -294,6 +326,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   __syncthreads();
   FStamp(a, rnd, kFStampHist, 2);
   unsigned long long* out = acc + 2 * static_cast<size_t>(tile.bin0);
+  if (a.debug_noflush) return;  // timing diagnostics only (LGAP_DEBUG_NOFLUSH): results are wrong
   if (MODE == 0) {
     // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
     // GlobalScaleExp; the guard keeps a degenerate max of 0 harmless)
@@ -307,6 +340,20 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       const long long qh = static_cast<long long>(hs) * (1ll << shh);
       if (qg) atomicAdd(&out[2 * i], static_cast<unsigned long long>(qg));
       if (qh) atomicAdd(&out[2 * i + 1], static_cast<unsigned long long>(qh));
+    }
+  } else if (MODE == 2) {
+    const bool pack = a.qpack != 0;
+    for (int i = t; i < tile.nbins; i += blockDim.x) {
+      const unsigned long long x = hist[i];
+      if (x == 0ull) continue;
+      if (pack) {
+        atomicAdd(&out[2 * i], x);
+      } else {
+        const unsigned long long hs = x & 0xFFFFFFFFull;
+        const long long gs = static_cast<long long>(x - hs) >> 32;
+        if (gs) atomicAdd(&out[2 * i], static_cast<unsigned long long>(gs));
+        if (hs) atomicAdd(&out[2 * i + 1], hs);
+      }
     }
   } else {
     for (int i = t; i < 2 * tile.nbins; i += blockDim.x) {
@@ -340,7 +387,9 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
-  const double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
+  double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
+  if (a.quant) QuantScales(a, &inv_g, &inv_h);
+  const bool qpack = a.quant && a.qpack;
   const size_t TB2 = 2 * static_cast<size_t>(a.TB);
   double* hs_full = reinterpret_cast<double*>(smem);
   double* hl_full = hs_full + 2 * a.max_bin;
@@ -353,7 +402,6 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     const int cs = xr.smaller, cl = xr.larger, p = xr.parent;
     const DevFeature fi = a.feat[f];
     const int nbin = fi.num_bin;
-    const int nv = 2 * (nbin - 1);
     const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
     unsigned long long* acc = a.acc + static_cast<size_t>(e) * TB2 + v0;
     const double* gp = (p >= 0 && cl >= 0) ? a.slots + static_cast<size_t>(p) * TB2 + v0 : nullptr;
@@ -376,18 +424,29 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       s_skip = !a.used_bytree[f];
       s_splp = p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
-    for (int v = t; v < nv; v += blockDim.x) {
-      const long long q = static_cast<long long>(acc[v]);
-      acc[v] = 0ull;
-      const double sv = static_cast<double>(q) * ((v & 1) ? inv_h : inv_g);
-      const int kk = v >> 1;
+    for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
+      const unsigned long long x0 = acc[2 * kk], x1 = acc[2 * kk + 1];
+      acc[2 * kk] = 0ull;
+      acc[2 * kk + 1] = 0ull;
+      long long q0 = static_cast<long long>(x0), q1 = static_cast<long long>(x1);
+      if (qpack) {
+        // packed g32|h32 in the even word (the odd word stays zero)
+        const unsigned long long hs = x0 & 0xFFFFFFFFull;
+        q0 = static_cast<long long>(x0 - hs) >> 32;
+        q1 = static_cast<long long>(hs);
+      }
+      const double sv0 = static_cast<double>(q0) * inv_g, sv1 = static_cast<double>(q1) * inv_h;
       const int b = kk < fi.mfb ? kk : kk + 1;
-      hs_full[2 * b + (v & 1)] = sv;
-      gs[v] = sv;
+      hs_full[2 * b] = sv0;
+      hs_full[2 * b + 1] = sv1;
+      gs[2 * kk] = sv0;
+      gs[2 * kk + 1] = sv1;
       if (gl) {
-        const double lv = gp[v] - sv;
-        hl_full[2 * b + (v & 1)] = lv;
-        gl[v] = lv;
+        const double l0 = gp[2 * kk] - sv0, l1 = gp[2 * kk + 1] - sv1;
+        hl_full[2 * b] = l0;
+        hl_full[2 * b + 1] = l1;
+        gl[2 * kk] = l0;
+        gl[2 * kk + 1] = l1;
       }
     }
     if (t < 2) {
@@ -1401,8 +1460,11 @@ void LaunchFrontierInit(const FArgs& a, hipStream_t s) {
 
 template <int THREADS>
 void LaunchHistT(const FArgs& a, size_t lds, hipStream_t s) {
-  const dim3 grid(a.hist_grid + a.kmax, a.num_tiles);
-  if (a.use_dp) {
+  const dim3 grid(std::max(a.hist_grid, a.kmax), a.num_tiles);
+  if (a.quant) {
+    if (a.width == 1) k_f_hist<1, 2, THREADS><<<grid, THREADS, lds, s>>>(a);
+    else k_f_hist<2, 2, THREADS><<<grid, THREADS, lds, s>>>(a);
+  } else if (a.use_dp) {
     if (a.width == 1) k_f_hist<1, 1, THREADS><<<grid, THREADS, lds, s>>>(a);
     else k_f_hist<2, 1, THREADS><<<grid, THREADS, lds, s>>>(a);
   } else {
@@ -1451,13 +1513,16 @@ int FrontierPartitionBlocksPerCU(int iters) {
 }
 
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
+  (void)use_dp;
+  (void)width;
   if (hist_lds > 64 * 1024) {
-    const void* fns[8] = {reinterpret_cast<const void*>(k_f_hist<1, 1, 512>), reinterpret_cast<const void*>(k_f_hist<2, 1, 512>),
-                          reinterpret_cast<const void*>(k_f_hist<1, 0, 512>), reinterpret_cast<const void*>(k_f_hist<2, 0, 512>),
-                          reinterpret_cast<const void*>(k_f_hist<1, 1, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 1, 1024>),
-                          reinterpret_cast<const void*>(k_f_hist<1, 0, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 0, 1024>)};
-    (void)use_dp;
-    (void)width;
+    const void* fns[12] = {
+        reinterpret_cast<const void*>(k_f_hist<1, 0, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 0, 512>),
+        reinterpret_cast<const void*>(k_f_hist<1, 1, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 1, 512>),
+        reinterpret_cast<const void*>(k_f_hist<1, 2, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 2, 512>),
+        reinterpret_cast<const void*>(k_f_hist<1, 0, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 0, 1024>),
+        reinterpret_cast<const void*>(k_f_hist<1, 1, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 1, 1024>),
+        reinterpret_cast<const void*>(k_f_hist<1, 2, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 2, 1024>)};
     for (const void* fn : fns) {
       HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds)));
     }

@@ -406,6 +406,29 @@ def test_device_quantized_training(lgb, gpu_required, rng, renew):
     assert (tc["split_feature"], tc["threshold"]) == (tg["split_feature"], tg["threshold"])
 
 
+@pytest.mark.parametrize("bins", [4, 16])
+def test_device_quantized_integer_histograms(lgb, gpu_required, rng, bins, monkeypatch):
+    """Quantized training on the frontier engine builds integer-level histograms (int8 g /
+    uint8 h per row, packed g32|h32 sums): with deterministic rounding the whole first tree
+    matches the host quantized learner, and the model matches the float-histogram path
+    (LGAP_QUANT_HIST=off) in accuracy."""
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    d = {"use_quantized_grad": True, "num_grad_quant_bins": bins, "stochastic_rounding": False}
+    tc = _trees(_train(lgb, X, y, "cpu", rounds=1, **d))[0]["tree_structure"]
+    bg = _train(lgb, X, y, "gpu", rounds=1, **d)
+    assert "frontier" in bg.device_name()
+    tg = _trees(bg)[0]["tree_structure"]
+    assert [s[:2] for s in _splits(tc, [])] == [s[:2] for s in _splits(tg, [])]
+    q = {"use_quantized_grad": True, "num_grad_quant_bins": bins}
+    a_int = _auc(y, _train(lgb, X, y, "gpu", rounds=30, **q).predict(X))
+    a_cpu = _auc(y, _train(lgb, X, y, "cpu", rounds=30, **q).predict(X))
+    monkeypatch.setenv("LGAP_QUANT_HIST", "off")
+    a_flt = _auc(y, _train(lgb, X, y, "gpu", rounds=30, **q).predict(X))
+    assert abs(a_int - a_cpu) < 5e-3, (a_int, a_cpu)
+    assert abs(a_int - a_flt) < 5e-3, (a_int, a_flt)
+
+
 @pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05, "cegb_penalty_feature_coupled": [1, 2, 3, 4, 5, 6]},
                                    {"monotone_constraints": [1, -1, 0, 0, 0, 0],
                                     "monotone_constraints_method": "intermediate"},
@@ -706,6 +729,7 @@ def test_frontier_engine_matches_sequential_chain(lgb, gpu_required, rng, extra)
     def structure(model):
         return [ln for ln in model.splitlines() if ln.startswith(("split_feature=", "threshold=", "left_child=",
                                                                    "right_child=", "decision_type=", "num_leaves="))]
+    assert "frontier engine" in outs[0]["name"] and "frontier" not in outs[1]["name"], outs[0]["name"]
     assert structure(outs[0]["model"]) == structure(outs[1]["model"])
 
 
