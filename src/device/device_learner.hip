@@ -3387,12 +3387,12 @@ class DeviceTreeLearner : public TreeLearner {
     per_cu = std::max(1, std::min(cap, per_cu - 1));
     fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
     fscan_lds_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + static_cast<size_t>(cat_p2_) * 2 * (sizeof(int) + sizeof(double));
-    FrontierSetLds(hist_lds_bytes_, fscan_lds_, use_dp_, width_);
+    FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
     // 512 (default) / 1024 threads per histogram block: 1024 measured 322.9 vs 331.0 it/s at 10M
     // (a longer tail: blocks finish further apart), 621 vs 738 at 1.25M
-    fhist_threads_ = 512;
+    fhist_threads_ = big_tiles_ ? 1024 : 512;  // one resident block per CU with 150 KB tiles
     if (const char* e = std::getenv("LGAP_FHIST_THREADS")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
     fpolicy_ = 1;
     if (const char* e = std::getenv("LGAP_FRONTIER_POLICY")) fpolicy_ = std::atoi(e) == 0 ? 0 : 1;
@@ -3478,6 +3478,13 @@ class DeviceTreeLearner : public TreeLearner {
       const double rows = static_cast<double>(N_);
       const double gl = a.qbins / 2, hl = a.qconst ? 1 : a.qbins;
       a.qpack = rows * gl < 2147483647.0 && rows * hl < 4294967295.0 ? 1 : 0;
+      // g16|h16 LDS bins: a sub-chunk's per-bin level sums stay within the 16-bit fields
+      const int sub = static_cast<int>(std::min(32767.0 / gl, 65535.0 / hl));
+      const char* e = std::getenv("LGAP_QUANT_LDS32");  // A/B knob: 0 keeps the 64-bit LDS bins
+      // single-tile data only: the 1.5x LDS would drop multi-tile grids (several blocks per
+      // CU) to one resident block (A/B, 12.5M x 500 GOSS: 87.7 it/s with 64-bit bins, 80.0)
+      const bool want = e != nullptr ? e[0] != '0' : num_tiles_ == 1;
+      a.qsub = a.quant && !use_dp_ && sub >= 2048 && want ? sub : 0;
     }
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
@@ -3490,7 +3497,7 @@ class DeviceTreeLearner : public TreeLearner {
   // One round: partition -> histograms -> scans -> select.
   void EnqueueFrontierRound(const FArgs& fa) {
     LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
-    LaunchFrontierHist(fa, hist_lds_bytes_, stream_);
+    LaunchFrontierHist(fa, FrontierHistLds(), stream_);
     LaunchFrontierScan(fa, fscan_lds_, stream_);
     LaunchFrontierSelect(fa, stream_);
   }
@@ -3507,7 +3514,7 @@ class DeviceTreeLearner : public TreeLearner {
       k_root_sums<<<root_blocks, kRootThreads, 0, stream_>>>(ra);
       k_root_final<<<1, kRootThreads, 0, stream_>>>(ra, root_blocks);
       HIP_CHECK(hipGetLastError());
-      LaunchFrontierHist(fa, hist_lds_bytes_, stream_);
+      LaunchFrontierHist(fa, FrontierHistLds(), stream_);
       LaunchFrontierScan(fa, fscan_lds_, stream_);
       LaunchFrontierSelect(fa, stream_);
     }
@@ -3785,6 +3792,11 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipGetLastError());
   }
 
+  // the frontier histogram's dynamic LDS: the tile plan's, plus the 32-bit bins of hist MODE 3
+  size_t FrontierHistLds() const {
+    return use_dp_ || !QuantHist() || MakeFArgs().qsub == 0 ? hist_lds_bytes_ : hist_lds_bytes_ * 3 / 2 + 64;
+  }
+
   // Integer-level histograms for quantized training (frontier hist MODE 2): int8 g and
   // uint8 h levels, i.e. num_grad_quant_bins <= 254.
   bool QuantHist() const {
@@ -3946,6 +3958,8 @@ class DeviceTreeLearner : public TreeLearner {
   // 256: 355, 384: 346, 512: 327 (the per-block flush of a full LDS tile is the fixed cost)
   int FrontierHistBlocks() const {
     if (config_->device_hist_blocks > 0 || std::getenv("LGAP_HIST_BLOCKS") != nullptr) return HistBlocks();
+    // several LDS tiles: the grid is row blocks x tiles, ~2 blocks per CU in all
+    if (num_tiles_ > 1) return HistBlocks();
     return std::max(1, HistBlocks() * 7 / 8);
   }
 
@@ -4135,9 +4149,27 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void BuildTiles() {
+    static const int env_kb = [] {
+      const char* e = std::getenv("LGAP_HIST_LDS_KB");  // A/B knob: LDS tile budget
+      return e ? std::max(16, std::min(150, std::atoi(e))) : 0;
+    }();
+    big_tiles_ = false;
+    PlanTiles(env_kb > 0 ? env_kb * 1024 : kHistLdsBytes);
+    // Wide rows split into narrow tiles (< 16 dwords = 64 B of a row per pass) re-gather a
+    // partial cache line of every row once per tile: serial training then plans tiles for one
+    // 150 KB block per CU (1024 threads in the frontier). A/B, LambdaRank 5M x 300 (255 bins,
+    // 11 tiles of 7 dwords at 56 KB): 79.8 -> 92.2 it/s; GOSS 12.5M x 500 (63 bins, 5 tiles
+    // of 28 dwords) keeps 56 KB (150 KB measured 76.8 -> 61.8).
+    if (env_kb == 0 && mode_ == DevParallel::kSerial && num_tiles_ > 1 && min_tile_dw_ < 16) {
+      big_tiles_ = true;
+      PlanTiles(150 * 1024);
+    }
+  }
+
+  void PlanTiles(int lds_budget) {
     const int per = 4 / width_;
     const size_t acc = use_dp_ ? 16 : 8;  // LDS bytes per bin (grad + hess)
-    const int max_bins = static_cast<int>(kHistLdsBytes / acc) - 64;
+    const int max_bins = static_cast<int>(lds_budget / acc) - 64;
     const int max_dw = kHistThreads / 2;
     std::vector<HistTile> tiles;
     hist_lds_bytes_ = 16;
@@ -4178,6 +4210,8 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
     }
     num_tiles_ = static_cast<int>(tiles.size());
+    min_tile_dw_ = 1 << 30;
+    for (size_t i = 0; i + 1 < tiles.size(); ++i) min_tile_dw_ = std::min(min_tile_dw_, tiles[i].d1 - tiles[i].d0);
     h_tiles_ = tiles;
   }
 
@@ -4650,6 +4684,8 @@ class DeviceTreeLearner : public TreeLearner {
   // frontier engine (frontier.h)
   bool frontier_ = false;
   int fhist_threads_ = 512;
+  bool big_tiles_ = false;  // BuildTiles chose 150 KB LDS tiles (wide rows)
+  int min_tile_dw_ = 0;
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;

@@ -145,6 +145,7 @@ struct FArgs {
   int quant;                  // 1: integer-level histograms (hist MODE 2)
   int qpack;                  // 1: one packed g32|h32 word per bin in the accumulator
   int qbins, qconst;          // num_grad_quant_bins, constant hessian
+  int qsub;                   // > 0: 32-bit g16|h16 LDS bins (hist MODE 3), folded every qsub rows
   // candidates of the current round: [kmax][2][F]
   SplitKey* ckey;
   SplitInfo* cinfo;

@@ -3,7 +3,7 @@
 // Launch shapes (fixed per learner; the work of a round is read on the device):
 //   k_f_init        1 x 256
 //   k_f_partition   resident grid x 256 (decoupled look-back needs co-residency)
-//   k_f_hist        max(hist_grid, kmax) x LDS tiles, 512 threads
+//   k_f_hist        max(hist_grid, ceil(hist_grid / 2) + kmax) x LDS tiles, 512 threads
 //   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature))
 //   k_f_select      1 x 1024
 #include <hip/hip_runtime.h>
@@ -148,11 +148,15 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
 //           flush adds each bin as ONE packed 64-bit word when the whole expansion's sums
 //           fit 32 bits (qpack: root rows x max level < 2^31), halving the global atomics.
 //           Reference: cuda_histogram_constructor.cu:251-450 (int16 / int32 packed bins).
+//   MODE 3  MODE 2 with 32-bit LDS atomics: g16|h16 packed into one ds_add_u32 per (row,
+//           group); the block walks its rows in sub-chunks small enough that no 16-bit
+//           field can overflow (a.qsub rows) and folds the narrow bins into the 64-bit
+//           LDS histogram after each one.
 // Zero bins are skipped by the flush (most of a small leaf's histogram).
 template <int W, int MODE>
 __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
                                           const int* gst, unsigned long long* hist, float sg, float sh, double dsg,
-                                          double dsh) {
+                                          double dsh, uint32_t* hist32 = nullptr) {
   const int tpr = tile.d1 - tile.d0;
   const int rpi = blockDim.x / tpr;
   const int myr = threadIdx.x / tpr;
@@ -166,7 +170,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
 #pragma unroll
   for (int k = 0; k < per; ++k) go[k] = gfirst + k < tile.g1 ? gst[gfirst + k - tile.g0] : -1;
   const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
-  const uint16_t* ghq = MODE == 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
+  const uint16_t* ghq = MODE >= 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
   const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
   const int base = buf < 0 ? start : 0;
   for (int p0 = rb + myr; p0 < re; p0 += rpi * R) {
@@ -182,13 +186,16 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
-      if (MODE == 2) q[j] = rows[j] >= 0 ? ghq[rows[j]] : 0u;
+      if (MODE >= 2) q[j] = rows[j] >= 0 ? ghq[rows[j]] : 0u;
       else v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      unsigned long long pg, ph = 0ull;
-      if (MODE == 2) {
+      unsigned long long pg = 0ull, ph = 0ull;
+      uint32_t p32 = 0u;
+      if (MODE == 3) {
+        p32 = (static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(q[j] >> 8))) << 16) + (q[j] & 0xFFu);
+      } else if (MODE == 2) {
         const long long ig = static_cast<int8_t>(q[j] >> 8);
         pg = (static_cast<unsigned long long>(ig) << 32) + (q[j] & 0xFFu);
       } else if (MODE == 0) {
@@ -204,7 +211,9 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
         const uint32_t b = W == 1 ? ((word[j] >> (8 * k)) & 0xFFu) : ((word[j] >> (16 * k)) & 0xFFFFu);
         if (b != 0u && go[k] >= 0) {
           const int o = go[k] + static_cast<int>(b);
-          if (MODE != 1) {
+          if (MODE == 3) {
+            atomicAdd(&hist32[o], p32);
+          } else if (MODE != 1) {
             atomicAdd(&hist[o], pg);
           } else {
             atomicAdd(&hist[2 * o], pg);
@@ -238,12 +247,14 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         hs = x.h_start;
       }
     }
-    // sum over e of ceil(cnt_e / c) <= total / c + ke <= gridDim.x: every working block gets a
-    // CU of its own (a grid above the CU count doubles some CUs' work and the round waits on
-    // them: A/B at 10M, 256 + k blocks 330 it/s vs 192 + k blocks 363 it/s)
+    // sum over e of ceil(cnt_e / c) <= total / c + ke <= hist_grid while ke <= hist_grid / 2:
+    // with hist_grid below the CU count every working block gets a CU of its own (256 + k
+    // blocks doubled some CUs' work and the round waited on them: A/B at 10M, 330 it/s vs
+    // 363 it/s). Many expansions over a small grid (wide data, many LDS tiles) still get
+    // >= hist_grid / 2 row-balanced chunks.
     const int total = WaveSum(cnt);
     const int ke = WaveSum(cnt > 0 ? 1 : 0);
-    const int slots = max(1, static_cast<int>(gridDim.x) - ke);
+    const int slots = max(max(1, a.hist_grid / 2), a.hist_grid - ke);
     const int c = max(a.hist_min_rows, (total + slots - 1) / slots);
     const int nb = (cnt + c - 1) / c;
     const int inc = WaveInclusiveScan(nb);
@@ -286,7 +297,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       const int row = FRowAt(a, buf, start + p);
       const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
       unsigned long long qg, qh;
-      if (MODE == 2) {
+      if (MODE >= 2) {
         const uint32_t qv = a.ghq[static_cast<size_t>(a.tp->cls) * a.N + row];
         qg = static_cast<unsigned long long>(static_cast<long long>(static_cast<int8_t>(qv >> 8)));
         qh = qv & 0xFFu;
@@ -317,13 +328,35 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   const float sg = ldexpf(1.f, bg), sh = ldexpf(1.f, bh);
   const int words = MODE != 1 ? tile.nbins : 2 * tile.nbins;
   unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
-  int* gst = reinterpret_cast<int*>(hist + words);
+  uint32_t* hist32 = reinterpret_cast<uint32_t*>(hist + words);
+  int* gst = reinterpret_cast<int*>(MODE == 3 ? reinterpret_cast<unsigned long long*>(hist32 + ((tile.nbins + 1) & ~1))
+                                              : hist + words);
   for (int i = t; i < words; i += blockDim.x) hist[i] = 0ull;
+  if (MODE == 3) {
+    for (int i = t; i < tile.nbins; i += blockDim.x) hist32[i] = 0u;
+  }
   for (int g = tile.g0 + t; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
   __syncthreads();
   FStamp(a, rnd, kFStampHist, 1);
-  FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh);
-  __syncthreads();
+  if (MODE == 3) {
+    for (int sb = rb; sb < re; sb += a.qsub) {
+      const int se = min(re, sb + a.qsub);
+      FHistRows<W, MODE>(a, tile, buf, start, sb, se, gst, hist, sg, sh, dsg, dsh, hist32);
+      __syncthreads();
+      for (int i = t; i < tile.nbins; i += blockDim.x) {
+        const uint32_t x = hist32[i];
+        if (x == 0u) continue;
+        hist32[i] = 0u;
+        const uint32_t hs = x & 0xFFFFu;
+        const long long gs = static_cast<int32_t>(x - hs) >> 16;
+        hist[i] += (static_cast<unsigned long long>(gs) << 32) + hs;
+      }
+      __syncthreads();
+    }
+  } else {
+    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh);
+    __syncthreads();
+  }
   FStamp(a, rnd, kFStampHist, 2);
   unsigned long long* out = acc + 2 * static_cast<size_t>(tile.bin0);
   if (a.debug_noflush) return;  // timing diagnostics only (LGAP_DEBUG_NOFLUSH): results are wrong
@@ -341,7 +374,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       if (qg) atomicAdd(&out[2 * i], static_cast<unsigned long long>(qg));
       if (qh) atomicAdd(&out[2 * i + 1], static_cast<unsigned long long>(qh));
     }
-  } else if (MODE == 2) {
+  } else if (MODE >= 2) {
     const bool pack = a.qpack != 0;
     for (int i = t; i < tile.nbins; i += blockDim.x) {
       const unsigned long long x = hist[i];
@@ -1460,8 +1493,12 @@ void LaunchFrontierInit(const FArgs& a, hipStream_t s) {
 
 template <int THREADS>
 void LaunchHistT(const FArgs& a, size_t lds, hipStream_t s) {
-  const dim3 grid(std::max(a.hist_grid, a.kmax), a.num_tiles);
-  if (a.quant) {
+  // working blocks <= max(hist_grid, ceil(hist_grid / 2) + ke): see the chunking in k_f_hist
+  const dim3 grid(std::max(a.hist_grid, a.hist_grid / 2 + a.hist_grid % 2 + a.kmax), a.num_tiles);
+  if (a.quant && a.qsub > 0) {
+    if (a.width == 1) k_f_hist<1, 3, THREADS><<<grid, THREADS, lds, s>>>(a);
+    else k_f_hist<2, 3, THREADS><<<grid, THREADS, lds, s>>>(a);
+  } else if (a.quant) {
     if (a.width == 1) k_f_hist<1, 2, THREADS><<<grid, THREADS, lds, s>>>(a);
     else k_f_hist<2, 2, THREADS><<<grid, THREADS, lds, s>>>(a);
   } else if (a.use_dp) {
@@ -1516,7 +1553,9 @@ void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
   (void)use_dp;
   (void)width;
   if (hist_lds > 64 * 1024) {
-    const void* fns[12] = {
+    const void* fns[16] = {
+        reinterpret_cast<const void*>(k_f_hist<1, 3, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 3, 512>),
+        reinterpret_cast<const void*>(k_f_hist<1, 3, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 3, 1024>),
         reinterpret_cast<const void*>(k_f_hist<1, 0, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 0, 512>),
         reinterpret_cast<const void*>(k_f_hist<1, 1, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 1, 512>),
         reinterpret_cast<const void*>(k_f_hist<1, 2, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 2, 512>),

@@ -429,6 +429,23 @@ def test_device_quantized_integer_histograms(lgb, gpu_required, rng, bins, monke
     assert abs(a_int - a_flt) < 5e-3, (a_int, a_flt)
 
 
+def test_device_quantized_regression_tracks_cpu(lgb, gpu_required):
+    """Integer-level histograms on a regression (non-constant range of gradients, 255 leaves):
+    the held-out l2 of the device quantized model tracks the host quantized learner's (4 levels
+    cost both the same accuracy against fp gradients)."""
+    from lambdagap_amd.utils import make_regression
+
+    X, y = make_regression(60000, num_features=40, seed=7)
+    Xv, yv = make_regression(20000, num_features=40, seed=8)
+    p = {"objective": "regression", "num_leaves": 255, "max_bin": 63, "verbosity": -1,
+         "use_quantized_grad": True, "num_grad_quant_bins": 4, "seed": 3}
+    l2 = {}
+    for dev in ("cpu", "gpu"):
+        b = lgb.train({**p, "device_type": dev}, lgb.Dataset(X, y), 30)
+        l2[dev] = float(np.mean((b.predict(Xv) - yv) ** 2))
+    assert abs(l2["gpu"] - l2["cpu"]) < 0.03 * l2["cpu"], l2
+
+
 @pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05, "cegb_penalty_feature_coupled": [1, 2, 3, 4, 5, 6]},
                                    {"monotone_constraints": [1, -1, 0, 0, 0, 0],
                                     "monotone_constraints_method": "intermediate"},
