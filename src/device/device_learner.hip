@@ -3461,6 +3461,10 @@ class DeviceTreeLearner : public TreeLearner {
     a.hist_grid = FrontierHistBlocks();
     a.hist_threads = fhist_threads_;
     a.debug_noflush = std::getenv("LGAP_DEBUG_NOFLUSH") != nullptr ? 1 : 0;
+    {
+      const char* e = std::getenv("LGAP_FLUSH_ROT");
+      a.flush_rot = e != nullptr && e[0] == '0' ? 0 : 1;
+    }
     a.part_tile = fpart_tile_;
     a.max_depth = config_->max_depth;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;

@@ -360,11 +360,15 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   FStamp(a, rnd, kFStampHist, 2);
   unsigned long long* out = acc + 2 * static_cast<size_t>(tile.bin0);
   if (a.debug_noflush) return;  // timing diagnostics only (LGAP_DEBUG_NOFLUSH): results are wrong
+  // every block starts its flush at its own offset of the tile, so the blocks' concurrent
+  // atomics hit different accumulator words instead of queueing on the same ones
+  const int rot = a.flush_rot ? static_cast<int>((static_cast<long long>(blockIdx.x) * tile.nbins) / gridDim.x) : 0;
   if (MODE == 0) {
     // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
     // GlobalScaleExp; the guard keeps a degenerate max of 0 harmless)
     const int shg = max(0, EG - bg), shh = max(0, EH - bh);
-    for (int i = t; i < tile.nbins; i += blockDim.x) {
+    for (int j = t; j < tile.nbins; j += blockDim.x) {
+      const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
       const unsigned long long x = hist[i];
       if (x == 0ull) continue;
       const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
@@ -376,7 +380,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     }
   } else if (MODE >= 2) {
     const bool pack = a.qpack != 0;
-    for (int i = t; i < tile.nbins; i += blockDim.x) {
+    for (int j = t; j < tile.nbins; j += blockDim.x) {
+      const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
       const unsigned long long x = hist[i];
       if (x == 0ull) continue;
       if (pack) {
@@ -389,7 +394,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       }
     }
   } else {
-    for (int i = t; i < 2 * tile.nbins; i += blockDim.x) {
+    for (int j = t; j < 2 * tile.nbins; j += blockDim.x) {
+      const int i = j < 2 * (tile.nbins - rot) ? j + 2 * rot : j + 2 * rot - 2 * tile.nbins;
       const unsigned long long x = hist[i];
       if (x) atomicAdd(&out[i], x);
     }
