@@ -2549,7 +2549,8 @@ class DeviceTreeLearner : public TreeLearner {
     const char* e = std::getenv("LGAP_DP_TRANSPORT");
     const std::string want = e ? e : "auto";
     if (want != "auto" && want != "xgmi" && want != "collective") Log::Fatal("LGAP_DP_TRANSPORT=%s: expected auto|xgmi|collective", want.c_str());
-    if (want == "collective" || P_ > kMaxXRanks) return;
+    // the data-parallel frontier engine exchanges through all-reduces (no owner buffers)
+    if (want == "collective" || P_ > kMaxXRanks || (frontier_ && want == "auto")) return;
     const size_t es = use_dp_ ? sizeof(double) : sizeof(float);
     ArenaLayout lay;
     x_off_hist_ = static_cast<int>(lay.Add<char>(static_cast<size_t>(P_) * 2 * bbin_ * es));
@@ -2638,6 +2639,7 @@ class DeviceTreeLearner : public TreeLearner {
     std::string m = mode_ == DevParallel::kFeature ? "feature-parallel"
                                                    : (voting_ ? "voting-parallel" : "data-parallel");
     m += ", " + std::to_string(P_) + " ranks, ";
+    if (frontier_) return m + "frontier engine, " + (HostStagedDP() ? "host-staged collectives" : "RCCL all-reduce per round");
     if (transport_ == 2) return m + "xGMI in-kernel exchange";
     if (HostStagedDP()) return m + "host-staged collectives";
     return m + "RCCL reduce-scatter/all-gather";
@@ -3322,10 +3324,30 @@ class DeviceTreeLearner : public TreeLearner {
   bool FrontierEligible() const {
     const char* e = std::getenv("LGAP_FRONTIER");
     if (e != nullptr && e[0] == '0') return false;
-    if (mode_ != DevParallel::kSerial || owner_scan_ || voting_ || distributed_) return false;
+    if (!FrontierSerial() && !FrontierDP()) return false;
     if (use_bynode_ || config_->extra_trees || scan_global_) return false;
     if (FrontierCapacity() > kFrontierMaxNodes || F_ <= 0) return false;
     return FrontierSelectLds(FrontierCapacity(), L_) <= 150 * 1024;
+  }
+  bool FrontierSerial() const {
+    return mode_ == DevParallel::kSerial && !owner_scan_ && !voting_ && !distributed_;
+  }
+  // Data-parallel frontier: every rank partitions / builds histograms of its own rows, the
+  // round's fixed-point accumulators are summed over ranks (one exact integer all-reduce per
+  // round, RCCL or the host-staged rehearsal transport), and every rank scans and selects
+  // redundantly: the select is deterministic in the summed histograms, so all ranks grow the
+  // same tree with no further exchange. Children's counts come from the summed histograms
+  // (the split record), row ranges from the local partition. LGAP_FRONTIER_DP=0: the
+  // sequential owner-scan chain instead. Reference: data_parallel_tree_learner.cpp:148-297.
+  // The exchange is an all-reduce (RCCL communicator or the host-staged rehearsal); an explicit
+  // LGAP_DP_TRANSPORT=xgmi keeps the sequential chain's in-kernel xGMI exchange.
+  bool FrontierDP() const {
+    const char* e = std::getenv("LGAP_FRONTIER_DP");
+    if (e != nullptr && e[0] == '0') return false;
+    const char* t = std::getenv("LGAP_DP_TRANSPORT");
+    if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
+    return mode_ == DevParallel::kData && data_parallel_ && owner_scan_ && distributed_ && !voting_ &&
+           (CommExists() || HostStagedDP());
   }
   int FrontierKmax() const {
     int k = kFrontierKmax;
@@ -3493,15 +3515,26 @@ class DeviceTreeLearner : public TreeLearner {
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
-    a.distributed = 0;
+    a.distributed = distributed_ ? 1 : 0;
+    if (distributed_) a.qpack = 0;  // the all-reduced level sums of every rank: keep two words per bin
     a.sp = MakeArgs().sp;
     return a;
   }
 
-  // One round: partition -> histograms -> scans -> select.
-  void EnqueueFrontierRound(const FArgs& fa) {
+  // Data-parallel frontier: sum the round's accumulators of the first `kb` expansions over
+  // the ranks (the rest are zero on every rank).
+  void FrontierExchange(int kb) {
+    if (!distributed_) return;
+    AllreduceSumU64(reinterpret_cast<unsigned long long*>(facc_.get()),
+                    static_cast<size_t>(std::max(1, std::min(kb, fkmax_))) * 2 * TB_, stream_);
+  }
+
+  // One round: partition -> histograms -> [all-reduce] -> scans -> select. `kb` bounds the
+  // round's expansion count (round r >= 1 of a tree has at most 2^(r-1) open nodes to expand).
+  void EnqueueFrontierRound(const FArgs& fa, int kb) {
     LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
     LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+    FrontierExchange(kb);
     LaunchFrontierScan(fa, fscan_lds_, stream_);
     LaunchFrontierSelect(fa, stream_);
   }
@@ -3518,11 +3551,19 @@ class DeviceTreeLearner : public TreeLearner {
       k_root_sums<<<root_blocks, kRootThreads, 0, stream_>>>(ra);
       k_root_final<<<1, kRootThreads, 0, stream_>>>(ra, root_blocks);
       HIP_CHECK(hipGetLastError());
+      if (distributed_) {
+        // global root sums and gradient maxima (the fixed-point scales must agree on all ranks)
+        AllreduceSumF64(reinterpret_cast<double*>(flsum_), 2, stream_);
+        AllreduceMaxU32(ghmax_.get(), 2, stream_);
+      }
       LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+      FrontierExchange(1);
       LaunchFrontierScan(fa, fscan_lds_, stream_);
       LaunchFrontierSelect(fa, stream_);
     }
-    for (int r = 0; r < rounds; ++r) EnqueueFrontierRound(fa);
+    for (int r = 0; r < rounds; ++r) {
+      EnqueueFrontierRound(fa, prologue && r < 7 ? (1 << r) : fkmax_);
+    }
   }
 
   hipGraphExec_t CaptureFrontier(int rounds, bool prologue) {
@@ -3539,8 +3580,21 @@ class DeviceTreeLearner : public TreeLearner {
   // Grow one tree: the root round plus a predicted number of rounds (the previous trees'
   // count) in one replay; if the tree is not finished, continuation replays of a few rounds
   // each until it is. Results: the committed splits, the final leaf ranges, the root output.
+  // a stream carrying RCCL collectives: a lost peer must not hang the process
+  void FrontierSync() {
+    if (distributed_ && !HostStagedDP()) {
+      WatchedStreamSync(stream_, CommTimeoutSeconds(config_->time_out), "frontier tree growth (RCCL all-reduce)");
+    } else {
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+  }
+
   void FrontierGrow(int* num_splits, int* num_leaves, SplitRec* hr, LeafRange* hrange, double* hlo) {
-    const bool use_graph = config_->device_use_graph;
+    // collectives: RCCL calls replay from the graph only on request (LGAP_DP_GRAPH=1, as in the
+    // sequential chain); the host-staged rehearsal transport synchronises inside its exchange
+    const bool use_graph = config_->device_use_graph && (!distributed_ || (DPGraphEnabled() && !HostStagedDP()));
+    if (use_graph && distributed_ && !fgraphs_.empty() && graph_comm_ != ActiveComm()) InvalidateGraph();
+    if (use_graph && distributed_) graph_comm_ = ActiveComm();
     const int pred = std::max(1, std::min(fpred_rounds_, L_));
     FState* hs = pin_fst_.Get(1);
     if (fgraph_gh_ != gh_.get()) {  // captured launches hold the gradient buffer's address
@@ -3558,7 +3612,7 @@ class DeviceTreeLearner : public TreeLearner {
     int launched = pred;
     for (;;) {
       HIP_CHECK(hipMemcpyAsync(hs, fst_, sizeof(FState), hipMemcpyDeviceToHost, stream_));
-      HIP_CHECK(hipStreamSynchronize(stream_));
+      FrontierSync();
       if (hs->done) break;
       if (launched > L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
       if (use_graph) {
@@ -3594,7 +3648,7 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(hlo, flout_, sizeof(double), hipMemcpyDeviceToHost, stream_));
     unsigned* hbar = pin_bar_.Get(4);
     HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    FrontierSync();
     if (hbar[2] != 0u) Log::Fatal("k_f_partition: a wait on published tile counts timed out (blocks not co-resident?)");
     if (fstamps_.size() && fstat_trees_ == 3) ReportFrontierStamps(hs->round);
     if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {

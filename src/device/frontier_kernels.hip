@@ -1464,7 +1464,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     for (int c = t; c < cid_next; c += blockDim.x) {
       const uint8_t sc = s_st[c];
       if (!(sc & kNodeExpanded)) continue;
-      const unsigned long long cnt = static_cast<unsigned long long>(a.nodes[c].count);
+      // data-parallel: the global count, so every rank steers its speculation the same way
+      const unsigned long long cnt = static_cast<unsigned long long>(a.distributed ? a.nodes[c].gcount : a.nodes[c].count);
       if (sc & kNodeCommitted) u += cnt;
       else wst += cnt;
     }

@@ -213,6 +213,25 @@ void AllreduceSumF32(float* dev_ptr, size_t count, hipStream_t stream) {
   AllreduceSum(dev_ptr, count, stream, ncclFloat32);
 }
 
+void AllreduceSumU64(unsigned long long* dev_ptr, size_t count, hipStream_t stream) {
+  AllreduceSum(dev_ptr, count, stream, ncclUint64);
+}
+
+void AllreduceMaxU32(unsigned* dev_ptr, size_t count, hipStream_t stream) {
+  if (count == 0) return;
+  if (HostStagedDP()) {
+    std::vector<unsigned> h(count);
+    HIP_CHECK(hipMemcpyAsync(h.data(), dev_ptr, count * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    for (auto& v : h) v = static_cast<unsigned>(Network::GlobalSyncUpByMax(static_cast<double>(v)));
+    HIP_CHECK(hipMemcpyAsync(dev_ptr, h.data(), count * sizeof(unsigned), hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    return;
+  }
+  if (!CommExists()) return;
+  NcclCheck(ncclAllReduce(dev_ptr, dev_ptr, count, ncclUint32, ncclMax, S().comm, stream), "ncclAllReduce(max)");
+}
+
 int DpSize() { return Network::num_machines() > 1 ? Network::num_machines() : std::max(1, S().size); }
 int DpRank() { return Network::num_machines() > 1 ? Network::rank() : S().rank; }
 

@@ -21,6 +21,10 @@ bool HostStagedDP();
 // In-place sum all-reduce of device doubles on `stream` (no-op without a communicator).
 void AllreduceSumF64(double* dev_ptr, size_t count, hipStream_t stream);
 void AllreduceSumF32(float* dev_ptr, size_t count, hipStream_t stream);
+// exact integer sums (fixed-point histograms: two's complement wraps like int64 addition)
+void AllreduceSumU64(unsigned long long* dev_ptr, size_t count, hipStream_t stream);
+// in-place max of device uint32 values (e.g. the float bits of non-negative maxima)
+void AllreduceMaxU32(unsigned* dev_ptr, size_t count, hipStream_t stream);
 // hipStreamSynchronize for streams carrying collectives: polls the communicator's
 // async error and aborts it after timeout_s (<= 0: no limit), raising a fatal error.
 void WatchedStreamSync(hipStream_t stream, double timeout_s, const char* what);

@@ -272,21 +272,25 @@ def test_data_parallel_path_single_rank(lgb, gpu_required, transport):
     assert res["max_abs_diff"] < 1e-3, res
 
 
-@pytest.mark.parametrize("world,transport", [(2, "collective"), (3, "collective"), (2, "xgmi"), (3, "xgmi"),
-                                             (4, "xgmi")])
+@pytest.mark.parametrize("world,transport", [(2, "collective"), (3, "collective"), (4, "collective"),
+                                             (2, "collective-seq"), (2, "xgmi"), (3, "xgmi"), (4, "xgmi")])
 def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
-    """P ranks share the one GPU. The device data-parallel learner exchanges owner histograms and
-    split candidates either through host-staged collectives (gloo) or through the xGMI in-kernel
-    exchange over IPC-mapped buffers (here all on one device). Every rank must grow the identical
-    model, and it must match the host data-parallel learner trained by the same ranks on the
-    same bins."""
+    """P ranks share the one GPU. "collective": the data-parallel FRONTIER engine (per-round exact
+    all-reduce of the fixed-point histograms through host-staged collectives, redundant scan and
+    select on every rank); "collective-seq": the sequential chain's owner histogram exchange over
+    the same collectives; "xgmi": the sequential chain's in-kernel exchange over IPC-mapped
+    buffers (here all on one device). Every rank must grow the identical model, and it must match
+    the host data-parallel learner trained by the same ranks on the same bins."""
     import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport.replace("-seq", ""),
+               LGAP_XGMI_TIMEOUT_S="20")
+    if transport == "collective-seq":
+        env["LGAP_FRONTIER_DP"] = "0"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
                         "--nproc-per-node", str(world), os.path.join(root, "scripts", "dp_multirank.py")],
                        capture_output=True, text=True, timeout=600, env=env, cwd=root)
@@ -295,6 +299,7 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
     assert res["world"] == world
     assert "data-parallel" in res["device_name"], res
     assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
+    assert ("frontier engine" in res["device_name"]) == (transport == "collective"), res
     assert res["ranks_identical"], res
     assert res["num_trees"] == 10
     # unit hessians (l2): the split structure must match the host learner tree for tree
