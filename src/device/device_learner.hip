@@ -260,10 +260,40 @@ __device__ __forceinline__ float HashUniform(uint32_t seed, uint32_t i) {
   return static_cast<float>(x >> 8) * (1.0f / 16777216.0f);
 }
 
+// 16-byte loads (two rows per float4), four in flight per thread, one atomic pair per block
+// (the per-wave atomics and 8-byte loads ran at ~0.75 TB/s: 106 us at 10M rows)
 __global__ __launch_bounds__(256) void k_qmax(const float2* gh, int n, unsigned* qmax) {
+  __shared__ float s_m[2][4];
   float mg = 0.f, mh = 0.f;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float2 v = gh[i];
+  if ((reinterpret_cast<uintptr_t>(gh) & 15u) != 0 && n > 0) {  // class slice at an odd row offset
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      mg = fabsf(gh[0].x);
+      mh = fabsf(gh[0].y);
+    }
+    ++gh;
+    --n;
+  }
+  const float4* g4 = reinterpret_cast<const float4*>(gh);
+  const int n4 = n / 2;
+  const int stride = gridDim.x * blockDim.x;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = g4[i + j * stride];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mg = fmaxf(mg, fmaxf(fabsf(v[j].x), fabsf(v[j].z)));
+      mh = fmaxf(mh, fmaxf(fabsf(v[j].y), fabsf(v[j].w)));
+    }
+  }
+  for (; i < n4; i += stride) {
+    const float4 v = g4[i];
+    mg = fmaxf(mg, fmaxf(fabsf(v.x), fabsf(v.z)));
+    mh = fmaxf(mh, fmaxf(fabsf(v.y), fabsf(v.w)));
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const float2 v = gh[n - 1];  // (n, gh: after the alignment step)
     mg = fmaxf(mg, fabsf(v.x));
     mh = fmaxf(mh, fabsf(v.y));
   }
@@ -271,7 +301,17 @@ __global__ __launch_bounds__(256) void k_qmax(const float2* gh, int n, unsigned*
     mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
     mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
   }
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    s_m[0][w] = mg;
+    s_m[1][w] = mh;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; ++k) {
+      mg = fmaxf(mg, s_m[0][k]);
+      mh = fmaxf(mh, s_m[1][k]);
+    }
     atomicMax(&qmax[0], __float_as_uint(mg));  // non-negative floats order as their bits
     atomicMax(&qmax[1], __float_as_uint(mh));
   }
@@ -3516,6 +3556,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
     a.distributed = distributed_ ? 1 : 0;
+    a.kcap = fcaps_on_ ? fkcap_.get() : nullptr;
+    a.kused = distributed_ ? fkused_.get() : nullptr;
     if (distributed_) a.qpack = 0;  // the all-reduced level sums of every rank: keep two words per bin
     a.sp = MakeArgs().sp;
     return a;
@@ -3562,8 +3604,25 @@ class DeviceTreeLearner : public TreeLearner {
       LaunchFrontierSelect(fa, stream_);
     }
     for (int r = 0; r < rounds; ++r) {
-      EnqueueFrontierRound(fa, prologue && r < 7 ? (1 << r) : fkmax_);
+      // round r + 1 of the tree (main replay) has at most 2^r open nodes, and at most its cap
+      int kb = prologue && r < 7 ? (1 << r) : fkmax_;
+      if (prologue && fcaps_on_ && r + 1 < kFrontierRoundCap) kb = std::min(kb, fcap_host_[r + 1]);
+      fstat_ar_exps_ += distributed_ ? std::max(1, std::min(kb, fkmax_)) : 0;
+      EnqueueFrontierRound(fa, kb);
     }
+  }
+
+  // Data-parallel: expansions round r (>= 1) may take: the bound 2^(r-1), tightened to 1.5x the
+  // most any of the last 4 trees took in that round (+1, at least 2). Identical on every rank
+  // (the history comes from the replicated select), so every rank sizes its all-reduces alike.
+  int FrontierRoundCap(int r) const {
+    int c = std::min(fkmax_, r - 1 < 7 ? (1 << (r - 1)) : fkmax_);
+    if (fkused_trees_ > 0) {
+      int m = 0;
+      for (int t = 0; t < std::min(fkused_trees_, 4); ++t) m = std::max(m, fkused_hist_[t][r]);
+      c = std::min(c, std::max(2, (3 * m + 1) / 2 + 1));
+    }
+    return std::max(1, c);
   }
 
   hipGraphExec_t CaptureFrontier(int rounds, bool prologue) {
@@ -3595,6 +3654,24 @@ class DeviceTreeLearner : public TreeLearner {
     const bool use_graph = config_->device_use_graph && (!distributed_ || (DPGraphEnabled() && !HostStagedDP()));
     if (use_graph && distributed_ && !fgraphs_.empty() && graph_comm_ != ActiveComm()) InvalidateGraph();
     if (use_graph && distributed_) graph_comm_ = ActiveComm();
+    // per-round caps need the eager enqueue (the all-reduce sizes change from tree to tree)
+    fcaps_on_ = distributed_ && !use_graph && std::getenv("LGAP_FRONTIER_KCAP") == nullptr;
+    if (distributed_) {
+      if (fkused_.size() < static_cast<size_t>(kFrontierRoundCap)) {
+        fkused_.Resize(kFrontierRoundCap);
+        fkcap_.Resize(kFrontierRoundCap);
+      }
+      fkused_.Zero(stream_);
+      if (fcaps_on_) {
+        const int pr = std::max(1, std::min(fpred_rounds_, L_));
+        int* hc = pin_kcap_.Get(kFrontierRoundCap);
+        for (int r = 0; r < kFrontierRoundCap; ++r) {
+          fcap_host_[r] = r == 0 ? 1 : (r <= pr ? FrontierRoundCap(r) : fkmax_);
+          hc[r] = fcap_host_[r];
+        }
+        HIP_CHECK(hipMemcpyAsync(fkcap_.get(), hc, sizeof(int) * kFrontierRoundCap, hipMemcpyHostToDevice, stream_));
+      }
+    }
     const int pred = std::max(1, std::min(fpred_rounds_, L_));
     FState* hs = pin_fst_.Get(1);
     if (fgraph_gh_ != gh_.get()) {  // captured launches hold the gradient buffer's address
@@ -3648,13 +3725,20 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(hlo, flout_, sizeof(double), hipMemcpyDeviceToHost, stream_));
     unsigned* hbar = pin_bar_.Get(4);
     HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
+    int* hku = distributed_ ? pin_kused_.Get(kFrontierRoundCap) : nullptr;
+    if (hku) HIP_CHECK(hipMemcpyAsync(hku, fkused_.get(), sizeof(int) * kFrontierRoundCap, hipMemcpyDeviceToHost, stream_));
     FrontierSync();
+    if (hku) {
+      std::memcpy(fkused_hist_[fkused_trees_ % 4], hku, sizeof(int) * kFrontierRoundCap);
+      ++fkused_trees_;
+    }
     if (hbar[2] != 0u) Log::Fatal("k_f_partition: a wait on published tile counts timed out (blocks not co-resident?)");
     if (fstamps_.size() && fstat_trees_ == 3) ReportFrontierStamps(hs->round);
     if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {
       std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max), wasted rows %.1f%%, "
-                   "alpha %.3f\n", fstat_trees_, static_cast<double>(fstat_rounds_) / fstat_trees_,
-                   static_cast<double>(fstat_spec_) / fstat_trees_, L_, 100.0 * fstat_waste_ / fstat_trees_, fspec_alpha_);
+                   "alpha %.3f, all-reduced expansion slots/tree %.1f\n", fstat_trees_,
+                   static_cast<double>(fstat_rounds_) / fstat_trees_, static_cast<double>(fstat_spec_) / fstat_trees_, L_,
+                   100.0 * fstat_waste_ / fstat_trees_, fspec_alpha_, fstat_ar_exps_ / fstat_trees_);
     }
   }
 
@@ -4768,6 +4852,14 @@ class DeviceTreeLearner : public TreeLearner {
   std::map<int, hipGraphExec_t> fgraphs_;
   hipGraphExec_t fcont_ = nullptr;
   int fpred_rounds_ = 16, frounds_hist_[4] = {1, 1, 1, 1}, frounds_pos_ = 0;
+  // data-parallel per-round expansion caps (= all-reduce sizes) from the last trees' rounds
+  bool fcaps_on_ = false;
+  int fcap_host_[kFrontierRoundCap] = {};
+  int fkused_hist_[4][kFrontierRoundCap] = {};
+  int fkused_trees_ = 0;
+  double fstat_ar_exps_ = 0.0;
+  DevBuf<int> fkcap_, fkused_;
+  PinnedBuf<int> pin_kcap_, pin_kused_;
   long long fstat_rounds_ = 0, fstat_spec_ = 0;
   double fstat_waste_ = 0.0, fspec_alpha_ = 1.0;
   bool fspec_fixed_ = false;

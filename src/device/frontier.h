@@ -50,6 +50,7 @@ namespace device {
 constexpr int kFrontierKmax = 64;   // expansions per round (compile-time cap)
 constexpr int kFrontierBufs = 4;    // depth-indexed row-index buffers
 constexpr int kFrontierIdx = 5;     // index buffers addressed by id: depth buffers {0, 1, 3, 4}, bag 2
+constexpr int kFrontierRoundCap = 64;  // rounds with their own expansion cap (later rounds: kmax)
 constexpr int kFrontierMaxNodes = 4096;  // computed-node capacity of the select's LDS image
 
 // entries of the select's sort of the alive nodes: a power of two >= C (C <= kFrontierMaxNodes)
@@ -164,6 +165,8 @@ struct FArgs {
   int spec_cap;     // speculative expansions per round beyond the budget (policy knob)
   int policy;       // 1: budget by global gain rank (default), 0: budget minus uncommitted expansions
   int distributed;  // children counts from the split record (global) instead of the partition
+  const int* kcap;  // [kFrontierRoundCap] per-round expansion caps (data-parallel: the all-reduce sizes), or null
+  int* kused;       // [kFrontierRoundCap] expansions each round actually took (host feedback), or null
   unsigned long long* stamps;  // diagnostics (LGAP_FSTAMPS=1): [round & 255][kernel 0..3][8] wall clock
   SplitParams sp;
 };

@@ -1356,8 +1356,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     // the host from the rows the previous trees' uncommitted expansions cost)
     const float alpha = a.tp->spec_alpha > 0.f ? a.tp->spec_alpha : 1.f;
     const int budget = static_cast<int>(alpha * static_cast<float>(R)) + a.spec_cap;
-    const int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
-                                  : min(a.kmax, max(1, cap_nodes));
+    int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
+                            : min(a.kmax, max(1, cap_nodes));
+    // data-parallel: the round's all-reduce covers only kcap[round] expansions
+    if (a.kcap != nullptr && rnd + 1 < kFrontierRoundCap) lim = min(lim, max(1, a.kcap[rnd + 1]));
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int p = t * kPer + q;
@@ -1376,6 +1378,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     FStamp(a, rnd, kFStampSel, 5);
     int K = s_k;
     if (K <= 0) done = 1;  // nothing can be expanded: (only reachable without a blocked node)
+    if (a.kused != nullptr && t == 0 && rnd + 1 < kFrontierRoundCap) a.kused[rnd + 1] = done ? 0 : K;
     if (!done && w == 0) {
       // expansion records, tiles prefix (wave 0; K <= 64)
       const int kTile = a.part_tile;
