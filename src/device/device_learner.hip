@@ -2462,6 +2462,10 @@ class DeviceTreeLearner : public TreeLearner {
       : config_(config), mode_(mode), data_parallel_(mode == DevParallel::kData) {}
 
   ~DeviceTreeLearner() override {
+    if (fres_host_) (void)hipHostFree(fres_host_);
+    for (auto& ev : tree_evt_) {
+      if (ev) (void)hipEventDestroy(ev);
+    }
     if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
     for (auto& kv : fgraphs_) (void)hipGraphExecDestroy(kv.second);
     if (fcont_) (void)hipGraphExecDestroy(fcont_);
@@ -2857,11 +2861,7 @@ class DeviceTreeLearner : public TreeLearner {
     ra.score = score_.get() + static_cast<size_t>(class_id) * N_;
     ra.label = label_.get();
     ra.weight = pp->kind == kPwMape ? aux_.get() : (weight_.size() ? weight_.get() : nullptr);
-    ra.idx0 = idx_[0].get();
-    ra.idx1 = idx_[1].get();
-    ra.idx2 = idx_[2].get();
-    ra.idx3 = idx_[3].get();
-    ra.idx4 = idx_[4].get();
+    for (int i = 0; i < kLeafIdxBufs; ++i) ra.idx[i] = i < kFrontierIdx ? idx_[i].get() : nullptr;
     ra.segs = renew_segs_.get();
     ra.seg_off = renew_off_.get();
     ra.num_leaves = nl;
@@ -3152,7 +3152,13 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t node_bytes = Round256(sizeof(TNode) * nn), cat_bytes = Round256(sizeof(TCat) * nn);
     const size_t leaf_bytes = Round256(sizeof(double) * nl), bit_bytes = sizeof(uint32_t) * std::max<size_t>(1, ct.size());
     const size_t total = node_bytes + cat_bytes + leaf_bytes + bit_bytes;
-    char* hp = pin_tree_.Get(total);
+    // staging ring: the host fills one pinned buffer while the copy out of the other may still
+    // be queued, so the score update returns without waiting for the GPU (the next iteration's
+    // launches queue behind the traversal instead of after a host round trip)
+    const int slot = tree_slot_++ & 1;
+    if (tree_evt_[slot] == nullptr) HIP_CHECK(hipEventCreateWithFlags(&tree_evt_[slot], hipEventDisableTiming));
+    else HIP_CHECK(hipEventSynchronize(tree_evt_[slot]));
+    char* hp = pin_tree_ring_[slot].Get(total);
     TNode* nodes = reinterpret_cast<TNode*>(hp);
     TCat* cats = reinterpret_cast<TCat*>(hp + node_bytes);
     for (int i = 0; i < nn; ++i) {
@@ -3196,22 +3202,23 @@ class DeviceTreeLearner : public TreeLearner {
     for (int l = 0; l < nl; ++l) lv[l] = tree->LeafOutput(l);
     uint32_t* cw = reinterpret_cast<uint32_t*>(hp + node_bytes + cat_bytes + leaf_bytes);
     for (size_t i = 0; i < ct.size(); ++i) cw[i] = ct[i];
-    tree_buf_.Resize(std::max(tree_buf_.size(), total));
-    HIP_CHECK(hipMemcpyAsync(tree_buf_.get(), hp, total, hipMemcpyHostToDevice, stream_));
-    const char* db = tree_buf_.get();
+    if (ttree_buf_.size() < total) {
+      HIP_CHECK(hipStreamSynchronize(stream_));  // queued traversals still read the old buffer
+      ttree_buf_.Resize(total);
+    }
+    HIP_CHECK(hipMemcpyAsync(ttree_buf_.get(), hp, total, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipEventRecord(tree_evt_[slot], stream_));
+    const char* db = ttree_buf_.get();
     if (rowbins == rowbins_.get() && n == N_ && stride_dw_ > 16 && colbins_.size() >= static_cast<size_t>(G_) * N_ * width_) {
       LaunchTraverseCols(colbins_.get(), width_, n, reinterpret_cast<const TNode*>(db), nn,
                          reinterpret_cast<const TCat*>(db + node_bytes),
                          reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                          reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
-      HIP_CHECK(hipStreamSynchronize(stream_));
       return;
     }
     LaunchTraverse(rowbins, stride_dw_, width_, n, reinterpret_cast<const TNode*>(db), nn,
                    reinterpret_cast<const TCat*>(db + node_bytes), reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                    reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
-    // the pinned staging buffer is reused by the next call: wait for the copy
-    HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
   // ---- validation sets on the device: packed rows (training layout), score, labels / weights
@@ -3434,6 +3441,16 @@ class DeviceTreeLearner : public TreeLearner {
     flcid_ = reinterpret_cast<int*>(b + o_lcid);
     fckey_ = reinterpret_cast<SplitKey*>(b + o_ckey);
     fcinfo_ = reinterpret_cast<SplitInfo*>(b + o_cinfo);
+    // replay results: coherent pinned host memory the results kernel writes directly
+    const size_t rbytes = FrontierResultBytes(L_);
+    if (rbytes > fres_bytes_) {
+      if (fres_host_) HIP_CHECK(hipHostFree(fres_host_));
+      void* hp = nullptr;
+      HIP_CHECK(hipHostMalloc(&hp, rbytes, hipHostMallocMapped | hipHostMallocCoherent));
+      fres_host_ = static_cast<char*>(hp);
+      HIP_CHECK(hipHostGetDevicePointer(&fres_dev_, hp, 0));
+      fres_bytes_ = rbytes;
+    }
     fslots_.Resize(C * 2 * static_cast<size_t>(TB_));
     facc_.Resize(K * 2 * static_cast<size_t>(TB_));
     facc_.Zero(stream_);  // the scan re-zeroes what it consumes: zero between rounds from here on
@@ -3441,7 +3458,7 @@ class DeviceTreeLearner : public TreeLearner {
     ftile_cap_ = DivUp(N_, fpart_tile_) + fkmax_ + 1;
     ftile_pub_.Resize(ftile_cap_);
     ftile_pub_.Zero(stream_);
-    for (int i = 3; i < 5; ++i) idx_[i].Resize(std::max(N_, 1));
+    for (int i = 3; i < kFrontierIdx; ++i) idx_[i].Resize(std::max(N_, 1));
     // the partition's look-back needs all of its blocks resident: occupancy minus a margin
     int per_cu = FrontierPartitionBlocksPerCU(part_iters_);
     int cap = 8;  // A/B knob LGAP_FPART_BPC (10M rows: 4 -> 327.9, 6 -> 334.7, 8 -> 337.3 it/s)
@@ -3673,7 +3690,9 @@ class DeviceTreeLearner : public TreeLearner {
       }
     }
     const int pred = std::max(1, std::min(fpred_rounds_, L_));
-    FState* hs = pin_fst_.Get(1);
+    const FResultHdr* hh = reinterpret_cast<const FResultHdr*>(fres_host_);
+    const FState* hs = &hh->st;
+    const FArgs fa_res = MakeFArgs();
     if (fgraph_gh_ != gh_.get()) {  // captured launches hold the gradient buffer's address
       InvalidateGraph();
       fgraph_gh_ = gh_.get();
@@ -3688,7 +3707,7 @@ class DeviceTreeLearner : public TreeLearner {
     constexpr int kCont = 4;
     int launched = pred;
     for (;;) {
-      HIP_CHECK(hipMemcpyAsync(hs, fst_, sizeof(FState), hipMemcpyDeviceToHost, stream_));
+      LaunchFrontierResults(fa_res, fres_dev_, stream_);
       FrontierSync();
       if (hs->done) break;
       if (launched > L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
@@ -3720,16 +3739,14 @@ class DeviceTreeLearner : public TreeLearner {
     fstat_trees_ += 1;
     *num_splits = hs->num_splits;
     *num_leaves = hs->num_leaves;
-    if (*num_splits > 0) HIP_CHECK(hipMemcpyAsync(hr, rec_.get(), sizeof(SplitRec) * *num_splits, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(hrange, range_.get(), sizeof(LeafRange) * *num_leaves, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(hlo, flout_, sizeof(double), hipMemcpyDeviceToHost, stream_));
-    unsigned* hbar = pin_bar_.Get(4);
-    HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
-    int* hku = distributed_ ? pin_kused_.Get(kFrontierRoundCap) : nullptr;
-    if (hku) HIP_CHECK(hipMemcpyAsync(hku, fkused_.get(), sizeof(int) * kFrontierRoundCap, hipMemcpyDeviceToHost, stream_));
-    FrontierSync();
-    if (hku) {
-      std::memcpy(fkused_hist_[fkused_trees_ % 4], hku, sizeof(int) * kFrontierRoundCap);
+    // (k_f_results already wrote the records, ranges, root output and flags with the state)
+    if (*num_splits > 0) std::memcpy(hr, fres_host_ + FrontierResultRecOffset(), sizeof(SplitRec) * *num_splits);
+    std::memcpy(hrange, fres_host_ + FrontierResultRangeOffset(L_), sizeof(LeafRange) * *num_leaves);
+    *hlo = hh->lout0;
+    unsigned hbar[4];
+    std::memcpy(hbar, hh->bar, sizeof(hbar));
+    if (distributed_) {
+      std::memcpy(fkused_hist_[fkused_trees_ % 4], hh->kused, sizeof(int) * kFrontierRoundCap);
       ++fkused_trees_;
     }
     if (hbar[2] != 0u) Log::Fatal("k_f_partition: a wait on published tile counts timed out (blocks not co-resident?)");
@@ -4853,18 +4870,20 @@ class DeviceTreeLearner : public TreeLearner {
   hipGraphExec_t fcont_ = nullptr;
   int fpred_rounds_ = 16, frounds_hist_[4] = {1, 1, 1, 1}, frounds_pos_ = 0;
   // data-parallel per-round expansion caps (= all-reduce sizes) from the last trees' rounds
+  char* fres_host_ = nullptr;  // FResultHdr + records + ranges (coherent pinned host memory)
+  void* fres_dev_ = nullptr;
+  size_t fres_bytes_ = 0;
   bool fcaps_on_ = false;
   int fcap_host_[kFrontierRoundCap] = {};
   int fkused_hist_[4][kFrontierRoundCap] = {};
   int fkused_trees_ = 0;
   double fstat_ar_exps_ = 0.0;
   DevBuf<int> fkcap_, fkused_;
-  PinnedBuf<int> pin_kcap_, pin_kused_;
+  PinnedBuf<int> pin_kcap_;
   long long fstat_rounds_ = 0, fstat_spec_ = 0;
   double fstat_waste_ = 0.0, fspec_alpha_ = 1.0;
   bool fspec_fixed_ = false;
   int fstat_trees_ = 0;
-  PinnedBuf<FState> pin_fst_;
   DevBuf<unsigned long long> fstamps_;
   const float2* fgraph_gh_ = nullptr;
   const Config* config_;
@@ -4896,7 +4915,8 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<float2> gh_;
   DevBuf<double> score_;
   DevBuf<float> label_, weight_, aux_;
-  DevBuf<int> idx_[5];
+  static_assert(kFrontierIdx <= kLeafIdxBufs, "leaf renewal addresses every index buffer");
+  DevBuf<int> idx_[kFrontierIdx];
   DevBuf<DevFeature> feat_;
   DevBuf<int> gstart_;
   DevBuf<HistTile> tiles_;
@@ -5003,6 +5023,10 @@ class DeviceTreeLearner : public TreeLearner {
   PinnedBuf<double> pin_lout_;
   PinnedBuf<float2> pin_gh_;
   PinnedBuf<char> pin_tree_;
+  PinnedBuf<char> pin_tree_ring_[2];  // TraverseTreeCompact staging (see there)
+  DevBuf<char> ttree_buf_;             // its device copy (stream-ordered reuse)
+  hipEvent_t tree_evt_[2] = {nullptr, nullptr};
+  unsigned tree_slot_ = 0;
   PinnedBuf<unsigned> pin_max_;
   // device row sampling
   DevBuf<uint2> samp_jump_;

@@ -48,8 +48,11 @@ namespace lgap {
 namespace device {
 
 constexpr int kFrontierKmax = 64;   // expansions per round (compile-time cap)
-constexpr int kFrontierBufs = 4;    // depth-indexed row-index buffers
-constexpr int kFrontierIdx = 5;     // index buffers addressed by id: depth buffers {0, 1, 3, 4}, bag 2
+#ifndef LGAP_FRONTIER_BUFS
+#define LGAP_FRONTIER_BUFS 4
+#endif
+constexpr int kFrontierBufs = LGAP_FRONTIER_BUFS;  // depth-indexed row-index buffers
+constexpr int kFrontierIdx = kFrontierBufs + 1;    // index buffers by id: depth buffers {0, 1, 3, ...}, bag 2
 constexpr int kFrontierRoundCap = 64;  // rounds with their own expansion cap (later rounds: kmax)
 constexpr int kFrontierMaxNodes = 4096;  // computed-node capacity of the select's LDS image
 
@@ -171,7 +174,24 @@ struct FArgs {
   SplitParams sp;
 };
 
+// Results of a replay, written by k_f_results straight into coherent pinned host memory (one
+// small kernel instead of five D2H copies, each ~19 us apart on the copy path): the header,
+// then (once the tree is done) SplitRec[L - 1] at FrontierResultRecOffset() and LeafRange[L]
+// after them.
+struct FResultHdr {
+  FState st;
+  unsigned bar[4];
+  double lout0;
+  int kused[kFrontierRoundCap];
+};
+__host__ __device__ inline size_t FrontierResultRecOffset() { return (sizeof(FResultHdr) + 15) & ~size_t(15); }
+__host__ __device__ inline size_t FrontierResultRangeOffset(int L) {
+  return FrontierResultRecOffset() + ((sizeof(SplitRec) * static_cast<size_t>(L > 1 ? L - 1 : 1) + 15) & ~size_t(15));
+}
+inline size_t FrontierResultBytes(int L) { return FrontierResultRangeOffset(L) + sizeof(LeafRange) * static_cast<size_t>(L); }
+
 // launchers (frontier_kernels.hip)
+void LaunchFrontierResults(const FArgs& a, void* host_out, hipStream_t s);
 void LaunchFrontierInit(const FArgs& a, hipStream_t s);
 void LaunchFrontierHist(const FArgs& a, size_t lds_bytes, hipStream_t s);
 void LaunchFrontierScan(const FArgs& a, size_t lds_bytes, hipStream_t s);

@@ -1494,7 +1494,34 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// k_f_results: the replay's state (and, once the tree is done, its split records and leaf
+// ranges) into the host-visible results buffer
+__global__ __launch_bounds__(256) void k_f_results(FArgs a, char* out) {
+  FResultHdr* h = reinterpret_cast<FResultHdr*>(out);
+  const FState st = *a.st;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    h->st = st;
+    for (int i = 0; i < 4; ++i) h->bar[i] = a.bar[i];
+    h->lout0 = a.lout[0];
+  }
+  if (t < kFrontierRoundCap) h->kused[t] = a.kused != nullptr ? a.kused[t] : 0;
+  if (!st.done) return;
+  const int nrec = static_cast<int>(sizeof(SplitRec) / 4) * st.num_splits;
+  uint32_t* rec = reinterpret_cast<uint32_t*>(out + FrontierResultRecOffset());
+  for (int i = t; i < nrec; i += blockDim.x) rec[i] = reinterpret_cast<const uint32_t*>(a.rec)[i];
+  const int nrange = static_cast<int>(sizeof(LeafRange) / 4) * st.num_leaves;
+  uint32_t* rng = reinterpret_cast<uint32_t*>(out + FrontierResultRangeOffset(a.L));
+  for (int i = t; i < nrange; i += blockDim.x) rng[i] = reinterpret_cast<const uint32_t*>(a.range_out)[i];
+}
+
+// ---------------------------------------------------------------------------
 // launchers
+
+void LaunchFrontierResults(const FArgs& a, void* host_out, hipStream_t s) {
+  k_f_results<<<1, 256, 0, s>>>(a, static_cast<char*>(host_out));
+  HIP_CHECK(hipGetLastError());
+}
 
 void LaunchFrontierInit(const FArgs& a, hipStream_t s) {
   k_f_init<<<1, 256, 0, s>>>(a);

@@ -25,15 +25,13 @@ struct LeafSeg {
   int pad;
 };
 
+constexpr int kLeafIdxBufs = 8;  // >= kFrontierIdx (frontier.h)
+
 struct RenewArgs {
   const double* score;  // class slice of the device score
   const float* label;
   const float* weight;  // per-row percentile weights (sample weights or MAPE label weights), nullptr: none
-  const int* idx0;
-  const int* idx1;
-  const int* idx2;
-  const int* idx3;  // frontier depth buffers 2 and 3
-  const int* idx4;
+  const int* idx[kLeafIdxBufs];  // row-index buffers by id (0/1 ping-pong, 2 bag, 3+ frontier depth buffers)
   const LeafSeg* segs;  // [num_leaves]
   const int* seg_off;   // [num_leaves + 1] offsets of the leaves in the gathered arrays
   int num_leaves;

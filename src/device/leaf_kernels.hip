@@ -21,12 +21,7 @@ constexpr int kPickThreads = 1024;
 __global__ __launch_bounds__(256) void k_renew_gather(RenewArgs a, double* __restrict__ keys, float* __restrict__ vals) {
   const int leaf = blockIdx.y;
   const LeafSeg sg = a.segs[leaf];
-  const int* idx = sg.buf == 0   ? a.idx0
-                   : sg.buf == 1 ? a.idx1
-                   : sg.buf == 2 ? a.idx2
-                   : sg.buf == 3 ? a.idx3
-                   : sg.buf == 4 ? a.idx4
-                                 : nullptr;
+  const int* idx = sg.buf >= 0 && sg.buf < kLeafIdxBufs ? a.idx[sg.buf] : nullptr;
   const int base = a.seg_off[leaf];
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < sg.count; i += gridDim.x * blockDim.x) {
     const int row = idx ? idx[sg.start + i] : sg.start + i;
