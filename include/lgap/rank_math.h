@@ -92,10 +92,18 @@ LGAP_HD inline bool TargetIsBinary(int t) {
          t == kTgtGapXPlus || t == kTgtGapSPlusPlus || t == kTgtGapXPlusPlus;
 }
 
+// RankDiscount evaluated directly (the host objective; queries too long for a table)
+struct RankDiscountFn {
+  LGAP_HD double operator()(int r) const { return RankDiscount(r); }
+};
+
 // delta_pair for ranks (i, j) (i < j), with high/low = the better/worse labelled doc.
-LGAP_HD inline double TargetDeltaPair(int t, int i, int j, int high_rank, int low_rank, double high_gain,
-                                      double low_gain, double high_label, double low_label, double inv_max_dcg,
-                                      double inv_max_bdcg, int k, double w) {
+// `RankDiscount` is the discount source: RankDiscountFn, or a per-query table of the same
+// values (the HIP kernel keeps one in LDS: two double log2 per pair were most of its work).
+template <typename Disc>
+LGAP_HD inline double TargetDeltaPairD(int t, int i, int j, int high_rank, int low_rank, double high_gain,
+                                       double low_gain, double high_label, double low_label, double inv_max_dcg,
+                                       double inv_max_bdcg, int k, double w, const Disc& RankDiscount) {
   switch (t) {
     case kTgtNdcg:
       return (high_gain - low_gain) * fabs(RankDiscount(high_rank) - RankDiscount(low_rank)) * inv_max_dcg;
@@ -136,6 +144,13 @@ LGAP_HD inline double TargetDeltaPair(int t, int i, int j, int high_rank, int lo
       return high_label - low_label;
   }
   return 0.0;
+}
+
+LGAP_HD inline double TargetDeltaPair(int t, int i, int j, int high_rank, int low_rank, double high_gain,
+                                      double low_gain, double high_label, double low_label, double inv_max_dcg,
+                                      double inv_max_bdcg, int k, double w) {
+  return TargetDeltaPairD(t, i, j, high_rank, low_rank, high_gain, low_gain, high_label, low_label, inv_max_dcg,
+                          inv_max_bdcg, k, w, RankDiscountFn());
 }
 
 }  // namespace lgap

@@ -61,6 +61,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <map>
 #include <memory>
 #include <string>
@@ -75,6 +76,7 @@
 #include "device/sample_kernels.h"
 #include "device/split_scan.h"
 #include "device/tree_kernels.h"
+#include "learner/forced_splits.h"
 #include "learner/serial_tree_learner.h"
 #include "lgap/common.h"
 #include "lgap/device_api.h"
@@ -2507,9 +2509,7 @@ class DeviceTreeLearner : public TreeLearner {
     device_name_ = std::string(prop.name[0] ? prop.name : "AMD GPU") + " (" + prop.gcnArchName + ")";
     num_cu_ = prop.multiProcessorCount;
     if (!stream_) HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    if (!config_->forcedsplits_filename.empty()) {
-      Log::Fatal("forcedsplits_filename is not supported by the HIP learner yet; use device_type=cpu");
-    }
+
     use_dp_ = config_->gpu_use_dp;
     UploadData();
     SetupOwnership();
@@ -3411,8 +3411,43 @@ class DeviceTreeLearner : public TreeLearner {
     return static_cast<int>(c);
   }
 
+  // forcedsplits_filename -> the FForced list the frontier select applies first (the host
+  // learner's order and skips: learner/forced_splits.h)
+  void UploadForcedSplits() {
+    fnum_forced_ = 0;
+    if (config_->forcedsplits_filename.empty()) return;
+    std::ifstream in(config_->forcedsplits_filename);
+    if (!in) {
+      Log::Warning("Forced splits file %s cannot be opened", config_->forcedsplits_filename.c_str());
+      return;
+    }
+    const std::string js((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    size_t pos = 0;
+    auto root = ParseForced(js, &pos);
+    const auto flat = FlattenForced(root.get(), [&](int f) {
+      if (f < 0 || f >= data_->num_total_features()) return false;
+      const int inner = data_->InnerIndex(f);
+      return inner >= 0 && data_->feature(inner).bin_type == BinType::Numerical;
+    });
+    std::vector<FForced> h(flat.size());
+    for (size_t i = 0; i < flat.size(); ++i) {
+      const int inner = data_->InnerIndex(flat[i].feature);
+      h[i].feature = inner;
+      h[i].threshold = static_cast<int>(data_->inner_mapper(inner).ValueToBin(flat[i].threshold));
+      h[i].left = flat[i].left;
+      h[i].right = flat[i].right;
+    }
+    fforced_.Resize(std::max<size_t>(1, h.size()));
+    if (!h.empty()) fforced_.Upload(h.data(), h.size(), stream_);
+    fnum_forced_ = static_cast<int>(h.size());
+  }
+
   void AllocFrontier() {
     frontier_ = FrontierEligible();
+    if (!frontier_ && !config_->forcedsplits_filename.empty()) {
+      Log::Fatal("forced splits on the device need the frontier engine (serial learner, num_leaves <= 512, "
+                 "no feature_fraction_bynode / extra_trees)");
+    }
     if (!frontier_) return;
     fkmax_ = FrontierKmax();
     fC_ = FrontierCapacity();
@@ -3422,7 +3457,8 @@ class DeviceTreeLearner : public TreeLearner {
                  o_bits = lay.Add<uint32_t>(K * kMaxCatWords), o_lsum = lay.Add<double2>(C), o_lout = lay.Add<double>(C),
                  o_bounds = lay.Add<LeafBounds>(C), o_key = lay.Add<SplitKey>(C), o_best = lay.Add<SplitInfo>(C),
                  o_spl = lay.Add<uint8_t>(C * F), o_ic = lay.Add<unsigned long long>(C), o_nst = lay.Add<uint8_t>(C),
-                 o_lcid = lay.Add<int>(L_), o_ckey = lay.Add<SplitKey>(K * 2 * F), o_cinfo = lay.Add<SplitInfo>(K * 2 * F);
+                 o_lcid = lay.Add<int>(L_), o_ckey = lay.Add<SplitKey>(K * 2 * F), o_cinfo = lay.Add<SplitInfo>(K * 2 * F),
+                 o_fbest = lay.Add<SplitInfo>(C), o_fkey = lay.Add<SplitKey>(C);
     farena_.Resize(lay.bytes());
     farena_.Zero(stream_);
     char* b = farena_.get();
@@ -3441,6 +3477,9 @@ class DeviceTreeLearner : public TreeLearner {
     flcid_ = reinterpret_cast<int*>(b + o_lcid);
     fckey_ = reinterpret_cast<SplitKey*>(b + o_ckey);
     fcinfo_ = reinterpret_cast<SplitInfo*>(b + o_cinfo);
+    ffbest_ = reinterpret_cast<SplitInfo*>(b + o_fbest);
+    ffkey_ = reinterpret_cast<SplitKey*>(b + o_fkey);
+    UploadForcedSplits();
     // replay results: coherent pinned host memory the results kernel writes directly
     const size_t rbytes = FrontierResultBytes(L_);
     if (rbytes > fres_bytes_) {
@@ -3532,6 +3571,10 @@ class DeviceTreeLearner : public TreeLearner {
     a.slots = fslots_.get();
     a.acc = reinterpret_cast<unsigned long long*>(facc_.get());
     a.ghmax = ghmax_.get();
+    a.forced = fnum_forced_ > 0 ? fforced_.get() : nullptr;
+    a.num_forced = fnum_forced_;
+    a.fbest = ffbest_;
+    a.fkey = ffkey_;
     a.ckey = fckey_;
     a.cinfo = fcinfo_;
     a.tile_pub = ftile_pub_.get();
@@ -4870,6 +4913,10 @@ class DeviceTreeLearner : public TreeLearner {
   hipGraphExec_t fcont_ = nullptr;
   int fpred_rounds_ = 16, frounds_hist_[4] = {1, 1, 1, 1}, frounds_pos_ = 0;
   // data-parallel per-round expansion caps (= all-reduce sizes) from the last trees' rounds
+  DevBuf<FForced> fforced_;
+  int fnum_forced_ = 0;
+  SplitInfo* ffbest_ = nullptr;
+  SplitKey* ffkey_ = nullptr;
   char* fres_host_ = nullptr;  // FResultHdr + records + ranges (coherent pinned host memory)
   void* fres_dev_ = nullptr;
   size_t fres_bytes_ = 0;
@@ -5004,7 +5051,7 @@ class DeviceTreeLearner : public TreeLearner {
   // multiclassova / unbiased LTR / long queries
   DevBuf<PointwiseParams> ova_params_;
   DevBuf<int> positions_, long_q_;
-  DevBuf<float> pos_bias_;
+  DevBuf<double> pos_bias_;
   DevBuf<long long> pos_acc_, long_off_;
   DevBuf<char> long_scratch_;
   int num_pos_ids_ = 0;

@@ -77,7 +77,13 @@ struct FNode {
   int gcount;             // global row count (data parallel: estimated from the split) / = count
   int depth, parent;
   int left;               // first child cid (right = left + 1), -1: not expanded
-  int pad;
+  int fidx;               // index of its forced split (FForced), -1: none
+};
+
+// One forced split (forcedsplits_filename) in the host learner's application order
+// (learner/forced_splits.h FlattenForced): inner feature, threshold bin, children indices.
+struct FForced {
+  int feature, threshold, left, right;
 };
 
 // One expansion (the split of node `parent`) of the current round.
@@ -92,7 +98,7 @@ struct FExp {
   int skip;                  // the children cannot split: no histogram / scan
   int smaller, larger;       // cids
   int h_buf, h_start, h_count;  // the smaller child's local rows
-  int pad;
+  int forced;                // the split is forced split `forced` (FForced index), -1: the node's best
 };
 
 struct FState {
@@ -106,7 +112,8 @@ struct FState {
   int blocked;      // cid the replay waits for (-1: none)
   int spec;         // expansions started so far
   long long used_rows, waste_rows;  // (when done) rows partitioned by committed / uncommitted expansions
-  int pad[2];
+  int forced_next;  // next forced split to apply (-1: forced splits over or none)
+  int pad;
 };
 
 // Arguments of the frontier kernels (device pointers into the learner's buffers).
@@ -143,6 +150,12 @@ struct FArgs {
   double* slots;              // [C][2 TB] per-node histograms (stored bins, fp64)
   unsigned long long* acc;    // [kmax][2 TB] per-expansion fixed-point accumulators (zero between rounds)
   const unsigned* ghmax;      // float bits of max|g|, max|h| over the root rows
+  // forced splits: the list, and per node the forced split at its threshold (scan) and its
+  // split predicate (for the expansion that applies it)
+  const FForced* forced;
+  int num_forced;
+  SplitInfo* fbest;  // [C]
+  SplitKey* fkey;    // [C]
   // quantized training (use_quantized_grad): per-row int8 levels, integer histograms
   const uint16_t* ghq;        // class-major: (g level int8) << 8 | (h level uint8)
   const unsigned* qmax;       // float bits of the quantizer's max|g|, max|h| (k_qmax)

@@ -93,7 +93,8 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
     s.blocked = -1;
     s.spec = 0;
     s.used_rows = s.waste_rows = 0;
-    s.pad[0] = s.pad[1] = 0;
+    s.forced_next = a.num_forced > 0 ? 0 : -1;
+    s.pad = 0;
     *a.st = s;
     FNode r;
     r.buf = tp.root_buf;
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
     r.depth = 0;
     r.parent = -1;
     r.left = -1;
-    r.pad = 0;
+    r.fidx = a.num_forced > 0 ? 0 : -1;
     a.nodes[0] = r;
     FExp x;
     x.parent = -1;
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
     x.h_buf = tp.root_buf;
     x.h_start = 0;
     x.h_count = tp.root_count;
-    x.pad = 0;
+    x.forced = -1;
     a.exps[0] = x;
     a.bounds[0] = LeafBounds();
     if (a.ic) a.ic[0] = ~0ull;
@@ -451,11 +452,13 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     double2 pre_sum = make_double2(0.0, 0.0);
     int pre_n = 0, pre_depth = 0;
     double pre_out = 0.0;
+    int pre_fidx = -1;
     LeafBounds pre_bounds;
     if (lane == 0 && my >= 0) {
       pre_sum = a.lsum[my];
       pre_n = a.nodes[my].gcount;
       pre_depth = a.nodes[my].depth;
+      pre_fidx = a.num_forced > 0 ? a.nodes[my].fidx : -1;
       pre_out = a.lout[my];
       pre_bounds = a.bounds[my];
     }
@@ -556,7 +559,8 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         }
         if (lane == 0) {
           a.spl[static_cast<size_t>(my) * F + f] = spl ? 1 : 0;
-          if (!spl) {
+          // (children of forced splits are scanned past max_depth: no regular split there)
+          if (!spl || (a.max_depth > 0 && depth >= a.max_depth)) {
             out->Reset();
           } else {
             out->feature = f;
@@ -572,6 +576,60 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
           p0.path_smooth = 0.0;
           a.lout[0] = LeafOutputRaw(sg, sh, p0, n, 0.0);
         }
+      }
+      if (lane == 0 && pre_fidx >= 0 && a.forced[pre_fidx].feature == f) {
+        // the node's forced split at its threshold (host ForceSplits / reference
+        // GatherInfoForThresholdNumerical: bins above the threshold go right, skipping the
+        // zero bin (MissingType::Zero) and the NaN bin; missing values go left)
+        const double pof = p < 0 ? LeafOutputRaw(sg, sh, [&] { SplitParams q = a.sp; q.path_smooth = 0.0; return q; }(), n, 0.0)
+                                 : pre_out;
+        const double* H = w ? hl_full : hs_full;
+        const int thr = a.forced[pre_fidx].threshold;
+        const bool na = fi.missing == 2, zero = fi.missing == 1;
+        const double cf = static_cast<double>(n) / sh;
+        double rg = 0.0, rh = 0.0;
+        int rc = 0;
+        for (int b = nbin - 1 - (na ? 1 : 0); b >= 1; --b) {
+          if (b <= thr) break;
+          if (zero && b == fi.default_bin) continue;
+          rg += H[2 * b];
+          rh += H[2 * b + 1];
+          rc += RoundCount(H[2 * b + 1] * cf);
+        }
+        const double lg = sg - rg, lh = sh - rh;
+        const int lc = n - rc;
+        SplitInfo fin;
+        fin.Reset();
+        fin.feature = f;
+        fin.threshold = static_cast<uint32_t>(thr);
+        fin.default_left = 1;
+        fin.left_sum_gradient = lg;
+        fin.left_sum_hessian = lh;
+        fin.right_sum_gradient = rg;
+        fin.right_sum_hessian = rh;
+        fin.left_count = lc;
+        fin.right_count = rc;
+        fin.left_output = LeafOutputRaw(lg, lh, a.sp, lc, pof);
+        fin.right_output = LeafOutputRaw(rg, rh, a.sp, rc, pof);
+        fin.gain = SplitGain(lg, lh, rg, rh, a.sp, 0, lc, rc, pof, LeafBounds()) - LeafGain(sg, sh, a.sp, n, pof) -
+                   a.sp.min_gain_to_split;
+        a.fbest[my] = fin;
+        SplitKey fk;
+        fk.gain = fin.gain;
+        fk.feature = f;
+        fk.threshold = static_cast<uint32_t>(thr);
+        fk.group = fi.group;
+        fk.offset = fi.offset;
+        fk.num_bin = fi.num_bin;
+        fk.mfb = fi.mfb;
+        fk.default_bin = fi.default_bin;
+        fk.missing = fi.missing;
+        fk.default_left = 1;
+        fk.is_cat = 0;
+        fk.pad0 = 0;
+        fk.pos = f;
+        fk.pad2 = 0;
+        a.fkey[my] = fk;
       }
       if (lane == 0) {
         SplitKey& kk = s_key[w];
@@ -668,7 +726,7 @@ __device__ int FSumCounts(const FArgs& a, int i0, int i1, unsigned epoch, int* s
 
 // children of expansion x (one thread)
 __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
-  const SplitInfo& bi = a.best[x.parent];
+  const SplitInfo& bi = x.forced >= 0 ? a.fbest[x.parent] : a.best[x.parent];
   const double lsg = bi.left_sum_gradient, lsh = bi.left_sum_hessian;
   const double rsg = bi.right_sum_gradient, rsh = bi.right_sum_hessian;
   const double lo = bi.left_output, ro = bi.right_output;
@@ -694,7 +752,8 @@ __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
   nl.depth = nr.depth = dep;
   nl.parent = nr.parent = x.parent;
   nl.left = nr.left = -1;
-  nl.pad = nr.pad = 0;
+  nl.fidx = x.forced >= 0 ? a.forced[x.forced].left : -1;
+  nr.fidx = x.forced >= 0 ? a.forced[x.forced].right : -1;
   a.nodes[l] = nl;
   a.nodes[r] = nr;
   a.lsum[l] = make_double2(lsg, lsh);
@@ -719,7 +778,11 @@ __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
     a.ic[r] = icm;
   }
   const int md = a.sp.min_data_in_leaf;
-  const bool skip = (a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2);
+  // children with forced splits of their own always get histograms (the forced split ignores
+  // min_data / max_depth, as the host learner's ForceSplits does); the scan keeps their
+  // regular candidates within max_depth
+  const bool forced_child = nl.fidx >= 0 || nr.fidx >= 0;
+  const bool skip = !forced_child && ((a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2));
   const bool left_smaller = glc < grc;
   FExp* xo = a.exps + e;
   xo->skip = skip ? 1 : 0;
@@ -1021,13 +1084,14 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   int* s_par = s_left + C;                                   // [C]
   int* s_dep = s_par + C;                                    // [C]
   int* s_rank = s_dep + C;                                   // [C] eligible: rank, else -1
-  int* s_lcid = s_rank + C;                                  // [L]
+  int* s_fidx = s_rank + C;                                  // [C] forced split index, -1: none
+  int* s_lcid = s_fidx + C;                                  // [L]
   int* s_c0 = s_lcid + L;                                    // [L] committed leaves of this launch
-  int* s_c1 = s_c0 + L;                                      // [L] their cids
+  int* s_c1 = s_c0 + L;                                      // [L] their cids (~cid: a forced split)
   uint8_t* s_st = reinterpret_cast<uint8_t*>(s_c1 + L);      // [C]
   __shared__ int s_cpos[2 * kFrontierKmax];  // this round's children: winning candidate position
   __shared__ int s_pc[2 * kFrontierKmax];    // pair -> child cid (-1: none / skipped)
-  __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_k, s_tiles;
+  __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_k, s_tiles, s_fnext, s_bforced;
   __shared__ int s_exp[kFrontierKmax];       // chosen expansions (cids) by order
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
@@ -1052,6 +1116,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     s_gain[c] = kf < 0 ? kMinScore : kg;
     s_feat[c] = kf;
     s_rank[c] = -1;
+    s_fidx[c] = nd.fidx;
   }
   for (int l = t; l < st.num_leaves; l += blockDim.x) s_lcid[l] = a.leaf_cid[l];
   if (t < 2 * kFrontierKmax) {
@@ -1158,10 +1223,56 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   __syncthreads();
   if (w == 0) {
     int nl = st.num_leaves, ns = st.num_splits, done = 0, blocked = -1, nc = 0;
+    int fnext = st.forced_next, bforced = 0;
     for (;;) {
       if (nl >= L) {
         done = 1;
         break;
+      }
+      if (fnext >= 0) {
+        // forced splits first, in the host learner's order (learner/forced_splits.h): the
+        // leaf holding forced split `fnext`; a non-positive forced gain ends forced splitting
+        int fl = -1;
+        for (int l = lane; l < nl; l += 64) {
+          if (s_fidx[s_lcid[l]] == fnext) fl = l;
+        }
+        const unsigned long long hit = __ballot(fl >= 0);
+        if (hit == 0ull) {
+          fnext = -1;
+        } else {
+          fl = __shfl(fl, __ffsll(static_cast<long long>(hit)) - 1, kWave);
+          const int c = s_lcid[fl];
+          const double fg = a.fbest[c].gain;  // (an earlier launch's scan wrote it)
+          if (!(fg > 0.0)) {
+            fnext = -1;
+          } else if (s_left[c] < 0) {
+            blocked = c;
+            bforced = 1;
+            break;
+          } else {
+            const int left = s_left[c];
+            if (lane == 0) {
+              s_c0[nc] = fl;
+              s_c1[nc] = ~c;
+              s_lcid[fl] = left;
+              s_lcid[nl] = left + 1;
+              s_st[c] |= kNodeCommitted;
+              const int fa = s_feat[left], fb = s_feat[left + 1];
+              s_lg[fl] = fa < 0 ? kMinScore : s_gain[left];
+              s_lf[fl] = fa < 0 ? 0x7fffffff : fa;
+              s_lg[nl] = fb < 0 ? kMinScore : s_gain[left + 1];
+              s_lf[nl] = fb < 0 ? 0x7fffffff : fb;
+            }
+            ++nc;
+            ++nl;
+            ++ns;
+            fnext = fnext + 1 < a.num_forced ? fnext + 1 : -1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            continue;
+          }
+        }
       }
       double bg = kMinScore;
       int bf = 0x7fffffff, bl = 0x7fffffff;
@@ -1217,6 +1328,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       s_done = done;
       s_blocked = blocked;
       s_ncommit = nc;
+      s_fnext = fnext;
+      s_bforced = bforced;
     }
   }
   __syncthreads();
@@ -1228,11 +1341,12 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
     for (int i = t; i < ncommit * kInfoWords; i += blockDim.x) {
       const int k = i / kInfoWords, j = i - k * kInfoWords;
+      const int c1 = s_c1[k];
       reinterpret_cast<uint32_t*>(&a.rec[st.num_splits + k].info)[j] =
-          reinterpret_cast<const uint32_t*>(a.best + s_c1[k])[j];
+          reinterpret_cast<const uint32_t*>(c1 >= 0 ? a.best + c1 : a.fbest + ~c1)[j];
     }
     for (int k = t; k < ncommit; k += blockDim.x) {
-      const int c = s_c1[k];
+      const int c = s_c1[k] >= 0 ? s_c1[k] : ~s_c1[k];
       const int left = s_left[c];
       SplitRec* r = a.rec + st.num_splits + k;
       r->leaf = s_c0[k];
@@ -1265,6 +1379,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         const uint8_t sc = s_st[c];
         alive = !(sc & kNodeCommitted) && s_feat[c] >= 0 && s_gain[c] > 0.0;
         elig = alive && !(sc & kNodeExpanded);
+        // while forced splits are pending, their nodes are expanded only by them (the blocked one)
+        if (elig && s_fnext >= 0 && s_fidx[c] >= 0 && c != s_blocked) elig = false;
         if (elig) {
           const int target = s_dep[c] + 1 - kFrontierBufs;
           if (target >= 1) {
@@ -1390,7 +1506,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         p = s_exp[lane];
         const int cpos = (p >= base && p - base < 2 * kFrontierKmax) ? s_cpos[p - base] : -1;
         nd = a.nodes[p];
-        kk = cpos >= 0 ? a.ckey[cpos] : a.key[p];
+        kk = p == s_blocked && s_bforced ? a.fkey[p] : (cpos >= 0 ? a.ckey[cpos] : a.key[p]);
         ntiles = max(1, (nd.count + kTile - 1) / kTile);
       }
       const int inc = WaveInclusiveScan(ntiles);
@@ -1417,7 +1533,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         x.skip = 0;
         x.smaller = x.larger = -1;
         x.h_buf = x.h_start = x.h_count = 0;
-        x.pad = 0;
+        x.forced = p == s_blocked && s_bforced ? s_fidx[p] : -1;
         a.exps[lane] = x;
         a.nodes[p].left = cid_next + 2 * lane;
         a.nstate[p] = s_st[p] | kNodeExpanded;
@@ -1441,6 +1557,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     ns_.num_splits = ns;
     ns_.done = done;
     ns_.blocked = s_blocked;
+    ns_.forced_next = s_fnext;
     if (!done) {
       ns_.k = s_k;
       ns_.total_tiles = s_tiles;
@@ -1560,7 +1677,7 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 }
 
 size_t FrontierSelectLds(int C, int L) {
-  return static_cast<size_t>(C) * (sizeof(double) + 5 * sizeof(int) + 1) + 64 +
+  return static_cast<size_t>(C) * (sizeof(double) + 6 * sizeof(int) + 1) + 64 +
          static_cast<size_t>(L) * (3 * sizeof(int) + sizeof(double) + sizeof(int)) + 64 +
          static_cast<size_t>(FrontierSortCap(C)) * (sizeof(double) + sizeof(int));
 }

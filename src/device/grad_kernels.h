@@ -44,7 +44,7 @@ struct RankKernelArgs {
   float2* gh = nullptr;
   // unbiased LambdaRank (rank_objective.hpp:554-591): score + bias[position] ranks the documents
   const int* positions = nullptr;  // per row, nullptr: no position bias
-  const float* pos_bias = nullptr;
+  const double* pos_bias = nullptr;  // learned position biases (fp64, as the reference's pos_biases_)
   // queries longer than kMaxDeviceQuery: their block works in global scratch
   int num_large = 0;
   const int* large_q = nullptr;          // the long queries
@@ -62,7 +62,7 @@ void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s);
 // per position d1 -= g, d2 -= h, cnt += 1, then bias += lr * (d1 - bias * reg * cnt) /
 // (|d2 - reg * cnt| + 0.001). `acc` holds 3 * num_pos int64 fixed-point sums.
 void LaunchPositionBiasUpdate(const float2* gh, const int* positions, int n, int num_pos, double lr, double reg,
-                              long long* acc, float* bias, hipStream_t s);
+                              long long* acc, double* bias, hipStream_t s);
 
 struct XendcgArgs {
   const int* qb = nullptr;  // query boundaries (num_queries + 1)

@@ -114,12 +114,17 @@ __device__ __forceinline__ float LamGet(unsigned long long v) {
   return static_cast<float>(static_cast<double>(static_cast<long long>(v)) * (1.0 / kLamScale));
 }
 
+struct LdsDiscount {
+  const double* tab;
+  __device__ double operator()(int r) const { return tab[r]; }
+};
+
 // LDS bytes of a block for queries of up to `max_cnt` documents (P = pow2 >= max_cnt)
 inline size_t RankLdsBytes(int max_cnt) {
   int P = 1;
   while (P < max_cnt) P <<= 1;
   return static_cast<size_t>(P) * (sizeof(double) + sizeof(int) + sizeof(float) + 2 * sizeof(unsigned long long)) +
-         static_cast<size_t>(P + 1) * sizeof(int);
+         static_cast<size_t>(P + 1) * (sizeof(int) + sizeof(double));
 }
 
 // kGlobal = false: one block per query, arrays in LDS sized by the dataset's largest query up
@@ -149,7 +154,9 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
   double* s_score = reinterpret_cast<double*>(base);
   unsigned long long* s_lam = reinterpret_cast<unsigned long long*>(s_score + Pa);
   unsigned long long* s_hes = s_lam + Pa;
-  int* s_idx = reinterpret_cast<int*>(s_hes + Pa);
+  // LDS launch: the query's rank discounts 1 / log2(2 + r), r <= cnt (RankDiscount)
+  double* s_disc = reinterpret_cast<double*>(s_hes + Pa);
+  int* s_idx = reinterpret_cast<int*>(kGlobal ? reinterpret_cast<double*>(s_hes + Pa) : s_disc + Pa + 1);
   float* s_lab = reinterpret_cast<float*>(s_idx + Pa);
   int* s_off = reinterpret_cast<int*>(s_lab + Pa);
   const bool full_sort = TargetNeedsFullSort(a.target) || a.target == kTgtPrecision;
@@ -162,6 +169,9 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
       s_hes[i] = 0ull;
     }
     s_idx[i] = i;
+  }
+  if (!kGlobal) {
+    for (int r = t; r <= cnt; r += blockDim.x) s_disc[r] = RankDiscount(r);
   }
   __syncthreads();
   // scores by original position; s_idx holds the ranking permutation
@@ -269,8 +279,10 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
     const int hl = static_cast<int>(s_lab[high]), ll = static_cast<int>(s_lab[low]);
     const double hg = hl < a.num_label_gain ? a.label_gain[hl] : 0.0;
     const double lg = ll < a.num_label_gain ? a.label_gain[ll] : 0.0;
-    double dp = TargetDeltaPair(a.target, i, j, hr, lr, hg, lg, s_lab[high], s_lab[low], inv_dcg, inv_bdcg, a.k,
-                                a.gap_weight);
+    double dp = kGlobal ? TargetDeltaPair(a.target, i, j, hr, lr, hg, lg, s_lab[high], s_lab[low], inv_dcg, inv_bdcg,
+                                          a.k, a.gap_weight)
+                        : TargetDeltaPairD(a.target, i, j, hr, lr, hg, lg, s_lab[high], s_lab[low], inv_dcg, inv_bdcg,
+                                           a.k, a.gap_weight, LdsDiscount{s_disc});
     if (dp == 0) continue;
     if (a.norm && best != worst) dp /= (0.01f + fabs(ds));
     double pl = TableSigmoid(a, ds);
@@ -441,7 +453,9 @@ __global__ __launch_bounds__(kWave) void k_metric_fold(const double* __restrict_
 
 // Position-bias statistics: per-position (-sum g, -sum h, count) as int64 fixed point
 // (order independent), then one block applies the Newton step.
-constexpr double kPosScale = 4294967296.0;  // 2^32
+// 2^24: a position's |sum| up to ~5e11 stays inside int64 (at 2^32 unnormalised lambdas of a
+// large dataset could approach the 2.1e9 limit)
+constexpr double kPosScale = 16777216.0;
 constexpr int kPosLds = 1024;
 
 __global__ __launch_bounds__(256) void k_pos_accum(const float2* __restrict__ gh, const int* __restrict__ positions, int n,
@@ -469,14 +483,14 @@ __global__ __launch_bounds__(256) void k_pos_accum(const float2* __restrict__ gh
 }
 
 __global__ __launch_bounds__(256) void k_pos_update(long long* __restrict__ acc, int num_pos, double lr, double reg,
-                                                    float* __restrict__ bias) {
+                                                    double* __restrict__ bias) {
   for (int p = threadIdx.x; p < num_pos; p += blockDim.x) {
     const double d1 = static_cast<double>(acc[3 * p]) / kPosScale;
     const double d2 = static_cast<double>(acc[3 * p + 1]) / kPosScale;
     const double cnt = static_cast<double>(acc[3 * p + 2]);
     const double av = d1 - bias[p] * reg * cnt;
     const double bv = d2 - reg * cnt;
-    bias[p] += static_cast<float>(lr * av / (fabs(bv) + 0.001));
+    bias[p] += lr * av / (fabs(bv) + 0.001);
     acc[3 * p] = acc[3 * p + 1] = acc[3 * p + 2] = 0;
   }
 }
@@ -501,7 +515,7 @@ void LaunchOvaGrad(int num_class, const PointwiseParams* params_dev, const doubl
 }
 
 void LaunchPositionBiasUpdate(const float2* gh, const int* positions, int n, int num_pos, double lr, double reg,
-                              long long* acc, float* bias, hipStream_t s) {
+                              long long* acc, double* bias, hipStream_t s) {
   if (n <= 0 || num_pos <= 0) return;
   k_pos_accum<<<std::min(GridFor(n), 1024), 256, 0, s>>>(gh, positions, n, num_pos, acc);
   HIP_CHECK(hipGetLastError());

@@ -434,7 +434,9 @@ void Dataset::Construct(const RowSource& src, const Config& cfg, const Dataset* 
   num_data_ = src.num_rows();
   num_total_features_ = src.num_cols();
   keep_raw_ = cfg.linear_tree || (reference != nullptr && reference->keep_raw_);
-  device_pack_ = (cfg.device_type == "gpu" || cfg.device_type == "cuda") && cfg.device_binning;
+  // device binning keeps its packed rows for the learner to adopt: training sets only (a
+  // validation set's rows are uploaded by DeviceAddValidSet, a kept copy would sit unused)
+  device_pack_ = (cfg.device_type == "gpu" || cfg.device_type == "cuda") && cfg.device_binning && reference == nullptr;
   if (reference != nullptr) {
     if (reference->num_total_features_ != num_total_features_) {
       Log::Fatal("The number of features in data (%d) is not the same as it was in training data (%d).",

@@ -5,6 +5,7 @@
 // second-order approximation), solved by Cholesky.
 #include <algorithm>
 #include <cmath>
+#include <unordered_map>
 
 #include "lgap/log.h"
 #include "parallel_tree_learner.h"
@@ -86,7 +87,13 @@ class LinearTreeLearner : public SerialTreeLearner {
       }
       std::sort(feats.begin(), feats.end());
       feats.erase(std::unique(feats.begin(), feats.end()), feats.end());
-      const std::vector<double> old_coef = tree->LeafCoeffs(l);
+      // old coefficients by real feature id (the rebuilt list may drop / reorder features)
+      std::unordered_map<int, double> old_by_feature;
+      {
+        const auto& of = tree->LeafFeatures(l);
+        const auto& oc = tree->LeafCoeffs(l);
+        for (size_t j = 0; j < of.size() && j < oc.size(); ++j) old_by_feature[of[j]] = oc[j];
+      }
       const double old_const = tree->LeafConst(l);
       std::vector<int> real(feats.size());
       for (size_t j = 0; j < feats.size(); ++j) real[j] = train_data_->feature(feats[j]).real_index;
@@ -96,7 +103,8 @@ class LinearTreeLearner : public SerialTreeLearner {
         tree->SetLeafConst(l, decay * old_const + (1.0 - decay) * tree->LeafOutput(l) * shrink);
       } else {
         for (size_t j = 0; j < feats.size(); ++j) {
-          const double o = j < old_coef.size() ? old_coef[j] : 0.0;
+          const auto it = old_by_feature.find(real[j]);
+          const double o = it != old_by_feature.end() ? it->second : 0.0;
           coef[j] = decay * o + (1.0 - decay) * z[j] * shrink;
         }
         tree->SetLeafConst(l, decay * old_const + (1.0 - decay) * z[feats.size()] * shrink);

@@ -5,6 +5,7 @@
 // feature sampling by tree / node, interaction constraints, forced splits,
 // refit and L1/quantile leaf renewal.
 #include "serial_tree_learner.h"
+#include "forced_splits.h"
 #include "lgap/omp_errors.h"
 
 #include <omp.h>
@@ -898,47 +899,7 @@ void SerialTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* ri
   }
 }
 
-// Forced splits from a JSON file: {"feature": f, "threshold": t, "left": {...}, "right": {...}}.
-namespace {
-struct ForcedNode {
-  int feature = -1;
-  double threshold = 0.0;
-  std::unique_ptr<ForcedNode> left, right;
-};
-std::unique_ptr<ForcedNode> ParseForced(const std::string& s, size_t* pos) {
-  auto skip = [&] { while (*pos < s.size() && std::isspace(static_cast<unsigned char>(s[*pos]))) ++*pos; };
-  skip();
-  if (*pos >= s.size() || s[*pos] != '{') return nullptr;
-  ++*pos;
-  auto node = std::make_unique<ForcedNode>();
-  while (*pos < s.size()) {
-    skip();
-    if (s[*pos] == '}') {
-      ++*pos;
-      break;
-    }
-    if (s[*pos] == ',') {
-      ++*pos;
-      continue;
-    }
-    size_t q1 = s.find('"', *pos), q2 = s.find('"', q1 + 1);
-    std::string key = s.substr(q1 + 1, q2 - q1 - 1);
-    *pos = s.find(':', q2) + 1;
-    skip();
-    if (key == "left" || key == "right") {
-      auto child = ParseForced(s, pos);
-      (key == "left" ? node->left : node->right) = std::move(child);
-    } else {
-      char* e;
-      double v = std::strtod(s.c_str() + *pos, &e);
-      *pos = e - s.c_str();
-      if (key == "feature") node->feature = static_cast<int>(v);
-      else if (key == "threshold") node->threshold = v;
-    }
-  }
-  return node;
-}
-}  // namespace
+// Forced splits from a JSON file: ForcedNode / ParseForced in learner/forced_splits.h.
 
 // reference gbdt.cpp CheckForcedSplitFeatures: every node's feature must exist in the data
 void SerialTreeLearner::CheckForcedSplitFeatures() const {

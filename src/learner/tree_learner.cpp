@@ -31,7 +31,12 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   // (voting runs on the device; its global pass redraws no extra-trees thresholds)
   if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
   if (CegbPenalty::Enabled(c)) return "cost-effective gradient boosting";
-  if (!c->forcedsplits_filename.empty()) return "forced splits";
+  // forced splits run on the device's frontier engine (serial learner); elsewhere on the host
+  if (!c->forcedsplits_filename.empty() &&
+      !(learner_type == "serial" && c->feature_fraction_bynode >= 1.0 && !c->extra_trees && c->num_leaves <= 512 &&
+        c->max_bin <= 1024)) {
+    return "forced splits";
+  }
   if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {
     return "intermediate/advanced monotone constraints";
   }

@@ -468,15 +468,57 @@ def test_host_policy_over_device_histograms(lgb, gpu_required, rng, extra):
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
 
 
+FORCED_TREES = [
+    {"feature": 4, "threshold": 0.1, "left": {"feature": 5, "threshold": -0.2}},
+    # two levels on both sides, children pushed left then right (breadth-first order)
+    {"feature": 0, "threshold": 0.0,
+     "left": {"feature": 1, "threshold": 0.3, "left": {"feature": 2, "threshold": -0.5}},
+     "right": {"feature": 3, "threshold": -0.1, "right": {"feature": 2, "threshold": 0.5}}},
+    # the left child's forced split cannot gain (every row goes left): forced splitting stops
+    # there and the right child's forced split is never applied
+    {"feature": 4, "threshold": 0.0, "left": {"feature": 5, "threshold": 1e9},
+     "right": {"feature": 3, "threshold": 0.2}},
+    # a node without a feature inside the tree: that node and its subtree are skipped
+    {"feature": 1, "threshold": 0.0, "left": {"threshold": 0.0, "left": {"feature": 0, "threshold": 0}},
+     "right": {"feature": 2, "threshold": 0.1}},
+]
+
+
+@pytest.mark.parametrize("case", range(len(FORCED_TREES)))
+def test_forced_splits_on_device(lgb, gpu_required, rng, tmp_path, case):
+    """Forced splits on the device-resident frontier engine (no host split policy): the select
+    applies the flattened forced list first, each forced split computed by the scan at its
+    threshold; the first tree matches the host learner split for split."""
+    import json
+
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    f = tmp_path / "forced.json"
+    f.write_text(json.dumps(FORCED_TREES[case]))
+    bc = _train(lgb, X, y, "cpu", rounds=3, forcedsplits_filename=str(f))
+    bg = _train(lgb, X, y, "gpu", rounds=3, gpu_use_dp=True, forcedsplits_filename=str(f))
+    assert "host split policy" not in bg.device_name() and "frontier engine" in bg.device_name()
+    for t in range(3):
+        tc, tg = _trees(bc)[t]["tree_structure"], _trees(bg)[t]["tree_structure"]
+        sc, sg = _splits(tc, []), _splits(tg, [])
+        assert [s[0] for s in sc] == [s[0] for s in sg], (t, sc[:6], sg[:6])
+        np.testing.assert_allclose([s[1] for s in sg], [s[1] for s in sc], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-4)
+
+
 def test_forced_splits_over_device_histograms(lgb, gpu_required, rng, tmp_path):
+    """Forced splits where the device frontier does not apply (feature_fraction_bynode): the
+    host split policy over HIP histograms."""
     import json
 
     X, z = _policy_data(rng)
     y = (z > 0).astype(float)
     f = tmp_path / "forced.json"
     f.write_text(json.dumps({"feature": 4, "threshold": 0.1, "left": {"feature": 5, "threshold": -0.2}}))
-    bc = _train(lgb, X, y, "cpu", rounds=2, forcedsplits_filename=str(f))
-    bg = _train(lgb, X, y, "gpu", rounds=2, gpu_use_dp=True, forcedsplits_filename=str(f))
+    kw = {"feature_fraction_bynode": 0.999, "forcedsplits_filename": str(f)}
+    bc = _train(lgb, X, y, "cpu", rounds=2, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=2, gpu_use_dp=True, **kw)
+    assert "host split policy" in bg.device_name()
     for b in (bc, bg):
         root = _trees(b)[0]["tree_structure"]
         assert root["split_feature"] == 4 and root["left_child"]["split_feature"] == 5

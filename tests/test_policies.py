@@ -247,3 +247,39 @@ def test_histogram_pool_size_bounds_cached_histograms(lgb, rng, pool_mb):
         Z[:, 0] = row[0]
         Z[:, 1] = grid
         assert np.all(np.diff(b.predict(Z)) <= 1e-10)
+
+
+def test_linear_tree_refit_keeps_coefficients_by_feature(lgb):
+    """Linear-tree refit matches each leaf's old coefficients to features by id
+    (linear_tree_learner.cpp; reference linear_tree_learner.cpp:357-363 blends old and new per
+    feature): with refit_decay_rate=1 every leaf keeps its own coefficients exactly."""
+    import json
+
+    rng = np.random.default_rng(5)
+    n = 4000
+    X = rng.standard_normal((n, 3))
+    y = 2.0 * X[:, 0] - 3.0 * X[:, 1] + 0.5 * X[:, 2] + 0.05 * rng.standard_normal(n)
+    params = {"objective": "regression", "linear_tree": True, "num_leaves": 4, "verbosity": -1, "seed": 1,
+              "refit_decay_rate": 1.0}
+    b = lgb.train(params, lgb.Dataset(X, y), 3)
+    X2 = X + 0.01 * rng.standard_normal(X.shape)
+    r = b.refit(X2, y, decay_rate=1.0)
+
+    def coefs(booster):
+        out = {}
+        for ti, t in enumerate(booster.dump_model()["tree_info"]):
+            stack = [t["tree_structure"]]
+            while stack:
+                nd = stack.pop()
+                if "split_index" in nd:
+                    stack += [nd["left_child"], nd["right_child"]]
+                else:
+                    for f, c in zip(nd.get("leaf_features", []), nd.get("leaf_coeff", [])):
+                        out[(ti, nd["leaf_index"], f)] = c
+        return out
+
+    old, new = coefs(b), coefs(r)
+    assert old, "the model has linear leaves"
+    assert set(new) == set(old)
+    for key, c in new.items():
+        assert c == pytest.approx(old[key], rel=1e-12, abs=1e-12), (key, c, old[key])
