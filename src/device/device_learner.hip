@@ -3216,6 +3216,12 @@ class DeviceTreeLearner : public TreeLearner {
                          reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
       return;
     }
+    if (nib_ && rowbins == rowbins_.get() && n == N_) {
+      LaunchTraverse(rowbins4_.get(), stride4_dw_, 0, n, reinterpret_cast<const TNode*>(db), nn,
+                     reinterpret_cast<const TCat*>(db + node_bytes), reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
+                     reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
+      return;
+    }
     LaunchTraverse(rowbins, stride_dw_, width_, n, reinterpret_cast<const TNode*>(db), nn,
                    reinterpret_cast<const TCat*>(db + node_bytes), reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                    reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
@@ -3582,6 +3588,12 @@ class DeviceTreeLearner : public TreeLearner {
     a.hist_min_rows = HistMinRows();
     a.hist_grid = FrontierHistBlocks();
     a.hist_threads = fhist_threads_;
+    if (nib_) {
+      a.rowbins = rowbins4_.get();
+      a.stride_dw = stride4_dw_;
+      a.tiles = ntile_.get();
+      a.hist_nib = 1;
+    }
     a.debug_noflush = std::getenv("LGAP_DEBUG_NOFLUSH") != nullptr ? 1 : 0;
     {
       const char* e = std::getenv("LGAP_FLUSH_ROT");
@@ -4346,6 +4358,7 @@ class DeviceTreeLearner : public TreeLearner {
     for (int g = 0; g < G_; ++g) gs[g] = data_->group(g).hist_start;
     h_gstart_ = gs;
     BuildTiles();
+    BuildNibbleRows();
     // labels / weights for the device objectives are uploaded lazily
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
@@ -4366,6 +4379,30 @@ class DeviceTreeLearner : public TreeLearner {
       big_tiles_ = true;
       PlanTiles(150 * 1024);
     }
+  }
+
+  // 4-bit rows for the frontier histograms and the training score update: 8-bit data whose
+  // every group has <= 16 bins (max_bin <= 15, no wide bundles) in one LDS tile. The 8-bit
+  // rows stay for everything else (validation sets, the sequential chain, device binning).
+  void BuildNibbleRows() {
+    nib_ = false;
+    const char* e = std::getenv("LGAP_NIBBLE");  // A/B knob: 0 keeps 8-bit rows
+    if (e != nullptr && e[0] == '0') return;
+    if (width_ != 1 || num_tiles_ != 1 || G_ <= 0 || N_ <= 0 || h_tiles_.empty() || h_tiles_[0].direct) return;
+    for (int g = 0; g < G_; ++g) {
+      if (data_->group(g).num_bin > 16) return;
+    }
+    stride4_dw_ = DivUp(G_, 8);
+    rowbins4_.Resize(static_cast<size_t>(N_) * stride4_dw_);
+    LaunchPackNibbles(rowbins_.get(), stride_dw_, N_, G_, rowbins4_.get(), stride4_dw_, stream_);
+    HistTile t = h_tiles_[0];
+    t.d0 = 0;
+    t.d1 = stride4_dw_;
+    ntile_.Resize(1);
+    ntile_.Upload(&t, 1, stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    nib_ = true;
+    Log::Debug("HIP learner: 4-bit rows (%d dwords per row instead of %d)", stride4_dw_, stride_dw_);
   }
 
   void PlanTiles(int lds_budget) {
@@ -4412,6 +4449,7 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(hist_lds_bytes_)));
     }
     num_tiles_ = static_cast<int>(tiles.size());
+    nib_ = false;
     min_tile_dw_ = 1 << 30;
     for (size_t i = 0; i + 1 < tiles.size(); ++i) min_tile_dw_ = std::min(min_tile_dw_, tiles[i].d1 - tiles[i].d0);
     h_tiles_ = tiles;
@@ -4886,6 +4924,10 @@ class DeviceTreeLearner : public TreeLearner {
   // frontier engine (frontier.h)
   bool frontier_ = false;
   int fhist_threads_ = 512;
+  bool nib_ = false;             // 4-bit rows built (BuildNibbleRows)
+  int stride4_dw_ = 0;
+  DevBuf<uint32_t> rowbins4_;
+  DevBuf<HistTile> ntile_;
   bool big_tiles_ = false;  // BuildTiles chose 150 KB LDS tiles (wide rows)
   int min_tile_dw_ = 0;
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;

@@ -173,6 +173,7 @@ struct FArgs {
   int hist_threads;  // 512 or 1024 threads per histogram block
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
+  int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)
   int part_tile;  // rows per partition tile (256 x rows per thread)
   int max_depth, use_monotone;
   double monotone_penalty;

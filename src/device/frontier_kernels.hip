@@ -163,7 +163,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   const int myr = threadIdx.x / tpr;
   const int myd = threadIdx.x - myr * tpr;
   if (myr >= rpi) return;
-  constexpr int per = 4 / W;
+  constexpr int per = W == 0 ? 8 : 4 / W;  // W = 0: 4-bit rows (8 groups per dword)
   constexpr int R = LGAP_FHIST_R;
   const int dw = tile.d0 + myd;
   const int gfirst = dw * per;
@@ -209,7 +209,9 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
       }
 #pragma unroll
       for (int k = 0; k < per; ++k) {
-        const uint32_t b = W == 1 ? ((word[j] >> (8 * k)) & 0xFFu) : ((word[j] >> (16 * k)) & 0xFFFFu);
+        const uint32_t b = W == 0   ? ((word[j] >> (4 * k)) & 0xFu)
+                           : W == 1 ? ((word[j] >> (8 * k)) & 0xFFu)
+                                    : ((word[j] >> (16 * k)) & 0xFFFFu);
         if (b != 0u && go[k] >= 0) {
           const int o = go[k] + static_cast<int>(b);
           if (MODE == 3) {
@@ -291,7 +293,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     const int rpi = blockDim.x / tpr;
     const int myr = t / tpr, myd = t - myr * tpr;
     if (myr >= rpi) return;
-    constexpr int per = 4 / W;
+    constexpr int per = W == 0 ? 8 : 4 / W;
     const int dw = tile.d0 + myd;
     const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
     for (int p = rb + myr; p < re; p += rpi) {
@@ -310,7 +312,9 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       }
 #pragma unroll
       for (int kk = 0; kk < per; ++kk) {
-        const uint32_t b = W == 1 ? ((word >> (8 * kk)) & 0xFFu) : ((word >> (16 * kk)) & 0xFFFFu);
+        const uint32_t b = W == 0   ? ((word >> (4 * kk)) & 0xFu)
+                           : W == 1 ? ((word >> (8 * kk)) & 0xFFu)
+                                    : ((word >> (16 * kk)) & 0xFFFFu);
         const int g = dw * per + kk;
         if (b != 0u && g < tile.g1) {
           const int o = gst[g - tile.g0] + static_cast<int>(b);
@@ -1649,7 +1653,13 @@ template <int THREADS>
 void LaunchHistT(const FArgs& a, size_t lds, hipStream_t s) {
   // working blocks <= max(hist_grid, ceil(hist_grid / 2) + ke): see the chunking in k_f_hist
   const dim3 grid(std::max(a.hist_grid, a.hist_grid / 2 + a.hist_grid % 2 + a.kmax), a.num_tiles);
-  if (a.quant && a.qsub > 0) {
+  if (a.hist_nib) {
+    // 4-bit rows (every group <= 16 bins, one LDS tile)
+    if (a.quant && a.qsub > 0) k_f_hist<0, 3, THREADS><<<grid, THREADS, lds, s>>>(a);
+    else if (a.quant) k_f_hist<0, 2, THREADS><<<grid, THREADS, lds, s>>>(a);
+    else if (a.use_dp) k_f_hist<0, 1, THREADS><<<grid, THREADS, lds, s>>>(a);
+    else k_f_hist<0, 0, THREADS><<<grid, THREADS, lds, s>>>(a);
+  } else if (a.quant && a.qsub > 0) {
     if (a.width == 1) k_f_hist<1, 3, THREADS><<<grid, THREADS, lds, s>>>(a);
     else k_f_hist<2, 3, THREADS><<<grid, THREADS, lds, s>>>(a);
   } else if (a.quant) {
@@ -1707,7 +1717,11 @@ void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
   (void)use_dp;
   (void)width;
   if (hist_lds > 64 * 1024) {
-    const void* fns[16] = {
+    const void* fns[24] = {
+        reinterpret_cast<const void*>(k_f_hist<0, 0, 512>),  reinterpret_cast<const void*>(k_f_hist<0, 1, 512>),
+        reinterpret_cast<const void*>(k_f_hist<0, 2, 512>),  reinterpret_cast<const void*>(k_f_hist<0, 3, 512>),
+        reinterpret_cast<const void*>(k_f_hist<0, 0, 1024>), reinterpret_cast<const void*>(k_f_hist<0, 1, 1024>),
+        reinterpret_cast<const void*>(k_f_hist<0, 2, 1024>), reinterpret_cast<const void*>(k_f_hist<0, 3, 1024>),
         reinterpret_cast<const void*>(k_f_hist<1, 3, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 3, 512>),
         reinterpret_cast<const void*>(k_f_hist<1, 3, 1024>), reinterpret_cast<const void*>(k_f_hist<2, 3, 1024>),
         reinterpret_cast<const void*>(k_f_hist<1, 0, 512>),  reinterpret_cast<const void*>(k_f_hist<2, 0, 512>),

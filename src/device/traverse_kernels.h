@@ -35,6 +35,13 @@ struct TCat {
 constexpr uint8_t kTOutLeft = 1, kTDefaultLeft = 2, kTCat = 4;
 
 // score[i] += value of row i's leaf, rows [0, n) of the packed matrix (stride_dw dwords/row)
+// 4-bit copy of 8-bit packed rows whose every group has <= 16 bins (max_bin <= 15 data):
+// out[row * stride4 + d] holds groups 8d..8d+7 as nibbles (reference dense_bin.hpp:18-97
+// IS_4BIT). Read by the frontier histograms (hist_nib) and the training score update (width 0).
+void LaunchPackNibbles(const uint32_t* rowbins, int stride_dw, int n, int groups, uint32_t* out, int stride4,
+                       hipStream_t s);
+
+// width: 0 = 4-bit rows, 1 = 8-bit, 2 = 16-bit group bins
 void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
                     const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,
                     int num_cu, hipStream_t s);

@@ -20,6 +20,7 @@ constexpr int kTMaxDw = 16;  // wider rows read global memory directly
 
 template <int W>
 __device__ __forceinline__ uint32_t GroupBin(const uint8_t* row, int g) {
+  if (W == 0) return (row[g >> 1] >> ((g & 1) * 4)) & 0xFu;  // 4-bit rows
   return W == 1 ? row[g] : reinterpret_cast<const uint16_t*>(row)[g];
 }
 
@@ -155,7 +156,34 @@ __global__ __launch_bounds__(kTThreads) void k_traverse_col(const uint8_t* __res
   }
 }
 
+__global__ __launch_bounds__(256) void k_pack_nibbles(const uint32_t* __restrict__ rowbins, int stride_dw, int n,
+                                                      int groups, uint32_t* __restrict__ out, int stride4) {
+  const long long total = static_cast<long long>(n) * stride4;
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long row = i / stride4;
+    const int d = static_cast<int>(i - row * stride4);
+    const uint32_t* r = rowbins + row * stride_dw;
+    uint32_t v = 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int g = 8 * d + k;
+      if (g < groups) v |= ((r[g >> 2] >> (8 * (g & 3))) & 0xFu) << (4 * k);
+    }
+    out[i] = v;
+  }
+}
+
 }  // namespace
+
+void LaunchPackNibbles(const uint32_t* rowbins, int stride_dw, int n, int groups, uint32_t* out, int stride4,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  const long long total = static_cast<long long>(n) * stride4;
+  const int grid = static_cast<int>(std::max<long long>(1, std::min<long long>((total + 255) / 256, 8192)));
+  k_pack_nibbles<<<grid, 256, 0, s>>>(rowbins, stride_dw, n, groups, out, stride4);
+  HIP_CHECK(hipGetLastError());
+}
 
 void LaunchTraverseCols(const uint8_t* colbins, int width, int n, const TNode* nodes, int num_nodes, const TCat* cats,
                         const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score, int num_cu,
@@ -180,7 +208,10 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
   const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + sizeof(double) * num_leaves +
                      (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
   const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
-  if (width == 1) {
+  if (width == 0) {
+    k_traverse<0><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                              num_leaves, score);
+  } else if (width == 1) {
     k_traverse<1><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
                                               num_leaves, score);
   } else {

@@ -797,6 +797,25 @@ def test_frontier_engine_matches_sequential_chain(lgb, gpu_required, rng, extra)
     assert structure(outs[0]["model"]) == structure(outs[1]["model"])
 
 
+@pytest.mark.parametrize("max_bin", [15, 7])
+def test_four_bit_rows_match_byte_rows(lgb, gpu_required, rng, monkeypatch, max_bin):
+    """max_bin <= 15: the frontier histograms and the training score update read 4-bit rows
+    (8 groups per dword, traverse_kernels.hip LaunchPackNibbles); the model is identical to the
+    one grown from the 8-bit rows (LGAP_NIBBLE=0), trees and training predictions."""
+    n = 30000
+    X = rng.standard_normal((n, 11))
+    X[rng.random(n) < 0.05, 3] = np.nan
+    y = (X[:, 0] - 0.6 * X[:, 1] + 0.4 * X[:, 2] * X[:, 4] + 0.3 * rng.standard_normal(n) > 0).astype(float)
+    params = {"objective": "binary", "num_leaves": 31, "max_bin": max_bin, "device_type": "gpu", "verbosity": -1}
+    models = []
+    for nib in ("1", "0"):
+        monkeypatch.setenv("LGAP_NIBBLE", nib)
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 10)
+        models.append((b.model_to_string().split("end of trees")[0], b.predict(X, raw_score=True)))
+    assert models[0][0] == models[1][0]
+    np.testing.assert_array_equal(models[0][1], models[1][1])
+
+
 def test_wide_rows_training_score(lgb, gpu_required, rng):
     """Rows wider than 16 dwords (120 features): the training score update walks the group-major
     copy (traverse_kernels.hip, k_traverse_col); the boosted model tracks the CPU learner's."""
