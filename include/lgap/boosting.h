@@ -117,6 +117,7 @@ class GBDT {
   virtual bool NeedAccuratePrediction() const { return objective() == nullptr || objective()->NeedAccuratePrediction(); }
   int GetCurrentIteration() const { return static_cast<int>(models_.size()) / std::max(1, num_tree_per_iteration_); }
   int MaxFeatureIdx() const { return max_feature_idx_; }
+  const std::string& parser_config() const { return parser_config_str_; }
   const std::vector<std::string>& FeatureNames() const { return feature_names_; }
   std::vector<std::string>& MutableFeatureNames() { return feature_names_; }
   double GetLeafValue(int tree, int leaf) const { return models_[tree]->LeafOutput(leaf); }

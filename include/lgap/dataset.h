@@ -120,6 +120,9 @@ class Dataset {
 
   void SaveBinary(const std::string& filename) const;
   static std::unique_ptr<Dataset> LoadBinary(const std::string& filename);
+  // custom parser config (parser_config_file) the rows were parsed with; kept in the model
+  const std::string& parser_config() const { return parser_config_; }
+  void set_parser_config(const std::string& c) { parser_config_ = c; }
   // in-memory form of the binary file (LGBM_DatasetSerializeReferenceToBinary)
   void SerializeBinary(std::vector<char>* out) const;
   static std::unique_ptr<Dataset> DeserializeBinary(const char* data, size_t size);
@@ -224,6 +227,7 @@ class Dataset {
   data_size_t num_data_ = 0;
   int num_total_features_ = 0;
   std::vector<std::string> feature_names_;
+  std::string parser_config_;
   std::vector<BinMapper> mappers_;  // per real feature
   std::vector<int> used_map_;       // real -> inner or -1
   std::vector<FeatureInfo> features_;

@@ -39,6 +39,7 @@ void GBDT::Init(const Config* config, const Dataset* train_data, const Objective
                 const std::vector<const Metric*>& training_metrics) {
   config_ = config;
   train_data_ = train_data;
+  if (train_data != nullptr && !train_data->parser_config().empty()) parser_config_str_ = train_data->parser_config();
   objective_ = objective;
   iter_ = 0;
   num_class_ = config->num_class;

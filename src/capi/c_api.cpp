@@ -4,6 +4,7 @@
 #include "lgap/omp_errors.h"
 #include "lgap/threading.h"
 #include "lgap/c_api.h"
+#include "lgap/parser.h"
 
 #include <omp.h>
 
@@ -896,11 +897,28 @@ int LGBM_BoosterPredictForFile(BoosterHandle handle, const char* data_filename, 
   int label_idx = 0;
   Config pc = ParseConfig(parameter);
   if (!pc.label_column.empty() && !common::StartsWith(pc.label_column, "name:")) label_idx = common::AtoiOrDie(pc.label_column);
-  ParseTextFile(data_filename, data_has_header != 0, label_idx, &rows, &labels, nullptr, nullptr, {}, -1, nullptr, -1,
-                nullptr);
-  // a file without the label column has one fewer column than the model: shift back in that case
   const int nf = b->boosting_->MaxFeatureIdx() + 1;
-  if (rows.ncol == nf - 1 && label_idx == 0) {
+  const std::string& parser_cfg = b->boosting_->parser_config();
+  if (!parser_cfg.empty()) {
+    // the model was trained on rows of a custom parser: predict through the same class
+    auto parser = CreateCustomParser(parser_cfg);
+    std::ifstream in(data_filename);
+    std::string line;
+    if (data_has_header) std::getline(in, line);
+    while (std::getline(in, line)) {
+      if (!line.empty() && line.back() == '\r') line.pop_back();
+      rows.rows.emplace_back();
+      double lab = 0.0;
+      parser->ParseOneLine(line.c_str(), &rows.rows.back(), &lab);
+      labels.push_back(static_cast<float>(lab));
+    }
+    rows.ncol = nf;
+  } else {
+    ParseTextFile(data_filename, data_has_header != 0, label_idx, &rows, &labels, nullptr, nullptr, {}, -1, nullptr, -1,
+                  nullptr);
+  }
+  // a file without the label column has one fewer column than the model: shift back in that case
+  if (parser_cfg.empty() && rows.ncol == nf - 1 && label_idx == 0) {
     for (auto& r : rows.rows) {
       for (auto& kv : r) kv.first += 1;
     }

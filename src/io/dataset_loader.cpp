@@ -17,6 +17,8 @@
 #include "lgap/log.h"
 #include "lgap/random.h"
 
+#include "lgap/parser.h"
+
 namespace lgap {
 
 namespace {
@@ -411,7 +413,7 @@ std::unique_ptr<Dataset> LoadDatasetFromFile(const std::string& filename, const 
   std::vector<int> ignore = common::StartsWith(cfg.ignore_column, "name:")
                                 ? ResolveColumnList(cfg.ignore_column, feat_names)
                                 : ResolveColumnList(cfg.ignore_column, {});
-  if (cfg.two_round) {
+  if (cfg.two_round && cfg.parser_config_file.empty()) {
     TwoRoundSpec sp;
     sp.label_idx = label_idx;
     sp.weight_idx = weight_idx;
@@ -435,8 +437,38 @@ std::unique_ptr<Dataset> LoadDatasetFromFile(const std::string& filename, const 
   OwnedSparseSource rows;
   std::vector<float> labels, weights;
   std::vector<double> gids;
-  ParseTextFile(filename, cfg.header, label_idx, &rows, &labels, nullptr, nullptr, ignore, weight_idx, &weights,
-                group_idx, &gids);
+  // custom parser plugin (parser_config_file): every line through the registered class
+  const std::string parser_cfg = cfg.parser_config_file.empty()
+                                     ? std::string()
+                                     : GenerateParserConfigStr(filename, cfg.parser_config_file, cfg.header, label_idx);
+  if (!parser_cfg.empty()) {
+    auto parser = CreateCustomParser(parser_cfg);
+    auto lines = ReadAllLines(filename);
+    const size_t first = cfg.header && !lines.empty() ? 1 : 0;
+    const size_t nl = lines.size() - first;
+    rows.rows.assign(nl, {});
+    labels.assign(nl, 0.0f);
+    std::vector<int> maxcol(omp_get_max_threads(), -1);
+    OmpErrors errs;
+#pragma omp parallel for schedule(static, 1024)
+    for (size_t r = 0; r < nl; ++r) {
+      errs.Run([&] {
+        double lab = 0.0;
+        parser->ParseOneLine(lines[first + r].c_str(), &rows.rows[r], &lab);
+        labels[r] = static_cast<float>(lab);
+        int& m = maxcol[omp_get_thread_num()];
+        for (const auto& kv : rows.rows[r]) m = std::max(m, kv.first);
+      });
+    }
+    errs.Rethrow();
+    int mc = std::max(-1, parser->NumFeatures() - 1);
+    for (int m : maxcol) mc = std::max(mc, m);
+    rows.ncol = mc + 1;
+    weight_idx = group_idx = -1;
+  } else {
+    ParseTextFile(filename, cfg.header, label_idx, &rows, &labels, nullptr, nullptr, ignore, weight_idx, &weights,
+                  group_idx, &gids);
+  }
   if (reference) rows.ncol = std::max(rows.ncol, reference->num_total_features());
   data_size_t n = static_cast<data_size_t>(rows.rows.size());
 
@@ -495,6 +527,7 @@ std::unique_ptr<Dataset> LoadDatasetFromFile(const std::string& filename, const 
   if (weight_idx >= 0) ds->metadata().SetWeights(weights.data(), n);
   if (!qb.empty()) ds->metadata().SetQueryBoundaries(qb);
   if (num_machines <= 1 || cfg.pre_partition) ds->metadata().LoadSideFiles(filename);
+  ds->set_parser_config(parser_cfg);
   Log::Info("Loaded %d rows x %d features from %s", n, ds->num_total_features(), filename.c_str());
   if (cfg.save_binary) ds->SaveBinary(filename + ".bin");
   return ds;
