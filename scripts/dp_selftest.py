@@ -36,14 +36,19 @@ def main() -> int:
     params = {"objective": "binary", "num_leaves": 31, "device_type": "gpu", "verbosity": -1, "seed": 1,
               "min_data_in_leaf": 20}
     out = {}
-    for mode in ("single", "dp"):
-        os.environ["LGAP_FORCE_DEVICE_DP"] = "1" if mode == "dp" else "0"
+    for mode in ("single", "dp", "dp_serial"):
+        os.environ["LGAP_FORCE_DEVICE_DP"] = "0" if mode == "single" else "1"
+        # dp: RCCL exchange pipelined with the histogram / scan halves (frontier engine);
+        # dp_serial: LGAP_DP_PIPELINE=0, the same exchange in series on the compute stream
+        os.environ["LGAP_DP_PIPELINE"] = "0" if mode == "dp_serial" else "1"
         b = lgb.train(params, lgb.Dataset(X, y, params=params), 8, keep_training_booster=True)
         out[mode] = b
     pa, pb = out["single"].predict(X), out["dp"].predict(X)
     ta = [t["tree_structure"].get("split_feature") for t in out["single"].dump_model()["tree_info"]]
     tb = [t["tree_structure"].get("split_feature") for t in out["dp"].dump_model()["tree_info"]]
+    pc = out["dp_serial"].predict(X)
     print(json.dumps({"max_abs_diff": float(np.max(np.abs(pa - pb))), "root_features_equal": ta == tb,
+                      "pipeline_vs_serial_equal": bool(np.array_equal(pb, pc)),
                       "dp_path": "data-parallel" in out["dp"].device_name(),
                       "dp_name": out["dp"].device_name(),
                       "single_path": "parallel" not in out["single"].device_name(),

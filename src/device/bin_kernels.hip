@@ -6,7 +6,9 @@
 // include/LightGBM/bin.h:612-650: NaN / zero handling, binary search over the upper
 // bounds, categorical lookup) and the bundle packing of Dataset::PackRows (reference
 // src/io/dataset.cpp:325-441) — runs here, one thread per (row, group), so a row's
-// group bytes are written by consecutive lanes. Bundled features are applied in
+// group bytes are written by consecutive lanes; rows are staged through LDS in tiles with
+// coalesced loads (k_pack_tiles), and chunk k + 1 of the matrix uploads on a copy stream
+// while chunk k packs. Bundled features are applied in
 // ascending column order with the host's rule (a value whose encoded bin is the
 // group's zero only writes when its feature owns the group's default), so the
 // result is bit-identical to the host packer.
@@ -103,6 +105,72 @@ __global__ __launch_bounds__(256) void k_pack_rows(const T* __restrict__ x, int 
   }
 }
 
+// The same packing over row tiles staged in LDS: a block loads `R` consecutive rows of the
+// input matrix with coalesced 16-byte loads (the per-(row, group) kernel above reads each
+// row's columns at a stride of ncol elements, one scattered access per value), then packs
+// (row, group) items from LDS. R * ncol * sizeof(T) <= kPackTileBytes.
+constexpr int kPackTileBytes = 48 * 1024;
+
+template <typename T, int W>
+__global__ __launch_bounds__(256) void k_pack_tiles(const T* __restrict__ x, int nrow, int ncol, int num_groups, int R,
+                                                    const BinGroup* __restrict__ groups, const BinFeat* __restrict__ feats,
+                                                    const double* __restrict__ bounds, const int* __restrict__ lut,
+                                                    int stride, uint8_t* __restrict__ out) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  T* tile = reinterpret_cast<T*>(lds_raw);
+  const int t = threadIdx.x;
+  for (long long r0 = static_cast<long long>(blockIdx.x) * R; r0 < nrow; r0 += static_cast<long long>(gridDim.x) * R) {
+    const int rows = static_cast<int>(min(static_cast<long long>(R), nrow - r0));
+    const long long n = static_cast<long long>(rows) * ncol;
+    const T* src = x + r0 * ncol;
+    __syncthreads();  // the previous tile's items are packed
+    constexpr int per = 16 / sizeof(T);
+    const long long head = (reinterpret_cast<uintptr_t>(src) & 15u) == 0 ? n / per : 0;
+    for (long long i = t; i < head; i += 256) reinterpret_cast<uint4*>(tile)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (long long i = head * per + t; i < n; i += 256) tile[i] = src[i];
+    __syncthreads();
+    const int items = rows * num_groups;
+    for (int it = t; it < items; it += 256) {
+      const int row = it / num_groups;
+      const int g = it - row * num_groups;
+      const BinGroup gr = groups[g];
+      int gb = gr.tmpl;
+      const T* xr = tile + static_cast<size_t>(row) * ncol;
+      for (int k = 0; k < gr.count; ++k) {
+        const BinFeat f = feats[gr.first + k];
+        const double v = static_cast<double>(xr[f.col]);
+        if (!(v != v || fabs(v) > kZeroThreshold)) continue;
+        const uint32_t b = DevValueToBin(f, bounds, lut, v);
+        const int e = b == static_cast<uint32_t>(f.mfb) ? 0 : f.offset + static_cast<int>(b) - (b > static_cast<uint32_t>(f.mfb) ? 1 : 0);
+        if (e == 0 && !f.owner) continue;
+        gb = e;
+      }
+      uint8_t* o = out + static_cast<size_t>(r0 + row) * stride;
+      if (W == 1) o[g] = static_cast<uint8_t>(gb);
+      else reinterpret_cast<uint16_t*>(o)[g] = static_cast<uint16_t>(gb);
+    }
+  }
+}
+
+template <typename T>
+void LaunchPack(const T* x, int rows, int ncol, int G, int W, const BinGroup* groups, const BinFeat* feats,
+                const double* bounds, const int* lut, int stride, uint8_t* dst, int num_cu, hipStream_t s) {
+  const size_t row_bytes = sizeof(T) * static_cast<size_t>(ncol);
+  if (row_bytes <= static_cast<size_t>(kPackTileBytes)) {
+    const int R = static_cast<int>(std::min<size_t>(1024, kPackTileBytes / row_bytes));
+    const size_t lds = row_bytes * R;
+    const int grid = std::max(1, std::min(DivUp(rows, R), num_cu * 4));
+    if (W == 1) k_pack_tiles<T, 1><<<grid, 256, lds, s>>>(x, rows, ncol, G, R, groups, feats, bounds, lut, stride, dst);
+    else k_pack_tiles<T, 2><<<grid, 256, lds, s>>>(x, rows, ncol, G, R, groups, feats, bounds, lut, stride, dst);
+  } else {
+    const long long work = static_cast<long long>(rows) * G;
+    const int grid = static_cast<int>(std::max<long long>(1, std::min<long long>(65536, (work + 255) / 256)));
+    if (W == 1) k_pack_rows<T, 1><<<grid, 256, 0, s>>>(x, rows, ncol, G, groups, feats, bounds, lut, stride, dst);
+    else k_pack_rows<T, 2><<<grid, 256, 0, s>>>(x, rows, ncol, G, groups, feats, bounds, lut, stride, dst);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
 // padding bytes of each packed row (stride beyond num_groups * width) are zero
 __global__ void k_zero_pad(uint8_t* out, int nrow, int stride, int used) {
   const int pad = stride - used;
@@ -188,8 +256,15 @@ bool DevicePackDense(const Dataset& ds, const void* data, bool f64, int nrow, in
   if (feats.empty()) feats.resize(1);
   if (bounds.empty()) bounds.resize(1);
   if (lut.empty()) lut.resize(1);
-  hipStream_t s;
+  // two streams: chunk k + 1 uploads (copy stream) while chunk k packs (compute stream)
+  hipStream_t s, cs;
   HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  hipEvent_t up[2], packed[2];
+  for (int i = 0; i < 2; ++i) {
+    HIP_CHECK(hipEventCreateWithFlags(&up[i], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&packed[i], hipEventDisableTiming));
+  }
   DevBuf<BinGroup> d_groups;
   DevBuf<BinFeat> d_feats;
   DevBuf<double> d_bounds;
@@ -201,30 +276,34 @@ bool DevicePackDense(const Dataset& ds, const void* data, bool f64, int nrow, in
   const size_t out_bytes = static_cast<size_t>(nrow) * stride;
   void* d_out = nullptr;
   HIP_CHECK(hipMalloc(&d_out, std::max<size_t>(out_bytes, 1)));
-  // the matrix in row chunks of <= 1 GiB
+  int dev = 0, num_cu = 256;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  // the matrix in row chunks of <= 256 MiB, double-buffered
   const size_t es = f64 ? 8 : 4;
   const size_t row_bytes = es * static_cast<size_t>(ncol);
-  const int chunk = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nrow, (size_t(1) << 30) / std::max<size_t>(row_bytes, 1))));
-  // (one stream: each chunk's upload follows the previous chunk's kernel)
+  const int chunk = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nrow, (size_t(256) << 20) / std::max<size_t>(row_bytes, 1))));
   DevBuf<char> d_in[2];
   d_in[0].Resize(row_bytes * chunk);
   if (nrow > chunk) d_in[1].Resize(row_bytes * chunk);
-  int slot = 0;
-  for (int r0 = 0; r0 < nrow; r0 += chunk, slot ^= 1) {
+  int slot = 0, n_chunk = 0;
+  for (int r0 = 0; r0 < nrow; r0 += chunk, slot ^= 1, ++n_chunk) {
     const int rows = std::min(chunk, nrow - r0);
     const char* src = static_cast<const char*>(data) + row_bytes * r0;
-    HIP_CHECK(hipMemcpyAsync(d_in[slot].get(), src, row_bytes * rows, hipMemcpyHostToDevice, s));
+    // the slot's previous chunk must be packed before it is overwritten
+    if (n_chunk >= 2) HIP_CHECK(hipStreamWaitEvent(cs, packed[slot], 0));
+    HIP_CHECK(hipMemcpyAsync(d_in[slot].get(), src, row_bytes * rows, hipMemcpyHostToDevice, cs));
+    HIP_CHECK(hipEventRecord(up[slot], cs));
+    HIP_CHECK(hipStreamWaitEvent(s, up[slot], 0));
     uint8_t* dst = static_cast<uint8_t*>(d_out) + static_cast<size_t>(r0) * stride;
-    const long long work = static_cast<long long>(rows) * G;
-    const int grid = static_cast<int>(std::max<long long>(1, std::min<long long>(65536, (work + 255) / 256)));
     if (f64) {
-      if (W == 1) k_pack_rows<double, 1><<<grid, 256, 0, s>>>(reinterpret_cast<const double*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
-      else k_pack_rows<double, 2><<<grid, 256, 0, s>>>(reinterpret_cast<const double*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
+      LaunchPack(reinterpret_cast<const double*>(d_in[slot].get()), rows, ncol, G, W, d_groups.get(), d_feats.get(),
+                 d_bounds.get(), d_lut.get(), stride, dst, num_cu, s);
     } else {
-      if (W == 1) k_pack_rows<float, 1><<<grid, 256, 0, s>>>(reinterpret_cast<const float*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
-      else k_pack_rows<float, 2><<<grid, 256, 0, s>>>(reinterpret_cast<const float*>(d_in[slot].get()), rows, ncol, G, d_groups.get(), d_feats.get(), d_bounds.get(), d_lut.get(), stride, dst);
+      LaunchPack(reinterpret_cast<const float*>(d_in[slot].get()), rows, ncol, G, W, d_groups.get(), d_feats.get(),
+                 d_bounds.get(), d_lut.get(), stride, dst, num_cu, s);
     }
-    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(packed[slot], s));
   }
   if (stride > G * W) {
     k_zero_pad<<<1024, 256, 0, s>>>(static_cast<uint8_t*>(d_out), nrow, stride, G * W);
@@ -235,6 +314,12 @@ bool DevicePackDense(const Dataset& ds, const void* data, bool f64, int nrow, in
                              hipMemcpyDeviceToHost, s));
   }
   HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipStreamSynchronize(cs));
+  for (int i = 0; i < 2; ++i) {
+    HIP_CHECK(hipEventDestroy(up[i]));
+    HIP_CHECK(hipEventDestroy(packed[i]));
+  }
+  HIP_CHECK(hipStreamDestroy(cs));
   HIP_CHECK(hipStreamDestroy(s));
   if (keep_device_copy) {
     std::lock_guard<std::mutex> lock(g_kept_mu);

@@ -33,19 +33,27 @@
 // are captured into hipGraphs (main graph for the predicted round count plus a
 // 4-round continuation graph replayed until the tree is done).
 //
-// SEQUENTIAL engine (data/voting-parallel, bynode sampling, extra-trees, the
-// global-scan path for very wide bins): a FIXED kernel sequence per split:
-//   select     best leaf (argmax over leaves of the per-leaf best split)
-//   p_count / p_scan / p_scatter   stable partition of the parent range
-//   post       leaf bookkeeping: ranges, sums, depth, monotone bounds, smaller /
-//              larger child, histogram-slot handoff, min_data / max_depth
-//   hist       LDS-privatised histogram of the smaller child
-//   scan       one wave per feature: subtraction trick, mfb reconstruction,
-//              both-direction threshold scans, categorical scan, extra-trees draws
+// SEQUENTIAL engine (feature/voting-parallel, the xGMI data-parallel transport, bynode
+// sampling, extra-trees, the global-scan path for very wide bins): a FIXED kernel
+// sequence per split (kernels: seq_kernels.h, seq_{hist,scan,vote,partition}_kernels.hip):
+//   partition  best-leaf select from the candidate table, stable partition of the
+//              parent range (decoupled look-back), post-split bookkeeping: ranges,
+//              sums, depth, monotone bounds, smaller / larger child, slot handoff
+//   hist       LDS fixed-point histograms of the smaller child into per-block slab rows
+//   scan       one workgroup per feature: slab fold (or the owner rows), parent -
+//              smaller subtraction, mfb reconstruction, threshold / categorical scans
 // Every launch has a fixed grid and exits early when the tree is done, so the
-// sequence is captured once into a hipGraph and replayed per tree. Data-parallel
-// training all-reduces the smaller child's histogram (and the root sums) over
-// RCCL between `hist` and `scan`; every rank then scans all features redundantly.
+// sequence is captured once into a hipGraph and replayed per tree.
+//
+// Data parallel (tree_learner=data): by default the FRONTIER engine runs on every
+// rank over its own rows, the round's fixed-point accumulators are all-reduced
+// exactly (RCCL uint64 sums; the first half of a round's all-reduce overlaps the
+// second half's histograms on a comm stream), and every rank scans and selects
+// redundantly. With the xGMI transport, the sequential chain pushes each owner its
+// bins (in-kernel exchange over IPC-mapped buffers, or RCCL reduce-scatter), scans
+// only the features it owns and fills one slice of the candidate table that all
+// ranks then read. Voting parallel elects top-k features per child and exchanges
+// only their histograms.
 //
 // After either engine: leaf outputs / renew (leaf_kernels.hip), then the score
 // update walks the new tree in group-bin space (traverse_kernels.hip).
@@ -74,6 +82,7 @@
 #include "device/frontier.h"
 #include "device/traverse_kernels.h"
 #include "device/sample_kernels.h"
+#include "device/seq_kernels.h"
 #include "device/split_scan.h"
 #include "device/tree_kernels.h"
 #include "learner/forced_splits.h"
@@ -89,2351 +98,8 @@ namespace lgap {
 namespace device {
 namespace {
 
-#ifndef LGAP_HIST_THREADS
-#define LGAP_HIST_THREADS 512
-#endif
-#ifndef LGAP_SCAN_UNROLL
-#define LGAP_SCAN_UNROLL 8  // slab rows in flight per lane in the k_reduce_scan fold
-#endif
-#ifndef LGAP_HIST_R
-#define LGAP_HIST_R 16
-#endif
-constexpr int kHistThreads = LGAP_HIST_THREADS;
-constexpr int kHistMinRows = 1024;  // A/B on MI355X: 1024 beats 2048 / 512 / 4096 at 1.25M and 10M rows
-constexpr int kHistLdsBytes = 56 * 1024;
-constexpr int kPartThreads = 256;
-constexpr int kPartIters = 16;  // rows per thread of the two-kernel partition (k_part_count / k_part_scatter)
-constexpr int kTileRows = kPartThreads * kPartIters;
-constexpr int kScanWaves = 4;
-#ifndef LGAP_SCAN_FOLD
-#define LGAP_SCAN_FOLD 1  // 1: half-wave row streams, one value per lane; 2: quarter-wave streams, value pairs
-#endif
-#ifndef LGAP_SCAN_THREADS
-#define LGAP_SCAN_THREADS 1024  // k_reduce_scan block size (the fold and the slot update use all waves)
-#endif
-constexpr int kScanThreads = LGAP_SCAN_THREADS;
-constexpr int kNodeThreads = 256;
 
-struct Args {
-  const uint32_t* rowbins;
-  const uint8_t* colbins;
-  const float2* gh;
-  int* idx[5];  // 0/1 ping-pong (frontier: depth buffers 0, 1), 2 bag, 3/4 frontier depth buffers 2, 3
-  int N, stride_dw, width, num_groups, TB, F, L, max_tiles;
-  const int* gstart;
-  const DevFeature* feat;
-  const HistTile* tiles;
-  const uint8_t* used_bytree;
-  const uint8_t* bynode;
-  const TreeParams* tp;
-  Ctl* ctl;       // control block this launch reads (never written while the launch runs)
-  Ctl* ctl_next;  // k_partition writes the post-split control block here (double buffer)
-  LeafRange* range;
-  double2* lsum;
-  double* lout;
-  int* gcount;
-  int* depth;
-  int* slot;
-  LeafBounds* bounds;
-  SplitInfo* best;
-  SplitRec* rec;
-  double* slots;
-  double* staging;
-  float* staging_f;  // data-parallel all-reduce row of the fp32 (default) histogram path
-  void* hist_slab;
-  unsigned* ghmax;  // float bits of max|g|, max|h| over the root rows
-  uint8_t* splittable;
-  int* tile_cnt;
-  int* tile_off;
-  unsigned* rng;
-  int max_cat_bin;
-  int max_bin;  // largest feature num_bin (LDS sizing of k_reduce_scan)
-  int cat_p2;   // power of two >= the largest categorical num_bin (categorical sort scratch), 1 without
-  char* scan_scratch;        // global-memory scan scratch (features wider than the LDS budget), else null
-  size_t scan_scratch_stride;  // bytes per block
-  int max_depth;
-  int fuse_post;
-  unsigned long long* stamps;  // optional phase timestamps (LGAP_STAMPS=1)
-  int distributed;
-  int use_monotone;
-  double monotone_penalty;
-  // interaction constraints: bit k of ic_feat[f] = constraint set k holds f;
-  // ic_leaf[leaf] = sets that hold every feature on the leaf's branch
-  const unsigned long long* ic_feat;
-  unsigned long long* ic_leaf;
-  double* root_part;  // per-block (sum g, sum h, max|g|, max|h|) of k_root_sums
-  unsigned* bar;      // {-, -, error flag of k_partition's bounded waits}
-  SplitKey* leaf_key;  // [L] compact best split per leaf (next to best)
-  unsigned long long* tile_pub;  // k_partition tile counts tagged with the split epoch
-  int hist_min_rows;  // rows per k_hist block (fewer rows: more blocks and slab rows)
-  // ---- owner-computes split finding (tree_learner=data|feature); single GPU: P = 1, Fmax = F
-  int P, rank, Fmax;  // ranks, this rank, candidate block width (most features any rank owns)
-  int cand_rows;        // blocks of the candidate table the select reads (P for data / feature parallel)
-  const int* own_feat;  // [Fmax] features of the groups this rank owns (-1: padding); nullptr: identity
-  char* cand;           // candidate table [P] blocks of cand_stride bytes (tree_kernels.h)
-  int cand_stride;
-  int cand_key_bytes;   // SplitKey part of a block (SplitInfo part follows)
-  int scan_src;         // 0: fold the k_hist slab rows; 1: sum the `nparts` owner rows of `rx`
-  // split slab fold (scan_src 0): fold_chunks blocks per feature each fold a run of the slab
-  // rows into fold_part; the last to arrive on fold_cnt[j] sums the runs and scans
-  int fold_chunks, fold_feats;
-  double* fold_part;   // [fold_chunks][2 * TB]
-  unsigned* fold_cnt;  // [F]: a multiple of fold_chunks between launches
-  int nparts;
-  const void* rx;       // owner rows: nparts x (2 * bbin) values of the bins this rank owns
-  int own_bin0;         // first histogram bin this rank owns
-  int bbin;             // owner block width (bins, padded to the largest block)
-  const int* bin_lo;    // [P + 1] owner bin bounds (k_hist_owner permutation)
-  int transport;        // 0: collectives between kernels (RCCL / host-staged), 2: xGMI in-kernel exchange
-  const XPeers* xp;     // xGMI: every rank's exchange buffer
-  int x_off_hist, x_off_cand, x_off_flag, x_off_root;  // offsets inside an exchange buffer
-  unsigned* xcnt;       // local arrival counters of the exchanges [4]
-  unsigned xsession;    // high word of the exchange tags (new per learner state)
-  unsigned long long xtimeout;  // bound of an exchange wait (wall_clock64 ticks, 100 MHz)
-  int xfault;           // LGAP_XGMI_FAULT=1: never signal (failure-detection tests)
-  // ---- voting parallel (tree_learner=voting): local scan, top-k vote, elected histograms
-  int vote;             // 1: k_reduce_scan is the LOCAL pass (local sums / counts, no masks or penalties)
-  double2* hsum_part;   // [hist blocks] local (sum g, sum h) of the smaller child's rows per k_hist block
-  double2* lsum_loc;    // [L] local leaf sums
-  int topk;             // elected features per child (min(top_k, F))
-  const char* lcand;    // local candidate table (keys [2][F], infos [2][F] at lcand_key_bytes)
-  int lcand_key_bytes;
-  VoteRec* vrec;        // collective transport: gathered local top-k records [P][2 * topk]
-  void* vhist;          // collective transport: packed elected histograms (all-reduced in place)
-  int vcap;             // values of one packed row (2 * topk * 2 * (max_bin - 1))
-  int* elect;           // [2][topk + 2]: count, first-value offset, then the elected features (ascending)
-  SplitParams sp;
-};
-
-__device__ __forceinline__ SplitKey* CandKey(const Args& a, int r, int sel, int j) {
-  return reinterpret_cast<SplitKey*>(a.cand + static_cast<size_t>(r) * a.cand_stride) + sel * a.Fmax + j;
-}
-__device__ __forceinline__ SplitInfo* CandInfo(const Args& a, int r, int sel, int j) {
-  return reinterpret_cast<SplitInfo*>(a.cand + static_cast<size_t>(r) * a.cand_stride + a.cand_key_bytes) +
-         sel * a.Fmax + j;
-}
-// full record of the candidate at table position `pos` (SplitKey::pos) of child `sel`
-__device__ __forceinline__ SplitInfo* CandInfoPos(const Args& a, int sel, int pos) {
-  const int r = pos / a.Fmax;
-  return CandInfo(a, r, sel, pos - r * a.Fmax);
-}
-
-// ---------------------------------------------------------------------------
-// small device helpers
-
-__device__ __forceinline__ uint32_t ColBin(const Args& a, int g, int row) {
-  const size_t o = static_cast<size_t>(g) * a.N + row;
-  return a.width == 1 ? a.colbins[o] : reinterpret_cast<const uint16_t*>(a.colbins)[o];
-}
-
-__device__ __forceinline__ int RowAt(const Args& a, int buf, int pos) { return buf < 0 ? pos : a.idx[buf][pos]; }
-
-// Diagnostic phase stamps: [kernel 0..4][split 0..255][block 0..1][stamp 0..7], 100 MHz wall clock.
-__device__ __forceinline__ void Stamp(const Args& a, int kernel, int i) {
-  if (a.stamps != nullptr && blockIdx.x < 2 && blockIdx.y == 0 && threadIdx.x == 0) {
-    const int split = a.ctl->num_splits & 255;
-    a.stamps[((static_cast<size_t>(kernel) * 256 + split) * 2 + blockIdx.x) * 8 + i] = wall_clock64();
-  }
-}
-// Latest exit over all blocks of a kernel (slot 0, stamp 7), for kernel-span / gap analysis.
-__device__ __forceinline__ void StampEnd(const Args& a, int kernel) {
-  if (a.stamps != nullptr && threadIdx.x == 0) {
-    const int split = a.ctl->num_splits & 255;
-    atomicMax(&a.stamps[((static_cast<size_t>(kernel) * 256 + split) * 2) * 8 + 7], wall_clock64());
-  }
-}
-// A stamp of a given block role (slot 0) for a given split, with an explicit clock value.
-__device__ __forceinline__ void StampAt(const Args& a, int kernel, int split, int i, unsigned long long v) {
-  if (a.stamps != nullptr && threadIdx.x == 0) a.stamps[((static_cast<size_t>(kernel) * 256 + (split & 255)) * 2) * 8 + i] = v;
-}
-
-// ---------------------------------------------------------------------------
-// quantized-gradient training (reference gradient_discretizer.cpp:66-160):
-// max |g|, |h| over the rows, then integer levels with stochastic rounding,
-// stored de-scaled in place so the fixed-point histograms sum exact integers.
-
-__device__ __forceinline__ float HashUniform(uint32_t seed, uint32_t i) {
-  uint32_t x = i * 0x9E3779B1u + seed * 0x85EBCA77u;
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return static_cast<float>(x >> 8) * (1.0f / 16777216.0f);
-}
-
-// 16-byte loads (two rows per float4), four in flight per thread, one atomic pair per block
-// (the per-wave atomics and 8-byte loads ran at ~0.75 TB/s: 106 us at 10M rows)
-__global__ __launch_bounds__(256) void k_qmax(const float2* gh, int n, unsigned* qmax) {
-  __shared__ float s_m[2][4];
-  float mg = 0.f, mh = 0.f;
-  if ((reinterpret_cast<uintptr_t>(gh) & 15u) != 0 && n > 0) {  // class slice at an odd row offset
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      mg = fabsf(gh[0].x);
-      mh = fabsf(gh[0].y);
-    }
-    ++gh;
-    --n;
-  }
-  const float4* g4 = reinterpret_cast<const float4*>(gh);
-  const int n4 = n / 2;
-  const int stride = gridDim.x * blockDim.x;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    float4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = g4[i + j * stride];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      mg = fmaxf(mg, fmaxf(fabsf(v[j].x), fabsf(v[j].z)));
-      mh = fmaxf(mh, fmaxf(fabsf(v[j].y), fabsf(v[j].w)));
-    }
-  }
-  for (; i < n4; i += stride) {
-    const float4 v = g4[i];
-    mg = fmaxf(mg, fmaxf(fabsf(v.x), fabsf(v.z)));
-    mh = fmaxf(mh, fmaxf(fabsf(v.y), fabsf(v.w)));
-  }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const float2 v = gh[n - 1];  // (n, gh: after the alignment step)
-    mg = fmaxf(mg, fabsf(v.x));
-    mh = fmaxf(mh, fabsf(v.y));
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
-    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    s_m[0][w] = mg;
-    s_m[1][w] = mh;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < 4; ++k) {
-      mg = fmaxf(mg, s_m[0][k]);
-      mh = fmaxf(mh, s_m[1][k]);
-    }
-    atomicMax(&qmax[0], __float_as_uint(mg));  // non-negative floats order as their bits
-    atomicMax(&qmax[1], __float_as_uint(mh));
-  }
-}
-
-// ghq (frontier engine, hist MODE 2): the same levels as int8 g << 8 | uint8 h
-__global__ __launch_bounds__(256) void k_quantize(float2* gh, float2* gh_true, uint16_t* ghq, int n, const unsigned* qmax,
-                                                  int bins, int const_hess, uint32_t seed, int stochastic) {
-  const double mg = __uint_as_float(qmax[0]), mh = __uint_as_float(qmax[1]);
-  const double gs = mg / (bins / 2), hs = const_hess ? mh : mh / bins;
-  const double ig = gs > 0 ? 1.0 / gs : 0.0, ih = hs > 0 ? 1.0 / hs : 0.0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float2 v = gh[i];
-    if (gh_true) gh_true[i] = v;
-    const double rg = stochastic ? HashUniform(seed, 2u * i) : 0.5;
-    const double rh = stochastic ? HashUniform(seed, 2u * i + 1u) : 0.5;
-    const double x = v.x * ig;
-    const int q = static_cast<int>(v.x >= 0.f ? x + rg : x - rg);  // truncation toward zero
-    const int qh = const_hess ? 1 : static_cast<int>(v.y * ih + rh);
-    float2 o;
-    o.x = static_cast<float>(q * gs);
-    o.y = static_cast<float>(qh * hs);
-    gh[i] = o;
-    if (ghq) ghq[i] = static_cast<uint16_t>((static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(q))) << 8) |
-                                            static_cast<uint32_t>(qh & 0xFF));
-  }
-}
-
-// ---------------------------------------------------------------------------
-// tree setup
-
-__global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
-  const TreeParams tp = *a.tp;
-  const int t = threadIdx.x;
-  if (t == 0) {
-    Ctl c;
-    c.num_leaves = 1;
-    c.done = 0;
-    c.smaller = 0;
-    c.larger = -1;
-    c.skip = 0;
-    c.num_splits = 0;
-    c.split_leaf = -1;
-    c.new_leaf = -1;
-    c.parent_buf = tp.root_buf;
-    c.parent_start = 0;
-    c.parent_count = tp.root_count;
-    c.target_buf = 0;
-    c.left_count = 0;
-    c.cls = tp.cls;
-    c.scan_round = 0;
-    c.max_count = tp.root_count;
-    c.hist_nb = 0;
-    // the split epoch keeps increasing across trees (tile_pub tags must never repeat)
-    const unsigned e0 = a.ctl->epoch, e1 = a.ctl_next ? a.ctl_next->epoch : 0u;
-    c.epoch = (e0 > e1 ? e0 : e1) + 1u;
-    c.pad1 = c.pad2 = 0;
-    c.plg = c.plh = 0.0;
-    *a.ctl = c;
-    LeafRange r;
-    r.buf = tp.root_buf;
-    r.start = 0;
-    r.count = tp.root_count;
-    r.pad = 0;
-    a.range[0] = r;
-    a.lsum[0] = make_double2(0.0, 0.0);
-    a.ghmax[0] = 0u;
-    a.ghmax[1] = 0u;
-    a.gcount[0] = tp.root_gcount;
-    a.depth[0] = 0;
-    a.lout[0] = 0.0;
-    if (a.ic_leaf) a.ic_leaf[0] = ~0ull;
-  }
-  for (int i = t; i < a.L; i += blockDim.x) {
-    a.slot[i] = i;
-    a.bounds[i] = LeafBounds();
-    a.best[i].Reset();
-    a.leaf_key[i].feature = -1;
-    a.leaf_key[i].gain = kMinScore;
-  }
-  for (int f = t; f < a.F; f += blockDim.x) a.splittable[f] = 1;
-  if (a.fold_cnt) {
-    for (int f = t; f < a.F; f += blockDim.x) a.fold_cnt[f] = 0u;
-  }
-}
-
-// Root statistics in two steps: per-block partials (no atomics: 1024 blocks x
-// device-scope fp64 atomics on one address serialised to ~97 us), then one block
-// folds them and writes lsum[0] and the histogram scale maxima.
-constexpr int kRootThreads = 256;
-__global__ __launch_bounds__(kRootThreads) void k_root_sums(Args a) {
-  __shared__ double sh[4][kRootThreads / 64];
-  const TreeParams tp = *a.tp;
-  const float2* gh = a.gh + static_cast<size_t>(tp.cls) * a.N;
-  double g = 0.0, h = 0.0;
-  float mg = 0.f, mh = 0.f;
-  const int stride = gridDim.x * blockDim.x;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tp.root_count; i += stride) {
-    const float2 v = gh[RowAt(a, tp.root_buf, i)];
-    g += v.x;
-    h += v.y;
-    mg = fmaxf(mg, fabsf(v.x));
-    mh = fmaxf(mh, fabsf(v.y));
-  }
-  g = WaveSum(g);
-  h = WaveSum(h);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
-    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sh[0][w] = g;
-    sh[1][w] = h;
-    sh[2][w] = mg;
-    sh[3][w] = mh;
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    double v = sh[threadIdx.x][0];
-    for (int i = 1; i < kRootThreads / 64; ++i) {
-      v = threadIdx.x < 2 ? v + sh[threadIdx.x][i] : fmax(v, sh[threadIdx.x][i]);
-    }
-    a.root_part[4 * blockIdx.x + threadIdx.x] = v;
-  }
-}
-
-__global__ __launch_bounds__(kRootThreads) void k_root_final(Args a, int nblocks) {
-  __shared__ double sh[4][kRootThreads / 64];
-  double g = 0.0, h = 0.0, mg = 0.0, mh = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
-    g += a.root_part[4 * b];
-    h += a.root_part[4 * b + 1];
-    mg = fmax(mg, a.root_part[4 * b + 2]);
-    mh = fmax(mh, a.root_part[4 * b + 3]);
-  }
-  g = WaveSum(g);
-  h = WaveSum(h);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mg = fmax(mg, __shfl_xor(mg, o, kWave));
-    mh = fmax(mh, __shfl_xor(mh, o, kWave));
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sh[0][w] = g;
-    sh[1][w] = h;
-    sh[2][w] = mg;
-    sh[3][w] = mh;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < kRootThreads / 64; ++i) {
-      g += sh[0][i];
-      h += sh[1][i];
-      mg = fmax(mg, sh[2][i]);
-      mh = fmax(mh, sh[3][i]);
-    }
-    a.lsum[0] = make_double2(g, h);
-    a.ghmax[0] = __float_as_uint(static_cast<float>(mg));
-    a.ghmax[1] = __float_as_uint(static_cast<float>(mh));
-  }
-}
-
-// ---------------------------------------------------------------------------
-// histogram of the smaller leaf.
-//
-// gfx950 executes LDS float atomics (ds_add_f32/f64) at a small fraction of the
-// integer rate (measured, scripts/hist_micro.hip: 10M x 28 root histogram 2.06 ms
-// with ds_add_f32 vs 0.195 ms with ds_add_u64), so the per-block histogram is
-// accumulated in FIXED POINT:
-//   default    one ds_add_u64 per (row, group): signed g in the high 32 bits,
-//              signed h in the low 32 bits, each scaled by the largest power of two
-//              <= 2^30 / (rows_in_block * max|.|) so no partial sum can overflow (and
-//              constant hessians are exact); low-part borrows are undone
-//              when unpacking. Per-value resolution ~2^-30 * rows * max|g|, below
-//              the error of fp32 accumulation for any bin with more than a few
-//              hundred rows.
-//   gpu_use_dp two ds_add_u64 (g, h) at scale ~2^62 / (rows * max|.|): ~2^-47
-//              relative, indistinguishable from the CPU's double sums.
-// Each active block unpacks its LDS histogram to real values and stores it into
-// its own slab row (plain coalesced stores); k_hist_reduce sums the rows into
-// `staging` (fp64). No float atomics anywhere on the hot path.
-
-__device__ __forceinline__ int HistActiveBlocks(int n, int grid, int min_rows) {
-  int nb = (n + min_rows - 1) / min_rows;
-  return nb > grid ? grid : nb;
-}
-
-// MODE 0: packed (g32|h32) in one u64; MODE 1: two u64 (gpu_use_dp)
-template <int W, int MODE>
-__device__ __forceinline__ void HistRowsFixed(const Args& a, const HistTile& tile, const LeafRange& r, int cls, int rb,
-                                              int re, const int* gst, unsigned long long* hist, float sg, float sh,
-                                              double dsg, double dsh, double* rsum_g, double* rsum_h) {
-  const int tpr = tile.d1 - tile.d0;
-  const int rpi = blockDim.x / tpr;
-  const int myr = threadIdx.x / tpr;
-  const int myd = threadIdx.x - myr * tpr;
-  *rsum_g = 0.0;
-  *rsum_h = 0.0;
-  if (myr >= rpi) return;
-  constexpr int per = 4 / W;
-  constexpr int R = LGAP_HIST_R;  // rows in flight per thread
-  const int dw = tile.d0 + myd;
-  const int gfirst = dw * per;
-  int go[per];
-#pragma unroll
-  for (int k = 0; k < per; ++k) go[k] = gfirst + k < tile.g1 ? gst[gfirst + k - tile.g0] : -1;
-  const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
-  const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf] + r.start;
-  const int base = r.buf < 0 ? r.start : 0;
-  // voting: the first dword's thread of each row also sums the row's (g, h) (local leaf sums)
-  const bool sums = a.hsum_part != nullptr && myd == 0;
-  double tg = 0.0, th = 0.0;
-  for (int p0 = rb + myr; p0 < re; p0 += rpi * R) {
-    int rows[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int p = p0 + j * rpi;
-      rows[j] = p < re ? (idx ? idx[p] : base + p) : -1;
-    }
-    uint32_t word[R];
-    float2 v[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
-      v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
-    }
-    if (sums) {
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        tg += v[j].x;
-        th += v[j].y;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      unsigned long long pg, ph = 0ull;
-      if (MODE == 0) {
-        const long long ig = __float2int_rn(v[j].x * sg);
-        const long long ih = __float2int_rn(v[j].y * sh);
-        pg = (static_cast<unsigned long long>(ig) << 32) + static_cast<unsigned long long>(ih);
-      } else {
-        pg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v[j].x) * dsg));
-        ph = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v[j].y) * dsh));
-      }
-#pragma unroll
-      for (int k = 0; k < per; ++k) {
-        const uint32_t b = W == 1 ? ((word[j] >> (8 * k)) & 0xFFu) : ((word[j] >> (16 * k)) & 0xFFFFu);
-        if (b != 0u && go[k] >= 0) {
-          const int o = go[k] + static_cast<int>(b);
-          if (MODE == 0) {
-            atomicAdd(&hist[o], pg);
-          } else {
-            atomicAdd(&hist[2 * o], pg);
-            atomicAdd(&hist[2 * o + 1], ph);
-          }
-        }
-      }
-    }
-  }
-  *rsum_g = tg;
-  *rsum_h = th;
-}
-
-// Rows of the (rare) tiles whose bins exceed the LDS budget: fp64 atomics into
-// the block's own slab row (global memory, no cross-block contention).
-template <int W, typename Acc>
-__device__ void HistRowsDirect(const Args& a, const HistTile& tile, const LeafRange& r, int cls, int rb, int re,
-                               const int* gst, Acc* hist, double* rsum_g, double* rsum_h) {
-  const int tpr = tile.d1 - tile.d0;
-  const int rpi = blockDim.x / tpr;
-  const int myr = threadIdx.x / tpr;
-  const int myd = threadIdx.x - myr * tpr;
-  *rsum_g = 0.0;
-  *rsum_h = 0.0;
-  if (myr >= rpi) return;
-  constexpr int per = 4 / W;
-  const int dw = tile.d0 + myd;
-  const float2* gh = a.gh + static_cast<size_t>(cls) * a.N;
-  const int* idx = r.buf < 0 ? nullptr : a.idx[r.buf] + r.start;
-  const int base = r.buf < 0 ? r.start : 0;
-  const bool sums = a.hsum_part != nullptr && myd == 0;
-  double tg = 0.0, th = 0.0;
-  for (int p = rb + myr; p < re; p += rpi) {
-    const int row = idx ? idx[p] : base + p;
-    const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
-    const float2 v = gh[row];
-    if (sums) {
-      tg += v.x;
-      th += v.y;
-    }
-#pragma unroll
-    for (int k = 0; k < per; ++k) {
-      const uint32_t b = W == 1 ? ((word >> (8 * k)) & 0xFFu) : ((word >> (16 * k)) & 0xFFFFu);
-      const int g = dw * per + k;
-      if (b != 0u && g < tile.g1) {
-        const int o = gst[g - tile.g0] + static_cast<int>(b);
-        atomicAdd(&hist[2 * o], static_cast<Acc>(v.x));
-        atomicAdd(&hist[2 * o + 1], static_cast<Acc>(v.y));
-      }
-    }
-  }
-  *rsum_g = tg;
-  *rsum_h = th;
-}
-
-// voting: block sum of the per-thread row sums -> hsum_part[blockIdx.x] (first tile's blocks)
-__device__ void PublishRowSums(const Args& a, double tg, double th) {
-  if (a.hsum_part == nullptr || blockIdx.y != 0) return;
-  __shared__ double s_rs[2][kHistThreads / 64];
-  tg = WaveSum(tg);
-  th = WaveSum(th);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    s_rs[0][w] = tg;
-    s_rs[1][w] = th;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double g = 0.0, h = 0.0;
-    for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) g += s_rs[0][i], h += s_rs[1][i];
-    a.hsum_part[blockIdx.x] = make_double2(g, h);
-  }
-}
-
-template <int W, int MODE>
-__global__ __launch_bounds__(kHistThreads) void k_hist(Args a) {
-  extern __shared__ __align__(8) unsigned char lds_raw[];
-  const Ctl* cp = a.ctl;
-  if (cp->done || cp->skip) return;
-  const int leaf = cp->smaller;
-  const int cls = cp->cls;
-  const HistTile tile = a.tiles[blockIdx.y];
-  const LeafRange r = a.range[leaf];
-  const int n = r.count;
-  const int nb = HistActiveBlocks(n, gridDim.x, a.hist_min_rows);
-  if (static_cast<int>(blockIdx.x) >= nb) return;
-  const int chunk = (n + nb - 1) / nb;
-  const int rb = blockIdx.x * chunk;
-  const int re = min(n, rb + chunk);
-  Stamp(a, 2, 0);
-  double* slab = reinterpret_cast<double*>(a.hist_slab) + (static_cast<size_t>(blockIdx.x) * a.TB + tile.bin0) * 2;
-  float* slabf = reinterpret_cast<float*>(a.hist_slab) + (static_cast<size_t>(blockIdx.x) * a.TB + tile.bin0) * 2;
-  if (tile.direct) {
-    int* gst = reinterpret_cast<int*>(lds_raw);
-    for (int i = threadIdx.x; i < 2 * tile.nbins; i += blockDim.x) {
-      if (MODE == 0) slabf[i] = 0.f;
-      else slab[i] = 0.0;
-    }
-    for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
-    __threadfence_block();
-    __syncthreads();
-    double tg, th;
-    if (MODE == 0) HistRowsDirect<W, float>(a, tile, r, cls, rb, re, gst, slabf, &tg, &th);
-    else HistRowsDirect<W, double>(a, tile, r, cls, rb, re, gst, slab, &tg, &th);
-    PublishRowSums(a, tg, th);
-    return;
-  }
-  const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
-  const double rows_in_block = static_cast<double>(re - rb > 0 ? re - rb : 1);
-  const double kPk = 1073741824.0;            // 2^30
-  const double kDp = 4611686018427387904.0;   // 2^62
-  // Scales are POWERS OF TWO (the largest not above the overflow bound): scaling is then an
-  // exponent shift, de-scaling is exact, and a value with few significant bits (a constant
-  // hessian: l2, quantile, ...) is quantized exactly. A non-power-of-two scale rounded every
-  // h = 1 the same way: a systematic relative bias of up to 0.5 / scale that the
-  // parent - smaller subtraction carried, as an absolute error of the root-size bins, into
-  // small deep leaves (near-zero or negative hessian sums, exploding outputs at ~8M rows).
-  const double sgd = gmax > 0.f ? Pow2AtMost(kPk / (rows_in_block * gmax)) : 1.0;
-  const double shd = hmax > 0.f ? Pow2AtMost(kPk / (rows_in_block * hmax)) : 1.0;
-  const double dsg = gmax > 0.f ? Pow2AtMost(kDp / (rows_in_block * gmax)) : 1.0;
-  const double dsh = hmax > 0.f ? Pow2AtMost(kDp / (rows_in_block * hmax)) : 1.0;
-  const float sg = static_cast<float>(sgd), sh = static_cast<float>(shd);
-  const int words = MODE == 0 ? tile.nbins : 2 * tile.nbins;
-  unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
-  int* gst = reinterpret_cast<int*>(hist + words);
-  for (int i = threadIdx.x; i < words; i += blockDim.x) hist[i] = 0ull;
-  for (int g = tile.g0 + threadIdx.x; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
-  __syncthreads();
-  Stamp(a, 2, 1);
-  double tg, th;
-  HistRowsFixed<W, MODE>(a, tile, r, cls, rb, re, gst, hist, sg, sh, dsg, dsh, &tg, &th);
-  __syncthreads();
-  PublishRowSums(a, tg, th);
-  Stamp(a, 2, 2);
-  if (MODE == 0) {
-    const double ig = 1.0 / (static_cast<double>(sg)), ih = 1.0 / (static_cast<double>(sh));
-    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
-      const unsigned long long x = hist[i];
-      const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
-      const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
-      slabf[2 * i] = static_cast<float>(static_cast<double>(gs) * ig);
-      slabf[2 * i + 1] = static_cast<float>(static_cast<double>(hs) * ih);
-    }
-  } else {
-    const double ig = 1.0 / dsg, ih = 1.0 / dsh;
-    for (int i = threadIdx.x; i < tile.nbins; i += blockDim.x) {
-      slab[2 * i] = static_cast<double>(static_cast<long long>(hist[2 * i])) * ig;
-      slab[2 * i + 1] = static_cast<double>(static_cast<long long>(hist[2 * i + 1])) * ih;
-    }
-  }
-  StampEnd(a, 2);
-}
-
-// out[v] = sum over the active blocks' slab rows (v over 2 * TB values), folded
-// in fp64. Used where the full histogram must exist in one place: data-parallel
-// training (all-reduced over RCCL before the scan; fp32 rows unless gpu_use_dp,
-// half the bytes on the wire) and the kernel tests (fp64 staging).
-template <typename Acc, typename Out>
-__global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid, Out* __restrict__ out) {
-  __shared__ double part[16][64];
-  const Ctl* cp = a.ctl;
-  if (cp->done || cp->skip) return;
-  const int n = a.range[cp->smaller].count;
-  const int nb = cp->hist_nb > 0 ? cp->hist_nb : HistActiveBlocks(n, hist_grid, a.hist_min_rows);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const size_t V = 2 * static_cast<size_t>(a.TB);
-  const size_t v = static_cast<size_t>(blockIdx.x) * 64 + lane;
-  const Acc* slab = reinterpret_cast<const Acc*>(a.hist_slab);
-  double s = 0.0;
-  if (v < V) {
-    for (int p = w; p < nb; p += 16) s += static_cast<double>(slab[static_cast<size_t>(p) * V + v]);
-  }
-  part[w][lane] = s;
-  __syncthreads();
-  if (w == 0 && v < V) {
-    double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += part[i][lane];
-    out[v] = static_cast<Out>(t);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Owner-computes data parallelism (reference data_parallel_tree_learner.cpp:225-302,
-// 305-450 and parallel_tree_learner.h:209-232, redesigned for one node of MI355X):
-// ranks own contiguous, bin-balanced ranges of feature groups; per split the
-// smaller child's histogram is reduce-scattered by ownership, each rank scans only
-// the features it owns, and the per-feature candidates are all-gathered into the
-// candidate table every rank's select reads (so every rank applies the same split).
-//
-// Two transports carry the two exchanges:
-//  * collectives between kernels (transport 0): k_hist_owner writes the owner-permuted
-//    histogram row, ncclReduceScatter delivers this rank's block, k_reduce_scan writes
-//    its candidate block, ncclAllGather completes the table (host-staged for the
-//    one-GPU multi-process rehearsal);
-//  * xGMI in-kernel exchange (transport 2): the same kernels PUSH their payloads into
-//    the peers' IPC-mapped exchange buffers (uncached device memory) and complete the
-//    exchange inside the launch: every block makes its stores visible system-wide and
-//    arrives on a local counter; the last block to arrive tags flag[kind][me] in every
-//    peer and waits until all ranks tagged its own flags. The consumer is the next
-//    kernel on the stream, so no collective call, host round trip or extra launch sits
-//    in the split chain, and the whole tree still replays as one hipGraph.
-// Tags are (session << 32) | split epoch: strictly increasing, never reset, so a flag
-// is only ever compared for "reached". Every wait is bounded (error bar[3]).
-
-constexpr int kXKindHist = 0, kXKindCand = 1, kXKindRoot = 2;
-
-__device__ __forceinline__ unsigned long long XTag(const Args& a, unsigned epoch) {
-  return (static_cast<unsigned long long>(a.xsession) << 32) | epoch;
-}
-
-// flag[kind][src] inside rank `owner`'s exchange buffer
-__device__ __forceinline__ unsigned long long* XFlag(const Args& a, int owner, int kind, int src) {
-  return reinterpret_cast<unsigned long long*>(a.xp->base[owner] + a.x_off_flag) + kind * kMaxXRanks + src;
-}
-
-// spin until every rank has tagged flag[kind][*] of this rank with `tag` (one lane)
-__device__ bool XWaitAll(const Args& a, int kind, unsigned long long tag) {
-  const unsigned long long t0 = wall_clock64();
-  for (int q = 0; q < a.P; ++q) {
-    unsigned long long* f = XFlag(a, a.rank, kind, q);
-    unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < tag) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((++spins & 255u) == 0u &&
-          (wall_clock64() - t0 > a.xtimeout || __hip_atomic_load(&a.bar[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        __hip_atomic_store(&a.bar[3], 1u + kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  return true;
-}
-
-// Called by every thread of every block after the block's pushes to the peers.
-__device__ void XArriveAndExchange(const Args& a, int kind, unsigned long long tag) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();  // this block's peer stores are complete before it arrives
-    const unsigned nb = gridDim.x * gridDim.y;
-    if (atomicAdd(&a.xcnt[kind], 1u) == nb - 1u) {
-      atomicExch(&a.xcnt[kind], 0u);  // every block of this launch has arrived
-      __threadfence_system();
-      for (int q = 0; q < a.P && !(a.xfault && a.xsession > 0); ++q) {
-        __hip_atomic_store(XFlag(a, q, kind, a.rank), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      XWaitAll(a, kind, tag);
-    }
-  }
-}
-
-// Fold the smaller child's slab rows into the owner-permuted layout: destination q of
-// [P][2 * bbin] takes value 2 * bin_lo[r] + l of the local histogram (r = q / (2 bbin),
-// l = q % (2 bbin)); padding positions carry zeros. Transport 0 writes the row to
-// `stage` (then ncclReduceScatter); transport 2 pushes block r straight into rank r's
-// receive row `me` and completes the exchange in-kernel.
-template <typename Acc>
-__global__ __launch_bounds__(1024) void k_hist_owner(Args a, int hist_grid, Acc* __restrict__ stage) {
-  __shared__ double part[16][64];
-  const Ctl* cp = a.ctl;
-  if (cp->done || cp->skip) return;
-  const int n = a.range[cp->smaller].count;
-  const int nb = cp->hist_nb > 0 ? cp->hist_nb : HistActiveBlocks(n, hist_grid, a.hist_min_rows);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int V2 = 2 * a.bbin;
-  const int q = blockIdx.x * 64 + lane;
-  const int r = q / V2;
-  const int l = q - r * V2;
-  const bool valid = r < a.P && l < 2 * (a.bin_lo[r + 1] - a.bin_lo[r]);
-  const size_t V = 2 * static_cast<size_t>(a.TB);
-  const size_t v = valid ? 2 * static_cast<size_t>(a.bin_lo[r]) + l : 0;
-  const Acc* slab = reinterpret_cast<const Acc*>(a.hist_slab);
-  double s = 0.0;
-  if (valid) {
-    for (int p = w; p < nb; p += 16) s += static_cast<double>(slab[static_cast<size_t>(p) * V + v]);
-  }
-  part[w][lane] = s;
-  __syncthreads();
-  if (w == 0 && r < a.P) {
-    double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += part[i][lane];
-    if (a.transport == 2) {
-      if (valid) reinterpret_cast<Acc*>(a.xp->base[r] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + l] = static_cast<Acc>(t);
-    } else {
-      stage[q] = valid ? static_cast<Acc>(t) : static_cast<Acc>(0);
-    }
-  }
-  if (a.transport == 2) XArriveAndExchange(a, kXKindHist, XTag(a, cp->epoch));
-}
-
-// Root sums across ranks on the xGMI transport (one block): push (sum g, sum h) into
-// every rank's root rows, exchange, then every rank folds the rows in rank order (the
-// same fp64 result everywhere).
-__global__ __launch_bounds__(64) void k_x_root(Args a) {
-  const Ctl* cp = a.ctl;
-  if (threadIdx.x == 0) {
-    const double2 mine = a.lsum[0];
-    for (int q = 0; q < a.P; ++q) reinterpret_cast<double2*>(a.xp->base[q] + a.x_off_root)[a.rank] = mine;
-  }
-  XArriveAndExchange(a, kXKindRoot, XTag(a, cp->epoch));
-  if (threadIdx.x == 0) {
-    const double2* rows = reinterpret_cast<const double2*>(a.xp->base[a.rank] + a.x_off_root);
-    double g = 0.0, h = 0.0;
-    for (int q = 0; q < a.P; ++q) {
-      const double2 x = rows[q];
-      g += x.x;
-      h += x.y;
-    }
-    a.lsum[0] = make_double2(g, h);
-  }
-}
-
-// Transport self-test (run once when the exchange is set up): `rounds` exchanges of a
-// known pattern through the histogram rows; counts mismatching values into err[0].
-// Rounds alternate between the two halves of the rows (nvals <= bbin): a rank that has
-// finished round r may already push round r + 1 while a peer still checks round r.
-__global__ __launch_bounds__(256) void k_x_selftest(Args a, int round, int nvals, unsigned* err) {
-  const int V2 = 2 * a.bbin;
-  const int half = (round & 1) * nvals;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
-    for (int q = 0; q < a.P; ++q) {
-      reinterpret_cast<float*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + half + i] =
-          static_cast<float>(a.rank * 131 + round * 7 + (i & 1023));
-    }
-  }
-  XArriveAndExchange(a, kXKindHist, XTag(a, static_cast<unsigned>(round + 1)));
-}
-
-__global__ __launch_bounds__(256) void k_x_selfcheck(Args a, int round, int nvals, unsigned* err) {
-  const int V2 = 2 * a.bbin;
-  const int half = (round & 1) * nvals;
-  const float* rows = reinterpret_cast<const float*>(a.xp->base[a.rank] + a.x_off_hist);
-  unsigned bad = 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
-    for (int q = 0; q < a.P; ++q) {
-      bad += rows[static_cast<size_t>(q) * V2 + half + i] != static_cast<float>(q * 131 + round * 7 + (i & 1023)) ? 1u : 0u;
-    }
-  }
-  if (bad) atomicAdd(err, bad);
-}
-
-// One workgroup (16 waves) per feature this rank owns (every feature on one GPU):
-//  1. the smaller child's histogram of the feature into LDS: the sum of the active
-//     histogram blocks' slab rows (single GPU / feature parallel), or of the owner rows
-//     the data-parallel exchange delivered (scan_src 1)
-//  2. smaller child's histogram -> its slot; larger child = parent - smaller
-//     (the parent histogram lives in the larger child's slot)
-//  3. reconstruct the most-frequent bin of each child, then wave 0 scans the
-//     smaller child and wave 1 the larger one concurrently, from LDS
-//  4. the block writes both candidates into this rank's block of the candidate table
-//     (on the xGMI transport: into every rank's table, then the in-kernel exchange)
-// kGlobal: the block's scratch (histograms, partials, categorical sort) lives in its slice of
-// global memory instead of LDS — features wider than the LDS budget (max_bin in the thousands;
-// reference cuda_best_split_finder.cu:1561 global-memory variant).
-template <typename Acc, bool kGlobal>
-__global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_grid) {
-  extern __shared__ __align__(16) unsigned char smem_dyn[];
-  // (kGlobal launches never split the fold: blockIdx.x is the feature slot)
-  unsigned char* smem = kGlobal ? reinterpret_cast<unsigned char*>(a.scan_scratch) + blockIdx.x * a.scan_scratch_stride
-                                : smem_dyn;
-  const Ctl c = *a.ctl;
-  if (c.done || c.skip) return;
-  const int C = a.fold_chunks;
-  int j = blockIdx.x, ch = 0;
-  if (C > 1) {
-    // the C chunk blocks of a feature take consecutive places in XCD order (blocks b and b + 8
-    // usually share an XCD, so the last arriver reads its partners' runs from its own L2;
-    // speed only): the grid is padded to a multiple of 8
-    const int q = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    j = q / C;
-    ch = q - j * C;
-    if (j >= a.fold_feats) return;
-  }
-  const int f = a.own_feat ? a.own_feat[j] : j;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  Stamp(a, 3, 0);
-  __shared__ int s_skip_both, s_rand[2];
-  __shared__ double s_sum[2][2];
-  __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
-  __shared__ SplitKey s_key[2];
-  SplitInfo* s_out = reinterpret_cast<SplitInfo*>(s_out_raw);
-  if (t < 2) {
-    s_out[t].Reset();
-    SplitKey k;
-    k.gain = kMinScore;
-    k.feature = -1;
-    k.threshold = 0;
-    k.group = k.offset = k.num_bin = k.mfb = k.default_bin = 0;
-    k.missing = k.default_left = k.is_cat = k.pad0 = 0;
-    k.pos = a.rank * a.Fmax + j;
-    k.pad2 = 0;
-    s_key[t] = k;
-  }
-  if (t == 0 && j == 0 && c.num_leaves == 1) {
-    // root output (every rank: the host reads it back with the tree)
-    SplitParams p0 = a.sp;
-    p0.path_smooth = 0.0;
-    a.lout[0] = LeafOutputRaw(a.lsum[0].x, a.lsum[0].y, p0, a.gcount[0], 0.0);
-  }
-  if (f >= 0) {
-    // Loads that do not depend on the histogram are issued first so their latency hides
-    // under the fold: slots of the two children, the parent (larger child's slot) values
-    // this thread subtracts, the leaf statistics the scanning waves read (held by lane 0
-    // of waves 0 / 1 until used) and the feature masks.
-    const int s_slot = a.slot[c.smaller];
-    const int l_slot = c.larger >= 0 ? a.slot[c.larger] : -1;
-    const DevFeature fi = a.feat[f];
-    const int nbin = fi.num_bin;
-    const int nst = nbin - 1;
-    const int nv = 2 * nst;  // stored values of this feature
-    const size_t slot_stride = 2 * static_cast<size_t>(a.TB);
-    const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
-    double* gs = a.slots + s_slot * slot_stride + v0;
-    double* gl = l_slot >= 0 ? a.slots + l_slot * slot_stride + v0 : nullptr;
-    constexpr int kPre = 2;  // parent values per thread held in registers (nv <= kPre * blockDim)
-    double parent[kPre];
-#pragma unroll
-    for (int k = 0; k < kPre; ++k) {
-      const int v = t + k * kScanThreads;
-      parent[k] = (gl && v < nv) ? gl[v] : 0.0;
-    }
-    const int my_leaf = (w == 0) ? c.smaller : (w == 1 ? c.larger : -1);
-    double2 pre_sum = make_double2(0.0, 0.0);
-    int pre_n = 0, pre_depth = 0;
-    double pre_out = 0.0;
-    LeafBounds pre_bounds;
-    if (lane == 0 && my_leaf >= 0) {
-      pre_sum = a.lsum[my_leaf];
-      pre_n = a.vote ? a.range[my_leaf].count : a.gcount[my_leaf];
-      pre_out = a.lout[my_leaf];
-      pre_bounds = a.bounds[my_leaf];
-      pre_depth = a.depth[my_leaf];
-    }
-    int pre_used = 1, pre_spl = 1;
-    if (t == 0) {
-      pre_used = a.used_bytree[f];
-      // the voting learner's local pass tries every feature (no splittable inheritance)
-      pre_spl = (c.larger >= 0 && !a.vote) ? a.splittable[static_cast<size_t>(s_slot) * a.F + f] : 1;
-    }
-    double* hs_full = reinterpret_cast<double*>(smem);                 // 2 * nbin: smaller child, full
-    double* hl_full = hs_full + 2 * a.max_bin;                          // 2 * nbin: larger child, full
-    double* part = hl_full + 2 * a.max_bin;                             // [16][64]
-    int* order = reinterpret_cast<int*>(part + 16 * 64);                // [2][cat_p2] categorical scratch
-    double* ckey = reinterpret_cast<double*>(order + 2 * a.cat_p2);     // [2][cat_p2] ctr sort keys
-    (void)part;
-    const int n_small = a.range[c.smaller].count;
-    // 1. smaller child's histogram into hs_full at stored positions (mfb filled in step 3)
-    if (a.scan_src == 1) {
-      // owner rows of the data-parallel exchange: nparts rows of 2 * bbin values
-      const Acc* rows = reinterpret_cast<const Acc*>(a.rx) + 2 * static_cast<size_t>(fi.hist_offset - a.own_bin0);
-      const size_t stride = 2 * static_cast<size_t>(a.bbin);
-      for (int v = t; v < nv; v += blockDim.x) {
-        double acc = 0.0;
-        for (int p = 0; p < a.nparts; ++p) acc += static_cast<double>(rows[static_cast<size_t>(p) * stride + v]);
-        const int k = v >> 1;
-        const int b = k < fi.mfb ? k : k + 1;
-        hs_full[2 * b + (v & 1)] = acc;
-      }
-    } else {
-      const int nb = c.hist_nb > 0 ? c.hist_nb : HistActiveBlocks(n_small, hist_grid, a.hist_min_rows);
-      const size_t V = 2 * static_cast<size_t>(a.TB);
-      const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
-      const Acc* slab = reinterpret_cast<const Acc*>(a.hist_slab);
-      // each wave owns 32 values, its two half-waves stride over the slab rows;
-      // no barrier until all values are reduced
-#if LGAP_SCAN_FOLD == 2
-      // 16-lane quarter-waves each own 32 values as 16 pairs (one 2-element load per row) and
-      // stride over the slab rows 4 apart: half the dependent loads per lane of the half-wave form
-      const int quarter = lane >> 4, q = lane & 15;
-      for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
-        const int v = vbase + 2 * q;  // nv is even, so v < nv implies v + 1 < nv
-        double acc0 = 0.0, acc1 = 0.0;
-        if (v < nv) {
-          const Acc* col = slab + v0 + v;
-#pragma unroll LGAP_SCAN_UNROLL
-          for (int p = quarter; p < nb; p += 4) {
-            const Acc* e = col + static_cast<size_t>(p) * V;
-            acc0 += static_cast<double>(e[0]);
-            acc1 += static_cast<double>(e[1]);
-          }
-        }
-        acc0 += __shfl_xor(acc0, 16, kWave);
-        acc1 += __shfl_xor(acc1, 16, kWave);
-        acc0 += __shfl_xor(acc0, 32, kWave);
-        acc1 += __shfl_xor(acc1, 32, kWave);
-        if (lane < 16 && v < nv) {
-          const int k = v >> 1;  // (v, v + 1) are the (grad, hess) of stored bin k
-          const int b = k < fi.mfb ? k : k + 1;
-          hs_full[2 * b] = acc0;
-          hs_full[2 * b + 1] = acc1;
-        }
-      }
-#else
-      const int half = lane >> 5;
-      // this block's run of slab rows (all of them unless the fold is split)
-      const int p0 = C > 1 ? static_cast<int>((static_cast<long long>(ch) * nb) / C) : 0;
-      const int p1 = C > 1 ? static_cast<int>((static_cast<long long>(ch + 1) * nb) / C) : nb;
-      double* run = C > 1 ? a.fold_part + static_cast<size_t>(ch) * V + v0 : nullptr;
-      for (int vbase = w * 32; vbase < nv; vbase += (kScanThreads / 64) * 32) {
-        const int v = vbase + (lane & 31);
-        double acc = 0.0;
-        if (v < nv) {
-          const Acc* col = slab + v0 + v;
-#pragma unroll LGAP_SCAN_UNROLL
-          for (int p = p0 + half; p < p1; p += 2) acc += static_cast<double>(col[static_cast<size_t>(p) * V]);
-        }
-        acc += __shfl_xor(acc, 32, kWave);
-        if (lane < 32 && v < nv) {
-          if (run) {
-            run[v] = acc;
-          } else {
-            const int k = v >> 1;
-            const int b = k < fi.mfb ? k : k + 1;
-            hs_full[2 * b + (v & 1)] = acc;
-          }
-        }
-      }
-      if (C > 1) {
-        // in-launch combine (one agent release per block, one acquire in the last arriver):
-        // runs stored -> release -> ticket; the block drawing the last ticket of this launch
-        // acquires and sums the C runs in chunk order (deterministic)
-        __shared__ int s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          const unsigned old = __hip_atomic_fetch_add(&a.fold_cnt[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_last = (old % static_cast<unsigned>(C)) == static_cast<unsigned>(C - 1) ? 1 : 0;
-        }
-        __syncthreads();
-        if (!s_last) return;
-        if (t == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        const double* runs = a.fold_part + v0;
-        for (int v = t; v < nv; v += blockDim.x) {
-          double acc = 0.0;
-          for (int r = 0; r < C; ++r) acc += runs[static_cast<size_t>(r) * V + v];
-          const int k = v >> 1;
-          const int b = k < fi.mfb ? k : k + 1;
-          hs_full[2 * b + (v & 1)] = acc;
-        }
-      }
-#endif
-    }
-    __syncthreads();
-    Stamp(a, 3, 1);
-    // 2. slots: smaller <- reduced; larger <- parent - smaller
-    auto slot_update = [&](int v, double pv) {
-      const int k = v >> 1;
-      const int b = k < fi.mfb ? k : k + 1;
-      const double sv = hs_full[2 * b + (v & 1)];
-      gs[v] = sv;
-      if (gl) {
-        const double lv = pv - sv;
-        gl[v] = lv;
-        hl_full[2 * b + (v & 1)] = lv;
-      }
-    };
-#pragma unroll
-    for (int k = 0; k < kPre; ++k) {
-      const int v = t + k * kScanThreads;
-      if (v < nv) slot_update(v, parent[k]);
-    }
-    for (int v = t + kPre * kScanThreads; v < nv; v += kScanThreads) slot_update(v, gl ? gl[v] : 0.0);
-    if (t == 0) {
-      const bool skip_both = !pre_used || !pre_spl;
-      s_skip_both = skip_both ? 1 : 0;
-      // extra-trees draws in the host learner's order: smaller leaf first, then larger
-      s_rand[0] = s_rand[1] = 0;
-      if (a.sp.extra_trees && !skip_both && fi.bin_type == 0 && fi.num_bin - 2 > 0) {
-        s_rand[0] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
-        if (c.larger >= 0) s_rand[1] = RandNextInt(&a.rng[f], 0, fi.num_bin - 2);
-      }
-    }
-    __syncthreads();
-    Stamp(a, 3, 2);
-    // 3. most-frequent bin = leaf total - stored bins
-    if (w < 2) {
-      const int leaf = w == 0 ? c.smaller : c.larger;
-      if (leaf >= 0) {
-        double* H = w == 0 ? hs_full : hl_full;
-        double sgs = 0.0, shs = 0.0;
-        for (int b = lane; b < nbin; b += 64) {
-          if (b == fi.mfb) continue;
-          sgs += H[2 * b];
-          shs += H[2 * b + 1];
-        }
-        sgs = WaveSum(sgs);
-        shs = WaveSum(shs);
-        double2 sums = pre_sum;  // lane 0's prefetched leaf sums (only lane 0 uses them)
-        if (a.vote) {
-          // voting local pass: the smaller child's local sums are the k_hist row sums; the
-          // larger child's are the split leaf's local sums (Ctl) minus them
-          const int nbp = HistActiveBlocks(n_small, hist_grid, a.hist_min_rows);
-          double pg = 0.0, ph = 0.0;
-          for (int p = lane; p < nbp; p += 64) {
-            const double2 x = a.hsum_part[p];
-            pg += x.x;
-            ph += x.y;
-          }
-          pg = WaveSum(pg);
-          ph = WaveSum(ph);
-          sums = w == 0 ? make_double2(pg, ph) : make_double2(c.plg - pg, c.plh - ph);
-          if (j == 0 && lane == 0) a.lsum_loc[leaf] = sums;
-        }
-        if (lane == 0) {
-          H[2 * fi.mfb] = sums.x - sgs;
-          H[2 * fi.mfb + 1] = sums.y - shs;
-          s_sum[w][0] = sums.x;
-          s_sum[w][1] = sums.y;
-        }
-      }
-    }
-    __syncthreads();
-    Stamp(a, 3, 3);
-    const int sel = w;
-    const int leaf = sel == 0 ? c.smaller : c.larger;
-    if (w < 2 && leaf >= 0) {
-      SplitInfo* out = &s_out[sel];  // built in LDS, published by the whole block below
-      if (!s_skip_both) {
-        const double* H = sel ? hl_full : hs_full;
-        const int lslot = sel ? l_slot : s_slot;
-        const double sg = s_sum[sel][0], sh = s_sum[sel][1];
-        const int n = __shfl(pre_n, 0, kWave);
-        double po;
-        if (c.num_leaves == 1) {
-          SplitParams p0 = a.sp;
-          p0.path_smooth = 0.0;
-          po = LeafOutputRaw(sg, sh, p0, n, 0.0);
-        } else {
-          po = __shfl(pre_out, 0, kWave);
-        }
-        LeafBounds bounds;
-        bounds.min = __shfl(pre_bounds.min, 0, kWave);
-        bounds.max = __shfl(pre_bounds.max, 0, kWave);
-        const int depth = __shfl(pre_depth, 0, kWave);
-        bool sp;
-        if (fi.bin_type == 0) {
-          sp = ScanNumericalWave(a.sp, fi, H, sg, sh, n, po, bounds, s_rand[sel], out);
-        } else {
-          // categorical: the wave-parallel one-hot / ctr-sorted scan
-          FeatureScanMeta m;
-          m.num_bin = fi.num_bin;
-          m.default_bin = static_cast<uint32_t>(fi.default_bin);
-          m.missing_type = fi.missing;
-          m.bin_type = fi.bin_type;
-          m.monotone = fi.monotone;
-          m.penalty = fi.penalty;
-          int rt = 0;
-          if (a.sp.extra_trees && lane == 0) {
-            // (categorical draws happen here; numerical ones were drawn above)
-            if (fi.num_bin <= a.sp.max_cat_to_onehot) {
-              if (fi.num_bin - 1 > 0) rt = RandNextInt(&a.rng[f], 1, fi.num_bin);
-            } else {
-              const double cf = n / (sh + 2 * kEpsilon);
-              int used = 0;
-              for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(H[2 * b + 1] * cf) >= a.sp.cat_smooth;
-              const int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
-              const int max_thr = max(min(max_num_cat, used) - 1, 0);
-              if (max_thr > 0) rt = RandNextInt(&a.rng[f], 0, max_thr);
-            }
-          }
-          m.rand_threshold = __shfl(rt, 0, kWave);
-          if (lane == 0) out->Reset();
-          sp = ScanCategoricalWave(a.sp, m, H, sg, sh, n, po, bounds, a.cat_p2, order + sel * a.cat_p2,
-                                   ckey + sel * a.cat_p2, out);
-        }
-        if (lane == 0) {
-          if (!a.vote) a.splittable[static_cast<size_t>(lslot) * a.F + f] = sp ? 1 : 0;
-          if (!sp) {
-            out->Reset();
-          } else {
-            out->feature = f;
-            // (the voting learner's local pass ranks raw gains: penalties and node masks
-            // apply in its global pass, k_vote_scan)
-            if (!a.vote) {
-              if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
-              if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
-              if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
-            }
-          }
-        }
-      }
-      if (lane == 0) {
-        // the compact candidate the partition's select reads
-        SplitKey& k = s_key[sel];
-        k.feature = out->feature;
-        k.gain = SafeGain(*out);
-        k.threshold = out->threshold;
-        k.group = fi.group;
-        k.offset = fi.offset;
-        k.num_bin = fi.num_bin;
-        k.mfb = fi.mfb;
-        k.default_bin = fi.default_bin;
-        k.missing = fi.missing;
-        k.default_left = out->default_left;
-        k.is_cat = fi.bin_type != 0 ? 1 : 0;
-      }
-    }
-  }
-  __syncthreads();
-  // 4. publish the two candidates (dword-parallel copies of the LDS records)
-  {
-    constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
-    constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-    constexpr int kWords = 2 * (kKeyWords + kInfoWords);
-    const int q0 = a.transport == 2 ? 0 : a.rank;
-    const int q1 = a.transport == 2 ? a.P : a.rank + 1;
-    for (int q = q0; q < q1; ++q) {
-      char* tbl = a.transport == 2 ? a.xp->base[q] + a.x_off_cand : a.cand;
-      for (int i = t; i < kWords; i += blockDim.x) {
-        const int sel = i / (kKeyWords + kInfoWords);
-        const int o = i - sel * (kKeyWords + kInfoWords);
-        char* blk = tbl + static_cast<size_t>(a.rank) * a.cand_stride;
-        if (o < kKeyWords) {
-          reinterpret_cast<uint32_t*>(reinterpret_cast<SplitKey*>(blk) + sel * a.Fmax + j)[o] =
-              reinterpret_cast<const uint32_t*>(&s_key[sel])[o];
-        } else {
-          reinterpret_cast<uint32_t*>(reinterpret_cast<SplitInfo*>(blk + a.cand_key_bytes) + sel * a.Fmax + j)[o - kKeyWords] =
-              reinterpret_cast<const uint32_t*>(&s_out[sel])[o - kKeyWords];
-        }
-      }
-    }
-  }
-  Stamp(a, 3, 4);
-  if (a.transport == 2) XArriveAndExchange(a, kXKindCand, XTag(a, c.epoch));
-  if (t == 0 && a.stamps) {
-    atomicMax(&a.stamps[((static_cast<size_t>(3) * 256 + (a.ctl->num_splits & 255)) * 2) * 8 + 7], wall_clock64());
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Voting parallel (PV-Tree; reference voting_parallel_tree_learner.cpp:243-399), on the
-// device. Rows are sharded like data parallel, but the per-split exchange carries only
-// what the vote needs:
-//   k_hist        local histogram of the smaller child (+ its local (sum g, sum h))
-//   k_reduce_scan LOCAL pass over every feature: local sums / counts, min_data and
-//                 min_sum_hessian divided by the ranks -> local candidate table
-//   k_vote_local  this rank's top-k per child -> VoteRec rows, all-gathered (xGMI push
-//                 + in-kernel exchange, or ncclAllGather)
-//   k_vote_pack   every block elects the same <= top_k features per child from the
-//                 gathered rows (GlobalVoting: gain weighted by count / mean leaf count,
-//                 best record per feature, top_k), and packs this rank's local histogram
-//                 of one elected feature; the packed rows are summed over the ranks
-//                 (xGMI push + in-kernel exchange, or ncclAllReduce)
-//   k_vote_scan   GLOBAL pass over the elected features only (global sums and counts,
-//                 split penalties, node masks) -> the candidate table the partition's
-//                 select reads. Every rank computes the same table: no further exchange.
-// The local histograms stay in the slots (parent - smaller subtraction stays local).
-
-constexpr int kVoteThreads = 256;
-
-// best record first: higher gain, then smaller feature (SplitInfo::BetterThan)
-__device__ __forceinline__ bool VoteBetter(double ga, int fa, double gb, int fb) {
-  return ga != gb ? ga > gb : fa < fb;
-}
-
-__global__ __launch_bounds__(kVoteThreads) void k_vote_local(Args a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const Ctl c = *a.ctl;
-  if (c.done || c.skip) return;
-  const int F = a.F, K = a.topk, t = threadIdx.x;
-  double* s_gain = reinterpret_cast<double*>(smem);
-  int* s_cnt = reinterpret_cast<int*>(s_gain + F);
-  __shared__ int s_n[kVoteThreads / 64];
-  const SplitKey* keys = reinterpret_cast<const SplitKey*>(a.lcand);
-  const SplitInfo* infos = reinterpret_cast<const SplitInfo*>(a.lcand + a.lcand_key_bytes);
-  for (int sel = 0; sel < 2; ++sel) {
-    const int leaf = sel ? c.larger : c.smaller;
-    int nv = 0;
-    for (int f = t; f < F; f += blockDim.x) {
-      const SplitKey k = keys[sel * F + f];
-      const bool valid = leaf >= 0 && k.feature >= 0;
-      s_gain[f] = valid ? k.gain : kMinScore;
-      s_cnt[f] = valid ? infos[sel * F + f].left_count + infos[sel * F + f].right_count : -1;
-      nv += valid ? 1 : 0;
-    }
-    const int nvalid = BlockSumInt(nv, s_n);  // (barrier inside: the LDS arrays are complete)
-    for (int f = t; f < F; f += blockDim.x) {
-      if (s_cnt[f] < 0) continue;
-      const double g = s_gain[f];
-      int rank = 0;
-      for (int j = 0; j < F && rank < K; ++j) rank += (s_cnt[j] >= 0 && VoteBetter(s_gain[j], j, g, f)) ? 1 : 0;
-      if (rank < K) {
-        VoteRec r;
-        r.gain = g;
-        r.feature = f;
-        r.count = s_cnt[f];
-        const size_t o = static_cast<size_t>(a.rank) * 2 * K + sel * K + rank;
-        if (a.transport == 2) {
-          for (int q = 0; q < a.P; ++q) reinterpret_cast<VoteRec*>(a.xp->base[q] + a.x_off_cand)[o] = r;
-        } else {
-          a.vrec[o] = r;
-        }
-      }
-    }
-    for (int i = nvalid + t; i < K; i += blockDim.x) {
-      VoteRec r;
-      r.gain = kMinScore;
-      r.feature = -1;
-      r.count = 0;
-      const size_t o = static_cast<size_t>(a.rank) * 2 * K + sel * K + i;
-      if (a.transport == 2) {
-        for (int q = 0; q < a.P; ++q) reinterpret_cast<VoteRec*>(a.xp->base[q] + a.x_off_cand)[o] = r;
-      } else {
-        a.vrec[o] = r;
-      }
-    }
-    __syncthreads();
-  }
-  if (a.transport == 2) XArriveAndExchange(a, kXKindCand, XTag(a, c.epoch));
-}
-
-// GlobalVoting of child `sel` over the gathered rows (same result in every block and on
-// every rank): s_list[0..n) = the elected features in ascending order; returns n.
-__device__ int ElectChild(const Args& a, const Ctl& c, int sel, const VoteRec* recs, double* s_w, int* s_f,
-                          int* s_flag, int* s_list, int* s_tmp) {
-  const int K = a.topk, R = a.P * K, t = threadIdx.x;
-  const int leaf = sel ? c.larger : c.smaller;
-  // mean leaf count per rank in float, as the reference's score_t mean_num_data
-  const float mean = leaf >= 0 ? static_cast<float>(a.gcount[leaf]) / static_cast<float>(a.P) : 1.f;
-  for (int i = t; i < R; i += blockDim.x) {
-    const int r = i / K, k = i - r * K;
-    const VoteRec v = recs[static_cast<size_t>(r) * 2 * K + sel * K + k];
-    const double w = v.gain * v.count / static_cast<double>(mean);
-    const bool valid = leaf >= 0 && v.feature >= 0 && w > kMinScore;
-    s_w[i] = w;
-    s_f[i] = valid ? v.feature : -1;
-  }
-  __syncthreads();
-  // the best record of each feature (first in gather order on equal weighted gain)
-  for (int i = t; i < R; i += blockDim.x) {
-    int best = s_f[i] >= 0 ? 1 : 0;
-    for (int j = 0; j < R && best; ++j) {
-      if (j != i && s_f[j] == s_f[i] && (s_w[j] > s_w[i] || (s_w[j] == s_w[i] && j < i))) best = 0;
-    }
-    s_flag[i] = best;
-  }
-  __syncthreads();
-  // elected: feature-best records ranked < K by (weighted gain desc, feature asc)
-  int ne = 0;
-  for (int i = t; i < R; i += blockDim.x) {
-    int el = 0;
-    if (s_flag[i]) {
-      int rank = 0;
-      for (int j = 0; j < R && rank < K; ++j) rank += (s_flag[j] && VoteBetter(s_w[j], s_f[j], s_w[i], s_f[i])) ? 1 : 0;
-      el = rank < K ? 1 : 0;
-    }
-    ne += el;
-    s_tmp[i] = el;
-  }
-  __syncthreads();
-  for (int i = t; i < R; i += blockDim.x) s_flag[i] = s_tmp[i];
-  const int n = BlockSumInt(ne, s_tmp + R);
-  for (int i = t; i < R; i += blockDim.x) {
-    if (!s_flag[i]) continue;
-    int pos = 0;
-    for (int j = 0; j < R; ++j) pos += (s_flag[j] && s_f[j] < s_f[i]) ? 1 : 0;
-    s_list[pos] = s_f[i];
-  }
-  __syncthreads();
-  return n;
-}
-
-__device__ __forceinline__ int VoteValues(const Args& a, int f) { return 2 * (a.feat[f].num_bin - 1); }
-
-// One block per (child, elected rank): elect (redundantly per block), then pack this
-// rank's local histogram of the block's feature into the packed row at its offset.
-template <typename Acc>
-__global__ __launch_bounds__(kVoteThreads) void k_vote_pack(Args a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const Ctl c = *a.ctl;
-  if (c.done || c.skip) return;
-  const int K = a.topk, R = a.P * K, t = threadIdx.x;
-  double* s_w = reinterpret_cast<double*>(smem);
-  int* s_f = reinterpret_cast<int*>(s_w + R);
-  int* s_flag = s_f + R;
-  int* s_tmp = s_flag + R;                     // R + kVoteThreads / 64
-  int* s_list = s_tmp + R + kVoteThreads / 64;  // [2][K]
-  __shared__ int s_n[2];
-  const VoteRec* recs = a.transport == 2 ? reinterpret_cast<const VoteRec*>(a.xp->base[a.rank] + a.x_off_cand) : a.vrec;
-  for (int sel = 0; sel < 2; ++sel) {
-    const int n = ElectChild(a, c, sel, recs, s_w, s_f, s_flag, s_list + sel * K, s_tmp);
-    if (t == 0) s_n[sel] = n;
-    __syncthreads();
-  }
-  const int sel = blockIdx.x / K, k = blockIdx.x - sel * K;
-  int base0 = 0;
-  for (int i = 0; i < s_n[0]; ++i) base0 += VoteValues(a, s_list[i]);
-  if (blockIdx.x == 0 && t < 2) {
-    int* e = a.elect + t * (K + 2);
-    e[0] = s_n[t];
-    e[1] = t == 0 ? 0 : base0;
-  }
-  if (blockIdx.x == 0) {
-    for (int i = t; i < 2 * K; i += blockDim.x) {
-      const int sl = i / K, kk = i - sl * K;
-      a.elect[sl * (K + 2) + 2 + kk] = kk < s_n[sl] ? s_list[sl * K + kk] : -1;
-    }
-  }
-  const int leaf = sel ? c.larger : c.smaller;
-  if (k < s_n[sel] && leaf >= 0) {
-    const int f = s_list[sel * K + k];
-    int off = sel ? base0 : 0;
-    for (int i = 0; i < k; ++i) off += VoteValues(a, s_list[sel * K + i]);
-    const int nv = VoteValues(a, f);
-    const double* src = a.slots + static_cast<size_t>(a.slot[leaf]) * 2 * a.TB + 2 * static_cast<size_t>(a.feat[f].hist_offset);
-    for (int v = t; v < nv; v += blockDim.x) {
-      const Acc x = static_cast<Acc>(src[v]);
-      if (a.transport == 2) {
-        for (int q = 0; q < a.P; ++q) {
-          reinterpret_cast<Acc*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * a.vcap + off + v] = x;
-        }
-      } else {
-        reinterpret_cast<Acc*>(a.vhist)[off + v] = x;
-      }
-    }
-  }
-  if (a.transport == 2) XArriveAndExchange(a, kXKindHist, XTag(a, c.epoch));
-}
-
-// Global pass: block k, wave `sel` scans elected feature k of child sel from the summed
-// packed rows with the GLOBAL leaf statistics; writes the candidate table (one row of
-// 2 x top_k positions) that the partition's select reads.
-template <typename Acc, bool kGlobal>
-__global__ __launch_bounds__(128) void k_vote_scan(Args a) {
-  extern __shared__ __align__(16) unsigned char smem_dyn[];
-  // (kGlobal launches never split the fold: blockIdx.x is the feature slot)
-  unsigned char* smem = kGlobal ? reinterpret_cast<unsigned char*>(a.scan_scratch) + blockIdx.x * a.scan_scratch_stride
-                                : smem_dyn;
-  const Ctl c = *a.ctl;
-  if (c.done || c.skip) return;
-  const int K = a.topk, k = blockIdx.x, t = threadIdx.x, lane = t & 63, sel = t >> 6;
-  __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
-  SplitInfo* out = reinterpret_cast<SplitInfo*>(s_out_raw) + sel;
-  double* H = reinterpret_cast<double*>(smem) + sel * 2 * a.max_bin;
-  int* order = reinterpret_cast<int*>(reinterpret_cast<double*>(smem) + 4 * a.max_bin) + sel * a.cat_p2;
-  double* ckey = reinterpret_cast<double*>(reinterpret_cast<int*>(reinterpret_cast<double*>(smem) + 4 * a.max_bin) +
-                                           2 * a.cat_p2) + sel * a.cat_p2;
-  const int* e = a.elect + sel * (K + 2);
-  const int leaf = sel ? c.larger : c.smaller;
-  SplitKey key;
-  key.gain = kMinScore;
-  key.feature = -1;
-  key.threshold = 0;
-  key.group = key.offset = key.num_bin = key.mfb = key.default_bin = 0;
-  key.missing = key.default_left = key.is_cat = key.pad0 = 0;
-  key.pos = k;  // table row 0, column k of child sel (CandInfoPos(a, sel, k))
-  key.pad2 = 0;
-  if (lane == 0) out->Reset();
-  if (leaf >= 0 && k < e[0]) {
-    const int f = e[2 + k];
-    const DevFeature fi = a.feat[f];
-    int off = e[1];
-    for (int i = 0; i < k; ++i) off += VoteValues(a, e[2 + i]);
-    const int nv = 2 * (fi.num_bin - 1);
-    const Acc* rows = a.transport == 2 ? reinterpret_cast<const Acc*>(a.xp->base[a.rank] + a.x_off_hist)
-                                       : reinterpret_cast<const Acc*>(a.vhist);
-    const int nparts = a.transport == 2 ? a.P : 1;
-    double sgs = 0.0, shs = 0.0;
-    for (int v = lane; v < nv; v += 64) {
-      double acc = 0.0;
-      for (int p = 0; p < nparts; ++p) acc += static_cast<double>(rows[static_cast<size_t>(p) * a.vcap + off + v]);
-      const int kb = v >> 1;
-      const int b = kb < fi.mfb ? kb : kb + 1;
-      H[2 * b + (v & 1)] = acc;
-      if (v & 1) shs += acc;
-      else sgs += acc;
-    }
-    sgs = WaveSum(sgs);
-    shs = WaveSum(shs);
-    const double2 sums = a.lsum[leaf];
-    const int n = a.gcount[leaf];
-    if (lane == 0) {
-      H[2 * fi.mfb] = sums.x - sgs;
-      H[2 * fi.mfb + 1] = sums.y - shs;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    double po;
-    if (c.num_leaves == 1) {
-      SplitParams p0 = a.sp;
-      p0.path_smooth = 0.0;
-      po = LeafOutputRaw(sums.x, sums.y, p0, n, 0.0);
-    } else {
-      po = a.lout[leaf];
-    }
-    const LeafBounds bounds = a.bounds[leaf];
-    bool sp;
-    if (fi.bin_type == 0) {
-      sp = ScanNumericalWave(a.sp, fi, H, sums.x, sums.y, n, po, bounds, 0, out);
-    } else {
-      FeatureScanMeta m;
-      m.num_bin = fi.num_bin;
-      m.default_bin = static_cast<uint32_t>(fi.default_bin);
-      m.missing_type = fi.missing;
-      m.bin_type = fi.bin_type;
-      m.monotone = fi.monotone;
-      m.penalty = fi.penalty;
-      m.rand_threshold = 0;
-      if (lane == 0) out->Reset();
-      sp = ScanCategoricalWave(a.sp, m, H, sums.x, sums.y, n, po, bounds, a.cat_p2, order, ckey, out);
-    }
-    if (lane == 0) {
-      if (!sp) {
-        out->Reset();
-      } else {
-        out->feature = f;
-        if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, a.depth[leaf]);
-        if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
-        if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
-      }
-      key.feature = out->feature;
-      key.gain = SafeGain(*out);
-      key.threshold = out->threshold;
-      key.group = fi.group;
-      key.offset = fi.offset;
-      key.num_bin = fi.num_bin;
-      key.mfb = fi.mfb;
-      key.default_bin = fi.default_bin;
-      key.missing = fi.missing;
-      key.default_left = out->default_left;
-      key.is_cat = fi.bin_type != 0 ? 1 : 0;
-    }
-  }
-  __syncthreads();
-  if (lane == 0) *CandKey(a, 0, sel, k) = key;
-  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-  for (int i = lane; i < kInfoWords; i += 64) {
-    reinterpret_cast<uint32_t*>(CandInfo(a, 0, sel, k))[i] = reinterpret_cast<const uint32_t*>(out)[i];
-  }
-}
-
-// quant_train_renew_leaf: per-leaf sums of the unquantized (g, h); one block per leaf
-__global__ __launch_bounds__(kNodeThreads) void k_leaf_true_sums(Args a, const float2* gh_true, int num_leaves,
-                                                                  double2* out) {
-  __shared__ double sh[2][kNodeThreads / 64];
-  const int leaf = blockIdx.x;
-  if (leaf >= num_leaves) return;
-  const LeafRange r = a.range[leaf];
-  double g = 0.0, h = 0.0;
-  for (int i = threadIdx.x; i < r.count; i += blockDim.x) {
-    const float2 v = gh_true[RowAt(a, r.buf, r.start + i)];
-    g += v.x;
-    h += v.y;
-  }
-  g = WaveSum(g);
-  h = WaveSum(h);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sh[0][w] = g;
-    sh[1][w] = h;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double tg = 0.0, th = 0.0;
-    for (int k = 0; k < kNodeThreads / 64; ++k) tg += sh[0][k], th += sh[1][k];
-    out[leaf] = make_double2(tg, th);
-  }
-}
-
-// Copy a SplitInfo with one dword per thread (no serial per-thread struct copy).
-__device__ __forceinline__ void CopySplitInfoBlock(SplitInfo* dst, const SplitInfo* src) {
-  constexpr int kWords = static_cast<int>(sizeof(SplitInfo) / 4);
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
-  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-  for (int i = threadIdx.x; i < kWords; i += blockDim.x) d[i] = s[i];
-}
-
-// ---------------------------------------------------------------------------
-// best-leaf selection, replicated in every block of k_part_count
-
-__device__ __forceinline__ bool CandBetter(double ga, int fa, int la, double gb, int fb, int lb) {
-  if (ga != gb) return ga > gb;
-  if (fa != fb) return fa < fb;
-  return la < lb;
-}
-
-struct SelState {
-  int done;       // no further split
-  int leaf;       // leaf to split
-  int sel;        // winner source: 0/1 = candidate table row of the smaller/larger child, -1 = best[leaf]
-  int feature;
-  int new_best[2];  // candidate-table position of the smaller/larger child's best (-1: none)
-};
-
-// ---------------------------------------------------------------------------
-// stable partition of the split leaf's row indices
-
-__device__ void FillSplitDesc(const Args& a, const SplitInfo& s, SplitDesc* d) {
-  const DevFeature fi = a.feat[s.feature];
-  d->group = fi.group;
-  d->offset = fi.offset;
-  d->num_bin = fi.num_bin;
-  d->mfb = fi.mfb;
-  d->default_bin = fi.default_bin;
-  d->missing = fi.missing;
-  d->thr = static_cast<int>(s.threshold);
-  d->default_left = s.default_left;
-  d->is_cat = fi.bin_type != 0;
-  for (int w = 0; w < kMaxCatWords; ++w) d->bits[w] = d->is_cat ? s.cat_bitset[w] : 0u;
-}
-
-__device__ __forceinline__ void WaveArgBest4(double* g, int* f, int* l, int* o) {
-  const int src = WaveArgBestLane(*g, *f, *l);
-  *g = ReadLane(*g, src);
-  *f = ReadLane(*f, src);
-  *l = ReadLane(*l, src);
-  *o = ReadLane(*o, src);
-}
-
-struct SelOut {
-  SelState st;
-  SplitDesc d;
-  LeafRange pr;
-  SplitKey key[2];  // the two children's winning keys (persisted by block 0)
-};
-
-__device__ void SelectFromKeys(const Args& a, const Ctl& c, SelOut* so) {
-  constexpr int kW = kPartThreads / 64;
-  constexpr int kNone = 0x7fffffff;
-  __shared__ double s_g[3][kW];
-  __shared__ int s_f[3][kW], s_l[3][kW], s_o[3][kW];
-  __shared__ int s_owner[3], s_win_cat;
-  __shared__ LeafRange s_rng[kPartThreads];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  double g3[3] = {kMinScore, kMinScore, kMinScore};
-  int f3[3] = {kNone, kNone, kNone};
-  int l3[3] = {0, 0, kNone};
-  SplitKey k3_0, k3_1, k3_2;  // (named: a runtime-indexed array would live in scratch)
-  if (!c.skip) {
-    // the two children's candidates: every position of the table (all ranks' blocks)
-    const int np = a.cand_rows * a.Fmax;
-#pragma unroll
-    for (int sel = 0; sel < 2; ++sel) {
-      const int leaf = sel ? c.larger : c.smaller;
-      if (leaf < 0) continue;
-      for (int p = t; p < np; p += blockDim.x) {
-        const int r = p / a.Fmax;
-        const SplitKey k = *CandKey(a, r, sel, p - r * a.Fmax);
-        if (k.feature >= 0 && CandBetter(k.gain, k.feature, 0, g3[sel], f3[sel], 0)) {
-          g3[sel] = k.gain;
-          f3[sel] = k.feature;
-          if (sel == 0) k3_0 = k;
-          else k3_1 = k;
-        }
-      }
-    }
-  }
-  for (int l = t; l < c.num_leaves; l += blockDim.x) {
-    if (l == c.smaller || l == c.larger) continue;
-    const SplitKey k = a.leaf_key[l];
-    const double g = k.feature < 0 ? kMinScore : k.gain;
-    const int f = k.feature < 0 ? kNone : k.feature;
-    if (CandBetter(g, f, l, g3[2], f3[2], l3[2])) {
-      g3[2] = g;
-      f3[2] = f;
-      l3[2] = l;
-      k3_2 = k;
-    }
-  }
-  if (t <= c.num_leaves && t < kPartThreads) s_rng[t] = a.range[t];
-  Stamp(a, 0, 4);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    int o = t;
-    WaveArgBest4(&g3[k], &f3[k], &l3[k], &o);
-    if (lane == 0) {
-      s_g[k][w] = g3[k];
-      s_f[k][w] = f3[k];
-      s_l[k][w] = l3[k];
-      s_o[k][w] = o;
-    }
-  }
-  __syncthreads();
-  Stamp(a, 0, 5);
-  if (t == 0) {
-    for (int k = 0; k < 3; ++k) {
-      for (int i = 1; i < kW; ++i) {
-        if (CandBetter(s_g[k][i], s_f[k][i], s_l[k][i], s_g[k][0], s_f[k][0], s_l[k][0])) {
-          s_g[k][0] = s_g[k][i];
-          s_f[k][0] = s_f[k][i];
-          s_l[k][0] = s_l[k][i];
-          s_o[k][0] = s_o[k][i];
-        }
-      }
-      s_owner[k] = s_f[k][0] == kNone ? -1 : s_o[k][0];
-    }
-    SelState& st = so->st;
-    st.new_best[0] = -1;  // positions: filled in by the owning threads below
-    st.new_best[1] = -1;
-    double bg = s_g[2][0];
-    int bf = s_f[2][0], bl = s_l[2][0], cat = 2;
-    for (int sel = 0; sel < 2; ++sel) {
-      const int leaf = sel ? c.larger : c.smaller;
-      if (leaf < 0 || s_f[sel][0] == kNone) continue;
-      if (CandBetter(s_g[sel][0], s_f[sel][0], leaf, bg, bf, bl)) {
-        bg = s_g[sel][0];
-        bf = s_f[sel][0];
-        bl = leaf;
-        cat = sel;
-      }
-    }
-    st.leaf = bl;
-    st.feature = bf;
-    st.done = (bl == kNone || bf == kNone || !(bg > 0.0)) ? 1 : 0;
-    st.sel = cat == 2 ? -1 : cat;
-    s_win_cat = st.done ? -1 : cat;
-  }
-  __syncthreads();
-  if (t == s_owner[0]) {
-    so->key[0] = k3_0;
-    so->st.new_best[0] = k3_0.pos;
-  }
-  if (t == s_owner[1]) {
-    so->key[1] = k3_1;
-    so->st.new_best[1] = k3_1.pos;
-  }
-  const int wc = s_win_cat;
-  if (wc >= 0 && t == s_owner[wc]) {
-    const SplitKey k = wc == 0 ? k3_0 : (wc == 1 ? k3_1 : k3_2);
-    SplitDesc& d = so->d;
-    d.group = k.group;
-    d.offset = k.offset;
-    d.num_bin = k.num_bin;
-    d.mfb = k.mfb;
-    d.default_bin = k.default_bin;
-    d.missing = k.missing;
-    d.thr = static_cast<int>(k.threshold);
-    d.default_left = k.default_left;
-    d.is_cat = k.is_cat;
-    if (k.is_cat) {
-      const SplitInfo* win = wc < 2 ? CandInfoPos(a, wc, k.pos) : &a.best[so->st.leaf];
-      for (int i = 0; i < kMaxCatWords; ++i) d.bits[i] = win->cat_bitset[i];
-    }
-    const int leaf = so->st.leaf;
-    so->pr = leaf < kPartThreads ? s_rng[leaf] : a.range[leaf];
-  }
-  Stamp(a, 0, 6);
-  __syncthreads();
-}
-
-
-// Block 0 of the partition: persist the two children's bests (full record + compact
-// key) for later selects, and the `done` decision in both control buffers.
-__device__ void PersistChildBests(const Args& a, const Ctl& c, const SelOut& so) {
-  const SelState& st = so.st;
-  if (c.smaller >= 0 && st.new_best[0] >= 0) CopySplitInfoBlock(&a.best[c.smaller], CandInfoPos(a, 0, st.new_best[0]));
-  if (c.larger >= 0 && st.new_best[1] >= 0) CopySplitInfoBlock(&a.best[c.larger], CandInfoPos(a, 1, st.new_best[1]));
-  if (threadIdx.x == 0) {
-    if (c.smaller >= 0) {
-      if (st.new_best[0] >= 0) {
-        a.leaf_key[c.smaller] = so.key[0];
-      } else {
-        a.best[c.smaller].Reset();
-        a.leaf_key[c.smaller].feature = -1;
-        a.leaf_key[c.smaller].gain = kMinScore;
-      }
-    }
-    if (c.larger >= 0) {
-      if (st.new_best[1] >= 0) {
-        a.leaf_key[c.larger] = so.key[1];
-      } else {
-        a.best[c.larger].Reset();
-        a.leaf_key[c.larger].feature = -1;
-        a.leaf_key[c.larger].gain = kMinScore;
-      }
-    }
-    if (st.done) {
-      // both control buffers: later launches read either
-      a.ctl->done = 1;
-      a.ctl_next->done = 1;
-    }
-  }
-}
-
-// Select the leaf to split (replicated), persist the decision (block 0), then
-// count the rows going left per 4096-row tile of the parent range.
-__global__ __launch_bounds__(kPartThreads) void k_part_count(Args a) {
-  __shared__ SelOut so;
-  __shared__ int sh[8];
-  Ctl* cp = a.ctl;
-  const Ctl c = *cp;
-  if (c.done) return;
-  // no leaf has more tiles than this: surplus blocks have nothing to count
-  if (blockIdx.x > 0 && static_cast<int>(blockIdx.x) >= (c.max_count + kTileRows - 1) / kTileRows) return;
-  Stamp(a, 0, 0);
-  SelectFromKeys(a, c, &so);
-  Stamp(a, 0, 1);
-  const SelState& st = so.st;
-  if (blockIdx.x == 0) PersistChildBests(a, c, so);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (!c.skip) cp->scan_round = c.scan_round + 1;
-    if (!st.done) {
-      const LeafRange pr = so.pr;
-      cp->split_leaf = st.leaf;
-      cp->new_leaf = c.num_leaves;
-      cp->parent_buf = pr.buf;
-      cp->parent_start = pr.start;
-      cp->parent_count = pr.count;
-      cp->target_buf = pr.buf == 0 ? 1 : 0;
-    }
-  }
-  if (st.done) return;
-  const SplitDesc& d = so.d;
-  const LeafRange pr = so.pr;
-  Stamp(a, 0, 2);
-  const int ntiles = (pr.count + kTileRows - 1) / kTileRows;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    // all 16 index loads in flight, then all 16 split-column loads
-    int rows[kPartIters];
-    const int pos0 = tile * kTileRows + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kPartIters; ++k) {
-      const int pos = pos0 + k * kPartThreads;
-      rows[k] = pos < pr.count ? RowAt(a, pr.buf, pr.start + pos) : -1;
-    }
-    uint32_t gb[kPartIters];
-#pragma unroll
-    for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
-    int cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kPartIters; ++k) cnt += (rows[k] >= 0 && GoLeft(d, gb[k])) ? 1 : 0;
-    cnt = BlockSumInt(cnt, sh);
-    if (threadIdx.x == 0) a.tile_cnt[tile] = cnt;
-  }
-  Stamp(a, 0, 3);
-}
-
-// Post-split bookkeeping (BeforeFindBestSplit of the two children); run by
-// block 0 of k_part_scatter after its own tiles. Touches only state that no
-// other k_part_scatter block reads. All loads are issued before any store.
-// `win` is the applied split: best[split_leaf] in the two-kernel path, or the
-// record the fused kernel selected from (visible to every block: written by an
-// earlier kernel, unlike best[] entries persisted by block 0 in the same launch).
-__device__ void PostSplit(const Args& a, const Ctl& c, int left_count, const SplitInfo* win) {
-  __shared__ int s_skip, s_from, s_to;
-  const int l = c.split_leaf, r = c.new_leaf;
-  if (threadIdx.x == 0) {
-    const SplitInfo& bi = *win;
-    const double lsg = bi.left_sum_gradient, lsh = bi.left_sum_hessian;
-    const double rsg = bi.right_sum_gradient, rsh = bi.right_sum_hessian;
-    const double lo = bi.left_output, ro = bi.right_output;
-    const int ilc = bi.left_count, irc = bi.right_count;
-    const int8_t mono = bi.monotone_type;
-    const int16_t ncat = bi.num_cat_threshold;
-    if (a.ic_leaf) {
-      const unsigned long long m = a.ic_leaf[l] & a.ic_feat[bi.feature];
-      a.ic_leaf[l] = m;
-      a.ic_leaf[r] = m;
-    }
-    const int dep = a.depth[l] + 1;
-    LeafBounds bl = a.bounds[l];
-    const int ps = a.slot[l];
-    // ---- stores
-    const int lc = left_count, rc = c.parent_count - lc;
-    LeafRange rl, rr;
-    rl.buf = rr.buf = c.target_buf;
-    rl.start = c.parent_start;
-    rl.count = lc;
-    rr.start = c.parent_start + lc;
-    rr.count = rc;
-    rl.pad = rr.pad = 0;
-    a.range[l] = rl;
-    a.range[r] = rr;
-    const int glc = a.distributed ? ilc : lc;
-    const int grc = a.distributed ? irc : rc;
-    SplitRec& rec = a.rec[c.num_splits];
-    rec.leaf = l;
-    rec.left_count = glc;
-    rec.right_count = grc;
-    rec.pad = 0;
-    a.lsum[l] = make_double2(lsg, lsh);
-    a.lsum[r] = make_double2(rsg, rsh);
-    a.lout[l] = lo;
-    a.lout[r] = ro;
-    a.gcount[l] = glc;
-    a.gcount[r] = grc;
-    a.depth[l] = dep;
-    a.depth[r] = dep;
-    LeafBounds br = bl;
-    if (a.use_monotone && ncat == 0) {
-      const double mid = (lo + ro) / 2.0f;
-      if (mono < 0) {
-        bl.min = fmax(bl.min, mid);
-        br.max = fmin(br.max, mid);
-      } else if (mono > 0) {
-        bl.max = fmin(bl.max, mid);
-        br.min = fmax(br.min, mid);
-      }
-    }
-    a.bounds[l] = bl;
-    a.bounds[r] = br;
-    const int smaller = glc < grc ? l : r;
-    const int larger = glc < grc ? r : l;
-    const int md = a.sp.min_data_in_leaf;
-    const bool skip = (a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2);
-    Ctl nc = c;
-    if (a.lsum_loc) {
-      // voting: the split leaf's local sums, for the larger child's local pass
-      const double2 pl = a.lsum_loc[l];
-      nc.plg = pl.x;
-      nc.plh = pl.y;
-    }
-    nc.num_splits = c.num_splits + 1;
-    nc.num_leaves = c.num_leaves + 1;
-    nc.left_count = lc;
-    nc.smaller = smaller;
-    nc.larger = larger;
-    nc.skip = skip ? 1 : 0;
-    nc.epoch = c.epoch + 1u;
-    int to = -1;
-    if (!skip) {
-      if (larger == r) {
-        a.slot[r] = ps;
-        a.slot[l] = r;
-        to = r;
-      } else {
-        a.slot[r] = r;
-        to = r;
-      }
-    }
-    *a.ctl_next = nc;
-    s_from = ps;
-    s_to = to;
-    s_skip = skip ? 1 : 0;
-  }
-  // the split record (dword-parallel copy of the winning SplitInfo)
-  CopySplitInfoBlock(&a.rec[c.num_splits].info, win);
-  // largest leaf after this split (grid bound of the next partition kernels)
-  {
-    __shared__ int s_mx[kPartThreads / 64];
-    int mx = 0;
-    for (int q = threadIdx.x; q <= c.num_leaves; q += blockDim.x) {
-      int cnt;
-      if (q == l) cnt = left_count;
-      else if (q == r) cnt = c.parent_count - left_count;
-      else cnt = a.range[q].count;
-      mx = max(mx, cnt);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, kWave));
-    if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int i = 1; i < static_cast<int>(blockDim.x >> 6); ++i) mx = max(mx, s_mx[i]);
-      a.ctl_next->max_count = mx;
-    }
-  }
-  __syncthreads();
-  if (!s_skip) {
-    const uint8_t* src = a.splittable + static_cast<size_t>(s_from) * a.F;
-    uint8_t* dst = a.splittable + static_cast<size_t>(s_to) * a.F;
-    for (int f = threadIdx.x; f < a.F; f += blockDim.x) dst[f] = src[f];
-  }
-}
-
-// Scatter rows into the target index buffer (stable: lefts in order, then
-// rights in order). Each block derives its tiles' offsets from the tile counts
-// itself; block 0 finishes with the post-split bookkeeping.
-__global__ __launch_bounds__(kPartThreads) void k_part_scatter(Args a) {
-  __shared__ SplitDesc d;
-  __shared__ int s_wl[kPartIters][kPartThreads / 64];
-  __shared__ int s_wv[kPartIters][kPartThreads / 64];
-  __shared__ int sh[8];
-  const Ctl* cp = a.ctl;
-  const Ctl c = *cp;
-  if (c.done) return;
-  const int pbuf = c.parent_buf, pstart = c.parent_start, pcount = c.parent_count;
-  const int ntiles = (pcount + kTileRows - 1) / kTileRows;
-  // the post-split bookkeeping runs on the first block without tiles (in parallel
-  // with the scatter), or after block 0's tiles when every block has tiles
-  const int post_block = (a.fuse_post == 2 && ntiles < static_cast<int>(gridDim.x)) ? ntiles : 0;
-  const int bid = static_cast<int>(blockIdx.x);
-  if (bid > 0 && bid >= ntiles && bid != post_block) return;
-  int* out = a.idx[c.target_buf] + pstart;
-  Stamp(a, 1, 0);
-  if (threadIdx.x == 0 && bid < ntiles) FillSplitDesc(a, a.best[c.split_leaf], &d);
-  int nl = 0;
-  for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += a.tile_cnt[i];
-  const int nl_total = BlockSumInt(nl, sh);
-  Stamp(a, 1, 1);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int pre = 0;
-    for (int i = threadIdx.x; i < tile; i += blockDim.x) pre += a.tile_cnt[i];
-    int lbase = BlockSumInt(pre, sh);
-    int rbase = tile * kTileRows - lbase;
-    int rows[kPartIters];
-    const int pos0 = tile * kTileRows + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kPartIters; ++k) {
-      const int pos = pos0 + k * kPartThreads;
-      rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
-    }
-    uint32_t gb[kPartIters];
-#pragma unroll
-    for (int k = 0; k < kPartIters; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
-#pragma unroll
-    for (int k = 0; k < kPartIters; ++k) {
-      const bool valid = rows[k] >= 0;
-      const bool left = valid && GoLeft(d, gb[k]);
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      if (lane == 0) {
-        s_wl[k][w] = __popcll(ml);
-        s_wv[k][w] = __popcll(mv);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPartIters; ++k) {
-      const bool valid = rows[k] >= 0;
-      const bool left = valid && GoLeft(d, gb[k]);
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      int pl = 0, pv = 0, tl = 0, tv = 0;
-#pragma unroll
-      for (int i = 0; i < kPartThreads / 64; ++i) {
-        if (i < w) {
-          pl += s_wl[k][i];
-          pv += s_wv[k][i];
-        }
-        tl += s_wl[k][i];
-        tv += s_wv[k][i];
-      }
-      if (valid) {
-        const int rl = pl + __popcll(ml & lt_mask);
-        const int rv = pv + __popcll(mv & lt_mask);
-        if (left) out[lbase + rl] = rows[k];
-        else out[nl_total + rbase + (rv - rl)] = rows[k];
-      }
-      lbase += tl;
-      rbase += tv - tl;
-    }
-    __syncthreads();
-  }
-  Stamp(a, 1, 2);
-  if (bid == post_block && a.fuse_post) PostSplit(a, c, nl_total, &a.best[c.split_leaf]);
-  Stamp(a, 1, 3);
-}
-
-// ---------------------------------------------------------------------------
-// Fused partition (select + count + scatter + post-split in ONE launch), with no
-// grid barrier:
-//  * select reads only compact SplitKeys (children's per-feature candidates, the
-//    older leaves' bests) and the leaf ranges in one round of independent loads;
-//    the winner's key is the partition predicate, no dependent descriptor loads;
-//  * every block publishes its tiles' left counts as 64-bit {epoch, count}
-//    granules (one agent-scope store each, no fences needed);
-//  * a tile waits only for its PREDECESSORS' counts (decoupled look-back): lefts go
-//    to [0, nl) in order, rights are placed from the END of the range in reverse
-//    order, which needs the rights before the tile, not the global left total;
-//  * a spare block (or block 0) gathers all counts for the total and runs the
-//    post-split bookkeeping concurrently with the scatter.
-// The control block it reads (a.ctl) is never written during the launch: the
-// post-split state goes to a.ctl_next (double buffer), so no block can observe a
-// half-updated split. Histograms are order independent (fixed point), so the
-// reversed right child changes no result. Every wait is bounded: a timeout raises
-// the sticky error flag bar[2] that the host checks after the tree.
-
-__device__ __forceinline__ void PublishCount(unsigned long long* p, unsigned epoch, int cnt) {
-  const unsigned long long v = (static_cast<unsigned long long>(epoch) << 32) | static_cast<unsigned>(cnt);
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// count of tile i of this split (bounded spin; on timeout raise the error flag and use 0)
-__device__ __forceinline__ int AwaitCount(const Args& a, int i, unsigned epoch) {
-  unsigned spins = 0;
-  for (;;) {
-    const unsigned long long v = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (static_cast<unsigned>(v >> 32) == epoch) return static_cast<int>(static_cast<unsigned>(v));
-    __builtin_amdgcn_s_sleep(1);
-    if ((++spins & 1023u) == 0u &&
-        (spins > (1u << 22) || __hip_atomic_load(&a.bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-      __hip_atomic_store(&a.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return 0;
-    }
-  }
-}
-
-// sum of the published counts of tiles [0, n)
-__device__ int SumCounts(const Args& a, int n, unsigned epoch, int* sh) {
-  int s = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s += AwaitCount(a, i, epoch);
-  return BlockSumInt(s, sh);
-}
-
-// ITERS rows per thread: tiles of 256 * ITERS rows. Smaller tiles spread a leaf over more
-// blocks (more loads in flight, shorter look-back chains per block); A/B on MI355X:
-// 10M rows 8 > 16 (+6%) and 4, 1.25M rows 4 > 8 > 16 (+18% over 16). See PartIters().
-template <int ITERS>
-__global__ __launch_bounds__(kPartThreads) void k_partition(Args a) {
-  constexpr int kTile = kPartThreads * ITERS;
-  __shared__ SelOut so;
-  __shared__ int sh[8];
-  __shared__ int s_wl[ITERS][kPartThreads / 64];
-  __shared__ int s_wv[ITERS][kPartThreads / 64];
-  const unsigned long long t_start = a.stamps ? wall_clock64() : 0ull;
-  const Ctl c = *a.ctl;
-  if (c.done) return;
-  const int bid = static_cast<int>(blockIdx.x);
-  // no leaf has more tiles than this; one block beyond may be the post-split block
-  if (bid > (c.max_count + kTile - 1) / kTile) return;
-  Stamp(a, 0, 0);
-  SelectFromKeys(a, c, &so);
-  Stamp(a, 0, 1);
-  const SelState& st = so.st;
-  if (bid == 0) PersistChildBests(a, c, so);
-  if (st.done) return;
-  const SplitInfo* win = st.sel >= 0 ? CandInfoPos(a, st.sel, st.new_best[st.sel]) : &a.best[st.leaf];
-  const LeafRange pr = so.pr;
-  const SplitDesc& d = so.d;
-  const unsigned epoch = c.epoch;
-  const int ntiles = (pr.count + kTile - 1) / kTile;
-  const int participants = ntiles < static_cast<int>(gridDim.x) ? ntiles : static_cast<int>(gridDim.x);
-  const bool has_post_block = participants < static_cast<int>(gridDim.x);
-  const int post_block = has_post_block ? participants : 0;
-  if (bid >= participants && bid != post_block) return;
-  Stamp(a, 0, 2);
-  const int pbuf = pr.buf, pstart = pr.start, pcount = pr.count;
-  const int tbuf = pbuf == 0 ? 1 : 0;
-  int* out = a.idx[tbuf] + pstart;
-  // phase 1: count this block's tiles and publish them (the first tile's rows stay in registers)
-  int rows0[ITERS];
-  uint32_t gb0[ITERS];
-  for (int tile = bid; tile < ntiles; tile += gridDim.x) {
-    int rows[ITERS];
-    const int pos0 = tile * kTile + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < ITERS; ++k) {
-      const int pos = pos0 + k * kPartThreads;
-      rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
-    }
-    uint32_t gb[ITERS];
-#pragma unroll
-    for (int k = 0; k < ITERS; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
-    int cnt = 0;
-#pragma unroll
-    for (int k = 0; k < ITERS; ++k) cnt += (rows[k] >= 0 && GoLeft(d, gb[k])) ? 1 : 0;
-    cnt = BlockSumInt(cnt, sh);
-    if (threadIdx.x == 0) PublishCount(&a.tile_pub[tile], epoch, cnt);
-    if (tile == bid) {
-#pragma unroll
-      for (int k = 0; k < ITERS; ++k) {
-        rows0[k] = rows[k];
-        gb0[k] = gb[k];
-      }
-    }
-  }
-  Stamp(a, 0, 3);
-  // the post-split block: total lefts from every tile, bookkeeping next to the scatter
-  if (has_post_block && bid == post_block) {
-    const int nl_total = SumCounts(a, ntiles, epoch, sh);
-    const unsigned long long t_cnt = a.stamps ? wall_clock64() : 0ull;
-    Ctl pc = c;
-    pc.split_leaf = st.leaf;
-    pc.new_leaf = c.num_leaves;
-    pc.parent_buf = pbuf;
-    pc.parent_start = pstart;
-    pc.parent_count = pcount;
-    pc.target_buf = tbuf;
-    if (!c.skip) pc.scan_round = c.scan_round + 1;
-    pc.hist_nb = 0;
-    PostSplit(a, pc, nl_total, win);
-    if (a.stamps) {
-      StampAt(a, 4, c.num_splits, 0, t_start);
-      StampAt(a, 4, c.num_splits, 1, t_cnt);
-      StampAt(a, 4, c.num_splits, 2, wall_clock64());
-    }
-    return;
-  }
-  // phase 2: per tile, lefts before it (look-back) -> scatter
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int tile = bid; tile < ntiles; tile += gridDim.x) {
-    int lbase = SumCounts(a, tile, epoch, sh);
-    if (tile == bid) Stamp(a, 1, 0);
-    int rbase = tile * kTile - lbase;  // rights before this tile
-    int rows[ITERS];
-    uint32_t gb[ITERS];
-    if (tile == bid) {
-#pragma unroll
-      for (int k = 0; k < ITERS; ++k) {
-        rows[k] = rows0[k];
-        gb[k] = gb0[k];
-      }
-    } else {
-      const int pos0 = tile * kTile + threadIdx.x;
-#pragma unroll
-      for (int k = 0; k < ITERS; ++k) {
-        const int pos = pos0 + k * kPartThreads;
-        rows[k] = pos < pcount ? RowAt(a, pbuf, pstart + pos) : -1;
-      }
-#pragma unroll
-      for (int k = 0; k < ITERS; ++k) gb[k] = rows[k] >= 0 ? ColBin(a, d.group, rows[k]) : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < ITERS; ++k) {
-      const bool valid = rows[k] >= 0;
-      const bool left = valid && GoLeft(d, gb[k]);
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      if (lane == 0) {
-        s_wl[k][w] = __popcll(ml);
-        s_wv[k][w] = __popcll(mv);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < ITERS; ++k) {
-      const bool valid = rows[k] >= 0;
-      const bool left = valid && GoLeft(d, gb[k]);
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      int pl = 0, pv = 0, tl = 0, tv = 0;
-#pragma unroll
-      for (int i = 0; i < kPartThreads / 64; ++i) {
-        if (i < w) {
-          pl += s_wl[k][i];
-          pv += s_wv[k][i];
-        }
-        tl += s_wl[k][i];
-        tv += s_wv[k][i];
-      }
-      if (valid) {
-        const int rl = pl + __popcll(ml & lt_mask);
-        const int rv = pv + __popcll(mv & lt_mask);
-        if (left) out[lbase + rl] = rows[k];
-        else out[pcount - 1 - (rbase + (rv - rl))] = rows[k];  // rights fill the range from its end
-      }
-      lbase += tl;
-      rbase += tv - tl;
-    }
-    __syncthreads();
-  }
-  Stamp(a, 1, 2);
-  if (!has_post_block && bid == 0) {
-    // every block has tiles: block 0 runs the post-split after its own
-    const int nl_total = SumCounts(a, ntiles, epoch, sh);
-    Ctl pc = c;
-    pc.split_leaf = st.leaf;
-    pc.new_leaf = c.num_leaves;
-    pc.parent_buf = pbuf;
-    pc.parent_start = pstart;
-    pc.parent_count = pcount;
-    pc.target_buf = tbuf;
-    if (!c.skip) pc.scan_round = c.scan_round + 1;
-    pc.hist_nb = 0;
-    PostSplit(a, pc, nl_total, win);
-  }
-  if (a.stamps && threadIdx.x == 0) {
-    atomicMax(&a.stamps[((static_cast<size_t>(0) * 256 + (c.num_splits & 255)) * 2) * 8 + 7], wall_clock64());
-  }
-}
-
-__global__ __launch_bounds__(kPartThreads) void k_post(Args a) {
-  __shared__ int sh[8];
-  const Ctl c = *a.ctl;
-  if (c.done) return;
-  const int ntiles = (c.parent_count + kTileRows - 1) / kTileRows;
-  int nl = 0;
-  for (int i = threadIdx.x; i < ntiles; i += blockDim.x) nl += a.tile_cnt[i];
-  PostSplit(a, c, BlockSumInt(nl, sh), &a.best[c.split_leaf]);
-}
-
-// ---------------------------------------------------------------------------
-// score update of the tree just grown from its final leaf ranges (every row, no
-// bagging): each leaf adds its value to its rows (serial_tree_learner
-// AddPredictionToScore via the data partition). Opt-in (LGAP_SCORE_PATH=leaves):
-// the scattered 8 B score updates touch one cache line per row, and the
-// LDS-staged traversal below measured faster on MI355X (10M rows: 374 us -> see
-// profiles/README.md).
-__global__ __launch_bounds__(256) void k_add_leaves(Args a, const double* __restrict__ leaf_value,
-                                                    double* __restrict__ score) {
-  const int leaf = blockIdx.y;
-  const LeafRange r = a.range[leaf];
-  const double v = leaf_value[leaf];
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < r.count; i += gridDim.x * blockDim.x) {
-    score[RowAt(a, r.buf, r.start + i)] += v;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// score update: traverse one uploaded tree over the packed rows
-
-// One row per thread. A block first stages its 256 contiguous packed rows in LDS
-// with coalesced dword loads (rows are stride_dw dwords, not 16 B aligned), so
-// the per-level bin reads of the traversal are LDS hits instead of dependent
-// global loads; rows wider than kTraverseMaxDw read global memory directly.
-constexpr int kTraverseThreads = 256;
-constexpr int kTraverseMaxDw = 16;
-
-__device__ __forceinline__ bool NodeGoLeft(const DevNode& nd, uint32_t gb, const uint32_t* __restrict__ cat_bits) {
-  const uint32_t b = DecodeBin(nd.offset, nd.num_bin, nd.mfb, gb);
-  if (nd.decision & 1) {
-    const uint32_t wd = b >> 5;
-    return static_cast<int>(wd) < nd.cat_nwords && ((cat_bits[nd.cat_begin + wd] >> (b & 31u)) & 1u);
-  }
-  if ((nd.missing == 1 && b == static_cast<uint32_t>(nd.default_bin)) ||
-      (nd.missing == 2 && b == static_cast<uint32_t>(nd.num_bin - 1))) {
-    return (nd.decision & 2) != 0;
-  }
-  return b <= static_cast<uint32_t>(nd.threshold);
-}
-
-__global__ __launch_bounds__(kTraverseThreads) void k_add_tree(const uint32_t* __restrict__ rowbins, int stride_dw,
-                                                               int width, int N, const DevNode* __restrict__ nodes,
-                                                               int num_nodes, const uint32_t* __restrict__ cat_bits,
-                                                               const double* __restrict__ leaf_value,
-                                                               double* __restrict__ score) {
-  extern __shared__ uint32_t s_dyn[];
-  DevNode* s_nodes = reinterpret_cast<DevNode*>(s_dyn);
-  uint32_t* s_rows = s_dyn + num_nodes * (sizeof(DevNode) / 4);
-  for (int i = threadIdx.x; i < num_nodes; i += blockDim.x) s_nodes[i] = nodes[i];
-  const bool staged = stride_dw <= kTraverseMaxDw;
-  for (long long base = static_cast<long long>(blockIdx.x) * kTraverseThreads; base < N;
-       base += static_cast<long long>(gridDim.x) * kTraverseThreads) {
-    const int rows = static_cast<int>(min(static_cast<long long>(kTraverseThreads), N - base));
-    const int i = static_cast<int>(base) + threadIdx.x;
-    const uint8_t* row;
-    if (staged) {
-      __syncthreads();  // previous chunk's readers are done (and the nodes are in place)
-      const uint32_t* src = rowbins + base * stride_dw;
-      const int ndw = rows * stride_dw;
-      for (int k = threadIdx.x; k < ndw; k += kTraverseThreads) s_rows[k] = src[k];
-      __syncthreads();
-      row = reinterpret_cast<const uint8_t*>(s_rows + threadIdx.x * stride_dw);
-    } else {
-      if (base == static_cast<long long>(blockIdx.x) * kTraverseThreads) __syncthreads();
-      row = reinterpret_cast<const uint8_t*>(rowbins + static_cast<size_t>(i) * stride_dw);
-    }
-    if (threadIdx.x >= rows) continue;
-    int node = 0;
-    while (node >= 0) {
-      const DevNode& nd = s_nodes[node];
-      const uint32_t gb = width == 1 ? row[nd.group] : reinterpret_cast<const uint16_t*>(row)[nd.group];
-      node = NodeGoLeft(nd, gb, cat_bits) ? nd.left : nd.right;
-    }
-    score[i] += leaf_value[~node];
-  }
-}
-
-// group-major copy of the packed rows: col[g * N + i] = group bin g of row i (coalesced writes;
-// each row's dword run is read by consecutive groups' threads of other waves through L2)
-template <typename T>
-__global__ __launch_bounds__(256) void k_transpose_bins(const uint32_t* __restrict__ rowbins, int stride_dw, int N, int G,
-                                                        uint8_t* __restrict__ colbins) {
-  const long long total = static_cast<long long>(G) * N;
-  for (long long idx = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
-       idx += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int g = static_cast<int>(idx / N);
-    const int i = static_cast<int>(idx - static_cast<long long>(g) * N);
-    const T* row = reinterpret_cast<const T*>(rowbins + static_cast<size_t>(i) * stride_dw);
-    reinterpret_cast<T*>(colbins)[idx] = row[g];
-  }
-}
-
-// ---------------------------------------------------------------------------
+using namespace seq;  // NOLINT: the sequential chain's kernels and argument block
 
 template <typename T>
 class PinnedBuf {
@@ -2473,6 +139,10 @@ class DeviceTreeLearner : public TreeLearner {
     if (fcont_) (void)hipGraphExecDestroy(fcont_);
     if (!x_peers_.empty()) XgmiClose(x_local_, &x_peers_);
     if (x_local_) (void)hipFree(x_local_);
+    for (auto& ev : pipe_ev_) {
+      if (ev) (void)hipEventDestroy(ev);
+    }
+    if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
 
@@ -3588,6 +1258,10 @@ class DeviceTreeLearner : public TreeLearner {
     a.hist_min_rows = HistMinRows();
     a.hist_grid = FrontierHistBlocks();
     a.hist_threads = fhist_threads_;
+    {
+      const char* e = std::getenv("LGAP_FHIST_RPT");  // A/B knob
+      a.hist_rpt = e != nullptr && e[0] == '1' ? 1 : 0;
+    }
     if (nib_) {
       a.rowbins = rowbins4_.get();
       a.stride_dw = stride4_dw_;
@@ -3624,6 +1298,8 @@ class DeviceTreeLearner : public TreeLearner {
       const bool want = e != nullptr ? e[0] != '0' : num_tiles_ == 1;
       a.qsub = a.quant && !use_dp_ && sub >= 2048 && want ? sub : 0;
     }
+    a.e_lo = 0;
+    a.e_hi = kFrontierKmax;
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
@@ -3643,13 +1319,61 @@ class DeviceTreeLearner : public TreeLearner {
                     static_cast<size_t>(std::max(1, std::min(kb, fkmax_))) * 2 * TB_, stream_);
   }
 
+  // Data-parallel rounds with at least two expansions pipeline the exchange with histogram
+  // and scan work (RCCL only: the host-staged rehearsal transport synchronises anyway):
+  //
+  //   compute: partition | hist A | hist B |  wait  | scan A |  wait  | scan B | select
+  //   comm:                       | wait A | all-reduce A | wait B | all-reduce B |
+  //
+  // A / B are the first / second half of the round's expansions (their accumulator rows are
+  // contiguous), so half A's all-reduce overlaps half B's histograms and half B's overlaps
+  // half A's scans. The histogram grid stops short of the CU count (7/8), which leaves the
+  // RCCL kernel CUs of its own. LGAP_DP_PIPELINE=0 keeps the serial order.
+  bool FrontierPipelined(int kb) const {
+    if (!distributed_ || HostStagedDP() || !CommExists() || kb < 2) return false;
+    const char* e = std::getenv("LGAP_DP_PIPELINE");
+    return e == nullptr || e[0] != '0';
+  }
+
+  void EnsureCommStream() {
+    if (comm_stream_ != nullptr) return;
+    HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+    for (auto& ev : pipe_ev_) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+
   // One round: partition -> histograms -> [all-reduce] -> scans -> select. `kb` bounds the
   // round's expansion count (round r >= 1 of a tree has at most 2^(r-1) open nodes to expand).
   void EnqueueFrontierRound(const FArgs& fa, int kb) {
     LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
-    LaunchFrontierHist(fa, FrontierHistLds(), stream_);
-    FrontierExchange(kb);
-    LaunchFrontierScan(fa, fscan_lds_, stream_);
+    if (!FrontierPipelined(kb)) {
+      LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+      FrontierExchange(kb);
+      LaunchFrontierScan(fa, fscan_lds_, stream_);
+    } else {
+      EnsureCommStream();
+      kb = std::min(kb, fkmax_);
+      const int kh = (kb + 1) / 2;
+      FArgs fa_a = fa, fa_b = fa;
+      fa_a.e_hi = kh;
+      fa_b.e_lo = kh;
+      auto* acc = reinterpret_cast<unsigned long long*>(facc_.get());
+      const size_t row = 2 * static_cast<size_t>(TB_);
+      LaunchFrontierHist(fa_a, FrontierHistLds(), stream_);
+      HIP_CHECK(hipEventRecord(pipe_ev_[0], stream_));
+      LaunchFrontierHist(fa_b, FrontierHistLds(), stream_);
+      HIP_CHECK(hipEventRecord(pipe_ev_[1], stream_));
+      HIP_CHECK(hipStreamWaitEvent(comm_stream_, pipe_ev_[0], 0));
+      AllreduceSumU64(acc, static_cast<size_t>(kh) * row, comm_stream_);
+      HIP_CHECK(hipEventRecord(pipe_ev_[2], comm_stream_));
+      HIP_CHECK(hipStreamWaitEvent(comm_stream_, pipe_ev_[1], 0));
+      AllreduceSumU64(acc + static_cast<size_t>(kh) * row, static_cast<size_t>(kb - kh) * row, comm_stream_);
+      HIP_CHECK(hipEventRecord(pipe_ev_[3], comm_stream_));
+      HIP_CHECK(hipStreamWaitEvent(stream_, pipe_ev_[2], 0));
+      LaunchFrontierScan(fa_a, fscan_lds_, stream_);
+      HIP_CHECK(hipStreamWaitEvent(stream_, pipe_ev_[3], 0));
+      LaunchFrontierScan(fa_b, fscan_lds_, stream_);
+      ++fstat_pipelined_;
+    }
     LaunchFrontierSelect(fa, stream_);
   }
 
@@ -3808,9 +1532,10 @@ class DeviceTreeLearner : public TreeLearner {
     if (fstamps_.size() && fstat_trees_ == 3) ReportFrontierStamps(hs->round);
     if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {
       std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max), wasted rows %.1f%%, "
-                   "alpha %.3f, all-reduced expansion slots/tree %.1f\n", fstat_trees_,
+                   "alpha %.3f, all-reduced expansion slots/tree %.1f, pipelined rounds/tree %.2f\n", fstat_trees_,
                    static_cast<double>(fstat_rounds_) / fstat_trees_, static_cast<double>(fstat_spec_) / fstat_trees_, L_,
-                   100.0 * fstat_waste_ / fstat_trees_, fspec_alpha_, fstat_ar_exps_ / fstat_trees_);
+                   100.0 * fstat_waste_ / fstat_trees_, fspec_alpha_, fstat_ar_exps_ / fstat_trees_,
+                   static_cast<double>(fstat_pipelined_) / fstat_trees_);
     }
   }
 
@@ -4967,6 +2692,10 @@ class DeviceTreeLearner : public TreeLearner {
   int fkused_hist_[4][kFrontierRoundCap] = {};
   int fkused_trees_ = 0;
   double fstat_ar_exps_ = 0.0;
+  long long fstat_pipelined_ = 0;
+  // data-parallel pipeline: the comm stream and its fork / join events (EnqueueFrontierRound)
+  hipStream_t comm_stream_ = nullptr;
+  hipEvent_t pipe_ev_[4] = {nullptr, nullptr, nullptr, nullptr};
   DevBuf<int> fkcap_, fkused_;
   PinnedBuf<int> pin_kcap_;
   long long fstat_rounds_ = 0, fstat_spec_ = 0;

@@ -171,6 +171,7 @@ struct FArgs {
   unsigned* bar;  // bar[2]: bounded-wait error flag
   int hist_min_rows, hist_grid;
   int hist_threads;  // 512 or 1024 threads per histogram block
+  int hist_rpt;      // row-per-thread histogram loop (FHistRowsRPT) where the shape allows
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)
@@ -185,6 +186,10 @@ struct FArgs {
   const int* kcap;  // [kFrontierRoundCap] per-round expansion caps (data-parallel: the all-reduce sizes), or null
   int* kused;       // [kFrontierRoundCap] expansions each round actually took (host feedback), or null
   unsigned long long* stamps;  // diagnostics (LGAP_FSTAMPS=1): [round & 255][kernel 0..3][8] wall clock
+  // expansion range [e_lo, e_hi) a k_f_hist / k_f_scan launch covers (data-parallel pipeline:
+  // the first half's all-reduce runs on the comm stream while the second half's histograms
+  // build); 0 / kFrontierKmax: the whole round
+  int e_lo, e_hi;
   SplitParams sp;
 };
 

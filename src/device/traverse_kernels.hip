@@ -42,7 +42,9 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
   extern __shared__ __align__(16) unsigned char lds[];
   TNode* s_nodes = reinterpret_cast<TNode*>(lds);
   double* s_leaf = reinterpret_cast<double*>(lds + ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)));
-  uint32_t* s_rows = reinterpret_cast<uint32_t*>(s_leaf + num_leaves);
+  // 16-byte aligned row staging (uint4 stores)
+  uint32_t* s_rows = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(s_leaf) +
+                                                 ((sizeof(double) * num_leaves + 15) & ~size_t(15)));
   const int t = threadIdx.x;
   for (int i = t; i < num_nodes * static_cast<int>(sizeof(TNode) / 4); i += kTThreads) {
     reinterpret_cast<uint32_t*>(s_nodes)[i] = reinterpret_cast<const uint32_t*>(nodes)[i];
@@ -52,11 +54,24 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
   for (long long base = static_cast<long long>(blockIdx.x) * kTRows; base < n;
        base += static_cast<long long>(gridDim.x) * kTRows) {
     const int rows = static_cast<int>(min(static_cast<long long>(kTRows), n - base));
+    // this chunk's scores, loaded before the walk so their latency hides behind it
+    double sc[kTRowsPerThread];
+#pragma unroll
+    for (int j = 0; j < kTRowsPerThread; ++j) {
+      const int r = t + j * kTThreads;
+      sc[j] = r < rows ? score[base + r] : 0.0;
+    }
     if (staged) {
       __syncthreads();  // the previous chunk's walks are done (first pass: nodes / leaves in place)
       const uint32_t* src = rowbins + base * stride_dw;
       const int ndw = rows * stride_dw;
-      for (int k = t; k < ndw; k += kTThreads) s_rows[k] = src[k];
+      // 16-byte loads where the chunk is 16-byte aligned (kTRows * stride_dw dwords per chunk:
+      // always, for rows from a 16-byte aligned buffer), dword loads for the tail
+      const int nq = (reinterpret_cast<uintptr_t>(src) & 15u) == 0 ? ndw >> 2 : 0;
+      const uint4* src4 = reinterpret_cast<const uint4*>(src);
+      uint4* dst4 = reinterpret_cast<uint4*>(s_rows);
+      for (int k = t; k < nq; k += kTThreads) dst4[k] = src4[k];
+      for (int k = 4 * nq + t; k < ndw; k += kTThreads) s_rows[k] = src[k];
       __syncthreads();
     } else if (base == static_cast<long long>(blockIdx.x) * kTRows) {
       __syncthreads();
@@ -95,7 +110,7 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
 #pragma unroll
     for (int j = 0; j < kTRowsPerThread; ++j) {
       const int r = t + j * kTThreads;
-      if (r < rows) score[base + r] += s_leaf[~node[j]];
+      if (r < rows) score[base + r] = sc[j] + s_leaf[~node[j]];
     }
   }
 }
@@ -205,7 +220,7 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
                     const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,
                     int num_cu, hipStream_t s) {
   if (n <= 0) return;
-  const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + sizeof(double) * num_leaves +
+  const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + ((sizeof(double) * num_leaves + 15) & ~size_t(15)) +
                      (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
   const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
   if (width == 0) {
