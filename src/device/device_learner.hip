@@ -1277,6 +1277,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.max_depth = config_->max_depth;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
     a.monotone_penalty = config_->monotone_penalty;
+    a.cegb_split = CegbPenalty::Enabled(config_) ? config_->cegb_tradeoff * config_->cegb_penalty_split : 0.0;
     a.max_bin = max_bin_;
     a.cat_p2 = cat_p2_;
     a.use_dp = use_dp_ ? 1 : 0;
@@ -2404,6 +2405,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.distributed = distributed_ ? 1 : 0;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
     a.monotone_penalty = config_->monotone_penalty;
+    a.cegb_split = CegbPenalty::Enabled(config_) ? config_->cegb_tradeoff * config_->cegb_penalty_split : 0.0;
     a.ic_feat = use_ic_ ? ic_feat_.get() : nullptr;
     a.ic_leaf = use_ic_ ? ic_leaf_.get() : nullptr;
     a.root_part = root_part_.get();

@@ -178,6 +178,7 @@ struct FArgs {
   int part_tile;  // rows per partition tile (256 x rows per thread)
   int max_depth, use_monotone;
   double monotone_penalty;
+  double cegb_split;  // cegb_tradeoff * cegb_penalty_split (per row of the node), 0: none
   int max_bin, cat_p2;
   int use_dp;       // gpu_use_dp: 64-bit LDS accumulators
   int spec_cap;     // speculative expansions per round beyond the budget (policy knob)

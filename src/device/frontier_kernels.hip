@@ -686,6 +686,9 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
             out->Reset();
           } else {
             out->feature = f;
+            // cost-effective gradient boosting, split penalty (host CegbPenalty::DeltaGain:
+            // subtracted before the monotone penalty multiplies the gain)
+            if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
             if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
             if (a.ic && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
           }

@@ -111,6 +111,7 @@ struct Args {
   int distributed;
   int use_monotone;
   double monotone_penalty;
+  double cegb_split;  // cegb_tradeoff * cegb_penalty_split (per row of the leaf), 0: none
   // interaction constraints: bit k of ic_feat[f] = constraint set k holds f;
   // ic_leaf[leaf] = sets that hold every feature on the leaf's branch
   const unsigned long long* ic_feat;

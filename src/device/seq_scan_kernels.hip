@@ -332,6 +332,9 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
             // (the voting learner's local pass ranks raw gains: penalties and node masks
             // apply in its global pass, k_vote_scan)
             if (!a.vote) {
+              // cost-effective gradient boosting, split penalty (host CegbPenalty::DeltaGain:
+              // subtracted before the monotone penalty multiplies the gain)
+              if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
               if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
               if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();

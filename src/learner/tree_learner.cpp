@@ -30,7 +30,12 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   if (linear_tree) return "linear_tree";
   // (voting runs on the device; its global pass redraws no extra-trees thresholds)
   if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
-  if (CegbPenalty::Enabled(c)) return "cost-effective gradient boosting";
+  // CEGB's split penalty runs in the device scans; the feature penalties need per-row /
+  // per-leaf usage state the host policy keeps (leaf_constraints.cpp CegbPenalty)
+  if (!c->cegb_penalty_feature_coupled.empty() || !c->cegb_penalty_feature_lazy.empty() ||
+      (CegbPenalty::Enabled(c) && learner_type == "voting")) {
+    return "cost-effective gradient boosting (feature penalties)";
+  }
   // forced splits run on the device's frontier engine (serial learner); elsewhere on the host
   if (!c->forcedsplits_filename.empty() &&
       !(learner_type == "serial" && c->feature_fraction_bynode >= 1.0 && !c->extra_trees && c->num_leaves <= 512 &&

@@ -470,6 +470,27 @@ def test_host_policy_over_device_histograms(lgb, gpu_required, rng, extra):
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.1},
+                                   {"cegb_penalty_split": 0.05, "cegb_tradeoff": 0.5, "num_leaves": 63},
+                                   {"cegb_penalty_split": 0.02, "extra_trees": True}])
+def test_device_cegb_split_penalty(lgb, gpu_required, rng, extra):
+    """CEGB's split penalty (tradeoff x penalty_split x rows of the leaf) is applied by the device
+    scans (frontier engine, and the sequential chain with extra_trees): no host split policy, and
+    the model matches the CPU learner's, whose penalty prunes splits of small leaves."""
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    bc = _train(lgb, X, y, "cpu", rounds=4, **extra)
+    bg = _train(lgb, X, y, "gpu", rounds=4, gpu_use_dp=True, **extra)
+    assert "host split policy" not in bg.device_name()
+    tc, tg = _trees(bc), _trees(bg)
+    assert [t["num_leaves"] for t in tc] == [t["num_leaves"] for t in tg]
+    assert [s[:2] for s in _splits(tc[0]["tree_structure"], [])] == [s[:2] for s in _splits(tg[0]["tree_structure"], [])]
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
+    # the penalty bites: fewer leaves than without it
+    b0 = _train(lgb, X, y, "gpu", rounds=1, gpu_use_dp=True, **{k: v for k, v in extra.items() if "cegb" not in k})
+    assert _trees(b0)[0]["num_leaves"] >= tg[0]["num_leaves"]
+
+
 FORCED_TREES = [
     {"feature": 4, "threshold": 0.1, "left": {"feature": 5, "threshold": -0.2}},
     # two levels on both sides, children pushed left then right (breadth-first order)
