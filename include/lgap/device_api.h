@@ -16,6 +16,8 @@ namespace device {
 int DeviceCount();
 // hipDeviceSynchronize on the current device (no-op without a GPU).
 void DeviceSynchronize();
+// Total memory of the current device in bytes (0 without a GPU).
+size_t DeviceTotalMemory();
 // RCCL communicator over xGMI for the multi-GPU learners.
 std::string CommGetUniqueId();
 void CommInit(const std::string& unique_id, int num_ranks, int rank, int device_id);

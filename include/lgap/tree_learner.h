@@ -84,8 +84,10 @@ class TreeLearner {
   virtual void DeviceSample(int plan, int iter) { (void)plan; (void)iter; }
   virtual std::string DeviceName() const { return "cpu"; }
 
+  // `train` (optional) lets the factory size the device learner's per-leaf histograms
+  // against histogram_pool_size / the device memory before choosing it.
   static std::unique_ptr<TreeLearner> Create(const std::string& learner_type, const std::string& device_type,
-                                             bool linear_tree, const Config* config);
+                                             bool linear_tree, const Config* config, const Dataset* train = nullptr);
 };
 
 }  // namespace lgap

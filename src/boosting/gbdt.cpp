@@ -53,7 +53,7 @@ void GBDT::Init(const Config* config, const Dataset* train_data, const Objective
   feature_names_ = train_data->feature_names();
   feature_infos_ = train_data->feature_infos();
   monotone_constraints_ = config->monotone_constraints;
-  learner_ = TreeLearner::Create(config->tree_learner, config->device_type, config->linear_tree, config);
+  learner_ = TreeLearner::Create(config->tree_learner, config->device_type, config->linear_tree, config, train_data);
   learner_->Init(train_data, objective && objective->IsConstantHessian());
   device_mode_ = learner_->OwnsScore();
   sampler_ = std::make_unique<SampleStrategy>(config, train_data, objective, num_tree_per_iteration_);

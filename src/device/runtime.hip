@@ -117,6 +117,13 @@ int DeviceCount() {
   return n;
 }
 
+size_t DeviceTotalMemory() {
+  if (DeviceCount() <= 0) return 0;
+  size_t free_b = 0, total_b = 0;
+  HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+  return total_b;
+}
+
 void DeviceSynchronize() {
   if (DeviceCount() > 0) HIP_CHECK(hipDeviceSynchronize());
 }

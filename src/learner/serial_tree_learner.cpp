@@ -243,9 +243,10 @@ SplitParams SerialTreeLearner::MakeParams() const {
 void SerialTreeLearner::ResetHistPool() {
   const int L = config_->num_leaves;
   int cap = L;
-  if (config_->histogram_pool_size > 0) {
+  const double pool_mb = config_->histogram_pool_size > 0 ? config_->histogram_pool_size : pool_budget_mb_;
+  if (pool_mb > 0) {
     const double per_leaf = 16.0 * train_data_->num_total_bin();  // (grad, hess) doubles per bin
-    cap = static_cast<int>(config_->histogram_pool_size * 1024 * 1024 / per_leaf);
+    cap = static_cast<int>(pool_mb * 1024 * 1024 / per_leaf);
   }
   hist_cap_ = std::min(std::max(2, cap), L);
   Log::Debug("Histogram pool: %d of %d leaves", hist_cap_, L);

@@ -93,6 +93,8 @@ class SerialTreeLearner : public TreeLearner {
   std::string DeviceName() const override;
   // device_type=gpu with a host split policy: histograms are built by the HIP kernels
   void EnableDeviceHistograms() { want_device_hist_ = true; }
+  // bound of the live leaf histograms in MB when histogram_pool_size is unset (<= 0: none)
+  void SetHistPoolBudgetMB(double mb) { pool_budget_mb_ = mb; }
 
  protected:
   // ---- hooks for the parallel learners
@@ -154,6 +156,7 @@ class SerialTreeLearner : public TreeLearner {
   // produced longest ago is dropped first (reference HistogramPool LRU,
   // feature_histogram.hpp:1367-1594)
   int hist_cap_ = 0, hist_live_ = 0;
+  double pool_budget_mb_ = 0.0;
   int64_t hist_clock_ = 0;
   std::vector<int64_t> hist_stamp_;
   std::vector<std::vector<char>> splittable_;        // per leaf, per feature

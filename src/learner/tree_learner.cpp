@@ -25,8 +25,25 @@ std::unique_ptr<TreeLearner> CreateHost(const std::string& learner_type, bool li
   return nullptr;
 }
 
+// The device learner keeps one fp64 (g, h) histogram per open leaf (2 x 8 bytes per bin,
+// device_learner.hip slots; the frontier engine adds its speculation slots inside an 8 GiB
+// cap). When num_leaves of them exceed histogram_pool_size (MB, when set) or half of the
+// device memory, training takes the host learner, whose LRU pool bounds the live
+// histograms and rebuilds evicted ones from rows (reference feature_histogram.hpp
+// HistogramPool), with the histograms still built by the HIP kernels.
+bool DeviceHistogramsExceedPool(const Config* c, const Dataset* train) {
+  if (train == nullptr) return false;
+  const double per_leaf = 16.0 * static_cast<double>(std::max(1, train->num_total_bin()));
+  const double need = per_leaf * std::max(2, c->num_leaves);
+  double budget = 0.5 * static_cast<double>(device::DeviceTotalMemory());
+  if (c->histogram_pool_size > 0) budget = c->histogram_pool_size * 1024.0 * 1024.0;
+  return budget > 0 && need > budget;
+}
+
 // Why the device-resident learner cannot serve `config` (nullptr = it can).
-const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, const Config* c) {
+const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, const Config* c,
+                             const Dataset* train) {
+  if (DeviceHistogramsExceedPool(c, train)) return "per-leaf device histograms above the histogram pool";
   if (linear_tree) return "linear_tree";
   // (voting runs on the device; its global pass redraws no extra-trees thresholds)
   if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
@@ -55,16 +72,21 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
 }  // namespace
 
 std::unique_ptr<TreeLearner> TreeLearner::Create(const std::string& learner_type, const std::string& device_type,
-                                                 bool linear_tree, const Config* config) {
+                                                 bool linear_tree, const Config* config, const Dataset* train) {
   if (device_type == "gpu" || device_type == "cuda") {
     if (device::DeviceCount() <= 0) {
       Log::Fatal("device_type=%s requested but no AMD GPU (gfx950) is visible to HIP", device_type.c_str());
     }
-    const char* why = HostPolicyReason(learner_type, linear_tree, config);
+    const char* why = HostPolicyReason(learner_type, linear_tree, config, train);
     if (why == nullptr) return device::CreateDeviceTreeLearner(config, learner_type);
     Log::Info("%s: host split policy over HIP histograms", why);
     auto learner = CreateHost(learner_type, linear_tree, config);
-    static_cast<SerialTreeLearner*>(learner.get())->EnableDeviceHistograms();
+    auto* serial = static_cast<SerialTreeLearner*>(learner.get());
+    serial->EnableDeviceHistograms();
+    // routed here by the histogram bound: keep the host pool within the same budget
+    if (DeviceHistogramsExceedPool(config, train) && config->histogram_pool_size <= 0) {
+      serial->SetHistPoolBudgetMB(0.5 * static_cast<double>(device::DeviceTotalMemory()) / (1024.0 * 1024.0));
+    }
     return learner;
   }
   if (device_type != "cpu") Log::Fatal("Unknown device type %s", device_type.c_str());

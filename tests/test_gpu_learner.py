@@ -491,6 +491,25 @@ def test_device_cegb_split_penalty(lgb, gpu_required, rng, extra):
     assert _trees(b0)[0]["num_leaves"] >= tg[0]["num_leaves"]
 
 
+def test_histogram_pool_bound_routes_to_pooled_learner(lgb, gpu_required, rng):
+    """num_leaves per-leaf device histograms above histogram_pool_size: training takes the host
+    learner's LRU histogram pool (evicted histograms rebuilt from rows by the HIP kernels) instead
+    of the device learner's one-slot-per-leaf store; the model equals the pooled CPU learner's."""
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    # 6 features x 255 bins x 16 B ~ 24 KB per leaf: 63 leaves ~ 1.5 MB > 1 MB
+    extra = {"num_leaves": 63, "histogram_pool_size": 1.0}
+    bc = _train(lgb, X, y, "cpu", rounds=3, **extra)
+    bg = _train(lgb, X, y, "gpu", rounds=3, gpu_use_dp=True, **extra)
+    assert "host split policy" in bg.device_name()
+    assert [s[:2] for s in _splits(_trees(bc)[0]["tree_structure"], [])] == \
+        [s[:2] for s in _splits(_trees(bg)[0]["tree_structure"], [])]
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
+    # within the pool: the device learner
+    bd = _train(lgb, X, y, "gpu", rounds=1, num_leaves=63, histogram_pool_size=64.0)
+    assert "host split policy" not in bd.device_name()
+
+
 FORCED_TREES = [
     {"feature": 4, "threshold": 0.1, "left": {"feature": 5, "threshold": -0.2}},
     # two levels on both sides, children pushed left then right (breadth-first order)
