@@ -873,7 +873,7 @@ def test_row_per_thread_histograms_match(lgb, gpu_required, rng, monkeypatch, fe
     models = []
     for rpt in ("1", "0"):
         monkeypatch.setenv("LGAP_FHIST_RPT", rpt)
-        b = lgb.train(params, lgb.Dataset(X, y, params=params), 10)
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 10, keep_training_booster=True)
         assert "frontier" in b.device_name()
         models.append((b.model_to_string().split("end of trees")[0], b.predict(X, raw_score=True)))
     assert models[0][0] == models[1][0]
