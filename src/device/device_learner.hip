@@ -1329,11 +1329,15 @@ class DeviceTreeLearner : public TreeLearner {
   // A / B are the first / second half of the round's expansions (their accumulator rows are
   // contiguous), so half A's all-reduce overlaps half B's histograms and half B's overlaps
   // half A's scans. The histogram grid stops short of the CU count (7/8), which leaves the
-  // RCCL kernel CUs of its own. LGAP_DP_PIPELINE=0 keeps the serial order.
+  // RCCL kernel CUs of its own. Opt-in (LGAP_DP_PIPELINE=1): on a one-rank communicator the
+  // extra launches and the two cross-stream event waits per round cost more than an
+  // all-reduce of a round's accumulators (1.25M rows: 529.6 it/s pipelined vs 754.5 serial;
+  // 10M: 289.2 vs 361.0; profiles/r03/dp_pipeline_ab.txt), so the serial order is the default
+  // until a multi-GPU node shows the overlap paying for them.
   bool FrontierPipelined(int kb) const {
     if (!distributed_ || HostStagedDP() || !CommExists() || kb < 2) return false;
     const char* e = std::getenv("LGAP_DP_PIPELINE");
-    return e == nullptr || e[0] != '0';
+    return e != nullptr && e[0] == '1';
   }
 
   void EnsureCommStream() {
