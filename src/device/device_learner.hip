@@ -1301,6 +1301,7 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
+    a.sel_bitonic = std::getenv("LGAP_SEL_BITONIC") != nullptr ? 1 : 0;
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;

@@ -191,6 +191,7 @@ struct FArgs {
   // the first half's all-reduce runs on the comm stream while the second half's histograms
   // build); 0 / kFrontierKmax: the whole round
   int e_lo, e_hi;
+  int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
   SplitParams sp;
 };
 

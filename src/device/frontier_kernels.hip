@@ -1543,6 +1543,27 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     // uncommitted node. The blocked node always goes first.
     int P2 = 64;
     while (P2 < na) P2 <<= 1;
+    if (na <= static_cast<int>(blockDim.x) && !a.sel_bitonic) {
+      // rank sort (one barrier instead of the bitonic network's log2(P2)(log2(P2)+1)/2): thread
+      // i's position = alive nodes ordered before it; keys are unique (cids), so the ranks are
+      // a permutation and the order is the bitonic sort's
+      int ri = 0, ci = 0, pos = 0;
+      double gi = 0.0;
+      if (t < na) {
+        ri = s_ac[t];
+        ci = ri >= 0 ? ri : ~ri;
+        gi = s_gain[ci];
+        for (int j = 0; j < na; ++j) {
+          const int rj = s_ac[j];
+          const int cj = rj >= 0 ? rj : ~rj;
+          const double gj = s_gain[cj];
+          pos += (gj > gi || (gj == gi && cj < ci)) ? 1 : 0;
+        }
+      }
+      __syncthreads();  // (s_sc may alias nothing here, but keep reads before the scatter)
+      if (t < na) s_sc[pos] = ri;
+      __syncthreads();
+    } else {
     for (int i = t; i < P2; i += blockDim.x) {
       if (i < na) {
         const int c = s_ac[i] >= 0 ? s_ac[i] : ~s_ac[i];
@@ -1573,6 +1594,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         }
         __syncthreads();
       }
+    }
     }
     // eligible ranks: exclusive scan of the eligible (non-blocked) flags in sorted order
     constexpr int kPer = kFrontierMaxNodes / kFSelThreads;  // <= 4 positions per thread
