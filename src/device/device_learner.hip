@@ -1050,7 +1050,12 @@ class DeviceTreeLearner : public TreeLearner {
     if (!FrontierSerial() && !FrontierDP()) return false;
     if (use_bynode_ || config_->extra_trees || scan_global_) return false;
     if (FrontierCapacity() > kFrontierMaxNodes || F_ <= 0) return false;
-    return FrontierSelectLds(FrontierCapacity(), L_) <= 150 * 1024;
+    return FrontierSelectLds(FrontierCapacity(), L_) + (CegbCoupled() ? F_ + 16 : 0) <= 150 * 1024;
+  }
+  // CEGB coupled feature penalties run in the frontier select (FArgs::cegb_coupled); the lazy
+  // per-row penalties stay a host policy (tree_learner.cpp routes those configurations)
+  bool CegbCoupled() const {
+    return !config_->cegb_penalty_feature_coupled.empty() && config_->cegb_penalty_feature_lazy.empty();
   }
   bool FrontierSerial() const {
     return mode_ == DevParallel::kSerial && !owner_scan_ && !voting_ && !distributed_;
@@ -1124,6 +1129,10 @@ class DeviceTreeLearner : public TreeLearner {
       Log::Fatal("forced splits on the device need the frontier engine (serial learner, num_leaves <= 512, "
                  "no feature_fraction_bynode / extra_trees)");
     }
+    if (!frontier_ && CegbCoupled()) {
+      Log::Fatal("cegb_penalty_feature_coupled on the device needs the frontier engine (serial learner, "
+                 "num_leaves <= 496, no feature_fraction_bynode / extra_trees)");
+    }
     if (!frontier_) return;
     fkmax_ = FrontierKmax();
     fC_ = FrontierCapacity();
@@ -1156,6 +1165,25 @@ class DeviceTreeLearner : public TreeLearner {
     ffbest_ = reinterpret_cast<SplitInfo*>(b + o_fbest);
     ffkey_ = reinterpret_cast<SplitKey*>(b + o_fkey);
     UploadForcedSplits();
+    if (CegbCoupled()) {
+      // tradeoff x coupled penalty per inner feature; used flags and the event count persist
+      // over the trees of this training set (host CegbPenalty::Init)
+      const auto& cp = config_->cegb_penalty_feature_coupled;
+      if (static_cast<int>(cp.size()) != data_->num_total_features()) {
+        Log::Fatal("cegb_penalty_feature_coupled should be the same size as feature number.");
+      }
+      std::vector<double> h(F_);
+      for (int f = 0; f < F_; ++f) h[f] = config_->cegb_tradeoff * cp[data_->feature(f).real_index];
+      cegb_coupled_.Resize(F_);
+      cegb_coupled_.Upload(h.data(), h.size(), stream_);
+      cegb_used_.Resize(F_);
+      cegb_used_.Zero(stream_);
+      cegb_epoch_.Resize(1);
+      cegb_epoch_.Zero(stream_);
+      fnkey_.Resize(C * F);
+      fninfo_.Resize(C * F);
+      fnuep_.Resize(C);
+    }
     // replay results: coherent pinned host memory the results kernel writes directly
     const size_t rbytes = FrontierResultBytes(L_);
     if (rbytes > fres_bytes_) {
@@ -1301,6 +1329,15 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
+    if (CegbCoupled() && cegb_coupled_.size() >= static_cast<size_t>(F_)) {
+      a.cegb_coupled = cegb_coupled_.get();
+      a.cegb_tradeoff = config_->cegb_tradeoff;
+      a.cegb_used = cegb_used_.get();
+      a.cegb_epoch = cegb_epoch_.get();
+      a.nkey = fnkey_.get();
+      a.ninfo = fninfo_.get();
+      a.nuep = fnuep_.get();
+    }
     a.sel_bitonic = std::getenv("LGAP_SEL_BITONIC") != nullptr ? 1 : 0;
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
@@ -2688,6 +2725,14 @@ class DeviceTreeLearner : public TreeLearner {
   int fpred_rounds_ = 16, frounds_hist_[4] = {1, 1, 1, 1}, frounds_pos_ = 0;
   // data-parallel per-round expansion caps (= all-reduce sizes) from the last trees' rounds
   DevBuf<FForced> fforced_;
+  // CEGB coupled penalties (frontier select): penalties, used flags, event count, per-node
+  // raw candidates and the event count each node's best was scored at
+  DevBuf<double> cegb_coupled_;
+  DevBuf<uint8_t> cegb_used_;
+  DevBuf<unsigned> cegb_epoch_;
+  DevBuf<SplitKey> fnkey_;
+  DevBuf<SplitInfo> fninfo_;
+  DevBuf<int> fnuep_;
   int fnum_forced_ = 0;
   SplitInfo* ffbest_ = nullptr;
   SplitKey* ffkey_ = nullptr;

@@ -69,6 +69,7 @@ __host__ __device__ inline int FrontierDepthBuf(int j) { return j < 2 ? j : j + 
 // node state bits (FArgs::nstate)
 constexpr uint8_t kNodeExpanded = 1;   // children computed
 constexpr uint8_t kNodeCommitted = 2;  // its split is part of the tree (replay)
+constexpr uint8_t kNodeDead = 4;       // below an expansion the CEGB replay invalidated: never used
 // stamp slots: kernel ids and the per-kernel slot count (slot 7: latest block exit)
 constexpr int kFStampPart = 0, kFStampHist = 1, kFStampScan = 2, kFStampSel = 3, kFStampSlots = 8;
 
@@ -179,6 +180,18 @@ struct FArgs {
   int max_depth, use_monotone;
   double monotone_penalty;
   double cegb_split;  // cegb_tradeoff * cegb_penalty_split (per row of the node), 0: none
+  // CEGB coupled feature penalties (cegb_penalty_feature_coupled) on the device, host
+  // CegbPenalty semantics: the scan publishes RAW candidate gains (key.pad0 = monotone type)
+  // and the select applies split / coupled / monotone penalties against the persistent
+  // used-feature flags; a feature's first use in the replay refunds the other leaves' stored
+  // candidates (leaf-index chain, as the host's per-leaf table) and invalidates speculation
+  const double* cegb_coupled;  // [F] tradeoff x coupled penalty per inner feature, null: off
+  double cegb_tradeoff;
+  uint8_t* cegb_used;          // [F] feature used by a split (persists across trees)
+  unsigned* cegb_epoch;        // [1] first-use events so far
+  SplitKey* nkey;              // [C][F] every computed node's raw per-feature candidates
+  SplitInfo* ninfo;            // [C][F]
+  int* nuep;                   // [C] cegb_epoch its best was computed at
   int max_bin, cat_p2;
   int use_dp;       // gpu_use_dp: 64-bit LDS accumulators
   int spec_cap;     // speculative expansions per round beyond the budget (policy knob)
@@ -222,7 +235,13 @@ void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s)
 int FrontierPartitionBlocksPerCU(int iters);
 // one-time kernel attributes (dynamic LDS above 64 KiB)
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width);
-size_t FrontierSelectLds(int C, int L);
+// dynamic LDS of k_f_select (CEGB coupled penalties add F bytes of used flags after it)
+__host__ __device__ inline size_t FrontierSelectLds(int C, int L) {
+  return static_cast<size_t>(C) * (sizeof(double) + 6 * sizeof(int) + 1) + 64 +
+         static_cast<size_t>(L) * (3 * sizeof(int) + sizeof(double) + sizeof(int)) + 64 +
+         static_cast<size_t>(FrontierSortCap(C)) * (sizeof(double) + sizeof(int));
+}
+
 
 }  // namespace device
 }  // namespace lgap

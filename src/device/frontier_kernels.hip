@@ -687,9 +687,12 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
           } else {
             out->feature = f;
             // cost-effective gradient boosting, split penalty (host CegbPenalty::DeltaGain:
-            // subtracted before the monotone penalty multiplies the gain)
-            if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
-            if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
+            // subtracted before the monotone penalty multiplies the gain). With coupled
+            // penalties the candidate stays raw: the select applies every penalty (CegbAdjust)
+            if (a.cegb_coupled == nullptr) {
+              if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
+              if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
+            }
             if (a.ic && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
           }
         }
@@ -769,6 +772,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         kk.missing = fi.missing;
         kk.default_left = out->default_left;
         kk.is_cat = fi.bin_type != 0 ? 1 : 0;
+        kk.pad0 = a.cegb_coupled != nullptr && out->feature >= 0 ? out->monotone_type : 0;
       }
     }
     __syncthreads();
@@ -1197,6 +1201,29 @@ __device__ __forceinline__ bool FBetter(double ga, int fa, int la, double gb, in
   return la < lb;
 }
 
+// CEGB with coupled penalties: the penalised gain of a RAW candidate key at the current
+// used-feature flags (host SerialTreeLearner::ScoreFeature: gain -= CegbPenalty::DeltaGain,
+// then the monotone penalty multiplies a monotone split; key.pad0 = its monotone type)
+__device__ __forceinline__ double CegbAdjust(const FArgs& a, const SplitKey& k, int n, int depth, const uint8_t* used) {
+  if (k.feature < 0) return kMinScore;
+  double delta = a.cegb_split * n;
+  if (!used[k.feature]) delta += a.cegb_coupled[k.feature];
+  double g = k.gain - delta;
+  if (k.pad0 != 0) g *= MonotonePenaltyAt(a.monotone_penalty, depth);
+  return g;
+}
+
+// copy the stored raw candidate (node x, feature slot f) into node c's best / key with gain g
+// (one lane: the CEGB refund / re-score paths are rare)
+__device__ __forceinline__ void CegbSetBest(const FArgs& a, int c, size_t src, double g) {
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+  for (int i = 0; i < kInfoWords; ++i) reinterpret_cast<uint32_t*>(a.best + c)[i] = reinterpret_cast<const uint32_t*>(a.ninfo + src)[i];
+  for (int i = 0; i < kKeyWords; ++i) reinterpret_cast<uint32_t*>(a.key + c)[i] = reinterpret_cast<const uint32_t*>(a.nkey + src)[i];
+  a.best[c].gain = g;
+  a.key[c].gain = g;
+}
+
 constexpr int kSelWaves = kFSelThreads / 64;
 constexpr int kSelPairs = 2 * kFrontierKmax / kSelWaves;  // (expansion, child) pairs per wave
 
@@ -1244,6 +1271,13 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     s_fidx[c] = nd.fidx;
   }
   for (int l = t; l < st.num_leaves; l += blockDim.x) s_lcid[l] = a.leaf_cid[l];
+  // CEGB coupled penalties: used-feature flags (after the sort scratch) and the event count
+  const bool cegb = a.cegb_coupled != nullptr;
+  uint8_t* s_used = reinterpret_cast<uint8_t*>(smem + FrontierSelectLds(C, L));
+  const unsigned epoch0 = cegb ? *a.cegb_epoch : 0u;
+  if (cegb) {
+    for (int f = t; f < F; f += blockDim.x) s_used[f] = a.cegb_used[f];
+  }
   if (t < 2 * kFrontierKmax) {
     int c = -1;
     if (t < np) {
@@ -1260,12 +1294,18 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   // ---- A. children of the last round: best over features (all pairs' keys in flight)
   {
     double bg[kSelPairs];
-    int bf[kSelPairs], bp[kSelPairs];
+    int bf[kSelPairs], bp[kSelPairs], pn[kSelPairs], pd[kSelPairs];
 #pragma unroll
     for (int j = 0; j < kSelPairs; ++j) {
       bg[j] = kMinScore;
       bf[j] = 0x7fffffff;
       bp[j] = -1;
+      pn[j] = pd[j] = 0;
+      const int q = w + j * kSelWaves;
+      if (cegb && q < np && s_pc[q] >= 0) {
+        pn[j] = a.nodes[s_pc[q]].gcount;
+        pd[j] = s_dep[s_pc[q]];
+      }
     }
     for (int f0 = 0; f0 < F; f0 += 64) {
       const int f = f0 + lane;
@@ -1275,7 +1315,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         if (q < np && f < F && s_pc[q] >= 0) {
           const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
           const int kf = kk.feature;
-          const double g = kf < 0 ? kMinScore : kk.gain;
+          const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used) : kk.gain);
           const int ff = kf < 0 ? 0x7fffffff : kf;
           if (FBetter(g, ff, 0, bg[j], bf[j], 0)) {
             bg[j] = g;
@@ -1322,10 +1362,40 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         kz.pad2 = 0;
         a.key[c] = kz;
       }
+      if (cegb) {
+        // the child's raw candidates of every feature, kept for refunds / re-scoring (skipped
+        // expansions' children: none); its best carries the penalised gain
+        constexpr int kRow = kKeyWords + kInfoWords;
+        const size_t dst = static_cast<size_t>(c) * F;
+        for (int i = lane; i < F * kRow; i += 64) {
+          const int f = i / kRow, o = i - f * kRow;
+          const size_t src = static_cast<size_t>(q) * F + f;
+          if (pc < 0) {
+            if (o == 0) a.nkey[dst + f].feature = -1;
+          } else if (o < kKeyWords) {
+            reinterpret_cast<uint32_t*>(a.nkey + dst + f)[o] = reinterpret_cast<const uint32_t*>(a.ckey + src)[o];
+          } else {
+            reinterpret_cast<uint32_t*>(a.ninfo + dst + f)[o - kKeyWords] = reinterpret_cast<const uint32_t*>(a.cinfo + src)[o - kKeyWords];
+          }
+        }
+        if (lane == 0) a.nuep[c] = static_cast<int>(epoch0);
+      }
       if (lane == 0) {
         s_gain[c] = valid ? g : kMinScore;
         s_feat[c] = valid ? ff : -1;
-        s_cpos[c - base] = valid ? static_cast<int>(static_cast<size_t>(q) * F + fpos) : -1;
+        // (CEGB: the penalised best lives in best / key only)
+        s_cpos[c - base] = valid && !cegb ? static_cast<int>(static_cast<size_t>(q) * F + fpos) : -1;
+      }
+    }
+  }
+  __syncthreads();
+  if (cegb) {
+    // penalised gains into the best / key records phase A copied (raw) above
+    for (int q = t; q < np; q += blockDim.x) {
+      const int c = s_pc[q];
+      if (c >= 0 && s_feat[c] >= 0) {
+        a.best[c].gain = s_gain[c];
+        a.key[c].gain = s_gain[c];
       }
     }
   }
@@ -1349,6 +1419,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   if (w == 0) {
     int nl = st.num_leaves, ns = st.num_splits, done = 0, blocked = -1, nc = 0;
     int fnext = st.forced_next, bforced = 0;
+    unsigned epoch = epoch0;  // CEGB first-use events (wave-uniform)
     for (;;) {
       if (nl >= L) {
         done = 1;
@@ -1428,6 +1499,122 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         blocked = c;
         break;
       }
+      if (cegb) {
+        if (!s_used[bf]) {
+          // first use of feature bf (host CegbPenalty::OnSplit): every other leaf's stored
+          // candidate on bf -- the last valid one along its leaf index's chain of left
+          // children, as the host's per-leaf table -- is refunded and may become its best
+          const double refund = a.cegb_coupled[bf];
+          for (int l = lane; l < nl; l += 64) {
+            if (l == bl || !(s_lg[l] > kMinScore)) continue;
+            int x = s_lcid[l], found = -1;
+            for (;;) {
+              if (a.nkey[static_cast<size_t>(x) * F + bf].feature >= 0) {
+                found = x;
+                break;
+              }
+              const int px = s_par[x];
+              if (px < 0 || s_left[px] != x) break;
+              x = px;
+            }
+            if (found < 0) continue;
+            const size_t src = static_cast<size_t>(found) * F + bf;
+            const double rg = a.nkey[src].gain + refund;
+            if (!FBetter(rg, bf, 0, s_lg[l], s_lf[l], 0)) continue;
+            const int cl = s_lcid[l];
+            s_lg[l] = rg;
+            s_lf[l] = bf;
+            s_gain[cl] = rg;
+            s_feat[cl] = bf;
+            CegbSetBest(a, cl, src, rg);
+            if (cl >= base && cl - base < 2 * kFrontierKmax) s_cpos[cl - base] = -1;
+          }
+          // speculation grown under the old gains is void: uncommitted expansions become
+          // unexpanded again, everything below them dead
+          for (int x = lane; x < cid_next; x += 64) {
+            const uint8_t sx = s_st[x];
+            if ((sx & kNodeExpanded) && !(sx & kNodeCommitted) && x != c) {
+              s_st[x] = static_cast<uint8_t>((sx & ~kNodeExpanded) | 0x80);  // 0x80: children to kill
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          for (bool more = true; more;) {  // parents precede children (cids grow with depth)
+            bool ch = false;
+            for (int x = lane; x < cid_next; x += 64) {
+              const int px = s_par[x];
+              if (px < 0 || (s_st[x] & kNodeDead)) continue;
+              if ((s_st[px] & 0x80) || (s_st[px] & kNodeDead)) {
+                s_st[x] = static_cast<uint8_t>(s_st[x] | kNodeDead);
+                ch = true;
+              }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            more = __ballot(ch) != 0ull;
+          }
+          for (int x = lane; x < cid_next; x += 64) {
+            const uint8_t sx = s_st[x];
+            if (sx & 0x80) {
+              s_left[x] = -1;
+              a.nodes[x].left = -1;
+            }
+            const uint8_t nsx = static_cast<uint8_t>(sx & ~0x80);
+            s_st[x] = nsx;
+            if (nsx != sx || (nsx & kNodeDead)) a.nstate[x] = nsx;
+          }
+          if (lane == 0) {
+            s_used[bf] = 1;
+            a.cegb_used[bf] = 1;
+            *a.cegb_epoch = epoch + 1u;
+          }
+          ++epoch;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        // the children are scored at the flags after this split (the host evaluates them
+        // after OnSplit): re-score from their raw candidates when an event came since
+#pragma unroll 1
+        for (int ch = left; ch <= left + 1; ++ch) {
+          if (static_cast<unsigned>(a.nuep[ch]) == epoch) continue;
+          const int n = a.nodes[ch].gcount, d = s_dep[ch];
+          double cg = kMinScore;
+          int cf = 0x7fffffff, cp = -1;
+          for (int f = lane; f < F; f += 64) {
+            const SplitKey& kk = a.nkey[static_cast<size_t>(ch) * F + f];
+            if (kk.feature < 0) continue;
+            const double g = CegbAdjust(a, kk, n, d, s_used);
+            if (FBetter(g, kk.feature, 0, cg, cf, 0)) {
+              cg = g;
+              cf = kk.feature;
+              cp = f;
+            }
+          }
+          const int src = WaveArgBestLane(cg, cf, 0);
+          cg = ReadLane(cg, src);
+          cf = ReadLane(cf, src);
+          cp = ReadLane(cp, src);
+          if (lane == 0) {
+            if (cp >= 0) {
+              CegbSetBest(a, ch, static_cast<size_t>(ch) * F + cp, cg);
+            } else {
+              a.best[ch].Reset();
+              a.key[ch].feature = -1;
+              a.key[ch].gain = kMinScore;
+            }
+            s_gain[ch] = cp >= 0 ? cg : kMinScore;
+            s_feat[ch] = cp >= 0 ? cf : -1;
+            a.nuep[ch] = static_cast<int>(epoch);
+            if (ch >= base && ch - base < 2 * kFrontierKmax) s_cpos[ch - base] = -1;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+      }
       if (lane == 0) {
         s_c0[nc] = bl;
         s_c1[nc] = c;
@@ -1502,7 +1689,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       bool alive = false, elig = false, unc = false;
       if (c < cid_next) {
         const uint8_t sc = s_st[c];
-        alive = !(sc & kNodeCommitted) && s_feat[c] >= 0 && s_gain[c] > 0.0;
+        alive = !(sc & (kNodeCommitted | kNodeDead)) && s_feat[c] >= 0 && s_gain[c] > 0.0;
         elig = alive && !(sc & kNodeExpanded);
         // while forced splits are pending, their nodes are expanded only by them (the blocked one)
         if (elig && s_fnext >= 0 && s_fidx[c] >= 0 && c != s_blocked) elig = false;
@@ -1829,14 +2016,9 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
   HIP_CHECK(hipGetLastError());
 }
 
-size_t FrontierSelectLds(int C, int L) {
-  return static_cast<size_t>(C) * (sizeof(double) + 6 * sizeof(int) + 1) + 64 +
-         static_cast<size_t>(L) * (3 * sizeof(int) + sizeof(double) + sizeof(int)) + 64 +
-         static_cast<size_t>(FrontierSortCap(C)) * (sizeof(double) + sizeof(int));
-}
 
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
-  k_f_select<<<1, kFSelThreads, FrontierSelectLds(a.C, a.L), s>>>(a);
+  k_f_select<<<1, kFSelThreads, FrontierSelectLds(a.C, a.L) + (a.cegb_coupled != nullptr ? a.F + 16 : 0), s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -491,6 +491,28 @@ def test_device_cegb_split_penalty(lgb, gpu_required, rng, extra):
     assert _trees(b0)[0]["num_leaves"] >= tg[0]["num_leaves"]
 
 
+@pytest.mark.parametrize("extra", [{"cegb_penalty_feature_coupled": [500, 300, 100, 100, 30, 30]},
+                                   {"cegb_penalty_feature_coupled": [0, 0, 40, 40, 10, 10], "cegb_penalty_split": 0.002,
+                                    "cegb_tradeoff": 0.7, "num_leaves": 63},
+                                   {"cegb_penalty_feature_coupled": [3000, 100, 60, 60, 20, 40],
+                                    "monotone_constraints": [1, -1, 0, 0, 0, 0]}])
+def test_device_cegb_coupled_penalties(lgb, gpu_required, rng, extra):
+    """CEGB coupled feature penalties in the frontier select: raw candidates kept per node, the
+    penalty of a feature not yet used by any split subtracted, and a feature's first use in the
+    replay refunding every other leaf's stored candidate (leaf-index chain) and voiding the
+    speculative expansions grown under the old gains. Trees equal the host CegbPenalty learner's
+    split for split, over several trees (the used flags persist across trees)."""
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    bc = _train(lgb, X, y, "cpu", rounds=4, **extra)
+    bg = _train(lgb, X, y, "gpu", rounds=4, gpu_use_dp=True, **extra)
+    assert "host split policy" not in bg.device_name() and "frontier" in bg.device_name()
+    tc, tg = _trees(bc), _trees(bg)
+    for a, b in zip(tc, tg):
+        assert [s[:2] for s in _splits(a["tree_structure"], [])] == [s[:2] for s in _splits(b["tree_structure"], [])]
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-4)
+
+
 def test_histogram_pool_bound_routes_to_pooled_learner(lgb, gpu_required, rng):
     """num_leaves per-leaf device histograms above histogram_pool_size: training takes the host
     learner's LRU histogram pool (evicted histograms rebuilt from rows by the HIP kernels) instead
