@@ -5,7 +5,7 @@ set -u
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "cegb or frontier_engine or forced_splits_on or first_tree or host_policy" > $OUT/tc.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "cegb or frontier_engine or forced_splits_on or host_policy" > $OUT/tc.log 2>&1; rc=$?
 grep -E "PASS|FAIL|Error|assert" $OUT/tc.log | tail -40
 [ $rc -ne 0 ] && exit $rc
 run() {  # run <name> <limit> <cmd...>

@@ -1286,10 +1286,6 @@ class DeviceTreeLearner : public TreeLearner {
     a.hist_min_rows = HistMinRows();
     a.hist_grid = FrontierHistBlocks();
     a.hist_threads = fhist_threads_;
-    {
-      const char* e = std::getenv("LGAP_FHIST_RPT");  // A/B knob
-      a.hist_rpt = e != nullptr && e[0] == '1' ? 1 : 0;
-    }
     if (nib_) {
       a.rowbins = rowbins4_.get();
       a.stride_dw = stride4_dw_;

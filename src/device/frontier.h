@@ -172,7 +172,6 @@ struct FArgs {
   unsigned* bar;  // bar[2]: bounded-wait error flag
   int hist_min_rows, hist_grid;
   int hist_threads;  // 512 or 1024 threads per histogram block
-  int hist_rpt;      // row-per-thread histogram loop (FHistRowsRPT) where the shape allows
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)

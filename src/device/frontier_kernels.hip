@@ -23,9 +23,6 @@ namespace {
 constexpr int kFPartThreads = 256;
 constexpr int kFScanThreads = 256;
 constexpr int kFSelThreads = 1024;
-#ifndef LGAP_FHIST_RPT_R
-#define LGAP_FHIST_RPT_R 4  // rows in flight per lane of the row-per-thread histogram loop
-#endif
 #ifndef LGAP_FHIST_R
 #define LGAP_FHIST_R 16
 #endif
@@ -231,121 +228,6 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   }
 }
 
-// Row-per-thread variant of FHistRows for single-tile 8-bit rows of NDW <= 8 dwords
-// (MODE 0 / 3): a lane loads its whole row and its (g, h) once, then adds the row's
-// groups dword by dword starting at dword (lane % NDW). The rotation keeps a wave's
-// concurrent LDS atomics spread over NDW dwords' groups, as in the dword-per-lane loop
-// (without it all 64 lanes hit one group's bins at once: measured slower), with about
-// 2 * NDW / 3 times fewer load instructions per row (one (g, h) load instead of NDW).
-template <int MODE, int NDW>
-__device__ __forceinline__ void FHistRowsRPT(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
-                                             const int* gst, unsigned long long* hist, float sg, float sh,
-                                             uint32_t* hist32) {
-  constexpr int R = LGAP_FHIST_RPT_R;
-  const int rot = (threadIdx.x & 63) % NDW;
-  // group offsets in this lane's rotated dword order (go[s][k]: dword (rot + s) mod NDW, byte k)
-  int go[NDW][4];
-#pragma unroll
-  for (int s = 0; s < NDW; ++s) {
-    const int d = rot + s < NDW ? rot + s : rot + s - NDW;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int g = 4 * d + k;
-      go[s][k] = g < tile.g1 ? gst[g - tile.g0] : -1;
-    }
-  }
-  const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
-  const uint16_t* ghq = MODE >= 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
-  const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
-  const int base = buf < 0 ? start : 0;
-  const int step = static_cast<int>(blockDim.x);
-  for (int p0 = rb + static_cast<int>(threadIdx.x); p0 < re; p0 += step * R) {
-    int rows[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int p = p0 + j * step;
-      rows[j] = p < re ? (idx ? idx[p] : base + p) : -1;
-    }
-    uint32_t w[R][NDW];
-    float2 v[R];
-    uint32_t q[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      // unconditional loads (row 0 stands in for a missing row; its bins are masked below) so
-      // the row's dwords merge into wide loads
-      const uint32_t* src = a.rowbins + static_cast<size_t>(rows[j] >= 0 ? rows[j] : 0) * NDW;
-#pragma unroll
-      for (int d = 0; d < NDW; ++d) w[j][d] = src[d];
-      if (rows[j] < 0) {
-#pragma unroll
-        for (int d = 0; d < NDW; ++d) w[j][d] = 0u;
-      }
-      if (MODE >= 2) q[j] = rows[j] >= 0 ? ghq[rows[j]] : 0u;
-      else v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      unsigned long long pg = 0ull;
-      uint32_t p32 = 0u;
-      if (MODE == 3) {
-        p32 = (static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(q[j] >> 8))) << 16) + (q[j] & 0xFFu);
-      } else {
-        const long long ig = __float2int_rn(v[j].x * sg);
-        const long long ih = __float2int_rn(v[j].y * sh);
-        pg = (static_cast<unsigned long long>(ig) << 32) + static_cast<unsigned long long>(ih);
-      }
-      // rotate the row's words by `rot` (barrel stages of 1, 2, 4 dwords mod NDW)
-      uint32_t ww[NDW];
-#pragma unroll
-      for (int d = 0; d < NDW; ++d) ww[d] = w[j][d];
-#pragma unroll
-      for (int b = 1; b < NDW; b <<= 1) {
-        uint32_t t2[NDW];
-        const bool on = (rot & b) != 0;
-#pragma unroll
-        for (int d = 0; d < NDW; ++d) t2[d] = on ? ww[(d + b) % NDW] : ww[d];
-#pragma unroll
-        for (int d = 0; d < NDW; ++d) ww[d] = t2[d];
-      }
-#pragma unroll
-      for (int s = 0; s < NDW; ++s) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t bin = (ww[s] >> (8 * k)) & 0xFFu;
-          if (bin != 0u && go[s][k] >= 0) {
-            const int o = go[s][k] + static_cast<int>(bin);
-            if (MODE == 3) atomicAdd(&hist32[o], p32);
-            else atomicAdd(&hist[o], pg);
-          }
-        }
-      }
-    }
-  }
-}
-
-// FHistRows or, when enabled (FArgs::hist_rpt) and the shape allows, FHistRowsRPT
-template <int W, int MODE>
-__device__ __forceinline__ void FHistRowsSel(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
-                                             const int* gst, unsigned long long* hist, float sg, float sh, double dsg,
-                                             double dsh, uint32_t* hist32 = nullptr) {
-  if constexpr (W == 1 && (MODE == 0 || MODE == 3)) {
-    if (a.hist_rpt && tile.d0 == 0 && tile.d1 == a.stride_dw) {
-      switch (a.stride_dw) {
-        case 1: FHistRowsRPT<MODE, 1>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        case 2: FHistRowsRPT<MODE, 2>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        case 3: FHistRowsRPT<MODE, 3>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        case 4: FHistRowsRPT<MODE, 4>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        case 5: FHistRowsRPT<MODE, 5>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        case 6: FHistRowsRPT<MODE, 6>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        case 7: FHistRowsRPT<MODE, 7>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        case 8: FHistRowsRPT<MODE, 8>(a, tile, buf, start, rb, re, gst, hist, sg, sh, hist32); return;
-        default: break;
-      }
-    }
-  }
-  FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh, hist32);
-}
-
 template <int W, int MODE, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   extern __shared__ __align__(8) unsigned char lds_raw[];
@@ -464,7 +346,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   if (MODE == 3) {
     for (int sb = rb; sb < re; sb += a.qsub) {
       const int se = min(re, sb + a.qsub);
-      FHistRowsSel<W, MODE>(a, tile, buf, start, sb, se, gst, hist, sg, sh, dsg, dsh, hist32);
+      FHistRows<W, MODE>(a, tile, buf, start, sb, se, gst, hist, sg, sh, dsg, dsh, hist32);
       __syncthreads();
       for (int i = t; i < tile.nbins; i += blockDim.x) {
         const uint32_t x = hist32[i];
@@ -477,7 +359,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       __syncthreads();
     }
   } else {
-    FHistRowsSel<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh);
+    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh);
     __syncthreads();
   }
   FStamp(a, rnd, kFStampHist, 2);
@@ -1227,6 +1109,7 @@ __device__ __forceinline__ void CegbSetBest(const FArgs& a, int c, size_t src, d
 constexpr int kSelWaves = kFSelThreads / 64;
 constexpr int kSelPairs = 2 * kFrontierKmax / kSelWaves;  // (expansion, child) pairs per wave
 
+template <bool kCegb>
 __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int C = a.C, L = a.L, F = a.F;
@@ -1272,7 +1155,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   }
   for (int l = t; l < st.num_leaves; l += blockDim.x) s_lcid[l] = a.leaf_cid[l];
   // CEGB coupled penalties: used-feature flags (after the sort scratch) and the event count
-  const bool cegb = a.cegb_coupled != nullptr;
+  constexpr bool cegb = kCegb;  // CEGB coupled penalties: its own instantiation (registers)
   uint8_t* s_used = reinterpret_cast<uint8_t*>(smem + FrontierSelectLds(C, L));
   const unsigned epoch0 = cegb ? *a.cegb_epoch : 0u;
   if (cegb) {
@@ -2018,7 +1901,8 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 
 
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
-  k_f_select<<<1, kFSelThreads, FrontierSelectLds(a.C, a.L) + (a.cegb_coupled != nullptr ? a.F + 16 : 0), s>>>(a);
+  if (a.cegb_coupled != nullptr) k_f_select<true><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L) + a.F + 16, s>>>(a);
+  else k_f_select<false><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L), s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 

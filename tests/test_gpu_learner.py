@@ -453,7 +453,8 @@ def test_device_quantized_regression_tracks_cpu(lgb, gpu_required):
     assert abs(l2["gpu"] - l2["cpu"]) < 0.03 * l2["cpu"], l2
 
 
-@pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05, "cegb_penalty_feature_coupled": [1, 2, 3, 4, 5, 6]},
+@pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05,
+                                    "cegb_penalty_feature_lazy": [0.01, 0.02, 0.03, 0.04, 0.05, 0.06]},
                                    {"monotone_constraints": [1, -1, 0, 0, 0, 0],
                                     "monotone_constraints_method": "intermediate"},
                                    {"linear_tree": True, "objective": "regression"}])
@@ -875,28 +876,6 @@ def test_four_bit_rows_match_byte_rows(lgb, gpu_required, rng, monkeypatch, max_
     for nib in ("1", "0"):
         monkeypatch.setenv("LGAP_NIBBLE", nib)
         b = lgb.train(params, lgb.Dataset(X, y, params=params), 10)
-        models.append((b.model_to_string().split("end of trees")[0], b.predict(X, raw_score=True)))
-    assert models[0][0] == models[1][0]
-    np.testing.assert_array_equal(models[0][1], models[1][1])
-
-
-@pytest.mark.parametrize("features,quantized", [(11, False), (28, False), (28, True), (30, False)])
-def test_row_per_thread_histograms_match(lgb, gpu_required, rng, monkeypatch, features, quantized):
-    """The row-per-thread histogram loop (frontier_kernels.hip FHistRowsRPT: a lane loads its whole
-    row with wide loads and adds its groups in a lane-rotated dword order) sums the same integers as
-    the dword-per-lane loop, so the model is bit-identical with LGAP_FHIST_RPT on and off (rows of
-    3, 7 and 8 dwords; fp and quantized integer-level histograms)."""
-    n = 40000
-    X = rng.standard_normal((n, features))
-    X[rng.random(n) < 0.05, 2] = np.nan
-    y = (X[:, 0] - 0.6 * X[:, 1] + 0.4 * X[:, 2] * X[:, 4] + 0.3 * rng.standard_normal(n) > 0).astype(float)
-    params = {"objective": "binary", "num_leaves": 31, "device_type": "gpu", "verbosity": -1,
-              "use_quantized_grad": quantized}
-    models = []
-    for rpt in ("1", "0"):
-        monkeypatch.setenv("LGAP_FHIST_RPT", rpt)
-        b = lgb.train(params, lgb.Dataset(X, y, params=params), 10, keep_training_booster=True)
-        assert "frontier" in b.device_name()
         models.append((b.model_to_string().split("end of trees")[0], b.predict(X, raw_score=True)))
     assert models[0][0] == models[1][0]
     np.testing.assert_array_equal(models[0][1], models[1][1])
