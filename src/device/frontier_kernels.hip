@@ -1108,6 +1108,7 @@ __device__ __forceinline__ void CegbSetBest(const FArgs& a, int c, size_t src, d
 
 constexpr int kSelWaves = kFSelThreads / 64;
 constexpr int kSelPairs = 2 * kFrontierKmax / kSelWaves;  // (expansion, child) pairs per wave
+constexpr int kSelRankMax = 256;  // alive nodes up to which the select ranks instead of sorting
 
 template <bool kCegb>
 __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
@@ -1613,24 +1614,25 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     // uncommitted node. The blocked node always goes first.
     int P2 = 64;
     while (P2 < na) P2 <<= 1;
-    if (na <= static_cast<int>(blockDim.x) && !a.sel_bitonic) {
-      // rank sort (one barrier instead of the bitonic network's log2(P2)(log2(P2)+1)/2): thread
-      // i's position = alive nodes ordered before it; keys are unique (cids), so the ranks are
-      // a permutation and the order is the bitonic sort's
-      int ri = 0, ci = 0, pos = 0;
-      double gi = 0.0;
+    if (na <= kSelRankMax && !a.sel_bitonic) {
+      // rank sort (two barriers instead of the bitonic network's log2(P2)(log2(P2)+1)/2):
+      // thread i's position = alive nodes ordered before it; keys are unique (cids), so the
+      // ranks are a permutation and the order is the bitonic sort's. O(na) broadcast LDS reads
+      // per thread: beyond kSelRankMax nodes the network is cheaper (255-leaf trees)
+      for (int i = t; i < na; i += blockDim.x) s_sg[i] = s_gain[s_ac[i] >= 0 ? s_ac[i] : ~s_ac[i]];
+      __syncthreads();
+      int ri = 0, pos = 0;
       if (t < na) {
         ri = s_ac[t];
-        ci = ri >= 0 ? ri : ~ri;
-        gi = s_gain[ci];
+        const int ci = ri >= 0 ? ri : ~ri;
+        const double gi = s_sg[t];
         for (int j = 0; j < na; ++j) {
           const int rj = s_ac[j];
           const int cj = rj >= 0 ? rj : ~rj;
-          const double gj = s_gain[cj];
+          const double gj = s_sg[j];
           pos += (gj > gi || (gj == gi && cj < ci)) ? 1 : 0;
         }
       }
-      __syncthreads();  // (s_sc may alias nothing here, but keep reads before the scatter)
       if (t < na) s_sc[pos] = ri;
       __syncthreads();
     } else {
