@@ -1212,9 +1212,11 @@ class DeviceTreeLearner : public TreeLearner {
     FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
-    // 512 (default) / 1024 threads per histogram block: 1024 measured 322.9 vs 331.0 it/s at 10M
-    // (a longer tail: blocks finish further apart), 621 vs 738 at 1.25M
-    fhist_threads_ = big_tiles_ ? 1024 : 512;  // one resident block per CU with 150 KB tiles
+    // 512 / 1024 threads per histogram block. Round 3 (after the grid cap at 7/8 of the CUs),
+    // paired on one box: single-tile rows at 10M 370.6 / 368.9 (1024) vs 363.6 / 365.4 (512),
+    // quantized 405.6 vs 398.3; at 1.25M mixed (737.9 / 778.4 vs 779.2 / 770.0). Multi-tile rows
+    // keep 512 (two resident 56 KB blocks per CU); 150 KB tiles hold one block per CU.
+    fhist_threads_ = big_tiles_ || (num_tiles_ == 1 && N_ >= 4000000) ? 1024 : 512;
     if (const char* e = std::getenv("LGAP_FHIST_THREADS")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
     fpolicy_ = 1;
     if (const char* e = std::getenv("LGAP_FRONTIER_POLICY")) fpolicy_ = std::atoi(e) == 0 ? 0 : 1;
