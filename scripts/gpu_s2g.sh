@@ -5,7 +5,7 @@ set -u
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_learner.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "cegb or frontier_engine or forced_splits_on or host_policy or quantized" > $OUT/tc.log 2>&1 || { tail -30 $OUT/tc.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_learner.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "cegb or frontier_engine or forced_splits_on or host_policy or quantized or bagging" > $OUT/tc.log 2>&1 || { tail -30 $OUT/tc.log; exit 1; }
 tail -1 $OUT/tc.log
 run() {  # run <name> <limit> <cmd...>
   local name=$1 lim=$2; shift 2

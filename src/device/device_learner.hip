@@ -1050,13 +1050,14 @@ class DeviceTreeLearner : public TreeLearner {
     if (!FrontierSerial() && !FrontierDP()) return false;
     if (use_bynode_ || config_->extra_trees || scan_global_) return false;
     if (FrontierCapacity() > kFrontierMaxNodes || F_ <= 0) return false;
-    return FrontierSelectLds(FrontierCapacity(), L_) + (CegbCoupled() ? F_ + 16 : 0) <= 150 * 1024;
+    return FrontierSelectLds(FrontierCapacity(), L_) + (CegbRaw() ? F_ + 16 : 0) <= 150 * 1024;
   }
-  // CEGB coupled feature penalties run in the frontier select (FArgs::cegb_coupled); the lazy
-  // per-row penalties stay a host policy (tree_learner.cpp routes those configurations)
-  bool CegbCoupled() const {
-    return !config_->cegb_penalty_feature_coupled.empty() && config_->cegb_penalty_feature_lazy.empty();
-  }
+  // CEGB feature penalties in the frontier select: coupled (FArgs::cegb_coupled: refunds on a
+  // feature's first use) and lazy (FArgs::cegb_lazy: per-row marks, unmarked-row counts per
+  // node). Either makes the scans publish raw gains (FArgs::cegb_raw).
+  bool CegbCoupled() const { return !config_->cegb_penalty_feature_coupled.empty(); }
+  bool CegbLazy() const { return !config_->cegb_penalty_feature_lazy.empty(); }
+  bool CegbRaw() const { return CegbCoupled() || CegbLazy(); }
   bool FrontierSerial() const {
     return mode_ == DevParallel::kSerial && !owner_scan_ && !voting_ && !distributed_;
   }
@@ -1129,8 +1130,8 @@ class DeviceTreeLearner : public TreeLearner {
       Log::Fatal("forced splits on the device need the frontier engine (serial learner, num_leaves <= 512, "
                  "no feature_fraction_bynode / extra_trees)");
     }
-    if (!frontier_ && CegbCoupled()) {
-      Log::Fatal("cegb_penalty_feature_coupled on the device needs the frontier engine (serial learner, "
+    if (!frontier_ && CegbRaw()) {
+      Log::Fatal("cegb_penalty_feature_coupled / _lazy on the device need the frontier engine (serial learner, "
                  "num_leaves <= 496, no feature_fraction_bynode / extra_trees)");
     }
     if (!frontier_) return;
@@ -1165,6 +1166,12 @@ class DeviceTreeLearner : public TreeLearner {
     ffbest_ = reinterpret_cast<SplitInfo*>(b + o_fbest);
     ffkey_ = reinterpret_cast<SplitKey*>(b + o_fkey);
     UploadForcedSplits();
+    if (CegbRaw()) {
+      fnkey_.Resize(C * F);
+      fninfo_.Resize(C * F);
+      fnuep_.Resize(C);
+      fnuep_.Zero(stream_);
+    }
     if (CegbCoupled()) {
       // tradeoff x coupled penalty per inner feature; used flags and the event count persist
       // over the trees of this training set (host CegbPenalty::Init)
@@ -1180,9 +1187,24 @@ class DeviceTreeLearner : public TreeLearner {
       cegb_used_.Zero(stream_);
       cegb_epoch_.Resize(1);
       cegb_epoch_.Zero(stream_);
-      fnkey_.Resize(C * F);
-      fninfo_.Resize(C * F);
-      fnuep_.Resize(C);
+    }
+    if (CegbLazy()) {
+      // tradeoff x lazy penalty per inner feature; per-row marks persist over the trees
+      const auto& lp = config_->cegb_penalty_feature_lazy;
+      if (static_cast<int>(lp.size()) != data_->num_total_features()) {
+        Log::Fatal("cegb_penalty_feature_lazy should be the same size as feature number.");
+      }
+      std::vector<double> h(F_);
+      for (int f = 0; f < F_; ++f) h[f] = config_->cegb_tradeoff * lp[data_->feature(f).real_index];
+      cegb_lazy_.Resize(F_);
+      cegb_lazy_.Upload(h.data(), h.size(), stream_);
+      lazy_words_ = (F_ + 31) / 32;
+      lazy_bits_.Resize(static_cast<size_t>(std::max(N_, 1)) * lazy_words_);
+      lazy_bits_.Zero(stream_);
+      lazy_acc_.Resize(K * F);
+      lazy_acc_.Zero(stream_);
+      fnlazy_.Resize(C * F);
+      fnpath_.Resize(C * lazy_words_);
     }
     // replay results: coherent pinned host memory the results kernel writes directly
     const size_t rbytes = FrontierResultBytes(L_);
@@ -1327,14 +1349,25 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
-    if (CegbCoupled() && cegb_coupled_.size() >= static_cast<size_t>(F_)) {
-      a.cegb_coupled = cegb_coupled_.get();
+    if (CegbRaw() && fnuep_.size() > 0) {
+      a.cegb_raw = 1;
       a.cegb_tradeoff = config_->cegb_tradeoff;
-      a.cegb_used = cegb_used_.get();
-      a.cegb_epoch = cegb_epoch_.get();
       a.nkey = fnkey_.get();
       a.ninfo = fninfo_.get();
       a.nuep = fnuep_.get();
+      if (CegbCoupled()) {
+        a.cegb_coupled = cegb_coupled_.get();
+        a.cegb_used = cegb_used_.get();
+        a.cegb_epoch = cegb_epoch_.get();
+      }
+      if (CegbLazy()) {
+        a.cegb_lazy = cegb_lazy_.get();
+        a.lazy_bits = lazy_bits_.get();
+        a.lazy_words = lazy_words_;
+        a.lazy_acc = lazy_acc_.get();
+        a.nlazy = fnlazy_.get();
+        a.npath = fnpath_.get();
+      }
     }
     a.sel_bitonic = std::getenv("LGAP_SEL_BITONIC") != nullptr ? 1 : 0;
     a.spec_cap = fspec_cap_;
@@ -1386,6 +1419,7 @@ class DeviceTreeLearner : public TreeLearner {
   // round's expansion count (round r >= 1 of a tree has at most 2^(r-1) open nodes to expand).
   void EnqueueFrontierRound(const FArgs& fa, int kb) {
     LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
     if (!FrontierPipelined(kb)) {
       LaunchFrontierHist(fa, FrontierHistLds(), stream_);
       FrontierExchange(kb);
@@ -1436,6 +1470,7 @@ class DeviceTreeLearner : public TreeLearner {
         AllreduceMaxU32(ghmax_.get(), 2, stream_);
       }
       LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+      if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
       FrontierExchange(1);
       LaunchFrontierScan(fa, fscan_lds_, stream_);
       LaunchFrontierSelect(fa, stream_);
@@ -1529,7 +1564,12 @@ class DeviceTreeLearner : public TreeLearner {
     for (;;) {
       LaunchFrontierResults(fa_res, fres_dev_, stream_);
       FrontierSync();
-      if (hs->done) break;
+      if (hs->done) {
+        // CEGB lazy: the final leaves' rows are marked for their paths' features (stream order:
+        // before the next tree's replay)
+        if (fa_res.cegb_lazy != nullptr) LaunchFrontierLazyMark(fa_res, stream_);
+        break;
+      }
       if (launched > L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
       if (use_graph) {
         if (!fcont_) fcont_ = CaptureFrontier(kCont, false);
@@ -2731,6 +2771,13 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<SplitKey> fnkey_;
   DevBuf<SplitInfo> fninfo_;
   DevBuf<int> fnuep_;
+  // CEGB lazy penalties: penalties, per-row marks, round counts, per-node counts and paths
+  DevBuf<double> cegb_lazy_;
+  DevBuf<uint32_t> lazy_bits_;
+  DevBuf<int> lazy_acc_;
+  DevBuf<int> fnlazy_;
+  DevBuf<uint32_t> fnpath_;
+  int lazy_words_ = 0;
   int fnum_forced_ = 0;
   SplitInfo* ffbest_ = nullptr;
   SplitKey* ffkey_ = nullptr;

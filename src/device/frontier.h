@@ -100,6 +100,7 @@ struct FExp {
   int smaller, larger;       // cids
   int h_buf, h_start, h_count;  // the smaller child's local rows
   int forced;                // the split is forced split `forced` (FForced index), -1: the node's best
+  int feature;               // inner feature of the split (-1: the root pseudo-expansion)
 };
 
 struct FState {
@@ -191,6 +192,16 @@ struct FArgs {
   SplitKey* nkey;              // [C][F] every computed node's raw per-feature candidates
   SplitInfo* ninfo;            // [C][F]
   int* nuep;                   // [C] cegb_epoch its best was computed at
+  int cegb_raw;                // 1: scans publish raw gains, the select applies the CEGB penalties
+  // CEGB lazy per-row penalties (cegb_penalty_feature_lazy): a node's cost for feature f is
+  // pen_f x its rows not yet marked for f (marks of earlier trees; features on the node's own
+  // path count zero: the host marks a split leaf's rows for its feature as it splits)
+  const double* cegb_lazy;     // [F] tradeoff x lazy penalty per inner feature, null: off
+  uint32_t* lazy_bits;         // [N][lazy_words] per-row marks (features used on the row's path)
+  int lazy_words;
+  int* lazy_acc;               // [kmax][F] the round's smaller-child unmarked counts (zero between rounds)
+  int* nlazy;                  // [C][F] unmarked counts per node
+  uint32_t* npath;             // [C][lazy_words] features on the node's path
   int max_bin, cat_p2;
   int use_dp;       // gpu_use_dp: 64-bit LDS accumulators
   int spec_cap;     // speculative expansions per round beyond the budget (policy knob)
@@ -229,6 +240,10 @@ void LaunchFrontierInit(const FArgs& a, hipStream_t s);
 void LaunchFrontierHist(const FArgs& a, size_t lds_bytes, hipStream_t s);
 void LaunchFrontierScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
+// CEGB lazy penalties: unmarked-row counts of the round's smaller children; after a tree, the
+// final leaves' rows marked for the features on their paths
+void LaunchFrontierLazyCounts(const FArgs& a, hipStream_t s);
+void LaunchFrontierLazyMark(const FArgs& a, hipStream_t s);
 void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s);
 // resident 256-thread partition blocks per CU (the look-back needs every block resident)
 int FrontierPartitionBlocksPerCU(int iters);

@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
     x.h_start = 0;
     x.h_count = tp.root_count;
     x.forced = -1;
+    x.feature = -1;
     a.exps[0] = x;
     a.bounds[0] = LeafBounds();
     if (a.ic) a.ic[0] = ~0ull;
@@ -571,7 +572,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
             // cost-effective gradient boosting, split penalty (host CegbPenalty::DeltaGain:
             // subtracted before the monotone penalty multiplies the gain). With coupled
             // penalties the candidate stays raw: the select applies every penalty (CegbAdjust)
-            if (a.cegb_coupled == nullptr) {
+            if (!a.cegb_raw) {
               if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
             }
@@ -654,7 +655,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         kk.missing = fi.missing;
         kk.default_left = out->default_left;
         kk.is_cat = fi.bin_type != 0 ? 1 : 0;
-        kk.pad0 = a.cegb_coupled != nullptr && out->feature >= 0 ? out->monotone_type : 0;
+        kk.pad0 = a.cegb_raw && out->feature >= 0 ? out->monotone_type : 0;
       }
     }
     __syncthreads();
@@ -1086,10 +1087,12 @@ __device__ __forceinline__ bool FBetter(double ga, int fa, int la, double gb, in
 // CEGB with coupled penalties: the penalised gain of a RAW candidate key at the current
 // used-feature flags (host SerialTreeLearner::ScoreFeature: gain -= CegbPenalty::DeltaGain,
 // then the monotone penalty multiplies a monotone split; key.pad0 = its monotone type)
-__device__ __forceinline__ double CegbAdjust(const FArgs& a, const SplitKey& k, int n, int depth, const uint8_t* used) {
+__device__ __forceinline__ double CegbAdjust(const FArgs& a, const SplitKey& k, int n, int depth, const uint8_t* used,
+                                             int node) {
   if (k.feature < 0) return kMinScore;
   double delta = a.cegb_split * n;
-  if (!used[k.feature]) delta += a.cegb_coupled[k.feature];
+  if (a.cegb_coupled != nullptr && !used[k.feature]) delta += a.cegb_coupled[k.feature];
+  if (a.cegb_lazy != nullptr) delta += a.cegb_lazy[k.feature] * a.nlazy[static_cast<size_t>(node) * a.F + k.feature];
   double g = k.gain - delta;
   if (k.pad0 != 0) g *= MonotonePenaltyAt(a.monotone_penalty, depth);
   return g;
@@ -1158,8 +1161,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   // CEGB coupled penalties: used-feature flags (after the sort scratch) and the event count
   constexpr bool cegb = kCegb;  // CEGB coupled penalties: its own instantiation (registers)
   uint8_t* s_used = reinterpret_cast<uint8_t*>(smem + FrontierSelectLds(C, L));
-  const unsigned epoch0 = cegb ? *a.cegb_epoch : 0u;
-  if (cegb) {
+  const unsigned epoch0 = cegb && a.cegb_coupled != nullptr ? *a.cegb_epoch : 0u;
+  if (cegb && a.cegb_coupled != nullptr) {
     for (int f = t; f < F; f += blockDim.x) s_used[f] = a.cegb_used[f];
   }
   if (t < 2 * kFrontierKmax) {
@@ -1175,6 +1178,23 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   }
   __syncthreads();
   FStamp(a, rnd, kFStampSel, 1);
+  if (cegb && a.cegb_lazy != nullptr) {
+    // CEGB lazy penalties: unmarked-row counts of this round's children, the smaller's from
+    // the round's counts (k_f_lazy), the larger's as parent - smaller (the split feature is on
+    // both children's paths: zero)
+    for (int i = t; i < np * F; i += blockDim.x) {
+      const int q = i / F, f = i - q * F;
+      const int c = s_pc[q];
+      if (c < 0) continue;
+      const FExp& x = a.exps[q >> 1];
+      const int cnt = a.lazy_acc[static_cast<size_t>(q >> 1) * F + f];
+      const int v = c == x.smaller ? cnt : (f == x.feature ? 0 : a.nlazy[static_cast<size_t>(x.parent) * F + f] - cnt);
+      a.nlazy[static_cast<size_t>(c) * F + f] = v;
+    }
+    __syncthreads();
+    for (int i = t; i < kprev * F; i += blockDim.x) a.lazy_acc[i] = 0;
+    __syncthreads();
+  }
   // ---- A. children of the last round: best over features (all pairs' keys in flight)
   {
     double bg[kSelPairs];
@@ -1199,7 +1219,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         if (q < np && f < F && s_pc[q] >= 0) {
           const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
           const int kf = kk.feature;
-          const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used) : kk.gain);
+          const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used, s_pc[q]) : kk.gain);
           const int ff = kf < 0 ? 0x7fffffff : kf;
           if (FBetter(g, ff, 0, bg[j], bf[j], 0)) {
             bg[j] = g;
@@ -1384,7 +1404,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         break;
       }
       if (cegb) {
-        if (!s_used[bf]) {
+        if (a.cegb_coupled != nullptr && !s_used[bf]) {
           // first use of feature bf (host CegbPenalty::OnSplit): every other leaf's stored
           // candidate on bf -- the last valid one along its leaf index's chain of left
           // children, as the host's per-leaf table -- is refunded and may become its best
@@ -1470,7 +1490,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
           for (int f = lane; f < F; f += 64) {
             const SplitKey& kk = a.nkey[static_cast<size_t>(ch) * F + f];
             if (kk.feature < 0) continue;
-            const double g = CegbAdjust(a, kk, n, d, s_used);
+            const double g = CegbAdjust(a, kk, n, d, s_used, ch);
             if (FBetter(g, kk.feature, 0, cg, cf, 0)) {
               cg = g;
               cf = kk.feature;
@@ -1753,6 +1773,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         x.smaller = x.larger = -1;
         x.h_buf = x.h_start = x.h_count = 0;
         x.forced = p == s_blocked && s_bforced ? s_fidx[p] : -1;
+        x.feature = kk.feature;
         a.exps[lane] = x;
         a.nodes[p].left = cid_next + 2 * lane;
         a.nstate[p] = s_st[p] | kNodeExpanded;
@@ -1854,8 +1875,87 @@ __global__ __launch_bounds__(256) void k_f_results(FArgs a, char* out) {
 // ---------------------------------------------------------------------------
 // launchers
 
+// ---------------------------------------------------------------------------
+// CEGB lazy penalties (host CegbPenalty::DeltaGain / OnSplit): per-row feature marks.
+// k_f_lazy: block (chunk, e) counts, per feature, the rows of expansion e's smaller child not
+// marked for it (earlier trees' marks, and the child's path features counted as marked), and
+// writes both children's path masks. k_f_lazy_mark (after a tree): every final leaf's rows
+// get the features on its path.
+constexpr int kLazyChunks = 64;
+
+__global__ __launch_bounds__(256) void k_f_lazy(FArgs a) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  const FState* sp = a.st;
+  if (sp->done) return;
+  const int e = blockIdx.y;
+  if (e >= sp->k) return;
+  const FExp x = a.exps[e];
+  if (x.skip) return;
+  const int lw = a.lazy_words, F = a.F, t = threadIdx.x;
+  uint32_t* s_mask = reinterpret_cast<uint32_t*>(lds_raw);
+  int* s_cnt = reinterpret_cast<int*>(s_mask + lw);
+  for (int i = t; i < lw; i += blockDim.x) {
+    uint32_t m = x.parent >= 0 ? a.npath[static_cast<size_t>(x.parent) * lw + i] : 0u;
+    if (x.feature >= 0 && (x.feature >> 5) == i) m |= 1u << (x.feature & 31);
+    if (i == lw - 1 && (F & 31) != 0) m |= ~0u << (F & 31);  // bits past F: never counted
+    s_mask[i] = m;
+    if (blockIdx.x == 0) {
+      a.npath[static_cast<size_t>(x.smaller) * lw + i] = m;
+      if (x.larger >= 0) a.npath[static_cast<size_t>(x.larger) * lw + i] = m;
+    }
+  }
+  for (int f = t; f < F; f += blockDim.x) s_cnt[f] = 0;
+  __syncthreads();
+  const int n = x.h_count;
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int rb = blockIdx.x * chunk, re = min(n, rb + chunk);
+  for (int p = rb + t; p < re; p += blockDim.x) {
+    const int row = FRowAt(a, x.h_buf, x.h_start + p);
+    const uint32_t* bits = a.lazy_bits + static_cast<size_t>(row) * lw;
+    for (int i = 0; i < lw; ++i) {
+      uint32_t u = ~(bits[i] | s_mask[i]);
+      while (u) {
+        const int b = __ffs(u) - 1;
+        atomicAdd(&s_cnt[(i << 5) + b], 1);
+        u &= u - 1u;
+      }
+    }
+  }
+  __syncthreads();
+  for (int f = t; f < F; f += blockDim.x) {
+    if (s_cnt[f]) atomicAdd(&a.lazy_acc[static_cast<size_t>(e) * F + f], s_cnt[f]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_f_lazy_mark(FArgs a) {
+  const int l = blockIdx.y;
+  if (!a.st->done || l >= a.st->num_leaves) return;
+  const int c = a.leaf_cid[l];
+  const LeafRange r = a.range_out[l];
+  const int lw = a.lazy_words;
+  const uint32_t* m = a.npath + static_cast<size_t>(c) * lw;
+  const int chunk = (r.count + gridDim.x - 1) / gridDim.x;
+  const int rb = blockIdx.x * chunk, re = min(r.count, rb + chunk);
+  for (int p = rb + threadIdx.x; p < re; p += blockDim.x) {
+    const int row = FRowAt(a, r.buf, r.start + p);
+    uint32_t* bits = a.lazy_bits + static_cast<size_t>(row) * lw;
+    for (int i = 0; i < lw; ++i) bits[i] |= m[i];
+  }
+}
+
 void LaunchFrontierResults(const FArgs& a, void* host_out, hipStream_t s) {
   k_f_results<<<1, 256, 0, s>>>(a, static_cast<char*>(host_out));
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierLazyCounts(const FArgs& a, hipStream_t s) {
+  const size_t lds = sizeof(uint32_t) * a.lazy_words + sizeof(int) * a.F;
+  k_f_lazy<<<dim3(kLazyChunks, a.kmax), 256, lds, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierLazyMark(const FArgs& a, hipStream_t s) {
+  k_f_lazy_mark<<<dim3(16, a.L), 256, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1903,7 +2003,7 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 
 
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
-  if (a.cegb_coupled != nullptr) k_f_select<true><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L) + a.F + 16, s>>>(a);
+  if (a.cegb_raw) k_f_select<true><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L) + a.F + 16, s>>>(a);
   else k_f_select<false><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L), s>>>(a);
   HIP_CHECK(hipGetLastError());
 }

@@ -47,14 +47,14 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   if (linear_tree) return "linear_tree";
   // (voting runs on the device; its global pass redraws no extra-trees thresholds)
   if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
-  // CEGB: the split penalty runs in the device scans, the coupled feature penalties in the
-  // frontier select (serial learner: its replay refunds leaves and voids speculation on a
-  // feature's first use); the lazy per-row penalties stay a host policy
-  // (leaf_constraints.cpp CegbPenalty)
+  // CEGB: the split penalty runs in the device scans, the coupled and lazy feature penalties
+  // in the frontier engine (serial learner: the select's replay refunds leaves and voids
+  // speculation on a feature's first use; per-row marks count each node's unmarked rows)
   const bool frontier_ok = learner_type == "serial" && c->feature_fraction_bynode >= 1.0 && !c->extra_trees &&
                            c->num_leaves <= 496 && c->max_bin <= 1024 && c->forcedsplits_filename.empty() &&
                            c->interaction_constraints_vector.empty();
-  if (!c->cegb_penalty_feature_lazy.empty() || (!c->cegb_penalty_feature_coupled.empty() && !frontier_ok) ||
+  const bool feature_pens = !c->cegb_penalty_feature_coupled.empty() || !c->cegb_penalty_feature_lazy.empty();
+  if ((feature_pens && (!frontier_ok || (train != nullptr && train->num_features() > 8192))) ||
       (CegbPenalty::Enabled(c) && learner_type == "voting")) {
     return "cost-effective gradient boosting (feature penalties)";
   }

@@ -453,7 +453,7 @@ def test_device_quantized_regression_tracks_cpu(lgb, gpu_required):
     assert abs(l2["gpu"] - l2["cpu"]) < 0.03 * l2["cpu"], l2
 
 
-@pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05,
+@pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05, "feature_fraction_bynode": 0.8,
                                     "cegb_penalty_feature_lazy": [0.01, 0.02, 0.03, 0.04, 0.05, 0.06]},
                                    {"monotone_constraints": [1, -1, 0, 0, 0, 0],
                                     "monotone_constraints_method": "intermediate"},
@@ -496,13 +496,20 @@ def test_device_cegb_split_penalty(lgb, gpu_required, rng, extra):
                                    {"cegb_penalty_feature_coupled": [0, 0, 40, 40, 10, 10], "cegb_penalty_split": 0.002,
                                     "cegb_tradeoff": 0.7, "num_leaves": 63},
                                    {"cegb_penalty_feature_coupled": [3000, 100, 60, 60, 20, 40],
-                                    "monotone_constraints": [1, -1, 0, 0, 0, 0]}])
+                                    "monotone_constraints": [1, -1, 0, 0, 0, 0]},
+                                   {"cegb_penalty_split": 0.05,
+                                    "cegb_penalty_feature_lazy": [0.01, 0.02, 0.03, 0.04, 0.05, 0.06]},
+                                   {"cegb_penalty_feature_lazy": [0.05, 0.1, 0.1, 0.1, 0.1, 0.1],
+                                    "cegb_penalty_feature_coupled": [0, 0, 40, 40, 10, 10], "bagging_fraction": 0.8,
+                                    "bagging_freq": 1}])
 def test_device_cegb_coupled_penalties(lgb, gpu_required, rng, extra):
-    """CEGB coupled feature penalties in the frontier select: raw candidates kept per node, the
+    """CEGB feature penalties in the frontier engine. Coupled: raw candidates kept per node, the
     penalty of a feature not yet used by any split subtracted, and a feature's first use in the
     replay refunding every other leaf's stored candidate (leaf-index chain) and voiding the
-    speculative expansions grown under the old gains. Trees equal the host CegbPenalty learner's
-    split for split, over several trees (the used flags persist across trees)."""
+    speculative expansions grown under the old gains. Lazy: per-row feature marks (a final
+    leaf's rows marked for its path after each tree), each node's unmarked-row counts (smaller
+    child counted, larger = parent - smaller). Trees equal the host CegbPenalty learner's split
+    for split, over several trees (used flags and marks persist across trees)."""
     X, z = _policy_data(rng)
     y = (z > 0).astype(float)
     bc = _train(lgb, X, y, "cpu", rounds=4, **extra)
