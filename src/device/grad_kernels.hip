@@ -38,6 +38,34 @@ __global__ __launch_bounds__(256) void k_pointwise(PointwiseParams p, const doub
   }
 }
 
+// Two rows per thread with 16-byte score / gh and 8-byte label (weight, aux) accesses: the
+// one-row kernel moved ~3.4 TB/s in 4- and 8-byte lane accesses (58 us at 10M rows).
+__global__ __launch_bounds__(256) void k_pointwise2(PointwiseParams p, const double* __restrict__ score,
+                                                    const float* __restrict__ label, const float* __restrict__ weight,
+                                                    const float* __restrict__ aux, int n, float2* __restrict__ gh) {
+  const int pairs = n >> 1;
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < pairs; i += stride) {
+    const double2 sc = reinterpret_cast<const double2*>(score)[i];
+    const float2 lb = reinterpret_cast<const float2*>(label)[i];
+    const float2 w = weight ? reinterpret_cast<const float2*>(weight)[i] : make_float2(1.f, 1.f);
+    const float2 ax = aux ? reinterpret_cast<const float2*>(aux)[i] : make_float2(0.f, 0.f);
+    score_t g0, h0, g1, h1;
+    PointwiseGradient(p, sc.x, static_cast<double>(lb.x), weight ? static_cast<double>(w.x) : 1.0, weight != nullptr,
+                      aux ? static_cast<double>(ax.x) : 0.0, &g0, &h0);
+    PointwiseGradient(p, sc.y, static_cast<double>(lb.y), weight ? static_cast<double>(w.y) : 1.0, weight != nullptr,
+                      aux ? static_cast<double>(ax.y) : 0.0, &g1, &h1);
+    reinterpret_cast<float4*>(gh)[i] = make_float4(g0, h0, g1, h1);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int i = n - 1;
+    score_t g, h;
+    PointwiseGradient(p, score[i], static_cast<double>(label[i]), weight ? static_cast<double>(weight[i]) : 1.0,
+                      weight != nullptr, aux ? static_cast<double>(aux[i]) : 0.0, &g, &h);
+    gh[i] = make_float2(g, h);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_softmax(int K, double factor, const double* __restrict__ score,
                                                  const float* __restrict__ label, const float* __restrict__ weight,
                                                  int n, float2* __restrict__ gh) {
@@ -526,7 +554,12 @@ void LaunchPositionBiasUpdate(const float2* gh, const int* positions, int n, int
 void LaunchPointwiseGrad(const PointwiseParams& p, const double* score, const float* label, const float* weight,
                          const float* aux, int n, float2* gh, hipStream_t s) {
   if (n <= 0) return;
-  k_pointwise<<<GridFor(n), 256, 0, s>>>(p, score, label, weight, aux, n, gh);
+  auto al = [](const void* q, uintptr_t b) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & (b - 1)) == 0; };
+  if (n >= 2 && al(score, 16) && al(gh, 16) && al(label, 8) && al(weight, 8) && al(aux, 8)) {
+    k_pointwise2<<<GridFor((n + 1) / 2), 256, 0, s>>>(p, score, label, weight, aux, n, gh);
+  } else {
+    k_pointwise<<<GridFor(n), 256, 0, s>>>(p, score, label, weight, aux, n, gh);
+  }
   HIP_CHECK(hipGetLastError());
 }
 
