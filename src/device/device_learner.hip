@@ -1183,10 +1183,14 @@ class DeviceTreeLearner : public TreeLearner {
       for (int f = 0; f < F_; ++f) h[f] = config_->cegb_tradeoff * cp[data_->feature(f).real_index];
       cegb_coupled_.Resize(F_);
       cegb_coupled_.Upload(h.data(), h.size(), stream_);
+      // the used flags survive ResetConfig on the same training set (host CegbPenalty::Init)
+      const bool fresh = cegb_data_ != data_ || cegb_used_.size() != static_cast<size_t>(F_);
       cegb_used_.Resize(F_);
-      cegb_used_.Zero(stream_);
       cegb_epoch_.Resize(1);
-      cegb_epoch_.Zero(stream_);
+      if (fresh) {
+        cegb_used_.Zero(stream_);
+        cegb_epoch_.Zero(stream_);
+      }
     }
     if (CegbLazy()) {
       // tradeoff x lazy penalty per inner feature; per-row marks persist over the trees
@@ -1199,13 +1203,16 @@ class DeviceTreeLearner : public TreeLearner {
       cegb_lazy_.Resize(F_);
       cegb_lazy_.Upload(h.data(), h.size(), stream_);
       lazy_words_ = (F_ + 31) / 32;
-      lazy_bits_.Resize(static_cast<size_t>(std::max(N_, 1)) * lazy_words_);
-      lazy_bits_.Zero(stream_);
+      const size_t nbits = static_cast<size_t>(std::max(N_, 1)) * lazy_words_;
+      const bool fresh = cegb_data_ != data_ || lazy_bits_.size() != nbits;
+      lazy_bits_.Resize(nbits);
+      if (fresh) lazy_bits_.Zero(stream_);  // per-row marks survive ResetConfig on the same data
       lazy_acc_.Resize(K * F);
       lazy_acc_.Zero(stream_);
       fnlazy_.Resize(C * F);
       fnpath_.Resize(C * lazy_words_);
     }
+    cegb_data_ = data_;
     // replay results: coherent pinned host memory the results kernel writes directly
     const size_t rbytes = FrontierResultBytes(L_);
     if (rbytes > fres_bytes_) {
@@ -2778,6 +2785,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<int> fnlazy_;
   DevBuf<uint32_t> fnpath_;
   int lazy_words_ = 0;
+  const Dataset* cegb_data_ = nullptr;  // training set the CEGB usage state belongs to
   int fnum_forced_ = 0;
   SplitInfo* ffbest_ = nullptr;
   SplitKey* ffkey_ = nullptr;
