@@ -35,6 +35,9 @@ def main() -> int:
     y = y.astype(float)
     params = {"objective": "binary", "num_leaves": 31, "device_type": "gpu", "verbosity": -1, "seed": 1,
               "min_data_in_leaf": 20}
+    if os.environ.get("DP_SELFTEST_QUANTIZED") == "1":
+        # packed g32|h32 accumulators, one word per bin in the all-reduce
+        params.update({"use_quantized_grad": True, "num_grad_quant_bins": 4})
     out = {}
     for mode in ("single", "dp", "dp_serial"):
         os.environ["LGAP_FORCE_DEVICE_DP"] = "0" if mode == "single" else "1"

@@ -1224,6 +1224,17 @@ class DeviceTreeLearner : public TreeLearner {
       fres_bytes_ = rbytes;
     }
     fslots_.Resize(C * 2 * static_cast<size_t>(TB_));
+    // global row count (data parallel: the packed quantized accumulators must hold every
+    // rank's level sums)
+    fglobal_rows_ = static_cast<double>(N_);
+    if (distributed_) {
+      DevBuf<double> gr(1);
+      const double nloc = static_cast<double>(N_);
+      gr.Upload(&nloc, 1, stream_);
+      AllreduceSumF64(gr.get(), 1, stream_);
+      HIP_CHECK(hipMemcpyAsync(&fglobal_rows_, gr.get(), sizeof(double), hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
     facc_.Resize(K * 2 * static_cast<size_t>(TB_));
     facc_.Zero(stream_);  // the scan re-zeroes what it consumes: zero between rounds from here on
     fpart_tile_ = kPartThreads * part_iters_;
@@ -1383,9 +1394,20 @@ class DeviceTreeLearner : public TreeLearner {
     a.distributed = distributed_ ? 1 : 0;
     a.kcap = fcaps_on_ ? fkcap_.get() : nullptr;
     a.kused = distributed_ ? fkused_.get() : nullptr;
-    if (distributed_) a.qpack = 0;  // the all-reduced level sums of every rank: keep two words per bin
+    if (distributed_) {
+      // the all-reduced level sums of every rank: packed only when the GLOBAL rows fit
+      const double gl = a.qbins / 2, hl = a.qconst ? 1 : a.qbins;
+      a.qpack = fglobal_rows_ * gl < 2147483647.0 && fglobal_rows_ * hl < 4294967295.0 ? 1 : 0;
+    }
     a.sp = MakeArgs().sp;
     return a;
+  }
+
+  // accumulator words per histogram bin of the frontier (k_f_hist): 1 with packed quantized
+  // level sums (qpack), else 2
+  int AccWordsPerBin() const {
+    const FArgs fa = MakeFArgs();
+    return fa.quant && fa.qpack ? 1 : 2;
   }
 
   // Data-parallel frontier: sum the round's accumulators of the first `kb` expansions over
@@ -1393,7 +1415,7 @@ class DeviceTreeLearner : public TreeLearner {
   void FrontierExchange(int kb) {
     if (!distributed_) return;
     AllreduceSumU64(reinterpret_cast<unsigned long long*>(facc_.get()),
-                    static_cast<size_t>(std::max(1, std::min(kb, fkmax_))) * 2 * TB_, stream_);
+                    static_cast<size_t>(std::max(1, std::min(kb, fkmax_))) * AccWordsPerBin() * TB_, stream_);
   }
 
   // Data-parallel rounds with at least two expansions pipeline the exchange with histogram
@@ -1439,7 +1461,7 @@ class DeviceTreeLearner : public TreeLearner {
       fa_a.e_hi = kh;
       fa_b.e_lo = kh;
       auto* acc = reinterpret_cast<unsigned long long*>(facc_.get());
-      const size_t row = 2 * static_cast<size_t>(TB_);
+      const size_t row = static_cast<size_t>(AccWordsPerBin()) * TB_;
       LaunchFrontierHist(fa_a, FrontierHistLds(), stream_);
       HIP_CHECK(hipEventRecord(pipe_ev_[0], stream_));
       LaunchFrontierHist(fa_b, FrontierHistLds(), stream_);
@@ -2798,6 +2820,7 @@ class DeviceTreeLearner : public TreeLearner {
   int fkused_trees_ = 0;
   double fstat_ar_exps_ = 0.0;
   long long fstat_pipelined_ = 0;
+  double fglobal_rows_ = 0.0;  // rows over all ranks (qpack bound of the data-parallel frontier)
   // data-parallel pipeline: the comm stream and its fork / join events (EnqueueFrontierRound)
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t pipe_ev_[4] = {nullptr, nullptr, nullptr, nullptr};

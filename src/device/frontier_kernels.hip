@@ -281,7 +281,10 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   if (e < 0) return;
   const int rb = s_rb, re = s_re, buf = s_buf, start = s_start;
   const HistTile tile = a.tiles[blockIdx.y];
-  unsigned long long* acc = a.acc + static_cast<size_t>(e) * 2 * a.TB;
+  // accumulator words per bin: 1 when quantized level sums are packed g32|h32 (qpack: the
+  // expansion's rows are compact, so a data-parallel all-reduce moves half the bytes), else 2
+  const int pw = a.quant && a.qpack ? 1 : 2;
+  unsigned long long* acc = a.acc + static_cast<size_t>(e) * pw * a.TB;
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
   const double dsg = ldexp(1.0, EG), dsh = ldexp(1.0, EH);
@@ -319,8 +322,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         const int g = dw * per + kk;
         if (b != 0u && g < tile.g1) {
           const int o = gst[g - tile.g0] + static_cast<int>(b);
-          if (qg) atomicAdd(&acc[2 * o], qg);
-          if (qh) atomicAdd(&acc[2 * o + 1], qh);
+          if (qg) atomicAdd(&acc[pw * o], qg);
+          if (qh) atomicAdd(&acc[pw * o + 1], qh);
         }
       }
     }
@@ -364,7 +367,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     __syncthreads();
   }
   FStamp(a, rnd, kFStampHist, 2);
-  unsigned long long* out = acc + 2 * static_cast<size_t>(tile.bin0);
+  unsigned long long* out = acc + pw * static_cast<size_t>(tile.bin0);
   if (a.debug_noflush) return;  // timing diagnostics only (LGAP_DEBUG_NOFLUSH): results are wrong
   // every block starts its flush at its own offset of the tile, so the blocks' concurrent
   // atomics hit different accumulator words instead of queueing on the same ones
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       const unsigned long long x = hist[i];
       if (x == 0ull) continue;
       if (pack) {
-        atomicAdd(&out[2 * i], x);
+        atomicAdd(&out[i], x);  // (pw == 1)
       } else {
         const unsigned long long hs = x & 0xFFFFFFFFull;
         const long long gs = static_cast<long long>(x - hs) >> 32;
@@ -448,7 +451,8 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     const DevFeature fi = a.feat[f];
     const int nbin = fi.num_bin;
     const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
-    unsigned long long* acc = a.acc + static_cast<size_t>(e) * TB2 + v0;
+    const size_t pw = qpack ? 1 : 2;  // accumulator words per bin (see k_f_hist)
+    unsigned long long* acc = a.acc + static_cast<size_t>(e) * pw * a.TB + pw * static_cast<size_t>(fi.hist_offset);
     const double* gp = (p >= 0 && cl >= 0) ? a.slots + static_cast<size_t>(p) * TB2 + v0 : nullptr;
     double* gs = a.slots + static_cast<size_t>(cs) * TB2 + v0;
     double* gl = cl >= 0 ? a.slots + static_cast<size_t>(cl) * TB2 + v0 : nullptr;
@@ -472,12 +476,12 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       s_splp = p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
     for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
-      const unsigned long long x0 = acc[2 * kk], x1 = acc[2 * kk + 1];
-      acc[2 * kk] = 0ull;
-      acc[2 * kk + 1] = 0ull;
+      const unsigned long long x0 = acc[pw * kk], x1 = qpack ? 0ull : acc[2 * kk + 1];
+      acc[pw * kk] = 0ull;
+      if (!qpack) acc[2 * kk + 1] = 0ull;
       long long q0 = static_cast<long long>(x0), q1 = static_cast<long long>(x1);
       if (qpack) {
-        // packed g32|h32 in the even word (the odd word stays zero)
+        // packed g32|h32, one word per bin
         const unsigned long long hs = x0 & 0xFFFFFFFFull;
         q0 = static_cast<long long>(x0 - hs) >> 32;
         q1 = static_cast<long long>(hs);

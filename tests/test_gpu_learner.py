@@ -249,7 +249,7 @@ def test_device_goss(lgb, gpu_required):
     assert abs(ag - ac) < 1e-3, (ag, ac)
 
 
-@pytest.mark.parametrize("transport", ["collective", "xgmi"])
+@pytest.mark.parametrize("transport", ["collective", "xgmi", "collective-quantized"])
 def test_data_parallel_path_single_rank(lgb, gpu_required, transport):
     """The owner-computes data-parallel learner path (owner exchange of the histogram, owned-feature
     scan, candidate table, global counts) on a one-rank communicator must reproduce the
@@ -260,7 +260,8 @@ def test_data_parallel_path_single_rank(lgb, gpu_required, transport):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20")
+    env = dict(os.environ, LGAP_DP_TRANSPORT=transport.replace("-quantized", ""), LGAP_XGMI_TIMEOUT_S="20",
+               DP_SELFTEST_QUANTIZED="1" if transport.endswith("quantized") else "0")
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "dp_selftest.py")], capture_output=True,
                        text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
