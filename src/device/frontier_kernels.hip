@@ -1735,8 +1735,12 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
     __syncthreads();
     FStamp(a, rnd, kFStampSel, 5);
-    int K = s_k;
+    // (the node capacity bounds the round: expansions voided by CEGB first-use events leave
+    // dead cids behind, so the reserve for the remaining splits is not a guarantee then)
+    int K = min(s_k, (C - cid_next) / 2);
     if (K <= 0) done = 1;  // nothing can be expanded: (only reachable without a blocked node)
+    __syncthreads();
+    if (t == 0) s_k = K > 0 ? K : 0;
     if (a.kused != nullptr && t == 0 && rnd + 1 < kFrontierRoundCap) a.kused[rnd + 1] = done ? 0 : K;
     if (!done && w == 0) {
       // expansion records, tiles prefix (wave 0; K <= 64)
