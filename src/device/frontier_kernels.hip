@@ -1898,7 +1898,6 @@ __global__ __launch_bounds__(256) void k_f_lazy(FArgs a) {
   const int e = blockIdx.y;
   if (e >= sp->k) return;
   const FExp x = a.exps[e];
-  if (x.skip) return;
   const int lw = a.lazy_words, F = a.F, t = threadIdx.x;
   uint32_t* s_mask = reinterpret_cast<uint32_t*>(lds_raw);
   int* s_cnt = reinterpret_cast<int*>(s_mask + lw);
@@ -1912,6 +1911,9 @@ __global__ __launch_bounds__(256) void k_f_lazy(FArgs a) {
       if (x.larger >= 0) a.npath[static_cast<size_t>(x.larger) * lw + i] = m;
     }
   }
+  // (children of a skipped expansion cannot split: their path masks are all they need, for
+  // the marks after the tree)
+  if (x.skip) return;
   for (int f = t; f < F; f += blockDim.x) s_cnt[f] = 0;
   __syncthreads();
   const int n = x.h_count;
