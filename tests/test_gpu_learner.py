@@ -502,7 +502,9 @@ def test_device_cegb_split_penalty(lgb, gpu_required, rng, extra):
                                     "cegb_penalty_feature_lazy": [0.01, 0.02, 0.03, 0.04, 0.05, 0.06]},
                                    {"cegb_penalty_feature_lazy": [0.05, 0.1, 0.1, 0.1, 0.1, 0.1],
                                     "cegb_penalty_feature_coupled": [0, 0, 40, 40, 10, 10], "bagging_fraction": 0.8,
-                                    "bagging_freq": 1}])
+                                    "bagging_freq": 1},
+                                   {"cegb_penalty_feature_lazy": [0.02, 0.02, 0.05, 0.05, 0.1, 0.1],
+                                    "min_data_in_leaf": 300, "num_leaves": 63}])
 def test_device_cegb_coupled_penalties(lgb, gpu_required, rng, extra):
     """CEGB feature penalties in the frontier engine. Coupled: raw candidates kept per node, the
     penalty of a feature not yet used by any split subtracted, and a feature's first use in the
