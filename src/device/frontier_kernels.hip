@@ -1556,25 +1556,15 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   FStamp(a, rnd, kFStampSel, 3);
   const int nl = s_nl, ns = s_ns, ncommit = s_ncommit;
   int done = s_done;
-  // ---- C. committed splits -> records (all threads: one load round), leaf table, states
-  {
-    constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-    for (int i = t; i < ncommit * kInfoWords; i += blockDim.x) {
-      const int k = i / kInfoWords, j = i - k * kInfoWords;
-      const int c1 = s_c1[k];
-      reinterpret_cast<uint32_t*>(&a.rec[st.num_splits + k].info)[j] =
-          reinterpret_cast<const uint32_t*>(c1 >= 0 ? a.best + c1 : a.fbest + ~c1)[j];
-    }
-    for (int k = t; k < ncommit; k += blockDim.x) {
-      const int c = s_c1[k] >= 0 ? s_c1[k] : ~s_c1[k];
-      const int left = s_left[c];
-      SplitRec* r = a.rec + st.num_splits + k;
-      r->leaf = s_c0[k];
-      r->left_count = a.nodes[left].gcount;
-      r->right_count = a.nodes[left + 1].gcount;
-      r->pad = 0;
-      a.nstate[c] = s_st[c];
-    }
+  // ---- C. committed splits -> (leaf, cid) records, leaf table, states. The full records
+  // (SplitInfo, children counts) are gathered once per tree by k_f_results: a committed
+  // node's best never changes, and the copy no longer sits on every round's critical path
+  for (int k = t; k < ncommit; k += blockDim.x) {
+    const int c = s_c1[k] >= 0 ? s_c1[k] : ~s_c1[k];
+    SplitRec* r = a.rec + st.num_splits + k;
+    r->leaf = s_c0[k];
+    r->pad = s_c1[k];  // committed cid (~cid: a forced split); k_f_results resolves it
+    a.nstate[c] = s_st[c];
   }
   for (int l = t; l < nl; l += blockDim.x) a.leaf_cid[l] = s_lcid[l];
   FStamp(a, rnd, kFStampSel, 4);
@@ -1872,9 +1862,28 @@ __global__ __launch_bounds__(256) void k_f_results(FArgs a, char* out) {
   }
   if (t < kFrontierRoundCap) h->kused[t] = a.kused != nullptr ? a.kused[t] : 0;
   if (!st.done) return;
-  const int nrec = static_cast<int>(sizeof(SplitRec) / 4) * st.num_splits;
+  // the committed splits' records: (leaf, cid) from the selects, SplitInfo and children counts
+  // gathered here, into the device records (later device consumers) and the pinned copy
+  constexpr int kRecWords = static_cast<int>(sizeof(SplitRec) / 4);
+  const int nrec = kRecWords * st.num_splits;
   uint32_t* rec = reinterpret_cast<uint32_t*>(out + FrontierResultRecOffset());
-  for (int i = t; i < nrec; i += blockDim.x) rec[i] = reinterpret_cast<const uint32_t*>(a.rec)[i];
+  for (int i = t; i < nrec; i += blockDim.x) {
+    const int k = i / kRecWords, j = i - k * kRecWords;
+    const int c1 = a.rec[k].pad;
+    const int c = c1 >= 0 ? c1 : ~c1;
+    uint32_t v;
+    if (j == 0) {
+      v = static_cast<uint32_t>(a.rec[k].leaf);
+    } else if (j == 1 || j == 2) {
+      v = static_cast<uint32_t>(a.nodes[a.nodes[c].left + (j - 1)].gcount);
+    } else if (j == 3) {
+      v = 0u;
+    } else {
+      v = reinterpret_cast<const uint32_t*>(c1 >= 0 ? a.best + c1 : a.fbest + c)[j - 4];
+    }
+    rec[i] = v;
+    if (j != 0 && j != 3) reinterpret_cast<uint32_t*>(a.rec)[i] = v;  // (leaf / cid words stay)
+  }
   const int nrange = static_cast<int>(sizeof(LeafRange) / 4) * st.num_leaves;
   uint32_t* rng = reinterpret_cast<uint32_t*>(out + FrontierResultRangeOffset(a.L));
   for (int i = t; i < nrange; i += blockDim.x) rng[i] = reinterpret_cast<const uint32_t*>(a.range_out)[i];
