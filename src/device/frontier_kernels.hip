@@ -1851,7 +1851,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
 // ---------------------------------------------------------------------------
 // k_f_results: the replay's state (and, once the tree is done, its split records and leaf
 // ranges) into the host-visible results buffer
-__global__ __launch_bounds__(256) void k_f_results(FArgs a, char* out) {
+__global__ __launch_bounds__(1024) void k_f_results(FArgs a, char* out) {
   FResultHdr* h = reinterpret_cast<FResultHdr*>(out);
   const FState st = *a.st;
   const int t = threadIdx.x;
@@ -1963,7 +1963,7 @@ __global__ __launch_bounds__(256) void k_f_lazy_mark(FArgs a) {
 }
 
 void LaunchFrontierResults(const FArgs& a, void* host_out, hipStream_t s) {
-  k_f_results<<<1, 256, 0, s>>>(a, static_cast<char*>(host_out));
+  k_f_results<<<1, 1024, 0, s>>>(a, static_cast<char*>(host_out));  // (gathers the tree's records)
   HIP_CHECK(hipGetLastError());
 }
 
