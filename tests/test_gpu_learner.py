@@ -276,7 +276,8 @@ def test_data_parallel_path_single_rank(lgb, gpu_required, transport):
 
 
 @pytest.mark.parametrize("world,transport", [(2, "collective"), (3, "collective"), (4, "collective"),
-                                             (2, "collective-seq"), (2, "xgmi"), (3, "xgmi"), (4, "xgmi")])
+                                             (2, "collective-seq"), (2, "xgmi"), (3, "xgmi"), (4, "xgmi"),
+                                             (3, "collective-quantized")])
 def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
     """P ranks share the one GPU. "collective": the data-parallel FRONTIER engine (per-round exact
     all-reduce of the fixed-point histograms through host-staged collectives, redundant scan and
@@ -290,8 +291,10 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    quantized = transport.endswith("-quantized")
+    transport = transport.replace("-quantized", "")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport.replace("-seq", ""),
-               LGAP_XGMI_TIMEOUT_S="20")
+               LGAP_XGMI_TIMEOUT_S="20", DP_QUANTIZED="1" if quantized else "0")
     if transport == "collective-seq":
         env["LGAP_FRONTIER_DP"] = "0"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
@@ -305,6 +308,11 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
     assert ("frontier engine" in res["device_name"]) == (transport == "collective"), res
     assert res["ranks_identical"], res
     assert res["num_trees"] == 10
+    if quantized:
+        # device and host quantizers round stochastically with different streams: the models
+        # agree in quality, not split for split
+        assert abs(res["auc_gpu"] - res["auc_cpu"]) < 5e-3, res
+        return
     # unit hessians (l2): the split structure must match the host learner tree for tree
     assert res["identical_leading_trees"] == 10, res
     assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
