@@ -29,6 +29,11 @@ bool CommActive();
 // Single-process HIP tree learner (device_type=gpu|cuda) and its data-parallel
 // variant (tree_learner=data|voting|feature with an RCCL communicator).
 std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const std::string& parallel_mode);
+// Whether the device learner's frontier engine can grow `config`'s trees on `train` (learner
+// type, sampling options and the engine's fixed LDS / node-capacity shape). The options only
+// the frontier implements on the device (forced splits, CEGB feature penalties) route to the
+// host split policy when it cannot.
+bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type);
 
 // GPU histogram engine for the host learners (the reference's GPUTreeLearner
 // split, src/treelearner/gpu_tree_learner.cpp: histograms on the device, split

@@ -903,6 +903,7 @@ int LGBM_BoosterPredictForFile(BoosterHandle handle, const char* data_filename, 
     // the model was trained on rows of a custom parser: predict through the same class
     auto parser = CreateCustomParser(parser_cfg);
     std::ifstream in(data_filename);
+    if (!in) Log::Fatal("Data file %s doesn't exist.", data_filename);
     std::string line;
     if (data_has_header) std::getline(in, line);
     while (std::getline(in, line)) {
@@ -911,6 +912,11 @@ int LGBM_BoosterPredictForFile(BoosterHandle handle, const char* data_filename, 
       double lab = 0.0;
       parser->ParseOneLine(line.c_str(), &rows.rows.back(), &lab);
       labels.push_back(static_cast<float>(lab));
+      for (const auto& kv : rows.rows.back()) {
+        if (kv.first < 0 || kv.first >= nf) {
+          Log::Fatal("The custom parser produced feature index %d, but the model has %d features", kv.first, nf);
+        }
+      }
     }
     rows.ncol = nf;
   } else {

@@ -2,6 +2,7 @@
 
 #include <omp.h>
 
+#include <atomic>
 #include <mutex>
 
 namespace lgap {
@@ -11,6 +12,9 @@ std::mutex g_mu;
 int g_default = -1;
 int g_max = -1;
 int g_omp_default = 0;  // OpenMP's team size before the library changed it
+// the team size every API entry applies (-1: nothing set, OpenMP's default stays); written under
+// g_mu by the setters, read lock-free by ApplyNumThreads (hot single-row predict paths)
+std::atomic<int> g_apply{-1};
 
 int Effective() {
   if (g_omp_default <= 0) g_omp_default = omp_get_max_threads();
@@ -25,6 +29,7 @@ void SetDefaultNumThreads(int num_threads) {
   (void)Effective();
   g_default = num_threads > 0 ? num_threads : -1;
   omp_set_num_threads(Effective());
+  g_apply.store(g_default <= 0 && g_max <= 0 ? -1 : Effective(), std::memory_order_release);
 }
 
 void SetMaxNumThreads(int num_threads) {
@@ -32,15 +37,12 @@ void SetMaxNumThreads(int num_threads) {
   (void)Effective();
   g_max = num_threads > 0 ? num_threads : -1;
   omp_set_num_threads(Effective());
+  g_apply.store(g_default <= 0 && g_max <= 0 ? -1 : Effective(), std::memory_order_release);
 }
 
 void ApplyNumThreads() {
-  int n;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (g_default <= 0 && g_max <= 0) return;  // nothing set: OpenMP's own default stays
-    n = Effective();
-  }
+  const int n = g_apply.load(std::memory_order_acquire);
+  if (n <= 0) return;  // nothing set: OpenMP's own default stays
   if (omp_get_max_threads() != n) omp_set_num_threads(n);
 }
 

@@ -124,6 +124,38 @@ class PinnedBuf {
 // Parallel modes of the device learner (tree_learner=serial|data|feature|voting).
 enum class DevParallel { kSerial, kData, kFeature, kVoting };
 
+// Computed-node capacity of one frontier tree: every committed node (2 L - 1) plus room for
+// speculation (8 L + 2 kmax, fewer when the per-node fp64 histograms would exceed ~8 GiB).
+int FrontierCapacityFor(int L, int TB) {
+  const long long lo = 4LL * L + 2 * kFrontierKmax, hi = 8LL * L + 2 * kFrontierKmax;
+  const long long slot_bytes = 16LL * std::max(TB, 1);
+  const long long fit = (8LL << 30) / slot_bytes;
+  const long long c = std::max(lo, std::min({hi, fit, static_cast<long long>(kFrontierMaxNodes)}));
+  return static_cast<int>(c);
+}
+
+// LDS of the frontier's k_f_scan: two full fp64 (g, h) histograms of the widest feature plus
+// the categorical sort arrays (index, ctr) of both scanning waves.
+size_t FrontierScanLds(int max_bin, int max_cat_bin) {
+  int cat_p2 = 1;
+  while (cat_p2 < max_cat_bin) cat_p2 <<= 1;
+  return static_cast<size_t>(max_bin) * 4 * sizeof(double) + static_cast<size_t>(cat_p2) * 2 * (sizeof(int) + sizeof(double));
+}
+
+// Whether a tree of L leaves over TB total bins / F features fits the frontier engine's fixed
+// resources: the select's LDS image of the computed nodes (plus the CEGB used flags), the node
+// capacity, and the scan's LDS. LGAP_FRONTIER=0 forces the sequential chain (A/B runs). The
+// learner factory routes with the same predicate (FrontierServes), so a configuration the
+// frontier cannot hold takes the host split policy instead of failing at allocation.
+bool FrontierShapeFits(int L, int TB, int F, int max_bin, int max_cat_bin, bool cegb_raw) {
+  const char* e = std::getenv("LGAP_FRONTIER");
+  if (e != nullptr && e[0] == '0') return false;
+  const int C = FrontierCapacityFor(std::max(2, L), TB);
+  if (C > kFrontierMaxNodes || F <= 0) return false;
+  if (FrontierScanLds(max_bin, max_cat_bin) > 150 * 1024) return false;
+  return FrontierSelectLds(C, std::max(2, L)) + (cegb_raw ? F + 16 : 0) <= 150 * 1024;
+}
+
 class DeviceTreeLearner : public TreeLearner {
  public:
   DeviceTreeLearner(const Config* config, DevParallel mode)
@@ -1045,12 +1077,9 @@ class DeviceTreeLearner : public TreeLearner {
   // the computed-node image of the select must fit its LDS. LGAP_FRONTIER=0 forces the
   // sequential chain (A/B runs).
   bool FrontierEligible() const {
-    const char* e = std::getenv("LGAP_FRONTIER");
-    if (e != nullptr && e[0] == '0') return false;
     if (!FrontierSerial() && !FrontierDP()) return false;
-    if (use_bynode_ || config_->extra_trees || scan_global_) return false;
-    if (FrontierCapacity() > kFrontierMaxNodes || F_ <= 0) return false;
-    return FrontierSelectLds(FrontierCapacity(), L_) + (CegbRaw() ? F_ + 16 : 0) <= 150 * 1024;
+    if (use_bynode_ || config_->extra_trees) return false;
+    return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, CegbRaw());
   }
   // CEGB feature penalties in the frontier select: coupled (FArgs::cegb_coupled: refunds on a
   // feature's first use) and lazy (FArgs::cegb_lazy: per-row marks, unmarked-row counts per
@@ -1085,13 +1114,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
   // computed nodes of one tree: every committed node (2 L - 1) plus room for speculation
   // (8 L + 2 kmax, fewer when the per-node fp64 histograms would exceed ~8 GiB)
-  int FrontierCapacity() const {
-    const long long lo = 4LL * L_ + 2 * kFrontierKmax, hi = 8LL * L_ + 2 * kFrontierKmax;
-    const long long slot_bytes = 16LL * std::max(TB_, 1);
-    const long long fit = (8LL << 30) / slot_bytes;
-    const long long c = std::max(lo, std::min({hi, fit, static_cast<long long>(kFrontierMaxNodes)}));
-    return static_cast<int>(c);
-  }
+  int FrontierCapacity() const { return FrontierCapacityFor(L_, TB_); }
 
   // forcedsplits_filename -> the FForced list the frontier select applies first (the host
   // learner's order and skips: learner/forced_splits.h)
@@ -1127,12 +1150,13 @@ class DeviceTreeLearner : public TreeLearner {
   void AllocFrontier() {
     frontier_ = FrontierEligible();
     if (!frontier_ && !config_->forcedsplits_filename.empty()) {
-      Log::Fatal("forced splits on the device need the frontier engine (serial learner, num_leaves <= 512, "
-                 "no feature_fraction_bynode / extra_trees)");
+      // (TreeLearner::Create routes these by FrontierServes: reaching here is a routing bug)
+      Log::Fatal("forced splits on the device need the frontier engine (serial learner, no "
+                 "feature_fraction_bynode / extra_trees, frontier LDS shape)");
     }
     if (!frontier_ && CegbRaw()) {
       Log::Fatal("cegb_penalty_feature_coupled / _lazy on the device need the frontier engine (serial learner, "
-                 "num_leaves <= 496, no feature_fraction_bynode / extra_trees)");
+                 "no feature_fraction_bynode / extra_trees, frontier LDS shape)");
     }
     if (!frontier_) return;
     fkmax_ = FrontierKmax();
@@ -1248,7 +1272,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (const char* e = std::getenv("LGAP_FPART_BPC")) cap = std::max(1, std::atoi(e));
     per_cu = std::max(1, std::min(cap, per_cu - 1));
     fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
-    fscan_lds_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + static_cast<size_t>(cat_p2_) * 2 * (sizeof(int) + sizeof(double));
+    fscan_lds_ = FrontierScanLds(max_bin_, has_cat_ ? max_cat_bin_ : 1);
     FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
@@ -2991,6 +3015,21 @@ std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const
   if (parallel_mode == "voting") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kVoting);
   Log::Fatal("Unknown tree learner type %s", parallel_mode.c_str());
   return nullptr;
+}
+
+bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type) {
+  if (learner_type != "serial" || config->feature_fraction_bynode < 1.0 || config->extra_trees) return false;
+  if (config->interaction_constraints_vector.size() > 64) return false;
+  if (train == nullptr) return config->num_leaves <= 256;  // (no data yet: a conservative shape)
+  int max_bin = 2, max_cat_bin = 1;
+  for (int f = 0; f < train->num_features(); ++f) {
+    const FeatureInfo& fi = train->feature(f);
+    max_bin = std::max(max_bin, fi.num_bin);
+    if (fi.bin_type == BinType::Categorical) max_cat_bin = std::max(max_cat_bin, fi.num_bin);
+  }
+  const bool cegb_raw = !config->cegb_penalty_feature_coupled.empty() || !config->cegb_penalty_feature_lazy.empty();
+  return FrontierShapeFits(std::max(2, config->num_leaves), train->num_total_bin(), train->num_features(), max_bin,
+                           max_cat_bin, cegb_raw);
 }
 
 namespace {

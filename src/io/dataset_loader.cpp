@@ -522,7 +522,10 @@ std::unique_ptr<Dataset> LoadDatasetFromFile(const std::string& filename, const 
     c2.ignore_column = ig;
   }
   auto ds = std::make_unique<Dataset>();
-  ds->Construct(rows, c2, reference, reference ? std::vector<std::string>() : feat_names, cats);
+  // a custom parser defines its own column layout: the raw header's names would not line up
+  // with it, so its features take the default Column_i names (reference dataset_loader.cpp:86-89)
+  const bool header_names = !reference && parser_cfg.empty();
+  ds->Construct(rows, c2, reference, header_names ? feat_names : std::vector<std::string>(), cats);
   ds->metadata().SetLabel(labels.data(), n);
   if (weight_idx >= 0) ds->metadata().SetWeights(weights.data(), n);
   if (!qb.empty()) ds->metadata().SetQueryBoundaries(qb);

@@ -27,16 +27,17 @@ std::unique_ptr<TreeLearner> CreateHost(const std::string& learner_type, bool li
 
 // The device learner keeps one fp64 (g, h) histogram per open leaf (2 x 8 bytes per bin,
 // device_learner.hip slots; the frontier engine adds its speculation slots inside an 8 GiB
-// cap). When num_leaves of them exceed histogram_pool_size (MB, when set) or half of the
-// device memory, training takes the host learner, whose LRU pool bounds the live
-// histograms and rebuilds evicted ones from rows (reference feature_histogram.hpp
-// HistogramPool), with the histograms still built by the HIP kernels.
+// cap). When num_leaves of them exceed half of the device memory, training takes the host
+// learner, whose LRU pool bounds the live histograms and rebuilds evicted ones from rows
+// (reference feature_histogram.hpp HistogramPool), with the histograms still built by the HIP
+// kernels. histogram_pool_size stays what it is in the reference, a bound on the HOST cache: it
+// does not move device training to the host policy (288 GB of HBM per MI355X hold the device
+// histograms of any realistic num_leaves).
 bool DeviceHistogramsExceedPool(const Config* c, const Dataset* train) {
   if (train == nullptr) return false;
   const double per_leaf = 16.0 * static_cast<double>(std::max(1, train->num_total_bin()));
   const double need = per_leaf * std::max(2, c->num_leaves);
-  double budget = 0.5 * static_cast<double>(device::DeviceTotalMemory());
-  if (c->histogram_pool_size > 0) budget = c->histogram_pool_size * 1024.0 * 1024.0;
+  const double budget = 0.5 * static_cast<double>(device::DeviceTotalMemory());
   return budget > 0 && need > budget;
 }
 
@@ -49,21 +50,19 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
   // CEGB: the split penalty runs in the device scans, the coupled and lazy feature penalties
   // in the frontier engine (serial learner: the select's replay refunds leaves and voids
-  // speculation on a feature's first use; per-row marks count each node's unmarked rows)
-  const bool frontier_ok = learner_type == "serial" && c->feature_fraction_bynode >= 1.0 && !c->extra_trees &&
-                           c->num_leaves <= 496 && c->max_bin <= 1024 && c->forcedsplits_filename.empty() &&
-                           c->interaction_constraints_vector.empty();
+  // speculation on a feature's first use; per-row marks count each node's unmarked rows).
+  // Forced splits also run on the frontier only. Both route by the frontier's own shape
+  // predicate (device::FrontierServes: the select / scan LDS and node capacity), so a
+  // configuration the frontier cannot hold trains under the host policy instead of failing.
   const bool feature_pens = !c->cegb_penalty_feature_coupled.empty() || !c->cegb_penalty_feature_lazy.empty();
-  if ((feature_pens && (!frontier_ok || (train != nullptr && train->num_features() > 8192))) ||
-      (CegbPenalty::Enabled(c) && learner_type == "voting")) {
+  const bool needs_frontier = feature_pens || !c->forcedsplits_filename.empty();
+  const bool frontier_ok = needs_frontier && device::FrontierServes(c, train, learner_type) &&
+                           (!feature_pens || ((train == nullptr || train->num_features() <= 8192) &&
+                                              c->interaction_constraints_vector.empty()));
+  if ((feature_pens && !frontier_ok) || (CegbPenalty::Enabled(c) && learner_type == "voting")) {
     return "cost-effective gradient boosting (feature penalties)";
   }
-  // forced splits run on the device's frontier engine (serial learner); elsewhere on the host
-  if (!c->forcedsplits_filename.empty() &&
-      !(learner_type == "serial" && c->feature_fraction_bynode >= 1.0 && !c->extra_trees && c->num_leaves <= 512 &&
-        c->max_bin <= 1024)) {
-    return "forced splits";
-  }
+  if (!c->forcedsplits_filename.empty() && !frontier_ok) return "forced splits";
   if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {
     return "intermediate/advanced monotone constraints";
   }

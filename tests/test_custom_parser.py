@@ -44,3 +44,25 @@ def test_registered_parser_trains_saves_and_predicts(lgb, tmp_path):
     b_file.save_model(str(model))
     loaded = lgb.Booster(model_file=str(model))
     np.testing.assert_allclose(loaded.predict(str(f)), b_arr.predict(X), rtol=1e-12, atol=1e-12)
+
+
+def test_custom_parser_with_header_uses_default_names(lgb, tmp_path):
+    """With header=true and a custom parser the raw header's names do not describe the parser's
+    columns (the label moves, widths may differ): the features get the default Column_i names
+    (reference dataset_loader.cpp:86-89) and the model equals one trained on the arrays."""
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((500, 3))
+    y = (X[:, 0] - X[:, 2] > 0).astype(float)
+    f = tmp_path / "rows_h.txt"
+    with open(f, "w") as fo:
+        fo.write("label_first_name;b;c;d\n")
+        for row, lab in zip(X, y):
+            fo.write(";".join(f"{v:.17g}" for v in row) + f";{lab:g}\n")
+    cfg = tmp_path / "parser.json"
+    cfg.write_text('{"className": "lambdagap.label_last", "delimiter": ";"}')
+    params = {"objective": "binary", "num_leaves": 7, "verbosity": -1, "min_data_in_leaf": 5}
+    ds = lgb.Dataset(str(f), params={"parser_config_file": str(cfg), "header": True})
+    b_file = lgb.train(params, ds, 4)
+    assert b_file.feature_name() == ["Column_0", "Column_1", "Column_2"]
+    b_arr = lgb.train(params, lgb.Dataset(X, y), 4)
+    np.testing.assert_allclose(b_file.predict(X), b_arr.predict(X), rtol=1e-12, atol=1e-12)
