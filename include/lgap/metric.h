@@ -12,6 +12,7 @@
 #include "lgap/meta.h"
 #include "lgap/objective.h"
 #include "lgap/pointwise_metric.h"
+#include "lgap/rank_metric_spec.h"
 
 namespace lgap {
 
@@ -30,6 +31,10 @@ class Metric {
   // and turn the device's weighted loss sum into the metric value.
   virtual bool DevicePointwise(const ObjectiveFunction*, PwMetricParams*) const { return false; }
   virtual std::vector<double> FinishSum(double) const { return {}; }
+  // Ranking / AUC metrics a device learner evaluates from its device-resident score: the
+  // description (lgap/rank_metric_spec.h), and the values from the device's raw sums.
+  virtual bool DeviceRankSpec(RankMetricSpec*) const { return false; }
+  virtual std::vector<double> FinishRank(const std::vector<double>&) const { return {}; }
 };
 
 class DCGCalculator {

@@ -13,6 +13,7 @@
 #include "lgap/config.h"
 #include "lgap/dataset.h"
 #include "lgap/objective.h"
+#include "lgap/rank_metric_spec.h"
 #include "lgap/tree.h"
 
 namespace lgap {
@@ -80,6 +81,9 @@ class TreeLearner {
   virtual void DeviceGetValidScore(int /*id*/, std::vector<double>*) {}
   virtual void DeviceSetValidScore(int /*id*/, const std::vector<double>&) {}
   virtual bool DeviceEvalPointwiseValid(int /*id*/, const PwMetricParams&, int /*k*/, double* /*sum*/) { return false; }
+  // Ranking / AUC metric of the training set (id < 0) or device validation set `id`, class k,
+  // on the device score: raw sums for Metric::FinishRank (false: evaluate on the host)
+  virtual bool DeviceEvalRank(int /*id*/, const RankMetricSpec&, int /*k*/, std::vector<double>* /*out*/) { return false; }
   virtual bool SupportsDeviceSampling() const { return false; }
   virtual void DeviceSample(int plan, int iter) { (void)plan; (void)iter; }
   virtual std::string DeviceName() const { return "cpu"; }

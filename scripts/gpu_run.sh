@@ -1,0 +1,30 @@
+#!/bin/bash
+# One gpurun call, parameterised: each named step runs under its own time limit and the call
+# stops at the first failing step (no GPU work after a fault, abort or time-out).
+#   bash scripts/gpu_run.sh tests:<pytest args> | smoke | bench:<bench args> | prof:<bench args> | py:<script args> ...
+# e.g. bash scripts/gpu_run.sh "tests:tests/test_device_metrics.py" "bench:--steps 40 --warmup 3"
+set -u
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+i=0
+for step in "$@"; do
+  i=$((i + 1))
+  kind=${step%%:*}
+  arg=${step#*:}
+  [ "$arg" = "$step" ] && arg=""
+  log=$OUT/step${i}_${kind}.log
+  case $kind in
+    tests) timeout -k 10 900 python -u -m pytest ${arg:-tests -m gpu} -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $log 2>&1 ;;
+    smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
+    bench) timeout -k 10 400 python bench.py $arg > $log 2>&1 ;;
+    prof)  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof$i -o run -- python3 bench.py $arg > $log 2>&1 &&
+             python scripts/prof_summary.py $OUT/prof$i "bench.py $arg" 12 > $OUT/prof${i}_summary.md 2>&1 && rm -rf $OUT/prof$i ;;
+    py)    timeout -k 10 600 python -u $arg > $log 2>&1 ;;
+    *) echo "unknown step $kind"; exit 2 ;;
+  esac
+  rc=$?
+  echo "=== step $i $kind rc=$rc"; tail -4 $log | cut -c1-400
+  [ -f $OUT/prof${i}_summary.md ] && head -24 $OUT/prof${i}_summary.md
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done

@@ -390,9 +390,9 @@ void GBDT::RollbackOneIter() {
 
 std::vector<double> GBDT::EvalOne(const Metric* m, const double* score) const { return m->Eval(score, objective_); }
 
-// Training metrics: pointwise metrics are evaluated where the score lives (the
-// device learner's HBM copy, no N-double download); everything else reads the
-// training score on the host. `*score` is fetched lazily and reused.
+// Training metrics: pointwise, AUC / average precision and query metrics are evaluated where
+// the score lives (the device learner's HBM copy, no N-double download); everything else reads
+// the training score on the host. `*score` is fetched lazily and reused.
 std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
   PwMetricParams p;
   const char* off = std::getenv("LGAP_DEVICE_METRICS");  // "0": always evaluate on the host (A/B, tests)
@@ -402,6 +402,12 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
     double sum = 0.0;
     if (learner_->DeviceEvalPointwise(p, 0, &sum)) return m->FinishSum(sum);
   }
+  // ranking / AUC metrics: sorted on the device, only their sums come back
+  RankMetricSpec rs;
+  if (allow && device_mode_ && num_tree_per_iteration_ == 1 && m->DeviceRankSpec(&rs)) {
+    std::vector<double> raw;
+    if (learner_->DeviceEvalRank(-1, rs, 0, &raw)) return m->FinishRank(raw);
+  }
   if (*score == nullptr) {
     int64_t len;
     *score = GetTrainingScore(&len);
@@ -409,13 +415,21 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
   return EvalOne(m, *score);
 }
 
-// Validation metrics: pointwise ones on the device-resident validation score, the rest
-// (AUC, NDCG, ...) on the host copy, refreshed once when stale.
+// Validation metrics: pointwise, AUC / average precision and the query metrics (NDCG, MAP,
+// precision@k) on the device-resident validation score; the rest (multiclass, auc_mu) on the
+// host copy, refreshed once when stale.
 std::vector<double> GBDT::EvalValid(size_t d, const Metric* m) {
   PwMetricParams p;
   if (valid_dev_[d] >= 0 && num_tree_per_iteration_ == 1 && m->DevicePointwise(objective_, &p)) {
     double sum = 0.0;
     if (learner_->DeviceEvalPointwiseValid(valid_dev_[d], p, 0, &sum)) return m->FinishSum(sum);
+  }
+  RankMetricSpec rs;
+  const char* off = std::getenv("LGAP_DEVICE_METRICS");
+  const bool allow = off == nullptr || std::strcmp(off, "0") != 0;
+  if (allow && valid_dev_[d] >= 0 && num_tree_per_iteration_ == 1 && m->DeviceRankSpec(&rs)) {
+    std::vector<double> raw;
+    if (learner_->DeviceEvalRank(valid_dev_[d], rs, 0, &raw)) return m->FinishRank(raw);
   }
   return EvalOne(m, ValidScore(d));
 }

@@ -78,6 +78,7 @@
 #include "device/grad_kernels.h"
 #include "device/hip_common.h"
 #include "device/leaf_kernels.h"
+#include "device/metric_kernels.h"
 #include "device/runtime_internal.h"
 #include "device/frontier.h"
 #include "device/traverse_kernels.h"
@@ -92,6 +93,7 @@
 #include "lgap/network.h"
 #include "lgap/objective.h"
 #include "lgap/rank_math.h"
+#include "lgap/metric.h"
 #include "lgap/split_math.h"
 
 namespace lgap {
@@ -736,12 +738,7 @@ class DeviceTreeLearner : public TreeLearner {
   bool DeviceEvalPointwise(const PwMetricParams& p, int k, double* sum) override {
     if (score_.size() < static_cast<size_t>(k + 1) * N_ || N_ <= 0) return false;
     ScopedTimer timer("Device::EvalMetric");
-    const Metadata& md = data_->metadata();
-    if (metric_label_.size() == 0) {
-      metric_label_.Upload(md.label(), N_, stream_);  // the raw labels (objectives may relabel theirs)
-      if (md.weights()) metric_weight_.Upload(md.weights(), N_, stream_);
-      metric_partial_.Resize(kMetricBlocks + 1);
-    }
+    EnsureMetricLabels();
     LaunchPointwiseMetric(p, score_.get() + static_cast<size_t>(k) * N_, metric_label_.get(),
                           metric_weight_.size() ? metric_weight_.get() : nullptr, N_, metric_partial_.get(),
                           kMetricBlocks, metric_partial_.get() + kMetricBlocks, stream_);
@@ -943,6 +940,7 @@ class DeviceTreeLearner : public TreeLearner {
     const Metadata& md = v->metadata();
     if (md.label()) dv->label.Upload(md.label(), dv->n, stream_);
     if (md.weights()) dv->weight.Upload(md.weights(), dv->n, stream_);
+    dv->host_label = md.label();
     HIP_CHECK(hipStreamSynchronize(stream_));
     valid_.push_back(std::move(dv));
     return static_cast<int>(valid_.size()) - 1;
@@ -979,6 +977,113 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipStreamSynchronize(stream_));
     *sum = h[0];
     return true;
+  }
+
+  // Ranking / AUC metrics on the device score (metric_kernels.h): the training set (id < 0)
+  // or a device validation set. The metric's per-query tables are uploaded once per metric;
+  // only the metric's raw sums come back (no score download).
+  bool DeviceEvalRank(int id, const RankMetricSpec& spec, int k, std::vector<double>* out) override {
+    const double* score = nullptr;
+    const float* label = nullptr;
+    const float* weight = nullptr;
+    const void* host_label = nullptr;
+    int n = 0;
+    if (id < 0) {
+      n = N_;
+      if (n <= 0 || score_.size() < static_cast<size_t>(k + 1) * N_) return false;
+      EnsureMetricLabels();
+      score = score_.get() + static_cast<size_t>(k) * N_;
+      label = metric_label_.get();
+      weight = metric_weight_.size() ? metric_weight_.get() : nullptr;
+      host_label = data_->metadata().label();
+    } else {
+      if (id >= static_cast<int>(valid_.size())) return false;
+      DevValid& v = *valid_[id];
+      if (v.label.size() == 0) return false;
+      n = v.n;
+      score = v.score.get() + static_cast<size_t>(k) * n;
+      label = v.label.get();
+      weight = v.weight.size() ? v.weight.get() : nullptr;
+      host_label = v.host_label;
+    }
+    if (spec.num_data != n || spec.label != host_label) return false;
+    if ((spec.weights != nullptr) != (weight != nullptr)) return false;
+    const bool query = spec.kind >= RankMetricSpec::kNDCG;
+    if (query && (spec.num_queries <= 0 || spec.query_boundaries == nullptr || spec.eval_at.empty() ||
+                  spec.eval_at.size() > static_cast<size_t>(RankMetricSpec::kMaxEvalAt))) {
+      return false;
+    }
+    ScopedTimer timer("Device::EvalRankMetric");
+    auto& slot = rank_states_[spec.owner];
+    if (!slot || slot->kind != spec.kind || slot->n != n || slot->nq != spec.num_queries || slot->host_label != host_label ||
+        slot->host_qb != static_cast<const void*>(spec.query_boundaries) || slot->ks != spec.eval_at) {
+      slot = std::make_unique<RankEvalState>();
+      RankEvalState& r = *slot;
+      r.kind = spec.kind;
+      r.n = n;
+      r.nq = spec.num_queries;
+      r.host_label = host_label;
+      r.host_qb = spec.query_boundaries;
+      r.ks = spec.eval_at;
+      if (query) {
+        const int nq = spec.num_queries, ne = static_cast<int>(spec.eval_at.size());
+        std::vector<int> qb(spec.query_boundaries, spec.query_boundaries + nq + 1);
+        int maxq = 1;
+        for (int q = 0; q < nq; ++q) maxq = std::max(maxq, qb[q + 1] - qb[q]);
+        r.qb.Upload(qb, stream_);
+        if (spec.query_weights) r.qw.Upload(spec.query_weights, nq, stream_);
+        r.ks_dev.Upload(spec.eval_at, stream_);
+        if (spec.kind == RankMetricSpec::kNDCG) {
+          if (spec.inv_max.size() != static_cast<size_t>(nq) * ne || spec.label_gain.empty()) return false;
+          r.inv_max.Upload(spec.inv_max, stream_);
+          r.gain.Upload(spec.label_gain, stream_);
+          std::vector<double> disc(maxq);  // DCGCalculator::Init's discount table
+          for (int i = 0; i < maxq; ++i) disc[i] = 1.0 / std::log2(2.0 + i);
+          r.disc.Upload(disc, stream_);
+        } else if (spec.kind == RankMetricSpec::kMAP) {
+          if (spec.npos.size() != static_cast<size_t>(nq)) return false;
+          r.npos.Upload(spec.npos, stream_);
+        }
+        r.scratch.Resize(QueryMetricScratchBytes(n, nq, ne));
+      } else {
+        r.scratch.Resize(AucScratchBytes(n));
+      }
+      r.out.Resize(RankMetricSpec::kMaxEvalAt);
+    }
+    RankEvalState& r = *slot;
+    int nout = 2;
+    if (query) {
+      QueryMetricArgs qa;
+      qa.kind = spec.kind;
+      qa.qb = r.qb.get();
+      qa.nq = r.nq;
+      qa.qw = r.qw.size() ? r.qw.get() : nullptr;
+      qa.inv_max = r.inv_max.size() ? r.inv_max.get() : nullptr;
+      qa.npos = r.npos.size() ? r.npos.get() : nullptr;
+      qa.ks = r.ks_dev.get();
+      qa.ne = static_cast<int>(r.ks.size());
+      qa.gain = r.gain.size() ? r.gain.get() : nullptr;
+      qa.ngain = static_cast<int>(r.gain.size());
+      qa.disc = r.disc.size() ? r.disc.get() : nullptr;
+      LaunchQueryMetric(qa, score, label, n, r.scratch.get(), r.scratch.size(), r.out.get(), stream_);
+      nout = qa.ne;
+    } else {
+      LaunchAucMetric(spec.kind == RankMetricSpec::kAveragePrecision, score, label, weight, n, r.scratch.get(),
+                      r.scratch.size(), r.out.get(), stream_);
+    }
+    double* h = pin_metric_.Get(RankMetricSpec::kMaxEvalAt);
+    HIP_CHECK(hipMemcpyAsync(h, r.out.get(), sizeof(double) * nout, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    out->assign(h, h + nout);
+    return true;
+  }
+
+  void EnsureMetricLabels() {
+    if (metric_label_.size() != 0) return;
+    const Metadata& md = data_->metadata();
+    metric_label_.Upload(md.label(), N_, stream_);  // the raw labels (objectives may relabel theirs)
+    if (md.weights()) metric_weight_.Upload(md.weights(), N_, stream_);
+    metric_partial_.Resize(kMetricBlocks + 1);
   }
 
   std::unique_ptr<Tree> DeviceTrain(int class_id, bool is_first_tree) override {
@@ -2964,7 +3069,21 @@ class DeviceTreeLearner : public TreeLearner {
     DevBuf<uint32_t> rowbins;
     DevBuf<double> score;
     DevBuf<float> label, weight;
+    const float* host_label = nullptr;  // the dataset's labels (identity check of metric specs)
   };
+  // per-metric device tables of the ranking / AUC metrics (DeviceEvalRank), keyed by the metric
+  struct RankEvalState {
+    int kind = -1, n = 0, nq = 0;
+    const void* host_label = nullptr;
+    const void* host_qb = nullptr;
+    std::vector<int> ks;
+    DevBuf<int> qb, npos, ks_dev;
+    DevBuf<float> qw;
+    DevBuf<double> inv_max, gain, disc, out;
+    DevBuf<char> scratch;
+  };
+  std::map<const void*, std::unique_ptr<RankEvalState>> rank_states_;
+  PinnedBuf<double> pin_metric_;
   std::vector<std::unique_ptr<DevValid>> valid_;
   // refit / leaf renewal
   DevBuf<int> leaf_pred_dev_, renew_off_, renew_nz_;

@@ -6,6 +6,8 @@
 // visible: no silent CPU fallback.
 #include "lgap/tree_learner.h"
 
+#include <cstdlib>
+
 #include "lgap/device_api.h"
 #include "lgap/log.h"
 #include "parallel_tree_learner.h"
@@ -37,7 +39,9 @@ bool DeviceHistogramsExceedPool(const Config* c, const Dataset* train) {
   if (train == nullptr) return false;
   const double per_leaf = 16.0 * static_cast<double>(std::max(1, train->num_total_bin()));
   const double need = per_leaf * std::max(2, c->num_leaves);
-  const double budget = 0.5 * static_cast<double>(device::DeviceTotalMemory());
+  double budget = 0.5 * static_cast<double>(device::DeviceTotalMemory());
+  // LGAP_DEVICE_HIST_BUDGET_MB: a smaller device budget (tests of the pooled route)
+  if (const char* e = std::getenv("LGAP_DEVICE_HIST_BUDGET_MB")) budget = std::atof(e) * 1024.0 * 1024.0;
   return budget > 0 && need > budget;
 }
 
@@ -89,7 +93,9 @@ std::unique_ptr<TreeLearner> TreeLearner::Create(const std::string& learner_type
     serial->EnableDeviceHistograms();
     // routed here by the histogram bound: keep the host pool within the same budget
     if (DeviceHistogramsExceedPool(config, train) && config->histogram_pool_size <= 0) {
-      serial->SetHistPoolBudgetMB(0.5 * static_cast<double>(device::DeviceTotalMemory()) / (1024.0 * 1024.0));
+      double mb = 0.5 * static_cast<double>(device::DeviceTotalMemory()) / (1024.0 * 1024.0);
+      if (const char* e = std::getenv("LGAP_DEVICE_HIST_BUDGET_MB")) mb = std::atof(e);
+      serial->SetHistPoolBudgetMB(mb);
     }
     return learner;
   }

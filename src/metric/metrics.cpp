@@ -14,6 +14,7 @@
 #include "lgap/common.h"
 #include "lgap/log.h"
 #include "lgap/metric.h"
+#include "lgap/parallel_sort.h"
 #include "lgap/pointwise_metric.h"
 
 namespace lgap {
@@ -233,11 +234,32 @@ class AUCMetric : public Metric {
   }
   const std::vector<std::string>& GetName() const override { return name_; }
   double factor_to_bigger_better() const override { return 1.0; }
+  bool DeviceRankSpec(RankMetricSpec* out) const override {
+    out->kind = ap_ ? RankMetricSpec::kAveragePrecision : RankMetricSpec::kAUC;
+    out->owner = this;
+    out->num_data = n_;
+    out->label = label_;
+    out->weights = w_;
+    return true;
+  }
+  // device sums {accumulator, positive weight} -> the value, as the end of Eval below
+  std::vector<double> FinishRank(const std::vector<double>& v) const override {
+    const double accum = v[0], sum_pos = v[1];
+    double r = 1.0;
+    if (ap_) {
+      if (sum_pos > 0.0 && sum_pos != sumw_) r = accum / sum_pos;
+    } else if (sum_pos > 0.0 && sum_pos != sumw_) {
+      r = accum / (sum_pos * (sumw_ - sum_pos));
+    }
+    return {r};
+  }
   std::vector<double> Eval(const double* score, const ObjectiveFunction*) const override {
     if (n_ == 0) return {1.0};
     std::vector<data_size_t> idx(n_);
     std::iota(idx.begin(), idx.end(), 0);
-    std::sort(idx.begin(), idx.end(), [score](data_size_t a, data_size_t b) { return score[a] > score[b]; });
+    // tied scores form one group below, so their order is free: an unstable parallel sort
+    // (reference binary_metric.hpp:200 Common::ParallelSort)
+    common::ParallelSort(&idx, [score](data_size_t a, data_size_t b) { return score[a] > score[b]; });
     double cur_pos = 0, sum_pos = 0, accum = 0, cur_neg = 0;
     double sum_pred_pos = 0, accum_prec = 1.0;
     double thr = score[idx[0]];
@@ -467,6 +489,30 @@ class QueryMetric : public Metric {
   }
   const std::vector<std::string>& GetName() const override { return name_; }
   double factor_to_bigger_better() const override { return 1.0; }
+  bool DeviceRankSpec(RankMetricSpec* out) const override {
+    if (eval_at_.empty() || eval_at_.size() > static_cast<size_t>(RankMetricSpec::kMaxEvalAt)) return false;
+    out->kind = k_ == NDCG ? RankMetricSpec::kNDCG : (k_ == MAP ? RankMetricSpec::kMAP : RankMetricSpec::kPrecision);
+    out->owner = this;
+    out->num_data = n_;
+    out->label = label_;
+    out->num_queries = nq_;
+    out->query_boundaries = qb_;
+    out->query_weights = qw_;
+    out->eval_at = eval_at_;
+    if (k_ == NDCG) {
+      out->label_gain = DCGCalculator::label_gain();
+      out->inv_max.clear();
+      for (const auto& v : inv_max_) out->inv_max.insert(out->inv_max.end(), v.begin(), v.end());
+    } else if (k_ == MAP) {
+      out->npos.assign(npos_.begin(), npos_.end());
+    }
+    return true;
+  }
+  std::vector<double> FinishRank(const std::vector<double>& v) const override {
+    std::vector<double> r(v);
+    for (auto& x : r) x /= sumqw_;
+    return r;
+  }
   std::vector<double> Eval(const double* score, const ObjectiveFunction*) const override {
     const size_t ne = eval_at_.size();
     std::vector<double> result(ne, 0.0);

@@ -532,23 +532,49 @@ def test_device_cegb_coupled_penalties(lgb, gpu_required, rng, extra):
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-4)
 
 
-def test_histogram_pool_bound_routes_to_pooled_learner(lgb, gpu_required, rng):
-    """num_leaves per-leaf device histograms above histogram_pool_size: training takes the host
-    learner's LRU histogram pool (evicted histograms rebuilt from rows by the HIP kernels) instead
-    of the device learner's one-slot-per-leaf store; the model equals the pooled CPU learner's."""
+def test_histogram_pool_bound_routes_to_pooled_learner(lgb, gpu_required, rng, monkeypatch):
+    """num_leaves per-leaf device histograms above the device budget (half the HBM; here a small
+    budget through LGAP_DEVICE_HIST_BUDGET_MB): training takes the host learner's LRU histogram
+    pool (evicted histograms rebuilt from rows by the HIP kernels) instead of the device learner's
+    one-slot-per-leaf store; the model equals the pooled CPU learner's. A user-set
+    histogram_pool_size bounds only the host cache, as in the reference: the device learner stays."""
     X, z = _policy_data(rng)
     y = (z > 0).astype(float)
     # 6 features x 255 bins x 16 B ~ 24 KB per leaf: 63 leaves ~ 1.5 MB > 1 MB
     extra = {"num_leaves": 63, "histogram_pool_size": 1.0}
     bc = _train(lgb, X, y, "cpu", rounds=3, **extra)
+    monkeypatch.setenv("LGAP_DEVICE_HIST_BUDGET_MB", "1")
     bg = _train(lgb, X, y, "gpu", rounds=3, gpu_use_dp=True, **extra)
     assert "host split policy" in bg.device_name()
     assert [s[:2] for s in _splits(_trees(bc)[0]["tree_structure"], [])] == \
         [s[:2] for s in _splits(_trees(bg)[0]["tree_structure"], [])]
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
-    # within the pool: the device learner
-    bd = _train(lgb, X, y, "gpu", rounds=1, num_leaves=63, histogram_pool_size=64.0)
+    monkeypatch.delenv("LGAP_DEVICE_HIST_BUDGET_MB")
+    # a small user histogram_pool_size alone keeps the device learner
+    bd = _train(lgb, X, y, "gpu", rounds=1, num_leaves=63, histogram_pool_size=1.0)
     assert "host split policy" not in bd.device_name()
+
+
+def test_frontier_only_options_fall_back_when_the_frontier_cannot_hold_them(lgb, gpu_required, rng, tmp_path):
+    """Forced splits and CEGB feature penalties run on the frontier engine only. A tree the
+    frontier's select cannot hold in LDS (num_leaves=400: ~169 KB node image) takes the host split
+    policy over HIP histograms instead of failing at allocation (device::FrontierServes)."""
+    import json
+
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    f = tmp_path / "forced.json"
+    f.write_text(json.dumps({"feature": 4, "threshold": 0.1, "left": {"feature": 5, "threshold": -0.2}}))
+    kw = {"num_leaves": 400, "min_data_in_leaf": 2, "forcedsplits_filename": str(f)}
+    bg = _train(lgb, X, y, "gpu", rounds=2, gpu_use_dp=True, **kw)
+    assert "host split policy" in bg.device_name()
+    root = _trees(bg)[0]["tree_structure"]
+    assert root["split_feature"] == 4 and root["left_child"]["split_feature"] == 5
+    bc = _train(lgb, X, y, "cpu", rounds=2, **kw)
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
+    pen = [0.5] * X.shape[1]
+    bp = _train(lgb, X, y, "gpu", rounds=1, num_leaves=400, min_data_in_leaf=2, cegb_penalty_feature_coupled=pen)
+    assert "host split policy" in bp.device_name()
 
 
 FORCED_TREES = [
