@@ -273,6 +273,19 @@ LIGHTGBM_C_EXPORT int LGBM_DatasetGetGroupBins(DatasetHandle handle, uint16_t* o
 // out_hist has 2 * num_total_bin doubles; group bin 0 (all features at their most frequent bin) stays 0.
 LIGHTGBM_C_EXPORT int LGBM_DeviceHistogram(DatasetHandle handle, const float* grad, const float* hess,
                                            const int32_t* rows, int32_t num_rows, double* out_hist);
+// Direct tests of the frontier engine's production kernels with a device learner configured by
+// `parameters`: k_f_hist over k row subsets (rows concatenated, offsets[k + 1]) -> out
+// [k][num_total_bin][2] at the kernel's fixed-point scale (quantized: integer level sums, levels
+// [num_data] = g level << 8 | h level); k_f_partition of k parents -> the device's children lists
+// and left counts next to the host learner's stable partition (exp_*).
+LIGHTGBM_C_EXPORT int LGBM_DeviceTestFrontierHist(DatasetHandle handle, const char* parameters, const float* grad,
+                                                  const float* hess, const int32_t* rows, const int32_t* offsets,
+                                                  int k, double* out, uint16_t* levels);
+LIGHTGBM_C_EXPORT int LGBM_DeviceTestFrontierPartition(DatasetHandle handle, const char* parameters,
+                                                       const int32_t* rows, const int32_t* offsets, int k,
+                                                       const int32_t* feats, const int32_t* thr, const int32_t* dleft,
+                                                       const uint32_t* catbits, int32_t* out_rows, int32_t* out_left,
+                                                       int32_t* exp_rows, int32_t* exp_left);
 // One device row-sampling pass (the HIP bagging / GOSS kernels) over host arrays: mode 1 bagging,
 // 2 balanced bagging, 3 GOSS; `rounds` > 1 re-bags with the advanced streams and reports the last.
 // grad/hess (num_class * num_rows, class-major) are scaled in place by GOSS. Returns the kept

@@ -55,6 +55,18 @@ std::unique_ptr<HistogramBackend> CreateHistogramBackend(const Config* config, c
 void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, const int* rows, int num_rows,
                      double* out);
 
+// Direct tests of the frontier's production kernels (tests/test_frontier_kernels.py):
+// k_f_hist over k row subsets (rows concatenated, offsets[k + 1]) -> out[k][num_total_bin][2]
+// at the kernel's fixed-point scale (quantized training: integer level sums; levels[N] the
+// quantized g << 8 | h levels); k_f_partition of k parents split by (inner feature, threshold
+// bin / categorical bin set, default_left) -> the device's children lists and left counts, and
+// the host learner's stable partition of the same split.
+void TestFrontierHist(const Dataset* data, const Config& config, const float* grad, const float* hess, const int* rows,
+                      const int* offsets, int k, double* out, uint16_t* levels);
+void TestFrontierPartition(const Dataset* data, const Config& config, const int* rows, const int* offsets, int k,
+                           const int* feats, const int* thr, const int* dleft, const uint32_t* catbits, int* out_rows,
+                           int* out_left, int* exp_rows, int* exp_left);
+
 // One pass of the device row-sampling kernels over host arrays (LGBM_DeviceSampleRows):
 // returns the kept-row count, rows in out_rows, GOSS scaling applied to grad / hess.
 int SampleRowsOnDevice(int mode, int num_rows, int num_class, float* grad, float* hess, const float* label,

@@ -13,7 +13,8 @@ import numpy as np
 
 from ..basic import _LIB, Booster, Dataset, _check
 
-__all__ = ["group_layout", "group_bins", "device_histogram", "device_sample_rows", "booster_gradients"]
+__all__ = ["group_layout", "group_bins", "device_histogram", "device_sample_rows", "booster_gradients",
+           "frontier_histogram", "frontier_partition"]
 
 
 def group_layout(ds: Dataset) -> Tuple[int, int, int, np.ndarray]:
@@ -90,3 +91,70 @@ def booster_gradients(booster: Booster) -> Tuple[np.ndarray, np.ndarray]:
     _check(_LIB.LGBM_BoosterGetGradients(booster.handle, ctypes.byref(n), g.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                                          h.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
     return g, h
+
+
+def _param_str(params: Optional[dict]) -> bytes:
+    return " ".join(f"{k}={v}" for k, v in (params or {}).items()).encode()
+
+
+def _subsets(subsets):
+    rows = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.int32) for s in subsets]), dtype=np.int32)
+    offsets = np.zeros(len(subsets) + 1, dtype=np.int32)
+    offsets[1:] = np.cumsum([len(s) for s in subsets])
+    return rows, offsets
+
+
+def frontier_histogram(ds: Dataset, grad: np.ndarray, hess: np.ndarray, subsets, params: Optional[dict] = None
+                       ) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    """One launch of the frontier engine's production histogram kernel (k_f_hist) over several row
+    subsets at once, one expansion each, with a device learner set up by ``params``.
+
+    Returns ([k, num_total_bin, 2] sums at the kernel's fixed-point scale -- integer level sums under
+    use_quantized_grad --, and for quantized training the per-row levels as (g_level, h_level))."""
+    ds.construct()
+    tb = group_layout(ds)[1]
+    rows, offsets = _subsets(subsets)
+    k = len(subsets)
+    g = np.ascontiguousarray(grad, dtype=np.float32)
+    h = np.ascontiguousarray(hess, dtype=np.float32)
+    out = np.zeros(k * tb * 2, dtype=np.float64)
+    levels = np.zeros(ds.num_data(), dtype=np.uint16)
+    i32 = ctypes.POINTER(ctypes.c_int32)
+    _check(_LIB.LGBM_DeviceTestFrontierHist(
+        ds.handle, ctypes.c_char_p(_param_str(params)), g.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+        h.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), rows.ctypes.data_as(i32), offsets.ctypes.data_as(i32),
+        ctypes.c_int(k), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+        levels.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))))
+    lv = None
+    if (params or {}).get("use_quantized_grad"):
+        lv = np.stack([(levels >> 8).astype(np.uint8).view(np.int8).astype(np.int64),
+                       (levels & 0xFF).astype(np.int64)], axis=1)
+    return out.reshape(k, tb, 2), lv
+
+
+def frontier_partition(ds: Dataset, subsets, splits, params: Optional[dict] = None):
+    """One launch of the frontier engine's production partition kernel (k_f_partition) over several
+    parents at once. ``splits``: per parent (inner feature, threshold bin, default_left, categorical
+    bins or None). Returns (device children lists, device left counts, host learner's lists, host
+    left counts); each parent's list holds its lefts in order, then its rights."""
+    ds.construct()
+    rows, offsets = _subsets(subsets)
+    k = len(subsets)
+    feats = np.array([s[0] for s in splits], dtype=np.int32)
+    thr = np.array([s[1] for s in splits], dtype=np.int32)
+    dleft = np.array([int(s[2]) for s in splits], dtype=np.int32)
+    bits = np.zeros((k, 32), dtype=np.uint32)  # kMaxCatWords (split_math.h) words per parent
+    for e, s in enumerate(splits):
+        for b in (s[3] if len(s) > 3 and s[3] is not None else []):
+            bits[e, b >> 5] |= np.uint32(1 << (b & 31))
+    out_rows = np.zeros(max(rows.size, 1), dtype=np.int32)
+    exp_rows = np.zeros(max(rows.size, 1), dtype=np.int32)
+    out_left = np.zeros(k, dtype=np.int32)
+    exp_left = np.zeros(k, dtype=np.int32)
+    i32 = ctypes.POINTER(ctypes.c_int32)
+    _check(_LIB.LGBM_DeviceTestFrontierPartition(
+        ds.handle, ctypes.c_char_p(_param_str(params)), rows.ctypes.data_as(i32), offsets.ctypes.data_as(i32),
+        ctypes.c_int(k), feats.ctypes.data_as(i32), thr.ctypes.data_as(i32), dleft.ctypes.data_as(i32),
+        bits.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), out_rows.ctypes.data_as(i32),
+        out_left.ctypes.data_as(i32), exp_rows.ctypes.data_as(i32), exp_left.ctypes.data_as(i32)))
+    return out_rows[:rows.size], out_left, exp_rows[:rows.size], exp_left

@@ -46,7 +46,23 @@ def main() -> int:
                 "min_sum_hessian_in_leaf": 100, "device_type": "gpu", "verbosity": -1, "seed": 7}
         ds = lgb.Dataset(X, y, params=base, free_raw_data=False).construct()
     variants = args.variant or ["device_use_graph=1", "device_use_graph=0"]
-    boosters = []
+    boosters, benvs = [], []
+
+    class _Env:  # a variant's environment knobs, applied while its booster is set up and updated
+        def __init__(self, envs):
+            self.envs = envs
+
+        def __enter__(self):
+            self.saved = {k: os.environ.get(k) for k in self.envs}
+            os.environ.update(self.envs)
+
+        def __exit__(self, *exc):
+            for k, old_v in self.saved.items():
+                if old_v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = old_v
+
     for v in variants:
         p = dict(base)
         envs = {}
@@ -56,26 +72,23 @@ def main() -> int:
                 envs[k[4:]] = val
             else:
                 p[k] = val
-        saved = {k: os.environ.get(k) for k in envs}
-        os.environ.update(envs)
-        boosters.append(lgb.Booster(params=p, train_set=ds))
-        for k, old_v in saved.items():
-            if old_v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = old_v
-    for b in boosters:
-        for _ in range(args.warmup):
-            b.update()
+        benvs.append(_Env(envs))
+        with benvs[-1]:
+            boosters.append(lgb.Booster(params=p, train_set=ds))
+    for b, env in zip(boosters, benvs):
+        with env:
+            for _ in range(args.warmup):
+                b.update()
     device_synchronize()
     times = [[] for _ in boosters]
     for _ in range(args.rounds):
         for i, b in enumerate(boosters):
             device_synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.block):
-                b.update()
-            device_synchronize()
+            with benvs[i]:
+                t0 = time.perf_counter()
+                for _ in range(args.block):
+                    b.update()
+                device_synchronize()
             times[i].append(1000.0 * (time.perf_counter() - t0) / args.block)
     out = {v: {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(np.min(t)), 4)}
            for v, t in zip(variants, times)}

@@ -1215,6 +1215,29 @@ int LGBM_DeviceHistogram(DatasetHandle handle, const float* grad, const float* h
   API_END();
 }
 
+// Direct frontier-kernel tests (device_api.h TestFrontierHist / TestFrontierPartition): a device
+// learner with `parameters` on the Dataset, one k_f_hist / k_f_partition launch over row subsets.
+int LGBM_DeviceTestFrontierHist(DatasetHandle handle, const char* parameters, const float* grad, const float* hess,
+                                const int32_t* rows, const int32_t* offsets, int k, double* out, uint16_t* levels) {
+  API_BEGIN();
+  Config cfg = ParseConfig(parameters);
+  cfg.device_type = "gpu";
+  device::TestFrontierHist(D(handle)->ds.get(), cfg, grad, hess, rows, offsets, k, out, levels);
+  API_END();
+}
+
+int LGBM_DeviceTestFrontierPartition(DatasetHandle handle, const char* parameters, const int32_t* rows,
+                                     const int32_t* offsets, int k, const int32_t* feats, const int32_t* thr,
+                                     const int32_t* dleft, const uint32_t* catbits, int32_t* out_rows,
+                                     int32_t* out_left, int32_t* exp_rows, int32_t* exp_left) {
+  API_BEGIN();
+  Config cfg = ParseConfig(parameters);
+  cfg.device_type = "gpu";
+  device::TestFrontierPartition(D(handle)->ds.get(), cfg, rows, offsets, k, feats, thr, dleft, catbits, out_rows,
+                                out_left, exp_rows, exp_left);
+  API_END();
+}
+
 int LGBM_DeviceSampleRows(int mode, int32_t num_rows, int num_class, float* grad, float* hess, const float* label,
                           double fraction, double pos_fraction, double neg_fraction, double top_rate,
                           double other_rate, int bagging_seed, uint32_t goss_seed, int rounds, int32_t* out_rows,

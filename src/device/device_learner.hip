@@ -1517,6 +1517,10 @@ class DeviceTreeLearner : public TreeLearner {
       }
     }
     a.sel_bitonic = std::getenv("LGAP_SEL_BITONIC") != nullptr ? 1 : 0;
+    {
+      const char* e = std::getenv("LGAP_PART_NT");
+      a.part_nt = e != nullptr && e[0] == '1' ? 1 : 0;
+    }
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
@@ -2046,6 +2050,174 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   // One histogram of (g, h) over `rows` (identity when null) into `out` (2 * TB doubles).
+  // ---- direct tests of the frontier's production kernels (tests/test_frontier_kernels.py)
+
+  // k_f_hist over k row subsets at once (one expansion each, as a round of the frontier):
+  // out[k][TB][2] = the accumulators at the tree's global fixed-point scale (quantized
+  // training: the integer level sums), levels[N] = the quantized levels (g << 8 | h).
+  void TestFrontierHist(const float* g, const float* h, const int* rows, const int* offsets, int k, double* out,
+                        uint16_t* levels) {
+    if (!frontier_) Log::Fatal("TestFrontierHist: the frontier engine is not enabled for this configuration");
+    if (k < 1 || k > fkmax_) Log::Fatal("TestFrontierHist: %d subsets (1..%d)", k, fkmax_);
+    const int total = offsets[k];
+    if (total > N_) Log::Fatal("TestFrontierHist: %d rows over the subsets (at most %d)", total, N_);
+    K_ = 1;
+    DeviceSetGradients(g, h, 1);
+    TreeParams* tp = pin_tp_.Get(1);
+    std::memset(tp, 0, sizeof(TreeParams));
+    tp->root_buf = -1;
+    tp->root_count = tp->root_gcount = N_;
+    tp->spec_alpha = 1.f;
+    HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
+    float mg = 0.f, mh = 0.f;
+    for (int i = 0; i < N_; ++i) {
+      mg = std::max(mg, std::fabs(g[i]));
+      mh = std::max(mh, std::fabs(h[i]));
+    }
+    unsigned* hm = pin_max_.Get(2);
+    std::memcpy(&hm[0], &mg, 4);
+    std::memcpy(&hm[1], &mh, 4);
+    HIP_CHECK(hipMemcpyAsync(ghmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
+    if (config_->use_quantized_grad) QuantizeGradients(0);
+    idx_[3].Upload(rows, total, stream_);
+    FState st;
+    std::memset(&st, 0, sizeof(st));
+    st.round = 1;
+    st.k = k;
+    st.num_leaves = 1;
+    std::vector<FExp> ex(k);
+    for (int e = 0; e < k; ++e) {
+      std::memset(&ex[e], 0, sizeof(FExp));
+      ex[e].h_buf = 3;
+      ex[e].h_start = offsets[e];
+      ex[e].h_count = offsets[e + 1] - offsets[e];
+      ex[e].forced = -1;
+    }
+    HIP_CHECK(hipMemcpyAsync(fst_, &st, sizeof(FState), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(fexps_, ex.data(), sizeof(FExp) * k, hipMemcpyHostToDevice, stream_));
+    facc_.Zero(stream_);
+    const FArgs fa = MakeFArgs();
+    LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+    const int pw = fa.quant && fa.qpack ? 1 : 2;
+    std::vector<unsigned long long> acc(static_cast<size_t>(k) * pw * TB_);
+    HIP_CHECK(hipMemcpyAsync(acc.data(), facc_.get(), acc.size() * 8, hipMemcpyDeviceToHost, stream_));
+    if (fa.quant && levels != nullptr) HIP_CHECK(hipMemcpyAsync(levels, ghq_.get(), sizeof(uint16_t) * N_, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    facc_.Zero(stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    // the kernel's global scale (frontier_kernels.hip GlobalScaleExp)
+    auto scale_exp = [&](float m) {
+      if (!(m > 0.f)) return 0;
+      int e;
+      (void)std::frexp(4611686018427387904.0 / (static_cast<double>(N_) * m), &e);
+      return e - 1;
+    };
+    const double ig = fa.quant ? 1.0 : std::ldexp(1.0, -scale_exp(mg)), ih = fa.quant ? 1.0 : std::ldexp(1.0, -scale_exp(mh));
+    for (int e = 0; e < k; ++e) {
+      for (int b = 0; b < TB_; ++b) {
+        const size_t o = (static_cast<size_t>(e) * TB_ + b) * pw;
+        long long qg, qh;
+        if (pw == 1) {
+          const unsigned long long hs = acc[o] & 0xFFFFFFFFull;
+          qg = static_cast<long long>(acc[o] - hs) >> 32;
+          qh = static_cast<long long>(hs);
+        } else {
+          qg = static_cast<long long>(acc[o]);
+          qh = static_cast<long long>(acc[o + 1]);
+        }
+        out[(static_cast<size_t>(e) * TB_ + b) * 2] = static_cast<double>(qg) * ig;
+        out[(static_cast<size_t>(e) * TB_ + b) * 2 + 1] = static_cast<double>(qh) * ih;
+      }
+    }
+  }
+
+  // k_f_partition of k parents at once (row subsets, split by inner feature feats[e] at
+  // threshold bin thr[e] / the categorical bins of catbits[e]): out_rows = the device's
+  // children lists (lefts in order, then rights), out_left = left counts; exp_rows / exp_left =
+  // the host learner's partition (SerialTreeLearner::Split's predicate, stable).
+  void TestFrontierPartition(const int* rows, const int* offsets, int k, const int* feats, const int* thr,
+                             const int* dleft, const uint32_t* catbits, int* out_rows, int* out_left, int* exp_rows,
+                             int* exp_left) {
+    if (!frontier_) Log::Fatal("TestFrontierPartition: the frontier engine is not enabled for this configuration");
+    if (k < 1 || k > fkmax_ || 3 * k > fC_) Log::Fatal("TestFrontierPartition: %d parents (1..%d)", k, fkmax_);
+    const int total = offsets[k];
+    if (total > N_) Log::Fatal("TestFrontierPartition: %d rows over the subsets (at most %d)", total, N_);
+    FState st;
+    HIP_CHECK(hipMemcpyAsync(&st, fst_, sizeof(FState), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    idx_[0].Upload(rows, total, stream_);
+    std::vector<FExp> ex(k);
+    std::vector<uint32_t> bits(static_cast<size_t>(fkmax_) * kMaxCatWords, 0u);
+    int tiles = 0;
+    for (int e = 0; e < k; ++e) {
+      const int f = feats[e];
+      if (f < 0 || f >= F_) Log::Fatal("TestFrontierPartition: feature %d", f);
+      const FeatureInfo& fi = data_->feature(f);
+      FExp& x = ex[e];
+      std::memset(&x, 0, sizeof(FExp));
+      x.parent = e;
+      x.left = k + 2 * e;
+      x.count = offsets[e + 1] - offsets[e];
+      x.start = offsets[e];
+      x.src_buf = 0;
+      x.dst_buf = 1;
+      x.ntiles = std::max(1, DivUp(x.count, fpart_tile_));
+      x.tile0 = tiles;
+      tiles += x.ntiles;
+      x.group = fi.group;
+      x.offset = fi.offset;
+      x.num_bin = fi.num_bin;
+      x.mfb = static_cast<int>(fi.mfb);
+      x.default_bin = static_cast<int>(fi.default_bin);
+      x.missing = static_cast<int>(fi.missing);
+      x.thr = thr[e];
+      x.default_left = dleft[e];
+      x.is_cat = fi.bin_type == BinType::Categorical ? 1 : 0;
+      x.forced = -1;
+      x.feature = f;
+      for (int w = 0; w < kMaxCatWords; ++w) bits[static_cast<size_t>(e) * kMaxCatWords + w] = catbits[static_cast<size_t>(e) * kMaxCatWords + w];
+      // host oracle: the serial learner's predicate, stable
+      std::vector<int> l, r;
+      const uint32_t nan_bin = static_cast<uint32_t>(fi.num_bin - 1);
+      for (int i = 0; i < x.count; ++i) {
+        const int row = rows[x.start + i];
+        const uint32_t b = data_->FeatureBin(row, f);
+        bool go;
+        if (x.is_cat) {
+          go = b < 32u * kMaxCatWords && ((catbits[static_cast<size_t>(e) * kMaxCatWords + (b >> 5)] >> (b & 31u)) & 1u);
+        } else if ((fi.missing == MissingType::Zero && b == fi.default_bin) || (fi.missing == MissingType::NaN && b == nan_bin)) {
+          go = dleft[e] != 0;
+        } else {
+          go = b <= static_cast<uint32_t>(thr[e]);
+        }
+        (go ? l : r).push_back(row);
+      }
+      exp_left[e] = static_cast<int>(l.size());
+      std::copy(l.begin(), l.end(), exp_rows + x.start);
+      std::copy(r.begin(), r.end(), exp_rows + x.start + l.size());
+    }
+    if (tiles > ftile_cap_) Log::Fatal("TestFrontierPartition: %d tiles (capacity %d)", tiles, ftile_cap_);
+    st.round = 1;
+    st.k = k;
+    st.total_tiles = tiles;
+    st.done = 0;
+    st.epoch = st.epoch + 1u;
+    HIP_CHECK(hipMemcpyAsync(fst_, &st, sizeof(FState), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(fexps_, ex.data(), sizeof(FExp) * k, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(fbits_, bits.data(), sizeof(uint32_t) * bits.size(), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemsetAsync(fbest_, 0, sizeof(SplitInfo) * k, stream_));
+    const FArgs fa = MakeFArgs();
+    LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    HIP_CHECK(hipMemcpyAsync(out_rows, idx_[1].get(), sizeof(int) * total, hipMemcpyDeviceToHost, stream_));
+    std::vector<FNode> nodes(3 * static_cast<size_t>(k));
+    HIP_CHECK(hipMemcpyAsync(nodes.data(), fnodes_, sizeof(FNode) * nodes.size(), hipMemcpyDeviceToHost, stream_));
+    unsigned hbar[4];
+    HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), sizeof(hbar), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (hbar[2] != 0u) Log::Fatal("TestFrontierPartition: a look-back wait timed out");
+    for (int e = 0; e < k; ++e) out_left[e] = nodes[k + 2 * e].count;
+  }
+
   void TestHistogram(const float* g, const float* h, const int* rows, int n, double* out) {
     K_ = 1;
     gh_.Resize(static_cast<size_t>(N_));
@@ -2328,8 +2500,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void BuildTiles() {
-    static const int env_kb = [] {
-      const char* e = std::getenv("LGAP_HIST_LDS_KB");  // A/B knob: LDS tile budget
+    const int env_kb = [] {
+      const char* e = std::getenv("LGAP_HIST_LDS_KB");  // A/B / test knob: LDS tile budget
       return e ? std::max(16, std::min(150, std::atoi(e))) : 0;
     }();
     big_tiles_ = false;
@@ -3177,6 +3349,23 @@ class DeviceHistogramBackend final : public HistogramBackend {
 std::unique_ptr<HistogramBackend> CreateHistogramBackend(const Config* config, const Dataset* data) {
   if (DeviceCount() <= 0) Log::Fatal("HIP histogram backend: no AMD GPU visible to HIP");
   return std::make_unique<DeviceHistogramBackend>(config, data);
+}
+
+void TestFrontierHist(const Dataset* data, const Config& config, const float* grad, const float* hess, const int* rows,
+                      const int* offsets, int k, double* out, uint16_t* levels) {
+  if (DeviceCount() <= 0) Log::Fatal("TestFrontierHist: no AMD GPU visible to HIP");
+  DeviceTreeLearner learner(&config, DevParallel::kSerial);
+  learner.Init(data, false);
+  learner.TestFrontierHist(grad, hess, rows, offsets, k, out, levels);
+}
+
+void TestFrontierPartition(const Dataset* data, const Config& config, const int* rows, const int* offsets, int k,
+                           const int* feats, const int* thr, const int* dleft, const uint32_t* catbits, int* out_rows,
+                           int* out_left, int* exp_rows, int* exp_left) {
+  if (DeviceCount() <= 0) Log::Fatal("TestFrontierPartition: no AMD GPU visible to HIP");
+  DeviceTreeLearner learner(&config, DevParallel::kSerial);
+  learner.Init(data, false);
+  learner.TestFrontierPartition(rows, offsets, k, feats, thr, dleft, catbits, out_rows, out_left, exp_rows, exp_left);
 }
 
 void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, const int* rows, int num_rows,

@@ -215,6 +215,7 @@ struct FArgs {
   // build); 0 / kFrontierKmax: the whole round
   int e_lo, e_hi;
   int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
+  int part_nt;      // A/B knob (LGAP_PART_NT=1): the partition's row-index scatter with non-temporal stores
   SplitParams sp;
 };
 

@@ -998,8 +998,9 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
       if (valid) {
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
-        if (left) out[lbase + rl] = rows[j][i];
-        else out[x.count - 1 - (rbase + (rv - rl))] = rows[j][i];
+        int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
+        if (a.part_nt) __builtin_nontemporal_store(rows[j][i], dst);
+        else *dst = rows[j][i];
       }
       lbase += tl;
       rbase += tv - tl;
@@ -1057,8 +1058,9 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
       if (valid) {
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
-        if (left) out[lbase + rl] = rr[i];
-        else out[x.count - 1 - (rbase + (rv - rl))] = rr[i];
+        int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
+        if (a.part_nt) __builtin_nontemporal_store(rr[i], dst);
+        else *dst = rr[i];
       }
       lbase += tl;
       rbase += tv - tl;
