@@ -1182,7 +1182,7 @@ class DeviceTreeLearner : public TreeLearner {
   // the computed-node image of the select must fit its LDS. LGAP_FRONTIER=0 forces the
   // sequential chain (A/B runs).
   bool FrontierEligible() const {
-    if (!FrontierSerial() && !FrontierDP()) return false;
+    if (!FrontierSerial() && !FrontierDP() && !FrontierVoting() && !FrontierFeature()) return false;
     if (use_bynode_ || config_->extra_trees) return false;
     return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, CegbRaw());
   }
@@ -1211,6 +1211,31 @@ class DeviceTreeLearner : public TreeLearner {
     if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
     return mode_ == DevParallel::kData && data_parallel_ && owner_scan_ && distributed_ && !voting_ &&
            (CommExists() || HostStagedDP());
+  }
+  // Voting-parallel frontier (PV-Tree per round): the local pass of every expansion's children,
+  // one all-gather of the round's top-k vote records, the election, one exact integer
+  // all-reduce of only the elected features' rows, and the global pass over them; every rank
+  // then selects redundantly, as the data-parallel frontier does. LGAP_FRONTIER_VOTING=0 or an
+  // explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain (its in-kernel xGMI exchange).
+  // Reference: voting_parallel_tree_learner.cpp:243-399.
+  bool FrontierVoting() const {
+    const char* e = std::getenv("LGAP_FRONTIER_VOTING");
+    if (e != nullptr && e[0] == '0') return false;
+    const char* t = std::getenv("LGAP_DP_TRANSPORT");
+    if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
+    return mode_ == DevParallel::kVoting && voting_ && distributed_ && (CommExists() || HostStagedDP());
+  }
+  // Feature-parallel frontier: every rank holds all rows and grows the same partition and
+  // histograms; the scans cover this rank's features (the groups it owns), each child's best is
+  // all-gathered and the best over ranks is the child's candidate. LGAP_FRONTIER_FEATURE=0 or
+  // an explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain.
+  // Reference: feature_parallel_tree_learner.cpp:23-80.
+  bool FrontierFeature() const {
+    const char* e = std::getenv("LGAP_FRONTIER_FEATURE");
+    if (e != nullptr && e[0] == '0') return false;
+    const char* t = std::getenv("LGAP_DP_TRANSPORT");
+    if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
+    return mode_ == DevParallel::kFeature && owner_scan_ && !distributed_ && (CommExists() || HostStagedDP());
   }
   int FrontierKmax() const {
     int k = kFrontierKmax;
@@ -1366,6 +1391,24 @@ class DeviceTreeLearner : public TreeLearner {
     }
     facc_.Resize(K * 2 * static_cast<size_t>(TB_));
     facc_.Zero(stream_);  // the scan re-zeroes what it consumes: zero between rounds from here on
+    ffeature_ = FrontierFeature();
+    if (ffeature_) {
+      std::vector<uint8_t> own(F_, 0);
+      for (int f : h_own_feat_) {
+        if (f >= 0) own[f] = 1;
+      }
+      ffowned_.Upload(own, stream_);
+      ffpb_.Resize(static_cast<size_t>(P_) * 2 * K);
+    }
+    fvoting_ = FrontierVoting();
+    if (fvoting_) {
+      flsum_loc_.Resize(C);
+      fltot_.Resize(2 * K);
+      fltot_.Zero(stream_);  // k_f_vote re-zeroes what the round consumed
+      fvrec_.Resize(static_cast<size_t>(P_) * 2 * K * topk_);
+      fvelect_.Resize(2 * K * static_cast<size_t>(topk_ + 1));
+      fvrows_.Resize(2 * K * static_cast<size_t>(topk_) * 2 * max_bin_);
+    }
     fpart_tile_ = kPartThreads * part_iters_;
     ftile_cap_ = DivUp(N_, fpart_tile_) + fkmax_ + 1;
     ftile_pub_.Resize(ftile_cap_);
@@ -1533,6 +1576,26 @@ class DeviceTreeLearner : public TreeLearner {
       a.qpack = fglobal_rows_ * gl < 2147483647.0 && fglobal_rows_ * hl < 4294967295.0 ? 1 : 0;
     }
     a.sp = MakeArgs().sp;
+    if (ffeature_) {
+      a.fowned = ffowned_.get();
+      a.fpb = ffpb_.get();
+      a.vote_P = P_;
+      a.vote_rank = rank_;
+    }
+    if (fvoting_) {
+      a.voting = 1;
+      a.vote_k = topk_;
+      a.vote_P = P_;
+      a.vote_rank = rank_;
+      a.sp_local = a.sp;
+      a.sp_local.min_data_in_leaf = config_->min_data_in_leaf / P_;  // integer division (reference :61-63)
+      a.sp_local.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf / P_;
+      a.lsum_loc = flsum_loc_.get();
+      a.ltot = fltot_.get();
+      a.vrec = fvrec_.get();
+      a.velect = fvelect_.get();
+      a.vrows = reinterpret_cast<unsigned long long*>(fvrows_.get());
+    }
     return a;
   }
 
@@ -1546,7 +1609,7 @@ class DeviceTreeLearner : public TreeLearner {
   // Data-parallel frontier: sum the round's accumulators of the first `kb` expansions over
   // the ranks (the rest are zero on every rank).
   void FrontierExchange(int kb) {
-    if (!distributed_) return;
+    if (!distributed_ || fvoting_) return;
     AllreduceSumU64(reinterpret_cast<unsigned long long*>(facc_.get()),
                     static_cast<size_t>(std::max(1, std::min(kb, fkmax_))) * AccWordsPerBin() * TB_, stream_);
   }
@@ -1579,10 +1642,39 @@ class DeviceTreeLearner : public TreeLearner {
 
   // One round: partition -> histograms -> [all-reduce] -> scans -> select. `kb` bounds the
   // round's expansion count (round r >= 1 of a tree has at most 2^(r-1) open nodes to expand).
+  // Voting: after the round's local-pass scan, the vote all-gather, the election, the exact
+  // all-reduce of the elected rows (kb expansions' worth), the global pass.
+  void FrontierVoteExchange(const FArgs& fa, int kb) {
+    LaunchFrontierVote(fa, stream_);
+    AllGatherInPlace(fvrec_.get(), sizeof(VoteRec) * 2 * static_cast<size_t>(fkmax_) * topk_, stream_);
+    LaunchFrontierElect(fa, stream_);
+    const size_t rows = 2 * static_cast<size_t>(std::max(1, std::min(kb, fkmax_))) * topk_ * 2 * max_bin_;
+    AllreduceSumU64(reinterpret_cast<unsigned long long*>(fvrows_.get()), rows, stream_);
+    LaunchFrontierVoteScan(fa, FrontierVoteScanLds(), stream_);
+  }
+  size_t FrontierVoteScanLds() const {
+    return static_cast<size_t>(max_bin_) * 2 * sizeof(double) + static_cast<size_t>(cat_p2_) * (sizeof(int) + sizeof(double));
+  }
+
+  // Feature parallel: this rank's per-child bests all-gathered, the best over ranks kept.
+  void FrontierFeatureExchange(const FArgs& fa) {
+    LaunchFrontierPairBest(fa, stream_);
+    AllGatherInPlace(ffpb_.get(), sizeof(FPairBest) * 2 * static_cast<size_t>(fkmax_), stream_);
+    LaunchFrontierPairMerge(fa, stream_);
+  }
+
   void EnqueueFrontierRound(const FArgs& fa, int kb) {
     LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
     if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
-    if (!FrontierPipelined(kb)) {
+    if (ffeature_) {
+      LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+      LaunchFrontierScan(fa, fscan_lds_, stream_);
+      FrontierFeatureExchange(fa);
+    } else if (fvoting_) {
+      LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+      LaunchFrontierScan(fa, fscan_lds_, stream_);
+      FrontierVoteExchange(fa, kb);
+    } else if (!FrontierPipelined(kb)) {
       LaunchFrontierHist(fa, FrontierHistLds(), stream_);
       FrontierExchange(kb);
       LaunchFrontierScan(fa, fscan_lds_, stream_);
@@ -1635,6 +1727,8 @@ class DeviceTreeLearner : public TreeLearner {
       if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
       FrontierExchange(1);
       LaunchFrontierScan(fa, fscan_lds_, stream_);
+      if (fvoting_) FrontierVoteExchange(fa, 1);
+      if (ffeature_) FrontierFeatureExchange(fa);
       LaunchFrontierSelect(fa, stream_);
     }
     for (int r = 0; r < rounds; ++r) {
@@ -1675,7 +1769,7 @@ class DeviceTreeLearner : public TreeLearner {
   // each until it is. Results: the committed splits, the final leaf ranges, the root output.
   // a stream carrying RCCL collectives: a lost peer must not hang the process
   void FrontierSync() {
-    if (distributed_ && !HostStagedDP()) {
+    if ((distributed_ || ffeature_) && !HostStagedDP()) {
       WatchedStreamSync(stream_, CommTimeoutSeconds(config_->time_out), "frontier tree growth (RCCL all-reduce)");
     } else {
       HIP_CHECK(hipStreamSynchronize(stream_));
@@ -1685,9 +1779,11 @@ class DeviceTreeLearner : public TreeLearner {
   void FrontierGrow(int* num_splits, int* num_leaves, SplitRec* hr, LeafRange* hrange, double* hlo) {
     // collectives: RCCL calls replay from the graph only on request (LGAP_DP_GRAPH=1, as in the
     // sequential chain); the host-staged rehearsal transport synchronises inside its exchange
-    const bool use_graph = config_->device_use_graph && (!distributed_ || (DPGraphEnabled() && !HostStagedDP()));
-    if (use_graph && distributed_ && !fgraphs_.empty() && graph_comm_ != ActiveComm()) InvalidateGraph();
-    if (use_graph && distributed_) graph_comm_ = ActiveComm();
+    // (feature parallel exchanges candidates over collectives too, without distributed rows)
+    const bool comm = distributed_ || ffeature_;
+    const bool use_graph = config_->device_use_graph && (!comm || (DPGraphEnabled() && !HostStagedDP()));
+    if (use_graph && comm && !fgraphs_.empty() && graph_comm_ != ActiveComm()) InvalidateGraph();
+    if (use_graph && comm) graph_comm_ = ActiveComm();
     // per-round caps need the eager enqueue (the all-reduce sizes change from tree to tree)
     fcaps_on_ = distributed_ && !use_graph && std::getenv("LGAP_FRONTIER_KCAP") == nullptr;
     if (distributed_) {
@@ -3070,6 +3166,17 @@ class DeviceTreeLearner : public TreeLearner {
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
+  // feature-parallel frontier (FrontierFeature)
+  bool ffeature_ = false;
+  DevBuf<uint8_t> ffowned_;
+  DevBuf<FPairBest> ffpb_;
+  // voting-parallel frontier (FrontierVoting)
+  bool fvoting_ = false;
+  DevBuf<double2> flsum_loc_;
+  DevBuf<unsigned long long> fltot_;
+  DevBuf<VoteRec> fvrec_;
+  DevBuf<int> fvelect_;
+  DevBuf<unsigned long long> fvrows_;
   FState* fst_ = nullptr;
   FNode* fnodes_ = nullptr;
   FExp* fexps_ = nullptr;

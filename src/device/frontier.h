@@ -81,6 +81,12 @@ struct FNode {
   int fidx;               // index of its forced split (FForced), -1: none
 };
 
+// Feature parallel: one rank's best candidate of one child (SplitInfo::BetterThan order).
+struct FPairBest {
+  SplitKey key;
+  SplitInfo info;
+};
+
 // One forced split (forcedsplits_filename) in the host learner's application order
 // (learner/forced_splits.h FlattenForced): inner feature, threshold bin, children indices.
 struct FForced {
@@ -214,6 +220,23 @@ struct FArgs {
   // the first half's all-reduce runs on the comm stream while the second half's histograms
   // build); 0 / kFrontierKmax: the whole round
   int e_lo, e_hi;
+  // Voting parallel (PV-Tree) on the frontier (k_f_scan is then the LOCAL pass): local leaf
+  // statistics and min_data / min_hessian divided by the rank count, local top-k votes per
+  // child, the elected features' fixed-point rows summed over ranks, a GLOBAL pass over them.
+  // Reference: voting_parallel_tree_learner.cpp:243-399.
+  int voting;
+  int vote_k, vote_P, vote_rank;
+  SplitParams sp_local;
+  double2* lsum_loc;          // [C] local (sum g, sum h) of every computed node
+  unsigned long long* ltot;   // [kmax][2] the round's smaller children's local totals (global fixed-point scale)
+  VoteRec* vrec;              // [P][kmax][2][K] local top-k records, all-gathered
+  int* velect;                // [kmax][2][K + 1] elected count, elected features ascending
+  unsigned long long* vrows;  // [kmax][2][K][2 max_bin] elected features' local fixed-point rows, summed in place
+  // Feature parallel on the frontier: every rank holds all rows and grows the same partition;
+  // k_f_scan scans the features this rank owns (fowned), each child's best is all-gathered and
+  // the best over ranks becomes the child's candidate. Reference: feature_parallel_tree_learner.cpp:23-80.
+  const uint8_t* fowned;  // [F] 1: this rank scans the feature (null: every feature)
+  struct FPairBest* fpb;  // [P][kmax][2] per-child best of each rank, all-gathered
   int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
   int part_nt;      // A/B knob (LGAP_PART_NT=1): the partition's row-index scatter with non-temporal stores
   SplitParams sp;
@@ -246,6 +269,16 @@ void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
 void LaunchFrontierLazyCounts(const FArgs& a, hipStream_t s);
 void LaunchFrontierLazyMark(const FArgs& a, hipStream_t s);
 void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s);
+// voting parallel: local top-k per child (after the local-pass k_f_scan), election and
+// packing of the elected features' local rows (after the vote all-gather), global pass over
+// the summed rows (after their all-reduce)
+void LaunchFrontierVote(const FArgs& a, hipStream_t s);
+void LaunchFrontierElect(const FArgs& a, hipStream_t s);
+void LaunchFrontierVoteScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
+// feature parallel: this rank's per-child best -> fpb[rank] (before the all-gather); the best
+// over ranks -> the candidate table (after it)
+void LaunchFrontierPairBest(const FArgs& a, hipStream_t s);
+void LaunchFrontierPairMerge(const FArgs& a, hipStream_t s);
 // resident 256-thread partition blocks per CU (the look-back needs every block resident)
 int FrontierPartitionBlocksPerCU(int iters);
 // one-time kernel attributes (dynamic LDS above 64 KiB)

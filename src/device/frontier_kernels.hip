@@ -288,6 +288,30 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
   const double dsg = ldexp(1.0, EG), dsh = ldexp(1.0, EH);
+  if (a.ltot != nullptr && blockIdx.y == 0) {
+    // voting: the smaller child's LOCAL (sum g, sum h) at the global fixed-point scale (integer
+    // levels when quantized), exact and order free; the first tile's blocks count each row once
+    __shared__ unsigned long long s_tot[2];
+    if (t < 2) s_tot[t] = 0ull;
+    __syncthreads();
+    long long sg = 0, sh = 0;
+    for (int p = rb + t; p < re; p += blockDim.x) {
+      const int row = FRowAt(a, buf, start + p);
+      if (a.quant) {
+        const uint32_t qv = a.ghq[static_cast<size_t>(a.tp->cls) * a.N + row];
+        sg += static_cast<int8_t>(qv >> 8);
+        sh += static_cast<long long>(qv & 0xFFu);
+      } else {
+        const float2 v = a.gh[static_cast<size_t>(a.tp->cls) * a.N + row];
+        sg += __double2ll_rn(static_cast<double>(v.x) * dsg);
+        sh += __double2ll_rn(static_cast<double>(v.y) * dsh);
+      }
+    }
+    if (sg) atomicAdd(&s_tot[0], static_cast<unsigned long long>(sg));
+    if (sh) atomicAdd(&s_tot[1], static_cast<unsigned long long>(sh));
+    __syncthreads();
+    if (t < 2 && s_tot[t]) atomicAdd(&a.ltot[2 * e + t], s_tot[t]);
+  }
   if (tile.direct) {
     // groups too wide for LDS: each row's fixed-point value straight into the accumulator
     int* gst = reinterpret_cast<int*>(lds_raw);
@@ -470,10 +494,25 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       pre_fidx = a.num_forced > 0 ? a.nodes[my].fidx : -1;
       pre_out = a.lout[my];
       pre_bounds = a.bounds[my];
+      if (a.voting) {
+        // voting's LOCAL pass: this rank's rows and sums (the smaller child's from the round's
+        // exact local totals, the larger's as the parent's local sums minus them)
+        pre_n = a.nodes[my].count;
+        const double2 sm = make_double2(static_cast<double>(static_cast<long long>(a.ltot[2 * e])) * inv_g,
+                                        static_cast<double>(static_cast<long long>(a.ltot[2 * e + 1])) * inv_h);
+        if (my == cs) {
+          pre_sum = sm;
+        } else {
+          const double2 ps = a.lsum_loc[p];
+          pre_sum = make_double2(ps.x - sm.x, ps.y - sm.y);
+        }
+        if (f == 0) a.lsum_loc[my] = pre_sum;
+      }
     }
     if (t == 0) {
-      s_skip = !a.used_bytree[f];
-      s_splp = p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1;
+      // (feature parallel: only the features this rank owns)
+      s_skip = !a.used_bytree[f] || (a.fowned != nullptr && !a.fowned[f]);
+      s_splp = p >= 0 && !a.voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
     for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
       const unsigned long long x0 = acc[pw * kk], x1 = qpack ? 0ull : acc[2 * kk + 1];
@@ -536,14 +575,15 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       const double sg = __shfl(pre_sum.x, 0, kWave), sh = __shfl(pre_sum.y, 0, kWave);
       const int n = __shfl(pre_n, 0, kWave);
       const int depth = __shfl(pre_depth, 0, kWave);
+      const SplitParams& spp = a.voting ? a.sp_local : a.sp;
       if (!skip_both) {
         const double* H = w ? hl_full : hs_full;
         double po;
         if (p < 0) {
-          SplitParams p0 = a.sp;
+          SplitParams p0 = spp;
           p0.path_smooth = 0.0;
           po = LeafOutputRaw(sg, sh, p0, n, 0.0);
-          if (f == 0 && lane == 0) a.lout[0] = po;
+          if (f == 0 && lane == 0 && !a.voting) a.lout[0] = po;  // (voting: the global root output, k_f_elect)
         } else {
           po = __shfl(pre_out, 0, kWave);
         }
@@ -552,7 +592,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         bounds.max = __shfl(pre_bounds.max, 0, kWave);
         bool spl;
         if (fi.bin_type == 0) {
-          spl = ScanNumericalWave(a.sp, fi, H, sg, sh, n, po, bounds, 0, out);
+          spl = ScanNumericalWave(spp, fi, H, sg, sh, n, po, bounds, 0, out);
         } else {
           FeatureScanMeta m;
           m.num_bin = fi.num_bin;
@@ -563,7 +603,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
           m.penalty = fi.penalty;
           m.rand_threshold = 0;
           if (lane == 0) out->Reset();
-          spl = ScanCategoricalWave(a.sp, m, H, sg, sh, n, po, bounds, a.cat_p2, order + w * a.cat_p2,
+          spl = ScanCategoricalWave(spp, m, H, sg, sh, n, po, bounds, a.cat_p2, order + w * a.cat_p2,
                                     ckey + w * a.cat_p2, out);
         }
         if (lane == 0) {
@@ -576,17 +616,18 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
             // cost-effective gradient boosting, split penalty (host CegbPenalty::DeltaGain:
             // subtracted before the monotone penalty multiplies the gain). With coupled
             // penalties the candidate stays raw: the select applies every penalty (CegbAdjust)
-            if (!a.cegb_raw) {
+            // (voting's local pass ranks raw gains: penalties belong to the global pass)
+            if (!a.cegb_raw && !a.voting) {
               if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
             }
-            if (a.ic && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
+            if (a.ic && !a.voting && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
           }
         }
       } else if (lane == 0) {
         // feature not tried: the children inherit the parent's flag
         a.spl[static_cast<size_t>(my) * F + f] = static_cast<uint8_t>(s_splp);
-        if (p < 0 && f == 0) {
+        if (p < 0 && f == 0 && !a.voting) {
           SplitParams p0 = a.sp;
           p0.path_smooth = 0.0;
           a.lout[0] = LeafOutputRaw(sg, sh, p0, n, 0.0);
@@ -1848,6 +1889,364 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Voting parallel (PV-Tree) on the frontier: after the LOCAL pass of k_f_scan every rank
+//  k_f_vote        ranks each child's local candidates (gain desc, feature asc) and writes its
+//                  top-k (gain, feature, local rows) records; the candidate table is cleared
+//  (all-gather of the records)
+//  k_f_elect       GlobalVoting per child (the best record of each feature weighted by its local
+//                  rows over the mean rows per rank, top-k of those), then this rank's local
+//                  fixed-point rows of the elected features
+//  (sum all-reduce of the rows: exact integers, identical on every rank)
+//  k_f_vote_scan   the GLOBAL pass: each elected feature scanned from the summed rows with the
+//                  global leaf statistics and penalties, into the candidate table the select reads
+// Reference: voting_parallel_tree_learner.cpp:243-399 (FindBestSplits, GlobalVoting :150-181).
+constexpr int kVoteThreads = 256;
+
+__device__ __forceinline__ bool FVoteBetter(double ga, int fa, double gb, int fb) {
+  return ga != gb ? ga > gb : fa < fb;
+}
+
+// the child cid of candidate pair q (2 e + sel) of the current round, -1: none / skipped
+__device__ __forceinline__ int FPairChild(const FArgs& a, int k, int q) {
+  const int e = q >> 1;
+  if (e >= k) return -1;
+  const FExp& x = a.exps[e];
+  if (x.skip) return -1;
+  return (q & 1) ? x.larger : x.smaller;
+}
+
+__global__ __launch_bounds__(kVoteThreads) void k_f_vote(FArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int k = stp->k, q = blockIdx.x, F = a.F, K = a.vote_k, t = threadIdx.x;
+  if ((q >> 1) >= k) return;
+  const int c = FPairChild(a, k, q);
+  double* s_gain = reinterpret_cast<double*>(smem);
+  int* s_cnt = reinterpret_cast<int*>(s_gain + F);
+  __shared__ int s_n[kVoteThreads / 64];
+  int nv = 0;
+  for (int f = t; f < F; f += blockDim.x) {
+    const size_t o = static_cast<size_t>(q) * F + f;
+    const SplitKey kk = a.ckey[o];
+    const bool valid = c >= 0 && kk.feature >= 0;
+    s_gain[f] = valid ? kk.gain : kMinScore;
+    s_cnt[f] = valid ? a.cinfo[o].left_count + a.cinfo[o].right_count : -1;
+    nv += valid ? 1 : 0;
+  }
+  const int nvalid = BlockSumInt(nv, s_n);  // (barrier inside: the LDS arrays are complete)
+  VoteRec* out = a.vrec + (static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q) * K;
+  for (int f = t; f < F; f += blockDim.x) {
+    if (s_cnt[f] < 0) continue;
+    const double g = s_gain[f];
+    int rank = 0;
+    for (int j = 0; j < F && rank < K; ++j) rank += (s_cnt[j] >= 0 && FVoteBetter(s_gain[j], j, g, f)) ? 1 : 0;
+    if (rank < K) {
+      VoteRec r;
+      r.gain = g;
+      r.feature = f;
+      r.count = s_cnt[f];
+      out[rank] = r;
+    }
+  }
+  for (int i = nvalid + t; i < K; i += blockDim.x) {
+    VoteRec r;
+    r.gain = kMinScore;
+    r.feature = -1;
+    r.count = 0;
+    out[i] = r;
+  }
+  // the local candidates are consumed: the global pass fills the elected features' entries
+  for (int f = t; f < F; f += blockDim.x) {
+    SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+    kk.feature = -1;
+    kk.gain = kMinScore;
+  }
+  if (t == 0 && (q & 1) == 0) {
+    a.ltot[2 * (q >> 1)] = 0ull;  // (the round's local totals are consumed: zero for the next round)
+    a.ltot[2 * (q >> 1) + 1] = 0ull;
+  }
+}
+
+// GlobalVoting of one child over the gathered records (identical on every rank): s_list[0, n)
+// the elected features ascending; returns n
+__device__ int FElect(const FArgs& a, int q, int c, double* s_w, int* s_f, int* s_flag, int* s_tmp, int* s_list) {
+  const int K = a.vote_k, P = a.vote_P, R = P * K, t = threadIdx.x;
+  // mean child rows per rank in float, as the reference's mean_num_data
+  const float mean = static_cast<float>(a.nodes[c].gcount) / static_cast<float>(P);
+  for (int i = t; i < R; i += blockDim.x) {
+    const int r = i / K, j = i - r * K;
+    const VoteRec v = a.vrec[(static_cast<size_t>(r) * 2 * a.kmax + q) * K + j];
+    const double w = v.gain * v.count / static_cast<double>(mean);
+    const bool valid = v.feature >= 0 && w > kMinScore;
+    s_w[i] = w;
+    s_f[i] = valid ? v.feature : -1;
+  }
+  __syncthreads();
+  // the best record of each feature (first in gather order on equal weighted gain)
+  for (int i = t; i < R; i += blockDim.x) {
+    int best = s_f[i] >= 0 ? 1 : 0;
+    for (int j = 0; j < R && best; ++j) {
+      if (j != i && s_f[j] == s_f[i] && (s_w[j] > s_w[i] || (s_w[j] == s_w[i] && j < i))) best = 0;
+    }
+    s_flag[i] = best;
+  }
+  __syncthreads();
+  int ne = 0;
+  for (int i = t; i < R; i += blockDim.x) {
+    int el = 0;
+    if (s_flag[i]) {
+      int rank = 0;
+      for (int j = 0; j < R && rank < K; ++j) rank += (s_flag[j] && FVoteBetter(s_w[j], s_f[j], s_w[i], s_f[i])) ? 1 : 0;
+      el = rank < K ? 1 : 0;
+    }
+    ne += el;
+    s_tmp[i] = el;
+  }
+  __syncthreads();
+  for (int i = t; i < R; i += blockDim.x) s_flag[i] = s_tmp[i];
+  const int n = BlockSumInt(ne, s_tmp + R);
+  for (int i = t; i < R; i += blockDim.x) {
+    if (!s_flag[i]) continue;
+    int pos = 0;
+    for (int j = 0; j < R; ++j) pos += (s_flag[j] && s_f[j] < s_f[i]) ? 1 : 0;
+    s_list[pos] = s_f[i];
+  }
+  __syncthreads();
+  return n;
+}
+
+__global__ __launch_bounds__(kVoteThreads) void k_f_elect(FArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int k = stp->k, q = blockIdx.x, K = a.vote_k, R = a.vote_P * K, t = threadIdx.x;
+  if ((q >> 1) >= k) return;
+  const int c = FPairChild(a, k, q);
+  int* el = a.velect + static_cast<size_t>(q) * (K + 1);
+  if (q == 0 && a.exps[0].parent < 0 && t == 0) {
+    // the root round: the root's GLOBAL output (the local pass computed local ones only)
+    const double2 sm = a.lsum[0];
+    SplitParams p0 = a.sp;
+    p0.path_smooth = 0.0;
+    a.lout[0] = LeafOutputRaw(sm.x, sm.y, p0, a.nodes[0].gcount, 0.0);
+  }
+  if (c < 0) {
+    if (t == 0) el[0] = 0;
+    return;
+  }
+  double* s_w = reinterpret_cast<double*>(smem);
+  int* s_f = reinterpret_cast<int*>(s_w + R);
+  int* s_flag = s_f + R;
+  int* s_tmp = s_flag + R;                     // R + kVoteThreads / 64
+  int* s_list = s_tmp + R + kVoteThreads / 64;  // [K]
+  const int n = FElect(a, q, c, s_w, s_f, s_flag, s_tmp, s_list);
+  if (t == 0) el[0] = n;
+  for (int j = t; j < n; j += blockDim.x) el[1 + j] = s_list[j];
+  // this rank's local rows of the elected features: the child's local fp64 histogram (its node
+  // slot) back at the fixed-point scale (the smaller child's slot holds exact integers)
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
+  double sg = ldexp(1.0, EG), sh = ldexp(1.0, EH);
+  if (a.quant) {
+    double gs, hs;
+    QuantScales(a, &gs, &hs);
+    sg = 1.0 / gs;
+    sh = 1.0 / hs;
+  }
+  const size_t row = 2 * static_cast<size_t>(a.max_bin);
+  const double* slot = a.slots + static_cast<size_t>(c) * 2 * a.TB;
+  for (int j = 0; j < n; ++j) {
+    const DevFeature fi = a.feat[s_list[j]];
+    unsigned long long* dst = a.vrows + (static_cast<size_t>(q) * K + j) * row;
+    const double* src = slot + 2 * static_cast<size_t>(fi.hist_offset);
+    for (int v = t; v < 2 * (fi.num_bin - 1); v += blockDim.x) {
+      dst[v] = static_cast<unsigned long long>(__double2ll_rn(src[v] * ((v & 1) ? sh : sg)));
+    }
+  }
+}
+
+// one wave per (pair, elected slot)
+__global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int K = a.vote_k, k = stp->k, F = a.F, lane = threadIdx.x;
+  const int q = blockIdx.x / K, j = blockIdx.x - q * K;
+  if ((q >> 1) >= k) return;
+  const int c = FPairChild(a, k, q);
+  if (c < 0) return;
+  const int* el = a.velect + static_cast<size_t>(q) * (K + 1);
+  if (j >= el[0]) return;
+  const int f = el[1 + j];
+  const DevFeature fi = a.feat[f];
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
+  double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
+  if (a.quant) QuantScales(a, &inv_g, &inv_h);
+  double* H = reinterpret_cast<double*>(smem);                                   // [2 max_bin]
+  int* order = reinterpret_cast<int*>(H + 2 * a.max_bin);                         // [cat_p2]
+  double* ckey = reinterpret_cast<double*>(order + a.cat_p2);                     // [cat_p2]
+  __shared__ __align__(8) unsigned char s_out_raw[sizeof(SplitInfo)];
+  SplitInfo* out = reinterpret_cast<SplitInfo*>(s_out_raw);
+  const unsigned long long* rows = a.vrows + (static_cast<size_t>(q) * K + j) * 2 * a.max_bin;
+  const double2 sums = a.lsum[c];
+  const int n = a.nodes[c].gcount;
+  double sgs = 0.0, shs = 0.0;
+  for (int v = lane; v < 2 * (fi.num_bin - 1); v += 64) {
+    const double x = static_cast<double>(static_cast<long long>(rows[v])) * ((v & 1) ? inv_h : inv_g);
+    const int kb = v >> 1;
+    const int b = kb < fi.mfb ? kb : kb + 1;
+    H[2 * b + (v & 1)] = x;
+    if (v & 1) shs += x;
+    else sgs += x;
+  }
+  sgs = WaveSum(sgs);
+  shs = WaveSum(shs);
+  if (lane == 0) {
+    H[2 * fi.mfb] = sums.x - sgs;
+    H[2 * fi.mfb + 1] = sums.y - shs;
+    out->Reset();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const FNode nd = a.nodes[c];
+  double po;
+  if (nd.parent < 0) {
+    SplitParams p0 = a.sp;
+    p0.path_smooth = 0.0;
+    po = LeafOutputRaw(sums.x, sums.y, p0, n, 0.0);
+  } else {
+    po = a.lout[c];
+  }
+  const LeafBounds bounds = a.bounds[c];
+  bool spl;
+  if (fi.bin_type == 0) {
+    spl = ScanNumericalWave(a.sp, fi, H, sums.x, sums.y, n, po, bounds, 0, out);
+  } else {
+    FeatureScanMeta m;
+    m.num_bin = fi.num_bin;
+    m.default_bin = static_cast<uint32_t>(fi.default_bin);
+    m.missing_type = fi.missing;
+    m.bin_type = fi.bin_type;
+    m.monotone = fi.monotone;
+    m.penalty = fi.penalty;
+    m.rand_threshold = 0;
+    spl = ScanCategoricalWave(a.sp, m, H, sums.x, sums.y, n, po, bounds, a.cat_p2, order, ckey, out);
+  }
+  if (lane == 0) {
+    if (!spl || (a.max_depth > 0 && nd.depth >= a.max_depth)) {
+      out->Reset();
+    } else {
+      out->feature = f;
+      if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, nd.depth);
+      if (a.ic && (a.ic[c] & a.ic_feat[f]) == 0ull) out->Reset();
+    }
+    SplitKey kk;
+    kk.feature = out->feature;
+    kk.gain = SafeGain(*out);
+    kk.threshold = out->threshold;
+    kk.group = fi.group;
+    kk.offset = fi.offset;
+    kk.num_bin = fi.num_bin;
+    kk.mfb = fi.mfb;
+    kk.default_bin = fi.default_bin;
+    kk.missing = fi.missing;
+    kk.default_left = out->default_left;
+    kk.is_cat = fi.bin_type != 0 ? 1 : 0;
+    kk.pad0 = 0;
+    kk.pos = f;
+    kk.pad2 = 0;
+    a.ckey[static_cast<size_t>(q) * F + f] = kk;
+  }
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int i = lane; i < kInfoWords; i += 64) {
+    reinterpret_cast<uint32_t*>(a.cinfo + static_cast<size_t>(q) * F + f)[i] = reinterpret_cast<const uint32_t*>(out)[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Feature parallel: one wave per child pair. k_f_pair_best: this rank's best over its owned
+// features' candidates; k_f_pair_merge (after the all-gather): the best over the ranks'
+// records replaces the pair's candidate row (gain desc, then feature asc: the order of the
+// sequential select, so the tree equals the one-rank tree).
+__global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int k = stp->k, q = blockIdx.x, F = a.F, lane = threadIdx.x;
+  if ((q >> 1) >= k) return;
+  const int c = FPairChild(a, k, q);
+  double bg = kMinScore;
+  int bf = 0x7fffffff, bp = -1;
+  for (int f = lane; f < F && c >= 0; f += 64) {
+    const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+    if (kk.feature < 0) continue;
+    if (FBetter(kk.gain, kk.feature, 0, bg, bf, 0)) {
+      bg = kk.gain;
+      bf = kk.feature;
+      bp = f;
+    }
+  }
+  const int src = WaveArgBestLane(bg, bf, 0);
+  bp = ReadLane(bp, src);
+  FPairBest* out = a.fpb + static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q;
+  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  if (bp < 0) {
+    if (lane == 0) {
+      out->key.feature = -1;
+      out->key.gain = kMinScore;
+    }
+    return;
+  }
+  const size_t o = static_cast<size_t>(q) * F + bp;
+  for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
+    if (i < kKeyWords) reinterpret_cast<uint32_t*>(&out->key)[i] = reinterpret_cast<const uint32_t*>(a.ckey + o)[i];
+    else reinterpret_cast<uint32_t*>(&out->info)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(a.cinfo + o)[i - kKeyWords];
+  }
+}
+
+__global__ __launch_bounds__(64) void k_f_pair_merge(FArgs a) {
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int k = stp->k, q = blockIdx.x, F = a.F, lane = threadIdx.x, P = a.vote_P;
+  if ((q >> 1) >= k) return;
+  double bg = kMinScore;
+  int bf = 0x7fffffff, br = -1;
+  for (int r = lane; r < P; r += 64) {
+    const SplitKey& kk = a.fpb[static_cast<size_t>(r) * 2 * a.kmax + q].key;
+    if (kk.feature < 0) continue;
+    if (FBetter(kk.gain, kk.feature, 0, bg, bf, 0)) {
+      bg = kk.gain;
+      bf = kk.feature;
+      br = r;
+    }
+  }
+  const int src = WaveArgBestLane(bg, bf, 0);
+  br = ReadLane(br, src);
+  bf = ReadLane(bf, src);
+  for (int f = lane; f < F; f += 64) {
+    if (f == bf) continue;
+    SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+    kk.feature = -1;
+    kk.gain = kMinScore;
+  }
+  if (br < 0) return;
+  const FPairBest* in = a.fpb + static_cast<size_t>(br) * 2 * a.kmax + q;
+  const size_t o = static_cast<size_t>(q) * F + bf;
+  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
+    if (i < kKeyWords) reinterpret_cast<uint32_t*>(a.ckey + o)[i] = reinterpret_cast<const uint32_t*>(&in->key)[i];
+    else reinterpret_cast<uint32_t*>(a.cinfo + o)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(&in->info)[i - kKeyWords];
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2026,6 +2425,34 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
   if (a.cegb_raw) k_f_select<true><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L) + a.F + 16, s>>>(a);
   else k_f_select<false><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L), s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierVote(const FArgs& a, hipStream_t s) {
+  const size_t lds = static_cast<size_t>(a.F) * (sizeof(double) + sizeof(int));
+  k_f_vote<<<2 * a.kmax, kVoteThreads, lds, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierElect(const FArgs& a, hipStream_t s) {
+  const size_t R = static_cast<size_t>(a.vote_P) * a.vote_k;
+  const size_t lds = R * (sizeof(double) + 3 * sizeof(int)) + sizeof(int) * (kVoteThreads / 64) + sizeof(int) * a.vote_k + 16;
+  k_f_elect<<<2 * a.kmax, kVoteThreads, lds, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierVoteScan(const FArgs& a, size_t lds, hipStream_t s) {
+  k_f_vote_scan<<<2 * a.kmax * a.vote_k, 64, lds, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierPairBest(const FArgs& a, hipStream_t s) {
+  k_f_pair_best<<<2 * a.kmax, 64, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierPairMerge(const FArgs& a, hipStream_t s) {
+  k_f_pair_merge<<<2 * a.kmax, 64, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -338,17 +338,20 @@ def test_feature_parallel_multirank_rehearsal(lgb, gpu_required, transport):
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert "feature-parallel" in res["device_name"], res
+    # collectives: the frontier engine (per-child bests all-gathered each round)
+    assert ("frontier engine" in res["device_name"]) == (transport == "collective"), res
     assert res["ranks_identical"], res
     assert res["identical_leading_trees"] == 10, res
     assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
 
 
-@pytest.mark.parametrize("world,transport,topk", [(2, "collective", 3), (3, "xgmi", 3), (2, "xgmi", 20),
-                                                  (4, "xgmi", 2)])
+@pytest.mark.parametrize("world,transport,topk", [(2, "collective", 3), (3, "collective", 20), (4, "collective", 2),
+                                                  (3, "xgmi", 3), (2, "xgmi", 20), (4, "xgmi", 2)])
 def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport, topk):
     """Device voting-parallel (PV-Tree: local scan, top-k vote all-gathered, elected features'
     histograms summed, global scan of the elected features only), P ranks sharing the GPU: every
-    rank grows the identical model, equal to the host voting learner tree for tree."""
+    rank grows the identical model, equal to the host voting learner tree for tree. Over
+    collectives it runs on the frontier engine (all expansions of a round voted at once)."""
     import json
     import os
     import subprocess
@@ -364,6 +367,9 @@ def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert "voting-parallel" in res["device_name"], res
     assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
+    # collectives: the frontier engine (local pass, vote all-gather, elected rows all-reduced
+    # exactly, global pass per round); xGMI keeps the sequential chain's in-kernel exchange
+    assert ("frontier engine" in res["device_name"]) == (transport == "collective"), res
     assert res["ranks_identical"], res
     assert res["num_trees"] == 10
     assert res["identical_leading_trees"] == 10, res
