@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun call, parameterised: each named step runs under its own time limit and the call
 # stops at the first failing step (no GPU work after a fault, abort or time-out).
-#   bash scripts/gpu_run.sh tests:<pytest args> | smoke | bench:<bench args> | prof:<bench args> | py:<script args> ...
+#   bash scripts/gpu_run.sh tests:<pytest files>[|<-k expression>] | smoke | bench:<bench args> | prof:<bench args> | py:<script args> ...
 # e.g. bash scripts/gpu_run.sh "tests:tests/test_device_metrics.py" "bench:--steps 40 --warmup 3"
 set -u
 OUT=gpurun_out
@@ -15,7 +15,12 @@ for step in "$@"; do
   [ "$arg" = "$step" ] && arg=""
   log=$OUT/step${i}_${kind}.log
   case $kind in
-    tests) timeout -k 10 900 python -u -m pytest ${arg:-tests -m gpu} -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $log 2>&1 ;;
+    tests) files=${arg%%|*}; kexpr=""; [ "$files" != "$arg" ] && kexpr=${arg#*|}
+           if [ -n "$kexpr" ]; then
+             timeout -k 10 900 python -u -m pytest ${files:-tests -m gpu} -k "$kexpr" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $log 2>&1
+           else
+             timeout -k 10 900 python -u -m pytest ${files:-tests -m gpu} -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $log 2>&1
+           fi ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
     bench) timeout -k 10 400 python bench.py $arg > $log 2>&1 ;;
     prof)  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof$i -o run -- python3 bench.py $arg > $log 2>&1 &&

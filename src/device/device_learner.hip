@@ -1113,7 +1113,11 @@ class DeviceTreeLearner : public TreeLearner {
     uint8_t* um = pin_mask_.Get(static_cast<size_t>(F_) * (1 + 2 * L_));
     for (int f = 0; f < F_; ++f) um[f] = used[f] ? 1 : 0;
     HIP_CHECK(hipMemcpyAsync(used_bytree_.get(), um, F_, hipMemcpyHostToDevice, stream_));
+    Random byn_state;
     if (use_bynode_) {
+      // the tree's masks in the host's draw order (root, then smaller / larger child of each
+      // scanned split); the stream is rewound below to the draws the tree actually used
+      byn_state = col_sampler_.rng_state();
       Tree dummy(2);
       uint8_t* bm = um + F_;
       for (int r = 0; r < 2 * L_; ++r) {
@@ -1126,10 +1130,16 @@ class DeviceTreeLearner : public TreeLearner {
     LeafRange* hrange = pin_range_.Get(L_);
     double* hlo = pin_lout_.Get(1);
     int num_splits = 0, num_leaves = 1;
+    bynode_draws_ = 0;
     if (frontier_) {
       FrontierGrow(&num_splits, &num_leaves, hr, hrange, hlo);
     } else {
       SequentialGrow(&num_splits, &num_leaves, hr, hrange, hlo);
+    }
+    if (use_bynode_) {
+      col_sampler_.set_rng_state(byn_state);
+      Tree dummy(2);
+      for (int r = 0; r < std::min(bynode_draws_, 2 * L_); ++r) (void)col_sampler_.GetByNode(&dummy, 0);
     }
     auto tree = std::make_unique<Tree>(L_, false, false);
     tree->SetLeafOutput(0, hlo[0]);
@@ -1183,9 +1193,14 @@ class DeviceTreeLearner : public TreeLearner {
   // sequential chain (A/B runs).
   bool FrontierEligible() const {
     if (!FrontierSerial() && !FrontierDP() && !FrontierVoting() && !FrontierFeature()) return false;
-    if (use_bynode_ || config_->extra_trees) return false;
-    return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, CegbRaw());
+    if (config_->extra_trees) return false;
+    // by-node sampling: the single-device frontier (masks in the host's draw order, FArgs::bynode)
+    if (use_bynode_ && (!FrontierSerial() || !config_->interaction_constraints_vector.empty())) return false;
+    return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, RawCands());
   }
+  // per-node raw candidates of every feature (FArgs::cegb_raw): CEGB feature penalties, and
+  // by-node sampling (a node is scored once its mask is known)
+  bool RawCands() const { return CegbRaw() || use_bynode_; }
   // CEGB feature penalties in the frontier select: coupled (FArgs::cegb_coupled: refunds on a
   // feature's first use) and lazy (FArgs::cegb_lazy: per-row marks, unmarked-row counts per
   // node). Either makes the scans publish raw gains (FArgs::cegb_raw).
@@ -1320,7 +1335,7 @@ class DeviceTreeLearner : public TreeLearner {
     ffbest_ = reinterpret_cast<SplitInfo*>(b + o_fbest);
     ffkey_ = reinterpret_cast<SplitKey*>(b + o_fkey);
     UploadForcedSplits();
-    if (CegbRaw()) {
+    if (RawCands()) {
       fnkey_.Resize(C * F);
       fninfo_.Resize(C * F);
       fnuep_.Resize(C);
@@ -1539,7 +1554,7 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
-    if (CegbRaw() && fnuep_.size() > 0) {
+    if (RawCands() && fnuep_.size() > 0) {
       a.cegb_raw = 1;
       a.cegb_tradeoff = config_->cegb_tradeoff;
       a.nkey = fnkey_.get();
@@ -1576,6 +1591,7 @@ class DeviceTreeLearner : public TreeLearner {
       a.qpack = fglobal_rows_ * gl < 2147483647.0 && fglobal_rows_ * hl < 4294967295.0 ? 1 : 0;
     }
     a.sp = MakeArgs().sp;
+    a.bynode = use_bynode_ ? bynode_.get() : nullptr;
     if (ffeature_) {
       a.fowned = ffowned_.get();
       a.fpb = ffpb_.get();
@@ -1857,6 +1873,7 @@ class DeviceTreeLearner : public TreeLearner {
     fstat_trees_ += 1;
     *num_splits = hs->num_splits;
     *num_leaves = hs->num_leaves;
+    bynode_draws_ = hs->byn;
     // (k_f_results already wrote the records, ranges, root output and flags with the state)
     if (*num_splits > 0) std::memcpy(hr, fres_host_ + FrontierResultRecOffset(), sizeof(SplitRec) * *num_splits);
     std::memcpy(hrange, fres_host_ + FrontierResultRangeOffset(L_), sizeof(LeafRange) * *num_leaves);
@@ -1964,6 +1981,7 @@ class DeviceTreeLearner : public TreeLearner {
     }
     // the control buffer written last holds the final tree state
     const Ctl* hc = hc2[1].num_splits > hc2[0].num_splits ? &hc2[1] : &hc2[0];
+    bynode_draws_ = 1 + 2 * hc->scan_round;  // the root's mask, two per scanned split
     *num_splits = hc->num_splits;
     *num_leaves = hc->num_leaves;
   }
@@ -3247,6 +3265,7 @@ class DeviceTreeLearner : public TreeLearner {
   int N_ = 0, F_ = 0, G_ = 0, TB_ = 0, width_ = 1, stride_dw_ = 1, L_ = 2, K_ = 1;
   int device_id_ = 0, num_cu_ = 256, num_tiles_ = 0, max_tiles_ = 1, max_cat_bin_ = 1;
   bool has_cat_ = false, use_bag_ = false, use_bynode_ = false, use_dp_ = false;
+  int bynode_draws_ = 0;  // by-node masks the last tree used (the host sampler's GetByNode calls)
   data_size_t bag_cnt_ = 0;
   size_t hist_lds_bytes_ = 0, scan_lds_bytes_ = 0;
   int max_bin_ = 2, cat_p2_ = 1;

@@ -121,7 +121,7 @@ struct FState {
   int spec;         // expansions started so far
   long long used_rows, waste_rows;  // (when done) rows partitioned by committed / uncommitted expansions
   int forced_next;  // next forced split to apply (-1: forced splits over or none)
-  int pad;
+  int byn;          // feature_fraction_bynode: masks drawn so far (the host's GetByNode calls)
 };
 
 // Arguments of the frontier kernels (device pointers into the learner's buffers).
@@ -236,6 +236,11 @@ struct FArgs {
   // k_f_scan scans the features this rank owns (fowned), each child's best is all-gathered and
   // the best over ranks becomes the child's candidate. Reference: feature_parallel_tree_learner.cpp:23-80.
   const uint8_t* fowned;  // [F] 1: this rank scans the feature (null: every feature)
+  // feature_fraction_bynode: the tree's by-node masks [2 L][F] in the host's draw order (the
+  // root's, then smaller / larger child of every split whose children are scanned). Candidates
+  // stay raw per node (cegb_raw); a node's mask is known once its parent commits, so the
+  // replay scores the children then, and only leaves of the committed tree are expanded.
+  const uint8_t* bynode;
   struct FPairBest* fpb;  // [P][kmax][2] per-child best of each rank, all-gathered
   int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
   int part_nt;      // A/B knob (LGAP_PART_NT=1): the partition's row-index scatter with non-temporal stores

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
     s.spec = 0;
     s.used_rows = s.waste_rows = 0;
     s.forced_next = a.num_forced > 0 ? 0 : -1;
-    s.pad = 0;
+    s.byn = a.bynode != nullptr ? 1 : 0;  // (the root's mask: row 0)
     *a.st = s;
     FNode r;
     r.buf = tp.root_buf;
@@ -1263,7 +1263,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
 #pragma unroll
       for (int j = 0; j < kSelPairs; ++j) {
         const int q = w + j * kSelWaves;
-        if (q < np && f < F && s_pc[q] >= 0) {
+        // (bynode: the root is scored at its mask, row 0; other children when their parent commits)
+        if (q < np && f < F && s_pc[q] >= 0 && !(cegb && a.bynode != nullptr && s_pc[q] == 0 && !a.bynode[f])) {
           const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
           const int kf = kk.feature;
           const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used, s_pc[q]) : kk.gain);
@@ -1367,9 +1368,11 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     s_lf[l] = f < 0 ? 0x7fffffff : f;
   }
   __syncthreads();
+  __shared__ int s_byn;
   if (w == 0) {
     int nl = st.num_leaves, ns = st.num_splits, done = 0, blocked = -1, nc = 0;
     int fnext = st.forced_next, bforced = 0;
+    int byn = st.byn;  // bynode masks drawn (wave-uniform)
     unsigned epoch = epoch0;  // CEGB first-use events (wave-uniform)
     for (;;) {
       if (nl >= L) {
@@ -1527,16 +1530,31 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         // the children are scored at the flags after this split (the host evaluates them
-        // after OnSplit): re-score from their raw candidates when an event came since
+        // after OnSplit): re-score from their raw candidates when an event came since. With
+        // by-node sampling always: the children's masks are the next two draws (smaller child
+        // first, as the host's FindBestSplits), unless they are not scanned at all (max_depth /
+        // min_data: the host draws nothing for them either)
+        const uint8_t* cmask[2] = {nullptr, nullptr};
+        if (a.bynode != nullptr) {
+          const int gl = a.nodes[left].gcount, gr = a.nodes[left + 1].gcount, md = a.sp.min_data_in_leaf;
+          const bool skip = (a.max_depth > 0 && s_dep[left] >= a.max_depth) || (gl < 2 * md && gr < 2 * md);
+          if (!skip) {
+            const bool left_smaller = gl < gr;
+            cmask[left_smaller ? 0 : 1] = a.bynode + static_cast<size_t>(byn) * F;
+            cmask[left_smaller ? 1 : 0] = a.bynode + static_cast<size_t>(byn + 1) * F;
+            byn += 2;
+          }
+        }
 #pragma unroll 1
         for (int ch = left; ch <= left + 1; ++ch) {
-          if (static_cast<unsigned>(a.nuep[ch]) == epoch) continue;
+          const uint8_t* mk = cmask[ch - left];
+          if (a.bynode == nullptr && static_cast<unsigned>(a.nuep[ch]) == epoch) continue;
           const int n = a.nodes[ch].gcount, d = s_dep[ch];
           double cg = kMinScore;
           int cf = 0x7fffffff, cp = -1;
           for (int f = lane; f < F; f += 64) {
             const SplitKey& kk = a.nkey[static_cast<size_t>(ch) * F + f];
-            if (kk.feature < 0) continue;
+            if (kk.feature < 0 || (a.bynode != nullptr && (mk == nullptr || !mk[f]))) continue;
             const double g = CegbAdjust(a, kk, n, d, s_used, ch);
             if (FBetter(g, kk.feature, 0, cg, cf, 0)) {
               cg = g;
@@ -1593,6 +1611,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       s_ncommit = nc;
       s_fnext = fnext;
       s_bforced = bforced;
+      s_byn = byn;
     }
   }
   __syncthreads();
@@ -1634,6 +1653,9 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         elig = alive && !(sc & kNodeExpanded);
         // while forced splits are pending, their nodes are expanded only by them (the blocked one)
         if (elig && s_fnext >= 0 && s_fidx[c] >= 0 && c != s_blocked) elig = false;
+        // by-node sampling: a node's split is known once its mask is, i.e. once it is a leaf of
+        // the committed tree (its parent committed)
+        if (elig && a.bynode != nullptr && s_par[c] >= 0 && !(s_st[s_par[c]] & kNodeCommitted)) elig = false;
         if (elig) {
           const int target = s_dep[c] + 1 - kFrontierBufs;
           if (target >= 1) {
@@ -1839,6 +1861,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     ns_.done = done;
     ns_.blocked = s_blocked;
     ns_.forced_next = s_fnext;
+    ns_.byn = s_byn;
     if (!done) {
       ns_.k = s_k;
       ns_.total_tiles = s_tiles;

@@ -336,7 +336,7 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
               // subtracted before the monotone penalty multiplies the gain)
               if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
-              if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
+              if (a.bynode && !a.bynode[static_cast<size_t>(c.scan_round == 0 ? 0 : 2 * c.scan_round - 1 + sel) * a.F + f]) out->Reset();
               if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
             }
           }

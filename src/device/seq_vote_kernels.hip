@@ -265,7 +265,7 @@ __global__ __launch_bounds__(128) void k_vote_scan(Args a) {
       } else {
         out->feature = f;
         if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, a.depth[leaf]);
-        if (a.bynode && !a.bynode[(static_cast<size_t>(c.scan_round) * 2 + sel) * a.F + f]) out->Reset();
+        if (a.bynode && !a.bynode[static_cast<size_t>(c.scan_round == 0 ? 0 : 2 * c.scan_round - 1 + sel) * a.F + f]) out->Reset();
         if (a.ic_feat && (a.ic_leaf[leaf] & a.ic_feat[f]) == 0ull) out->Reset();
       }
       key.feature = out->feature;

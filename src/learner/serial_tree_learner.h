@@ -25,6 +25,10 @@ class ColSampler {
   void ResetByTree();
   std::vector<int8_t> GetByNode(const Tree* tree, int leaf);
   const std::vector<int8_t>& is_feature_used_bytree() const { return used_bytree_; }
+  // the node sampler's random state: a device learner that pre-draws a tree's by-node masks
+  // rewinds to it and replays only the draws the tree used, so the stream stays the host's
+  const Random& rng_state() const { return rand_; }
+  void set_rng_state(const Random& r) { rand_ = r; }
 
  private:
   static int GetCnt(size_t total, double fraction);

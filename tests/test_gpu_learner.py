@@ -943,3 +943,26 @@ def test_wide_rows_training_score(lgb, gpu_required, rng):
     bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y), 8)
     bg = lgb.train({**params, "device_type": "gpu", "gpu_use_dp": True}, lgb.Dataset(X, y), 8)
     np.testing.assert_allclose(bg.predict(X[:3000]), bc.predict(X[:3000]), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("extra", [{"feature_fraction_bynode": 0.6},
+                                   {"feature_fraction_bynode": 0.5, "feature_fraction": 0.8, "num_leaves": 31},
+                                   {"feature_fraction_bynode": 0.7, "max_depth": 3, "min_data_in_leaf": 50}])
+def test_bynode_sampling_on_frontier_matches_cpu(lgb, gpu_required, rng, extra):
+    """feature_fraction_bynode on the frontier engine: the tree's masks in the host's draw order
+    (root, then smaller / larger child of every scanned split), each child scored when its parent
+    commits in the replay, and the sampler rewound to the draws the tree used, so every tree (not
+    only the first) equals the CPU learner's."""
+    X = rng.standard_normal((30000, 12))
+    z = X[:, 0] - 0.8 * X[:, 1] + 0.5 * X[:, 2] * X[:, 3] + 0.3 * X[:, 4] + 0.2 * rng.standard_normal(30000)
+    y = (z > 0).astype(float)
+    kw = {"num_leaves": 15, "feature_fraction_seed": 5}
+    kw.update(extra)
+    bc = _train(lgb, X, y, "cpu", rounds=6, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=6, gpu_use_dp=True, **kw)
+    assert "frontier engine" in bg.device_name(), bg.device_name()
+    for t in range(6):
+        sc = _splits(_trees(bc)[t]["tree_structure"], [])
+        sg = _splits(_trees(bg)[t]["tree_structure"], [])
+        assert [s[0] for s in sc] == [s[0] for s in sg], (t, sc[:6], sg[:6])
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-4)
