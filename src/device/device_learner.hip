@@ -1669,7 +1669,7 @@ class DeviceTreeLearner : public TreeLearner {
     LaunchFrontierVoteScan(fa, FrontierVoteScanLds(), stream_);
   }
   size_t FrontierVoteScanLds() const {
-    return static_cast<size_t>(max_bin_) * 2 * sizeof(double) + static_cast<size_t>(cat_p2_) * (sizeof(int) + sizeof(double));
+    return static_cast<size_t>(max_bin_) * 2 * sizeof(double) + static_cast<size_t>(cat_p2_) * (2 * sizeof(int) + sizeof(double));
   }
 
   // Feature parallel: this rank's per-child bests all-gathered, the best over ranks kept.

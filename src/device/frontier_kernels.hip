@@ -2109,8 +2109,8 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
   double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
   if (a.quant) QuantScales(a, &inv_g, &inv_h);
   double* H = reinterpret_cast<double*>(smem);                                   // [2 max_bin]
-  int* order = reinterpret_cast<int*>(H + 2 * a.max_bin);                         // [cat_p2]
-  double* ckey = reinterpret_cast<double*>(order + a.cat_p2);                     // [cat_p2]
+  int* order = reinterpret_cast<int*>(H + 2 * a.max_bin);                         // [cat_p2] (+ pad)
+  double* ckey = reinterpret_cast<double*>(order + 2 * a.cat_p2);                 // [cat_p2], 8-byte aligned
   __shared__ __align__(8) unsigned char s_out_raw[sizeof(SplitInfo)];
   SplitInfo* out = reinterpret_cast<SplitInfo*>(s_out_raw);
   const unsigned long long* rows = a.vrows + (static_cast<size_t>(q) * K + j) * 2 * a.max_bin;
