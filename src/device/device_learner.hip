@@ -1193,7 +1193,8 @@ class DeviceTreeLearner : public TreeLearner {
   // sequential chain (A/B runs).
   bool FrontierEligible() const {
     if (!FrontierSerial() && !FrontierDP() && !FrontierVoting() && !FrontierFeature()) return false;
-    if (config_->extra_trees) return false;
+    // extra trees: the single-device frontier (one expansion per round: FArgs::xrng)
+    if (config_->extra_trees && !FrontierSerial()) return false;
     // by-node sampling: the single-device frontier (masks in the host's draw order, FArgs::bynode)
     if (use_bynode_ && (!FrontierSerial() || !config_->interaction_constraints_vector.empty())) return false;
     return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, RawCands());
@@ -1592,6 +1593,7 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.sp = MakeArgs().sp;
     a.bynode = use_bynode_ ? bynode_.get() : nullptr;
+    a.xrng = config_->extra_trees ? rng_.get() : nullptr;
     if (ffeature_) {
       a.fowned = ffowned_.get();
       a.fpb = ffpb_.get();

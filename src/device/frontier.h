@@ -241,6 +241,11 @@ struct FArgs {
   // stay raw per node (cegb_raw); a node's mask is known once its parent commits, so the
   // replay scores the children then, and only leaves of the committed tree are expanded.
   const uint8_t* bynode;
+  // extra_trees: per-feature random streams (Random(extra_seed + f), persistent across trees;
+  // null: off). Draws follow the host's order (each scanned node: smaller child, then larger),
+  // which the frontier keeps by expanding only the node the replay is blocked on: at its scan
+  // every earlier split of the sequential order is committed.
+  unsigned* xrng;
   struct FPairBest* fpb;  // [P][kmax][2] per-child best of each rank, all-gathered
   int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
   int part_nt;      // A/B knob (LGAP_PART_NT=1): the partition's row-index scatter with non-temporal stores

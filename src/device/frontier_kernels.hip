@@ -446,7 +446,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
 //  3. the two candidates -> the round's candidate table [e][sel][f]
 __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ int s_skip, s_splp;
+  __shared__ int s_skip, s_splp, s_rand[2], s_xn[2];
+  __shared__ double s_xh[2];
   __shared__ __align__(8) unsigned char s_out_raw[2 * sizeof(SplitInfo)];
   __shared__ SplitKey s_key[2];
   SplitInfo* s_out = reinterpret_cast<SplitInfo*>(s_out_raw);
@@ -567,9 +568,36 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       if (lane == 0) {
         H[2 * fi.mfb] = pre_sum.x - sgs;
         H[2 * fi.mfb + 1] = pre_sum.y - shs;
+        s_xn[w] = pre_n;
+        s_xh[w] = pre_sum.y;
       }
     }
     __syncthreads();
+    if (a.xrng != nullptr && t == 0) {
+      // extra-trees thresholds, drawn in the host learner's order: the smaller child, then the
+      // larger one (one expansion per round here: no other item advances this feature's stream)
+      s_rand[0] = s_rand[1] = 0;
+      if (!skip_both) {
+        for (int sel = 0; sel < 2; ++sel) {
+          if ((sel == 0 ? cs : cl) < 0) continue;
+          unsigned* r = &a.xrng[f];
+          if (fi.bin_type == 0) {
+            if (fi.num_bin - 2 > 0) s_rand[sel] = RandNextInt(r, 0, fi.num_bin - 2);
+          } else if (fi.num_bin <= a.sp.max_cat_to_onehot) {
+            if (fi.num_bin - 1 > 0) s_rand[sel] = RandNextInt(r, 1, fi.num_bin);
+          } else {
+            const double* H = sel == 0 ? hs_full : hl_full;
+            const double cf = s_xn[sel] / (s_xh[sel] + 2 * kEpsilon);
+            int used = 0;
+            for (int b = 1; b < fi.num_bin; ++b) used += RoundCount(H[2 * b + 1] * cf) >= a.sp.cat_smooth;
+            const int max_num_cat = min(a.sp.max_cat_threshold, (used + 1) / 2);
+            const int max_thr = max(min(max_num_cat, used) - 1, 0);
+            if (max_thr > 0) s_rand[sel] = RandNextInt(r, 0, max_thr);
+          }
+        }
+      }
+    }
+    if (a.xrng != nullptr) __syncthreads();
     if (w < 2 && my >= 0) {
       SplitInfo* out = &s_out[w];
       const double sg = __shfl(pre_sum.x, 0, kWave), sh = __shfl(pre_sum.y, 0, kWave);
@@ -591,8 +619,9 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         bounds.min = __shfl(pre_bounds.min, 0, kWave);
         bounds.max = __shfl(pre_bounds.max, 0, kWave);
         bool spl;
+        const int rt = a.xrng != nullptr ? s_rand[w] : 0;
         if (fi.bin_type == 0) {
-          spl = ScanNumericalWave(spp, fi, H, sg, sh, n, po, bounds, 0, out);
+          spl = ScanNumericalWave(spp, fi, H, sg, sh, n, po, bounds, rt, out);
         } else {
           FeatureScanMeta m;
           m.num_bin = fi.num_bin;
@@ -601,7 +630,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
           m.bin_type = fi.bin_type;
           m.monotone = fi.monotone;
           m.penalty = fi.penalty;
-          m.rand_threshold = 0;
+          m.rand_threshold = rt;
           if (lane == 0) out->Reset();
           spl = ScanCategoricalWave(spp, m, H, sg, sh, n, po, bounds, a.cat_p2, order + w * a.cat_p2,
                                     ckey + w * a.cat_p2, out);
@@ -1656,6 +1685,9 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         // by-node sampling: a node's split is known once its mask is, i.e. once it is a leaf of
         // the committed tree (its parent committed)
         if (elig && a.bynode != nullptr && s_par[c] >= 0 && !(s_st[s_par[c]] & kNodeCommitted)) elig = false;
+        // extra trees: only the node the replay waits for (its children's random thresholds are
+        // drawn when every earlier split of the sequential order has been scanned)
+        if (elig && a.xrng != nullptr && c != s_blocked) elig = false;
         if (elig) {
           const int target = s_dep[c] + 1 - kFrontierBufs;
           if (target >= 1) {

@@ -966,3 +966,28 @@ def test_bynode_sampling_on_frontier_matches_cpu(lgb, gpu_required, rng, extra):
         sg = _splits(_trees(bg)[t]["tree_structure"], [])
         assert [s[0] for s in sc] == [s[0] for s in sg], (t, sc[:6], sg[:6])
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("extra", [{}, {"num_leaves": 31, "extra_seed": 11}, {"max_depth": 4, "min_data_in_leaf": 40}])
+def test_extra_trees_on_frontier_matches_cpu(lgb, gpu_required, rng, extra):
+    """extra_trees on the frontier engine: per-feature random streams drawn in the host's order
+    (each scanned node's smaller child, then its larger one), kept by expanding only the node the
+    replay waits for; numerical and categorical (one-hot and ctr-sorted) thresholds; every tree
+    equals the CPU learner's."""
+    n = 30000
+    X = rng.standard_normal((n, 8))
+    X[:, 6] = rng.integers(0, 3, n)    # one-hot categorical
+    X[:, 7] = rng.integers(0, 25, n)   # many-category categorical
+    z = X[:, 0] - 0.8 * X[:, 1] + 0.4 * (X[:, 7] % 5 == 1) + 0.3 * (X[:, 6] == 2) + 0.3 * rng.standard_normal(n)
+    y = (z > 0).astype(float)
+    kw = {"num_leaves": 15, "extra_trees": True, "categorical_feature": [6, 7], "min_data_per_group": 20,
+          "cat_smooth": 5}
+    kw.update(extra)
+    bc = _train(lgb, X, y, "cpu", rounds=5, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=5, gpu_use_dp=True, **kw)
+    assert "frontier engine" in bg.device_name(), bg.device_name()
+    for t in range(5):
+        sc = _splits(_trees(bc)[t]["tree_structure"], [])
+        sg = _splits(_trees(bg)[t]["tree_structure"], [])
+        assert [s[0] for s in sc] == [s[0] for s in sg], (t, sc[:6], sg[:6])
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-4)
