@@ -26,6 +26,19 @@ for step in "$@"; do
     prof)  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof$i -o run -- python3 bench.py $arg > $log 2>&1 &&
              python scripts/prof_summary.py $OUT/prof$i "bench.py $arg" 12 > $OUT/prof${i}_summary.md 2>&1 && rm -rf $OUT/prof$i ;;
     py)    timeout -k 10 600 python -u $arg > $log 2>&1 ;;
+    # three counter passes (one per block budget: SQ / TCC fetch / TCC write), each in its own
+    # run, summarised per kernel by scripts/pmc_summary.py; <args>: a python script and its
+    # arguments (e.g. pmc:bench.py --steps 3 --warmup 1)
+    pmc)   rc=0; j=0
+           for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS" "FETCH_SIZE TCC_HIT_sum" "WRITE_SIZE TCC_MISS_sum"; do
+             j=$((j + 1))
+             timeout -s KILL 240 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d $PWD/$OUT/pmc${i}_$j -o run -- python3 $arg >> $log 2>&1 || { rc=$?; break; }
+           done
+           if [ $rc -eq 0 ]; then
+             python scripts/pmc_summary.py "$arg" $OUT/pmc${i}_* > $OUT/pmc${i}_summary.md 2>&1; rm -rf $OUT/pmc${i}_[0-9]
+             head -20 $OUT/pmc${i}_summary.md
+           fi
+           (exit $rc) ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
   rc=$?

@@ -5,9 +5,11 @@ usage: pmc_summary.py <title> <pass dir> [<pass dir> ...]
 Each pass directory holds the csv files of one `rocprofv3 --pmc ... --kernel-trace
 --output-format csv` run. Counter values are averaged per dispatch of a kernel and
 joined with the mean dispatch duration of the same run. Derived columns:
-  HBM GB/s   (2 x FETCH_SIZE + WRITE_SIZE) / duration; FETCH_SIZE is doubled because on
-             gfx950 it reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md,
-             HBM) -- an upper estimate for narrower access patterns
+  raw GB/s   (FETCH_SIZE + WRITE_SIZE) / duration: the counters as reported (a LOWER bound
+             when the kernel's reads are wide and coalesced)
+  2xF GB/s   (2 x FETCH_SIZE + WRITE_SIZE) / duration: FETCH_SIZE doubled, because on gfx950
+             it reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM) -- an
+             UPPER estimate for narrower access patterns (gathers); quote the raw column
   L2 hit %   TCC_HIT / (TCC_HIT + TCC_MISS)
   LDS confl  SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (extra LDS cycles per LDS instruction)
   wait %     SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
@@ -61,7 +63,8 @@ def main():
             dur[k].extend(v)
     print(f"# {title}\n")
     print("Per-dispatch means over the profiled run(s): " + ", ".join(f"`{d}`" for d in dirs) + "\n")
-    cols = ["calls", "avg us", "FETCH KB", "WRITE KB", "HBM GB/s", "L2 hit %", "LDS confl", "wait %", "issue %"]
+    cols = ["calls", "avg us", "FETCH KB", "WRITE KB", "raw GB/s", "2xF GB/s", "L2 hit %", "LDS confl", "wait %",
+            "issue %"]
     print("| kernel | " + " | ".join(cols) + " |")
     print("|---|" + "---:|" * len(cols))
     rows = []
@@ -70,6 +73,7 @@ def main():
         t = sum(dur[k]) / len(dur[k]) if dur.get(k) else float("nan")
         fetch, write = m.get("FETCH_SIZE", float("nan")), m.get("WRITE_SIZE", float("nan"))
         bw = (2 * fetch + write) * 1024 / (t * 1e-6) / 1e9 if t == t and t > 0 else float("nan")
+        raw = (fetch + write) * 1024 / (t * 1e-6) / 1e9 if t == t and t > 0 else float("nan")
         hit, miss = m.get("TCC_HIT_sum", float("nan")), m.get("TCC_MISS_sum", float("nan"))
         l2 = 100.0 * hit / (hit + miss) if hit + miss > 0 else float("nan")
         lds = m.get("SQ_ACTIVE_INST_LDS", 0.0)
@@ -77,7 +81,7 @@ def main():
         cyc = m.get("SQ_WAVE_CYCLES", 0.0)
         wait = 100.0 * m.get("SQ_WAIT_ANY", float("nan")) / cyc if cyc > 0 else float("nan")
         issue = 100.0 * m.get("SQ_WAIT_INST_ANY", float("nan")) / cyc if cyc > 0 else float("nan")
-        rows.append((t * len(dur.get(k, [])), k, [len(dur.get(k, [])), t, fetch, write, bw, l2, confl, wait, issue]))
+        rows.append((t * len(dur.get(k, [])), k, [len(dur.get(k, [])), t, fetch, write, raw, bw, l2, confl, wait, issue]))
     for _, k, v in sorted(rows, key=lambda r: -r[0] if r[0] == r[0] else 0):
         cells = [str(v[0])] + [("%.1f" % x) if x == x else "-" for x in v[1:]]
         print(f"| `{k}` | " + " | ".join(cells) + " |")
