@@ -173,6 +173,8 @@ class Dataset {
   // raw values of used features (kept only for linear_tree)
   bool has_raw() const { return !raw_.empty(); }
   double raw(data_size_t i, int inner) const { return raw_[static_cast<size_t>(i) * features_.size() + inner]; }
+  // [num_data][num_features] raw values of the used features (linear_tree; empty otherwise)
+  const std::vector<float>& raw_values() const { return raw_; }
 
   // Raw group bin of row i in group g.
   inline uint32_t GroupBin(data_size_t i, int g) const {

@@ -34,6 +34,9 @@ std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const
 // the frontier implements on the device (forced splits, CEGB feature penalties) route to the
 // host split policy when it cannot.
 bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type);
+// Whether the device learner fits linear_tree leaves itself (fp64 MFMA Gram systems): serial
+// learner, float gradients, raw values kept, and at most 30 branch features per leaf.
+bool LinearOnDevice(const Config* config, const Dataset* train, const std::string& learner_type);
 
 // GPU histogram engine for the host learners (the reference's GPUTreeLearner
 // split, src/treelearner/gpu_tree_learner.cpp: histograms on the device, split

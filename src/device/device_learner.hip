@@ -79,6 +79,7 @@
 #include "device/hip_common.h"
 #include "device/leaf_kernels.h"
 #include "device/metric_kernels.h"
+#include "device/linear_kernels.h"
 #include "device/runtime_internal.h"
 #include "device/frontier.h"
 #include "device/traverse_kernels.h"
@@ -87,6 +88,8 @@
 #include "device/split_scan.h"
 #include "device/tree_kernels.h"
 #include "learner/forced_splits.h"
+#include "learner/linear_solve.h"
+#include "learner/parallel_tree_learner.h"
 #include "learner/serial_tree_learner.h"
 #include "lgap/common.h"
 #include "lgap/device_api.h"
@@ -216,6 +219,23 @@ class DeviceTreeLearner : public TreeLearner {
 
     use_dp_ = config_->gpu_use_dp;
     UploadData();
+    linear_ = config_->linear_tree;
+    if (linear_) {
+      // linear leaves read the raw feature values (Dataset constructed with linear_tree=true)
+      if (!train->has_raw() && F_ > 0) {
+        Log::Fatal("linear_tree requires the Dataset to keep raw feature values (construct it with linear_tree=true)");
+      }
+      const auto& raw = train->raw_values();
+      lin_has_nan_ = false;
+      for (float v : raw) {
+        if (std::isnan(v)) {
+          lin_has_nan_ = true;
+          break;
+        }
+      }
+      if (!raw.empty()) lin_raw_.Upload(raw, stream_);
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
     SetupOwnership();
     ResetConfig(config_);
     SetupTransport();
@@ -490,7 +510,13 @@ class DeviceTreeLearner : public TreeLearner {
 
   std::unique_ptr<Tree> FitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred, const score_t* g,
                                           const score_t* h) override {
-    // refit is a one-off host pass over leaf assignments; the host learner computes it
+    // refit is a one-off host pass over leaf assignments; the host learner computes it (linear
+    // trees: the host linear learner, which re-solves the leaf models)
+    if (linear_) {
+      auto host = CreateLinearTreeLearner(config_);
+      host->Init(data_, false);
+      return host->FitByExistingTree(old_tree, leaf_pred, g, h);
+    }
     SerialTreeLearner host(config_);
     host.Init(data_, false);
     return host.FitByExistingTree(old_tree, leaf_pred, g, h);
@@ -502,8 +528,9 @@ class DeviceTreeLearner : public TreeLearner {
   std::unique_ptr<Tree> DeviceFitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
                                                 int class_id) override {
     ScopedTimer timer("Device::Refit");
-    if (static_cast<data_size_t>(leaf_pred.size()) != N_ || gh_.size() < static_cast<size_t>(class_id + 1) * N_) {
-      return nullptr;
+    if (static_cast<data_size_t>(leaf_pred.size()) != N_ || gh_.size() < static_cast<size_t>(class_id + 1) * N_ ||
+        old_tree->is_linear()) {
+      return nullptr;  // (linear trees: the host linear learner's refit, FitByExistingTree)
     }
     const int L = old_tree->num_leaves();
     leaf_pred_dev_.Upload(leaf_pred, stream_);
@@ -756,7 +783,10 @@ class DeviceTreeLearner : public TreeLearner {
       if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, N_, tree->LeafOutput(0), stream_);
       return;
     }
-    if (tree->is_linear()) Log::Fatal("Linear trees cannot be applied on the device");
+    if (tree->is_linear()) {
+      TraverseLinear(tree, s);
+      return;
+    }
     static const int score_path = [] {
       const char* e = std::getenv("LGAP_SCORE_PATH");
       return e == nullptr ? 0 : (std::strcmp(e, "leaves") == 0 ? 1 : (std::strcmp(e, "traverse") == 0 ? 2 : 0));
@@ -908,6 +938,14 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(ttree_buf_.get(), hp, total, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipEventRecord(tree_evt_[slot], stream_));
     const char* db = ttree_buf_.get();
+    if (lin_pending_ != nullptr) {
+      LaunchTraverseLinear(rowbins, stride_dw_, width_, n, reinterpret_cast<const TNode*>(db), nn,
+                           reinterpret_cast<const TCat*>(db + node_bytes),
+                           reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
+                           reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, *lin_pending_, s, num_cu_,
+                           stream_);
+      return;
+    }
     if (rowbins == rowbins_.get() && n == N_ && stride_dw_ > 16 && colbins_.size() >= static_cast<size_t>(G_) * N_ * width_) {
       LaunchTraverseCols(colbins_.get(), width_, n, reinterpret_cast<const TNode*>(db), nn,
                          reinterpret_cast<const TCat*>(db + node_bytes),
@@ -928,6 +966,7 @@ class DeviceTreeLearner : public TreeLearner {
 
   // ---- validation sets on the device: packed rows (training layout), score, labels / weights
   int DeviceAddValidSet(const Dataset* v, const std::vector<double>& score) override {
+    if (linear_) return -1;  // linear leaves need the set's raw values: validation scored on the host
     if (v->row_stride() != data_->row_stride() || v->bin_width() != width_ || v->num_data() <= 0) return -1;
     ScopedTimer timer("Device::AddValidSet");
     auto dv = std::make_unique<DevValid>();
@@ -1078,6 +1117,141 @@ class DeviceTreeLearner : public TreeLearner {
     return true;
   }
 
+  // ---- linear-leaf trees (linear_tree=true; reference linear_tree_learner.cpp:180-360)
+  // The structure comes from the frontier / sequential chain as for any tree; each leaf's
+  // Gram system over the numerical features on its branch is accumulated by the fp64 MFMA
+  // kernel over the leaf's rows (linear_kernels.hip) and solved on the host (linear_solve.h),
+  // as LinearTreeLearner::Train does on the host. The first tree keeps constant leaves.
+  void FitLinearLeaves(Tree* tree, bool is_first_tree, int class_id) {
+    ScopedTimer timer("Device::LinearLeaves");
+    tree->SetIsLinear(true);
+    tree->InitLinear();
+    const int nl = tree->num_leaves();
+    if (is_first_tree || nl <= 1) {
+      for (int l = 0; l < nl; ++l) tree->SetLeafConst(l, tree->LeafOutput(l));
+      return;
+    }
+    if (static_cast<int>(h_range_.size()) != nl) Log::Fatal("linear leaves: %d leaf ranges for %d leaves", static_cast<int>(h_range_.size()), nl);
+    // distinct numerical features split on along each leaf's branch, sorted (inner indices)
+    std::vector<int> parent(std::max(1, nl - 1), -1);
+    for (int p = 0; p < nl - 1; ++p) {
+      if (tree->left_child(p) >= 0) parent[tree->left_child(p)] = p;
+      if (tree->right_child(p) >= 0) parent[tree->right_child(p)] = p;
+    }
+    std::vector<std::vector<int>> feats(nl);
+    std::vector<int> off(nl + 1, 0), flat;
+    int max_m = 1, max_cnt = 1;
+    for (int l = 0; l < nl; ++l) {
+      for (int node = tree->leaf_parent(l); node >= 0; node = parent[node]) {
+        const int f = tree->split_feature_inner(node);
+        if (data_->feature(f).bin_type == BinType::Numerical) feats[l].push_back(f);
+      }
+      std::sort(feats[l].begin(), feats[l].end());
+      feats[l].erase(std::unique(feats[l].begin(), feats[l].end()), feats[l].end());
+      off[l + 1] = off[l] + static_cast<int>(feats[l].size());
+      flat.insert(flat.end(), feats[l].begin(), feats[l].end());
+      max_m = std::max(max_m, static_cast<int>(feats[l].size()) + 1);
+      max_cnt = std::max(max_cnt, h_range_[l].count);
+    }
+    if (max_m > kLinMaxM) Log::Fatal("linear leaves on the device: %d branch features (at most %d)", max_m - 1, kLinMaxM - 1);
+    std::vector<LeafSeg> segs(nl);
+    for (int l = 0; l < nl; ++l) {
+      segs[l].buf = h_range_[l].buf;
+      segs[l].start = h_range_[l].start;
+      segs[l].count = h_range_[l].count;
+      segs[l].pad = 0;
+    }
+    lin_segs_.Upload(segs, stream_);
+    lin_off_.Upload(off, stream_);
+    if (flat.empty()) flat.push_back(0);
+    lin_feats_.Upload(flat, stream_);
+    LinearGramArgs ga;
+    ga.raw = lin_raw_.get();
+    ga.F = F_;
+    ga.gh = gh_.get() + static_cast<size_t>(class_id) * N_;
+    for (int i = 0; i < kLeafIdxBufs; ++i) ga.idx[i] = i < kFrontierIdx ? idx_[i].get() : nullptr;
+    ga.segs = lin_segs_.get();
+    ga.feat_off = lin_off_.get();
+    ga.feats = lin_feats_.get();
+    ga.num_leaves = nl;
+    // row chunks per leaf: enough blocks to cover the CUs, a few thousand rows each
+    ga.chunks = std::max(1, std::min(std::max(1, 2 * num_cu_ / nl), DivUp(max_cnt, 4096)));
+    lin_partial_.Resize(std::max(lin_partial_.size(), LinearGramPartialDoubles(nl, ga.chunks)));
+    lin_out_.Resize(std::max(lin_out_.size(), static_cast<size_t>(nl) * kLinDim * kLinDim));
+    lin_usable_.Resize(std::max(lin_usable_.size(), static_cast<size_t>(nl)));
+    LaunchLinearGram(ga, max_m, lin_partial_.get(), lin_out_.get(), lin_usable_.get(), stream_);
+    std::vector<double> gram(static_cast<size_t>(nl) * kLinDim * kLinDim);
+    std::vector<long long> usable(nl);
+    lin_out_.Download(gram.data(), gram.size(), stream_);
+    lin_usable_.Download(usable.data(), nl, stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int l = 0; l < nl; ++l) {
+      const int k = static_cast<int>(feats[l].size()), m = k + 1;
+      const double* G = gram.data() + static_cast<size_t>(l) * kLinDim * kLinDim;
+      std::vector<double> A(static_cast<size_t>(m) * m), b(m), z;
+      for (int i = 0; i < m; ++i) {
+        for (int j = 0; j < m; ++j) A[static_cast<size_t>(i) * m + j] = G[i * kLinDim + j];
+        b[i] = -G[i * kLinDim + m];
+      }
+      const int64_t use = lin_has_nan_ ? usable[l] : h_range_[l].count;
+      if (!SolveLinearLeaf(std::move(A), b, use, m, config_->linear_lambda, &z)) {
+        tree->SetLeafConst(l, tree->LeafOutput(l));
+        continue;
+      }
+      // coefficients that round to zero are dropped (reference :365-369)
+      std::vector<double> coef;
+      std::vector<int> inner, real;
+      for (int j = 0; j < k; ++j) {
+        if (Tree::IsZero(z[j])) continue;
+        coef.push_back(z[j]);
+        inner.push_back(feats[l][j]);
+        real.push_back(data_->feature(feats[l][j]).real_index);
+      }
+      tree->SetLeafConst(l, z[k]);
+      tree->SetLeafCoeffs(l, coef);
+      tree->SetLeafFeatures(l, real);
+      tree->SetLeafFeaturesInner(l, inner);
+    }
+  }
+
+  // score update of a linear-leaf tree: the traversal evaluates the leaf's model at the row's
+  // raw values (8- / 16-bit training rows)
+  void TraverseLinear(const Tree* tree, double* s) {
+    const int nl = tree->num_leaves();
+    std::vector<int> off(nl + 1, 0), feat;
+    std::vector<double> coef, cnst(nl);
+    for (int l = 0; l < nl; ++l) {
+      const auto& fi = tree->LeafFeaturesInner(l);
+      const auto& c = tree->LeafCoeffs(l);
+      for (size_t j = 0; j < fi.size() && j < c.size(); ++j) {
+        feat.push_back(fi[j]);
+        coef.push_back(c[j]);
+      }
+      off[l + 1] = static_cast<int>(feat.size());
+      cnst[l] = tree->LeafConst(l);
+    }
+    if (feat.empty()) {
+      feat.push_back(0);
+      coef.push_back(0.0);
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_));  // (the previous tree's linear arrays may still be read)
+    lin_toff_.Upload(off, stream_);
+    lin_tfeat_.Upload(feat, stream_);
+    lin_tcoef_.Upload(coef, stream_);
+    lin_tcnst_.Upload(cnst, stream_);
+    LinearLeaves lin;
+    lin.raw = lin_raw_.get();
+    lin.F = F_;
+    lin.off = lin_toff_.get();
+    lin.feat = lin_tfeat_.get();
+    lin.coef = lin_tcoef_.get();
+    lin.cnst = lin_tcnst_.get();
+    lin_pending_ = &lin;
+    TraverseTreeCompact(tree, rowbins_.get(), N_, s);
+    lin_pending_ = nullptr;
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
   void EnsureMetricLabels() {
     if (metric_label_.size() != 0) return;
     const Metadata& md = data_->metadata();
@@ -1179,6 +1353,7 @@ class DeviceTreeLearner : public TreeLearner {
     }
     h_range_.assign(hrange, hrange + num_leaves);
     if (config_->use_quantized_grad && config_->quant_train_renew_leaf) RenewQuantizedLeaves(tree.get());
+    if (linear_) FitLinearLeaves(tree.get(), is_first_tree, class_id);
     if (stamps_.size() && !frontier_ && ++stamp_trees_ == 3) ReportStamps(num_splits);
     tree->RecomputeMaxDepth();
     last_trained_ = tree.get();
@@ -3186,6 +3361,14 @@ class DeviceTreeLearner : public TreeLearner {
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
+  // linear-leaf trees (FitLinearLeaves / TraverseLinear)
+  bool linear_ = false, lin_has_nan_ = false;
+  DevBuf<float> lin_raw_;
+  DevBuf<LeafSeg> lin_segs_;
+  DevBuf<int> lin_off_, lin_feats_, lin_toff_, lin_tfeat_;
+  DevBuf<double> lin_partial_, lin_out_, lin_tcoef_, lin_tcnst_;
+  DevBuf<long long> lin_usable_;
+  const LinearLeaves* lin_pending_ = nullptr;  // set around TraverseLinear's traversal
   // feature-parallel frontier (FrontierFeature)
   bool ffeature_ = false;
   DevBuf<uint8_t> ffowned_;
@@ -3434,6 +3617,15 @@ std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const
   if (parallel_mode == "voting") return std::make_unique<DeviceTreeLearner>(config, DevParallel::kVoting);
   Log::Fatal("Unknown tree learner type %s", parallel_mode.c_str());
   return nullptr;
+}
+
+bool LinearOnDevice(const Config* config, const Dataset* train, const std::string& learner_type) {
+  if (learner_type != "serial" || config->use_quantized_grad || train == nullptr || !train->has_raw()) return false;
+  // the Gram tile holds <= kLinMaxM - 1 branch features: bounded by the features, the leaves
+  // and the depth
+  long long k = std::min<long long>(train->num_features(), std::max(1, config->num_leaves) - 1);
+  if (config->max_depth > 0) k = std::min<long long>(k, config->max_depth);
+  return k + 1 <= kLinMaxM;
 }
 
 bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type) {

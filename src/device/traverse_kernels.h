@@ -46,6 +46,13 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
                     const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,
                     int num_cu, hipStream_t s);
 
+// linear-leaf trees (linear_kernels.h LinearLeaves): score[i] += the leaf's linear model at
+// row i's raw values (its constant output when one of them is NaN); 8- / 16-bit rows
+struct LinearLeaves;
+void LaunchTraverseLinear(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
+                          const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves,
+                          const LinearLeaves& lin, double* score, int num_cu, hipStream_t s);
+
 // the same over the group-major copy colbins[g * n + row] (wide training rows)
 void LaunchTraverseCols(const uint8_t* colbins, int width, int n, const TNode* nodes, int num_nodes, const TCat* cats,
                         const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score, int num_cu,

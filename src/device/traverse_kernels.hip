@@ -8,6 +8,7 @@
 #include <algorithm>
 
 #include "device/hip_common.h"
+#include "device/linear_kernels.h"
 
 namespace lgap {
 namespace device {
@@ -33,12 +34,24 @@ __device__ __forceinline__ bool CatLeft(const TCat& c, const uint32_t* bits, uin
   return static_cast<int>(w) < c.nwords && ((bits[c.begin + w] >> (b & 31u)) & 1u);
 }
 
-template <int W>
+// a linear leaf's value for row `row` (reference linear tree Predict: the leaf's constant output
+// when any of the model's features is NaN)
+__device__ __forceinline__ double LinearValue(const LinearLeaves& lin, int leaf, long long row, double leaf_out) {
+  double v = lin.cnst[leaf];
+  for (int q = lin.off[leaf]; q < lin.off[leaf + 1]; ++q) {
+    const float x = lin.raw[row * lin.F + lin.feat[q]];
+    if (__builtin_isnan(x)) return leaf_out;
+    v += lin.coef[q] * static_cast<double>(x);
+  }
+  return v;
+}
+
+template <int W, bool LIN>
 __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restrict__ rowbins, int stride_dw, int n,
                                                         const TNode* __restrict__ nodes, int num_nodes,
                                                         const TCat* __restrict__ cats, const uint32_t* __restrict__ cat_bits,
                                                         const double* __restrict__ leaf_value, int num_leaves,
-                                                        double* __restrict__ score) {
+                                                        double* __restrict__ score, LinearLeaves lin) {
   extern __shared__ __align__(16) unsigned char lds[];
   TNode* s_nodes = reinterpret_cast<TNode*>(lds);
   double* s_leaf = reinterpret_cast<double*>(lds + ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)));
@@ -110,7 +123,10 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
 #pragma unroll
     for (int j = 0; j < kTRowsPerThread; ++j) {
       const int r = t + j * kTThreads;
-      if (r < rows) score[base + r] = sc[j] + s_leaf[~node[j]];
+      if (r < rows) {
+        const double lv = LIN ? LinearValue(lin, ~node[j], base + r, s_leaf[~node[j]]) : s_leaf[~node[j]];
+        score[base + r] = sc[j] + lv;
+      }
     }
   }
 }
@@ -223,15 +239,33 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
   const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + ((sizeof(double) * num_leaves + 15) & ~size_t(15)) +
                      (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
   const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
+  LinearLeaves none{};
   if (width == 0) {
-    k_traverse<0><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
-                                              num_leaves, score);
+    k_traverse<0, false><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                                     num_leaves, score, none);
   } else if (width == 1) {
-    k_traverse<1><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
-                                              num_leaves, score);
+    k_traverse<1, false><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                                     num_leaves, score, none);
   } else {
-    k_traverse<2><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
-                                              num_leaves, score);
+    k_traverse<2, false><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                                     num_leaves, score, none);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchTraverseLinear(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
+                          const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves,
+                          const LinearLeaves& lin, double* score, int num_cu, hipStream_t s) {
+  if (n <= 0) return;
+  const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + ((sizeof(double) * num_leaves + 15) & ~size_t(15)) +
+                     (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
+  const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
+  if (width == 1) {
+    k_traverse<1, true><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                                    num_leaves, score, lin);
+  } else {
+    k_traverse<2, true><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
+                                                    num_leaves, score, lin);
   }
   HIP_CHECK(hipGetLastError());
 }

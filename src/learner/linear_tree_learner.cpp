@@ -8,6 +8,7 @@
 #include <unordered_map>
 
 #include "lgap/log.h"
+#include "linear_solve.h"
 #include "parallel_tree_learner.h"
 
 namespace lgap {
@@ -187,35 +188,7 @@ class LinearTreeLearner : public SerialTreeLearner {
         for (int c = 0; c <= a; ++c) A[a * m + c] += hx * x[c];
       }
     }
-    if (usable < m) return false;
-    for (int j = 0; j < k; ++j) A[j * m + j] += config_->linear_lambda;
-    // Cholesky on the lower triangle
-    std::vector<double> L(A.size(), 0.0);
-    for (int i = 0; i < m; ++i) {
-      for (int j = 0; j <= i; ++j) {
-        double s = A[i * m + j];
-        for (int t = 0; t < j; ++t) s -= L[i * m + t] * L[j * m + t];
-        if (i == j) {
-          if (!(s > 1e-12)) return false;
-          L[i * m + i] = std::sqrt(s);
-        } else {
-          L[i * m + j] = s / L[j * m + j];
-        }
-      }
-    }
-    std::vector<double> y(m);
-    out->assign(m, 0.0);
-    for (int i = 0; i < m; ++i) {
-      double s = b[i];
-      for (int t = 0; t < i; ++t) s -= L[i * m + t] * y[t];
-      y[i] = s / L[i * m + i];
-    }
-    for (int i = m - 1; i >= 0; --i) {
-      double s = y[i];
-      for (int t = i + 1; t < m; ++t) s -= L[t * m + i] * (*out)[t];
-      (*out)[i] = s / L[i * m + i];
-    }
-    return true;
+    return SolveLinearLeaf(std::move(A), b, usable, m, config_->linear_lambda, out);
   }
   bool has_nan_ = false;
 };

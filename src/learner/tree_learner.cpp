@@ -49,7 +49,8 @@ bool DeviceHistogramsExceedPool(const Config* c, const Dataset* train) {
 const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, const Config* c,
                              const Dataset* train) {
   if (DeviceHistogramsExceedPool(c, train)) return "per-leaf device histograms above the histogram pool";
-  if (linear_tree) return "linear_tree";
+  // linear leaves: on the device (MFMA Gram systems) within its shape, else the host learner
+  if (linear_tree && !device::LinearOnDevice(c, train, learner_type)) return "linear_tree";
   // (voting runs on the device; its global pass redraws no extra-trees thresholds)
   if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
   // CEGB: the split penalty runs in the device scans, the coupled and lazy feature penalties

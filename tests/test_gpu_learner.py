@@ -471,8 +471,7 @@ def test_device_quantized_regression_tracks_cpu(lgb, gpu_required):
 @pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05, "feature_fraction_bynode": 0.8,
                                     "cegb_penalty_feature_lazy": [0.01, 0.02, 0.03, 0.04, 0.05, 0.06]},
                                    {"monotone_constraints": [1, -1, 0, 0, 0, 0],
-                                    "monotone_constraints_method": "intermediate"},
-                                   {"linear_tree": True, "objective": "regression"}])
+                                    "monotone_constraints_method": "intermediate"}])
 def test_host_policy_over_device_histograms(lgb, gpu_required, rng, extra):
     """Options only the host learners implement run the host split policy over HIP histograms
     (the reference's GPUTreeLearner arrangement); the model matches the CPU learner."""
@@ -991,3 +990,45 @@ def test_extra_trees_on_frontier_matches_cpu(lgb, gpu_required, rng, extra):
         sg = _splits(_trees(bg)[t]["tree_structure"], [])
         assert [s[0] for s in sc] == [s[0] for s in sg], (t, sc[:6], sg[:6])
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("extra", [{}, {"linear_lambda": 0.5, "num_leaves": 15}, {"nan": True}])
+def test_linear_tree_on_device_matches_cpu(lgb, gpu_required, rng, extra):
+    """linear_tree on the device learner: the structure from the frontier engine, each leaf's
+    Gram system [X'HX | X'g] accumulated by the fp64 MFMA kernel over the leaf's rows, solved on
+    the host; the training score updated by the traversal's linear leaf evaluation. Equal to the
+    host linear learner within fp64 round-off (rows with NaN features keep the constant)."""
+    extra = dict(extra)
+    nan = extra.pop("nan", False)
+    n = 20000
+    X = rng.standard_normal((n, 6))
+    z = 1.5 * X[:, 0] - X[:, 1] + 0.7 * X[:, 2] * X[:, 3] + 0.3 * rng.standard_normal(n)
+    if nan:
+        X[rng.random(X.shape) < 0.02] = np.nan
+    kw = {"objective": "regression", "linear_tree": True, "num_leaves": 7}
+    kw.update(extra)
+    bc = _train(lgb, X, z, "cpu", rounds=5, **kw)
+    bg = _train(lgb, X, z, "gpu", rounds=5, gpu_use_dp=True, **kw)
+    assert "host split policy" not in bg.device_name() and "frontier engine" in bg.device_name()
+    tc, tg = _trees(bc), _trees(bg)
+    for t in range(5):
+        assert [s[:2] for s in _splits(tc[t]["tree_structure"], [])] == [s[:2] for s in _splits(tg[t]["tree_structure"], [])]
+    np.testing.assert_allclose(bg.predict(X), bc.predict(X), rtol=1e-4, atol=1e-4)
+    # the device-resident training score (traversal with linear leaves) equals the model's prediction
+    ev = {}
+    bg2 = lgb.train({**kw, "device_type": "gpu", "gpu_use_dp": True, "verbosity": -1, "metric": "l2", "seed": 1,
+                     "min_data_in_leaf": 20, "deterministic": True},
+                    lgb.Dataset(X, z), 5, valid_sets=[lgb.Dataset(X, z)], valid_names=["train"],
+                    callbacks=[lgb.record_evaluation(ev)])
+    np.testing.assert_allclose(ev["train"]["l2"][-1], float(np.mean((bg2.predict(X) - z) ** 2)), rtol=1e-9)
+
+
+def test_linear_tree_wide_branches_take_the_host_policy(lgb, gpu_required, rng):
+    """Leaves that can carry more than 30 branch features (beyond the device Gram tile) train
+    under the host linear learner over HIP histograms."""
+    n = 6000
+    X = rng.standard_normal((n, 40))
+    z = X[:, :5].sum(axis=1) + 0.1 * rng.standard_normal(n)
+    kw = {"objective": "regression", "linear_tree": True, "num_leaves": 48, "min_data_in_leaf": 10}
+    bg = _train(lgb, X, z, "gpu", rounds=2, **kw)
+    assert "host split policy" in bg.device_name()
