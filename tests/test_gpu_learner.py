@@ -1016,10 +1016,10 @@ def test_linear_tree_on_device_matches_cpu(lgb, gpu_required, rng, extra):
     np.testing.assert_allclose(bg.predict(X), bc.predict(X), rtol=1e-4, atol=1e-4)
     # the device-resident training score (traversal with linear leaves) equals the model's prediction
     ev = {}
-    bg2 = lgb.train({**kw, "device_type": "gpu", "gpu_use_dp": True, "verbosity": -1, "metric": "l2", "seed": 1,
-                     "min_data_in_leaf": 20, "deterministic": True},
-                    lgb.Dataset(X, z), 5, valid_sets=[lgb.Dataset(X, z)], valid_names=["train"],
-                    callbacks=[lgb.record_evaluation(ev)])
+    p2 = {**kw, "device_type": "gpu", "gpu_use_dp": True, "verbosity": -1, "metric": "l2", "seed": 1,
+          "min_data_in_leaf": 20, "deterministic": True}
+    ds = lgb.Dataset(X, z, params=p2)
+    bg2 = lgb.train(p2, ds, 5, valid_sets=[ds], valid_names=["train"], callbacks=[lgb.record_evaluation(ev)])
     np.testing.assert_allclose(ev["train"]["l2"][-1], float(np.mean((bg2.predict(X) - z) ** 2)), rtol=1e-9)
 
 
