@@ -2351,7 +2351,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (!frontier_) Log::Fatal("TestFrontierHist: the frontier engine is not enabled for this configuration");
     if (k < 1 || k > fkmax_) Log::Fatal("TestFrontierHist: %d subsets (1..%d)", k, fkmax_);
     const int total = offsets[k];
-    if (total > N_) Log::Fatal("TestFrontierHist: %d rows over the subsets (at most %d)", total, N_);
+    if (idx_[3].size() < static_cast<size_t>(total)) idx_[3].Resize(total);  // (subsets may overlap)
     K_ = 1;
     DeviceSetGradients(g, h, 1);
     TreeParams* tp = pin_tp_.Get(1);
