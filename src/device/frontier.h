@@ -177,6 +177,12 @@ struct FArgs {
   // partition look-back
   unsigned long long* tile_pub;
   unsigned* bar;  // bar[2]: bounded-wait error flag
+  // per-child best split in the scan (scan_best = 1): the last item of an expansion to finish
+  // (completion ticket) takes the arg-max over the features for both children and writes
+  // best / key, so the select's phase A only reads the winners' candidate positions
+  int scan_best;
+  unsigned* scan_ticket;  // [kmax] finished items per expansion (reset by the last one)
+  int* scan_cpos;         // [2 kmax] winning candidate position per child pair, -1: none
   int hist_min_rows, hist_grid;
   int hist_threads;  // 512 or 1024 threads per histogram block
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)

@@ -468,10 +468,30 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   double* hl_full = hs_full + 2 * a.max_bin;
   int* order = reinterpret_cast<int*>(hl_full + 2 * a.max_bin);
   double* ckey = reinterpret_cast<double*>(order + 2 * a.cat_p2);
+  __shared__ int s_last;
   for (int item = blockIdx.x; item < total; item += gridDim.x) {
     const int e = e0 + item / F, f = item - (e - e0) * F;
     const FExp& xr = a.exps[e];
-    if (xr.skip) continue;
+    if (xr.skip) {
+      // (scan_best: the children of a skipped expansion get empty records, once)
+      if (a.scan_best && f == 0 && t < 2) {
+        const int c = t == 0 ? xr.smaller : xr.larger;
+        if (c >= 0) {
+          a.best[c].Reset();
+          SplitKey kz;
+          kz.gain = kMinScore;
+          kz.feature = -1;
+          kz.threshold = 0;
+          kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
+          kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
+          kz.pos = -1;
+          kz.pad2 = 0;
+          a.key[c] = kz;
+        }
+        a.scan_cpos[2 * e + t] = -1;
+      }
+      continue;
+    }
     const int cs = xr.smaller, cl = xr.larger, p = xr.parent;
     const DevFeature fi = a.feat[f];
     const int nbin = fi.num_bin;
@@ -748,6 +768,56 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       }
     }
     __syncthreads();  // LDS reused by the next item
+    if (a.scan_best) {
+      // completion ticket of expansion e: the last of its F items picks both children's best
+      if (t == 0) {
+        __threadfence();  // this item's candidates, visible device-wide before the ticket
+        const unsigned old = atomicAdd(&a.scan_ticket[e], 1u);
+        s_last = old == static_cast<unsigned>(F - 1) ? 1 : 0;
+      }
+      __syncthreads();
+      if (s_last) {
+        __threadfence();
+        if (w < 2) {
+          const int c = w == 0 ? cs : cl;
+          const size_t q = static_cast<size_t>(e) * 2 + w;
+          double bg = kMinScore;
+          int bf = 0x7fffffff, bp = -1;
+          if (c >= 0) {
+            for (int ff = lane; ff < F; ff += 64) {
+              const SplitKey& kk = a.ckey[q * F + ff];
+              if (kk.feature < 0) continue;
+              if (kk.gain > bg || (kk.gain == bg && kk.feature < bf)) {
+                bg = kk.gain;
+                bf = kk.feature;
+                bp = ff;
+              }
+            }
+          }
+          const int src = WaveArgBestLane(bg, bf, 0);
+          bp = ReadLane(bp, src);
+          constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+          constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+          if (c >= 0 && bp >= 0) {
+            const size_t pos = q * F + bp;
+            for (int i = lane; i < kInfoWords + kKeyWords; i += 64) {
+              if (i < kInfoWords) {
+                reinterpret_cast<uint32_t*>(a.best + c)[i] = reinterpret_cast<const uint32_t*>(a.cinfo + pos)[i];
+              } else {
+                reinterpret_cast<uint32_t*>(a.key + c)[i - kInfoWords] = reinterpret_cast<const uint32_t*>(a.ckey + pos)[i - kInfoWords];
+              }
+            }
+          } else if (c >= 0 && lane == 0) {
+            a.best[c].Reset();
+            a.key[c].gain = kMinScore;
+            a.key[c].feature = -1;
+            a.key[c].pos = -1;
+          }
+          if (lane == 0) a.scan_cpos[q] = (c >= 0 && bp >= 0) ? static_cast<int>(q * F + bp) : -1;
+        }
+        if (t == 0) a.scan_ticket[e] = 0u;
+      }
+    }
   }
   FStampEnd(a, rnd, kFStampScan);
 }
@@ -1271,8 +1341,15 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     for (int i = t; i < kprev * F; i += blockDim.x) a.lazy_acc[i] = 0;
     __syncthreads();
   }
-  // ---- A. children of the last round: best over features (all pairs' keys in flight)
-  {
+  // ---- A. children of the last round: best over features (all pairs' keys in flight); with
+  // scan_best the scan's last item per expansion already did it (best / key written, in the
+  // image above): only the winners' candidate positions are read
+  if (a.scan_best && !cegb) {
+    for (int q = t; q < np; q += blockDim.x) {
+      const int pc = s_pc[q];
+      if (pc >= 0) s_cpos[pc - base] = a.scan_cpos[q];
+    }
+  } else {
     double bg[kSelPairs];
     int bf[kSelPairs], bp[kSelPairs], pn[kSelPairs], pd[kSelPairs];
 #pragma unroll
