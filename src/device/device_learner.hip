@@ -33,9 +33,9 @@
 // are captured into hipGraphs (main graph for the predicted round count plus a
 // 4-round continuation graph replayed until the tree is done).
 //
-// SEQUENTIAL engine (feature/voting-parallel, the xGMI data-parallel transport, bynode
-// sampling, extra-trees, the global-scan path for very wide bins): a FIXED kernel
-// sequence per split (kernels: seq_kernels.h, seq_{hist,scan,vote,partition}_kernels.hip):
+// SEQUENTIAL engine (the explicit xGMI transports of the distributed learners, histogram
+// budgets the frontier's select cannot hold in LDS): a FIXED kernel sequence per split
+// (kernels: seq_kernels.h, seq_{hist,scan,vote,partition}_kernels.hip):
 //   partition  best-leaf select from the candidate table, stable partition of the
 //              parent range (decoupled look-back), post-split bookkeeping: ranges,
 //              sums, depth, monotone bounds, smaller / larger child, slot handoff
@@ -45,15 +45,24 @@
 // Every launch has a fixed grid and exits early when the tree is done, so the
 // sequence is captured once into a hipGraph and replayed per tree.
 //
-// Data parallel (tree_learner=data): by default the FRONTIER engine runs on every
-// rank over its own rows, the round's fixed-point accumulators are all-reduced
-// exactly (RCCL uint64 sums; the first half of a round's all-reduce overlaps the
-// second half's histograms on a comm stream), and every rank scans and selects
-// redundantly. With the xGMI transport, the sequential chain pushes each owner its
-// bins (in-kernel exchange over IPC-mapped buffers, or RCCL reduce-scatter), scans
-// only the features it owns and fills one slice of the candidate table that all
-// ranks then read. Voting parallel elects top-k features per child and exchanges
-// only their histograms.
+// Distributed frontier modes (one rank per GPU, exchanges over RCCL or the host-staged
+// rehearsal transport):
+//   data     every rank partitions / histograms its own rows; the round's fixed-point
+//            accumulators are all-reduced exactly (one RCCL uint64 all-reduce per round,
+//            serialised between the histograms and the scans; LGAP_DP_PIPELINE=1 splits it
+//            in halves on a comm stream), and every rank scans and selects redundantly
+//   voting   the local pass (local sums / counts / config), one all-gather of the round's
+//            top-k votes, the election, one exact all-reduce of the elected rows only, and
+//            the global pass over them (PV-Tree per round)
+//   feature  every rank holds all rows and grows the same partition; each scans the
+//            features of the groups it owns and the per-child bests are all-gathered
+// With LGAP_DP_TRANSPORT=xgmi the sequential chain pushes each owner its bins (in-kernel
+// exchange over IPC-mapped buffers), scans only the features it owns and fills one slice of
+// the candidate table that all ranks then read.
+//
+// By-node sampling and extra trees also run on the frontier (masks / random thresholds drawn
+// in the host learner's order); linear_tree leaves are fitted after the structure (fp64 MFMA
+// Gram systems, linear_kernels.hip).
 //
 // After either engine: leaf outputs / renew (leaf_kernels.hip), then the score
 // update walks the new tree in group-bin space (traverse_kernels.hip).
