@@ -1591,6 +1591,8 @@ class DeviceTreeLearner : public TreeLearner {
     }
     facc_.Resize(K * 2 * static_cast<size_t>(TB_));
     facc_.Zero(stream_);  // the scan re-zeroes what it consumes: zero between rounds from here on
+    fpart_ticket_.Resize(1);
+    fpart_ticket_.Zero(stream_);
     fscan_ticket_.Resize(K);
     fscan_ticket_.Zero(stream_);  // (the last item of each expansion re-zeroes its ticket)
     fscan_cpos_.Resize(2 * K);
@@ -1786,6 +1788,8 @@ class DeviceTreeLearner : public TreeLearner {
       const char* e = std::getenv("LGAP_SCAN_BEST");
       a.scan_best = (e == nullptr || e[0] != '0') && !RawCands() && !fvoting_ && !ffeature_ ? 1 : 0;
       a.scan_ticket = fscan_ticket_.get();
+      const char* pt = std::getenv("LGAP_PART_TICKET");
+      a.part_ticket = pt != nullptr && pt[0] == '0' ? nullptr : fpart_ticket_.get();
       a.scan_cpos = fscan_cpos_.get();
     }
     a.xrng = config_->extra_trees ? rng_.get() : nullptr;
@@ -3381,7 +3385,7 @@ class DeviceTreeLearner : public TreeLearner {
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
-  DevBuf<unsigned> fscan_ticket_;
+  DevBuf<unsigned> fscan_ticket_, fpart_ticket_;
   DevBuf<int> fscan_cpos_;
   // linear-leaf trees (FitLinearLeaves / TraverseLinear)
   bool linear_ = false, lin_has_nan_ = false;

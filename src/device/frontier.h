@@ -180,6 +180,11 @@ struct FArgs {
   // per-child best split in the scan (scan_best = 1): the last item of an expansion to finish
   // (completion ticket) takes the arg-max over the features for both children and writes
   // best / key, so the select's phase A only reads the winners' candidate positions
+  // partition tiles by dispatch order (part_ticket != null): each block takes a ticket when it
+  // starts and owns the contiguous tiles [ticket * per, (ticket + 1) * per), so its look-back only
+  // waits on blocks that started before it -- no co-residency assumption (the select / init zero
+  // the counter for the next launch)
+  unsigned* part_ticket;
   int scan_best;
   unsigned* scan_ticket;  // [kmax] finished items per expansion (reset by the last one)
   int* scan_cpos;         // [2 kmax] winning candidate position per child pair, -1: none

@@ -2,7 +2,7 @@
 //
 // Launch shapes (fixed per learner; the work of a round is read on the device):
 //   k_f_init        1 x 256
-//   k_f_partition   resident grid x 256 (decoupled look-back needs co-residency)
+//   k_f_partition   grid x 256 (tiles owned by dispatch ticket: no co-residency needed)
 //   k_f_hist        max(hist_grid, ceil(hist_grid / 2) + kmax) x LDS tiles, 512 threads
 //   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature))
 //   k_f_select      1 x 1024
@@ -132,6 +132,7 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
   }
   for (int i = t; i < a.C; i += blockDim.x) a.nstate[i] = 0;
   for (int f = t; f < a.F; f += blockDim.x) a.spl[f] = 1;
+  if (t == 0 && a.part_ticket != nullptr) *a.part_ticket = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -965,7 +966,9 @@ __device__ __forceinline__ void BlockSumMulti(int* v, int* sh) {
   for (int m = 0; m < M; ++m) v[m] = sh[m * 4] + sh[m * 4 + 1] + sh[m * 4 + 2] + sh[m * 4 + 3];
 }
 
-// A block owns tiles bid + j * G. The first MAXT of them live in registers for the whole
+// A block owns tiles base + j * stride: its ticket's contiguous range (part_ticket), or
+// blockIdx.x + j * gridDim.x (LGAP_PART_TICKET=0, which needs every block resident). The
+// first MAXT of them live in registers for the whole
 // launch: their loads are issued together (row ids, then bins), their counts reduced in one
 // block sum, their look-back sums loaded in one round, their scatter ballots published in one
 // LDS barrier, so a block pays a few memory round trips instead of a few per tile. Tiles
@@ -987,9 +990,22 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
   const unsigned epoch = stp->epoch;
   const int rnd = stp->round;
   FStamp(a, rnd, kFStampPart, 0);
-  const int bid = static_cast<int>(blockIdx.x), G = static_cast<int>(gridDim.x);
-  if (bid >= T) return;
+  const int G = static_cast<int>(gridDim.x);
   const int t = threadIdx.x;
+  // this block's tiles: base + j * stride for base + j * stride < lim (j < MAXT in registers,
+  // the rest one by one). Ticketed: the contiguous range of the block's dispatch ticket.
+  int base = static_cast<int>(blockIdx.x), stride = G, lim = T;
+  if (a.part_ticket != nullptr) {
+    __shared__ int s_vid;
+    if (t == 0) s_vid = static_cast<int>(atomicAdd(a.part_ticket, 1u));
+    __syncthreads();
+    const int per = (T + G - 1) / G;
+    base = s_vid * per;
+    stride = 1;
+    lim = min(T, base + per);
+  }
+  if (base >= lim) return;
+  const int bid = base;
   // the round's expansions (dword-parallel copy) and their categorical sets
   constexpr int kXWords = static_cast<int>(sizeof(FExp) / 4);
   for (int i = t; i < k * kXWords; i += blockDim.x) {
@@ -1030,8 +1046,8 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
   unsigned lbits = 0u, vbits = 0u;  // bit j * ITERS + i: row valid / goes left
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
-    const int tile = bid + j * G;
-    ex[j] = tile < T ? find(tile) : -1;
+    const int tile = bid + j * stride;
+    ex[j] = tile < lim ? find(tile) : -1;
     const int e = ex[j] < 0 ? 0 : ex[j];
     const FExp& x = s_x[e];
     const int pos0 = (tile - x.tile0) * kTile + t;
@@ -1067,11 +1083,11 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
   if (t == 0) {
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
-      if (ex[j] >= 0) FPublish(&a.tile_pub[bid + j * G], epoch, cnt[j]);
+      if (ex[j] >= 0) FPublish(&a.tile_pub[bid + j * stride], epoch, cnt[j]);
     }
   }
   // ---- tiles beyond MAXT: count and publish one by one
-  for (int tile = bid + MAXT * G; tile < T; tile += G) {
+  for (int tile = bid + MAXT * stride; tile < lim; tile += stride) {
     const int e = find(tile);
     const FExp& x = s_x[e];
     const int pos0 = (tile - x.tile0) * kTile + t;
@@ -1093,7 +1109,7 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
   for (int j = 0; j < MAXT; ++j) {
     lb[j] = 0;
     if (ex[j] < 0) continue;
-    lb[j] = FThreadCounts(a, s_x[ex[j]].tile0, bid + j * G, epoch);
+    lb[j] = FThreadCounts(a, s_x[ex[j]].tile0, bid + j * stride, epoch);
   }
   BlockSumMulti<MAXT>(lb, sh);
 #pragma unroll
@@ -1114,7 +1130,7 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
     if (ex[j] < 0) continue;
     const int e = ex[j];
     const FExp& x = s_x[e];
-    const int tile = bid + j * G;
+    const int tile = bid + j * stride;
     const int tt = tile - x.tile0;
     int lbase = lb[j];
     int rbase = tt * kTile - lbase;
@@ -1148,7 +1164,7 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
     if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
   }
   // ---- tiles beyond MAXT: look-back and scatter one by one
-  for (int tile = bid + MAXT * G; tile < T; tile += G) {
+  for (int tile = bid + MAXT * stride; tile < lim; tile += stride) {
     const int e = find(tile);
     const FExp& x = s_x[e];
     int lcur[1] = {FThreadCounts(a, x.tile0, tile, epoch)};
@@ -1982,6 +1998,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       ns_.total_tiles = 0;
     }
     *a.st = ns_;
+    if (a.part_ticket != nullptr) *a.part_ticket = 0u;  // (the next round's partition tickets)
   }
   FStamp(a, rnd, kFStampSel, 6);
   FStampEnd(a, rnd, kFStampSel);
