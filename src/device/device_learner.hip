@@ -424,6 +424,8 @@ class DeviceTreeLearner : public TreeLearner {
 
   void ResetConfig(const Config* config) override {
     config_ = config;
+    fused_grad_ready_ = false;
+    fused_obj_ = nullptr;
     col_sampler_.Init(data_, config_);
     L_ = std::max(2, config_->num_leaves);
     AllocState();
@@ -537,6 +539,7 @@ class DeviceTreeLearner : public TreeLearner {
   std::unique_ptr<Tree> DeviceFitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
                                                 int class_id) override {
     ScopedTimer timer("Device::Refit");
+    fused_grad_ready_ = false;
     if (static_cast<data_size_t>(leaf_pred.size()) != N_ || gh_.size() < static_cast<size_t>(class_id + 1) * N_ ||
         old_tree->is_linear()) {
       return nullptr;  // (linear trees: the host linear learner's refit, FitByExistingTree)
@@ -692,6 +695,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceInitScore(const std::vector<double>& host_score, int num_tree_per_iter) override {
+    fused_grad_ready_ = false;
     K_ = num_tree_per_iter;
     score_.Resize(static_cast<size_t>(K_) * N_);
     score_.Upload(host_score, stream_);
@@ -703,6 +707,15 @@ class DeviceTreeLearner : public TreeLearner {
   void DeviceComputeGradients(const ObjectiveFunction* obj) override {
     ScopedTimer timer("Device::ComputeGradients");
     PrepareObjective(obj);
+    const bool pointwise = obj->device_kind() == DeviceGradKind::kPointwise && K_ == 1;
+    if (pointwise && fused_grad_ready_ && fused_obj_ == obj) {
+      // the last score update already computed them (LaunchTraverseGrad): nothing has touched
+      // the score or the gradients since
+      fused_grad_ready_ = false;
+      return;
+    }
+    fused_grad_ready_ = false;
+    fused_obj_ = pointwise ? obj : nullptr;  // (the next score update may compute them fused)
     switch (obj->device_kind()) {
       case DeviceGradKind::kPointwise:
         LaunchPointwiseGrad(*obj->pointwise(), score_.get(), label_.get(), weight_.size() ? weight_.get() : nullptr,
@@ -740,6 +753,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceSetGradients(const score_t* g, const score_t* h, int num_class) override {
+    fused_grad_ready_ = false;
+    fused_obj_ = nullptr;
     const size_t n = static_cast<size_t>(num_class) * N_;
     if (gh_.size() < n) gh_.Resize(n);
     float2* p = pin_gh_.Get(n);
@@ -768,6 +783,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceAddConstant(double v, int k) override {
+    fused_grad_ready_ = false;
     LaunchAddConstant(score_.get() + static_cast<size_t>(k) * N_, N_, v, stream_);
   }
 
@@ -787,6 +803,7 @@ class DeviceTreeLearner : public TreeLearner {
 
   void DeviceAddTreeToScore(const Tree* tree, int k) override {
     ScopedTimer timer("Device::AddTreeToScore");
+    fused_grad_ready_ = false;
     double* s = score_.get() + static_cast<size_t>(k) * N_;
     if (tree->num_leaves() <= 1) {
       if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, N_, tree->LeafOutput(0), stream_);
@@ -818,7 +835,16 @@ class DeviceTreeLearner : public TreeLearner {
       return;
     }
     last_trained_ = nullptr;
+    // single-class pointwise objectives: the traversal also computes the next iteration's
+    // gradients at the updated score (one pass over the rows; LGAP_FUSE_GRAD=0 keeps two)
+    static const bool fuse_ok = [] {
+      const char* e = std::getenv("LGAP_FUSE_GRAD");
+      return e == nullptr || e[0] != '0';
+    }();
+    fuse_pending_ = fuse_ok && fused_obj_ != nullptr && K_ == 1 && k == 0 && label_.size() >= static_cast<size_t>(N_);
     TraverseTree(tree, rowbins_.get(), N_, s);
+    fused_grad_ready_ = fuse_pending_ && fuse_done_;
+    fuse_pending_ = fuse_done_ = false;
   }
 
   // score[i] += tree(row i) over packed rows of the training layout (training or validation set)
@@ -960,6 +986,18 @@ class DeviceTreeLearner : public TreeLearner {
                          reinterpret_cast<const TCat*>(db + node_bytes),
                          reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                          reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
+      return;
+    }
+    if (fuse_pending_ && rowbins == rowbins_.get() && n == N_ && fused_obj_ != nullptr) {
+      const PointwiseParams& pp = *fused_obj_->pointwise();
+      const uint32_t* rb = nib_ ? rowbins4_.get() : rowbins;
+      LaunchTraverseGrad(rb, nib_ ? stride4_dw_ : stride_dw_, nib_ ? 0 : width_, n, reinterpret_cast<const TNode*>(db), nn,
+                         reinterpret_cast<const TCat*>(db + node_bytes),
+                         reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
+                         reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, pp, label_.get(),
+                         weight_.size() ? weight_.get() : nullptr, aux_.size() ? aux_.get() : nullptr, gh_.get(),
+                         num_cu_, stream_);
+      fuse_done_ = true;
       return;
     }
     if (nib_ && rowbins == rowbins_.get() && n == N_) {
@@ -3386,6 +3424,9 @@ class DeviceTreeLearner : public TreeLearner {
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
   DevBuf<unsigned> fscan_ticket_, fpart_ticket_;
+  // score update fused with the next pointwise gradients (DeviceAddTreeToScore)
+  const ObjectiveFunction* fused_obj_ = nullptr;  // pointwise objective of the last gradient pass
+  bool fused_grad_ready_ = false, fuse_pending_ = false, fuse_done_ = false;
   DevBuf<int> fscan_cpos_;
   // linear-leaf trees (FitLinearLeaves / TraverseLinear)
   bool linear_ = false, lin_has_nan_ = false;

@@ -15,6 +15,8 @@
 
 #include <cstdint>
 
+#include "lgap/pointwise.h"
+
 namespace lgap {
 namespace device {
 
@@ -45,6 +47,14 @@ void LaunchPackNibbles(const uint32_t* rowbins, int stride_dw, int n, int groups
 void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
                     const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,
                     int num_cu, hipStream_t s);
+
+// the traversal fused with the next iteration's pointwise gradients (lgap/pointwise.h): score[i]
+// += leaf value, then gh[i] = gradient / hessian at the new score (one pass over the rows instead
+// of a traversal and a gradient kernel)
+void LaunchTraverseGrad(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
+                        const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves,
+                        double* score, const PointwiseParams& p, const float* label, const float* weight,
+                        const float* aux, float2* gh, int num_cu, hipStream_t s);
 
 // linear-leaf trees (linear_kernels.h LinearLeaves): score[i] += the leaf's linear model at
 // row i's raw values (its constant output when one of them is NaN); 8- / 16-bit rows

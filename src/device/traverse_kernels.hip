@@ -9,6 +9,7 @@
 
 #include "device/hip_common.h"
 #include "device/linear_kernels.h"
+#include "lgap/pointwise.h"
 
 namespace lgap {
 namespace device {
@@ -46,12 +47,23 @@ __device__ __forceinline__ double LinearValue(const LinearLeaves& lin, int leaf,
   return v;
 }
 
-template <int W, bool LIN>
+// the next iteration's pointwise gradients from the updated score (GRAD instantiation of
+// k_traverse: the score update of the last tree deferred into the gradient pass)
+struct GradEpilogue {
+  PointwiseParams p;
+  const float* label;
+  const float* weight;  // nullptr: unweighted
+  const float* aux;     // MAPE label weights, nullptr: none
+  float2* gh;
+};
+
+template <int W, bool LIN, bool GRAD = false>
 __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restrict__ rowbins, int stride_dw, int n,
                                                         const TNode* __restrict__ nodes, int num_nodes,
                                                         const TCat* __restrict__ cats, const uint32_t* __restrict__ cat_bits,
                                                         const double* __restrict__ leaf_value, int num_leaves,
-                                                        double* __restrict__ score, LinearLeaves lin) {
+                                                        double* __restrict__ score, LinearLeaves lin,
+                                                        GradEpilogue ge = GradEpilogue{}) {
   extern __shared__ __align__(16) unsigned char lds[];
   TNode* s_nodes = reinterpret_cast<TNode*>(lds);
   double* s_leaf = reinterpret_cast<double*>(lds + ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)));
@@ -125,7 +137,15 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
       const int r = t + j * kTThreads;
       if (r < rows) {
         const double lv = LIN ? LinearValue(lin, ~node[j], base + r, s_leaf[~node[j]]) : s_leaf[~node[j]];
-        score[base + r] = sc[j] + lv;
+        const double ns = sc[j] + lv;
+        score[base + r] = ns;
+        if (GRAD) {
+          const long long i = base + r;
+          score_t g, h;
+          PointwiseGradient(ge.p, ns, static_cast<double>(ge.label[i]), ge.weight ? static_cast<double>(ge.weight[i]) : 1.0,
+                            ge.weight != nullptr, ge.aux ? static_cast<double>(ge.aux[i]) : 0.0, &g, &h);
+          ge.gh[i] = make_float2(g, h);
+        }
       }
     }
   }
@@ -249,6 +269,34 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
   } else {
     k_traverse<2, false><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
                                                      num_leaves, score, none);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchTraverseGrad(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
+                        const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves,
+                        double* score, const PointwiseParams& p, const float* label, const float* weight,
+                        const float* aux, float2* gh, int num_cu, hipStream_t s) {
+  if (n <= 0) return;
+  const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + ((sizeof(double) * num_leaves + 15) & ~size_t(15)) +
+                     (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
+  const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
+  LinearLeaves none{};
+  GradEpilogue ge;
+  ge.p = p;
+  ge.label = label;
+  ge.weight = weight;
+  ge.aux = aux;
+  ge.gh = gh;
+  if (width == 0) {
+    k_traverse<0, false, true><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits,
+                                                           leaf_value, num_leaves, score, none, ge);
+  } else if (width == 1) {
+    k_traverse<1, false, true><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits,
+                                                           leaf_value, num_leaves, score, none, ge);
+  } else {
+    k_traverse<2, false, true><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits,
+                                                           leaf_value, num_leaves, score, none, ge);
   }
   HIP_CHECK(hipGetLastError());
 }
