@@ -837,10 +837,8 @@ class DeviceTreeLearner : public TreeLearner {
     last_trained_ = nullptr;
     // single-class pointwise objectives: the traversal also computes the next iteration's
     // gradients at the updated score (one pass over the rows; LGAP_FUSE_GRAD=0 keeps two)
-    static const bool fuse_ok = [] {
-      const char* e = std::getenv("LGAP_FUSE_GRAD");
-      return e == nullptr || e[0] != '0';
-    }();
+    const char* fe = std::getenv("LGAP_FUSE_GRAD");
+    const bool fuse_ok = fe == nullptr || fe[0] != '0';
     fuse_pending_ = fuse_ok && fused_obj_ != nullptr && K_ == 1 && k == 0 && label_.size() >= static_cast<size_t>(N_);
     TraverseTree(tree, rowbins_.get(), N_, s);
     fused_grad_ready_ = fuse_pending_ && fuse_done_;
