@@ -1730,6 +1730,11 @@ class DeviceTreeLearner : public TreeLearner {
     a.slots = fslots_.get();
     a.acc = reinterpret_cast<unsigned long long*>(facc_.get());
     a.ghmax = ghmax_.get();
+    a.sum_mult = distributed_ && !ffeature_ ? std::max(1, P_) : 1;  // (max-reduced local sums)
+    {
+      const char* e = std::getenv("LGAP_FIXED_SUMBOUND");
+      a.sum_bound = e == nullptr || std::atoi(e) != 0;
+    }
     a.forced = fnum_forced_ > 0 ? fforced_.get() : nullptr;
     a.num_forced = fnum_forced_;
     a.fbest = ffbest_;
@@ -1974,7 +1979,7 @@ class DeviceTreeLearner : public TreeLearner {
       if (distributed_) {
         // global root sums and gradient maxima (the fixed-point scales must agree on all ranks)
         AllreduceSumF64(reinterpret_cast<double*>(flsum_), 2, stream_);
-        AllreduceMaxU32(ghmax_.get(), 2, stream_);
+        AllreduceMaxU32(ghmax_.get(), 4, stream_);
       }
       LaunchFrontierHist(fa, FrontierHistLds(), stream_);
       if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
@@ -2420,15 +2425,20 @@ class DeviceTreeLearner : public TreeLearner {
     tp->root_count = tp->root_gcount = N_;
     tp->spec_alpha = 1.f;
     HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
-    float mg = 0.f, mh = 0.f;
+    // the scale bounds of k_root_final: max |value| and sum |value| (rounded up)
+    float bnd[4] = {0.f, 0.f, 0.f, 0.f};
+    double sg = 0.0, sh = 0.0;
     for (int i = 0; i < N_; ++i) {
-      mg = std::max(mg, std::fabs(g[i]));
-      mh = std::max(mh, std::fabs(h[i]));
+      bnd[0] = std::max(bnd[0], std::fabs(g[i]));
+      bnd[1] = std::max(bnd[1], std::fabs(h[i]));
+      sg += std::fabs(static_cast<double>(g[i]));
+      sh += std::fabs(static_cast<double>(h[i]));
     }
-    unsigned* hm = pin_max_.Get(2);
-    std::memcpy(&hm[0], &mg, 4);
-    std::memcpy(&hm[1], &mh, 4);
-    HIP_CHECK(hipMemcpyAsync(ghmax_.get(), hm, 8, hipMemcpyHostToDevice, stream_));
+    bnd[2] = std::nextafter(static_cast<float>(sg * (1.0 + 0x1p-20)), INFINITY);
+    bnd[3] = std::nextafter(static_cast<float>(sh * (1.0 + 0x1p-20)), INFINITY);
+    unsigned* hm = pin_max_.Get(4);
+    std::memcpy(hm, bnd, 16);
+    HIP_CHECK(hipMemcpyAsync(ghmax_.get(), hm, 16, hipMemcpyHostToDevice, stream_));
     if (config_->use_quantized_grad) QuantizeGradients(0);
     idx_[3].Upload(rows, total, stream_);
     FState st;
@@ -2457,13 +2467,10 @@ class DeviceTreeLearner : public TreeLearner {
     facc_.Zero(stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
     // the kernel's global scale (frontier_kernels.hip GlobalScaleExp)
-    auto scale_exp = [&](float m) {
-      if (!(m > 0.f)) return 0;
-      int e;
-      (void)std::frexp(4611686018427387904.0 / (static_cast<double>(N_) * m), &e);
-      return e - 1;
-    };
-    const double ig = fa.quant ? 1.0 : std::ldexp(1.0, -scale_exp(mg)), ih = fa.quant ? 1.0 : std::ldexp(1.0, -scale_exp(mh));
+    constexpr double k62 = 4611686018427387904.0;
+    const float sb2 = fa.sum_bound ? bnd[2] : INFINITY, sb3 = fa.sum_bound ? bnd[3] : INFINITY;
+    const double ig = fa.quant ? 1.0 : std::ldexp(1.0, -FixedPointExp(k62, N_, bnd[0], sb2));
+    const double ih = fa.quant ? 1.0 : std::ldexp(1.0, -FixedPointExp(k62, N_, bnd[1], sb3));
     for (int e = 0; e < k; ++e) {
       for (int b = 0; b < TB_; ++b) {
         const size_t o = (static_cast<size_t>(e) * TB_ + b) * pw;
@@ -2968,14 +2975,14 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t o_tp = lay.Add<TreeParams>(1), o_ctl = lay.Add<Ctl>(2), o_range = lay.Add<LeafRange>(L),
                  o_lsum = lay.Add<double2>(L), o_lout = lay.Add<double>(L), o_gcount = lay.Add<int>(L),
                  o_depth = lay.Add<int>(L), o_slot = lay.Add<int>(L), o_bounds = lay.Add<LeafBounds>(L),
-                 o_best = lay.Add<SplitInfo>(L), o_rec = lay.Add<SplitRec>(L), o_ghmax = lay.Add<unsigned>(2),
+                 o_best = lay.Add<SplitInfo>(L), o_rec = lay.Add<SplitRec>(L), o_ghmax = lay.Add<unsigned>(4),
                  o_spl = lay.Add<uint8_t>(L * F_), o_tcnt = lay.Add<int>(max_tiles_), o_toff = lay.Add<int>(max_tiles_),
                  o_used = lay.Add<uint8_t>(std::max(F_, 1)), o_byn = lay.Add<uint8_t>(use_bynode_ ? 2 * L * F_ : 1),
                  o_rng = lay.Add<unsigned>(std::max(F_, 1)), o_feat = lay.Add<DevFeature>(h_feats_.size()),
                  o_gst = lay.Add<int>(h_gstart_.size()), o_tiles = lay.Add<HistTile>(h_tiles_.size()),
                  o_icf = lay.Add<unsigned long long>(std::max(F_, 1)), o_icl = lay.Add<unsigned long long>(L),
                  o_qmax = lay.Add<unsigned>(2), o_tsum = lay.Add<double2>(L),
-                 o_rpart = lay.Add<double>(4 * static_cast<size_t>(std::max(1, 4 * num_cu_))),
+                 o_rpart = lay.Add<double>(6 * static_cast<size_t>(std::max(1, 4 * num_cu_))),
                  o_bar = lay.Add<unsigned>(4), o_lkey = lay.Add<SplitKey>(L),
                  o_tpub = lay.Add<unsigned long long>(max_tiles_), o_xcnt = lay.Add<unsigned>(4),
                  o_own = lay.Add<int>(Fmax_), o_binlo = lay.Add<int>(P_ + 1);
@@ -2992,7 +2999,7 @@ class DeviceTreeLearner : public TreeLearner {
     bounds_.Attach(reinterpret_cast<LeafBounds*>(base + o_bounds), L);
     best_.Attach(reinterpret_cast<SplitInfo*>(base + o_best), L);
     rec_.Attach(reinterpret_cast<SplitRec*>(base + o_rec), L);
-    ghmax_.Attach(reinterpret_cast<unsigned*>(base + o_ghmax), 2);
+    ghmax_.Attach(reinterpret_cast<unsigned*>(base + o_ghmax), 4);
     splittable_.Attach(reinterpret_cast<uint8_t*>(base + o_spl), L * F_);
     tile_cnt_.Attach(reinterpret_cast<int*>(base + o_tcnt), max_tiles_);
     tile_off_.Attach(reinterpret_cast<int*>(base + o_toff), max_tiles_);
@@ -3006,7 +3013,7 @@ class DeviceTreeLearner : public TreeLearner {
     ic_leaf_.Attach(reinterpret_cast<unsigned long long*>(base + o_icl), L);
     qmax_.Attach(reinterpret_cast<unsigned*>(base + o_qmax), 2);
     true_sums_.Attach(reinterpret_cast<double2*>(base + o_tsum), L);
-    root_part_.Attach(reinterpret_cast<double*>(base + o_rpart), 4 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
+    root_part_.Attach(reinterpret_cast<double*>(base + o_rpart), 6 * static_cast<size_t>(std::max(1, 4 * num_cu_)));
     bar_.Attach(reinterpret_cast<unsigned*>(base + o_bar), 4);
     leaf_key_.Attach(reinterpret_cast<SplitKey*>(base + o_lkey), L);
     tile_pub_.Attach(reinterpret_cast<unsigned long long*>(base + o_tpub), max_tiles_);

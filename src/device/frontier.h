@@ -56,6 +56,21 @@ constexpr int kFrontierIdx = kFrontierBufs + 1;    // index buffers by id: depth
 constexpr int kFrontierRoundCap = 64;  // rounds with their own expansion cap (later rounds: kmax)
 constexpr int kFrontierMaxNodes = 4096;  // computed-node capacity of the select's LDS image
 
+// Fixed-point exponent e of a sum over `rows` rows of values with max |v| = vmax and
+// sum |v| <= vsum over ALL rows: the largest e with 2^e * min(rows * vmax, vsum) <= limit,
+// so no partial sum over any subset of those rows can exceed `limit` in magnitude. The
+// sum bound is what keeps heavy-tailed gradients (max|g| >> typical |g|) resolved: with
+// rows * max alone, one outlier in 10M rows sets every row's quantum. 0 for a zero bound.
+// (Shared by the kernels and the host test hooks, which must agree on the scale.)
+__host__ __device__ inline int FixedPointExp(double limit, double rows, float vmax, float vsum) {
+  double b = rows * static_cast<double>(vmax);
+  if (static_cast<double>(vsum) < b) b = static_cast<double>(vsum);
+  if (!(b > 0.0)) return 0;
+  int e;
+  (void)frexp(limit / b, &e);
+  return e - 1;
+}
+
 // entries of the select's sort of the alive nodes: a power of two >= C (C <= kFrontierMaxNodes)
 __host__ __device__ inline int FrontierSortCap(int C) {
   int p = 64;
@@ -157,7 +172,9 @@ struct FArgs {
   // histograms
   double* slots;              // [C][2 TB] per-node histograms (stored bins, fp64)
   unsigned long long* acc;    // [kmax][2 TB] per-expansion fixed-point accumulators (zero between rounds)
-  const unsigned* ghmax;      // float bits of max|g|, max|h| over the root rows
+  const unsigned* ghmax;      // float bits of max|g|, max|h|, sum|g|, sum|h| over the root rows
+  int sum_mult;               // ranks whose root rows the global sums span (row-sharded DP / voting), else 1
+  int sum_bound;              // use the sum|value| bounds (LGAP_FIXED_SUMBOUND=0: max only, the round-3 scale)
   // forced splits: the list, and per node the forced split at its threshold (scan) and its
   // split predicate (for the expansion that applies it)
   const FForced* forced;

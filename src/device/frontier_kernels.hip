@@ -55,15 +55,16 @@ __device__ __forceinline__ int Pow2Exp(double x) {
 }
 
 // Global fixed-point exponents of the tree: every accumulator holds value * 2^E with
-// 2^E <= 2^62 / (root rows * max|value|), so no sum over any subset of the root's rows can
-// overflow an int64 and every partial of every block, expansion and rank is EXACT integer
-// arithmetic at one shared scale (deterministic and order free).
+// 2^E <= 2^62 / min(root rows * max|value|, sum|value|), so no sum over any subset of the
+// root's rows can overflow an int64 and every partial of every block, expansion and rank is
+// EXACT integer arithmetic at one shared scale (deterministic and order free). Row-sharded
+// ranks max-reduce their local sums: the global sum is at most sum_mult times that.
 __device__ __forceinline__ void GlobalScaleExp(const FArgs& a, int* eg, int* eh) {
   const double n = static_cast<double>(a.tp->root_gcount > 0 ? a.tp->root_gcount : 1);
-  const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
   constexpr double k62 = 4611686018427387904.0;
-  *eg = gmax > 0.f ? Pow2Exp(k62 / (n * gmax)) : 0;
-  *eh = hmax > 0.f ? Pow2Exp(k62 / (n * hmax)) : 0;
+  const float m = a.sum_bound ? static_cast<float>(a.sum_mult > 1 ? a.sum_mult : 1) : INFINITY;
+  *eg = FixedPointExp(k62, n, __uint_as_float(a.ghmax[0]), __uint_as_float(a.ghmax[2]) * m);
+  *eh = FixedPointExp(k62, n, __uint_as_float(a.ghmax[1]), __uint_as_float(a.ghmax[3]) * m);
 }
 
 // Quantized training: the value of one g / h level (must match k_quantize in
@@ -354,11 +355,13 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     }
     return;
   }
-  const float gmax = __uint_as_float(a.ghmax[0]), hmax = __uint_as_float(a.ghmax[1]);
+  // block scale: 2^30 / min(block rows * max, this rank's sum of |value| over all its rows)
   const double rows_in_block = static_cast<double>(re - rb > 0 ? re - rb : 1);
   constexpr double k30 = 1073741824.0;
-  const int bg = gmax > 0.f ? Pow2Exp(k30 / (rows_in_block * gmax)) : 0;
-  const int bh = hmax > 0.f ? Pow2Exp(k30 / (rows_in_block * hmax)) : 0;
+  const float sbg = a.sum_bound ? __uint_as_float(a.ghmax[2]) : INFINITY;
+  const float sbh = a.sum_bound ? __uint_as_float(a.ghmax[3]) : INFINITY;
+  const int bg = FixedPointExp(k30, rows_in_block, __uint_as_float(a.ghmax[0]), sbg);
+  const int bh = FixedPointExp(k30, rows_in_block, __uint_as_float(a.ghmax[1]), sbh);
   const float sg = ldexpf(1.f, bg), sh = ldexpf(1.f, bh);
   const int words = MODE != 1 ? tile.nbins : 2 * tile.nbins;
   unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);

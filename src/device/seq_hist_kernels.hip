@@ -139,8 +139,7 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
     r.pad = 0;
     a.range[0] = r;
     a.lsum[0] = make_double2(0.0, 0.0);
-    a.ghmax[0] = 0u;
-    a.ghmax[1] = 0u;
+    for (int j = 0; j < 4; ++j) a.ghmax[j] = 0u;
     a.gcount[0] = tp.root_gcount;
     a.depth[0] = 0;
     a.lout[0] = 0.0;
@@ -161,79 +160,78 @@ __global__ __launch_bounds__(kNodeThreads) void k_init_tree(Args a) {
 
 // Root statistics in two steps: per-block partials (no atomics: 1024 blocks x
 // device-scope fp64 atomics on one address serialised to ~97 us), then one block
-// folds them and writes lsum[0] and the histogram scale maxima.
+// folds them and writes lsum[0] and the histogram scale bounds (max|g|, max|h|, and
+// sum|g|, sum|h| rounded up: frontier.h FixedPointExp).
+constexpr int kRootStats = 6;  // sum g, sum h, max|g|, max|h|, sum|g|, sum|h|
+
+__device__ __forceinline__ double RootFold(int i, double x, double y) { return i == 2 || i == 3 ? fmax(x, y) : x + y; }
+__device__ __forceinline__ void RootWaveFold(double* v) {
+#pragma unroll
+  for (int j = 0; j < kRootStats; ++j) {
+    if (j == 2 || j == 3) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v[j] = fmax(v[j], __shfl_xor(v[j], o, kWave));
+    } else {
+      v[j] = WaveSum(v[j]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kRootThreads) void k_root_sums(Args a) {
-  __shared__ double sh[4][kRootThreads / 64];
+  __shared__ double sh[kRootStats][kRootThreads / 64];
   const TreeParams tp = *a.tp;
   const float2* gh = a.gh + static_cast<size_t>(tp.cls) * a.N;
-  double g = 0.0, h = 0.0;
-  float mg = 0.f, mh = 0.f;
+  double v[kRootStats] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const int stride = gridDim.x * blockDim.x;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tp.root_count; i += stride) {
-    const float2 v = gh[RowAt(a, tp.root_buf, i)];
-    g += v.x;
-    h += v.y;
-    mg = fmaxf(mg, fabsf(v.x));
-    mh = fmaxf(mh, fabsf(v.y));
+    const float2 x = gh[RowAt(a, tp.root_buf, i)];
+    v[0] += x.x;
+    v[1] += x.y;
+    v[2] = fmax(v[2], fabs(static_cast<double>(x.x)));
+    v[3] = fmax(v[3], fabs(static_cast<double>(x.y)));
+    v[4] += fabs(static_cast<double>(x.x));
+    v[5] += fabs(static_cast<double>(x.y));
   }
-  g = WaveSum(g);
-  h = WaveSum(h);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
-    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
-  }
+  RootWaveFold(v);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    sh[0][w] = g;
-    sh[1][w] = h;
-    sh[2][w] = mg;
-    sh[3][w] = mh;
+#pragma unroll
+    for (int j = 0; j < kRootStats; ++j) sh[j][w] = v[j];
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
-    double v = sh[threadIdx.x][0];
-    for (int i = 1; i < kRootThreads / 64; ++i) {
-      v = threadIdx.x < 2 ? v + sh[threadIdx.x][i] : fmax(v, sh[threadIdx.x][i]);
-    }
-    a.root_part[4 * blockIdx.x + threadIdx.x] = v;
+  if (threadIdx.x < kRootStats) {
+    const int j = threadIdx.x;
+    double x = sh[j][0];
+    for (int i = 1; i < kRootThreads / 64; ++i) x = RootFold(j, x, sh[j][i]);
+    a.root_part[kRootStats * blockIdx.x + j] = x;
   }
 }
 
 __global__ __launch_bounds__(kRootThreads) void k_root_final(Args a, int nblocks) {
-  __shared__ double sh[4][kRootThreads / 64];
-  double g = 0.0, h = 0.0, mg = 0.0, mh = 0.0;
+  __shared__ double sh[kRootStats][kRootThreads / 64];
+  double v[kRootStats] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
-    g += a.root_part[4 * b];
-    h += a.root_part[4 * b + 1];
-    mg = fmax(mg, a.root_part[4 * b + 2]);
-    mh = fmax(mh, a.root_part[4 * b + 3]);
-  }
-  g = WaveSum(g);
-  h = WaveSum(h);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mg = fmax(mg, __shfl_xor(mg, o, kWave));
-    mh = fmax(mh, __shfl_xor(mh, o, kWave));
+    for (int j = 0; j < kRootStats; ++j) v[j] = RootFold(j, v[j], a.root_part[kRootStats * b + j]);
   }
+  RootWaveFold(v);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    sh[0][w] = g;
-    sh[1][w] = h;
-    sh[2][w] = mg;
-    sh[3][w] = mh;
+#pragma unroll
+    for (int j = 0; j < kRootStats; ++j) sh[j][w] = v[j];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int i = 1; i < kRootThreads / 64; ++i) {
-      g += sh[0][i];
-      h += sh[1][i];
-      mg = fmax(mg, sh[2][i]);
-      mh = fmax(mh, sh[3][i]);
+#pragma unroll
+      for (int j = 0; j < kRootStats; ++j) v[j] = RootFold(j, v[j], sh[j][i]);
     }
-    a.lsum[0] = make_double2(g, h);
-    a.ghmax[0] = __float_as_uint(static_cast<float>(mg));
-    a.ghmax[1] = __float_as_uint(static_cast<float>(mh));
+    a.lsum[0] = make_double2(v[0], v[1]);
+    a.ghmax[0] = __float_as_uint(static_cast<float>(v[2]));
+    a.ghmax[1] = __float_as_uint(static_cast<float>(v[3]));
+    // (the fp64 sums of |value| are exact to ~1e-9 relative: a 2^-20 margin, rounded up)
+    a.ghmax[2] = __float_as_uint(__double2float_ru(v[4] * (1.0 + 0x1p-20)));
+    a.ghmax[3] = __float_as_uint(__double2float_ru(v[5] * (1.0 + 0x1p-20)));
   }
 }
 

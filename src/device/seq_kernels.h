@@ -95,7 +95,7 @@ struct Args {
   double* staging;
   float* staging_f;  // data-parallel all-reduce row of the fp32 (default) histogram path
   void* hist_slab;
-  unsigned* ghmax;  // float bits of max|g|, max|h| over the root rows
+  unsigned* ghmax;  // float bits of max|g|, max|h|, sum|g|, sum|h| over the root rows
   uint8_t* splittable;
   int* tile_cnt;
   int* tile_off;
@@ -116,7 +116,7 @@ struct Args {
   // ic_leaf[leaf] = sets that hold every feature on the leaf's branch
   const unsigned long long* ic_feat;
   unsigned long long* ic_leaf;
-  double* root_part;  // per-block (sum g, sum h, max|g|, max|h|) of k_root_sums
+  double* root_part;  // per-block (sum g, sum h, max|g|, max|h|, sum|g|, sum|h|) of k_root_sums
   unsigned* bar;      // {-, -, error flag of k_partition's bounded waits}
   SplitKey* leaf_key;  // [L] compact best split per leaf (next to best)
   unsigned long long* tile_pub;  // k_partition tile counts tagged with the split epoch
