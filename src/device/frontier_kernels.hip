@@ -1658,11 +1658,13 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         // after OnSplit): re-score from their raw candidates when an event came since. With
         // by-node sampling always: the children's masks are the next two draws (smaller child
         // first, as the host's FindBestSplits), unless they are not scanned at all (max_depth /
-        // min_data: the host draws nothing for them either)
+        // min_data, or the tree's last split: the host's loop ends before scanning them and
+        // draws nothing for them either)
         const uint8_t* cmask[2] = {nullptr, nullptr};
         if (a.bynode != nullptr) {
           const int gl = a.nodes[left].gcount, gr = a.nodes[left + 1].gcount, md = a.sp.min_data_in_leaf;
-          const bool skip = (a.max_depth > 0 && s_dep[left] >= a.max_depth) || (gl < 2 * md && gr < 2 * md);
+          const bool skip = nl + 1 >= L || (a.max_depth > 0 && s_dep[left] >= a.max_depth) ||
+                            (gl < 2 * md && gr < 2 * md);
           if (!skip) {
             const bool left_smaller = gl < gr;
             cmask[left_smaller ? 0 : 1] = a.bynode + static_cast<size_t>(byn) * F;
