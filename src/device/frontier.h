@@ -122,6 +122,8 @@ struct FExp {
   int h_buf, h_start, h_count;  // the smaller child's local rows
   int forced;                // the split is forced split `forced` (FForced index), -1: the node's best
   int feature;               // inner feature of the split (-1: the root pseudo-expansion)
+  int last;                  // the tree's last split (the node the replay waits for, at num_leaves - 1
+                             // leaves): its children are never scanned (as in the host's loop)
 };
 
 struct FState {

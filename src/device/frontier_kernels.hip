@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
     x.h_count = tp.root_count;
     x.forced = -1;
     x.feature = -1;
+    x.last = 0;
     a.exps[0] = x;
     a.bounds[0] = LeafBounds();
     if (a.ic) a.ic[0] = ~0ull;
@@ -942,7 +943,7 @@ __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
   // min_data / max_depth, as the host learner's ForceSplits does); the scan keeps their
   // regular candidates within max_depth
   const bool forced_child = nl.fidx >= 0 || nr.fidx >= 0;
-  const bool skip = !forced_child && ((a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2));
+  const bool skip = x.last || (!forced_child && ((a.max_depth > 0 && dep >= a.max_depth) || (grc < md * 2 && glc < md * 2)));
   const bool left_smaller = glc < grc;
   FExp* xo = a.exps + e;
   xo->skip = skip ? 1 : 0;
@@ -1967,6 +1968,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         x.h_buf = x.h_start = x.h_count = 0;
         x.forced = p == s_blocked && s_bforced ? s_fidx[p] : -1;
         x.feature = kk.feature;
+        x.last = p == s_blocked && nl + 1 >= L ? 1 : 0;
         a.exps[lane] = x;
         a.nodes[p].left = cid_next + 2 * lane;
         a.nstate[p] = s_st[p] | kNodeExpanded;
