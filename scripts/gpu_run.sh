@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun call, parameterised: each named step runs under its own time limit and the call
 # stops at the first failing step (no GPU work after a fault, abort or time-out).
-#   bash scripts/gpu_run.sh tests:<pytest files>[|<-k expression>] | smoke | bench:<bench args> | prof:<bench args> | py:<script args> ...
+#   bash scripts/gpu_run.sh tests:<pytest files>[|<-k expression>] | smoke | bench:<bench args> | prof:<bench args> | py:<script args> | sh:<command> ...
 # e.g. bash scripts/gpu_run.sh "tests:tests/test_device_metrics.py" "bench:--steps 40 --warmup 3"
 set -u
 OUT=gpurun_out
@@ -26,6 +26,7 @@ for step in "$@"; do
     prof)  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof$i -o run -- python3 bench.py $arg > $log 2>&1 &&
              python scripts/prof_summary.py $OUT/prof$i "bench.py $arg" 12 > $OUT/prof${i}_summary.md 2>&1 && rm -rf $OUT/prof$i ;;
     py)    timeout -k 10 600 python -u $arg > $log 2>&1 ;;
+    sh)    timeout -k 10 600 bash -c "$arg" > $log 2>&1 ;;
     # three counter passes (one per block budget: SQ / TCC fetch / TCC write), each in its own
     # run, summarised per kernel by scripts/pmc_summary.py; <args>: a python script and its
     # arguments (e.g. pmc:bench.py --steps 3 --warmup 1)

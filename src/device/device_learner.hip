@@ -1826,11 +1826,16 @@ class DeviceTreeLearner : public TreeLearner {
     {
       // the per-child best in the scan (completion ticket); the select keeps it for raw CEGB /
       // by-node candidates and for the voting / feature exchanges, which rewrite the candidates
+      // (opt-in, LGAP_SCAN_BEST=1: A/B at 10M and 1.25M 2-5% slower than the select's phase A)
       const char* e = std::getenv("LGAP_SCAN_BEST");
-      a.scan_best = (e == nullptr || e[0] != '0') && !RawCands() && !fvoting_ && !ffeature_ ? 1 : 0;
+      a.scan_best = e != nullptr && e[0] == '1' && !RawCands() && !fvoting_ && !ffeature_ ? 1 : 0;
       a.scan_ticket = fscan_ticket_.get();
+      // LGAP_PART_TICKET: 0 strided tiles, 1 atomic dispatch tickets, else (default) contiguous
+      // tiles in block order (A/B 10M: the shared ticket atomic cost ~17 us per round)
       const char* pt = std::getenv("LGAP_PART_TICKET");
-      a.part_ticket = pt != nullptr && pt[0] == '0' ? nullptr : fpart_ticket_.get();
+      const int pmode = pt == nullptr ? 2 : std::atoi(pt);
+      a.part_ticket = pmode == 1 ? fpart_ticket_.get() : nullptr;
+      a.part_contig = pmode == 2 ? 1 : 0;
       a.scan_cpos = fscan_cpos_.get();
     }
     a.xrng = config_->extra_trees ? rng_.get() : nullptr;

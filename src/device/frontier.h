@@ -199,10 +199,13 @@ struct FArgs {
   // per-child best split in the scan (scan_best = 1): the last item of an expansion to finish
   // (completion ticket) takes the arg-max over the features for both children and writes
   // best / key, so the select's phase A only reads the winners' candidate positions
-  // partition tiles by dispatch order (part_ticket != null): each block takes a ticket when it
-  // starts and owns the contiguous tiles [ticket * per, (ticket + 1) * per), so its look-back only
-  // waits on blocks that started before it -- no co-residency assumption (the select / init zero
-  // the counter for the next launch)
+  // partition tile ownership. part_contig (default): block b owns the balanced contiguous range
+  // [b T / G, (b + 1) T / G), so its look-back only waits on lower blocks, which the in-order
+  // dispatch started before it -- no co-residency assumption. part_ticket != null
+  // (LGAP_PART_TICKET=1): the same with an atomic dispatch ticket instead of blockIdx (the
+  // select / init zero the counter for the next launch). Neither (LGAP_PART_TICKET=0): tiles
+  // blockIdx + j G, which needs every block resident.
+  int part_contig;
   unsigned* part_ticket;
   int scan_best;
   unsigned* scan_ticket;  // [kmax] finished items per expansion (reset by the last one)

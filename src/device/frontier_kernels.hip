@@ -2,7 +2,7 @@
 //
 // Launch shapes (fixed per learner; the work of a round is read on the device):
 //   k_f_init        1 x 256
-//   k_f_partition   grid x 256 (tiles owned by dispatch ticket: no co-residency needed)
+//   k_f_partition   grid x 256 (contiguous tiles in block order: no co-residency needed)
 //   k_f_hist        max(hist_grid, ceil(hist_grid / 2) + kmax) x LDS tiles, 512 threads
 //   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature))
 //   k_f_select      1 x 1024
@@ -970,9 +970,9 @@ __device__ __forceinline__ void BlockSumMulti(int* v, int* sh) {
   for (int m = 0; m < M; ++m) v[m] = sh[m * 4] + sh[m * 4 + 1] + sh[m * 4 + 2] + sh[m * 4 + 3];
 }
 
-// A block owns tiles base + j * stride: its ticket's contiguous range (part_ticket), or
-// blockIdx.x + j * gridDim.x (LGAP_PART_TICKET=0, which needs every block resident). The
-// first MAXT of them live in registers for the whole
+// A block owns tiles base + j * stride: a contiguous range in block order (part_contig) or in
+// ticket order (part_ticket), or blockIdx.x + j * gridDim.x (LGAP_PART_TICKET=0, which needs
+// every block resident). The first MAXT of them live in registers for the whole
 // launch: their loads are issued together (row ids, then bins), their counts reduced in one
 // block sum, their look-back sums loaded in one round, their scatter ballots published in one
 // LDS barrier, so a block pays a few memory round trips instead of a few per tile. Tiles
@@ -999,7 +999,14 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
   // this block's tiles: base + j * stride for base + j * stride < lim (j < MAXT in registers,
   // the rest one by one). Ticketed: the contiguous range of the block's dispatch ticket.
   int base = static_cast<int>(blockIdx.x), stride = G, lim = T;
-  if (a.part_ticket != nullptr) {
+  if (a.part_contig) {
+    // contiguous, balanced ranges in block order: a block only waits on tiles of LOWER blocks,
+    // which the in-order dispatch started before it (no co-residency needed, no ticket atomic:
+    // one shared ticket address serialised ~256 device-scope atomics at every launch)
+    base = static_cast<int>((static_cast<long long>(blockIdx.x) * T) / G);
+    lim = static_cast<int>((static_cast<long long>(blockIdx.x + 1) * T) / G);
+    stride = 1;
+  } else if (a.part_ticket != nullptr) {
     __shared__ int s_vid;
     if (t == 0) s_vid = static_cast<int>(atomicAdd(a.part_ticket, 1u));
     __syncthreads();
