@@ -199,8 +199,8 @@ struct FArgs {
   // per-child best split in the scan (scan_best = 1): the last item of an expansion to finish
   // (completion ticket) takes the arg-max over the features for both children and writes
   // best / key, so the select's phase A only reads the winners' candidate positions
-  // partition tile ownership. part_contig (default): block b owns the balanced contiguous range
-  // [b T / G, (b + 1) T / G), so its look-back only waits on lower blocks, which the in-order
+  // partition tile ownership. part_contig (default): block b owns the contiguous range
+  // [b per, (b + 1) per), per = ceil(T / G), so its look-back only waits on lower blocks, which the in-order
   // dispatch started before it -- no co-residency assumption. part_ticket != null
   // (LGAP_PART_TICKET=1): the same with an atomic dispatch ticket instead of blockIdx (the
   // select / init zero the counter for the next launch). Neither (LGAP_PART_TICKET=0): tiles

@@ -1000,11 +1000,13 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
   // the rest one by one). Ticketed: the contiguous range of the block's dispatch ticket.
   int base = static_cast<int>(blockIdx.x), stride = G, lim = T;
   if (a.part_contig) {
-    // contiguous, balanced ranges in block order: a block only waits on tiles of LOWER blocks,
-    // which the in-order dispatch started before it (no co-residency needed, no ticket atomic:
-    // one shared ticket address serialised ~256 device-scope atomics at every launch)
-    base = static_cast<int>((static_cast<long long>(blockIdx.x) * T) / G);
-    lim = static_cast<int>((static_cast<long long>(blockIdx.x + 1) * T) / G);
+    // contiguous ranges of ceil(T / G) tiles in block order (the work in the lowest blocks, which
+    // the dispatcher starts first): a block only waits on tiles of LOWER blocks, which the
+    // in-order dispatch started before it (no co-residency needed, and no ticket atomic: one
+    // shared ticket address serialised ~256 device-scope atomics at every launch)
+    const int per = (T + G - 1) / G;
+    base = static_cast<int>(blockIdx.x) * per;
+    lim = min(T, base + per);
     stride = 1;
   } else if (a.part_ticket != nullptr) {
     __shared__ int s_vid;

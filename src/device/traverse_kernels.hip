@@ -6,6 +6,7 @@
 #include "device/traverse_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device/hip_common.h"
 #include "device/linear_kernels.h"
@@ -19,6 +20,16 @@ constexpr int kTThreads = 256;
 constexpr int kTRowsPerThread = 2;
 constexpr int kTRows = kTThreads * kTRowsPerThread;
 constexpr int kTMaxDw = 16;  // wider rows read global memory directly
+
+// Row-walk grid: LGAP_TRAVERSE_BLOCKS_PER_CU blocks per CU, grid-stride over the chunks (0: one
+// chunk per block, the hardware overlapping one block's loads with another's walk)
+int TraverseGrid(long long n, int num_cu) {
+  const char* e = std::getenv("LGAP_TRAVERSE_BLOCKS_PER_CU");
+  const int per = e != nullptr ? std::atoi(e) : 8;
+  const long long chunks = (n + kTRows - 1) / kTRows;
+  if (per <= 0) return static_cast<int>(std::max<long long>(1, std::min<long long>(chunks, 1 << 30)));
+  return static_cast<int>(std::max<long long>(1, std::min<long long>(chunks, static_cast<long long>(num_cu) * per)));
+}
 
 template <int W>
 __device__ __forceinline__ uint32_t GroupBin(const uint8_t* row, int g) {
@@ -79,12 +90,19 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
   for (long long base = static_cast<long long>(blockIdx.x) * kTRows; base < n;
        base += static_cast<long long>(gridDim.x) * kTRows) {
     const int rows = static_cast<int>(min(static_cast<long long>(kTRows), n - base));
-    // this chunk's scores, loaded before the walk so their latency hides behind it
+    // this chunk's scores (and, for the gradient epilogue, labels / weights), loaded before the
+    // walk so their latency hides behind it
     double sc[kTRowsPerThread];
+    float lb[kTRowsPerThread], wt[kTRowsPerThread], ax[kTRowsPerThread];
 #pragma unroll
     for (int j = 0; j < kTRowsPerThread; ++j) {
       const int r = t + j * kTThreads;
       sc[j] = r < rows ? score[base + r] : 0.0;
+      if (GRAD) {
+        lb[j] = r < rows ? ge.label[base + r] : 0.f;
+        wt[j] = r < rows && ge.weight ? ge.weight[base + r] : 1.f;
+        ax[j] = r < rows && ge.aux ? ge.aux[base + r] : 0.f;
+      }
     }
     if (staged) {
       __syncthreads();  // the previous chunk's walks are done (first pass: nodes / leaves in place)
@@ -140,11 +158,10 @@ __global__ __launch_bounds__(kTThreads) void k_traverse(const uint32_t* __restri
         const double ns = sc[j] + lv;
         score[base + r] = ns;
         if (GRAD) {
-          const long long i = base + r;
           score_t g, h;
-          PointwiseGradient(ge.p, ns, static_cast<double>(ge.label[i]), ge.weight ? static_cast<double>(ge.weight[i]) : 1.0,
-                            ge.weight != nullptr, ge.aux ? static_cast<double>(ge.aux[i]) : 0.0, &g, &h);
-          ge.gh[i] = make_float2(g, h);
+          PointwiseGradient(ge.p, ns, static_cast<double>(lb[j]), static_cast<double>(wt[j]), ge.weight != nullptr,
+                            static_cast<double>(ax[j]), &g, &h);
+          ge.gh[base + r] = make_float2(g, h);
         }
       }
     }
@@ -258,7 +275,7 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
   if (n <= 0) return;
   const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + ((sizeof(double) * num_leaves + 15) & ~size_t(15)) +
                      (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
-  const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
+  const int grid = TraverseGrid(n, num_cu);
   LinearLeaves none{};
   if (width == 0) {
     k_traverse<0, false><<<grid, kTThreads, lds, s>>>(rowbins, stride_dw, n, nodes, num_nodes, cats, cat_bits, leaf_value,
@@ -280,7 +297,7 @@ void LaunchTraverseGrad(const uint32_t* rowbins, int stride_dw, int width, int n
   if (n <= 0) return;
   const size_t lds = ((sizeof(TNode) * num_nodes + 15) & ~size_t(15)) + ((sizeof(double) * num_leaves + 15) & ~size_t(15)) +
                      (stride_dw <= kTMaxDw ? sizeof(uint32_t) * kTRows * stride_dw : 0);
-  const int grid = std::max(1, std::min(DivUp(n, kTRows), num_cu * 8));
+  const int grid = TraverseGrid(n, num_cu);
   LinearLeaves none{};
   GradEpilogue ge;
   ge.p = p;
