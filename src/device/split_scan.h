@@ -145,8 +145,10 @@ __device__ bool ScanNumericalWave(const SplitParams& p, const DevFeature& fi, co
   // and gain as the one before, and the host scan keeps the first of such exact ties. The
   // parallel prefix may round the two positions differently, so empty-bin positions after
   // the first evaluated one are skipped (the host rule, independent of summation order).
-  const int first_rev = (skip_def && top == fi.default_bin) ? top - 1 : top;
-  const int first_fwd = (skip_def && fi.default_bin == 0) ? 1 : 0;
+  // (extra trees evaluate ONE threshold, the random one: an empty bin there is still a split,
+  // so nothing is skipped)
+  const int first_rev = use_rand ? -1 : (skip_def && top == fi.default_bin) ? top - 1 : top;
+  const int first_fwd = use_rand ? 0x7fffffff : (skip_def && fi.default_bin == 0) ? 1 : 0;
   // reverse pass: position i <-> bin nb - 1 - i (the right side grows from the top bin)
   for (int base = 0; base < nb; base += 64 * K) {
     double pg[K], ph[K];
