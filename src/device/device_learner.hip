@@ -1662,7 +1662,8 @@ class DeviceTreeLearner : public TreeLearner {
     per_cu = std::max(1, std::min(cap, per_cu - 1));
     fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
     fscan_lds_ = FrontierScanLds(max_bin_, has_cat_ ? max_cat_bin_ : 1);
-    FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
+    // (the attribute covers a second histogram copy whatever LGAP_HIST_COPIES says later)
+    FrontierSetLds(FrontierHistLds() + (HistCopiesFit() ? HistCopyBytes() : 0), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
     // 512 / 1024 threads per histogram block. Round 3 (after the grid cap at 7/8 of the CUs),
@@ -1783,6 +1784,7 @@ class DeviceTreeLearner : public TreeLearner {
       const bool want = e != nullptr ? e[0] != '0' : num_tiles_ == 1;
       a.qsub = a.quant && !use_dp_ && sub >= 2048 && want ? sub : 0;
     }
+    a.hist_copies = HistCopies(a.qsub);
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
     if (RawCands() && fnuep_.size() > 0) {
@@ -2337,7 +2339,21 @@ class DeviceTreeLearner : public TreeLearner {
 
   // the frontier histogram's dynamic LDS: the tile plan's, plus the 32-bit bins of hist MODE 3
   size_t FrontierHistLds() const {
-    return use_dp_ || !QuantHist() || MakeFArgs().qsub == 0 ? hist_lds_bytes_ : hist_lds_bytes_ * 3 / 2 + 64;
+    const FArgs fa = MakeFArgs();
+    const size_t b = use_dp_ || !QuantHist() || fa.qsub == 0 ? hist_lds_bytes_ : hist_lds_bytes_ * 3 / 2 + 64;
+    return fa.hist_copies > 1 ? b + HistCopyBytes() : b;
+  }
+
+  // Two LDS copies of the frontier histogram (k_f_hist: even / odd waves apart): one non-direct
+  // tile whose second copy still fits 150 KB, not the 32-bit MODE 3 (LGAP_HIST_COPIES=1: one)
+  size_t HistCopyBytes() const { return h_tiles_.empty() ? 0 : static_cast<size_t>(h_tiles_[0].nbins) * (use_dp_ ? 16 : 8); }
+  bool HistCopiesFit() const {
+    return num_tiles_ == 1 && !h_tiles_.empty() && !h_tiles_[0].direct && hist_lds_bytes_ + HistCopyBytes() <= 150 * 1024;
+  }
+  int HistCopies(int qsub) const {
+    if (!HistCopiesFit() || qsub > 0) return 1;
+    const char* e = std::getenv("LGAP_HIST_COPIES");
+    return e != nullptr && std::atoi(e) == 1 ? 1 : 2;
   }
 
   // Integer-level histograms for quantized training (frontier hist MODE 2): int8 g and

@@ -365,11 +365,15 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   const int bh = FixedPointExp(k30, rows_in_block, __uint_as_float(a.ghmax[1]), sbh);
   const float sg = ldexpf(1.f, bg), sh = ldexpf(1.f, bh);
   const int words = MODE != 1 ? tile.nbins : 2 * tile.nbins;
+  // two LDS copies of the histogram when they fit (hist_copies = 2, single-tile data): even
+  // and odd waves accumulate into different copies, halving same-bin atomic collisions (a deep
+  // node's rows crowd few bins of its split features); the flush adds the two
+  const int copies = MODE == 3 ? 1 : (a.hist_copies > 1 ? 2 : 1);
   unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
   uint32_t* hist32 = reinterpret_cast<uint32_t*>(hist + words);
   int* gst = reinterpret_cast<int*>(MODE == 3 ? reinterpret_cast<unsigned long long*>(hist32 + ((tile.nbins + 1) & ~1))
-                                              : hist + words);
-  for (int i = t; i < words; i += blockDim.x) hist[i] = 0ull;
+                                              : hist + copies * words);
+  for (int i = t; i < copies * words; i += blockDim.x) hist[i] = 0ull;
   if (MODE == 3) {
     for (int i = t; i < tile.nbins; i += blockDim.x) hist32[i] = 0u;
   }
@@ -392,7 +396,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       __syncthreads();
     }
   } else {
-    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh);
+    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist + (copies > 1 ? ((t >> 6) & 1) * words : 0), sg, sh, dsg,
+                       dsh);
     __syncthreads();
   }
   FStamp(a, rnd, kFStampHist, 2);
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     const int shg = max(0, EG - bg), shh = max(0, EH - bh);
     for (int j = t; j < tile.nbins; j += blockDim.x) {
       const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
-      const unsigned long long x = hist[i];
+      const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);  // (packed fields: exact)
       if (x == 0ull) continue;
       const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
       const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
@@ -420,7 +425,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     const bool pack = a.qpack != 0;
     for (int j = t; j < tile.nbins; j += blockDim.x) {
       const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
-      const unsigned long long x = hist[i];
+      const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);
       if (x == 0ull) continue;
       if (pack) {
         atomicAdd(&out[i], x);  // (pw == 1)
@@ -434,7 +439,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   } else {
     for (int j = t; j < 2 * tile.nbins; j += blockDim.x) {
       const int i = j < 2 * (tile.nbins - rot) ? j + 2 * rot : j + 2 * rot - 2 * tile.nbins;
-      const unsigned long long x = hist[i];
+      const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);
       if (x) atomicAdd(&out[i], x);
     }
   }
