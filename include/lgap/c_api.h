@@ -281,6 +281,11 @@ LIGHTGBM_C_EXPORT int LGBM_DeviceHistogram(DatasetHandle handle, const float* gr
 LIGHTGBM_C_EXPORT int LGBM_DeviceTestFrontierHist(DatasetHandle handle, const char* parameters, const float* grad,
                                                   const float* hess, const int32_t* rows, const int32_t* offsets,
                                                   int k, double* out, uint16_t* levels);
+// k_f_scan of the root round (all rows) next to the host split_math.h scan of the same histogram:
+// out / ref [num_features][8] (gain, threshold, left count, default_left, left sum g, left sum h,
+// valid, categorical thresholds).
+LIGHTGBM_C_EXPORT int LGBM_DeviceTestFrontierScan(DatasetHandle handle, const char* parameters, const float* grad,
+                                                  const float* hess, double* out, double* ref);
 LIGHTGBM_C_EXPORT int LGBM_DeviceTestFrontierPartition(DatasetHandle handle, const char* parameters,
                                                        const int32_t* rows, const int32_t* offsets, int k,
                                                        const int32_t* feats, const int32_t* thr, const int32_t* dleft,

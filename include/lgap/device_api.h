@@ -66,6 +66,10 @@ void DeviceHistogram(const Dataset* data, const float* grad, const float* hess, 
 // the host learner's stable partition of the same split.
 void TestFrontierHist(const Dataset* data, const Config& config, const float* grad, const float* hess, const int* rows,
                       const int* offsets, int k, double* out, uint16_t* levels);
+// k_f_scan of the root round over all rows -> out[F][8] (gain, threshold, left count, default_left,
+// left sum g, left sum h, valid, categorical thresholds), ref[F][8] the host split_math.h scan
+void TestFrontierScan(const Dataset* data, const Config& config, const float* grad, const float* hess, double* out,
+                      double* ref);
 void TestFrontierPartition(const Dataset* data, const Config& config, const int* rows, const int* offsets, int k,
                            const int* feats, const int* thr, const int* dleft, const uint32_t* catbits, int* out_rows,
                            int* out_left, int* exp_rows, int* exp_left);

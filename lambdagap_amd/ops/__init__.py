@@ -132,6 +132,26 @@ def frontier_histogram(ds: Dataset, grad: np.ndarray, hess: np.ndarray, subsets,
     return out.reshape(k, tb, 2), lv
 
 
+def frontier_scan(ds: Dataset, grad: np.ndarray, hess: np.ndarray, params: Optional[dict] = None
+                  ) -> Tuple[np.ndarray, np.ndarray]:
+    """The frontier engine's production split scan (k_f_scan) of the root round over all rows, next
+    to the host learner's split_math.h scan of the same rows' exact histogram.
+
+    Returns (device, host) arrays [num_features, 8]: gain, threshold, left count, default_left,
+    left sum g, left sum h, valid (a split exists), categorical thresholds."""
+    ds.construct()
+    nf = ds.num_feature()
+    g = np.ascontiguousarray(grad, dtype=np.float32)
+    h = np.ascontiguousarray(hess, dtype=np.float32)
+    out = np.zeros(nf * 8, dtype=np.float64)
+    ref = np.zeros(nf * 8, dtype=np.float64)
+    dp = ctypes.POINTER(ctypes.c_double)
+    _check(_LIB.LGBM_DeviceTestFrontierScan(
+        ds.handle, ctypes.c_char_p(_param_str(params)), g.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+        h.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), out.ctypes.data_as(dp), ref.ctypes.data_as(dp)))
+    return out.reshape(nf, 8), ref.reshape(nf, 8)
+
+
 def frontier_partition(ds: Dataset, subsets, splits, params: Optional[dict] = None):
     """One launch of the frontier engine's production partition kernel (k_f_partition) over several
     parents at once. ``splits``: per parent (inner feature, threshold bin, default_left, categorical

@@ -1226,6 +1226,15 @@ int LGBM_DeviceTestFrontierHist(DatasetHandle handle, const char* parameters, co
   API_END();
 }
 
+int LGBM_DeviceTestFrontierScan(DatasetHandle handle, const char* parameters, const float* grad, const float* hess,
+                                double* out, double* ref) {
+  API_BEGIN();
+  Config cfg = ParseConfig(parameters);
+  cfg.device_type = "gpu";
+  device::TestFrontierScan(D(handle)->ds.get(), cfg, grad, hess, out, ref);
+  API_END();
+}
+
 int LGBM_DeviceTestFrontierPartition(DatasetHandle handle, const char* parameters, const int32_t* rows,
                                      const int32_t* offsets, int k, const int32_t* feats, const int32_t* thr,
                                      const int32_t* dleft, const uint32_t* catbits, int32_t* out_rows,

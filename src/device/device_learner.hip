@@ -2429,6 +2429,98 @@ class DeviceTreeLearner : public TreeLearner {
   // One histogram of (g, h) over `rows` (identity when null) into `out` (2 * TB doubles).
   // ---- direct tests of the frontier's production kernels (tests/test_frontier_kernels.py)
 
+  // The root round's k_f_scan (init, root sums, k_f_hist, k_f_scan over all rows) -> out[F][8]
+  // per feature: gain, threshold, left count, default_left, left sum g, left sum h, valid,
+  // categorical thresholds; ref[F][8] the host's split_math.h scan of the exact fp64 histogram
+  // of the same rows (FindBestNumerical / FindBestCategorical with the learner's SplitParams).
+  void TestFrontierScan(const float* g, const float* h, double* out, double* ref) {
+    if (!frontier_) Log::Fatal("TestFrontierScan: the frontier engine is not enabled for this configuration");
+    K_ = 1;
+    DeviceSetGradients(g, h, 1);
+    TreeParams* tp = pin_tp_.Get(1);
+    std::memset(tp, 0, sizeof(TreeParams));
+    tp->root_buf = -1;
+    tp->root_count = tp->root_gcount = N_;
+    tp->spec_alpha = 1.f;
+    HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
+    if (config_->use_quantized_grad) QuantizeGradients(0);
+    const FArgs fa = MakeFArgs();
+    LaunchFrontierInit(fa, stream_);
+    Args ra = MakeArgs(0);
+    ra.lsum = flsum_;
+    const int root_blocks = RootBlocks();
+    k_root_sums<<<root_blocks, kRootThreads, 0, stream_>>>(ra);
+    k_root_final<<<1, kRootThreads, 0, stream_>>>(ra, root_blocks);
+    HIP_CHECK(hipGetLastError());
+    facc_.Zero(stream_);
+    LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+    LaunchFrontierScan(fa, fscan_lds_, stream_);
+    std::vector<SplitInfo> dev(F_);
+    double2 root_sum;
+    HIP_CHECK(hipMemcpyAsync(dev.data(), fcinfo_, sizeof(SplitInfo) * F_, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(&root_sum, flsum_, sizeof(double2), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    facc_.Zero(stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    auto put = [](double* o, const SplitInfo& si) {
+      o[0] = si.gain;
+      o[1] = static_cast<double>(si.threshold);
+      o[2] = static_cast<double>(si.left_count);
+      o[3] = si.default_left ? 1.0 : 0.0;
+      o[4] = si.left_sum_gradient;
+      o[5] = si.left_sum_hessian;
+      o[6] = si.feature >= 0 ? 1.0 : 0.0;
+      o[7] = static_cast<double>(si.num_cat_threshold);
+    };
+    for (int f = 0; f < F_; ++f) put(out + 8 * static_cast<size_t>(f), dev[f]);
+    // host oracle: the same rows' exact fp64 histogram and the split_math.h scans, over the
+    // device's own (g, h) (quantized training: the de-quantized levels k_quantize left in gh)
+    std::vector<float2> ghd(N_);
+    HIP_CHECK(hipMemcpy(ghd.data(), gh_.get(), sizeof(float2) * N_, hipMemcpyDeviceToHost));
+    std::vector<double> hg(N_), hh(N_);
+    for (int i = 0; i < N_; ++i) {
+      hg[i] = ghd[i].x;
+      hh[i] = ghd[i].y;
+    }
+    double sg = 0.0, sh = 0.0;
+    for (int i = 0; i < N_; ++i) {
+      sg += hg[i];
+      sh += hh[i];
+    }
+    const SplitParams sp = fa.sp;
+    SplitParams p0 = sp;
+    p0.path_smooth = 0.0;
+    const double po = LeafOutputRaw(root_sum.x, root_sum.y, p0, N_, 0.0);
+    for (int f = 0; f < F_; ++f) {
+      const FeatureInfo& fi = data_->feature(f);
+      std::vector<double> full(2 * static_cast<size_t>(fi.num_bin), 0.0);
+      for (int i = 0; i < N_; ++i) {
+        const uint32_t b = data_->FeatureBin(i, f);
+        full[2 * b] += hg[i];
+        full[2 * b + 1] += hh[i];
+      }
+      FeatureScanMeta m;
+      m.num_bin = fi.num_bin;
+      m.default_bin = fi.default_bin;
+      m.missing_type = static_cast<int8_t>(fi.missing);
+      m.bin_type = static_cast<int8_t>(fi.bin_type);
+      m.monotone = fi.monotone;
+      m.penalty = fi.penalty;
+      SplitInfo r;
+      r.Reset();
+      bool ok;
+      if (fi.bin_type == BinType::Numerical) {
+        ok = FindBestNumerical(full.data(), m, sp, sg, sh, N_, po, LeafBounds(), &r);
+      } else {
+        std::vector<int> order(fi.num_bin);
+        ok = FindBestCategorical(full.data(), m, sp, sg, sh, N_, po, LeafBounds(), order.data(), &r);
+      }
+      r.feature = ok ? f : -1;
+      if (!ok) r.gain = kMinScore;
+      put(ref + 8 * static_cast<size_t>(f), r);
+    }
+  }
+
   // k_f_hist over k row subsets at once (one expansion each, as a round of the frontier):
   // out[k][TB][2] = the accumulators at the tree's global fixed-point scale (quantized
   // training: the integer level sums), levels[N] = the quantized levels (g << 8 | h).
@@ -3770,6 +3862,14 @@ void TestFrontierHist(const Dataset* data, const Config& config, const float* gr
   DeviceTreeLearner learner(&config, DevParallel::kSerial);
   learner.Init(data, false);
   learner.TestFrontierHist(grad, hess, rows, offsets, k, out, levels);
+}
+
+void TestFrontierScan(const Dataset* data, const Config& config, const float* grad, const float* hess, double* out,
+                      double* ref) {
+  if (DeviceCount() <= 0) Log::Fatal("TestFrontierScan: no AMD GPU visible to HIP");
+  DeviceTreeLearner learner(&config, DevParallel::kSerial);
+  learner.Init(data, false);
+  learner.TestFrontierScan(grad, hess, out, ref);
 }
 
 void TestFrontierPartition(const Dataset* data, const Config& config, const int* rows, const int* offsets, int k,

@@ -132,3 +132,45 @@ def test_frontier_partition_matches_host(lgb, gpu_required, rng, monkeypatch, pa
         np.testing.assert_array_equal(seg[:nl], ref[:nl])
         np.testing.assert_array_equal(seg[nl:][::-1], ref[nl:])
         assert np.array_equal(np.sort(seg), s)  # nothing lost or duplicated
+
+
+SCAN_CASES = {
+    "fixed_point": ({}, 1e-6),
+    "fp64": ({"gpu_use_dp": True}, 1e-9),
+    "quantized": ({"use_quantized_grad": True, "num_grad_quant_bins": 16}, 1e-9),
+    "missing_nan_as_zero": ({"zero_as_missing": True}, 1e-6),
+    "regularised": ({"lambda_l1": 0.5, "lambda_l2": 2.0, "min_data_in_leaf": 300, "max_delta_step": 0.7}, 1e-6),
+    "max_bin_63": ({"max_bin": 63}, 1e-6),
+}
+
+
+@pytest.mark.parametrize("case", sorted(SCAN_CASES))
+def test_frontier_scan_matches_host_split_math(lgb, gpu_required, rng, case):
+    """k_f_scan (numerical scans both directions with NaN / zero missing values, categorical one-hot
+    and ctr-sorted scans, most-frequent-bin reconstruction from the leaf sums) against the host
+    learner's split_math.h scans of the exact fp64 histogram of the same rows: the same features
+    are splittable, with the same threshold, default direction and left count, and gains within
+    the accumulation's precision."""
+    from lambdagap_amd import ops
+
+    params, rtol = SCAN_CASES[case]
+    X, y = _data(rng)
+    X[:, 5] = rng.integers(0, 3, len(y))            # one-hot categorical
+    base = {"objective": "binary", "num_leaves": 31, "verbosity": -1, "device_type": "gpu", "cat_smooth": 5}
+    base.update(params)
+    ds = lgb.Dataset(X, y, params=base, categorical_feature=[3, 5]).construct()
+    n = len(y)
+    p = 1.0 / (1.0 + np.exp(-0.3 * rng.standard_normal(n)))
+    g = (p - y).astype(np.float32)
+    h = (p * (1.0 - p)).astype(np.float32)
+    dev, ref = ops.frontier_scan(ds, g, h, base)
+    np.testing.assert_array_equal(dev[:, 6], ref[:, 6])
+    assert ref[:, 6].sum() >= 6, ref[:, 6]                   # most features have a split
+    ok = ref[:, 6] > 0
+    np.testing.assert_allclose(dev[ok, 0], ref[ok, 0], rtol=rtol, atol=rtol)   # gain
+    np.testing.assert_array_equal(dev[ok, 2], ref[ok, 2])                       # left count
+    np.testing.assert_array_equal(dev[ok, 7], ref[ok, 7])                       # categorical thresholds
+    num = ok & (ref[:, 7] == 0)
+    np.testing.assert_array_equal(dev[num, 1], ref[num, 1])                     # threshold bin
+    np.testing.assert_array_equal(dev[num, 3], ref[num, 3])                     # default direction
+    np.testing.assert_allclose(dev[ok, 4:6], ref[ok, 4:6], rtol=max(rtol, 1e-9), atol=1e-6)
