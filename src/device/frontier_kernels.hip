@@ -583,6 +583,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       s_key[t] = kz;
     }
     __syncthreads();
+    if (item == static_cast<int>(blockIdx.x)) FStamp(a, rnd, kFStampScan, 1);  // (loads + histograms in LDS)
     const bool skip_both = s_skip || !s_splp;
     // most-frequent bin = leaf total - stored bins
     if (w < 2 && my >= 0) {
@@ -763,6 +764,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       }
     }
     __syncthreads();
+    if (item == static_cast<int>(blockIdx.x)) FStamp(a, rnd, kFStampScan, 2);  // (scans done)
     // publish the candidates (dword-parallel copies of the LDS records)
     constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
     constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
@@ -778,6 +780,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       }
     }
     __syncthreads();  // LDS reused by the next item
+    if (item == static_cast<int>(blockIdx.x)) FStamp(a, rnd, kFStampScan, 3);
     if (a.scan_best) {
       // completion ticket of expansion e: the last of its F items picks both children's best
       if (t == 0) {
