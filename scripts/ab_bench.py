@@ -26,19 +26,32 @@ def main() -> int:
     ap.add_argument("--block", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--preset", default="higgs", choices=["higgs", "ltr"])
+    ap.add_argument("--preset", default="higgs", choices=["higgs", "ltr", "goss"])
+    ap.add_argument("--quantized", action="store_true", help="use_quantized_grad=true, 4 levels (goss / ltr)")
     ap.add_argument("--features", type=int, default=300)
     args = ap.parse_args()
     import lambdagap_amd as lgb
     from lambdagap_amd.parallel import device_synchronize
     from lambdagap_amd.utils import make_higgs_like
 
-    if args.preset == "ltr":
+    if args.preset == "goss":
+        from lambdagap_amd.models import preset
+        from lambdagap_amd.utils import make_regression
+
+        X, y = make_regression(args.rows, num_features=args.features, seed=7)
+        base = preset("regression_goss", verbosity=-1, seed=7)
+        if args.quantized:
+            base.update(use_quantized_grad=True, num_grad_quant_bins=4)
+        ds = lgb.Dataset(X, y, params=base, free_raw_data=True).construct()
+        del X
+    elif args.preset == "ltr":
         from lambdagap_amd.models import preset
         from lambdagap_amd.utils import make_ranking
 
         X, y, g = make_ranking(max(1, args.rows // 120), num_features=args.features, docs_per_query=(60, 180), seed=7)
         base = preset("ltr", verbosity=-1, seed=7)
+        if args.quantized:
+            base.update(use_quantized_grad=True, num_grad_quant_bins=4)
         ds = lgb.Dataset(X, y, group=g, params=base, free_raw_data=False).construct()
     else:
         X, y = make_higgs_like(args.rows, seed=7)

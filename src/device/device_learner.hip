@@ -201,6 +201,7 @@ class DeviceTreeLearner : public TreeLearner {
     TB_ = train->num_total_bin();
     width_ = train->bin_width();
     stride_dw_ = train->row_stride() / 4;
+    tstride_dw_ = stride_dw_;
     const bool parallel = mode_ != DevParallel::kSerial;
     if (parallel && !CommActive() && !HostStagedDP() && Network::num_machines() > 1) {
       Log::Fatal("Parallel HIP training needs an RCCL communicator (LGBM_DeviceCommInit)");
@@ -899,8 +900,9 @@ class DeviceTreeLearner : public TreeLearner {
     const double* dl = reinterpret_cast<const double*>(tree_buf_.get() + node_bytes);
     const uint32_t* dc = reinterpret_cast<const uint32_t*>(tree_buf_.get() + node_bytes + leaf_bytes);
     const int grid = std::min(DivUp(n, kTraverseThreads), num_cu_ * 8);
-    const size_t lds = node_bytes + (stride_dw_ <= kTraverseMaxDw ? sizeof(uint32_t) * kTraverseThreads * stride_dw_ : 0);
-    k_add_tree<<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins, stride_dw_, width_, n, dn, nn, dc, dl, s);
+    const int sdw = StrideOf(rowbins);
+    const size_t lds = node_bytes + (sdw <= kTraverseMaxDw ? sizeof(uint32_t) * kTraverseThreads * sdw : 0);
+    k_add_tree<<<std::max(grid, 1), kTraverseThreads, lds, stream_>>>(rowbins, sdw, width_, n, dn, nn, dc, dl, s);
     HIP_CHECK(hipGetLastError());
     // the pinned staging buffer is reused by the next call: wait for the copy
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -972,7 +974,7 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipEventRecord(tree_evt_[slot], stream_));
     const char* db = ttree_buf_.get();
     if (lin_pending_ != nullptr) {
-      LaunchTraverseLinear(rowbins, stride_dw_, width_, n, reinterpret_cast<const TNode*>(db), nn,
+      LaunchTraverseLinear(rowbins, StrideOf(rowbins), width_, n, reinterpret_cast<const TNode*>(db), nn,
                            reinterpret_cast<const TCat*>(db + node_bytes),
                            reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                            reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, *lin_pending_, s, num_cu_,
@@ -989,7 +991,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (fuse_pending_ && rowbins == rowbins_.get() && n == N_ && fused_obj_ != nullptr) {
       const PointwiseParams& pp = *fused_obj_->pointwise();
       const uint32_t* rb = nib_ ? rowbins4_.get() : rowbins;
-      LaunchTraverseGrad(rb, nib_ ? stride4_dw_ : stride_dw_, nib_ ? 0 : width_, n, reinterpret_cast<const TNode*>(db), nn,
+      LaunchTraverseGrad(rb, nib_ ? stride4_dw_ : StrideOf(rowbins), nib_ ? 0 : width_, n, reinterpret_cast<const TNode*>(db), nn,
                          reinterpret_cast<const TCat*>(db + node_bytes),
                          reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                          reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, pp, label_.get(),
@@ -1004,7 +1006,7 @@ class DeviceTreeLearner : public TreeLearner {
                      reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
       return;
     }
-    LaunchTraverse(rowbins, stride_dw_, width_, n, reinterpret_cast<const TNode*>(db), nn,
+    LaunchTraverse(rowbins, StrideOf(rowbins), width_, n, reinterpret_cast<const TNode*>(db), nn,
                    reinterpret_cast<const TCat*>(db + node_bytes), reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
                    reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
   }
@@ -1698,7 +1700,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.gh = gh_.get();
     for (int i = 0; i < kFrontierIdx; ++i) a.idx[i] = idx_[i].get();
     a.N = N_;
-    a.stride_dw = stride_dw_;
+    a.stride_dw = tstride_dw_;
     a.width = width_;
     a.num_groups = G_;
     a.TB = TB_;
@@ -2884,6 +2886,34 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipGetLastError());
   }
 
+  // dword stride of a packed-row buffer: the training rows may be padded (RowAlign), validation
+  // rows keep the dataset's stride
+  int StrideOf(const uint32_t* rb) const { return rb == rowbins_.get() ? tstride_dw_ : stride_dw_; }
+
+  // Wide rows in several LDS tiles: tiles cut at multiples of RowAlign() dwords and the training
+  // rows padded to a multiple of it, so every tile's slice of a row is whole aligned 32 / 64 /
+  // 128-byte sectors instead of straddling them (LGAP_ROW_ALIGN_DW: 0 off, 8, 16 or 32)
+  int RowAlign() const {
+    const char* e = std::getenv("LGAP_ROW_ALIGN_DW");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v == 8 || v == 16 || v == 32 ? v : 0;
+  }
+
+  void PadTrainingRows(int align) {
+    const int pad = DivUp(stride_dw_, align) * align;
+    if (pad == stride_dw_ || N_ <= 0) return;
+    uint32_t* p = nullptr;
+    const size_t n = static_cast<size_t>(N_) * pad;
+    HIP_CHECK(hipMalloc(&p, n * sizeof(uint32_t)));
+    HIP_CHECK(hipMemsetAsync(p, 0, n * sizeof(uint32_t), stream_));
+    HIP_CHECK(hipMemcpy2DAsync(p, pad * sizeof(uint32_t), rowbins_.get(), stride_dw_ * sizeof(uint32_t),
+                               stride_dw_ * sizeof(uint32_t), N_, hipMemcpyDeviceToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    rowbins_.Adopt(p, n);
+    tstride_dw_ = pad;
+    Log::Debug("HIP learner: training rows padded from %d to %d dwords (tiles aligned to %d)", stride_dw_, pad, align);
+  }
+
   static double XTimeoutSeconds() {
     static const double t = [] {
       const char* e = std::getenv("LGAP_XGMI_TIMEOUT_S");
@@ -2971,6 +3001,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void BuildTiles() {
+    row_align_ = RowAlign();
     const int env_kb = [] {
       const char* e = std::getenv("LGAP_HIST_LDS_KB");  // A/B / test knob: LDS tile budget
       return e ? std::max(16, std::min(150, std::atoi(e))) : 0;
@@ -2986,6 +3017,7 @@ class DeviceTreeLearner : public TreeLearner {
       big_tiles_ = true;
       PlanTiles(150 * 1024);
     }
+    if (num_tiles_ > 1 && row_align_ > 0) PadTrainingRows(row_align_);
   }
 
   // 4-bit rows for the frontier histograms and the training score update: 8-bit data whose
@@ -3001,7 +3033,7 @@ class DeviceTreeLearner : public TreeLearner {
     }
     stride4_dw_ = DivUp(G_, 8);
     rowbins4_.Resize(static_cast<size_t>(N_) * stride4_dw_);
-    LaunchPackNibbles(rowbins_.get(), stride_dw_, N_, G_, rowbins4_.get(), stride4_dw_, stream_);
+    LaunchPackNibbles(rowbins_.get(), tstride_dw_, N_, G_, rowbins4_.get(), stride4_dw_, stream_);
     HistTile t = h_tiles_[0];
     t.d0 = 0;
     t.d1 = stride4_dw_;
@@ -3034,6 +3066,14 @@ class DeviceTreeLearner : public TreeLearner {
         if (bins + wb > max_bins && e > d) break;
         bins += wb;
         ++e;
+      }
+      if (row_align_ > 0 && e < nd && e - d >= row_align_ && (e - d) % row_align_ != 0) {
+        // cut at the alignment (the rows are padded to it when there are several tiles)
+        const int ea = d + (e - d) / row_align_ * row_align_;
+        for (int x = ea; x < e; ++x) {
+          for (int g = x * per; g < std::min(G_, (x + 1) * per); ++g) bins -= data_->group(g).num_bin;
+        }
+        e = ea;
       }
       t.d1 = e;
       t.g1 = std::min(G_, e * per);
@@ -3238,7 +3278,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.gh = gh_.get();
     for (int i = 0; i < 5; ++i) a.idx[i] = idx_[i].get();
     a.N = N_;
-    a.stride_dw = stride_dw_;
+    a.stride_dw = tstride_dw_;
     a.width = width_;
     a.num_groups = G_;
     a.TB = TB_;
@@ -3633,6 +3673,8 @@ class DeviceTreeLearner : public TreeLearner {
   bool distributed_ = false;
   const Dataset* data_ = nullptr;
   int N_ = 0, F_ = 0, G_ = 0, TB_ = 0, width_ = 1, stride_dw_ = 1, L_ = 2, K_ = 1;
+  int row_align_ = 0;     // tile / padded-row alignment in dwords (RowAlign), 0: none
+  int tstride_dw_ = 1;   // row stride of the TRAINING rows (rowbins_): stride_dw_, or padded (RowAlign)
   int device_id_ = 0, num_cu_ = 256, num_tiles_ = 0, max_tiles_ = 1, max_cat_bin_ = 1;
   bool has_cat_ = false, use_bag_ = false, use_bynode_ = false, use_dp_ = false;
   int bynode_draws_ = 0;  // by-node masks the last tree used (the host sampler's GetByNode calls)
