@@ -2446,6 +2446,11 @@ class DeviceTreeLearner : public TreeLearner {
     tp->spec_alpha = 1.f;
     HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
     if (config_->use_quantized_grad) QuantizeGradients(0);
+    {
+      uint8_t* um = pin_mask_.Get(static_cast<size_t>(F_));
+      std::memset(um, 1, static_cast<size_t>(F_));  // every feature in use (no feature_fraction)
+      HIP_CHECK(hipMemcpyAsync(used_bytree_.get(), um, F_, hipMemcpyHostToDevice, stream_));
+    }
     const FArgs fa = MakeFArgs();
     LaunchFrontierInit(fa, stream_);
     Args ra = MakeArgs(0);
