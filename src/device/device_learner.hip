@@ -836,10 +836,11 @@ class DeviceTreeLearner : public TreeLearner {
       return;
     }
     last_trained_ = nullptr;
-    // single-class pointwise objectives: the traversal also computes the next iteration's
-    // gradients at the updated score (one pass over the rows; LGAP_FUSE_GRAD=0 keeps two)
+    // single-class pointwise objectives: LGAP_FUSE_GRAD=1 has the traversal also compute the
+    // next iteration's gradients at the updated score (one pass over the rows). Opt-in: its 115
+    // VGPRs halve the walk's occupancy (10M: 238 us fused vs 150 + 44 us for the two kernels)
     const char* fe = std::getenv("LGAP_FUSE_GRAD");
-    const bool fuse_ok = fe == nullptr || fe[0] != '0';
+    const bool fuse_ok = fe != nullptr && fe[0] == '1';
     fuse_pending_ = fuse_ok && fused_obj_ != nullptr && K_ == 1 && k == 0 && label_.size() >= static_cast<size_t>(N_);
     TraverseTree(tree, rowbins_.get(), N_, s);
     fused_grad_ready_ = fuse_pending_ && fuse_done_;
@@ -1834,10 +1835,13 @@ class DeviceTreeLearner : public TreeLearner {
       const char* e = std::getenv("LGAP_SCAN_BEST");
       a.scan_best = e != nullptr && e[0] == '1' && !RawCands() && !fvoting_ && !ffeature_ ? 1 : 0;
       a.scan_ticket = fscan_ticket_.get();
-      // LGAP_PART_TICKET: 0 strided tiles, 1 atomic dispatch tickets, else (default) contiguous
-      // tiles in block order (A/B 10M: the shared ticket atomic cost ~17 us per round)
+      // LGAP_PART_TICKET: 0 strided tiles, 1 atomic dispatch tickets, 2 contiguous tiles in block
+      // order. Default: strided on one process (A/B 10M, same box: 2.91 vs 2.98 ms/iter for block
+      // order, 3.11 for tickets; a kernel on another stream only delays the blocks it displaces,
+      // it finishes), block order when ranks exchange (an RCCL kernel waiting on peers could
+      // hold the CUs a strided partition needs)
       const char* pt = std::getenv("LGAP_PART_TICKET");
-      const int pmode = pt == nullptr ? 2 : std::atoi(pt);
+      const int pmode = pt != nullptr ? std::atoi(pt) : (distributed_ ? 2 : 0);
       a.part_ticket = pmode == 1 ? fpart_ticket_.get() : nullptr;
       a.part_contig = pmode == 2 ? 1 : 0;
       a.scan_cpos = fscan_cpos_.get();
@@ -2354,8 +2358,9 @@ class DeviceTreeLearner : public TreeLearner {
   }
   int HistCopies(int qsub) const {
     if (!HistCopiesFit() || qsub > 0) return 1;
+    // (opt-in, LGAP_HIST_COPIES=2: flat at 10M, 2.99 vs 2.98 ms/iter)
     const char* e = std::getenv("LGAP_HIST_COPIES");
-    return e != nullptr && std::atoi(e) == 1 ? 1 : 2;
+    return e != nullptr && std::atoi(e) == 2 ? 2 : 1;
   }
 
   // Integer-level histograms for quantized training (frontier hist MODE 2): int8 g and
@@ -2899,8 +2904,10 @@ class DeviceTreeLearner : public TreeLearner {
   // rows padded to a multiple of it, so every tile's slice of a row is whole aligned 32 / 64 /
   // 128-byte sectors instead of straddling them (LGAP_ROW_ALIGN_DW: 0 off, 8, 16 or 32)
   int RowAlign() const {
+    // (default 16: A/B on one box, GOSS 5M x 500 quantized 10.95 -> 10.40 ms/iter, LambdaRank
+    // 3M x 300 9.52 -> 9.30)
     const char* e = std::getenv("LGAP_ROW_ALIGN_DW");
-    const int v = e != nullptr ? std::atoi(e) : 0;
+    const int v = e != nullptr ? std::atoi(e) : 16;
     return v == 8 || v == 16 || v == 32 ? v : 0;
   }
 

@@ -176,4 +176,4 @@ def test_frontier_scan_matches_host_split_math(lgb, gpu_required, rng, case):
     num = ok & (ref[:, 7] == 0)
     np.testing.assert_array_equal(dev[num, 1], ref[num, 1])                     # threshold bin
     np.testing.assert_array_equal(dev[num, 3], ref[num, 3])                     # default direction
-    np.testing.assert_allclose(dev[ok, 4:6], ref[ok, 4:6], rtol=max(rtol, 1e-9), atol=1e-6)
+    np.testing.assert_allclose(dev[ok, 4:6], ref[ok, 4:6], rtol=rtol, atol=5 * rtol)      # left sums
