@@ -2177,6 +2177,15 @@ class DeviceTreeLearner : public TreeLearner {
       }
       std::fprintf(stderr, "fstamps %s (%d rounds, us from block-0 start; t7 = last block exit):%s\n", names[k], cnt,
                    line.c_str());
+      if (at(0, k, 0)) {
+        // the root round alone (the largest histogram / partition of the tree)
+        std::string root;
+        for (int i = 1; i < kFStampSlots; ++i) {
+          const unsigned long long v = at(0, k, i);
+          if (v >= at(0, k, 0) && v) root += " t" + std::to_string(i) + "=" + common::FormatG((v - at(0, k, 0)) * 0.01);
+        }
+        std::fprintf(stderr, "fstamps %s root round:%s\n", names[k], root.c_str());
+      }
     }
     double gap[4] = {0};
     int cnt = 0;

@@ -41,6 +41,12 @@ __device__ __forceinline__ void FStamp(const FArgs& a, int r, int kern, int i) {
     a.stamps[((static_cast<size_t>(r & 255) * 4 + kern) * kFStampSlots) + i] = wall_clock64();
   }
 }
+// latest time over ALL blocks that reached point `i` (slots 4-6: the spread behind block 0's)
+__device__ __forceinline__ void FStampMax(const FArgs& a, int r, int kern, int i) {
+  if (a.stamps != nullptr && threadIdx.x == 0) {
+    atomicMax(&a.stamps[((static_cast<size_t>(r & 255) * 4 + kern) * kFStampSlots) + i], wall_clock64());
+  }
+}
 __device__ __forceinline__ void FStampEnd(const FArgs& a, int r, int kern) {
   if (a.stamps != nullptr && threadIdx.x == 0) {
     atomicMax(&a.stamps[((static_cast<size_t>(r & 255) * 4 + kern) * kFStampSlots) + 7], wall_clock64());
@@ -282,6 +288,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   __syncthreads();
   const int e = s_e;
   if (e < 0) return;
+  FStampMax(a, rnd, kFStampHist, 4);  // (latest start of a working block)
   const int rb = s_rb, re = s_re, buf = s_buf, start = s_start;
   const HistTile tile = a.tiles[blockIdx.y];
   // accumulator words per bin: 1 when quantized level sums are packed g32|h32 (qpack: the
@@ -401,6 +408,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     __syncthreads();
   }
   FStamp(a, rnd, kFStampHist, 2);
+  FStampMax(a, rnd, kFStampHist, 5);  // (latest block done with its rows)
   unsigned long long* out = acc + pw * static_cast<size_t>(tile.bin0);
   if (a.debug_noflush) return;  // timing diagnostics only (LGAP_DEBUG_NOFLUSH): results are wrong
   // every block starts its flush at its own offset of the tile, so the blocks' concurrent
@@ -444,6 +452,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     }
   }
   FStamp(a, rnd, kFStampHist, 3);
+  FStampMax(a, rnd, kFStampHist, 6);  // (latest block done issuing its flush)
   FStampEnd(a, rnd, kFStampHist);
 }
 
