@@ -3039,6 +3039,13 @@ class DeviceTreeLearner : public TreeLearner {
       PlanTiles(150 * 1024);
     }
     if (num_tiles_ > 1 && row_align_ > 0) PadTrainingRows(row_align_);
+    // single-tile rows padded to whole sectors (LGAP_ROW_PAD_SINGLE=8: 28-byte rows -> 32 bytes,
+    // so a gathered row never straddles two sectors; experiment knob)
+    if (num_tiles_ == 1) {
+      const char* e = std::getenv("LGAP_ROW_PAD_SINGLE");
+      const int v = e != nullptr ? std::atoi(e) : 0;
+      if (v == 8 || v == 16) PadTrainingRows(v);
+    }
   }
 
   // 4-bit rows for the frontier histograms and the training score update: 8-bit data whose
