@@ -40,6 +40,11 @@ for step in "$@"; do
              head -20 $OUT/pmc${i}_summary.md
            fi
            (exit $rc) ;;
+    # one counter pass of your own: pmcx:<counters>|<python script and args>; the per-kernel means
+    # of each counter land in pmcx<i>_summary.csv
+    pmcx)  ctrs=${arg%%|*}; prog=${arg#*|}
+           timeout -s KILL 240 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d $PWD/$OUT/pmcx$i -o run -- python3 $prog > $log 2>&1 &&
+             python scripts/pmc_counters.py $OUT/pmcx$i > $OUT/pmcx${i}_summary.csv 2>&1 && rm -rf $OUT/pmcx$i && head -20 $OUT/pmcx${i}_summary.csv ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
   rc=$?
