@@ -141,9 +141,11 @@ SCAN_CASES = {
     "fixed_point": ({}, 2e-5),
     "fp64": ({"gpu_use_dp": True}, 1e-9),
     "quantized": ({"use_quantized_grad": True, "num_grad_quant_bins": 16}, 1e-9),
-    "missing_zero": ({"zero_as_missing": True}, 2e-5),
-    "regularised": ({"lambda_l1": 0.5, "lambda_l2": 2.0, "min_data_in_leaf": 300, "max_delta_step": 0.7}, 2e-5),
-    "max_bin_63": ({"max_bin": 63}, 2e-5),
+    # (the scan logic cases accumulate fp64-equivalent: their direction / threshold ties are exact)
+    "missing_zero": ({"zero_as_missing": True, "gpu_use_dp": True}, 1e-9),
+    "regularised": ({"lambda_l1": 0.5, "lambda_l2": 2.0, "min_data_in_leaf": 300, "max_delta_step": 0.7,
+                     "gpu_use_dp": True}, 1e-9),
+    "max_bin_63": ({"max_bin": 63, "gpu_use_dp": True}, 1e-9),
 }
 
 
