@@ -463,7 +463,13 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
 //  2. most-frequent bins from the leaf sums; wave 0 scans the smaller child, wave 1 the
 //     larger one (split_scan.h), both from LDS
 //  3. the two candidates -> the round's candidate table [e][sel][f]
+// EXT: the voting local pass, extra-trees draws, feature-parallel ownership and the scan-side
+// best; the plain instantiation (serial / data-parallel) compiles none of it
+template <bool EXT>
 __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
+  const bool voting = EXT && a.voting != 0;
+  const bool xtrees = EXT && a.xrng != nullptr;
+  const bool scan_best = EXT && a.scan_best != 0;
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_skip, s_splp, s_rand[2], s_xn[2];
   __shared__ double s_xh[2];
@@ -493,7 +499,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     const FExp& xr = a.exps[e];
     if (xr.skip) {
       // (scan_best: the children of a skipped expansion get empty records, once)
-      if (a.scan_best && f == 0 && t < 2) {
+      if (scan_best && f == 0 && t < 2) {
         const int c = t == 0 ? xr.smaller : xr.larger;
         if (c >= 0) {
           a.best[c].Reset();
@@ -534,7 +540,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       pre_fidx = a.num_forced > 0 ? a.nodes[my].fidx : -1;
       pre_out = a.lout[my];
       pre_bounds = a.bounds[my];
-      if (a.voting) {
+      if (voting) {
         // voting's LOCAL pass: this rank's rows and sums (the smaller child's from the round's
         // exact local totals, the larger's as the parent's local sums minus them)
         pre_n = a.nodes[my].count;
@@ -551,8 +557,8 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     }
     if (t == 0) {
       // (feature parallel: only the features this rank owns)
-      s_skip = !a.used_bytree[f] || (a.fowned != nullptr && !a.fowned[f]);
-      s_splp = p >= 0 && !a.voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
+      s_skip = !a.used_bytree[f] || (EXT && a.fowned != nullptr && !a.fowned[f]);
+      s_splp = p >= 0 && !voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
     for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
       const unsigned long long x0 = acc[pw * kk], x1 = qpack ? 0ull : acc[2 * kk + 1];
@@ -613,7 +619,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       }
     }
     __syncthreads();
-    if (a.xrng != nullptr && t == 0) {
+    if (xtrees && t == 0) {
       // extra-trees thresholds, drawn in the host learner's order: the smaller child, then the
       // larger one (one expansion per round here: no other item advances this feature's stream)
       s_rand[0] = s_rand[1] = 0;
@@ -637,13 +643,13 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         }
       }
     }
-    if (a.xrng != nullptr) __syncthreads();
+    if (xtrees) __syncthreads();
     if (w < 2 && my >= 0) {
       SplitInfo* out = &s_out[w];
       const double sg = __shfl(pre_sum.x, 0, kWave), sh = __shfl(pre_sum.y, 0, kWave);
       const int n = __shfl(pre_n, 0, kWave);
       const int depth = __shfl(pre_depth, 0, kWave);
-      const SplitParams& spp = a.voting ? a.sp_local : a.sp;
+      const SplitParams& spp = voting ? a.sp_local : a.sp;
       if (!skip_both) {
         const double* H = w ? hl_full : hs_full;
         double po;
@@ -651,7 +657,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
           SplitParams p0 = spp;
           p0.path_smooth = 0.0;
           po = LeafOutputRaw(sg, sh, p0, n, 0.0);
-          if (f == 0 && lane == 0 && !a.voting) a.lout[0] = po;  // (voting: the global root output, k_f_elect)
+          if (f == 0 && lane == 0 && !voting) a.lout[0] = po;  // (voting: the global root output, k_f_elect)
         } else {
           po = __shfl(pre_out, 0, kWave);
         }
@@ -659,7 +665,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         bounds.min = __shfl(pre_bounds.min, 0, kWave);
         bounds.max = __shfl(pre_bounds.max, 0, kWave);
         bool spl;
-        const int rt = a.xrng != nullptr ? s_rand[w] : 0;
+        const int rt = xtrees ? s_rand[w] : 0;
         if (fi.bin_type == 0) {
           spl = ScanNumericalWave(spp, fi, H, sg, sh, n, po, bounds, rt, out);
         } else {
@@ -686,17 +692,17 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
             // subtracted before the monotone penalty multiplies the gain). With coupled
             // penalties the candidate stays raw: the select applies every penalty (CegbAdjust)
             // (voting's local pass ranks raw gains: penalties belong to the global pass)
-            if (!a.cegb_raw && !a.voting) {
+            if (!a.cegb_raw && !voting) {
               if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
             }
-            if (a.ic && !a.voting && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
+            if (a.ic && !voting && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
           }
         }
       } else if (lane == 0) {
         // feature not tried: the children inherit the parent's flag
         a.spl[static_cast<size_t>(my) * F + f] = static_cast<uint8_t>(s_splp);
-        if (p < 0 && f == 0 && !a.voting) {
+        if (p < 0 && f == 0 && !voting) {
           SplitParams p0 = a.sp;
           p0.path_smooth = 0.0;
           a.lout[0] = LeafOutputRaw(sg, sh, p0, n, 0.0);
@@ -790,7 +796,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     }
     __syncthreads();  // LDS reused by the next item
     if (item == static_cast<int>(blockIdx.x)) FStamp(a, rnd, kFStampScan, 3);
-    if (a.scan_best) {
+    if (scan_best) {
       // completion ticket of expansion e: the last of its F items picks both children's best
       if (t == 0) {
         __threadfence();  // this item's candidates, visible device-wide before the ticket
@@ -2599,7 +2605,8 @@ void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
 
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
   const int grid = std::max(1, std::min(a.kmax * a.F, 4096));
-  k_f_scan<<<grid, kFScanThreads, lds, s>>>(a);
+  if (a.voting || a.xrng != nullptr || a.fowned != nullptr || a.scan_best) k_f_scan<true><<<grid, kFScanThreads, lds, s>>>(a);
+  else k_f_scan<false><<<grid, kFScanThreads, lds, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -2676,7 +2683,9 @@ void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
     }
   }
   if (scan_lds > 64 * 1024) {
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan), hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(scan_lds)));
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(scan_lds)));
   }
 }
