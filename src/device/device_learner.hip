@@ -1658,6 +1658,14 @@ class DeviceTreeLearner : public TreeLearner {
     ftile_pub_.Resize(ftile_cap_);
     ftile_pub_.Zero(stream_);
     for (int i = 3; i < kFrontierIdx; ++i) idx_[i].Resize(std::max(N_, 1));
+    // (g, h) carried next to the depth buffers' indices (LGAP_CARRY_GH=0: gathered by row)
+    carry_gh_ = [] {
+      const char* e = std::getenv("LGAP_CARRY_GH");
+      return e == nullptr || e[0] != '0';
+    }();
+    for (int i = 0; i < kFrontierIdx; ++i) {
+      if (carry_gh_ && i != 2) fghb_[i].Resize(std::max(N_, 1));
+    }
     // the partition's look-back needs all of its blocks resident: occupancy minus a margin
     int per_cu = FrontierPartitionBlocksPerCU(part_iters_);
     int cap = 8;  // A/B knob LGAP_FPART_BPC (10M rows: 4 -> 327.9, 6 -> 334.7, 8 -> 337.3 it/s)
@@ -1700,6 +1708,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.colbins = colbins_.get();
     a.gh = gh_.get();
     for (int i = 0; i < kFrontierIdx; ++i) a.idx[i] = idx_[i].get();
+    for (int i = 0; i < kFrontierIdx; ++i) a.ghb[i] = fghb_[i].size() ? fghb_[i].get() : nullptr;
     a.N = N_;
     a.stride_dw = tstride_dw_;
     a.width = width_;
@@ -1772,6 +1781,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.ghq = ghq_.get();
     a.qmax = qmax_.get();
     a.quant = QuantHist() && ghq_.size() >= static_cast<size_t>(K_) * N_ ? 1 : 0;
+    a.carry_gh = carry_gh_ && !a.quant ? 1 : 0;  // (quantized histograms read the int8 levels)
     a.qbins = std::max(2, config_->num_grad_quant_bins);
     a.qconst = is_const_hess_ ? 1 : 0;
     {
@@ -2591,7 +2601,8 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(fst_, &st, sizeof(FState), hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemcpyAsync(fexps_, ex.data(), sizeof(FExp) * k, hipMemcpyHostToDevice, stream_));
     facc_.Zero(stream_);
-    const FArgs fa = MakeFArgs();
+    FArgs fa = MakeFArgs();
+    fa.carry_gh = 0;  // (the subsets' rows were uploaded without their (g, h))
     LaunchFrontierHist(fa, FrontierHistLds(), stream_);
     const int pw = fa.quant && fa.qpack ? 1 : 2;
     std::vector<unsigned long long> acc(static_cast<size_t>(k) * pw * TB_);
@@ -3730,6 +3741,8 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<float> label_, weight_, aux_;
   static_assert(kFrontierIdx <= kLeafIdxBufs, "leaf renewal addresses every index buffer");
   DevBuf<int> idx_[kFrontierIdx];
+  DevBuf<float2> fghb_[kFrontierIdx];  // (g, h) next to the frontier's depth-buffer indices
+  bool carry_gh_ = false;
   DevBuf<DevFeature> feat_;
   DevBuf<int> gstart_;
   DevBuf<HistTile> tiles_;

@@ -147,6 +147,11 @@ struct FArgs {
   const uint8_t* colbins;
   const float2* gh;  // class-major (cls from tp)
   int* idx[kFrontierIdx];
+  // (g, h) carried alongside the depth buffers' row indices (carry_gh): the partition writes each
+  // row's (g, h) next to its index, so the histograms read them contiguously instead of
+  // gathering a sector per row (null: buffers without, the root / bag read gh[row])
+  float2* ghb[kFrontierIdx];
+  int carry_gh;
   int N, stride_dw, width, num_groups, TB, F, L, C, kmax;
   const int* gstart;
   const DevFeature* feat;

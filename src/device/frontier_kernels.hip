@@ -168,6 +168,9 @@ template <int W, int MODE>
 __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
                                           const int* gst, unsigned long long* hist, float sg, float sh, double dsg,
                                           double dsh, uint32_t* hist32 = nullptr) {
+  // (g, h) of position p: carried next to the index list (contiguous) or gathered by row
+  const float2* ghp = MODE < 2 && buf >= 0 && a.carry_gh ? a.ghb[buf] : nullptr;
+  if (ghp != nullptr) ghp += start;
   const int tpr = tile.d1 - tile.d0;
   const int rpi = blockDim.x / tpr;
   const int myr = threadIdx.x / tpr;
@@ -181,6 +184,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
 #pragma unroll
   for (int k = 0; k < per; ++k) go[k] = gfirst + k < tile.g1 ? gst[gfirst + k - tile.g0] : -1;
   const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
+  const float2* gsrc = ghp != nullptr ? ghp : gh;  // (indexed by position, or by row)
   const uint16_t* ghq = MODE >= 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
   const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
   const int base = buf < 0 ? start : 0;
@@ -198,7 +202,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
     for (int j = 0; j < R; ++j) {
       word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
       if (MODE >= 2) q[j] = rows[j] >= 0 ? ghq[rows[j]] : 0u;
-      else v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
+      else v[j] = rows[j] >= 0 ? gsrc[ghp != nullptr ? p0 + j * rpi : rows[j]] : make_float2(0.f, 0.f);
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -312,7 +316,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         sg += static_cast<int8_t>(qv >> 8);
         sh += static_cast<long long>(qv & 0xFFu);
       } else {
-        const float2 v = a.gh[static_cast<size_t>(a.tp->cls) * a.N + row];
+        const float2 v = buf >= 0 && a.carry_gh && a.ghb[buf] != nullptr ? a.ghb[buf][start + p]
+                                                                          : a.gh[static_cast<size_t>(a.tp->cls) * a.N + row];
         sg += __double2ll_rn(static_cast<double>(v.x) * dsg);
         sh += __double2ll_rn(static_cast<double>(v.y) * dsh);
       }
@@ -334,6 +339,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     constexpr int per = W == 0 ? 8 : 4 / W;
     const int dw = tile.d0 + myd;
     const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
+    const float2* ghp = MODE < 2 && buf >= 0 && a.carry_gh && a.ghb[buf] != nullptr ? a.ghb[buf] + start : nullptr;
     for (int p = rb + myr; p < re; p += rpi) {
       const int row = FRowAt(a, buf, start + p);
       const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         qh = qv & 0xFFu;
         if (a.qpack) qg = (qg << 32) + qh, qh = 0ull;
       } else {
-        const float2 v = gh[row];
+        const float2 v = ghp != nullptr ? ghp[p] : gh[row];
         qg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.x) * dsg));
         qh = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.y) * dsh));
       }
@@ -1001,7 +1007,7 @@ __device__ __forceinline__ void BlockSumMulti(int* v, int* sh) {
 // LDS barrier, so a block pays a few memory round trips instead of a few per tile. Tiles
 // beyond MAXT (a grid smaller than the round's tiles / MAXT) take the per-tile path.
 template <int ITERS, int MAXT>
-__global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
+__global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(ITERS == 8 ? 5 : 1))) void k_f_partition(FArgs a) {
   static_assert(kFPartThreads == 256, "4 waves per block");
   static_assert(MAXT * ITERS <= 32, "left / valid bits of a thread fit one word");
   constexpr int kTile = kFPartThreads * ITERS;
@@ -1171,6 +1177,19 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
     int lbase = lb[j];
     int rbase = tt * kTile - lbase;
     int* out = a.idx[x.dst_buf] + x.start;
+    // carried (g, h): the source's (contiguous in the parent's list, or by row at the root / bag)
+    float2 gv[ITERS];
+    float2* gout = nullptr;
+    if (a.carry_gh) {
+      gout = a.ghb[x.dst_buf] + x.start;
+      const float2* gsrc = x.src_buf >= 0 ? a.ghb[x.src_buf] : nullptr;
+      const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
+#pragma unroll
+      for (int i = 0; i < ITERS; ++i) {
+        const int r = rows[j][i];
+        gv[i] = r < 0 ? make_float2(0.f, 0.f) : (gsrc != nullptr ? gsrc[x.start + tt * kTile + t + i * kFPartThreads] : gh[r]);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < ITERS; ++i) {
       const bool valid = (vbits >> (j * ITERS + i)) & 1u;
@@ -1193,6 +1212,7 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
         int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
         if (a.part_nt) __builtin_nontemporal_store(rows[j][i], dst);
         else *dst = rows[j][i];
+        if (gout != nullptr) gout[dst - out] = gv[i];
       }
       lbase += tl;
       rbase += tv - tl;
@@ -1231,6 +1251,18 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
     }
     __syncthreads();
     int* out = a.idx[x.dst_buf] + x.start;
+    float2 gv[ITERS];
+    float2* gout = nullptr;
+    if (a.carry_gh) {
+      gout = a.ghb[x.dst_buf] + x.start;
+      const float2* gsrc = x.src_buf >= 0 ? a.ghb[x.src_buf] : nullptr;
+      const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
+#pragma unroll
+      for (int i = 0; i < ITERS; ++i) {
+        const int r = rr[i];
+        gv[i] = r < 0 ? make_float2(0.f, 0.f) : (gsrc != nullptr ? gsrc[x.start + pos0 + i * kFPartThreads] : gh[r]);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < ITERS; ++i) {
       const bool valid = (vb1 >> i) & 1u;
@@ -1253,6 +1285,7 @@ __global__ __launch_bounds__(kFPartThreads) void k_f_partition(FArgs a) {
         int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
         if (a.part_nt) __builtin_nontemporal_store(rr[i], dst);
         else *dst = rr[i];
+        if (gout != nullptr) gout[dst - out] = gv[i];
       }
       lbase += tl;
       rbase += tv - tl;
