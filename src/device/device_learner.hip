@@ -1658,10 +1658,11 @@ class DeviceTreeLearner : public TreeLearner {
     ftile_pub_.Resize(ftile_cap_);
     ftile_pub_.Zero(stream_);
     for (int i = 3; i < kFrontierIdx; ++i) idx_[i].Resize(std::max(N_, 1));
-    // (g, h) carried next to the depth buffers' indices (LGAP_CARRY_GH=0: gathered by row)
+    // (g, h) carried next to the depth buffers' indices (opt-in, LGAP_CARRY_GH=1: at 10M the
+    // histograms gain 6 us per round and the partition loses 12.6 us moving them)
     carry_gh_ = [] {
       const char* e = std::getenv("LGAP_CARRY_GH");
-      return e == nullptr || e[0] != '0';
+      return e != nullptr && e[0] == '1';
     }();
     for (int i = 0; i < kFrontierIdx; ++i) {
       if (carry_gh_ && i != 2) fghb_[i].Resize(std::max(N_, 1));
