@@ -69,6 +69,7 @@ def main() -> int:
         params["use_quantized_grad"] = True
         params["num_grad_quant_bins"] = 4
     gen_s = time.time() - t0
+    print(f"# data generated in {gen_s:.1f} s", file=sys.stderr, flush=True)
     t0 = time.time()
     train = lgb.Dataset(X, y, group=g, params=params, free_raw_data=True)
     valid = lgb.Dataset(Xv, yv, group=gv, reference=train)
@@ -76,9 +77,11 @@ def main() -> int:
     rows = int(len(y))
     del X
     construct_s = time.time() - t0
+    print(f"# dataset + booster in {construct_s:.1f} s ({booster.device_name()})", file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         booster.update()
     device_synchronize()
+    print("# warmup done", file=sys.stderr, flush=True)
     t = time.perf_counter()
     for _ in range(args.steps):
         booster.update()
