@@ -1799,6 +1799,7 @@ class DeviceTreeLearner : public TreeLearner {
       a.qsub = a.quant && !use_dp_ && sub >= 2048 && want ? sub : 0;
     }
     a.hist_copies = HistCopies(a.qsub);
+    a.hist_il = !use_dp_ && a.qsub == 0 && HistInterleave() ? 1 : 0;
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
     if (RawCands() && fnuep_.size() > 0) {
@@ -2921,6 +2922,12 @@ class DeviceTreeLearner : public TreeLearner {
   // rows keep the dataset's stride
   int StrideOf(const uint32_t* rb) const { return rb == rowbins_.get() ? tstride_dw_ : stride_dw_; }
 
+  // bank-interleaved LDS histograms (frontier MODE 0 / 2; LGAP_HIST_IL=0: packed bins)
+  static bool HistInterleave() {
+    const char* e = std::getenv("LGAP_HIST_IL");
+    return e == nullptr || e[0] != '0';
+  }
+
   // Wide rows in several LDS tiles: tiles cut at multiples of RowAlign() dwords and the training
   // rows padded to a multiple of it, so every tile's slice of a row is whole aligned 32 / 64 /
   // 128-byte sectors instead of straddling them (LGAP_ROW_ALIGN_DW: 0 off, 8, 16 or 32)
@@ -3120,6 +3127,18 @@ class DeviceTreeLearner : public TreeLearner {
       t.nbins = bins;
       // a single dword of huge bundles that cannot fit: accumulate straight into global memory
       t.direct = bins > max_bins ? 1 : 0;
+      // bank-interleaved LDS slots (k_f_hist il): (largest group's bins) x (groups rounded up to
+      // 16), when that stays within 1.25x of the packed tile and the 150 KB block budget
+      t.pad = 0;
+      if (!t.direct && HistInterleave()) {
+        int maxb = 0;
+        for (int g = t.g0; g < t.g1; ++g) maxb = std::max(maxb, data_->group(g).num_bin);
+        const size_t il = static_cast<size_t>(maxb) * ((t.g1 - t.g0 + 15) & ~15) * 8;
+        if (il <= static_cast<size_t>(bins) * 8 * 5 / 4 + 4096 && il + sizeof(int) * (t.g1 - t.g0) + 16 <= 150 * 1024) {
+          t.pad = maxb;
+          hist_lds_bytes_ = std::max(hist_lds_bytes_, il + sizeof(int) * (t.g1 - t.g0) + 16);
+        }
+      }
       tiles.push_back(t);
       if (!t.direct) {
         hist_lds_bytes_ = std::max(hist_lds_bytes_, static_cast<size_t>(bins) * acc + sizeof(int) * (t.g1 - t.g0) + 16);

@@ -218,6 +218,7 @@ struct FArgs {
   int hist_min_rows, hist_grid;
   int hist_threads;  // 512 or 1024 threads per histogram block
   int hist_copies;   // LDS histogram copies per block (2: even / odd waves apart; single-tile data)
+  int hist_il;       // bank-interleaved LDS histograms (tiles with pad = their largest group's bins)
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)

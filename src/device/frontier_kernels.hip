@@ -164,10 +164,16 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
 //           field can overflow (a.qsub rows) and folds the narrow bins into the 64-bit
 //           LDS histogram after each one.
 // Zero bins are skipped by the flush (most of a small leaf's histogram).
+// Bank-interleaved LDS layout (il_gp > 0, MODE 0 / 2): bin b of the tile's local group g at slot
+// b * il_gp + g (il_gp = group count rounded up to 16), so a ds_add_u64 of group g always hits
+// bank pair g mod 16 whatever the bin. A lane adds its dword's groups in an order rotated by its
+// row (row r starts at group r mod per): the 16 lanes of a bank group (two or three rows of the
+// dword-per-lane mapping) then hit different bank pairs, instead of colliding on random bins
+// ~3-4 ways (the row phase of a histogram is bound by these conflicts).
 template <int W, int MODE>
 __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
                                           const int* gst, unsigned long long* hist, float sg, float sh, double dsg,
-                                          double dsh, uint32_t* hist32 = nullptr) {
+                                          double dsh, uint32_t* hist32 = nullptr, int il_gp = 0) {
   // (g, h) of position p: carried next to the index list (contiguous) or gathered by row
   const float2* ghp = MODE < 2 && buf >= 0 && a.carry_gh ? a.ghb[buf] : nullptr;
   if (ghp != nullptr) ghp += start;
@@ -180,9 +186,24 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   constexpr int R = LGAP_FHIST_R;
   const int dw = tile.d0 + myd;
   const int gfirst = dw * per;
-  int go[per];
+  // per k (the k-th add of a row): the group's LDS base (interleaved: its local index) and its
+  // bit shift in the dword, rotated by the row when interleaved
+  int go[per], gsh[per];
+  const int rot = (MODE == 0 || MODE == 2) && il_gp > 0 ? (myr & (per - 1)) : 0;
 #pragma unroll
-  for (int k = 0; k < per; ++k) go[k] = gfirst + k < tile.g1 ? gst[gfirst + k - tile.g0] : -1;
+  for (int kk = 0; kk < per; ++kk) {
+    int gv = -1, sv = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+      if (k == ((kk + rot) & (per - 1))) {
+        const int gl = gfirst + k - tile.g0;
+        gv = gfirst + k < tile.g1 ? (il_gp > 0 ? gl : gst[gl]) : -1;
+        sv = (W == 0 ? 4 : W == 1 ? 8 : 16) * k;
+      }
+    }
+    go[kk] = gv;
+    gsh[kk] = sv;
+  }
   const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
   const float2* gsrc = ghp != nullptr ? ghp : gh;  // (indexed by position, or by row)
   const uint16_t* ghq = MODE >= 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
@@ -223,11 +244,9 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
       }
 #pragma unroll
       for (int k = 0; k < per; ++k) {
-        const uint32_t b = W == 0   ? ((word[j] >> (4 * k)) & 0xFu)
-                           : W == 1 ? ((word[j] >> (8 * k)) & 0xFFu)
-                                    : ((word[j] >> (16 * k)) & 0xFFFFu);
+        const uint32_t b = (word[j] >> gsh[k]) & (W == 0 ? 0xFu : W == 1 ? 0xFFu : 0xFFFFu);
         if (b != 0u && go[k] >= 0) {
-          const int o = go[k] + static_cast<int>(b);
+          const int o = il_gp > 0 ? static_cast<int>(b) * il_gp + go[k] : go[k] + static_cast<int>(b);
           if (MODE == 3) {
             atomicAdd(&hist32[o], p32);
           } else if (MODE != 1) {
@@ -377,11 +396,14 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   const int bg = FixedPointExp(k30, rows_in_block, __uint_as_float(a.ghmax[0]), sbg);
   const int bh = FixedPointExp(k30, rows_in_block, __uint_as_float(a.ghmax[1]), sbh);
   const float sg = ldexpf(1.f, bg), sh = ldexpf(1.f, bh);
-  const int words = MODE != 1 ? tile.nbins : 2 * tile.nbins;
+  // bank-interleaved slots (FHistRows): tile.pad = the tile's largest group bin count, 0 = off
+  const int ng = tile.g1 - tile.g0;
+  const int il_gp = (MODE == 0 || MODE == 2) && a.hist_il && tile.pad > 0 ? ((ng + 15) & ~15) : 0;
+  const int words = il_gp > 0 ? tile.pad * il_gp : (MODE != 1 ? tile.nbins : 2 * tile.nbins);
   // two LDS copies of the histogram when they fit (hist_copies = 2, single-tile data): even
   // and odd waves accumulate into different copies, halving same-bin atomic collisions (a deep
   // node's rows crowd few bins of its split features); the flush adds the two
-  const int copies = MODE == 3 ? 1 : (a.hist_copies > 1 ? 2 : 1);
+  const int copies = MODE == 3 || il_gp > 0 ? 1 : (a.hist_copies > 1 ? 2 : 1);
   unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
   uint32_t* hist32 = reinterpret_cast<uint32_t*>(hist + words);
   int* gst = reinterpret_cast<int*>(MODE == 3 ? reinterpret_cast<unsigned long long*>(hist32 + ((tile.nbins + 1) & ~1))
@@ -410,7 +432,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     }
   } else {
     FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist + (copies > 1 ? ((t >> 6) & 1) * words : 0), sg, sh, dsg,
-                       dsh);
+                       dsh, nullptr, il_gp);
     __syncthreads();
   }
   FStamp(a, rnd, kFStampHist, 2);
@@ -420,34 +442,43 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   // every block starts its flush at its own offset of the tile, so the blocks' concurrent
   // atomics hit different accumulator words instead of queueing on the same ones
   const int rot = a.flush_rot ? static_cast<int>((static_cast<long long>(blockIdx.x) * tile.nbins) / gridDim.x) : 0;
-  if (MODE == 0) {
+  if (MODE == 0 || MODE >= 2) {
     // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
     // GlobalScaleExp; the guard keeps a degenerate max of 0 harmless)
     const int shg = max(0, EG - bg), shh = max(0, EH - bh);
-    for (int j = t; j < tile.nbins; j += blockDim.x) {
-      const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
-      const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);  // (packed fields: exact)
-      if (x == 0ull) continue;
-      const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
-      const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
-      const long long qg = gs * (1ll << shg);
-      const long long qh = static_cast<long long>(hs) * (1ll << shh);
-      if (qg) atomicAdd(&out[2 * i], static_cast<unsigned long long>(qg));
-      if (qh) atomicAdd(&out[2 * i + 1], static_cast<unsigned long long>(qh));
-    }
-  } else if (MODE >= 2) {
     const bool pack = a.qpack != 0;
-    for (int j = t; j < tile.nbins; j += blockDim.x) {
-      const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
-      const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);
-      if (x == 0ull) continue;
-      if (pack) {
+    auto flush = [&](int i, unsigned long long x) {
+      if (MODE == 0) {
+        const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
+        const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
+        const long long qg = gs * (1ll << shg);
+        const long long qh = static_cast<long long>(hs) * (1ll << shh);
+        if (qg) atomicAdd(&out[2 * i], static_cast<unsigned long long>(qg));
+        if (qh) atomicAdd(&out[2 * i + 1], static_cast<unsigned long long>(qh));
+      } else if (pack) {
         atomicAdd(&out[i], x);  // (pw == 1)
       } else {
         const unsigned long long hs = x & 0xFFFFFFFFull;
         const long long gs = static_cast<long long>(x - hs) >> 32;
         if (gs) atomicAdd(&out[2 * i], static_cast<unsigned long long>(gs));
         if (hs) atomicAdd(&out[2 * i + 1], hs);
+      }
+    };
+    if (il_gp > 0) {
+      // one group per wave: consecutive lanes flush consecutive accumulator words
+      const int nw = static_cast<int>(blockDim.x) >> 6, lane = t & 63;
+      for (int gl = t >> 6; gl < ng; gl += nw) {
+        const int b0 = gst[gl], nb = (gl + 1 < ng ? gst[gl + 1] : tile.nbins) - b0;
+        for (int b = lane; b < nb; b += 64) {
+          const unsigned long long x = hist[b * il_gp + gl];
+          if (x != 0ull) flush(b0 + b, x);
+        }
+      }
+    } else {
+      for (int j = t; j < tile.nbins; j += blockDim.x) {
+        const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
+        const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);  // (packed fields: exact)
+        if (x != 0ull) flush(i, x);
       }
     }
   } else {
