@@ -465,9 +465,12 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       }
     };
     if (il_gp > 0) {
-      // one group per wave: consecutive lanes flush consecutive accumulator words
+      // one group per wave: consecutive lanes flush consecutive accumulator words; each block
+      // starts at its own group, so concurrent blocks' atomics hit different accumulator lines
       const int nw = static_cast<int>(blockDim.x) >> 6, lane = t & 63;
-      for (int gl = t >> 6; gl < ng; gl += nw) {
+      const int g_rot = static_cast<int>(blockIdx.x % static_cast<unsigned>(ng));
+      for (int gi = t >> 6; gi < ng; gi += nw) {
+        const int gl = gi + g_rot < ng ? gi + g_rot : gi + g_rot - ng;
         const int b0 = gst[gl], nb = (gl + 1 < ng ? gst[gl + 1] : tile.nbins) - b0;
         for (int b = lane; b < nb; b += 64) {
           const unsigned long long x = hist[b * il_gp + gl];
