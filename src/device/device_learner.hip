@@ -1800,6 +1800,13 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.hist_copies = HistCopies(a.qsub);
     a.hist_il = !use_dp_ && a.qsub == 0 && HistInterleave() ? 1 : 0;
+    {
+      // one wave per scan item on wide data (LGAP_SCAN_WAVE: 0 never, 1 always, default F >= 64)
+      const char* e = std::getenv("LGAP_SCAN_WAVE");
+      const int v = e != nullptr ? std::atoi(e) : -1;
+      const bool fits = kFScanWaves * FrontierScanWaveBytes(max_bin_, cat_p2_) <= 150 * 1024;
+      a.scan_wave = fits && (v == 1 || (v < 0 && F_ >= 64)) ? 1 : 0;
+    }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
     if (RawCands() && fnuep_.size() > 0) {

@@ -219,6 +219,7 @@ struct FArgs {
   int hist_threads;  // 512 or 1024 threads per histogram block
   int hist_copies;   // LDS histogram copies per block (2: even / odd waves apart; single-tile data)
   int hist_il;       // bank-interleaved LDS histograms (tiles with pad = their largest group's bins)
+  int scan_wave;     // k_f_scan_w (one wave per (expansion, feature)) instead of one block per item
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)
@@ -313,6 +314,15 @@ void LaunchFrontierResults(const FArgs& a, void* host_out, hipStream_t s);
 void LaunchFrontierInit(const FArgs& a, hipStream_t s);
 void LaunchFrontierHist(const FArgs& a, size_t lds_bytes, hipStream_t s);
 void LaunchFrontierScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
+
+// Wave-per-item scan (k_f_scan_w, wide data): per wave the two fp64 (g, h) histograms of the
+// widest feature and one categorical sort slot (index, ctr); four waves per block.
+constexpr int kFScanWaves = 4;
+__host__ __device__ inline size_t FrontierScanWaveBytes(int max_bin, int cat_p2) {
+  const size_t b = static_cast<size_t>(max_bin) * 4 * sizeof(double) + static_cast<size_t>((cat_p2 + 1) & ~1) * sizeof(int) +
+                   static_cast<size_t>(cat_p2) * sizeof(double);
+  return (b + 15) & ~static_cast<size_t>(15);
+}
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
 // CEGB lazy penalties: unmarked-row counts of the round's smaller children; after a tree, the
 // final leaves' rows marked for the features on their paths

@@ -894,6 +894,195 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_f_scan_w: k_f_scan with ONE WAVE per (expansion, feature) item, the smaller child scanned
+// before the larger one by the same wave. For wide data a round holds thousands of items and
+// the block kernel (two of its four waves scanning, 183 VGPRs: two resident blocks per CU)
+// is bound by how many items run at once; here four items share a block and nothing waits
+// on a block barrier. The same records as k_f_scan's plain instantiation for numerical
+// features without forced splits (LaunchFrontierScan routes everything else to k_f_scan).
+__device__ __forceinline__ void FWaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ __align__(8) unsigned char s_out_raw[kFScanWaves * sizeof(SplitInfo)];
+  __shared__ SplitKey s_key[kFScanWaves];
+  const FState* stp = a.st;
+  if (stp->done) return;
+  const int e0 = a.e_lo, e1 = min(stp->k, a.e_hi), F = a.F;
+  const int total = max(0, e1 - e0) * F;
+  const int rnd = stp->round;
+  FStamp(a, rnd, kFStampScan, 0);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
+  double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
+  if (a.quant) QuantScales(a, &inv_g, &inv_h);
+  const bool qpack = a.quant && a.qpack;
+  const size_t TB2 = 2 * static_cast<size_t>(a.TB);
+  double* hs_full = reinterpret_cast<double*>(smem + w * FrontierScanWaveBytes(a.max_bin, a.cat_p2));
+  double* hl_full = hs_full + 2 * a.max_bin;
+  SplitInfo* out = reinterpret_cast<SplitInfo*>(s_out_raw) + w;
+  SplitKey* key = &s_key[w];
+  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  for (int item = static_cast<int>(blockIdx.x) * kFScanWaves + w; item < total;
+       item += static_cast<int>(gridDim.x) * kFScanWaves) {
+    const int e = e0 + item / F, f = item - (e - e0) * F;
+    const FExp& xr = a.exps[e];
+    if (xr.skip) continue;
+    const int cs = xr.smaller, cl = xr.larger, p = xr.parent;
+    const DevFeature fi = a.feat[f];
+    const int nbin = fi.num_bin;
+    const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
+    const size_t pw = qpack ? 1 : 2;
+    unsigned long long* acc = a.acc + static_cast<size_t>(e) * pw * a.TB + pw * static_cast<size_t>(fi.hist_offset);
+    const double* gp = (p >= 0 && cl >= 0) ? a.slots + static_cast<size_t>(p) * TB2 + v0 : nullptr;
+    double* gs = a.slots + static_cast<size_t>(cs) * TB2 + v0;
+    double* gl = cl >= 0 ? a.slots + static_cast<size_t>(cl) * TB2 + v0 : nullptr;
+    const bool skip_both = !a.used_bytree[f] || !(p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1);
+    const int splp = p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1;
+#pragma unroll 1
+    for (int kk = lane; kk < nbin - 1; kk += 64) {
+      const unsigned long long x0 = acc[pw * kk], x1 = qpack ? 0ull : acc[2 * kk + 1];
+      acc[pw * kk] = 0ull;
+      if (!qpack) acc[2 * kk + 1] = 0ull;
+      long long q0 = static_cast<long long>(x0), q1 = static_cast<long long>(x1);
+      if (qpack) {
+        const unsigned long long hs = x0 & 0xFFFFFFFFull;
+        q0 = static_cast<long long>(x0 - hs) >> 32;
+        q1 = static_cast<long long>(hs);
+      }
+      const double sv0 = static_cast<double>(q0) * inv_g, sv1 = static_cast<double>(q1) * inv_h;
+      const int b = kk < fi.mfb ? kk : kk + 1;
+      hs_full[2 * b] = sv0;
+      hs_full[2 * b + 1] = sv1;
+      gs[2 * kk] = sv0;
+      gs[2 * kk + 1] = sv1;
+      if (gl) {
+        const double l0 = gp[2 * kk] - sv0, l1 = gp[2 * kk + 1] - sv1;
+        hl_full[2 * b] = l0;
+        hl_full[2 * b + 1] = l1;
+        gl[2 * kk] = l0;
+        gl[2 * kk + 1] = l1;
+      }
+    }
+    FWaveSync();
+    // most-frequent bins = leaf totals - stored bins
+    const int nsel = cl >= 0 ? 2 : 1;
+#pragma unroll 1
+    for (int sel = 0; sel < nsel; ++sel) {
+      double* H = sel ? hl_full : hs_full;
+      const double2 lsum = a.lsum[sel ? cl : cs];
+      double sgs = 0.0, shs = 0.0;
+#pragma unroll 1
+      for (int b = lane; b < nbin; b += 64) {
+        if (b == fi.mfb) continue;
+        sgs += H[2 * b];
+        shs += H[2 * b + 1];
+      }
+      sgs = WaveSum(sgs);
+      shs = WaveSum(shs);
+      if (lane == 0) {
+        H[2 * fi.mfb] = lsum.x - sgs;
+        H[2 * fi.mfb + 1] = lsum.y - shs;
+      }
+    }
+    FWaveSync();
+#pragma unroll 1
+    for (int sel = 0; sel < nsel; ++sel) {
+      const int my = sel ? cl : cs;
+      const double* H = sel ? hl_full : hs_full;
+      // the child's statistics (uniform loads: every lane reads the same words)
+      const double2 lsum = a.lsum[my];
+      const FNode nd = a.nodes[my];
+      const double pre_out = a.lout[my];
+      const LeafBounds bnd = a.bounds[my];
+      if (lane == 0) {
+        out->Reset();
+        SplitKey kz;
+        kz.gain = kMinScore;
+        kz.feature = -1;
+        kz.threshold = 0;
+        kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
+        kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
+        kz.pos = f;
+        kz.pad2 = 0;
+        *key = kz;
+      }
+      FWaveSync();
+      const double sg = lsum.x, sh = lsum.y;
+      const int n = nd.gcount;
+      const int depth = nd.depth;
+      if (!skip_both) {
+        double po;
+        if (p < 0) {
+          SplitParams p0 = a.sp;
+          p0.path_smooth = 0.0;
+          po = LeafOutputRaw(sg, sh, p0, n, 0.0);
+          if (f == 0 && lane == 0) a.lout[0] = po;
+        } else {
+          po = pre_out;
+        }
+        const LeafBounds bounds = bnd;
+        // (numerical features only: LaunchFrontierScan routes categorical data to k_f_scan)
+        const bool spl = ScanNumericalWave(a.sp, fi, H, sg, sh, n, po, bounds, 0, out);
+        if (lane == 0) {
+          a.spl[static_cast<size_t>(my) * F + f] = spl ? 1 : 0;
+          if (!spl || (a.max_depth > 0 && depth >= a.max_depth)) {
+            out->Reset();
+          } else {
+            out->feature = f;
+            if (!a.cegb_raw) {
+              if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
+              if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
+            }
+            if (a.ic && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
+          }
+        }
+      } else if (lane == 0) {
+        a.spl[static_cast<size_t>(my) * F + f] = static_cast<uint8_t>(splp);
+        if (p < 0 && f == 0) {
+          SplitParams p0 = a.sp;
+          p0.path_smooth = 0.0;
+          a.lout[0] = LeafOutputRaw(sg, sh, p0, n, 0.0);
+        }
+      }
+      if (lane == 0) {
+        key->feature = out->feature;
+        key->gain = SafeGain(*out);
+        key->threshold = out->threshold;
+        key->group = fi.group;
+        key->offset = fi.offset;
+        key->num_bin = fi.num_bin;
+        key->mfb = fi.mfb;
+        key->default_bin = fi.default_bin;
+        key->missing = fi.missing;
+        key->default_left = out->default_left;
+        key->is_cat = fi.bin_type != 0 ? 1 : 0;
+        key->pad0 = a.cegb_raw && out->feature >= 0 ? out->monotone_type : 0;
+      }
+      FWaveSync();
+      // publish (dword-parallel copy of the LDS records)
+      const size_t q = (static_cast<size_t>(e) * 2 + sel) * F + f;
+      for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
+        if (i < kKeyWords) {
+          reinterpret_cast<uint32_t*>(a.ckey + q)[i] = reinterpret_cast<const uint32_t*>(key)[i];
+        } else {
+          reinterpret_cast<uint32_t*>(a.cinfo + q)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(out)[i - kKeyWords];
+        }
+      }
+      FWaveSync();  // (out / key reused by the next child)
+    }
+    FWaveSync();  // (the histograms in LDS reused by the next item)
+  }
+  FStampEnd(a, rnd, kFStampScan);
+}
+
+// ---------------------------------------------------------------------------
 // k_f_partition: stable 2-way partition of every expanded parent (reference
 // data_partition.hpp:101 / cuda_data_partition.cu:290-937, as one launch).
 // Tiles of all expansions are numbered globally ([tile0_e, tile0_e + ntiles_e) for
@@ -2674,8 +2863,16 @@ void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
 }
 
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
+  const bool ext = a.voting || a.xrng != nullptr || a.fowned != nullptr || a.scan_best;
+  if (a.scan_wave && !ext && a.num_forced == 0) {
+    // one wave per item: enough blocks for every item of the widest round, at most 8 per CU's worth
+    const int grid = std::max(1, std::min((a.kmax * a.F + kFScanWaves - 1) / kFScanWaves, 2048));
+    k_f_scan_w<<<grid, kFScanWaves * 64, kFScanWaves * FrontierScanWaveBytes(a.max_bin, a.cat_p2), s>>>(a);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int grid = std::max(1, std::min(a.kmax * a.F, 4096));
-  if (a.voting || a.xrng != nullptr || a.fowned != nullptr || a.scan_best) k_f_scan<true><<<grid, kFScanThreads, lds, s>>>(a);
+  if (ext) k_f_scan<true><<<grid, kFScanThreads, lds, s>>>(a);
   else k_f_scan<false><<<grid, kFScanThreads, lds, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
@@ -2758,6 +2955,9 @@ void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(scan_lds)));
   }
+  // (the wave kernel: four waves' histograms, up to 4 x 32 KB for 1024-bin features)
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan_w), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(std::min<size_t>(160 * 1024, 4 * scan_lds))));
 }
 
 }  // namespace device
