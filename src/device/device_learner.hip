@@ -1805,7 +1805,7 @@ class DeviceTreeLearner : public TreeLearner {
       const char* e = std::getenv("LGAP_SCAN_WAVE");
       const int v = e != nullptr ? std::atoi(e) : -1;
       const bool fits = kFScanWaves * FrontierScanWaveBytes(max_bin_, cat_p2_) <= 150 * 1024;
-      a.scan_wave = fits && (v == 1 || (v < 0 && F_ >= 64)) ? 1 : 0;
+      a.scan_wave = fits && !has_cat_ && (v == 1 || (v < 0 && F_ >= 64)) ? 1 : 0;  // (numerical features only)
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
