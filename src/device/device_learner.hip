@@ -3140,10 +3140,12 @@ class DeviceTreeLearner : public TreeLearner {
       if (!t.direct && HistInterleave()) {
         int maxb = 0;
         for (int g = t.g0; g < t.g1; ++g) maxb = std::max(maxb, data_->group(g).num_bin);
+        // (plus the packed image the interleaved slots are transposed into before the flush)
         const size_t il = static_cast<size_t>(maxb) * ((t.g1 - t.g0 + 15) & ~15) * 8;
-        if (il <= static_cast<size_t>(bins) * 8 * 5 / 4 + 4096 && il + sizeof(int) * (t.g1 - t.g0) + 16 <= 150 * 1024) {
+        const size_t need = il + sizeof(int) * ((t.g1 - t.g0 + 1) & ~1) + static_cast<size_t>(bins) * 8 + 16;
+        if (il <= static_cast<size_t>(bins) * 8 * 5 / 4 + 4096 && need <= 150 * 1024) {
           t.pad = maxb;
-          hist_lds_bytes_ = std::max(hist_lds_bytes_, il + sizeof(int) * (t.g1 - t.g0) + 16);
+          hist_lds_bytes_ = std::max(hist_lds_bytes_, need);
         }
       }
       tiles.push_back(t);

@@ -411,6 +411,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   uint32_t* hist32 = reinterpret_cast<uint32_t*>(hist + words);
   int* gst = reinterpret_cast<int*>(MODE == 3 ? reinterpret_cast<unsigned long long*>(hist32 + ((tile.nbins + 1) & ~1))
                                               : hist + copies * words);
+  // (interleaved: the packed image the flush reads, after gst)
+  unsigned long long* packed = il_gp > 0 ? reinterpret_cast<unsigned long long*>(gst + ((ng + 1) & ~1)) : nullptr;
   for (int i = t; i < copies * words; i += blockDim.x) hist[i] = 0ull;
   if (MODE == 3) {
     for (int i = t; i < tile.nbins; i += blockDim.x) hist32[i] = 0u;
@@ -436,6 +438,17 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   } else {
     FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist + (copies > 1 ? ((t >> 6) & 1) * words : 0), sg, sh, dsg,
                        dsh, nullptr, il_gp);
+    __syncthreads();
+  }
+  if (il_gp > 0) {
+    // interleaved slots -> the packed image (conflict-free reads in slot order), so the flush
+    // below reads consecutive bins of a group from consecutive words
+    for (int sl = t; sl < words; sl += blockDim.x) {
+      const int b = sl / il_gp, gl = sl - b * il_gp;
+      if (gl >= ng) continue;
+      const int nb = (gl + 1 < ng ? gst[gl + 1] : tile.nbins) - gst[gl];
+      if (b < nb) packed[gst[gl] + b] = hist[sl];
+    }
     __syncthreads();
   }
   FStamp(a, rnd, kFStampHist, 2);
@@ -468,17 +481,10 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       }
     };
     if (il_gp > 0) {
-      // one group per wave: consecutive lanes flush consecutive accumulator words; each block
-      // starts at its own group, so concurrent blocks' atomics hit different accumulator lines
-      const int nw = static_cast<int>(blockDim.x) >> 6, lane = t & 63;
-      const int g_rot = static_cast<int>(blockIdx.x % static_cast<unsigned>(ng));
-      for (int gi = t >> 6; gi < ng; gi += nw) {
-        const int gl = gi + g_rot < ng ? gi + g_rot : gi + g_rot - ng;
-        const int b0 = gst[gl], nb = (gl + 1 < ng ? gst[gl + 1] : tile.nbins) - b0;
-        for (int b = lane; b < nb; b += 64) {
-          const unsigned long long x = hist[b * il_gp + gl];
-          if (x != 0ull) flush(b0 + b, x);
-        }
+      for (int j = t; j < tile.nbins; j += blockDim.x) {
+        const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
+        const unsigned long long x = packed[i];
+        if (x != 0ull) flush(i, x);
       }
     } else {
       for (int j = t; j < tile.nbins; j += blockDim.x) {
