@@ -1799,7 +1799,7 @@ class DeviceTreeLearner : public TreeLearner {
       a.qsub = a.quant && !use_dp_ && sub >= 2048 && want ? sub : 0;
     }
     a.hist_copies = HistCopies(a.qsub);
-    a.hist_il = !use_dp_ && a.qsub == 0 && HistInterleave() ? 1 : 0;
+    a.hist_il = !use_dp_ && a.qsub == 0 ? HistInterleave() : 0;
     {
       // one wave per scan item on wide data (LGAP_SCAN_WAVE: 0 never, 1 always, default F >= 64)
       const char* e = std::getenv("LGAP_SCAN_WAVE");
@@ -2930,9 +2930,10 @@ class DeviceTreeLearner : public TreeLearner {
   int StrideOf(const uint32_t* rb) const { return rb == rowbins_.get() ? tstride_dw_ : stride_dw_; }
 
   // bank-interleaved LDS histograms (frontier MODE 0 / 2; LGAP_HIST_IL=0: packed bins)
-  static bool HistInterleave() {
+  // (1: the root round's contiguous rows only, 2: every round)
+  static int HistInterleave() {
     const char* e = std::getenv("LGAP_HIST_IL");
-    return e == nullptr || e[0] != '0';
+    return e == nullptr ? 1 : std::atoi(e);
   }
 
   // Wide rows in several LDS tiles: tiles cut at multiples of RowAlign() dwords and the training
@@ -3137,7 +3138,7 @@ class DeviceTreeLearner : public TreeLearner {
       // bank-interleaved LDS slots (k_f_hist il): (largest group's bins) x (groups rounded up to
       // 16), when that stays within 1.25x of the packed tile and the 150 KB block budget
       t.pad = 0;
-      if (!t.direct && HistInterleave()) {
+      if (!t.direct && HistInterleave() > 0) {
         int maxb = 0;
         for (int g = t.g0; g < t.g1; ++g) maxb = std::max(maxb, data_->group(g).num_bin);
         // (plus the packed image the interleaved slots are transposed into before the flush)

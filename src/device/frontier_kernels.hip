@@ -401,7 +401,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   // (only over contiguous rows -- the root without a bag -- where the adds, not the row gathers,
   // bound the pass: A/B at 10M, root round 184 -> 161 us; deeper rounds lose on the flush, whose
   // per-group reads of interleaved slots conflict)
-  const int il_gp = (MODE == 0 || MODE == 2) && a.hist_il && tile.pad > 0 && buf < 0 ? ((ng + 15) & ~15) : 0;
+  const int il_gp = (MODE == 0 || MODE == 2) && a.hist_il && tile.pad > 0 && (buf < 0 || a.hist_il > 1) ? ((ng + 15) & ~15) : 0;
   const int words = il_gp > 0 ? tile.pad * il_gp : (MODE != 1 ? tile.nbins : 2 * tile.nbins);
   // two LDS copies of the histogram when they fit (hist_copies = 2, single-tile data): even
   // and odd waves accumulate into different copies, halving same-bin atomic collisions (a deep
