@@ -1806,6 +1806,8 @@ class DeviceTreeLearner : public TreeLearner {
       const int v = e != nullptr ? std::atoi(e) : -1;
       const bool fits = kFScanWaves * FrontierScanWaveBytes(max_bin_, cat_p2_) <= 150 * 1024;
       a.scan_wave = fits && !has_cat_ && (v == 1 || (v < 0 && F_ >= 64)) ? 1 : 0;  // (numerical features only)
+      const char* g = std::getenv("LGAP_SCAN_GRID");
+      a.scan_grid = g != nullptr ? std::max(0, std::atoi(g)) : 0;
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;

@@ -2877,7 +2877,7 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
     HIP_CHECK(hipGetLastError());
     return;
   }
-  const int grid = std::max(1, std::min(a.kmax * a.F, 4096));
+  const int grid = std::max(1, std::min(a.kmax * a.F, a.scan_grid > 0 ? a.scan_grid : 4096));
   if (ext) k_f_scan<true><<<grid, kFScanThreads, lds, s>>>(a);
   else k_f_scan<false><<<grid, kFScanThreads, lds, s>>>(a);
   HIP_CHECK(hipGetLastError());
