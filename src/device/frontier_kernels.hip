@@ -2961,9 +2961,9 @@ void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(scan_lds)));
   }
-  // (the wave kernel: four waves' histograms, up to 4 x 32 KB for 1024-bin features)
+  // (the wave kernel: four waves' histograms; the learner uses it only when they fit 150 KB)
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_f_scan_w), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                static_cast<int>(std::min<size_t>(160 * 1024, 4 * scan_lds))));
+                                static_cast<int>(std::min<size_t>(150 * 1024, 4 * scan_lds))));
 }
 
 }  // namespace device
