@@ -2810,9 +2810,14 @@ class DeviceTreeLearner : public TreeLearner {
       const char* e = std::getenv("LGAP_HIST_BLOCKS");  // A/B knob
       return e ? std::max(0, std::atoi(e)) : 0;
     }();
+    // (multi-tile: as many row blocks per tile as the CUs hold at once over all tiles -- two
+    // blocks per CU when the tile's LDS allows, one for 150 KB tiles. Every row block flushes
+    // its whole tile with global atomics: LambdaRank 2M x 300 moved 130 MB of atomics per
+    // histogram launch with 102 row blocks x 5 tiles of 128 KB, twice the resident blocks)
+    const int bpc = std::max(1, std::min(2, static_cast<int>((160 * 1024) / std::max<size_t>(hist_lds_bytes_, 1))));
     const int want = config_->device_hist_blocks > 0 ? config_->device_hist_blocks
                      : env_blocks > 0                ? env_blocks
-                                                     : std::min(num_cu_, std::max(1, 2 * num_cu_ / std::max(1, num_tiles_)));
+                                                     : std::min(num_cu_, std::max(1, bpc * num_cu_ / std::max(1, num_tiles_)));
     // partial-histogram slab: one row of 2 * TB accumulators per block, capped at 4 GiB
     const size_t row_bytes = 2 * static_cast<size_t>(TB_) * (use_dp_ ? 8 : 4);
     const int mem_cap = static_cast<int>(std::max<size_t>(1, (size_t(4) << 30) / std::max<size_t>(row_bytes, 1)));
