@@ -1810,6 +1810,8 @@ class DeviceTreeLearner : public TreeLearner {
       // mostly-idle blocks being dispatched every round; A/B 10M 2.850 vs 2.875, 1.25M 1.331 vs 1.341)
       const char* g = std::getenv("LGAP_SCAN_GRID");
       a.scan_grid = g != nullptr ? std::max(0, std::atoi(g)) : 512;
+      const char* sr = std::getenv("LGAP_SEL_BLOCK_RANK");
+      a.sel_block_rank = sr != nullptr && sr[0] == '1' ? 1 : 0;
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;

@@ -221,6 +221,7 @@ struct FArgs {
   int hist_il;       // bank-interleaved LDS histograms (tiles with pad = their largest group's bins)
   int scan_wave;     // k_f_scan_w (one wave per (expansion, feature)) instead of one block per item
   int scan_grid;     // cap of the block scan's grid (A/B knob LGAP_SCAN_GRID; 0: 4096)
+  int sel_block_rank;  // the select's block-wide rank / scan for <= 64 alive nodes too (A/B knob)
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)

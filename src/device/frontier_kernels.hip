@@ -2119,6 +2119,52 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     // position is within the speculation budget: best-first order commits at most R more
     // splits and takes them roughly by gain. Policy 0 budgets R minus every expanded but
     // uncommitted node. The blocked node always goes first.
+    if (na <= 64 && !a.sel_bitonic && !a.sel_block_rank) {
+      // one wave ranks, scans and takes (no block barriers): each lane one alive node, its
+      // position = alive nodes with a better key (gain desc, cid asc; keys are unique)
+      if (w == 0) {
+        int r = -1, ci = 0x7fffffff;
+        double gi = -INFINITY;
+        if (lane < na) {
+          r = s_ac[lane];
+          ci = r >= 0 ? r : ~r;
+          gi = s_gain[ci];
+        }
+        int pos = 0;
+        for (int j = 0; j < na; ++j) {
+          const double gj = __shfl(gi, j, kWave);
+          const int cj = __shfl(ci, j, kWave);
+          pos += (gj > gi || (gj == gi && cj < ci)) ? 1 : 0;
+        }
+        if (lane < na) s_sc[pos] = r;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int rc = lane < na ? s_sc[lane] : -1;  // lane = sorted position
+        const bool fl = rc >= 0 && rc != blocked;
+        const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const int ex = __popcll(__ballot(fl) & lt);
+        const int cap_nodes = (C - cid_next) / 2 - (R - 1);
+        const float alpha = a.tp->spec_alpha > 0.f ? a.tp->spec_alpha : 1.f;
+        const int budget = static_cast<int>(alpha * static_cast<float>(R)) + a.spec_cap;
+        int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
+                                : min(a.kmax, max(1, cap_nodes));
+        if (a.kcap != nullptr && rnd + 1 < kFrontierRoundCap) lim = min(lim, max(1, a.kcap[rnd + 1]));
+        int kk = 0;
+        if (rc >= 0) {
+          const int rr = rc == blocked ? 0 : ex + (blocked >= 0 ? 1 : 0);
+          const bool take = a.policy == 0 || rc == blocked || lane < budget;
+          if (take && rr < lim) {
+            s_exp[rr] = rc;
+            kk = rr + 1;
+          }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) kk = max(kk, __shfl_xor(kk, o, kWave));
+        if (lane == 0) s_k = kk;
+      }
+      __syncthreads();
+    } else {
     int P2 = 64;
     while (P2 < na) P2 <<= 1;
     if (na <= kSelRankMax && !a.sel_bitonic) {
@@ -2217,6 +2263,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       ex += fl[q];
     }
     __syncthreads();
+    }
     FStamp(a, rnd, kFStampSel, 5);
     // (the node capacity bounds the round: expansions voided by CEGB first-use events leave
     // dead cids behind, so the reserve for the remaining splits is not a guarantee then)
