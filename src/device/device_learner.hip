@@ -3078,11 +3078,12 @@ class DeviceTreeLearner : public TreeLearner {
       PlanTiles(150 * 1024);
     }
     if (num_tiles_ > 1 && row_align_ > 0) PadTrainingRows(row_align_);
-    // single-tile rows padded to whole sectors (LGAP_ROW_PAD_SINGLE=8: 28-byte rows -> 32 bytes,
-    // so a gathered row never straddles two sectors; experiment knob)
+    // single-tile rows padded to whole 32-byte sectors from 4M rows (LGAP_ROW_PAD_SINGLE=0/8/16):
+    // 28-byte rows -> 32 bytes, so a gathered row never straddles two sectors (A/B 10M 2.838 vs
+    // 2.874 ms/iter; 1.25M flat)
     if (num_tiles_ == 1) {
       const char* e = std::getenv("LGAP_ROW_PAD_SINGLE");
-      const int v = e != nullptr ? std::atoi(e) : 0;
+      const int v = e != nullptr ? std::atoi(e) : (N_ >= (4 << 20) && stride_dw_ > 4 && stride_dw_ < 8 ? 8 : 0);
       if (v == 8 || v == 16) PadTrainingRows(v);
     }
   }
