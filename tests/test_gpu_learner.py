@@ -1063,3 +1063,27 @@ def test_linear_tree_wide_branches_take_the_host_policy(lgb, gpu_required, rng):
     kw = {"objective": "regression", "linear_tree": True, "num_leaves": 48, "min_data_in_leaf": 10}
     bg = _train(lgb, X, z, "gpu", rounds=2, **kw)
     assert "host split policy" in bg.device_name()
+
+
+@pytest.mark.parametrize("extra", [{}, {"num_leaves": 63, "monotone_constraints": [1] + [0] * 79},
+                                   {"use_quantized_grad": True, "num_grad_quant_bins": 8}])
+def test_wide_data_wave_scan_matches_cpu(lgb, gpu_required, rng, extra):
+    """Wide numerical data (80 features, so the frontier scans one (expansion, feature) item per
+    wave: k_f_scan_w) grows the CPU learner's trees; the row-aligned multi-tile layout (a narrow
+    LDS budget forces several tiles) keeps the histograms exact."""
+    n, nf = 20000, 80
+    X = rng.standard_normal((n, nf))
+    X[rng.random((n, nf)) < 0.05] = np.nan
+    z = X[:, 0] - 0.7 * np.nan_to_num(X[:, 1]) + 0.4 * np.nan_to_num(X[:, 5]) * np.nan_to_num(X[:, 9])
+    y = (z + 0.3 * rng.standard_normal(n) > 0).astype(float)
+    kw = {"num_leaves": 31, "min_data_in_leaf": 20}
+    kw.update(extra)
+    bc = _train(lgb, X, y, "cpu", rounds=4, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=4, gpu_use_dp=not extra.get("use_quantized_grad", False), **kw)
+    assert "frontier engine" in bg.device_name(), bg.device_name()
+    for t in range(4):
+        sc = _splits(_trees(bc)[t]["tree_structure"], [])
+        sg = _splits(_trees(bg)[t]["tree_structure"], [])
+        assert [s[0] for s in sc] == [s[0] for s in sg], (t, sc[:6], sg[:6])
+    np.testing.assert_allclose(bg.predict(X[:2000], raw_score=True), bc.predict(X[:2000], raw_score=True),
+                               rtol=1e-4, atol=1e-4)
