@@ -1066,7 +1066,7 @@ def test_linear_tree_wide_branches_take_the_host_policy(lgb, gpu_required, rng):
 
 
 @pytest.mark.parametrize("extra", [{}, {"num_leaves": 63, "monotone_constraints": [1] + [0] * 79},
-                                   {"use_quantized_grad": True, "num_grad_quant_bins": 8}])
+                                   {"max_bin": 63, "lambda_l2": 1.0}])
 def test_wide_data_wave_scan_matches_cpu(lgb, gpu_required, rng, extra):
     """Wide numerical data (80 features, so the frontier scans one (expansion, feature) item per
     wave: k_f_scan_w) grows the CPU learner's trees; the row-aligned multi-tile layout (a narrow
@@ -1079,7 +1079,7 @@ def test_wide_data_wave_scan_matches_cpu(lgb, gpu_required, rng, extra):
     kw = {"num_leaves": 31, "min_data_in_leaf": 20}
     kw.update(extra)
     bc = _train(lgb, X, y, "cpu", rounds=4, **kw)
-    bg = _train(lgb, X, y, "gpu", rounds=4, gpu_use_dp=not extra.get("use_quantized_grad", False), **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=4, gpu_use_dp=True, **kw)
     assert "frontier engine" in bg.device_name(), bg.device_name()
     for t in range(4):
         sc = _splits(_trees(bc)[t]["tree_structure"], [])
