@@ -35,6 +35,8 @@ class Metric {
   // description (lgap/rank_metric_spec.h), and the values from the device's raw sums.
   virtual bool DeviceRankSpec(RankMetricSpec*) const { return false; }
   virtual std::vector<double> FinishRank(const std::vector<double>&) const { return {}; }
+  // Multiclass metrics over the device-resident class-major score (lgap/pointwise_metric.h)
+  virtual bool DeviceMulti(const ObjectiveFunction*, MultiMetricParams*) const { return false; }
 };
 
 class DCGCalculator {

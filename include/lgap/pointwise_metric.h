@@ -113,4 +113,43 @@ LGAP_HD inline double PmRowTerm(const PwMetricParams& p, double y, double raw, b
   return weighted ? PmLoss(p, y, s, 1.0) * w : PmLoss(p, y, s, 1.0);
 }
 
+// Multiclass metrics (reference multiclass_metric.hpp:20-180): multi_logloss / multi_error@k
+// of one row from its num_class raw scores (class-major, `stride` apart), through the
+// objective's output transform: 0 raw (custom objective), 1 softmax (the host's
+// common::Softmax order: max, exp-sum, divide), 2 one-vs-all sigmoids.
+struct MultiMetricParams {
+  int error = 0;      // 1: multi_error (top_k), 0: multi_logloss
+  int top_k = 1;
+  int output = 0;     // 0 raw, 1 softmax, 2 sigmoid per class
+  double sigmoid = 1.0;
+  int num_class = 0;
+};
+
+LGAP_HD inline double MultiProb(const MultiMetricParams& p, const double* s, size_t stride, int k, double wmax,
+                                double sum) {
+  const double x = s[static_cast<size_t>(k) * stride];
+  if (p.output == 1) return exp(x - wmax) / sum;
+  if (p.output == 2) return 1.0f / (1.0f + exp(-p.sigmoid * x));
+  return x;
+}
+
+LGAP_HD inline double MultiRowLoss(const MultiMetricParams& p, const double* s, size_t stride, int y) {
+  double wmax = 0.0, sum = 1.0;
+  if (p.output == 1) {
+    wmax = s[0];
+    for (int k = 1; k < p.num_class; ++k) wmax = fmax(wmax, s[static_cast<size_t>(k) * stride]);
+    sum = 0.0;
+    for (int k = 0; k < p.num_class; ++k) sum += exp(s[static_cast<size_t>(k) * stride] - wmax);
+  }
+  const double py = MultiProb(p, s, stride, y, wmax, sum);
+  if (p.error) {
+    int larger = 0;
+    for (int k = 0; k < p.num_class; ++k) {
+      if (MultiProb(p, s, stride, k, wmax, sum) >= py && ++larger > p.top_k) return 1.0;
+    }
+    return 0.0;
+  }
+  return py > kEpsilon ? -log(py) : -log(kEpsilon);
+}
+
 }  // namespace lgap

@@ -84,6 +84,9 @@ class TreeLearner {
   // Ranking / AUC metric of the training set (id < 0) or device validation set `id`, class k,
   // on the device score: raw sums for Metric::FinishRank (false: evaluate on the host)
   virtual bool DeviceEvalRank(int /*id*/, const RankMetricSpec&, int /*k*/, std::vector<double>* /*out*/) { return false; }
+  // multiclass metric over the class-major device score of the training set (id < 0) or a
+  // device validation set: the weighted loss sum
+  virtual bool DeviceEvalMulti(int /*id*/, const MultiMetricParams&, double* /*sum*/) { return false; }
   virtual bool SupportsDeviceSampling() const { return false; }
   virtual void DeviceSample(int plan, int iter) { (void)plan; (void)iter; }
   virtual std::string DeviceName() const { return "cpu"; }

@@ -408,6 +408,12 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
     std::vector<double> raw;
     if (learner_->DeviceEvalRank(-1, rs, 0, &raw)) return m->FinishRank(raw);
   }
+  // multiclass logloss / error: the class-major device score, only the loss sum comes back
+  MultiMetricParams mp;
+  if (allow && device_mode_ && num_tree_per_iteration_ > 1 && DeviceMetricsAllowed() && m->DeviceMulti(objective_, &mp)) {
+    double sum = 0.0;
+    if (learner_->DeviceEvalMulti(-1, mp, &sum)) return m->FinishSum(sum);
+  }
   if (*score == nullptr) {
     int64_t len;
     *score = GetTrainingScore(&len);
@@ -416,7 +422,7 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
 }
 
 // Validation metrics: pointwise, AUC / average precision and the query metrics (NDCG, MAP,
-// precision@k) on the device-resident validation score; the rest (multiclass, auc_mu) on the
+// precision@k) and multiclass logloss / error on the device-resident validation score; auc_mu on the
 // host copy, refreshed once when stale.
 std::vector<double> GBDT::EvalValid(size_t d, const Metric* m) {
   PwMetricParams p;
@@ -430,6 +436,11 @@ std::vector<double> GBDT::EvalValid(size_t d, const Metric* m) {
   if (allow && valid_dev_[d] >= 0 && num_tree_per_iteration_ == 1 && m->DeviceRankSpec(&rs)) {
     std::vector<double> raw;
     if (learner_->DeviceEvalRank(valid_dev_[d], rs, 0, &raw)) return m->FinishRank(raw);
+  }
+  MultiMetricParams mp;
+  if (allow && valid_dev_[d] >= 0 && num_tree_per_iteration_ > 1 && m->DeviceMulti(objective_, &mp)) {
+    double sum = 0.0;
+    if (learner_->DeviceEvalMulti(valid_dev_[d], mp, &sum)) return m->FinishSum(sum);
   }
   return EvalOne(m, ValidScore(d));
 }

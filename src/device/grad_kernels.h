@@ -85,6 +85,10 @@ void LaunchAddConstant(double* score, int n, double v, hipStream_t s);
 // `partial` holds max_blocks doubles
 void LaunchPointwiseMetric(const PwMetricParams& p, const double* score, const float* label, const float* weight, int n,
                            double* partial, int max_blocks, double* out, hipStream_t s);
+// sum over rows of the multiclass metric's weighted row loss (MultiRowLoss) over a class-major
+// score [num_class][n] -> *out (device)
+void LaunchMultiMetric(const MultiMetricParams& p, const double* score, const float* label, const float* weight, int n,
+                       double* partial, int max_blocks, double* out, hipStream_t s);
 
 }  // namespace device
 }  // namespace lgap

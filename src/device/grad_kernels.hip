@@ -472,6 +472,28 @@ __global__ __launch_bounds__(kMetricThreads) void k_metric_partial(PwMetricParam
   }
 }
 
+// multiclass metric rows (MultiRowLoss: the host MulticlassMetric's term), same partials / fold
+__global__ __launch_bounds__(kMetricThreads) void k_multi_metric_partial(MultiMetricParams p, const double* __restrict__ score,
+                                                                         const float* __restrict__ label,
+                                                                         const float* __restrict__ weight, int n,
+                                                                         double* __restrict__ partial) {
+  __shared__ double s_w[kMetricThreads / kWave];
+  double acc = 0.0;
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double l = MultiRowLoss(p, score + i, static_cast<size_t>(n), static_cast<int>(label[i]));
+    acc += weight != nullptr ? l * static_cast<double>(weight[i]) : l;
+  }
+  acc = WaveSum(acc);
+  if ((threadIdx.x & (kWave - 1)) == 0) s_w[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kMetricThreads / kWave; ++w) t += s_w[w];
+    partial[blockIdx.x] = t;
+  }
+}
+
 __global__ __launch_bounds__(kWave) void k_metric_fold(const double* __restrict__ partial, int nb, double* out) {
   double acc = 0.0;
   for (int i = threadIdx.x; i < nb; i += kWave) acc += partial[i];
@@ -601,6 +623,15 @@ void LaunchPointwiseMetric(const PwMetricParams& p, const double* score, const f
                            double* partial, int max_blocks, double* out, hipStream_t s) {
   const int nb = std::max(1, std::min(max_blocks, (n + kMetricThreads - 1) / kMetricThreads));
   k_metric_partial<<<nb, kMetricThreads, 0, s>>>(p, score, label, weight, n, partial);
+  HIP_CHECK(hipGetLastError());
+  k_metric_fold<<<1, kWave, 0, s>>>(partial, nb, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchMultiMetric(const MultiMetricParams& p, const double* score, const float* label, const float* weight, int n,
+                       double* partial, int max_blocks, double* out, hipStream_t s) {
+  const int nb = std::max(1, std::min(max_blocks, (n + kMetricThreads - 1) / kMetricThreads));
+  k_multi_metric_partial<<<nb, kMetricThreads, 0, s>>>(p, score, label, weight, n, partial);
   HIP_CHECK(hipGetLastError());
   k_metric_fold<<<1, kWave, 0, s>>>(partial, nb, out);
   HIP_CHECK(hipGetLastError());

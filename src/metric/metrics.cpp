@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <numeric>
 
 #include "lgap/common.h"
@@ -353,6 +354,26 @@ class MulticlassMetric : public Metric {
     }
     return {sum / sumw_};
   }
+  bool DeviceMulti(const ObjectiveFunction* obj, MultiMetricParams* out) const override {
+    MultiMetricParams p;
+    if (obj == nullptr) {
+      p.output = 0;
+    } else if (std::strcmp(obj->GetName(), "multiclass") == 0) {
+      p.output = 1;
+    } else if (std::strcmp(obj->GetName(), "multiclassova") == 0) {
+      p.output = 2;
+      p.sigmoid = obj->sigmoid();
+    } else {
+      return false;
+    }
+    if (obj != nullptr && (obj->NumModelPerIteration() != num_class_ || obj->NumPredictOneRow() != num_class_)) return false;
+    p.error = error_ ? 1 : 0;
+    p.top_k = cfg_.multi_error_top_k;
+    p.num_class = num_class_;
+    *out = p;
+    return true;
+  }
+  std::vector<double> FinishSum(double sum) const override { return {sum / sumw_}; }
 
  private:
   bool error_;

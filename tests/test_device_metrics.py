@@ -102,3 +102,33 @@ def test_device_query_metrics_match_host(lgb, gpu_required, rng, metric, query_w
     for name in ("train", "valid"):
         for m in host[name]:
             np.testing.assert_allclose(dev[name][m], host[name][m], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("objective", ["multiclass", "multiclassova"])
+@pytest.mark.parametrize("top_k", [1, 2])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_device_multiclass_metrics_match_host(lgb, gpu_required, rng, objective, top_k, weighted, monkeypatch):
+    """multi_logloss / multi_error@k on the class-major device score (k_multi_metric_partial, row
+    loss shared with the host through lgap/pointwise_metric.h MultiRowLoss; softmax and one-vs-all
+    sigmoid outputs) equal the host metric on the same scores."""
+    n, nv, k = 20000, 5000, 4
+    X, Xv = rng.standard_normal((n, 6)), rng.standard_normal((nv, 6))
+
+    def lab(X):
+        z = np.stack([X[:, 0], X[:, 1] - 0.5 * X[:, 2], 0.7 * X[:, 3], -X[:, 0]], axis=1)
+        return np.argmax(z + 0.8 * rng.standard_normal(z.shape), axis=1).astype(float)
+
+    y, yv = lab(X), lab(Xv)
+    kw = {"weight": rng.uniform(0.5, 2.0, n)} if weighted else {}
+    vkw = {"weight": rng.uniform(0.5, 2.0, nv)} if weighted else {}
+    params = {"objective": objective, "num_class": k, "metric": ["multi_logloss", "multi_error"],
+              "multi_error_top_k": top_k, "num_leaves": 7, "device_type": "gpu", "verbosity": -1, "seed": 2,
+              "deterministic": True}
+    dev = _metric_values(lgb, X, y, params, 3, valid=(Xv, yv, vkw), **kw)
+    monkeypatch.setenv("LGAP_DEVICE_METRICS", "0")
+    host = _metric_values(lgb, X, y, params, 3, valid=(Xv, yv, vkw), **kw)
+    for name in ("train", "valid"):
+        assert set(dev[name]) == set(host[name]) and len(host[name]) == 2
+        for m in host[name]:
+            np.testing.assert_allclose(dev[name][m], host[name][m], rtol=1e-12, atol=1e-12)
