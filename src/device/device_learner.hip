@@ -1066,6 +1066,38 @@ class DeviceTreeLearner : public TreeLearner {
     return true;
   }
 
+  bool DeviceEvalMulti(int id, const MultiMetricParams& p, double* sum) override {
+    const double* score = nullptr;
+    const float* label = nullptr;
+    const float* weight = nullptr;
+    int n = 0;
+    if (id < 0) {
+      n = N_;
+      if (n <= 0 || score_.size() < static_cast<size_t>(p.num_class) * N_) return false;
+      EnsureMetricLabels();
+      score = score_.get();
+      label = metric_label_.get();
+      weight = metric_weight_.size() ? metric_weight_.get() : nullptr;
+    } else {
+      if (id >= static_cast<int>(valid_.size())) return false;
+      DevValid& v = *valid_[id];
+      n = v.n;
+      if (v.label.size() == 0 || n <= 0 || v.score.size() < static_cast<size_t>(p.num_class) * n) return false;
+      score = v.score.get();
+      label = v.label.get();
+      weight = v.weight.size() ? v.weight.get() : nullptr;
+    }
+    ScopedTimer timer("Device::EvalMultiMetric");
+    if (metric_partial_.size() < static_cast<size_t>(kMetricBlocks + 1)) metric_partial_.Resize(kMetricBlocks + 1);
+    LaunchMultiMetric(p, score, label, weight, n, metric_partial_.get(), kMetricBlocks, metric_partial_.get() + kMetricBlocks,
+                      stream_);
+    double* h = pin_lout_.Get(1);
+    HIP_CHECK(hipMemcpyAsync(h, metric_partial_.get() + kMetricBlocks, sizeof(double), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    *sum = h[0];
+    return true;
+  }
+
   // Ranking / AUC metrics on the device score (metric_kernels.h): the training set (id < 0)
   // or a device validation set. The metric's per-query tables are uploaded once per metric;
   // only the metric's raw sums come back (no score download).
@@ -1812,6 +1844,10 @@ class DeviceTreeLearner : public TreeLearner {
       a.scan_grid = g != nullptr ? std::max(0, std::atoi(g)) : 512;
       const char* sr = std::getenv("LGAP_SEL_BLOCK_RANK");
       a.sel_block_rank = sr != nullptr && sr[0] == '1' ? 1 : 0;
+      const char* lr = std::getenv("LGAP_SEL_LDS_REPLAY");
+      a.sel_lds_replay = lr != nullptr && lr[0] == '1' ? 1 : 0;
+      const char* sl = std::getenv("LGAP_SEL_EARLY");
+      a.sel_early = sl != nullptr && sl[0] == '1' ? 1 : 0;
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
@@ -1838,7 +1874,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.sel_bitonic = std::getenv("LGAP_SEL_BITONIC") != nullptr ? 1 : 0;
     {
       const char* e = std::getenv("LGAP_PART_NT");
-      a.part_nt = e != nullptr && e[0] == '1' ? 1 : 0;
+      a.part_nt = e != nullptr ? std::atoi(e) : 0;
     }
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;

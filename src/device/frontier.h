@@ -222,6 +222,8 @@ struct FArgs {
   int scan_wave;     // k_f_scan_w (one wave per (expansion, feature)) instead of one block per item
   int scan_grid;     // cap of the block scan's grid (A/B knob LGAP_SCAN_GRID; 0: 4096)
   int sel_block_rank;  // the select's block-wide rank / scan for <= 64 alive nodes too (A/B knob)
+  int sel_lds_replay;  // A/B knob (LGAP_SEL_LDS_REPLAY=1): the replay's leaf keys in LDS (else registers when L <= 64)
+  int sel_early;       // A/B knob (LGAP_SEL_EARLY=1): phase A's candidate loads in the image's load round
   int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
   int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)
@@ -291,7 +293,7 @@ struct FArgs {
   unsigned* xrng;
   struct FPairBest* fpb;  // [P][kmax][2] per-child best of each rank, all-gathered
   int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
-  int part_nt;      // A/B knob (LGAP_PART_NT=1): the partition's row-index scatter with non-temporal stores
+  int part_nt;      // A/B knob (LGAP_PART_NT): the partition's row-index scatter stores, 1 non-temporal, 2 write-through (sc1)
   SplitParams sp;
 };
 

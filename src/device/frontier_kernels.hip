@@ -1104,6 +1104,19 @@ __device__ __forceinline__ void FPublish(unsigned long long* p, unsigned epoch, 
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a scattered row index: plain (written back from the XCD's L2 at the kernel boundary),
+// non-temporal (1), or write-through sc1 (2: nothing left dirty for the boundary to write back)
+__device__ __forceinline__ void FStoreRow(int mode, int* dst, int v) {
+  if (mode == 2) {
+    __hip_atomic_store((__attribute__((address_space(1))) int*)(dst), v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else if (mode == 1) {
+    __builtin_nontemporal_store(v, dst);
+  } else {
+    *dst = v;
+  }
+}
+
 __device__ __forceinline__ int FAwait(const FArgs& a, int i, unsigned epoch) {
   unsigned spins = 0;
   for (;;) {
@@ -1442,8 +1455,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
         int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
-        if (a.part_nt) __builtin_nontemporal_store(rows[j][i], dst);
-        else *dst = rows[j][i];
+        FStoreRow(a.part_nt, dst, rows[j][i]);
         if (gout != nullptr) gout[dst - out] = gv[i];
       }
       lbase += tl;
@@ -1515,8 +1527,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
         int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
-        if (a.part_nt) __builtin_nontemporal_store(rr[i], dst);
-        else *dst = rr[i];
+        FStoreRow(a.part_nt, dst, rr[i]);
         if (gout != nullptr) gout[dst - out] = gv[i];
       }
       lbase += tl;
@@ -1639,6 +1650,53 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     s_pc[t] = c;
     s_cpos[t] = -1;
   }
+  // ---- A, loads (LGAP_SEL_EARLY=1). Without CEGB the candidate keys of this round's children
+  // can be read in the image's load round: the arg-max over a pair's features does not depend
+  // on its child, whose validity (from the expansion record, loaded alongside) is applied
+  // afterwards (A/B: 10M 2.905 vs 2.843 ms/iter, 1.25M 1.317 vs 1.310 -- opt-in)
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+  static_assert(kInfoWords + kKeyWords <= 64, "one record word per lane");
+  const bool early = !cegb && !a.scan_best && a.sel_early;
+  const float spec_alpha = a.tp->spec_alpha;  // (phase D; loaded here, off its critical path)
+  double eg[kSelPairs];
+  int ef[kSelPairs], ep[kSelPairs], epc[kSelPairs];
+#pragma unroll
+  for (int j = 0; j < kSelPairs; ++j) {
+    eg[j] = kMinScore;
+    ef[j] = 0x7fffffff;
+    ep[j] = -1;
+    epc[j] = -1;
+  }
+  if (early) {
+#pragma unroll
+    for (int j = 0; j < kSelPairs; ++j) {
+      const int q = w + j * kSelWaves;
+      if (q < np) {
+        const FExp& x = a.exps[q >> 1];
+        const int ch = (q & 1) ? x.larger : x.smaller;
+        epc[j] = x.skip ? -2 - ch : ch;
+      }
+    }
+    for (int f0 = 0; f0 < F; f0 += 64) {
+      const int f = f0 + lane;
+#pragma unroll
+      for (int j = 0; j < kSelPairs; ++j) {
+        const int q = w + j * kSelWaves;
+        if (q < np && f < F) {
+          const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+          const int kf = kk.feature;
+          const double g = kf < 0 ? kMinScore : kk.gain;
+          const int ff = kf < 0 ? 0x7fffffff : kf;
+          if (FBetter(g, ff, 0, eg[j], ef[j], 0)) {
+            eg[j] = g;
+            ef[j] = ff;
+            ep[j] = f;
+          }
+        }
+      }
+    }
+  }
   __syncthreads();
   FStamp(a, rnd, kFStampSel, 1);
   if (cegb && a.cegb_lazy != nullptr) {
@@ -1661,10 +1719,53 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   // ---- A. children of the last round: best over features (all pairs' keys in flight); with
   // scan_best the scan's last item per expansion already did it (best / key written, in the
   // image above): only the winners' candidate positions are read
+  // the winners' full records (SplitInfo + SplitKey, one word per lane) are loaded now and
+  // stored at the end of the launch: only later launches read best / key of this round's
+  // children (this one reads them through s_cpos from the candidate table)
+  uint32_t cw[kSelPairs];
+  int cdst[kSelPairs];
+#pragma unroll
+  for (int j = 0; j < kSelPairs; ++j) cdst[j] = -1;
   if (a.scan_best && !cegb) {
     for (int q = t; q < np; q += blockDim.x) {
       const int pc = s_pc[q];
       if (pc >= 0) s_cpos[pc - base] = a.scan_cpos[q];
+    }
+  } else if (early) {
+#pragma unroll
+    for (int j = 0; j < kSelPairs; ++j) {
+      const int q = w + j * kSelWaves;
+      if (q >= np) continue;
+      const int pc = epc[j];
+      if (pc == -1) continue;  // no child (root round's second pair)
+      const int c = pc >= 0 ? pc : -2 - pc;
+      const int src = WaveArgBestLane(eg[j], ef[j], 0);
+      const double g = ReadLane(eg[j], src);
+      const int ff = ReadLane(ef[j], src);
+      const int fpos = ReadLane(ep[j], src);
+      const bool valid = pc >= 0 && ff != 0x7fffffff && fpos >= 0;
+      const size_t pos = static_cast<size_t>(q) * F + (fpos >= 0 ? fpos : 0);
+      if (valid) {
+        cw[j] = lane < kInfoWords ? reinterpret_cast<const uint32_t*>(a.cinfo + pos)[lane]
+                                  : reinterpret_cast<const uint32_t*>(a.ckey + pos)[lane - kInfoWords];
+        cdst[j] = c;
+      } else if (lane == 0) {
+        a.best[c].Reset();
+        SplitKey kz;
+        kz.gain = kMinScore;
+        kz.feature = -1;
+        kz.threshold = 0;
+        kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
+        kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
+        kz.pos = -1;
+        kz.pad2 = 0;
+        a.key[c] = kz;
+      }
+      if (lane == 0) {
+        s_gain[c] = valid ? g : kMinScore;
+        s_feat[c] = valid ? ff : -1;
+        s_cpos[c - base] = valid ? static_cast<int>(pos) : -1;
+      }
     }
   } else {
     double bg[kSelPairs];
@@ -1700,8 +1801,6 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         }
       }
     }
-    constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-    constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
 #pragma unroll
     for (int j = 0; j < kSelPairs; ++j) {
       const int q = w + j * kSelWaves;
@@ -1797,6 +1896,60 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     int fnext = st.forced_next, bforced = 0;
     int byn = st.byn;  // bynode masks drawn (wave-uniform)
     unsigned epoch = epoch0;  // CEGB first-use events (wave-uniform)
+    if (!cegb && fnext < 0 && L <= 64 && !a.sel_lds_replay) {
+      // leaf l's (gain, feature, cid) in lane l's registers: per committed split one wave max
+      // and two dependent LDS reads (the winner's left child, then its two children's keys)
+      int lc = lane < nl ? s_lcid[lane] : -1;
+      double lg = kMinScore;
+      int lf = 0x7fffffff;
+      if (lc >= 0) {
+        const int f = s_feat[lc];
+        lg = f < 0 ? kMinScore : s_gain[lc];
+        lf = f < 0 ? 0x7fffffff : f;
+      }
+      for (;;) {
+        if (nl >= L) {
+          done = 1;
+          break;
+        }
+        const double mg = WaveMaxDpp(lg);
+        const unsigned long long tie = __ballot(lg == mg);
+        const int src = __popcll(tie) == 1 ? __ffsll(static_cast<long long>(tie)) - 1 : WaveArgBestLane(lg, lf, lane);
+        const double bg = ReadLane(lg, src);
+        const int bf = ReadLane(lf, src);
+        if (bf == 0x7fffffff || !(bg > 0.0)) {
+          done = 1;
+          break;
+        }
+        const int c = ReadLane(lc, src);
+        const int left = s_left[c];
+        if (left < 0) {
+          blocked = c;
+          break;
+        }
+        const int fa = s_feat[left], fb = s_feat[left + 1];
+        const double ga = s_gain[left], gb = s_gain[left + 1];
+        if (lane == src) {
+          lc = left;
+          lg = fa < 0 ? kMinScore : ga;
+          lf = fa < 0 ? 0x7fffffff : fa;
+        }
+        if (lane == nl) {
+          lc = left + 1;
+          lg = fb < 0 ? kMinScore : gb;
+          lf = fb < 0 ? 0x7fffffff : fb;
+        }
+        if (lane == 0) {
+          s_c0[nc] = src;
+          s_c1[nc] = c;
+          s_st[c] |= kNodeCommitted;
+        }
+        ++nc;
+        ++nl;
+        ++ns;
+      }
+      if (lane < nl) s_lcid[lane] = lc;
+    } else
     for (;;) {
       if (nl >= L) {
         done = 1;
@@ -2131,9 +2284,9 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
           gi = s_gain[ci];
         }
         int pos = 0;
-        for (int j = 0; j < na; ++j) {
-          const double gj = __shfl(gi, j, kWave);
-          const int cj = __shfl(ci, j, kWave);
+        for (int j = 0; j < na; ++j) {  // (uniform j: scalar lane reads, no LDS permutes)
+          const double gj = ReadLane(gi, j);
+          const int cj = ReadLane(ci, j);
           pos += (gj > gi || (gj == gi && cj < ci)) ? 1 : 0;
         }
         if (lane < na) s_sc[pos] = r;
@@ -2145,7 +2298,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
         const int ex = __popcll(__ballot(fl) & lt);
         const int cap_nodes = (C - cid_next) / 2 - (R - 1);
-        const float alpha = a.tp->spec_alpha > 0.f ? a.tp->spec_alpha : 1.f;
+        const float alpha = spec_alpha > 0.f ? spec_alpha : 1.f;
         const int budget = static_cast<int>(alpha * static_cast<float>(R)) + a.spec_cap;
         int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
                                 : min(a.kmax, max(1, cap_nodes));
@@ -2242,7 +2395,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     const int cap_nodes = (C - cid_next) / 2 - (R - 1);
     // policy 1 budget: the best `alpha` fraction of the remaining splits (alpha tuned per tree by
     // the host from the rows the previous trees' uncommitted expansions cost)
-    const float alpha = a.tp->spec_alpha > 0.f ? a.tp->spec_alpha : 1.f;
+    const float alpha = spec_alpha > 0.f ? spec_alpha : 1.f;
     const int budget = static_cast<int>(alpha * static_cast<float>(R)) + a.spec_cap;
     int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
                             : min(a.kmax, max(1, cap_nodes));
@@ -2350,6 +2503,13 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
     *a.st = ns_;
     if (a.part_ticket != nullptr) *a.part_ticket = 0u;  // (the next round's partition tickets)
+  }
+#pragma unroll
+  for (int j = 0; j < kSelPairs; ++j) {
+    const int c = cdst[j];
+    if (c < 0) continue;
+    if (lane < kInfoWords) reinterpret_cast<uint32_t*>(a.best + c)[lane] = cw[j];
+    else reinterpret_cast<uint32_t*>(a.key + c)[lane - kInfoWords] = cw[j];
   }
   FStamp(a, rnd, kFStampSel, 6);
   FStampEnd(a, rnd, kFStampSel);
