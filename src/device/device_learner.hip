@@ -1721,7 +1721,7 @@ class DeviceTreeLearner : public TreeLearner {
     fspec_alpha_ = 1.0;
     fspec_fixed_ = false;
     if (const char* e = std::getenv("LGAP_FRONTIER_ALPHA")) {  // fixed speculation depth (A/B)
-      fspec_alpha_ = std::max(0.01, std::min(1.0, std::atof(e)));
+      fspec_alpha_ = std::max(0.01, std::min(4.0, std::atof(e)));
       fspec_fixed_ = true;
     }
     if (std::getenv("LGAP_FSTAMPS")) {
@@ -2416,7 +2416,9 @@ class DeviceTreeLearner : public TreeLearner {
   // the frontier histogram's dynamic LDS: the tile plan's, plus the 32-bit bins of hist MODE 3
   size_t FrontierHistLds() const {
     const FArgs fa = MakeFArgs();
-    const size_t b = use_dp_ || !QuantHist() || fa.qsub == 0 ? hist_lds_bytes_ : hist_lds_bytes_ * 3 / 2 + 64;
+    // (the interleaved slots' reserve only where k_f_hist can use them: fixed-point and MODE 2)
+    const size_t plan = use_dp_ || fa.qsub > 0 ? hist_lds_plain_ : hist_lds_bytes_;
+    const size_t b = use_dp_ || !QuantHist() || fa.qsub == 0 ? plan : plan * 3 / 2 + 64;
     return fa.hist_copies > 1 ? b + HistCopyBytes() : b;
   }
 
@@ -3155,6 +3157,7 @@ class DeviceTreeLearner : public TreeLearner {
     const int max_dw = kHistThreads / 2;
     std::vector<HistTile> tiles;
     hist_lds_bytes_ = 16;
+    hist_lds_plain_ = 16;
     int d = 0;
     const int nd = DivUp(G_, per);
     while (d < nd) {
@@ -3199,11 +3202,10 @@ class DeviceTreeLearner : public TreeLearner {
         }
       }
       tiles.push_back(t);
-      if (!t.direct) {
-        hist_lds_bytes_ = std::max(hist_lds_bytes_, static_cast<size_t>(bins) * acc + sizeof(int) * (t.g1 - t.g0) + 16);
-      } else {
-        hist_lds_bytes_ = std::max(hist_lds_bytes_, sizeof(int) * (t.g1 - t.g0) + 16);
-      }
+      const size_t plain = t.direct ? sizeof(int) * (t.g1 - t.g0) + 16
+                                    : static_cast<size_t>(bins) * acc + sizeof(int) * (t.g1 - t.g0) + 16;
+      hist_lds_bytes_ = std::max(hist_lds_bytes_, plain);
+      hist_lds_plain_ = std::max(hist_lds_plain_, plain);
       d = e;
     }
     if (hist_lds_bytes_ > 64 * 1024) {
@@ -3798,6 +3800,7 @@ class DeviceTreeLearner : public TreeLearner {
   int bynode_draws_ = 0;  // by-node masks the last tree used (the host sampler's GetByNode calls)
   data_size_t bag_cnt_ = 0;
   size_t hist_lds_bytes_ = 0, scan_lds_bytes_ = 0;
+  size_t hist_lds_plain_ = 0;  // the tile plan's LDS without the interleaved slots' reserve
   int max_bin_ = 2, cat_p2_ = 1;
   bool scan_global_ = false;
   size_t scan_scratch_stride_ = 0;

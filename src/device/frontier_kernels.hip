@@ -1586,6 +1586,7 @@ __device__ __forceinline__ void CegbSetBest(const FArgs& a, int c, size_t src, d
 constexpr int kSelWaves = kFSelThreads / 64;
 constexpr int kSelPairs = 2 * kFrontierKmax / kSelWaves;  // (expansion, child) pairs per wave
 constexpr int kSelRankMax = 256;  // alive nodes up to which the select ranks instead of sorting
+constexpr int kSelLPer = 4;       // leaves per lane of the register replay (L <= 256)
 
 template <bool kCegb>
 __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
@@ -1896,32 +1897,56 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     int fnext = st.forced_next, bforced = 0;
     int byn = st.byn;  // bynode masks drawn (wave-uniform)
     unsigned epoch = epoch0;  // CEGB first-use events (wave-uniform)
-    if (!cegb && fnext < 0 && L <= 64 && !a.sel_lds_replay) {
-      // leaf l's (gain, feature, cid) in lane l's registers: per committed split one wave max
-      // and two dependent LDS reads (the winner's left child, then its two children's keys)
-      int lc = lane < nl ? s_lcid[lane] : -1;
-      double lg = kMinScore;
-      int lf = 0x7fffffff;
-      if (lc >= 0) {
-        const int f = s_feat[lc];
-        lg = f < 0 ? kMinScore : s_gain[lc];
-        lf = f < 0 ? 0x7fffffff : f;
+    if (!cegb && fnext < 0 && L <= 64 * kSelLPer && !a.sel_lds_replay) {
+      // leaf l's (gain, feature, cid) in registers of lane l % 64, slot l / 64: per committed
+      // split one wave max and two dependent LDS reads (the winner's left child, then its two
+      // children's keys)
+      const int nslot = (L + 63) >> 6;
+      int lc[kSelLPer];
+      double lg[kSelLPer];
+      int lf[kSelLPer];
+#pragma unroll
+      for (int j = 0; j < kSelLPer; ++j) {
+        const int l = lane + 64 * j;
+        lc[j] = j < nslot && l < nl ? s_lcid[l] : -1;
+        lg[j] = kMinScore;
+        lf[j] = 0x7fffffff;
+        if (lc[j] >= 0) {
+          const int f = s_feat[lc[j]];
+          lg[j] = f < 0 ? kMinScore : s_gain[lc[j]];
+          lf[j] = f < 0 ? 0x7fffffff : f;
+        }
       }
       for (;;) {
         if (nl >= L) {
           done = 1;
           break;
         }
-        const double mg = WaveMaxDpp(lg);
-        const unsigned long long tie = __ballot(lg == mg);
-        const int src = __popcll(tie) == 1 ? __ffsll(static_cast<long long>(tie)) - 1 : WaveArgBestLane(lg, lf, lane);
-        const double bg = ReadLane(lg, src);
-        const int bf = ReadLane(lf, src);
+        // the lane's best slot (slots in leaf order: FBetter's leaf tie-break holds)
+        double pg = lg[0];
+        int pf = lf[0], pl = lane;
+#pragma unroll
+        for (int j = 1; j < kSelLPer; ++j) {
+          if (j < nslot && FBetter(lg[j], lf[j], lane + 64 * j, pg, pf, pl)) {
+            pg = lg[j];
+            pf = lf[j];
+            pl = lane + 64 * j;
+          }
+        }
+        const double mg = WaveMaxDpp(pg);
+        const unsigned long long tie = __ballot(pg == mg);
+        const int src = __popcll(tie) == 1 ? __ffsll(static_cast<long long>(tie)) - 1 : WaveArgBestLane(pg, pf, pl);
+        const double bg = ReadLane(pg, src);
+        const int bf = ReadLane(pf, src);
+        const int bl = ReadLane(pl, src);
         if (bf == 0x7fffffff || !(bg > 0.0)) {
           done = 1;
           break;
         }
-        const int c = ReadLane(lc, src);
+        int cl = -1;
+#pragma unroll
+        for (int j = 0; j < kSelLPer; ++j) cl = (bl >> 6) == j ? lc[j] : cl;
+        const int c = ReadLane(cl, src);
         const int left = s_left[c];
         if (left < 0) {
           blocked = c;
@@ -1929,18 +1954,21 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         }
         const int fa = s_feat[left], fb = s_feat[left + 1];
         const double ga = s_gain[left], gb = s_gain[left + 1];
-        if (lane == src) {
-          lc = left;
-          lg = fa < 0 ? kMinScore : ga;
-          lf = fa < 0 ? 0x7fffffff : fa;
-        }
-        if (lane == nl) {
-          lc = left + 1;
-          lg = fb < 0 ? kMinScore : gb;
-          lf = fb < 0 ? 0x7fffffff : fb;
+#pragma unroll
+        for (int j = 0; j < kSelLPer; ++j) {
+          if (lane + 64 * j == bl) {
+            lc[j] = left;
+            lg[j] = fa < 0 ? kMinScore : ga;
+            lf[j] = fa < 0 ? 0x7fffffff : fa;
+          }
+          if (lane + 64 * j == nl) {
+            lc[j] = left + 1;
+            lg[j] = fb < 0 ? kMinScore : gb;
+            lf[j] = fb < 0 ? 0x7fffffff : fb;
+          }
         }
         if (lane == 0) {
-          s_c0[nc] = src;
+          s_c0[nc] = bl;
           s_c1[nc] = c;
           s_st[c] |= kNodeCommitted;
         }
@@ -1948,7 +1976,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         ++nl;
         ++ns;
       }
-      if (lane < nl) s_lcid[lane] = lc;
+#pragma unroll
+      for (int j = 0; j < kSelLPer; ++j) {
+        if (lane + 64 * j < nl) s_lcid[lane + 64 * j] = lc[j];
+      }
     } else
     for (;;) {
       if (nl >= L) {

@@ -1103,3 +1103,25 @@ def _splits_in_order(node, out=None):
         _splits_in_order(node["left_child"], out)
         _splits_in_order(node["right_child"], out)
     return sorted(out)
+
+
+@pytest.mark.parametrize("quantized", [False, True])
+def test_interleaved_root_histogram_rows_4m(lgb, gpu_required, quantized, monkeypatch):
+    """From 4M rows the single-tile plan reserves LDS for the interleaved root histogram
+    (k_f_hist il); fixed-point and quantized (MODE 3 sub-chunk folding) training launch within
+    the LDS budget and grow the same trees as with the interleave off (integer sums)."""
+    rng = np.random.default_rng(17)
+    n = 4_200_000
+    X = rng.standard_normal((n, 10)).astype(np.float32)
+    y = (X[:, 0] - 0.6 * X[:, 1] + 0.3 * rng.standard_normal(n) > 0).astype(np.float32)
+    params = {"objective": "binary", "num_leaves": 31, "device_type": "gpu", "verbosity": -1, "seed": 3,
+              "deterministic": True, "use_quantized_grad": quantized, "num_grad_quant_bins": 4}
+
+    def model():
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 3, keep_training_booster=True)
+        assert "frontier engine" in b.device_name()
+        return b.model_to_string()
+
+    with_il = model()
+    monkeypatch.setenv("LGAP_HIST_IL", "0")
+    assert model() == with_il
