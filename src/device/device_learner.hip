@@ -74,6 +74,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1358,9 +1359,11 @@ class DeviceTreeLearner : public TreeLearner {
       gcount = cached_gcount_;
     }
     tp->root_gcount = gcount;
-    tp->spec_alpha = static_cast<float>(fspec_alpha_);
+    const bool tune = frontier_ && stune_.on;
+    tp->spec_alpha = static_cast<float>(tune ? stune_.Alpha() : fspec_alpha_);
     tp->pad[0] = tp->pad[1] = tp->pad[2] = 0;
     HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
+    const auto t_tree0 = std::chrono::steady_clock::now();
     if (config_->use_quantized_grad) QuantizeGradients(class_id);
     col_sampler_.ResetByTree();
     const auto& used = col_sampler_.is_feature_used_bytree();
@@ -1387,6 +1390,7 @@ class DeviceTreeLearner : public TreeLearner {
     bynode_draws_ = 0;
     if (frontier_) {
       FrontierGrow(&num_splits, &num_leaves, hr, hrange, hlo);
+      if (tune) stune_.Record(std::chrono::duration<double>(std::chrono::steady_clock::now() - t_tree0).count());
     } else {
       SequentialGrow(&num_splits, &num_leaves, hr, hrange, hlo);
     }
@@ -1728,6 +1732,13 @@ class DeviceTreeLearner : public TreeLearner {
     if (const char* e = std::getenv("LGAP_FRONTIER_ALPHA")) {  // fixed speculation depth (A/B)
       fspec_alpha_ = std::max(0.01, std::min(4.0, std::atof(e)));
       fspec_fixed_ = true;
+    }
+    // timed speculation tuner: one process, >= 128 leaves, no fixed alpha / throttle requested
+    {
+      const char* tn = std::getenv("LGAP_FRONTIER_TUNE");
+      stune_ = SpecTuner();
+      stune_.on = !distributed_ && L_ >= 128 && std::getenv("LGAP_FRONTIER_ALPHA") == nullptr &&
+                  std::getenv("LGAP_FRONTIER_ADAPT") == nullptr && !(tn != nullptr && tn[0] == '0');
     }
     if (std::getenv("LGAP_FSTAMPS")) {
       fstamps_.Resize(256 * 4 * kFStampSlots);
@@ -2211,7 +2222,7 @@ class DeviceTreeLearner : public TreeLearner {
       std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max), wasted rows %.1f%%, "
                    "alpha %.3f, all-reduced expansion slots/tree %.1f, pipelined rounds/tree %.2f\n", fstat_trees_,
                    static_cast<double>(fstat_rounds_) / fstat_trees_, static_cast<double>(fstat_spec_) / fstat_trees_, L_,
-                   100.0 * fstat_waste_ / fstat_trees_, fspec_alpha_, fstat_ar_exps_ / fstat_trees_,
+                   100.0 * fstat_waste_ / fstat_trees_, stune_.on ? stune_.lo : fspec_alpha_, fstat_ar_exps_ / fstat_trees_,
                    static_cast<double>(fstat_pipelined_) / fstat_trees_);
     }
   }
@@ -3790,6 +3801,41 @@ class DeviceTreeLearner : public TreeLearner {
   long long fstat_rounds_ = 0, fstat_spec_ = 0;
   double fstat_waste_ = 0.0, fspec_alpha_ = 1.0;
   bool fspec_fixed_ = false;
+  // Speculation budget tuned on measured tree times (trees share the exact split sequence
+  // whatever the budget, so only the time changes): pairs of consecutive trees at alpha and
+  // 1.5 alpha, six pairs per decision; a budget that is >= 2% faster on average becomes the
+  // base, a >= 2% slower one sends the base down (floor 1), otherwise the base rests 48 trees
+  struct SpecTuner {
+    bool on = false;
+    double lo = 1.0, t_lo = 0.0, dsum = 0.0;
+    int phase = 0, pairs = 0, rest = 0;
+    double Alpha() const { return rest > 0 || phase == 0 ? lo : std::min(4.0, lo * 1.5); }
+    void Record(double dt) {
+      if (rest > 0) {
+        --rest;
+        return;
+      }
+      if (phase == 0) {
+        t_lo = dt;
+        phase = 1;
+        return;
+      }
+      phase = 0;
+      dsum += t_lo > 0.0 ? (dt - t_lo) / t_lo : 0.0;
+      if (++pairs < 6) return;
+      const double m = dsum / pairs;
+      pairs = 0;
+      dsum = 0.0;
+      if (m < -0.02 && lo < 4.0) {
+        lo = std::min(4.0, lo * 1.5);
+      } else if (m > 0.02 && lo > 1.0) {
+        lo = std::max(1.0, lo / 1.5);
+      } else {
+        rest = 48;
+      }
+    }
+  };
+  SpecTuner stune_;
   int fstat_trees_ = 0;
   DevBuf<unsigned long long> fstamps_;
   const float2* fgraph_gh_ = nullptr;
