@@ -37,6 +37,9 @@ class Metric {
   virtual std::vector<double> FinishRank(const std::vector<double>&) const { return {}; }
   // Multiclass metrics over the device-resident class-major score (lgap/pointwise_metric.h)
   virtual bool DeviceMulti(const ObjectiveFunction*, MultiMetricParams*) const { return false; }
+  // auc_mu: the per-pair accumulators the device computes (lgap/rank_metric_spec.h) -> value
+  virtual bool DeviceAucMu(AucMuSpec*) const { return false; }
+  virtual std::vector<double> FinishAucMu(const std::vector<double>&) const { return {}; }
 };
 
 class DCGCalculator {

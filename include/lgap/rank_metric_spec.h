@@ -31,4 +31,20 @@ struct RankMetricSpec {
   static constexpr int kMaxEvalAt = 32;
 };
 
+// auc_mu (reference multiclass_metric.hpp AucMuMetric): for every class pair (i < j) the rows
+// of classes i and j, scored by t1 * sum_m v_m score_m (v = cw[i] - cw[j], t1 = v_i - v_j),
+// give S_ij = sum over i-rows of w * (j-weight scored below + half the tied j-weight): a
+// binary AUC accumulator with class i positive. The device returns S_ij per pair.
+struct AucMuSpec {
+  const void* owner = nullptr;
+  data_size_t num_data = 0;
+  const label_t* label = nullptr;
+  const label_t* weights = nullptr;
+  int num_class = 0;
+  const std::vector<data_size_t>* sorted = nullptr;  // rows ordered by class (stable)
+  const std::vector<int>* sizes = nullptr;           // rows per class
+  const std::vector<std::vector<double>>* cw = nullptr;
+  static constexpr int kMaxClass = 64;
+};
+
 }  // namespace lgap

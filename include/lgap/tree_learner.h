@@ -87,6 +87,8 @@ class TreeLearner {
   // multiclass metric over the class-major device score of the training set (id < 0) or a
   // device validation set: the weighted loss sum
   virtual bool DeviceEvalMulti(int /*id*/, const MultiMetricParams&, double* /*sum*/) { return false; }
+  // auc_mu per-pair accumulators S_ij (pairs i < j in row-major order) on the device score
+  virtual bool DeviceEvalAucMu(int /*id*/, const AucMuSpec&, std::vector<double>* /*out*/) { return false; }
   virtual bool SupportsDeviceSampling() const { return false; }
   virtual void DeviceSample(int plan, int iter) { (void)plan; (void)iter; }
   virtual std::string DeviceName() const { return "cpu"; }

@@ -414,6 +414,11 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
     double sum = 0.0;
     if (learner_->DeviceEvalMulti(-1, mp, &sum)) return m->FinishSum(sum);
   }
+  AucMuSpec am;
+  if (allow && device_mode_ && num_tree_per_iteration_ > 1 && DeviceMetricsAllowed() && m->DeviceAucMu(&am)) {
+    std::vector<double> s;
+    if (learner_->DeviceEvalAucMu(-1, am, &s)) return m->FinishAucMu(s);
+  }
   if (*score == nullptr) {
     int64_t len;
     *score = GetTrainingScore(&len);
@@ -422,7 +427,7 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
 }
 
 // Validation metrics: pointwise, AUC / average precision and the query metrics (NDCG, MAP,
-// precision@k) and multiclass logloss / error on the device-resident validation score; auc_mu on the
+// precision@k), multiclass logloss / error and auc_mu on the device-resident validation score; the rest on the
 // host copy, refreshed once when stale.
 std::vector<double> GBDT::EvalValid(size_t d, const Metric* m) {
   PwMetricParams p;
@@ -441,6 +446,11 @@ std::vector<double> GBDT::EvalValid(size_t d, const Metric* m) {
   if (allow && valid_dev_[d] >= 0 && num_tree_per_iteration_ > 1 && m->DeviceMulti(objective_, &mp)) {
     double sum = 0.0;
     if (learner_->DeviceEvalMulti(valid_dev_[d], mp, &sum)) return m->FinishSum(sum);
+  }
+  AucMuSpec am;
+  if (allow && valid_dev_[d] >= 0 && num_tree_per_iteration_ > 1 && m->DeviceAucMu(&am)) {
+    std::vector<double> s;
+    if (learner_->DeviceEvalAucMu(valid_dev_[d], am, &s)) return m->FinishAucMu(s);
   }
   return EvalOne(m, ValidScore(d));
 }

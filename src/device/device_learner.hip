@@ -1099,6 +1099,86 @@ class DeviceTreeLearner : public TreeLearner {
     return true;
   }
 
+  bool DeviceEvalAucMu(int id, const AucMuSpec& spec, std::vector<double>* out) override {
+    const int K = spec.num_class;
+    if (K < 2 || K > kAucMuMaxClass || spec.sorted == nullptr || spec.sizes == nullptr || spec.cw == nullptr) return false;
+    const double* score = nullptr;
+    const float* weight = nullptr;
+    const void* host_label = nullptr;
+    int n = 0;
+    if (id < 0) {
+      n = N_;
+      if (n <= 0 || score_.size() < static_cast<size_t>(K) * N_) return false;
+      EnsureMetricLabels();
+      score = score_.get();
+      weight = metric_weight_.size() ? metric_weight_.get() : nullptr;
+      host_label = data_->metadata().label();
+    } else {
+      if (id >= static_cast<int>(valid_.size())) return false;
+      DevValid& v = *valid_[id];
+      n = v.n;
+      if (v.label.size() == 0 || n <= 0 || v.score.size() < static_cast<size_t>(K) * n) return false;
+      score = v.score.get();
+      weight = v.weight.size() ? v.weight.get() : nullptr;
+      host_label = v.host_label;
+    }
+    if (spec.num_data != n || spec.label != host_label || (spec.weights != nullptr) != (weight != nullptr)) return false;
+    if (static_cast<int>(spec.sorted->size()) != n || static_cast<int>(spec.sizes->size()) != K) return false;
+    ScopedTimer timer("Device::EvalAucMu");
+    auto& slot = aucmu_states_[spec.owner];
+    const int npairs = K * (K - 1) / 2;
+    int maxpair = 0;
+    for (int i = 0; i < K; ++i)
+      for (int j = i + 1; j < K; ++j) maxpair = std::max(maxpair, (*spec.sizes)[i] + (*spec.sizes)[j]);
+    if (!slot || slot->n != n || slot->host_label != host_label) {
+      slot = std::make_unique<AucMuState>();
+      slot->n = n;
+      slot->host_label = host_label;
+      std::vector<int> idx(spec.sorted->begin(), spec.sorted->end());
+      slot->idx.Upload(idx, stream_);
+      HIP_CHECK(hipStreamSynchronize(stream_));  // (idx is a local staging vector)
+      slot->dist.Resize(std::max(maxpair, 1));
+      slot->lab.Resize(std::max(maxpair, 1));
+      slot->w.Resize(std::max(maxpair, 1));
+      slot->scratch.Resize(AucScratchBytes(std::max(maxpair, 1)));
+      slot->out.Resize(2 * static_cast<size_t>(npairs));
+    }
+    AucMuState& st = *slot;
+    AucMuPairArgs pa;
+    pa.score = score;
+    pa.n = n;
+    pa.K = K;
+    pa.idx = st.idx.get();
+    pa.weight = weight;
+    pa.out_score = st.dist.get();
+    pa.out_label = st.lab.get();
+    pa.out_w = st.w.get();
+    const auto& cw = *spec.cw;
+    int istart = 0, q = 0;
+    for (int i = 0; i < K; ++i) {
+      int jstart = istart + (*spec.sizes)[i];
+      for (int j = i + 1; j < K; ++j, ++q) {
+        for (int c = 0; c < K; ++c) pa.v[c] = cw[i][c] - cw[j][c];
+        pa.t1 = pa.v[i] - pa.v[j];
+        pa.istart = istart;
+        pa.ni = (*spec.sizes)[i];
+        pa.jstart = jstart;
+        pa.nj = (*spec.sizes)[j];
+        LaunchAucMuPair(pa, stream_);
+        LaunchAucMetric(false, st.dist.get(), st.lab.get(), weight != nullptr ? st.w.get() : nullptr, pa.ni + pa.nj,
+                        st.scratch.get(), st.scratch.size(), st.out.get() + 2 * q, stream_);
+        jstart += (*spec.sizes)[j];
+      }
+      istart += (*spec.sizes)[i];
+    }
+    std::vector<double> h(2 * static_cast<size_t>(npairs));
+    st.out.Download(h.data(), h.size(), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    out->assign(npairs, 0.0);
+    for (int p = 0; p < npairs; ++p) (*out)[p] = h[2 * p];
+    return true;
+  }
+
   // Ranking / AUC metrics on the device score (metric_kernels.h): the training set (id < 0)
   // or a device validation set. The metric's per-query tables are uploaded once per metric;
   // only the metric's raw sums come back (no score download).
@@ -3967,6 +4047,16 @@ class DeviceTreeLearner : public TreeLearner {
     DevBuf<char> scratch;
   };
   std::map<const void*, std::unique_ptr<RankEvalState>> rank_states_;
+  // auc_mu tables per metric: the class-ordered row index, one pair's scored rows, the pairs' sums
+  struct AucMuState {
+    int n = 0;
+    const void* host_label = nullptr;
+    DevBuf<int> idx;
+    DevBuf<double> dist, out;
+    DevBuf<float> lab, w;
+    DevBuf<char> scratch;
+  };
+  std::map<const void*, std::unique_ptr<AucMuState>> aucmu_states_;
   PinnedBuf<double> pin_metric_;
   std::vector<std::unique_ptr<DevValid>> valid_;
   // refit / leaf renewal

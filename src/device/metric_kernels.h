@@ -23,6 +23,24 @@ size_t AucScratchBytes(int n);
 void LaunchAucMetric(bool average_precision, const double* score, const float* label, const float* weight, int n,
                      void* scratch, size_t scratch_bytes, double* out, hipStream_t s);
 
+// auc_mu: one class pair's rows (classes i and j, from the class-ordered row index) scored by
+// t1 * sum_m v_m score[m][row] in the host's order and without contraction; labels 1 for class
+// i rows (the AUC's positives), 0 for class j rows.
+constexpr int kAucMuMaxClass = 64;
+struct AucMuPairArgs {
+  const double* score;  // [K][n] class-major
+  int n, K;
+  const int* idx;       // rows ordered by class
+  int istart, ni, jstart, nj;
+  double t1;
+  double v[kAucMuMaxClass];
+  const float* weight;  // nullptr: 1
+  double* out_score;
+  float* out_label;
+  float* out_w;
+};
+void LaunchAucMuPair(const AucMuPairArgs& a, hipStream_t s);
+
 struct QueryMetricArgs {
   int kind;               // RankMetricSpec::Kind (kNDCG, kMAP, kPrecision)
   const int* qb;          // [nq + 1] query boundaries

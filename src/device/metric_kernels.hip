@@ -254,6 +254,25 @@ void LaunchAucMetric(bool average_precision, const double* score, const float* l
   HIP_CHECK(hipGetLastError());
 }
 
+__global__ __launch_bounds__(kMThreads) void k_aucmu_pair(AucMuPairArgs a) {
+  const int m = a.ni + a.nj;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += gridDim.x * blockDim.x) {
+    const int row = q < a.ni ? a.idx[a.istart + q] : a.idx[a.jstart + q - a.ni];
+    double va = 0.0;
+    for (int c = 0; c < a.K; ++c) va = __dadd_rn(va, __dmul_rn(a.v[c], a.score[static_cast<size_t>(c) * a.n + row]));
+    a.out_score[q] = __dmul_rn(a.t1, va);
+    a.out_label[q] = q < a.ni ? 1.f : 0.f;
+    a.out_w[q] = a.weight != nullptr ? a.weight[row] : 1.f;
+  }
+}
+
+void LaunchAucMuPair(const AucMuPairArgs& a, hipStream_t s) {
+  const int m = a.ni + a.nj;
+  if (m <= 0) return;
+  k_aucmu_pair<<<StreamGrid(m), kMThreads, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
 size_t QueryMetricScratchBytes(int n, int nq, int ne) {
   const size_t m = static_cast<size_t>(std::max(n, 1));
   size_t tmp = 0;

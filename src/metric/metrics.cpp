@@ -449,10 +449,29 @@ class AucMuMetric : public Metric {
       }
       istart += sizes_[i];
     }
-    double ans = 0;
+    std::vector<double> flat;
     for (int i = 0; i < num_class_; ++i)
-      for (int j = i + 1; j < num_class_; ++j)
-        ans += w_ ? (S[i][j] / cls_w_[i]) / cls_w_[j] : (S[i][j] / sizes_[i]) / sizes_[j];
+      for (int j = i + 1; j < num_class_; ++j) flat.push_back(S[i][j]);
+    return FinishAucMu(flat);
+  }
+  bool DeviceAucMu(AucMuSpec* out) const override {
+    if (num_class_ < 2 || num_class_ > AucMuSpec::kMaxClass) return false;
+    out->owner = this;
+    out->num_data = n_;
+    out->label = label_;
+    out->weights = w_;
+    out->num_class = num_class_;
+    out->sorted = &sorted_;
+    out->sizes = &sizes_;
+    out->cw = &cw_;
+    return true;
+  }
+  std::vector<double> FinishAucMu(const std::vector<double>& S) const override {
+    double ans = 0;
+    size_t q = 0;
+    for (int i = 0; i < num_class_; ++i)
+      for (int j = i + 1; j < num_class_; ++j, ++q)
+        ans += w_ ? (S[q] / cls_w_[i]) / cls_w_[j] : (S[q] / sizes_[i]) / sizes_[j];
     ans = (2.0 * ans / num_class_) / (num_class_ - 1);
     return {ans};
   }

@@ -132,3 +132,32 @@ def test_device_multiclass_metrics_match_host(lgb, gpu_required, rng, objective,
         assert set(dev[name]) == set(host[name]) and len(host[name]) == 2
         for m in host[name]:
             np.testing.assert_allclose(dev[name][m], host[name][m], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("custom_weights", [False, True])
+def test_device_auc_mu_matches_host(lgb, gpu_required, rng, weighted, custom_weights, monkeypatch):
+    """auc_mu on the device (per class pair: rows of the two classes scored by the weight-vector
+    projection, then the binary AUC kernels) equals the host metric on the same scores."""
+    n, nv, k = 15000, 4000, 5
+    X, Xv = rng.standard_normal((n, 6)), rng.standard_normal((nv, 6))
+
+    def lab(X):
+        z = np.stack([X[:, 0], X[:, 1] - 0.5 * X[:, 2], 0.7 * X[:, 3], -X[:, 0], X[:, 4] * X[:, 5]], axis=1)
+        return np.argmax(z + 0.8 * rng.standard_normal(z.shape), axis=1).astype(float)
+
+    y, yv = lab(X), lab(Xv)
+    kw = {"weight": rng.uniform(0.5, 2.0, n)} if weighted else {}
+    vkw = {"weight": rng.uniform(0.5, 2.0, nv)} if weighted else {}
+    params = {"objective": "multiclass", "num_class": k, "metric": ["auc_mu"], "num_leaves": 7,
+              "device_type": "gpu", "verbosity": -1, "seed": 2, "deterministic": True}
+    if custom_weights:
+        w = rng.uniform(0.5, 1.5, (k, k))
+        np.fill_diagonal(w, 0.0)
+        params["auc_mu_weights"] = [float(x) for x in w.ravel()]
+    dev = _metric_values(lgb, X, y, params, 3, valid=(Xv, yv, vkw), **kw)
+    monkeypatch.setenv("LGAP_DEVICE_METRICS", "0")
+    host = _metric_values(lgb, X, y, params, 3, valid=(Xv, yv, vkw), **kw)
+    for name in ("train", "valid"):
+        np.testing.assert_allclose(dev[name]["auc_mu"], host[name]["auc_mu"], rtol=1e-12, atol=1e-12)
