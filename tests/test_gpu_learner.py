@@ -1125,3 +1125,29 @@ def test_interleaved_root_histogram_rows_4m(lgb, gpu_required, quantized, monkey
     with_il = model()
     monkeypatch.setenv("LGAP_HIST_IL", "0")
     assert model() == with_il
+
+
+def test_speculation_budget_does_not_change_trees(lgb, gpu_required, monkeypatch):
+    """The frontier's speculation budget (fixed alpha, the timed tuner, the waste throttle) only
+    decides which nodes are expanded ahead of the replay: the committed split sequence, and so
+    the model, is the same under every budget."""
+    rng = np.random.default_rng(23)
+    n = 60000
+    X = rng.standard_normal((n, 12))
+    y = X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.3 * rng.standard_normal(n)
+    params = {"objective": "regression", "num_leaves": 255, "min_data_in_leaf": 5, "device_type": "gpu",
+              "verbosity": -1, "seed": 4, "deterministic": True}
+
+    def model(**env):
+        for k in ("LGAP_FRONTIER_ALPHA", "LGAP_FRONTIER_TUNE", "LGAP_FRONTIER_ADAPT"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 30, keep_training_booster=True)
+        assert "frontier engine" in b.device_name()
+        return b.model_to_string()
+
+    base = model(LGAP_FRONTIER_TUNE="0")
+    assert model() == base  # timed tuner (>= 128 leaves, one process)
+    assert model(LGAP_FRONTIER_ALPHA="3") == base
+    assert model(LGAP_FRONTIER_ADAPT="1") == base
