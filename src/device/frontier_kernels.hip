@@ -1884,20 +1884,24 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   double* s_sg = reinterpret_cast<double*>(smem + ((reinterpret_cast<uintptr_t>(s_lf + L) -
                                                     reinterpret_cast<uintptr_t>(smem) + 15) & ~uintptr_t(15)));  // [P2max]
   int* s_sc = reinterpret_cast<int*>(s_sg + FrontierSortCap(C));      // [P2max]
-  for (int l = t; l < st.num_leaves; l += blockDim.x) {
-    const int c = s_lcid[l];
-    const int f = s_feat[c];
-    s_lg[l] = f < 0 ? kMinScore : s_gain[c];
-    s_lf[l] = f < 0 ? 0x7fffffff : f;
+  // (the register replay below reads the leaves' keys itself: no LDS image, no barrier)
+  const bool reg_replay = !cegb && st.forced_next < 0 && L <= 64 * kSelLPer && !a.sel_lds_replay;
+  if (!reg_replay) {
+    for (int l = t; l < st.num_leaves; l += blockDim.x) {
+      const int c = s_lcid[l];
+      const int f = s_feat[c];
+      s_lg[l] = f < 0 ? kMinScore : s_gain[c];
+      s_lf[l] = f < 0 ? 0x7fffffff : f;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   __shared__ int s_byn;
   if (w == 0) {
     int nl = st.num_leaves, ns = st.num_splits, done = 0, blocked = -1, nc = 0;
     int fnext = st.forced_next, bforced = 0;
     int byn = st.byn;  // bynode masks drawn (wave-uniform)
     unsigned epoch = epoch0;  // CEGB first-use events (wave-uniform)
-    if (!cegb && fnext < 0 && L <= 64 * kSelLPer && !a.sel_lds_replay) {
+    if (reg_replay) {
       // leaf l's (gain, feature, cid) in registers of lane l % 64, slot l / 64: per committed
       // split one wave max and two dependent LDS reads (the winner's left child, then its two
       // children's keys)
