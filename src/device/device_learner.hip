@@ -1746,8 +1746,14 @@ class DeviceTreeLearner : public TreeLearner {
     }
     facc_.Resize(K * 2 * static_cast<size_t>(TB_));
     facc_.Zero(stream_);  // the scan re-zeroes what it consumes: zero between rounds from here on
-    fpart_ticket_.Resize(1);
-    fpart_ticket_.Zero(stream_);
+    // partial-histogram slab: one row of TB words (gpu_use_dp: 2 TB) per histogram block
+    {
+      const int rows = FrontierHistRows(FrontierHistBlocks(), K);
+      fhslab_stride_ = static_cast<size_t>(TB_) * (use_dp_ && !QuantHist() ? 2 : 1);
+      fhslab_.Resize(static_cast<size_t>(rows) * fhslab_stride_);
+      fhmeta_.Resize(rows);
+      if (num_tiles_ > 256) Log::Fatal("frontier histograms: %d LDS tiles (at most 256)", num_tiles_);
+    }
     fscan_ticket_.Resize(K);
     fscan_ticket_.Zero(stream_);  // (the last item of each expansion re-zeroes its ticket)
     fscan_cpos_.Resize(2 * K);
@@ -1774,24 +1780,15 @@ class DeviceTreeLearner : public TreeLearner {
     ftile_pub_.Resize(ftile_cap_);
     ftile_pub_.Zero(stream_);
     for (int i = 3; i < kFrontierIdx; ++i) idx_[i].Resize(std::max(N_, 1));
-    // (g, h) carried next to the depth buffers' indices (opt-in, LGAP_CARRY_GH=1: at 10M the
-    // histograms gain 6 us per round and the partition loses 12.6 us moving them)
-    carry_gh_ = [] {
-      const char* e = std::getenv("LGAP_CARRY_GH");
-      return e != nullptr && e[0] == '1';
-    }();
-    for (int i = 0; i < kFrontierIdx; ++i) {
-      if (carry_gh_ && i != 2) fghb_[i].Resize(std::max(N_, 1));
-    }
-    // the partition's look-back needs all of its blocks resident: occupancy minus a margin
+    // partition grid: the resident blocks (a look-back past a block that is not resident counts
+    // the tile itself, k_f_partition / FAwait)
     int per_cu = FrontierPartitionBlocksPerCU(part_iters_);
     int cap = 8;  // A/B knob LGAP_FPART_BPC (10M rows: 4 -> 327.9, 6 -> 334.7, 8 -> 337.3 it/s)
     if (const char* e = std::getenv("LGAP_FPART_BPC")) cap = std::max(1, std::atoi(e));
     per_cu = std::max(1, std::min(cap, per_cu - 1));
     fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
     fscan_lds_ = FrontierScanLds(max_bin_, has_cat_ ? max_cat_bin_ : 1);
-    // (the attribute covers a second histogram copy whatever LGAP_HIST_COPIES says later)
-    FrontierSetLds(FrontierHistLds() + (HistCopiesFit() ? HistCopyBytes() : 0), fscan_lds_, use_dp_, width_);
+    FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
     if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
     // 512 / 1024 threads per histogram block. Round 3 (after the grid cap at 7/8 of the CUs),
@@ -1837,7 +1834,6 @@ class DeviceTreeLearner : public TreeLearner {
     a.colbins = colbins_.get();
     a.gh = gh_.get();
     for (int i = 0; i < kFrontierIdx; ++i) a.idx[i] = idx_[i].get();
-    for (int i = 0; i < kFrontierIdx; ++i) a.ghb[i] = fghb_[i].size() ? fghb_[i].get() : nullptr;
     a.N = N_;
     a.stride_dw = tstride_dw_;
     a.width = width_;
@@ -1871,6 +1867,10 @@ class DeviceTreeLearner : public TreeLearner {
     a.range_out = range_.get();
     a.slots = fslots_.get();
     a.acc = reinterpret_cast<unsigned long long*>(facc_.get());
+    a.hslab = fhslab_.get();
+    a.hslab_stride = fhslab_stride_;
+    a.hmeta = reinterpret_cast<int2*>(fhmeta_.get());
+    a.red_grid = 2 * num_cu_;
     a.ghmax = ghmax_.get();
     a.sum_mult = distributed_ && !ffeature_ ? std::max(1, P_) : 1;  // (max-reduced local sums)
     {
@@ -1894,11 +1894,6 @@ class DeviceTreeLearner : public TreeLearner {
       a.tiles = ntile_.get();
       a.hist_nib = 1;
     }
-    a.debug_noflush = std::getenv("LGAP_DEBUG_NOFLUSH") != nullptr ? 1 : 0;
-    {
-      const char* e = std::getenv("LGAP_FLUSH_ROT");
-      a.flush_rot = e != nullptr && e[0] == '0' ? 0 : 1;
-    }
     a.part_tile = fpart_tile_;
     a.max_depth = config_->max_depth;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
@@ -1910,7 +1905,6 @@ class DeviceTreeLearner : public TreeLearner {
     a.ghq = ghq_.get();
     a.qmax = qmax_.get();
     a.quant = QuantHist() && ghq_.size() >= static_cast<size_t>(K_) * N_ ? 1 : 0;
-    a.carry_gh = carry_gh_ && !a.quant ? 1 : 0;  // (quantized histograms read the int8 levels)
     a.qbins = std::max(2, config_->num_grad_quant_bins);
     a.qconst = is_const_hess_ ? 1 : 0;
     {
@@ -1926,7 +1920,6 @@ class DeviceTreeLearner : public TreeLearner {
       const bool want = e != nullptr ? e[0] != '0' : num_tiles_ == 1;
       a.qsub = a.quant && !use_dp_ && sub >= 2048 && want ? sub : 0;
     }
-    a.hist_copies = HistCopies(a.qsub);
     a.hist_il = !use_dp_ && a.qsub == 0 ? HistInterleave() : 0;
     {
       // one wave per scan item on wide data (LGAP_SCAN_WAVE: 0 never, 1 always, default F >= 64)
@@ -1968,10 +1961,6 @@ class DeviceTreeLearner : public TreeLearner {
       }
     }
     a.sel_bitonic = std::getenv("LGAP_SEL_BITONIC") != nullptr ? 1 : 0;
-    {
-      const char* e = std::getenv("LGAP_PART_NT");
-      a.part_nt = e != nullptr ? std::atoi(e) : 0;
-    }
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
@@ -1992,15 +1981,6 @@ class DeviceTreeLearner : public TreeLearner {
       const char* e = std::getenv("LGAP_SCAN_BEST");
       a.scan_best = e != nullptr && e[0] == '1' && !RawCands() && !fvoting_ && !ffeature_ ? 1 : 0;
       a.scan_ticket = fscan_ticket_.get();
-      // LGAP_PART_TICKET: 0 strided tiles, 1 atomic dispatch tickets, 2 contiguous tiles in block
-      // order. Default: strided on one process (A/B 10M, same box: 2.91 vs 2.98 ms/iter for block
-      // order, 3.11 for tickets; a kernel on another stream only delays the blocks it displaces,
-      // it finishes), block order when ranks exchange (an RCCL kernel waiting on peers could
-      // hold the CUs a strided partition needs)
-      const char* pt = std::getenv("LGAP_PART_TICKET");
-      const int pmode = pt != nullptr ? std::atoi(pt) : (distributed_ ? 2 : 0);
-      a.part_ticket = pmode == 1 ? fpart_ticket_.get() : nullptr;
-      a.part_contig = pmode == 2 ? 1 : 0;
       a.scan_cpos = fscan_cpos_.get();
     }
     a.xrng = config_->extra_trees ? rng_.get() : nullptr;
@@ -2296,7 +2276,6 @@ class DeviceTreeLearner : public TreeLearner {
       std::memcpy(fkused_hist_[fkused_trees_ % 4], hh->kused, sizeof(int) * kFrontierRoundCap);
       ++fkused_trees_;
     }
-    if (hbar[2] != 0u) Log::Fatal("k_f_partition: a wait on published tile counts timed out (blocks not co-resident?)");
     if (fstamps_.size() && fstat_trees_ == 3) ReportFrontierStamps(hs->round);
     if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {
       std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max), wasted rows %.1f%%, "
@@ -2515,20 +2494,7 @@ class DeviceTreeLearner : public TreeLearner {
     // (the interleaved slots' reserve only where k_f_hist can use them: fixed-point and MODE 2)
     const size_t plan = use_dp_ || fa.qsub > 0 ? hist_lds_plain_ : hist_lds_bytes_;
     const size_t b = use_dp_ || !QuantHist() || fa.qsub == 0 ? plan : plan * 3 / 2 + 64;
-    return fa.hist_copies > 1 ? b + HistCopyBytes() : b;
-  }
-
-  // Two LDS copies of the frontier histogram (k_f_hist: even / odd waves apart): one non-direct
-  // tile whose second copy still fits 150 KB, not the 32-bit MODE 3 (LGAP_HIST_COPIES=1: one)
-  size_t HistCopyBytes() const { return h_tiles_.empty() ? 0 : static_cast<size_t>(h_tiles_[0].nbins) * (use_dp_ ? 16 : 8); }
-  bool HistCopiesFit() const {
-    return num_tiles_ == 1 && !h_tiles_.empty() && !h_tiles_[0].direct && hist_lds_bytes_ + HistCopyBytes() <= 150 * 1024;
-  }
-  int HistCopies(int qsub) const {
-    if (!HistCopiesFit() || qsub > 0) return 1;
-    // (opt-in, LGAP_HIST_COPIES=2: flat at 10M, 2.99 vs 2.98 ms/iter)
-    const char* e = std::getenv("LGAP_HIST_COPIES");
-    return e != nullptr && std::atoi(e) == 2 ? 2 : 1;
+    return b;
   }
 
   // Integer-level histograms for quantized training (frontier hist MODE 2): int8 g and
@@ -2751,7 +2717,6 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(fexps_, ex.data(), sizeof(FExp) * k, hipMemcpyHostToDevice, stream_));
     facc_.Zero(stream_);
     FArgs fa = MakeFArgs();
-    fa.carry_gh = 0;  // (the subsets' rows were uploaded without their (g, h))
     LaunchFrontierHist(fa, FrontierHistLds(), stream_);
     const int pw = fa.quant && fa.qpack ? 1 : 2;
     std::vector<unsigned long long> acc(static_cast<size_t>(k) * pw * TB_);
@@ -2858,16 +2823,30 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(fexps_, ex.data(), sizeof(FExp) * k, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemcpyAsync(fbits_, bits.data(), sizeof(uint32_t) * bits.size(), hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(fbest_, 0, sizeof(SplitInfo) * k, stream_));
-    const FArgs fa = MakeFArgs();
+    FArgs fa = MakeFArgs();
     LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
     HIP_CHECK(hipMemcpyAsync(out_rows, idx_[1].get(), sizeof(int) * total, hipMemcpyDeviceToHost, stream_));
     std::vector<FNode> nodes(3 * static_cast<size_t>(k));
     HIP_CHECK(hipMemcpyAsync(nodes.data(), fnodes_, sizeof(FNode) * nodes.size(), hipMemcpyDeviceToHost, stream_));
-    unsigned hbar[4];
-    HIP_CHECK(hipMemcpyAsync(hbar, bar_.get(), sizeof(hbar), hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-    if (hbar[2] != 0u) Log::Fatal("TestFrontierPartition: a look-back wait timed out");
     for (int e = 0; e < k; ++e) out_left[e] = nodes[k + 2 * e].count;
+    // the look-back's fallback (a predecessor's block not resident: the waiting thread counts the
+    // tile itself) must place every row exactly where the published counts do: the same launch
+    // again with every look-back self-counted
+    st.epoch = st.epoch + 1u;
+    HIP_CHECK(hipMemcpyAsync(fst_, &st, sizeof(FState), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(fexps_, ex.data(), sizeof(FExp) * k, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemsetAsync(idx_[1].get(), 0xff, sizeof(int) * total, stream_));
+    fa.part_selfcount = 1;
+    LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    std::vector<int> rows2(total);
+    HIP_CHECK(hipMemcpyAsync(rows2.data(), idx_[1].get(), sizeof(int) * total, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(nodes.data(), fnodes_, sizeof(FNode) * nodes.size(), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int e = 0; e < k; ++e) {
+      if (nodes[k + 2 * e].count != out_left[e]) Log::Fatal("TestFrontierPartition: self-counted look-back, parent %d: left count differs", e);
+    }
+    if (!std::equal(rows2.begin(), rows2.end(), out_rows)) Log::Fatal("TestFrontierPartition: self-counted look-back places rows differently");
   }
 
   void TestHistogram(const float* g, const float* h, const int* rows, int n, double* out) {
@@ -3797,7 +3776,7 @@ class DeviceTreeLearner : public TreeLearner {
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
-  DevBuf<unsigned> fscan_ticket_, fpart_ticket_;
+  DevBuf<unsigned> fscan_ticket_;
   // score update fused with the next pointwise gradients (DeviceAddTreeToScore)
   const ObjectiveFunction* fused_obj_ = nullptr;  // pointwise objective of the last gradient pass
   bool fused_grad_ready_ = false, fuse_pending_ = false, fuse_done_ = false;
@@ -3838,6 +3817,9 @@ class DeviceTreeLearner : public TreeLearner {
   SplitInfo* fcinfo_ = nullptr;
   DevBuf<double> fslots_;
   DevBuf<unsigned long long> facc_;
+  DevBuf<unsigned long long> fhslab_;  // k_f_hist partial rows
+  size_t fhslab_stride_ = 0;
+  DevBuf<long long> fhmeta_;           // (int2 per row)
   DevBuf<unsigned long long> ftile_pub_;
   std::map<int, hipGraphExec_t> fgraphs_;
   hipGraphExec_t fcont_ = nullptr;
@@ -3954,8 +3936,6 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<float> label_, weight_, aux_;
   static_assert(kFrontierIdx <= kLeafIdxBufs, "leaf renewal addresses every index buffer");
   DevBuf<int> idx_[kFrontierIdx];
-  DevBuf<float2> fghb_[kFrontierIdx];  // (g, h) next to the frontier's depth-buffer indices
-  bool carry_gh_ = false;
   DevBuf<DevFeature> feat_;
   DevBuf<int> gstart_;
   DevBuf<HistTile> tiles_;

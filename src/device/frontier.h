@@ -147,11 +147,6 @@ struct FArgs {
   const uint8_t* colbins;
   const float2* gh;  // class-major (cls from tp)
   int* idx[kFrontierIdx];
-  // (g, h) carried alongside the depth buffers' row indices (carry_gh): the partition writes each
-  // row's (g, h) next to its index, so the histograms read them contiguously instead of
-  // gathering a sector per row (null: buffers without, the root / bag read gh[row])
-  float2* ghb[kFrontierIdx];
-  int carry_gh;
   int N, stride_dw, width, num_groups, TB, F, L, C, kmax;
   const int* gstart;
   const DevFeature* feat;
@@ -179,6 +174,10 @@ struct FArgs {
   // histograms
   double* slots;              // [C][2 TB] per-node histograms (stored bins, fp64)
   unsigned long long* acc;    // [kmax][2 TB] per-expansion fixed-point accumulators (zero between rounds)
+  unsigned long long* hslab;  // [hist rows][hslab_stride] k_f_hist's per-block partial histograms (raw LDS words)
+  size_t hslab_stride;        // words per slab row (TB, x2 for gpu_use_dp)
+  int2* hmeta;                // [hist rows] MODE 0: the block's fixed-point exponents (bg, bh)
+  int red_grid;               // k_f_reduce blocks
   const unsigned* ghmax;      // float bits of max|g|, max|h|, sum|g|, sum|h| over the root rows
   int sum_mult;               // ranks whose root rows the global sums span (row-sharded DP / voting), else 1
   int sum_bound;              // use the sum|value| bounds (LGAP_FIXED_SUMBOUND=0: max only, the round-3 scale)
@@ -200,32 +199,22 @@ struct FArgs {
   SplitInfo* cinfo;
   // partition look-back
   unsigned long long* tile_pub;
-  unsigned* bar;  // bar[2]: bounded-wait error flag
+  unsigned* bar;
   // per-child best split in the scan (scan_best = 1): the last item of an expansion to finish
   // (completion ticket) takes the arg-max over the features for both children and writes
   // best / key, so the select's phase A only reads the winners' candidate positions
-  // partition tile ownership. part_contig (default): block b owns the contiguous range
-  // [b per, (b + 1) per), per = ceil(T / G), so its look-back only waits on lower blocks, which the in-order
-  // dispatch started before it -- no co-residency assumption. part_ticket != null
-  // (LGAP_PART_TICKET=1): the same with an atomic dispatch ticket instead of blockIdx (the
-  // select / init zero the counter for the next launch). Neither (LGAP_PART_TICKET=0): tiles
-  // blockIdx + j G, which needs every block resident.
-  int part_contig;
-  unsigned* part_ticket;
   int scan_best;
   unsigned* scan_ticket;  // [kmax] finished items per expansion (reset by the last one)
   int* scan_cpos;         // [2 kmax] winning candidate position per child pair, -1: none
+  int part_selfcount;  // test hook: every look-back counts its predecessor tiles itself (FTileCount)
   int hist_min_rows, hist_grid;
   int hist_threads;  // 512 or 1024 threads per histogram block
-  int hist_copies;   // LDS histogram copies per block (2: even / odd waves apart; single-tile data)
   int hist_il;       // bank-interleaved LDS histograms (tiles with pad = their largest group's bins)
   int scan_wave;     // k_f_scan_w (one wave per (expansion, feature)) instead of one block per item
   int scan_grid;     // cap of the block scan's grid (A/B knob LGAP_SCAN_GRID; 0: 4096)
   int sel_block_rank;  // the select's block-wide rank / scan for <= 64 alive nodes too (A/B knob)
   int sel_lds_replay;  // A/B knob (LGAP_SEL_LDS_REPLAY=1): the replay's leaf keys in LDS (else registers when L <= 64)
   int sel_early;       // A/B knob (LGAP_SEL_EARLY=1): phase A's candidate loads in the image's load round
-  int debug_noflush;  // diagnostics: skip the histogram flush (invalid models; timing only)
-  int flush_rot;      // per-block rotated flush order (LGAP_FLUSH_ROT=0 disables)
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)
   int part_tile;  // rows per partition tile (256 x rows per thread)
   int max_depth, use_monotone;
@@ -293,7 +282,6 @@ struct FArgs {
   unsigned* xrng;
   struct FPairBest* fpb;  // [P][kmax][2] per-child best of each rank, all-gathered
   int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
-  int part_nt;      // A/B knob (LGAP_PART_NT): the partition's row-index scatter stores, 1 non-temporal, 2 write-through (sc1)
   SplitParams sp;
 };
 
@@ -316,7 +304,8 @@ inline size_t FrontierResultBytes(int L) { return FrontierResultRangeOffset(L) +
 // launchers (frontier_kernels.hip)
 void LaunchFrontierResults(const FArgs& a, void* host_out, hipStream_t s);
 void LaunchFrontierInit(const FArgs& a, hipStream_t s);
-void LaunchFrontierHist(const FArgs& a, size_t lds_bytes, hipStream_t s);
+void LaunchFrontierHist(const FArgs& a, size_t lds_bytes, hipStream_t s);  // k_f_hist + k_f_reduce
+int FrontierHistRows(int hist_grid, int kmax);  // k_f_hist's grid.x (partial slab rows)
 void LaunchFrontierScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
 
 // Wave-per-item scan (k_f_scan_w, wide data): per wave the two fp64 (g, h) histograms of the
@@ -343,7 +332,7 @@ void LaunchFrontierVoteScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
 // over ranks -> the candidate table (after it)
 void LaunchFrontierPairBest(const FArgs& a, hipStream_t s);
 void LaunchFrontierPairMerge(const FArgs& a, hipStream_t s);
-// resident 256-thread partition blocks per CU (the look-back needs every block resident)
+// resident 256-thread partition blocks per CU (the grid size; the look-back does not need them resident)
 int FrontierPartitionBlocksPerCU(int iters);
 // one-time kernel attributes (dynamic LDS above 64 KiB)
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width);

@@ -140,7 +140,6 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
   }
   for (int i = t; i < a.C; i += blockDim.x) a.nstate[i] = 0;
   for (int f = t; f < a.F; f += blockDim.x) a.spl[f] = 1;
-  if (t == 0 && a.part_ticket != nullptr) *a.part_ticket = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -174,9 +173,6 @@ template <int W, int MODE>
 __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
                                           const int* gst, unsigned long long* hist, float sg, float sh, double dsg,
                                           double dsh, uint32_t* hist32 = nullptr, int il_gp = 0) {
-  // (g, h) of position p: carried next to the index list (contiguous) or gathered by row
-  const float2* ghp = MODE < 2 && buf >= 0 && a.carry_gh ? a.ghb[buf] : nullptr;
-  if (ghp != nullptr) ghp += start;
   const int tpr = tile.d1 - tile.d0;
   const int rpi = blockDim.x / tpr;
   const int myr = threadIdx.x / tpr;
@@ -205,7 +201,6 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
     gsh[kk] = sv;
   }
   const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
-  const float2* gsrc = ghp != nullptr ? ghp : gh;  // (indexed by position, or by row)
   const uint16_t* ghq = MODE >= 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
   const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
   const int base = buf < 0 ? start : 0;
@@ -223,7 +218,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
     for (int j = 0; j < R; ++j) {
       word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
       if (MODE >= 2) q[j] = rows[j] >= 0 ? ghq[rows[j]] : 0u;
-      else v[j] = rows[j] >= 0 ? gsrc[ghp != nullptr ? p0 + j * rpi : rows[j]] : make_float2(0.f, 0.f);
+      else v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -261,6 +256,34 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   }
 }
 
+// Row chunking of a round's histograms (wave 0, lane = expansion; identical in k_f_hist, which
+// assigns the chunks to blocks, and k_f_reduce, which sums each expansion's blocks): chunk rows c
+// for the whole round, nb chunks of expansion `lane` in blocks [inc - nb, inc).
+// sum over e of ceil(cnt_e / c) <= total / c + ke <= hist_grid while ke <= hist_grid / 2: with
+// hist_grid below the CU count every working block gets a CU of its own (256 + k blocks doubled
+// some CUs' work and the round waited on them: A/B at 10M, 330 it/s vs 363 it/s). Many expansions
+// over a small grid (wide data, many LDS tiles) still get >= hist_grid / 2 row-balanced chunks.
+__device__ __forceinline__ void FHistChunks(const FArgs& a, int k, int* cnt, int* hb, int* hs, int* nb, int* inc) {
+  const int t = threadIdx.x;
+  *cnt = 0;
+  *hb = -1;
+  *hs = 0;
+  if (t < k && t >= a.e_lo && t < a.e_hi) {
+    const FExp& x = a.exps[t];
+    if (!x.skip) {
+      *cnt = x.h_count;
+      *hb = x.h_buf;
+      *hs = x.h_start;
+    }
+  }
+  const int total = WaveSum(*cnt);
+  const int ke = WaveSum(*cnt > 0 ? 1 : 0);
+  const int slots = max(max(1, a.hist_grid / 2), a.hist_grid - ke);
+  const int c = max(a.hist_min_rows, (total + slots - 1) / slots);
+  *nb = (*cnt + c - 1) / c;
+  *inc = WaveInclusiveScan(*nb);
+}
+
 template <int W, int MODE, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   extern __shared__ __align__(8) unsigned char lds_raw[];
@@ -272,28 +295,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   const int rnd = sp->round;
   FStamp(a, rnd, kFStampHist, 0);
   if (t < 64) {
-    // per-expansion chunking (identical in every block): chunk rows c for the whole round,
-    // nb_e chunks of expansion e, blocks [pre_e, pre_e + nb_e)
-    int cnt = 0, hb = -1, hs = 0;
-    if (t < k && t >= a.e_lo && t < a.e_hi) {
-      const FExp& x = a.exps[t];
-      if (!x.skip) {
-        cnt = x.h_count;
-        hb = x.h_buf;
-        hs = x.h_start;
-      }
-    }
-    // sum over e of ceil(cnt_e / c) <= total / c + ke <= hist_grid while ke <= hist_grid / 2:
-    // with hist_grid below the CU count every working block gets a CU of its own (256 + k
-    // blocks doubled some CUs' work and the round waited on them: A/B at 10M, 330 it/s vs
-    // 363 it/s). Many expansions over a small grid (wide data, many LDS tiles) still get
-    // >= hist_grid / 2 row-balanced chunks.
-    const int total = WaveSum(cnt);
-    const int ke = WaveSum(cnt > 0 ? 1 : 0);
-    const int slots = max(max(1, a.hist_grid / 2), a.hist_grid - ke);
-    const int c = max(a.hist_min_rows, (total + slots - 1) / slots);
-    const int nb = (cnt + c - 1) / c;
-    const int inc = WaveInclusiveScan(nb);
+    int cnt, hb, hs, nb, inc;
+    FHistChunks(a, k, &cnt, &hb, &hs, &nb, &inc);
     const int bx = static_cast<int>(blockIdx.x);
     const bool mine = nb > 0 && bx >= inc - nb && bx < inc;
     const unsigned long long m = __ballot(mine);
@@ -335,8 +338,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         sg += static_cast<int8_t>(qv >> 8);
         sh += static_cast<long long>(qv & 0xFFu);
       } else {
-        const float2 v = buf >= 0 && a.carry_gh && a.ghb[buf] != nullptr ? a.ghb[buf][start + p]
-                                                                          : a.gh[static_cast<size_t>(a.tp->cls) * a.N + row];
+        const float2 v = a.gh[static_cast<size_t>(a.tp->cls) * a.N + row];
         sg += __double2ll_rn(static_cast<double>(v.x) * dsg);
         sh += __double2ll_rn(static_cast<double>(v.y) * dsh);
       }
@@ -358,7 +360,6 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
     constexpr int per = W == 0 ? 8 : 4 / W;
     const int dw = tile.d0 + myd;
     const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
-    const float2* ghp = MODE < 2 && buf >= 0 && a.carry_gh && a.ghb[buf] != nullptr ? a.ghb[buf] + start : nullptr;
     for (int p = rb + myr; p < re; p += rpi) {
       const int row = FRowAt(a, buf, start + p);
       const uint32_t word = a.rowbins[static_cast<size_t>(row) * a.stride_dw + dw];
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         qh = qv & 0xFFu;
         if (a.qpack) qg = (qg << 32) + qh, qh = 0ull;
       } else {
-        const float2 v = ghp != nullptr ? ghp[p] : gh[row];
+        const float2 v = gh[row];
         qg = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.x) * dsg));
         qh = static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v.y) * dsh));
       }
@@ -403,17 +404,13 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   // per-group reads of interleaved slots conflict)
   const int il_gp = (MODE == 0 || MODE == 2) && a.hist_il && tile.pad > 0 && (buf < 0 || a.hist_il > 1) ? ((ng + 15) & ~15) : 0;
   const int words = il_gp > 0 ? tile.pad * il_gp : (MODE != 1 ? tile.nbins : 2 * tile.nbins);
-  // two LDS copies of the histogram when they fit (hist_copies = 2, single-tile data): even
-  // and odd waves accumulate into different copies, halving same-bin atomic collisions (a deep
-  // node's rows crowd few bins of its split features); the flush adds the two
-  const int copies = MODE == 3 || il_gp > 0 ? 1 : (a.hist_copies > 1 ? 2 : 1);
   unsigned long long* hist = reinterpret_cast<unsigned long long*>(lds_raw);
   uint32_t* hist32 = reinterpret_cast<uint32_t*>(hist + words);
   int* gst = reinterpret_cast<int*>(MODE == 3 ? reinterpret_cast<unsigned long long*>(hist32 + ((tile.nbins + 1) & ~1))
-                                              : hist + copies * words);
-  // (interleaved: the packed image the flush reads, after gst)
+                                              : hist + words);
+  // (interleaved: the packed image the partial store reads, after gst)
   unsigned long long* packed = il_gp > 0 ? reinterpret_cast<unsigned long long*>(gst + ((ng + 1) & ~1)) : nullptr;
-  for (int i = t; i < copies * words; i += blockDim.x) hist[i] = 0ull;
+  for (int i = t; i < words; i += blockDim.x) hist[i] = 0ull;
   if (MODE == 3) {
     for (int i = t; i < tile.nbins; i += blockDim.x) hist32[i] = 0u;
   }
@@ -436,13 +433,12 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       __syncthreads();
     }
   } else {
-    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist + (copies > 1 ? ((t >> 6) & 1) * words : 0), sg, sh, dsg,
-                       dsh, nullptr, il_gp);
+    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh, nullptr, il_gp);
     __syncthreads();
   }
   if (il_gp > 0) {
-    // interleaved slots -> the packed image (conflict-free reads in slot order), so the flush
-    // below reads consecutive bins of a group from consecutive words
+    // interleaved slots -> the packed image (conflict-free reads in slot order), so the partial
+    // store below writes consecutive bins of a group to consecutive words
     for (int sl = t; sl < words; sl += blockDim.x) {
       const int b = sl / il_gp, gl = sl - b * il_gp;
       if (gl >= ng) continue;
@@ -453,56 +449,136 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   }
   FStamp(a, rnd, kFStampHist, 2);
   FStampMax(a, rnd, kFStampHist, 5);  // (latest block done with its rows)
-  unsigned long long* out = acc + pw * static_cast<size_t>(tile.bin0);
-  if (a.debug_noflush) return;  // timing diagnostics only (LGAP_DEBUG_NOFLUSH): results are wrong
-  // every block starts its flush at its own offset of the tile, so the blocks' concurrent
-  // atomics hit different accumulator words instead of queueing on the same ones
-  const int rot = a.flush_rot ? static_cast<int>((static_cast<long long>(blockIdx.x) * tile.nbins) / gridDim.x) : 0;
-  if (MODE == 0 || MODE >= 2) {
-    // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
-    // GlobalScaleExp; the guard keeps a degenerate max of 0 harmless)
-    const int shg = max(0, EG - bg), shh = max(0, EH - bh);
-    const bool pack = a.qpack != 0;
-    auto flush = [&](int i, unsigned long long x) {
-      if (MODE == 0) {
-        const int hs = static_cast<int>(static_cast<unsigned int>(x & 0xFFFFFFFFull));
-        const long long gs = static_cast<long long>(x - static_cast<unsigned long long>(static_cast<long long>(hs))) >> 32;
-        const long long qg = gs * (1ll << shg);
-        const long long qh = static_cast<long long>(hs) * (1ll << shh);
-        if (qg) atomicAdd(&out[2 * i], static_cast<unsigned long long>(qg));
-        if (qh) atomicAdd(&out[2 * i + 1], static_cast<unsigned long long>(qh));
-      } else if (pack) {
-        atomicAdd(&out[i], x);  // (pw == 1)
-      } else {
-        const unsigned long long hs = x & 0xFFFFFFFFull;
-        const long long gs = static_cast<long long>(x - hs) >> 32;
-        if (gs) atomicAdd(&out[2 * i], static_cast<unsigned long long>(gs));
-        if (hs) atomicAdd(&out[2 * i + 1], hs);
+  // The block's histogram -> its row of the partial slab with plain coalesced stores, raw (block
+  // scale for MODE 0, its exponents in hmeta); k_f_reduce sums each expansion's rows at the
+  // global scale. (A per-block flush of every bin with 64-bit global atomics executes at the
+  // memory side at ~1.3 TB/s of added bytes: at 224 blocks x 7,140 bins x 2 words that was the
+  // 13-18 us tail of every histogram launch.)
+  const int sw = MODE == 1 ? 2 : 1;  // slab words per bin
+  unsigned long long* prow = a.hslab + static_cast<size_t>(blockIdx.x) * a.hslab_stride + static_cast<size_t>(sw) * tile.bin0;
+  const unsigned long long* src = il_gp > 0 ? packed : hist;
+  for (int j = t; j < sw * tile.nbins; j += blockDim.x) prow[j] = src[j];
+  if (MODE == 0 && t == 0) a.hmeta[blockIdx.x] = make_int2(bg, bh);  // (every tile's block: the same value)
+  FStamp(a, rnd, kFStampHist, 3);
+  FStampMax(a, rnd, kFStampHist, 6);  // (latest block done issuing its partial)
+  FStampEnd(a, rnd, kFStampHist);
+}
+
+// ---------------------------------------------------------------------------
+// k_f_reduce: the round's partial histograms (k_f_hist's slab rows) summed per expansion into
+// its accumulator at the tree's global fixed-point scale (exact integer sums, order free).
+// Work item = (expansion e, LDS tile, 256-bin chunk of the tile, group of kRedRows of e's row
+// blocks): one thread per bin issues its kRedRows partial loads together; an expansion whose
+// rows span one group stores its sums, more groups add theirs with 64-bit atomics (at most
+// ceil(blocks / kRedRows) per bin instead of one per block). Reference counterpart: the
+// per-block histogram merge of cuda_histogram_constructor.cu:20-70 (CUDA: block atomics into
+// global memory).
+constexpr int kRedThreads = 256;
+constexpr int kRedRows = 16;
+constexpr int kRedMaxTiles = 256;
+
+template <int MODE>
+__global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
+  __shared__ int s_nb[kFrontierKmax], s_b0[kFrontierKmax], s_w0[kFrontierKmax + 1];
+  __shared__ int s_tc[kRedMaxTiles + 1];  // chunk prefix over the LDS tiles (direct tiles: none)
+  const FState* sp = a.st;
+  if (sp->done) return;
+  const int k = sp->k;
+  const int t = threadIdx.x;
+  const int rnd = sp->round;
+  if (t < 64) {
+    int cnt, hb, hs, nb, inc;
+    FHistChunks(a, k, &cnt, &hb, &hs, &nb, &inc);
+    if (t < kFrontierKmax) {
+      s_nb[t] = nb;
+      s_b0[t] = inc - nb;
+    }
+    // work items per expansion: bin chunks x row groups (prefix over the expansions)
+    int nch = 0;
+    for (int y = 0; y < a.num_tiles; ++y) nch += a.tiles[y].direct ? 0 : (a.tiles[y].nbins + kRedThreads - 1) / kRedThreads;
+    const int items = ((nb + kRedRows - 1) / kRedRows) * nch;
+    const int winc = WaveInclusiveScan(items);
+    if (t < kFrontierKmax) s_w0[t + 1] = winc;
+    if (t == 0) s_w0[0] = 0;
+  }
+  if (t == 64) {
+    int c = 0;
+    for (int y = 0; y < a.num_tiles && y < kRedMaxTiles; ++y) {
+      s_tc[y] = c;
+      c += a.tiles[y].direct ? 0 : (a.tiles[y].nbins + kRedThreads - 1) / kRedThreads;
+    }
+    s_tc[min(a.num_tiles, kRedMaxTiles)] = c;
+  }
+  __syncthreads();
+  const int nch = s_tc[min(a.num_tiles, kRedMaxTiles)];
+  const int W = s_w0[k];
+  if (W == 0 || nch == 0) return;
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
+  const int pw = a.quant && a.qpack ? 1 : 2;  // accumulator words per bin (see k_f_hist)
+  constexpr int sw = MODE == 1 ? 2 : 1;       // slab words per bin
+  for (int w = blockIdx.x; w < W; w += gridDim.x) {
+    int e = 0;
+    while (e + 1 < k && s_w0[e + 1] <= w) ++e;
+    const int r = w - s_w0[e];
+    const int grp = r / nch, ch = r - grp * nch;
+    int y = 0;
+    while (y + 1 < a.num_tiles && s_tc[y + 1] <= ch) ++y;
+    const HistTile tile = a.tiles[y];
+    const int i = (ch - s_tc[y]) * kRedThreads + t;  // bin of the tile
+    if (i >= tile.nbins) continue;
+    const int nb = s_nb[e];
+    const int r0 = s_b0[e] + grp * kRedRows, r1 = min(s_b0[e] + nb, r0 + kRedRows);
+    const size_t col = static_cast<size_t>(sw) * (tile.bin0 + i);
+    long long g = 0, h = 0;
+    unsigned long long x0[kRedRows], x1[kRedRows];
+#pragma unroll
+    for (int j = 0; j < kRedRows; ++j) {
+      const int row = r0 + j;
+      x0[j] = row < r1 ? a.hslab[static_cast<size_t>(row) * a.hslab_stride + col] : 0ull;
+      x1[j] = MODE == 1 && row < r1 ? a.hslab[static_cast<size_t>(row) * a.hslab_stride + col + 1] : 0ull;
+    }
+    if (MODE == 0) {
+#pragma unroll
+      for (int j = 0; j < kRedRows; ++j) {
+        if (r0 + j >= r1) continue;
+        const int2 m = a.hmeta[r0 + j];  // (uniform: scalar loads)
+        const int hv = static_cast<int>(static_cast<unsigned int>(x0[j] & 0xFFFFFFFFull));
+        const long long gv = static_cast<long long>(x0[j] - static_cast<unsigned long long>(static_cast<long long>(hv))) >> 32;
+        // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
+        // GlobalScaleExp; the guard keeps a degenerate max of 0 harmless)
+        g += gv * (1ll << max(0, EG - m.x));
+        h += static_cast<long long>(hv) * (1ll << max(0, EH - m.y));
       }
-    };
-    if (il_gp > 0) {
-      for (int j = t; j < tile.nbins; j += blockDim.x) {
-        const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
-        const unsigned long long x = packed[i];
-        if (x != 0ull) flush(i, x);
+    } else if (MODE == 1) {
+#pragma unroll
+      for (int j = 0; j < kRedRows; ++j) {
+        g += static_cast<long long>(x0[j]);
+        h += static_cast<long long>(x1[j]);
       }
+    } else if (pw == 1) {
+      // packed g32|h32 level sums: the packed words add exactly (qpack bounds every field)
+#pragma unroll
+      for (int j = 0; j < kRedRows; ++j) g += static_cast<long long>(x0[j]);
     } else {
-      for (int j = t; j < tile.nbins; j += blockDim.x) {
-        const int i = j < tile.nbins - rot ? j + rot : j + rot - tile.nbins;
-        const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);  // (packed fields: exact)
-        if (x != 0ull) flush(i, x);
+#pragma unroll
+      for (int j = 0; j < kRedRows; ++j) {
+        const unsigned long long hv = x0[j] & 0xFFFFFFFFull;
+        g += static_cast<long long>(x0[j] - hv) >> 32;
+        h += static_cast<long long>(hv);
       }
     }
-  } else {
-    for (int j = t; j < 2 * tile.nbins; j += blockDim.x) {
-      const int i = j < 2 * (tile.nbins - rot) ? j + 2 * rot : j + 2 * rot - 2 * tile.nbins;
-      const unsigned long long x = hist[i] + (copies > 1 ? hist[words + i] : 0ull);
-      if (x) atomicAdd(&out[i], x);
+    unsigned long long* out = a.acc + static_cast<size_t>(e) * pw * a.TB + static_cast<size_t>(pw) * (tile.bin0 + i);
+    if (nb <= kRedRows) {
+      // the expansion's only row group: the accumulator is zero here (the scan re-zeroes it)
+      if (g) out[0] = static_cast<unsigned long long>(g);
+      if (pw == 2 && h) out[1] = static_cast<unsigned long long>(h);
+    } else {
+      if (g) atomicAdd(&out[0], static_cast<unsigned long long>(g));
+      if (pw == 2 && h) atomicAdd(&out[1], static_cast<unsigned long long>(h));
     }
   }
-  FStamp(a, rnd, kFStampHist, 3);
-  FStampMax(a, rnd, kFStampHist, 6);  // (latest block done issuing its flush)
-  FStampEnd(a, rnd, kFStampHist);
+  (void)rnd;
 }
 
 // ---------------------------------------------------------------------------
@@ -1104,36 +1180,31 @@ __device__ __forceinline__ void FPublish(unsigned long long* p, unsigned epoch, 
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// a scattered row index: plain (written back from the XCD's L2 at the kernel boundary),
-// non-temporal (1), or write-through sc1 (2: nothing left dirty for the boundary to write back)
-__device__ __forceinline__ void FStoreRow(int mode, int* dst, int v) {
-  if (mode == 2) {
-    __hip_atomic_store((__attribute__((address_space(1))) int*)(dst), v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  } else if (mode == 1) {
-    __builtin_nontemporal_store(v, dst);
-  } else {
-    *dst = v;
+// split predicate of expansion x on group bin gb (GoLeft of split_scan.h, categorical set in `bits`)
+__device__ __forceinline__ bool FGoLeft(const FExp& x, const uint32_t* bits, uint32_t gb) {
+  const uint32_t b = DecodeBin(x.offset, x.num_bin, x.mfb, gb);
+  if (x.is_cat) {
+    const uint32_t wd = b >> 5;
+    return wd < static_cast<uint32_t>(kMaxCatWords) && ((bits[wd] >> (b & 31u)) & 1u);
   }
+  if ((x.missing == 1 && b == static_cast<uint32_t>(x.default_bin)) ||
+      (x.missing == 2 && b == static_cast<uint32_t>(x.num_bin - 1))) {
+    return x.default_left != 0;
+  }
+  return b <= static_cast<uint32_t>(x.thr);
 }
 
-__device__ __forceinline__ int FAwait(const FArgs& a, int i, unsigned epoch) {
-  unsigned spins = 0;
-  for (;;) {
-    const unsigned long long v = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (static_cast<unsigned>(v >> 32) == epoch) return static_cast<int>(static_cast<unsigned>(v));
-    __builtin_amdgcn_s_sleep(1);
-    if ((++spins & 1023u) == 0u &&
-        (spins > (1u << 22) || __hip_atomic_load(&a.bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-      __hip_atomic_store(&a.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return 0;
-    }
-  }
-}
+// Look-back without co-residency. Strided tile ownership lets block b wait on tiles of blocks
+// dispatched after it; when those are not resident (a kernel on another stream, an RCCL kernel
+// waiting on peers, another process holding CUs) a bounded poll gives up, and the block counts
+// the missing predecessor tiles itself (FLookbackSlow) -- the same pure function of the tile's rows
+// its owner evaluates -- and publishes the identical values. Nothing is paid while the owners run.
+constexpr unsigned kLookbackSpins = 2048;  // s_sleep(1) polls (~100 us) before a tile is counted here
 
-// this thread's share of the published counts of tiles [i0, i1): the loads of a batch are
-// issued together (one round trip per batch of 8), only tiles not yet published are re-polled
-__device__ __forceinline__ int FThreadCounts(const FArgs& a, int i0, int i1, unsigned epoch) {
+// this thread's share of the published counts of tiles [i0, i1): the loads of a batch are issued
+// together (one round trip per batch of 8), only tiles not yet published are re-polled; a tile
+// still unpublished after the bound sets *miss (the caller's block then takes FLookbackSlow)
+__device__ __forceinline__ int FThreadCounts(const FArgs& a, int i0, int i1, unsigned epoch, bool* miss) {
   constexpr int B = 8;
   const int stride = static_cast<int>(blockDim.x);
   int s = 0;
@@ -1148,15 +1219,54 @@ __device__ __forceinline__ int FThreadCounts(const FArgs& a, int i0, int i1, uns
 #pragma unroll
     for (int b = 0; b < B; ++b) {
       const int i = base + b * stride;
-      s += static_cast<unsigned>(v[b] >> 32) == epoch ? static_cast<int>(static_cast<unsigned>(v[b])) : FAwait(a, i, epoch);
+      unsigned spins = 0;
+      while (static_cast<unsigned>(v[b] >> 32) != epoch && spins < kLookbackSpins) {
+        __builtin_amdgcn_s_sleep(1);
+        v[b] = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ++spins;
+      }
+      if (static_cast<unsigned>(v[b] >> 32) == epoch) s += static_cast<int>(static_cast<unsigned>(v[b]));
+      else *miss = true;
     }
   }
+  if (a.part_selfcount) *miss = true;  // (test hook: every look-back through the slow path)
   return s;
 }
 
-// sum of the published counts of tiles [i0, i1)
-__device__ int FSumCounts(const FArgs& a, int i0, int i1, unsigned epoch, int* sh) {
-  return BlockSumInt(FThreadCounts(a, i0, i1, epoch), sh);
+// Sum of the left counts of tiles [i0, i1) of expansion x, block-cooperatively: published counts
+// read (not waited for), every unpublished tile counted by the whole block and published. The
+// rare path of the look-back (and every look-back under the part_selfcount test hook).
+__device__ int FLookbackSlow(const FArgs& a, const FExp& x, const uint32_t* bits, int i0, int i1, unsigned epoch,
+                             int* sh, int* s_list, int* s_nlist) {
+  const int t = threadIdx.x;
+  int total = 0;
+  for (int b0 = i0; b0 < i1; b0 += blockDim.x) {
+    const int i = b0 + t;
+    int c = 0;
+    if (t == 0) *s_nlist = 0;
+    __syncthreads();
+    if (i < i1) {
+      const unsigned long long v = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (static_cast<unsigned>(v >> 32) == epoch && !a.part_selfcount) c = static_cast<int>(static_cast<unsigned>(v));
+      else s_list[atomicAdd(s_nlist, 1)] = i;
+    }
+    total += BlockSumInt(c, sh);  // (its barriers also publish s_list / s_nlist)
+    const int nm = *s_nlist;
+    for (int m = 0; m < nm; ++m) {
+      const int tile = s_list[m];
+      const int p0 = (tile - x.tile0) * a.part_tile, p1 = min(x.count, p0 + a.part_tile);
+      int cc = 0;
+      for (int p = p0 + t; p < p1; p += blockDim.x) {
+        const int row = FRowAt(a, x.src_buf, x.start + p);
+        cc += FGoLeft(x, bits, FColBin(a, x.group, row)) ? 1 : 0;
+      }
+      cc = BlockSumInt(cc, sh);
+      if (t == 0) FPublish(&a.tile_pub[tile], epoch, cc);
+      total += cc;
+    }
+    __syncthreads();  // (s_list / s_nlist reused)
+  }
+  return total;
 }
 
 // children of expansion x (one thread)
@@ -1244,13 +1354,13 @@ __device__ __forceinline__ void BlockSumMulti(int* v, int* sh) {
   for (int m = 0; m < M; ++m) v[m] = sh[m * 4] + sh[m * 4 + 1] + sh[m * 4 + 2] + sh[m * 4 + 3];
 }
 
-// A block owns tiles base + j * stride: a contiguous range in block order (part_contig) or in
-// ticket order (part_ticket), or blockIdx.x + j * gridDim.x (LGAP_PART_TICKET=0, which needs
-// every block resident). The first MAXT of them live in registers for the whole
-// launch: their loads are issued together (row ids, then bins), their counts reduced in one
-// block sum, their look-back sums loaded in one round, their scatter ballots published in one
-// LDS barrier, so a block pays a few memory round trips instead of a few per tile. Tiles
-// beyond MAXT (a grid smaller than the round's tiles / MAXT) take the per-tile path.
+// Block b owns tiles b + j * G (strided: concurrently running blocks stream neighbouring tiles).
+// The first MAXT of them live in registers for the whole launch: their loads are issued together
+// (row ids, then bins), their counts reduced in one block sum, their look-back sums loaded in one
+// round, their scatter ballots published in one LDS barrier, so a block pays a few memory round
+// trips instead of a few per tile. Tiles beyond MAXT (a grid smaller than the round's tiles /
+// MAXT) take the per-tile path. A look-back on a tile whose owner has not run yet counts that
+// tile itself (FAwait): the grid needs no co-residency.
 template <int ITERS, int MAXT>
 __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(ITERS == 8 ? 5 : 1))) void k_f_partition(FArgs a) {
   static_assert(kFPartThreads == 256, "4 waves per block");
@@ -1262,6 +1372,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
   __shared__ int sh[MAXT * 4];
   __shared__ int s_wl[MAXT][ITERS][kFPartThreads / 64];
   __shared__ int s_wv[MAXT][ITERS][kFPartThreads / 64];
+  __shared__ int s_list[kFPartThreads], s_nlist;  // (FLookbackSlow)
   const FState* stp = a.st;
   if (stp->done) return;
   const int k = stp->k, T = stp->total_tiles;
@@ -1270,29 +1381,8 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
   FStamp(a, rnd, kFStampPart, 0);
   const int G = static_cast<int>(gridDim.x);
   const int t = threadIdx.x;
-  // this block's tiles: base + j * stride for base + j * stride < lim (j < MAXT in registers,
-  // the rest one by one). Ticketed: the contiguous range of the block's dispatch ticket.
-  int base = static_cast<int>(blockIdx.x), stride = G, lim = T;
-  if (a.part_contig) {
-    // contiguous ranges of ceil(T / G) tiles in block order (the work in the lowest blocks, which
-    // the dispatcher starts first): a block only waits on tiles of LOWER blocks, which the
-    // in-order dispatch started before it (no co-residency needed, and no ticket atomic: one
-    // shared ticket address serialised ~256 device-scope atomics at every launch)
-    const int per = (T + G - 1) / G;
-    base = static_cast<int>(blockIdx.x) * per;
-    lim = min(T, base + per);
-    stride = 1;
-  } else if (a.part_ticket != nullptr) {
-    __shared__ int s_vid;
-    if (t == 0) s_vid = static_cast<int>(atomicAdd(a.part_ticket, 1u));
-    __syncthreads();
-    const int per = (T + G - 1) / G;
-    base = s_vid * per;
-    stride = 1;
-    lim = min(T, base + per);
-  }
-  if (base >= lim) return;
-  const int bid = base;
+  const int bid = static_cast<int>(blockIdx.x), stride = G, lim = T;
+  if (bid >= lim) return;
   // the round's expansions (dword-parallel copy) and their categorical sets
   constexpr int kXWords = static_cast<int>(sizeof(FExp) / 4);
   for (int i = t; i < k * kXWords; i += blockDim.x) {
@@ -1311,20 +1401,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
     }
     return lo;
   };
-  // split predicate of expansion e (GoLeft of split_scan.h, categorical set read from LDS)
-  auto go_left = [&](int e, uint32_t gb) {
-    const FExp& x = s_x[e];
-    const uint32_t b = DecodeBin(x.offset, x.num_bin, x.mfb, gb);
-    if (x.is_cat) {
-      const uint32_t wd = b >> 5;
-      return wd < static_cast<uint32_t>(kMaxCatWords) && ((s_bits[e][wd] >> (b & 31u)) & 1u);
-    }
-    if ((x.missing == 1 && b == static_cast<uint32_t>(x.default_bin)) ||
-        (x.missing == 2 && b == static_cast<uint32_t>(x.num_bin - 1))) {
-      return x.default_left != 0;
-    }
-    return b <= static_cast<uint32_t>(x.thr);
-  };
+  auto go_left = [&](int e, uint32_t gb) { return FGoLeft(s_x[e], s_bits[e], gb); };
   FStamp(a, rnd, kFStampPart, 1);
   const int lane = t & 63, w = t >> 6;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1392,13 +1469,21 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
   FStamp(a, rnd, kFStampPart, 2);
   // ---- register tiles: look-back sums of all of them in one round, then one ballot barrier
   int lb[MAXT];
+  bool miss = false;
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
     lb[j] = 0;
     if (ex[j] < 0) continue;
-    lb[j] = FThreadCounts(a, s_x[ex[j]].tile0, bid + j * stride, epoch);
+    lb[j] = FThreadCounts(a, s_x[ex[j]].tile0, bid + j * stride, epoch, &miss);
   }
   BlockSumMulti<MAXT>(lb, sh);
+  if (__syncthreads_or(miss ? 1 : 0)) {
+    // a predecessor's block has not published within the poll bound (not resident): count here
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      if (ex[j] >= 0) lb[j] = FLookbackSlow(a, s_x[ex[j]], s_bits[ex[j]], s_x[ex[j]].tile0, bid + j * stride, epoch, sh, s_list, &s_nlist);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
 #pragma unroll
@@ -1422,19 +1507,6 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
     int lbase = lb[j];
     int rbase = tt * kTile - lbase;
     int* out = a.idx[x.dst_buf] + x.start;
-    // carried (g, h): the source's (contiguous in the parent's list, or by row at the root / bag)
-    float2 gv[ITERS];
-    float2* gout = nullptr;
-    if (a.carry_gh) {
-      gout = a.ghb[x.dst_buf] + x.start;
-      const float2* gsrc = x.src_buf >= 0 ? a.ghb[x.src_buf] : nullptr;
-      const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
-#pragma unroll
-      for (int i = 0; i < ITERS; ++i) {
-        const int r = rows[j][i];
-        gv[i] = r < 0 ? make_float2(0.f, 0.f) : (gsrc != nullptr ? gsrc[x.start + tt * kTile + t + i * kFPartThreads] : gh[r]);
-      }
-    }
 #pragma unroll
     for (int i = 0; i < ITERS; ++i) {
       const bool valid = (vbits >> (j * ITERS + i)) & 1u;
@@ -1455,8 +1527,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
         int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
-        FStoreRow(a.part_nt, dst, rows[j][i]);
-        if (gout != nullptr) gout[dst - out] = gv[i];
+        *dst = rows[j][i];
       }
       lbase += tl;
       rbase += tv - tl;
@@ -1467,8 +1538,10 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
   for (int tile = bid + MAXT * stride; tile < lim; tile += stride) {
     const int e = find(tile);
     const FExp& x = s_x[e];
-    int lcur[1] = {FThreadCounts(a, x.tile0, tile, epoch)};
+    bool miss1 = false;
+    int lcur[1] = {FThreadCounts(a, x.tile0, tile, epoch, &miss1)};
     BlockSumMulti<1>(lcur, sh);
+    if (__syncthreads_or(miss1 ? 1 : 0)) lcur[0] = FLookbackSlow(a, x, s_bits[e], x.tile0, tile, epoch, sh, s_list, &s_nlist);
     const int tt = tile - x.tile0;
     int lbase = lcur[0];
     int rbase = tt * kTile - lbase;
@@ -1495,18 +1568,6 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
     }
     __syncthreads();
     int* out = a.idx[x.dst_buf] + x.start;
-    float2 gv[ITERS];
-    float2* gout = nullptr;
-    if (a.carry_gh) {
-      gout = a.ghb[x.dst_buf] + x.start;
-      const float2* gsrc = x.src_buf >= 0 ? a.ghb[x.src_buf] : nullptr;
-      const float2* gh = a.gh + static_cast<size_t>(a.tp->cls) * a.N;
-#pragma unroll
-      for (int i = 0; i < ITERS; ++i) {
-        const int r = rr[i];
-        gv[i] = r < 0 ? make_float2(0.f, 0.f) : (gsrc != nullptr ? gsrc[x.start + pos0 + i * kFPartThreads] : gh[r]);
-      }
-    }
 #pragma unroll
     for (int i = 0; i < ITERS; ++i) {
       const bool valid = (vb1 >> i) & 1u;
@@ -1527,8 +1588,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
         const int rl = pl + __popcll(ml & lt_mask);
         const int rv = pv + __popcll(mv & lt_mask);
         int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
-        FStoreRow(a.part_nt, dst, rr[i]);
-        if (gout != nullptr) gout[dst - out] = gv[i];
+        *dst = rr[i];
       }
       lbase += tl;
       rbase += tv - tl;
@@ -2553,7 +2613,6 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       ns_.total_tiles = 0;
     }
     *a.st = ns_;
-    if (a.part_ticket != nullptr) *a.part_ticket = 0u;  // (the next round's partition tickets)
   }
 #pragma unroll
   for (int j = 0; j < kSelPairs; ++j) {
@@ -3098,7 +3157,7 @@ void LaunchFrontierInit(const FArgs& a, hipStream_t s) {
 template <int THREADS>
 void LaunchHistT(const FArgs& a, size_t lds, hipStream_t s) {
   // working blocks <= max(hist_grid, ceil(hist_grid / 2) + ke): see the chunking in k_f_hist
-  const dim3 grid(std::max(a.hist_grid, a.hist_grid / 2 + a.hist_grid % 2 + a.kmax), a.num_tiles);
+  const dim3 grid(FrontierHistRows(a.hist_grid, a.kmax), a.num_tiles);
   if (a.hist_nib) {
     // 4-bit rows (every group <= 16 bins, one LDS tile)
     if (a.quant && a.qsub > 0) k_f_hist<0, 3, THREADS><<<grid, THREADS, lds, s>>>(a);
@@ -3121,9 +3180,19 @@ void LaunchHistT(const FArgs& a, size_t lds, hipStream_t s) {
   HIP_CHECK(hipGetLastError());
 }
 
+// the histograms' slab rows: one per block of k_f_hist's grid
+int FrontierHistRows(int hist_grid, int kmax) { return std::max(hist_grid, hist_grid / 2 + hist_grid % 2 + kmax); }
+
 void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
   if (a.hist_threads == 1024) LaunchHistT<1024>(a, lds, s);
   else LaunchHistT<512>(a, lds, s);
+  // the partial rows' reduction (same MODE precedence as the histogram: quantized levels, then
+  // gpu_use_dp's 64-bit pairs, then the fixed-point packed words)
+  const int grid = std::max(1, std::min(a.red_grid, 4096));
+  if (a.quant) k_f_reduce<2><<<grid, kRedThreads, 0, s>>>(a);
+  else if (a.use_dp) k_f_reduce<1><<<grid, kRedThreads, 0, s>>>(a);
+  else k_f_reduce<0><<<grid, kRedThreads, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
 }
 
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
