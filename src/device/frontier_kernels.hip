@@ -263,19 +263,25 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
 // hist_grid below the CU count every working block gets a CU of its own (256 + k blocks doubled
 // some CUs' work and the round waited on them: A/B at 10M, 330 it/s vs 363 it/s). Many expansions
 // over a small grid (wide data, many LDS tiles) still get >= hist_grid / 2 row-balanced chunks.
-__device__ __forceinline__ void FHistChunks(const FArgs& a, int k, int* cnt, int* hb, int* hs, int* nb, int* inc) {
+// (the record fields are loaded by FHistChunkLoad before the round state is known: one round of
+// independent loads, then FHistChunks masks them by the round's expansion count)
+struct FChunkSrc {
+  int cnt, buf, start;
+};
+__device__ __forceinline__ FChunkSrc FHistChunkLoad(const FArgs& a) {
+  FChunkSrc c{0, -1, 0};
   const int t = threadIdx.x;
-  *cnt = 0;
-  *hb = -1;
-  *hs = 0;
-  if (t < k && t >= a.e_lo && t < a.e_hi) {
+  if (t < kFrontierKmax) {
     const FExp& x = a.exps[t];
-    if (!x.skip) {
-      *cnt = x.h_count;
-      *hb = x.h_buf;
-      *hs = x.h_start;
-    }
+    c.cnt = x.skip ? 0 : x.h_count;
+    c.buf = x.h_buf;
+    c.start = x.h_start;
   }
+  return c;
+}
+__device__ __forceinline__ void FHistChunks(const FArgs& a, int k, const FChunkSrc& src, int* cnt, int* nb, int* inc) {
+  const int t = threadIdx.x;
+  *cnt = t < k && t >= a.e_lo && t < a.e_hi ? src.cnt : 0;
   const int total = WaveSum(*cnt);
   const int ke = WaveSum(*cnt > 0 ? 1 : 0);
   const int slots = max(max(1, a.hist_grid / 2), a.hist_grid - ke);
@@ -289,14 +295,22 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   extern __shared__ __align__(8) unsigned char lds_raw[];
   __shared__ int s_e, s_rb, s_re, s_buf, s_start;
   const FState* sp = a.st;
+  const int t = threadIdx.x;
+  // one round of independent loads before the first wait: the round state, every expansion's
+  // chunking fields, the tile, the first group starts, the fixed-point scale inputs
+  const FChunkSrc csrc = FHistChunkLoad(a);
+  const HistTile tile = a.tiles[blockIdx.y];
+  const int ng0 = tile.g1 - tile.g0;
+  const int gst0 = t < ng0 ? a.gstart[tile.g0 + t] : 0;
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
   if (sp->done) return;
   const int k = sp->k;
-  const int t = threadIdx.x;
   const int rnd = sp->round;
   FStamp(a, rnd, kFStampHist, 0);
   if (t < 64) {
-    int cnt, hb, hs, nb, inc;
-    FHistChunks(a, k, &cnt, &hb, &hs, &nb, &inc);
+    int cnt, nb, inc;
+    FHistChunks(a, k, csrc, &cnt, &nb, &inc);
     const int bx = static_cast<int>(blockIdx.x);
     const bool mine = nb > 0 && bx >= inc - nb && bx < inc;
     const unsigned long long m = __ballot(mine);
@@ -306,8 +320,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       s_e = t;
       s_rb = j * chunk;
       s_re = min(cnt, (j + 1) * chunk);
-      s_buf = hb;
-      s_start = hs;
+      s_buf = csrc.buf;
+      s_start = csrc.start;
     }
     if (t == 0 && m == 0ull) s_e = -1;
   }
@@ -316,13 +330,10 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   if (e < 0) return;
   FStampMax(a, rnd, kFStampHist, 4);  // (latest start of a working block)
   const int rb = s_rb, re = s_re, buf = s_buf, start = s_start;
-  const HistTile tile = a.tiles[blockIdx.y];
   // accumulator words per bin: 1 when quantized level sums are packed g32|h32 (qpack: the
   // expansion's rows are compact, so a data-parallel all-reduce moves half the bytes), else 2
   const int pw = a.quant && a.qpack ? 1 : 2;
   unsigned long long* acc = a.acc + static_cast<size_t>(e) * pw * a.TB;
-  int EG, EH;
-  GlobalScaleExp(a, &EG, &EH);
   const double dsg = ldexp(1.0, EG), dsh = ldexp(1.0, EH);
   if (a.ltot != nullptr && blockIdx.y == 0) {
     // voting: the smaller child's LOCAL (sum g, sum h) at the global fixed-point scale (integer
@@ -351,7 +362,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   if (tile.direct) {
     // groups too wide for LDS: each row's fixed-point value straight into the accumulator
     int* gst = reinterpret_cast<int*>(lds_raw);
-    for (int g = tile.g0 + t; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g];
+    for (int g = t; g < ng0; g += blockDim.x) gst[g] = g == t ? gst0 : a.gstart[tile.g0 + g];
     __syncthreads();
     const int tpr = tile.d1 - tile.d0;
     const int rpi = blockDim.x / tpr;
@@ -414,7 +425,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   if (MODE == 3) {
     for (int i = t; i < tile.nbins; i += blockDim.x) hist32[i] = 0u;
   }
-  for (int g = tile.g0 + t; g < tile.g1; g += blockDim.x) gst[g - tile.g0] = a.gstart[g] - tile.bin0;
+  for (int g = t; g < ng0; g += blockDim.x) gst[g] = (g == t ? gst0 : a.gstart[tile.g0 + g]) - tile.bin0;
   __syncthreads();
   FStamp(a, rnd, kFStampHist, 1);
   if (MODE == 3) {
@@ -481,40 +492,50 @@ template <int MODE>
 __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   __shared__ int s_nb[kFrontierKmax], s_b0[kFrontierKmax], s_w0[kFrontierKmax + 1];
   __shared__ int s_tc[kRedMaxTiles + 1];  // chunk prefix over the LDS tiles (direct tiles: none)
+  __shared__ int s_wc[kRedThreads / 64];
   const FState* sp = a.st;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // one round of independent loads: state, expansion chunking fields, this thread's tile
+  const FChunkSrc csrc = FHistChunkLoad(a);
+  int tch = 0;  // bin chunks of tile t
+  if (t < a.num_tiles) {
+    const HistTile ty = a.tiles[t];
+    tch = ty.direct ? 0 : (ty.nbins + kRedThreads - 1) / kRedThreads;
+  }
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
   if (sp->done) return;
   const int k = sp->k;
-  const int t = threadIdx.x;
-  const int rnd = sp->round;
+  // chunk prefix over the tiles (block scan; num_tiles <= kRedThreads)
+  const int tinc = WaveInclusiveScan(tch);
+  if (lane == 63) s_wc[wv] = tinc;
+  __syncthreads();
+  int woff = 0;
+  for (int q = 0; q < wv; ++q) woff += s_wc[q];
+  if (t < a.num_tiles) s_tc[t] = woff + tinc - tch;
+  if (t == 0) {
+    int tot = 0;
+    for (int q = 0; q < kRedThreads / 64; ++q) tot += s_wc[q];
+    s_tc[a.num_tiles] = tot;
+  }
   if (t < 64) {
-    int cnt, hb, hs, nb, inc;
-    FHistChunks(a, k, &cnt, &hb, &hs, &nb, &inc);
+    int cnt, nb, inc;
+    FHistChunks(a, k, csrc, &cnt, &nb, &inc);
     if (t < kFrontierKmax) {
       s_nb[t] = nb;
       s_b0[t] = inc - nb;
     }
     // work items per expansion: bin chunks x row groups (prefix over the expansions)
-    int nch = 0;
-    for (int y = 0; y < a.num_tiles; ++y) nch += a.tiles[y].direct ? 0 : (a.tiles[y].nbins + kRedThreads - 1) / kRedThreads;
+    const int nch = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
     const int items = ((nb + kRedRows - 1) / kRedRows) * nch;
     const int winc = WaveInclusiveScan(items);
     if (t < kFrontierKmax) s_w0[t + 1] = winc;
     if (t == 0) s_w0[0] = 0;
   }
-  if (t == 64) {
-    int c = 0;
-    for (int y = 0; y < a.num_tiles && y < kRedMaxTiles; ++y) {
-      s_tc[y] = c;
-      c += a.tiles[y].direct ? 0 : (a.tiles[y].nbins + kRedThreads - 1) / kRedThreads;
-    }
-    s_tc[min(a.num_tiles, kRedMaxTiles)] = c;
-  }
   __syncthreads();
-  const int nch = s_tc[min(a.num_tiles, kRedMaxTiles)];
+  const int nch = s_tc[a.num_tiles];
   const int W = s_w0[k];
   if (W == 0 || nch == 0) return;
-  int EG, EH;
-  GlobalScaleExp(a, &EG, &EH);
   const int pw = a.quant && a.qpack ? 1 : 2;  // accumulator words per bin (see k_f_hist)
   constexpr int sw = MODE == 1 ? 2 : 1;       // slab words per bin
   for (int w = blockIdx.x; w < W; w += gridDim.x) {
@@ -578,7 +599,6 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
       if (pw == 2 && h) atomicAdd(&out[1], static_cast<unsigned long long>(h));
     }
   }
-  (void)rnd;
 }
 
 // ---------------------------------------------------------------------------
@@ -602,14 +622,22 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   __shared__ SplitKey s_key[2];
   SplitInfo* s_out = reinterpret_cast<SplitInfo*>(s_out_raw);
   const FState* stp = a.st;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int e0 = a.e_lo, F = a.F;
+  // the first item's expansion and feature records load with the round state (one round of
+  // independent loads before the first wait; later items load their own)
+  const int e_pre = min(e0 + static_cast<int>(blockIdx.x) / F, kFrontierKmax - 1);
+  const int f_pre = static_cast<int>(blockIdx.x) % F;
+  const int pre_skip = a.exps[e_pre].skip, pre_cs = a.exps[e_pre].smaller, pre_cl = a.exps[e_pre].larger,
+            pre_p = a.exps[e_pre].parent;
+  const DevFeature fi_pre = a.feat[f_pre];
+  int EG, EH;
+  GlobalScaleExp(a, &EG, &EH);
   if (stp->done) return;
-  const int e0 = a.e_lo, e1 = min(stp->k, a.e_hi), F = a.F;
+  const int e1 = min(stp->k, a.e_hi);
   const int total = max(0, e1 - e0) * F;
   const int rnd = stp->round;
   FStamp(a, rnd, kFStampScan, 0);
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  int EG, EH;
-  GlobalScaleExp(a, &EG, &EH);
   double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
   if (a.quant) QuantScales(a, &inv_g, &inv_h);
   const bool qpack = a.quant && a.qpack;
@@ -621,11 +649,14 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   __shared__ int s_last;
   for (int item = blockIdx.x; item < total; item += gridDim.x) {
     const int e = e0 + item / F, f = item - (e - e0) * F;
-    const FExp& xr = a.exps[e];
-    if (xr.skip) {
+    const bool first = item == static_cast<int>(blockIdx.x);
+    const int x_skip = first ? pre_skip : a.exps[e].skip;
+    const int x_cs = first ? pre_cs : a.exps[e].smaller, x_cl = first ? pre_cl : a.exps[e].larger;
+    const int x_p = first ? pre_p : a.exps[e].parent;
+    if (x_skip) {
       // (scan_best: the children of a skipped expansion get empty records, once)
       if (scan_best && f == 0 && t < 2) {
-        const int c = t == 0 ? xr.smaller : xr.larger;
+        const int c = t == 0 ? x_cs : x_cl;
         if (c >= 0) {
           a.best[c].Reset();
           SplitKey kz;
@@ -642,8 +673,8 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       }
       continue;
     }
-    const int cs = xr.smaller, cl = xr.larger, p = xr.parent;
-    const DevFeature fi = a.feat[f];
+    const int cs = x_cs, cl = x_cl, p = x_p;
+    const DevFeature fi = first ? fi_pre : a.feat[f];
     const int nbin = fi.num_bin;
     const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
     const size_t pw = qpack ? 1 : 2;  // accumulator words per bin (see k_f_hist)
