@@ -221,6 +221,10 @@ def _transport(device_name: str, args) -> str:
         return "xgmi (in-kernel IPC exchange)"
     if "host-staged" in device_name or args.dp_host_transport:
         return "host-staged (rehearsal)"
+    if "owner reduce-scatter" in device_name:
+        return "rccl reduce-scatter by feature owner + best-split all-gather"
+    if "all-reduce" in device_name:
+        return "rccl all-reduce"
     return "rccl"
 
 

@@ -404,7 +404,7 @@ std::vector<double> GBDT::EvalTraining(const Metric* m, const double** score) {
   }
   // ranking / AUC metrics: sorted on the device, only their sums come back
   RankMetricSpec rs;
-  if (allow && device_mode_ && num_tree_per_iteration_ == 1 && m->DeviceRankSpec(&rs)) {
+  if (allow && device_mode_ && num_tree_per_iteration_ == 1 && DeviceMetricsAllowed() && m->DeviceRankSpec(&rs)) {
     std::vector<double> raw;
     if (learner_->DeviceEvalRank(-1, rs, 0, &raw)) return m->FinishRank(raw);
   }

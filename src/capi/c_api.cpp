@@ -8,6 +8,7 @@
 
 #include <omp.h>
 
+#include <algorithm>
 #include <cstring>
 #include <functional>
 #include <fstream>
@@ -912,11 +913,15 @@ int LGBM_BoosterPredictForFile(BoosterHandle handle, const char* data_filename, 
       double lab = 0.0;
       parser->ParseOneLine(line.c_str(), &rows.rows.back(), &lab);
       labels.push_back(static_cast<float>(lab));
-      for (const auto& kv : rows.rows.back()) {
-        if (kv.first < 0 || kv.first >= nf) {
-          Log::Fatal("The custom parser produced feature index %d, but the model has %d features", kv.first, nf);
-        }
+      // a negative index is a parser bug; an index past the model's features (a column the
+      // training data never had) is dropped, as the reference's CopyToPredictBuffer
+      // (predictor.hpp:259) ignores it under predict_disable_shape_check
+      auto& r = rows.rows.back();
+      for (const auto& kv : r) {
+        if (kv.first < 0) Log::Fatal("The custom parser produced feature index %d", kv.first);
       }
+      r.erase(std::remove_if(r.begin(), r.end(), [nf](const auto& kv) { return kv.first >= nf; }),
+              r.end());
     }
     rows.ncol = nf;
   } else {

@@ -327,9 +327,12 @@ class DeviceTreeLearner : public TreeLearner {
     if (!owner_scan_ && !voting_) return;
     const char* e = std::getenv("LGAP_DP_TRANSPORT");
     const std::string want = e ? e : "auto";
-    if (want != "auto" && want != "xgmi" && want != "collective") Log::Fatal("LGAP_DP_TRANSPORT=%s: expected auto|xgmi|collective", want.c_str());
-    // the data-parallel frontier engine exchanges through all-reduces (no owner buffers)
-    if (want == "collective" || P_ > kMaxXRanks || (frontier_ && want == "auto")) return;
+    if (want != "auto" && want != "xgmi" && want != "collective" && want != "allreduce") {
+      Log::Fatal("LGAP_DP_TRANSPORT=%s: expected auto|xgmi|collective|allreduce", want.c_str());
+    }
+    // the data-parallel frontier engine exchanges through collectives (no xGMI owner buffers):
+    // owner reduce-scatter (auto / collective) or the per-round all-reduce (allreduce)
+    if (want == "collective" || want == "allreduce" || P_ > kMaxXRanks || (frontier_ && want == "auto")) return;
     const size_t es = use_dp_ ? sizeof(double) : sizeof(float);
     ArenaLayout lay;
     x_off_hist_ = static_cast<int>(lay.Add<char>(static_cast<size_t>(P_) * 2 * bbin_ * es));
@@ -418,7 +421,12 @@ class DeviceTreeLearner : public TreeLearner {
     std::string m = mode_ == DevParallel::kFeature ? "feature-parallel"
                                                    : (voting_ ? "voting-parallel" : "data-parallel");
     m += ", " + std::to_string(P_) + " ranks, ";
-    if (frontier_) return m + "frontier engine, " + (HostStagedDP() ? "host-staged collectives" : "RCCL all-reduce per round");
+    if (frontier_) {
+      const std::string via = HostStagedDP() ? "host-staged collectives" : "RCCL";
+      if (fowner_) return m + "frontier engine, owner reduce-scatter + best-split all-gather per round (" + via + ")";
+      if (ffeature_ || fvoting_) return m + "frontier engine, " + via;
+      return m + "frontier engine, all-reduce per round (" + via + ")";
+    }
     if (transport_ == 2) return m + "xGMI in-kernel exchange";
     if (HostStagedDP()) return m + "host-staged collectives";
     return m + "RCCL reduce-scatter/all-gather";
@@ -1217,8 +1225,10 @@ class DeviceTreeLearner : public TreeLearner {
     auto& slot = rank_states_[spec.owner];
     if (!slot || slot->kind != spec.kind || slot->n != n || slot->nq != spec.num_queries || slot->host_label != host_label ||
         slot->host_qb != static_cast<const void*>(spec.query_boundaries) || slot->ks != spec.eval_at) {
-      slot = std::make_unique<RankEvalState>();
-      RankEvalState& r = *slot;
+      // built aside and installed only when complete: a rejected spec leaves no half-built
+      // state behind a matching key
+      auto fresh = std::make_unique<RankEvalState>();
+      RankEvalState& r = *fresh;
       r.kind = spec.kind;
       r.n = n;
       r.nq = spec.num_queries;
@@ -1249,6 +1259,9 @@ class DeviceTreeLearner : public TreeLearner {
         r.scratch.Resize(AucScratchBytes(n));
       }
       r.out.Resize(RankMetricSpec::kMaxEvalAt);
+      // the uploads' host sources (qb, disc, ...) are locals of this scope
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      slot = std::move(fresh);
     }
     RankEvalState& r = *slot;
     int nout = 2;
@@ -1567,6 +1580,22 @@ class DeviceTreeLearner : public TreeLearner {
     return mode_ == DevParallel::kData && data_parallel_ && owner_scan_ && distributed_ && !voting_ &&
            (CommExists() || HostStagedDP());
   }
+  // Owner-computes data-parallel rounds (the default data-parallel frontier): the round's
+  // fixed-point accumulators are REDUCE-SCATTERED by feature-group ownership (SetupOwnership:
+  // contiguous, bin-balanced group ranges), so each rank receives only the summed bins of its own
+  // features (half the bytes of the all-reduce) and scans only those (1/P of the scan work); each
+  // child's best over the owned features is all-gathered and the best over ranks becomes the
+  // child's candidate (the feature-parallel exchange, k_f_pair_best / k_f_pair_merge); every rank
+  // then selects redundantly from identical candidates. Reference:
+  // data_parallel_tree_learner.cpp:284-297 (ReduceScatter of the smaller leaf's histograms by
+  // feature ownership), :305-450 (owner scans, SyncUpGlobalBestSplit). Raw per-feature candidates
+  // (CEGB penalties, by-node sampling) and forced splits need every feature's scan on every rank:
+  // they keep the all-reduce, as does LGAP_DP_TRANSPORT=allreduce (A/B).
+  bool FrontierOwner() const {
+    if (!FrontierDP() || RawCands() || !config_->forcedsplits_filename.empty() || config_->extra_trees) return false;
+    const char* t = std::getenv("LGAP_DP_TRANSPORT");
+    return !(t != nullptr && std::strcmp(t, "allreduce") == 0);
+  }
   // Voting-parallel frontier (PV-Tree per round): the local pass of every expansion's children,
   // one all-gather of the round's top-k vote records, the election, one exact integer
   // all-reduce of only the elected features' rows, and the global pass over them; every rank
@@ -1752,19 +1781,33 @@ class DeviceTreeLearner : public TreeLearner {
       fhslab_stride_ = static_cast<size_t>(TB_) * (use_dp_ && !QuantHist() ? 2 : 1);
       fhslab_.Resize(static_cast<size_t>(rows) * fhslab_stride_);
       fhmeta_.Resize(rows);
+
       if (num_tiles_ > 256) Log::Fatal("frontier histograms: %d LDS tiles (at most 256)", num_tiles_);
     }
-    fscan_ticket_.Resize(K);
-    fscan_ticket_.Zero(stream_);  // (the last item of each expansion re-zeroes its ticket)
-    fscan_cpos_.Resize(2 * K);
     ffeature_ = FrontierFeature();
-    if (ffeature_) {
+    fowner_ = FrontierOwner();
+    if (ffeature_ || fowner_) {
       std::vector<uint8_t> own(F_, 0);
+      std::vector<int> list;
       for (int f : h_own_feat_) {
-        if (f >= 0) own[f] = 1;
+        if (f >= 0) {
+          own[f] = 1;
+          list.push_back(f);
+        }
       }
       ffowned_.Upload(own, stream_);
+      fown_n_ = static_cast<int>(list.size());
+      fown_list_.Resize(std::max<size_t>(1, list.size()));
+      if (!list.empty()) fown_list_.Upload(list.data(), list.size(), stream_);
       ffpb_.Resize(static_cast<size_t>(P_) * 2 * K);
+    }
+    if (fowner_) {
+      // send layout [rank][kmax][widest owner's bins] (>= the plain layout), receive [kmax][own bins]
+      fown_b0_.Upload(h_bin_lo_, stream_);
+      const size_t send = static_cast<size_t>(P_) * K * bbin_ * 2;
+      if (facc_.size() < send) facc_.Resize(send);
+      facc_.Zero(stream_);
+      facc_recv_.Resize(static_cast<size_t>(K) * bbin_ * 2);
     }
     fvoting_ = FrontierVoting();
     if (fvoting_) {
@@ -1780,13 +1823,10 @@ class DeviceTreeLearner : public TreeLearner {
     ftile_pub_.Resize(ftile_cap_);
     ftile_pub_.Zero(stream_);
     for (int i = 3; i < kFrontierIdx; ++i) idx_[i].Resize(std::max(N_, 1));
-    // partition grid: the resident blocks (a look-back past a block that is not resident counts
-    // the tile itself, k_f_partition / FAwait)
-    int per_cu = FrontierPartitionBlocksPerCU(part_iters_);
-    int cap = 8;  // A/B knob LGAP_FPART_BPC (10M rows: 4 -> 327.9, 6 -> 334.7, 8 -> 337.3 it/s)
-    if (const char* e = std::getenv("LGAP_FPART_BPC")) cap = std::max(1, std::atoi(e));
-    per_cu = std::max(1, std::min(cap, per_cu - 1));
-    fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
+    // partition grid: one block per tile of the tile capacity, so every tile of any round is in a
+    // block's registers (blocks beyond the resident ones start as earlier ones finish; a block only
+    // waits on lower blocks' tiles)
+    fpart_grid_ = std::max(1, ftile_cap_);
     fscan_lds_ = FrontierScanLds(max_bin_, has_cat_ ? max_cat_bin_ : 1);
     FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
@@ -1814,8 +1854,11 @@ class DeviceTreeLearner : public TreeLearner {
     {
       const char* tn = std::getenv("LGAP_FRONTIER_TUNE");
       stune_ = SpecTuner();
-      stune_.on = !distributed_ && L_ >= 128 && std::getenv("LGAP_FRONTIER_ALPHA") == nullptr &&
-                  std::getenv("LGAP_FRONTIER_ADAPT") == nullptr && !(tn != nullptr && tn[0] == '0');
+      // (not with raw CEGB candidates or forced splits: there the select's replay of speculated
+      // expansions depends on what was speculated, and the budget must not follow wall-clock time)
+      stune_.on = !distributed_ && L_ >= 128 && !RawCands() && fnum_forced_ == 0 &&
+                  std::getenv("LGAP_FRONTIER_ALPHA") == nullptr && std::getenv("LGAP_FRONTIER_ADAPT") == nullptr &&
+                  !(tn != nullptr && tn[0] == '0');
     }
     if (std::getenv("LGAP_FSTAMPS")) {
       fstamps_.Resize(256 * 4 * kFStampSlots);
@@ -1869,7 +1912,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.acc = reinterpret_cast<unsigned long long*>(facc_.get());
     a.hslab = fhslab_.get();
     a.hslab_stride = fhslab_stride_;
-    a.hmeta = reinterpret_cast<int2*>(fhmeta_.get());
+    a.hmeta = fhmeta_.get();
     a.red_grid = 2 * num_cu_;
     a.ghmax = ghmax_.get();
     a.sum_mult = distributed_ && !ffeature_ ? std::max(1, P_) : 1;  // (max-reduced local sums)
@@ -1929,14 +1972,7 @@ class DeviceTreeLearner : public TreeLearner {
       a.scan_wave = fits && !has_cat_ && (v == 1 || (v < 0 && F_ >= 64)) ? 1 : 0;  // (numerical features only)
       // (block scan grid cap: 512 blocks loop over a large round's items instead of 4096
       // mostly-idle blocks being dispatched every round; A/B 10M 2.850 vs 2.875, 1.25M 1.331 vs 1.341)
-      const char* g = std::getenv("LGAP_SCAN_GRID");
-      a.scan_grid = g != nullptr ? std::max(0, std::atoi(g)) : 512;
-      const char* sr = std::getenv("LGAP_SEL_BLOCK_RANK");
-      a.sel_block_rank = sr != nullptr && sr[0] == '1' ? 1 : 0;
-      const char* lr = std::getenv("LGAP_SEL_LDS_REPLAY");
-      a.sel_lds_replay = lr != nullptr && lr[0] == '1' ? 1 : 0;
-      const char* sl = std::getenv("LGAP_SEL_EARLY");
-      a.sel_early = sl != nullptr && sl[0] == '1' ? 1 : 0;
+      a.scan_grid = 512;
     }
     a.e_lo = 0;
     a.e_hi = kFrontierKmax;
@@ -1960,7 +1996,6 @@ class DeviceTreeLearner : public TreeLearner {
         a.npath = fnpath_.get();
       }
     }
-    a.sel_bitonic = std::getenv("LGAP_SEL_BITONIC") != nullptr ? 1 : 0;
     a.spec_cap = fspec_cap_;
     a.policy = fpolicy_;
     a.stamps = fstamps_.size() ? fstamps_.get() : nullptr;
@@ -1974,21 +2009,23 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.sp = MakeArgs().sp;
     a.bynode = use_bynode_ ? bynode_.get() : nullptr;
-    {
-      // the per-child best in the scan (completion ticket); the select keeps it for raw CEGB /
-      // by-node candidates and for the voting / feature exchanges, which rewrite the candidates
-      // (opt-in, LGAP_SCAN_BEST=1: A/B at 10M and 1.25M 2-5% slower than the select's phase A)
-      const char* e = std::getenv("LGAP_SCAN_BEST");
-      a.scan_best = e != nullptr && e[0] == '1' && !RawCands() && !fvoting_ && !ffeature_ ? 1 : 0;
-      a.scan_ticket = fscan_ticket_.get();
-      a.scan_cpos = fscan_cpos_.get();
-    }
     a.xrng = config_->extra_trees ? rng_.get() : nullptr;
-    if (ffeature_) {
+    if (ffeature_ || fowner_) {
       a.fowned = ffowned_.get();
       a.fpb = ffpb_.get();
       a.vote_P = P_;
       a.vote_rank = rank_;
+      a.fown_list = fown_list_.get();
+      a.fown_n = fown_n_;
+    }
+    a.xkb = fkmax_;
+    if (fowner_) {
+      a.own = 1;
+      a.own_P = P_;
+      a.own_rank = rank_;
+      a.own_w = bbin_;
+      a.own_b0 = fown_b0_.get();
+      a.acc_recv = facc_recv_.get();
     }
     if (fvoting_) {
       a.voting = 1;
@@ -2017,7 +2054,7 @@ class DeviceTreeLearner : public TreeLearner {
   // Data-parallel frontier: sum the round's accumulators of the first `kb` expansions over
   // the ranks (the rest are zero on every rank).
   void FrontierExchange(int kb) {
-    if (!distributed_ || fvoting_) return;
+    if (!distributed_ || fvoting_ || fowner_) return;
     AllreduceSumU64(reinterpret_cast<unsigned long long*>(facc_.get()),
                     static_cast<size_t>(std::max(1, std::min(kb, fkmax_))) * AccWordsPerBin() * TB_, stream_);
   }
@@ -2064,6 +2101,20 @@ class DeviceTreeLearner : public TreeLearner {
     return static_cast<size_t>(max_bin_) * 2 * sizeof(double) + static_cast<size_t>(cat_p2_) * (2 * sizeof(int) + sizeof(double));
   }
 
+  // Owner-computes data-parallel round (FrontierOwner): histograms + reduce into the per-rank
+  // chunks, the reduce-scatter, owner-only scans, the per-child bests exchanged. `kb` = the
+  // round's expansion bound (the chunk stride the reduce and the reduce-scatter agree on).
+  void FrontierOwnerRound(const FArgs& fa, int kb) {
+    FArgs fr = fa;
+    fr.xkb = std::max(1, std::min(kb, fkmax_));
+    LaunchFrontierHist(fr, FrontierHistLds(), stream_);
+    if (fr.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fr, stream_);
+    ReduceScatterSumU64(reinterpret_cast<unsigned long long*>(facc_.get()), facc_recv_.get(),
+                        static_cast<size_t>(fr.xkb) * bbin_ * AccWordsPerBin(), stream_);
+    LaunchFrontierScan(fr, fscan_lds_, stream_);
+    FrontierFeatureExchange(fr);
+  }
+
   // Feature parallel: this rank's per-child bests all-gathered, the best over ranks kept.
   void FrontierFeatureExchange(const FArgs& fa) {
     LaunchFrontierPairBest(fa, stream_);
@@ -2073,6 +2124,11 @@ class DeviceTreeLearner : public TreeLearner {
 
   void EnqueueFrontierRound(const FArgs& fa, int kb) {
     LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    if (fowner_) {
+      FrontierOwnerRound(fa, kb);
+      LaunchFrontierSelect(fa, stream_);
+      return;
+    }
     if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
     if (ffeature_) {
       LaunchFrontierHist(fa, FrontierHistLds(), stream_);
@@ -2131,12 +2187,16 @@ class DeviceTreeLearner : public TreeLearner {
         AllreduceSumF64(reinterpret_cast<double*>(flsum_), 2, stream_);
         AllreduceMaxU32(ghmax_.get(), 4, stream_);
       }
-      LaunchFrontierHist(fa, FrontierHistLds(), stream_);
-      if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
-      FrontierExchange(1);
-      LaunchFrontierScan(fa, fscan_lds_, stream_);
-      if (fvoting_) FrontierVoteExchange(fa, 1);
-      if (ffeature_) FrontierFeatureExchange(fa);
+      if (fowner_) {
+        FrontierOwnerRound(fa, 1);
+      } else {
+        LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+        if (fa.cegb_lazy != nullptr) LaunchFrontierLazyCounts(fa, stream_);
+        FrontierExchange(1);
+        LaunchFrontierScan(fa, fscan_lds_, stream_);
+        if (fvoting_) FrontierVoteExchange(fa, 1);
+        if (ffeature_) FrontierFeatureExchange(fa);
+      }
       LaunchFrontierSelect(fa, stream_);
     }
     for (int r = 0; r < rounds; ++r) {
@@ -2895,7 +2955,9 @@ class DeviceTreeLearner : public TreeLearner {
       const int v = std::atoi(e);
       if (v == 4 || v == 8 || v == 16) return v;
     }
-    return N_ >= 8000000 ? 8 : 4;
+    // (frontier A/B: 4096-row tiles at 10M, 1024-row tiles at 1.25M; the sequential chain's
+    // partition uses the same rows per thread)
+    return N_ >= 8000000 ? 16 : 4;
   }
 
   typedef void (*PartitionFn)(Args);
@@ -3776,11 +3838,9 @@ class DeviceTreeLearner : public TreeLearner {
   int fC_ = 0, fkmax_ = 1, fpart_tile_ = 2048, ftile_cap_ = 1, fpart_grid_ = 1, fspec_cap_ = 0, fpolicy_ = 1;
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
-  DevBuf<unsigned> fscan_ticket_;
   // score update fused with the next pointwise gradients (DeviceAddTreeToScore)
   const ObjectiveFunction* fused_obj_ = nullptr;  // pointwise objective of the last gradient pass
   bool fused_grad_ready_ = false, fuse_pending_ = false, fuse_done_ = false;
-  DevBuf<int> fscan_cpos_;
   // linear-leaf trees (FitLinearLeaves / TraverseLinear)
   bool linear_ = false, lin_has_nan_ = false;
   DevBuf<float> lin_raw_;
@@ -3791,6 +3851,10 @@ class DeviceTreeLearner : public TreeLearner {
   const LinearLeaves* lin_pending_ = nullptr;  // set around TraverseLinear's traversal
   // feature-parallel frontier (FrontierFeature)
   bool ffeature_ = false;
+  bool fowner_ = false;  // data-parallel owner-computes rounds (FrontierOwner)
+  int fown_n_ = 0;
+  DevBuf<int> fown_list_, fown_b0_;
+  DevBuf<unsigned long long> facc_recv_;
   DevBuf<uint8_t> ffowned_;
   DevBuf<FPairBest> ffpb_;
   // voting-parallel frontier (FrontierVoting)
@@ -3819,7 +3883,8 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<unsigned long long> facc_;
   DevBuf<unsigned long long> fhslab_;  // k_f_hist partial rows
   size_t fhslab_stride_ = 0;
-  DevBuf<long long> fhmeta_;           // (int2 per row)
+  DevBuf<long long> fhmeta_;           // per row: bh << 32 | bg
+
   DevBuf<unsigned long long> ftile_pub_;
   std::map<int, hipGraphExec_t> fgraphs_;
   hipGraphExec_t fcont_ = nullptr;

@@ -174,10 +174,20 @@ struct FArgs {
   // histograms
   double* slots;              // [C][2 TB] per-node histograms (stored bins, fp64)
   unsigned long long* acc;    // [kmax][2 TB] per-expansion fixed-point accumulators (zero between rounds)
-  unsigned long long* hslab;  // [hist rows][hslab_stride] k_f_hist's per-block partial histograms (raw LDS words)
+  unsigned long long* hslab;  // [hist rows][hslab_stride] k_f_hist's per-block histograms (raw LDS words)
   size_t hslab_stride;        // words per slab row (TB, x2 for gpu_use_dp)
-  int2* hmeta;                // [hist rows] MODE 0: the block's fixed-point exponents (bg, bh)
+  long long* hmeta;           // [hist rows] MODE 0: the block's fixed-point exponents (bh << 32 | bg)
   int red_grid;               // k_f_reduce blocks
+  // data-parallel owner-computes (reference data_parallel_tree_learner.cpp:284-297): the reduce
+  // writes the round's accumulators as P per-rank chunks [xkb][own_w] (rank r's chunk = the bins of
+  // the groups it owns, [own_b0[r], own_b0[r + 1])), a reduce-scatter sums each chunk into its
+  // owner's acc_recv, the owner scans only its features and the per-child bests are all-gathered
+  int own, own_P, own_rank, own_w;
+  const int* own_b0;           // [P + 1]
+  unsigned long long* acc_recv;  // [xkb][own_w] x (1 or 2 words)
+  int xkb;                     // expansions the round's exchange covers (the chunk stride)
+  const int* fown_list;        // owned features (scan items; null: every feature)
+  int fown_n;
   const unsigned* ghmax;      // float bits of max|g|, max|h|, sum|g|, sum|h| over the root rows
   int sum_mult;               // ranks whose root rows the global sums span (row-sharded DP / voting), else 1
   int sum_bound;              // use the sum|value| bounds (LGAP_FIXED_SUMBOUND=0: max only, the round-3 scale)
@@ -200,21 +210,12 @@ struct FArgs {
   // partition look-back
   unsigned long long* tile_pub;
   unsigned* bar;
-  // per-child best split in the scan (scan_best = 1): the last item of an expansion to finish
-  // (completion ticket) takes the arg-max over the features for both children and writes
-  // best / key, so the select's phase A only reads the winners' candidate positions
-  int scan_best;
-  unsigned* scan_ticket;  // [kmax] finished items per expansion (reset by the last one)
-  int* scan_cpos;         // [2 kmax] winning candidate position per child pair, -1: none
   int part_selfcount;  // test hook: every look-back counts its predecessor tiles itself (FTileCount)
   int hist_min_rows, hist_grid;
   int hist_threads;  // 512 or 1024 threads per histogram block
   int hist_il;       // bank-interleaved LDS histograms (tiles with pad = their largest group's bins)
   int scan_wave;     // k_f_scan_w (one wave per (expansion, feature)) instead of one block per item
   int scan_grid;     // cap of the block scan's grid (A/B knob LGAP_SCAN_GRID; 0: 4096)
-  int sel_block_rank;  // the select's block-wide rank / scan for <= 64 alive nodes too (A/B knob)
-  int sel_lds_replay;  // A/B knob (LGAP_SEL_LDS_REPLAY=1): the replay's leaf keys in LDS (else registers when L <= 64)
-  int sel_early;       // A/B knob (LGAP_SEL_EARLY=1): phase A's candidate loads in the image's load round
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)
   int part_tile;  // rows per partition tile (256 x rows per thread)
   int max_depth, use_monotone;
@@ -281,7 +282,6 @@ struct FArgs {
   // every earlier split of the sequential order is committed.
   unsigned* xrng;
   struct FPairBest* fpb;  // [P][kmax][2] per-child best of each rank, all-gathered
-  int sel_bitonic;  // A/B knob (LGAP_SEL_BITONIC=1): the select's bitonic sort instead of the rank sort
   SplitParams sp;
 };
 
@@ -321,7 +321,7 @@ void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
 // final leaves' rows marked for the features on their paths
 void LaunchFrontierLazyCounts(const FArgs& a, hipStream_t s);
 void LaunchFrontierLazyMark(const FArgs& a, hipStream_t s);
-void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s);
+void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s);  // one block per tile
 // voting parallel: local top-k per child (after the local-pass k_f_scan), election and
 // packing of the elected features' local rows (after the vote all-gather), global pass over
 // the summed rows (after their all-reduce)
@@ -332,8 +332,6 @@ void LaunchFrontierVoteScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
 // over ranks -> the candidate table (after it)
 void LaunchFrontierPairBest(const FArgs& a, hipStream_t s);
 void LaunchFrontierPairMerge(const FArgs& a, hipStream_t s);
-// resident 256-thread partition blocks per CU (the grid size; the look-back does not need them resident)
-int FrontierPartitionBlocksPerCU(int iters);
 // one-time kernel attributes (dynamic LDS above 64 KiB)
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width);
 // dynamic LDS of k_f_select (CEGB coupled penalties add F bytes of used flags after it)

@@ -81,6 +81,16 @@ __device__ __forceinline__ void QuantScales(const FArgs& a, double* gs, double* 
   *hs = a.qconst ? mh : mh / a.qbins;
 }
 
+// Word offset of (expansion e, bin b) in the round's accumulators: [e][TB] x pw words, or --
+// data-parallel owner-computes -- [owner rank][xkb][own_w] x pw words, the layout the
+// reduce-scatter splits by rank (rank r owns the groups of bins [own_b0[r], own_b0[r + 1]))
+__device__ __forceinline__ size_t FAccAt(const FArgs& a, int e, int b, int pw) {
+  if (!a.own) return (static_cast<size_t>(e) * a.TB + b) * pw;
+  int r = 0;
+  while (r + 1 < a.own_P && a.own_b0[r + 1] <= b) ++r;
+  return ((static_cast<size_t>(r) * a.xkb + e) * a.own_w + (b - a.own_b0[r])) * pw;
+}
+
 // ---------------------------------------------------------------------------
 // tree setup: the root node, the root "round" (one pseudo-expansion whose smaller child
 // is the root), the committed-leaf table and the node states.
@@ -333,7 +343,6 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   // accumulator words per bin: 1 when quantized level sums are packed g32|h32 (qpack: the
   // expansion's rows are compact, so a data-parallel all-reduce moves half the bytes), else 2
   const int pw = a.quant && a.qpack ? 1 : 2;
-  unsigned long long* acc = a.acc + static_cast<size_t>(e) * pw * a.TB;
   const double dsg = ldexp(1.0, EG), dsh = ldexp(1.0, EH);
   if (a.ltot != nullptr && blockIdx.y == 0) {
     // voting: the smaller child's LOCAL (sum g, sum h) at the global fixed-point scale (integer
@@ -361,6 +370,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   }
   if (tile.direct) {
     // groups too wide for LDS: each row's fixed-point value straight into the accumulator
+    if (a.own && e >= a.xkb) return;  // (never: the round's bound covers its expansions)
     int* gst = reinterpret_cast<int*>(lds_raw);
     for (int g = t; g < ng0; g += blockDim.x) gst[g] = g == t ? gst0 : a.gstart[tile.g0 + g];
     __syncthreads();
@@ -392,9 +402,9 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
                                     : ((word >> (16 * kk)) & 0xFFFFu);
         const int g = dw * per + kk;
         if (b != 0u && g < tile.g1) {
-          const int o = gst[g - tile.g0] + static_cast<int>(b);
-          if (qg) atomicAdd(&acc[pw * o], qg);
-          if (qh) atomicAdd(&acc[pw * o + 1], qh);
+          const size_t o = FAccAt(a, e, gst[g - tile.g0] + static_cast<int>(b), pw);
+          if (qg) atomicAdd(&a.acc[o], qg);
+          if (qh) atomicAdd(&a.acc[o + 1], qh);
         }
       }
     }
@@ -469,7 +479,10 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   unsigned long long* prow = a.hslab + static_cast<size_t>(blockIdx.x) * a.hslab_stride + static_cast<size_t>(sw) * tile.bin0;
   const unsigned long long* src = il_gp > 0 ? packed : hist;
   for (int j = t; j < sw * tile.nbins; j += blockDim.x) prow[j] = src[j];
-  if (MODE == 0 && t == 0) a.hmeta[blockIdx.x] = make_int2(bg, bh);  // (every tile's block: the same value)
+  if (MODE == 0 && t == 0) {
+    a.hmeta[blockIdx.x] = static_cast<long long>((static_cast<unsigned long long>(static_cast<unsigned>(bh)) << 32) |
+                                                 static_cast<unsigned>(bg));  // (every tile's block: the same value)
+  }
   FStamp(a, rnd, kFStampHist, 3);
   FStampMax(a, rnd, kFStampHist, 6);  // (latest block done issuing its partial)
   FStampEnd(a, rnd, kFStampHist);
@@ -541,6 +554,7 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   for (int w = blockIdx.x; w < W; w += gridDim.x) {
     int e = 0;
     while (e + 1 < k && s_w0[e + 1] <= w) ++e;
+    if (a.own && e >= a.xkb) continue;  // (never: the round's bound covers its expansions)
     const int r = w - s_w0[e];
     const int grp = r / nch, ch = r - grp * nch;
     int y = 0;
@@ -563,7 +577,8 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
 #pragma unroll
       for (int j = 0; j < kRedRows; ++j) {
         if (r0 + j >= r1) continue;
-        const int2 m = a.hmeta[r0 + j];  // (uniform: scalar loads)
+        const long long mm = a.hmeta[r0 + j];  // (uniform: scalar loads; bh << 32 | bg)
+        const int2 m = make_int2(static_cast<int>(mm & 0xFFFFFFFFll), static_cast<int>(mm >> 32));
         const int hv = static_cast<int>(static_cast<unsigned int>(x0[j] & 0xFFFFFFFFull));
         const long long gv = static_cast<long long>(x0[j] - static_cast<unsigned long long>(static_cast<long long>(hv))) >> 32;
         // exact shift of the block's fixed-point sums to the global scale (2^EG >= 2^bg: see
@@ -589,7 +604,7 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
         h += static_cast<long long>(hv);
       }
     }
-    unsigned long long* out = a.acc + static_cast<size_t>(e) * pw * a.TB + static_cast<size_t>(pw) * (tile.bin0 + i);
+    unsigned long long* out = a.acc + FAccAt(a, e, tile.bin0 + i, pw);
     if (nb <= kRedRows) {
       // the expansion's only row group: the accumulator is zero here (the scan re-zeroes it)
       if (g) out[0] = static_cast<unsigned long long>(g);
@@ -614,7 +629,6 @@ template <bool EXT>
 __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   const bool voting = EXT && a.voting != 0;
   const bool xtrees = EXT && a.xrng != nullptr;
-  const bool scan_best = EXT && a.scan_best != 0;
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_skip, s_splp, s_rand[2], s_xn[2];
   __shared__ double s_xh[2];
@@ -626,8 +640,12 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   const int e0 = a.e_lo, F = a.F;
   // the first item's expansion and feature records load with the round state (one round of
   // independent loads before the first wait; later items load their own)
-  const int e_pre = min(e0 + static_cast<int>(blockIdx.x) / F, kFrontierKmax - 1);
-  const int f_pre = static_cast<int>(blockIdx.x) % F;
+  // items: (expansion, feature) over every feature, or (owner-computes / feature parallel) over
+  // this rank's owned features only (fown_list)
+  const int NF = a.fown_list != nullptr ? a.fown_n : F;
+  const int e_pre = min(e0 + static_cast<int>(blockIdx.x) / max(NF, 1), kFrontierKmax - 1);
+  const int f_pre = a.fown_list != nullptr ? (NF > 0 ? a.fown_list[static_cast<int>(blockIdx.x) % NF] : 0)
+                                           : static_cast<int>(blockIdx.x) % F;
   const int pre_skip = a.exps[e_pre].skip, pre_cs = a.exps[e_pre].smaller, pre_cl = a.exps[e_pre].larger,
             pre_p = a.exps[e_pre].parent;
   const DevFeature fi_pre = a.feat[f_pre];
@@ -635,9 +653,24 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   GlobalScaleExp(a, &EG, &EH);
   if (stp->done) return;
   const int e1 = min(stp->k, a.e_hi);
-  const int total = max(0, e1 - e0) * F;
+  const int total = max(0, e1 - e0) * NF;
   const int rnd = stp->round;
   FStamp(a, rnd, kFStampScan, 0);
+  if (!voting && blockIdx.x == 0 && t == 0 && e0 == 0 && pre_p < 0) {
+    // the root round: the root's output (whatever features this rank scans: owner-computes and
+    // feature-parallel ranks scan only their own; voting: k_f_elect writes the global one)
+    const double2 rs = a.lsum[0];
+    SplitParams p0 = a.sp;
+    p0.path_smooth = 0.0;
+    a.lout[0] = LeafOutputRaw(rs.x, rs.y, p0, a.nodes[0].gcount, 0.0);
+  }
+  if (a.own) {
+    // the reduce-scatter consumed the send layout: zero it for the next round's k_f_reduce
+    const size_t nz = static_cast<size_t>(a.own_P) * a.xkb * a.own_w * (a.quant && a.qpack ? 1 : 2);
+    for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nz; i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+      a.acc[i] = 0ull;
+    }
+  }
   double inv_g = ldexp(1.0, -EG), inv_h = ldexp(1.0, -EH);
   if (a.quant) QuantScales(a, &inv_g, &inv_h);
   const bool qpack = a.quant && a.qpack;
@@ -648,29 +681,13 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   double* ckey = reinterpret_cast<double*>(order + 2 * a.cat_p2);
   __shared__ int s_last;
   for (int item = blockIdx.x; item < total; item += gridDim.x) {
-    const int e = e0 + item / F, f = item - (e - e0) * F;
+    const int e = e0 + item / NF, fi_ = item - (e - e0) * NF;
+    const int f = a.fown_list != nullptr ? a.fown_list[fi_] : fi_;
     const bool first = item == static_cast<int>(blockIdx.x);
     const int x_skip = first ? pre_skip : a.exps[e].skip;
     const int x_cs = first ? pre_cs : a.exps[e].smaller, x_cl = first ? pre_cl : a.exps[e].larger;
     const int x_p = first ? pre_p : a.exps[e].parent;
     if (x_skip) {
-      // (scan_best: the children of a skipped expansion get empty records, once)
-      if (scan_best && f == 0 && t < 2) {
-        const int c = t == 0 ? x_cs : x_cl;
-        if (c >= 0) {
-          a.best[c].Reset();
-          SplitKey kz;
-          kz.gain = kMinScore;
-          kz.feature = -1;
-          kz.threshold = 0;
-          kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
-          kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
-          kz.pos = -1;
-          kz.pad2 = 0;
-          a.key[c] = kz;
-        }
-        a.scan_cpos[2 * e + t] = -1;
-      }
       continue;
     }
     const int cs = x_cs, cl = x_cl, p = x_p;
@@ -678,7 +695,10 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     const int nbin = fi.num_bin;
     const size_t v0 = 2 * static_cast<size_t>(fi.hist_offset);
     const size_t pw = qpack ? 1 : 2;  // accumulator words per bin (see k_f_hist)
-    unsigned long long* acc = a.acc + static_cast<size_t>(e) * pw * a.TB + pw * static_cast<size_t>(fi.hist_offset);
+    // (owner-computes: this rank's summed chunk of the reduce-scatter)
+    unsigned long long* acc =
+        a.own ? a.acc_recv + (static_cast<size_t>(e) * a.own_w + (fi.hist_offset - a.own_b0[a.own_rank])) * pw
+              : a.acc + static_cast<size_t>(e) * pw * a.TB + pw * static_cast<size_t>(fi.hist_offset);
     const double* gp = (p >= 0 && cl >= 0) ? a.slots + static_cast<size_t>(p) * TB2 + v0 : nullptr;
     double* gs = a.slots + static_cast<size_t>(cs) * TB2 + v0;
     double* gl = cl >= 0 ? a.slots + static_cast<size_t>(cl) * TB2 + v0 : nullptr;
@@ -813,7 +833,6 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
           SplitParams p0 = spp;
           p0.path_smooth = 0.0;
           po = LeafOutputRaw(sg, sh, p0, n, 0.0);
-          if (f == 0 && lane == 0 && !voting) a.lout[0] = po;  // (voting: the global root output, k_f_elect)
         } else {
           po = __shfl(pre_out, 0, kWave);
         }
@@ -858,11 +877,6 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       } else if (lane == 0) {
         // feature not tried: the children inherit the parent's flag
         a.spl[static_cast<size_t>(my) * F + f] = static_cast<uint8_t>(s_splp);
-        if (p < 0 && f == 0 && !voting) {
-          SplitParams p0 = a.sp;
-          p0.path_smooth = 0.0;
-          a.lout[0] = LeafOutputRaw(sg, sh, p0, n, 0.0);
-        }
       }
       if (lane == 0 && pre_fidx >= 0 && a.forced[pre_fidx].feature == f) {
         // the node's forced split at its threshold (host ForceSplits / reference
@@ -952,56 +966,6 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     }
     __syncthreads();  // LDS reused by the next item
     if (item == static_cast<int>(blockIdx.x)) FStamp(a, rnd, kFStampScan, 3);
-    if (scan_best) {
-      // completion ticket of expansion e: the last of its F items picks both children's best
-      if (t == 0) {
-        __threadfence();  // this item's candidates, visible device-wide before the ticket
-        const unsigned old = atomicAdd(&a.scan_ticket[e], 1u);
-        s_last = old == static_cast<unsigned>(F - 1) ? 1 : 0;
-      }
-      __syncthreads();
-      if (s_last) {
-        __threadfence();
-        if (w < 2) {
-          const int c = w == 0 ? cs : cl;
-          const size_t q = static_cast<size_t>(e) * 2 + w;
-          double bg = kMinScore;
-          int bf = 0x7fffffff, bp = -1;
-          if (c >= 0) {
-            for (int ff = lane; ff < F; ff += 64) {
-              const SplitKey& kk = a.ckey[q * F + ff];
-              if (kk.feature < 0) continue;
-              if (kk.gain > bg || (kk.gain == bg && kk.feature < bf)) {
-                bg = kk.gain;
-                bf = kk.feature;
-                bp = ff;
-              }
-            }
-          }
-          const int src = WaveArgBestLane(bg, bf, 0);
-          bp = ReadLane(bp, src);
-          constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-          constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
-          if (c >= 0 && bp >= 0) {
-            const size_t pos = q * F + bp;
-            for (int i = lane; i < kInfoWords + kKeyWords; i += 64) {
-              if (i < kInfoWords) {
-                reinterpret_cast<uint32_t*>(a.best + c)[i] = reinterpret_cast<const uint32_t*>(a.cinfo + pos)[i];
-              } else {
-                reinterpret_cast<uint32_t*>(a.key + c)[i - kInfoWords] = reinterpret_cast<const uint32_t*>(a.ckey + pos)[i - kInfoWords];
-              }
-            }
-          } else if (c >= 0 && lane == 0) {
-            a.best[c].Reset();
-            a.key[c].gain = kMinScore;
-            a.key[c].feature = -1;
-            a.key[c].pos = -1;
-          }
-          if (lane == 0) a.scan_cpos[q] = (c >= 0 && bp >= 0) ? static_cast<int>(q * F + bp) : -1;
-        }
-        if (t == 0) a.scan_ticket[e] = 0u;
-      }
-    }
   }
   FStampEnd(a, rnd, kFStampScan);
 }
@@ -1198,17 +1162,20 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
 // ---------------------------------------------------------------------------
 // k_f_partition: stable 2-way partition of every expanded parent (reference
 // data_partition.hpp:101 / cuda_data_partition.cu:290-937, as one launch).
-// Tiles of all expansions are numbered globally ([tile0_e, tile0_e + ntiles_e) for
-// expansion e). Every block first counts all of its tiles and publishes each count as a
-// 64-bit {epoch, count} granule, then scatters its tiles: a tile waits only for the
-// counts of the earlier tiles OF ITS EXPANSION (decoupled look-back); lefts go to the
-// front of the parent's range in order, rights fill it from the end. The block that
-// scatters an expansion's last tile knows its total left count and writes the two
+// Tiles of all expansions are numbered globally ([tile0_e, tile0_e + ntiles_e) for expansion e);
+// block b owns the MAXT contiguous tiles [b MAXT, b MAXT + MAXT). A block counts its tiles,
+// publishes each count, finds the exclusive left-count prefix of its first tile by a decoupled
+// look-back over the earlier tiles OF ITS EXPANSION, publishes its tiles' inclusive prefixes and
+// scatters: lefts go to the front of the parent's range in order, rights fill it from the end.
+// The block that scatters an expansion's last tile knows its total left count and writes the two
 // children (post-split bookkeeping of serial_tree_learner.cpp:766-922).
 
-__device__ __forceinline__ void FPublish(unsigned long long* p, unsigned epoch, int cnt) {
-  const unsigned long long v = (static_cast<unsigned long long>(epoch) << 32) | static_cast<unsigned>(cnt);
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// tile granule {epoch:32 | inclusive:1 | value:31}: a tile's left count, or (inclusive) the left
+// count of its expansion's tiles up to and including it
+__device__ __forceinline__ void FPublish(unsigned long long* p, unsigned epoch, int v, bool incl) {
+  const unsigned long long w = (static_cast<unsigned long long>(epoch) << 32) | (incl ? 0x80000000ull : 0ull) |
+                               static_cast<unsigned>(v);
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // split predicate of expansion x on group bin gb (GoLeft of split_scan.h, categorical set in `bits`)
@@ -1225,79 +1192,102 @@ __device__ __forceinline__ bool FGoLeft(const FExp& x, const uint32_t* bits, uin
   return b <= static_cast<uint32_t>(x.thr);
 }
 
-// Look-back without co-residency. Strided tile ownership lets block b wait on tiles of blocks
-// dispatched after it; when those are not resident (a kernel on another stream, an RCCL kernel
-// waiting on peers, another process holding CUs) a bounded poll gives up, and the block counts
-// the missing predecessor tiles itself (FLookbackSlow) -- the same pure function of the tile's rows
-// its owner evaluates -- and publishes the identical values. Nothing is paid while the owners run.
 constexpr unsigned kLookbackSpins = 2048;  // s_sleep(1) polls (~100 us) before a tile is counted here
 
-// this thread's share of the published counts of tiles [i0, i1): the loads of a batch are issued
-// together (one round trip per batch of 8), only tiles not yet published are re-polled; a tile
-// still unpublished after the bound sets *miss (the caller's block then takes FLookbackSlow)
-__device__ __forceinline__ int FThreadCounts(const FArgs& a, int i0, int i1, unsigned epoch, bool* miss) {
-  constexpr int B = 8;
-  const int stride = static_cast<int>(blockDim.x);
-  int s = 0;
-  for (int base = i0 + static_cast<int>(threadIdx.x); base < i1; base += B * stride) {
-    unsigned long long v[B];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const int i = base + b * stride;
-      v[b] = i < i1 ? __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : (static_cast<unsigned long long>(epoch) << 32);
-    }
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const int i = base + b * stride;
-      unsigned spins = 0;
-      while (static_cast<unsigned>(v[b] >> 32) != epoch && spins < kLookbackSpins) {
-        __builtin_amdgcn_s_sleep(1);
-        v[b] = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ++spins;
-      }
-      if (static_cast<unsigned>(v[b] >> 32) == epoch) s += static_cast<int>(static_cast<unsigned>(v[b]));
-      else *miss = true;
-    }
-  }
-  if (a.part_selfcount) *miss = true;  // (test hook: every look-back through the slow path)
-  return s;
-}
+constexpr int kLookbackPer = 4;  // predecessors per thread and window (1,024 per window)
 
-// Sum of the left counts of tiles [i0, i1) of expansion x, block-cooperatively: published counts
-// read (not waited for), every unpublished tile counted by the whole block and published. The
-// rare path of the look-back (and every look-back under the part_selfcount test hook).
-__device__ int FLookbackSlow(const FArgs& a, const FExp& x, const uint32_t* bits, int i0, int i1, unsigned epoch,
-                             int* sh, int* s_list, int* s_nlist) {
+struct FLookbackLds {
+  int near, nmiss, list[256 * kLookbackPer], val[256 * kLookbackPer], red[4];
+};
+
+// Exclusive left-count prefix of tile i of expansion x (block-cooperative): windows of
+// kLookbackPer x blockDim predecessors, nearest first, their granules loaded in one round; a window
+// holding an inclusive granule ends the walk. Blocks own contiguous tiles, so a block only waits on
+// LOWER blocks. A predecessor still unpublished after the poll bound (its block not running:
+// nothing here assumes co-residency or dispatch order) is counted by this block -- the same pure
+// function of the tile's rows its owner evaluates -- and published (the identical value). The
+// part_selfcount test hook counts every predecessor here.
+__device__ int FLookback(const FArgs& a, const FExp& x, const uint32_t* bits, int i, unsigned epoch, FLookbackLds* L) {
   const int t = threadIdx.x;
-  int total = 0;
-  for (int b0 = i0; b0 < i1; b0 += blockDim.x) {
-    const int i = b0 + t;
-    int c = 0;
-    if (t == 0) *s_nlist = 0;
-    __syncthreads();
-    if (i < i1) {
-      const unsigned long long v = __hip_atomic_load(&a.tile_pub[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (static_cast<unsigned>(v >> 32) == epoch && !a.part_selfcount) c = static_cast<int>(static_cast<unsigned>(v));
-      else s_list[atomicAdd(s_nlist, 1)] = i;
+  const int nt = static_cast<int>(blockDim.x);
+  constexpr int kInf = 0x7fffffff;
+  int excl = 0;
+  for (int hi = i; hi > x.tile0;) {
+    const int lo = max(x.tile0, hi - kLookbackPer * nt);
+    // predecessor d = u * nt + t (0 = the nearest) is tile hi - 1 - d
+    unsigned long long v[kLookbackPer];
+    bool have[kLookbackPer];
+    if (t == 0) {
+      L->near = kInf;
+      L->nmiss = 0;
     }
-    total += BlockSumInt(c, sh);  // (its barriers also publish s_list / s_nlist)
-    const int nm = *s_nlist;
-    for (int m = 0; m < nm; ++m) {
-      const int tile = s_list[m];
-      const int p0 = (tile - x.tile0) * a.part_tile, p1 = min(x.count, p0 + a.part_tile);
-      int cc = 0;
-      for (int p = p0 + t; p < p1; p += blockDim.x) {
-        const int row = FRowAt(a, x.src_buf, x.start + p);
-        cc += FGoLeft(x, bits, FColBin(a, x.group, row)) ? 1 : 0;
+#pragma unroll
+    for (int u = 0; u < kLookbackPer; ++u) {
+      const int j = hi - 1 - (u * nt + t);
+      v[u] = j >= lo ? __hip_atomic_load(&a.tile_pub[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kLookbackPer; ++u) {
+      const int j = hi - 1 - (u * nt + t);
+      have[u] = false;
+      if (j < lo) continue;
+      for (unsigned spins = 0; static_cast<unsigned>(v[u] >> 32) != epoch && spins < kLookbackSpins; ++spins) {
+        __builtin_amdgcn_s_sleep(1);
+        v[u] = __hip_atomic_load(&a.tile_pub[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      cc = BlockSumInt(cc, sh);
-      if (t == 0) FPublish(&a.tile_pub[tile], epoch, cc);
-      total += cc;
+      have[u] = static_cast<unsigned>(v[u] >> 32) == epoch && !a.part_selfcount;
     }
-    __syncthreads();  // (s_list / s_nlist reused)
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kLookbackPer; ++u) {
+      const int j = hi - 1 - (u * nt + t);
+      if (j >= lo && !have[u]) L->list[atomicAdd(&L->nmiss, 1)] = j;
+    }
+    __syncthreads();
+    const int nm = L->nmiss;
+    if (nm > 0) {
+      // rare: count the unpublished predecessors with the whole block, one tile at a time
+      for (int m = 0; m < nm; ++m) {
+        const int tile = L->list[m];
+        const int p0 = (tile - x.tile0) * a.part_tile, p1 = min(x.count, p0 + a.part_tile);
+        int cc = 0;
+        for (int p = p0 + t; p < p1; p += nt) {
+          const int row = FRowAt(a, x.src_buf, x.start + p);
+          cc += FGoLeft(x, bits, FColBin(a, x.group, row)) ? 1 : 0;
+        }
+        cc = BlockSumInt(cc, L->red);
+        if (t == 0) {
+          L->val[hi - 1 - tile] = cc;
+          FPublish(&a.tile_pub[tile], epoch, cc, false);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kLookbackPer; ++u) {
+        const int j = hi - 1 - (u * nt + t);
+        if (j >= lo && !have[u]) {
+          v[u] = static_cast<unsigned long long>(static_cast<unsigned>(L->val[u * nt + t]));  // (an aggregate)
+          have[u] = true;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kLookbackPer; ++u) {
+      if (have[u] && (v[u] & 0x80000000ull) != 0ull) atomicMin(&L->near, u * nt + t);
+    }
+    __syncthreads();
+    const int near = L->near;
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < kLookbackPer; ++u) {
+      const int j = hi - 1 - (u * nt + t);
+      if (j >= lo && u * nt + t <= near) c += static_cast<int>(v[u] & 0x7fffffffull);
+    }
+    excl += BlockSumInt(c, L->red);
+    if (near != kInf) break;
+    hi = lo;
   }
-  return total;
+  return excl;
 }
 
 // children of expansion x (one thread)
@@ -1385,13 +1375,6 @@ __device__ __forceinline__ void BlockSumMulti(int* v, int* sh) {
   for (int m = 0; m < M; ++m) v[m] = sh[m * 4] + sh[m * 4 + 1] + sh[m * 4 + 2] + sh[m * 4 + 3];
 }
 
-// Block b owns tiles b + j * G (strided: concurrently running blocks stream neighbouring tiles).
-// The first MAXT of them live in registers for the whole launch: their loads are issued together
-// (row ids, then bins), their counts reduced in one block sum, their look-back sums loaded in one
-// round, their scatter ballots published in one LDS barrier, so a block pays a few memory round
-// trips instead of a few per tile. Tiles beyond MAXT (a grid smaller than the round's tiles /
-// MAXT) take the per-tile path. A look-back on a tile whose owner has not run yet counts that
-// tile itself (FAwait): the grid needs no co-residency.
 template <int ITERS, int MAXT>
 __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(ITERS == 8 ? 5 : 1))) void k_f_partition(FArgs a) {
   static_assert(kFPartThreads == 256, "4 waves per block");
@@ -1403,7 +1386,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
   __shared__ int sh[MAXT * 4];
   __shared__ int s_wl[MAXT][ITERS][kFPartThreads / 64];
   __shared__ int s_wv[MAXT][ITERS][kFPartThreads / 64];
-  __shared__ int s_list[kFPartThreads], s_nlist;  // (FLookbackSlow)
+  __shared__ FLookbackLds s_lb;
   const FState* stp = a.st;
   if (stp->done) return;
   const int k = stp->k, T = stp->total_tiles;
@@ -1412,8 +1395,7 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
   FStamp(a, rnd, kFStampPart, 0);
   const int G = static_cast<int>(gridDim.x);
   const int t = threadIdx.x;
-  const int bid = static_cast<int>(blockIdx.x), stride = G, lim = T;
-  if (bid >= lim) return;
+  if (static_cast<int>(blockIdx.x) * MAXT >= T) return;
   // the round's expansions (dword-parallel copy) and their categorical sets
   constexpr int kXWords = static_cast<int>(sizeof(FExp) / 4);
   for (int i = t; i < k * kXWords; i += blockDim.x) {
@@ -1436,196 +1418,120 @@ __global__ __launch_bounds__(kFPartThreads) __attribute__((amdgpu_waves_per_eu(I
   FStamp(a, rnd, kFStampPart, 1);
   const int lane = t & 63, w = t >> 6;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // ---- register tiles: counts
-  int ex[MAXT], rows[MAXT][ITERS];
-  unsigned lbits = 0u, vbits = 0u;  // bit j * ITERS + i: row valid / goes left
-#pragma unroll
-  for (int j = 0; j < MAXT; ++j) {
-    const int tile = bid + j * stride;
-    ex[j] = tile < lim ? find(tile) : -1;
-    const int e = ex[j] < 0 ? 0 : ex[j];
-    const FExp& x = s_x[e];
-    const int pos0 = (tile - x.tile0) * kTile + t;
-#pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const int pos = pos0 + i * kFPartThreads;
-      rows[j][i] = (ex[j] >= 0 && pos < x.count) ? FRowAt(a, x.src_buf, x.start + pos) : -1;
-    }
-  }
-  int cnt[MAXT];
-  {
-    uint32_t gb[MAXT][ITERS];
+  // passes of G * MAXT tiles (one pass whenever the grid covers the tile capacity, as the learner
+  // sizes it)
+  for (int bid = static_cast<int>(blockIdx.x) * MAXT; bid < T; bid += G * MAXT) {
+    // ---- counts of the block's tiles (loads issued together: row ids, then bins)
+    int ex[MAXT], rows[MAXT][ITERS];
+    unsigned lbits = 0u, vbits = 0u;  // bit j * ITERS + i: row valid / goes left
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
-      const int g = s_x[ex[j] < 0 ? 0 : ex[j]].group;
-#pragma unroll
-      for (int i = 0; i < ITERS; ++i) gb[j][i] = rows[j][i] >= 0 ? FColBin(a, g, rows[j][i]) : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < MAXT; ++j) {
-      cnt[j] = 0;
+      const int tile = bid + j;
+      ex[j] = tile < T ? find(tile) : -1;
+      const int e = ex[j] < 0 ? 0 : ex[j];
+      const FExp& x = s_x[e];
+      const int pos0 = (tile - x.tile0) * kTile + t;
 #pragma unroll
       for (int i = 0; i < ITERS; ++i) {
-        const bool valid = rows[j][i] >= 0;
-        const bool left = valid && go_left(ex[j], gb[j][i]);
-        vbits |= (valid ? 1u : 0u) << (j * ITERS + i);
-        lbits |= (left ? 1u : 0u) << (j * ITERS + i);
-        cnt[j] += left ? 1 : 0;
+        const int pos = pos0 + i * kFPartThreads;
+        rows[j][i] = (ex[j] >= 0 && pos < x.count) ? FRowAt(a, x.src_buf, x.start + pos) : -1;
       }
     }
-  }
-  BlockSumMulti<MAXT>(cnt, sh);
-  if (t == 0) {
+    int cnt[MAXT];
+    {
+      uint32_t gb[MAXT][ITERS];
 #pragma unroll
-    for (int j = 0; j < MAXT; ++j) {
-      if (ex[j] >= 0) FPublish(&a.tile_pub[bid + j * stride], epoch, cnt[j]);
-    }
-  }
-  // ---- tiles beyond MAXT: count and publish one by one
-  for (int tile = bid + MAXT * stride; tile < lim; tile += stride) {
-    const int e = find(tile);
-    const FExp& x = s_x[e];
-    const int pos0 = (tile - x.tile0) * kTile + t;
-    int c = 0;
+      for (int j = 0; j < MAXT; ++j) {
+        const int g = s_x[ex[j] < 0 ? 0 : ex[j]].group;
 #pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const int pos = pos0 + i * kFPartThreads;
-      const int row = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
-      c += (row >= 0 && go_left(e, FColBin(a, x.group, row))) ? 1 : 0;
-    }
-    int cc[1] = {c};
-    BlockSumMulti<1>(cc, sh);
-    if (t == 0) FPublish(&a.tile_pub[tile], epoch, cc[0]);
-  }
-  FStamp(a, rnd, kFStampPart, 2);
-  // ---- register tiles: look-back sums of all of them in one round, then one ballot barrier
-  int lb[MAXT];
-  bool miss = false;
-#pragma unroll
-  for (int j = 0; j < MAXT; ++j) {
-    lb[j] = 0;
-    if (ex[j] < 0) continue;
-    lb[j] = FThreadCounts(a, s_x[ex[j]].tile0, bid + j * stride, epoch, &miss);
-  }
-  BlockSumMulti<MAXT>(lb, sh);
-  if (__syncthreads_or(miss ? 1 : 0)) {
-    // a predecessor's block has not published within the poll bound (not resident): count here
-#pragma unroll
-    for (int j = 0; j < MAXT; ++j) {
-      if (ex[j] >= 0) lb[j] = FLookbackSlow(a, s_x[ex[j]], s_bits[ex[j]], s_x[ex[j]].tile0, bid + j * stride, epoch, sh, s_list, &s_nlist);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < MAXT; ++j) {
-#pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const unsigned long long ml = __ballot((lbits >> (j * ITERS + i)) & 1u);
-      const unsigned long long mv = __ballot((vbits >> (j * ITERS + i)) & 1u);
-      if (lane == 0) {
-        s_wl[j][i][w] = __popcll(ml);
-        s_wv[j][i][w] = __popcll(mv);
+        for (int i = 0; i < ITERS; ++i) gb[j][i] = rows[j][i] >= 0 ? FColBin(a, g, rows[j][i]) : 0u;
       }
-    }
-  }
-  __syncthreads();
 #pragma unroll
-  for (int j = 0; j < MAXT; ++j) {
-    if (ex[j] < 0) continue;
-    const int e = ex[j];
-    const FExp& x = s_x[e];
-    const int tile = bid + j * stride;
-    const int tt = tile - x.tile0;
-    int lbase = lb[j];
-    int rbase = tt * kTile - lbase;
-    int* out = a.idx[x.dst_buf] + x.start;
+      for (int j = 0; j < MAXT; ++j) {
+        cnt[j] = 0;
 #pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const bool valid = (vbits >> (j * ITERS + i)) & 1u;
-      const bool left = (lbits >> (j * ITERS + i)) & 1u;
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      int pl = 0, pv = 0, tl = 0, tv = 0;
-#pragma unroll
-      for (int q = 0; q < kFPartThreads / 64; ++q) {
-        if (q < w) {
-          pl += s_wl[j][i][q];
-          pv += s_wv[j][i][q];
+        for (int i = 0; i < ITERS; ++i) {
+          const bool valid = rows[j][i] >= 0;
+          const bool left = valid && go_left(ex[j], gb[j][i]);
+          vbits |= (valid ? 1u : 0u) << (j * ITERS + i);
+          lbits |= (left ? 1u : 0u) << (j * ITERS + i);
+          cnt[j] += left ? 1 : 0;
         }
-        tl += s_wl[j][i][q];
-        tv += s_wv[j][i][q];
       }
-      if (valid) {
-        const int rl = pl + __popcll(ml & lt_mask);
-        const int rv = pv + __popcll(mv & lt_mask);
-        int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
-        *dst = rows[j][i];
-      }
-      lbase += tl;
-      rbase += tv - tl;
     }
-    if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
-  }
-  // ---- tiles beyond MAXT: look-back and scatter one by one
-  for (int tile = bid + MAXT * stride; tile < lim; tile += stride) {
-    const int e = find(tile);
-    const FExp& x = s_x[e];
-    bool miss1 = false;
-    int lcur[1] = {FThreadCounts(a, x.tile0, tile, epoch, &miss1)};
-    BlockSumMulti<1>(lcur, sh);
-    if (__syncthreads_or(miss1 ? 1 : 0)) lcur[0] = FLookbackSlow(a, x, s_bits[e], x.tile0, tile, epoch, sh, s_list, &s_nlist);
-    const int tt = tile - x.tile0;
-    int lbase = lcur[0];
-    int rbase = tt * kTile - lbase;
-    int rr[ITERS];
-    unsigned lb1 = 0u, vb1 = 0u;
-    const int pos0 = tt * kTile + t;
+    BlockSumMulti<MAXT>(cnt, sh);
+    // aggregates first (a tile that starts its expansion publishes its count as inclusive)
+    if (t == 0) {
 #pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const int pos = pos0 + i * kFPartThreads;
-      rr[i] = pos < x.count ? FRowAt(a, x.src_buf, x.start + pos) : -1;
+      for (int j = 0; j < MAXT; ++j) {
+        if (ex[j] >= 0) FPublish(&a.tile_pub[bid + j], epoch, cnt[j], bid + j == s_x[ex[j]].tile0);
+      }
+    }
+    FStamp(a, rnd, kFStampPart, 2);
+    // ---- exclusive prefixes: a look-back for the block's first tile only (a later tile of the
+    // block continues its predecessor's expansion, or is the first tile of the next one)
+    int lb[MAXT];
+    lb[0] = ex[0] >= 0 && bid > s_x[ex[0]].tile0 ? FLookback(a, s_x[ex[0]], s_bits[ex[0]], bid, epoch, &s_lb) : 0;
+#pragma unroll
+    for (int j = 1; j < MAXT; ++j) lb[j] = ex[j] >= 0 && ex[j] == ex[j - 1] ? lb[j - 1] + cnt[j - 1] : 0;
+    if (t == 0) {
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        if (ex[j] >= 0 && bid + j > s_x[ex[j]].tile0) FPublish(&a.tile_pub[bid + j], epoch, lb[j] + cnt[j], true);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const bool valid = rr[i] >= 0;
-      const bool left = valid && go_left(e, FColBin(a, x.group, rr[i]));
-      vb1 |= (valid ? 1u : 0u) << i;
-      lb1 |= (left ? 1u : 0u) << i;
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      if (lane == 0) {
-        s_wl[0][i][w] = __popcll(ml);
-        s_wv[0][i][w] = __popcll(mv);
+    for (int j = 0; j < MAXT; ++j) {
+#pragma unroll
+      for (int i = 0; i < ITERS; ++i) {
+        const unsigned long long ml = __ballot((lbits >> (j * ITERS + i)) & 1u);
+        const unsigned long long mv = __ballot((vbits >> (j * ITERS + i)) & 1u);
+        if (lane == 0) {
+          s_wl[j][i][w] = __popcll(ml);
+          s_wv[j][i][w] = __popcll(mv);
+        }
       }
     }
     __syncthreads();
-    int* out = a.idx[x.dst_buf] + x.start;
+    // ---- scatter
 #pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const bool valid = (vb1 >> i) & 1u;
-      const bool left = (lb1 >> i) & 1u;
-      const unsigned long long ml = __ballot(left);
-      const unsigned long long mv = __ballot(valid);
-      int pl = 0, pv = 0, tl = 0, tv = 0;
+    for (int j = 0; j < MAXT; ++j) {
+      if (ex[j] < 0) continue;
+      const int e = ex[j];
+      const FExp& x = s_x[e];
+      const int tile = bid + j;
+      const int tt = tile - x.tile0;
+      int lbase = lb[j];
+      int rbase = tt * kTile - lbase;
+      int* out = a.idx[x.dst_buf] + x.start;
 #pragma unroll
-      for (int q = 0; q < kFPartThreads / 64; ++q) {
-        if (q < w) {
-          pl += s_wl[0][i][q];
-          pv += s_wv[0][i][q];
+      for (int i = 0; i < ITERS; ++i) {
+        const bool valid = (vbits >> (j * ITERS + i)) & 1u;
+        const bool left = (lbits >> (j * ITERS + i)) & 1u;
+        const unsigned long long ml = __ballot(left);
+        const unsigned long long mv = __ballot(valid);
+        int pl = 0, pv = 0, tl = 0, tv = 0;
+#pragma unroll
+        for (int q = 0; q < kFPartThreads / 64; ++q) {
+          if (q < w) {
+            pl += s_wl[j][i][q];
+            pv += s_wv[j][i][q];
+          }
+          tl += s_wl[j][i][q];
+          tv += s_wv[j][i][q];
         }
-        tl += s_wl[0][i][q];
-        tv += s_wv[0][i][q];
+        if (valid) {
+          const int rl = pl + __popcll(ml & lt_mask);
+          const int rv = pv + __popcll(mv & lt_mask);
+          int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
+          *dst = rows[j][i];
+        }
+        lbase += tl;
+        rbase += tv - tl;
       }
-      if (valid) {
-        const int rl = pl + __popcll(ml & lt_mask);
-        const int rv = pv + __popcll(mv & lt_mask);
-        int* dst = left ? out + lbase + rl : out + (x.count - 1 - (rbase + (rv - rl)));
-        *dst = rr[i];
-      }
-      lbase += tl;
-      rbase += tv - tl;
+      if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
     }
-    __syncthreads();
-    if (tt == x.ntiles - 1 && t == 0) FPostSplit(a, e, x, lbase);
+    __syncthreads();  // (LDS ballot counts reused by the next pass)
   }
   FStamp(a, rnd, kFStampPart, 3);
   FStampEnd(a, rnd, kFStampPart);
@@ -1742,53 +1648,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     s_pc[t] = c;
     s_cpos[t] = -1;
   }
-  // ---- A, loads (LGAP_SEL_EARLY=1). Without CEGB the candidate keys of this round's children
-  // can be read in the image's load round: the arg-max over a pair's features does not depend
-  // on its child, whose validity (from the expansion record, loaded alongside) is applied
-  // afterwards (A/B: 10M 2.905 vs 2.843 ms/iter, 1.25M 1.317 vs 1.310 -- opt-in)
   constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
   constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
   static_assert(kInfoWords + kKeyWords <= 64, "one record word per lane");
-  const bool early = !cegb && !a.scan_best && a.sel_early;
   const float spec_alpha = a.tp->spec_alpha;  // (phase D; loaded here, off its critical path)
-  double eg[kSelPairs];
-  int ef[kSelPairs], ep[kSelPairs], epc[kSelPairs];
-#pragma unroll
-  for (int j = 0; j < kSelPairs; ++j) {
-    eg[j] = kMinScore;
-    ef[j] = 0x7fffffff;
-    ep[j] = -1;
-    epc[j] = -1;
-  }
-  if (early) {
-#pragma unroll
-    for (int j = 0; j < kSelPairs; ++j) {
-      const int q = w + j * kSelWaves;
-      if (q < np) {
-        const FExp& x = a.exps[q >> 1];
-        const int ch = (q & 1) ? x.larger : x.smaller;
-        epc[j] = x.skip ? -2 - ch : ch;
-      }
-    }
-    for (int f0 = 0; f0 < F; f0 += 64) {
-      const int f = f0 + lane;
-#pragma unroll
-      for (int j = 0; j < kSelPairs; ++j) {
-        const int q = w + j * kSelWaves;
-        if (q < np && f < F) {
-          const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
-          const int kf = kk.feature;
-          const double g = kf < 0 ? kMinScore : kk.gain;
-          const int ff = kf < 0 ? 0x7fffffff : kf;
-          if (FBetter(g, ff, 0, eg[j], ef[j], 0)) {
-            eg[j] = g;
-            ef[j] = ff;
-            ep[j] = f;
-          }
-        }
-      }
-    }
-  }
   __syncthreads();
   FStamp(a, rnd, kFStampSel, 1);
   if (cegb && a.cegb_lazy != nullptr) {
@@ -1808,58 +1671,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     for (int i = t; i < kprev * F; i += blockDim.x) a.lazy_acc[i] = 0;
     __syncthreads();
   }
-  // ---- A. children of the last round: best over features (all pairs' keys in flight); with
-  // scan_best the scan's last item per expansion already did it (best / key written, in the
-  // image above): only the winners' candidate positions are read
-  // the winners' full records (SplitInfo + SplitKey, one word per lane) are loaded now and
-  // stored at the end of the launch: only later launches read best / key of this round's
-  // children (this one reads them through s_cpos from the candidate table)
-  uint32_t cw[kSelPairs];
-  int cdst[kSelPairs];
-#pragma unroll
-  for (int j = 0; j < kSelPairs; ++j) cdst[j] = -1;
-  if (a.scan_best && !cegb) {
-    for (int q = t; q < np; q += blockDim.x) {
-      const int pc = s_pc[q];
-      if (pc >= 0) s_cpos[pc - base] = a.scan_cpos[q];
-    }
-  } else if (early) {
-#pragma unroll
-    for (int j = 0; j < kSelPairs; ++j) {
-      const int q = w + j * kSelWaves;
-      if (q >= np) continue;
-      const int pc = epc[j];
-      if (pc == -1) continue;  // no child (root round's second pair)
-      const int c = pc >= 0 ? pc : -2 - pc;
-      const int src = WaveArgBestLane(eg[j], ef[j], 0);
-      const double g = ReadLane(eg[j], src);
-      const int ff = ReadLane(ef[j], src);
-      const int fpos = ReadLane(ep[j], src);
-      const bool valid = pc >= 0 && ff != 0x7fffffff && fpos >= 0;
-      const size_t pos = static_cast<size_t>(q) * F + (fpos >= 0 ? fpos : 0);
-      if (valid) {
-        cw[j] = lane < kInfoWords ? reinterpret_cast<const uint32_t*>(a.cinfo + pos)[lane]
-                                  : reinterpret_cast<const uint32_t*>(a.ckey + pos)[lane - kInfoWords];
-        cdst[j] = c;
-      } else if (lane == 0) {
-        a.best[c].Reset();
-        SplitKey kz;
-        kz.gain = kMinScore;
-        kz.feature = -1;
-        kz.threshold = 0;
-        kz.group = kz.offset = kz.num_bin = kz.mfb = kz.default_bin = 0;
-        kz.missing = kz.default_left = kz.is_cat = kz.pad0 = 0;
-        kz.pos = -1;
-        kz.pad2 = 0;
-        a.key[c] = kz;
-      }
-      if (lane == 0) {
-        s_gain[c] = valid ? g : kMinScore;
-        s_feat[c] = valid ? ff : -1;
-        s_cpos[c - base] = valid ? static_cast<int>(pos) : -1;
-      }
-    }
-  } else {
+  // ---- A. children of the last round: best over features (all pairs' keys in flight)
+  {
     double bg[kSelPairs];
     int bf[kSelPairs], bp[kSelPairs], pn[kSelPairs], pd[kSelPairs];
 #pragma unroll
@@ -1976,7 +1789,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
                                                     reinterpret_cast<uintptr_t>(smem) + 15) & ~uintptr_t(15)));  // [P2max]
   int* s_sc = reinterpret_cast<int*>(s_sg + FrontierSortCap(C));      // [P2max]
   // (the register replay below reads the leaves' keys itself: no LDS image, no barrier)
-  const bool reg_replay = !cegb && st.forced_next < 0 && L <= 64 * kSelLPer && !a.sel_lds_replay;
+  const bool reg_replay = !cegb && st.forced_next < 0 && L <= 64 * kSelLPer;
   if (!reg_replay) {
     for (int l = t; l < st.num_leaves; l += blockDim.x) {
       const int c = s_lcid[l];
@@ -2398,7 +2211,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     // position is within the speculation budget: best-first order commits at most R more
     // splits and takes them roughly by gain. Policy 0 budgets R minus every expanded but
     // uncommitted node. The blocked node always goes first.
-    if (na <= 64 && !a.sel_bitonic && !a.sel_block_rank) {
+    if (na <= 64) {
       // one wave ranks, scans and takes (no block barriers): each lane one alive node, its
       // position = alive nodes with a better key (gain desc, cid asc; keys are unique)
       if (w == 0) {
@@ -2447,7 +2260,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     } else {
     int P2 = 64;
     while (P2 < na) P2 <<= 1;
-    if (na <= kSelRankMax && !a.sel_bitonic) {
+    if (na <= kSelRankMax) {
       // rank sort (two barriers instead of the bitonic network's log2(P2)(log2(P2)+1)/2):
       // thread i's position = alive nodes ordered before it; keys are unique (cids), so the
       // ranks are a permutation and the order is the bitonic sort's. O(na) broadcast LDS reads
@@ -2644,13 +2457,6 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       ns_.total_tiles = 0;
     }
     *a.st = ns_;
-  }
-#pragma unroll
-  for (int j = 0; j < kSelPairs; ++j) {
-    const int c = cdst[j];
-    if (c < 0) continue;
-    if (lane < kInfoWords) reinterpret_cast<uint32_t*>(a.best + c)[lane] = cw[j];
-    else reinterpret_cast<uint32_t*>(a.key + c)[lane - kInfoWords] = cw[j];
   }
   FStamp(a, rnd, kFStampSel, 6);
   FStampEnd(a, rnd, kFStampSel);
@@ -2985,6 +2791,8 @@ __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
   double bg = kMinScore;
   int bf = 0x7fffffff, bp = -1;
   for (int f = lane; f < F && c >= 0; f += 64) {
+    // (candidates of features this rank does not own are stale: their items never ran)
+    if (a.fowned != nullptr && !a.fowned[f]) continue;
     const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
     if (kk.feature < 0) continue;
     if (FBetter(kk.gain, kk.feature, 0, bg, bf, 0)) {
@@ -3227,7 +3035,7 @@ void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
 }
 
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
-  const bool ext = a.voting || a.xrng != nullptr || a.fowned != nullptr || a.scan_best;
+  const bool ext = a.voting || a.xrng != nullptr || a.fowned != nullptr;
   if (a.scan_wave && !ext && a.num_forced == 0) {
     // one wave per item: enough blocks for every item of the widest round, at most 8 per CU's worth
     const int grid = std::max(1, std::min((a.kmax * a.F + kFScanWaves - 1) / kFScanWaves, 2048));
@@ -3276,21 +3084,15 @@ void LaunchFrontierPairMerge(const FArgs& a, hipStream_t s) {
   HIP_CHECK(hipGetLastError());
 }
 
+// one block per tile (A/B of the tile shapes at 1.25M / 10M rows: 1024-row tiles 884-886 it/s vs
+// 855 for two per block, 4096-row tiles at 10M 397.7 vs 394.3 for two 2048-row tiles per block)
 void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s) {
-  if (iters == 4) k_f_partition<4, 4><<<grid, kFPartThreads, 0, s>>>(a);
+  if (iters == 4) k_f_partition<4, 1><<<grid, kFPartThreads, 0, s>>>(a);
   else if (iters == 16) k_f_partition<16, 1><<<grid, kFPartThreads, 0, s>>>(a);
-  else k_f_partition<8, 2><<<grid, kFPartThreads, 0, s>>>(a);
+  else k_f_partition<8, 1><<<grid, kFPartThreads, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 
-int FrontierPartitionBlocksPerCU(int iters) {
-  int per_cu = 0;
-  const void* fn = iters == 4 ? reinterpret_cast<const void*>(k_f_partition<4, 4>)
-                              : (iters == 16 ? reinterpret_cast<const void*>(k_f_partition<16, 1>)
-                                             : reinterpret_cast<const void*>(k_f_partition<8, 2>));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kFPartThreads, 0));
-  return per_cu;
-}
 
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width) {
   (void)use_dp;

@@ -186,7 +186,6 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
   double* s_disc = reinterpret_cast<double*>(s_hes + Pa);
   int* s_idx = reinterpret_cast<int*>(kGlobal ? reinterpret_cast<double*>(s_hes + Pa) : s_disc + Pa + 1);
   float* s_lab = reinterpret_cast<float*>(s_idx + Pa);
-  int* s_off = reinterpret_cast<int*>(s_lab + Pa);
   const bool full_sort = TargetNeedsFullSort(a.target) || a.target == kTgtPrecision;
   for (int i = t; i < P; i += blockDim.x) {
     if (i < cnt) {
@@ -202,8 +201,30 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
     for (int r = t; r <= cnt; r += blockDim.x) s_disc[r] = RankDiscount(r);
   }
   __syncthreads();
-  // scores by original position; s_idx holds the ranking permutation
-  if (full_sort) {
+  // scores by original position; s_idx holds the ranking permutation (score desc, index asc:
+  // RankBefore's keys are unique). Up to one document per thread: a rank sort (each thread counts
+  // the documents before its own, one barrier); longer queries: the bitonic network.
+  if (full_sort && cnt <= kRankThreads) {
+    int pos = 0;
+    const double si = t < cnt ? s_score[t] : 0.0;
+    if (t < cnt) {
+      int j = 0;
+      for (; j + 8 <= cnt; j += 8) {
+        double s8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s8[u] = s_score[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pos += (s8[u] > si || (s8[u] == si && j + u < t)) ? 1 : 0;
+      }
+      for (; j < cnt; ++j) {
+        const double sj = s_score[j];
+        pos += (sj > si || (sj == si && j < t)) ? 1 : 0;
+      }
+    }
+    __syncthreads();  // (every thread read the identity order's s_idx before it is overwritten)
+    if (t < cnt) s_idx[pos] = t;
+    __syncthreads();
+  } else if (full_sort) {
     for (int k = 2; k <= P; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
         for (int i = t; i < P; i += blockDim.x) {
@@ -259,70 +280,63 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
     for (int i = t; i < cnt; i += blockDim.x) s_idx[i] = i;
     __syncthreads();
   }
-  // flattened pair space: s_off[i] = sum_{i' < i} |J(i')|
+  // Pairs: ONE WAVE per rank i (round robin over the waves), its lanes over the j range of
+  // TargetJRange -- no flattened pair index, no per-pair search. The i document's lambda /
+  // hessian terms sum in registers (64-bit fixed point per pair, exact and order free) and land
+  // with one atomic per (wave, i); each lane's j document takes its own (distinct lanes, distinct
+  // documents: no conflicts).
   const int i_end = TargetIEnd(a.target, cnt, a.k);
-  if (t == 0) {
-    int acc = 0;
-    for (int i = 0; i < i_end; ++i) {
-      s_off[i] = acc;
-      int js, je;
-      TargetJRange(a.target, i, cnt, a.k, &js, &je);
-      acc += je > js ? je - js : 0;
-    }
-    s_off[i_end > 0 ? i_end : 0] = acc;
-  }
-  __syncthreads();
-  const int total = i_end > 0 ? s_off[i_end] : 0;
   const bool binary = TargetIsBinary(a.target);
   const double inv_dcg = a.inv_max_dcg ? a.inv_max_dcg[q] : 0.0;
   const double inv_bdcg = a.inv_max_bdcg ? a.inv_max_bdcg[q] : 0.0;
   double sum_lambdas = 0.0;
-  int count = 0;
-  for (int p = t; p < total; p += blockDim.x) {
-    int lo = 0, hi = i_end - 1;
-    while (lo < hi) {  // last i with s_off[i] <= p
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] <= p) lo = mid;
-      else hi = mid - 1;
-    }
-    const int i = lo;
+  const int lane = t & (kWave - 1), wave = t / kWave;
+  for (int i = wave; i < i_end; i += kRankThreads / kWave) {
     int js, je;
     TargetJRange(a.target, i, cnt, a.k, &js, &je);
-    const int j = js + (p - s_off[i]);
-    const int di = s_idx[i], dj = s_idx[j];
-    if (s_score[di] == kMinScore || s_score[dj] == kMinScore) continue;
-    const float li = s_lab[di], lj = s_lab[dj];
-    if (li == lj) continue;
-    if (binary && li > 0 && lj > 0) continue;
-    int hr, lr;
-    if (li > lj) {
-      hr = i;
-      lr = j;
-    } else {
-      hr = j;
-      lr = i;
+    const int di = s_idx[i];
+    const double sdi = s_score[di];
+    const float li = s_lab[di];
+    long long li_lam = 0, li_hes = 0;  // (fixed point, kLamScale)
+    if (sdi != kMinScore) {
+      for (int j = js + lane; j < je; j += kWave) {
+        const int dj = s_idx[j];
+        const double sdj = s_score[dj];
+        if (sdj == kMinScore) continue;
+        const float lj = s_lab[dj];
+        if (li == lj) continue;
+        if (binary && li > 0 && lj > 0) continue;
+        const bool i_high = li > lj;
+        const int hr = i_high ? i : j, lr = i_high ? j : i;
+        const float lh = i_high ? li : lj, ll = i_high ? lj : li;
+        const double ds = i_high ? sdi - sdj : sdj - sdi;
+        const int hl = static_cast<int>(lh), lli = static_cast<int>(ll);
+        const double hg = hl < a.num_label_gain ? a.label_gain[hl] : 0.0;
+        const double lg = lli < a.num_label_gain ? a.label_gain[lli] : 0.0;
+        double dp = kGlobal ? TargetDeltaPair(a.target, i, j, hr, lr, hg, lg, lh, ll, inv_dcg, inv_bdcg, a.k, a.gap_weight)
+                            : TargetDeltaPairD(a.target, i, j, hr, lr, hg, lg, lh, ll, inv_dcg, inv_bdcg, a.k,
+                                               a.gap_weight, LdsDiscount{s_disc});
+        if (dp == 0) continue;
+        if (a.norm && best != worst) dp /= (0.01f + fabs(ds));
+        double pl = TableSigmoid(a, ds);
+        double ph = pl * (1.0f - pl);
+        pl *= -a.sigmoid * dp;
+        ph *= a.sigmoid * a.sigmoid * dp;
+        // high doc: +pl, low doc: -pl (pl <= 0); both take ph
+        const long long qpl = __double2ll_rn(pl * kLamScale), qph = __double2ll_rn(ph * kLamScale);
+        li_lam += i_high ? qpl : -qpl;
+        li_hes += qph;
+        atomicAdd(&s_lam[dj], static_cast<unsigned long long>(i_high ? -qpl : qpl));
+        atomicAdd(&s_hes[dj], static_cast<unsigned long long>(qph));
+        sum_lambdas -= 2 * pl;
+      }
     }
-    const int high = s_idx[hr], low = s_idx[lr];
-    const double ds = s_score[high] - s_score[low];
-    const int hl = static_cast<int>(s_lab[high]), ll = static_cast<int>(s_lab[low]);
-    const double hg = hl < a.num_label_gain ? a.label_gain[hl] : 0.0;
-    const double lg = ll < a.num_label_gain ? a.label_gain[ll] : 0.0;
-    double dp = kGlobal ? TargetDeltaPair(a.target, i, j, hr, lr, hg, lg, s_lab[high], s_lab[low], inv_dcg, inv_bdcg,
-                                          a.k, a.gap_weight)
-                        : TargetDeltaPairD(a.target, i, j, hr, lr, hg, lg, s_lab[high], s_lab[low], inv_dcg, inv_bdcg,
-                                           a.k, a.gap_weight, LdsDiscount{s_disc});
-    if (dp == 0) continue;
-    if (a.norm && best != worst) dp /= (0.01f + fabs(ds));
-    double pl = TableSigmoid(a, ds);
-    double ph = pl * (1.0f - pl);
-    pl *= -a.sigmoid * dp;
-    ph *= a.sigmoid * a.sigmoid * dp;
-    LamAdd(&s_lam[low], -pl);
-    LamAdd(&s_hes[low], ph);
-    LamAdd(&s_lam[high], pl);
-    LamAdd(&s_hes[high], ph);
-    sum_lambdas -= 2 * pl;
-    ++count;
+    li_lam = WaveSumLL(li_lam);
+    li_hes = WaveSumLL(li_hes);
+    if (lane == 0) {
+      if (li_lam) atomicAdd(&s_lam[di], static_cast<unsigned long long>(li_lam));
+      if (li_hes) atomicAdd(&s_hes[di], static_cast<unsigned long long>(li_hes));
+    }
   }
   sum_lambdas = WaveSum(sum_lambdas);
   if ((t & 63) == 0) s_red[t >> 6] = sum_lambdas;
@@ -331,7 +345,6 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
   for (int w = 0; w < kRankThreads / kWave; ++w) sl += s_red[w];
   double f = 1.0;
   if (a.norm && sl > 0) f = log2(1 + sl) / sl;
-  (void)count;
   for (int i = t; i < cnt; i += blockDim.x) {
     float g = LamGet(s_lam[i]), h = LamGet(s_hes[i]);
     if (a.norm && sl > 0) {

@@ -96,6 +96,12 @@ __device__ __forceinline__ float WaveSum(float v) {
   return __int_as_float(ReadLane(__float_as_int(WaveScanDpp(v, [](float x, float y) { return x + y; })), 63));
 }
 __device__ __forceinline__ int WaveSum(int v) { return ReadLane(WaveInclusiveSumDpp(v), 63); }
+// 64-bit integer wave sum (butterfly: the total in every lane)
+__device__ __forceinline__ long long WaveSumLL(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
 // inclusive prefix sum across the 64 lanes
 template <typename T>
 __device__ __forceinline__ T WaveInclusiveScan(T v) {

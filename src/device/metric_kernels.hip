@@ -254,6 +254,12 @@ void LaunchAucMetric(bool average_precision, const double* score, const float* l
   HIP_CHECK(hipGetLastError());
 }
 
+// auc_mu pair scores (t1 * v . score of each row of classes i and j), ranked by the AUC kernels
+// above. Ties: the AUC kernels group EXACTLY equal scores (reduce-by-key on equal_to<double>);
+// the host AucMu (metrics.cpp, reference multiclass_metric.hpp AucMuMetric) counts two pair
+// scores closer than kEpsilon (1e-15) as a tie. Scores a few ulps apart are therefore half-ties
+// on the host and ordered here: a documented divergence below 1e-15 of the score scale, pinned
+// by tests only for exact ties (test_device_metrics.py).
 __global__ __launch_bounds__(kMThreads) void k_aucmu_pair(AucMuPairArgs a) {
   const int m = a.ni + a.nj;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += gridDim.x * blockDim.x) {

@@ -272,6 +272,32 @@ void ReduceScatterSum(const void* send, void* recv, size_t count, bool f64, hipS
             "ncclReduceScatter");
 }
 
+// Reduce-scatter of exact 64-bit integer sums (the data-parallel frontier's fixed-point
+// accumulators): `send` = DpSize() chunks of `count` words, `recv` = this rank's chunk summed.
+void ReduceScatterSumU64(const unsigned long long* send, unsigned long long* recv, size_t count, hipStream_t stream) {
+  if (count == 0) return;
+  if (HostStagedDP()) {
+    const int n = Network::num_machines();
+    thread_local std::vector<char> h, o;
+    h.resize(sizeof(uint64_t) * count * n);
+    o.resize(sizeof(uint64_t) * count);
+    HIP_CHECK(hipMemcpyAsync(h.data(), send, h.size(), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    std::vector<comm_size_t> start(n), len(n, static_cast<comm_size_t>(sizeof(uint64_t) * count));
+    for (int i = 0; i < n; ++i) start[i] = static_cast<comm_size_t>(sizeof(uint64_t) * count * i);
+    Network::ReduceScatter(h.data(), static_cast<comm_size_t>(h.size()), static_cast<int>(sizeof(uint64_t)), start.data(),
+                           len.data(), o.data(), static_cast<comm_size_t>(o.size()), Network::SumReducer<uint64_t>());
+    HIP_CHECK(hipMemcpyAsync(recv, o.data(), o.size(), hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    return;
+  }
+  if (!CommExists()) {
+    HIP_CHECK(hipMemcpyAsync(recv, send, sizeof(uint64_t) * count, hipMemcpyDeviceToDevice, stream));
+    return;
+  }
+  NcclCheck(ncclReduceScatter(send, recv, count, ncclUint64, ncclSum, S().comm, stream), "ncclReduceScatter(u64)");
+}
+
 // In-place allgather: `buf` holds DpSize() blocks of `bytes` each, this rank's block filled.
 void AllGatherInPlace(void* buf, size_t bytes, hipStream_t stream) {
   if (bytes == 0) return;

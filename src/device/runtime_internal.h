@@ -39,6 +39,7 @@ int DpRank();
 // `send`: DpSize() blocks of `count` fp32 (fp64 with f64) values; recv: this rank's block
 // summed over ranks (ncclReduceScatter, or host-staged for the rehearsal transport)
 void ReduceScatterSum(const void* send, void* recv, size_t count, bool f64, hipStream_t stream);
+void ReduceScatterSumU64(const unsigned long long* send, unsigned long long* recv, size_t count, hipStream_t stream);
 // in-place allgather of DpSize() blocks of `bytes` (this rank's block filled)
 void AllGatherInPlace(void* buf, size_t bytes, hipStream_t stream);
 // map every rank's exchange buffer (same size / layout on all ranks) into this process

@@ -66,3 +66,27 @@ def test_custom_parser_with_header_uses_default_names(lgb, tmp_path):
     assert b_file.feature_name() == ["Column_0", "Column_1", "Column_2"]
     b_arr = lgb.train(params, lgb.Dataset(X, y), 4)
     np.testing.assert_allclose(b_file.predict(X), b_arr.predict(X), rtol=1e-12, atol=1e-12)
+
+
+def test_custom_parser_predict_drops_columns_the_model_never_saw(lgb, tmp_path):
+    """Predicting a file through the model's custom parser: a feature index past the model's
+    features (a column training never had) is ignored, as the reference's CopyToPredictBuffer
+    (predictor.hpp:259) ignores it; the predictions equal those of the training columns."""
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((400, 4))
+    y = (X[:, 1] - X[:, 3] > 0).astype(float)
+    f = tmp_path / "rows.txt"
+    with open(f, "w") as fo:
+        for row, lab in zip(X, y):
+            fo.write(";".join(f"{v:.17g}" for v in row) + f";{lab:g}\n")
+    cfg = tmp_path / "parser.json"
+    cfg.write_text('{"className": "lambdagap.label_last", "delimiter": ";"}')
+    params = {"objective": "binary", "num_leaves": 7, "verbosity": -1, "min_data_in_leaf": 5}
+    bst = lgb.train(params, lgb.Dataset(str(f), params={"parser_config_file": str(cfg)}), 4)
+    # one extra trailing column: the parser reads it as the label and the old label column as
+    # feature 4, which the 4-feature model never saw
+    wide = tmp_path / "rows_wide.txt"
+    with open(wide, "w") as fo:
+        for row, lab in zip(X, y):
+            fo.write(";".join(f"{v:.17g}" for v in row) + f";{lab:g};7\n")
+    np.testing.assert_allclose(bst.predict(str(wide)), bst.predict(X), rtol=1e-12, atol=1e-12)

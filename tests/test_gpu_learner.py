@@ -307,12 +307,14 @@ def test_data_parallel_path_single_rank(lgb, gpu_required, transport):
 
 
 @pytest.mark.parametrize("world,transport", [(2, "collective"), (3, "collective"), (4, "collective"),
-                                             (2, "collective-seq"), (2, "xgmi"), (3, "xgmi"), (4, "xgmi"),
-                                             (3, "collective-quantized")])
+                                             (3, "allreduce"), (2, "collective-seq"), (2, "xgmi"), (3, "xgmi"),
+                                             (4, "xgmi"), (3, "collective-quantized")])
 def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
-    """P ranks share the one GPU. "collective": the data-parallel FRONTIER engine (per-round exact
-    all-reduce of the fixed-point histograms through host-staged collectives, redundant scan and
-    select on every rank); "collective-seq": the sequential chain's owner histogram exchange over
+    """P ranks share the one GPU. "collective": the data-parallel FRONTIER engine, owner-computes
+    (per-round exact reduce-scatter of the fixed-point histograms by feature-group owner through
+    host-staged collectives, owner-only scans, per-child bests all-gathered, redundant select on
+    every rank); "allreduce": the same engine with the per-round all-reduce and redundant scans
+    of every feature; "collective-seq": the sequential chain's owner histogram exchange over
     the same collectives; "xgmi": the sequential chain's in-kernel exchange over IPC-mapped
     buffers (here all on one device). Every rank must grow the identical model, and it must match
     the host data-parallel learner trained by the same ranks on the same bins."""
@@ -336,7 +338,11 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
     assert res["world"] == world
     assert "data-parallel" in res["device_name"], res
     assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
-    assert ("frontier engine" in res["device_name"]) == (transport == "collective"), res
+    assert ("frontier engine" in res["device_name"]) == (transport in ("collective", "allreduce")), res
+    if transport == "collective":
+        assert "owner reduce-scatter" in res["device_name"], res
+    if transport == "allreduce":
+        assert "all-reduce per round" in res["device_name"], res
     assert res["ranks_identical"], res
     assert res["num_trees"] == 10
     if quantized:
