@@ -434,8 +434,6 @@ class DeviceTreeLearner : public TreeLearner {
 
   void ResetConfig(const Config* config) override {
     config_ = config;
-    fused_grad_ready_ = false;
-    fused_obj_ = nullptr;
     col_sampler_.Init(data_, config_);
     L_ = std::max(2, config_->num_leaves);
     AllocState();
@@ -549,7 +547,6 @@ class DeviceTreeLearner : public TreeLearner {
   std::unique_ptr<Tree> DeviceFitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred,
                                                 int class_id) override {
     ScopedTimer timer("Device::Refit");
-    fused_grad_ready_ = false;
     if (static_cast<data_size_t>(leaf_pred.size()) != N_ || gh_.size() < static_cast<size_t>(class_id + 1) * N_ ||
         old_tree->is_linear()) {
       return nullptr;  // (linear trees: the host linear learner's refit, FitByExistingTree)
@@ -583,6 +580,7 @@ class DeviceTreeLearner : public TreeLearner {
       delta[i] = new_v;  // the refit score holds only the refit trees so far (GBDT::RefitTree)
     }
     refit_delta_.Upload(delta, stream_);
+    FlushScore();
     LaunchAddLeafDelta(score_.get() + static_cast<size_t>(class_id) * N_, leaf_pred_dev_.get(), refit_delta_.get(), N_,
                        stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -611,6 +609,7 @@ class DeviceTreeLearner : public TreeLearner {
     renew_segs_.Upload(segs, stream_);
     renew_off_.Upload(off, stream_);
     RenewArgs ra;
+    FlushScore();
     ra.score = score_.get() + static_cast<size_t>(class_id) * N_;
     ra.label = label_.get();
     ra.weight = pp->kind == kPwMape ? aux_.get() : (weight_.size() ? weight_.get() : nullptr);
@@ -705,7 +704,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceInitScore(const std::vector<double>& host_score, int num_tree_per_iter) override {
-    fused_grad_ready_ = false;
+    pend_.on = false;  // (the uploaded score replaces everything)
     K_ = num_tree_per_iter;
     score_.Resize(static_cast<size_t>(K_) * N_);
     score_.Upload(host_score, stream_);
@@ -717,15 +716,15 @@ class DeviceTreeLearner : public TreeLearner {
   void DeviceComputeGradients(const ObjectiveFunction* obj) override {
     ScopedTimer timer("Device::ComputeGradients");
     PrepareObjective(obj);
-    const bool pointwise = obj->device_kind() == DeviceGradKind::kPointwise && K_ == 1;
-    if (pointwise && fused_grad_ready_ && fused_obj_ == obj) {
-      // the last score update already computed them (LaunchTraverseGrad): nothing has touched
-      // the score or the gradients since
-      fused_grad_ready_ = false;
+    if (pend_.on && pend_.k == 0 && K_ == 1 && obj->device_kind() == DeviceGradKind::kPointwise) {
+      // the deferred leaf add of the last tree, fused with this gradient pass
+      pend_.on = false;
+      LaunchLeafMapAddGrad(leaf_map_.get(), pend_lv_.get(), pend_.nl, N_, score_.get(), *obj->pointwise(), label_.get(),
+                           weight_.size() ? weight_.get() : nullptr, aux_.size() ? aux_.get() : nullptr, gh_.get(),
+                           num_cu_, stream_);
       return;
     }
-    fused_grad_ready_ = false;
-    fused_obj_ = pointwise ? obj : nullptr;  // (the next score update may compute them fused)
+    FlushScore();
     switch (obj->device_kind()) {
       case DeviceGradKind::kPointwise:
         LaunchPointwiseGrad(*obj->pointwise(), score_.get(), label_.get(), weight_.size() ? weight_.get() : nullptr,
@@ -763,8 +762,6 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceSetGradients(const score_t* g, const score_t* h, int num_class) override {
-    fused_grad_ready_ = false;
-    fused_obj_ = nullptr;
     const size_t n = static_cast<size_t>(num_class) * N_;
     if (gh_.size() < n) gh_.Resize(n);
     float2* p = pin_gh_.Get(n);
@@ -787,19 +784,21 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void DeviceGetScore(std::vector<double>* out) const override {
+    FlushScore();
     out->resize(static_cast<size_t>(K_) * N_);
     score_.Download(out->data(), out->size(), stream_);
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
   void DeviceAddConstant(double v, int k) override {
-    fused_grad_ready_ = false;
+    FlushScore();
     LaunchAddConstant(score_.get() + static_cast<size_t>(k) * N_, N_, v, stream_);
   }
 
   bool DeviceEvalPointwise(const PwMetricParams& p, int k, double* sum) override {
     if (score_.size() < static_cast<size_t>(k + 1) * N_ || N_ <= 0) return false;
     ScopedTimer timer("Device::EvalMetric");
+    FlushScore();
     EnsureMetricLabels();
     LaunchPointwiseMetric(p, score_.get() + static_cast<size_t>(k) * N_, metric_label_.get(),
                           metric_weight_.size() ? metric_weight_.get() : nullptr, N_, metric_partial_.get(),
@@ -813,7 +812,7 @@ class DeviceTreeLearner : public TreeLearner {
 
   void DeviceAddTreeToScore(const Tree* tree, int k) override {
     ScopedTimer timer("Device::AddTreeToScore");
-    fused_grad_ready_ = false;
+    FlushScore();
     double* s = score_.get() + static_cast<size_t>(k) * N_;
     if (tree->num_leaves() <= 1) {
       if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, N_, tree->LeafOutput(0), stream_);
@@ -823,37 +822,93 @@ class DeviceTreeLearner : public TreeLearner {
       TraverseLinear(tree, s);
       return;
     }
-    static const int score_path = [] {
-      const char* e = std::getenv("LGAP_SCORE_PATH");
-      return e == nullptr ? 0 : (std::strcmp(e, "leaves") == 0 ? 1 : (std::strcmp(e, "traverse") == 0 ? 2 : 0));
-    }();
-    if (score_path == 1 && tree == last_trained_ && !use_bag_ && tree->num_leaves() == static_cast<int>(h_range_.size())) {
-      last_trained_ = nullptr;
-      const int nl = tree->num_leaves();
-      double* lv = reinterpret_cast<double*>(pin_tree_.Get(sizeof(double) * nl));
-      int mx = 1;
-      for (int l = 0; l < nl; ++l) {
-        lv[l] = tree->LeafOutput(l);
-        mx = std::max(mx, h_range_[l].count);
-      }
-      tree_buf_.Resize(std::max(tree_buf_.size(), sizeof(double) * nl));
-      HIP_CHECK(hipMemcpyAsync(tree_buf_.get(), lv, sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
-      const dim3 grid(std::max(1, std::min(DivUp(mx, 256), 4 * num_cu_ / std::max(1, nl) + 1)), nl);
-      k_add_leaves<<<grid, 256, 0, stream_>>>(MakeArgs(), reinterpret_cast<const double*>(tree_buf_.get()), s);
-      HIP_CHECK(hipGetLastError());
-      HIP_CHECK(hipStreamSynchronize(stream_));
-      return;
-    }
+    const bool fresh = tree == last_trained_;
     last_trained_ = nullptr;
-    // single-class pointwise objectives: LGAP_FUSE_GRAD=1 has the traversal also compute the
-    // next iteration's gradients at the updated score (one pass over the rows). Opt-in: its 115
-    // VGPRs halve the walk's occupancy (10M: 238 us fused vs 150 + 44 us for the two kernels)
-    const char* fe = std::getenv("LGAP_FUSE_GRAD");
-    const bool fuse_ok = fe != nullptr && fe[0] == '1';
-    fuse_pending_ = fuse_ok && fused_obj_ != nullptr && K_ == 1 && k == 0 && label_.size() >= static_cast<size_t>(N_);
+    if (fresh && frontier_ && !use_bag_ && LeafMapScore(tree, k)) return;
     TraverseTree(tree, rowbins_.get(), N_, s);
-    fused_grad_ready_ = fuse_pending_ && fuse_done_;
-    fuse_pending_ = fuse_done_ = false;
+  }
+
+  // Score update from the leaf ranges of the frontier tree just grown (traverse_kernels.h
+  // LaunchLeafMap): without bagging every row sits in exactly one leaf's index segment, so the
+  // rows' leaves come from those segments instead of a walk of the tree over the packed rows.
+  // The map is built here; the add itself is deferred (pend_) into the next pointwise
+  // gradient pass, or flushed by the first reader of the score (FlushScore). Uploads go
+  // through the traversal's staging ring (no host wait).
+  bool LeafMapScore(const Tree* tree, int k) {
+    const int nl = tree->num_leaves();
+    if (nl != static_cast<int>(h_range_.size()) || nl > kLMMaxLeaves) return false;
+    long long total = 0;
+    for (const auto& r : h_range_) {
+      if (r.buf < 0 || r.buf >= kFrontierIdx) return false;  // (a partitioned leaf: an index buffer)
+      total += r.count;
+    }
+    if (total != N_) return false;
+    const size_t seg_bytes = Round256(sizeof(LeafSeg) * nl), off_bytes = Round256(sizeof(int) * (nl + 1));
+    const size_t bytes = seg_bytes + off_bytes + sizeof(double) * nl;
+    const int slot = tree_slot_++ & 1;
+    if (tree_evt_[slot] == nullptr) HIP_CHECK(hipEventCreateWithFlags(&tree_evt_[slot], hipEventDisableTiming));
+    else HIP_CHECK(hipEventSynchronize(tree_evt_[slot]));
+    char* hp = pin_tree_ring_[slot].Get(bytes);
+    LeafSeg* segs = reinterpret_cast<LeafSeg*>(hp);
+    int* off = reinterpret_cast<int*>(hp + seg_bytes);
+    double* lv = reinterpret_cast<double*>(hp + seg_bytes + off_bytes);
+    // the frontier partition writes a right child's rows from its range's end: a leaf's rows
+    // descend when it lies right of an odd number of its ancestors' splits (LeafMapArgs::segs)
+    leaf_desc_.assign(nl, 0);
+    std::vector<std::pair<int, int>>& stack = leaf_walk_;
+    stack.assign(1, {0, 0});
+    while (!stack.empty()) {
+      const auto [node, par] = stack.back();
+      stack.pop_back();
+      const int ch[2] = {tree->left_child(node), tree->right_child(node)};
+      for (int side = 0; side < 2; ++side) {
+        if (ch[side] < 0) leaf_desc_[~ch[side]] = static_cast<uint8_t>(par ^ side);
+        else stack.push_back({ch[side], par ^ side});
+      }
+    }
+    off[0] = 0;
+    for (int l = 0; l < nl; ++l) {
+      segs[l].buf = h_range_[l].buf;
+      segs[l].start = h_range_[l].start;
+      segs[l].count = h_range_[l].count;
+      segs[l].pad = leaf_desc_[l];
+      off[l + 1] = off[l] + h_range_[l].count;
+      lv[l] = tree->LeafOutput(l);
+    }
+    if (ttree_buf_.size() < bytes) {
+      HIP_CHECK(hipStreamSynchronize(stream_));  // queued score updates still read the old buffer
+      ttree_buf_.Resize(bytes);
+    }
+    HIP_CHECK(hipMemcpyAsync(ttree_buf_.get(), hp, bytes, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipEventRecord(tree_evt_[slot], stream_));
+    const size_t bound_ints = LeafTileBoundsInts(N_, nl);
+    const size_t map_bytes = Round256(static_cast<size_t>(N_) * (nl > 256 ? 2 : 1));
+    if (leaf_bounds_.size() < bound_ints || leaf_map_.size() < map_bytes || pend_lv_.size() < static_cast<size_t>(kLMMaxLeaves)) {
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      leaf_bounds_.Resize(std::max(leaf_bounds_.size(), bound_ints));
+      leaf_map_.Resize(std::max(leaf_map_.size(), map_bytes));
+      pend_lv_.Resize(kLMMaxLeaves);
+    }
+    LeafMapArgs la;
+    for (int i = 0; i < kLeafIdxBufs; ++i) la.idx[i] = i < kFrontierIdx ? idx_[i].get() : nullptr;
+    la.segs = reinterpret_cast<const LeafSeg*>(ttree_buf_.get());
+    la.seg_off = reinterpret_cast<const int*>(ttree_buf_.get() + seg_bytes);
+    la.leaf_value = reinterpret_cast<const double*>(ttree_buf_.get() + seg_bytes + off_bytes);
+    la.num_leaves = nl;
+    la.n = N_;
+    LaunchLeafMap(la, leaf_bounds_.get(), leaf_map_.get(), pend_lv_.get(), stream_);
+    pend_.on = true;
+    pend_.k = k;
+    pend_.nl = nl;
+    return true;
+  }
+
+  // the deferred leaf add of LeafMapScore, before anything reads (or adds to) the score
+  void FlushScore() const {
+    if (!pend_.on) return;
+    pend_.on = false;
+    LaunchLeafMapAdd(leaf_map_.get(), pend_lv_.get(), pend_.nl, N_, score_.get() + static_cast<size_t>(pend_.k) * N_,
+                     num_cu_, stream_);
   }
 
   // score[i] += tree(row i) over packed rows of the training layout (training or validation set)
@@ -862,7 +917,7 @@ class DeviceTreeLearner : public TreeLearner {
       if (tree->LeafOutput(0) != 0.0) LaunchAddConstant(s, n, tree->LeafOutput(0), stream_);
       return;
     }
-    if (tree->num_leaves() <= 32767 && !std::getenv("LGAP_OLD_TRAVERSE")) {
+    if (tree->num_leaves() <= 32767) {
       TraverseTreeCompact(tree, rowbins, n, s);
       return;
     }
@@ -998,18 +1053,6 @@ class DeviceTreeLearner : public TreeLearner {
                          reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, num_cu_, stream_);
       return;
     }
-    if (fuse_pending_ && rowbins == rowbins_.get() && n == N_ && fused_obj_ != nullptr) {
-      const PointwiseParams& pp = *fused_obj_->pointwise();
-      const uint32_t* rb = nib_ ? rowbins4_.get() : rowbins;
-      LaunchTraverseGrad(rb, nib_ ? stride4_dw_ : StrideOf(rowbins), nib_ ? 0 : width_, n, reinterpret_cast<const TNode*>(db), nn,
-                         reinterpret_cast<const TCat*>(db + node_bytes),
-                         reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
-                         reinterpret_cast<const double*>(db + node_bytes + cat_bytes), nl, s, pp, label_.get(),
-                         weight_.size() ? weight_.get() : nullptr, aux_.size() ? aux_.get() : nullptr, gh_.get(),
-                         num_cu_, stream_);
-      fuse_done_ = true;
-      return;
-    }
     if (nib_ && rowbins == rowbins_.get() && n == N_) {
       LaunchTraverse(rowbins4_.get(), stride4_dw_, 0, n, reinterpret_cast<const TNode*>(db), nn,
                      reinterpret_cast<const TCat*>(db + node_bytes), reinterpret_cast<const uint32_t*>(db + node_bytes + cat_bytes + leaf_bytes),
@@ -1081,6 +1124,7 @@ class DeviceTreeLearner : public TreeLearner {
     const float* weight = nullptr;
     int n = 0;
     if (id < 0) {
+      FlushScore();
       n = N_;
       if (n <= 0 || score_.size() < static_cast<size_t>(p.num_class) * N_) return false;
       EnsureMetricLabels();
@@ -1115,6 +1159,7 @@ class DeviceTreeLearner : public TreeLearner {
     const void* host_label = nullptr;
     int n = 0;
     if (id < 0) {
+      FlushScore();
       n = N_;
       if (n <= 0 || score_.size() < static_cast<size_t>(K) * N_) return false;
       EnsureMetricLabels();
@@ -1197,6 +1242,7 @@ class DeviceTreeLearner : public TreeLearner {
     const void* host_label = nullptr;
     int n = 0;
     if (id < 0) {
+      FlushScore();
       n = N_;
       if (n <= 0 || score_.size() < static_cast<size_t>(k + 1) * N_) return false;
       EnsureMetricLabels();
@@ -3839,8 +3885,6 @@ class DeviceTreeLearner : public TreeLearner {
   size_t fscan_lds_ = 0;
   DevBuf<char> farena_;
   // score update fused with the next pointwise gradients (DeviceAddTreeToScore)
-  const ObjectiveFunction* fused_obj_ = nullptr;  // pointwise objective of the last gradient pass
-  bool fused_grad_ready_ = false, fuse_pending_ = false, fuse_done_ = false;
   // linear-leaf trees (FitLinearLeaves / TraverseLinear)
   bool linear_ = false, lin_has_nan_ = false;
   DevBuf<float> lin_raw_;
@@ -4108,6 +4152,16 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<int> leaf_pred_dev_, renew_off_, renew_nz_;
   DevBuf<double> refit_partial_, refit_sums_, refit_delta_, renew_out_;
   DevBuf<LeafSeg> renew_segs_;
+  DevBuf<int> leaf_bounds_;  // LeafMapScore: per-leaf tile bounds
+  DevBuf<uint8_t> leaf_map_;  // LeafMapScore: leaf of every row (uint8 / uint16)
+  DevBuf<double> pend_lv_;    // LeafMapScore: the pending add's leaf values
+  struct PendingAdd {
+    bool on = false;
+    int k = 0, nl = 0;
+  };
+  mutable PendingAdd pend_;  // a tree's leaf add not yet applied to score_ (FlushScore)
+  std::vector<uint8_t> leaf_desc_;  // LeafMapScore: per-leaf row direction
+  std::vector<std::pair<int, int>> leaf_walk_;
   DevBuf<char> renew_scratch_;
   // multiclassova / unbiased LTR / long queries
   DevBuf<PointwiseParams> ova_params_;

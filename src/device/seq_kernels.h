@@ -292,8 +292,6 @@ __global__ void k_part_scatter(Args a);
 template <int ITERS>
 __global__ void k_partition(Args a);
 __global__ void k_post(Args a);
-__global__ void k_add_leaves(Args a, const double* __restrict__ leaf_value,
-                                                    double* __restrict__ score);
 __global__ void k_add_tree(const uint32_t* __restrict__ rowbins, int stride_dw,
                                                                int width, int N, const DevNode* __restrict__ nodes,
                                                                int num_nodes, const uint32_t* __restrict__ cat_bits,

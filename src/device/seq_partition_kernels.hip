@@ -713,23 +713,6 @@ __global__ __launch_bounds__(kPartThreads) void k_post(Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// score update of the tree just grown from its final leaf ranges (every row, no
-// bagging): each leaf adds its value to its rows (serial_tree_learner
-// AddPredictionToScore via the data partition). Opt-in (LGAP_SCORE_PATH=leaves):
-// the scattered 8 B score updates touch one cache line per row, and the
-// LDS-staged traversal below measured faster on MI355X (10M rows: 374 us -> see
-// profiles/README.md).
-__global__ __launch_bounds__(256) void k_add_leaves(Args a, const double* __restrict__ leaf_value,
-                                                    double* __restrict__ score) {
-  const int leaf = blockIdx.y;
-  const LeafRange r = a.range[leaf];
-  const double v = leaf_value[leaf];
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < r.count; i += gridDim.x * blockDim.x) {
-    score[RowAt(a, r.buf, r.start + i)] += v;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // score update: traverse one uploaded tree over the packed rows
 
 // One row per thread. A block first stages its 256 contiguous packed rows in LDS

@@ -15,6 +15,7 @@
 
 #include <cstdint>
 
+#include "device/leaf_kernels.h"
 #include "lgap/pointwise.h"
 
 namespace lgap {
@@ -48,13 +49,35 @@ void LaunchTraverse(const uint32_t* rowbins, int stride_dw, int width, int n, co
                     const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves, double* score,
                     int num_cu, hipStream_t s);
 
-// the traversal fused with the next iteration's pointwise gradients (lgap/pointwise.h): score[i]
-// += leaf value, then gh[i] = gradient / hessian at the new score (one pass over the rows instead
-// of a traversal and a gradient kernel)
-void LaunchTraverseGrad(const uint32_t* rowbins, int stride_dw, int width, int n, const TNode* nodes, int num_nodes,
-                        const TCat* cats, const uint32_t* cat_bits, const double* leaf_value, int num_leaves,
-                        double* score, const PointwiseParams& p, const float* label, const float* weight,
-                        const float* aux, float2* gh, int num_cu, hipStream_t s);
+// Score update from the final leaf ranges of the frontier tree just grown (reference
+// serial_tree_learner.cpp AddPredictionToScore via data_partition_, CUDA twin
+// cuda_data_partition.cu AddPredictionToScoreKernel), when every row sits in exactly one
+// leaf's row-index segment (no bagging). Instead of walking the tree over the packed rows:
+//  LaunchLeafMap   a first pass finds where each leaf's rows (monotone along the segment: the
+//                  frontier partition's left / right placement) cross every kLTRows-row tile
+//                  boundary; then one block per tile gathers the tile's row -> leaf map into
+//                  LDS from those runs and writes it out coalesced (uint8 <= 256 leaves, else
+//                  uint16). No scattered global writes; the leaf values are copied to lv_out.
+//  LaunchLeafMapAdd       score[i] += lv[map[i]] (deferred by the learner until the score is read)
+//  LaunchLeafMapAddGrad   the same fused with the next iteration's pointwise gradients
+constexpr int kLTShift = 12, kLTRows = 1 << kLTShift;
+constexpr int kLMMaxLeaves = 1024;  // larger trees take the traversal
+struct LeafMapArgs {
+  const int* idx[kLeafIdxBufs];  // row-index buffers by id (LeafSeg::buf; -1: identity rows)
+  const LeafSeg* segs;           // [num_leaves]; pad bit 0: the segment's rows descend
+  const int* seg_off;            // [num_leaves + 1] leaf-major positions of the segments
+  const double* leaf_value;      // [num_leaves]
+  int num_leaves;
+  int n;                         // rows == seg_off[num_leaves]
+};
+// ints of the tile-bounds scratch for n rows and num_leaves leaves
+size_t LeafTileBoundsInts(int n, int num_leaves);
+void LaunchLeafMap(const LeafMapArgs& a, int* bounds, void* map, double* lv_out, hipStream_t s);
+void LaunchLeafMapAdd(const void* map, const double* lv, int num_leaves, int n, double* score, int num_cu,
+                      hipStream_t s);
+void LaunchLeafMapAddGrad(const void* map, const double* lv, int num_leaves, int n, double* score,
+                          const PointwiseParams& p, const float* label, const float* weight, const float* aux, float2* gh,
+                          int num_cu, hipStream_t s);
 
 // linear-leaf trees (linear_kernels.h LinearLeaves): score[i] += the leaf's linear model at
 // row i's raw values (its constant output when one of them is NaN); 8- / 16-bit rows

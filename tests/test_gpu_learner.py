@@ -968,8 +968,9 @@ def test_four_bit_rows_match_byte_rows(lgb, gpu_required, rng, monkeypatch, max_
 
 
 def test_wide_rows_training_score(lgb, gpu_required, rng):
-    """Rows wider than 16 dwords (120 features): the training score update walks the group-major
-    copy (traverse_kernels.hip, k_traverse_col); the boosted model tracks the CPU learner's."""
+    """Rows wider than 16 dwords (120 features): with bagging the training score update walks the
+    group-major copy (traverse_kernels.hip, k_traverse_col), without it it comes from the leaf
+    ranges; both equal the model's prediction and the boosted model tracks the CPU learner's."""
     n, f = 30000, 120
     X = rng.standard_normal((n, f))
     X[:, 3] = rng.integers(0, 7, n)
@@ -977,8 +978,33 @@ def test_wide_rows_training_score(lgb, gpu_required, rng):
     params = {"objective": "regression", "num_leaves": 31, "verbosity": -1, "categorical_feature": [3],
               "min_data_in_leaf": 40}
     bc = lgb.train({**params, "device_type": "cpu"}, lgb.Dataset(X, y), 8)
-    bg = lgb.train({**params, "device_type": "gpu", "gpu_use_dp": True}, lgb.Dataset(X, y), 8)
-    np.testing.assert_allclose(bg.predict(X[:3000]), bc.predict(X[:3000]), rtol=1e-4, atol=1e-4)
+    for extra in ({}, {"bagging_fraction": 0.8, "bagging_freq": 1}):  # leaf-range update / column walk
+        bg = lgb.train({**params, "device_type": "gpu", "gpu_use_dp": True, **extra}, lgb.Dataset(X, y), 8,
+                       keep_training_booster=True)
+        np.testing.assert_allclose(bg._Booster__inner_predict(0), bg.predict(X), rtol=0, atol=1e-9)
+        if not extra:
+            np.testing.assert_allclose(bg.predict(X[:3000]), bc.predict(X[:3000]), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("extra", [{}, {"objective": "multiclass", "num_class": 3},
+                                   {"num_leaves": 1100, "min_data_in_leaf": 2, "min_sum_hessian_in_leaf": 0},
+                                   {"num_leaves": 300, "min_data_in_leaf": 5},
+                                   {"bagging_fraction": 0.7, "bagging_freq": 1}, {"data_sample_strategy": "goss"}])
+def test_leaf_range_score_update_matches_predict(lgb, gpu_required, rng, extra):
+    """The training score update from the final leaf ranges (traverse_kernels.hip k_leaf_bounds /
+    k_leaf_tile_add: per-tile runs of every leaf's ascending rows, an LDS row -> leaf map) equals
+    the model's prediction on the training rows. n = 20001 is not a multiple of the 4096-row tile
+    and makes the multiclass class slices 8-byte (not 16-byte) aligned; 1100 leaves exceed the
+    path's 1024-leaf limit and bagging / GOSS leave rows out of the leaves: those take the
+    traversal."""
+    n = 20001
+    X = rng.standard_normal((n, 10))
+    z = X[:, 0] - 0.6 * X[:, 1] + 0.4 * X[:, 2] * X[:, 3] + 0.3 * rng.standard_normal(n)
+    y = np.digitize(z, [-0.5, 0.5]).astype(float) if extra.get("objective") == "multiclass" else (z > 0).astype(float)
+    params = {"objective": "binary", "num_leaves": 63, "device_type": "gpu", "verbosity": -1, **extra}
+    b = lgb.train(params, lgb.Dataset(X, y), 6, keep_training_booster=True)
+    # (the inner scores come back through the objective's output transform, as predict's)
+    np.testing.assert_allclose(b._Booster__inner_predict(0), b.predict(X), rtol=0, atol=1e-9)
 
 
 @pytest.mark.parametrize("extra", [{"feature_fraction_bynode": 0.6},
