@@ -3807,7 +3807,6 @@ class DeviceTreeLearner : public TreeLearner {
     if (obj->device_kind() == DeviceGradKind::kLambdarank) {
       LambdarankTables t;
       if (!GetLambdarankTables(obj, &t)) Log::Fatal("lambdarank tables unavailable");
-      rank_table_.Upload(*t.table, stream_);
       rank_gain_.Upload(*t.label_gain, stream_);
       rank_inv_dcg_.Upload(*t.inv_max_dcg, stream_);
       rank_inv_bdcg_.Upload(*t.inv_max_bdcg, stream_);
@@ -3821,8 +3820,7 @@ class DeviceTreeLearner : public TreeLearner {
       r.tmin = t.tmin;
       r.tmax = t.tmax;
       r.tfactor = t.tfactor;
-      r.table_size = static_cast<int>(t.table->size());
-      r.table = rank_table_.get();
+      r.table_size = static_cast<int>(t.table->size());  // (the kernel evaluates the bins itself)
       r.label_gain = rank_gain_.get();
       r.num_label_gain = static_cast<int>(t.label_gain->size());
       r.inv_max_dcg = rank_inv_dcg_.get();
@@ -3832,6 +3830,14 @@ class DeviceTreeLearner : public TreeLearner {
       r.max_query = 1;
       for (data_size_t q = 0; q < md.num_queries(); ++q) {
         r.max_query = std::max(r.max_query, md.query_boundaries()[q + 1] - md.query_boundaries()[q]);
+      }
+      {
+        // 1 / log2(2 + r) for every rank of the longest query (the host objective's values)
+        std::vector<double> disc(static_cast<size_t>(std::max(r.max_query, 2)) + 1);
+        for (size_t i = 0; i < disc.size(); ++i) disc[i] = RankDiscount(static_cast<int>(i));
+        rank_disc_.Upload(disc, stream_);
+        HIP_CHECK(hipStreamSynchronize(stream_));  // (the host vector dies here)
+        r.disc = rank_disc_.get();
       }
       r.label = label_.get();
       r.weight = weight_.size() ? weight_.get() : nullptr;
@@ -4112,7 +4118,7 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<unsigned> rng_;
   DevBuf<char> tree_buf_;
   // lambdarank tables
-  DevBuf<double> rank_table_, rank_gain_, rank_inv_dcg_, rank_inv_bdcg_;
+  DevBuf<double> rank_disc_, rank_gain_, rank_inv_dcg_, rank_inv_bdcg_;
   DevBuf<int> rank_qb_;
   RankKernelArgs rank_args_;
   DevBuf<unsigned> xendcg_state_;

@@ -29,9 +29,9 @@ struct RankKernelArgs {
   double sigmoid = 1.0;
   double gap_weight = 1.0;
   double tmin = -50.0, tmax = 50.0, tfactor = 1.0;
-  int table_size = 0;
-  const double* table = nullptr;        // sigmoid lookup table
+  int table_size = 0;  // bins of the host sigmoid table (tmin / tmax / tfactor: its range)
   const double* label_gain = nullptr;
+  const double* disc = nullptr;        // 1 / log2(2 + r), r <= max_query
   int num_label_gain = 0;
   const double* inv_max_dcg = nullptr;  // per query
   const double* inv_max_bdcg = nullptr;

@@ -114,6 +114,8 @@ __global__ void k_add_constant(double* score, int n, double v) {
 }
 
 constexpr int kRankThreads = 256;
+constexpr int kNdcgMaxI = 32;  // NDCG register path: truncation levels up to this
+constexpr int kRankLdsGains = 64;  // label gains staged in LDS
 
 __device__ __forceinline__ bool RankBefore(double sa, int ia, double sb, int ib, int cnt) {
   const bool va = ia < cnt, vb = ib < cnt;
@@ -122,24 +124,37 @@ __device__ __forceinline__ bool RankBefore(double sa, int ia, double sb, int ib,
   return ia < ib;
 }
 
-__device__ __forceinline__ double TableSigmoid(const RankKernelArgs& a, double s) {
-  if (s <= a.tmin) return a.table[0];
-  if (s >= a.tmax) return a.table[a.table_size - 1];
-  return a.table[static_cast<size_t>((s - a.tmin) * a.tfactor)];
+
+// Wave sums of 16 per-lane values at once (reduce-scatter butterfly: xor 32 / 16 / 8 / 4 halve
+// the values each lane carries, xor 2 / 1 finish): returns the total of value index
+// 8 b5 + 4 b4 + 2 b3 + b2 (lane bits), the same in the 4 lanes of a group.
+__device__ __forceinline__ float WaveSum16(const float (&v)[16], int lane) {
+  float a8[8], a4[4], a2[2];
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) a8[q] = (h5 ? v[q + 8] : v[q]) + __shfl_xor(h5 ? v[q] : v[q + 8], 32, kWave);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a4[q] = (h4 ? a8[q + 4] : a8[q]) + __shfl_xor(h4 ? a8[q] : a8[q + 4], 16, kWave);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) a2[q] = (h3 ? a4[q + 2] : a4[q]) + __shfl_xor(h3 ? a4[q] : a4[q + 2], 8, kWave);
+  float a1 = (h2 ? a2[1] : a2[0]) + __shfl_xor(h2 ? a2[0] : a2[1], 4, kWave);
+  a1 += __shfl_xor(a1, 2, kWave);
+  a1 += __shfl_xor(a1, 1, kWave);
+  return a1;
 }
 
-// Per-document lambda / hessian sums accumulate as 64-bit fixed point with one
-// integer ds_add_u64 each (LDS float atomics are ~10x slower on gfx950, and the
-// integer sums do not depend on the order the pairs land in: deterministic).
-// |pair term| <= sigmoid * |delta| / 0.01 and a document has < 2048 partners, so
-// 2^36 of scale keeps every sum far inside int64 at 1.5e-11 resolution.
-constexpr double kLamScale = 68719476736.0;  // 2^36
-
-__device__ __forceinline__ void LamAdd(unsigned long long* p, double v) {
-  atomicAdd(p, static_cast<unsigned long long>(__double2ll_rn(v * kLamScale)));
-}
-__device__ __forceinline__ float LamGet(unsigned long long v) {
-  return static_cast<float>(static_cast<double>(static_cast<long long>(v)) * (1.0 / kLamScale));
+// The host objective's sigmoid table entry for a score difference (rank_objective.cpp
+// BuildSigmoidTable / GetSigmoid): the same clamps and bin index in double, then the bin's
+// value 1 / (1 + exp(s_bin * sigmoid)) evaluated in fp32 instead of read from the 8 MiB table
+// (a dependent global load per pair).
+// (bin_step / bin_base: the bin's sigmoid * score as step * idx + base, in fp32)
+__device__ __forceinline__ float TableSigmoidF(const RankKernelArgs& a, double s, float bin_step, float bin_base) {
+  int idx;
+  if (s <= a.tmin) idx = 0;
+  else if (s >= a.tmax) idx = a.table_size - 1;
+  else idx = static_cast<int>((s - a.tmin) * a.tfactor);
+  const float e = __expf(static_cast<float>(idx) * bin_step + bin_base);
+  return __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 struct LdsDiscount {
@@ -147,23 +162,36 @@ struct LdsDiscount {
   __device__ double operator()(int r) const { return tab[r]; }
 };
 
-// LDS bytes of a block for queries of up to `max_cnt` documents (P = pow2 >= max_cnt)
+// Block bytes (LDS, or global scratch for a long query) for queries of up to `max_cnt`
+// documents (P = pow2 >= max_cnt): scores, label gains, per-wave lambda / hessian sums,
+// discounts, ranking, labels
 inline size_t RankLdsBytes(int max_cnt) {
   int P = 1;
   while (P < max_cnt) P <<= 1;
-  return static_cast<size_t>(P) * (sizeof(double) + sizeof(int) + sizeof(float) + 2 * sizeof(unsigned long long)) +
-         static_cast<size_t>(P + 1) * (sizeof(int) + sizeof(double));
+  return static_cast<size_t>(P) * (2 * sizeof(double) + 2 * (kRankThreads / kWave) * sizeof(float) + sizeof(int) +
+                                   sizeof(float)) +
+         static_cast<size_t>(P + 1) * sizeof(double);
 }
 
 // kGlobal = false: one block per query, arrays in LDS sized by the dataset's largest query up
 // to kMaxDeviceQuery (short queries then fit many blocks per CU); longer queries are skipped
 // and handled by the kGlobal = true launch (one block per long query, the same arrays in its
-// own slice of global scratch; the integer accumulators become global atomics).
-template <bool kGlobal>
+// own slice of global scratch).
+//
+// Pairs: ONE WAVE per rank i (round robin over the waves), its lanes over the j range of
+// TargetJRange. The pair math runs in fp32 (the score difference and the sigmoid bin index in
+// fp64, as the host). Each wave accumulates into its OWN per-document lambda / hessian arrays
+// (distinct lanes: distinct documents; the wave's ranks in program order), the rank-i side
+// summed over the lanes first; the per-document totals add the four waves' arrays in wave
+// order. Every sum runs in a fixed order: deterministic without atomics.
+template <bool kGlobal, int TGT>
 __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, int Pmax) {
+  const int target = TGT >= 0 ? TGT : a.target;  // (TGT >= 0: the target's switch folded away)
+  constexpr int kWaves = kRankThreads / kWave;
   extern __shared__ __align__(8) unsigned char s_dyn[];
-  __shared__ double s_red[kRankThreads / kWave];
-  __shared__ int s_redi[kRankThreads / kWave];
+  __shared__ double s_red[kWaves];
+  __shared__ double s_lg[kRankLdsGains];   // label_gain (the first kRankLdsGains)
+  __shared__ int s_pos2[kRankThreads / 2];  // rank sort: the second half's counts
 
   const int q = kGlobal ? a.large_q[blockIdx.x] : static_cast<int>(blockIdx.x);
   const int t = threadIdx.x;
@@ -180,31 +208,59 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
   const int Pa = kGlobal ? P : Pmax;  // array length
   unsigned char* base = kGlobal ? reinterpret_cast<unsigned char*>(a.large_scratch + a.large_off[blockIdx.x]) : s_dyn;
   double* s_score = reinterpret_cast<double*>(base);
-  unsigned long long* s_lam = reinterpret_cast<unsigned long long*>(s_score + Pa);
-  unsigned long long* s_hes = s_lam + Pa;
-  // LDS launch: the query's rank discounts 1 / log2(2 + r), r <= cnt (RankDiscount)
-  double* s_disc = reinterpret_cast<double*>(s_hes + Pa);
-  int* s_idx = reinterpret_cast<int*>(kGlobal ? reinterpret_cast<double*>(s_hes + Pa) : s_disc + Pa + 1);
+  double* s_gain = s_score + Pa;                           // label_gain[label]
+  float* s_acc = reinterpret_cast<float*>(s_gain + Pa);    // [wave][lambda | hessian][Pa], by rank
+  double* s_disc = reinterpret_cast<double*>(s_acc + 2 * kWaves * Pa);  // 1 / log2(2 + r), r <= cnt
+  int* s_idx = reinterpret_cast<int*>(s_disc + Pa + 1);
   float* s_lab = reinterpret_cast<float*>(s_idx + Pa);
-  const bool full_sort = TargetNeedsFullSort(a.target) || a.target == kTgtPrecision;
+  const bool full_sort = TargetNeedsFullSort(target) || target == kTgtPrecision;
   for (int i = t; i < P; i += blockDim.x) {
     if (i < cnt) {
       // unbiased LTR ranks by score + the position's learned bias (host: adj[j])
       s_score[i] = a.positions ? a.score[start + i] + a.pos_bias[a.positions[start + i]] : a.score[start + i];
       s_lab[i] = a.label[start + i];
-      s_lam[i] = 0ull;
-      s_hes[i] = 0ull;
+#pragma unroll
+      for (int w = 0; w < 2 * kWaves; ++w) s_acc[w * Pa + i] = 0.f;
     }
     s_idx[i] = i;
   }
-  if (!kGlobal) {
-    for (int r = t; r <= cnt; r += blockDim.x) s_disc[r] = RankDiscount(r);
-  }
+  for (int r = t; r <= cnt; r += blockDim.x) s_disc[r] = a.disc[r];
+  if (t < min(a.num_label_gain, kRankLdsGains)) s_lg[t] = a.label_gain[t];
+  // (gains from the label once the LDS table is in: no dependent global load per document)
+  auto gain_of = [&](float lb) {
+    const int li = static_cast<int>(lb);
+    return li < a.num_label_gain ? (li < kRankLdsGains ? s_lg[li] : a.label_gain[li]) : 0.0;
+  };
   __syncthreads();
   // scores by original position; s_idx holds the ranking permutation (score desc, index asc:
   // RankBefore's keys are unique). Up to one document per thread: a rank sort (each thread counts
   // the documents before its own, one barrier); longer queries: the bitonic network.
-  if (full_sort && cnt <= kRankThreads) {
+  if (full_sort && cnt <= kRankThreads / 2) {
+    // two threads per document, each counting the documents before it in one half
+    const int d = t % (kRankThreads / 2), h = t / (kRankThreads / 2);
+    const int half = (cnt + 1) >> 1, j0 = h * half, j1 = min(cnt, j0 + half);
+    int pos = 0;
+    if (d < cnt) {
+      const double si = s_score[d];
+      int j = j0;
+      for (; j + 8 <= j1; j += 8) {
+        double s8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s8[u] = s_score[j + u];
+        // (bitwise, not short-circuit: no branch per comparison)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pos += static_cast<int>((s8[u] > si) | ((s8[u] == si) & (j + u < d)));
+      }
+      for (; j < j1; ++j) {
+        const double sj = s_score[j];
+        pos += static_cast<int>((sj > si) | ((sj == si) & (j < d)));
+      }
+      if (h == 1) s_pos2[d] = pos;
+    }
+    __syncthreads();
+    if (h == 0 && d < cnt) s_idx[pos + s_pos2[d]] = d;
+    __syncthreads();
+  } else if (full_sort && cnt <= kRankThreads) {
     int pos = 0;
     const double si = t < cnt ? s_score[t] : 0.0;
     if (t < cnt) {
@@ -214,11 +270,11 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
 #pragma unroll
         for (int u = 0; u < 8; ++u) s8[u] = s_score[j + u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) pos += (s8[u] > si || (s8[u] == si && j + u < t)) ? 1 : 0;
+        for (int u = 0; u < 8; ++u) pos += static_cast<int>((s8[u] > si) | ((s8[u] == si) & (j + u < t)));
       }
       for (; j < cnt; ++j) {
         const double sj = s_score[j];
-        pos += (sj > si || (sj == si && j < t)) ? 1 : 0;
+        pos += static_cast<int>((sj > si) | ((sj == si) & (j < t)));
       }
     }
     __syncthreads();  // (every thread read the identity order's s_idx before it is overwritten)
@@ -247,7 +303,7 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
   }
   // best / worst scores
   double best, worst;
-  if (TargetNeedsFullSort(a.target)) {
+  if (TargetNeedsFullSort(target)) {
     best = s_score[s_idx[0]];
     int wi = cnt - 1;
     if (wi > 0 && s_score[s_idx[wi]] == kMinScore) wi -= 1;
@@ -265,100 +321,208 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankKernelArgs a, i
     if ((t & 63) == 0) s_red[t >> 6] = mx;
     __syncthreads();
     mx = s_red[0];
-    for (int w = 1; w < kRankThreads / kWave; ++w) mx = fmax(mx, s_red[w]);
+    for (int w = 1; w < kWaves; ++w) mx = fmax(mx, s_red[w]);
     __syncthreads();
     if ((t & 63) == 0) s_red[t >> 6] = mn;
     __syncthreads();
     mn = s_red[0];
-    for (int w = 1; w < kRankThreads / kWave; ++w) mn = fmin(mn, s_red[w]);
+    for (int w = 1; w < kWaves; ++w) mn = fmin(mn, s_red[w]);
     __syncthreads();
     best = mx;
     worst = mn;
   }
-  // identity order for the order-free targets (the host iterates idx = 0..cnt-1)
+  // identity order for the order-free targets (the host iterates idx = 0..cnt-1); ranked
+  // targets: scores / labels / gains permuted into rank order (s_idx: rank -> document)
   if (!full_sort) {
     for (int i = t; i < cnt; i += blockDim.x) s_idx[i] = i;
     __syncthreads();
-  }
-  // Pairs: ONE WAVE per rank i (round robin over the waves), its lanes over the j range of
-  // TargetJRange -- no flattened pair index, no per-pair search. The i document's lambda /
-  // hessian terms sum in registers (64-bit fixed point per pair, exact and order free) and land
-  // with one atomic per (wave, i); each lane's j document takes its own (distinct lanes, distinct
-  // documents: no conflicts).
-  const int i_end = TargetIEnd(a.target, cnt, a.k);
-  const bool binary = TargetIsBinary(a.target);
-  const double inv_dcg = a.inv_max_dcg ? a.inv_max_dcg[q] : 0.0;
-  const double inv_bdcg = a.inv_max_bdcg ? a.inv_max_bdcg[q] : 0.0;
-  double sum_lambdas = 0.0;
-  const int lane = t & (kWave - 1), wave = t / kWave;
-  for (int i = wave; i < i_end; i += kRankThreads / kWave) {
-    int js, je;
-    TargetJRange(a.target, i, cnt, a.k, &js, &je);
-    const int di = s_idx[i];
-    const double sdi = s_score[di];
-    const float li = s_lab[di];
-    long long li_lam = 0, li_hes = 0;  // (fixed point, kLamScale)
-    if (sdi != kMinScore) {
-      for (int j = js + lane; j < je; j += kWave) {
-        const int dj = s_idx[j];
-        const double sdj = s_score[dj];
-        if (sdj == kMinScore) continue;
-        const float lj = s_lab[dj];
-        if (li == lj) continue;
-        if (binary && li > 0 && lj > 0) continue;
-        const bool i_high = li > lj;
-        const int hr = i_high ? i : j, lr = i_high ? j : i;
-        const float lh = i_high ? li : lj, ll = i_high ? lj : li;
-        const double ds = i_high ? sdi - sdj : sdj - sdi;
-        const int hl = static_cast<int>(lh), lli = static_cast<int>(ll);
-        const double hg = hl < a.num_label_gain ? a.label_gain[hl] : 0.0;
-        const double lg = lli < a.num_label_gain ? a.label_gain[lli] : 0.0;
-        double dp = kGlobal ? TargetDeltaPair(a.target, i, j, hr, lr, hg, lg, lh, ll, inv_dcg, inv_bdcg, a.k, a.gap_weight)
-                            : TargetDeltaPairD(a.target, i, j, hr, lr, hg, lg, lh, ll, inv_dcg, inv_bdcg, a.k,
-                                               a.gap_weight, LdsDiscount{s_disc});
-        if (dp == 0) continue;
-        if (a.norm && best != worst) dp /= (0.01f + fabs(ds));
-        double pl = TableSigmoid(a, ds);
-        double ph = pl * (1.0f - pl);
-        pl *= -a.sigmoid * dp;
-        ph *= a.sigmoid * a.sigmoid * dp;
-        // high doc: +pl, low doc: -pl (pl <= 0); both take ph
-        const long long qpl = __double2ll_rn(pl * kLamScale), qph = __double2ll_rn(ph * kLamScale);
-        li_lam += i_high ? qpl : -qpl;
-        li_hes += qph;
-        atomicAdd(&s_lam[dj], static_cast<unsigned long long>(i_high ? -qpl : qpl));
-        atomicAdd(&s_hes[dj], static_cast<unsigned long long>(qph));
-        sum_lambdas -= 2 * pl;
+  } else if (!kGlobal && cnt <= kRankThreads) {
+    const int d = t < cnt ? s_idx[t] : 0;
+    double sc = 0.0;
+    float lb = 0.f;
+    if (t < cnt) {
+      sc = s_score[d];
+      lb = s_lab[d];
+    }
+    __syncthreads();
+    if (t < cnt) {
+      s_score[t] = sc;
+      s_lab[t] = lb;
+      s_gain[t] = gain_of(lb);
+    }
+    __syncthreads();
+  } else if (!kGlobal) {
+    // (a long query in global scratch keeps document order and reads through s_idx)
+    constexpr int kPer = kMaxDeviceQuery / kRankThreads;
+    double sc[kPer], gn[kPer];
+    float lb[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int r = u * kRankThreads + t;
+      if (r < cnt) {
+        const int d = s_idx[r];
+        sc[u] = s_score[d];
+        lb[u] = s_lab[d];
+        gn[u] = gain_of(lb[u]);
       }
     }
-    li_lam = WaveSumLL(li_lam);
-    li_hes = WaveSumLL(li_hes);
-    if (lane == 0) {
-      if (li_lam) atomicAdd(&s_lam[di], static_cast<unsigned long long>(li_lam));
-      if (li_hes) atomicAdd(&s_hes[di], static_cast<unsigned long long>(li_hes));
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int r = u * kRankThreads + t;
+      if (r < cnt) {
+        s_score[r] = sc[u];
+        s_gain[r] = gn[u];
+        s_lab[r] = lb[u];
+      }
+    }
+    __syncthreads();
+  }
+  if (kGlobal || !full_sort) {
+    for (int i = t; i < cnt; i += blockDim.x) s_gain[i] = gain_of(s_lab[i]);
+    __syncthreads();
+  }
+  // document of rank r in the score / label / gain arrays
+  auto at = [&](int r) { return kGlobal && full_sort ? s_idx[r] : r; };
+  const int i_end = TargetIEnd(target, cnt, a.k);
+  const bool binary = TargetIsBinary(target);
+  const bool norm = a.norm && best != worst;
+  const double inv_dcg = a.inv_max_dcg ? a.inv_max_dcg[q] : 0.0;
+  const double inv_bdcg = a.inv_max_bdcg ? a.inv_max_bdcg[q] : 0.0;
+  const float sig = static_cast<float>(a.sigmoid), sig2 = sig * sig;
+  const float bin_step = static_cast<float>(a.sigmoid / a.tfactor), bin_base = static_cast<float>(a.tmin * a.sigmoid);
+  float sum_lambdas = 0.f;  // (this lane's pairs; the block total in fp64)
+  const int lane = t & (kWave - 1), wave = t / kWave;
+  float* w_lam = s_acc + 2 * wave * Pa;
+  float* w_hes = w_lam + Pa;
+  if (TGT == kTgtNdcg && !kGlobal && i_end <= kNdcgMaxI) {
+    // NDCG, truncation <= 32: each lane keeps ONE rank j per 64-rank chunk (its score / label /
+    // gain / discount in registers) and the wave's ranks i = wave + 4m as a register array, so
+    // the pair loop touches no LDS: the j side sums in registers across the wave's ranks, the
+    // i side in ilam[m] across the chunks (one wave sum per rank at the end)
+    constexpr int kM = kNdcgMaxI / kWaves;
+    float ilam[kM], ihes[kM];
+#pragma unroll
+    for (int m = 0; m < kM; ++m) ilam[m] = ihes[m] = 0.f;
+    for (int c = 0; c < cnt; c += kWave) {
+      const int j = c + lane;
+      const bool inb = j < cnt;
+      const double sdj = inb ? s_score[j] : kMinScore, gj = inb ? s_gain[j] : 0.0, dj = s_disc[inb ? j : 0];
+      const float lj = inb ? s_lab[j] : 0.f;
+      float jlam = 0.f, jhes = 0.f;
+#pragma unroll
+      for (int m = 0; m < kM; ++m) {
+        const int i = wave + kWaves * m;
+        if (i >= i_end) break;
+        const double sdi = s_score[i], gi = s_gain[i], di = s_disc[i];
+        const float li = s_lab[i];
+        const bool live = j > i && sdj != kMinScore && sdi != kMinScore && li != lj;
+        const bool i_high = li > lj;
+        const double ds = i_high ? sdi - sdj : sdj - sdi;
+        // (hg - lg) * |D(high rank) - D(low rank)| / maxDCG: the pair is symmetric in the ranks
+        const double dp = (i_high ? gi - gj : gj - gi) * fabs(di - dj) * inv_dcg;
+        float dpf = live ? static_cast<float>(dp) : 0.0f;
+        if (norm) dpf *= __builtin_amdgcn_rcpf(0.01f + static_cast<float>(fabs(ds)));
+        float pl = TableSigmoidF(a, live ? ds : 0.0, bin_step, bin_base);
+        float ph = pl * (1.0f - pl);
+        pl *= -sig * dpf;
+        ph *= sig2 * dpf;
+        ilam[m] += i_high ? pl : -pl;
+        ihes[m] += ph;
+        jlam += i_high ? -pl : pl;
+        jhes += ph;
+        sum_lambdas -= 2.0f * pl;
+      }
+      if (inb) {
+        w_lam[j] = jlam;
+        w_hes[j] = jhes;
+      }
+    }
+    static_assert(kM == 8, "WaveSum16 reduces 8 ranks' lambda + hessian");
+    float v16[16];
+#pragma unroll
+    for (int m = 0; m < kM; ++m) {
+      v16[m] = ilam[m];
+      v16[m + kM] = ihes[m];
+    }
+    const float tot = WaveSum16(v16, lane);
+    const int vi = lane >> 2, m = vi & (kM - 1), i = wave + kWaves * m;
+    if ((lane & 3) == 0 && i < i_end) (vi < kM ? w_lam : w_hes)[i] += tot;
+  } else {
+    for (int i = wave; i < i_end; i += kWaves) {
+      int js, je;
+      TargetJRange(target, i, cnt, a.k, &js, &je);
+      const int di = at(i);
+      const double sdi = s_score[di], gi = s_gain[di];
+      const float li = s_lab[di];
+      float li_lam = 0.f, li_hes = 0.f;
+      if (sdi != kMinScore) {
+        // branch-free body (a skipped pair's terms are masked to zero): nearly every wave has a
+        // live pair, so the branches only cost
+        for (int j = js + lane; j < je; j += kWave) {
+          const int dj = at(j);
+          const double sdj = s_score[dj];
+          const float lj = s_lab[dj];
+          const bool live = sdj != kMinScore && li != lj && !(binary && li > 0 && lj > 0);
+          const bool i_high = li > lj;
+          const int hr = i_high ? i : j, lr = i_high ? j : i;
+          const float lh = i_high ? li : lj, ll = i_high ? lj : li;
+          const double ds = i_high ? sdi - sdj : sdj - sdi;
+          const double gj = s_gain[dj], hg = i_high ? gi : gj, lg = i_high ? gj : gi;
+          const double dp = TargetDeltaPairD(target, i, j, hr, lr, hg, lg, lh, ll, inv_dcg, inv_bdcg, a.k, a.gap_weight,
+                                             LdsDiscount{s_disc});
+          float dpf = live ? static_cast<float>(dp) : 0.0f;
+          if (norm) dpf *= __builtin_amdgcn_rcpf(0.01f + static_cast<float>(fabs(ds)));
+          float pl = TableSigmoidF(a, live ? ds : 0.0, bin_step, bin_base);
+          float ph = pl * (1.0f - pl);
+          pl *= -sig * dpf;
+          ph *= sig2 * dpf;
+          // high doc: +pl, low doc: -pl (pl <= 0); both take ph
+          li_lam += i_high ? pl : -pl;
+          li_hes += ph;
+          w_lam[j] += i_high ? -pl : pl;
+          w_hes[j] += ph;
+          sum_lambdas -= 2.0f * pl;
+        }
+      }
+      li_lam = WaveSum(li_lam);
+      li_hes = WaveSum(li_hes);
+      if (lane == 0) {
+        w_lam[i] += li_lam;
+        w_hes[i] += li_hes;
+      }
     }
   }
-  sum_lambdas = WaveSum(sum_lambdas);
-  if ((t & 63) == 0) s_red[t >> 6] = sum_lambdas;
+  const double wsum = WaveSum(static_cast<double>(sum_lambdas));
+  if ((t & 63) == 0) s_red[t >> 6] = wsum;
   __syncthreads();
   double sl = 0.0;
-  for (int w = 0; w < kRankThreads / kWave; ++w) sl += s_red[w];
-  double f = 1.0;
-  if (a.norm && sl > 0) f = log2(1 + sl) / sl;
-  for (int i = t; i < cnt; i += blockDim.x) {
-    float g = LamGet(s_lam[i]), h = LamGet(s_hes[i]);
+  for (int w = 0; w < kWaves; ++w) sl += s_red[w];
+  // (one lane evaluates the fp64 log2; the others read it)
+  __shared__ double s_f;
+  if (t == 0) s_f = a.norm && sl > 0 ? log2(1 + sl) / sl : 1.0;
+  __syncthreads();
+  const double f = s_f;
+  for (int i = t; i < cnt; i += blockDim.x) {  // i: rank
+    double lam = 0.0, hes = 0.0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      lam += s_acc[2 * w * Pa + i];
+      hes += s_acc[(2 * w + 1) * Pa + i];
+    }
+    const int d = s_idx[i];
+    float g = static_cast<float>(lam), h = static_cast<float>(hes);
     if (a.norm && sl > 0) {
       g = static_cast<float>(g * f);
       h = static_cast<float>(h * f);
     }
     if (a.weight) {
-      const float w = a.weight[start + i];
+      const float w = a.weight[start + d];
       g = static_cast<float>(g * w);
       h = static_cast<float>(h * w);
     }
-    out[i] = make_float2(g, h);
+    out[d] = make_float2(g, h);
   }
-  (void)s_redi;
 }
 
 int GridFor(int n) {
@@ -611,13 +775,18 @@ void LaunchLambdarankGrad(const RankKernelArgs& a, hipStream_t s) {
   while (Pmax < std::max(2, std::min(a.max_query, kMaxDeviceQuery))) Pmax <<= 1;
   const size_t lds = RankLdsBytes(Pmax);
   if (lds > 64 * 1024) {
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_lambdarank<false>),
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_lambdarank<false, kTgtNdcg>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_lambdarank<false, -1>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   }
-  k_lambdarank<false><<<a.num_queries, kRankThreads, lds, s>>>(a, Pmax);
+  // NDCG (the default target) gets its own instantiation: the per-pair target switch of the
+  // generic one was most of the pair loop's branches
+  if (a.target == kTgtNdcg) k_lambdarank<false, kTgtNdcg><<<a.num_queries, kRankThreads, lds, s>>>(a, Pmax);
+  else k_lambdarank<false, -1><<<a.num_queries, kRankThreads, lds, s>>>(a, Pmax);
   HIP_CHECK(hipGetLastError());
   if (a.num_large > 0) {
-    k_lambdarank<true><<<a.num_large, kRankThreads, 0, s>>>(a, 0);
+    k_lambdarank<true, -1><<<a.num_large, kRankThreads, 0, s>>>(a, 0);
     HIP_CHECK(hipGetLastError());
   }
 }
