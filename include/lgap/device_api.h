@@ -5,8 +5,10 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "lgap/config.h"
+#include "lgap/split_math.h"
 #include "lgap/tree_learner.h"
 
 namespace lgap {
@@ -50,6 +52,35 @@ class HistogramBackend {
   // out: 2 * num_total_bin doubles (group bin 0 left zero, as the host builder)
   virtual void Histogram(const int* rows, int num_rows, double* out) = 0;
   virtual std::string DeviceName() const = 0;
+
+  // ---- device-resident histograms and device split scans (intermediate / advanced monotone
+  // constraints: src/device/policy_scan.h). The host keeps only the tree, the row partition and
+  // the constraint bookkeeping; histograms never leave the device, scans return SplitInfo rows.
+  // Allocates `num_slots` histogram slots of 2 * num_total_bin doubles; false: not available.
+  virtual bool EnableResidentSlots(int num_slots) { (void)num_slots; return false; }
+  // slot <- histogram of `rows` (all rows when null)
+  virtual void HistogramToSlot(const int* rows, int num_rows, int slot) { (void)rows; (void)num_rows; (void)slot; }
+  // larger <- larger - smaller (the parent's histogram held by the larger child's slot)
+  virtual void SubtractSlots(int larger, int smaller) { (void)larger; (void)smaller; }
+  // Scans the batch's leaves over every feature. Per leaf r: slot, row count, sums, parent output;
+  // per (r, f): enable flag, flat bounds and (advanced) the offset of lmin / lmax / rmin / rmax
+  // (num_bin doubles each) in `tb`, or -1. Returns out[r * F + f] (feature -1 when the feature
+  // cannot split) and splittable[r * F + f].
+  struct ScanBatch {
+    std::vector<int> slot, count;
+    std::vector<double> sum_g, sum_h, parent_output;
+    std::vector<uint8_t> enable;
+    std::vector<double> bmin, bmax;
+    std::vector<long long> tb_off;
+    std::vector<double> tb;
+    void Clear() {
+      slot.clear(); count.clear(); sum_g.clear(); sum_h.clear(); parent_output.clear();
+      enable.clear(); bmin.clear(); bmax.clear(); tb_off.clear(); tb.clear();
+    }
+  };
+  virtual void ScanSlots(const ScanBatch& batch, const SplitParams& params, SplitInfo* out, uint8_t* splittable) {
+    (void)batch; (void)params; (void)out; (void)splittable;
+  }
 };
 std::unique_ptr<HistogramBackend> CreateHistogramBackend(const Config* config, const Dataset* data);
 

@@ -92,6 +92,7 @@
 #include "device/linear_kernels.h"
 #include "device/runtime_internal.h"
 #include "device/frontier.h"
+#include "device/policy_scan.h"
 #include "device/traverse_kernels.h"
 #include "device/sample_kernels.h"
 #include "device/seq_kernels.h"
@@ -1649,8 +1650,6 @@ class DeviceTreeLearner : public TreeLearner {
   // explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain (its in-kernel xGMI exchange).
   // Reference: voting_parallel_tree_learner.cpp:243-399.
   bool FrontierVoting() const {
-    const char* e = std::getenv("LGAP_FRONTIER_VOTING");
-    if (e != nullptr && e[0] == '0') return false;
     const char* t = std::getenv("LGAP_DP_TRANSPORT");
     if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
     return mode_ == DevParallel::kVoting && voting_ && distributed_ && (CommExists() || HostStagedDP());
@@ -1661,16 +1660,12 @@ class DeviceTreeLearner : public TreeLearner {
   // an explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain.
   // Reference: feature_parallel_tree_learner.cpp:23-80.
   bool FrontierFeature() const {
-    const char* e = std::getenv("LGAP_FRONTIER_FEATURE");
-    if (e != nullptr && e[0] == '0') return false;
     const char* t = std::getenv("LGAP_DP_TRANSPORT");
     if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
     return mode_ == DevParallel::kFeature && owner_scan_ && !distributed_ && (CommExists() || HostStagedDP());
   }
   int FrontierKmax() const {
-    int k = kFrontierKmax;
-    if (const char* e = std::getenv("LGAP_FRONTIER_K")) k = std::max(1, std::min(kFrontierKmax, std::atoi(e)));
-    return std::max(1, std::min(k, L_ - 1));
+    return std::max(1, std::min(kFrontierKmax, L_ - 1));
   }
   // computed nodes of one tree: every committed node (2 L - 1) plus room for speculation
   // (8 L + 2 kmax, fewer when the per-node fp64 histograms would exceed ~8 GiB)
@@ -1876,7 +1871,6 @@ class DeviceTreeLearner : public TreeLearner {
     fscan_lds_ = FrontierScanLds(max_bin_, has_cat_ ? max_cat_bin_ : 1);
     FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
-    if (const char* e = std::getenv("LGAP_FRONTIER_SPEC")) fspec_cap_ = std::max(0, std::atoi(e));
     // 512 / 1024 threads per histogram block. Round 3 (after the grid cap at 7/8 of the CUs),
     // paired on one box: single-tile rows at 10M 370.6 / 368.9 (1024) vs 363.6 / 365.4 (512),
     // quantized 405.6 vs 398.3; at 1.25M mixed (737.9 / 778.4 vs 779.2 / 770.0). Multi-tile rows
@@ -1884,7 +1878,6 @@ class DeviceTreeLearner : public TreeLearner {
     fhist_threads_ = big_tiles_ || (num_tiles_ == 1 && N_ >= 4000000) ? 1024 : 512;
     if (const char* e = std::getenv("LGAP_FHIST_THREADS")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
     fpolicy_ = 1;
-    if (const char* e = std::getenv("LGAP_FRONTIER_POLICY")) fpolicy_ = std::atoi(e) == 0 ? 0 : 1;
     // speculation budget: every eligible node within the remaining splits (alpha 1). The
     // waste-driven throttle (LGAP_FRONTIER_ADAPT=1: alpha x0.75 while > 12% of the partitioned
     // rows go to never-committed expansions) trades rows for rounds and loses where rounds cost
@@ -2011,11 +2004,9 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.hist_il = !use_dp_ && a.qsub == 0 ? HistInterleave() : 0;
     {
-      // one wave per scan item on wide data (LGAP_SCAN_WAVE: 0 never, 1 always, default F >= 64)
-      const char* e = std::getenv("LGAP_SCAN_WAVE");
-      const int v = e != nullptr ? std::atoi(e) : -1;
+      // one wave per scan item on wide data (F >= 64, numerical features only)
       const bool fits = kFScanWaves * FrontierScanWaveBytes(max_bin_, cat_p2_) <= 150 * 1024;
-      a.scan_wave = fits && !has_cat_ && (v == 1 || (v < 0 && F_ >= 64)) ? 1 : 0;  // (numerical features only)
+      a.scan_wave = fits && !has_cat_ && F_ >= 64 ? 1 : 0;
       // (block scan grid cap: 512 blocks loop over a large round's items instead of 4096
       // mostly-idle blocks being dispatched every round; A/B 10M 2.850 vs 2.875, 1.25M 1.331 vs 1.341)
       a.scan_grid = 512;
@@ -2299,7 +2290,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (use_graph && comm && !fgraphs_.empty() && graph_comm_ != ActiveComm()) InvalidateGraph();
     if (use_graph && comm) graph_comm_ = ActiveComm();
     // per-round caps need the eager enqueue (the all-reduce sizes change from tree to tree)
-    fcaps_on_ = distributed_ && !use_graph && std::getenv("LGAP_FRONTIER_KCAP") == nullptr;
+    fcaps_on_ = distributed_ && !use_graph;
     if (distributed_) {
       if (fkused_.size() < static_cast<size_t>(kFrontierRoundCap)) {
         fkused_.Resize(kFrontierRoundCap);
@@ -2647,12 +2638,33 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void BackendHistogram(const int* rows, int n, double* out) {
-    // a full row set is order-free for a histogram: skip the index upload
-    const bool all = rows == nullptr || n == N_;
     if (n == 0) {
       std::memset(out, 0, sizeof(double) * 2 * static_cast<size_t>(TB_));
       return;
     }
+    BackendHistogramStaging(rows, n);
+    staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  // the same histogram left on the device, in `dst` (2 * TB doubles)
+  void BackendHistogramDevice(const int* rows, int n, double* dst) {
+    if (n == 0) {
+      HIP_CHECK(hipMemsetAsync(dst, 0, sizeof(double) * 2 * static_cast<size_t>(TB_), stream_));
+      return;
+    }
+    BackendHistogramStaging(rows, n);
+    HIP_CHECK(hipMemcpyAsync(dst, staging_.get(), sizeof(double) * 2 * static_cast<size_t>(TB_),
+                             hipMemcpyDeviceToDevice, stream_));
+    // (the row upload below reuses idx_[2] and the pinned control records: one histogram in flight)
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  hipStream_t BackendStream() const { return stream_; }
+
+  void BackendHistogramStaging(const int* rows, int n) {
+    // a full row set is order-free for a histogram: skip the index upload
+    const bool all = rows == nullptr || n == N_;
     if (!all) idx_[2].Upload(rows, n, stream_);
     Ctl* hc = pin_ctl_.Get(1);
     std::memset(hc, 0, sizeof(Ctl));
@@ -2669,8 +2681,6 @@ class DeviceTreeLearner : public TreeLearner {
     const Args args = MakeArgs();
     LaunchHist(args, /*collective=*/false);
     LaunchHistReduce(args);
-    staging_.Download(out, 2 * static_cast<size_t>(TB_), stream_);
-    HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
   // One histogram of (g, h) over `rows` (identity when null) into `out` (2 * TB doubles).
@@ -3012,12 +3022,8 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   int HistMinRows() const {
-    static const int env_rows = [] {
-      const char* e = std::getenv("LGAP_HIST_MIN_ROWS");  // A/B knob
-      return e ? std::max(0, std::atoi(e)) : 0;
-    }();
     if (config_->device_hist_min_rows > 0) return config_->device_hist_min_rows;
-    return env_rows > 0 ? env_rows : kHistMinRows;
+    return kHistMinRows;
   }
 
   int RootBlocks() const { return std::max(1, std::min(DivUp(N_, kRootThreads), 4 * num_cu_)); }
@@ -3029,17 +3035,12 @@ class DeviceTreeLearner : public TreeLearner {
     // Wide data (many LDS feature tiles): the grid is row blocks x tiles, so fewer row blocks
     // still fill the chip while the slab rows the scan folds (each one 8 B x all bins) shrink:
     // LambdaRank 1M x 300 (11 tiles) 17.7 -> 16.4 ms/iter at 46 row blocks instead of 256.
-    static const int env_blocks = [] {
-      const char* e = std::getenv("LGAP_HIST_BLOCKS");  // A/B knob
-      return e ? std::max(0, std::atoi(e)) : 0;
-    }();
     // (multi-tile: as many row blocks per tile as the CUs hold at once over all tiles -- two
     // blocks per CU when the tile's LDS allows, one for 150 KB tiles. Every row block flushes
     // its whole tile with global atomics: LambdaRank 2M x 300 moved 130 MB of atomics per
     // histogram launch with 102 row blocks x 5 tiles of 128 KB, twice the resident blocks)
     const int bpc = std::max(1, std::min(2, static_cast<int>((160 * 1024) / std::max<size_t>(hist_lds_bytes_, 1))));
     const int want = config_->device_hist_blocks > 0 ? config_->device_hist_blocks
-                     : env_blocks > 0                ? env_blocks
                                                      : std::min(num_cu_, std::max(1, bpc * num_cu_ / std::max(1, num_tiles_)));
     // partial-histogram slab: one row of 2 * TB accumulators per block, capped at 4 GiB
     const size_t row_bytes = 2 * static_cast<size_t>(TB_) * (use_dp_ ? 8 : 4);
@@ -3051,7 +3052,7 @@ class DeviceTreeLearner : public TreeLearner {
   // count at the grid), 7/8 of the CUs: A/B at 10M rows 224 blocks 363 it/s, 192: 361,
   // 256: 355, 384: 346, 512: 327 (the per-block flush of a full LDS tile is the fixed cost)
   int FrontierHistBlocks() const {
-    if (config_->device_hist_blocks > 0 || std::getenv("LGAP_HIST_BLOCKS") != nullptr) return HistBlocks();
+    if (config_->device_hist_blocks > 0) return HistBlocks();
     // several LDS tiles: the grid is row blocks x tiles, ~2 blocks per CU in all
     if (num_tiles_ > 1) return HistBlocks();
     return std::max(1, HistBlocks() * 7 / 8);
@@ -3175,9 +3176,7 @@ class DeviceTreeLearner : public TreeLearner {
   int RowAlign() const {
     // (default 16: A/B on one box, GOSS 5M x 500 quantized 10.95 -> 10.40 ms/iter, LambdaRank
     // 3M x 300 9.52 -> 9.30)
-    const char* e = std::getenv("LGAP_ROW_ALIGN_DW");
-    const int v = e != nullptr ? std::atoi(e) : 16;
-    return v == 8 || v == 16 || v == 32 ? v : 0;
+    return 16;
   }
 
   void PadTrainingRows(int align) {
@@ -3303,9 +3302,7 @@ class DeviceTreeLearner : public TreeLearner {
     // 28-byte rows -> 32 bytes, so a gathered row never straddles two sectors (A/B 10M 2.838 vs
     // 2.874 ms/iter; 1.25M flat)
     if (num_tiles_ == 1) {
-      const char* e = std::getenv("LGAP_ROW_PAD_SINGLE");
-      const int v = e != nullptr ? std::atoi(e) : (N_ >= (4 << 20) && stride_dw_ > 4 && stride_dw_ < 8 ? 8 : 0);
-      if (v == 8 || v == 16) PadTrainingRows(v);
+      if (N_ >= (4 << 20) && stride_dw_ > 4 && stride_dw_ < 8) PadTrainingRows(8);
     }
   }
 
@@ -3421,9 +3418,7 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, PartitionKernel(), kPartThreads, 0));
       // the occupancy API can overstate residency by one block per CU (MI355X_MICROARCH.md): keep a margin
       per_cu = std::max(1, per_cu - 1);
-      const char* cap_env = std::getenv("LGAP_PART_BLOCKS_PER_CU");  // A/B knob (default 4)
-      const int cap = cap_env ? std::max(1, std::atoi(cap_env)) : 4;
-      fused_blocks_ = std::min({max_tiles_ + 1, cap * num_cu_, per_cu * num_cu_});
+      fused_blocks_ = std::min({max_tiles_ + 1, 4 * num_cu_, per_cu * num_cu_});
     }
     use_bynode_ = config_->feature_fraction_bynode < 1.0;
     // every small per-tree structure + the static feature metadata in one allocation
@@ -3550,7 +3545,6 @@ class DeviceTreeLearner : public TreeLearner {
     // MI355X, 10M rows C=8 222 it/s, C=4 229, C=1 232; 1.25M C=8 348, C=1 386 -- the release /
     // ticket / acquire hand-off costs more than the shorter fold saves
     fold_chunks_ = 1;
-    if (const char* e = std::getenv("LGAP_SCAN_CHUNKS")) fold_chunks_ = std::max(1, std::min(16, std::atoi(e)));
 #if LGAP_SCAN_FOLD == 2
     fold_chunks_ = 1;
 #endif
@@ -3563,10 +3557,6 @@ class DeviceTreeLearner : public TreeLearner {
     // addresses, so a later bag (host upload or device draw) must not reallocate
     for (int i = 0; i < 3; ++i) idx_[i].Resize(std::max(N_, 1));
     if (bag_cnt_ == 0) bag_cnt_ = N_;
-    if (getenv("LGAP_STAMPS")) {
-      stamps_.Resize(5 * 256 * 2 * 8);
-      stamps_.Zero(stream_);
-    }
     AllocFrontier();
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
@@ -3624,7 +3614,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.scan_scratch_stride = scan_scratch_stride_;
     a.max_depth = config_->max_depth;
     // 0: separate k_post kernel, 1: block 0 after its tiles, 2: first spare block
-    a.fuse_post = getenv("LGAP_SPLIT_POST") ? 0 : config_->device_post_mode;
+    a.fuse_post = config_->device_post_mode;
     a.stamps = stamps_.size() ? stamps_.get() : nullptr;
     a.distributed = distributed_ ? 1 : 0;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
@@ -3742,11 +3732,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   static bool DPGraphEnabled() {
-    static const bool on = [] {
-      const char* e = std::getenv("LGAP_DP_GRAPH");
-      return e != nullptr && std::strcmp(e, "1") == 0;
-    }();
-    return on;
+    return false;
   }
 
   void InvalidateGraph() {
@@ -4251,14 +4237,119 @@ class DeviceHistogramBackend final : public HistogramBackend {
     cfg_.device_hist_blocks = user->device_hist_blocks;
     learner_ = std::make_unique<DeviceTreeLearner>(&cfg_, DevParallel::kSerial);
     learner_->Init(data, false);
+    data_ = data;
   }
   void SetGradients(const float* g, const float* h, int n) override { learner_->BackendSetGradients(g, h, n); }
   void Histogram(const int* rows, int n, double* out) override { learner_->BackendHistogram(rows, n, out); }
   std::string DeviceName() const override { return learner_->DeviceName(); }
 
+  // ---- resident slots + device scans (policy_scan.h)
+  bool EnableResidentSlots(int num_slots) override {
+    int max_bin = 2;
+    std::vector<PolicyFeat> feats(data_->num_features());
+    for (int f = 0; f < data_->num_features(); ++f) {
+      const FeatureInfo& fi = data_->feature(f);
+      PolicyFeat& p = feats[f];
+      p.hist_offset = fi.hist_offset;
+      p.num_bin = fi.num_bin;
+      p.mfb = static_cast<int>(fi.mfb);
+      p.default_bin = static_cast<int>(fi.default_bin);
+      p.missing = static_cast<int8_t>(fi.missing);
+      p.bin_type = static_cast<int8_t>(fi.bin_type);
+      p.monotone = fi.monotone;
+      p.pad = 0;
+      p.penalty = fi.penalty;
+      max_bin = std::max(max_bin, fi.num_bin);
+    }
+    // the scan's LDS holds one full feature histogram and its sort order (<= 64 KiB)
+    if (static_cast<size_t>(max_bin) * (2 * sizeof(double) + sizeof(int)) > 64 * 1024) return false;
+    max_bin_ = max_bin;
+    stride_ = 2 * static_cast<size_t>(data_->num_total_bin());
+    slots_.Resize(static_cast<size_t>(std::max(1, num_slots)) * stride_);
+    feat_.Upload(feats, learner_->BackendStream());
+    HIP_CHECK(hipStreamSynchronize(learner_->BackendStream()));
+    num_slots_ = num_slots;
+    return true;
+  }
+  void HistogramToSlot(const int* rows, int n, int slot) override {
+    CheckSlot(slot);
+    learner_->BackendHistogramDevice(rows, n, slots_.get() + static_cast<size_t>(slot) * stride_);
+  }
+  void SubtractSlots(int larger, int smaller) override {
+    CheckSlot(larger);
+    CheckSlot(smaller);
+    LaunchPolicySubtract(slots_.get() + static_cast<size_t>(larger) * stride_,
+                         slots_.get() + static_cast<size_t>(smaller) * stride_, stride_, learner_->BackendStream());
+  }
+  void ScanSlots(const ScanBatch& b, const SplitParams& params, SplitInfo* out, uint8_t* splittable) override {
+    const int R = static_cast<int>(b.slot.size());
+    const int F = data_->num_features();
+    if (R == 0 || F == 0) return;
+    hipStream_t s = learner_->BackendStream();
+    std::vector<PolicyReq> req(R);
+    for (int r = 0; r < R; ++r) {
+      CheckSlot(b.slot[r]);
+      req[r].slot = b.slot[r];
+      req[r].count = b.count[r];
+      req[r].sum_g = b.sum_g[r];
+      req[r].sum_h = b.sum_h[r];
+      req[r].parent_output = b.parent_output[r];
+    }
+    const size_t items = static_cast<size_t>(R) * F;
+    if (b.enable.size() != items || b.bmin.size() != items || b.bmax.size() != items || b.tb_off.size() != items) {
+      Log::Fatal("HIP policy scan: batch of %d leaves x %d features is malformed", R, F);
+    }
+    std::vector<PolicyBound> bnd(items);
+    for (size_t i = 0; i < items; ++i) {
+      bnd[i].min = b.bmin[i];
+      bnd[i].max = b.bmax[i];
+      bnd[i].tb_off = b.tb_off[i];
+      const int nb = data_->feature(static_cast<int>(i % F)).num_bin;
+      if (b.tb_off[i] >= 0 && static_cast<size_t>(b.tb_off[i]) + 4 * static_cast<size_t>(nb) > b.tb.size()) {
+        Log::Fatal("HIP policy scan: threshold bounds offset %lld outside %zu values", b.tb_off[i], b.tb.size());
+      }
+    }
+    req_.Upload(req, s);
+    bnd_.Upload(bnd, s);
+    en_.Upload(b.enable, s);
+    if (!b.tb.empty()) tb_.Upload(b.tb, s);
+    if (out_.size() < items) out_.Resize(items);
+    if (sp_.size() < items) sp_.Resize(items);
+    PolicyScanArgs a;
+    a.slots = slots_.get();
+    a.slot_stride = stride_;
+    a.feat = feat_.get();
+    a.F = F;
+    a.R = R;
+    a.max_bin = max_bin_;
+    a.req = req_.get();
+    a.bnd = bnd_.get();
+    a.enable = en_.get();
+    a.tb = b.tb.empty() ? nullptr : tb_.get();
+    a.p = params;
+    a.out = out_.get();
+    a.splittable = sp_.get();
+    LaunchPolicyScan(a, s);
+    out_.Download(out, items, s);
+    sp_.Download(splittable, items, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
+
  private:
+  void CheckSlot(int slot) const {
+    if (slot < 0 || slot >= num_slots_) Log::Fatal("HIP histogram slot %d outside [0, %d)", slot, num_slots_);
+  }
   Config cfg_;
   std::unique_ptr<DeviceTreeLearner> learner_;
+  const Dataset* data_ = nullptr;
+  int max_bin_ = 2, num_slots_ = 0;
+  size_t stride_ = 0;
+  DevBuf<double> slots_, tb_;
+  DevBuf<PolicyFeat> feat_;
+  DevBuf<PolicyReq> req_;
+  DevBuf<PolicyBound> bnd_;
+  DevBuf<uint8_t> en_, sp_;
+  DevBuf<SplitInfo> out_;
 };
 }  // namespace
 

@@ -181,6 +181,7 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian
     CheckForcedSplitFeatures();
   }
   if (want_device_hist_) hist_backend_ = device::CreateHistogramBackend(config_, train_data);
+  SetupResident();
   Log::Info("Number of data points in the train set: %d, number of used features: %d", num_data_, num_features_);
 }
 
@@ -194,9 +195,19 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
     leaf_count_global_.assign(config->num_leaves, 0);
   }
   if (train_data_ != nullptr) ResetHistPool();
+  if (train_data_ != nullptr) SetupResident();
   col_sampler_.Init(train_data_, config_);
   use_monotone_ = !config_->monotone_constraints.empty();
   SetupPolicies();
+}
+
+// Device-resident leaf histograms (EnableDeviceScans): one device slot per leaf, no LRU pool (the
+// factory only asks for it when num_leaves slots fit the device's histogram budget).
+void SerialTreeLearner::SetupResident() {
+  resident_ = hist_backend_ && want_device_scans_ && hist_backend_->EnableResidentSlots(config_->num_leaves);
+  if (!resident_) return;
+  dslot_.resize(config_->num_leaves);
+  dvalid_.assign(config_->num_leaves, 0);
 }
 
 void SerialTreeLearner::SetupPolicies() {
@@ -510,6 +521,10 @@ void SerialTreeLearner::BeforeTrain() {
   for (auto& s : splittable_) std::fill(s.begin(), s.end(), 1);
   if (intermediate_monotone_) mono_.Reset();
   if (cegb_) cegb_->BeforeTree();
+  if (resident_) {
+    for (size_t l = 0; l < dslot_.size(); ++l) dslot_[l] = static_cast<int>(l);
+    std::fill(dvalid_.begin(), dvalid_.end(), 0);
+  }
   double sg, sh;
   ComputeLeafSums(partition_.indices(0), partition_.count(0), &sg, &sh);
   InitLeafStat(&smaller_, 0, sg, sh, 0.0);
@@ -655,9 +670,14 @@ bool SerialTreeLearner::BeforeFindBestSplit(const Tree* tree, int left, int righ
       std::swap(hist_[left], hist_[right]);
       std::swap(hist_stamp_[left], hist_stamp_[right]);
       std::swap(splittable_[left], splittable_[right]);
+      if (resident_) {
+        std::swap(dslot_[left], dslot_[right]);
+        std::swap(dvalid_[left], dvalid_[right]);
+      }
     }
     hist_stamp_[larger_.leaf] = ++hist_clock_;
-    has_parent_hist_ = hist_[larger_.leaf].size() == static_cast<size_t>(2 * train_data_->num_total_bin());
+    has_parent_hist_ = resident_ ? dvalid_[larger_.leaf] != 0
+                                 : hist_[larger_.leaf].size() == static_cast<size_t>(2 * train_data_->num_total_bin());
     // the smaller child inherits the parent's splittable flags too
     splittable_[smaller_.leaf] = splittable_[larger_.leaf];
   }
@@ -671,6 +691,17 @@ void SerialTreeLearner::FindBestSplits(const Tree* tree) {
 
 void SerialTreeLearner::ConstructHistograms(bool use_subtract) {
   ScopedTimer timer("SerialTreeLearner::ConstructHistograms");
+  if (resident_) {
+    hist_backend_->HistogramToSlot(partition_.indices(smaller_.leaf), partition_.count(smaller_.leaf),
+                                   dslot_[smaller_.leaf]);
+    dvalid_[smaller_.leaf] = 1;
+    if (larger_.leaf >= 0 && !use_subtract) {
+      hist_backend_->HistogramToSlot(partition_.indices(larger_.leaf), partition_.count(larger_.leaf),
+                                     dslot_[larger_.leaf]);
+      dvalid_[larger_.leaf] = 1;
+    }
+    return;
+  }
   BuildHistogram(partition_.indices(smaller_.leaf), partition_.count(smaller_.leaf), HistOf(smaller_.leaf).data());
   if (larger_.leaf >= 0 && !use_subtract) {
     BuildHistogram(partition_.indices(larger_.leaf), partition_.count(larger_.leaf), HistOf(larger_.leaf).data());
@@ -686,6 +717,44 @@ void SerialTreeLearner::FindBestSplitsFromHistograms(const Tree* tree, bool use_
   if (has_larger) node_l = col_sampler_.GetByNode(tree, larger_.leaf);
   const double po_s = ParentOutput(tree, smaller_);
   const double po_l = has_larger ? ParentOutput(tree, larger_) : 0.0;
+  if (resident_) {
+    // the same flow on the device: subtraction in the larger child's slot, one scan launch for
+    // both children, only their per-feature SplitInfo rows come back
+    if (use_subtract && has_larger) hist_backend_->SubtractSlots(dslot_[larger_.leaf], dslot_[smaller_.leaf]);
+    auto& spl_s = splittable_[smaller_.leaf];
+    std::vector<char> en(num_features_);
+    for (int f = 0; f < num_features_; ++f) {
+      en[f] = bytree[f] && feature_mask_[f] && !(use_subtract && !spl_s[f]);
+    }
+    std::vector<const LeafStat*> leaves{&smaller_};
+    std::vector<double> po{po_s};
+    std::vector<const std::vector<char>*> ens{&en};
+    if (has_larger) {
+      leaves.push_back(&larger_);
+      po.push_back(po_l);
+      ens.push_back(&en);
+    }
+    std::vector<SplitInfo> out;
+    std::vector<uint8_t> sp;
+    DeviceScanLeaves(tree, leaves, po, ens, &out, &sp);
+    SplitInfo best_s, best_l;
+    best_s.Reset();
+    best_l.Reset();
+    for (int f = 0; f < num_features_; ++f) {
+      if (!en[f]) continue;
+      spl_s[f] = sp[f];
+      if (node_s[f] && out[f].feature >= 0 && out[f].BetterThan(best_s)) best_s = out[f];
+      if (has_larger) {
+        const size_t j = static_cast<size_t>(num_features_) + f;
+        splittable_[larger_.leaf][f] = sp[j];
+        if (node_l[f] && out[j].feature >= 0 && out[j].BetterThan(best_l)) best_l = out[j];
+      }
+    }
+    best_split_per_leaf_[smaller_.leaf] = best_s;
+    if (has_larger) best_split_per_leaf_[larger_.leaf] = best_l;
+    SyncBestSplits();
+    return;
+  }
   const double* hs = HistOf(smaller_.leaf).data();
   if (use_subtract && has_larger) {
     double* hl = HistOf(larger_.leaf).data();
@@ -751,7 +820,10 @@ SplitInfo SerialTreeLearner::ScoreFeature(const Tree* tree, const double* group_
 // histogram; its statistics come from the pending best split
 void SerialTreeLearner::RecomputeBestSplit(const Tree* tree, int leaf) {
   SplitInfo& cur = best_split_per_leaf_[leaf];
-  if (hist_[leaf].size() != static_cast<size_t>(2 * train_data_->num_total_bin())) {
+  if (resident_ && !dvalid_[leaf]) {
+    hist_backend_->HistogramToSlot(partition_.indices(leaf), partition_.count(leaf), dslot_[leaf]);
+    dvalid_[leaf] = 1;
+  } else if (!resident_ && hist_[leaf].size() != static_cast<size_t>(2 * train_data_->num_total_bin())) {
     // dropped from the histogram pool: rebuilt from the leaf's rows (the reference skips the
     // rescan here, serial_tree_learner.cpp:1025-1031, leaving a split that may break the
     // tightened bounds)
@@ -774,6 +846,18 @@ void SerialTreeLearner::RecomputeBestSplit(const Tree* tree, int leaf) {
   const std::vector<int8_t> node_used = col_sampler_.GetByNode(tree, leaf);
   SplitInfo best;
   best.Reset();
+  if (resident_) {
+    std::vector<char> en(num_features_);
+    for (int f = 0; f < num_features_; ++f) en[f] = bytree[f] && feature_mask_[f] && splittable_[leaf][f];
+    std::vector<SplitInfo> out;
+    std::vector<uint8_t> sp;
+    DeviceScanLeaves(tree, {&ls}, {po}, {&en}, &out, &sp);
+    for (int f = 0; f < num_features_; ++f) {
+      if (en[f] && node_used[f] && out[f].feature >= 0 && out[f].BetterThan(best)) best = out[f];
+    }
+    cur = best;
+    return;
+  }
   for (int f = 0; f < num_features_; ++f) {
     if (!bytree[f] || !feature_mask_[f] || !splittable_[leaf][f]) continue;
     bool sp;
@@ -781,6 +865,60 @@ void SerialTreeLearner::RecomputeBestSplit(const Tree* tree, int leaf) {
     if (node_used[f] && s.feature >= 0 && s.BetterThan(best)) best = s;
   }
   cur = best;
+}
+
+void SerialTreeLearner::DeviceScanLeaves(const Tree* tree, const std::vector<const LeafStat*>& leaves,
+                                         const std::vector<double>& po,
+                                         const std::vector<const std::vector<char>*>& enable,
+                                         std::vector<SplitInfo>* out, std::vector<uint8_t>* splittable) {
+  ScopedTimer timer("SerialTreeLearner::DeviceScanLeaves");
+  const int F = num_features_;
+  const int R = static_cast<int>(leaves.size());
+  auto& b = scan_batch_;
+  b.Clear();
+  const bool advanced = intermediate_monotone_ && mono_.advanced();
+  std::vector<double> scratch;
+  for (int r = 0; r < R; ++r) {
+    const LeafStat& ls = *leaves[r];
+    b.slot.push_back(dslot_[ls.leaf]);
+    b.count.push_back(ls.global_count);
+    b.sum_g.push_back(ls.sum_g);
+    b.sum_h.push_back(ls.sum_h);
+    b.parent_output.push_back(po[r]);
+    for (int f = 0; f < F; ++f) {
+      const bool en = (*enable[r])[f] != 0;
+      b.enable.push_back(en ? 1 : 0);
+      long long off = -1;
+      LeafBounds lb = bounds_[ls.leaf];
+      if (en && advanced && train_data_->feature(f).bin_type == BinType::Numerical) {
+        // advanced monotone: the feature's per-threshold child bounds (ScoreFeature's host path)
+        ThresholdBounds tb;
+        LeafBounds flat;
+        if (mono_.ThresholdBoundsFor(tree, f, ls.leaf, &scratch, &tb, &flat)) {
+          const int nb = train_data_->feature(f).num_bin;
+          off = static_cast<long long>(b.tb.size());
+          for (const double* arr : {tb.lmin, tb.lmax, tb.rmin, tb.rmax}) b.tb.insert(b.tb.end(), arr, arr + nb);
+        }
+        lb = flat;
+      }
+      b.bmin.push_back(lb.min);
+      b.bmax.push_back(lb.max);
+      b.tb_off.push_back(off);
+    }
+  }
+  out->assign(static_cast<size_t>(R) * F, SplitInfo());
+  splittable->assign(static_cast<size_t>(R) * F, 0);
+  hist_backend_->ScanSlots(b, MakeParams(), out->data(), splittable->data());
+  // ScoreFeature's adjustments of a found split: CEGB deduction, then the monotone penalty
+  for (int r = 0; r < R; ++r) {
+    const LeafStat& ls = *leaves[r];
+    for (int f = 0; f < F; ++f) {
+      SplitInfo& s = (*out)[static_cast<size_t>(r) * F + f];
+      if (s.feature < 0) continue;
+      if (cegb_) s.gain -= cegb_->DeltaGain(f, ls.leaf, partition_.indices(ls.leaf), partition_.count(ls.leaf), s);
+      if (s.monotone_type != 0) s.gain *= MonotonePenalty(tree, ls.leaf);
+    }
+  }
 }
 
 void SerialTreeLearner::RenewQuantizedLeaves(Tree* tree) const {
@@ -1092,6 +1230,7 @@ void SerialTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj
 }
 
 std::string SerialTreeLearner::DeviceName() const {
+  if (resident_) return hist_backend_->DeviceName() + " (HIP histograms and split scans, host constraint bookkeeping)";
   return hist_backend_ ? hist_backend_->DeviceName() + " (HIP histograms, host split policy)" : "cpu";
 }
 

@@ -97,6 +97,10 @@ class SerialTreeLearner : public TreeLearner {
   std::string DeviceName() const override;
   // device_type=gpu with a host split policy: histograms are built by the HIP kernels
   void EnableDeviceHistograms() { want_device_hist_ = true; }
+  // ... and, for the monotone intermediate / advanced policies, device-resident leaf histograms
+  // with device split scans (HistogramBackend::ScanSlots): the host keeps the tree, the row
+  // partition and the constraint bookkeeping only
+  void EnableDeviceScans() { want_device_scans_ = true; }
   // bound of the live leaf histograms in MB when histogram_pool_size is unset (<= 0: none)
   void SetHistPoolBudgetMB(double mb) { pool_budget_mb_ = mb; }
 
@@ -125,6 +129,7 @@ class SerialTreeLearner : public TreeLearner {
   std::vector<double>& HistOf(int leaf);
   void ResetHistPool();
   void SetupPolicies();
+  void SetupResident();
   int ForceSplits(Tree* tree, int* left_leaf, int* right_leaf);
   void CheckForcedSplitFeatures() const;
   // BestSplitForFeature + CEGB deduction + monotone split penalty (ComputeBestSplitForFeature)
@@ -134,6 +139,11 @@ class SerialTreeLearner : public TreeLearner {
   void RecomputeBestSplit(const Tree* tree, int leaf);
   // quant_train_renew_leaf: leaf outputs from the true (unquantized) gradient sums
   void RenewQuantizedLeaves(Tree* tree) const;
+  // device-resident mode (EnableDeviceScans): scans of `leaves` on the device, ScoreFeature's
+  // CEGB / monotone-penalty adjustments on the host; out[r * F + f], splittable the same
+  void DeviceScanLeaves(const Tree* tree, const std::vector<const LeafStat*>& leaves, const std::vector<double>& po,
+                        const std::vector<const std::vector<char>*>& enable, std::vector<SplitInfo>* out,
+                        std::vector<uint8_t>* splittable);
 
   const Config* config_;
   const Dataset* train_data_ = nullptr;
@@ -180,6 +190,11 @@ class SerialTreeLearner : public TreeLearner {
   const score_t* true_hessians_ = nullptr;
   std::unique_ptr<device::HistogramBackend> hist_backend_;
   bool want_device_hist_ = false;
+  bool want_device_scans_ = false;
+  bool resident_ = false;           // leaf histograms live in device slots (dslot_)
+  std::vector<int> dslot_;          // leaf -> device histogram slot
+  std::vector<char> dvalid_;        // leaf's slot holds its histogram
+  device::HistogramBackend::ScanBatch scan_batch_;
   std::string forced_json_;
   bool forced_rescored_ = false;  // ForceSplits left every leaf's best split current
   std::vector<Random> extra_rands_;

@@ -69,13 +69,23 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   }
   if (!c->forcedsplits_filename.empty() && !frontier_ok) return "forced splits";
   if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {
-    return "intermediate/advanced monotone constraints";
+    return "intermediate/advanced monotone constraints (device scans, host constraint walk)";
   }
   if (!c->interaction_constraints_vector.empty() &&
       (c->feature_fraction_bynode < 1.0 || c->interaction_constraints_vector.size() > 64)) {
     return "interaction constraints with by-node sampling / more than 64 sets";
   }
   return nullptr;
+}
+
+// Intermediate / advanced monotone constraints keep the leaves' histograms on the device and scan
+// them there (SerialTreeLearner::EnableDeviceScans, device/policy_scan.h): the serial learner's
+// constraint walk runs on the host between device launches. Extra-trees draws (which read the
+// host histogram) and forced splits keep the host scans.
+bool DeviceScansServe(const std::string& learner_type, bool linear_tree, const Config* c, const Dataset* train) {
+  return learner_type == "serial" && !linear_tree && !c->monotone_constraints.empty() &&
+         c->monotone_constraints_method != "basic" && !c->extra_trees && c->forcedsplits_filename.empty() &&
+         !DeviceHistogramsExceedPool(c, train);
 }
 
 }  // namespace
@@ -92,6 +102,7 @@ std::unique_ptr<TreeLearner> TreeLearner::Create(const std::string& learner_type
     auto learner = CreateHost(learner_type, linear_tree, config);
     auto* serial = static_cast<SerialTreeLearner*>(learner.get());
     serial->EnableDeviceHistograms();
+    if (DeviceScansServe(learner_type, linear_tree, config, train)) serial->EnableDeviceScans();
     // routed here by the histogram bound: keep the host pool within the same budget
     if (DeviceHistogramsExceedPool(config, train) && config->histogram_pool_size <= 0) {
       double mb = 0.5 * static_cast<double>(device::DeviceTotalMemory()) / (1024.0 * 1024.0);

@@ -506,9 +506,7 @@ def test_device_quantized_regression_tracks_cpu(lgb, gpu_required):
 
 
 @pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.05, "feature_fraction_bynode": 0.8,
-                                    "cegb_penalty_feature_lazy": [0.01, 0.02, 0.03, 0.04, 0.05, 0.06]},
-                                   {"monotone_constraints": [1, -1, 0, 0, 0, 0],
-                                    "monotone_constraints_method": "intermediate"}])
+                                    "cegb_penalty_feature_lazy": [0.01, 0.02, 0.03, 0.04, 0.05, 0.06]}])
 def test_host_policy_over_device_histograms(lgb, gpu_required, rng, extra):
     """Options only the host learners implement run the host split policy over HIP histograms
     (the reference's GPUTreeLearner arrangement); the model matches the CPU learner."""
@@ -520,6 +518,52 @@ def test_host_policy_over_device_histograms(lgb, gpu_required, rng, extra):
     tc, tg = _trees(bc)[0], _trees(bg)[0]
     assert [s[:2] for s in _splits(tc["tree_structure"], [])][:4] == [s[:2] for s in _splits(tg["tree_structure"], [])][:4]
     np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-3, atol=1e-3)
+
+
+def _monotone_reference_xy(rng, x3_to_category, n=3000):
+    """the data of test_policies._reference_monotone_set (reference test_engine.py:2118-2146)"""
+    x1, x2, x3 = rng.uniform(size=n), rng.uniform(size=n), rng.uniform(size=n)
+    X = np.column_stack((x1, x2, np.digitize(x3, bins=np.arange(0, 1, 0.01)) if x3_to_category else x3))
+    s = 10.0 * (rng.uniform(size=6) + 0.5)
+    y = (s[0] * x1 + np.sin(s[1] * np.pi * x1) - s[2] * x2 - np.cos(s[3] * np.pi * x2) - s[4] * x3
+         - np.cos(s[5] * np.pi * x3) + rng.normal(0.0, 0.01, size=n))
+    return X, y
+
+
+@pytest.mark.parametrize("x3_to_category", [True, False])
+@pytest.mark.parametrize("interactions", [True, False])
+@pytest.mark.parametrize("method", ["intermediate", "advanced"])
+def test_device_monotone_constraints_reference_cases(lgb, gpu_required, rng, x3_to_category, interactions, method):
+    """Intermediate / advanced monotone constraints with device_type=gpu: the leaves' histograms
+    stay on the device and every scan (children and the constraint walk's rescans, with flat or
+    per-threshold bounds) runs there (device/policy_scan.h). The reference's test_monotone_constraints
+    cases hold, and the trees equal the CPU learner's split for split."""
+    from lambdagap_amd.basic import Dataset
+
+    X, y = _monotone_reference_xy(rng, x3_to_category)
+    params = {"objective": "regression", "min_data": 20, "num_leaves": 20, "monotone_constraints": [1, -1, 0],
+              "monotone_constraints_method": method, "use_missing": False, "verbosity": -1, "gpu_use_dp": True,
+              "deterministic": True}
+    if interactions:
+        params["interaction_constraints"] = [[0], [1], [2]]
+    cat = [2] if x3_to_category else []
+    models = {}
+    for dev in ("cpu", "gpu"):
+        p = dict(params, device_type=dev)
+        models[dev] = lgb.train(p, Dataset(X, y, categorical_feature=cat, params=p), 30, keep_training_booster=True)
+    bg, bc = models["gpu"], models["cpu"]
+    assert "host split policy" not in bg.device_name() and "split scans" in bg.device_name(), bg.device_name()
+    n = 1000
+    v = np.linspace(0, 1, n).reshape((n, 1))
+    for fixed in np.linspace(0, 1, n)[:10]:
+        fx = fixed * np.ones((n, 1))
+        assert (np.diff(bg.predict(np.column_stack((v, fx, fx)))) >= 0).all()
+        assert (np.diff(bg.predict(np.column_stack((fx, v, fx)))) <= 0).all()
+    tc, tg = _trees(bc), _trees(bg)
+    assert [t["num_leaves"] for t in tc] == [t["num_leaves"] for t in tg]
+    for a, b in zip(tc[:5], tg[:5]):
+        assert [s[:2] for s in _splits(a["tree_structure"], [])] == [s[:2] for s in _splits(b["tree_structure"], [])]
+    np.testing.assert_allclose(bg.predict(X), bc.predict(X), rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.1},
