@@ -2152,11 +2152,14 @@ class DeviceTreeLearner : public TreeLearner {
     FrontierFeatureExchange(fr);
   }
 
-  // Feature parallel: this rank's per-child bests all-gathered, the best over ranks kept.
+  // Feature parallel: this rank's per-child bests all-gathered (the select takes the best over
+  // ranks in its phase A: no merge launch). CEGB's raw per-feature candidates would need every
+  // feature's scan on every rank: those configurations never reach these modes (FrontierOwner,
+  // the factory's FrontierServes).
   void FrontierFeatureExchange(const FArgs& fa) {
+    if (fa.cegb_raw) Log::Fatal("frontier feature exchange: raw CEGB candidates are not exchanged");
     LaunchFrontierPairBest(fa, stream_);
     AllGatherInPlace(ffpb_.get(), sizeof(FPairBest) * 2 * static_cast<size_t>(fkmax_), stream_);
-    LaunchFrontierPairMerge(fa, stream_);
   }
 
   void EnqueueFrontierRound(const FArgs& fa, int kb) {

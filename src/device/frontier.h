@@ -328,10 +328,9 @@ void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s)
 void LaunchFrontierVote(const FArgs& a, hipStream_t s);
 void LaunchFrontierElect(const FArgs& a, hipStream_t s);
 void LaunchFrontierVoteScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
-// feature parallel: this rank's per-child best -> fpb[rank] (before the all-gather); the best
-// over ranks -> the candidate table (after it)
+// feature parallel / owner-computes data parallel: this rank's per-child best -> fpb[rank] (before
+// the all-gather; k_f_select's phase A takes the best over the ranks after it)
 void LaunchFrontierPairBest(const FArgs& a, hipStream_t s);
-void LaunchFrontierPairMerge(const FArgs& a, hipStream_t s);
 // one-time kernel attributes (dynamic LDS above 64 KiB)
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width);
 // dynamic LDS of k_f_select (CEGB coupled penalties add F bytes of used flags after it)

@@ -1671,7 +1671,12 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     for (int i = t; i < kprev * F; i += blockDim.x) a.lazy_acc[i] = 0;
     __syncthreads();
   }
-  // ---- A. children of the last round: best over features (all pairs' keys in flight)
+  // ---- A. children of the last round: best over features (all pairs' keys in flight). Feature-
+  // parallel and owner-computes data-parallel rounds: best over the RANKS' per-child records
+  // (fpb, all-gathered after k_f_pair_best; gain desc, then feature asc -- the order of the
+  // sequential select), the record copied from the winning rank's fpb entry
+  const bool merge = a.fpb != nullptr;
+  const int nsrc = merge ? a.vote_P : F;
   {
     double bg[kSelPairs];
     int bf[kSelPairs], bp[kSelPairs], pn[kSelPairs], pd[kSelPairs];
@@ -1687,14 +1692,14 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         pd[j] = s_dep[s_pc[q]];
       }
     }
-    for (int f0 = 0; f0 < F; f0 += 64) {
+    for (int f0 = 0; f0 < nsrc; f0 += 64) {
       const int f = f0 + lane;
 #pragma unroll
       for (int j = 0; j < kSelPairs; ++j) {
         const int q = w + j * kSelWaves;
         // (bynode: the root is scored at its mask, row 0; other children when their parent commits)
-        if (q < np && f < F && s_pc[q] >= 0 && !(cegb && a.bynode != nullptr && s_pc[q] == 0 && !a.bynode[f])) {
-          const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+        if (q < np && f < nsrc && s_pc[q] >= 0 && !(cegb && a.bynode != nullptr && s_pc[q] == 0 && !a.bynode[f])) {
+          const SplitKey& kk = merge ? a.fpb[static_cast<size_t>(f) * 2 * a.kmax + q].key : a.ckey[static_cast<size_t>(q) * F + f];
           const int kf = kk.feature;
           const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used, s_pc[q]) : kk.gain);
           const int ff = kf < 0 ? 0x7fffffff : kf;
@@ -1722,11 +1727,14 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       // reads the candidate table, which an earlier launch wrote)
       if (valid) {
         const size_t pos = static_cast<size_t>(q) * F + fpos;
+        const FPairBest* pb = merge ? a.fpb + static_cast<size_t>(fpos) * 2 * a.kmax + q : nullptr;
+        const uint32_t* si = reinterpret_cast<const uint32_t*>(merge ? &pb->info : a.cinfo + pos);
+        const uint32_t* sk = reinterpret_cast<const uint32_t*>(merge ? &pb->key : a.ckey + pos);
         for (int i = lane; i < kInfoWords + kKeyWords; i += 64) {
           if (i < kInfoWords) {
-            reinterpret_cast<uint32_t*>(a.best + c)[i] = reinterpret_cast<const uint32_t*>(a.cinfo + pos)[i];
+            reinterpret_cast<uint32_t*>(a.best + c)[i] = si[i];
           } else {
-            reinterpret_cast<uint32_t*>(a.key + c)[i - kInfoWords] = reinterpret_cast<const uint32_t*>(a.ckey + pos)[i - kInfoWords];
+            reinterpret_cast<uint32_t*>(a.key + c)[i - kInfoWords] = sk[i - kInfoWords];
           }
         }
       } else if (lane == 0) {
@@ -1763,7 +1771,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         s_gain[c] = valid ? g : kMinScore;
         s_feat[c] = valid ? ff : -1;
         // (CEGB: the penalised best lives in best / key only)
-        s_cpos[c - base] = valid && !cegb ? static_cast<int>(static_cast<size_t>(q) * F + fpos) : -1;
+        // (merged ranks' records: the next expansions read best / key, written above)
+        s_cpos[c - base] = valid && !cegb && !merge ? static_cast<int>(static_cast<size_t>(q) * F + fpos) : -1;
       }
     }
   }
@@ -2779,9 +2788,9 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
 
 // ---------------------------------------------------------------------------
 // Feature parallel: one wave per child pair. k_f_pair_best: this rank's best over its owned
-// features' candidates; k_f_pair_merge (after the all-gather): the best over the ranks'
-// records replaces the pair's candidate row (gain desc, then feature asc: the order of the
-// sequential select, so the tree equals the one-rank tree).
+// features' candidates -> fpb[rank]; after the all-gather the select's phase A takes the best over
+// the ranks' records (gain desc, then feature asc: the order of the sequential select, so the tree
+// equals the one-rank tree).
 __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
   const FState* stp = a.st;
   if (stp->done) return;
@@ -2817,42 +2826,6 @@ __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
   for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
     if (i < kKeyWords) reinterpret_cast<uint32_t*>(&out->key)[i] = reinterpret_cast<const uint32_t*>(a.ckey + o)[i];
     else reinterpret_cast<uint32_t*>(&out->info)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(a.cinfo + o)[i - kKeyWords];
-  }
-}
-
-__global__ __launch_bounds__(64) void k_f_pair_merge(FArgs a) {
-  const FState* stp = a.st;
-  if (stp->done) return;
-  const int k = stp->k, q = blockIdx.x, F = a.F, lane = threadIdx.x, P = a.vote_P;
-  if ((q >> 1) >= k) return;
-  double bg = kMinScore;
-  int bf = 0x7fffffff, br = -1;
-  for (int r = lane; r < P; r += 64) {
-    const SplitKey& kk = a.fpb[static_cast<size_t>(r) * 2 * a.kmax + q].key;
-    if (kk.feature < 0) continue;
-    if (FBetter(kk.gain, kk.feature, 0, bg, bf, 0)) {
-      bg = kk.gain;
-      bf = kk.feature;
-      br = r;
-    }
-  }
-  const int src = WaveArgBestLane(bg, bf, 0);
-  br = ReadLane(br, src);
-  bf = ReadLane(bf, src);
-  for (int f = lane; f < F; f += 64) {
-    if (f == bf) continue;
-    SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
-    kk.feature = -1;
-    kk.gain = kMinScore;
-  }
-  if (br < 0) return;
-  const FPairBest* in = a.fpb + static_cast<size_t>(br) * 2 * a.kmax + q;
-  const size_t o = static_cast<size_t>(q) * F + bf;
-  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
-  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-  for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
-    if (i < kKeyWords) reinterpret_cast<uint32_t*>(a.ckey + o)[i] = reinterpret_cast<const uint32_t*>(&in->key)[i];
-    else reinterpret_cast<uint32_t*>(a.cinfo + o)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(&in->info)[i - kKeyWords];
   }
 }
 
@@ -3079,10 +3052,6 @@ void LaunchFrontierPairBest(const FArgs& a, hipStream_t s) {
   HIP_CHECK(hipGetLastError());
 }
 
-void LaunchFrontierPairMerge(const FArgs& a, hipStream_t s) {
-  k_f_pair_merge<<<2 * a.kmax, 64, 0, s>>>(a);
-  HIP_CHECK(hipGetLastError());
-}
 
 // one block per tile (A/B of the tile shapes at 1.25M / 10M rows: 1024-row tiles 884-886 it/s vs
 // 855 for two per block, 4096-row tiles at 10M 397.7 vs 394.3 for two 2048-row tiles per block)
