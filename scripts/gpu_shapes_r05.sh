@@ -25,3 +25,7 @@ run ltr5m 600 python scripts/bench_suite.py --config ltr --rows 5000000 --featur
 run goss12 900 python scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --steps 10 --warmup 12
 run goss12q 900 python scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --steps 10 --warmup 12 --quantized
 run vote12 900 python scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --learner voting --steps 10 --warmup 12
+run pltr 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/pltr -o run -- python3 scripts/bench_suite.py --config ltr --rows 5000000 --features 300 --steps 10 --warmup 3
+python scripts/prof_summary.py $OUT/pltr "LambdaRank 5M x 300, 255 leaves" 13 > $OUT/pltr_summary.md 2>&1; rm -rf $OUT/pltr
+run pgoss 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/pgoss -o run -- python3 scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --steps 10 --warmup 12
+python scripts/prof_summary.py $OUT/pgoss "regression EFB + GOSS 12.5M x 500, 255 leaves, fp" 22 > $OUT/pgoss_summary.md 2>&1; rm -rf $OUT/pgoss

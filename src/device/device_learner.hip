@@ -1859,7 +1859,12 @@ class DeviceTreeLearner : public TreeLearner {
       fvelect_.Resize(2 * K * static_cast<size_t>(topk_ + 1));
       fvrows_.Resize(2 * K * static_cast<size_t>(topk_) * 2 * max_bin_);
     }
-    fpart_tile_ = kPartThreads * part_iters_;
+    // frontier tile rows: the chain's rows per thread, or (LGAP_PART_ITERS=32) 8192-row tiles
+    fpart_iters_ = part_iters_;
+    if (const char* e = std::getenv("LGAP_PART_ITERS")) {
+      if (std::atoi(e) == 32) fpart_iters_ = 32;
+    }
+    fpart_tile_ = kPartThreads * fpart_iters_;
     ftile_cap_ = DivUp(N_, fpart_tile_) + fkmax_ + 1;
     ftile_pub_.Resize(ftile_cap_);
     ftile_pub_.Zero(stream_);
@@ -2163,7 +2168,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
 
   void EnqueueFrontierRound(const FArgs& fa, int kb) {
-    LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    LaunchFrontierPartition(fa, fpart_iters_, fpart_grid_, stream_);
     if (fowner_) {
       FrontierOwnerRound(fa, kb);
       LaunchFrontierSelect(fa, stream_);
@@ -2943,7 +2948,7 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(fbits_, bits.data(), sizeof(uint32_t) * bits.size(), hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(fbest_, 0, sizeof(SplitInfo) * k, stream_));
     FArgs fa = MakeFArgs();
-    LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    LaunchFrontierPartition(fa, fpart_iters_, fpart_grid_, stream_);
     HIP_CHECK(hipMemcpyAsync(out_rows, idx_[1].get(), sizeof(int) * total, hipMemcpyDeviceToHost, stream_));
     std::vector<FNode> nodes(3 * static_cast<size_t>(k));
     HIP_CHECK(hipMemcpyAsync(nodes.data(), fnodes_, sizeof(FNode) * nodes.size(), hipMemcpyDeviceToHost, stream_));
@@ -2957,7 +2962,7 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipMemcpyAsync(fexps_, ex.data(), sizeof(FExp) * k, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(idx_[1].get(), 0xff, sizeof(int) * total, stream_));
     fa.part_selfcount = 1;
-    LaunchFrontierPartition(fa, part_iters_, fpart_grid_, stream_);
+    LaunchFrontierPartition(fa, fpart_iters_, fpart_grid_, stream_);
     std::vector<int> rows2(total);
     HIP_CHECK(hipMemcpyAsync(rows2.data(), idx_[1].get(), sizeof(int) * total, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(nodes.data(), fnodes_, sizeof(FNode) * nodes.size(), hipMemcpyDeviceToHost, stream_));
@@ -4099,6 +4104,7 @@ class DeviceTreeLearner : public TreeLearner {
   PinnedBuf<unsigned> pin_bar_;
   int fused_blocks_ = 0;  // k_partition grid (0: two-kernel partition)
   int part_iters_ = 8;    // rows per thread of the fused partition (PartIters())
+  int fpart_iters_ = 8;   // rows per thread of the frontier partition
   const Tree* last_trained_ = nullptr;  // DeviceTrain's tree: its leaf ranges are still on the device
   DevBuf<float2> gh_true_;
   DevBuf<uint16_t> ghq_;  // quantized levels for the frontier's integer histograms
