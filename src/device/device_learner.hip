@@ -1859,11 +1859,9 @@ class DeviceTreeLearner : public TreeLearner {
       fvelect_.Resize(2 * K * static_cast<size_t>(topk_ + 1));
       fvrows_.Resize(2 * K * static_cast<size_t>(topk_) * 2 * max_bin_);
     }
-    // frontier tile rows: the chain's rows per thread, or (LGAP_PART_ITERS=32) 8192-row tiles
+    // frontier tile rows: the chain's rows per thread (8192-row tiles were an A/B loss: 10M 400.9
+    // vs 408.9 it/s, 1.25M 746 vs 878; profiles/r05/ab_partition_8192_tiles.log)
     fpart_iters_ = part_iters_;
-    if (const char* e = std::getenv("LGAP_PART_ITERS")) {
-      if (std::atoi(e) == 32) fpart_iters_ = 32;
-    }
     fpart_tile_ = kPartThreads * fpart_iters_;
     ftile_cap_ = DivUp(N_, fpart_tile_) + fkmax_ + 1;
     ftile_pub_.Resize(ftile_cap_);

@@ -3058,7 +3058,6 @@ void LaunchFrontierPairBest(const FArgs& a, hipStream_t s) {
 void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s) {
   if (iters == 4) k_f_partition<4, 1><<<grid, kFPartThreads, 0, s>>>(a);
   else if (iters == 16) k_f_partition<16, 1><<<grid, kFPartThreads, 0, s>>>(a);
-  else if (iters == 32) k_f_partition<32, 1><<<grid, kFPartThreads, 0, s>>>(a);
   else k_f_partition<8, 1><<<grid, kFPartThreads, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
