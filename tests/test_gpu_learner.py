@@ -566,6 +566,41 @@ def test_device_monotone_constraints_reference_cases(lgb, gpu_required, rng, x3_
     np.testing.assert_allclose(bg.predict(X), bc.predict(X), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("extra", [
+    {"monotone_constraints_method": "advanced", "bagging_fraction": 0.7, "bagging_freq": 1, "lambda_l1": 0.5,
+     "path_smooth": 2.0, "max_depth": 7},
+    {"monotone_constraints_method": "intermediate", "cegb_penalty_split": 0.02, "min_data_in_leaf": 40,
+     "monotone_penalty": 1.0},
+    {"monotone_constraints_method": "advanced", "objective": "regression", "max_delta_step": 0.5, "num_leaves": 63},
+])
+def test_device_monotone_scans_with_other_policies(lgb, gpu_required, rng, extra):
+    """The device scans of the monotone policies combined with bagging, L1 / path smoothing /
+    max_delta_step, the CEGB split penalty (applied on the host to the device's records) and the
+    monotone split penalty: trees equal the CPU learner's, outputs monotone in the constrained
+    features."""
+    X, z = _policy_data(rng)
+    extra = dict(extra)
+    obj = extra.pop("objective", "binary")
+    y = z if obj == "regression" else (z > 0).astype(float)
+    kw = dict(extra, objective=obj, monotone_constraints=[1, -1, 0, 0, 0, 0])
+    bc = _train(lgb, X, y, "cpu", rounds=6, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=6, gpu_use_dp=True, **kw)
+    assert "split scans" in bg.device_name(), bg.device_name()
+    tc, tg = _trees(bc), _trees(bg)
+    assert [t["num_leaves"] for t in tc] == [t["num_leaves"] for t in tg]
+    for a, b in zip(tc, tg):
+        assert [s[:2] for s in _splits(a["tree_structure"], [])] == [s[:2] for s in _splits(b["tree_structure"], [])]
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-6, atol=1e-6)
+    grid = np.linspace(-3, 3, 50)
+    for row in X[:10]:
+        Z = np.repeat(row[None, :], len(grid), 0)
+        Z[:, 0] = grid
+        assert np.all(np.diff(bg.predict(Z, raw_score=True)) >= -1e-10)
+        Z = np.repeat(row[None, :], len(grid), 0)
+        Z[:, 1] = grid
+        assert np.all(np.diff(bg.predict(Z, raw_score=True)) <= 1e-10)
+
+
 @pytest.mark.parametrize("extra", [{"cegb_penalty_split": 0.1},
                                    {"cegb_penalty_split": 0.05, "cegb_tradeoff": 0.5, "num_leaves": 63},
                                    {"cegb_penalty_split": 0.02, "extra_trees": True}])
