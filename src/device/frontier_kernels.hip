@@ -214,24 +214,40 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   const uint16_t* ghq = MODE >= 2 ? a.ghq + static_cast<size_t>(a.tp->cls) * a.N : nullptr;
   const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
   const int base = buf < 0 ? start : 0;
-  for (int p0 = rb + myr; p0 < re; p0 += rpi * R) {
-    int rows[R];
+  // Two-stage software pipeline over chunks of R/2 rows per thread: while chunk i's LDS adds run,
+  // chunk i+1's row words / gradients and chunk i+2's row indices are already in flight (the
+  // waves of a block otherwise wait on their index -> row round trips in step with each other).
+  // Rows past the range load nothing (row -1: word 0, no add).
+  constexpr int R2 = R / 2;
+  const int step = rpi * R2;
+  auto load_rows = [&](int p0, int* rows) {
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
+    for (int j = 0; j < R2; ++j) {
       const int p = p0 + j * rpi;
       rows[j] = p < re ? (idx ? idx[p] : base + p) : -1;
     }
-    uint32_t word[R];
-    float2 v[R];
-    uint32_t q[R];
+  };
+  auto load_data = [&](const int* rows, uint32_t* word, float2* v, uint32_t* q) {
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
+    for (int j = 0; j < R2; ++j) {
       word[j] = rows[j] >= 0 ? a.rowbins[static_cast<size_t>(rows[j]) * a.stride_dw + dw] : 0u;
       if (MODE >= 2) q[j] = rows[j] >= 0 ? ghq[rows[j]] : 0u;
       else v[j] = rows[j] >= 0 ? gh[rows[j]] : make_float2(0.f, 0.f);
     }
+  };
+  int rn[R2];
+  uint32_t word[R2], q[R2];
+  float2 v[R2];
+  load_rows(rb + myr, rn);
+  load_data(rn, word, v, q);
+  load_rows(rb + myr + step, rn);
+  for (int p0 = rb + myr; p0 < re; p0 += step) {
+    uint32_t wn[R2], qn[R2];
+    float2 vn[R2];
+    load_data(rn, wn, vn, qn);
+    load_rows(p0 + 2 * step, rn);
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
+    for (int j = 0; j < R2; ++j) {
       unsigned long long pg = 0ull, ph = 0ull;
       uint32_t p32 = 0u;
       if (MODE == 3) {
@@ -262,6 +278,12 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
           }
         }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < R2; ++j) {
+      word[j] = wn[j];
+      q[j] = qn[j];
+      v[j] = vn[j];
     }
   }
 }
@@ -731,13 +753,19 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
         if (f == 0) a.lsum_loc[my] = pre_sum;
       }
     }
+    // Every global load of the item is issued before the first store that needs a wait: thread
+    // 0's flags (stored to LDS after the bin loop) and, per bin, the accumulator words and the
+    // parent's bins (read before the re-zeroing / slot stores, which the compiler must otherwise
+    // assume alias them): one memory round trip instead of three or four.
+    int skip_v = 0, splp_v = 1;
     if (t == 0) {
       // (feature parallel: only the features this rank owns)
-      s_skip = !a.used_bytree[f] || (EXT && a.fowned != nullptr && !a.fowned[f]);
-      s_splp = p >= 0 && !voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
+      skip_v = !a.used_bytree[f] || (EXT && a.fowned != nullptr && !a.fowned[f]);
+      splp_v = p >= 0 && !voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
     for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
       const unsigned long long x0 = acc[pw * kk], x1 = qpack ? 0ull : acc[2 * kk + 1];
+      const double gp0 = gl ? gp[2 * kk] : 0.0, gp1 = gl ? gp[2 * kk + 1] : 0.0;
       acc[pw * kk] = 0ull;
       if (!qpack) acc[2 * kk + 1] = 0ull;
       long long q0 = static_cast<long long>(x0), q1 = static_cast<long long>(x1);
@@ -754,12 +782,16 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       gs[2 * kk] = sv0;
       gs[2 * kk + 1] = sv1;
       if (gl) {
-        const double l0 = gp[2 * kk] - sv0, l1 = gp[2 * kk + 1] - sv1;
+        const double l0 = gp0 - sv0, l1 = gp1 - sv1;
         hl_full[2 * b] = l0;
         hl_full[2 * b + 1] = l1;
         gl[2 * kk] = l0;
         gl[2 * kk + 1] = l1;
       }
+    }
+    if (t == 0) {
+      s_skip = skip_v;
+      s_splp = splp_v;
     }
     if (t < 2) {
       s_out[t].Reset();
@@ -1020,31 +1052,57 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
     const double* gp = (p >= 0 && cl >= 0) ? a.slots + static_cast<size_t>(p) * TB2 + v0 : nullptr;
     double* gs = a.slots + static_cast<size_t>(cs) * TB2 + v0;
     double* gl = cl >= 0 ? a.slots + static_cast<size_t>(cl) * TB2 + v0 : nullptr;
+    // One round of loads for the item: the flags, both children's statistics (uniform) and up to
+    // 64 x kScanWU bins of accumulator words and parent bins, all issued before the first store
+    // (the re-zeroing and slot stores may alias the parent's bins for the compiler: loading in
+    // the same iteration as the stores serialised one round trip per 64 bins, twice)
     const bool skip_both = !a.used_bytree[f] || !(p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1);
     const int splp = p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1;
+    const double2 cls0 = a.lsum[cs];
+    const double2 cls1 = cl >= 0 ? a.lsum[cl] : cls0;
+    const FNode cnd0 = a.nodes[cs];
+    const FNode cnd1 = cl >= 0 ? a.nodes[cl] : cnd0;
+    const double cpo0 = a.lout[cs], cpo1 = cl >= 0 ? a.lout[cl] : cpo0;
+    const LeafBounds cbd0 = a.bounds[cs], cbd1 = cl >= 0 ? a.bounds[cl] : cbd0;
+    constexpr int kScanWU = 4;
 #pragma unroll 1
-    for (int kk = lane; kk < nbin - 1; kk += 64) {
-      const unsigned long long x0 = acc[pw * kk], x1 = qpack ? 0ull : acc[2 * kk + 1];
-      acc[pw * kk] = 0ull;
-      if (!qpack) acc[2 * kk + 1] = 0ull;
-      long long q0 = static_cast<long long>(x0), q1 = static_cast<long long>(x1);
-      if (qpack) {
-        const unsigned long long hs = x0 & 0xFFFFFFFFull;
-        q0 = static_cast<long long>(x0 - hs) >> 32;
-        q1 = static_cast<long long>(hs);
+    for (int k0 = lane; k0 < nbin - 1; k0 += 64 * kScanWU) {
+      unsigned long long x0[kScanWU], x1[kScanWU];
+      double pg0[kScanWU], pg1[kScanWU];
+#pragma unroll
+      for (int u = 0; u < kScanWU; ++u) {
+        const int kk = k0 + 64 * u;
+        const bool ok = kk < nbin - 1;
+        x0[u] = ok ? acc[pw * kk] : 0ull;
+        x1[u] = ok && !qpack ? acc[2 * kk + 1] : 0ull;
+        pg0[u] = ok && gl ? gp[2 * kk] : 0.0;
+        pg1[u] = ok && gl ? gp[2 * kk + 1] : 0.0;
       }
-      const double sv0 = static_cast<double>(q0) * inv_g, sv1 = static_cast<double>(q1) * inv_h;
-      const int b = kk < fi.mfb ? kk : kk + 1;
-      hs_full[2 * b] = sv0;
-      hs_full[2 * b + 1] = sv1;
-      gs[2 * kk] = sv0;
-      gs[2 * kk + 1] = sv1;
-      if (gl) {
-        const double l0 = gp[2 * kk] - sv0, l1 = gp[2 * kk + 1] - sv1;
-        hl_full[2 * b] = l0;
-        hl_full[2 * b + 1] = l1;
-        gl[2 * kk] = l0;
-        gl[2 * kk + 1] = l1;
+#pragma unroll
+      for (int u = 0; u < kScanWU; ++u) {
+        const int kk = k0 + 64 * u;
+        if (kk >= nbin - 1) continue;
+        acc[pw * kk] = 0ull;
+        if (!qpack) acc[2 * kk + 1] = 0ull;
+        long long q0 = static_cast<long long>(x0[u]), q1 = static_cast<long long>(x1[u]);
+        if (qpack) {
+          const unsigned long long hs = x0[u] & 0xFFFFFFFFull;
+          q0 = static_cast<long long>(x0[u] - hs) >> 32;
+          q1 = static_cast<long long>(hs);
+        }
+        const double sv0 = static_cast<double>(q0) * inv_g, sv1 = static_cast<double>(q1) * inv_h;
+        const int b = kk < fi.mfb ? kk : kk + 1;
+        hs_full[2 * b] = sv0;
+        hs_full[2 * b + 1] = sv1;
+        gs[2 * kk] = sv0;
+        gs[2 * kk + 1] = sv1;
+        if (gl) {
+          const double l0 = pg0[u] - sv0, l1 = pg1[u] - sv1;
+          hl_full[2 * b] = l0;
+          hl_full[2 * b + 1] = l1;
+          gl[2 * kk] = l0;
+          gl[2 * kk + 1] = l1;
+        }
       }
     }
     FWaveSync();
@@ -1053,7 +1111,7 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
 #pragma unroll 1
     for (int sel = 0; sel < nsel; ++sel) {
       double* H = sel ? hl_full : hs_full;
-      const double2 lsum = a.lsum[sel ? cl : cs];
+      const double2 lsum = sel ? cls1 : cls0;
       double sgs = 0.0, shs = 0.0;
 #pragma unroll 1
       for (int b = lane; b < nbin; b += 64) {
@@ -1073,11 +1131,11 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
     for (int sel = 0; sel < nsel; ++sel) {
       const int my = sel ? cl : cs;
       const double* H = sel ? hl_full : hs_full;
-      // the child's statistics (uniform loads: every lane reads the same words)
-      const double2 lsum = a.lsum[my];
-      const FNode nd = a.nodes[my];
-      const double pre_out = a.lout[my];
-      const LeafBounds bnd = a.bounds[my];
+      // the child's statistics (loaded with the item's bins)
+      const double2 lsum = sel ? cls1 : cls0;
+      const FNode nd = sel ? cnd1 : cnd0;
+      const double pre_out = sel ? cpo1 : cpo0;
+      const LeafBounds bnd = sel ? cbd1 : cbd0;
       if (lane == 0) {
         out->Reset();
         SplitKey kz;
