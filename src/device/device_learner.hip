@@ -1867,10 +1867,14 @@ class DeviceTreeLearner : public TreeLearner {
     ftile_pub_.Resize(ftile_cap_);
     ftile_pub_.Zero(stream_);
     for (int i = 3; i < kFrontierIdx; ++i) idx_[i].Resize(std::max(N_, 1));
-    // partition grid: one block per tile of the tile capacity, so every tile of any round is in a
-    // block's registers (blocks beyond the resident ones start as earlier ones finish; a block only
-    // waits on lower blocks' tiles)
-    fpart_grid_ = std::max(1, ftile_cap_);
+    // partition grid: the resident blocks (at most one per tile of the tile capacity); a block
+    // takes tiles b, b + G, ... in passes and only waits on lower tiles. A grid of the full tile
+    // capacity (2.4K blocks at 10M) left ~1.2K blocks with no tile in a typical round, dispatched
+    // behind the working ones: each still read the round state before exiting, at the kernel's tail.
+    {
+      const int per_cu = std::max(1, FrontierPartitionBlocksPerCU(fpart_iters_));
+      fpart_grid_ = std::max(1, std::min(ftile_cap_, per_cu * num_cu_));
+    }
     fscan_lds_ = FrontierScanLds(max_bin_, has_cat_ ? max_cat_bin_ : 1);
     FrontierSetLds(FrontierHistLds(), fscan_lds_, use_dp_, width_);
     fspec_cap_ = 0;
@@ -1955,7 +1959,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.hslab = fhslab_.get();
     a.hslab_stride = fhslab_stride_;
     a.hmeta = fhmeta_.get();
-    a.red_grid = 2 * num_cu_;
+    a.red_grid = (num_tiles_ > 1 ? 4 : 2) * num_cu_;  // (wide data: many reduce items per round)
     a.ghmax = ghmax_.get();
     a.sum_mult = distributed_ && !ffeature_ ? std::max(1, P_) : 1;  // (max-reduced local sums)
     {

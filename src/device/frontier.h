@@ -322,6 +322,7 @@ void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
 void LaunchFrontierLazyCounts(const FArgs& a, hipStream_t s);
 void LaunchFrontierLazyMark(const FArgs& a, hipStream_t s);
 void LaunchFrontierPartition(const FArgs& a, int iters, int grid, hipStream_t s);  // one block per tile
+int FrontierPartitionBlocksPerCU(int iters);
 // voting parallel: local top-k per child (after the local-pass k_f_scan), election and
 // packing of the elected features' local rows (after the vote all-gather), global pass over
 // the summed rows (after their all-reduce)

@@ -528,6 +528,7 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   __shared__ int s_nb[kFrontierKmax], s_b0[kFrontierKmax], s_w0[kFrontierKmax + 1];
   __shared__ int s_tc[kRedMaxTiles + 1];  // chunk prefix over the LDS tiles (direct tiles: none)
   __shared__ int s_wc[kRedThreads / 64];
+  __shared__ int s_tb0[kRedMaxTiles], s_tnb[kRedMaxTiles];  // tiles' first bin / bin count
   const FState* sp = a.st;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   // one round of independent loads: state, expansion chunking fields, this thread's tile
@@ -536,6 +537,10 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   if (t < a.num_tiles) {
     const HistTile ty = a.tiles[t];
     tch = ty.direct ? 0 : (ty.nbins + kRedThreads - 1) / kRedThreads;
+    // (kept in LDS: a work item's tile record is then no dependent global load of its own --
+    // wide data runs many items per block, LambdaRank 5M x 300 ~12, each paying it)
+    s_tb0[t] = ty.bin0;
+    s_tnb[t] = ty.nbins;
   }
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
@@ -581,12 +586,12 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
     const int grp = r / nch, ch = r - grp * nch;
     int y = 0;
     while (y + 1 < a.num_tiles && s_tc[y + 1] <= ch) ++y;
-    const HistTile tile = a.tiles[y];
+    const int tbin0 = s_tb0[y];
     const int i = (ch - s_tc[y]) * kRedThreads + t;  // bin of the tile
-    if (i >= tile.nbins) continue;
+    if (i >= s_tnb[y]) continue;
     const int nb = s_nb[e];
     const int r0 = s_b0[e] + grp * kRedRows, r1 = min(s_b0[e] + nb, r0 + kRedRows);
-    const size_t col = static_cast<size_t>(sw) * (tile.bin0 + i);
+    const size_t col = static_cast<size_t>(sw) * (tbin0 + i);
     long long g = 0, h = 0;
     unsigned long long x0[kRedRows], x1[kRedRows];
 #pragma unroll
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
         h += static_cast<long long>(hv);
       }
     }
-    unsigned long long* out = a.acc + FAccAt(a, e, tile.bin0 + i, pw);
+    unsigned long long* out = a.acc + FAccAt(a, e, tbin0 + i, pw);
     if (nb <= kRedRows) {
       // the expansion's only row group: the accumulator is zero here (the scan re-zeroes it)
       if (g) out[0] = static_cast<unsigned long long>(g);
@@ -3110,6 +3115,16 @@ void LaunchFrontierPairBest(const FArgs& a, hipStream_t s) {
   HIP_CHECK(hipGetLastError());
 }
 
+
+// resident k_f_partition blocks per CU (occupancy of the instantiation the learner launches)
+int FrontierPartitionBlocksPerCU(int iters) {
+  int per_cu = 0;
+  const void* fn = iters == 4    ? reinterpret_cast<const void*>(k_f_partition<4, 1>)
+                   : iters == 16 ? reinterpret_cast<const void*>(k_f_partition<16, 1>)
+                                 : reinterpret_cast<const void*>(k_f_partition<8, 1>);
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kFPartThreads, 0));
+  return per_cu;
+}
 
 // one block per tile (A/B of the tile shapes at 1.25M / 10M rows: 1024-row tiles 884-886 it/s vs
 // 855 for two per block, 4096-row tiles at 10M 397.7 vs 394.3 for two 2048-row tiles per block)
