@@ -179,10 +179,28 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
 // row (row r starts at group r mod per): the 16 lanes of a bank group (two or three rows of the
 // dword-per-lane mapping) then hit different bank pairs, instead of colliding on random bins
 // ~3-4 ways (the row phase of a histogram is bound by these conflicts).
+// the first pipeline chunk's row indices of this thread (FHistRows' load_rows of its first chunk),
+// issued by k_f_hist before it zeroes its LDS histogram so the index round trip overlaps that
+constexpr int kFHistR2 = LGAP_FHIST_R / 2;
+__device__ __forceinline__ void FHistFirstRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
+                                               int* rn) {
+  const int tpr = tile.d1 - tile.d0;
+  const int rpi = blockDim.x / tpr;
+  const int myr = threadIdx.x / tpr;
+  const int* idx = buf < 0 ? nullptr : a.idx[buf] + start;
+  const int base = buf < 0 ? start : 0;
+#pragma unroll
+  for (int j = 0; j < kFHistR2; ++j) {
+    const int p = rb + myr + j * rpi;
+    rn[j] = myr < rpi && p < re ? (idx ? idx[p] : base + p) : -1;
+  }
+}
+
 template <int W, int MODE>
 __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, int buf, int start, int rb, int re,
                                           const int* gst, unsigned long long* hist, float sg, float sh, double dsg,
-                                          double dsh, uint32_t* hist32 = nullptr, int il_gp = 0) {
+                                          double dsh, uint32_t* hist32 = nullptr, int il_gp = 0,
+                                          const int* first_rows = nullptr) {
   const int tpr = tile.d1 - tile.d0;
   const int rpi = blockDim.x / tpr;
   const int myr = threadIdx.x / tpr;
@@ -219,6 +237,7 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   // waves of a block otherwise wait on their index -> row round trips in step with each other).
   // Rows past the range load nothing (row -1: word 0, no add).
   constexpr int R2 = R / 2;
+  static_assert(R2 == kFHistR2, "first-chunk prefetch width");
   const int step = rpi * R2;
   auto load_rows = [&](int p0, int* rows) {
 #pragma unroll
@@ -238,7 +257,12 @@ __device__ __forceinline__ void FHistRows(const FArgs& a, const HistTile& tile, 
   int rn[R2];
   uint32_t word[R2], q[R2];
   float2 v[R2];
-  load_rows(rb + myr, rn);
+  if (first_rows != nullptr) {
+#pragma unroll
+    for (int j = 0; j < R2; ++j) rn[j] = first_rows[j];
+  } else {
+    load_rows(rb + myr, rn);
+  }
   load_data(rn, word, v, q);
   load_rows(rb + myr + step, rn);
   for (int p0 = rb + myr; p0 < re; p0 += step) {
@@ -453,6 +477,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
                                               : hist + words);
   // (interleaved: the packed image the partial store reads, after gst)
   unsigned long long* packed = il_gp > 0 ? reinterpret_cast<unsigned long long*>(gst + ((ng + 1) & ~1)) : nullptr;
+  int first_rows[kFHistR2];
+  if (MODE != 3) FHistFirstRows(a, tile, buf, start, rb, re, first_rows);
   for (int i = t; i < words; i += blockDim.x) hist[i] = 0ull;
   if (MODE == 3) {
     for (int i = t; i < tile.nbins; i += blockDim.x) hist32[i] = 0u;
@@ -476,7 +502,7 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
       __syncthreads();
     }
   } else {
-    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh, nullptr, il_gp);
+    FHistRows<W, MODE>(a, tile, buf, start, rb, re, gst, hist, sg, sh, dsg, dsh, nullptr, il_gp, first_rows);
     __syncthreads();
   }
   if (il_gp > 0) {
@@ -3073,9 +3099,23 @@ void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
   const bool ext = a.voting || a.xrng != nullptr || a.fowned != nullptr;
   if (a.scan_wave && !ext && a.num_forced == 0) {
-    // one wave per item: enough blocks for every item of the widest round, at most 8 per CU's worth
-    const int grid = std::max(1, std::min((a.kmax * a.F + kFScanWaves - 1) / kFScanWaves, 2048));
-    k_f_scan_w<<<grid, kFScanWaves * 64, kFScanWaves * FrontierScanWaveBytes(a.max_bin, a.cat_p2), s>>>(a);
+    // one wave per item, items grid-strided over the RESIDENT blocks: a grid sized for the widest
+    // round (up to 2048 blocks) left most blocks without an item in a typical round, dispatched
+    // after the resident ones finished (the partition's tail, profiles/r05/ab_notes.md)
+    const size_t lds = kFScanWaves * FrontierScanWaveBytes(a.max_bin, a.cat_p2);
+    static thread_local size_t cached_lds = 0;
+    static thread_local int cached_resident = 0;
+    if (cached_lds != lds || cached_resident <= 0) {
+      int per_cu = 0, dev = 0, cus = 0;
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_f_scan_w),
+                                                             kFScanWaves * 64, lds));
+      HIP_CHECK(hipGetDevice(&dev));
+      HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      cached_lds = lds;
+      cached_resident = std::max(1, per_cu) * std::max(1, cus);
+    }
+    const int grid = std::max(1, std::min({(a.kmax * a.F + kFScanWaves - 1) / kFScanWaves, 2048, cached_resident}));
+    k_f_scan_w<<<grid, kFScanWaves * 64, lds, s>>>(a);
     HIP_CHECK(hipGetLastError());
     return;
   }

@@ -183,6 +183,8 @@ __global__ __launch_bounds__(kRootThreads) void k_root_sums(Args a) {
   const float2* gh = a.gh + static_cast<size_t>(tp.cls) * a.N;
   double v[kRootStats] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const int stride = gridDim.x * blockDim.x;
+  // (unrolled: four rows' loads in flight per thread; the per-thread sums keep their order)
+#pragma unroll 4
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tp.root_count; i += stride) {
     const float2 x = gh[RowAt(a, tp.root_buf, i)];
     v[0] += x.x;
