@@ -1262,3 +1262,63 @@ def test_speculation_budget_does_not_change_trees(lgb, gpu_required, monkeypatch
     assert model() == base  # timed tuner (>= 128 leaves, one process)
     assert model(LGAP_FRONTIER_ALPHA="3") == base
     assert model(LGAP_FRONTIER_ADAPT="1") == base
+
+
+_GPU_LOAD = r"""
+import sys, time
+import torch
+a = torch.randn(6144, 6144, device="cuda")
+b = torch.empty_like(a)
+torch.cuda.synchronize()
+print("ready", flush=True)
+t0 = time.time()
+while time.time() - t0 < float(sys.argv[1]):
+    for _ in range(8):
+        torch.matmul(a, a, out=b)
+    torch.cuda.synchronize()
+"""
+
+
+def test_training_under_concurrent_gpu_load(lgb, gpu_required):
+    """The frontier partition assumes nothing about co-residency: with another process's long
+    matmul kernels occupying CUs (fewer of the partition's blocks resident, look-backs waiting on
+    blocks that have not started), training completes and grows the same trees as without the
+    load (profiles/r05/ab_notes.md, resident partition grid)."""
+    import subprocess
+    import sys
+    import time
+
+    from lambdagap_amd.utils import make_higgs_like
+
+    X, y = make_higgs_like(2_000_000, seed=11)
+    params = {"objective": "binary", "num_leaves": 63, "device_type": "gpu", "verbosity": -1}
+
+    def model():
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 8)
+        s = b.model_to_string()
+        return s[:s.index("parameters:")]
+
+    ref = model()
+    load = subprocess.Popen([sys.executable, "-c", _GPU_LOAD, "60"], stdout=subprocess.PIPE, text=True)
+    try:
+        import select
+
+        t0 = time.time()
+        line = ""
+        while time.time() - t0 < 90 and load.poll() is None:
+            ready, _, _ = select.select([load.stdout], [], [], 1.0)
+            if ready:
+                line = load.stdout.readline()
+                if line.startswith("ready"):
+                    break
+        if not line.startswith("ready"):
+            pytest.skip("the GPU load process did not start (torch import / device unavailable)")
+        time.sleep(1.0)
+        t1 = time.time()
+        got = model()
+        assert load.poll() is None, "the load ended before training did"
+        assert got == ref
+        assert time.time() - t1 < 60
+    finally:
+        load.kill()
+        load.wait()
