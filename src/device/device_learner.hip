@@ -2222,13 +2222,13 @@ class DeviceTreeLearner : public TreeLearner {
   void EnqueueFrontier(int rounds, bool prologue) {
     const FArgs fa = MakeFArgs();
     if (prologue) {
-      LaunchFrontierInit(fa, stream_);
       Args ra = MakeArgs(0);
       ra.lsum = flsum_;  // root sums -> the root node; ghmax -> the fixed-point scales
       const int root_blocks = RootBlocks();
       k_root_sums<<<root_blocks, kRootThreads, 0, stream_>>>(ra);
-      k_root_final<<<1, kRootThreads, 0, stream_>>>(ra, root_blocks);
       HIP_CHECK(hipGetLastError());
+      // the tree setup and k_root_final's fold of the partials in one launch
+      LaunchFrontierInitRoot(fa, ra.root_part, root_blocks, ghmax_.get(), stream_);
       if (distributed_) {
         // global root sums and gradient maxima (the fixed-point scales must agree on all ranks)
         AllreduceSumF64(reinterpret_cast<double*>(flsum_), 2, stream_);

@@ -304,6 +304,8 @@ inline size_t FrontierResultBytes(int L) { return FrontierResultRangeOffset(L) +
 // launchers (frontier_kernels.hip)
 void LaunchFrontierResults(const FArgs& a, void* host_out, hipStream_t s);
 void LaunchFrontierInit(const FArgs& a, hipStream_t s);
+// k_f_init + the fold of seq::k_root_sums' per-block partials (k_root_final's order) in one launch
+void LaunchFrontierInitRoot(const FArgs& a, const double* root_part, int nblocks, unsigned* ghmax, hipStream_t s);
 void LaunchFrontierHist(const FArgs& a, size_t lds_bytes, hipStream_t s);  // k_f_hist + k_f_reduce
 int FrontierHistRows(int hist_grid, int kmax);  // k_f_hist's grid.x (partial slab rows)
 void LaunchFrontierScan(const FArgs& a, size_t lds_bytes, hipStream_t s);

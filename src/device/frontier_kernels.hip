@@ -94,7 +94,7 @@ __device__ __forceinline__ size_t FAccAt(const FArgs& a, int e, int b, int pw) {
 // ---------------------------------------------------------------------------
 // tree setup: the root node, the root "round" (one pseudo-expansion whose smaller child
 // is the root), the committed-leaf table and the node states.
-__global__ __launch_bounds__(256) void k_f_init(FArgs a) {
+__device__ __forceinline__ void FInitTree(const FArgs& a) {
   const TreeParams tp = *a.tp;
   const int t = threadIdx.x;
   if (t == 0) {
@@ -150,6 +150,51 @@ __global__ __launch_bounds__(256) void k_f_init(FArgs a) {
   }
   for (int i = t; i < a.C; i += blockDim.x) a.nstate[i] = 0;
   for (int f = t; f < a.F; f += blockDim.x) a.spl[f] = 1;
+}
+
+__global__ __launch_bounds__(256) void k_f_init(FArgs a) { FInitTree(a); }
+
+// The tree setup fused with the root statistics' final fold (one launch less per tree): the
+// per-block partials of seq::k_root_sums (sum g, sum h, max|g|, max|h|, sum|g|, sum|h|) folded in
+// exactly k_root_final's order -> the root's sums and the fixed-point scale bounds.
+constexpr int kRootStatsF = 6;
+__device__ __forceinline__ double FRootFold(int i, double x, double y) { return i == 2 || i == 3 ? fmax(x, y) : x + y; }
+__global__ __launch_bounds__(256) void k_f_init_root(FArgs a, const double* __restrict__ root_part, int nblocks,
+                                                     unsigned* __restrict__ ghmax) {
+  __shared__ double sh[kRootStatsF][256 / 64];
+  double v[kRootStatsF] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
+#pragma unroll
+    for (int j = 0; j < kRootStatsF; ++j) v[j] = FRootFold(j, v[j], root_part[kRootStatsF * b + j]);
+  }
+  FInitTree(a);
+#pragma unroll
+  for (int j = 0; j < kRootStatsF; ++j) {
+    if (j == 2 || j == 3) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v[j] = fmax(v[j], __shfl_xor(v[j], o, kWave));
+    } else {
+      v[j] = WaveSum(v[j]);
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int j = 0; j < kRootStatsF; ++j) sh[j][w] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < static_cast<int>(blockDim.x / 64); ++i) {
+#pragma unroll
+      for (int j = 0; j < kRootStatsF; ++j) v[j] = FRootFold(j, v[j], sh[j][i]);
+    }
+    a.lsum[0] = make_double2(v[0], v[1]);
+    ghmax[0] = __float_as_uint(static_cast<float>(v[2]));
+    ghmax[1] = __float_as_uint(static_cast<float>(v[3]));
+    // (the fp64 sums of |value| are exact to ~1e-9 relative: a 2^-20 margin, rounded up)
+    ghmax[2] = __float_as_uint(__double2float_ru(v[4] * (1.0 + 0x1p-20)));
+    ghmax[3] = __float_as_uint(__double2float_ru(v[5] * (1.0 + 0x1p-20)));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3092,6 +3137,11 @@ void LaunchFrontierLazyCounts(const FArgs& a, hipStream_t s) {
 
 void LaunchFrontierLazyMark(const FArgs& a, hipStream_t s) {
   k_f_lazy_mark<<<dim3(16, a.L), 256, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierInitRoot(const FArgs& a, const double* root_part, int nblocks, unsigned* ghmax, hipStream_t s) {
+  k_f_init_root<<<1, 256, 0, s>>>(a, root_part, nblocks, ghmax);
   HIP_CHECK(hipGetLastError());
 }
 
