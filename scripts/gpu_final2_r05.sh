@@ -24,6 +24,6 @@ run bench40 300 python bench.py --steps 40 --warmup 5
 run b1p25 300 python bench.py --rows 1250000 --steps 50 --warmup 5
 run b1m 300 python bench.py --rows 1000000 --steps 50 --warmup 5
 run owner1p25 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp
-run st10 300 env LGAP_FSTAMPS=1 LGAP_FRONTIER_STATS=1 python bench.py --steps 10 --warmup 1
+run st10 300 env LGAP_FSTAMPS=1 python bench.py --steps 10 --warmup 1
 run prof 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run -- python3 bench.py --steps 20 --warmup 3
 python scripts/prof_summary.py $OUT/prof "Headline 10M x 28, 63 leaves (round-5 final)" 23 > $OUT/prof_summary.md 2>&1; rm -rf $OUT/prof

@@ -18,8 +18,8 @@ run() {  # run <name> <limit> <cmd...>
   grep -E "^\{|fstamps|frontier:" $OUT/$name.log | cut -c1-400 >> $OUT/steps.log
   [ $rc -eq 0 ] || exit $rc
 }
-LGAP_FSTAMPS=1 LGAP_FRONTIER_STATS=1 run st10 300 python bench.py --steps 10 --warmup 1
-LGAP_FSTAMPS=1 LGAP_FRONTIER_STATS=1 run st1p25 300 python bench.py --rows 1250000 --steps 20 --warmup 3
+LGAP_FSTAMPS=1 run st10 300 python bench.py --steps 10 --warmup 1
+LGAP_FSTAMPS=1 run st1p25 300 python bench.py --rows 1250000 --steps 20 --warmup 3
 run pdp 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/pdp -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 3 --rehearse-dp
 python scripts/prof_summary.py $OUT/pdp "owner-computes DP rehearsal, 1.25M x 28, one-rank RCCL" 23 > $OUT/pdp_summary.md 2>&1; rm -rf $OUT/pdp
 run p1p25 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/p1 -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 3

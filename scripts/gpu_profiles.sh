@@ -17,5 +17,5 @@ prof p1 "1.25M x 28 (per-rank share at N=8), 63 leaves, frontier engine, round 3
 prof pq "10M x 28, 63 leaves, use_quantized_grad (int8-level histograms), round 3" 23 python3 bench.py --steps 20 --warmup 3 --quantized
 prof pltr "LambdaRank 5M x 300, 255 leaves, frontier engine, 150 KB LDS tiles, round 3 (bench_suite --steps 10 --warmup 5)" 15 python3 scripts/bench_suite.py --config ltr --rows 5000000 --steps 10 --warmup 5
 prof pgoss "regression EFB+GOSS 12.5M x 500, 255 leaves, quantized, round 3 (bench_suite --steps 10 --warmup 12)" 22 python3 scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --steps 10 --warmup 12 --quantized
-LGAP_FSTAMPS=1 LGAP_FRONTIER_STATS=1 timeout -k 10 300 python bench.py --steps 10 --warmup 1 > $OUT/st10.log 2>&1 || exit $?
+LGAP_FSTAMPS=1 timeout -k 10 300 python bench.py --steps 10 --warmup 1 > $OUT/st10.log 2>&1 || exit $?
 grep -E "fstamps|frontier:" $OUT/st10.log

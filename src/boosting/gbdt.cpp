@@ -265,9 +265,10 @@ void GBDT::UpdateScore(const Tree* tree, int k) {
 // mode "exit" ends the process at once (no cleanup, sockets / communicator
 // dropped), "hang" stops it in place so its peers' timeouts / the collective
 // watchdog must notice, "throw" raises a fatal error through the normal path.
+// LGAP_FAULT_INJECT=xgmi is the device learner's: its in-kernel xGMI exchange never signals.
 static void MaybeInjectFault(int iter) {
   static const char* spec = std::getenv("LGAP_FAULT_INJECT");
-  if (spec == nullptr || *spec == '\0') return;
+  if (spec == nullptr || *spec == '\0' || std::strcmp(spec, "xgmi") == 0) return;
   int rank = -1, at = -1;
   char mode[16] = {0};
   if (std::sscanf(spec, "%d:%d:%15s", &rank, &at, mode) != 3) Log::Fatal("Malformed LGAP_FAULT_INJECT=%s", spec);

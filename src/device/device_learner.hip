@@ -1632,7 +1632,7 @@ class DeviceTreeLearner : public TreeLearner {
   // contiguous, bin-balanced group ranges), so each rank receives only the summed bins of its own
   // features (half the bytes of the all-reduce) and scans only those (1/P of the scan work); each
   // child's best over the owned features is all-gathered and the best over ranks becomes the
-  // child's candidate (the feature-parallel exchange, k_f_pair_best / k_f_pair_merge); every rank
+  // child's candidate (the feature-parallel exchange: k_f_pair_best, then the select's phase A); every rank
   // then selects redundantly from identical candidates. Reference:
   // data_parallel_tree_learner.cpp:284-297 (ReduceScatter of the smaller leaf's histograms by
   // feature ownership), :305-450 (owner scans, SyncUpGlobalBestSplit). Raw per-feature candidates
@@ -1646,7 +1646,7 @@ class DeviceTreeLearner : public TreeLearner {
   // Voting-parallel frontier (PV-Tree per round): the local pass of every expansion's children,
   // one all-gather of the round's top-k vote records, the election, one exact integer
   // all-reduce of only the elected features' rows, and the global pass over them; every rank
-  // then selects redundantly, as the data-parallel frontier does. LGAP_FRONTIER_VOTING=0 or an
+  // then selects redundantly, as the data-parallel frontier does. An
   // explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain (its in-kernel xGMI exchange).
   // Reference: voting_parallel_tree_learner.cpp:243-399.
   bool FrontierVoting() const {
@@ -1656,7 +1656,7 @@ class DeviceTreeLearner : public TreeLearner {
   }
   // Feature-parallel frontier: every rank holds all rows and grows the same partition and
   // histograms; the scans cover this rank's features (the groups it owns), each child's best is
-  // all-gathered and the best over ranks is the child's candidate. LGAP_FRONTIER_FEATURE=0 or
+  // all-gathered and the best over ranks is the child's candidate. An
   // an explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain.
   // Reference: feature_parallel_tree_learner.cpp:23-80.
   bool FrontierFeature() const {
@@ -1885,26 +1885,30 @@ class DeviceTreeLearner : public TreeLearner {
     fhist_threads_ = big_tiles_ || (num_tiles_ == 1 && N_ >= 4000000) ? 1024 : 512;
     if (const char* e = std::getenv("LGAP_FHIST_THREADS")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
     fpolicy_ = 1;
-    // speculation budget: every eligible node within the remaining splits (alpha 1). The
-    // waste-driven throttle (LGAP_FRONTIER_ADAPT=1: alpha x0.75 while > 12% of the partitioned
+    // speculation budget: every eligible node within the remaining splits (alpha 1). One knob,
+    // LGAP_FRONTIER_SPEC, picks another budget for A/B: "fixed" (alpha 1, no tuner), a number
+    // (that fixed alpha) or "adapt". The
+    // waste-driven throttle ("adapt": alpha x0.75 while > 12% of the partitioned
     // rows go to never-committed expansions) trades rows for rounds and loses where rounds cost
     // more than rows: 255 leaves x 500 iterations at 10M, 93.5 it/s adaptive vs 141.4 fixed
     // (139 vs 76 rounds per tree); 1.25M x 150 iterations, 2.07 vs 1.73 ms per iteration
     fspec_alpha_ = 1.0;
-    fspec_fixed_ = std::getenv("LGAP_FRONTIER_ADAPT") == nullptr;
-    if (const char* e = std::getenv("LGAP_FRONTIER_ALPHA")) {  // fixed speculation depth (A/B)
-      fspec_alpha_ = std::max(0.01, std::min(4.0, std::atof(e)));
-      fspec_fixed_ = true;
+    const char* spec_env = std::getenv("LGAP_FRONTIER_SPEC");
+    const std::string spec = spec_env != nullptr ? spec_env : "";
+    fspec_fixed_ = spec != "adapt";
+    if (!spec.empty() && spec != "adapt" && spec != "fixed") {  // a fixed speculation depth (A/B)
+      char* end = nullptr;
+      const double alpha = std::strtod(spec.c_str(), &end);
+      if (end == spec.c_str() || *end != '\0') Log::Fatal("LGAP_FRONTIER_SPEC=%s: expected fixed|adapt|<alpha>", spec.c_str());
+      fspec_alpha_ = std::max(0.01, std::min(4.0, alpha));
     }
-    // timed speculation tuner: one process, >= 128 leaves, no fixed alpha / throttle requested
+    // timed speculation tuner: one process, >= 128 leaves, no other budget requested
     {
-      const char* tn = std::getenv("LGAP_FRONTIER_TUNE");
       stune_ = SpecTuner();
       // (not with raw CEGB candidates or forced splits: there the select's replay of speculated
       // expansions depends on what was speculated, and the budget must not follow wall-clock time)
       stune_.on = !distributed_ && L_ >= 128 && !RawCands() && fnum_forced_ == 0 &&
-                  std::getenv("LGAP_FRONTIER_ALPHA") == nullptr && std::getenv("LGAP_FRONTIER_ADAPT") == nullptr &&
-                  !(tn != nullptr && tn[0] == '0');
+                  spec.empty();
     }
     if (std::getenv("LGAP_FSTAMPS")) {
       fstamps_.Resize(256 * 4 * kFStampSlots);
@@ -2384,7 +2388,7 @@ class DeviceTreeLearner : public TreeLearner {
       ++fkused_trees_;
     }
     if (fstamps_.size() && fstat_trees_ == 3) ReportFrontierStamps(hs->round);
-    if (std::getenv("LGAP_FRONTIER_STATS") && fstat_trees_ % 10 == 0) {
+    if (fstamps_.size() && fstat_trees_ % 10 == 0) {  // (LGAP_FSTAMPS: stamps and round statistics)
       std::fprintf(stderr, "frontier: %d trees, %.2f rounds/tree, %.2f expansions/tree (%d leaves max), wasted rows %.1f%%, "
                    "alpha %.3f, all-reduced expansion slots/tree %.1f, pipelined rounds/tree %.2f\n", fstat_trees_,
                    static_cast<double>(fstat_rounds_) / fstat_trees_, static_cast<double>(fstat_spec_) / fstat_trees_, L_,
@@ -3678,7 +3682,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.xcnt = xcnt_.get();
     a.xsession = xsession_;
     a.xtimeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
-    a.xfault = std::getenv("LGAP_XGMI_FAULT") != nullptr && std::getenv("LGAP_XGMI_FAULT")[0] == '1';
+    a.xfault = std::getenv("LGAP_FAULT_INJECT") != nullptr && std::strcmp(std::getenv("LGAP_FAULT_INJECT"), "xgmi") == 0;
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;

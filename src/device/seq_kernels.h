@@ -145,7 +145,7 @@ struct Args {
   unsigned* xcnt;       // local arrival counters of the exchanges [4]
   unsigned xsession;    // high word of the exchange tags (new per learner state)
   unsigned long long xtimeout;  // bound of an exchange wait (wall_clock64 ticks, 100 MHz)
-  int xfault;           // LGAP_XGMI_FAULT=1: never signal (failure-detection tests)
+  int xfault;           // LGAP_FAULT_INJECT=xgmi: never signal (failure-detection tests)
   // ---- voting parallel (tree_learner=voting): local scan, top-k vote, elected histograms
   int vote;             // 1: k_reduce_scan is the LOCAL pass (local sums / counts, no masks or penalties)
   double2* hsum_part;   // [hist blocks] local (sum g, sum h) of the smaller child's rows per k_hist block

@@ -775,7 +775,7 @@ def test_collective_watchdog_aborts_on_timeout(lgb, gpu_required):
 
 
 def test_xgmi_exchange_timeout_raises(lgb, gpu_required):
-    """xGMI transport failure detection: a rank that stops signalling (LGAP_XGMI_FAULT=1 drops
+    """xGMI transport failure detection: a rank that stops signalling (LGAP_FAULT_INJECT=xgmi drops
     every flag after the set-up self-test) makes the in-kernel exchange wait run into its bound;
     the learner raises instead of hanging the GPU."""
     import json
@@ -784,7 +784,7 @@ def test_xgmi_exchange_timeout_raises(lgb, gpu_required):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, LGAP_DP_TRANSPORT="xgmi", LGAP_XGMI_FAULT="1", LGAP_XGMI_TIMEOUT_S="0.5",
+    env = dict(os.environ, LGAP_DP_TRANSPORT="xgmi", LGAP_FAULT_INJECT="xgmi", LGAP_XGMI_TIMEOUT_S="0.5",
                LGAP_COMM_TIMEOUT_S="120")
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "watchdog_selftest.py")], capture_output=True,
                        env=env, text=True, timeout=300)
@@ -1250,18 +1250,17 @@ def test_speculation_budget_does_not_change_trees(lgb, gpu_required, monkeypatch
               "verbosity": -1, "seed": 4, "deterministic": True}
 
     def model(**env):
-        for k in ("LGAP_FRONTIER_ALPHA", "LGAP_FRONTIER_TUNE", "LGAP_FRONTIER_ADAPT"):
-            monkeypatch.delenv(k, raising=False)
+        monkeypatch.delenv("LGAP_FRONTIER_SPEC", raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         b = lgb.train(params, lgb.Dataset(X, y, params=params), 30, keep_training_booster=True)
         assert "frontier engine" in b.device_name()
         return b.model_to_string()
 
-    base = model(LGAP_FRONTIER_TUNE="0")
+    base = model(LGAP_FRONTIER_SPEC="fixed")
     assert model() == base  # timed tuner (>= 128 leaves, one process)
-    assert model(LGAP_FRONTIER_ALPHA="3") == base
-    assert model(LGAP_FRONTIER_ADAPT="1") == base
+    assert model(LGAP_FRONTIER_SPEC="3") == base
+    assert model(LGAP_FRONTIER_SPEC="adapt") == base
 
 
 _GPU_LOAD = r"""
