@@ -114,6 +114,38 @@ namespace lgap {
 namespace device {
 namespace {
 
+// Kernel-variant overrides for the coverage tests and A/B runs, all in one knob:
+// LGAP_KERNEL="key=value,key=value" with the keys fhist_threads (512 | 1024), hist_lds_kb (LDS
+// tile budget), quant_lds32 (0 | 1), part_iters (4 | 8 | 16), hist_il (0 | 1), nibble (0: 8-bit
+// rows), quant_hist (off: float histograms under quantized training), scan_global (1). Returns
+// the key's value, nullptr when it is not set. Read at each use: tests change the environment
+// between trainings in one process.
+const char* KernelOverride(const char* key) {
+  static const char* const kKeys[] = {"fhist_threads", "hist_lds_kb", "quant_lds32", "part_iters",
+                                      "hist_il",       "nibble",      "quant_hist",  "scan_global"};
+  thread_local std::string val;
+  const char* e = std::getenv("LGAP_KERNEL");
+  if (e == nullptr) return nullptr;
+  const std::string s(e);
+  const char* found = nullptr;
+  for (size_t p = 0; p < s.size();) {
+    size_t q = s.find(',', p);
+    if (q == std::string::npos) q = s.size();
+    const std::string item = s.substr(p, q - p);
+    const size_t eq = item.find('=');
+    const std::string k = item.substr(0, eq);
+    bool known = false;
+    for (const char* kk : kKeys) known = known || k == kk;
+    if (!known) Log::Fatal("LGAP_KERNEL: unknown key '%s'", k.c_str());
+    if (k == key) {
+      val = eq == std::string::npos ? "1" : item.substr(eq + 1);
+      found = val.c_str();
+    }
+    p = q + 1;
+  }
+  return found;
+}
+
 
 using namespace seq;  // NOLINT: the sequential chain's kernels and argument block
 
@@ -1883,7 +1915,7 @@ class DeviceTreeLearner : public TreeLearner {
     // quantized 405.6 vs 398.3; at 1.25M mixed (737.9 / 778.4 vs 779.2 / 770.0). Multi-tile rows
     // keep 512 (two resident 56 KB blocks per CU); 150 KB tiles hold one block per CU.
     fhist_threads_ = big_tiles_ || (num_tiles_ == 1 && N_ >= 4000000) ? 1024 : 512;
-    if (const char* e = std::getenv("LGAP_FHIST_THREADS")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
+    if (const char* e = KernelOverride("fhist_threads")) fhist_threads_ = std::atoi(e) == 1024 ? 1024 : 512;
     fpolicy_ = 1;
     // speculation budget: every eligible node within the remaining splits (alpha 1). One knob,
     // LGAP_FRONTIER_SPEC, picks another budget for A/B: "fixed" (alpha 1, no tuner), a number
@@ -2007,7 +2039,7 @@ class DeviceTreeLearner : public TreeLearner {
       a.qpack = rows * gl < 2147483647.0 && rows * hl < 4294967295.0 ? 1 : 0;
       // g16|h16 LDS bins: a sub-chunk's per-bin level sums stay within the 16-bit fields
       const int sub = static_cast<int>(std::min(32767.0 / gl, 65535.0 / hl));
-      const char* e = std::getenv("LGAP_QUANT_LDS32");  // A/B knob: 0 keeps the 64-bit LDS bins
+      const char* e = KernelOverride("quant_lds32");  // A/B knob: 0 keeps the 64-bit LDS bins
       // single-tile data only: the 1.5x LDS would drop multi-tile grids (several blocks per
       // CU) to one resident block (A/B, 12.5M x 500 GOSS: 87.7 it/s with 64-bit bins, 80.0)
       const bool want = e != nullptr ? e[0] != '0' : num_tiles_ == 1;
@@ -2612,7 +2644,7 @@ class DeviceTreeLearner : public TreeLearner {
   // uint8 h levels, i.e. num_grad_quant_bins <= 254.
   bool QuantHist() const {
     return config_->use_quantized_grad && std::max(2, config_->num_grad_quant_bins) <= 254 &&
-           std::getenv("LGAP_QUANT_HIST") == nullptr;  // LGAP_QUANT_HIST=off: A/B against float histograms
+           KernelOverride("quant_hist") == nullptr;  // LGAP_KERNEL=quant_hist=off: A/B against float histograms
   }
 
   void RenewQuantizedLeaves(Tree* tree) {
@@ -3019,9 +3051,9 @@ class DeviceTreeLearner : public TreeLearner {
   // Fused-partition tile: 8 rows per thread from 8M rows per GPU up, 4 below (A/B:
   // 10M 227 it/s at 8 vs 225 at 4 vs 214 at 16; 5M 3.42 ms/iter at 4 vs 3.48 at 8;
   // 2.5M 2.83 vs 2.92; 1.25M 390 it/s at 4 vs 368 at 8 vs 330 at 16).
-  // LGAP_PART_ITERS (4 / 8 / 16) overrides.
+  // LGAP_KERNEL=part_iters=4 / 8 / 16 overrides.
   int PartIters() const {
-    if (const char* e = std::getenv("LGAP_PART_ITERS")) {
+    if (const char* e = KernelOverride("part_iters")) {
       const int v = std::atoi(e);
       if (v == 4 || v == 8 || v == 16) return v;
     }
@@ -3176,11 +3208,11 @@ class DeviceTreeLearner : public TreeLearner {
   // rows keep the dataset's stride
   int StrideOf(const uint32_t* rb) const { return rb == rowbins_.get() ? tstride_dw_ : stride_dw_; }
 
-  // bank-interleaved LDS histograms (frontier MODE 0 / 2; LGAP_HIST_IL=0: packed bins)
+  // bank-interleaved LDS histograms (frontier MODE 0 / 2; LGAP_KERNEL=hist_il=0: packed bins)
   // (1: the root round's contiguous rows only, 2: every round; default 1 from 4M rows: A/B one
   // box, 10M 2.864 / 2.885 / 2.875 ms for 1 / 2 / 0, 1.25M 1.358 / 1.375 / 1.341)
   int HistInterleave() const {
-    const char* e = std::getenv("LGAP_HIST_IL");
+    const char* e = KernelOverride("hist_il");
     return e != nullptr ? std::atoi(e) : (N_ >= (4 << 20) ? 1 : 0);
   }
 
@@ -3273,7 +3305,7 @@ class DeviceTreeLearner : public TreeLearner {
     scan_lds_bytes_ = static_cast<size_t>(max_bin_) * 4 * sizeof(double) + 16 * 64 * sizeof(double) +
                       static_cast<size_t>(cat_p2_) * 2 * (sizeof(int) + sizeof(double));
     // wider than the LDS budget: the scan kernels work in global scratch (one slice per block)
-    scan_global_ = scan_lds_bytes_ > 150 * 1024 || std::getenv("LGAP_SCAN_GLOBAL") != nullptr;
+    scan_global_ = scan_lds_bytes_ > 150 * 1024 || KernelOverride("scan_global") != nullptr;
     scan_scratch_stride_ = Round256(scan_lds_bytes_);
     if (scan_global_) {
       scan_scratch_.Resize(scan_scratch_stride_ * static_cast<size_t>(std::max(F_, 1)));
@@ -3297,7 +3329,7 @@ class DeviceTreeLearner : public TreeLearner {
   void BuildTiles() {
     row_align_ = RowAlign();
     const int env_kb = [] {
-      const char* e = std::getenv("LGAP_HIST_LDS_KB");  // A/B / test knob: LDS tile budget
+      const char* e = KernelOverride("hist_lds_kb");  // A/B / test knob: LDS tile budget
       return e ? std::max(16, std::min(150, std::atoi(e))) : 0;
     }();
     big_tiles_ = false;
@@ -3325,7 +3357,7 @@ class DeviceTreeLearner : public TreeLearner {
   // rows stay for everything else (validation sets, the sequential chain, device binning).
   void BuildNibbleRows() {
     nib_ = false;
-    const char* e = std::getenv("LGAP_NIBBLE");  // A/B knob: 0 keeps 8-bit rows
+    const char* e = KernelOverride("nibble");  // A/B knob: 0 keeps 8-bit rows
     if (e != nullptr && e[0] == '0') return;
     if (width_ != 1 || num_tiles_ != 1 || G_ <= 0 || N_ <= 0 || h_tiles_.empty() || h_tiles_[0].direct) return;
     for (int g = 0; g < G_; ++g) {

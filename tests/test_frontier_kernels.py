@@ -51,13 +51,13 @@ def _subsets(rng, n):
 
 
 CASES = {
-    "fixed_point_1024": ({}, {"LGAP_FHIST_THREADS": "1024"}),
-    "fixed_point_512_many_tiles": ({}, {"LGAP_FHIST_THREADS": "512", "LGAP_HIST_LDS_KB": "16"}),
+    "fixed_point_1024": ({}, {"LGAP_KERNEL": "fhist_threads=1024"}),
+    "fixed_point_512_many_tiles": ({}, {"LGAP_KERNEL": "fhist_threads=512,hist_lds_kb=16"}),
     "fp64": ({"gpu_use_dp": True}, {}),
-    "quantized_lds64": ({"use_quantized_grad": True, "num_grad_quant_bins": 4}, {"LGAP_QUANT_LDS32": "0"}),
-    "quantized_lds32": ({"use_quantized_grad": True, "num_grad_quant_bins": 16}, {"LGAP_QUANT_LDS32": "1"}),
+    "quantized_lds64": ({"use_quantized_grad": True, "num_grad_quant_bins": 4}, {"LGAP_KERNEL": "quant_lds32=0"}),
+    "quantized_lds32": ({"use_quantized_grad": True, "num_grad_quant_bins": 16}, {"LGAP_KERNEL": "quant_lds32=1"}),
     "four_bit_rows": ({"max_bin": 15}, {}),
-    "direct_tiles": ({"max_bin": 3000, "min_data_in_bin": 1}, {"LGAP_HIST_LDS_KB": "16"}),
+    "direct_tiles": ({"max_bin": 3000, "min_data_in_bin": 1}, {"LGAP_KERNEL": "hist_lds_kb=16"}),
 }
 
 
@@ -105,7 +105,7 @@ def test_frontier_histogram_matches_index_add(lgb, gpu_required, rng, monkeypatc
 def test_frontier_partition_matches_host(lgb, gpu_required, rng, monkeypatch, part_iters):
     from lambdagap_amd import ops
 
-    monkeypatch.setenv("LGAP_PART_ITERS", part_iters)
+    monkeypatch.setenv("LGAP_KERNEL", f"part_iters={part_iters}")
     X, y = _data(rng, n=60_000)
     base = {"objective": "binary", "num_leaves": 31, "verbosity": -1, "device_type": "gpu"}
     ds = lgb.Dataset(X, y, params=base, categorical_feature=[3]).construct()

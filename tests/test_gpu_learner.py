@@ -470,7 +470,7 @@ def test_device_quantized_integer_histograms(lgb, gpu_required, rng, bins, monke
     """Quantized training on the frontier engine builds integer-level histograms (int8 g /
     uint8 h per row, packed g32|h32 sums): with deterministic rounding the whole first tree
     matches the host quantized learner, and the model matches the float-histogram path
-    (LGAP_QUANT_HIST=off) in accuracy."""
+    (LGAP_KERNEL=quant_hist=off) in accuracy."""
     X, z = _policy_data(rng)
     y = (z > 0).astype(float)
     d = {"use_quantized_grad": True, "num_grad_quant_bins": bins, "stochastic_rounding": False}
@@ -482,7 +482,7 @@ def test_device_quantized_integer_histograms(lgb, gpu_required, rng, bins, monke
     q = {"use_quantized_grad": True, "num_grad_quant_bins": bins}
     a_int = _auc(y, _train(lgb, X, y, "gpu", rounds=30, **q).predict(X))
     a_cpu = _auc(y, _train(lgb, X, y, "cpu", rounds=30, **q).predict(X))
-    monkeypatch.setenv("LGAP_QUANT_HIST", "off")
+    monkeypatch.setenv("LGAP_KERNEL", "quant_hist=off")
     a_flt = _auc(y, _train(lgb, X, y, "gpu", rounds=30, **q).predict(X))
     assert abs(a_int - a_cpu) < 5e-3, (a_int, a_cpu)
     assert abs(a_int - a_flt) < 5e-3, (a_int, a_flt)
@@ -933,7 +933,7 @@ def test_device_categorical_wide(lgb, gpu_required, rng, ncat, onehot):
 
 def test_device_max_bin_8191_global_scan(lgb, gpu_required, rng):
     """max_bin=8191: the split scan works in global scratch (features wider than the LDS budget)
-    and matches the CPU learner; the same global path forced on ordinary bins (LGAP_SCAN_GLOBAL)
+    and matches the CPU learner; the same global path forced on ordinary bins (LGAP_KERNEL=scan_global=1)
     grows the model of the sequential chain's LDS path."""
     import os
     import subprocess
@@ -956,7 +956,7 @@ def test_device_max_bin_8191_global_scan(lgb, gpu_required, rng):
     outs = []
     # the global-memory scan is a variant of the sequential device chain (the frontier engine has
     # no global-scan variant): compare it with that chain's LDS scan
-    for env in ({"LGAP_FRONTIER": "0"}, {"LGAP_FRONTIER": "0", "LGAP_SCAN_GLOBAL": "1"}):
+    for env in ({"LGAP_FRONTIER": "0"}, {"LGAP_FRONTIER": "0", "LGAP_KERNEL": "scan_global=1"}):
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                            env=dict(os.environ, **env))
         assert r.returncode == 0, r.stderr[-2000:]
@@ -1031,7 +1031,7 @@ def test_frontier_engine_matches_sequential_chain(lgb, gpu_required, rng, extra)
 def test_four_bit_rows_match_byte_rows(lgb, gpu_required, rng, monkeypatch, max_bin):
     """max_bin <= 15: the frontier histograms and the training score update read 4-bit rows
     (8 groups per dword, traverse_kernels.hip LaunchPackNibbles); the model is identical to the
-    one grown from the 8-bit rows (LGAP_NIBBLE=0), trees and training predictions."""
+    one grown from the 8-bit rows (LGAP_KERNEL=nibble=0), trees and training predictions."""
     n = 30000
     X = rng.standard_normal((n, 11))
     X[rng.random(n) < 0.05, 3] = np.nan
@@ -1039,7 +1039,7 @@ def test_four_bit_rows_match_byte_rows(lgb, gpu_required, rng, monkeypatch, max_
     params = {"objective": "binary", "num_leaves": 31, "max_bin": max_bin, "device_type": "gpu", "verbosity": -1}
     models = []
     for nib in ("1", "0"):
-        monkeypatch.setenv("LGAP_NIBBLE", nib)
+        monkeypatch.setenv("LGAP_KERNEL", f"nibble={nib}")
         b = lgb.train(params, lgb.Dataset(X, y, params=params), 10)
         models.append((b.model_to_string().split("end of trees")[0], b.predict(X, raw_score=True)))
     assert models[0][0] == models[1][0]
@@ -1234,7 +1234,7 @@ def test_interleaved_root_histogram_rows_4m(lgb, gpu_required, quantized, monkey
         return b.model_to_string()
 
     with_il = model()
-    monkeypatch.setenv("LGAP_HIST_IL", "0")
+    monkeypatch.setenv("LGAP_KERNEL", "hist_il=0")
     assert model() == with_il
 
 
