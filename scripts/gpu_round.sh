@@ -21,6 +21,10 @@ for s in "$@"; do
     info) step info 300 python -c "import lambdagap_amd as l; print('devices', l.device_count())";;
     kernels) step kernels 900 python -m pytest tests/test_gpu_kernels.py -q --timeout 300 -p no:cacheprovider;;
     dp1) step dp1 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "single_rank";;
+    xg) step xg 1000 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "xgmi or single_rank";;
+    xgbench) step x1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_DP_TRANSPORT=xgmi step x1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=collective step x1coll 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && step x10single 300 python bench.py --steps 30 --warmup 3 && LGAP_DP_TRANSPORT=xgmi step x10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp;;
+    xgq) LGAP_DP_TRANSPORT=xgmi step x1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=xgmi step x10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp && step x1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5;;
+    xgprof) LGAP_DP_TRANSPORT=xgmi step xgprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/xgprof -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 --rehearse-dp && python scripts/prof_summary.py $OUT/xgprof "1.25M rows, DP frontier xGMI (1 rank)" 22 > $OUT/xgprof_summary.md;;
     dpmulti) step dpmulti 1100 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank";;
     fp) step fp 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "feature_parallel";;
     dpbench) step b1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_DP_TRANSPORT=xgmi step b1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=collective step b1coll 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && step b10single 300 python bench.py --steps 30 --warmup 3 && LGAP_DP_TRANSPORT=xgmi step b10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp;;

@@ -219,6 +219,8 @@ class DeviceTreeLearner : public TreeLearner {
     if (fcont_) (void)hipGraphExecDestroy(fcont_);
     if (!x_peers_.empty()) XgmiClose(x_local_, &x_peers_);
     if (x_local_) (void)hipFree(x_local_);
+    if (!fx_peers_.empty()) XgmiClose(fx_local_, &fx_peers_);
+    if (fx_local_) (void)hipFree(fx_local_);
     for (auto& ev : pipe_ev_) {
       if (ev) (void)hipEventDestroy(ev);
     }
@@ -363,9 +365,16 @@ class DeviceTreeLearner : public TreeLearner {
     if (want != "auto" && want != "xgmi" && want != "collective" && want != "allreduce") {
       Log::Fatal("LGAP_DP_TRANSPORT=%s: expected auto|xgmi|collective|allreduce", want.c_str());
     }
-    // the data-parallel frontier engine exchanges through collectives (no xGMI owner buffers):
-    // owner reduce-scatter (auto / collective) or the per-round all-reduce (allreduce)
-    if (want == "collective" || want == "allreduce" || P_ > kMaxXRanks || (frontier_ && want == "auto")) return;
+    // the distributed frontier engine: the in-kernel xGMI exchange (auto / xgmi) where its
+    // exchanges are the owner histogram chunks and the per-child bests (owner-computes data
+    // parallel, feature parallel); collectives otherwise (collective, allreduce, voting, raw
+    // per-feature candidates)
+    if (frontier_) {
+      if ((want == "auto" || want == "xgmi") && (fowner_ || ffeature_) && P_ <= kMaxXRanks) SetupFrontierXgmi(want == "xgmi");
+      else if (want == "xgmi") Log::Warning("xGMI transport: this frontier configuration exchanges through collectives");
+      return;
+    }
+    if (want == "collective" || want == "allreduce" || P_ > kMaxXRanks) return;
     const size_t es = use_dp_ ? sizeof(double) : sizeof(float);
     ArenaLayout lay;
     x_off_hist_ = static_cast<int>(lay.Add<char>(static_cast<size_t>(P_) * 2 * bbin_ * es));
@@ -421,6 +430,69 @@ class DeviceTreeLearner : public TreeLearner {
     InvalidateGraph();
   }
 
+  // The distributed frontier's in-kernel exchange (FArgs::xg): one uncached exchange buffer per
+  // rank at identical offsets -- [receive chunk: kmax x owned bins x 2 words][per-child best
+  // records: P x 2 kmax][root rows: P][flags: kinds x P] -- IPC-mapped by every peer, then a
+  // self-test of remote atomics, stores and the handshake on every rank. Any failure on any rank
+  // keeps the collectives on all ranks (fatal when LGAP_DP_TRANSPORT=xgmi asked for it).
+  // Reference: data_parallel_tree_learner.cpp:284-298 (ReduceScatter of the histograms by owner),
+  // :443 (SyncUpGlobalBestSplit); here both are pushes from the producing kernels.
+  void SetupFrontierXgmi(bool required) {
+    const size_t recv_words = std::max<size_t>(static_cast<size_t>(kFrontierKmax) * bbin_ * 2, 8192);
+    ArenaLayout lay;
+    fxo_recv_ = static_cast<unsigned>(lay.Add<unsigned long long>(recv_words));
+    fxo_fpb_ = static_cast<unsigned>(lay.Add<FPairBest>(static_cast<size_t>(P_) * 2 * kFrontierKmax));
+    fxo_root_ = static_cast<unsigned>(lay.Add<FXRoot>(kMaxXRanks));
+    fxo_flag_ = static_cast<unsigned>(lay.Add<unsigned long long>(static_cast<size_t>(kFXKinds) * kMaxXRanks));
+    const size_t bytes = lay.bytes();
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+    }
+    int ok = p != nullptr ? 1 : 0;
+    if (ok) HIP_CHECK(hipMemset(p, 0, bytes));
+    if (P_ > 1) ok = Network::GlobalSyncUpByMin(ok);
+    auto fail = [&](const char* why) {
+      if (p) (void)hipFree(p);
+      fx_local_ = nullptr;
+      if (required) Log::Fatal("xGMI transport: %s", why);
+      Log::Warning("xGMI transport unavailable (%s); using collectives", why);
+    };
+    if (!ok) return fail("cannot allocate the uncached exchange buffer");
+    fx_local_ = static_cast<char*>(p);
+    if (!XgmiOpen(fx_local_, &fx_peers_)) return fail("peer exchange buffers could not be mapped");
+    fxep_.Resize(1);
+    fxep_.Zero(stream_);
+    fxcnt_.Resize(kFXKinds);
+    fxcnt_.Zero(stream_);
+    fxg_ = true;
+    // self-test (session-0 tags, below every training tag)
+    FArgs a = MakeFArgs();
+    a.xsession = 0;
+    a.xtimeout = static_cast<unsigned long long>(100e6 * std::min(30.0, XTimeoutSeconds()));
+    DevBuf<unsigned> err(1);
+    err.Zero(stream_);
+    const int nvals = static_cast<int>(std::min<size_t>(recv_words / 2, 4096));
+    for (int round = 0; round < 4; ++round) LaunchFrontierXSelfTest(a, round, nvals, err.get(), stream_);
+    unsigned h = 0;
+    err.Download(&h, 1, stream_);
+    unsigned* hb = pin_bar_.Get(4);
+    HIP_CHECK(hipMemcpyAsync(hb, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    int good = h == 0u && hb[3] == 0u ? 1 : 0;
+    if (!good) Log::Warning("frontier xGMI self-test on rank %d: %u wrong values, wait status %u", rank_, h, hb[3]);
+    if (P_ > 1) good = Network::GlobalSyncUpByMin(good);
+    if (!good) {
+      fxg_ = false;
+      bar_.Zero(stream_);
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      XgmiClose(fx_local_, &fx_peers_);
+      return fail("self-test failed");
+    }
+    InvalidateGraph();
+  }
+
   // Three exchanges of a known pattern through the histogram rows (session 0 tags,
   // below every training tag), checked value by value on every rank.
   bool XgmiSelfTest() {
@@ -456,6 +528,8 @@ class DeviceTreeLearner : public TreeLearner {
     m += ", " + std::to_string(P_) + " ranks, ";
     if (frontier_) {
       const std::string via = HostStagedDP() ? "host-staged collectives" : "RCCL";
+      if (FrontierXg() && fowner_) return m + "frontier engine, owner histogram chunks + best-split push per round (xGMI in-kernel exchange)";
+      if (FrontierXg()) return m + "frontier engine, best-split push per round (xGMI in-kernel exchange)";
       if (fowner_) return m + "frontier engine, owner reduce-scatter + best-split all-gather per round (" + via + ")";
       if (ffeature_ || fvoting_) return m + "frontier engine, " + via;
       return m + "frontier engine, all-reduce per round (" + via + ")";
@@ -1642,6 +1716,8 @@ class DeviceTreeLearner : public TreeLearner {
   bool FrontierSerial() const {
     return mode_ == DevParallel::kSerial && !owner_scan_ && !voting_ && !distributed_;
   }
+  // the frontier's exchanges run in-kernel over xGMI (SetupFrontierXgmi; FArgs::xg)
+  bool FrontierXg() const { return fxg_ && frontier_ && (fowner_ || ffeature_); }
   // Data-parallel frontier: every rank partitions / builds histograms of its own rows, the
   // round's fixed-point accumulators are summed over ranks (one exact integer all-reduce per
   // round, RCCL or the host-staged rehearsal transport), and every rank scans and selects
@@ -1649,13 +1725,12 @@ class DeviceTreeLearner : public TreeLearner {
   // same tree with no further exchange. Children's counts come from the summed histograms
   // (the split record), row ranges from the local partition. LGAP_FRONTIER_DP=0: the
   // sequential owner-scan chain instead. Reference: data_parallel_tree_learner.cpp:148-297.
-  // The exchange is an all-reduce (RCCL communicator or the host-staged rehearsal); an explicit
-  // LGAP_DP_TRANSPORT=xgmi keeps the sequential chain's in-kernel xGMI exchange.
+  // The exchanges: the owner-computes rounds below (FrontierOwner) over the in-kernel xGMI
+  // transport (FrontierXg, the default where every rank maps every peer) or RCCL / the host-staged
+  // rehearsal collectives; the per-round all-reduce for configurations that need every feature.
   bool FrontierDP() const {
     const char* e = std::getenv("LGAP_FRONTIER_DP");
     if (e != nullptr && e[0] == '0') return false;
-    const char* t = std::getenv("LGAP_DP_TRANSPORT");
-    if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
     return mode_ == DevParallel::kData && data_parallel_ && owner_scan_ && distributed_ && !voting_ &&
            (CommExists() || HostStagedDP());
   }
@@ -1688,12 +1763,9 @@ class DeviceTreeLearner : public TreeLearner {
   }
   // Feature-parallel frontier: every rank holds all rows and grows the same partition and
   // histograms; the scans cover this rank's features (the groups it owns), each child's best is
-  // all-gathered and the best over ranks is the child's candidate. An
-  // an explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain.
+  // exchanged (pushed over xGMI, or all-gathered) and the best over ranks is the child's candidate.
   // Reference: feature_parallel_tree_learner.cpp:23-80.
   bool FrontierFeature() const {
-    const char* t = std::getenv("LGAP_DP_TRANSPORT");
-    if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
     return mode_ == DevParallel::kFeature && owner_scan_ && !distributed_ && (CommExists() || HostStagedDP());
   }
   int FrontierKmax() const {
@@ -2107,6 +2179,25 @@ class DeviceTreeLearner : public TreeLearner {
       a.own_b0 = fown_b0_.get();
       a.acc_recv = facc_recv_.get();
     }
+    if (FrontierXg()) {
+      // in-kernel exchange: the owner's receive chunk and the per-child best rows live in this
+      // rank's exchange buffer; the chunk stride covers every expansion a round can hold
+      a.xg = 1;
+      a.xP = P_;
+      a.xrank = rank_;
+      for (int q = 0; q < P_; ++q) a.xpeer[q] = fx_peers_[q];
+      a.xo_recv = fxo_recv_;
+      a.xo_fpb = fxo_fpb_;
+      a.xo_root = fxo_root_;
+      a.xo_flag = fxo_flag_;
+      a.xep = fxep_.get();
+      a.xcnt = fxcnt_.get();
+      a.xtimeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
+      a.xsession = 1;
+      a.xfault = std::getenv("LGAP_FAULT_INJECT") != nullptr && std::strcmp(std::getenv("LGAP_FAULT_INJECT"), "xgmi") == 0;
+      a.fpb = reinterpret_cast<FPairBest*>(fx_local_ + fxo_fpb_);
+      if (fowner_) a.acc_recv = reinterpret_cast<unsigned long long*>(fx_local_ + fxo_recv_);
+    }
     if (fvoting_) {
       a.voting = 1;
       a.vote_k = topk_;
@@ -2185,6 +2276,14 @@ class DeviceTreeLearner : public TreeLearner {
   // chunks, the reduce-scatter, owner-only scans, the per-child bests exchanged. `kb` = the
   // round's expansion bound (the chunk stride the reduce and the reduce-scatter agree on).
   void FrontierOwnerRound(const FArgs& fa, int kb) {
+    if (fa.xg) {
+      // xGMI: k_f_reduce adds into the owners' chunks and completes the exchange in-kernel;
+      // the owner scans its features; k_f_pair_best pushes the per-child bests to every rank
+      LaunchFrontierHist(fa, FrontierHistLds(), stream_);
+      LaunchFrontierScan(fa, fscan_lds_, stream_);
+      LaunchFrontierPairBest(fa, stream_);
+      return;
+    }
     FArgs fr = fa;
     fr.xkb = std::max(1, std::min(kb, fkmax_));
     LaunchFrontierHist(fr, FrontierHistLds(), stream_);
@@ -2202,7 +2301,7 @@ class DeviceTreeLearner : public TreeLearner {
   void FrontierFeatureExchange(const FArgs& fa) {
     if (fa.cegb_raw) Log::Fatal("frontier feature exchange: raw CEGB candidates are not exchanged");
     LaunchFrontierPairBest(fa, stream_);
-    AllGatherInPlace(ffpb_.get(), sizeof(FPairBest) * 2 * static_cast<size_t>(fkmax_), stream_);
+    if (!fa.xg) AllGatherInPlace(ffpb_.get(), sizeof(FPairBest) * 2 * static_cast<size_t>(fkmax_), stream_);
   }
 
   void EnqueueFrontierRound(const FArgs& fa, int kb) {
@@ -2265,7 +2364,10 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipGetLastError());
       // the tree setup and k_root_final's fold of the partials in one launch
       LaunchFrontierInitRoot(fa, ra.root_part, root_blocks, ghmax_.get(), stream_);
-      if (distributed_) {
+      if (distributed_ && fa.xg) {
+        // global root sums and gradient maxima, exchanged in-kernel (xGMI transport)
+        LaunchFrontierXRoot(fa, ghmax_.get(), stream_);
+      } else if (distributed_) {
         // global root sums and gradient maxima (the fixed-point scales must agree on all ranks)
         AllreduceSumF64(reinterpret_cast<double*>(flsum_), 2, stream_);
         AllreduceMaxU32(ghmax_.get(), 4, stream_);
@@ -2320,7 +2422,7 @@ class DeviceTreeLearner : public TreeLearner {
   // each until it is. Results: the committed splits, the final leaf ranges, the root output.
   // a stream carrying RCCL collectives: a lost peer must not hang the process
   void FrontierSync() {
-    if ((distributed_ || ffeature_) && !HostStagedDP()) {
+    if ((distributed_ || ffeature_) && !HostStagedDP() && !FrontierXg()) {
       WatchedStreamSync(stream_, CommTimeoutSeconds(config_->time_out), "frontier tree growth (RCCL all-reduce)");
     } else {
       HIP_CHECK(hipStreamSynchronize(stream_));
@@ -2331,12 +2433,13 @@ class DeviceTreeLearner : public TreeLearner {
     // collectives: RCCL calls replay from the graph only on request (LGAP_DP_GRAPH=1, as in the
     // sequential chain); the host-staged rehearsal transport synchronises inside its exchange
     // (feature parallel exchanges candidates over collectives too, without distributed rows)
-    const bool comm = distributed_ || ffeature_;
+    // (the xGMI transport keeps every exchange inside the kernels: a tree replays as one graph)
+    const bool comm = (distributed_ || ffeature_) && !FrontierXg();
     const bool use_graph = config_->device_use_graph && (!comm || (DPGraphEnabled() && !HostStagedDP()));
     if (use_graph && comm && !fgraphs_.empty() && graph_comm_ != ActiveComm()) InvalidateGraph();
     if (use_graph && comm) graph_comm_ = ActiveComm();
     // per-round caps need the eager enqueue (the all-reduce sizes change from tree to tree)
-    fcaps_on_ = distributed_ && !use_graph;
+    fcaps_on_ = distributed_ && !use_graph && !FrontierXg();
     if (distributed_) {
       if (fkused_.size() < static_cast<size_t>(kFrontierRoundCap)) {
         fkused_.Resize(kFrontierRoundCap);
@@ -2415,6 +2518,11 @@ class DeviceTreeLearner : public TreeLearner {
     *hlo = hh->lout0;
     unsigned hbar[4];
     std::memcpy(hbar, hh->bar, sizeof(hbar));
+    if (hbar[3] != 0u) {
+      static const char* const kinds[kFXKinds] = {"histogram", "split candidates", "root sums", "self-test"};
+      Log::Fatal("xGMI exchange (%s) timed out on rank %d after %.0f s: a peer stopped training",
+                 kinds[std::min<unsigned>(hbar[3] - 1u, kFXKinds - 1)], rank_, XTimeoutSeconds());
+    }
     if (distributed_) {
       std::memcpy(fkused_hist_[fkused_trees_ % 4], hh->kused, sizeof(int) * kFrontierRoundCap);
       ++fkused_trees_;
@@ -4137,6 +4245,12 @@ class DeviceTreeLearner : public TreeLearner {
   int x_off_hist_ = 0, x_off_cand_ = 0, x_off_flag_ = 0, x_off_root_ = 0;
   DevBuf<XPeers> xpeers_;
   unsigned xsession_ = 0;
+  // frontier xGMI transport (SetupFrontierXgmi; FArgs::xg)
+  bool fxg_ = false;
+  char* fx_local_ = nullptr;
+  std::vector<char*> fx_peers_;
+  unsigned fxo_recv_ = 0, fxo_fpb_ = 0, fxo_root_ = 0, fxo_flag_ = 0;
+  DevBuf<unsigned> fxep_, fxcnt_;
   int cached_gcount_ = -1, cached_gcount_local_ = -1;
   DevBuf<unsigned long long> tile_pub_;
   PinnedBuf<unsigned> pin_bar_;

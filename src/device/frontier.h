@@ -283,6 +283,31 @@ struct FArgs {
   unsigned* xrng;
   struct FPairBest* fpb;  // [P][kmax][2] per-child best of each rank, all-gathered
   SplitParams sp;
+  // xGMI in-kernel exchange of the distributed frontier (owner-computes data parallel and feature
+  // parallel; device_learner.hip SetupFrontierXgmi). Every rank holds one uncached exchange buffer
+  // at identical offsets, IPC-mapped by every peer: k_f_reduce adds each histogram bin straight into
+  // its OWNER's receive chunk (64-bit integer atomics over xGMI: exact, order free), k_f_pair_best
+  // stores this rank's per-child bests into every peer's record table, and the last block of each
+  // producing launch tags flag[kind][this rank] in every peer, then waits for all P tags of its own
+  // (bounded: bar[3]). The consumer is the next kernel on the stream: no collective call, host
+  // round trip or extra launch per round, and a tree replays as one hipGraph.
+  int xg;                        // 1: in-kernel exchange (xpeer valid)
+  int xP, xrank;
+  char* xpeer[kMaxXRanks];       // rank q's exchange buffer in this process's address space
+  unsigned xo_recv, xo_fpb, xo_root, xo_flag;  // byte offsets inside every rank's buffer
+  unsigned* xep;                 // [1] rounds exchanged so far: a round's tag is (xsession, *xep + 1)
+  unsigned* xcnt;                // [kFXKinds] block arrivals of the current producing launch
+  unsigned long long xtimeout;   // wall-clock ticks (100 MHz) a wait may spin before it gives up
+  unsigned xsession;             // high word of every tag (0: the set-up self-test)
+  int xfault;                    // test hook (LGAP_FAULT_INJECT=xgmi): this rank never signals
+};
+
+// exchange kinds of the frontier's xGMI transport (flag rows of the exchange buffer)
+constexpr int kFXHist = 0, kFXCand = 1, kFXRoot = 2, kFXTest = 3, kFXKinds = 4;
+// root exchange record: (sum g, sum h) and the four gradient bounds of k_f_init_root (float bits)
+struct FXRoot {
+  double g, h;
+  unsigned m[4];
 };
 
 // Results of a replay, written by k_f_results straight into coherent pinned host memory (one
@@ -334,6 +359,11 @@ void LaunchFrontierVoteScan(const FArgs& a, size_t lds_bytes, hipStream_t s);
 // feature parallel / owner-computes data parallel: this rank's per-child best -> fpb[rank] (before
 // the all-gather; k_f_select's phase A takes the best over the ranks after it)
 void LaunchFrontierPairBest(const FArgs& a, hipStream_t s);
+// xGMI transport: the root sums / gradient bounds exchanged and folded in rank order (replaces the
+// per-tree all-reduces), and the set-up self-test (round r: every rank adds a known pattern into
+// every peer's receive chunk, then checks and clears its own; mismatches counted into err)
+void LaunchFrontierXRoot(const FArgs& a, unsigned* ghmax, hipStream_t s);
+void LaunchFrontierXSelfTest(const FArgs& a, int round, int nvals, unsigned* err, hipStream_t s);
 // one-time kernel attributes (dynamic LDS above 64 KiB)
 void FrontierSetLds(size_t hist_lds, size_t scan_lds, bool use_dp, int width);
 // dynamic LDS of k_f_select (CEGB coupled penalties add F bytes of used flags after it)

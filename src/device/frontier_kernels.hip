@@ -91,6 +91,66 @@ __device__ __forceinline__ size_t FAccAt(const FArgs& a, int e, int b, int pw) {
   return ((static_cast<size_t>(r) * a.xkb + e) * a.own_w + (b - a.own_b0[r])) * pw;
 }
 
+// Accumulator words of (expansion e, bin b): the local round accumulators, or -- owner-computes
+// over the xGMI transport -- the receive chunk [kmax][own_w] x pw of b's OWNER rank, in that rank's
+// exchange buffer (feature parallel exchanges only its per-child bests: local accumulators)
+__device__ __forceinline__ unsigned long long* FAccPtr(const FArgs& a, int e, int b, int pw) {
+  if (!a.xg || !a.own) return a.acc + FAccAt(a, e, b, pw);
+  int r = 0;
+  while (r + 1 < a.own_P && a.own_b0[r + 1] <= b) ++r;
+  return reinterpret_cast<unsigned long long*>(a.xpeer[r] + a.xo_recv) +
+         (static_cast<size_t>(e) * a.own_w + (b - a.own_b0[r])) * pw;
+}
+
+// ---- xGMI transport handshake (FArgs::xg). Tags are (session << 32) | round: strictly
+// increasing for the life of the exchange buffer, so a flag is only compared for "reached".
+__device__ __forceinline__ unsigned long long FXTag(const FArgs& a, unsigned ep) {
+  return (static_cast<unsigned long long>(a.xsession) << 32) | ep;
+}
+__device__ __forceinline__ unsigned long long* FXFlag(const FArgs& a, int owner, int kind, int src) {
+  return reinterpret_cast<unsigned long long*>(a.xpeer[owner] + a.xo_flag) + kind * kMaxXRanks + src;
+}
+// one lane: spin (bounded by xtimeout; then bar[3] = 1 + kind) until every rank tagged this rank's
+// flag row `kind` with at least `tag`
+__device__ inline bool FXWaitAll(const FArgs& a, int kind, unsigned long long tag) {
+  const unsigned long long t0 = wall_clock64();
+  for (int q = 0; q < a.xP; ++q) {
+    unsigned long long* f = FXFlag(a, a.xrank, kind, q);
+    unsigned spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < tag) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 255u) == 0u &&
+          (wall_clock64() - t0 > a.xtimeout || __hip_atomic_load(&a.bar[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(&a.bar[3], 1u + kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return true;
+}
+// Every thread of every block of a producing launch calls this after its pushes: each wave waits
+// until its stores / atomics are acknowledged (they target uncached memory, so no cache needs a
+// write-back: a per-wave fence would write back the XCD's L2 once per wave, measured at ~40% of a
+// 1.25M-row iteration), the block arrives on the launch's counter, and the LAST block to arrive
+// releases system-wide, tags flag[kind][this rank] in every peer and waits until all P ranks
+// tagged its own row. Only that one block spins, so the peers' producers always find CUs.
+__device__ inline void FXArrive(const FArgs& a, int kind, unsigned long long tag) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nb = gridDim.x * gridDim.y;
+    if (atomicAdd(&a.xcnt[kind], 1u) == nb - 1u) {
+      atomicExch(&a.xcnt[kind], 0u);  // every block of this launch has arrived
+      __threadfence_system();
+      for (int q = 0; q < a.xP && !(a.xfault && a.xsession > 0); ++q) {
+        __hip_atomic_store(FXFlag(a, q, kind, a.xrank), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      FXWaitAll(a, kind, tag);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // tree setup: the root node, the root "round" (one pseudo-expansion whose smaller child
 // is the root), the committed-leaf table and the node states.
@@ -462,6 +522,8 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
   if (tile.direct) {
     // groups too wide for LDS: each row's fixed-point value straight into the accumulator
     if (a.own && e >= a.xkb) return;  // (never: the round's bound covers its expansions)
+    // (xGMI: every add lands in the owner's receive chunk; k_f_reduce, next on the stream,
+    // signals the round once all of this launch's adds are visible)
     int* gst = reinterpret_cast<int*>(lds_raw);
     for (int g = t; g < ng0; g += blockDim.x) gst[g] = g == t ? gst0 : a.gstart[tile.g0 + g];
     __syncthreads();
@@ -493,12 +555,13 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
                                     : ((word >> (16 * kk)) & 0xFFFFu);
         const int g = dw * per + kk;
         if (b != 0u && g < tile.g1) {
-          const size_t o = FAccAt(a, e, gst[g - tile.g0] + static_cast<int>(b), pw);
-          if (qg) atomicAdd(&a.acc[o], qg);
-          if (qh) atomicAdd(&a.acc[o + 1], qh);
+          unsigned long long* o = FAccPtr(a, e, gst[g - tile.g0] + static_cast<int>(b), pw);
+          if (qg) atomicAdd(o, qg);
+          if (qh) atomicAdd(o + 1, qh);
         }
       }
     }
+    if (a.xg && a.own) __builtin_amdgcn_s_waitcnt(0);  // (adds acknowledged before the launch ends)
     return;
   }
   // block scale: 2^30 / min(block rows * max, this rank's sum of |value| over all its rows)
@@ -615,6 +678,8 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   }
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
+  const bool xhist = a.xg && a.own;  // (xGMI owner-computes: the histogram exchange ends here)
+  const unsigned xep = xhist ? *a.xep : 0u;  // (this round's tag is xep + 1)
   if (sp->done) return;
   const int k = sp->k;
   // chunk prefix over the tiles (block scan; num_tiles <= kRedThreads)
@@ -645,8 +710,10 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   }
   __syncthreads();
   const int nch = s_tc[a.num_tiles];
-  const int W = s_w0[k];
-  if (W == 0 || nch == 0) return;
+  const int W = nch > 0 ? s_w0[k] : 0;
+  if (W == 0 && !xhist) return;  // (xGMI: a rank with no rows this round still signals it)
+  // xGMI with several ranks: every rank adds into the owner's chunk, so no plain first store
+  const bool shared_out = xhist && a.xP > 1;
   const int pw = a.quant && a.qpack ? 1 : 2;  // accumulator words per bin (see k_f_hist)
   constexpr int sw = MODE == 1 ? 2 : 1;       // slab words per bin
   for (int w = blockIdx.x; w < W; w += gridDim.x) {
@@ -702,8 +769,8 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
         h += static_cast<long long>(hv);
       }
     }
-    unsigned long long* out = a.acc + FAccAt(a, e, tbin0 + i, pw);
-    if (nb <= kRedRows) {
+    unsigned long long* out = FAccPtr(a, e, tbin0 + i, pw);
+    if (nb <= kRedRows && !shared_out) {
       // the expansion's only row group: the accumulator is zero here (the scan re-zeroes it)
       if (g) out[0] = static_cast<unsigned long long>(g);
       if (pw == 2 && h) out[1] = static_cast<unsigned long long>(h);
@@ -712,6 +779,8 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
       if (pw == 2 && h) atomicAdd(&out[1], static_cast<unsigned long long>(h));
     }
   }
+  // xGMI: the round's histogram exchange completes here (the owner's scan runs next)
+  if (xhist) FXArrive(a, kFXHist, FXTag(a, xep + 1u));
 }
 
 // ---------------------------------------------------------------------------
@@ -762,8 +831,9 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     p0.path_smooth = 0.0;
     a.lout[0] = LeafOutputRaw(rs.x, rs.y, p0, a.nodes[0].gcount, 0.0);
   }
-  if (a.own) {
+  if (a.own && !a.xg) {
     // the reduce-scatter consumed the send layout: zero it for the next round's k_f_reduce
+    // (xGMI: no send layout; the owner re-zeroes its receive chunk as it reads it, below)
     const size_t nz = static_cast<size_t>(a.own_P) * a.xkb * a.own_w * (a.quant && a.qpack ? 1 : 2);
     for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nz; i += static_cast<size_t>(gridDim.x) * blockDim.x) {
       a.acc[i] = 0ull;
@@ -1743,6 +1813,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
   if (st.done) return;
+  if (a.xg && t == 0) *a.xep += 1u;  // (xGMI: this round's exchanges are complete; next tag)
   const int kprev = st.k;
   const int cid_next = st.cid_next;
   const int np = 2 * kprev;
@@ -2970,11 +3041,39 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
 // features' candidates -> fpb[rank]; after the all-gather the select's phase A takes the best over
 // the ranks' records (gain desc, then feature asc: the order of the sequential select, so the tree
 // equals the one-rank tree).
+// xGMI transport: the record is stored into fpb[rank] of EVERY rank's exchange buffer and the
+// launch's last block completes the exchange (k_f_select, next on the stream, reads all P rows).
+__device__ __forceinline__ void FPairStore(const FArgs& a, int q, const SplitKey* key, const SplitInfo* info) {
+  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  const int lane = threadIdx.x;
+  const int np = a.xg ? a.xP : 1;
+  for (int r = 0; r < np; ++r) {
+    FPairBest* base = a.xg ? reinterpret_cast<FPairBest*>(a.xpeer[r] + a.xo_fpb) : a.fpb;
+    FPairBest* out = base + static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q;
+    if (key == nullptr) {
+      if (lane == 0) {
+        out->key.feature = -1;
+        out->key.gain = kMinScore;
+      }
+      continue;
+    }
+    for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
+      if (i < kKeyWords) reinterpret_cast<uint32_t*>(&out->key)[i] = reinterpret_cast<const uint32_t*>(key)[i];
+      else reinterpret_cast<uint32_t*>(&out->info)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(info)[i - kKeyWords];
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
   const FState* stp = a.st;
+  const unsigned xep = a.xg ? *a.xep : 0u;
   if (stp->done) return;
   const int k = stp->k, q = blockIdx.x, F = a.F, lane = threadIdx.x;
-  if ((q >> 1) >= k) return;
+  if ((q >> 1) >= k) {
+    if (a.xg) FXArrive(a, kFXCand, FXTag(a, xep + 1u));  // (every block arrives)
+    return;
+  }
   const int c = FPairChild(a, k, q);
   double bg = kMinScore;
   int bf = 0x7fffffff, bp = -1;
@@ -2991,21 +3090,75 @@ __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
   }
   const int src = WaveArgBestLane(bg, bf, 0);
   bp = ReadLane(bp, src);
-  FPairBest* out = a.fpb + static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q;
-  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
-  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-  if (bp < 0) {
-    if (lane == 0) {
-      out->key.feature = -1;
-      out->key.gain = kMinScore;
+  const size_t o = static_cast<size_t>(q) * F + (bp < 0 ? 0 : bp);
+  FPairStore(a, q, bp < 0 ? nullptr : a.ckey + o, bp < 0 ? nullptr : a.cinfo + o);
+  if (a.xg) FXArrive(a, kFXCand, FXTag(a, xep + 1u));
+}
+
+// xGMI root exchange (one block, once per tree, after k_f_init_root): this rank's root sums and
+// gradient bounds -> row `rank` of every peer's root table, the handshake, then every rank folds
+// the P rows in rank order (sums: the same fp64 result on every rank; bounds: max, as the
+// all-reduces this replaces).
+__global__ __launch_bounds__(64) void k_fx_root(FArgs a, unsigned* __restrict__ ghmax) {
+  const unsigned xep = *a.xep;
+  if (threadIdx.x < a.xP) {
+    FXRoot mine;
+    const double2 s = a.lsum[0];
+    mine.g = s.x;
+    mine.h = s.y;
+    for (int i = 0; i < 4; ++i) mine.m[i] = ghmax[i];
+    reinterpret_cast<FXRoot*>(a.xpeer[threadIdx.x] + a.xo_root)[a.xrank] = mine;
+  }
+  FXArrive(a, kFXRoot, FXTag(a, xep + 1u));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const FXRoot* rows = reinterpret_cast<const FXRoot*>(a.xpeer[a.xrank] + a.xo_root);
+    double g = 0.0, h = 0.0;
+    unsigned m[4] = {0u, 0u, 0u, 0u};
+    for (int q = 0; q < a.xP; ++q) {
+      const FXRoot x = rows[q];
+      g += x.g;
+      h += x.h;
+      for (int i = 0; i < 4; ++i) m[i] = max(m[i], x.m[i]);
     }
-    return;
+    a.lsum[0] = make_double2(g, h);
+    for (int i = 0; i < 4; ++i) ghmax[i] = m[i];
   }
-  const size_t o = static_cast<size_t>(q) * F + bp;
-  for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
-    if (i < kKeyWords) reinterpret_cast<uint32_t*>(&out->key)[i] = reinterpret_cast<const uint32_t*>(a.ckey + o)[i];
-    else reinterpret_cast<uint32_t*>(&out->info)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(a.cinfo + o)[i - kKeyWords];
+}
+
+// Set-up self-test of the transport (session 0): round r, every rank adds rank + 1 + r into
+// words [half, half + n) of every peer's receive chunk and stores a pattern word into its fpb row
+// there; after the handshake k_fx_check verifies its own chunk (sum over ranks) and clears it.
+// Halves alternate by round, so a rank already pushing round r + 1 never touches what a slower
+// peer still checks.
+__global__ __launch_bounds__(256) void k_fx_push(FArgs a, int round, int n) {
+  const int half = (round & 1) * n;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int q = 0; q < a.xP; ++q) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.xpeer[q] + a.xo_recv) + half + i,
+                static_cast<unsigned long long>(a.xrank + 1 + round));
+    }
   }
+  if (blockIdx.x == 0 && threadIdx.x < a.xP) {
+    reinterpret_cast<unsigned*>(a.xpeer[threadIdx.x] + a.xo_fpb)[a.xrank] = 0xA5000000u + 256u * round + a.xrank;
+  }
+  FXArrive(a, kFXTest, FXTag(a, static_cast<unsigned>(round + 1)));
+}
+__global__ __launch_bounds__(256) void k_fx_check(FArgs a, int round, int n, unsigned* err) {
+  const int half = (round & 1) * n;
+  const unsigned long long want =
+      static_cast<unsigned long long>(a.xP) * (a.xP + 1) / 2 + static_cast<unsigned long long>(a.xP) * round;
+  unsigned long long* rx = reinterpret_cast<unsigned long long*>(a.xpeer[a.xrank] + a.xo_recv);
+  unsigned bad = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    bad += rx[half + i] != want ? 1u : 0u;
+    rx[half + i] = 0ull;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < a.xP) {
+    const unsigned v = reinterpret_cast<const unsigned*>(a.xpeer[a.xrank] + a.xo_fpb)[threadIdx.x];
+    bad += v != 0xA5000000u + 256u * round + threadIdx.x ? 1u : 0u;
+  }
+  if (bad) atomicAdd(err, bad);
 }
 
 }  // namespace
@@ -3248,6 +3401,18 @@ void LaunchFrontierVoteScan(const FArgs& a, size_t lds, hipStream_t s) {
 
 void LaunchFrontierPairBest(const FArgs& a, hipStream_t s) {
   k_f_pair_best<<<2 * a.kmax, 64, 0, s>>>(a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierXRoot(const FArgs& a, unsigned* ghmax, hipStream_t s) {
+  if (a.xP > 64) std::abort();  // (kMaxXRanks <= 64: one lane per peer)
+  k_fx_root<<<1, 64, 0, s>>>(a, ghmax);
+  HIP_CHECK(hipGetLastError());
+}
+
+void LaunchFrontierXSelfTest(const FArgs& a, int round, int nvals, unsigned* err, hipStream_t s) {
+  k_fx_push<<<4, 256, 0, s>>>(a, round, nvals);
+  k_fx_check<<<4, 256, 0, s>>>(a, round, nvals, err);
   HIP_CHECK(hipGetLastError());
 }
 

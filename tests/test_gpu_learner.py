@@ -315,8 +315,10 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
     host-staged collectives, owner-only scans, per-child bests all-gathered, redundant select on
     every rank); "allreduce": the same engine with the per-round all-reduce and redundant scans
     of every feature; "collective-seq": the sequential chain's owner histogram exchange over
-    the same collectives; "xgmi": the sequential chain's in-kernel exchange over IPC-mapped
-    buffers (here all on one device). Every rank must grow the identical model, and it must match
+    the same collectives; "xgmi": the frontier engine's in-kernel exchange over IPC-mapped
+    buffers (here all on one device): k_f_reduce adds every bin into its owner's receive chunk,
+    k_f_pair_best pushes the per-child bests, the root sums are exchanged by k_fx_root, and no
+    collective runs while a tree grows. Every rank must grow the identical model, and it must match
     the host data-parallel learner trained by the same ranks on the same bins."""
     import json
     import os
@@ -338,9 +340,11 @@ def test_data_parallel_multirank_rehearsal(lgb, gpu_required, world, transport):
     assert res["world"] == world
     assert "data-parallel" in res["device_name"], res
     assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
-    assert ("frontier engine" in res["device_name"]) == (transport in ("collective", "allreduce")), res
+    assert ("frontier engine" in res["device_name"]) == (transport in ("collective", "allreduce", "xgmi")), res
     if transport == "collective":
         assert "owner reduce-scatter" in res["device_name"], res
+    if transport == "xgmi":
+        assert "owner histogram chunks" in res["device_name"], res
     if transport == "allreduce":
         assert "all-reduce per round" in res["device_name"], res
     assert res["ranks_identical"], res
@@ -375,8 +379,9 @@ def test_feature_parallel_multirank_rehearsal(lgb, gpu_required, transport):
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert "feature-parallel" in res["device_name"], res
-    # collectives: the frontier engine (per-child bests all-gathered each round)
-    assert ("frontier engine" in res["device_name"]) == (transport == "collective"), res
+    # the frontier engine (per-child bests all-gathered each round, or pushed over xGMI)
+    assert "frontier engine" in res["device_name"], res
+    assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
     assert res["ranks_identical"], res
     assert res["identical_leading_trees"] == 10, res
     assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
