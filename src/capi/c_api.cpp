@@ -907,6 +907,7 @@ int LGBM_BoosterPredictForFile(BoosterHandle handle, const char* data_filename, 
     if (!in) Log::Fatal("Data file %s doesn't exist.", data_filename);
     std::string line;
     if (data_has_header) std::getline(in, line);
+    int data_nf = 0;
     while (std::getline(in, line)) {
       if (!line.empty() && line.back() == '\r') line.pop_back();
       rows.rows.emplace_back();
@@ -914,11 +915,18 @@ int LGBM_BoosterPredictForFile(BoosterHandle handle, const char* data_filename, 
       parser->ParseOneLine(line.c_str(), &rows.rows.back(), &lab);
       labels.push_back(static_cast<float>(lab));
       // a negative index is a parser bug; an index past the model's features (a column the
-      // training data never had) is dropped, as the reference's CopyToPredictBuffer
-      // (predictor.hpp:259) ignores it under predict_disable_shape_check
+      // training data never had) is an error unless predict_disable_shape_check is set, and is
+      // then dropped, as the reference's CopyToPredictBuffer (predictor.hpp:259) ignores it
       auto& r = rows.rows.back();
       for (const auto& kv : r) {
         if (kv.first < 0) Log::Fatal("The custom parser produced feature index %d", kv.first);
+        data_nf = std::max(data_nf, kv.first + 1);
+      }
+      if (data_nf > nf && !pc.predict_disable_shape_check) {
+        // (reference predictor.hpp:176-178)
+        Log::Fatal("The number of features in data (%d) is not the same as it was in training data (%d).\n"
+                   "You can set ``predict_disable_shape_check=true`` to discard this error, but please be aware "
+                   "what you are doing.", data_nf, nf);
       }
       r.erase(std::remove_if(r.begin(), r.end(), [nf](const auto& kv) { return kv.first >= nf; }),
               r.end());

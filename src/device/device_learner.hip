@@ -119,11 +119,13 @@ namespace {
 // tile budget), quant_lds32 (0 | 1), part_iters (4 | 8 | 16), hist_il (0 | 1), nibble (0: 8-bit
 // rows), quant_hist (off: float histograms under quantized training), scan_global (1). Returns
 // the key's value, nullptr when it is not set. Read at each use: tests change the environment
-// between trainings in one process.
+// between trainings in one process. Each key's value has its own storage (a caller may hold the
+// values of several keys at once); empty items (a trailing comma) are skipped.
 const char* KernelOverride(const char* key) {
   static const char* const kKeys[] = {"fhist_threads", "hist_lds_kb", "quant_lds32", "part_iters",
                                       "hist_il",       "nibble",      "quant_hist",  "scan_global"};
-  thread_local std::string val;
+  constexpr int kNumKeys = static_cast<int>(sizeof(kKeys) / sizeof(kKeys[0]));
+  thread_local std::string vals[kNumKeys];
   const char* e = std::getenv("LGAP_KERNEL");
   if (e == nullptr) return nullptr;
   const std::string s(e);
@@ -132,16 +134,17 @@ const char* KernelOverride(const char* key) {
     size_t q = s.find(',', p);
     if (q == std::string::npos) q = s.size();
     const std::string item = s.substr(p, q - p);
+    p = q + 1;
+    if (item.empty()) continue;
     const size_t eq = item.find('=');
     const std::string k = item.substr(0, eq);
-    bool known = false;
-    for (const char* kk : kKeys) known = known || k == kk;
-    if (!known) Log::Fatal("LGAP_KERNEL: unknown key '%s'", k.c_str());
+    int idx = -1;
+    for (int i = 0; i < kNumKeys; ++i) idx = k == kKeys[i] ? i : idx;
+    if (idx < 0) Log::Fatal("LGAP_KERNEL: unknown key '%s'", k.c_str());
     if (k == key) {
-      val = eq == std::string::npos ? "1" : item.substr(eq + 1);
-      found = val.c_str();
+      vals[idx] = eq == std::string::npos ? "1" : item.substr(eq + 1);
+      found = vals[idx].c_str();
     }
-    p = q + 1;
   }
   return found;
 }

@@ -202,9 +202,16 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
 }
 
 // Device-resident leaf histograms (EnableDeviceScans): one device slot per leaf, no LRU pool (the
-// factory only asks for it when num_leaves slots fit the device's histogram budget).
+// factory only asks for it when num_leaves slots fit the device's histogram budget). Re-checked on
+// every ResetConfig: a reset that turns on extra_trees (random thresholds drawn from the host
+// histogram) or forced splits, leaves the intermediate / advanced method, or sets a
+// histogram_pool_size the slots exceed hands the scans back to the host.
 void SerialTreeLearner::SetupResident() {
-  resident_ = hist_backend_ && want_device_scans_ && hist_backend_->EnableResidentSlots(config_->num_leaves);
+  const double slot_mb = 16.0 * std::max(1, train_data_->num_total_bin()) * std::max(2, config_->num_leaves) / (1024.0 * 1024.0);
+  const bool serve = want_device_scans_ && !config_->extra_trees && config_->forcedsplits_filename.empty() &&
+                     !config_->monotone_constraints.empty() && config_->monotone_constraints_method != "basic" &&
+                     (config_->histogram_pool_size <= 0 || slot_mb <= config_->histogram_pool_size);
+  resident_ = hist_backend_ && serve && hist_backend_->EnableResidentSlots(config_->num_leaves);
   if (!resident_) return;
   dslot_.resize(config_->num_leaves);
   dvalid_.assign(config_->num_leaves, 0);

@@ -70,8 +70,9 @@ def test_custom_parser_with_header_uses_default_names(lgb, tmp_path):
 
 def test_custom_parser_predict_drops_columns_the_model_never_saw(lgb, tmp_path):
     """Predicting a file through the model's custom parser: a feature index past the model's
-    features (a column training never had) is ignored, as the reference's CopyToPredictBuffer
-    (predictor.hpp:259) ignores it; the predictions equal those of the training columns."""
+    features (a column training never had) is a shape error (reference predictor.hpp:176-178);
+    under predict_disable_shape_check it is ignored, as the reference's CopyToPredictBuffer
+    (predictor.hpp:259) ignores it, and the predictions equal those of the training columns."""
     rng = np.random.default_rng(2)
     X = rng.standard_normal((400, 4))
     y = (X[:, 1] - X[:, 3] > 0).astype(float)
@@ -89,4 +90,7 @@ def test_custom_parser_predict_drops_columns_the_model_never_saw(lgb, tmp_path):
     with open(wide, "w") as fo:
         for row, lab in zip(X, y):
             fo.write(";".join(f"{v:.17g}" for v in row) + f";{lab:g};7\n")
-    np.testing.assert_allclose(bst.predict(str(wide)), bst.predict(X), rtol=1e-12, atol=1e-12)
+    with pytest.raises(lgb.basic.LightGBMError, match="predict_disable_shape_check"):
+        bst.predict(str(wide))
+    np.testing.assert_allclose(bst.predict(str(wide), predict_disable_shape_check=True), bst.predict(X),
+                               rtol=1e-12, atol=1e-12)

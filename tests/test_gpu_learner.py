@@ -571,6 +571,30 @@ def test_device_monotone_constraints_reference_cases(lgb, gpu_required, rng, x3_
     np.testing.assert_allclose(bg.predict(X), bc.predict(X), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("method", ["intermediate", "advanced"])
+def test_device_monotone_scans_default_precision(lgb, gpu_required, rng, method):
+    """The default device_type=gpu setup (gpu_use_dp unset: fp32 (g, h) with fixed-point histogram
+    sums) routes intermediate / advanced monotone constraints to the device-resident scans too. Sums
+    differ from the CPU learner's doubles in the last bits, so the check is the constraint itself
+    plus agreement in prediction, not split-for-split equality."""
+    X, z = _policy_data(rng)
+    y = (z > 0).astype(float)
+    kw = {"objective": "binary", "monotone_constraints": [1, -1, 0, 0, 0, 0], "monotone_constraints_method": method}
+    bc = _train(lgb, X, y, "cpu", rounds=10, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=10, **kw)
+    assert "split scans" in bg.device_name(), bg.device_name()
+    pc, pg = bc.predict(X), bg.predict(X)
+    assert np.mean(np.abs(pg - pc)) < 5e-3, np.mean(np.abs(pg - pc))
+    grid = np.linspace(-3, 3, 50)
+    for row in X[:10]:
+        r = np.tile(row, (50, 1))
+        r[:, 0] = grid
+        assert (np.diff(bg.predict(r)) >= -1e-12).all()
+        r = np.tile(row, (50, 1))
+        r[:, 1] = grid
+        assert (np.diff(bg.predict(r)) <= 1e-12).all()
+
+
 @pytest.mark.parametrize("extra", [
     {"monotone_constraints_method": "advanced", "bagging_fraction": 0.7, "bagging_freq": 1, "lambda_l1": 0.5,
      "path_smooth": 2.0, "max_depth": 7},
