@@ -25,6 +25,8 @@ for s in "$@"; do
     xgbench) step x1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_DP_TRANSPORT=xgmi step x1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=collective step x1coll 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && step x10single 300 python bench.py --steps 30 --warmup 3 && LGAP_DP_TRANSPORT=xgmi step x10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp;;
     xgq) LGAP_DP_TRANSPORT=xgmi step x1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=xgmi step x10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp && step x1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5;;
     xgprof) LGAP_DP_TRANSPORT=xgmi step xgprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/xgprof -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 --rehearse-dp && python scripts/prof_summary.py $OUT/xgprof "1.25M rows, DP frontier xGMI (1 rank)" 22 > $OUT/xgprof_summary.md;;
+    learnerv) step learnerv 900 python -u -m pytest tests/test_gpu_learner.py tests/test_frontier_kernels.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider;;
+    shapes) step goss3m 600 python scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --steps 10 --warmup 2 && step ltr2m 600 python scripts/bench_suite.py --config ltr --rows 2000000 --features 300 --steps 10 --warmup 2;;
     dpmulti) step dpmulti 1100 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank";;
     fp) step fp 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "feature_parallel";;
     dpbench) step b1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_DP_TRANSPORT=xgmi step b1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=collective step b1coll 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && step b10single 300 python bench.py --steps 30 --warmup 3 && LGAP_DP_TRANSPORT=xgmi step b10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp;;
