@@ -373,7 +373,9 @@ class DeviceTreeLearner : public TreeLearner {
     // parallel, feature parallel); collectives otherwise (collective, allreduce, voting, raw
     // per-feature candidates)
     if (frontier_) {
-      if ((want == "auto" || want == "xgmi") && (fowner_ || ffeature_) && P_ <= kMaxXRanks) SetupFrontierXgmi(want == "xgmi");
+      if ((want == "auto" || want == "xgmi") && (fowner_ || ffeature_ || fvoting_) && P_ <= kMaxXRanks) {
+        SetupFrontierXgmi(want == "xgmi");
+      }
       else if (want == "xgmi") Log::Warning("xGMI transport: this frontier configuration exchanges through collectives");
       return;
     }
@@ -447,6 +449,12 @@ class DeviceTreeLearner : public TreeLearner {
     fxo_fpb_ = static_cast<unsigned>(lay.Add<FPairBest>(static_cast<size_t>(P_) * 2 * kFrontierKmax));
     fxo_root_ = static_cast<unsigned>(lay.Add<FXRoot>(kMaxXRanks));
     fxo_flag_ = static_cast<unsigned>(lay.Add<unsigned long long>(static_cast<size_t>(kFXKinds) * kMaxXRanks));
+    fxo_vrec_ = fxo_vrows_ = 0;
+    if (fvoting_) {
+      // voting: every rank's top-k records per child, the elected rows summed over ranks
+      fxo_vrec_ = lay.Add<VoteRec>(static_cast<size_t>(P_) * 2 * kFrontierKmax * topk_);
+      fxo_vrows_ = lay.Add<unsigned long long>(2 * static_cast<size_t>(kFrontierKmax) * topk_ * 2 * max_bin_);
+    }
     const size_t bytes = lay.bytes();
     void* p = nullptr;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
@@ -532,6 +540,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (frontier_) {
       const std::string via = HostStagedDP() ? "host-staged collectives" : "RCCL";
       if (FrontierXg() && fowner_) return m + "frontier engine, owner histogram chunks + best-split push per round (xGMI in-kernel exchange)";
+      if (FrontierXg() && fvoting_) return m + "frontier engine, top-k votes + elected rows per round (xGMI in-kernel exchange)";
       if (FrontierXg()) return m + "frontier engine, best-split push per round (xGMI in-kernel exchange)";
       if (fowner_) return m + "frontier engine, owner reduce-scatter + best-split all-gather per round (" + via + ")";
       if (ffeature_ || fvoting_) return m + "frontier engine, " + via;
@@ -1720,7 +1729,7 @@ class DeviceTreeLearner : public TreeLearner {
     return mode_ == DevParallel::kSerial && !owner_scan_ && !voting_ && !distributed_;
   }
   // the frontier's exchanges run in-kernel over xGMI (SetupFrontierXgmi; FArgs::xg)
-  bool FrontierXg() const { return fxg_ && frontier_ && (fowner_ || ffeature_); }
+  bool FrontierXg() const { return fxg_ && frontier_ && (fowner_ || ffeature_ || fvoting_); }
   // Data-parallel frontier: every rank partitions / builds histograms of its own rows, the
   // round's fixed-point accumulators are summed over ranks (one exact integer all-reduce per
   // round, RCCL or the host-staged rehearsal transport), and every rank scans and selects
@@ -1756,12 +1765,9 @@ class DeviceTreeLearner : public TreeLearner {
   // Voting-parallel frontier (PV-Tree per round): the local pass of every expansion's children,
   // one all-gather of the round's top-k vote records, the election, one exact integer
   // all-reduce of only the elected features' rows, and the global pass over them; every rank
-  // then selects redundantly, as the data-parallel frontier does. An
-  // explicit LGAP_DP_TRANSPORT=xgmi keeps the sequential chain (its in-kernel xGMI exchange).
-  // Reference: voting_parallel_tree_learner.cpp:243-399.
+  // then selects redundantly, as the data-parallel frontier does. Over xGMI the records and the
+  // elected rows are pushed in-kernel (FArgs::xg). Reference: voting_parallel_tree_learner.cpp:243-399.
   bool FrontierVoting() const {
-    const char* t = std::getenv("LGAP_DP_TRANSPORT");
-    if (t != nullptr && std::strcmp(t, "xgmi") == 0) return false;
     return mode_ == DevParallel::kVoting && voting_ && distributed_ && (CommExists() || HostStagedDP());
   }
   // Feature-parallel frontier: every rank holds all rows and grows the same partition and
@@ -2198,7 +2204,9 @@ class DeviceTreeLearner : public TreeLearner {
       a.xtimeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
       a.xsession = 1;
       a.xfault = std::getenv("LGAP_FAULT_INJECT") != nullptr && std::strcmp(std::getenv("LGAP_FAULT_INJECT"), "xgmi") == 0;
-      a.fpb = reinterpret_cast<FPairBest*>(fx_local_ + fxo_fpb_);
+      a.xo_vrec = fxo_vrec_;
+      a.xo_vrows = fxo_vrows_;
+      if (fowner_ || ffeature_) a.fpb = reinterpret_cast<FPairBest*>(fx_local_ + fxo_fpb_);
       if (fowner_) a.acc_recv = reinterpret_cast<unsigned long long*>(fx_local_ + fxo_recv_);
     }
     if (fvoting_) {
@@ -2214,6 +2222,11 @@ class DeviceTreeLearner : public TreeLearner {
       a.vrec = fvrec_.get();
       a.velect = fvelect_.get();
       a.vrows = reinterpret_cast<unsigned long long*>(fvrows_.get());
+      if (FrontierXg()) {
+        // (xGMI: the records and rows every rank pushes land in this rank's exchange buffer)
+        a.vrec = reinterpret_cast<VoteRec*>(fx_local_ + fxo_vrec_);
+        a.vrows = reinterpret_cast<unsigned long long*>(fx_local_ + fxo_vrows_);
+      }
     }
     return a;
   }
@@ -2264,6 +2277,13 @@ class DeviceTreeLearner : public TreeLearner {
   // Voting: after the round's local-pass scan, the vote all-gather, the election, the exact
   // all-reduce of the elected rows (kb expansions' worth), the global pass.
   void FrontierVoteExchange(const FArgs& fa, int kb) {
+    if (fa.xg) {
+      // xGMI: the records and the elected rows are pushed in-kernel (k_f_vote, k_f_elect)
+      LaunchFrontierVote(fa, stream_);
+      LaunchFrontierElect(fa, stream_);
+      LaunchFrontierVoteScan(fa, FrontierVoteScanLds(), stream_);
+      return;
+    }
     LaunchFrontierVote(fa, stream_);
     AllGatherInPlace(fvrec_.get(), sizeof(VoteRec) * 2 * static_cast<size_t>(fkmax_) * topk_, stream_);
     LaunchFrontierElect(fa, stream_);
@@ -2284,8 +2304,7 @@ class DeviceTreeLearner : public TreeLearner {
       // the owner scans its features; k_f_pair_best pushes the per-child bests to every rank
       LaunchFrontierHist(fa, FrontierHistLds(), stream_);
       LaunchFrontierScan(fa, fscan_lds_, stream_);
-      LaunchFrontierPairBest(fa, stream_);
-      return;
+      return;  // (the select pushes the per-child bests and merges the ranks' records)
     }
     FArgs fr = fa;
     fr.xkb = std::max(1, std::min(kb, fkmax_));
@@ -2303,8 +2322,9 @@ class DeviceTreeLearner : public TreeLearner {
   // the factory's FrontierServes).
   void FrontierFeatureExchange(const FArgs& fa) {
     if (fa.cegb_raw) Log::Fatal("frontier feature exchange: raw CEGB candidates are not exchanged");
+    if (fa.xg) return;  // (xGMI: the select pushes the per-child bests and merges the ranks' records)
     LaunchFrontierPairBest(fa, stream_);
-    if (!fa.xg) AllGatherInPlace(ffpb_.get(), sizeof(FPairBest) * 2 * static_cast<size_t>(fkmax_), stream_);
+    AllGatherInPlace(ffpb_.get(), sizeof(FPairBest) * 2 * static_cast<size_t>(fkmax_), stream_);
   }
 
   void EnqueueFrontierRound(const FArgs& fa, int kb) {
@@ -4253,6 +4273,7 @@ class DeviceTreeLearner : public TreeLearner {
   char* fx_local_ = nullptr;
   std::vector<char*> fx_peers_;
   unsigned fxo_recv_ = 0, fxo_fpb_ = 0, fxo_root_ = 0, fxo_flag_ = 0;
+  size_t fxo_vrec_ = 0, fxo_vrows_ = 0;
   DevBuf<unsigned> fxep_, fxcnt_;
   int cached_gcount_ = -1, cached_gcount_local_ = -1;
   DevBuf<unsigned long long> tile_pub_;

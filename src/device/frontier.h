@@ -290,11 +290,14 @@ struct FArgs {
   // stores this rank's per-child bests into every peer's record table, and the last block of each
   // producing launch tags flag[kind][this rank] in every peer, then waits for all P tags of its own
   // (bounded: bar[3]). The consumer is the next kernel on the stream: no collective call, host
-  // round trip or extra launch per round, and a tree replays as one hipGraph.
+  // round trip or extra launch per round, and a tree replays as one hipGraph. Voting parallel: k_f_vote
+// stores its top-k records into every rank's table, k_f_elect adds the elected features' local rows
+// into every rank's row block (the all-gather and the exact all-reduce of the collectives path).
   int xg;                        // 1: in-kernel exchange (xpeer valid)
   int xP, xrank;
   char* xpeer[kMaxXRanks];       // rank q's exchange buffer in this process's address space
   unsigned xo_recv, xo_fpb, xo_root, xo_flag;  // byte offsets inside every rank's buffer
+  size_t xo_vrec, xo_vrows;      // voting: the top-k records [P][2 kmax][K], the elected rows (summed)
   unsigned* xep;                 // [1] rounds exchanged so far: a round's tag is (xsession, *xep + 1)
   unsigned* xcnt;                // [kFXKinds] block arrivals of the current producing launch
   unsigned long long xtimeout;   // wall-clock ticks (100 MHz) a wait may spin before it gives up
@@ -303,7 +306,7 @@ struct FArgs {
 };
 
 // exchange kinds of the frontier's xGMI transport (flag rows of the exchange buffer)
-constexpr int kFXHist = 0, kFXCand = 1, kFXRoot = 2, kFXTest = 3, kFXKinds = 4;
+constexpr int kFXHist = 0, kFXCand = 1, kFXRoot = 2, kFXVote = 3, kFXVRows = 4, kFXTest = 5, kFXKinds = 6;
 // root exchange record: (sum g, sum h) and the four gradient bounds of k_f_init_root (float bits)
 struct FXRoot {
   double g, h;

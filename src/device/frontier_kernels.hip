@@ -3,9 +3,13 @@
 // Launch shapes (fixed per learner; the work of a round is read on the device):
 //   k_f_init        1 x 256
 //   k_f_partition   grid x 256 (contiguous tiles in block order: no co-residency needed)
-//   k_f_hist        max(hist_grid, ceil(hist_grid / 2) + kmax) x LDS tiles, 512 threads
-//   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature))
+//   k_f_hist        max(hist_grid, ceil(hist_grid / 2) + kmax) x LDS tiles, 512 or 1024 threads
+//                   (1024 for single-tile rows at >= 4M rows: the 10M headline)
+//   k_f_reduce      (2 or 4) x CUs x 256 (grid-stride over (expansion, bin chunk, row group))
+//   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature)); k_f_scan_w
+//                   one wave per item for wide numerical data
 //   k_f_select      1 x 1024
+//   k_fx_root       1 x 64 (xGMI transport: once per tree)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -129,6 +133,60 @@ __device__ inline bool FXWaitAll(const FArgs& a, int kind, unsigned long long ta
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   return true;
 }
+// Pushes into exchange buffers are SYSTEM-scope operations (atomics carry sc1, stores sc0 sc1): a
+// peer's IPC mapping of a buffer need not be uncached in the pushing process, so a plain store or
+// device-scope atomic could sit in the pusher's L2; at system scope the acknowledgement means the
+// value reached memory, so a wave's s_waitcnt before it arrives is enough -- no L2 write-back.
+__device__ __forceinline__ void FXAdd(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void FXStore(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void FXStoreRec(T* dst, const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "word records");
+  for (int i = 0; i < static_cast<int>(sizeof(T) / 4); ++i) {
+    FXStore(reinterpret_cast<uint32_t*>(dst) + i, reinterpret_cast<const uint32_t*>(&v)[i]);
+  }
+}
+
+// Reads of what peers pushed are system-scope too (sc0 sc1: past every cache), whatever the
+// mapping's cache policy: a line read in an earlier round must never be served stale.
+__device__ __forceinline__ uint32_t FXLoad(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long FXLoad64(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void FXStore64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T FXLoadRec(const T* src) {
+  T v;
+  for (int i = 0; i < static_cast<int>(sizeof(T) / 4); ++i) {
+    reinterpret_cast<uint32_t*>(&v)[i] = FXLoad(reinterpret_cast<const uint32_t*>(src) + i);
+  }
+  return v;
+}
+// (feature, gain) of a candidate key; `sys`: a record pushed by a peer (system-scope loads)
+__device__ __forceinline__ void FKeyFG(const SplitKey& kk, bool sys, int* f, double* g) {
+  if (!sys) {
+    *f = kk.feature;
+    *g = kk.gain;
+    return;
+  }
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&kk);
+  *f = static_cast<int>(FXLoad(w + offsetof(SplitKey, feature) / 4));
+  const unsigned long long lo = FXLoad(w + offsetof(SplitKey, gain) / 4), hi = FXLoad(w + offsetof(SplitKey, gain) / 4 + 1);
+  *g = __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+}
+
+// Whether a producing launch has peers to signal: one rank has none (its pushes are ordered for
+// the consumer by the kernel boundary), except under the fault-injection hook, which must wait.
+__device__ __forceinline__ bool FXPeers(const FArgs& a) { return a.xP > 1 || a.xfault; }
+
 // Every thread of every block of a producing launch calls this after its pushes: each wave waits
 // until its stores / atomics are acknowledged (they target uncached memory, so no cache needs a
 // write-back: a per-wave fence would write back the XCD's L2 once per wave, measured at ~40% of a
@@ -556,8 +614,13 @@ __global__ __launch_bounds__(THREADS) void k_f_hist(FArgs a) {
         const int g = dw * per + kk;
         if (b != 0u && g < tile.g1) {
           unsigned long long* o = FAccPtr(a, e, gst[g - tile.g0] + static_cast<int>(b), pw);
-          if (qg) atomicAdd(o, qg);
-          if (qh) atomicAdd(o + 1, qh);
+          if (a.xg && a.own) {
+            if (qg) FXAdd(o, qg);
+            if (qh) FXAdd(o + 1, qh);
+          } else {
+            if (qg) atomicAdd(o, qg);
+            if (qh) atomicAdd(o + 1, qh);
+          }
         }
       }
     }
@@ -770,7 +833,16 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
       }
     }
     unsigned long long* out = FAccPtr(a, e, tbin0 + i, pw);
-    if (nb <= kRedRows && !shared_out) {
+    if (xhist) {
+      // (xGMI: into the owner's receive chunk at system scope; one rank with one row group stores)
+      if (nb <= kRedRows && !shared_out) {
+        if (g) __hip_atomic_store(&out[0], static_cast<unsigned long long>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (pw == 2 && h) __hip_atomic_store(&out[1], static_cast<unsigned long long>(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        if (g) FXAdd(&out[0], static_cast<unsigned long long>(g));
+        if (pw == 2 && h) FXAdd(&out[1], static_cast<unsigned long long>(h));
+      }
+    } else if (nb <= kRedRows && !shared_out) {
       // the expansion's only row group: the accumulator is zero here (the scan re-zeroes it)
       if (g) out[0] = static_cast<unsigned long long>(g);
       if (pw == 2 && h) out[1] = static_cast<unsigned long long>(h);
@@ -780,7 +852,8 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
     }
   }
   // xGMI: the round's histogram exchange completes here (the owner's scan runs next)
-  if (xhist) FXArrive(a, kFXHist, FXTag(a, xep + 1u));
+  // (one rank: no peer to signal or wait for; the kernel boundary orders the chunk for the scan)
+  if (xhist && FXPeers(a)) FXArrive(a, kFXHist, FXTag(a, xep + 1u));
 }
 
 // ---------------------------------------------------------------------------
@@ -910,10 +983,17 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       splp_v = p >= 0 && !voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
     for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
-      const unsigned long long x0 = acc[pw * kk], x1 = qpack ? 0ull : acc[2 * kk + 1];
+      const bool sys = a.xg && a.own;  // (the receive chunk the ranks pushed into)
+      const unsigned long long x0 = sys ? FXLoad64(acc + pw * kk) : acc[pw * kk];
+      const unsigned long long x1 = qpack ? 0ull : (sys ? FXLoad64(acc + 2 * kk + 1) : acc[2 * kk + 1]);
       const double gp0 = gl ? gp[2 * kk] : 0.0, gp1 = gl ? gp[2 * kk + 1] : 0.0;
-      acc[pw * kk] = 0ull;
-      if (!qpack) acc[2 * kk + 1] = 0ull;
+      if (sys) {
+        FXStore64(acc + pw * kk, 0ull);
+        if (!qpack) FXStore64(acc + 2 * kk + 1, 0ull);
+      } else {
+        acc[pw * kk] = 0ull;
+        if (!qpack) acc[2 * kk + 1] = 0ull;
+      }
       long long q0 = static_cast<long long>(x0), q1 = static_cast<long long>(x1);
       if (qpack) {
         // packed g32|h32, one word per bin
@@ -1812,8 +1892,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   __shared__ int s_exp[kFrontierKmax];       // chosen expansions (cids) by order
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
+  const unsigned xep = a.xg ? *a.xep : 0u;  // (xGMI: this round's tag is xep + 1)
   if (st.done) return;
-  if (a.xg && t == 0) *a.xep += 1u;  // (xGMI: this round's exchanges are complete; next tag)
   const int kprev = st.k;
   const int cid_next = st.cid_next;
   const int np = 2 * kprev;
@@ -1884,6 +1964,50 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   // sequential select), the record copied from the winning rank's fpb entry
   const bool merge = a.fpb != nullptr;
   const int nsrc = merge ? a.vote_P : F;
+  if (!kCegb && a.xg && merge) {
+    // ---- A0 (xGMI transport): this rank's best per child over the features it owns -> fpb[rank]
+    // of every rank's exchange buffer, then the handshake (k_f_pair_best's job, folded into the
+    // one-block select: no launch of its own); phase A then merges the P ranks' records
+    constexpr int kKw = static_cast<int>(sizeof(SplitKey) / 4), kIw = static_cast<int>(sizeof(SplitInfo) / 4);
+    for (int q = w; q < np; q += kSelWaves) {
+      if (s_pc[q] < 0) continue;  // (no child, or a skipped expansion's: never merged)
+      double bg = kMinScore;
+      int bf = 0x7fffffff, bp = -1;
+      for (int i = lane; i < a.fown_n; i += 64) {
+        const int f = a.fown_list[i];
+        const SplitKey& kk = a.ckey[static_cast<size_t>(q) * F + f];
+        if (kk.feature >= 0 && FBetter(kk.gain, kk.feature, 0, bg, bf, 0)) {
+          bg = kk.gain;
+          bf = kk.feature;
+          bp = f;
+        }
+      }
+      bp = ReadLane(bp, WaveArgBestLane(bg, bf, 0));
+      const uint32_t* sk = reinterpret_cast<const uint32_t*>(a.ckey + static_cast<size_t>(q) * F + max(bp, 0));
+      const uint32_t* si = reinterpret_cast<const uint32_t*>(a.cinfo + static_cast<size_t>(q) * F + max(bp, 0));
+      const uint32_t v = lane < kKw ? sk[lane] : (lane < kKw + kIw ? si[lane - kKw] : 0u);
+      for (int r = 0; r < a.xP; ++r) {
+        FPairBest* out = reinterpret_cast<FPairBest*>(a.xpeer[r] + a.xo_fpb) + static_cast<size_t>(a.xrank) * 2 * a.kmax + q;
+        if (bp < 0) {
+          // (an empty record: feature -1, gain kMinScore)
+          if (lane == 0) FXStore(reinterpret_cast<uint32_t*>(&out->key.feature), static_cast<uint32_t>(-1));
+          if (lane < 2) FXStore(reinterpret_cast<uint32_t*>(&out->key.gain) + lane,
+                                static_cast<uint32_t>(static_cast<unsigned long long>(__double_as_longlong(kMinScore)) >> (32 * lane)));
+        } else if (lane < kKw) {
+          FXStore(reinterpret_cast<uint32_t*>(&out->key) + lane, v);
+        } else if (lane < kKw + kIw) {
+          FXStore(reinterpret_cast<uint32_t*>(&out->info) + (lane - kKw), v);
+        }
+      }
+    }
+    if (FXPeers(a)) {
+      FXArrive(a, kFXCand, FXTag(a, xep + 1u));  // (one block: it is the last to arrive, and waits)
+    } else {
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    __syncthreads();
+  }
+  if (a.xg && t == 0) *a.xep = xep + 1u;  // this round's exchanges are complete: the next round's tag
   {
     double bg[kSelPairs];
     int bf[kSelPairs], bp[kSelPairs], pn[kSelPairs], pd[kSelPairs];
@@ -1921,8 +2045,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
             kg[u][j] = kMinScore;
             if (pv[j] && f < nsrc) {
               const SplitKey& kk = merge ? a.fpb[static_cast<size_t>(f) * 2 * a.kmax + q].key : a.ckey[static_cast<size_t>(q) * F + f];
-              kf[u][j] = kk.feature;
-              kg[u][j] = kk.gain;
+              FKeyFG(kk, merge && a.xg, &kf[u][j], &kg[u][j]);
             }
           }
         }
@@ -1950,8 +2073,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         // (bynode: the root is scored at its mask, row 0; other children when their parent commits)
         if (q < np && f < nsrc && s_pc[q] >= 0 && !(cegb && a.bynode != nullptr && s_pc[q] == 0 && !a.bynode[f])) {
           const SplitKey& kk = merge ? a.fpb[static_cast<size_t>(f) * 2 * a.kmax + q].key : a.ckey[static_cast<size_t>(q) * F + f];
-          const int kf = kk.feature;
-          const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used, s_pc[q]) : kk.gain);
+          int kf;
+          double kgain;
+          FKeyFG(kk, merge && a.xg, &kf, &kgain);
+          const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used, s_pc[q]) : kgain);
           const int ff = kf < 0 ? 0x7fffffff : kf;
           if (FBetter(g, ff, 0, bg[j], bf[j], 0)) {
             bg[j] = g;
@@ -1980,11 +2105,12 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         const FPairBest* pb = merge ? a.fpb + static_cast<size_t>(fpos) * 2 * a.kmax + q : nullptr;
         const uint32_t* si = reinterpret_cast<const uint32_t*>(merge ? &pb->info : a.cinfo + pos);
         const uint32_t* sk = reinterpret_cast<const uint32_t*>(merge ? &pb->key : a.ckey + pos);
+        const bool sys = merge && a.xg;  // (a record a peer pushed)
         for (int i = lane; i < kInfoWords + kKeyWords; i += 64) {
           if (i < kInfoWords) {
-            reinterpret_cast<uint32_t*>(a.best + c)[i] = si[i];
+            reinterpret_cast<uint32_t*>(a.best + c)[i] = sys ? FXLoad(si + i) : si[i];
           } else {
-            reinterpret_cast<uint32_t*>(a.key + c)[i - kInfoWords] = sk[i - kInfoWords];
+            reinterpret_cast<uint32_t*>(a.key + c)[i - kInfoWords] = sys ? FXLoad(sk + i - kInfoWords) : sk[i - kInfoWords];
           }
         }
       } else if (lane == 0) {
@@ -2782,12 +2908,21 @@ __device__ __forceinline__ int FPairChild(const FArgs& a, int k, int q) {
   return (q & 1) ? x.larger : x.smaller;
 }
 
+__device__ void FVoteBody(const FArgs& a, int k, int q);
+
 __global__ __launch_bounds__(kVoteThreads) void k_f_vote(FArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
   const FState* stp = a.st;
+  const unsigned xep = a.xg ? *a.xep : 0u;
   if (stp->done) return;
-  const int k = stp->k, q = blockIdx.x, F = a.F, K = a.vote_k, t = threadIdx.x;
-  if ((q >> 1) >= k) return;
+  const int k = stp->k, q = blockIdx.x;
+  if ((q >> 1) < k) FVoteBody(a, k, q);
+  // xGMI: the records are in every rank's table once all ranks arrived (one rank: nothing to wait for)
+  if (a.xg && FXPeers(a)) FXArrive(a, kFXVote, FXTag(a, xep + 1u));
+}
+
+__device__ void FVoteBody(const FArgs& a, int k, int q) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int F = a.F, K = a.vote_k, t = threadIdx.x;
   const int c = FPairChild(a, k, q);
   double* s_gain = reinterpret_cast<double*>(smem);
   int* s_cnt = reinterpret_cast<int*>(s_gain + F);
@@ -2802,7 +2937,9 @@ __global__ __launch_bounds__(kVoteThreads) void k_f_vote(FArgs a) {
     nv += valid ? 1 : 0;
   }
   const int nvalid = BlockSumInt(nv, s_n);  // (barrier inside: the LDS arrays are complete)
-  VoteRec* out = a.vrec + (static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q) * K;
+  // (xGMI: the records go to row `rank` of every rank's table)
+  const int npeer = a.xg ? a.xP : 1;
+  const size_t roff = (static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q) * K;
   for (int f = t; f < F; f += blockDim.x) {
     if (s_cnt[f] < 0) continue;
     const double g = s_gain[f];
@@ -2813,7 +2950,8 @@ __global__ __launch_bounds__(kVoteThreads) void k_f_vote(FArgs a) {
       r.gain = g;
       r.feature = f;
       r.count = s_cnt[f];
-      out[rank] = r;
+      if (!a.xg) a.vrec[roff + rank] = r;
+      for (int p = 0; a.xg && p < npeer; ++p) FXStoreRec(reinterpret_cast<VoteRec*>(a.xpeer[p] + a.xo_vrec) + roff + rank, r);
     }
   }
   for (int i = nvalid + t; i < K; i += blockDim.x) {
@@ -2821,7 +2959,8 @@ __global__ __launch_bounds__(kVoteThreads) void k_f_vote(FArgs a) {
     r.gain = kMinScore;
     r.feature = -1;
     r.count = 0;
-    out[i] = r;
+    if (!a.xg) a.vrec[roff + i] = r;
+    for (int p = 0; a.xg && p < npeer; ++p) FXStoreRec(reinterpret_cast<VoteRec*>(a.xpeer[p] + a.xo_vrec) + roff + i, r);
   }
   // the local candidates are consumed: the global pass fills the elected features' entries
   for (int f = t; f < F; f += blockDim.x) {
@@ -2843,7 +2982,8 @@ __device__ int FElect(const FArgs& a, int q, int c, double* s_w, int* s_f, int* 
   const float mean = static_cast<float>(a.nodes[c].gcount) / static_cast<float>(P);
   for (int i = t; i < R; i += blockDim.x) {
     const int r = i / K, j = i - r * K;
-    const VoteRec v = a.vrec[(static_cast<size_t>(r) * 2 * a.kmax + q) * K + j];
+    const VoteRec* vp = a.vrec + (static_cast<size_t>(r) * 2 * a.kmax + q) * K + j;
+    const VoteRec v = a.xg ? FXLoadRec(vp) : *vp;
     const double w = v.gain * v.count / static_cast<double>(mean);
     const bool valid = v.feature >= 0 && w > kMinScore;
     s_w[i] = w;
@@ -2883,12 +3023,21 @@ __device__ int FElect(const FArgs& a, int q, int c, double* s_w, int* s_f, int* 
   return n;
 }
 
+__device__ void FElectBody(const FArgs& a, int k, int q);
+
 __global__ __launch_bounds__(kVoteThreads) void k_f_elect(FArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
   const FState* stp = a.st;
+  const unsigned xep = a.xg ? *a.xep : 0u;
   if (stp->done) return;
-  const int k = stp->k, q = blockIdx.x, K = a.vote_k, R = a.vote_P * K, t = threadIdx.x;
-  if ((q >> 1) >= k) return;
+  const int k = stp->k, q = blockIdx.x;
+  if ((q >> 1) < k) FElectBody(a, k, q);
+  // xGMI: every rank's rows are summed into every rank's row block once all ranks arrived
+  if (a.xg && FXPeers(a)) FXArrive(a, kFXVRows, FXTag(a, xep + 1u));
+}
+
+__device__ void FElectBody(const FArgs& a, int k, int q) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int K = a.vote_k, R = a.vote_P * K, t = threadIdx.x;
   const int c = FPairChild(a, k, q);
   int* el = a.velect + static_cast<size_t>(q) * (K + 1);
   if (q == 0 && a.exps[0].parent < 0 && t == 0) {
@@ -2925,10 +3074,16 @@ __global__ __launch_bounds__(kVoteThreads) void k_f_elect(FArgs a) {
   const double* slot = a.slots + static_cast<size_t>(c) * 2 * a.TB;
   for (int j = 0; j < n; ++j) {
     const DevFeature fi = a.feat[s_list[j]];
-    unsigned long long* dst = a.vrows + (static_cast<size_t>(q) * K + j) * row;
+    const size_t o = (static_cast<size_t>(q) * K + j) * row;
     const double* src = slot + 2 * static_cast<size_t>(fi.hist_offset);
     for (int v = t; v < 2 * (fi.num_bin - 1); v += blockDim.x) {
-      dst[v] = static_cast<unsigned long long>(__double2ll_rn(src[v] * ((v & 1) ? sh : sg)));
+      const unsigned long long x = static_cast<unsigned long long>(__double2ll_rn(src[v] * ((v & 1) ? sh : sg)));
+      if (!a.xg) {
+        a.vrows[o + v] = x;  // (summed over ranks in place by the all-reduce)
+      } else if (x != 0ull) {
+        // xGMI: added into every rank's row block (exact integers; k_f_vote_scan re-zeroes its own)
+        for (int p = 0; p < a.xP; ++p) FXAdd(reinterpret_cast<unsigned long long*>(a.xpeer[p] + a.xo_vrows) + o + v, x);
+      }
     }
   }
 }
@@ -2961,7 +3116,9 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
   const int n = a.nodes[c].gcount;
   double sgs = 0.0, shs = 0.0;
   for (int v = lane; v < 2 * (fi.num_bin - 1); v += 64) {
-    const double x = static_cast<double>(static_cast<long long>(rows[v])) * ((v & 1) ? inv_h : inv_g);
+    const unsigned long long rv = a.xg ? FXLoad64(rows + v) : rows[v];
+    const double x = static_cast<double>(static_cast<long long>(rv)) * ((v & 1) ? inv_h : inv_g);
+    if (a.xg) FXStore64(const_cast<unsigned long long*>(rows) + v, 0ull);  // (xGMI: the next round adds into it)
     const int kb = v >> 1;
     const int b = kb < fi.mfb ? kb : kb + 1;
     H[2 * b + (v & 1)] = x;
@@ -3041,39 +3198,11 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
 // features' candidates -> fpb[rank]; after the all-gather the select's phase A takes the best over
 // the ranks' records (gain desc, then feature asc: the order of the sequential select, so the tree
 // equals the one-rank tree).
-// xGMI transport: the record is stored into fpb[rank] of EVERY rank's exchange buffer and the
-// launch's last block completes the exchange (k_f_select, next on the stream, reads all P rows).
-__device__ __forceinline__ void FPairStore(const FArgs& a, int q, const SplitKey* key, const SplitInfo* info) {
-  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
-  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
-  const int lane = threadIdx.x;
-  const int np = a.xg ? a.xP : 1;
-  for (int r = 0; r < np; ++r) {
-    FPairBest* base = a.xg ? reinterpret_cast<FPairBest*>(a.xpeer[r] + a.xo_fpb) : a.fpb;
-    FPairBest* out = base + static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q;
-    if (key == nullptr) {
-      if (lane == 0) {
-        out->key.feature = -1;
-        out->key.gain = kMinScore;
-      }
-      continue;
-    }
-    for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
-      if (i < kKeyWords) reinterpret_cast<uint32_t*>(&out->key)[i] = reinterpret_cast<const uint32_t*>(key)[i];
-      else reinterpret_cast<uint32_t*>(&out->info)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(info)[i - kKeyWords];
-    }
-  }
-}
-
 __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
   const FState* stp = a.st;
-  const unsigned xep = a.xg ? *a.xep : 0u;
   if (stp->done) return;
   const int k = stp->k, q = blockIdx.x, F = a.F, lane = threadIdx.x;
-  if ((q >> 1) >= k) {
-    if (a.xg) FXArrive(a, kFXCand, FXTag(a, xep + 1u));  // (every block arrives)
-    return;
-  }
+  if ((q >> 1) >= k) return;
   const int c = FPairChild(a, k, q);
   double bg = kMinScore;
   int bf = 0x7fffffff, bp = -1;
@@ -3090,9 +3219,21 @@ __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
   }
   const int src = WaveArgBestLane(bg, bf, 0);
   bp = ReadLane(bp, src);
-  const size_t o = static_cast<size_t>(q) * F + (bp < 0 ? 0 : bp);
-  FPairStore(a, q, bp < 0 ? nullptr : a.ckey + o, bp < 0 ? nullptr : a.cinfo + o);
-  if (a.xg) FXArrive(a, kFXCand, FXTag(a, xep + 1u));
+  FPairBest* out = a.fpb + static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q;
+  constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
+  constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
+  if (bp < 0) {
+    if (lane == 0) {
+      out->key.feature = -1;
+      out->key.gain = kMinScore;
+    }
+    return;
+  }
+  const size_t o = static_cast<size_t>(q) * F + bp;
+  for (int i = lane; i < kKeyWords + kInfoWords; i += 64) {
+    if (i < kKeyWords) reinterpret_cast<uint32_t*>(&out->key)[i] = reinterpret_cast<const uint32_t*>(a.ckey + o)[i];
+    else reinterpret_cast<uint32_t*>(&out->info)[i - kKeyWords] = reinterpret_cast<const uint32_t*>(a.cinfo + o)[i - kKeyWords];
+  }
 }
 
 // xGMI root exchange (one block, once per tree, after k_f_init_root): this rank's root sums and
@@ -3107,16 +3248,17 @@ __global__ __launch_bounds__(64) void k_fx_root(FArgs a, unsigned* __restrict__ 
     mine.g = s.x;
     mine.h = s.y;
     for (int i = 0; i < 4; ++i) mine.m[i] = ghmax[i];
-    reinterpret_cast<FXRoot*>(a.xpeer[threadIdx.x] + a.xo_root)[a.xrank] = mine;
+    FXStoreRec(reinterpret_cast<FXRoot*>(a.xpeer[threadIdx.x] + a.xo_root) + a.xrank, mine);
   }
-  FXArrive(a, kFXRoot, FXTag(a, xep + 1u));
+  if (FXPeers(a)) FXArrive(a, kFXRoot, FXTag(a, xep + 1u));
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
     const FXRoot* rows = reinterpret_cast<const FXRoot*>(a.xpeer[a.xrank] + a.xo_root);
     double g = 0.0, h = 0.0;
     unsigned m[4] = {0u, 0u, 0u, 0u};
     for (int q = 0; q < a.xP; ++q) {
-      const FXRoot x = rows[q];
+      const FXRoot x = FXLoadRec(rows + q);
       g += x.g;
       h += x.h;
       for (int i = 0; i < 4; ++i) m[i] = max(m[i], x.m[i]);
@@ -3129,18 +3271,19 @@ __global__ __launch_bounds__(64) void k_fx_root(FArgs a, unsigned* __restrict__ 
 // Set-up self-test of the transport (session 0): round r, every rank adds rank + 1 + r into
 // words [half, half + n) of every peer's receive chunk and stores a pattern word into its fpb row
 // there; after the handshake k_fx_check verifies its own chunk (sum over ranks) and clears it.
-// Halves alternate by round, so a rank already pushing round r + 1 never touches what a slower
-// peer still checks.
+// Halves (of the chunk and of the pattern words) alternate by round, so a rank already pushing
+// round r + 1 never touches what a slower peer still checks.
 __global__ __launch_bounds__(256) void k_fx_push(FArgs a, int round, int n) {
   const int half = (round & 1) * n;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     for (int q = 0; q < a.xP; ++q) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.xpeer[q] + a.xo_recv) + half + i,
-                static_cast<unsigned long long>(a.xrank + 1 + round));
+      FXAdd(reinterpret_cast<unsigned long long*>(a.xpeer[q] + a.xo_recv) + half + i,
+            static_cast<unsigned long long>(a.xrank + 1 + round));
     }
   }
   if (blockIdx.x == 0 && threadIdx.x < a.xP) {
-    reinterpret_cast<unsigned*>(a.xpeer[threadIdx.x] + a.xo_fpb)[a.xrank] = 0xA5000000u + 256u * round + a.xrank;
+    FXStore(reinterpret_cast<uint32_t*>(a.xpeer[threadIdx.x] + a.xo_fpb) + (round & 1) * kMaxXRanks + a.xrank,
+            0xA5000000u + 256u * round + a.xrank);
   }
   FXArrive(a, kFXTest, FXTag(a, static_cast<unsigned>(round + 1)));
 }
@@ -3151,11 +3294,11 @@ __global__ __launch_bounds__(256) void k_fx_check(FArgs a, int round, int n, uns
   unsigned long long* rx = reinterpret_cast<unsigned long long*>(a.xpeer[a.xrank] + a.xo_recv);
   unsigned bad = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    bad += rx[half + i] != want ? 1u : 0u;
-    rx[half + i] = 0ull;
+    bad += FXLoad64(rx + half + i) != want ? 1u : 0u;
+    FXStore64(rx + half + i, 0ull);
   }
   if (blockIdx.x == 0 && threadIdx.x < a.xP) {
-    const unsigned v = reinterpret_cast<const unsigned*>(a.xpeer[a.xrank] + a.xo_fpb)[threadIdx.x];
+    const unsigned v = FXLoad(reinterpret_cast<const uint32_t*>(a.xpeer[a.xrank] + a.xo_fpb) + (round & 1) * kMaxXRanks + threadIdx.x);
     bad += v != 0xA5000000u + 256u * round + threadIdx.x ? 1u : 0u;
   }
   if (bad) atomicAdd(err, bad);

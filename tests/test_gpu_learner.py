@@ -392,8 +392,8 @@ def test_feature_parallel_multirank_rehearsal(lgb, gpu_required, transport):
 def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport, topk):
     """Device voting-parallel (PV-Tree: local scan, top-k vote all-gathered, elected features'
     histograms summed, global scan of the elected features only), P ranks sharing the GPU: every
-    rank grows the identical model, equal to the host voting learner tree for tree. Over
-    collectives it runs on the frontier engine (all expansions of a round voted at once)."""
+    rank grows the identical model, equal to the host voting learner tree for tree. Both transports
+    run on the frontier engine (all expansions of a round voted at once)."""
     import json
     import os
     import subprocess
@@ -409,9 +409,9 @@ def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert "voting-parallel" in res["device_name"], res
     assert ("xGMI" in res["device_name"]) == (transport == "xgmi"), res
-    # collectives: the frontier engine (local pass, vote all-gather, elected rows all-reduced
-    # exactly, global pass per round); xGMI keeps the sequential chain's in-kernel exchange
-    assert ("frontier engine" in res["device_name"]) == (transport == "collective"), res
+    # the frontier engine (local pass, top-k votes exchanged, elected rows summed exactly, global
+    # pass per round): over collectives (all-gather + all-reduce) or pushed in-kernel over xGMI
+    assert "frontier engine" in res["device_name"], res
     assert res["ranks_identical"], res
     assert res["num_trees"] == 10
     assert res["identical_leading_trees"] == 10, res
