@@ -33,9 +33,9 @@
 // are captured into hipGraphs (main graph for the predicted round count plus a
 // 4-round continuation graph replayed until the tree is done).
 //
-// SEQUENTIAL engine (the explicit xGMI transports of the distributed learners, histogram
-// budgets the frontier's select cannot hold in LDS): a FIXED kernel sequence per split
-// (kernels: seq_kernels.h, seq_{hist,scan,vote,partition}_kernels.hip):
+// SEQUENTIAL engine (configurations the frontier does not hold: histogram budgets its select
+// cannot hold in LDS, the distributed learners with extra trees or by-node sampling): a FIXED
+// kernel sequence per split (kernels: seq_kernels.h, seq_{hist,scan,vote,partition}_kernels.hip):
 //   partition  best-leaf select from the candidate table, stable partition of the
 //              parent range (decoupled look-back), post-split bookkeeping: ranges,
 //              sums, depth, monotone bounds, smaller / larger child, slot handoff
@@ -43,22 +43,24 @@
 //   scan       one workgroup per feature: slab fold (or the owner rows), parent -
 //              smaller subtraction, mfb reconstruction, threshold / categorical scans
 // Every launch has a fixed grid and exits early when the tree is done, so the
-// sequence is captured once into a hipGraph and replayed per tree.
+// sequence is captured once into a hipGraph and replayed per tree. Its distributed modes
+// exchange through collectives (RCCL or the host-staged rehearsal transport).
 //
-// Distributed frontier modes (one rank per GPU, exchanges over RCCL or the host-staged
-// rehearsal transport):
-//   data     every rank partitions / histograms its own rows; the round's fixed-point
-//            accumulators are all-reduced exactly (one RCCL uint64 all-reduce per round,
-//            serialised between the histograms and the scans; LGAP_DP_PIPELINE=1 splits it
-//            in halves on a comm stream), and every rank scans and selects redundantly
-//   voting   the local pass (local sums / counts / config), one all-gather of the round's
-//            top-k votes, the election, one exact all-reduce of the elected rows only, and
-//            the global pass over them (PV-Tree per round)
+// Distributed frontier modes (one rank per GPU). Default transport: the in-kernel xGMI exchange
+// (FArgs::xg: pushes into the peers' IPC-mapped exchange buffers, flag handshakes in the
+// producing launches' last blocks, no collective or extra launch per round); collectives
+// (RCCL / host-staged) when LGAP_DP_TRANSPORT=collective or the set-up self-test fails:
+//   data     owner-computes: every rank partitions / histograms its own rows, k_f_reduce adds
+//            each bin into its owner's receive chunk (collectives: one exact reduce-scatter),
+//            owners scan their features, the select pushes per-child bests and merges the
+//            ranks' records (collectives: k_f_pair_best + all-gather). Configurations that need
+//            every feature's candidates on every rank all-reduce the round's accumulators and
+//            scan redundantly (LGAP_DP_PIPELINE=1 splits that all-reduce on a comm stream)
+//   voting   the local pass (local sums / counts / config), the round's top-k votes exchanged,
+//            the election, the elected rows summed exactly over ranks, and the global pass
+//            over them (PV-Tree per round)
 //   feature  every rank holds all rows and grows the same partition; each scans the
-//            features of the groups it owns and the per-child bests are all-gathered
-// With LGAP_DP_TRANSPORT=xgmi the sequential chain pushes each owner its bins (in-kernel
-// exchange over IPC-mapped buffers), scans only the features it owns and fills one slice of
-// the candidate table that all ranks then read.
+//            features of the groups it owns and the per-child bests are exchanged
 //
 // By-node sampling and extra trees also run on the frontier (masks / random thresholds drawn
 // in the host learner's order); linear_tree leaves are fitted after the structure (fp64 MFMA
@@ -220,8 +222,6 @@ class DeviceTreeLearner : public TreeLearner {
     if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
     for (auto& kv : fgraphs_) (void)hipGraphExecDestroy(kv.second);
     if (fcont_) (void)hipGraphExecDestroy(fcont_);
-    if (!x_peers_.empty()) XgmiClose(x_local_, &x_peers_);
-    if (x_local_) (void)hipFree(x_local_);
     if (!fx_peers_.empty()) XgmiClose(fx_local_, &fx_peers_);
     if (fx_local_) (void)hipFree(fx_local_);
     for (auto& ev : pipe_ev_) {
@@ -357,11 +357,10 @@ class DeviceTreeLearner : public TreeLearner {
     }
   }
 
-  // Transport of the owner-computes exchanges. LGAP_DP_TRANSPORT = auto (default: xGMI
-  // in-kernel exchange when every rank maps every peer and the self-test passes, else
-  // collectives) | xgmi | collective.
+  // Transport of the distributed exchanges. LGAP_DP_TRANSPORT = auto (default: the frontier's
+  // xGMI in-kernel exchange when every rank maps every peer and the self-test passes, else
+  // collectives) | xgmi | collective | allreduce.
   void SetupTransport() {
-    transport_ = 0;
     if (!owner_scan_ && !voting_) return;
     const char* e = std::getenv("LGAP_DP_TRANSPORT");
     const std::string want = e ? e : "auto";
@@ -379,60 +378,8 @@ class DeviceTreeLearner : public TreeLearner {
       else if (want == "xgmi") Log::Warning("xGMI transport: this frontier configuration exchanges through collectives");
       return;
     }
-    if (want == "collective" || want == "allreduce" || P_ > kMaxXRanks) return;
-    const size_t es = use_dp_ ? sizeof(double) : sizeof(float);
-    ArenaLayout lay;
-    x_off_hist_ = static_cast<int>(lay.Add<char>(static_cast<size_t>(P_) * 2 * bbin_ * es));
-    x_off_cand_ = static_cast<int>(lay.Add<char>(static_cast<size_t>(P_) * cand_stride_));
-    x_off_flag_ = static_cast<int>(lay.Add<unsigned long long>(4 * kMaxXRanks));
-    x_off_root_ = static_cast<int>(lay.Add<double2>(kMaxXRanks));
-    x_bytes_ = lay.bytes();
-    // uncached device memory: peers' pushes land in HBM and every read of it is fresh
-    void* p = nullptr;
-    if (hipExtMallocWithFlags(&p, x_bytes_, hipDeviceMallocUncached) != hipSuccess) {
-      (void)hipGetLastError();
-      p = nullptr;
-      if (hipExtMallocWithFlags(&p, x_bytes_, hipDeviceMallocFinegrained) != hipSuccess) {
-        (void)hipGetLastError();
-        p = nullptr;
-      }
-    }
-    int ok = p != nullptr ? 1 : 0;
-    if (ok) HIP_CHECK(hipMemset(p, 0, x_bytes_));
-    if (P_ > 1) ok = Network::GlobalSyncUpByMin(ok);
-    if (!ok) {
-      if (p) (void)hipFree(p);
-      if (want == "xgmi") Log::Fatal("xGMI transport: cannot allocate the uncached exchange buffer");
-      Log::Warning("xGMI transport unavailable (exchange buffer); using collectives");
-      return;
-    }
-    x_local_ = static_cast<char*>(p);
-    if (!XgmiOpen(x_local_, &x_peers_)) {
-      (void)hipFree(x_local_);
-      x_local_ = nullptr;
-      if (want == "xgmi") Log::Fatal("xGMI transport: peer exchange buffers could not be mapped");
-      Log::Warning("xGMI transport unavailable (IPC mapping); using collectives");
-      return;
-    }
-    XPeers xp;
-    std::memset(&xp, 0, sizeof(xp));
-    for (int q = 0; q < P_; ++q) xp.base[q] = x_peers_[q];
-    xpeers_.Resize(1);
-    xpeers_.Upload(&xp, 1, stream_);
-    transport_ = 2;
-    const bool good = XgmiSelfTest();
-    int all_good = good ? 1 : 0;
-    if (P_ > 1) all_good = Network::GlobalSyncUpByMin(all_good);
-    if (!all_good) {
-      transport_ = 0;
-      XgmiClose(x_local_, &x_peers_);
-      (void)hipFree(x_local_);
-      x_local_ = nullptr;
-      if (want == "xgmi") Log::Fatal("xGMI transport: self-test failed");
-      Log::Warning("xGMI transport self-test failed; using collectives");
-      return;
-    }
-    InvalidateGraph();
+    // the sequential chain (configurations the frontier does not hold) exchanges through collectives
+    if (want == "xgmi") Log::Warning("xGMI transport: the sequential chain exchanges through collectives");
   }
 
   // The distributed frontier's in-kernel exchange (FArgs::xg): one uncached exchange buffer per
@@ -504,35 +451,6 @@ class DeviceTreeLearner : public TreeLearner {
     InvalidateGraph();
   }
 
-  // Three exchanges of a known pattern through the histogram rows (session 0 tags,
-  // below every training tag), checked value by value on every rank.
-  bool XgmiSelfTest() {
-    Args a = MakeArgs(0);
-    a.xsession = 0;
-    const double saved = a.xtimeout;
-    a.xtimeout = static_cast<unsigned long long>(100e6 * std::min(30.0, std::max(1.0, saved / 100e6)));
-    DevBuf<unsigned> err(1);
-    err.Zero(stream_);
-    const int nvals = std::min(bbin_, 2048);
-    for (int round = 0; round < 4; ++round) {
-      k_x_selftest<<<4, 256, 0, stream_>>>(a, round, nvals, err.get());
-      k_x_selfcheck<<<4, 256, 0, stream_>>>(a, round, nvals, err.get());
-    }
-    HIP_CHECK(hipGetLastError());
-    unsigned h[4] = {0, 0, 0, 0};
-    err.Download(h, 1, stream_);
-    unsigned* hb = pin_bar_.Get(4);
-    HIP_CHECK(hipMemcpyAsync(hb, bar_.get(), 4 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-    const bool ok = h[0] == 0u && hb[3] == 0u;
-    if (!ok) {
-      Log::Warning("xGMI self-test on rank %d: %u wrong values, wait status %u", rank_, h[0], hb[3]);
-      bar_.Zero(stream_);
-      HIP_CHECK(hipStreamSynchronize(stream_));
-    }
-    return ok;
-  }
-
   std::string ParallelDesc() const {
     std::string m = mode_ == DevParallel::kFeature ? "feature-parallel"
                                                    : (voting_ ? "voting-parallel" : "data-parallel");
@@ -546,7 +464,6 @@ class DeviceTreeLearner : public TreeLearner {
       if (ffeature_ || fvoting_) return m + "frontier engine, " + via;
       return m + "frontier engine, all-reduce per round (" + via + ")";
     }
-    if (transport_ == 2) return m + "xGMI in-kernel exchange";
     if (HostStagedDP()) return m + "host-staged collectives";
     return m + "RCCL reduce-scatter/all-gather";
   }
@@ -2624,7 +2541,7 @@ class DeviceTreeLearner : public TreeLearner {
     // enqueue stays ahead of the ~40 us splits. The host-staged rehearsal transport
     // synchronises inside its all-reduce and is never captured.
     // the xGMI transport keeps every exchange inside the kernels: the tree replays as one graph
-    const bool collectives = (owner_scan_ || voting_) && transport_ != 2;
+    const bool collectives = owner_scan_ || voting_;
     const bool use_graph = config_->device_use_graph && (!collectives || (DPGraphEnabled() && !HostStagedDP()));
     if (use_graph) {
       if (graph_exec_ && distributed_ && graph_comm_ != ActiveComm()) InvalidateGraph();
@@ -2649,10 +2566,6 @@ class DeviceTreeLearner : public TreeLearner {
       HIP_CHECK(hipStreamSynchronize(stream_));
     }
     if (hbar[2] != 0u) Log::Fatal("k_partition: a wait on published tile counts timed out (blocks not co-resident?)");
-    if (hbar[3] != 0u) {
-      Log::Fatal("xGMI exchange (%s) timed out on rank %d after %.0f s: a peer stopped training",
-                 hbar[3] == 1u ? "histogram" : (hbar[3] == 2u ? "split candidates" : "root sums"), rank_, XTimeoutSeconds());
-    }
     // the control buffer written last holds the final tree state
     const Ctl* hc = hc2[1].num_splits > hc2[0].num_splits ? &hc2[1] : &hc2[0];
     bynode_draws_ = 1 + 2 * hc->scan_round;  // the root's mask, two per scanned split
@@ -3254,7 +3167,7 @@ class DeviceTreeLearner : public TreeLearner {
         k_hist_owner<float><<<ogrid, 1024, 0, stream_>>>(a, HistBlocks(), reinterpret_cast<float*>(stage_.get()));
       }
       HIP_CHECK(hipGetLastError());
-      if (transport_ != 2) ReduceScatterSum(stage_.get(), rx_.get(), 2 * static_cast<size_t>(bbin_), use_dp_, stream_);
+      ReduceScatterSum(stage_.get(), rx_.get(), 2 * static_cast<size_t>(bbin_), use_dp_, stream_);
     }
   }
 
@@ -3274,7 +3187,7 @@ class DeviceTreeLearner : public TreeLearner {
     LaunchReduceScan(a, Fmax_);
     HIP_CHECK(hipGetLastError());
     // complete the candidate table (xGMI: inside k_reduce_scan)
-    if (owner_scan_ && transport_ != 2 && P_ > 1) AllGatherInPlace(cand_.get(), cand_stride_, stream_);
+    if (owner_scan_ && P_ > 1) AllGatherInPlace(cand_.get(), cand_stride_, stream_);
   }
 
   void LaunchReduceScan(const Args& a0, int grid) {
@@ -3282,7 +3195,7 @@ class DeviceTreeLearner : public TreeLearner {
     Args a = a0;
     // slab rows folded by fold_chunks_ blocks per feature (single GPU / feature parallel /
     // voting local pass); the exchange transport counts its blocks, so it keeps one per feature
-    if (fold_chunks_ > 1 && a.scan_src == 0 && !scan_global_ && a.transport != 2 && a.fold_cnt) {
+    if (fold_chunks_ > 1 && a.scan_src == 0 && !scan_global_ && a.fold_cnt) {
       a.fold_chunks = fold_chunks_;
       a.fold_feats = grid;
       grid = (grid * fold_chunks_ + 7) & ~7;
@@ -3308,7 +3221,6 @@ class DeviceTreeLearner : public TreeLearner {
     al.cand_stride = cand_stride_;
     al.rank = 0;
     al.P = 1;
-    al.transport = 0;
     al.own_feat = nullptr;
     al.sp.min_data_in_leaf = config_->min_data_in_leaf / P_;  // integer division (reference :61-63)
     al.sp.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf / P_;
@@ -3316,14 +3228,12 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipGetLastError());
     k_vote_local<<<1, kVoteThreads, vote_local_lds_, stream_>>>(a);
     HIP_CHECK(hipGetLastError());
-    if (transport_ != 2) AllGatherInPlace(vrec_.get(), 2 * static_cast<size_t>(topk_) * sizeof(VoteRec), stream_);
+    AllGatherInPlace(vrec_.get(), 2 * static_cast<size_t>(topk_) * sizeof(VoteRec), stream_);
     if (use_dp_) k_vote_pack<double><<<2 * topk_, kVoteThreads, vote_pack_lds_, stream_>>>(a);
     else k_vote_pack<float><<<2 * topk_, kVoteThreads, vote_pack_lds_, stream_>>>(a);
     HIP_CHECK(hipGetLastError());
-    if (transport_ != 2) {
-      if (use_dp_) AllreduceSumF64(reinterpret_cast<double*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
-      else AllreduceSumF32(reinterpret_cast<float*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
-    }
+    if (use_dp_) AllreduceSumF64(reinterpret_cast<double*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
+    else AllreduceSumF32(reinterpret_cast<float*>(vhist_.get()), static_cast<size_t>(vcap_), stream_);
     const size_t vlds = scan_global_ ? 0 : vote_scan_lds_;
     if (use_dp_) {
       if (scan_global_) k_vote_scan<double, true><<<topk_, 128, 0, stream_>>>(a);
@@ -3691,7 +3601,6 @@ class DeviceTreeLearner : public TreeLearner {
     }
     rx_.Resize(std::max<size_t>(1, 2 * static_cast<size_t>(bbin_) * (use_dp_ ? 8 : 4)));
     stage_.Resize(owner_scan_ ? static_cast<size_t>(P_) * 2 * bbin_ * (use_dp_ ? 8 : 4) : 1);
-    ++xsession_;  // exchange tags of this state start above every earlier one
     use_ic_ = !config_->interaction_constraints_vector.empty();
     if (use_ic_) {
       const auto& sets = config_->interaction_constraints_vector;
@@ -3809,7 +3718,7 @@ class DeviceTreeLearner : public TreeLearner {
     a.Fmax = Fmax_;
     a.cand_rows = owner_scan_ ? P_ : 1;
     a.own_feat = owner_scan_ ? own_feat_.get() : nullptr;
-    a.cand = transport_ == 2 && owner_scan_ ? x_local_ + x_off_cand_ : cand_.get();
+    a.cand = cand_.get();
     a.cand_stride = cand_stride_;
     a.cand_key_bytes = cand_key_bytes_;
     if (voting_) {
@@ -3828,24 +3737,13 @@ class DeviceTreeLearner : public TreeLearner {
       a.vcap = vcap_;
       a.elect = elect_.get();
     }
-    // data parallel: the scan sums owner rows (xGMI: every rank's pushed row; collectives:
-    // the reduce-scattered row); single GPU / feature parallel: the local slab rows
+    // data parallel: the scan reads the reduce-scattered owner row; single GPU / feature parallel:
+    // the local slab rows
     a.scan_src = (owner_scan_ && data_parallel_) ? 1 : 0;
-    a.nparts = transport_ == 2 ? P_ : 1;
-    a.rx = transport_ == 2 ? static_cast<const void*>(x_local_ + x_off_hist_) : static_cast<const void*>(rx_.get());
+    a.rx = rx_.get();
     a.own_bin0 = h_bin_lo_.empty() ? 0 : h_bin_lo_[rank_];
     a.bbin = bbin_;
     a.bin_lo = bin_lo_.get();
-    a.transport = transport_;
-    a.xp = transport_ == 2 ? xpeers_.get() : nullptr;
-    a.x_off_hist = x_off_hist_;
-    a.x_off_cand = x_off_cand_;
-    a.x_off_flag = x_off_flag_;
-    a.x_off_root = x_off_root_;
-    a.xcnt = xcnt_.get();
-    a.xsession = xsession_;
-    a.xtimeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
-    a.xfault = std::getenv("LGAP_FAULT_INJECT") != nullptr && std::strcmp(std::getenv("LGAP_FAULT_INJECT"), "xgmi") == 0;
     SplitParams& p = a.sp;
     p.lambda_l1 = config_->lambda_l1;
     p.lambda_l2 = config_->lambda_l2;
@@ -3873,10 +3771,7 @@ class DeviceTreeLearner : public TreeLearner {
     const int root_blocks = RootBlocks();
     k_root_sums<<<root_blocks, kRootThreads, 0, s>>>(a);
     k_root_final<<<1, kRootThreads, 0, s>>>(a, root_blocks);
-    if (distributed_) {
-      if (transport_ == 2) k_x_root<<<1, 64, 0, s>>>(a);
-      else AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
-    }
+    if (distributed_) AllreduceSumF64(reinterpret_cast<double*>(lsum_.get()), 2, s);
     LaunchHist(a);
     LaunchScan(a);
     for (int it = 0; it < L_ - 1; ++it) {
@@ -4260,14 +4155,6 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<VoteRec> vrec_;
   DevBuf<int> elect_;
   DevBuf<double2> hsum_part_, lsum_loc_;
-  // xGMI transport
-  int transport_ = 0;
-  char* x_local_ = nullptr;
-  std::vector<char*> x_peers_;
-  size_t x_bytes_ = 0;
-  int x_off_hist_ = 0, x_off_cand_ = 0, x_off_flag_ = 0, x_off_root_ = 0;
-  DevBuf<XPeers> xpeers_;
-  unsigned xsession_ = 0;
   // frontier xGMI transport (SetupFrontierXgmi; FArgs::xg)
   bool fxg_ = false;
   char* fx_local_ = nullptr;

@@ -504,41 +504,18 @@ __global__ __launch_bounds__(1024) void k_hist_reduce(Args a, int hist_grid, Out
 }
 
 // ---------------------------------------------------------------------------
-// Owner-computes data parallelism (reference data_parallel_tree_learner.cpp:225-302,
-// 305-450 and parallel_tree_learner.h:209-232, redesigned for one node of MI355X):
-// ranks own contiguous, bin-balanced ranges of feature groups; per split the
-// smaller child's histogram is reduce-scattered by ownership, each rank scans only
-// the features it owns, and the per-feature candidates are all-gathered into the
-// candidate table every rank's select reads (so every rank applies the same split).
-//
-// Two transports carry the two exchanges:
-//  * collectives between kernels (transport 0): k_hist_owner writes the owner-permuted
-//    histogram row, ncclReduceScatter delivers this rank's block, k_reduce_scan writes
-//    its candidate block, ncclAllGather completes the table (host-staged for the
-//    one-GPU multi-process rehearsal);
-//  * xGMI in-kernel exchange (transport 2): the same kernels PUSH their payloads into
-//    the peers' IPC-mapped exchange buffers (uncached device memory) and complete the
-//    exchange inside the launch: every block makes its stores visible system-wide and
-//    arrives on a local counter; the last block to arrive tags flag[kind][me] in every
-//    peer and waits until all ranks tagged its own flags. The consumer is the next
-//    kernel on the stream, so no collective call, host round trip or extra launch sits
-//    in the split chain, and the whole tree still replays as one hipGraph.
-// Tags are (session << 32) | split epoch: strictly increasing, never reset, so a flag
-// is only ever compared for "reached". Every wait is bounded (error bar[3]).
-
-
-
-// flag[kind][src] inside rank `owner`'s exchange buffer
-
-// spin until every rank has tagged flag[kind][*] of this rank with `tag` (one lane)
-
-// Called by every thread of every block after the block's pushes to the peers.
+// Owner-computes data parallelism on the sequential chain (reference
+// data_parallel_tree_learner.cpp:225-302, 305-450 and parallel_tree_learner.h:209-232): ranks own
+// contiguous, bin-balanced ranges of feature groups; per split the smaller child's histogram is
+// reduce-scattered by ownership (ncclReduceScatter, or the host-staged rehearsal collectives), each
+// rank scans only the features it owns, and the per-feature candidates are all-gathered into the
+// candidate table every rank's select reads. (The chain serves configurations the frontier engine
+// does not hold; the frontier's exchanges run in-kernel over xGMI, frontier_kernels.hip.)
 
 // Fold the smaller child's slab rows into the owner-permuted layout: destination q of
 // [P][2 * bbin] takes value 2 * bin_lo[r] + l of the local histogram (r = q / (2 bbin),
-// l = q % (2 bbin)); padding positions carry zeros. Transport 0 writes the row to
-// `stage` (then ncclReduceScatter); transport 2 pushes block r straight into rank r's
-// receive row `me` and completes the exchange in-kernel.
+// l = q % (2 bbin)); padding positions carry zeros. The row goes to `stage` (then
+// ncclReduceScatter).
 template <typename Acc>
 __global__ __launch_bounds__(1024) void k_hist_owner(Args a, int hist_grid, Acc* __restrict__ stage) {
   __shared__ double part[16][64];
@@ -565,64 +542,8 @@ __global__ __launch_bounds__(1024) void k_hist_owner(Args a, int hist_grid, Acc*
     double t = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += part[i][lane];
-    if (a.transport == 2) {
-      if (valid) reinterpret_cast<Acc*>(a.xp->base[r] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + l] = static_cast<Acc>(t);
-    } else {
-      stage[q] = valid ? static_cast<Acc>(t) : static_cast<Acc>(0);
-    }
+    stage[q] = valid ? static_cast<Acc>(t) : static_cast<Acc>(0);
   }
-  if (a.transport == 2) XArriveAndExchange(a, kXKindHist, XTag(a, cp->epoch));
-}
-
-// Root sums across ranks on the xGMI transport (one block): push (sum g, sum h) into
-// every rank's root rows, exchange, then every rank folds the rows in rank order (the
-// same fp64 result everywhere).
-__global__ __launch_bounds__(64) void k_x_root(Args a) {
-  const Ctl* cp = a.ctl;
-  if (threadIdx.x == 0) {
-    const double2 mine = a.lsum[0];
-    for (int q = 0; q < a.P; ++q) reinterpret_cast<double2*>(a.xp->base[q] + a.x_off_root)[a.rank] = mine;
-  }
-  XArriveAndExchange(a, kXKindRoot, XTag(a, cp->epoch));
-  if (threadIdx.x == 0) {
-    const double2* rows = reinterpret_cast<const double2*>(a.xp->base[a.rank] + a.x_off_root);
-    double g = 0.0, h = 0.0;
-    for (int q = 0; q < a.P; ++q) {
-      const double2 x = rows[q];
-      g += x.x;
-      h += x.y;
-    }
-    a.lsum[0] = make_double2(g, h);
-  }
-}
-
-// Transport self-test (run once when the exchange is set up): `rounds` exchanges of a
-// known pattern through the histogram rows; counts mismatching values into err[0].
-// Rounds alternate between the two halves of the rows (nvals <= bbin): a rank that has
-// finished round r may already push round r + 1 while a peer still checks round r.
-__global__ __launch_bounds__(256) void k_x_selftest(Args a, int round, int nvals, unsigned* err) {
-  const int V2 = 2 * a.bbin;
-  const int half = (round & 1) * nvals;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
-    for (int q = 0; q < a.P; ++q) {
-      reinterpret_cast<float*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * V2 + half + i] =
-          static_cast<float>(a.rank * 131 + round * 7 + (i & 1023));
-    }
-  }
-  XArriveAndExchange(a, kXKindHist, XTag(a, static_cast<unsigned>(round + 1)));
-}
-
-__global__ __launch_bounds__(256) void k_x_selfcheck(Args a, int round, int nvals, unsigned* err) {
-  const int V2 = 2 * a.bbin;
-  const int half = (round & 1) * nvals;
-  const float* rows = reinterpret_cast<const float*>(a.xp->base[a.rank] + a.x_off_hist);
-  unsigned bad = 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += gridDim.x * blockDim.x) {
-    for (int q = 0; q < a.P; ++q) {
-      bad += rows[static_cast<size_t>(q) * V2 + half + i] != static_cast<float>(q * 131 + round * 7 + (i & 1023)) ? 1u : 0u;
-    }
-  }
-  if (bad) atomicAdd(err, bad);
 }
 
 // One workgroup (16 waves) per feature this rank owns (every feature on one GPU):
@@ -634,7 +555,6 @@ __global__ __launch_bounds__(256) void k_x_selfcheck(Args a, int round, int nval
 //  3. reconstruct the most-frequent bin of each child, then wave 0 scans the
 //     smaller child and wave 1 the larger one concurrently, from LDS
 //  4. the block writes both candidates into this rank's block of the candidate table
-//     (on the xGMI transport: into every rank's table, then the in-kernel exchange)
 // kGlobal: the block's scratch (histograms, partials, categorical sort) lives in its slice of
 // global memory instead of LDS — features wider than the LDS budget (max_bin in the thousands;
 // reference cuda_best_split_finder.cu:1561 global-memory variant).

@@ -134,18 +134,10 @@ struct Args {
   int fold_chunks, fold_feats;
   double* fold_part;   // [fold_chunks][2 * TB]
   unsigned* fold_cnt;  // [F]: a multiple of fold_chunks between launches
-  int nparts;
-  const void* rx;       // owner rows: nparts x (2 * bbin) values of the bins this rank owns
+  const void* rx;       // owner row: the 2 * bbin reduce-scattered values of the bins this rank owns
   int own_bin0;         // first histogram bin this rank owns
   int bbin;             // owner block width (bins, padded to the largest block)
   const int* bin_lo;    // [P + 1] owner bin bounds (k_hist_owner permutation)
-  int transport;        // 0: collectives between kernels (RCCL / host-staged), 2: xGMI in-kernel exchange
-  const XPeers* xp;     // xGMI: every rank's exchange buffer
-  int x_off_hist, x_off_cand, x_off_flag, x_off_root;  // offsets inside an exchange buffer
-  unsigned* xcnt;       // local arrival counters of the exchanges [4]
-  unsigned xsession;    // high word of the exchange tags (new per learner state)
-  unsigned long long xtimeout;  // bound of an exchange wait (wall_clock64 ticks, 100 MHz)
-  int xfault;           // LGAP_FAULT_INJECT=xgmi: never signal (failure-detection tests)
   // ---- voting parallel (tree_learner=voting): local scan, top-k vote, elected histograms
   int vote;             // 1: k_reduce_scan is the LOCAL pass (local sums / counts, no masks or penalties)
   double2* hsum_part;   // [hist blocks] local (sum g, sum h) of the smaller child's rows per k_hist block
@@ -153,8 +145,8 @@ struct Args {
   int topk;             // elected features per child (min(top_k, F))
   const char* lcand;    // local candidate table (keys [2][F], infos [2][F] at lcand_key_bytes)
   int lcand_key_bytes;
-  VoteRec* vrec;        // collective transport: gathered local top-k records [P][2 * topk]
-  void* vhist;          // collective transport: packed elected histograms (all-reduced in place)
+  VoteRec* vrec;        // gathered local top-k records [P][2 * topk]
+  void* vhist;          // packed elected histograms (all-reduced in place)
   int vcap;             // values of one packed row (2 * topk * 2 * (max_bin - 1))
   int* elect;           // [2][topk + 2]: count, first-value offset, then the elected features (ascending)
   SplitParams sp;
@@ -204,7 +196,6 @@ __device__ __forceinline__ void StampAt(const Args& a, int kernel, int split, in
 
 
 constexpr int kRootThreads = 256;
-constexpr int kXKindHist = 0, kXKindCand = 1, kXKindRoot = 2;
 constexpr int kVoteThreads = 256;
 constexpr int kTraverseThreads = 256;
 constexpr int kTraverseMaxDw = 16;
@@ -212,48 +203,6 @@ constexpr int kTraverseMaxDw = 16;
 __device__ __forceinline__ int HistActiveBlocks(int n, int grid, int min_rows) {
   int nb = (n + min_rows - 1) / min_rows;
   return nb > grid ? grid : nb;
-}
-
-__device__ __forceinline__ unsigned long long XTag(const Args& a, unsigned epoch) {
-  return (static_cast<unsigned long long>(a.xsession) << 32) | epoch;
-}
-
-__device__ __forceinline__ unsigned long long* XFlag(const Args& a, int owner, int kind, int src) {
-  return reinterpret_cast<unsigned long long*>(a.xp->base[owner] + a.x_off_flag) + kind * kMaxXRanks + src;
-}
-
-__device__ inline bool XWaitAll(const Args& a, int kind, unsigned long long tag) {
-  const unsigned long long t0 = wall_clock64();
-  for (int q = 0; q < a.P; ++q) {
-    unsigned long long* f = XFlag(a, a.rank, kind, q);
-    unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < tag) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((++spins & 255u) == 0u &&
-          (wall_clock64() - t0 > a.xtimeout || __hip_atomic_load(&a.bar[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        __hip_atomic_store(&a.bar[3], 1u + kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  return true;
-}
-
-__device__ inline void XArriveAndExchange(const Args& a, int kind, unsigned long long tag) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();  // this block's peer stores are complete before it arrives
-    const unsigned nb = gridDim.x * gridDim.y;
-    if (atomicAdd(&a.xcnt[kind], 1u) == nb - 1u) {
-      atomicExch(&a.xcnt[kind], 0u);  // every block of this launch has arrived
-      __threadfence_system();
-      for (int q = 0; q < a.P && !(a.xfault && a.xsession > 0); ++q) {
-        __hip_atomic_store(XFlag(a, q, kind, a.rank), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      XWaitAll(a, kind, tag);
-    }
-  }
 }
 
 // seq_hist_kernels.hip
@@ -269,9 +218,6 @@ template <typename Acc, typename Out>
 __global__ void k_hist_reduce(Args a, int hist_grid, Out* __restrict__ out);
 template <typename Acc>
 __global__ void k_hist_owner(Args a, int hist_grid, Acc* __restrict__ stage);
-__global__ void k_x_root(Args a);
-__global__ void k_x_selftest(Args a, int round, int nvals, unsigned* err);
-__global__ void k_x_selfcheck(Args a, int round, int nvals, unsigned* err);
 
 // seq_scan_kernels.hip
 template <typename Acc, bool kGlobal>

@@ -100,12 +100,10 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     const int n_small = a.range[c.smaller].count;
     // 1. smaller child's histogram into hs_full at stored positions (mfb filled in step 3)
     if (a.scan_src == 1) {
-      // owner rows of the data-parallel exchange: nparts rows of 2 * bbin values
+      // the owner row the data-parallel reduce-scatter delivered (2 * bbin values)
       const Acc* rows = reinterpret_cast<const Acc*>(a.rx) + 2 * static_cast<size_t>(fi.hist_offset - a.own_bin0);
-      const size_t stride = 2 * static_cast<size_t>(a.bbin);
       for (int v = t; v < nv; v += blockDim.x) {
-        double acc = 0.0;
-        for (int p = 0; p < a.nparts; ++p) acc += static_cast<double>(rows[static_cast<size_t>(p) * stride + v]);
+        const double acc = static_cast<double>(rows[v]);
         const int k = v >> 1;
         const int b = k < fi.mfb ? k : k + 1;
         hs_full[2 * b + (v & 1)] = acc;
@@ -365,10 +363,8 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     constexpr int kKeyWords = static_cast<int>(sizeof(SplitKey) / 4);
     constexpr int kInfoWords = static_cast<int>(sizeof(SplitInfo) / 4);
     constexpr int kWords = 2 * (kKeyWords + kInfoWords);
-    const int q0 = a.transport == 2 ? 0 : a.rank;
-    const int q1 = a.transport == 2 ? a.P : a.rank + 1;
-    for (int q = q0; q < q1; ++q) {
-      char* tbl = a.transport == 2 ? a.xp->base[q] + a.x_off_cand : a.cand;
+    {
+      char* tbl = a.cand;
       for (int i = t; i < kWords; i += blockDim.x) {
         const int sel = i / (kKeyWords + kInfoWords);
         const int o = i - sel * (kKeyWords + kInfoWords);
@@ -384,7 +380,6 @@ __global__ __launch_bounds__(kScanThreads) void k_reduce_scan(Args a, int hist_g
     }
   }
   Stamp(a, 3, 4);
-  if (a.transport == 2) XArriveAndExchange(a, kXKindCand, XTag(a, c.epoch));
   if (t == 0 && a.stamps) {
     atomicMax(&a.stamps[((static_cast<size_t>(3) * 256 + (a.ctl->num_splits & 255)) * 2) * 8 + 7], wall_clock64());
   }

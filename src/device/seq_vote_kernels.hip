@@ -43,12 +43,7 @@ __global__ __launch_bounds__(kVoteThreads) void k_vote_local(Args a) {
         r.gain = g;
         r.feature = f;
         r.count = s_cnt[f];
-        const size_t o = static_cast<size_t>(a.rank) * 2 * K + sel * K + rank;
-        if (a.transport == 2) {
-          for (int q = 0; q < a.P; ++q) reinterpret_cast<VoteRec*>(a.xp->base[q] + a.x_off_cand)[o] = r;
-        } else {
-          a.vrec[o] = r;
-        }
+        a.vrec[static_cast<size_t>(a.rank) * 2 * K + sel * K + rank] = r;
       }
     }
     for (int i = nvalid + t; i < K; i += blockDim.x) {
@@ -56,16 +51,10 @@ __global__ __launch_bounds__(kVoteThreads) void k_vote_local(Args a) {
       r.gain = kMinScore;
       r.feature = -1;
       r.count = 0;
-      const size_t o = static_cast<size_t>(a.rank) * 2 * K + sel * K + i;
-      if (a.transport == 2) {
-        for (int q = 0; q < a.P; ++q) reinterpret_cast<VoteRec*>(a.xp->base[q] + a.x_off_cand)[o] = r;
-      } else {
-        a.vrec[o] = r;
-      }
+      a.vrec[static_cast<size_t>(a.rank) * 2 * K + sel * K + i] = r;
     }
     __syncthreads();
   }
-  if (a.transport == 2) XArriveAndExchange(a, kXKindCand, XTag(a, c.epoch));
 }
 
 // GlobalVoting of child `sel` over the gathered rows (same result in every block and on
@@ -135,7 +124,7 @@ __global__ __launch_bounds__(kVoteThreads) void k_vote_pack(Args a) {
   int* s_tmp = s_flag + R;                     // R + kVoteThreads / 64
   int* s_list = s_tmp + R + kVoteThreads / 64;  // [2][K]
   __shared__ int s_n[2];
-  const VoteRec* recs = a.transport == 2 ? reinterpret_cast<const VoteRec*>(a.xp->base[a.rank] + a.x_off_cand) : a.vrec;
+  const VoteRec* recs = a.vrec;
   for (int sel = 0; sel < 2; ++sel) {
     const int n = ElectChild(a, c, sel, recs, s_w, s_f, s_flag, s_list + sel * K, s_tmp);
     if (t == 0) s_n[sel] = n;
@@ -163,17 +152,9 @@ __global__ __launch_bounds__(kVoteThreads) void k_vote_pack(Args a) {
     const int nv = VoteValues(a, f);
     const double* src = a.slots + static_cast<size_t>(a.slot[leaf]) * 2 * a.TB + 2 * static_cast<size_t>(a.feat[f].hist_offset);
     for (int v = t; v < nv; v += blockDim.x) {
-      const Acc x = static_cast<Acc>(src[v]);
-      if (a.transport == 2) {
-        for (int q = 0; q < a.P; ++q) {
-          reinterpret_cast<Acc*>(a.xp->base[q] + a.x_off_hist)[static_cast<size_t>(a.rank) * a.vcap + off + v] = x;
-        }
-      } else {
-        reinterpret_cast<Acc*>(a.vhist)[off + v] = x;
-      }
+      reinterpret_cast<Acc*>(a.vhist)[off + v] = static_cast<Acc>(src[v]);
     }
   }
-  if (a.transport == 2) XArriveAndExchange(a, kXKindHist, XTag(a, c.epoch));
 }
 
 // Global pass: block k, wave `sel` scans elected feature k of child sel from the summed
@@ -211,13 +192,10 @@ __global__ __launch_bounds__(128) void k_vote_scan(Args a) {
     int off = e[1];
     for (int i = 0; i < k; ++i) off += VoteValues(a, e[2 + i]);
     const int nv = 2 * (fi.num_bin - 1);
-    const Acc* rows = a.transport == 2 ? reinterpret_cast<const Acc*>(a.xp->base[a.rank] + a.x_off_hist)
-                                       : reinterpret_cast<const Acc*>(a.vhist);
-    const int nparts = a.transport == 2 ? a.P : 1;
+    const Acc* rows = reinterpret_cast<const Acc*>(a.vhist);
     double sgs = 0.0, shs = 0.0;
     for (int v = lane; v < nv; v += 64) {
-      double acc = 0.0;
-      for (int p = 0; p < nparts; ++p) acc += static_cast<double>(rows[static_cast<size_t>(p) * a.vcap + off + v]);
+      const double acc = static_cast<double>(rows[off + v]);
       const int kb = v >> 1;
       const int b = kb < fi.mfb ? kb : kb + 1;
       H[2 * b + (v & 1)] = acc;
