@@ -41,8 +41,9 @@ def main() -> int:
         uid = dd.get_unique_id()
         dd._check(dd._LIB.LGBM_DeviceCommInit(dd._c_str(uid), ctypes.c_int64(len(uid)), ctypes.c_int(1),
                                               ctypes.c_int(0), ctypes.c_int(0)))
-        if args.learner == "data":
-            os.environ["LGAP_FORCE_DEVICE_DP"] = "1"
+        # (one machine: the configuration trains serial, as the reference; the knob keeps the
+        # parallel learner's path on the one-rank communicator)
+        os.environ["LGAP_FORCE_DEVICE_DP"] = "1" if args.learner == "data" else "voting"
 
     import numpy as np
 

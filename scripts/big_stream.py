@@ -69,6 +69,8 @@ def main() -> int:
         uid = dd.get_unique_id()
         _check(_LIB.LGBM_DeviceCommInit(_c_str(uid), ctypes.c_int64(len(uid)), ctypes.c_int(1), ctypes.c_int(0),
                                         ctypes.c_int(0)))
+        # (one machine trains serial, as in the reference: keep the voting learner's path)
+        os.environ["LGAP_FORCE_DEVICE_DP"] = "voting"
     params = preset("regression_goss", verbosity=-1, metric="l2", device_type=args.device)
     if args.learner == "voting":
         params["tree_learner"] = "voting"

@@ -27,6 +27,13 @@ for s in "$@"; do
     xgprof) LGAP_DP_TRANSPORT=xgmi step xgprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/xgprof -o run -- python3 bench.py --rows 1250000 --steps 20 --warmup 2 --rehearse-dp && python scripts/prof_summary.py $OUT/xgprof "1.25M rows, DP frontier xGMI (1 rank)" 22 > $OUT/xgprof_summary.md;;
     learnerv) step learnerv 900 python -u -m pytest tests/test_gpu_learner.py tests/test_frontier_kernels.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider;;
     shapes) step goss3m 600 python scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --steps 10 --warmup 2 && step ltr2m 600 python scripts/bench_suite.py --config ltr --rows 2000000 --features 300 --steps 10 --warmup 2;;
+    xgstamps) LGAP_FSTAMPS=1 LGAP_DP_TRANSPORT=xgmi step xgstamps 300 python bench.py --rows 1250000 --steps 12 --warmup 2 --rehearse-dp && LGAP_FSTAMPS=1 step serstamps 300 python bench.py --rows 1250000 --steps 12 --warmup 2 && LGAP_FSTAMPS=1 LGAP_DP_TRANSPORT=xgmi step xgstamps10 300 python bench.py --steps 12 --warmup 2 --rehearse-dp;;
+    mono) step mono 900 python scripts/bench_monotone.py --rows 1000000 --steps 20 --warmup 3;;
+    rehearse2x) step rehearse2x 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dp-host-transport --rows 1250000 --steps 20 --warmup 3;;
+    monotag) LGAP_TIMETAG=1 step monotag 300 python scripts/bench_monotone.py --rows 1000000 --steps 10 --warmup 2 --methods intermediate;;
+    big100) step big100 1150 python -u scripts/big_stream.py --rows 100000000 --features 500 --chunk 2000000 --steps 5 --warmup 1;;
+    big25) step big25 900 python -u scripts/big_stream.py --rows 25000000 --features 500 --chunk 2000000 --steps 5 --warmup 1;;
+    vote12) step vote12 900 python scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --learner voting --steps 10 --warmup 3;;
     dpmulti) step dpmulti 1100 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank";;
     fp) step fp 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "feature_parallel";;
     dpbench) step b1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_DP_TRANSPORT=xgmi step b1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=collective step b1coll 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && step b10single 300 python bench.py --steps 30 --warmup 3 && LGAP_DP_TRANSPORT=xgmi step b10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp;;

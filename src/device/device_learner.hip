@@ -245,13 +245,15 @@ class DeviceTreeLearner : public TreeLearner {
     if (parallel && !CommActive() && !HostStagedDP() && Network::num_machines() > 1) {
       Log::Fatal("Parallel HIP training needs an RCCL communicator (LGBM_DeviceCommInit)");
     }
-    // LGAP_FORCE_DEVICE_DP=1 routes a single-rank run through the data-parallel path
-    // (owner histogram exchange, candidate table, global counts): lets a 1-GPU box test it.
+    // LGAP_FORCE_DEVICE_DP=1 (or =voting) routes a single-rank run through the data-parallel (or
+    // voting-parallel) path on a one-rank communicator: the configuration sets tree_learner to
+    // serial for one machine, as the reference does, so a 1-GPU box needs this to run either path.
     const char* force_dp = std::getenv("LGAP_FORCE_DEVICE_DP");
-    const bool forced = CommExists() && force_dp && force_dp[0] == '1';
+    const bool force_vote = force_dp != nullptr && std::strcmp(force_dp, "voting") == 0;
+    const bool forced = CommExists() && force_dp != nullptr && (force_dp[0] == '1' || force_vote);
     if (forced && mode_ == DevParallel::kSerial) {
-      mode_ = DevParallel::kData;
-      data_parallel_ = true;
+      mode_ = force_vote ? DevParallel::kVoting : DevParallel::kData;
+      data_parallel_ = !force_vote;
     }
     const bool multi = CommActive() || HostStagedDP() || forced;
     // voting: a one-rank communicator also runs the voting path (single-GPU rehearsal)
