@@ -119,13 +119,15 @@ namespace {
 // Kernel-variant overrides for the coverage tests and A/B runs, all in one knob:
 // LGAP_KERNEL="key=value,key=value" with the keys fhist_threads (512 | 1024), hist_lds_kb (LDS
 // tile budget), quant_lds32 (0 | 1), part_iters (4 | 8 | 16), hist_il (0 | 1), nibble (0: 8-bit
-// rows), quant_hist (off: float histograms under quantized training), scan_global (1). Returns
+// rows), quant_hist (off: float histograms under quantized training), scan_global (1), scan_wave
+// (1: the wave-per-item scan below its 64-feature threshold). Returns
 // the key's value, nullptr when it is not set. Read at each use: tests change the environment
 // between trainings in one process. Each key's value has its own storage (a caller may hold the
 // values of several keys at once); empty items (a trailing comma) are skipped.
 const char* KernelOverride(const char* key) {
   static const char* const kKeys[] = {"fhist_threads", "hist_lds_kb", "quant_lds32", "part_iters",
-                                      "hist_il",       "nibble",      "quant_hist",  "scan_global"};
+                                      "hist_il",       "nibble",      "quant_hist",  "scan_global",
+                                      "scan_wave"};
   constexpr int kNumKeys = static_cast<int>(sizeof(kKeys) / sizeof(kKeys[0]));
   thread_local std::string vals[kNumKeys];
   const char* e = std::getenv("LGAP_KERNEL");
@@ -2049,7 +2051,8 @@ class DeviceTreeLearner : public TreeLearner {
     {
       // one wave per scan item on wide data (F >= 64, numerical features only)
       const bool fits = kFScanWaves * FrontierScanWaveBytes(max_bin_, cat_p2_) <= 150 * 1024;
-      a.scan_wave = fits && !has_cat_ && F_ >= 64 ? 1 : 0;
+      const char* sw = KernelOverride("scan_wave");  // coverage knob: the wave scan on narrow data
+      a.scan_wave = fits && !has_cat_ && (F_ >= 64 || (sw != nullptr && sw[0] == '1')) ? 1 : 0;
       // (block scan grid cap: 512 blocks loop over a large round's items instead of 4096
       // mostly-idle blocks being dispatched every round; A/B 10M 2.850 vs 2.875, 1.25M 1.331 vs 1.341)
       a.scan_grid = 512;

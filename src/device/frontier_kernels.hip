@@ -1284,10 +1284,26 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
     // the same iteration as the stores serialised one round trip per 64 bins, twice)
     const bool skip_both = !a.used_bytree[f] || !(p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1);
     const int splp = p >= 0 ? a.spl[static_cast<size_t>(p) * F + f] : 1;
-    const double2 cls0 = a.lsum[cs];
-    const double2 cls1 = cl >= 0 ? a.lsum[cl] : cls0;
-    const FNode cnd0 = a.nodes[cs];
-    const FNode cnd1 = cl >= 0 ? a.nodes[cl] : cnd0;
+    double2 cls0 = a.lsum[cs];
+    double2 cls1 = cl >= 0 ? a.lsum[cl] : cls0;
+    FNode cnd0 = a.nodes[cs];
+    FNode cnd1 = cl >= 0 ? a.nodes[cl] : cnd0;
+    if (a.voting) {
+      // voting's LOCAL pass (as k_f_scan): this rank's rows and sums -- the smaller child's from the
+      // round's exact local totals, the larger's as the parent's local sums minus them
+      cls0 = make_double2(static_cast<double>(static_cast<long long>(a.ltot[2 * e])) * inv_g,
+                          static_cast<double>(static_cast<long long>(a.ltot[2 * e + 1])) * inv_h);
+      if (cl >= 0) {
+        const double2 ps = a.lsum_loc[p];
+        cls1 = make_double2(ps.x - cls0.x, ps.y - cls0.y);
+      }
+      cnd0.gcount = cnd0.count;
+      cnd1.gcount = cnd1.count;
+      if (f == 0 && lane == 0) {
+        a.lsum_loc[cs] = cls0;
+        if (cl >= 0) a.lsum_loc[cl] = cls1;
+      }
+    }
     const double cpo0 = a.lout[cs], cpo1 = cl >= 0 ? a.lout[cl] : cpo0;
     const LeafBounds cbd0 = a.bounds[cs], cbd1 = cl >= 0 ? a.bounds[cl] : cbd0;
     constexpr int kScanWU = 4;
@@ -1378,35 +1394,37 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
       const double sg = lsum.x, sh = lsum.y;
       const int n = nd.gcount;
       const int depth = nd.depth;
+      const SplitParams& spp = a.voting ? a.sp_local : a.sp;
       if (!skip_both) {
         double po;
         if (p < 0) {
-          SplitParams p0 = a.sp;
+          SplitParams p0 = spp;
           p0.path_smooth = 0.0;
           po = LeafOutputRaw(sg, sh, p0, n, 0.0);
-          if (f == 0 && lane == 0) a.lout[0] = po;
+          if (f == 0 && lane == 0 && !a.voting) a.lout[0] = po;  // (voting: k_f_elect writes the global one)
         } else {
           po = pre_out;
         }
         const LeafBounds bounds = bnd;
         // (numerical features only: LaunchFrontierScan routes categorical data to k_f_scan)
-        const bool spl = ScanNumericalWave(a.sp, fi, H, sg, sh, n, po, bounds, 0, out);
+        const bool spl = ScanNumericalWave(spp, fi, H, sg, sh, n, po, bounds, 0, out);
         if (lane == 0) {
           a.spl[static_cast<size_t>(my) * F + f] = spl ? 1 : 0;
           if (!spl || (a.max_depth > 0 && depth >= a.max_depth)) {
             out->Reset();
           } else {
             out->feature = f;
-            if (!a.cegb_raw) {
+            // (voting's local pass ranks raw gains: penalties and masks belong to the global pass)
+            if (!a.cegb_raw && !a.voting) {
               if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
             }
-            if (a.ic && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
+            if (a.ic && !a.voting && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
           }
         }
       } else if (lane == 0) {
         a.spl[static_cast<size_t>(my) * F + f] = static_cast<uint8_t>(splp);
-        if (p < 0 && f == 0) {
+        if (p < 0 && f == 0 && !a.voting) {
           SplitParams p0 = a.sp;
           p0.path_smooth = 0.0;
           a.lout[0] = LeafOutputRaw(sg, sh, p0, n, 0.0);
@@ -2940,18 +2958,27 @@ __device__ void FVoteBody(const FArgs& a, int k, int q) {
   // (xGMI: the records go to row `rank` of every rank's table)
   const int npeer = a.xg ? a.xP : 1;
   const size_t roff = (static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q) * K;
-  for (int f = t; f < F; f += blockDim.x) {
-    if (s_cnt[f] < 0) continue;
+  // rank of feature f = the valid features ordered before it; one wave per feature, its lanes
+  // comparing 64 features at a time (ballot + popcount), stopping once the rank reaches K. (A lane
+  // per feature scanning all F serially kept every wave holding a top-K feature in a full F-long
+  // loop: 132 us per round at F = 500, GOSS 3M x 500.)
+  const int lane = t & 63, wv = t >> 6, nw = static_cast<int>(blockDim.x) >> 6;
+  for (int f = wv; f < F; f += nw) {
+    if (s_cnt[f] < 0) continue;  // (wave-uniform)
     const double g = s_gain[f];
     int rank = 0;
-    for (int j = 0; j < F && rank < K; ++j) rank += (s_cnt[j] >= 0 && FVoteBetter(s_gain[j], j, g, f)) ? 1 : 0;
-    if (rank < K) {
+    for (int j0 = 0; j0 < F && rank < K; j0 += 64) {
+      const int j = j0 + lane;
+      const bool better = j < F && s_cnt[j] >= 0 && FVoteBetter(s_gain[j], j, g, f);
+      rank += __popcll(__ballot(better));
+    }
+    if (rank < K && lane < npeer) {
       VoteRec r;
       r.gain = g;
       r.feature = f;
       r.count = s_cnt[f];
       if (!a.xg) a.vrec[roff + rank] = r;
-      for (int p = 0; a.xg && p < npeer; ++p) FXStoreRec(reinterpret_cast<VoteRec*>(a.xpeer[p] + a.xo_vrec) + roff + rank, r);
+      else FXStoreRec(reinterpret_cast<VoteRec*>(a.xpeer[lane] + a.xo_vrec) + roff + rank, r);
     }
   }
   for (int i = nvalid + t; i < K; i += blockDim.x) {
@@ -3489,7 +3516,8 @@ void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
 
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
   const bool ext = a.voting || a.xrng != nullptr || a.fowned != nullptr;
-  if (a.scan_wave && !ext && a.num_forced == 0) {
+  // (the wave kernel also runs voting's local pass: numerical features, no forced splits)
+  if (a.scan_wave && (!ext || (a.voting && a.xrng == nullptr && a.fowned == nullptr)) && a.num_forced == 0) {
     // one wave per item, items grid-strided over the RESIDENT blocks: a grid sized for the widest
     // round (up to 2048 blocks) left most blocks without an item in a typical round, dispatched
     // after the resident ones finished (the partition's tail, profiles/r05/ab_notes.md)

@@ -388,7 +388,8 @@ def test_feature_parallel_multirank_rehearsal(lgb, gpu_required, transport):
 
 
 @pytest.mark.parametrize("world,transport,topk", [(2, "collective", 3), (3, "collective", 20), (4, "collective", 2),
-                                                  (3, "xgmi", 3), (2, "xgmi", 20), (4, "xgmi", 2)])
+                                                  (3, "xgmi", 3), (2, "xgmi", 20), (4, "xgmi", 2),
+                                                  (3, "xgmi-wavescan", 3)])
 def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport, topk):
     """Device voting-parallel (PV-Tree: local scan, top-k vote all-gathered, elected features'
     histograms summed, global scan of the elected features only), P ranks sharing the GPU: every
@@ -400,8 +401,12 @@ def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20",
-               DP_LEARNER="voting", DP_TOPK=str(topk))
+    # "-wavescan": the local pass on the wave-per-item scan (the wide-data kernel; forced here)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport.replace("-wavescan", ""),
+               LGAP_XGMI_TIMEOUT_S="20", DP_LEARNER="voting", DP_TOPK=str(topk))
+    if transport.endswith("-wavescan"):
+        env["LGAP_KERNEL"] = "scan_wave=1"
+    transport = transport.replace("-wavescan", "")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
                         "--nproc-per-node", str(world), os.path.join(root, "scripts", "dp_multirank.py")],
                        capture_output=True, text=True, timeout=600, env=env, cwd=root)
