@@ -37,6 +37,7 @@ for s in "$@"; do
     voteprof) step voteprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/voteprof -o run -- python3 scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --learner voting --steps 10 --warmup 2 && python scripts/prof_summary.py $OUT/voteprof "GOSS 3M x 500 voting, one rank" 12 > $OUT/voteprof_summary.md && step serprof3 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/serprof3 -o run -- python3 scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --steps 10 --warmup 2 && python scripts/prof_summary.py $OUT/serprof3 "GOSS 3M x 500 serial" 12 > $OUT/serprof3_summary.md;;
     votet) step votet 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "voting";;
     vote3) step vote3 600 python scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --learner voting --steps 10 --warmup 2 && step ser3 600 python scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --steps 10 --warmup 2;;
+    ict) step ict 600 python -u -m pytest tests/test_gpu_learner.py tests/test_frontier_kernels.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "interaction or frontier or bynode";;
     dpmulti) step dpmulti 1100 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank";;
     fp) step fp 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "feature_parallel";;
     dpbench) step b1single 300 python bench.py --rows 1250000 --steps 50 --warmup 5 && LGAP_DP_TRANSPORT=xgmi step b1xgmi 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && LGAP_DP_TRANSPORT=collective step b1coll 300 python bench.py --rows 1250000 --steps 50 --warmup 5 --rehearse-dp && step b10single 300 python bench.py --steps 30 --warmup 3 && LGAP_DP_TRANSPORT=xgmi step b10xgmi 300 python bench.py --steps 30 --warmup 3 --rehearse-dp;;

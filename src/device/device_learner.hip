@@ -1743,6 +1743,10 @@ class DeviceTreeLearner : public TreeLearner {
       Log::Fatal("forced splits on the device need the frontier engine (serial learner, no "
                  "feature_fraction_bynode / extra_trees, frontier LDS shape)");
     }
+    if (!frontier_ && config_->interaction_constraints_vector.size() > 64) {
+      // (TreeLearner::Create routes these by FrontierServes: reaching here is a routing bug)
+      Log::Fatal("more than 64 interaction constraint sets on the device need the frontier engine");
+    }
     if (!frontier_ && CegbRaw()) {
       Log::Fatal("cegb_penalty_feature_coupled / _lazy on the device need the frontier engine (serial learner, "
                  "no feature_fraction_bynode / extra_trees, frontier LDS shape)");
@@ -1755,7 +1759,7 @@ class DeviceTreeLearner : public TreeLearner {
     const size_t o_st = lay.Add<FState>(1), o_nodes = lay.Add<FNode>(C), o_exps = lay.Add<FExp>(K),
                  o_bits = lay.Add<uint32_t>(K * kMaxCatWords), o_lsum = lay.Add<double2>(C), o_lout = lay.Add<double>(C),
                  o_bounds = lay.Add<LeafBounds>(C), o_key = lay.Add<SplitKey>(C), o_best = lay.Add<SplitInfo>(C),
-                 o_spl = lay.Add<uint8_t>(C * F), o_ic = lay.Add<unsigned long long>(C), o_nst = lay.Add<uint8_t>(C),
+                 o_spl = lay.Add<uint8_t>(C * F), o_ic = lay.Add<unsigned long long>(C * kFrontierIcWords), o_nst = lay.Add<uint8_t>(C),
                  o_lcid = lay.Add<int>(L_), o_ckey = lay.Add<SplitKey>(K * 2 * F), o_cinfo = lay.Add<SplitInfo>(K * 2 * F),
                  o_fbest = lay.Add<SplitInfo>(C), o_fkey = lay.Add<SplitKey>(C);
     farena_.Resize(lay.bytes());
@@ -1987,7 +1991,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.best = fbest_;
     a.spl = fspl_;
     a.ic = use_ic_ ? fic_ : nullptr;
-    a.ic_feat = use_ic_ ? ic_feat_.get() : nullptr;
+    a.ic_feat = use_ic_ ? fic_feat_.get() : nullptr;
+    a.ic_words = ic_words_;
     a.nstate = fnst_;
     a.leaf_cid = flcid_;
     a.rec = rec_.get();
@@ -3609,15 +3614,24 @@ class DeviceTreeLearner : public TreeLearner {
     use_ic_ = !config_->interaction_constraints_vector.empty();
     if (use_ic_) {
       const auto& sets = config_->interaction_constraints_vector;
-      if (sets.size() > 64) Log::Fatal("The HIP learner holds at most 64 interaction constraint sets");
+      // the frontier holds up to 256 sets (words of 64); the sequential chain's one word, 64
+      // (TreeLearner::Create routes more than 64 sets to the frontier or the host policy)
+      if (sets.size() > 64 * static_cast<size_t>(kFrontierIcWords)) {
+        Log::Fatal("The HIP learner holds at most %d interaction constraint sets", 64 * kFrontierIcWords);
+      }
+      ic_words_ = static_cast<int>((sets.size() + 63) / 64);
       std::vector<unsigned long long> m(std::max(F_, 1), 0ull);
+      std::vector<unsigned long long> mw(static_cast<size_t>(std::max(F_, 1)) * ic_words_, 0ull);
       for (int f = 0; f < F_; ++f) {
         const int real = data_->feature(f).real_index;
         for (size_t k = 0; k < sets.size(); ++k) {
-          if (std::find(sets[k].begin(), sets[k].end(), real) != sets[k].end()) m[f] |= 1ull << k;
+          if (std::find(sets[k].begin(), sets[k].end(), real) == sets[k].end()) continue;
+          if (k < 64) m[f] |= 1ull << k;
+          mw[static_cast<size_t>(f) * ic_words_ + k / 64] |= 1ull << (k % 64);
         }
       }
       ic_feat_.Upload(m, stream_);
+      fic_feat_.Upload(mw, stream_);
     }
     feat_.Upload(h_feats_, stream_);
     gstart_.Upload(h_gstart_, stream_);
@@ -4139,6 +4153,8 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<int> tile_cnt_, tile_off_;
   DevBuf<uint8_t> used_bytree_, bynode_;
   DevBuf<unsigned long long> ic_feat_, ic_leaf_;
+  DevBuf<unsigned long long> fic_feat_;  // [F][ic_words_] (the frontier's interaction-constraint words)
+  int ic_words_ = 1;
   DevBuf<unsigned> qmax_;
   DevBuf<double2> true_sums_;
   DevBuf<double> root_part_;
@@ -4289,7 +4305,7 @@ bool LinearOnDevice(const Config* config, const Dataset* train, const std::strin
 
 bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type) {
   if (learner_type != "serial" || config->feature_fraction_bynode < 1.0 || config->extra_trees) return false;
-  if (config->interaction_constraints_vector.size() > 64) return false;
+  if (config->interaction_constraints_vector.size() > 64 * static_cast<size_t>(kFrontierIcWords)) return false;
   if (train == nullptr) return config->num_leaves <= 256;  // (no data yet: a conservative shape)
   int max_bin = 2, max_cat_bin = 1;
   for (int f = 0; f < train->num_features(); ++f) {

@@ -55,6 +55,7 @@ constexpr int kFrontierBufs = LGAP_FRONTIER_BUFS;  // depth-indexed row-index bu
 constexpr int kFrontierIdx = kFrontierBufs + 1;    // index buffers by id: depth buffers {0, 1, 3, ...}, bag 2
 constexpr int kFrontierRoundCap = 64;  // rounds with their own expansion cap (later rounds: kmax)
 constexpr int kFrontierMaxNodes = 4096;  // computed-node capacity of the select's LDS image
+constexpr int kFrontierIcWords = 4;      // interaction-constraint sets on the frontier: 4 x 64
 
 // Fixed-point exponent e of a sum over `rows` rows of values with max |v| = vmax and
 // sum |v| <= vsum over ALL rows: the largest e with 2^e * min(rows * vmax, vsum) <= limit,
@@ -165,8 +166,9 @@ struct FArgs {
   SplitKey* key;        // [C] best split (compact)
   SplitInfo* best;      // [C] best split (full)
   uint8_t* spl;         // [C][F] feature still splittable below this node
-  unsigned long long* ic;        // [C] interaction-constraint sets (null: none)
-  const unsigned long long* ic_feat;
+  unsigned long long* ic;        // [C][ic_words] interaction-constraint sets a node's path allows (null: none)
+  const unsigned long long* ic_feat;  // [F][ic_words] the sets holding each feature
+  int ic_words;                  // 64-set words (up to kFrontierIcWords: 256 sets)
   uint8_t* nstate;      // [C]
   int* leaf_cid;        // [L] committed leaf -> cid
   SplitRec* rec;        // [L - 1] committed splits in order

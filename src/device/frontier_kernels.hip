@@ -106,6 +106,16 @@ __device__ __forceinline__ unsigned long long* FAccPtr(const FArgs& a, int e, in
          (static_cast<size_t>(e) * a.own_w + (b - a.own_b0[r])) * pw;
 }
 
+// Interaction constraints: feature f may split node c when some set allowed on c's path holds f
+// (reference col_sampler.hpp GetByNode's allowed features), as 64-set words.
+__device__ __forceinline__ bool FIcAllows(const FArgs& a, int c, int f) {
+  unsigned long long any = 0ull;
+  for (int w = 0; w < a.ic_words; ++w) {
+    any |= a.ic[static_cast<size_t>(c) * a.ic_words + w] & a.ic_feat[static_cast<size_t>(f) * a.ic_words + w];
+  }
+  return any != 0ull;
+}
+
 // ---- xGMI transport handshake (FArgs::xg). Tags are (session << 32) | round: strictly
 // increasing for the life of the exchange buffer, so a flag is only compared for "reached".
 __device__ __forceinline__ unsigned long long FXTag(const FArgs& a, unsigned ep) {
@@ -262,7 +272,9 @@ __device__ __forceinline__ void FInitTree(const FArgs& a) {
     x.last = 0;
     a.exps[0] = x;
     a.bounds[0] = LeafBounds();
-    if (a.ic) a.ic[0] = ~0ull;
+    if (a.ic) {
+      for (int w = 0; w < a.ic_words; ++w) a.ic[w] = ~0ull;
+    }
     a.leaf_cid[0] = 0;
     a.lout[0] = 0.0;
   }
@@ -1129,7 +1141,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
               if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
             }
-            if (a.ic && !voting && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
+            if (a.ic && !voting && !FIcAllows(a, my, f)) out->Reset();
           }
         }
       } else if (lane == 0) {
@@ -1419,7 +1431,7 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
               if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
               if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, depth);
             }
-            if (a.ic && !a.voting && (a.ic[my] & a.ic_feat[f]) == 0ull) out->Reset();
+            if (a.ic && !a.voting && !FIcAllows(a, my, f)) out->Reset();
           }
         }
       } else if (lane == 0) {
@@ -1603,7 +1615,6 @@ __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
   const int16_t ncat = bi.num_cat_threshold;
   const int feature = bi.feature;
   LeafBounds bl = a.bounds[x.parent];
-  const unsigned long long icm = a.ic ? (a.ic[x.parent] & a.ic_feat[feature]) : 0ull;
   const int rc = x.count - lc;
   const int glc = a.distributed ? ilc : lc;
   const int grc = a.distributed ? irc : rc;
@@ -1642,8 +1653,13 @@ __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
   a.bounds[l] = bl;
   a.bounds[r] = br;
   if (a.ic) {
-    a.ic[l] = icm;
-    a.ic[r] = icm;
+    // the children's sets: the parent's that also hold the split feature
+    for (int w = 0; w < a.ic_words; ++w) {
+      const unsigned long long icm = a.ic[static_cast<size_t>(x.parent) * a.ic_words + w] &
+                                     a.ic_feat[static_cast<size_t>(feature) * a.ic_words + w];
+      a.ic[static_cast<size_t>(l) * a.ic_words + w] = icm;
+      a.ic[static_cast<size_t>(r) * a.ic_words + w] = icm;
+    }
   }
   const int md = a.sp.min_data_in_leaf;
   // children with forced splits of their own always get histograms (the forced split ignores
@@ -3192,7 +3208,7 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
     } else {
       out->feature = f;
       if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, nd.depth);
-      if (a.ic && (a.ic[c] & a.ic_feat[f]) == 0ull) out->Reset();
+      if (a.ic && !FIcAllows(a, c, f)) out->Reset();
     }
     SplitKey kk;
     kk.feature = out->feature;

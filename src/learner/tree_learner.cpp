@@ -71,9 +71,11 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {
     return "intermediate/advanced monotone constraints (device scans, host constraint walk)";
   }
+  // (more than 64 sets: the frontier's multi-word masks, up to 256; the sequential chain holds 64)
   if (!c->interaction_constraints_vector.empty() &&
-      (c->feature_fraction_bynode < 1.0 || c->interaction_constraints_vector.size() > 64)) {
-    return "interaction constraints with by-node sampling / more than 64 sets";
+      (c->feature_fraction_bynode < 1.0 ||
+       (c->interaction_constraints_vector.size() > 64 && !device::FrontierServes(c, train, learner_type)))) {
+    return "interaction constraints with by-node sampling / more than 64 sets off the frontier";
   }
   return nullptr;
 }

@@ -430,9 +430,13 @@ def _policy_data(rng, n=20000):
 
 
 @pytest.mark.parametrize("extra", [{"interaction_constraints": [[0, 1], [1, 2, 3]]},
-                                   {"interaction_constraints": [[0], [2, 3, 4], [1, 5]], "num_leaves": 15}])
+                                   {"interaction_constraints": [[0], [2, 3, 4], [1, 5]], "num_leaves": 15},
+                                   # 100 sets (two 64-set words), the binding ones at positions 70 and 90
+                                   {"interaction_constraints": [[5]] * 70 + [[0, 1]] + [[4]] * 19 + [[1, 2, 3]]
+                                    + [[5]] * 9}])
 def test_device_interaction_constraints(lgb, gpu_required, rng, extra):
-    """Device-resident interaction constraints (per-leaf set masks) against the CPU learner."""
+    """Device-resident interaction constraints (per-leaf set masks, 64 sets per word) against the
+    CPU learner."""
     X, z = _policy_data(rng)
     y = (z > 0).astype(float)
     bc = _train(lgb, X, y, "cpu", rounds=5, **extra)
