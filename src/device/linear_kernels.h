@@ -16,8 +16,8 @@
 namespace lgap {
 namespace device {
 
-constexpr int kLinMaxM = 31;  // unknowns per leaf: <= 30 branch features + the constant
-constexpr int kLinDim = 32;   // [A | c] in two 16-wide tiles per dimension (c = column m)
+constexpr int kLinMaxM = 63;  // unknowns per leaf: <= 62 branch features + the constant
+constexpr int kLinDim = 64;   // [A | c] in up to four 16-wide tiles per dimension (c = column m)
 
 struct LinearGramArgs {
   const float* raw;          // [N][F] raw values of the inner features

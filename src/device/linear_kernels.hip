@@ -21,7 +21,8 @@ constexpr int kLinSlot = kLinDim * kLinDim + 1;  // [A | c] and the usable count
 // (C/D on gfx950 f64: col = l & 15, row = (l >> 4) + 4 reg).
 template <int T>
 __global__ __launch_bounds__(kLinThreads) void k_linear_gram(LinearGramArgs a, double* __restrict__ partial) {
-  __shared__ double s_g[4][kLinDim * kLinDim];
+  constexpr int D = 16 * T;  // the tiles' dimension
+  __shared__ double s_g[D * D];
   __shared__ long long s_use[4];
   const int leaf = blockIdx.y, chunk = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, rr = lane >> 4, cc = lane & 15;
@@ -74,21 +75,31 @@ __global__ __launch_bounds__(kLinThreads) void k_linear_gram(LinearGramArgs a, d
       }
     }
   }
-  // the wave's tiles -> LDS; the block's four waves summed in a fixed order
-  for (int i = lane; i < kLinDim * kLinDim; i += 64) s_g[w][i] = 0.0;
-#pragma unroll
-  for (int ti = 0; ti < T; ++ti) {
-#pragma unroll
-    for (int tj = 0; tj < T; ++tj) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s_g[w][(16 * ti + rr + 4 * r) * kLinDim + 16 * tj + cc] = acc[ti][tj][r];
-    }
-  }
+  // the block's four waves summed into one LDS image in a fixed order (wave 0 stores, waves 1-3
+  // add in turn): ((w0 + w1) + w2) + w3 for every element, one wave's image of LDS (32 KB at T = 4)
   usable = static_cast<long long>(WaveSum(static_cast<double>(usable)));
   if (lane == 0) s_use[w] = usable;
-  __syncthreads();
+  for (int ws = 0; ws < 4; ++ws) {
+    if (w == ws) {
+#pragma unroll
+      for (int ti = 0; ti < T; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < T; ++tj) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double& g = s_g[(16 * ti + rr + 4 * r) * D + 16 * tj + cc];
+            g = ws == 0 ? acc[ti][tj][r] : g + acc[ti][tj][r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
   double* out = partial + (static_cast<size_t>(chunk) * a.num_leaves + leaf) * kLinSlot;
-  for (int i = t; i < kLinDim * kLinDim; i += kLinThreads) out[i] = ((s_g[0][i] + s_g[1][i]) + s_g[2][i]) + s_g[3][i];
+  for (int i = t; i < kLinDim * kLinDim; i += kLinThreads) {
+    const int row = i / kLinDim, col = i - row * kLinDim;
+    out[i] = row < D && col < D ? s_g[row * D + col] : 0.0;
+  }
   if (t == 0) out[kLinDim * kLinDim] = static_cast<double>(((s_use[0] + s_use[1]) + s_use[2]) + s_use[3]);
 }
 
@@ -115,9 +126,10 @@ void LaunchLinearGram(const LinearGramArgs& a, int max_m, double* partial, doubl
   if (a.num_leaves <= 0) return;
   if (max_m > kLinMaxM) Log::Fatal("LaunchLinearGram: %d unknowns per leaf (at most %d)", max_m, kLinMaxM);
   const dim3 grid(std::max(1, a.chunks), a.num_leaves);
-  // one 16x16 tile per dimension while [A | c] fits it (m + 1 <= 16), two beyond
+  // one 16x16 tile per dimension while [A | c] fits it (m + 1 <= 16), two up to 32, four beyond
   if (max_m + 1 <= 16) k_linear_gram<1><<<grid, kLinThreads, 0, s>>>(a, partial);
-  else k_linear_gram<2><<<grid, kLinThreads, 0, s>>>(a, partial);
+  else if (max_m + 1 <= 32) k_linear_gram<2><<<grid, kLinThreads, 0, s>>>(a, partial);
+  else k_linear_gram<4><<<grid, kLinThreads, 0, s>>>(a, partial);
   HIP_CHECK(hipGetLastError());
   k_linear_fold<<<a.num_leaves, kLinThreads, 0, s>>>(partial, std::max(1, a.chunks), a.num_leaves, out, usable);
   HIP_CHECK(hipGetLastError());

@@ -1203,15 +1203,25 @@ def test_linear_tree_on_device_matches_cpu(lgb, gpu_required, rng, extra):
     np.testing.assert_allclose(ev["train"]["l2"][-1], float(np.mean((bg2.predict(X) - z) ** 2)), rtol=1e-9)
 
 
-def test_linear_tree_wide_branches_take_the_host_policy(lgb, gpu_required, rng):
-    """Leaves that can carry more than 30 branch features (beyond the device Gram tile) train
-    under the host linear learner over HIP histograms."""
+def test_linear_tree_wide_branches_on_device_and_beyond(lgb, gpu_required, rng):
+    """Leaves that can carry 31-62 branch features use the Gram kernel's four-tile instantiation
+    (64 x 64 [A | c], 284 VGPRs) and match the host linear learner; more than 62 train under the
+    host linear learner over HIP histograms."""
     n = 6000
     X = rng.standard_normal((n, 40))
-    z = X[:, :5].sum(axis=1) + 0.1 * rng.standard_normal(n)
+    z = X[:, :5].sum(axis=1) + 0.3 * X[:, 7] * X[:, 11] + 0.1 * rng.standard_normal(n)
     kw = {"objective": "regression", "linear_tree": True, "num_leaves": 48, "min_data_in_leaf": 10}
-    bg = _train(lgb, X, z, "gpu", rounds=2, **kw)
-    assert "host split policy" in bg.device_name()
+    bc = _train(lgb, X, z, "cpu", rounds=3, **kw)
+    bg = _train(lgb, X, z, "gpu", rounds=3, gpu_use_dp=True, **kw)
+    assert "host split policy" not in bg.device_name() and "frontier engine" in bg.device_name(), bg.device_name()
+    tc, tg = _trees(bc), _trees(bg)
+    for t in range(3):
+        assert [s[:2] for s in _splits(tc[t]["tree_structure"], [])] == [s[:2] for s in _splits(tg[t]["tree_structure"], [])]
+    np.testing.assert_allclose(bg.predict(X), bc.predict(X), rtol=1e-4, atol=1e-4)
+    X2 = rng.standard_normal((n, 70))
+    z2 = X2[:, :5].sum(axis=1) + 0.1 * rng.standard_normal(n)
+    bg2 = _train(lgb, X2, z2, "gpu", rounds=2, **dict(kw, num_leaves=80))
+    assert "host split policy" in bg2.device_name()
 
 
 @pytest.mark.parametrize("extra", [{}, {"num_leaves": 63, "monotone_constraints": [1] + [0] * 79},
