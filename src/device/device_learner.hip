@@ -428,11 +428,29 @@ class DeviceTreeLearner : public TreeLearner {
     fxep_.Zero(stream_);
     fxcnt_.Resize(kFXKinds);
     fxcnt_.Zero(stream_);
+    {
+      FXConf c;
+      std::memset(&c, 0, sizeof(c));
+      for (int q = 0; q < P_; ++q) c.peer[q] = fx_peers_[q];
+      c.o_recv = fxo_recv_;
+      c.o_fpb = fxo_fpb_;
+      c.o_root = fxo_root_;
+      c.o_flag = fxo_flag_;
+      c.o_vrec = fxo_vrec_;
+      c.o_vrows = fxo_vrows_;
+      c.ep = fxep_.get();
+      c.cnt = fxcnt_.get();
+      c.timeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
+      c.P = P_;
+      c.rank = rank_;
+      c.fault = std::getenv("LGAP_FAULT_INJECT") != nullptr && std::strcmp(std::getenv("LGAP_FAULT_INJECT"), "xgmi") == 0;
+      fxconf_.Resize(1);
+      fxconf_.Upload(&c, 1, stream_);
+    }
     fxg_ = true;
     // self-test (session-0 tags, below every training tag)
     FArgs a = MakeFArgs();
     a.xsession = 0;
-    a.xtimeout = static_cast<unsigned long long>(100e6 * std::min(30.0, XTimeoutSeconds()));
     DevBuf<unsigned> err(1);
     err.Zero(stream_);
     const int nvals = static_cast<int>(std::min<size_t>(recv_words / 2, 4096));
@@ -1890,6 +1908,12 @@ class DeviceTreeLearner : public TreeLearner {
     }
     fvoting_ = FrontierVoting();
     if (fvoting_) {
+      // voting's local pass: min_data / min_hessian divided by the ranks (reference :61-63, integer division)
+      SplitParams sl = MakeArgs().sp;
+      sl.min_data_in_leaf = config_->min_data_in_leaf / P_;
+      sl.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf / P_;
+      fsp_local_.Resize(1);
+      fsp_local_.Upload(&sl, 1, stream_);
       flsum_loc_.Resize(C);
       fltot_.Resize(2 * K);
       fltot_.Zero(stream_);  // k_f_vote re-zeroes what the round consumed
@@ -2119,20 +2143,8 @@ class DeviceTreeLearner : public TreeLearner {
       // in-kernel exchange: the owner's receive chunk and the per-child best rows live in this
       // rank's exchange buffer; the chunk stride covers every expansion a round can hold
       a.xg = 1;
-      a.xP = P_;
-      a.xrank = rank_;
-      for (int q = 0; q < P_; ++q) a.xpeer[q] = fx_peers_[q];
-      a.xo_recv = fxo_recv_;
-      a.xo_fpb = fxo_fpb_;
-      a.xo_root = fxo_root_;
-      a.xo_flag = fxo_flag_;
-      a.xep = fxep_.get();
-      a.xcnt = fxcnt_.get();
-      a.xtimeout = static_cast<unsigned long long>(100e6 * XTimeoutSeconds());
       a.xsession = 1;
-      a.xfault = std::getenv("LGAP_FAULT_INJECT") != nullptr && std::strcmp(std::getenv("LGAP_FAULT_INJECT"), "xgmi") == 0;
-      a.xo_vrec = fxo_vrec_;
-      a.xo_vrows = fxo_vrows_;
+      a.xc = fxconf_.get();
       if (fowner_ || ffeature_) a.fpb = reinterpret_cast<FPairBest*>(fx_local_ + fxo_fpb_);
       if (fowner_) a.acc_recv = reinterpret_cast<unsigned long long*>(fx_local_ + fxo_recv_);
     }
@@ -2141,9 +2153,7 @@ class DeviceTreeLearner : public TreeLearner {
       a.vote_k = topk_;
       a.vote_P = P_;
       a.vote_rank = rank_;
-      a.sp_local = a.sp;
-      a.sp_local.min_data_in_leaf = config_->min_data_in_leaf / P_;  // integer division (reference :61-63)
-      a.sp_local.min_sum_hessian_in_leaf = config_->min_sum_hessian_in_leaf / P_;
+      a.sp_local = fsp_local_.get();
       a.lsum_loc = flsum_loc_.get();
       a.ltot = fltot_.get();
       a.vrec = fvrec_.get();
@@ -4183,6 +4193,8 @@ class DeviceTreeLearner : public TreeLearner {
   unsigned fxo_recv_ = 0, fxo_fpb_ = 0, fxo_root_ = 0, fxo_flag_ = 0;
   size_t fxo_vrec_ = 0, fxo_vrows_ = 0;
   DevBuf<unsigned> fxep_, fxcnt_;
+  DevBuf<FXConf> fxconf_;          // FArgs::xc
+  DevBuf<SplitParams> fsp_local_;  // FArgs::sp_local (voting's local pass)
   int cached_gcount_ = -1, cached_gcount_local_ = -1;
   DevBuf<unsigned long long> tile_pub_;
   PinnedBuf<unsigned> pin_bar_;

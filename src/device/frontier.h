@@ -263,7 +263,7 @@ struct FArgs {
   // Reference: voting_parallel_tree_learner.cpp:243-399.
   int voting;
   int vote_k, vote_P, vote_rank;
-  SplitParams sp_local;
+  const SplitParams* sp_local;  // voting's local pass: min_data / min_hessian divided by the ranks (device memory)
   double2* lsum_loc;          // [C] local (sum g, sum h) of every computed node
   unsigned long long* ltot;   // [kmax][2] the round's smaller children's local totals (global fixed-point scale)
   VoteRec* vrec;              // [P][kmax][2][K] local top-k records, all-gathered
@@ -295,16 +295,24 @@ struct FArgs {
   // round trip or extra launch per round, and a tree replays as one hipGraph. Voting parallel: k_f_vote
 // stores its top-k records into every rank's table, k_f_elect adds the elected features' local rows
 // into every rank's row block (the all-gather and the exact all-reduce of the collectives path).
-  int xg;                        // 1: in-kernel exchange (xpeer valid)
-  int xP, xrank;
-  char* xpeer[kMaxXRanks];       // rank q's exchange buffer in this process's address space
-  unsigned xo_recv, xo_fpb, xo_root, xo_flag;  // byte offsets inside every rank's buffer
-  size_t xo_vrec, xo_vrows;      // voting: the top-k records [P][2 kmax][K], the elected rows (summed)
-  unsigned* xep;                 // [1] rounds exchanged so far: a round's tag is (xsession, *xep + 1)
-  unsigned* xcnt;                // [kFXKinds] block arrivals of the current producing launch
-  unsigned long long xtimeout;   // wall-clock ticks (100 MHz) a wait may spin before it gives up
+  int xg;                        // 1: in-kernel exchange (xc valid)
   unsigned xsession;             // high word of every tag (0: the set-up self-test)
-  int xfault;                    // test hook (LGAP_FAULT_INJECT=xgmi): this rank never signals
+  const struct FXConf* xc;       // the transport's per-learner constants (device memory)
+};
+
+// The xGMI transport's per-learner constants, in device memory (FArgs::xc): kept out of the kernel
+// arguments, which every frontier launch of a round carries (FArgs stays under 1 KiB: measured
+// ~0.5 us more per launch with the peers' pointers inline).
+struct FXConf {
+  char* peer[kMaxXRanks];        // rank q's exchange buffer in this process's address space
+  size_t o_recv, o_fpb, o_root, o_flag;  // byte offsets inside every rank's buffer
+  size_t o_vrec, o_vrows;        // voting: the top-k records [P][2 kmax][K], the elected rows (summed)
+  unsigned* ep;                  // [1] rounds exchanged so far: a round's tag is (xsession, *ep + 1)
+  unsigned* cnt;                 // [kFXKinds] block arrivals of the current producing launch
+  unsigned long long timeout;    // wall-clock ticks (100 MHz) a wait may spin before it gives up
+  int P, rank;
+  int fault;                     // test hook (LGAP_FAULT_INJECT=xgmi): this rank never signals
+  int pad;
 };
 
 // exchange kinds of the frontier's xGMI transport (flag rows of the exchange buffer)

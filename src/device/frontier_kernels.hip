@@ -102,7 +102,7 @@ __device__ __forceinline__ unsigned long long* FAccPtr(const FArgs& a, int e, in
   if (!a.xg || !a.own) return a.acc + FAccAt(a, e, b, pw);
   int r = 0;
   while (r + 1 < a.own_P && a.own_b0[r + 1] <= b) ++r;
-  return reinterpret_cast<unsigned long long*>(a.xpeer[r] + a.xo_recv) +
+  return reinterpret_cast<unsigned long long*>(a.xc->peer[r] + a.xc->o_recv) +
          (static_cast<size_t>(e) * a.own_w + (b - a.own_b0[r])) * pw;
 }
 
@@ -122,19 +122,19 @@ __device__ __forceinline__ unsigned long long FXTag(const FArgs& a, unsigned ep)
   return (static_cast<unsigned long long>(a.xsession) << 32) | ep;
 }
 __device__ __forceinline__ unsigned long long* FXFlag(const FArgs& a, int owner, int kind, int src) {
-  return reinterpret_cast<unsigned long long*>(a.xpeer[owner] + a.xo_flag) + kind * kMaxXRanks + src;
+  return reinterpret_cast<unsigned long long*>(a.xc->peer[owner] + a.xc->o_flag) + kind * kMaxXRanks + src;
 }
 // one lane: spin (bounded by xtimeout; then bar[3] = 1 + kind) until every rank tagged this rank's
 // flag row `kind` with at least `tag`
 __device__ inline bool FXWaitAll(const FArgs& a, int kind, unsigned long long tag) {
   const unsigned long long t0 = wall_clock64();
-  for (int q = 0; q < a.xP; ++q) {
-    unsigned long long* f = FXFlag(a, a.xrank, kind, q);
+  for (int q = 0; q < a.xc->P; ++q) {
+    unsigned long long* f = FXFlag(a, a.xc->rank, kind, q);
     unsigned spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < tag) {
       __builtin_amdgcn_s_sleep(2);
       if ((++spins & 255u) == 0u &&
-          (wall_clock64() - t0 > a.xtimeout || __hip_atomic_load(&a.bar[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          (wall_clock64() - t0 > a.xc->timeout || __hip_atomic_load(&a.bar[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
         __hip_atomic_store(&a.bar[3], 1u + kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;
       }
@@ -195,7 +195,7 @@ __device__ __forceinline__ void FKeyFG(const SplitKey& kk, bool sys, int* f, dou
 
 // Whether a producing launch has peers to signal: one rank has none (its pushes are ordered for
 // the consumer by the kernel boundary), except under the fault-injection hook, which must wait.
-__device__ __forceinline__ bool FXPeers(const FArgs& a) { return a.xP > 1 || a.xfault; }
+__device__ __forceinline__ bool FXPeers(const FArgs& a) { return a.xc->P > 1 || a.xc->fault; }
 
 // Every thread of every block of a producing launch calls this after its pushes: each wave waits
 // until its stores / atomics are acknowledged (they target uncached memory, so no cache needs a
@@ -208,11 +208,11 @@ __device__ inline void FXArrive(const FArgs& a, int kind, unsigned long long tag
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned nb = gridDim.x * gridDim.y;
-    if (atomicAdd(&a.xcnt[kind], 1u) == nb - 1u) {
-      atomicExch(&a.xcnt[kind], 0u);  // every block of this launch has arrived
+    if (atomicAdd(&a.xc->cnt[kind], 1u) == nb - 1u) {
+      atomicExch(&a.xc->cnt[kind], 0u);  // every block of this launch has arrived
       __threadfence_system();
-      for (int q = 0; q < a.xP && !(a.xfault && a.xsession > 0); ++q) {
-        __hip_atomic_store(FXFlag(a, q, kind, a.xrank), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int q = 0; q < a.xc->P && !(a.xc->fault && a.xsession > 0); ++q) {
+        __hip_atomic_store(FXFlag(a, q, kind, a.xc->rank), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       FXWaitAll(a, kind, tag);
     }
@@ -732,7 +732,9 @@ constexpr int kRedThreads = 256;
 constexpr int kRedRows = 16;
 constexpr int kRedMaxTiles = 256;
 
-template <int MODE>
+// XG: the owner-computes xGMI exchange (its own instantiation: the single-GPU reduce compiles none
+// of it)
+template <int MODE, bool XG>
 __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   __shared__ int s_nb[kFrontierKmax], s_b0[kFrontierKmax], s_w0[kFrontierKmax + 1];
   __shared__ int s_tc[kRedMaxTiles + 1];  // chunk prefix over the LDS tiles (direct tiles: none)
@@ -753,8 +755,8 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   }
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
-  const bool xhist = a.xg && a.own;  // (xGMI owner-computes: the histogram exchange ends here)
-  const unsigned xep = xhist ? *a.xep : 0u;  // (this round's tag is xep + 1)
+  const bool xhist = XG && a.xg && a.own;  // (xGMI owner-computes: the histogram exchange ends here)
+  const unsigned xep = xhist ? *a.xc->ep : 0u;  // (this round's tag is xep + 1)
   if (sp->done) return;
   const int k = sp->k;
   // chunk prefix over the tiles (block scan; num_tiles <= kRedThreads)
@@ -788,7 +790,7 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
   const int W = nch > 0 ? s_w0[k] : 0;
   if (W == 0 && !xhist) return;  // (xGMI: a rank with no rows this round still signals it)
   // xGMI with several ranks: every rank adds into the owner's chunk, so no plain first store
-  const bool shared_out = xhist && a.xP > 1;
+  const bool shared_out = xhist && a.xc->P > 1;
   const int pw = a.quant && a.qpack ? 1 : 2;  // accumulator words per bin (see k_f_hist)
   constexpr int sw = MODE == 1 ? 2 : 1;       // slab words per bin
   for (int w = blockIdx.x; w < W; w += gridDim.x) {
@@ -844,7 +846,7 @@ __global__ __launch_bounds__(kRedThreads) void k_f_reduce(FArgs a) {
         h += static_cast<long long>(hv);
       }
     }
-    unsigned long long* out = FAccPtr(a, e, tbin0 + i, pw);
+    unsigned long long* out = XG ? FAccPtr(a, e, tbin0 + i, pw) : a.acc + FAccAt(a, e, tbin0 + i, pw);
     if (xhist) {
       // (xGMI: into the owner's receive chunk at system scope; one rank with one row group stores)
       if (nb <= kRedRows && !shared_out) {
@@ -995,7 +997,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       splp_v = p >= 0 && !voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
     for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
-      const bool sys = a.xg && a.own;  // (the receive chunk the ranks pushed into)
+      const bool sys = EXT && a.xg && a.own;  // (the receive chunk the ranks pushed into)
       const unsigned long long x0 = sys ? FXLoad64(acc + pw * kk) : acc[pw * kk];
       const unsigned long long x1 = qpack ? 0ull : (sys ? FXLoad64(acc + 2 * kk + 1) : acc[2 * kk + 1]);
       const double gp0 = gl ? gp[2 * kk] : 0.0, gp1 = gl ? gp[2 * kk + 1] : 0.0;
@@ -1095,7 +1097,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       const double sg = __shfl(pre_sum.x, 0, kWave), sh = __shfl(pre_sum.y, 0, kWave);
       const int n = __shfl(pre_n, 0, kWave);
       const int depth = __shfl(pre_depth, 0, kWave);
-      const SplitParams& spp = voting ? a.sp_local : a.sp;
+      const SplitParams spp = voting ? *a.sp_local : a.sp;
       if (!skip_both) {
         const double* H = w ? hl_full : hs_full;
         double po;
@@ -1406,7 +1408,7 @@ __global__ __launch_bounds__(kFScanWaves * 64) void k_f_scan_w(FArgs a) {
       const double sg = lsum.x, sh = lsum.y;
       const int n = nd.gcount;
       const int depth = nd.depth;
-      const SplitParams& spp = a.voting ? a.sp_local : a.sp;
+      const SplitParams spp = a.voting ? *a.sp_local : a.sp;
       if (!skip_both) {
         double po;
         if (p < 0) {
@@ -1905,7 +1907,8 @@ constexpr int kSelLPer = 4;       // leaves per lane of the register replay (L <
 
 // kWide: more than 64 features (phase A loads two feature chunks per round of loads: its own
 // instantiation, so the headline's select keeps its register allocation)
-template <bool kCegb, bool kWide>
+// kXg: the xGMI transport's push / handshake / system-scope merge (its own instantiations)
+template <bool kCegb, bool kWide, bool kXg>
 __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int C = a.C, L = a.L, F = a.F;
@@ -1926,7 +1929,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   __shared__ int s_exp[kFrontierKmax];       // chosen expansions (cids) by order
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
-  const unsigned xep = a.xg ? *a.xep : 0u;  // (xGMI: this round's tag is xep + 1)
+  const unsigned xep = kXg ? *a.xc->ep : 0u;  // (xGMI: this round's tag is xep + 1)
   if (st.done) return;
   const int kprev = st.k;
   const int cid_next = st.cid_next;
@@ -1998,7 +2001,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   // sequential select), the record copied from the winning rank's fpb entry
   const bool merge = a.fpb != nullptr;
   const int nsrc = merge ? a.vote_P : F;
-  if (!kCegb && a.xg && merge) {
+  if (kXg && merge) {
     // ---- A0 (xGMI transport): this rank's best per child over the features it owns -> fpb[rank]
     // of every rank's exchange buffer, then the handshake (k_f_pair_best's job, folded into the
     // one-block select: no launch of its own); phase A then merges the P ranks' records
@@ -2020,8 +2023,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       const uint32_t* sk = reinterpret_cast<const uint32_t*>(a.ckey + static_cast<size_t>(q) * F + max(bp, 0));
       const uint32_t* si = reinterpret_cast<const uint32_t*>(a.cinfo + static_cast<size_t>(q) * F + max(bp, 0));
       const uint32_t v = lane < kKw ? sk[lane] : (lane < kKw + kIw ? si[lane - kKw] : 0u);
-      for (int r = 0; r < a.xP; ++r) {
-        FPairBest* out = reinterpret_cast<FPairBest*>(a.xpeer[r] + a.xo_fpb) + static_cast<size_t>(a.xrank) * 2 * a.kmax + q;
+      for (int r = 0; r < a.xc->P; ++r) {
+        FPairBest* out = reinterpret_cast<FPairBest*>(a.xc->peer[r] + a.xc->o_fpb) + static_cast<size_t>(a.xc->rank) * 2 * a.kmax + q;
         if (bp < 0) {
           // (an empty record: feature -1, gain kMinScore)
           if (lane == 0) FXStore(reinterpret_cast<uint32_t*>(&out->key.feature), static_cast<uint32_t>(-1));
@@ -2041,7 +2044,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
     __syncthreads();
   }
-  if (a.xg && t == 0) *a.xep = xep + 1u;  // this round's exchanges are complete: the next round's tag
+  if (kXg && t == 0) *a.xc->ep = xep + 1u;  // this round's exchanges are complete: the next round's tag
   {
     double bg[kSelPairs];
     int bf[kSelPairs], bp[kSelPairs], pn[kSelPairs], pd[kSelPairs];
@@ -2079,7 +2082,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
             kg[u][j] = kMinScore;
             if (pv[j] && f < nsrc) {
               const SplitKey& kk = merge ? a.fpb[static_cast<size_t>(f) * 2 * a.kmax + q].key : a.ckey[static_cast<size_t>(q) * F + f];
-              FKeyFG(kk, merge && a.xg, &kf[u][j], &kg[u][j]);
+              FKeyFG(kk, kXg && merge, &kf[u][j], &kg[u][j]);
             }
           }
         }
@@ -2109,7 +2112,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
           const SplitKey& kk = merge ? a.fpb[static_cast<size_t>(f) * 2 * a.kmax + q].key : a.ckey[static_cast<size_t>(q) * F + f];
           int kf;
           double kgain;
-          FKeyFG(kk, merge && a.xg, &kf, &kgain);
+          FKeyFG(kk, kXg && merge, &kf, &kgain);
           const double g = kf < 0 ? kMinScore : (cegb ? CegbAdjust(a, kk, pn[j], pd[j], s_used, s_pc[q]) : kgain);
           const int ff = kf < 0 ? 0x7fffffff : kf;
           if (FBetter(g, ff, 0, bg[j], bf[j], 0)) {
@@ -2139,7 +2142,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         const FPairBest* pb = merge ? a.fpb + static_cast<size_t>(fpos) * 2 * a.kmax + q : nullptr;
         const uint32_t* si = reinterpret_cast<const uint32_t*>(merge ? &pb->info : a.cinfo + pos);
         const uint32_t* sk = reinterpret_cast<const uint32_t*>(merge ? &pb->key : a.ckey + pos);
-        const bool sys = merge && a.xg;  // (a record a peer pushed)
+        const bool sys = kXg && merge;  // (a record a peer pushed)
         for (int i = lane; i < kInfoWords + kKeyWords; i += 64) {
           if (i < kInfoWords) {
             reinterpret_cast<uint32_t*>(a.best + c)[i] = sys ? FXLoad(si + i) : si[i];
@@ -2946,7 +2949,7 @@ __device__ void FVoteBody(const FArgs& a, int k, int q);
 
 __global__ __launch_bounds__(kVoteThreads) void k_f_vote(FArgs a) {
   const FState* stp = a.st;
-  const unsigned xep = a.xg ? *a.xep : 0u;
+  const unsigned xep = a.xg ? *a.xc->ep : 0u;
   if (stp->done) return;
   const int k = stp->k, q = blockIdx.x;
   if ((q >> 1) < k) FVoteBody(a, k, q);
@@ -2972,7 +2975,7 @@ __device__ void FVoteBody(const FArgs& a, int k, int q) {
   }
   const int nvalid = BlockSumInt(nv, s_n);  // (barrier inside: the LDS arrays are complete)
   // (xGMI: the records go to row `rank` of every rank's table)
-  const int npeer = a.xg ? a.xP : 1;
+  const int npeer = a.xg ? a.xc->P : 1;
   const size_t roff = (static_cast<size_t>(a.vote_rank) * 2 * a.kmax + q) * K;
   // rank of feature f = the valid features ordered before it; one wave per feature, its lanes
   // comparing 64 features at a time (ballot + popcount), stopping once the rank reaches K. (A lane
@@ -2994,7 +2997,7 @@ __device__ void FVoteBody(const FArgs& a, int k, int q) {
       r.feature = f;
       r.count = s_cnt[f];
       if (!a.xg) a.vrec[roff + rank] = r;
-      else FXStoreRec(reinterpret_cast<VoteRec*>(a.xpeer[lane] + a.xo_vrec) + roff + rank, r);
+      else FXStoreRec(reinterpret_cast<VoteRec*>(a.xc->peer[lane] + a.xc->o_vrec) + roff + rank, r);
     }
   }
   for (int i = nvalid + t; i < K; i += blockDim.x) {
@@ -3003,7 +3006,7 @@ __device__ void FVoteBody(const FArgs& a, int k, int q) {
     r.feature = -1;
     r.count = 0;
     if (!a.xg) a.vrec[roff + i] = r;
-    for (int p = 0; a.xg && p < npeer; ++p) FXStoreRec(reinterpret_cast<VoteRec*>(a.xpeer[p] + a.xo_vrec) + roff + i, r);
+    for (int p = 0; a.xg && p < npeer; ++p) FXStoreRec(reinterpret_cast<VoteRec*>(a.xc->peer[p] + a.xc->o_vrec) + roff + i, r);
   }
   // the local candidates are consumed: the global pass fills the elected features' entries
   for (int f = t; f < F; f += blockDim.x) {
@@ -3070,7 +3073,7 @@ __device__ void FElectBody(const FArgs& a, int k, int q);
 
 __global__ __launch_bounds__(kVoteThreads) void k_f_elect(FArgs a) {
   const FState* stp = a.st;
-  const unsigned xep = a.xg ? *a.xep : 0u;
+  const unsigned xep = a.xg ? *a.xc->ep : 0u;
   if (stp->done) return;
   const int k = stp->k, q = blockIdx.x;
   if ((q >> 1) < k) FElectBody(a, k, q);
@@ -3125,7 +3128,7 @@ __device__ void FElectBody(const FArgs& a, int k, int q) {
         a.vrows[o + v] = x;  // (summed over ranks in place by the all-reduce)
       } else if (x != 0ull) {
         // xGMI: added into every rank's row block (exact integers; k_f_vote_scan re-zeroes its own)
-        for (int p = 0; p < a.xP; ++p) FXAdd(reinterpret_cast<unsigned long long*>(a.xpeer[p] + a.xo_vrows) + o + v, x);
+        for (int p = 0; p < a.xc->P; ++p) FXAdd(reinterpret_cast<unsigned long long*>(a.xc->peer[p] + a.xc->o_vrows) + o + v, x);
       }
     }
   }
@@ -3284,23 +3287,23 @@ __global__ __launch_bounds__(64) void k_f_pair_best(FArgs a) {
 // the P rows in rank order (sums: the same fp64 result on every rank; bounds: max, as the
 // all-reduces this replaces).
 __global__ __launch_bounds__(64) void k_fx_root(FArgs a, unsigned* __restrict__ ghmax) {
-  const unsigned xep = *a.xep;
-  if (threadIdx.x < a.xP) {
+  const unsigned xep = *a.xc->ep;
+  if (threadIdx.x < a.xc->P) {
     FXRoot mine;
     const double2 s = a.lsum[0];
     mine.g = s.x;
     mine.h = s.y;
     for (int i = 0; i < 4; ++i) mine.m[i] = ghmax[i];
-    FXStoreRec(reinterpret_cast<FXRoot*>(a.xpeer[threadIdx.x] + a.xo_root) + a.xrank, mine);
+    FXStoreRec(reinterpret_cast<FXRoot*>(a.xc->peer[threadIdx.x] + a.xc->o_root) + a.xc->rank, mine);
   }
   if (FXPeers(a)) FXArrive(a, kFXRoot, FXTag(a, xep + 1u));
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const FXRoot* rows = reinterpret_cast<const FXRoot*>(a.xpeer[a.xrank] + a.xo_root);
+    const FXRoot* rows = reinterpret_cast<const FXRoot*>(a.xc->peer[a.xc->rank] + a.xc->o_root);
     double g = 0.0, h = 0.0;
     unsigned m[4] = {0u, 0u, 0u, 0u};
-    for (int q = 0; q < a.xP; ++q) {
+    for (int q = 0; q < a.xc->P; ++q) {
       const FXRoot x = FXLoadRec(rows + q);
       g += x.g;
       h += x.h;
@@ -3319,29 +3322,29 @@ __global__ __launch_bounds__(64) void k_fx_root(FArgs a, unsigned* __restrict__ 
 __global__ __launch_bounds__(256) void k_fx_push(FArgs a, int round, int n) {
   const int half = (round & 1) * n;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    for (int q = 0; q < a.xP; ++q) {
-      FXAdd(reinterpret_cast<unsigned long long*>(a.xpeer[q] + a.xo_recv) + half + i,
-            static_cast<unsigned long long>(a.xrank + 1 + round));
+    for (int q = 0; q < a.xc->P; ++q) {
+      FXAdd(reinterpret_cast<unsigned long long*>(a.xc->peer[q] + a.xc->o_recv) + half + i,
+            static_cast<unsigned long long>(a.xc->rank + 1 + round));
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x < a.xP) {
-    FXStore(reinterpret_cast<uint32_t*>(a.xpeer[threadIdx.x] + a.xo_fpb) + (round & 1) * kMaxXRanks + a.xrank,
-            0xA5000000u + 256u * round + a.xrank);
+  if (blockIdx.x == 0 && threadIdx.x < a.xc->P) {
+    FXStore(reinterpret_cast<uint32_t*>(a.xc->peer[threadIdx.x] + a.xc->o_fpb) + (round & 1) * kMaxXRanks + a.xc->rank,
+            0xA5000000u + 256u * round + a.xc->rank);
   }
   FXArrive(a, kFXTest, FXTag(a, static_cast<unsigned>(round + 1)));
 }
 __global__ __launch_bounds__(256) void k_fx_check(FArgs a, int round, int n, unsigned* err) {
   const int half = (round & 1) * n;
   const unsigned long long want =
-      static_cast<unsigned long long>(a.xP) * (a.xP + 1) / 2 + static_cast<unsigned long long>(a.xP) * round;
-  unsigned long long* rx = reinterpret_cast<unsigned long long*>(a.xpeer[a.xrank] + a.xo_recv);
+      static_cast<unsigned long long>(a.xc->P) * (a.xc->P + 1) / 2 + static_cast<unsigned long long>(a.xc->P) * round;
+  unsigned long long* rx = reinterpret_cast<unsigned long long*>(a.xc->peer[a.xc->rank] + a.xc->o_recv);
   unsigned bad = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     bad += FXLoad64(rx + half + i) != want ? 1u : 0u;
     FXStore64(rx + half + i, 0ull);
   }
-  if (blockIdx.x == 0 && threadIdx.x < a.xP) {
-    const unsigned v = FXLoad(reinterpret_cast<const uint32_t*>(a.xpeer[a.xrank] + a.xo_fpb) + (round & 1) * kMaxXRanks + threadIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x < a.xc->P) {
+    const unsigned v = FXLoad(reinterpret_cast<const uint32_t*>(a.xc->peer[a.xc->rank] + a.xc->o_fpb) + (round & 1) * kMaxXRanks + threadIdx.x);
     bad += v != 0xA5000000u + 256u * round + threadIdx.x ? 1u : 0u;
   }
   if (bad) atomicAdd(err, bad);
@@ -3524,9 +3527,10 @@ void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
   // the partial rows' reduction (same MODE precedence as the histogram: quantized levels, then
   // gpu_use_dp's 64-bit pairs, then the fixed-point packed words)
   const int grid = std::max(1, std::min(a.red_grid, 4096));
-  if (a.quant) k_f_reduce<2><<<grid, kRedThreads, 0, s>>>(a);
-  else if (a.use_dp) k_f_reduce<1><<<grid, kRedThreads, 0, s>>>(a);
-  else k_f_reduce<0><<<grid, kRedThreads, 0, s>>>(a);
+  const bool xg = a.xg && a.own;
+  if (a.quant) xg ? k_f_reduce<2, true><<<grid, kRedThreads, 0, s>>>(a) : k_f_reduce<2, false><<<grid, kRedThreads, 0, s>>>(a);
+  else if (a.use_dp) xg ? k_f_reduce<1, true><<<grid, kRedThreads, 0, s>>>(a) : k_f_reduce<1, false><<<grid, kRedThreads, 0, s>>>(a);
+  else xg ? k_f_reduce<0, true><<<grid, kRedThreads, 0, s>>>(a) : k_f_reduce<0, false><<<grid, kRedThreads, 0, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -3562,9 +3566,12 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 
 
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
-  if (a.cegb_raw) k_f_select<true, false><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L) + a.F + 16, s>>>(a);
-  else if (a.F > 64 || (a.fpb != nullptr && a.vote_P > 64)) k_f_select<false, true><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L), s>>>(a);
-  else k_f_select<false, false><<<1, kFSelThreads, FrontierSelectLds(a.C, a.L), s>>>(a);
+  const size_t lds = FrontierSelectLds(a.C, a.L);
+  const bool wide = a.F > 64 || (a.fpb != nullptr && a.vote_P > 64);
+  if (a.cegb_raw) k_f_select<true, false, false><<<1, kFSelThreads, lds + a.F + 16, s>>>(a);
+  else if (a.xg) wide ? k_f_select<false, true, true><<<1, kFSelThreads, lds, s>>>(a) : k_f_select<false, false, true><<<1, kFSelThreads, lds, s>>>(a);
+  else if (wide) k_f_select<false, true, false><<<1, kFSelThreads, lds, s>>>(a);
+  else k_f_select<false, false, false><<<1, kFSelThreads, lds, s>>>(a);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -3592,7 +3599,7 @@ void LaunchFrontierPairBest(const FArgs& a, hipStream_t s) {
 }
 
 void LaunchFrontierXRoot(const FArgs& a, unsigned* ghmax, hipStream_t s) {
-  if (a.xP > 64) std::abort();  // (kMaxXRanks <= 64: one lane per peer)
+  if (a.xc->P > 64) std::abort();  // (kMaxXRanks <= 64: one lane per peer)
   k_fx_root<<<1, 64, 0, s>>>(a, ghmax);
   HIP_CHECK(hipGetLastError());
 }
