@@ -37,6 +37,9 @@ for s in "$@"; do
     voteprof) step voteprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/voteprof -o run -- python3 scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --learner voting --steps 10 --warmup 2 && python scripts/prof_summary.py $OUT/voteprof "GOSS 3M x 500 voting, one rank" 12 > $OUT/voteprof_summary.md && step serprof3 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/serprof3 -o run -- python3 scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --steps 10 --warmup 2 && python scripts/prof_summary.py $OUT/serprof3 "GOSS 3M x 500 serial" 12 > $OUT/serprof3_summary.md;;
     votet) step votet 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "voting";;
     vote3) step vote3 600 python scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --learner voting --steps 10 --warmup 2 && step ser3 600 python scripts/bench_suite.py --config regression_goss --rows 3000000 --features 500 --steps 10 --warmup 2;;
+    bagt) step bagt 600 python -u -m pytest tests/test_gpu_learner.py tests/test_gpu_kernels.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "bag or goss";;
+    gossprof) step gossprof 900 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/gossprof -o run -- python3 scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --steps 5 --warmup 11 && python scripts/prof_summary.py $OUT/gossprof "GOSS 12.5M x 500 serial, bagged iterations" 16 > $OUT/gossprof_summary.md;;
+    oobab) for r in 2 4 8; do LGAP_KERNEL=oob_rows=$r step oob$r 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/oob$r -o run -- python3 scripts/bench_suite.py --config regression_goss --rows 12500000 --features 500 --steps 4 --warmup 11 && python scripts/prof_summary.py $OUT/oob$r "GOSS 12.5M x 500, oob_rows=$r" 15 > $OUT/oob${r}_summary.md || exit 1; done;;
     ict) step ict 600 python -u -m pytest tests/test_gpu_learner.py tests/test_frontier_kernels.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "interaction or frontier or bynode";;
     dpmulti) step dpmulti 1100 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "multirank";;
     fp) step fp 600 python -u -m pytest tests/test_gpu_learner.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "feature_parallel";;

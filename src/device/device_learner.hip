@@ -120,14 +120,15 @@ namespace {
 // LGAP_KERNEL="key=value,key=value" with the keys fhist_threads (512 | 1024), hist_lds_kb (LDS
 // tile budget), quant_lds32 (0 | 1), part_iters (4 | 8 | 16), hist_il (0 | 1), nibble (0: 8-bit
 // rows), quant_hist (off: float histograms under quantized training), scan_global (1), scan_wave
-// (1: the wave-per-item scan below its 64-feature threshold). Returns
+// (1: the wave-per-item scan below its 64-feature threshold), oob_rows (2 | 4 | 8: rows per
+// thread of the out-of-bag walk). Returns
 // the key's value, nullptr when it is not set. Read at each use: tests change the environment
 // between trainings in one process. Each key's value has its own storage (a caller may hold the
 // values of several keys at once); empty items (a trailing comma) are skipped.
 const char* KernelOverride(const char* key) {
   static const char* const kKeys[] = {"fhist_threads", "hist_lds_kb", "quant_lds32", "part_iters",
                                       "hist_il",       "nibble",      "quant_hist",  "scan_global",
-                                      "scan_wave"};
+                                      "scan_wave",     "oob_rows"};
   constexpr int kNumKeys = static_cast<int>(sizeof(kKeys) / sizeof(kKeys[0]));
   thread_local std::string vals[kNumKeys];
   const char* e = std::getenv("LGAP_KERNEL");
@@ -507,6 +508,7 @@ class DeviceTreeLearner : public TreeLearner {
       use_bag_ = true;
       idx_[2].Upload(used, n, stream_);
     }
+    oob_ok_ = false;  // (a host bag: no out-of-bag list, the score update walks every row)
   }
 
   // ---- row sampling on the device (sample_kernels.hip): the bag goes straight into idx_[2]
@@ -566,6 +568,11 @@ class DeviceTreeLearner : public TreeLearner {
     a.tile_cnt = samp_cnt_.get();
     a.tile_sel = samp_sel_.get();
     a.out = idx_[2].get();
+    // the frontier's score update walks only the out-of-bag rows (LeafMapScore)
+    if (frontier_ && width_ >= 1 && width_ <= 2) {
+      if (oob_.size() < static_cast<size_t>(N_)) oob_.Resize(std::max(N_, 1));
+      a.oob = oob_.get();
+    }
     a.total = samp_total_.get();
     LaunchSampleCount(a, stream_);
     LaunchSampleScatter(a, stream_);
@@ -577,6 +584,7 @@ class DeviceTreeLearner : public TreeLearner {
     bag_cnt_ = *cnt;
     use_bag_ = bag_cnt_ < N_;
     if (!use_bag_) bag_cnt_ = N_;
+    oob_ok_ = a.oob != nullptr;
     Log::Debug("Device %s, using %d data to train", a.mode == 3 ? "GOSS" : "bagging", bag_cnt_);
   }
 
@@ -882,27 +890,33 @@ class DeviceTreeLearner : public TreeLearner {
     }
     const bool fresh = tree == last_trained_;
     last_trained_ = nullptr;
-    if (fresh && frontier_ && !use_bag_ && LeafMapScore(tree, k)) return;
+    if (fresh && frontier_ && (!use_bag_ || oob_ok_) && LeafMapScore(tree, k)) return;
     TraverseTree(tree, rowbins_.get(), N_, s);
   }
 
   // Score update from the leaf ranges of the frontier tree just grown (traverse_kernels.h
-  // LaunchLeafMap): without bagging every row sits in exactly one leaf's index segment, so the
-  // rows' leaves come from those segments instead of a walk of the tree over the packed rows.
+  // LaunchLeafMap): every trained row sits in exactly one leaf's index segment, so the rows'
+  // leaves come from those segments instead of a walk of the tree over the packed rows. A
+  // bagged / GOSS tree (reference gbdt.cpp:495-516) adds the out-of-bag list the device sampler
+  // wrote (oob_) as one more segment, and only those rows walk the tree (LaunchLeafMapList).
   // The map is built here; the add itself is deferred (pend_) into the next pointwise
   // gradient pass, or flushed by the first reader of the score (FlushScore). Uploads go
   // through the traversal's staging ring (no host wait).
   bool LeafMapScore(const Tree* tree, int k) {
     const int nl = tree->num_leaves();
-    if (nl != static_cast<int>(h_range_.size()) || nl > kLMMaxLeaves) return false;
+    const bool bag = use_bag_;
+    const int nseg = nl + (bag ? 1 : 0);  // (bag: the out-of-bag rows, placeholder leaf nl)
+    if (nl != static_cast<int>(h_range_.size()) || nseg > kLMMaxLeaves) return false;
     long long total = 0;
     for (const auto& r : h_range_) {
       if (r.buf < 0 || r.buf >= kFrontierIdx) return false;  // (a partitioned leaf: an index buffer)
       total += r.count;
     }
-    if (total != N_) return false;
-    const size_t seg_bytes = Round256(sizeof(LeafSeg) * nl), off_bytes = Round256(sizeof(int) * (nl + 1));
-    const size_t bytes = seg_bytes + off_bytes + sizeof(double) * nl;
+    if (total != (bag ? bag_cnt_ : N_)) return false;
+    const size_t seg_bytes = Round256(sizeof(LeafSeg) * nseg), off_bytes = Round256(sizeof(int) * (nseg + 1));
+    const size_t map_part = Round256(seg_bytes + off_bytes + sizeof(double) * nseg);
+    const CompactLayout z = bag ? CompactTreeLayout(tree) : CompactLayout{0, 0, 0, 0};
+    const size_t bytes = map_part + z.total;
     const int slot = tree_slot_++ & 1;
     if (tree_evt_[slot] == nullptr) HIP_CHECK(hipEventCreateWithFlags(&tree_evt_[slot], hipEventDisableTiming));
     else HIP_CHECK(hipEventSynchronize(tree_evt_[slot]));
@@ -933,14 +947,23 @@ class DeviceTreeLearner : public TreeLearner {
       off[l + 1] = off[l] + h_range_[l].count;
       lv[l] = tree->LeafOutput(l);
     }
+    if (bag) {
+      segs[nl].buf = kLeafOobBuf;
+      segs[nl].start = 0;
+      segs[nl].count = N_ - bag_cnt_;
+      segs[nl].pad = 0;  // (ascending)
+      off[nl + 1] = N_;
+      lv[nl] = 0.0;
+      PackCompactTree(tree, hp + map_part, z);
+    }
     if (ttree_buf_.size() < bytes) {
       HIP_CHECK(hipStreamSynchronize(stream_));  // queued score updates still read the old buffer
       ttree_buf_.Resize(bytes);
     }
     HIP_CHECK(hipMemcpyAsync(ttree_buf_.get(), hp, bytes, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipEventRecord(tree_evt_[slot], stream_));
-    const size_t bound_ints = LeafTileBoundsInts(N_, nl);
-    const size_t map_bytes = Round256(static_cast<size_t>(N_) * (nl > 256 ? 2 : 1));
+    const size_t bound_ints = LeafTileBoundsInts(N_, nseg);
+    const size_t map_bytes = Round256(static_cast<size_t>(N_) * (nseg > 256 ? 2 : 1));
     if (leaf_bounds_.size() < bound_ints || leaf_map_.size() < map_bytes || pend_lv_.size() < static_cast<size_t>(kLMMaxLeaves)) {
       HIP_CHECK(hipStreamSynchronize(stream_));
       leaf_bounds_.Resize(std::max(leaf_bounds_.size(), bound_ints));
@@ -949,15 +972,27 @@ class DeviceTreeLearner : public TreeLearner {
     }
     LeafMapArgs la;
     for (int i = 0; i < kLeafIdxBufs; ++i) la.idx[i] = i < kFrontierIdx ? idx_[i].get() : nullptr;
-    la.segs = reinterpret_cast<const LeafSeg*>(ttree_buf_.get());
-    la.seg_off = reinterpret_cast<const int*>(ttree_buf_.get() + seg_bytes);
-    la.leaf_value = reinterpret_cast<const double*>(ttree_buf_.get() + seg_bytes + off_bytes);
-    la.num_leaves = nl;
+    static_assert(kFrontierIdx <= kLeafOobBuf, "the out-of-bag list's index-buffer id");
+    la.idx[kLeafOobBuf] = bag ? oob_.get() : nullptr;
+    const char* db = ttree_buf_.get();
+    la.segs = reinterpret_cast<const LeafSeg*>(db);
+    la.seg_off = reinterpret_cast<const int*>(db + seg_bytes);
+    la.leaf_value = reinterpret_cast<const double*>(db + seg_bytes + off_bytes);
+    la.num_leaves = nseg;
     la.n = N_;
     LaunchLeafMap(la, leaf_bounds_.get(), leaf_map_.get(), pend_lv_.get(), stream_);
+    if (bag) {
+      const char* dt = db + map_part;
+      const bool cols = stride_dw_ > 16 && colbins_.size() >= static_cast<size_t>(G_) * N_ * width_;
+      LaunchLeafMapList(cols ? colbins_.get() : nullptr, rowbins_.get(), stride_dw_, width_, N_, oob_.get(),
+                        N_ - bag_cnt_, reinterpret_cast<const TNode*>(dt), nl - 1,
+                        reinterpret_cast<const TCat*>(dt + z.cat), reinterpret_cast<const uint32_t*>(dt + z.bit), nseg,
+                        leaf_map_.get(), KernelOverride("oob_rows") ? std::atoi(KernelOverride("oob_rows")) : 4,
+                        num_cu_, stream_);
+    }
     pend_.on = true;
     pend_.k = k;
-    pend_.nl = nl;
+    pend_.nl = nseg;
     return true;
   }
 
@@ -1031,23 +1066,29 @@ class DeviceTreeLearner : public TreeLearner {
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
-  // Compact traversal (traverse_kernels.h): node predicates precomputed in group-bin space.
-  void TraverseTreeCompact(const Tree* tree, const uint32_t* rowbins, int n, double* s) {
+  // Compact tree staging (traverse_kernels.h TNode / TCat): offsets of the nodes, the
+  // categorical node data, the leaf values and the categorical words in one upload
+  struct CompactLayout {
+    size_t cat, leaf, bit, total;
+  };
+  static CompactLayout CompactTreeLayout(const Tree* tree) {
+    const int nn = tree->num_leaves() - 1, nl = tree->num_leaves();
+    const size_t node_bytes = Round256(sizeof(TNode) * nn), cat_bytes = Round256(sizeof(TCat) * nn);
+    const size_t leaf_bytes = Round256(sizeof(double) * nl);
+    const size_t bit_bytes = sizeof(uint32_t) * std::max<size_t>(1, tree->cat_threshold_inner().size());
+    CompactLayout z;
+    z.cat = node_bytes;
+    z.leaf = z.cat + cat_bytes;
+    z.bit = z.leaf + leaf_bytes;
+    z.total = z.bit + bit_bytes;
+    return z;
+  }
+  void PackCompactTree(const Tree* tree, char* hp, const CompactLayout& z) const {
     const int nn = tree->num_leaves() - 1, nl = tree->num_leaves();
     const auto& cb = tree->cat_boundaries_inner();
     const auto& ct = tree->cat_threshold_inner();
-    const size_t node_bytes = Round256(sizeof(TNode) * nn), cat_bytes = Round256(sizeof(TCat) * nn);
-    const size_t leaf_bytes = Round256(sizeof(double) * nl), bit_bytes = sizeof(uint32_t) * std::max<size_t>(1, ct.size());
-    const size_t total = node_bytes + cat_bytes + leaf_bytes + bit_bytes;
-    // staging ring: the host fills one pinned buffer while the copy out of the other may still
-    // be queued, so the score update returns without waiting for the GPU (the next iteration's
-    // launches queue behind the traversal instead of after a host round trip)
-    const int slot = tree_slot_++ & 1;
-    if (tree_evt_[slot] == nullptr) HIP_CHECK(hipEventCreateWithFlags(&tree_evt_[slot], hipEventDisableTiming));
-    else HIP_CHECK(hipEventSynchronize(tree_evt_[slot]));
-    char* hp = pin_tree_ring_[slot].Get(total);
     TNode* nodes = reinterpret_cast<TNode*>(hp);
-    TCat* cats = reinterpret_cast<TCat*>(hp + node_bytes);
+    TCat* cats = reinterpret_cast<TCat*>(hp + z.cat);
     for (int i = 0; i < nn; ++i) {
       const FeatureInfo& fi = data_->feature(tree->split_feature_inner(i));
       const int8_t dt = tree->decision_type(i);
@@ -1085,10 +1126,25 @@ class DeviceTreeLearner : public TreeLearner {
       d.tg = static_cast<uint16_t>(tg < offset ? 0 : tg);
       d.flags = static_cast<uint8_t>((out_left ? kTOutLeft : 0) | (dleft ? kTDefaultLeft : 0));
     }
-    double* lv = reinterpret_cast<double*>(hp + node_bytes + cat_bytes);
+    double* lv = reinterpret_cast<double*>(hp + z.leaf);
     for (int l = 0; l < nl; ++l) lv[l] = tree->LeafOutput(l);
-    uint32_t* cw = reinterpret_cast<uint32_t*>(hp + node_bytes + cat_bytes + leaf_bytes);
+    uint32_t* cw = reinterpret_cast<uint32_t*>(hp + z.bit);
     for (size_t i = 0; i < ct.size(); ++i) cw[i] = ct[i];
+  }
+
+  // Compact traversal (traverse_kernels.h): node predicates precomputed in group-bin space.
+  void TraverseTreeCompact(const Tree* tree, const uint32_t* rowbins, int n, double* s) {
+    const int nn = tree->num_leaves() - 1, nl = tree->num_leaves();
+    const CompactLayout z = CompactTreeLayout(tree);
+    const size_t node_bytes = z.cat, cat_bytes = z.leaf - z.cat, leaf_bytes = z.bit - z.leaf, total = z.total;
+    // staging ring: the host fills one pinned buffer while the copy out of the other may still
+    // be queued, so the score update returns without waiting for the GPU (the next iteration's
+    // launches queue behind the traversal instead of after a host round trip)
+    const int slot = tree_slot_++ & 1;
+    if (tree_evt_[slot] == nullptr) HIP_CHECK(hipEventCreateWithFlags(&tree_evt_[slot], hipEventDisableTiming));
+    else HIP_CHECK(hipEventSynchronize(tree_evt_[slot]));
+    char* hp = pin_tree_ring_[slot].Get(total);
+    PackCompactTree(tree, hp, z);
     if (ttree_buf_.size() < total) {
       HIP_CHECK(hipStreamSynchronize(stream_));  // queued traversals still read the old buffer
       ttree_buf_.Resize(total);
@@ -4252,6 +4308,8 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<int> leaf_bounds_;  // LeafMapScore: per-leaf tile bounds
   DevBuf<uint8_t> leaf_map_;  // LeafMapScore: leaf of every row (uint8 / uint16)
   DevBuf<double> pend_lv_;    // LeafMapScore: the pending add's leaf values
+  DevBuf<int> oob_;           // DeviceSample: the out-of-bag rows, ascending (LeafMapScore)
+  bool oob_ok_ = false;       // oob_ holds the current bag's complement
   struct PendingAdd {
     bool on = false;
     int k = 0, nl = 0;

@@ -42,6 +42,7 @@ struct SampleArgs {
   int* tile_cnt = nullptr;       // kept rows per tile
   unsigned* tile_sel = nullptr;  // GOSS, 4 words per tile: top threshold bits, key threshold, key mode, multiplier bits
   int* out = nullptr;            // kept rows, ascending
+  int* oob = nullptr;            // nullptr, or the rows NOT kept, ascending (out-of-bag score walk)
   int* total = nullptr;          // kept row count
 };
 

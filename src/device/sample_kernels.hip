@@ -226,7 +226,9 @@ __global__ __launch_bounds__(kThreads) void k_sample_scatter(SampleArgs a, int n
       before += k < w ? s_w[q][k] : 0;
       all += s_w[q][k];
     }
-    if (keep[q]) a.out[off + before + __popcll(mk[q] & lt)] = base + q * kThreads + t;
+    const int i = base + q * kThreads + t, kb = off + before + __popcll(mk[q] & lt);  // kept rows before i
+    if (keep[q]) a.out[kb] = i;
+    else if (a.oob != nullptr && i < a.N) a.oob[i - kb] = i;
     off += all;
   }
   if (a.mode == 3) {

@@ -72,6 +72,20 @@ struct LeafMapArgs {
 };
 // ints of the tile-bounds scratch for n rows and num_leaves leaves
 size_t LeafTileBoundsInts(int n, int num_leaves);
+// Bagged / GOSS trees (reference gbdt.cpp:495-516 UpdateScore: the in-bag rows take their leaf
+// from the learner's partition, only the out-of-bag rows walk the tree): LaunchLeafMap runs over
+// the leaves' segments plus one more, the ascending out-of-bag list (LeafMapArgs::idx
+// [kLeafOobBuf]) as a placeholder leaf num_leaves - 1 of value 0; LaunchLeafMapList then walks
+// the listed rows through the compact tree and overwrites their map entries with their leaves.
+// colbins != nullptr: the group-major copy colbins[g * n + row], else the packed rows.
+// map_leaves: the leaf count the map was built for (uint8 entries up to 256, else uint16).
+// rows_per_thread (2 / 4 / 8): independent walks per lane (the gathers of a deep level are
+// latency-bound: more walks in flight).
+constexpr int kLeafOobBuf = kLeafIdxBufs - 1;
+void LaunchLeafMapList(const uint8_t* colbins, const uint32_t* rowbins, int stride_dw, int width, int n,
+                       const int* list, int count, const TNode* nodes, int num_nodes, const TCat* cats,
+                       const uint32_t* cat_bits, int map_leaves, void* map, int rows_per_thread, int num_cu,
+                       hipStream_t s);
 void LaunchLeafMap(const LeafMapArgs& a, int* bounds, void* map, double* lv_out, hipStream_t s);
 void LaunchLeafMapAdd(const void* map, const double* lv, int num_leaves, int n, double* score, int num_cu,
                       hipStream_t s);

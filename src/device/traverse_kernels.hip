@@ -196,6 +196,75 @@ __global__ __launch_bounds__(kTThreads) void k_traverse_col(const uint8_t* __res
   }
 }
 
+// The out-of-bag rows of a bagged tree (LaunchLeafMapList): list[i] -> its leaf in map[row].
+// List positions are ascending rows, so a wave's row loads and map writes stay local; the walk
+// is k_traverse_col's (COL: group-major bins) or the packed rows' (W = 1 / 2 byte group bins).
+template <bool COL, int W, typename T, int R>
+__global__ __launch_bounds__(kTThreads) void k_traverse_list(const uint8_t* __restrict__ bins, long long stride, int n,
+                                                             const int* __restrict__ list, int count,
+                                                             const TNode* __restrict__ nodes, int num_nodes,
+                                                             const TCat* __restrict__ cats,
+                                                             const uint32_t* __restrict__ cat_bits, T* __restrict__ map) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  TNode* s_nodes = reinterpret_cast<TNode*>(lds);
+  const int t = threadIdx.x;
+  for (int i = t; i < num_nodes * static_cast<int>(sizeof(TNode) / 4); i += kTThreads) {
+    reinterpret_cast<uint32_t*>(s_nodes)[i] = reinterpret_cast<const uint32_t*>(nodes)[i];
+  }
+  __syncthreads();
+  for (int base = blockIdx.x * kTThreads * R; base < count; base += gridDim.x * kTThreads * R) {
+    int row[R], node[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int p = base + t + j * kTThreads;
+      row[j] = p < count ? list[p] : 0;
+      node[j] = p < count ? 0 : ~0;
+    }
+    // one level of all R walks per pass: the R node reads, then the R gathers issued together
+    // (finished walks re-read the root's node and skip their gather), then the R decisions
+    bool live = true;
+    while (live) {
+      live = false;
+      TNode nd[R];
+      uint32_t gb[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) nd[j] = s_nodes[node[j] < 0 ? 0 : node[j]];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        gb[j] = 0;
+        if (node[j] >= 0) {
+          if (COL) {
+            const size_t o = static_cast<size_t>(nd[j].group) * n + row[j];
+            gb[j] = W == 1 ? bins[o] : reinterpret_cast<const uint16_t*>(bins)[o];
+          } else {
+            gb[j] = GroupBin<W>(bins + static_cast<size_t>(row[j]) * stride, nd[j].group);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        if (node[j] < 0) continue;
+        bool left;
+        if (nd[j].flags & kTCat) {
+          left = CatLeft(cats[node[j]], cat_bits, gb[j]);
+        } else if (gb[j] < nd[j].lo || gb[j] > nd[j].hi) {
+          left = (nd[j].flags & kTOutLeft) != 0;
+        } else if (static_cast<int>(gb[j]) == nd[j].gmiss) {
+          left = (nd[j].flags & kTDefaultLeft) != 0;
+        } else {
+          left = gb[j] <= nd[j].tg;
+        }
+        node[j] = left ? nd[j].left : nd[j].right;
+        live |= node[j] >= 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (base + t + j * kTThreads < count) map[row[j]] = static_cast<T>(~node[j]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_pack_nibbles(const uint32_t* __restrict__ rowbins, int stride_dw, int n,
                                                       int groups, uint32_t* __restrict__ out, int stride4) {
   const long long total = static_cast<long long>(n) * stride4;
@@ -237,6 +306,48 @@ void LaunchTraverseCols(const uint8_t* colbins, int width, int n, const TNode* n
   } else {
     k_traverse_col<2><<<grid, kTThreads, lds, s>>>(colbins, n, nodes, num_nodes, cats, cat_bits, leaf_value, num_leaves,
                                                   score);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T, int R>
+void LaunchListT(const uint8_t* colbins, const uint32_t* rowbins, int stride_dw, int width, int n, const int* list,
+                 int count, const TNode* nodes, int num_nodes, const TCat* cats, const uint32_t* cat_bits, T* map,
+                 int num_cu, hipStream_t s) {
+  const size_t lds = sizeof(TNode) * static_cast<size_t>(std::max(num_nodes, 1));
+  const int grid = std::max(1, std::min(DivUp(count, kTThreads * R), num_cu * 8));
+  const long long stride = 4LL * stride_dw;
+  if (colbins != nullptr) {
+    if (width == 1) k_traverse_list<true, 1, T, R><<<grid, kTThreads, lds, s>>>(colbins, 0, n, list, count, nodes, num_nodes, cats, cat_bits, map);
+    else k_traverse_list<true, 2, T, R><<<grid, kTThreads, lds, s>>>(colbins, 0, n, list, count, nodes, num_nodes, cats, cat_bits, map);
+  } else {
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rowbins);
+    if (width == 1) k_traverse_list<false, 1, T, R><<<grid, kTThreads, lds, s>>>(rb, stride, n, list, count, nodes, num_nodes, cats, cat_bits, map);
+    else k_traverse_list<false, 2, T, R><<<grid, kTThreads, lds, s>>>(rb, stride, n, list, count, nodes, num_nodes, cats, cat_bits, map);
+  }
+}
+
+template <typename T>
+void LaunchListR(const uint8_t* colbins, const uint32_t* rowbins, int stride_dw, int width, int n, const int* list,
+                 int count, const TNode* nodes, int num_nodes, const TCat* cats, const uint32_t* cat_bits, T* map,
+                 int rows_per_thread, int num_cu, hipStream_t s) {
+  if (rows_per_thread <= 2) LaunchListT<T, 2>(colbins, rowbins, stride_dw, width, n, list, count, nodes, num_nodes, cats, cat_bits, map, num_cu, s);
+  else if (rows_per_thread <= 4) LaunchListT<T, 4>(colbins, rowbins, stride_dw, width, n, list, count, nodes, num_nodes, cats, cat_bits, map, num_cu, s);
+  else LaunchListT<T, 8>(colbins, rowbins, stride_dw, width, n, list, count, nodes, num_nodes, cats, cat_bits, map, num_cu, s);
+}
+
+void LaunchLeafMapList(const uint8_t* colbins, const uint32_t* rowbins, int stride_dw, int width, int n,
+                       const int* list, int count, const TNode* nodes, int num_nodes, const TCat* cats,
+                       const uint32_t* cat_bits, int map_leaves, void* map, int rows_per_thread, int num_cu,
+                       hipStream_t s) {
+  if (count <= 0) return;
+  if (width != 1 && width != 2) Log::Fatal("LaunchLeafMapList: group-bin width %d (8- / 16-bit rows)", width);
+  if (map_leaves <= 256) {
+    LaunchListR(colbins, rowbins, stride_dw, width, n, list, count, nodes, num_nodes, cats, cat_bits,
+                static_cast<uint8_t*>(map), rows_per_thread, num_cu, s);
+  } else {
+    LaunchListR(colbins, rowbins, stride_dw, width, n, list, count, nodes, num_nodes, cats, cat_bits,
+                static_cast<uint16_t*>(map), rows_per_thread, num_cu, s);
   }
   HIP_CHECK(hipGetLastError());
 }

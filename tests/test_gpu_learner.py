@@ -280,6 +280,41 @@ def test_device_goss(lgb, gpu_required):
     assert abs(ag - ac) < 1e-3, (ag, ac)
 
 
+@pytest.mark.parametrize("features", [28, 100])
+@pytest.mark.parametrize("kw", [{"bagging_fraction": 0.6, "bagging_freq": 1},
+                                {"data_sample_strategy": "goss", "learning_rate": 0.5},
+                                {"bagging_fraction": 0.5, "bagging_freq": 2, "objective": "multiclass", "num_class": 3}],
+                         ids=["bagging", "goss", "multiclass-bagging"])
+def test_bagged_score_update_walks_only_out_of_bag_rows(lgb, gpu_required, features, kw):
+    """A bagged / GOSS frontier tree scores its in-bag rows from the partition's leaf segments and
+    walks only the out-of-bag list the device sampler wrote (LeafMapScore + LaunchLeafMapList;
+    reference gbdt.cpp:495-516). The host-sampled run draws the same bags but has no out-of-bag
+    list, so every row walks the tree: the two must train the same model (a wrong score on any
+    row changes the next trees' gradients). Narrow rows walk the packed rows, 100 features the
+    group-major copy."""
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((30000, features)).astype(np.float32)
+    X[rng.random(X.shape) < 0.05] = np.nan
+    y = (X[:, 0] + 0.5 * np.nan_to_num(X[:, 1]) ** 2 - X[:, 2] * (X[:, 3] > 0) > 0.3).astype(np.float32)
+    if kw.get("objective") == "multiclass":
+        y = (np.nan_to_num(X[:, 0]) > 0).astype(np.float32) + (np.nan_to_num(X[:, 1]) > 0.5)
+    bd = _train(lgb, X, y, "gpu", rounds=12, **kw)
+    bh = _train(lgb, X, y, "gpu", rounds=12, device_sampling=False, **kw)
+    sd, sh = [], []
+    for t in _trees(bd):
+        _splits(t["tree_structure"], sd)
+    for t in _trees(bh):
+        _splits(t["tree_structure"], sh)
+    assert sd == sh
+    np.testing.assert_allclose(bd.predict(X[:5000], raw_score=True), bh.predict(X[:5000], raw_score=True),
+                               rtol=1e-6, atol=1e-7)
+    # the training score the device kept (every row: in-bag from the segments, out-of-bag walked)
+    # equals the model's prediction (both transformed: the inner predict is the objective's output)
+    inner = bd._Booster__inner_predict(0).reshape(-1)
+    pred = bd.predict(X).reshape(-1)  # (multiclass: row-major, as the inner predict)
+    np.testing.assert_allclose(inner, pred, rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("transport", ["collective", "xgmi", "collective-quantized"])
 def test_data_parallel_path_single_rank(lgb, gpu_required, transport):
     """The owner-computes data-parallel learner path (owner exchange of the histogram, owned-feature
