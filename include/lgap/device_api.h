@@ -36,6 +36,9 @@ std::unique_ptr<TreeLearner> CreateDeviceTreeLearner(const Config* config, const
 // the frontier implements on the device (forced splits, CEGB feature penalties) route to the
 // host split policy when it cannot.
 bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type);
+// The same for feature_fraction_bynode under interaction constraints: the frontier's select
+// draws each node's mask over the features its constraints allow (serial learner only).
+bool FrontierServesByNode(const Config* config, const Dataset* train, const std::string& learner_type);
 // Whether the device learner fits linear_tree leaves itself (fp64 MFMA Gram systems): serial
 // learner, float gradients, raw values kept, and at most 30 branch features per leaf.
 bool LinearOnDevice(const Config* config, const Dataset* train, const std::string& learner_type);

@@ -209,7 +209,8 @@ bool FrontierShapeFits(int L, int TB, int F, int max_bin, int max_cat_bin, bool 
   const int C = FrontierCapacityFor(std::max(2, L), TB);
   if (C > kFrontierMaxNodes || F <= 0) return false;
   if (FrontierScanLds(max_bin, max_cat_bin) > 150 * 1024) return false;
-  return FrontierSelectLds(C, std::max(2, L)) + (cegb_raw ? F + 16 : 0) <= 150 * 1024;
+  // (raw candidates: the CEGB used-feature flags and the by-node draws' scratch, F bytes each)
+  return FrontierSelectLds(C, std::max(2, L)) + (cegb_raw ? 2 * (F + 16) : 0) <= 150 * 1024;
 }
 
 class DeviceTreeLearner : public TreeLearner {
@@ -1614,27 +1615,41 @@ class DeviceTreeLearner : public TreeLearner {
     tp->root_gcount = gcount;
     const bool tune = frontier_ && stune_.on;
     tp->spec_alpha = static_cast<float>(tune ? stune_.Alpha() : fspec_alpha_);
-    tp->pad[0] = tp->pad[1] = tp->pad[2] = 0;
+    tp->byn_rng = 0;
+    tp->pad[0] = tp->pad[1] = 0;
     HIP_CHECK(hipMemcpyAsync(tparams_.get(), tp, sizeof(TreeParams), hipMemcpyHostToDevice, stream_));
     const auto t_tree0 = std::chrono::steady_clock::now();
     if (config_->use_quantized_grad) QuantizeGradients(class_id);
     col_sampler_.ResetByTree();
     const auto& used = col_sampler_.is_feature_used_bytree();
-    uint8_t* um = pin_mask_.Get(static_cast<size_t>(F_) * (1 + 2 * L_));
+    uint8_t* um = pin_mask_.Get(static_cast<size_t>(F_) * (1 + 2 * L_) + 8);
     for (int f = 0; f < F_; ++f) um[f] = used[f] ? 1 : 0;
     HIP_CHECK(hipMemcpyAsync(used_bytree_.get(), um, F_, hipMemcpyHostToDevice, stream_));
     Random byn_state;
+    const bool byn_dev = use_bynode_ && frontier_ && ByNodeOnDevice();
+    if (use_bynode_ && !frontier_ && ByNodeOnDevice()) {
+      Log::Fatal("feature_fraction_bynode with interaction constraints needs the frontier engine (shape / node capacity)");
+    }
     if (use_bynode_) {
       // the tree's masks in the host's draw order (root, then smaller / larger child of each
-      // scanned split); the stream is rewound below to the draws the tree actually used
+      // scanned split); the stream is rewound below to the draws the tree actually used. Under
+      // interaction constraints only the root's: the select draws the rest from its state on
       byn_state = col_sampler_.rng_state();
-      Tree dummy(2);
+      Tree dummy(2, true);  // (the root: no branch features; GetByNode reads them under constraints)
       uint8_t* bm = um + F_;
-      for (int r = 0; r < 2 * L_; ++r) {
+      const int rows = byn_dev ? 1 : 2 * L_;
+      for (int r = 0; r < rows; ++r) {
         auto m = col_sampler_.GetByNode(&dummy, 0);
         for (int f = 0; f < F_; ++f) bm[static_cast<size_t>(r) * F_ + f] = m[f] ? 1 : 0;
       }
-      HIP_CHECK(hipMemcpyAsync(bynode_.get(), bm, static_cast<size_t>(2 * L_) * F_, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipMemcpyAsync(bynode_.get(), bm, static_cast<size_t>(rows) * F_, hipMemcpyHostToDevice, stream_));
+      if (byn_dev) {
+        const unsigned st = col_sampler_.rng_state().state();
+        uint8_t* w = um + static_cast<size_t>(F_) * (1 + 2 * L_);
+        std::memcpy(w, &st, sizeof(st));
+        HIP_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(tparams_.get()) + offsetof(TreeParams, byn_rng), w, sizeof(st),
+                                 hipMemcpyHostToDevice, stream_));
+      }
     }
     SplitRec* hr = pin_rec_.Get(L_);
     LeafRange* hrange = pin_range_.Get(L_);
@@ -1647,7 +1662,9 @@ class DeviceTreeLearner : public TreeLearner {
     } else {
       SequentialGrow(&num_splits, &num_leaves, hr, hrange, hlo);
     }
-    if (use_bynode_) {
+    if (byn_dev) {
+      col_sampler_.set_rng_state(Random(static_cast<int>(bynode_rng_)));  // (the select's draws)
+    } else if (use_bynode_) {
       col_sampler_.set_rng_state(byn_state);
       Tree dummy(2);
       for (int r = 0; r < std::min(bynode_draws_, 2 * L_); ++r) (void)col_sampler_.GetByNode(&dummy, 0);
@@ -1707,13 +1724,16 @@ class DeviceTreeLearner : public TreeLearner {
     if (!FrontierSerial() && !FrontierDP() && !FrontierVoting() && !FrontierFeature()) return false;
     // extra trees: the single-device frontier (one expansion per round: FArgs::xrng)
     if (config_->extra_trees && !FrontierSerial()) return false;
-    // by-node sampling: the single-device frontier (masks in the host's draw order, FArgs::bynode)
-    if (use_bynode_ && (!FrontierSerial() || !config_->interaction_constraints_vector.empty())) return false;
+    // by-node sampling: the single-device frontier (masks in the host's draw order, FArgs::bynode;
+    // under interaction constraints drawn in the select, FArgs::byn_draw)
+    if (use_bynode_ && !FrontierSerial()) return false;
     return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, RawCands());
   }
   // per-node raw candidates of every feature (FArgs::cegb_raw): CEGB feature penalties, and
   // by-node sampling (a node is scored once its mask is known)
   bool RawCands() const { return CegbRaw() || use_bynode_; }
+  // by-node masks drawn in the select: each node's pool follows its interaction constraints
+  bool ByNodeOnDevice() const { return use_bynode_ && !config_->interaction_constraints_vector.empty(); }
   // CEGB feature penalties in the frontier select: coupled (FArgs::cegb_coupled: refunds on a
   // feature's first use) and lazy (FArgs::cegb_lazy: per-row marks, unmarked-row counts per
   // node). Either makes the scans publish raw gains (FArgs::cegb_raw).
@@ -1962,6 +1982,13 @@ class DeviceTreeLearner : public TreeLearner {
       facc_.Zero(stream_);
       facc_recv_.Resize(static_cast<size_t>(K) * bbin_ * 2);
     }
+    if (ByNodeOnDevice()) {
+      bool filt = false;
+      const std::vector<uint8_t> m = col_sampler_.ByNodeSampleModes(&fbyn_cnt_, &filt);
+      fbyn_reset_ = filt ? 1 : 0;
+      fbyn_mode_.Resize(m.size());
+      fbyn_mode_.Upload(m.data(), m.size(), stream_);
+    }
     fvoting_ = FrontierVoting();
     if (fvoting_) {
       // voting's local pass: min_data / min_hessian divided by the ranks (reference :61-63, integer division)
@@ -2177,6 +2204,10 @@ class DeviceTreeLearner : public TreeLearner {
     }
     a.sp = MakeArgs().sp;
     a.bynode = use_bynode_ ? bynode_.get() : nullptr;
+    a.byn_draw = frontier_ && ByNodeOnDevice() ? bynode_.get() : nullptr;
+    a.byn_mode = fbyn_mode_.size() ? fbyn_mode_.get() : nullptr;
+    a.byn_cnt = fbyn_cnt_;
+    a.byn_reset = fbyn_reset_;
     a.xrng = config_->extra_trees ? rng_.get() : nullptr;
     if (ffeature_ || fowner_) {
       a.fowned = ffowned_.get();
@@ -2528,6 +2559,7 @@ class DeviceTreeLearner : public TreeLearner {
     *num_splits = hs->num_splits;
     *num_leaves = hs->num_leaves;
     bynode_draws_ = hs->byn;
+    bynode_rng_ = hs->byn_rng;
     // (k_f_results already wrote the records, ranges, root output and flags with the state)
     if (*num_splits > 0) std::memcpy(hr, fres_host_ + FrontierResultRecOffset(), sizeof(SplitRec) * *num_splits);
     std::memcpy(hrange, fres_host_ + FrontierResultRangeOffset(L_), sizeof(LeafRange) * *num_leaves);
@@ -4251,6 +4283,9 @@ class DeviceTreeLearner : public TreeLearner {
   DevBuf<unsigned> fxep_, fxcnt_;
   DevBuf<FXConf> fxconf_;          // FArgs::xc
   DevBuf<SplitParams> fsp_local_;  // FArgs::sp_local (voting's local pass)
+  DevBuf<uint8_t> fbyn_mode_;      // FArgs::byn_mode (by-node draws in the select)
+  int fbyn_cnt_ = 0, fbyn_reset_ = 0;
+  unsigned bynode_rng_ = 0;        // the select's sampler state after the last tree (FState::byn_rng)
   int cached_gcount_ = -1, cached_gcount_local_ = -1;
   DevBuf<unsigned long long> tile_pub_;
   PinnedBuf<unsigned> pin_bar_;
@@ -4373,8 +4408,8 @@ bool LinearOnDevice(const Config* config, const Dataset* train, const std::strin
   return k + 1 <= kLinMaxM;
 }
 
-bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type) {
-  if (learner_type != "serial" || config->feature_fraction_bynode < 1.0 || config->extra_trees) return false;
+namespace {
+bool FrontierShapeFor(const Config* config, const Dataset* train, bool raw) {
   if (config->interaction_constraints_vector.size() > 64 * static_cast<size_t>(kFrontierIcWords)) return false;
   if (train == nullptr) return config->num_leaves <= 256;  // (no data yet: a conservative shape)
   int max_bin = 2, max_cat_bin = 1;
@@ -4383,9 +4418,20 @@ bool FrontierServes(const Config* config, const Dataset* train, const std::strin
     max_bin = std::max(max_bin, fi.num_bin);
     if (fi.bin_type == BinType::Categorical) max_cat_bin = std::max(max_cat_bin, fi.num_bin);
   }
-  const bool cegb_raw = !config->cegb_penalty_feature_coupled.empty() || !config->cegb_penalty_feature_lazy.empty();
   return FrontierShapeFits(std::max(2, config->num_leaves), train->num_total_bin(), train->num_features(), max_bin,
-                           max_cat_bin, cegb_raw);
+                           max_cat_bin, raw);
+}
+}  // namespace
+
+bool FrontierServes(const Config* config, const Dataset* train, const std::string& learner_type) {
+  if (learner_type != "serial" || config->feature_fraction_bynode < 1.0 || config->extra_trees) return false;
+  const bool cegb_raw = !config->cegb_penalty_feature_coupled.empty() || !config->cegb_penalty_feature_lazy.empty();
+  return FrontierShapeFor(config, train, cegb_raw);
+}
+
+bool FrontierServesByNode(const Config* config, const Dataset* train, const std::string& learner_type) {
+  if (learner_type != "serial" || config->extra_trees) return false;
+  return FrontierShapeFor(config, train, true);  // (by-node sampling keeps raw candidates)
 }
 
 namespace {

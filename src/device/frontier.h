@@ -140,6 +140,7 @@ struct FState {
   long long used_rows, waste_rows;  // (when done) rows partitioned by committed / uncommitted expansions
   int forced_next;  // next forced split to apply (-1: forced splits over or none)
   int byn;          // feature_fraction_bynode: masks drawn so far (the host's GetByNode calls)
+  unsigned byn_rng; // by-node draws in the select (FArgs::byn_draw): the column sampler's LCG state
 };
 
 // Arguments of the frontier kernels (device pointers into the learner's buffers).
@@ -278,6 +279,16 @@ struct FArgs {
   // stay raw per node (cegb_raw); a node's mask is known once its parent commits, so the
   // replay scores the children then, and only leaves of the committed tree are expanded.
   const uint8_t* bynode;
+  // by-node sampling under interaction constraints: a node's pool (the by-tree features its
+  // constraints allow) depends on its path, so the masks cannot be drawn ahead. The select draws
+  // rows 1.. itself when a split commits (smaller child first), Random::Sample over the pool with
+  // the column sampler's LCG (FState::byn_rng; the host draws the root's row 0 and takes the
+  // final state back), into byn_draw (== bynode). byn_mode[N]: Sample's branch for a pool of N
+  // (0 none, 1 all, 2 Bernoulli scan, 3 Floyd; host-computed: its log2 test stays the host's).
+  uint8_t* byn_draw;
+  const uint8_t* byn_mode;
+  int byn_cnt;    // GetCnt(by-tree feature count, feature_fraction_bynode)
+  int byn_reset;  // by-tree sampling on: the pool is filtered by used_bytree
   // extra_trees: per-feature random streams (Random(extra_seed + f), persistent across trees;
   // null: off). Draws follow the host's order (each scanned node: smaller child, then larger),
   // which the frontier keeps by expanding only the node the replay is blocked on: at its scan

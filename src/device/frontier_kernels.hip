@@ -240,6 +240,7 @@ __device__ __forceinline__ void FInitTree(const FArgs& a) {
     s.used_rows = s.waste_rows = 0;
     s.forced_next = a.num_forced > 0 ? 0 : -1;
     s.byn = a.bynode != nullptr ? 1 : 0;  // (the root's mask: row 0)
+    s.byn_rng = tp.byn_rng;
     *a.st = s;
     FNode r;
     r.buf = tp.root_buf;
@@ -1900,6 +1901,68 @@ __device__ __forceinline__ void CegbSetBest(const FArgs& a, int c, size_t src, d
   a.key[c].gain = g;
 }
 
+// By-node mask of node c under interaction constraints (FArgs::byn_draw; host ColSampler::GetByNode,
+// reference col_sampler.hpp:91-150): the pool is the features in ascending order that the by-tree
+// sample keeps and c's constraint sets allow; Random::Sample(N, K = min(byn_cnt, N)) picks pool
+// indices with the sampler's LCG. One lane draws (each step depends on the last), the wave counts
+// the pool and maps the picks back to features. s_pick: LDS scratch of F bytes. Called by a whole
+// wave; rng is wave-uniform.
+__device__ void FByNodeDraw(const FArgs& a, int c, uint8_t* mask, uint8_t* s_pick, unsigned* rng) {
+  const int lane = threadIdx.x & 63, F = a.F;
+  const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int N = 0;
+  for (int f0 = 0; f0 < F; f0 += 64) {
+    const int f = f0 + lane;
+    const bool in = f < F && (!a.byn_reset || a.used_bytree[f]) && FIcAllows(a, c, f);
+    N += __popcll(__ballot(in));
+  }
+  const int K = min(a.byn_cnt, N);
+  const int mode = a.byn_mode[N];
+  for (int i = lane; i < N; i += 64) s_pick[i] = mode == 1 ? 1 : 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  unsigned x = *rng;
+  if (lane == 0 && mode >= 2) {
+    if (mode == 2) {
+      // Bernoulli scan: row i kept with probability (K - kept so far) / (N - i)
+      int got = 0;
+      for (int i = 0; i < N; ++i) {
+        x = 214013u * x + 2531011u;
+        const float r = static_cast<float>(static_cast<int>((x >> 16) & 0x7FFFu)) / 32768.0f;
+        if (r < static_cast<double>(K - got) / static_cast<double>(N - i)) {
+          s_pick[i] = 1;
+          ++got;
+        }
+      }
+    } else {
+      // Floyd: v uniform in [0, r]; r itself when v was already taken
+      for (int r = N - K; r < N; ++r) {
+        x = 214013u * x + 2531011u;
+        const int v = static_cast<int>(x & 0x7FFFFFFFu) % (r + 1);
+        if (s_pick[v]) s_pick[r] = 1;
+        else s_pick[v] = 1;
+      }
+    }
+  }
+  *rng = static_cast<unsigned>(ReadLane(static_cast<int>(x), 0));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  int base = 0;
+  for (int f0 = 0; f0 < F; f0 += 64) {
+    const int f = f0 + lane;
+    const bool in = f < F && (!a.byn_reset || a.used_bytree[f]) && FIcAllows(a, c, f);
+    const unsigned long long b = __ballot(in);
+    if (f < F) mask[f] = in && s_pick[base + __popcll(b & lt)] ? 1 : 0;
+    base += __popcll(b);
+  }
+  // (the re-score's lanes read the mask back through the same cache)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 constexpr int kSelWaves = kFSelThreads / 64;
 constexpr int kSelPairs = 2 * kFrontierKmax / kSelWaves;  // (expansion, child) pairs per wave
 constexpr int kSelRankMax = 256;  // alive nodes up to which the select ranks instead of sorting
@@ -2222,10 +2285,12 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     __syncthreads();
   }
   __shared__ int s_byn;
+  __shared__ unsigned s_brng;
   if (w == 0) {
     int nl = st.num_leaves, ns = st.num_splits, done = 0, blocked = -1, nc = 0;
     int fnext = st.forced_next, bforced = 0;
     int byn = st.byn;  // bynode masks drawn (wave-uniform)
+    unsigned brng = st.byn_rng;  // (by-node draws in the select: the sampler's state, wave-uniform)
     unsigned epoch = epoch0;  // CEGB first-use events (wave-uniform)
     if (reg_replay) {
       // leaf l's (gain, feature, cid) in registers of lane l % 64, slot l / 64: per committed
@@ -2479,6 +2544,11 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
                             (gl < 2 * md && gr < 2 * md);
           if (!skip) {
             const bool left_smaller = gl < gr;
+            if (a.byn_draw != nullptr) {
+              // (interaction constraints: drawn here, over each child's own pool)
+              FByNodeDraw(a, left_smaller ? left : left + 1, a.byn_draw + static_cast<size_t>(byn) * F, s_used + F + 16, &brng);
+              FByNodeDraw(a, left_smaller ? left + 1 : left, a.byn_draw + static_cast<size_t>(byn + 1) * F, s_used + F + 16, &brng);
+            }
             cmask[left_smaller ? 0 : 1] = a.bynode + static_cast<size_t>(byn) * F;
             cmask[left_smaller ? 1 : 0] = a.bynode + static_cast<size_t>(byn + 1) * F;
             byn += 2;
@@ -2551,6 +2621,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       s_fnext = fnext;
       s_bforced = bforced;
       s_byn = byn;
+      s_brng = brng;
     }
   }
   __syncthreads();
@@ -2868,6 +2939,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     ns_.blocked = s_blocked;
     ns_.forced_next = s_fnext;
     ns_.byn = s_byn;
+    ns_.byn_rng = s_brng;
     if (!done) {
       ns_.k = s_k;
       ns_.total_tiles = s_tiles;
@@ -3568,7 +3640,7 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
   const size_t lds = FrontierSelectLds(a.C, a.L);
   const bool wide = a.F > 64 || (a.fpb != nullptr && a.vote_P > 64);
-  if (a.cegb_raw) k_f_select<true, false, false><<<1, kFSelThreads, lds + a.F + 16, s>>>(a);
+  if (a.cegb_raw) k_f_select<true, false, false><<<1, kFSelThreads, lds + (a.byn_draw != nullptr ? 2 : 1) * (a.F + 16), s>>>(a);
   else if (a.xg) wide ? k_f_select<false, true, true><<<1, kFSelThreads, lds, s>>>(a) : k_f_select<false, false, true><<<1, kFSelThreads, lds, s>>>(a);
   else if (wide) k_f_select<false, true, false><<<1, kFSelThreads, lds, s>>>(a);
   else k_f_select<false, false, false><<<1, kFSelThreads, lds, s>>>(a);

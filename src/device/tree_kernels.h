@@ -54,7 +54,8 @@ struct TreeParams {
   int cls;
   int root_gcount;  // global (all ranks) row count of the root
   float spec_alpha;  // frontier engine: speculation depth, fraction of the remaining budget (host-tuned per tree)
-  int pad[3];
+  unsigned byn_rng;  // frontier engine, by-node draws in the select (FArgs::byn_draw): the sampler's state after the root's
+  int pad[2];
 };
 
 struct Ctl {

@@ -106,6 +106,18 @@ std::vector<int8_t> ColSampler::GetByNode(const Tree* tree, int leaf) {
   return ret;
 }
 
+std::vector<uint8_t> ColSampler::ByNodeSampleModes(int* cnt, bool* filter_bytree) const {
+  *filter_bytree = need_reset_tree_;
+  *cnt = GetCnt(need_reset_tree_ ? static_cast<size_t>(used_cnt_tree_) : valid_.size(), frac_node_);
+  const int nf = data_->num_features();
+  std::vector<uint8_t> m(nf + 1);
+  for (int n = 0; n <= nf; ++n) {
+    const int k = std::min(*cnt, n);  // (GetByNode: min(cnt, pool size))
+    m[n] = static_cast<uint8_t>(k > n || k <= 0 ? 0 : (k == n ? 1 : (k > 1 && k > (n / std::log2(k)) ? 2 : 3)));
+  }
+  return m;
+}
+
 // ============================================================================
 // DataPartition
 void DataPartition::Init(data_size_t num_data, int num_leaves) {

@@ -29,6 +29,10 @@ class ColSampler {
   // rewinds to it and replays only the draws the tree used, so the stream stays the host's
   const Random& rng_state() const { return rand_; }
   void set_rng_state(const Random& r) { rand_ = r; }
+  // by-node masks drawn on the device (interaction constraints: each node's pool depends on its
+  // path): Random::Sample's branch for a pool of n = 0..num_features features (0 none, 1 all,
+  // 2 Bernoulli scan, 3 Floyd), the draw count, and whether the pool keeps only by-tree features
+  std::vector<uint8_t> ByNodeSampleModes(int* cnt, bool* filter_bytree) const;
 
  private:
   static int GetCnt(size_t total, double fraction);

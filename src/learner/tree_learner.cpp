@@ -71,9 +71,10 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {
     return "intermediate/advanced monotone constraints (device scans, host constraint walk)";
   }
-  // (more than 64 sets: the frontier's multi-word masks, up to 256; the sequential chain holds 64)
+  // (more than 64 sets: the frontier's multi-word masks, up to 256; the sequential chain holds 64.
+  // By-node sampling: the frontier's select draws each node's mask over its own allowed pool)
   if (!c->interaction_constraints_vector.empty() &&
-      (c->feature_fraction_bynode < 1.0 ||
+      ((c->feature_fraction_bynode < 1.0 && !device::FrontierServesByNode(c, train, learner_type)) ||
        (c->interaction_constraints_vector.size() > 64 && !device::FrontierServes(c, train, learner_type)))) {
     return "interaction constraints with by-node sampling / more than 64 sets off the frontier";
   }

@@ -1159,14 +1159,25 @@ def test_leaf_range_score_update_matches_predict(lgb, gpu_required, rng, extra):
     np.testing.assert_allclose(b._Booster__inner_predict(0), b.predict(X), rtol=0, atol=1e-9)
 
 
+_IC70 = [[(7 * i) % 12, (7 * i + 3) % 12, (5 * i + 1) % 12] for i in range(70)]
+
+
 @pytest.mark.parametrize("extra", [{"feature_fraction_bynode": 0.6},
                                    {"feature_fraction_bynode": 0.5, "feature_fraction": 0.8, "num_leaves": 31},
-                                   {"feature_fraction_bynode": 0.7, "max_depth": 3, "min_data_in_leaf": 50}])
+                                   {"feature_fraction_bynode": 0.7, "max_depth": 3, "min_data_in_leaf": 50},
+                                   {"feature_fraction_bynode": 0.6,
+                                    "interaction_constraints": [[0, 1, 2], [2, 3, 4, 5], [6, 7, 8, 9, 10, 11]]},
+                                   {"feature_fraction_bynode": 0.5, "feature_fraction": 0.8, "num_leaves": 31,
+                                    "interaction_constraints": [[0, 1], [1, 2, 3], [0, 4, 5, 6], [7, 8, 9, 10, 11]]},
+                                   {"feature_fraction_bynode": 0.3, "num_leaves": 31, "interaction_constraints": _IC70}],
+                         ids=["bynode", "bytree", "depth", "ic", "ic-bytree", "ic-70sets"])
 def test_bynode_sampling_on_frontier_matches_cpu(lgb, gpu_required, rng, extra):
     """feature_fraction_bynode on the frontier engine: the tree's masks in the host's draw order
     (root, then smaller / larger child of every scanned split), each child scored when its parent
     commits in the replay, and the sampler rewound to the draws the tree used, so every tree (not
-    only the first) equals the CPU learner's."""
+    only the first) equals the CPU learner's. Under interaction constraints each node's pool is the
+    features its sets allow, so the select draws the masks itself (Random::Sample's Bernoulli and
+    Floyd branches over the pool, the sampler's state handed back to the host after each tree)."""
     X = rng.standard_normal((30000, 12))
     z = X[:, 0] - 0.8 * X[:, 1] + 0.5 * X[:, 2] * X[:, 3] + 0.3 * X[:, 4] + 0.2 * rng.standard_normal(30000)
     y = (z > 0).astype(float)
