@@ -39,6 +39,9 @@ bool FrontierServes(const Config* config, const Dataset* train, const std::strin
 // The same for feature_fraction_bynode under interaction constraints: the frontier's select
 // draws each node's mask over the features its constraints allow (serial learner only).
 bool FrontierServesByNode(const Config* config, const Dataset* train, const std::string& learner_type);
+// intermediate monotone constraints in the serial frontier's select (FArgs::mono_inter): no by-node
+// sampling, extra trees, forced splits or CEGB, and the select's extra LDS fits
+bool FrontierServesMonoInter(const Config* config, const Dataset* train, const std::string& learner_type);
 // Whether the device learner fits linear_tree leaves itself (fp64 MFMA Gram systems): serial
 // learner, float gradients, raw values kept, and at most 30 branch features per leaf.
 bool LinearOnDevice(const Config* config, const Dataset* train, const std::string& learner_type);

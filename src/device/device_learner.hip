@@ -203,14 +203,16 @@ size_t FrontierScanLds(int max_bin, int max_cat_bin) {
 // capacity, and the scan's LDS. LGAP_FRONTIER=0 forces the sequential chain (A/B runs). The
 // learner factory routes with the same predicate (FrontierServes), so a configuration the
 // frontier cannot hold takes the host split policy instead of failing at allocation.
-bool FrontierShapeFits(int L, int TB, int F, int max_bin, int max_cat_bin, bool cegb_raw) {
+bool FrontierShapeFits(int L, int TB, int F, int max_bin, int max_cat_bin, bool cegb_raw, bool mono_inter) {
   const char* e = std::getenv("LGAP_FRONTIER");
   if (e != nullptr && e[0] == '0') return false;
   const int C = FrontierCapacityFor(std::max(2, L), TB);
   if (C > kFrontierMaxNodes || F <= 0) return false;
   if (FrontierScanLds(max_bin, max_cat_bin) > 150 * 1024) return false;
   // (raw candidates: the CEGB used-feature flags and the by-node draws' scratch, F bytes each)
-  return FrontierSelectLds(C, std::max(2, L)) + (cegb_raw ? 2 * (F + 16) : 0) <= 150 * 1024;
+  return FrontierSelectLds(C, std::max(2, L)) + (cegb_raw ? 2 * (F + 16) : 0) +
+             (mono_inter ? FrontierSelectMonoLds(C, std::max(2, L), F) : 0) <=
+         150 * 1024;
 }
 
 class DeviceTreeLearner : public TreeLearner {
@@ -1727,11 +1729,19 @@ class DeviceTreeLearner : public TreeLearner {
     // by-node sampling: the single-device frontier (masks in the host's draw order, FArgs::bynode;
     // under interaction constraints drawn in the select, FArgs::byn_draw)
     if (use_bynode_ && !FrontierSerial()) return false;
-    return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, RawCands());
+    if (MonoInter() && (!FrontierSerial() || RawCands() || config_->extra_trees || fnum_forced_ > 0 ||
+                        !config_->forcedsplits_filename.empty()))
+      return false;
+    return FrontierShapeFits(L_, TB_, F_, max_bin_, max_cat_bin_, RawCands(), MonoInter());
   }
   // per-node raw candidates of every feature (FArgs::cegb_raw): CEGB feature penalties, and
   // by-node sampling (a node is scored once its mask is known)
   bool RawCands() const { return CegbRaw() || use_bynode_; }
+  // intermediate monotone constraints in the frontier select (FArgs::mono_inter; the serial
+  // frontier only: TreeLearner::Create routes the other learners to the host policy)
+  bool MonoInter() const {
+    return !config_->monotone_constraints.empty() && config_->monotone_constraints_method == "intermediate";
+  }
   // by-node masks drawn in the select: each node's pool follows its interaction constraints
   bool ByNodeOnDevice() const { return use_bynode_ && !config_->interaction_constraints_vector.empty(); }
   // CEGB feature penalties in the frontier select: coupled (FArgs::cegb_coupled: refunds on a
@@ -1841,6 +1851,10 @@ class DeviceTreeLearner : public TreeLearner {
       // (TreeLearner::Create routes these by FrontierServes: reaching here is a routing bug)
       Log::Fatal("more than 64 interaction constraint sets on the device need the frontier engine");
     }
+    if (!frontier_ && MonoInter()) {
+      // (TreeLearner::Create routes these by FrontierServesMonoInter: reaching here is a routing bug)
+      Log::Fatal("intermediate monotone constraints on the device need the serial frontier engine");
+    }
     if (!frontier_ && CegbRaw()) {
       Log::Fatal("cegb_penalty_feature_coupled / _lazy on the device need the frontier engine (serial learner, "
                  "no feature_fraction_bynode / extra_trees, frontier LDS shape)");
@@ -1855,7 +1869,8 @@ class DeviceTreeLearner : public TreeLearner {
                  o_bounds = lay.Add<LeafBounds>(C), o_key = lay.Add<SplitKey>(C), o_best = lay.Add<SplitInfo>(C),
                  o_spl = lay.Add<uint8_t>(C * F), o_ic = lay.Add<unsigned long long>(C * kFrontierIcWords), o_nst = lay.Add<uint8_t>(C),
                  o_lcid = lay.Add<int>(L_), o_ckey = lay.Add<SplitKey>(K * 2 * F), o_cinfo = lay.Add<SplitInfo>(K * 2 * F),
-                 o_fbest = lay.Add<SplitInfo>(C), o_fkey = lay.Add<SplitKey>(C);
+                 o_fbest = lay.Add<SplitInfo>(C), o_fkey = lay.Add<SplitKey>(C),
+                 o_cbnd = lay.Add<LeafBounds>(MonoInter() ? C : 1);
     farena_.Resize(lay.bytes());
     farena_.Zero(stream_);
     char* b = farena_.get();
@@ -1876,6 +1891,7 @@ class DeviceTreeLearner : public TreeLearner {
     fcinfo_ = reinterpret_cast<SplitInfo*>(b + o_cinfo);
     ffbest_ = reinterpret_cast<SplitInfo*>(b + o_fbest);
     ffkey_ = reinterpret_cast<SplitKey*>(b + o_fkey);
+    fcbnd_ = MonoInter() ? reinterpret_cast<LeafBounds*>(b + o_cbnd) : nullptr;
     UploadForcedSplits();
     if (RawCands()) {
       fnkey_.Resize(C * F);
@@ -2136,6 +2152,8 @@ class DeviceTreeLearner : public TreeLearner {
     a.part_tile = fpart_tile_;
     a.max_depth = config_->max_depth;
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
+    a.mono_inter = fcbnd_ != nullptr ? 1 : 0;
+    a.cbnd = fcbnd_;
     a.monotone_penalty = config_->monotone_penalty;
     a.cegb_split = CegbPenalty::Enabled(config_) ? config_->cegb_tradeoff * config_->cegb_penalty_split : 0.0;
     a.max_bin = max_bin_;
@@ -2164,7 +2182,7 @@ class DeviceTreeLearner : public TreeLearner {
       // one wave per scan item on wide data (F >= 64, numerical features only)
       const bool fits = kFScanWaves * FrontierScanWaveBytes(max_bin_, cat_p2_) <= 150 * 1024;
       const char* sw = KernelOverride("scan_wave");  // coverage knob: the wave scan on narrow data
-      a.scan_wave = fits && !has_cat_ && (F_ >= 64 || (sw != nullptr && sw[0] == '1')) ? 1 : 0;
+      a.scan_wave = fits && !has_cat_ && !a.mono_inter && (F_ >= 64 || (sw != nullptr && sw[0] == '1')) ? 1 : 0;
       // (block scan grid cap: 512 blocks loop over a large round's items instead of 4096
       // mostly-idle blocks being dispatched every round; A/B 10M 2.850 vs 2.875, 1.25M 1.331 vs 1.341)
       a.scan_grid = 512;
@@ -2529,7 +2547,8 @@ class DeviceTreeLearner : public TreeLearner {
         if (fa_res.cegb_lazy != nullptr) LaunchFrontierLazyMark(fa_res, stream_);
         break;
       }
-      if (launched > L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
+      // (intermediate monotone: a split may wait on a round of rescans and one of expansion)
+      if (launched > (MonoInter() ? 3 : 1) * L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
       if (use_graph) {
         if (!fcont_) fcont_ = CaptureFrontier(kCont, false);
         HIP_CHECK(hipGraphLaunch(fcont_, stream_));
@@ -2684,6 +2703,7 @@ class DeviceTreeLearner : public TreeLearner {
   std::string DeviceName() const override {
     if (!owner_scan_ && !voting_) {
       if (!FrontierEligible()) return device_name_;
+      if (MonoInter()) return device_name_ + " [frontier engine, intermediate monotone walk + rescans]";
       return device_name_ + (QuantHist() ? " [frontier engine, int8-level histograms]" : " [frontier engine]");
     }
     return device_name_ + " [" + ParallelDesc() + "]";
@@ -3018,6 +3038,7 @@ class DeviceTreeLearner : public TreeLearner {
     std::memset(&st, 0, sizeof(st));
     st.round = 1;
     st.k = k;
+    st.kx = k;
     st.num_leaves = 1;
     std::vector<FExp> ex(k);
     for (int e = 0; e < k; ++e) {
@@ -3130,6 +3151,7 @@ class DeviceTreeLearner : public TreeLearner {
     if (tiles > ftile_cap_) Log::Fatal("TestFrontierPartition: %d tiles (capacity %d)", tiles, ftile_cap_);
     st.round = 1;
     st.k = k;
+    st.kx = k;
     st.total_tiles = tiles;
     st.done = 0;
     st.epoch = st.epoch + 1u;
@@ -4096,6 +4118,7 @@ class DeviceTreeLearner : public TreeLearner {
   double2* flsum_ = nullptr;
   double* flout_ = nullptr;
   LeafBounds* fbounds_ = nullptr;
+  LeafBounds* fcbnd_ = nullptr;  // intermediate monotone: the committed leaves' current bounds
   SplitKey* fkey_ = nullptr;
   SplitInfo* fbest_ = nullptr;
   uint8_t* fspl_ = nullptr;
@@ -4409,7 +4432,7 @@ bool LinearOnDevice(const Config* config, const Dataset* train, const std::strin
 }
 
 namespace {
-bool FrontierShapeFor(const Config* config, const Dataset* train, bool raw) {
+bool FrontierShapeFor(const Config* config, const Dataset* train, bool raw, bool mono_inter = false) {
   if (config->interaction_constraints_vector.size() > 64 * static_cast<size_t>(kFrontierIcWords)) return false;
   if (train == nullptr) return config->num_leaves <= 256;  // (no data yet: a conservative shape)
   int max_bin = 2, max_cat_bin = 1;
@@ -4419,7 +4442,7 @@ bool FrontierShapeFor(const Config* config, const Dataset* train, bool raw) {
     if (fi.bin_type == BinType::Categorical) max_cat_bin = std::max(max_cat_bin, fi.num_bin);
   }
   return FrontierShapeFits(std::max(2, config->num_leaves), train->num_total_bin(), train->num_features(), max_bin,
-                           max_cat_bin, raw);
+                           max_cat_bin, raw, mono_inter);
 }
 }  // namespace
 
@@ -4427,6 +4450,13 @@ bool FrontierServes(const Config* config, const Dataset* train, const std::strin
   if (learner_type != "serial" || config->feature_fraction_bynode < 1.0 || config->extra_trees) return false;
   const bool cegb_raw = !config->cegb_penalty_feature_coupled.empty() || !config->cegb_penalty_feature_lazy.empty();
   return FrontierShapeFor(config, train, cegb_raw);
+}
+
+bool FrontierServesMonoInter(const Config* config, const Dataset* train, const std::string& learner_type) {
+  if (learner_type != "serial" || config->feature_fraction_bynode < 1.0 || config->extra_trees) return false;
+  if (!config->forcedsplits_filename.empty() || CegbPenalty::Enabled(config)) return false;
+  if (config->monotone_constraints_method != "intermediate") return false;
+  return FrontierShapeFor(config, train, false, true);
 }
 
 bool FrontierServesByNode(const Config* config, const Dataset* train, const std::string& learner_type) {

@@ -86,6 +86,7 @@ __host__ __device__ inline int FrontierDepthBuf(int j) { return j < 2 ? j : j + 
 constexpr uint8_t kNodeExpanded = 1;   // children computed
 constexpr uint8_t kNodeCommitted = 2;  // its split is part of the tree (replay)
 constexpr uint8_t kNodeDead = 4;       // below an expansion the CEGB replay invalidated: never used
+constexpr uint8_t kNodeStale = 0x40;   // (select-local) intermediate monotone: record scanned under looser bounds
 // stamp slots: kernel ids and the per-kernel slot count (slot 7: latest block exit)
 constexpr int kFStampPart = 0, kFStampHist = 1, kFStampScan = 2, kFStampSel = 3, kFStampSlots = 8;
 
@@ -125,11 +126,14 @@ struct FExp {
   int feature;               // inner feature of the split (-1: the root pseudo-expansion)
   int last;                  // the tree's last split (the node the replay waits for, at num_leaves - 1
                              // leaves): its children are never scanned (as in the host's loop)
+  int rescan;                // intermediate monotone: no split, node `smaller` is re-scanned from its slot
+                             // under its tightened bounds (no tiles, no rows)
 };
 
 struct FState {
   int round;        // rounds run (including the root round)
-  int k;            // expansions of the current round
+  int k;            // expansions of the current round (rescans included)
+  int kx;           // of which split a node (children cids [cid_next - 2 kx, cid_next)); the rest rescans
   int total_tiles;  // partition tiles of the current round
   int done;
   unsigned epoch;   // never reset: tags the partition's published tile counts
@@ -222,6 +226,11 @@ struct FArgs {
   int hist_nib;       // rowbins / stride_dw / tiles describe 4-bit rows (8 groups per dword)
   int part_tile;  // rows per partition tile (256 x rows per thread)
   int max_depth, use_monotone;
+  // intermediate monotone constraints (monotone_constraints_method=intermediate): the select keeps
+  // each leaf's current bounds (cbnd), tightens them with the host's constraint walk as splits
+  // commit, and re-scans leaves whose bounds moved past the ones their record was scanned with
+  int mono_inter;
+  LeafBounds* cbnd;  // [C] current bounds of the committed tree's leaves (by cid)
   double monotone_penalty;
   double cegb_split;  // cegb_tradeoff * cegb_penalty_split (per row of the node), 0: none
   // CEGB coupled feature penalties (cegb_penalty_feature_coupled) on the device, host
@@ -368,6 +377,12 @@ __host__ __device__ inline size_t FrontierScanWaveBytes(int max_bin, int cat_p2)
   return (b + 15) & ~static_cast<size_t>(15);
 }
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
+// extra LDS of the intermediate-monotone select (after FrontierSelectLds): per-leaf current and
+// scan bounds, per-node thresholds, the committed node's ancestor levels, per-feature monotone types
+__host__ __device__ inline size_t FrontierSelectMonoLds(int C, int L, int F) {
+  return 16 + static_cast<size_t>(L) * (2 * 16 + 3 * sizeof(int) + 1) + static_cast<size_t>(C) * sizeof(int) +
+         static_cast<size_t>(F) + 16;
+}
 // CEGB lazy penalties: unmarked-row counts of the round's smaller children; after a tree, the
 // final leaves' rows marked for the features on their paths
 void LaunchFrontierLazyCounts(const FArgs& a, hipStream_t s);

@@ -229,6 +229,7 @@ __device__ __forceinline__ void FInitTree(const FArgs& a) {
     FState s;
     s.round = 0;
     s.k = 1;
+    s.kx = 1;
     s.total_tiles = 0;
     s.done = 0;
     s.epoch = a.st->epoch + 1u;
@@ -271,8 +272,10 @@ __device__ __forceinline__ void FInitTree(const FArgs& a) {
     x.forced = -1;
     x.feature = -1;
     x.last = 0;
+    x.rescan = 0;
     a.exps[0] = x;
     a.bounds[0] = LeafBounds();
+    if (a.cbnd) a.cbnd[0] = LeafBounds();
     if (a.ic) {
       for (int w = 0; w < a.ic_words; ++w) a.ic[w] = ~0ull;
     }
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
   const int f_pre = a.fown_list != nullptr ? (NF > 0 ? a.fown_list[static_cast<int>(blockIdx.x) % NF] : 0)
                                            : static_cast<int>(blockIdx.x) % F;
   const int pre_skip = a.exps[e_pre].skip, pre_cs = a.exps[e_pre].smaller, pre_cl = a.exps[e_pre].larger,
-            pre_p = a.exps[e_pre].parent;
+            pre_p = a.exps[e_pre].parent, pre_rs = EXT ? a.exps[e_pre].rescan : 0;
   const DevFeature fi_pre = a.feat[f_pre];
   int EG, EH;
   GlobalScaleExp(a, &EG, &EH);
@@ -943,6 +946,8 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     const int x_skip = first ? pre_skip : a.exps[e].skip;
     const int x_cs = first ? pre_cs : a.exps[e].smaller, x_cl = first ? pre_cl : a.exps[e].larger;
     const int x_p = first ? pre_p : a.exps[e].parent;
+    // (intermediate monotone: a re-scan of node x_cs from its slot, no accumulator)
+    const bool rescan = EXT && (first ? pre_rs : a.exps[e].rescan) != 0;
     if (x_skip) {
       continue;
     }
@@ -965,7 +970,18 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
     double pre_out = 0.0;
     int pre_fidx = -1;
     LeafBounds pre_bounds;
-    if (lane == 0 && my >= 0) {
+    if (lane == 0 && my >= 0 && rescan) {
+      // host RecomputeBestSplit (reference serial_tree_learner.cpp RecomputeBestSplitForLeaf):
+      // the leaf's statistics from its pending best split, parent output 0 unless path smoothing
+      const SplitInfo& bi = a.best[my];
+      pre_sum = make_double2(bi.left_sum_gradient + bi.right_sum_gradient, bi.left_sum_hessian + bi.right_sum_hessian);
+      pre_n = bi.left_count + bi.right_count;
+      pre_depth = a.nodes[my].depth;
+      SplitParams p0 = a.sp;
+      p0.path_smooth = 0.0;
+      pre_out = a.sp.path_smooth > kEpsilon ? LeafOutputRaw(pre_sum.x, pre_sum.y, p0, pre_n, 0.0) : 0.0;
+      pre_bounds = a.bounds[my];
+    } else if (lane == 0 && my >= 0) {
       pre_sum = a.lsum[my];
       pre_n = a.nodes[my].gcount;
       pre_depth = a.nodes[my].depth;
@@ -998,6 +1014,13 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
       splp_v = p >= 0 && !voting ? a.spl[static_cast<size_t>(p) * F + f] : 1;
     }
     for (int kk = t; kk < nbin - 1; kk += blockDim.x) {
+      if (rescan) {
+        // (the node's stored bins, as its first scan left them)
+        const int b = kk < fi.mfb ? kk : kk + 1;
+        hs_full[2 * b] = gs[2 * kk];
+        hs_full[2 * b + 1] = gs[2 * kk + 1];
+        continue;
+      }
       const bool sys = EXT && a.xg && a.own;  // (the receive chunk the ranks pushed into)
       const unsigned long long x0 = sys ? FXLoad64(acc + pw * kk) : acc[pw * kk];
       const unsigned long long x1 = qpack ? 0ull : (sys ? FXLoad64(acc + 2 * kk + 1) : acc[2 * kk + 1]);
@@ -1130,7 +1153,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
                                     ckey + w * a.cat_p2, out);
         }
         if (lane == 0) {
-          a.spl[static_cast<size_t>(my) * F + f] = spl ? 1 : 0;
+          if (!rescan) a.spl[static_cast<size_t>(my) * F + f] = spl ? 1 : 0;  // (a re-scan keeps the flags)
           // (children of forced splits are scanned past max_depth: no regular split there)
           if (!spl || (a.max_depth > 0 && depth >= a.max_depth)) {
             out->Reset();
@@ -1147,7 +1170,7 @@ __global__ __launch_bounds__(kFScanThreads) void k_f_scan(FArgs a) {
             if (a.ic && !voting && !FIcAllows(a, my, f)) out->Reset();
           }
         }
-      } else if (lane == 0) {
+      } else if (lane == 0 && !rescan) {
         // feature not tried: the children inherit the parent's flag
         a.spl[static_cast<size_t>(my) * F + f] = static_cast<uint8_t>(s_splp);
       }
@@ -1643,7 +1666,17 @@ __device__ void FPostSplit(const FArgs& a, int e, const FExp& x, int lc) {
   a.lout[l] = lo;
   a.lout[r] = ro;
   LeafBounds br = bl;
-  if (a.use_monotone && ncat == 0) {
+  if (a.use_monotone && ncat == 0 && a.mono_inter) {
+    // intermediate: the siblings bound each other by their actual outputs (host
+    // MonotoneLeafConstraints::AfterSplit; reference monotone_constraints.hpp:560-574)
+    if (mono < 0) {
+      bl.min = fmax(bl.min, ro);
+      br.max = fmin(br.max, lo);
+    } else if (mono > 0) {
+      bl.max = fmin(bl.max, ro);
+      br.min = fmax(br.min, lo);
+    }
+  } else if (a.use_monotone && ncat == 0) {
     const double mid = (lo + ro) / 2.0f;
     if (mono < 0) {
       bl.min = fmax(bl.min, mid);
@@ -1963,6 +1996,173 @@ __device__ void FByNodeDraw(const FArgs& a, int c, uint8_t* mask, uint8_t* s_pic
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// ---------------------------------------------------------------------------
+// Intermediate monotone constraints in the select (host MonotoneLeafConstraints, reference
+// monotone_constraints.hpp:516-857 IntermediateLeafConstraints). Each leaf of the committed tree
+// carries its CURRENT bounds (cb) and the bounds its best split was scanned with (sb). A commit
+// bounds the two children by each other's outputs and walks the committed tree: climbing from the
+// split node, every numerical monotone ancestor that borders it (the first of its (feature, side)
+// on the way up) bounds the leaves on its far side that can touch the new leaves. Bounds only
+// tighten, and a tighter bound never raises a split's gain (the clamped outputs move away from
+// the optimum; the order check cannot newly pass: both children clamp into one interval), so a
+// STALE leaf's recorded gain is an upper bound of its re-scan: the replay commits a clean leaf
+// only when no stale leaf's bound reaches its gain, otherwise it stops and the stale leaves are
+// re-scanned from their slots (FExp::rescan) in the next round.
+struct FMonoLds {
+  double2* cb = nullptr;   // [L] current bounds (min, max) of each leaf
+  double2* sb = nullptr;   // [L] the bounds its record was scanned with
+  int* thr = nullptr;      // [C] split threshold bin | is_cat << 31
+  int* ancd = nullptr;     // [L] ancestors of the committed node, by depth
+  int* lvf = nullptr;      // [L] climb level: split feature (-1: categorical)
+  int* lvt = nullptr;      // [L] climb level: threshold | 1 << 28 borders | 1 << 29 monotone | 1 << 30 decreasing
+  uint8_t* lvs = nullptr;  // [L] climb level: 1 = reached from the right child
+  int8_t* mono = nullptr;  // [F] monotone type of each feature
+};
+constexpr int kMonoBorder = 1 << 28, kMonoMono = 1 << 29, kMonoDec = 1 << 30, kMonoThr = (1 << 28) - 1;
+
+__device__ __forceinline__ bool FMonoStale(const FMonoLds& mo, int l) {
+  const double2 cb = mo.cb[l], sb = mo.sb[l];
+  return cb.x > sb.x || cb.y < sb.y;
+}
+
+// Wave 0 after committing node c's split (leaf bl keeps the left child `left`, the right child is
+// the new leaf nl - 1): host MonotoneLeafConstraints::AfterSplit (Climb / Descend)
+__device__ void FMonoCommit(const FArgs& a, const FMonoLds& mo, const int* s_par, const int* s_left, const int* s_feat,
+                            const int* s_dep, const int* s_lcid, const double* s_lg, int c, int left, int bl, int nl) {
+  const int lane = threadIdx.x & 63;
+  const SplitInfo& bi = a.best[c];
+  const double lo = bi.left_output, ro = bi.right_output;
+  const int mt = bi.monotone_type;
+  const LeafBounds sbl = a.bounds[left], sbr = a.bounds[left + 1];
+  const int cthr = mo.thr[c];
+  const int sf = s_feat[c];
+  const uint32_t sthr = static_cast<uint32_t>(cthr & 0x7fffffff);
+  const int D = s_dep[c];
+  const int nr = nl - 1;
+  {
+    // the children: the parent's current bounds, the siblings bounding each other by their outputs
+    const double2 pb = mo.cb[bl];
+    double2 lc = pb, rc = pb;
+    if (cthr >= 0 && mt != 0) {
+      if (mt < 0) {
+        lc.x = fmax(lc.x, ro);
+        rc.y = fmin(rc.y, lo);
+      } else {
+        lc.y = fmin(lc.y, ro);
+        rc.x = fmax(rc.x, lo);
+      }
+    }
+    FWaveSync();
+    if (lane == 0) {
+      mo.cb[bl] = lc;
+      mo.cb[nr] = rc;
+      mo.sb[bl] = make_double2(sbl.min, sbl.max);
+      mo.sb[nr] = make_double2(sbr.min, sbr.max);
+      int x = c;
+      for (int d = D - 1; d >= 0; --d) {  // the ancestors by depth
+        x = s_par[x];
+        mo.ancd[d] = x;
+      }
+    }
+  }
+  FWaveSync();
+  if (D == 0) return;
+  // climb level i: ancestor ancd[D - 1 - i], reached from ancd[D - i] (level 0: from c)
+  for (int i = lane; i < D; i += 64) {
+    const int P = mo.ancd[D - 1 - i];
+    const int node = i == 0 ? c : mo.ancd[D - i];
+    const int th = mo.thr[P];
+    mo.lvf[i] = th >= 0 ? s_feat[P] : -1;
+    mo.lvt[i] = th & kMonoThr;
+    mo.lvs[i] = s_left[P] + 1 == node ? 1 : 0;
+  }
+  FWaveSync();
+  // a level borders the new leaves when no lower level split on the same feature from the same
+  // side (those are the path entries the host pushes); bordering numerical monotone ones descend
+  bool any = false;
+  for (int i = lane; i < D; i += 64) {
+    const int f = mo.lvf[i];
+    const uint8_t side = mo.lvs[i];
+    bool border = f >= 0;
+    for (int j = 0; j < i && border; ++j) border = !(mo.lvf[j] == f && mo.lvs[j] == side);
+    if (border) {
+      int v = kMonoBorder;
+      const int m = mo.mono[f];
+      if (m != 0) {
+        v |= kMonoMono | (m < 0 ? kMonoDec : 0);
+        any = true;
+      }
+      mo.lvt[i] |= v;
+    }
+  }
+  if (__ballot(any) == 0ull) return;
+  FWaveSync();
+  for (int l = lane; l < nl; l += 64) {
+    if (l == bl || l == nr || !(s_lg[l] > kMinScore)) continue;  // (host: best gain kMinScore, no update)
+    const int x = s_lcid[l];
+    // the level where x's path meets c's (their lowest common ancestor)
+    int y = x, d = s_dep[x], lam = -1;
+    while (d > 0) {
+      y = s_par[y];
+      --d;
+      if (d < D && mo.ancd[d] == y) {
+        lam = D - 1 - d;
+        break;
+      }
+    }
+    if (lam < 0) continue;
+    const int lt = mo.lvt[lam];
+    if (!(lt & kMonoMono)) continue;
+    // Descend from the far child to x: every node on the way must let the path through (Borders
+    // against the entries below the level), and splits on the new split's feature decide which
+    // of the two new outputs x borders
+    bool use_l = true, use_r = true, reach = true;
+    int ch = x, yy = s_par[x];
+    while (yy != y && reach) {
+      const bool right = s_left[yy] + 1 == ch;
+      const int th = mo.thr[yy];
+      if (th >= 0) {
+        const int fy = s_feat[yy];
+        const uint32_t ty = static_cast<uint32_t>(th);
+        for (int j = 0; j < lam; ++j) {
+          const int tj = mo.lvt[j];
+          if (mo.lvf[j] != fy || !(tj & kMonoBorder)) continue;
+          const uint32_t tv = static_cast<uint32_t>(tj & kMonoThr);
+          const bool sj = mo.lvs[j] != 0;
+          if (right && !sj && ty >= tv) reach = false;
+          if (!right && sj && ty <= tv) reach = false;
+        }
+        if (fy == sf) {
+          if (!right && ty <= sthr) use_r = false;
+          if (right && ty >= sthr) use_l = false;
+        }
+      }
+      ch = yy;
+      yy = s_par[yy];
+    }
+    if (!reach) continue;
+    const bool from_right = mo.lvs[lam] != 0;
+    const bool tmax = (lt & kMonoDec) ? !from_right : from_right;
+    double vlo, vhi;
+    if (use_l && use_r) {
+      vlo = fmin(lo, ro);
+      vhi = fmax(lo, ro);
+    } else if (use_r) {
+      vlo = vhi = ro;
+    } else {
+      vlo = vhi = lo;
+    }
+    double2 cb = mo.cb[l];
+    if (tmax) {
+      if (vlo < cb.y) cb.y = vlo;
+    } else {
+      if (vhi > cb.x) cb.x = vhi;
+    }
+    mo.cb[l] = cb;
+  }
+  FWaveSync();
+}
+
 constexpr int kSelWaves = kFSelThreads / 64;
 constexpr int kSelPairs = 2 * kFrontierKmax / kSelWaves;  // (expansion, child) pairs per wave
 constexpr int kSelRankMax = 256;  // alive nodes up to which the select ranks instead of sorting
@@ -1971,7 +2171,8 @@ constexpr int kSelLPer = 4;       // leaves per lane of the register replay (L <
 // kWide: more than 64 features (phase A loads two feature chunks per round of loads: its own
 // instantiation, so the headline's select keeps its register allocation)
 // kXg: the xGMI transport's push / handshake / system-scope merge (its own instantiations)
-template <bool kCegb, bool kWide, bool kXg>
+// kMono: intermediate monotone constraints (FArgs::mono_inter; FMonoCommit below)
+template <bool kCegb, bool kWide, bool kXg, bool kMono>
 __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int C = a.C, L = a.L, F = a.F;
@@ -1986,10 +2187,25 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   int* s_c0 = s_lcid + L;                                    // [L] committed leaves of this launch
   int* s_c1 = s_c0 + L;                                      // [L] their cids (~cid: a forced split)
   uint8_t* s_st = reinterpret_cast<uint8_t*>(s_c1 + L);      // [C]
+  // intermediate monotone (kMono): after the common image (FrontierSelectMonoLds)
+  FMonoLds mo;
+  if (kMono) {
+    const size_t o = (FrontierSelectLds(C, L) + 15) & ~static_cast<size_t>(15);
+    mo.cb = reinterpret_cast<double2*>(smem + o);
+    mo.sb = mo.cb + L;
+    mo.thr = reinterpret_cast<int*>(mo.sb + L);
+    mo.ancd = mo.thr + C;
+    mo.lvf = mo.ancd + L;
+    mo.lvt = mo.lvf + L;
+    mo.lvs = reinterpret_cast<uint8_t*>(mo.lvt + L);
+    mo.mono = reinterpret_cast<int8_t*>(mo.lvs + L);
+  }
   __shared__ int s_cpos[2 * kFrontierKmax];  // this round's children: winning candidate position
   __shared__ int s_pc[2 * kFrontierKmax];    // pair -> child cid (-1: none / skipped)
   __shared__ int s_nl, s_ns, s_done, s_blocked, s_ncommit, s_k, s_tiles, s_fnext, s_bforced;
   __shared__ int s_exp[kFrontierKmax];       // chosen expansions (cids) by order
+  __shared__ int s_rsc[kMono ? kFrontierKmax : 1], s_rsl[kMono ? kFrontierKmax : 1];  // (kMono) stale leaves: cid, leaf
+  __shared__ int s_nrs, s_nr;  // (kMono) stale leaves listed, rescans taken
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
   const unsigned xep = kXg ? *a.xc->ep : 0u;  // (xGMI: this round's tag is xep + 1)
@@ -1999,8 +2215,9 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   const int np = 2 * kprev;
   const int rnd = st.round;
   FStamp(a, rnd, kFStampSel, 0);
-  // this round's children are cids [base, base + 2 kprev) (the root round: cid 0)
-  const int base = cid_next - 2 * kprev;
+  // this round's children are cids [base, base + 2 kx) (the root round: cid 0); pairs of the
+  // intermediate-monotone rescans after them name older cids
+  const int base = cid_next - 2 * st.kx;
   // ---- image of the computed nodes + the pairs of the last round (one load round)
   for (int c = t; c < cid_next; c += blockDim.x) {
     const SplitKey& kk = a.key[c];
@@ -2015,6 +2232,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     s_feat[c] = kf;
     s_rank[c] = -1;
     s_fidx[c] = nd.fidx;
+    if (kMono) mo.thr[c] = static_cast<int>(kk.threshold & 0x7fffffffu) | (kk.is_cat ? static_cast<int>(0x80000000u) : 0);
+  }
+  if (kMono) {
+    for (int f = t; f < F; f += blockDim.x) mo.mono[f] = a.feat[f].monotone;
   }
   for (int l = t; l < st.num_leaves; l += blockDim.x) s_lcid[l] = a.leaf_cid[l];
   // CEGB coupled penalties: used-feature flags (after the sort scratch) and the event count
@@ -2248,7 +2469,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         s_feat[c] = valid ? ff : -1;
         // (CEGB: the penalised best lives in best / key only)
         // (merged ranks' records: the next expansions read best / key, written above)
-        s_cpos[c - base] = valid && !cegb && !merge ? static_cast<int>(static_cast<size_t>(q) * F + fpos) : -1;
+        // (a rescan's pair names an older cid: its record is read back from best / key)
+        if (!kMono || (c >= base && c - base < 2 * kFrontierKmax)) {
+          s_cpos[c - base] = valid && !cegb && !merge ? static_cast<int>(static_cast<size_t>(q) * F + fpos) : -1;
+        }
       }
     }
   }
@@ -2274,13 +2498,18 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
                                                     reinterpret_cast<uintptr_t>(smem) + 15) & ~uintptr_t(15)));  // [P2max]
   int* s_sc = reinterpret_cast<int*>(s_sg + FrontierSortCap(C));      // [P2max]
   // (the register replay below reads the leaves' keys itself: no LDS image, no barrier)
-  const bool reg_replay = !cegb && st.forced_next < 0 && L <= 64 * kSelLPer;
+  const bool reg_replay = !cegb && !kMono && st.forced_next < 0 && L <= 64 * kSelLPer;
   if (!reg_replay) {
     for (int l = t; l < st.num_leaves; l += blockDim.x) {
       const int c = s_lcid[l];
       const int f = s_feat[c];
       s_lg[l] = f < 0 ? kMinScore : s_gain[c];
       s_lf[l] = f < 0 ? 0x7fffffff : f;
+      if (kMono) {
+        const LeafBounds cb = a.cbnd[c], sb = a.bounds[c];
+        mo.cb[l] = make_double2(cb.min, cb.max);
+        mo.sb[l] = make_double2(sb.min, sb.max);
+      }
     }
     __syncthreads();
   }
@@ -2428,6 +2657,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       }
       double bg = kMinScore;
       int bf = 0x7fffffff, bl = 0x7fffffff;
+      double sgm = -INFINITY;  // (kMono) the largest gain bound among stale leaves
       for (int l = lane; l < nl; l += 64) {
         const double g = s_lg[l];
         const int ff = s_lf[l];
@@ -2436,6 +2666,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
           bf = ff;
           bl = l;
         }
+        if (kMono && g > 0.0 && FMonoStale(mo, l)) sgm = fmax(sgm, g);
       }
       const double mg = WaveMaxDpp(bg);
       const unsigned long long tie = __ballot(bg == mg);
@@ -2448,6 +2679,15 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       if (bl == 0x7fffffff || bf == 0x7fffffff || !(bg > 0.0)) {
         done = 1;
         break;
+      }
+      // (kMono: a stale leaf may still beat the best: its re-scan decides; ties included, as the
+      // re-scanned record may win the feature / leaf tie-break. With max_delta_step or path
+      // smoothing the raw output can sit beyond a bound on the optimum's side, a tighter bound
+      // may then RAISE the gain: every stale leaf is re-scanned before the next commit)
+      if (kMono) {
+        const double sm = WaveMaxDpp(sgm);
+        const bool ub = !(a.sp.max_delta_step > 0.0) && !(a.sp.path_smooth > kEpsilon);
+        if (ub ? sm >= bg : sm > -INFINITY) break;
       }
       const int c = s_lcid[bl];
       const int left = s_left[c];
@@ -2611,6 +2851,36 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (kMono) FMonoCommit(a, mo, s_par, s_left, s_feat, s_dep, s_lcid, s_lg, c, left, bl, nl);
+    }
+    if (kMono) {
+      // stale leaves -> this round's rescans (phase D), marked ineligible for expansion; every
+      // leaf's current bounds back to the node table for the next select
+      const unsigned long long ltm = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+      int cnt = 0;
+      for (int l0 = 0; l0 < nl; l0 += 64) {
+        const int l = l0 + lane;
+        bool stl = false;
+        int x = -1;
+        if (l < nl) {
+          x = s_lcid[l];
+          const double2 cb = mo.cb[l];
+          LeafBounds lb;
+          lb.min = cb.x;
+          lb.max = cb.y;
+          a.cbnd[x] = lb;
+          stl = s_lg[l] > 0.0 && FMonoStale(mo, l);
+          if (stl) s_st[x] = static_cast<uint8_t>(s_st[x] | kNodeStale);
+        }
+        const unsigned long long m = __ballot(stl);
+        const int pos = cnt + __popcll(m & ltm);
+        if (stl && pos < kFrontierKmax) {
+          s_rsc[pos] = x;
+          s_rsl[pos] = l;
+        }
+        cnt += __popcll(m);
+      }
+      if (lane == 0) s_nrs = min(cnt, kFrontierKmax);
     }
     if (lane == 0) {
       s_nl = nl;
@@ -2669,6 +2939,9 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         // extra trees: only the node the replay waits for (its children's random thresholds are
         // drawn when every earlier split of the sequential order has been scanned)
         if (elig && a.xrng != nullptr && c != s_blocked) elig = false;
+        // intermediate monotone: only leaves of the committed tree (a node's bounds are known once
+        // its parent commits), and not while its record is stale (it is re-scanned instead)
+        if (kMono && elig && ((sc & kNodeStale) || (s_par[c] >= 0 && !(s_st[s_par[c]] & kNodeCommitted)))) elig = false;
         if (elig) {
           const int target = s_dep[c] + 1 - kFrontierBufs;
           if (target >= 1) {
@@ -2736,6 +3009,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         int lim = a.policy == 0 ? min(min(a.kmax, max(1, R - s_eu + a.spec_cap)), min(max(1, cap_nodes), s_ne))
                                 : min(a.kmax, max(1, cap_nodes));
         if (a.kcap != nullptr && rnd + 1 < kFrontierRoundCap) lim = min(lim, max(1, a.kcap[rnd + 1]));
+        if (kMono) lim = min(lim, max(1, a.kmax - min(s_nrs, a.kmax / 2)));  // (room for the rescans)
         int kk = 0;
         if (rc >= 0) {
           const int rr = rc == blocked ? 0 : ex + (blocked >= 0 ? 1 : 0);
@@ -2849,6 +3123,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
                             : min(a.kmax, max(1, cap_nodes));
     // data-parallel: the round's all-reduce covers only kcap[round] expansions
     if (a.kcap != nullptr && rnd + 1 < kFrontierRoundCap) lim = min(lim, max(1, a.kcap[rnd + 1]));
+    if (kMono) lim = min(lim, max(1, a.kmax - min(s_nrs, a.kmax / 2)));  // (room for the rescans)
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int p = t * kPer + q;
@@ -2869,9 +3144,15 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     // (the node capacity bounds the round: expansions voided by CEGB first-use events leave
     // dead cids behind, so the reserve for the remaining splits is not a guarantee then)
     int K = min(s_k, (C - cid_next) / 2);
-    if (K <= 0) done = 1;  // nothing can be expanded: (only reachable without a blocked node)
+    // (kMono: the stale leaves' rescans fill the slots the expansions leave)
+    const int NR = kMono ? max(0, min(s_nrs, a.kmax - max(K, 0))) : 0;
+    if (K <= 0 && NR == 0) done = 1;  // nothing can be expanded: (only reachable without a blocked node)
+    K = max(K, 0);
     __syncthreads();
-    if (t == 0) s_k = K > 0 ? K : 0;
+    if (t == 0) {
+      s_k = K;
+      s_nr = NR;
+    }
     if (a.kused != nullptr && t == 0 && rnd + 1 < kFrontierRoundCap) a.kused[rnd + 1] = done ? 0 : K;
     if (!done && w == 0) {
       // expansion records, tiles prefix (wave 0; K <= 64)
@@ -2914,9 +3195,44 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         x.forced = p == s_blocked && s_bforced ? s_fidx[p] : -1;
         x.feature = kk.feature;
         x.last = p == s_blocked && nl + 1 >= L ? 1 : 0;
+        x.rescan = 0;
         a.exps[lane] = x;
         a.nodes[p].left = cid_next + 2 * lane;
         a.nstate[p] = s_st[p] | kNodeExpanded;
+      }
+      if (kMono && lane >= K && lane < K + NR) {
+        // a rescan: node c's record again from its slot under its current bounds; an expansion
+        // grown from its stale record is void (children dead, the node unexpanded)
+        const int c = s_rsc[lane - K], l = s_rsl[lane - K];
+        FExp x;
+        x.parent = c;
+        x.left = -1;
+        x.depth = s_dep[c];
+        x.tile0 = inc;
+        x.ntiles = 0;
+        x.src_buf = x.start = x.count = x.dst_buf = 0;
+        x.group = x.offset = x.num_bin = x.mfb = x.default_bin = x.missing = x.thr = x.default_left = x.is_cat = 0;
+        x.skip = 0;
+        x.smaller = c;
+        x.larger = -1;
+        x.h_buf = x.h_start = x.h_count = 0;
+        x.forced = -1;
+        x.feature = -1;
+        x.last = 0;
+        x.rescan = 1;
+        a.exps[lane] = x;
+        const double2 cb = mo.cb[l];
+        LeafBounds lb;
+        lb.min = cb.x;
+        lb.max = cb.y;
+        a.bounds[c] = lb;
+        const int lf = s_left[c];
+        if (lf >= 0) {
+          a.nodes[c].left = -1;
+          a.nstate[lf] = static_cast<uint8_t>((s_st[lf] & ~kNodeStale) | kNodeDead);
+          a.nstate[lf + 1] = static_cast<uint8_t>((s_st[lf + 1] & ~kNodeStale) | kNodeDead);
+        }
+        a.nstate[c] = static_cast<uint8_t>(s_st[c] & ~(kNodeExpanded | kNodeStale));
       }
       if (lane == 63) s_tiles = inc;
     } else if (!done) {
@@ -2941,13 +3257,15 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     ns_.byn = s_byn;
     ns_.byn_rng = s_brng;
     if (!done) {
-      ns_.k = s_k;
+      ns_.k = s_k + (kMono ? s_nr : 0);
+      ns_.kx = s_k;
       ns_.total_tiles = s_tiles;
       ns_.epoch = st.epoch + 1u;
       ns_.cid_next = cid_next + 2 * s_k;
       ns_.spec = st.spec + s_k;
     } else {
       ns_.k = 0;
+      ns_.kx = 0;
       ns_.total_tiles = 0;
     }
     *a.st = ns_;
@@ -3607,8 +3925,9 @@ void LaunchFrontierHist(const FArgs& a, size_t lds, hipStream_t s) {
 }
 
 void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
-  const bool ext = a.voting || a.xrng != nullptr || a.fowned != nullptr;
-  // (the wave kernel also runs voting's local pass: numerical features, no forced splits)
+  const bool ext = a.voting || a.xrng != nullptr || a.fowned != nullptr || a.mono_inter;
+  // (the wave kernel also runs voting's local pass: numerical features, no forced splits; the
+  // intermediate-monotone rescans run on the block kernel)
   if (a.scan_wave && (!ext || (a.voting && a.xrng == nullptr && a.fowned == nullptr)) && a.num_forced == 0) {
     // one wave per item, items grid-strided over the RESIDENT blocks: a grid sized for the widest
     // round (up to 2048 blocks) left most blocks without an item in a typical round, dispatched
@@ -3640,10 +3959,18 @@ void LaunchFrontierScan(const FArgs& a, size_t lds, hipStream_t s) {
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s) {
   const size_t lds = FrontierSelectLds(a.C, a.L);
   const bool wide = a.F > 64 || (a.fpb != nullptr && a.vote_P > 64);
-  if (a.cegb_raw) k_f_select<true, false, false><<<1, kFSelThreads, lds + (a.byn_draw != nullptr ? 2 : 1) * (a.F + 16), s>>>(a);
-  else if (a.xg) wide ? k_f_select<false, true, true><<<1, kFSelThreads, lds, s>>>(a) : k_f_select<false, false, true><<<1, kFSelThreads, lds, s>>>(a);
-  else if (wide) k_f_select<false, true, false><<<1, kFSelThreads, lds, s>>>(a);
-  else k_f_select<false, false, false><<<1, kFSelThreads, lds, s>>>(a);
+  if (a.cegb_raw) {
+    k_f_select<true, false, false, false><<<1, kFSelThreads, lds + (a.byn_draw != nullptr ? 2 : 1) * (a.F + 16), s>>>(a);
+  } else if (a.mono_inter) {
+    const size_t ml = lds + FrontierSelectMonoLds(a.C, a.L, a.F);
+    wide ? k_f_select<false, true, false, true><<<1, kFSelThreads, ml, s>>>(a) : k_f_select<false, false, false, true><<<1, kFSelThreads, ml, s>>>(a);
+  } else if (a.xg) {
+    wide ? k_f_select<false, true, true, false><<<1, kFSelThreads, lds, s>>>(a) : k_f_select<false, false, true, false><<<1, kFSelThreads, lds, s>>>(a);
+  } else if (wide) {
+    k_f_select<false, true, false, false><<<1, kFSelThreads, lds, s>>>(a);
+  } else {
+    k_f_select<false, false, false, false><<<1, kFSelThreads, lds, s>>>(a);
+  }
   HIP_CHECK(hipGetLastError());
 }
 

@@ -68,7 +68,10 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
     return "cost-effective gradient boosting (feature penalties)";
   }
   if (!c->forcedsplits_filename.empty() && !frontier_ok) return "forced splits";
-  if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic") {
+  // intermediate monotone constraints: the frontier select walks the constraints and re-scans the
+  // leaves they tighten (device::FrontierServesMonoInter); advanced keeps the host walk
+  if (!c->monotone_constraints.empty() && c->monotone_constraints_method != "basic" &&
+      (linear_tree || !device::FrontierServesMonoInter(c, train, learner_type))) {
     return "intermediate/advanced monotone constraints (device scans, host constraint walk)";
   }
   // (more than 64 sets: the frontier's multi-word masks, up to 256; the sequential chain holds 64.

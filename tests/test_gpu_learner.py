@@ -601,7 +601,9 @@ def test_device_monotone_constraints_reference_cases(lgb, gpu_required, rng, x3_
         p = dict(params, device_type=dev)
         models[dev] = lgb.train(p, Dataset(X, y, categorical_feature=cat, params=p), 30, keep_training_booster=True)
     bg, bc = models["gpu"], models["cpu"]
-    assert "host split policy" not in bg.device_name() and "split scans" in bg.device_name(), bg.device_name()
+    # intermediate: the frontier select walks the constraints; advanced: device scans, host walk
+    want = "intermediate monotone walk" if method == "intermediate" else "split scans"
+    assert "host split policy" not in bg.device_name() and want in bg.device_name(), bg.device_name()
     n = 1000
     v = np.linspace(0, 1, n).reshape((n, 1))
     for fixed in np.linspace(0, 1, n)[:10]:
@@ -615,6 +617,48 @@ def test_device_monotone_constraints_reference_cases(lgb, gpu_required, rng, x3_
     np.testing.assert_allclose(bg.predict(X), bc.predict(X), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("extra", [
+    {},
+    {"num_leaves": 63, "objective": "regression"},
+    # (a regression target: a binary one at 127 leaves leaves pure nodes whose gains are rounding
+    # noise, ~1e-14, where CPU and device sums legitimately order differently -- basic too)
+    {"num_leaves": 127, "objective": "regression", "n": 60000},
+    {"path_smooth": 1.5, "lambda_l1": 0.3, "max_depth": 8},
+    {"monotone_penalty": 0.5, "lambda_l2": 1.0},
+    {"interaction_constraints": [[0, 1, 2], [1, 3, 4, 5]], "num_leaves": 47},
+    # (max_delta_step puts this data's gains at rounding-noise level, ~1e-13, for basic too)
+    {"bagging_fraction": 0.6, "bagging_freq": 1, "objective": "regression"},
+])
+def test_frontier_intermediate_monotone_matches_cpu(lgb, gpu_required, rng, extra):
+    """Intermediate monotone constraints in the frontier engine's select (FMonoCommit: the host's
+    constraint walk per committed split, stale leaves re-scanned from their slots): the trees equal
+    the CPU learner's split for split, in the same order, and the model is monotone."""
+    extra = dict(extra)
+    n = extra.pop("n", 20000)
+    X, z = _policy_data(rng, n)
+    obj = extra.pop("objective", "binary")
+    y = z if obj == "regression" else (z > 0).astype(float)
+    kw = dict(extra, objective=obj, monotone_constraints=[1, -1, 1, 0, -1, 0],
+              monotone_constraints_method="intermediate")
+    kw.setdefault("num_leaves", 31)
+    bc = _train(lgb, X, y, "cpu", rounds=8, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=8, gpu_use_dp=True, **kw)
+    assert "frontier engine, intermediate monotone walk" in bg.device_name(), bg.device_name()
+    tc, tg = _trees(bc), _trees(bg)
+    assert [t["num_leaves"] for t in tc] == [t["num_leaves"] for t in tg]
+    for a, b in zip(tc, tg):
+        sa, sb = _splits_in_order(a["tree_structure"]), _splits_in_order(b["tree_structure"])
+        assert [x[:2] for x in sa] == [x[:2] for x in sb]
+        np.testing.assert_allclose([x[2] for x in sa], [x[2] for x in sb], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(bg.predict(X, raw_score=True), bc.predict(X, raw_score=True), rtol=1e-6, atol=1e-6)
+    grid = np.linspace(-3, 3, 60)
+    for row in X[:8]:
+        for f, sign in ((0, 1), (1, -1), (2, 1), (4, -1)):
+            Z = np.repeat(row[None, :], len(grid), 0)
+            Z[:, f] = grid
+            assert np.all(sign * np.diff(bg.predict(Z, raw_score=True)) >= -1e-10)
+
+
 @pytest.mark.parametrize("method", ["intermediate", "advanced"])
 def test_device_monotone_scans_default_precision(lgb, gpu_required, rng, method):
     """The default device_type=gpu setup (gpu_use_dp unset: fp32 (g, h) with fixed-point histogram
@@ -626,7 +670,8 @@ def test_device_monotone_scans_default_precision(lgb, gpu_required, rng, method)
     kw = {"objective": "binary", "monotone_constraints": [1, -1, 0, 0, 0, 0], "monotone_constraints_method": method}
     bc = _train(lgb, X, y, "cpu", rounds=10, **kw)
     bg = _train(lgb, X, y, "gpu", rounds=10, **kw)
-    assert "split scans" in bg.device_name(), bg.device_name()
+    want = "intermediate monotone walk" if method == "intermediate" else "split scans"
+    assert want in bg.device_name(), bg.device_name()
     pc, pg = bc.predict(X), bg.predict(X)
     assert np.mean(np.abs(pg - pc)) < 5e-3, np.mean(np.abs(pg - pc))
     grid = np.linspace(-3, 3, 50)
@@ -658,6 +703,7 @@ def test_device_monotone_scans_with_other_policies(lgb, gpu_required, rng, extra
     kw = dict(extra, objective=obj, monotone_constraints=[1, -1, 0, 0, 0, 0])
     bc = _train(lgb, X, y, "cpu", rounds=6, **kw)
     bg = _train(lgb, X, y, "gpu", rounds=6, gpu_use_dp=True, **kw)
+    # (the CEGB split penalty keeps intermediate on the host walk over device scans)
     assert "split scans" in bg.device_name(), bg.device_name()
     tc, tg = _trees(bc), _trees(bg)
     assert [t["num_leaves"] for t in tc] == [t["num_leaves"] for t in tg]
