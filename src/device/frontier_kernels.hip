@@ -8,7 +8,8 @@
 //   k_f_reduce      (2 or 4) x CUs x 256 (grid-stride over (expansion, bin chunk, row group))
 //   k_f_scan        min(kmax * F, cap) x 256 (grid-stride over (expansion, feature)); k_f_scan_w
 //                   one wave per item for wide numerical data
-//   k_f_select      1 x 1024
+//   k_f_select      1 x 1024 (instantiations: CEGB / by-node raw candidates, wide phase A, xGMI
+//                   exchange, intermediate monotone walk + rescans)
 //   k_fx_root       1 x 64 (xGMI transport: once per tree)
 #include <hip/hip_runtime.h>
 
