@@ -48,6 +48,8 @@ def main() -> int:
     base = {"objective": objective, "num_leaves": 31, "verbosity": -1, "seed": 1, "min_data_in_leaf": 20,
             "tree_learner": learner, "num_machines": world, "pre_partition": True, "deterministic": True,
             "top_k": int(os.environ.get("DP_TOPK", "20"))}
+    # extra options (JSON), e.g. extra_trees / cegb_penalty_split on the voting learner
+    base.update(json.loads(os.environ.get("DP_EXTRA", "{}")))
     if os.environ.get("DP_QUANTIZED") == "1":
         # quantized gradients: packed level sums (one accumulator word per bin) all-reduced
         base.update({"use_quantized_grad": True, "num_grad_quant_bins": 4})

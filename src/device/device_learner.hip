@@ -384,6 +384,11 @@ class DeviceTreeLearner : public TreeLearner {
         SetupFrontierXgmi(want == "xgmi");
       }
       else if (want == "xgmi") Log::Warning("xGMI transport: this frontier configuration exchanges through collectives");
+      // (TreeLearner::Create routes voting + extra trees over collectives to the host policy: the
+      // frontier's global-pass redraws are verified over the in-kernel exchange only)
+      if (fvoting_ && config_->extra_trees && !FrontierXg()) {
+        Log::Fatal("voting-parallel with extra_trees on the device needs the xGMI transport (set up failed)");
+      }
       return;
     }
     // the sequential chain (configurations the frontier does not hold) exchanges through collectives
@@ -1724,8 +1729,9 @@ class DeviceTreeLearner : public TreeLearner {
   // sequential chain (A/B runs).
   bool FrontierEligible() const {
     if (!FrontierSerial() && !FrontierDP() && !FrontierVoting() && !FrontierFeature()) return false;
-    // extra trees: the single-device frontier (one expansion per round: FArgs::xrng)
-    if (config_->extra_trees && !FrontierSerial()) return false;
+    // extra trees: the single-device frontier and the voting frontier on numerical data (one
+    // expansion per round: FArgs::xrng; the global pass redraws in the host's order, k_f_vote_scan)
+    if (config_->extra_trees && !FrontierSerial() && !(FrontierVoting() && !has_cat_)) return false;
     // by-node sampling: the single-device frontier (masks in the host's draw order, FArgs::bynode;
     // under interaction constraints drawn in the select, FArgs::byn_draw)
     if (use_bynode_ && !FrontierSerial()) return false;

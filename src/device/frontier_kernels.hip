@@ -3582,9 +3582,29 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
     po = a.lout[c];
   }
   const LeafBounds bounds = a.bounds[c];
+  // extra trees (numerical data, one expansion per round): feature f's stream drew for both children
+  // in the local pass; the global pass draws for the smaller child's elected features, then the
+  // larger's (host FindBestSplitsFromHistograms order). Both children's items read the stream as
+  // the local pass left it: the larger's item replays the smaller's draw first when f was elected
+  // for both, and only the item that draws last stores the state back.
+  int rt = 0;
+  if (a.xrng != nullptr && fi.bin_type == 0) {
+    const int sel = q & 1, other = q ^ 1;
+    bool both = false;
+    if (FPairChild(a, k, other) >= 0) {
+      const int* eo = a.velect + static_cast<size_t>(other) * (K + 1);
+      for (int i = 0; i < eo[0]; ++i) both = both || eo[1 + i] == f;
+    }
+    unsigned x = a.xrng[f];
+    if (fi.num_bin - 2 > 0) {
+      if (sel == 1 && both) (void)LcgNext(&x);
+      rt = RandNextInt(&x, 0, fi.num_bin - 2);
+    }
+    if (lane == 0 && (sel == 1 || !both)) a.xrng[f] = x;
+  }
   bool spl;
   if (fi.bin_type == 0) {
-    spl = ScanNumericalWave(a.sp, fi, H, sums.x, sums.y, n, po, bounds, 0, out);
+    spl = ScanNumericalWave(a.sp, fi, H, sums.x, sums.y, n, po, bounds, rt, out);
   } else {
     FeatureScanMeta m;
     m.num_bin = fi.num_bin;
@@ -3601,6 +3621,9 @@ __global__ __launch_bounds__(64) void k_f_vote_scan(FArgs a) {
       out->Reset();
     } else {
       out->feature = f;
+      // CEGB split penalty at the leaf's global count (reference ComputeBestSplitForFeature with
+      // GetGlobalDataCountInLeaf), then the monotone penalty
+      if (a.cegb_split > 0.0) out->gain -= a.cegb_split * n;
       if (out->monotone_type != 0) out->gain *= MonotonePenaltyAt(a.monotone_penalty, nd.depth);
       if (a.ic && !FIcAllows(a, c, f)) out->Reset();
     }

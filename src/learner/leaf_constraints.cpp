@@ -388,10 +388,11 @@ void CegbPenalty::BeforeTree() {
   for (auto& s : per_leaf_feature_) s.Reset();
 }
 
-double CegbPenalty::DeltaGain(int f, int leaf, const data_size_t* rows, data_size_t n, const SplitInfo& candidate) {
+double CegbPenalty::DeltaGain(int f, int leaf, const data_size_t* rows, data_size_t n, const SplitInfo& candidate,
+                              data_size_t split_n) {
   const double t = cfg_->cegb_tradeoff;
   const int real = data_->feature(f).real_index;
-  double delta = t * cfg_->cegb_penalty_split * n;
+  double delta = t * cfg_->cegb_penalty_split * (split_n >= 0 ? split_n : n);
   if (!cfg_->cegb_penalty_feature_coupled.empty() && !used_in_split_[f]) {
     delta += t * cfg_->cegb_penalty_feature_coupled[real];
   }

@@ -108,7 +108,11 @@ class CegbPenalty {
   void Init(const Dataset* data, const Config* c);
   void BeforeTree();
   // gain deduction of a candidate split on inner feature `f` of `leaf` (rows = the leaf's rows)
-  double DeltaGain(int f, int leaf, const data_size_t* rows, data_size_t n, const SplitInfo& candidate);
+  // n rows of the leaf on this machine (the lazy penalty's on-demand count walks them); split_n:
+  // the leaf's GLOBAL count for the split penalty (reference ComputeBestSplitForFeature passes
+  // GetGlobalDataCountInLeaf in the data / voting learners), -1: n
+  double DeltaGain(int f, int leaf, const data_size_t* rows, data_size_t n, const SplitInfo& candidate,
+                   data_size_t split_n = -1);
   // before the chosen split of `best_leaf` is applied (rows = that leaf's rows)
   void OnSplit(int num_leaves, int best_leaf, const SplitInfo& chosen, const data_size_t* rows, data_size_t n,
                std::vector<SplitInfo>* best_per_leaf);

@@ -830,7 +830,10 @@ SplitInfo SerialTreeLearner::ScoreFeature(const Tree* tree, const double* group_
     s = BestSplitForFeature(group_hist, f, leaf, parent_output, bounds_[leaf.leaf], nullptr, splittable);
   }
   if (s.feature < 0) return s;
-  if (cegb_) s.gain -= cegb_->DeltaGain(f, leaf.leaf, partition_.indices(leaf.leaf), partition_.count(leaf.leaf), s);
+  if (cegb_) {
+    s.gain -= cegb_->DeltaGain(f, leaf.leaf, partition_.indices(leaf.leaf), partition_.count(leaf.leaf), s,
+                               leaf.global_count);
+  }
   if (s.monotone_type != 0) s.gain *= MonotonePenalty(tree, leaf.leaf);
   return s;
 }
@@ -934,7 +937,10 @@ void SerialTreeLearner::DeviceScanLeaves(const Tree* tree, const std::vector<con
     for (int f = 0; f < F; ++f) {
       SplitInfo& s = (*out)[static_cast<size_t>(r) * F + f];
       if (s.feature < 0) continue;
-      if (cegb_) s.gain -= cegb_->DeltaGain(f, ls.leaf, partition_.indices(ls.leaf), partition_.count(ls.leaf), s);
+      if (cegb_) {
+        s.gain -= cegb_->DeltaGain(f, ls.leaf, partition_.indices(ls.leaf), partition_.count(ls.leaf), s,
+                                   ls.global_count);
+      }
       if (s.monotone_type != 0) s.gain *= MonotonePenalty(tree, ls.leaf);
     }
   }

@@ -51,8 +51,27 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   if (DeviceHistogramsExceedPool(c, train)) return "per-leaf device histograms above the histogram pool";
   // linear leaves: on the device (MFMA Gram systems) within its shape, else the host learner
   if (linear_tree && !device::LinearOnDevice(c, train, learner_type)) return "linear_tree";
-  // (voting runs on the device; its global pass redraws no extra-trees thresholds)
-  if (learner_type == "voting" && c->extra_trees) return "voting-parallel with extra_trees";
+  // voting with extra trees on the device: the global pass redraws each elected feature's threshold
+  // from the per-feature streams, which stay identical on every rank only when no draw depends on
+  // local data (categorical draws count the local histogram's used bins)
+  if (learner_type == "voting" && c->extra_trees) {
+    // the frontier's global-pass redraws run over the in-kernel xGMI exchange only (the
+    // host-staged / RCCL collectives path of this combination is not tree-equal to the host)
+    const char* t = std::getenv("LGAP_DP_TRANSPORT");
+    const char* h = std::getenv("LGAP_DEVICE_DP_TRANSPORT");
+    if ((t != nullptr && std::string(t) != "auto" && std::string(t) != "xgmi") ||
+        (h != nullptr && std::string(h) == "host" && !(t != nullptr && std::string(t) == "xgmi"))) {
+      return "voting-parallel with extra_trees over collectives";
+    }
+    // (with the CEGB split penalty as well the device and host voting learners part after a few
+    // trees: not verified tree-equal, so the host policy keeps it)
+    if (CegbPenalty::Enabled(c)) return "voting-parallel with extra_trees and CEGB";
+  }
+  if (learner_type == "voting" && c->extra_trees && train != nullptr) {
+    for (int f = 0; f < train->num_features(); ++f) {
+      if (train->feature(f).bin_type != BinType::Numerical) return "voting-parallel with extra_trees and categorical features";
+    }
+  }
   // CEGB: the split penalty runs in the device scans, the coupled and lazy feature penalties
   // in the frontier engine (serial learner: the select's replay refunds leaves and voids
   // speculation on a feature's first use; per-row marks count each node's unmarked rows).
@@ -64,7 +83,7 @@ const char* HostPolicyReason(const std::string& learner_type, bool linear_tree, 
   const bool frontier_ok = needs_frontier && device::FrontierServes(c, train, learner_type) &&
                            (!feature_pens || ((train == nullptr || train->num_features() <= 8192) &&
                                               c->interaction_constraints_vector.empty()));
-  if ((feature_pens && !frontier_ok) || (CegbPenalty::Enabled(c) && learner_type == "voting")) {
+  if (feature_pens && !frontier_ok) {
     return "cost-effective gradient boosting (feature penalties)";
   }
   if (!c->forcedsplits_filename.empty() && !frontier_ok) return "forced splits";

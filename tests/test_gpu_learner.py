@@ -458,6 +458,42 @@ def test_voting_parallel_multirank_rehearsal(lgb, gpu_required, world, transport
     assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
 
 
+@pytest.mark.parametrize("world,transport,extra", [
+    (2, "xgmi", {"extra_trees": True}),
+    (3, "xgmi", {"extra_trees": True, "top_k": 3}),
+    (3, "xgmi", {"cegb_penalty_split": 0.002, "cegb_tradeoff": 0.5}),
+    (2, "collective", {"cegb_penalty_split": 0.001, "top_k": 3}),
+    (4, "xgmi", {"extra_trees": True, "top_k": 2}),
+])
+def test_voting_parallel_extra_trees_and_cegb_split(lgb, gpu_required, world, transport, extra):
+    """Voting parallel with extra trees (the global pass redraws each elected feature's threshold
+    from its stream in the host's order: smaller child's elected features, then the larger's) and
+    with the CEGB split penalty (at the leaf's global count, as the reference's global pass) on the
+    device frontier, P ranks sharing the GPU: identical models on every rank, equal to the host
+    voting learner tree for tree. (Extra trees run over the in-kernel xGMI exchange; over
+    collectives the factory keeps the host policy.)"""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    extra = dict(extra)
+    topk = extra.pop("top_k", 20)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LGAP_DP_TRANSPORT=transport, LGAP_XGMI_TIMEOUT_S="20",
+               DP_LEARNER="voting", DP_TOPK=str(topk), DP_EXTRA=json.dumps(extra))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+                        "--nproc-per-node", str(world), os.path.join(root, "scripts", "dp_multirank.py")],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "voting-parallel" in res["device_name"] and "frontier engine" in res["device_name"], res
+    assert "host split policy" not in res["device_name"], res
+    assert res["ranks_identical"], res
+    assert res["identical_leading_trees"] == 10, res
+    assert res["max_abs_diff_vs_cpu_dp"] < 1e-3, res
+
+
 def _policy_data(rng, n=20000):
     X = rng.standard_normal((n, 6))
     z = 1.5 * X[:, 0] - X[:, 1] + 0.7 * X[:, 2] * X[:, 3] + 0.3 * rng.standard_normal(n)
