@@ -128,7 +128,7 @@ namespace {
 const char* KernelOverride(const char* key) {
   static const char* const kKeys[] = {"fhist_threads", "hist_lds_kb", "quant_lds32", "part_iters",
                                       "hist_il",       "nibble",      "quant_hist",  "scan_global",
-                                      "scan_wave",     "oob_rows"};
+                                      "scan_wave",     "oob_rows",    "select_merge"};
   constexpr int kNumKeys = static_cast<int>(sizeof(kKeys) / sizeof(kKeys[0]));
   thread_local std::string vals[kNumKeys];
   const char* e = std::getenv("LGAP_KERNEL");
@@ -1876,7 +1876,7 @@ class DeviceTreeLearner : public TreeLearner {
                  o_spl = lay.Add<uint8_t>(C * F), o_ic = lay.Add<unsigned long long>(C * kFrontierIcWords), o_nst = lay.Add<uint8_t>(C),
                  o_lcid = lay.Add<int>(L_), o_ckey = lay.Add<SplitKey>(K * 2 * F), o_cinfo = lay.Add<SplitInfo>(K * 2 * F),
                  o_fbest = lay.Add<SplitInfo>(C), o_fkey = lay.Add<SplitKey>(C),
-                 o_cbnd = lay.Add<LeafBounds>(MonoInter() ? C : 1);
+                 o_cbnd = lay.Add<LeafBounds>(MonoInter() ? C : 1), o_sal = lay.Add<int>(C);
     farena_.Resize(lay.bytes());
     farena_.Zero(stream_);
     char* b = farena_.get();
@@ -1898,6 +1898,7 @@ class DeviceTreeLearner : public TreeLearner {
     ffbest_ = reinterpret_cast<SplitInfo*>(b + o_fbest);
     ffkey_ = reinterpret_cast<SplitKey*>(b + o_fkey);
     fcbnd_ = MonoInter() ? reinterpret_cast<LeafBounds*>(b + o_cbnd) : nullptr;
+    fsal_ = reinterpret_cast<int*>(b + o_sal);
     UploadForcedSplits();
     if (RawCands()) {
       fnkey_.Resize(C * F);
@@ -2160,6 +2161,9 @@ class DeviceTreeLearner : public TreeLearner {
     a.use_monotone = config_->monotone_constraints.empty() ? 0 : 1;
     a.mono_inter = fcbnd_ != nullptr ? 1 : 0;
     a.cbnd = fcbnd_;
+    // LGAP_KERNEL=select_merge=0: the select re-sorts the alive list every round (A/B)
+    const char* sm = KernelOverride("select_merge");
+    a.salive = sm != nullptr && sm[0] == '0' ? nullptr : fsal_;
     a.monotone_penalty = config_->monotone_penalty;
     a.cegb_split = CegbPenalty::Enabled(config_) ? config_->cegb_tradeoff * config_->cegb_penalty_split : 0.0;
     a.max_bin = max_bin_;
@@ -4125,6 +4129,7 @@ class DeviceTreeLearner : public TreeLearner {
   double* flout_ = nullptr;
   LeafBounds* fbounds_ = nullptr;
   LeafBounds* fcbnd_ = nullptr;  // intermediate monotone: the committed leaves' current bounds
+  int* fsal_ = nullptr;          // the select's alive order, carried to the next round
   SplitKey* fkey_ = nullptr;
   SplitInfo* fbest_ = nullptr;
   uint8_t* fspl_ = nullptr;

@@ -87,6 +87,7 @@ constexpr uint8_t kNodeExpanded = 1;   // children computed
 constexpr uint8_t kNodeCommitted = 2;  // its split is part of the tree (replay)
 constexpr uint8_t kNodeDead = 4;       // below an expansion the CEGB replay invalidated: never used
 constexpr uint8_t kNodeStale = 0x40;   // (select-local) intermediate monotone: record scanned under looser bounds
+constexpr uint8_t kNodeEligTmp = 0x20; // (select-local) eligible for expansion this round
 // stamp slots: kernel ids and the per-kernel slot count (slot 7: latest block exit)
 constexpr int kFStampPart = 0, kFStampHist = 1, kFStampScan = 2, kFStampSel = 3, kFStampSlots = 8;
 
@@ -145,6 +146,7 @@ struct FState {
   int forced_next;  // next forced split to apply (-1: forced splits over or none)
   int byn;          // feature_fraction_bynode: masks drawn so far (the host's GetByNode calls)
   unsigned byn_rng; // by-node draws in the select (FArgs::byn_draw): the column sampler's LCG state
+  int nsal;         // alive nodes in FArgs::salive (the last select's order; 0: none)
 };
 
 // Arguments of the frontier kernels (device pointers into the learner's buffers).
@@ -231,6 +233,7 @@ struct FArgs {
   // commit, and re-scans leaves whose bounds moved past the ones their record was scanned with
   int mono_inter;
   LeafBounds* cbnd;  // [C] current bounds of the committed tree's leaves (by cid)
+  int* salive;       // [C] the alive nodes by (gain desc, cid asc) as the last select ordered them
   double monotone_penalty;
   double cegb_split;  // cegb_tradeoff * cegb_penalty_split (per row of the node), 0: none
   // CEGB coupled feature penalties (cegb_penalty_feature_coupled) on the device, host

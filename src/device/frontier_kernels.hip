@@ -243,6 +243,7 @@ __device__ __forceinline__ void FInitTree(const FArgs& a) {
     s.forced_next = a.num_forced > 0 ? 0 : -1;
     s.byn = a.bynode != nullptr ? 1 : 0;  // (the root's mask: row 0)
     s.byn_rng = tp.byn_rng;
+    s.nsal = 0;
     *a.st = s;
     FNode r;
     r.buf = tp.root_buf;
@@ -2210,6 +2211,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
   const unsigned xep = kXg ? *a.xc->ep : 0u;  // (xGMI: this round's tag is xep + 1)
+  // keys final once computed (no CEGB re-scoring, no monotone rescans): the alive order carries over
+  constexpr bool kIncr = !kCegb && !kMono;
   if (st.done) return;
   const int kprev = st.k;
   const int cid_next = st.cid_next;
@@ -2899,6 +2902,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   FStamp(a, rnd, kFStampSel, 3);
   const int nl = s_nl, ns = s_ns, ncommit = s_ncommit;
   int done = s_done;
+  __shared__ int s_nsal;  // alive nodes ordered this round (FState::nsal)
+  if (t == 0) s_nsal = 0;
   // ---- C. committed splits -> (leaf, cid) records, leaf table, states. The full records
   // (SplitInfo, children counts) are gathered once per tree by k_f_results: a committed
   // node's best never changes, and the copy no longer sits on every round's critical path
@@ -2952,6 +2957,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
           }
         }
         unc = (sc & kNodeExpanded) && !(sc & kNodeCommitted);
+        if (kIncr && elig) s_st[c] = static_cast<uint8_t>(sc | kNodeEligTmp);  // (the merged order's flags)
       }
       const unsigned long long ma = __ballot(alive);
       const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -2970,6 +2976,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     }
     __syncthreads();
     const int na = min(s_na, cap_list);
+    if (t == 0) s_nsal = na;
     const int blocked = s_blocked;
     const int R = L - 1 - ns;  // splits the tree may still make
     // Order of the alive list by (gain desc, cid asc): a bitonic sort in LDS. Position p in the
@@ -3065,6 +3072,93 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       if (t < na) s_sc[pos] = ri;
       __syncthreads();
     } else {
+    // Beyond kSelRankMax alive nodes (255-leaf trees): the previous select's order, filtered to the
+    // nodes still alive, merged with the last round's children (rank-sorted among themselves).
+    // Outside CEGB / intermediate-monotone rescans a computed node's key never changes, so the
+    // merge is the full sort's order; if the counts disagree (they cannot) the network runs.
+    bool merged = false;
+    if (kIncr && a.salive != nullptr && st.nsal > 0) {
+      int* s_oc = reinterpret_cast<int*>(s_sg);  // [C] previous order, still alive
+      int* s_nw = s_oc + C;                      // [<= 2 kmax + 1] the new ones, ordered
+      int* s_nf = s_nw + 2 * kFrontierKmax + 1;  // [<= 2 kmax + 1] alive flags of the new ones
+      __shared__ int s_nk, s_nn;
+      const int nold = min(st.nsal, C);
+      const int lo = max(base, 0), nn = min(cid_next - lo, 2 * kFrontierKmax + 1);
+      auto live = [&](int c) {
+        return !(s_st[c] & (kNodeCommitted | kNodeDead)) && s_feat[c] >= 0 && s_gain[c] > 0.0;
+      };
+      for (int i = t; i < nold; i += blockDim.x) s_sc[i] = a.salive[i];
+      for (int i = t; i < nn; i += blockDim.x) s_nf[i] = live(lo + i) ? 1 : 0;
+      if (t == 0) s_nn = 0;
+      __syncthreads();
+      constexpr int kPm = kFrontierMaxNodes / kFSelThreads;
+      int keep[kPm], kloc = 0;
+#pragma unroll
+      for (int q = 0; q < kPm; ++q) {
+        const int p = t * kPm + q;
+        keep[q] = p < nold && s_sc[p] < lo && live(s_sc[p]) ? 1 : 0;
+        kloc += keep[q];
+      }
+      const int kinc = WaveInclusiveScan(kloc);
+      __shared__ int s_kw[kFSelThreads / 64];
+      if (lane == 63) s_kw[w] = kinc;
+      // the new ones' ranks among themselves (<= 129: broadcast reads)
+      int nr = -1;
+      if (t < nn && s_nf[t]) {
+        const int ci = lo + t;
+        const double gi = s_gain[ci];
+        nr = 0;
+        for (int j = 0; j < nn; ++j) {
+          if (!s_nf[j]) continue;
+          const double gj = s_gain[lo + j];
+          nr += (gj > gi || (gj == gi && lo + j < ci)) ? 1 : 0;
+        }
+        atomicAdd(&s_nn, 1);
+      }
+      __syncthreads();
+      int koff = 0;
+      for (int q = 0; q < w; ++q) koff += s_kw[q];
+      koff += kinc - kloc;
+      if (t == kFSelThreads - 1) s_nk = koff + kloc;
+#pragma unroll
+      for (int q = 0; q < kPm; ++q) {
+        if (keep[q]) s_oc[koff++] = s_sc[t * kPm + q];
+      }
+      if (nr >= 0) s_nw[nr] = lo + t;
+      __syncthreads();
+      const int nk = s_nk, nw = s_nn;
+      if (nk + nw == na) {
+        merged = true;
+        auto better = [&](int c1, int c2) {  // c1 before c2 (gain desc, cid asc)
+          const double g1 = s_gain[c1], g2 = s_gain[c2];
+          return g1 > g2 || (g1 == g2 && c1 < c2);
+        };
+        auto enc = [&](int c) { return (s_st[c] & kNodeEligTmp) ? c : ~c; };
+        for (int i = t; i < nk + nw; i += blockDim.x) {
+          if (i < nk) {
+            const int c = s_oc[i];
+            int l = 0, h = nw;  // new ones before c
+            while (l < h) {
+              const int m = (l + h) >> 1;
+              if (better(s_nw[m], c)) l = m + 1;
+              else h = m;
+            }
+            s_sc[i + l] = enc(c);
+          } else {
+            const int j = i - nk, c = s_nw[j];
+            int l = 0, h = nk;  // old ones before c
+            while (l < h) {
+              const int m = (l + h) >> 1;
+              if (better(s_oc[m], c)) l = m + 1;
+              else h = m;
+            }
+            s_sc[j + l] = enc(c);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (!merged) {
     for (int i = t; i < P2; i += blockDim.x) {
       if (i < na) {
         const int c = s_ac[i] >= 0 ? s_ac[i] : ~s_ac[i];
@@ -3095,6 +3189,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         }
         __syncthreads();
       }
+    }
     }
     }
     // eligible ranks: exclusive scan of the eligible (non-blocked) flags in sorted order
@@ -3142,6 +3237,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     __syncthreads();
     }
     FStamp(a, rnd, kFStampSel, 5);
+    // this round's order of the alive nodes, for the next select's merge
+    if (kIncr && a.salive != nullptr) {
+      for (int i = t; i < na; i += blockDim.x) a.salive[i] = s_sc[i] >= 0 ? s_sc[i] : ~s_sc[i];
+    }
     // (the node capacity bounds the round: expansions voided by CEGB first-use events leave
     // dead cids behind, so the reserve for the remaining splits is not a guarantee then)
     int K = min(s_k, (C - cid_next) / 2);
@@ -3199,7 +3298,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         x.rescan = 0;
         a.exps[lane] = x;
         a.nodes[p].left = cid_next + 2 * lane;
-        a.nstate[p] = s_st[p] | kNodeExpanded;
+        a.nstate[p] = static_cast<uint8_t>((s_st[p] & ~kNodeEligTmp) | kNodeExpanded);
       }
       if (kMono && lane >= K && lane < K + NR) {
         // a rescan: node c's record again from its slot under its current bounds; an expansion
@@ -3257,6 +3356,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     ns_.forced_next = s_fnext;
     ns_.byn = s_byn;
     ns_.byn_rng = s_brng;
+    ns_.nsal = done ? 0 : s_nsal;
     if (!done) {
       ns_.k = s_k + (kMono ? s_nr : 0);
       ns_.kx = s_k;

@@ -1439,6 +1439,35 @@ def test_speculation_budget_does_not_change_trees(lgb, gpu_required, monkeypatch
     assert model(LGAP_FRONTIER_SPEC="adapt") == base
 
 
+@pytest.mark.parametrize("extra", [{}, {"use_quantized_grad": True, "num_grad_quant_bins": 4},
+                                   {"num_leaves": 300, "min_data_in_leaf": 2}])
+def test_select_merged_alive_order_does_not_change_trees(lgb, gpu_required, monkeypatch, extra):
+    """Beyond 256 alive nodes the select merges the previous round's alive order with the last
+    round's children instead of re-sorting (FState::nsal, FArgs::salive): the same expansions and
+    the same model as the full sort (LGAP_KERNEL=select_merge=0)."""
+    rng = np.random.default_rng(29)
+    n = 80000
+    X = rng.standard_normal((n, 16))
+    y = X[:, 0] + 0.5 * X[:, 1] * X[:, 2] - 0.4 * np.abs(X[:, 3]) + 0.3 * rng.standard_normal(n)
+    params = {"objective": "regression", "num_leaves": 255, "min_data_in_leaf": 5, "device_type": "gpu",
+              "verbosity": -1, "seed": 4, "deterministic": True, **extra}
+
+    # (a fixed speculation budget: the timed tuner's budget follows measured tree times; 300 leaves
+    # is about the largest tree whose node image fits the select's LDS)
+    monkeypatch.setenv("LGAP_FRONTIER_SPEC", "fixed")
+
+    def model(merge):
+        if merge:
+            monkeypatch.delenv("LGAP_KERNEL", raising=False)
+        else:
+            monkeypatch.setenv("LGAP_KERNEL", "select_merge=0")
+        b = lgb.train(params, lgb.Dataset(X, y, params=params), 12, keep_training_booster=True)
+        assert "frontier engine" in b.device_name()
+        return b.model_to_string()
+
+    assert model(True) == model(False)
+
+
 _GPU_LOAD = r"""
 import sys, time
 import torch
