@@ -17,6 +17,9 @@ run_shape() {
   python scripts/pmc_summary.py "$name" $OUT/${name}_p1 $OUT/${name}_p2 $OUT/${name}_p3 > $OUT/${name}_pmc.md
   rm -rf $OUT/${name}_p1 $OUT/${name}_p2 $OUT/${name}_p3
 }
-run_shape ltr5m_x300 --config ltr --rows 5000000 --features 300 --steps 3 --warmup 1 || exit 1
-run_shape goss12m_x500 --config regression_goss --rows 12500000 --features 500 --steps 3 --warmup 11 || exit 1
+SHAPES=${SHAPES:-ltr goss}
+for s in $SHAPES; do
+  if [ $s = ltr ]; then run_shape ltr5m_x300 --config ltr --rows 5000000 --features 300 --steps 3 --warmup 1 || exit 1; fi
+  if [ $s = goss ]; then run_shape goss12m_x500 --config regression_goss --rows 12500000 --features 500 --steps 3 --warmup 11 || exit 1; fi
+done
 head -20 $OUT/*_pmc.md
