@@ -2927,6 +2927,39 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       s_ne = 0;
       s_eu = 0;
     }
+    if (kMono) {
+      // intermediate monotone: an expansion grown from a stale leaf's record is void -- its
+      // subtree dies (cids grow with depth: passes until no parent is newly dead), the leaf is
+      // unexpanded and waits for its rescan (0x80: select-local "state changed")
+      for (int i = t; i < s_nrs; i += blockDim.x) {
+        const int c = s_rsc[i], lf = s_left[c];
+        if (lf < 0) continue;
+        s_st[lf] = static_cast<uint8_t>(s_st[lf] | kNodeDead | 0x80);
+        s_st[lf + 1] = static_cast<uint8_t>(s_st[lf + 1] | kNodeDead | 0x80);
+        s_st[c] = static_cast<uint8_t>((s_st[c] & ~kNodeExpanded) | 0x80);
+        s_left[c] = -1;
+        a.nodes[c].left = -1;
+      }
+      __syncthreads();
+      for (;;) {
+        bool ch = false;
+        for (int x = t; x < cid_next; x += blockDim.x) {
+          const int px = s_par[x];
+          if (px >= 0 && (s_st[px] & kNodeDead) && !(s_st[x] & kNodeDead)) {
+            s_st[x] = static_cast<uint8_t>(s_st[x] | kNodeDead | 0x80);
+            ch = true;
+          }
+        }
+        if (!__syncthreads_or(ch)) break;
+      }
+      for (int x = t; x < cid_next; x += blockDim.x) {
+        const uint8_t sx = s_st[x];
+        if (sx & 0x80) {
+          s_st[x] = static_cast<uint8_t>(sx & ~0x80);
+          a.nstate[x] = static_cast<uint8_t>(sx & ~(0x80 | kNodeStale | kNodeEligTmp));
+        }
+      }
+    }
     __syncthreads();
     int* s_ac = s_rank;  // [C] compacted alive cids, ~cid when not eligible (reuses s_rank)
     const int cap_list = C;
@@ -2945,9 +2978,11 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         // extra trees: only the node the replay waits for (its children's random thresholds are
         // drawn when every earlier split of the sequential order has been scanned)
         if (elig && a.xrng != nullptr && c != s_blocked) elig = false;
-        // intermediate monotone: only leaves of the committed tree (a node's bounds are known once
-        // its parent commits), and not while its record is stale (it is re-scanned instead)
-        if (kMono && elig && ((sc & kNodeStale) || (s_par[c] >= 0 && !(s_st[s_par[c]] & kNodeCommitted)))) elig = false;
+        // intermediate monotone: not while its record is stale (it is re-scanned instead). A node
+        // below an uncommitted one is speculated on its provisional bounds (the parent's scanned
+        // ones, the sibling rule): they can only tighten by its commit, which the stale check
+        // and the subtree kill above catch
+        if (kMono && elig && (sc & kNodeStale)) elig = false;
         if (elig) {
           const int target = s_dep[c] + 1 - kFrontierBufs;
           if (target >= 1) {
@@ -3326,13 +3361,8 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         lb.min = cb.x;
         lb.max = cb.y;
         a.bounds[c] = lb;
-        const int lf = s_left[c];
-        if (lf >= 0) {
-          a.nodes[c].left = -1;
-          a.nstate[lf] = static_cast<uint8_t>((s_st[lf] & ~kNodeStale) | kNodeDead);
-          a.nstate[lf + 1] = static_cast<uint8_t>((s_st[lf + 1] & ~kNodeStale) | kNodeDead);
-        }
-        a.nstate[c] = static_cast<uint8_t>(s_st[c] & ~(kNodeExpanded | kNodeStale));
+        // (its expansion, if any, was voided at the start of phase D)
+        a.nstate[c] = static_cast<uint8_t>(s_st[c] & ~(kNodeExpanded | kNodeStale | kNodeEligTmp));
       }
       if (lane == 63) s_tiles = inc;
     } else if (!done) {
