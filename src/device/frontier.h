@@ -25,6 +25,18 @@
 //   k_f_select     one workgroup: per-child best split, replay of best-first order,
 //                  choice of the next round's expansions
 //
+// Intermediate monotone constraints (FArgs::mono_inter): a committed split also tightens the
+// bounds of leaves elsewhere in the tree (the host's constraint climb), so a leaf's record can go
+// stale after it was scanned. The select tracks each leaf's current bounds (cbnd) against the
+// ones its record was scanned with (bounds); a stale record is an upper bound of its re-scan, so
+// the replay only stops where a stale leaf could still win, and the next round re-scans the stale
+// leaves from their histogram slots (FExp::rescan: no tiles, no rows) and voids expansions grown
+// from their old records (the subtree dies).
+//
+// Beyond 256 alive nodes the select does not re-sort the alive list: keys never change once
+// computed (outside CEGB re-scoring and monotone rescans), so last round's order (salive) filtered
+// to the nodes still alive is merged with the children the round just scanned.
+//
 // Row lists: a node at depth d >= 1 keeps its row indices in depth buffer (d - 1) % 4
 // (the root: the bag or identity order). Children of depth-d nodes never overwrite
 // their parent's list, and a speculative expansion is only allowed where the list it
