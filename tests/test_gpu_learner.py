@@ -695,6 +695,46 @@ def test_frontier_intermediate_monotone_matches_cpu(lgb, gpu_required, rng, extr
             assert np.all(sign * np.diff(bg.predict(Z, raw_score=True)) >= -1e-10)
 
 
+@pytest.mark.parametrize("extra", [{"use_quantized_grad": True, "num_grad_quant_bins": 4},
+                                   {"categorical": True, "num_leaves": 63},
+                                   {"max_delta_step": 0.6, "objective": "regression", "num_leaves": 63}])
+def test_frontier_intermediate_monotone_other_modes(lgb, gpu_required, rng, extra):
+    """Intermediate monotone constraints on the frontier with quantized gradients (integer-level
+    histograms in the slots the rescans read), a categorical feature (bounds clamp its outputs),
+    and max_delta_step (no gain bound for stale records: every stale leaf is re-scanned before the
+    next commit): the model is monotone in the constrained features and tracks the CPU learner."""
+    extra = dict(extra)
+    X, z = _policy_data(rng, 30000)
+    cat = extra.pop("categorical", False)
+    if cat:
+        X[:, 5] = rng.integers(0, 12, len(X))
+        z = z + 0.3 * (X[:, 5] % 4)
+    obj = extra.pop("objective", "binary")
+    y = z if obj == "regression" else (z > 0).astype(float)
+    kw = dict(extra, objective=obj, monotone_constraints=[1, -1, 1, 0, -1, 0],
+              monotone_constraints_method="intermediate")
+    if cat:
+        kw["categorical_feature"] = [5]
+    bc = _train(lgb, X, y, "cpu", rounds=8, **kw)
+    bg = _train(lgb, X, y, "gpu", rounds=8, **kw)
+    assert "frontier engine, intermediate monotone walk" in bg.device_name(), bg.device_name()
+    pc, pg = bc.predict(X), bg.predict(X)
+    if obj == "regression":
+        lc, lg_ = float(np.mean((pc - y) ** 2)), float(np.mean((pg - y) ** 2))
+    else:
+        eps = 1e-12
+        lc = float(-np.mean(y * np.log(pc + eps) + (1 - y) * np.log(1 - pc + eps)))
+        lg_ = float(-np.mean(y * np.log(pg + eps) + (1 - y) * np.log(1 - pg + eps)))
+    # (quantized gradients: the device and host quantizers draw differently; same loss level)
+    assert abs(lg_ - lc) < 0.03 * lc, (lg_, lc)
+    grid = np.linspace(-3, 3, 60)
+    for row in X[:8]:
+        for f, sign in ((0, 1), (1, -1), (2, 1), (4, -1)):
+            Z = np.repeat(row[None, :], len(grid), 0)
+            Z[:, f] = grid
+            assert np.all(sign * np.diff(bg.predict(Z, raw_score=True)) >= -1e-10)
+
+
 @pytest.mark.parametrize("method", ["intermediate", "advanced"])
 def test_device_monotone_scans_default_precision(lgb, gpu_required, rng, method):
     """The default device_type=gpu setup (gpu_use_dp unset: fp32 (g, h) with fixed-point histogram
