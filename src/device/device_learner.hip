@@ -2558,7 +2558,9 @@ class DeviceTreeLearner : public TreeLearner {
         break;
       }
       // (intermediate monotone: a split may wait on a round of rescans and one of expansion)
-      if (launched > (MonoInter() ? 3 : 1) * L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
+      // (a bound against a replay that stops advancing; each split needs at most an expansion, a
+      // rescan and a re-expansion round, several per split when its speculation is voided)
+      if (launched > (MonoInter() ? 6 : 1) * L_ + 2 * kCont) Log::Fatal("frontier tree: not finished after %d rounds", launched);
       if (use_graph) {
         if (!fcont_) fcont_ = CaptureFrontier(kCont, false);
         HIP_CHECK(hipGraphLaunch(fcont_, stream_));
