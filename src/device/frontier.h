@@ -100,6 +100,8 @@ constexpr uint8_t kNodeCommitted = 2;  // its split is part of the tree (replay)
 constexpr uint8_t kNodeDead = 4;       // below an expansion the CEGB replay invalidated: never used
 constexpr uint8_t kNodeStale = 0x40;   // (select-local) intermediate monotone: record scanned under looser bounds
 constexpr uint8_t kNodeEligTmp = 0x20; // (select-local) eligible for expansion this round
+constexpr uint8_t kNodeRescanTmp = 0x10;  // (select-local) re-scanned in the last round (new key)
+constexpr uint8_t kNodeLocal = 0xF0;      // the select-local bits: never stored to FArgs::nstate
 // stamp slots: kernel ids and the per-kernel slot count (slot 7: latest block exit)
 constexpr int kFStampPart = 0, kFStampHist = 1, kFStampScan = 2, kFStampSel = 3, kFStampSlots = 8;
 

@@ -2211,8 +2211,11 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const FState st = *a.st;
   const unsigned xep = kXg ? *a.xc->ep : 0u;  // (xGMI: this round's tag is xep + 1)
-  // keys final once computed (no CEGB re-scoring, no monotone rescans): the alive order carries over
-  constexpr bool kIncr = !kCegb && !kMono;
+  // keys final once computed (no CEGB re-scoring; a monotone rescan's node re-enters as new): the
+  // alive order carries over
+  constexpr bool kIncr = !kCegb;
+  __shared__ int s_rscan[kMono ? kFrontierKmax : 1], s_nrsc;  // (kMono) the last round's rescanned cids
+  if (kMono && t == 0) s_nrsc = 0;
   if (st.done) return;
   const int kprev = st.k;
   const int cid_next = st.cid_next;
@@ -2471,6 +2474,11 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       if (lane == 0) {
         s_gain[c] = valid ? g : kMinScore;
         s_feat[c] = valid ? ff : -1;
+        if (kMono && (q >> 1) >= st.kx && pc >= 0) {
+          // (a rescan: its key changed; the merged alive order takes it as a new node)
+          s_st[c] = static_cast<uint8_t>(s_st[c] | kNodeRescanTmp);
+          s_rscan[atomicAdd(&s_nrsc, 1)] = c;
+        }
         // (CEGB: the penalised best lives in best / key only)
         // (merged ranks' records: the next expansions read best / key, written above)
         // (a rescan's pair names an older cid: its record is read back from best / key)
@@ -2912,7 +2920,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     SplitRec* r = a.rec + st.num_splits + k;
     r->leaf = s_c0[k];
     r->pad = s_c1[k];  // committed cid (~cid: a forced split); k_f_results resolves it
-    a.nstate[c] = s_st[c];
+    a.nstate[c] = static_cast<uint8_t>(s_st[c] & ~kNodeLocal);
   }
   for (int l = t; l < nl; l += blockDim.x) a.leaf_cid[l] = s_lcid[l];
   FStamp(a, rnd, kFStampSel, 4);
@@ -2956,7 +2964,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         const uint8_t sx = s_st[x];
         if (sx & 0x80) {
           s_st[x] = static_cast<uint8_t>(sx & ~0x80);
-          a.nstate[x] = static_cast<uint8_t>(sx & ~(0x80 | kNodeStale | kNodeEligTmp));
+          a.nstate[x] = static_cast<uint8_t>(sx & ~kNodeLocal);
         }
       }
     }
@@ -3113,17 +3121,20 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
     // merge is the full sort's order; if the counts disagree (they cannot) the network runs.
     bool merged = false;
     if (kIncr && a.salive != nullptr && st.nsal > 0) {
+      constexpr int kNewMax = 3 * kFrontierKmax + 1;  // children + (kMono) rescanned nodes
       int* s_oc = reinterpret_cast<int*>(s_sg);  // [C] previous order, still alive
-      int* s_nw = s_oc + C;                      // [<= 2 kmax + 1] the new ones, ordered
-      int* s_nf = s_nw + 2 * kFrontierKmax + 1;  // [<= 2 kmax + 1] alive flags of the new ones
+      int* s_nw = s_oc + C;                      // [kNewMax] the new ones, ordered
+      int* s_nf = s_nw + kNewMax;                // [kNewMax] alive flags of the new ones
       __shared__ int s_nk, s_nn;
       const int nold = min(st.nsal, C);
-      const int lo = max(base, 0), nn = min(cid_next - lo, 2 * kFrontierKmax + 1);
+      const int lo = max(base, 0), nch = min(cid_next - lo, 2 * kFrontierKmax + 1);
+      const int nn = nch + (kMono ? s_nrsc : 0);
       auto live = [&](int c) {
         return !(s_st[c] & (kNodeCommitted | kNodeDead)) && s_feat[c] >= 0 && s_gain[c] > 0.0;
       };
+      auto newc = [&](int i) { return kMono && i >= nch ? s_rscan[i - nch] : lo + i; };
       for (int i = t; i < nold; i += blockDim.x) s_sc[i] = a.salive[i];
-      for (int i = t; i < nn; i += blockDim.x) s_nf[i] = live(lo + i) ? 1 : 0;
+      for (int i = t; i < nn; i += blockDim.x) s_nf[i] = live(newc(i)) ? 1 : 0;
       if (t == 0) s_nn = 0;
       __syncthreads();
       constexpr int kPm = kFrontierMaxNodes / kFSelThreads;
@@ -3131,7 +3142,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
 #pragma unroll
       for (int q = 0; q < kPm; ++q) {
         const int p = t * kPm + q;
-        keep[q] = p < nold && s_sc[p] < lo && live(s_sc[p]) ? 1 : 0;
+        keep[q] = p < nold && s_sc[p] < lo && !(kMono && (s_st[s_sc[p]] & kNodeRescanTmp)) && live(s_sc[p]) ? 1 : 0;
         kloc += keep[q];
       }
       const int kinc = WaveInclusiveScan(kloc);
@@ -3140,13 +3151,14 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       // the new ones' ranks among themselves (<= 129: broadcast reads)
       int nr = -1;
       if (t < nn && s_nf[t]) {
-        const int ci = lo + t;
+        const int ci = newc(t);
         const double gi = s_gain[ci];
         nr = 0;
         for (int j = 0; j < nn; ++j) {
           if (!s_nf[j]) continue;
-          const double gj = s_gain[lo + j];
-          nr += (gj > gi || (gj == gi && lo + j < ci)) ? 1 : 0;
+          const int cj = newc(j);
+          const double gj = s_gain[cj];
+          nr += (gj > gi || (gj == gi && cj < ci)) ? 1 : 0;
         }
         atomicAdd(&s_nn, 1);
       }
@@ -3159,7 +3171,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       for (int q = 0; q < kPm; ++q) {
         if (keep[q]) s_oc[koff++] = s_sc[t * kPm + q];
       }
-      if (nr >= 0) s_nw[nr] = lo + t;
+      if (nr >= 0) s_nw[nr] = newc(t);
       __syncthreads();
       const int nk = s_nk, nw = s_nn;
       if (nk + nw == na) {
@@ -3333,7 +3345,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         x.rescan = 0;
         a.exps[lane] = x;
         a.nodes[p].left = cid_next + 2 * lane;
-        a.nstate[p] = static_cast<uint8_t>((s_st[p] & ~kNodeEligTmp) | kNodeExpanded);
+        a.nstate[p] = static_cast<uint8_t>((s_st[p] & ~kNodeLocal) | kNodeExpanded);
       }
       if (kMono && lane >= K && lane < K + NR) {
         // a rescan: node c's record again from its slot under its current bounds; an expansion
@@ -3362,7 +3374,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         lb.max = cb.y;
         a.bounds[c] = lb;
         // (its expansion, if any, was voided at the start of phase D)
-        a.nstate[c] = static_cast<uint8_t>(s_st[c] & ~(kNodeExpanded | kNodeStale | kNodeEligTmp));
+        a.nstate[c] = static_cast<uint8_t>(s_st[c] & ~(kNodeExpanded | kNodeLocal));
       }
       if (lane == 63) s_tiles = inc;
     } else if (!done) {

@@ -1480,11 +1480,14 @@ def test_speculation_budget_does_not_change_trees(lgb, gpu_required, monkeypatch
 
 
 @pytest.mark.parametrize("extra", [{}, {"use_quantized_grad": True, "num_grad_quant_bins": 4},
-                                   {"num_leaves": 300, "min_data_in_leaf": 2}])
+                                   {"num_leaves": 300, "min_data_in_leaf": 2},
+                                   {"monotone_constraints": [1, -1, 0, 1] + [0] * 12,
+                                    "monotone_constraints_method": "intermediate"}])
 def test_select_merged_alive_order_does_not_change_trees(lgb, gpu_required, monkeypatch, extra):
     """Beyond 256 alive nodes the select merges the previous round's alive order with the last
-    round's children instead of re-sorting (FState::nsal, FArgs::salive): the same expansions and
-    the same model as the full sort (LGAP_KERNEL=select_merge=0)."""
+    round's children (and, under intermediate monotone constraints, the nodes it re-scanned)
+    instead of re-sorting (FState::nsal, FArgs::salive): the same expansions and the same model as
+    the full sort (LGAP_KERNEL=select_merge=0)."""
     rng = np.random.default_rng(29)
     n = 80000
     X = rng.standard_normal((n, 16))
