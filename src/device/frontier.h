@@ -395,7 +395,8 @@ __host__ __device__ inline size_t FrontierScanWaveBytes(int max_bin, int cat_p2)
 }
 void LaunchFrontierSelect(const FArgs& a, hipStream_t s);
 // extra LDS of the intermediate-monotone select (after FrontierSelectLds): per-leaf current and
-// scan bounds, per-node thresholds, the committed node's ancestor levels, per-feature monotone types
+// scan bounds, per-node thresholds, the committed node's ancestor levels, per-feature monotone
+// types
 __host__ __device__ inline size_t FrontierSelectMonoLds(int C, int L, int F) {
   return 16 + static_cast<size_t>(L) * (2 * 16 + 3 * sizeof(int) + 1) + static_cast<size_t>(C) * sizeof(int) +
          static_cast<size_t>(F) + 16;

@@ -2019,6 +2019,9 @@ struct FMonoLds {
   int* lvt = nullptr;      // [L] climb level: threshold | 1 << 28 borders | 1 << 29 monotone | 1 << 30 decreasing
   uint8_t* lvs = nullptr;  // [L] climb level: 1 = reached from the right child
   int8_t* mono = nullptr;  // [F] monotone type of each feature
+  int* cl = nullptr;       // [C] leaf index of each cid that is a leaf of the committed tree
+  int* qa = nullptr;       // descent queues; these three live in the alive-sort area, unused
+  int* qb = nullptr;       // during the replay
 };
 constexpr int kMonoBorder = 1 << 28, kMonoMono = 1 << 29, kMonoDec = 1 << 30, kMonoThr = (1 << 28) - 1;
 
@@ -2030,7 +2033,7 @@ __device__ __forceinline__ bool FMonoStale(const FMonoLds& mo, int l) {
 // Wave 0 after committing node c's split (leaf bl keeps the left child `left`, the right child is
 // the new leaf nl - 1): host MonotoneLeafConstraints::AfterSplit (Climb / Descend)
 __device__ void FMonoCommit(const FArgs& a, const FMonoLds& mo, const int* s_par, const int* s_left, const int* s_feat,
-                            const int* s_dep, const int* s_lcid, const double* s_lg, int c, int left, int bl, int nl) {
+                            const int* s_dep, const uint8_t* s_st, const double* s_lg, int c, int left, int bl, int nl) {
   const int lane = threadIdx.x & 63;
   const SplitInfo& bi = a.best[c];
   const double lo = bi.left_output, ro = bi.right_output;
@@ -2099,68 +2102,101 @@ __device__ void FMonoCommit(const FArgs& a, const FMonoLds& mo, const int* s_par
   }
   if (__ballot(any) == 0ull) return;
   FWaveSync();
-  for (int l = lane; l < nl; l += 64) {
-    if (l == bl || l == nr || !(s_lg[l] > kMinScore)) continue;  // (host: best gain kMinScore, no update)
-    const int x = s_lcid[l];
-    // the level where x's path meets c's (their lowest common ancestor)
-    int y = x, d = s_dep[x], lam = -1;
-    while (d > 0) {
-      y = s_par[y];
-      --d;
-      if (d < D && mo.ancd[d] == y) {
-        lam = D - 1 - d;
-        break;
-      }
+  // Descend (host MonotoneLeafConstraints::Descend), top-down and pruned: a breadth-first walk of
+  // the far subtrees of the bordering monotone levels, one lane per queued node. An entry packs
+  // (node, level, use_left, use_right); a node lets the walk through a side unless a bordering
+  // split below its level, on the same feature, separates that side from the new leaves, and a
+  // split on the new split's own feature decides which new output each side borders. Every leaf
+  // lies in one far subtree (that of its lowest common ancestor with c): no two lanes write one
+  // leaf's bounds.
+  const unsigned long long ltm = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int nq = 0;
+  for (int i0 = 0; i0 < D; i0 += 64) {
+    const int i = i0 + lane;
+    bool push = false;
+    int ent = 0;
+    if (i < D && (mo.lvt[i] & kMonoMono)) {
+      const int P = mo.ancd[D - 1 - i];
+      const int node = i == 0 ? c : mo.ancd[D - i];
+      const int far = s_left[P] == node ? s_left[P] + 1 : s_left[P];
+      ent = far | (i << 16) | (3 << 28);
+      push = true;
     }
-    if (lam < 0) continue;
-    const int lt = mo.lvt[lam];
-    if (!(lt & kMonoMono)) continue;
-    // Descend from the far child to x: every node on the way must let the path through (Borders
-    // against the entries below the level), and splits on the new split's feature decide which
-    // of the two new outputs x borders
-    bool use_l = true, use_r = true, reach = true;
-    int ch = x, yy = s_par[x];
-    while (yy != y && reach) {
-      const bool right = s_left[yy] + 1 == ch;
-      const int th = mo.thr[yy];
-      if (th >= 0) {
-        const int fy = s_feat[yy];
-        const uint32_t ty = static_cast<uint32_t>(th);
-        for (int j = 0; j < lam; ++j) {
-          const int tj = mo.lvt[j];
-          if (mo.lvf[j] != fy || !(tj & kMonoBorder)) continue;
-          const uint32_t tv = static_cast<uint32_t>(tj & kMonoThr);
-          const bool sj = mo.lvs[j] != 0;
-          if (right && !sj && ty >= tv) reach = false;
-          if (!right && sj && ty <= tv) reach = false;
+    const unsigned long long m = __ballot(push);
+    if (push) mo.qa[nq + __popcll(m & ltm)] = ent;
+    nq += __popcll(m);
+  }
+  int* qcur = mo.qa;
+  int* qnext = mo.qb;
+  while (nq > 0) {
+    FWaveSync();
+    int nn = 0;
+    for (int e0 = 0; e0 < nq; e0 += 64) {
+      const int e = e0 + lane;
+      int o0 = -1, o1 = -1;
+      if (e < nq) {
+        const int ent = qcur[e];
+        const int x = ent & 0xFFFF, lam = (ent >> 16) & 0xFFF;
+        const bool ul = (ent >> 28) & 1, ur = (ent >> 29) & 1;
+        if (!(s_st[x] & kNodeCommitted)) {
+          // a leaf of the committed tree
+          const int l = mo.cl[x];
+          if (l != bl && l != nr && s_lg[l] > kMinScore) {  // (host: best gain kMinScore, no update)
+            const int lt = mo.lvt[lam];
+            const bool from_right = mo.lvs[lam] != 0;
+            const bool tmax = (lt & kMonoDec) ? !from_right : from_right;
+            double vlo, vhi;
+            if (ul && ur) {
+              vlo = fmin(lo, ro);
+              vhi = fmax(lo, ro);
+            } else if (ur) {
+              vlo = vhi = ro;
+            } else {
+              vlo = vhi = lo;
+            }
+            double2 cb = mo.cb[l];
+            if (tmax) {
+              if (vlo < cb.y) cb.y = vlo;
+            } else {
+              if (vhi > cb.x) cb.x = vhi;
+            }
+            mo.cb[l] = cb;
+          }
+        } else {
+          const int th = mo.thr[x];
+          bool gl = true, gr = true, lsr = true, rsl = true;
+          if (th >= 0) {
+            const int fx = s_feat[x];
+            const uint32_t tx = static_cast<uint32_t>(th);
+            for (int j = 0; j < lam; ++j) {
+              const int tj = mo.lvt[j];
+              if (mo.lvf[j] != fx || !(tj & kMonoBorder)) continue;
+              const uint32_t tv = static_cast<uint32_t>(tj & kMonoThr);
+              const bool sj = mo.lvs[j] != 0;
+              if (tx >= tv && !sj) gr = false;
+              if (tx <= tv && sj) gl = false;
+            }
+            if (fx == sf) {
+              if (tx <= sthr) lsr = false;
+              if (tx >= sthr) rsl = false;
+            }
+          }
+          const int lx = s_left[x];
+          if (gl) o0 = lx | (lam << 16) | ((ul ? 1 : 0) << 28) | ((lsr && ur ? 1 : 0) << 29);
+          if (gr) o1 = (lx + 1) | (lam << 16) | ((rsl && ul ? 1 : 0) << 28) | ((ur ? 1 : 0) << 29);
         }
-        if (fy == sf) {
-          if (!right && ty <= sthr) use_r = false;
-          if (right && ty >= sthr) use_l = false;
-        }
       }
-      ch = yy;
-      yy = s_par[yy];
+      const int cnt = (o0 >= 0 ? 1 : 0) + (o1 >= 0 ? 1 : 0);
+      const int inc = WaveInclusiveScan(cnt);
+      int pos = nn + inc - cnt;
+      if (o0 >= 0) qnext[pos++] = o0;
+      if (o1 >= 0) qnext[pos] = o1;
+      nn += ReadLane(inc, 63);
     }
-    if (!reach) continue;
-    const bool from_right = mo.lvs[lam] != 0;
-    const bool tmax = (lt & kMonoDec) ? !from_right : from_right;
-    double vlo, vhi;
-    if (use_l && use_r) {
-      vlo = fmin(lo, ro);
-      vhi = fmax(lo, ro);
-    } else if (use_r) {
-      vlo = vhi = ro;
-    } else {
-      vlo = vhi = lo;
-    }
-    double2 cb = mo.cb[l];
-    if (tmax) {
-      if (vlo < cb.y) cb.y = vlo;
-    } else {
-      if (vhi > cb.x) cb.x = vhi;
-    }
-    mo.cb[l] = cb;
+    int* tq = qcur;
+    qcur = qnext;
+    qnext = tq;
+    nq = nn;
   }
   FWaveSync();
 }
@@ -2509,6 +2545,12 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
   double* s_sg = reinterpret_cast<double*>(smem + ((reinterpret_cast<uintptr_t>(s_lf + L) -
                                                     reinterpret_cast<uintptr_t>(smem) + 15) & ~uintptr_t(15)));  // [P2max]
   int* s_sc = reinterpret_cast<int*>(s_sg + FrontierSortCap(C));      // [P2max]
+  if (kMono) {
+    // (FMonoCommit's descent queues and cid -> leaf map: the sort area is unused until phase D)
+    mo.qa = reinterpret_cast<int*>(s_sg);
+    mo.qb = mo.qa + FrontierSortCap(C);
+    mo.cl = s_sc;
+  }
   // (the register replay below reads the leaves' keys itself: no LDS image, no barrier)
   const bool reg_replay = !cegb && !kMono && st.forced_next < 0 && L <= 64 * kSelLPer;
   if (!reg_replay) {
@@ -2521,6 +2563,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         const LeafBounds cb = a.cbnd[c], sb = a.bounds[c];
         mo.cb[l] = make_double2(cb.min, cb.max);
         mo.sb[l] = make_double2(sb.min, sb.max);
+        mo.cl[c] = l;
       }
     }
     __syncthreads();
@@ -2850,6 +2893,10 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
         s_c1[nc] = c;
         s_lcid[bl] = left;
         s_lcid[nl] = left + 1;
+        if (kMono) {
+          mo.cl[left] = bl;
+          mo.cl[left + 1] = nl;
+        }
         s_st[c] |= kNodeCommitted;
         const int fl = s_feat[left], fr = s_feat[left + 1];
         s_lg[bl] = fl < 0 ? kMinScore : s_gain[left];
@@ -2863,7 +2910,7 @@ __global__ __launch_bounds__(kFSelThreads) void k_f_select(FArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (kMono) FMonoCommit(a, mo, s_par, s_left, s_feat, s_dep, s_lcid, s_lg, c, left, bl, nl);
+      if (kMono) FMonoCommit(a, mo, s_par, s_left, s_feat, s_dep, s_st, s_lg, c, left, bl, nl);
     }
     if (kMono) {
       // stale leaves -> this round's rescans (phase D), marked ineligible for expansion; every
