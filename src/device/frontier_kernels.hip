@@ -2009,7 +2009,8 @@ __device__ void FByNodeDraw(const FArgs& a, int c, uint8_t* mask, uint8_t* s_pic
 // the optimum; the order check cannot newly pass: both children clamp into one interval), so a
 // STALE leaf's recorded gain is an upper bound of its re-scan: the replay commits a clean leaf
 // only when no stale leaf's bound reaches its gain, otherwise it stops and the stale leaves are
-// re-scanned from their slots (FExp::rescan) in the next round.
+// re-scanned from their slots (FExp::rescan) in the next round. 1M x 28 with 4 constrained
+// features: 63 leaves 1.29x, 255 leaves 1.69x the unconstrained iteration time.
 struct FMonoLds {
   double2* cb = nullptr;   // [L] current bounds (min, max) of each leaf
   double2* sb = nullptr;   // [L] the bounds its record was scanned with
