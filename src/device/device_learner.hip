@@ -2075,8 +2075,16 @@ class DeviceTreeLearner : public TreeLearner {
       stune_ = SpecTuner();
       // (not with raw CEGB candidates or forced splits: there the select's replay of speculated
       // expansions depends on what was speculated, and the budget must not follow wall-clock time)
-      stune_.on = !distributed_ && L_ >= 128 && !RawCands() && fnum_forced_ == 0 &&
+      // Below 128 leaves the early trees are near-balanced and alpha 1 is their optimum (30-step
+      // A/B, profiles/r06/ab_notes.md); later trees grow chain-like and gain from deeper
+      // speculation (10M x 28 / 63 leaves over 500 iterations: 358 it/s at alpha 1, 377 at 1.5,
+      // 385 tuned). There the tuner starts probing after the first 64 trees. LGAP_SPEC_TUNE=0:
+      // off below 128 leaves; 1: probing from the first tree.
+      const char* te = std::getenv("LGAP_SPEC_TUNE");
+      const bool tune_small = te == nullptr || te[0] != '0';
+      stune_.on = !distributed_ && (L_ >= 128 || tune_small) && !RawCands() && fnum_forced_ == 0 &&
                   spec.empty();
+      if (L_ < 128 && te == nullptr) stune_.rest = 64;
     }
     if (std::getenv("LGAP_FSTAMPS")) {
       fstamps_.Resize(256 * 4 * kFStampSlots);
